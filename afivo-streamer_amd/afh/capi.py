@@ -1,0 +1,184 @@
+"""ctypes mirror of include/afivo_hip.h.
+
+The same structures and signatures serve two shared libraries:
+  * the product, libafivo_hip.so (prefix ``afh_``), built from csrc/;
+  * the test oracle, oracle/lib/libafo.so (prefix ``afo_``) -- loaded only by
+    tests/, __graft_entry__.smoke() and bench.py's cpu_baseline.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.dirname(HERE)
+REPO = os.path.dirname(PKG)
+HIP_LIB = os.path.join(PKG, "csrc", "libafivo_hip.so")
+ORACLE_LIB = os.path.join(REPO, "oracle", "lib", "libafo.so")
+
+AFH_OK = 0
+BC_DIRICHLET, BC_NEUMANN, BC_CONTINUOUS, BC_DIRICHLET_COPY = -10, -11, -12, -13
+RB_GC_INTERP, RB_GC_INTERP_LIM, RB_MG_SIDES = 1, 2, 3
+LIM_NONE, LIM_VANLEER, LIM_KOREN, LIM_MINMOD, LIM_MC, LIM_GMINMOD43, LIM_ZERO = range(1, 8)
+RATE_TABULATED_FIELD, RATE_CONSTANT, RATE_LINEAR, RATE_EXP_V1, RATE_EXP_V2 = range(1, 6)
+COARSE_CYCLES = 1
+MAX_SPECIES = 32
+MAX_REACTIONS = 128
+
+i32 = C.c_int32
+f64 = C.c_double
+P_i32 = C.POINTER(i32)
+P_f64 = C.POINTER(f64)
+
+
+class BoxMeta(C.Structure):
+    _fields_ = [("lvl", i32), ("ix", i32 * 3), ("parent", i32),
+                ("children", i32 * 8), ("neighbors", i32 * 6),
+                ("neighbor_mat", i32 * 27), ("r_min", f64 * 3), ("dr", f64 * 3)]
+
+
+BOX_META_DTYPE = np.dtype([("lvl", "<i4"), ("ix", "<i4", 3), ("parent", "<i4"),
+                           ("children", "<i4", 8), ("neighbors", "<i4", 6),
+                           ("neighbor_mat", "<i4", 27),
+                           ("r_min", "<f8", 3), ("dr", "<f8", 3)])
+
+
+class TreeDesc(C.Structure):
+    _fields_ = [("n_cell", i32), ("n_boxes", i32), ("highest_lvl", i32),
+                ("n_var_cell", i32), ("n_var_face", i32),
+                ("coarse_grid_size", i32 * 3), ("periodic", i32 * 3),
+                ("r_base", f64 * 3), ("dr_base", f64 * 3),
+                ("boxes", C.c_void_p),
+                ("lvl_ids", P_i32), ("lvl_ids_off", P_i32),
+                ("lvl_leaves", P_i32), ("lvl_leaves_off", P_i32),
+                ("lvl_parents", P_i32), ("lvl_parents_off", P_i32)]
+
+
+class BC(C.Structure):
+    _fields_ = [("type", i32), ("value", f64)]
+
+
+class LT(C.Structure):
+    _fields_ = [("n_points", i32), ("n_cols", i32), ("x_min", f64),
+                ("inv_fac", f64), ("rows_cols", P_f64)]
+
+
+class Reaction(C.Structure):
+    _fields_ = [("rate_type", i32), ("table_col", i32), ("rate_factor", f64),
+                ("c", f64 * 4), ("n_in", i32), ("ix_in", i32 * 4),
+                ("n_out", i32), ("ix_out", i32 * 4), ("mult_out", i32 * 4)]
+
+
+class FluidDesc(C.Structure):
+    _fields_ = [("n_species", i32), ("species_iv", i32 * MAX_SPECIES),
+                ("species_charge", i32 * MAX_SPECIES), ("i_electron", i32),
+                ("i_efld", i32), ("f_flux", i32), ("f_field", i32),
+                ("limiter", i32), ("gas_number_density", f64), ("td", LT),
+                ("chem", LT), ("n_reactions", i32),
+                ("reactions", C.POINTER(Reaction)), ("dt_chemistry_nmin", f64)]
+
+
+class MgDesc(C.Structure):
+    _fields_ = [("i_phi", i32), ("i_rhs", i32), ("i_tmp", i32),
+                ("n_cycle_down", i32), ("n_cycle_up", i32),
+                ("helmholtz_lambda", f64), ("coarse_mode", i32),
+                ("coarse_cycles", i32)]
+
+
+assert C.sizeof(BoxMeta) == BOX_META_DTYPE.itemsize, (C.sizeof(BoxMeta),
+                                                      BOX_META_DTYPE.itemsize)
+
+# name -> (restype, argtypes); names without prefix
+_VP = C.c_void_p
+_PVP = C.POINTER(C.c_void_p)
+SIGNATURES = {
+    "last_error": (C.c_char_p, []),
+    "tree_create": (i32, [C.POINTER(TreeDesc), i32, _PVP]),
+    "tree_destroy": (i32, [_VP]),
+    "tree_sync": (i32, [_VP]),
+    "set_cc_methods": (i32, [_VP, i32, C.POINTER(BC), i32, i32]),
+    "set_bc": (i32, [_VP, i32, i32, i32, f64]),
+    "cc_put": (i32, [_VP, i32, P_f64]),
+    "cc_get": (i32, [_VP, i32, P_f64]),
+    "fc_put": (i32, [_VP, i32, P_f64]),
+    "fc_get": (i32, [_VP, i32, P_f64]),
+    "gc_lvl": (i32, [_VP, i32, i32, i32]),
+    "gc_tree": (i32, [_VP, i32, i32]),
+    "restrict_tree": (i32, [_VP, i32]),
+    "tree_copy_cc": (i32, [_VP, i32, i32]),
+    "tree_maxabs_cc": (i32, [_VP, i32, P_f64]),
+    "mg_create": (i32, [_VP, C.POINTER(MgDesc), _PVP]),
+    "mg_destroy": (i32, [_VP]),
+    "mg_fas_vcycle": (i32, [_VP, i32, i32]),
+    "mg_compute_phi_gradient": (i32, [_VP, i32, f64, i32]),
+    "fluid_create": (i32, [_VP, C.POINTER(FluidDesc), _PVP]),
+    "fluid_destroy": (i32, [_VP]),
+    "field_set_rhs": (i32, [_VP, i32, i32]),
+    "flux_upwind_tree": (i32, [_VP, i32, P_f64]),
+    "flux_update_densities": (i32, [_VP, f64, i32, i32, P_i32, P_f64, i32,
+                                    i32, P_f64]),
+}
+ORACLE_EXTRA = {
+    "mg_gsrb_boxes": (i32, [_VP, i32, i32]),
+    "mg_update_coarse": (i32, [_VP, i32]),
+    "mg_solve_coarse": (i32, [_VP]),
+    "mg_correct_children": (i32, [_VP, i32]),
+}
+
+
+class AfhError(RuntimeError):
+    pass
+
+
+class Library:
+    """A loaded C-ABI library; call functions without their prefix."""
+
+    def __init__(self, path, prefix, extra=None):
+        if not os.path.exists(path):
+            raise AfhError("shared library not built: %s" % path)
+        self.path = path
+        self.prefix = prefix
+        self.lib = C.CDLL(path)
+        sigs = dict(SIGNATURES)
+        if extra:
+            sigs.update(extra)
+        self.fn = {}
+        for name, (res, args) in sigs.items():
+            f = getattr(self.lib, prefix + name)
+            f.restype = res
+            f.argtypes = args
+            self.fn[name] = f
+
+    def call(self, name, *args):
+        rc = self.fn[name](*args)
+        if rc != AFH_OK:
+            msg = self.fn["last_error"]().decode()
+            raise AfhError("%s%s failed (%d): %s" % (self.prefix, name, rc, msg))
+        return rc
+
+    def symbols(self):
+        return [self.prefix + n for n in self.fn]
+
+
+_loaded = {}
+
+
+def hip_library():
+    """The product library. Raises if it was not built -- no CPU fallback."""
+    if "hip" not in _loaded:
+        _loaded["hip"] = Library(HIP_LIB, "afh_")
+    return _loaded["hip"]
+
+
+def oracle_library():
+    """The test oracle (oracle/lib/libafo.so)."""
+    if "oracle" not in _loaded:
+        _loaded["oracle"] = Library(ORACLE_LIB, "afo_", ORACLE_EXTRA)
+    return _loaded["oracle"]
+
+
+def header_symbols():
+    """Every afh_* function declared in include/afivo_hip.h."""
+    import re
+    src = open(os.path.join(REPO, "include", "afivo_hip.h")).read()
+    return sorted(set(re.findall(r"\b(afh_[a-z_0-9]+)\s*\(", src)))

@@ -1,0 +1,252 @@
+"""Host-side mirror of the reference's operator surface over the C ABI.
+
+Names follow the Fortran routines they stand for: ``Tree`` is af_t with its
+box pool on the device, ``Multigrid`` is mg_t (mg_fas_vcycle,
+mg_compute_phi_gradient), ``Fluid`` is the m_fluid / m_field module state
+(field_set_rhs, flux_upwind_tree, flux_update_densities). Every method calls
+straight through to the shared library it was created with; there is no
+Python compute path.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import capi
+
+
+def _i32(a):
+    return np.ascontiguousarray(a, dtype=np.int32)
+
+
+def _lists(topo, kind):
+    h = int(topo["highest_lvl"])
+    arrs = [np.asarray(topo["lvl_%s_%d" % (kind, l)], np.int32) for l in range(1, h + 1)]
+    off = np.zeros(h + 1, np.int32)
+    off[1:] = np.cumsum([len(a) for a in arrs])
+    flat = np.concatenate(arrs) if arrs else np.zeros(0, np.int32)
+    return _i32(flat), off
+
+
+class Tree:
+    """af_t: topology + device box pool of n_var_cell / n_var_face variables."""
+
+    def __init__(self, lib, topo, n_var_cell, n_var_face, device=-1):
+        self.lib = lib
+        self.topo = topo
+        self.nc = int(topo["nc"])
+        self.n_boxes = int(topo["n_boxes"])
+        self.highest_lvl = int(topo["highest_lvl"])
+        self.n_var_cell = n_var_cell
+        self.n_var_face = n_var_face
+        nb = self.n_boxes
+        meta = np.zeros(nb, capi.BOX_META_DTYPE)
+        meta["lvl"] = topo["meta_lvl"]
+        meta["ix"] = topo["meta_ix"]
+        meta["parent"] = topo["meta_parent"]
+        meta["children"] = topo["meta_children"]
+        meta["neighbors"] = topo["meta_neighbors"]
+        meta["neighbor_mat"] = topo["meta_neighbor_mat"]
+        meta["r_min"] = topo["meta_r_min"]
+        meta["dr"] = topo["meta_dr"]
+        self._meta = meta
+        self._lists = {k: _lists(topo, k) for k in ("ids", "leaves", "parents")}
+        d = capi.TreeDesc()
+        d.n_cell, d.n_boxes, d.highest_lvl = self.nc, nb, self.highest_lvl
+        d.n_var_cell, d.n_var_face = n_var_cell, n_var_face
+        d.coarse_grid_size[:] = [int(x) for x in topo["coarse_grid_size"]]
+        d.periodic[:] = [0, 0, 0]
+        d.r_base[:] = [float(x) for x in topo["r_base"]]
+        d.dr_base[:] = [float(x) for x in topo["dr_base"]]
+        d.boxes = meta.ctypes.data
+        for k in ("ids", "leaves", "parents"):
+            flat, off = self._lists[k]
+            setattr(d, "lvl_%s" % k, flat.ctypes.data_as(capi.P_i32))
+            setattr(d, "lvl_%s_off" % k, off.ctypes.data_as(capi.P_i32))
+        h = C.c_void_p()
+        lib.call("tree_create", C.byref(d), device, C.byref(h))
+        self.h = h
+
+    # -- lifetime
+    def close(self):
+        if self.h:
+            self.lib.call("tree_destroy", self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def sync(self):
+        self.lib.call("tree_sync", self.h)
+
+    # -- methods / data
+    @property
+    def cc_shape(self):
+        n = self.nc + 2
+        return (self.n_boxes, n, n, n)
+
+    @property
+    def fc_shape(self):
+        n = self.nc + 1
+        return (self.n_boxes, 3, n, n, n)
+
+    def set_cc_methods(self, iv, bc, rb=capi.RB_GC_INTERP,
+                       prolong_limiter=capi.LIM_GMINMOD43):
+        """af_set_cc_methods; bc is a list of 6 (type, value) pairs."""
+        arr = (capi.BC * 6)()
+        for n, (t, v) in enumerate(bc):
+            arr[n].type, arr[n].value = int(t), float(v)
+        self.lib.call("set_cc_methods", self.h, iv, arr, rb, prolong_limiter)
+
+    def set_bc(self, iv, nb, bc_type, value):
+        self.lib.call("set_bc", self.h, iv, nb, bc_type, float(value))
+
+    def put_cc(self, iv, arr):
+        a = np.ascontiguousarray(arr, dtype=np.float64)
+        assert a.shape == self.cc_shape, (a.shape, self.cc_shape)
+        self.lib.call("cc_put", self.h, iv, a.ctypes.data_as(capi.P_f64))
+
+    def get_cc(self, iv):
+        a = np.empty(self.cc_shape)
+        self.lib.call("cc_get", self.h, iv, a.ctypes.data_as(capi.P_f64))
+        return a
+
+    def put_fc(self, ivf, arr):
+        a = np.ascontiguousarray(arr, dtype=np.float64)
+        assert a.shape == self.fc_shape
+        self.lib.call("fc_put", self.h, ivf, a.ctypes.data_as(capi.P_f64))
+
+    def get_fc(self, ivf):
+        a = np.empty(self.fc_shape)
+        self.lib.call("fc_get", self.h, ivf, a.ctypes.data_as(capi.P_f64))
+        return a
+
+    # -- afivo tree operations
+    def gc_lvl(self, lvl, iv, corners=True):
+        self.lib.call("gc_lvl", self.h, lvl, iv, int(corners))
+
+    def gc_tree(self, iv, corners=True):
+        self.lib.call("gc_tree", self.h, iv, int(corners))
+
+    def restrict_tree(self, iv):
+        self.lib.call("restrict_tree", self.h, iv)
+
+    def copy_cc(self, iv_from, iv_to):
+        self.lib.call("tree_copy_cc", self.h, iv_from, iv_to)
+
+    def maxabs_cc(self, iv):
+        out = C.c_double()
+        self.lib.call("tree_maxabs_cc", self.h, iv, C.byref(out))
+        return out.value
+
+
+class Multigrid:
+    """mg_t bound to a tree (mg_init / mg_fas_vcycle)."""
+
+    def __init__(self, tree, i_phi, i_rhs, i_tmp, n_cycle_down=2, n_cycle_up=2,
+                 helmholtz_lambda=0.0, coarse_cycles=20):
+        self.tree = tree
+        self.lib = tree.lib
+        d = capi.MgDesc(i_phi, i_rhs, i_tmp, n_cycle_down, n_cycle_up,
+                        helmholtz_lambda, capi.COARSE_CYCLES, coarse_cycles)
+        self.i_phi, self.i_rhs, self.i_tmp = i_phi, i_rhs, i_tmp
+        h = C.c_void_p()
+        self.lib.call("mg_create", tree.h, C.byref(d), C.byref(h))
+        self.h = h
+
+    def close(self):
+        if self.h:
+            self.lib.call("mg_destroy", self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def fas_vcycle(self, set_residual=True, highest_lvl=0):
+        self.lib.call("mg_fas_vcycle", self.h, int(set_residual), highest_lvl)
+
+    def compute_phi_gradient(self, i_fc, fac=-1.0, i_norm=0):
+        self.lib.call("mg_compute_phi_gradient", self.h, i_fc, fac, i_norm)
+
+    # oracle-only stage hooks
+    def _stage(self, name, *args):
+        self.lib.call(name, self.h, *args)
+
+
+class Fluid:
+    """The m_fluid / m_chemistry state (LFA, constant gas density)."""
+
+    def __init__(self, tree, species_iv, species_charge, i_electron, i_efld,
+                 f_flux, f_field, gas_number_density, td, chem, reactions,
+                 limiter=capi.LIM_KOREN, dt_chemistry_nmin=-1.0):
+        self.tree = tree
+        self.lib = tree.lib
+        d = capi.FluidDesc()
+        d.n_species = len(species_iv)
+        d.species_iv[:len(species_iv)] = list(species_iv)
+        d.species_charge[:len(species_iv)] = list(species_charge)
+        d.i_electron, d.i_efld, d.f_flux, d.f_field = i_electron, i_efld, f_flux, f_field
+        d.limiter = limiter
+        d.gas_number_density = gas_number_density
+        self._tables = []
+        for name, lt in (("td", td), ("chem", chem)):
+            rc = np.asfortranarray(lt["rows_cols"], dtype=np.float64)
+            flat = np.ascontiguousarray(rc.T.reshape(-1))  # column-major
+            self._tables.append(flat)
+            s = getattr(d, name)
+            s.n_points, s.n_cols = rc.shape
+            s.x_min, s.inv_fac = float(lt["x_min"]), float(lt["inv_fac"])
+            s.rows_cols = flat.ctypes.data_as(capi.P_f64)
+        arr = (capi.Reaction * max(1, len(reactions)))()
+        for n, r in enumerate(reactions):
+            a = arr[n]
+            a.rate_type = r.get("rate_type", capi.RATE_TABULATED_FIELD)
+            a.table_col = r.get("table_col", 0)
+            a.rate_factor = r.get("rate_factor", 1.0)
+            for q, c in enumerate(r.get("c", [])):
+                a.c[q] = c
+            a.n_in = len(r["ix_in"])
+            a.ix_in[:a.n_in] = r["ix_in"]
+            a.n_out = len(r["ix_out"])
+            a.ix_out[:a.n_out] = r["ix_out"]
+            a.mult_out[:a.n_out] = r["mult_out"]
+        self._reactions = arr
+        d.n_reactions = len(reactions)
+        d.reactions = C.cast(arr, C.POINTER(capi.Reaction))
+        d.dt_chemistry_nmin = dt_chemistry_nmin
+        h = C.c_void_p()
+        self.lib.call("fluid_create", tree.h, C.byref(d), C.byref(h))
+        self.h = h
+
+    def close(self):
+        if self.h:
+            self.lib.call("fluid_destroy", self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def field_set_rhs(self, i_rhs, s_in):
+        self.lib.call("field_set_rhs", self.h, i_rhs, s_in)
+
+    def flux_upwind_tree(self, s_deriv):
+        dt = (C.c_double * 2)()
+        self.lib.call("flux_upwind_tree", self.h, s_deriv, dt)
+        return dt[0], dt[1]
+
+    def flux_update_densities(self, dt, s_deriv, s_prev, w_prev, s_out, last_step):
+        sp = _i32(s_prev)
+        wp = np.ascontiguousarray(w_prev, dtype=np.float64)
+        out = (C.c_double * 2)()
+        self.lib.call("flux_update_densities", self.h, float(dt), s_deriv, len(sp),
+                      sp.ctypes.data_as(capi.P_i32), wp.ctypes.data_as(capi.P_f64),
+                      s_out, int(last_step), out)
+        return out[0], out[1]

@@ -1,0 +1,171 @@
+"""The streamer time step over the C ABI (src/streamer.f90 + m_fluid + m_field).
+
+``StreamerCase`` registers variables in the order the streamer does
+(species with num_steps+1 copies, phi with 2, electric_fld, rhs, tmp;
+src/m_chemistry.f90:262-270, src/m_streamer.f90:237-302), sets the
+ghost-cell methods of streamer.f90:81-84 / m_field.f90:349-350, and exposes
+field_compute (m_field.f90:405-485), forward_euler (m_fluid.f90:21-99) and a
+Heun step (af_advance, afivo/src/m_af_advance.f90:160-164).
+"""
+import math
+
+import numpy as np
+
+from . import capi
+from .model import Fluid, Multigrid, Tree
+
+# cc / fc variable indices (1-based, as af_add_cc_variable assigns them)
+IV = {"e": 1, "pos": 4, "neg": 7, "phi": 10, "phi_2": 11, "efld": 12,
+      "rhs": 13, "tmp": 14}
+N_VAR_CELL = 14
+FV = {"flux": 1, "field": 2}
+N_VAR_FACE = 2
+
+UC_EPS0 = 8.8541878176e-12
+UC_ELEM_CHARGE = 1.6022e-19
+UC_BOLTZMANN = 1.3806503e-23
+
+
+def standard_reactions():
+    """Old-style transport data model, src/m_chemistry.f90:205-239."""
+    return [
+        {"rate_type": capi.RATE_TABULATED_FIELD, "table_col": 1,
+         "rate_factor": 1.0, "ix_in": [1], "ix_out": [1, 2],
+         "mult_out": [2, 1]},  # e + M -> e + e + M+
+        {"rate_type": capi.RATE_TABULATED_FIELD, "table_col": 2,
+         "rate_factor": 1.0, "ix_in": [1], "ix_out": [3],
+         "mult_out": [1]},  # e + M -> M-
+    ]
+
+
+def gas_number_density(pressure_bar=1.0, temperature=300.0):
+    """Ideal gas law, src/m_gas.f90:174-176."""
+    return 1e5 * pressure_bar / (UC_BOLTZMANN * temperature)
+
+
+def tables_from(golden):
+    td = {"rows_cols": golden["td_rows_cols"], "x_min": golden["td_xmin"],
+          "inv_fac": golden["td_inv_fac"]}
+    chem = {"rows_cols": golden["chem_rows_cols"], "x_min": golden["chem_xmin"],
+            "inv_fac": golden["chem_inv_fac"]}
+    return td, chem
+
+
+class StreamerCase:
+    """One streamer simulation state on a tree, driven through `lib`."""
+
+    def __init__(self, lib, topo, td, chem, voltage, n_gas=None,
+                 coarse_cycles=20, device=-1):
+        self.lib = lib
+        self.topo = topo
+        self.tree = Tree(lib, topo, N_VAR_CELL, N_VAR_FACE, device=device)
+        t = self.tree
+        neumann0 = [(capi.BC_NEUMANN, 0.0)] * 6
+        for sp in ("e", "pos", "neg"):
+            for s in range(3):
+                t.set_cc_methods(IV[sp] + s, neumann0, capi.RB_GC_INTERP_LIM,
+                                 capi.LIM_GMINMOD43)
+        t.set_cc_methods(IV["efld"], neumann0, capi.RB_GC_INTERP)
+        self.voltage = voltage
+        for s in (0, 1):
+            t.set_cc_methods(IV["phi"] + s, self.phi_bc(voltage), capi.RB_MG_SIDES)
+        self.mg = Multigrid(t, IV["phi"], IV["rhs"], IV["tmp"],
+                            coarse_cycles=coarse_cycles)
+        self.n_gas = gas_number_density() if n_gas is None else n_gas
+        self.fluid = Fluid(t, [IV["e"], IV["pos"], IV["neg"]], [-1, 1, -1],
+                           IV["e"], IV["efld"], FV["flux"], FV["field"],
+                           self.n_gas, td, chem, standard_reactions())
+        self.domain = np.asarray(topo["domain"], float)
+
+    @staticmethod
+    def phi_bc(voltage):
+        """field_bc_homogeneous, src/m_field.f90:547-567."""
+        return [(capi.BC_NEUMANN, 0.0)] * 4 + [(capi.BC_DIRICHLET, 0.0),
+                                               (capi.BC_DIRICHLET, voltage)]
+
+    def set_voltage(self, voltage):
+        self.voltage = voltage
+        self.tree.set_bc(IV["phi"], 6, capi.BC_DIRICHLET, voltage)
+
+    def min_dr(self):
+        return float(np.min(self.topo["meta_dr"]))
+
+    def field_from_potential(self):
+        """m_field.f90:488-505."""
+        self.mg.compute_phi_gradient(FV["field"], -1.0, IV["efld"])
+        self.tree.gc_tree(IV["efld"])
+
+    def field_compute(self, s_in, n_vcycles=2, max_rel_residual=1e-4,
+                      check_residual=True):
+        """m_field.f90:405-485 with have_guess = .true.; returns residuals."""
+        self.fluid.field_set_rhs(IV["rhs"], s_in)
+        residuals = []
+        threshold = None
+        if check_residual:
+            max_rhs = self.tree.maxabs_cc(IV["rhs"])
+            threshold = max(1e-6, max_rhs * max_rel_residual,
+                            1e-10 * abs(self.voltage) /
+                            (self.domain[2] * self.min_dr()))
+        for _ in range(n_vcycles):
+            self.mg.fas_vcycle(True)
+            if check_residual:
+                residuals.append(self.tree.maxabs_cc(IV["tmp"]))
+                if residuals[-1] < threshold:
+                    break
+        self.field_from_potential()
+        return residuals
+
+    def forward_euler(self, dt, s_deriv, s_prev, w_prev, s_out, i_step,
+                      n_steps, **field_kw):
+        """m_fluid.f90:21-99 (without the CFL/ dt_max combination)."""
+        if i_step > 1:
+            self.field_compute(s_deriv, **field_kw)
+        d1 = self.fluid.flux_upwind_tree(s_deriv)
+        d2 = self.fluid.flux_update_densities(dt, s_deriv, s_prev, w_prev,
+                                              s_out, i_step == n_steps)
+        return [d1[0], d1[1], d2[0], d2[1]]
+
+    def heun_step(self, dt, **field_kw):
+        """af_advance with af_heuns_method (m_af_advance.f90:160-164)."""
+        l1 = self.forward_euler(dt, 0, [0], [1.0], 1, 1, 2, **field_kw)
+        l2 = self.forward_euler(0.5 * dt, 1, [0, 1], [0.5, 0.5], 0, 2, 2,
+                                **field_kw)
+        return [min(a, b) for a, b in zip(l1, l2)]
+
+
+def gaussian_seed(topo, r0, width, n0=5e18, bg=1e15):
+    """Initial densities on every box incl. ghost cells (the golden harness'
+    set_init), returned as (n_e, n_pos, n_neg, phi-guess factory input)."""
+    nc = int(topo["nc"])
+    idx = np.arange(nc + 2) - 0.5
+    r_min, dr = topo["meta_r_min"], topo["meta_dr"]
+    x = r_min[:, 0, None] + idx[None, :] * dr[:, 0, None]
+    y = r_min[:, 1, None] + idx[None, :] * dr[:, 1, None]
+    z = r_min[:, 2, None] + idx[None, :] * dr[:, 2, None]
+    d2 = ((x - r0[0]) ** 2)[:, None, None, :] + ((y - r0[1]) ** 2)[:, None, :, None] \
+        + ((z - r0[2]) ** 2)[:, :, None, None]
+    ne = bg + n0 * np.exp(-d2 / width ** 2)
+    return ne, x, y, z
+
+
+def seed_state(case, r0=None, width=None):
+    """S1-style seed: n_e = n_+ = 1e15 + 5e18 exp(-|r-r0|^2/w^2), n_- = 1e14,
+    phi = linear background."""
+    topo = case.topo
+    dom = np.asarray(topo["domain"], float)
+    r0 = 0.5 * dom if r0 is None else np.asarray(r0)
+    width = 0.025 * dom[2] if width is None else width
+    ne, x, y, z = gaussian_seed(topo, r0, width)
+    t = case.tree
+    t.put_cc(IV["e"], ne)
+    t.put_cc(IV["pos"], ne)
+    t.put_cc(IV["neg"], np.full(ne.shape, 1e14))
+    phi = np.broadcast_to(case.voltage * (z / dom[2])[:, :, None, None], ne.shape)
+    t.put_cc(IV["phi"], np.ascontiguousarray(phi))
+    t.gc_tree(IV["phi"])
+    return ne
+
+
+def cells(topo):
+    return sum(len(topo["lvl_leaves_%d" % l]) for l in
+               range(1, int(topo["highest_lvl"]) + 1)) * int(topo["nc"]) ** 3

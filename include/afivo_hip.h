@@ -1,0 +1,233 @@
+/*
+ * afivo_hip.h -- C ABI of the MI355X-native afivo-streamer hot path.
+ *
+ * The symbols below are what an ISO_C_BINDING layer under the reference's
+ * Fortran driver binds to (see INTEGRATION.md for the bind(C) stubs). Each
+ * entry point replaces one reference interface on the per-timestep path; the
+ * replaced routine is cited (file:line, paths relative to the reference root).
+ *
+ * Conventions (all mirror afivo so a Fortran caller passes its own numbers):
+ *   - box ids are 1-based; 0 = af_no_box, -1 = af_phys_boundary
+ *     (afivo/src/m_af_types.f90:37-40);
+ *   - variable indices (iv for cell-centred, ivf for face-centred) are 1-based,
+ *     state copies are consecutive indices (iv + s), as af_add_cc_variable
+ *     with n_copies lays them out;
+ *   - host arrays exchanged with afh_cc_put/get hold, per box, the Fortran
+ *     array box%cc(0:nc+1,0:nc+1,0:nc+1,iv) (i fastest), boxes in id order;
+ *     afh_fc_put/get hold box%fc(1:nc+1,1:nc+1,1:nc+1,1:3,ivf);
+ *   - every call returns AFH_OK (0) or a negative AFH_ERR_* code;
+ *     afh_last_error() gives a message (the Fortran shim turns it into
+ *     `error stop`, as the reference does on failure);
+ *   - all device work of one tree is ordered on one HIP stream; calls are
+ *     asynchronous unless they return host data (maxabs, dt limits, get).
+ *
+ * No torch types, no C++ types: plain pointers and sizes.
+ */
+#ifndef AFIVO_HIP_H
+#define AFIVO_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AFH_OK 0
+#define AFH_ERR_ARG -1
+#define AFH_ERR_UNSUPPORTED -2
+#define AFH_ERR_DEVICE -3
+#define AFH_ERR_STATE -4
+
+/* Boundary-condition types, afivo/src/m_af_types.f90:51-64 */
+#define AFH_BC_DIRICHLET -10
+#define AFH_BC_NEUMANN -11
+#define AFH_BC_CONTINUOUS -12
+#define AFH_BC_DIRICHLET_COPY -13
+
+/* Refinement-boundary ghost-cell methods (tree%cc_methods(iv)%rb) */
+#define AFH_RB_GC_INTERP 1     /* af_gc_interp, m_af_ghostcell.f90:394-498 */
+#define AFH_RB_GC_INTERP_LIM 2 /* af_gc_interp_lim, m_af_ghostcell.f90:503-612 */
+#define AFH_RB_MG_SIDES 3      /* mg_sides_rb, m_af_multigrid.f90:294-461 */
+
+/* Limiters, afivo/src/m_af_limiters.f90:12-25 */
+#define AFH_LIM_NONE 1
+#define AFH_LIM_VANLEER 2
+#define AFH_LIM_KOREN 3
+#define AFH_LIM_MINMOD 4
+#define AFH_LIM_MC 5
+#define AFH_LIM_GMINMOD43 6
+#define AFH_LIM_ZERO 7
+
+/* Reaction rate types, src/m_chemistry.f90:63-104 (subset on the path) */
+#define AFH_RATE_TABULATED_FIELD 1
+#define AFH_RATE_CONSTANT 2
+#define AFH_RATE_LINEAR 3
+#define AFH_RATE_EXP_V1 4
+#define AFH_RATE_EXP_V2 5
+
+/* Coarse-grid solver modes (replaces HYPRE PFMG, m_coarse_solver.f90) */
+#define AFH_COARSE_CYCLES 1 /* fixed number of device MG cycles */
+
+#define AFH_MAX_SPECIES 32
+#define AFH_MAX_REACTIONS 128
+
+/* Topology of one box: the box_t fields the hot path reads
+ * (afivo/src/m_af_types.f90:286-322). */
+typedef struct afh_box_meta {
+  int32_t lvl;
+  int32_t ix[3];
+  int32_t parent;
+  int32_t children[8];
+  int32_t neighbors[6];
+  int32_t neighbor_mat[27]; /* neighbor_mat(-1:1,-1:1,-1:1), i fastest */
+  double r_min[3];
+  double dr[3];
+} afh_box_meta;
+
+/* The af_t tree (m_af_types.f90:326-393): boxes plus per-level id lists. */
+typedef struct afh_tree_desc {
+  int32_t n_cell;
+  int32_t n_boxes; /* highest_id; boxes[0..n_boxes-1] have ids 1..n_boxes */
+  int32_t highest_lvl;
+  int32_t n_var_cell;
+  int32_t n_var_face;
+  int32_t coarse_grid_size[3];
+  int32_t periodic[3];
+  double r_base[3];
+  double dr_base[3];
+  const afh_box_meta *boxes;
+  /* lvl l (1-based) list = arr[off[l-1] .. off[l]-1]; off has highest_lvl+1 */
+  const int32_t *lvl_ids, *lvl_ids_off;
+  const int32_t *lvl_leaves, *lvl_leaves_off;
+  const int32_t *lvl_parents, *lvl_parents_off;
+} afh_tree_desc;
+
+/* One face of a physical boundary: replaces an af_subr_bc callback whose
+ * value is uniform over the face (af_bc_neumann_zero, field_bc_homogeneous,
+ * ..., m_af_ghostcell.f90:614-652, src/m_field.f90:547-605). */
+typedef struct afh_bc {
+  int32_t type;  /* AFH_BC_* */
+  double value;  /* bc_val */
+} afh_bc;
+
+/* Lookup table with linear x-spacing, src/lookup_table_fortran/
+ * m_lookup_table.f90 LT_t (rows_cols is column-major: (n_points, n_cols)). */
+typedef struct afh_lt {
+  int32_t n_points;
+  int32_t n_cols;
+  double x_min;
+  double inv_fac;
+  const double *rows_cols;
+} afh_lt;
+
+/* One reaction, src/m_chemistry.f90 reaction_t / tiny_react_t (23-48). */
+typedef struct afh_reaction {
+  int32_t rate_type;  /* AFH_RATE_* */
+  int32_t table_col;  /* lookup_table_index for tabulated rates (1-based) */
+  double rate_factor; /* c0 */
+  double c[4];        /* rate_data */
+  int32_t n_in;
+  int32_t ix_in[4];   /* 1-based species index into afh_fluid_desc lists */
+  int32_t n_out;
+  int32_t ix_out[4];
+  int32_t mult_out[4];
+} afh_reaction;
+
+/* The fluid model state the m_fluid callbacks read (LFA, constant gas
+ * density): species registry (m_chemistry.f90:262-300), flux species
+ * (m_streamer.f90:237-260), transport + chemistry tables. */
+typedef struct afh_fluid_desc {
+  int32_t n_species;
+  int32_t species_iv[AFH_MAX_SPECIES];     /* cc index of state 0 */
+  int32_t species_charge[AFH_MAX_SPECIES];
+  int32_t i_electron;   /* flux species (state 0 index) */
+  int32_t i_efld;       /* |E| cell-centred (i_electric_fld) */
+  int32_t f_flux;       /* flux_elec face variable */
+  int32_t f_field;      /* electric field face variable */
+  int32_t limiter;      /* AFH_LIM_KOREN in the reference */
+  double gas_number_density;
+  afh_lt td;            /* transport table: col 1 mobility*N, col 2 D*N */
+  afh_lt chem;          /* chemtbl_fld */
+  int32_t n_reactions;
+  const afh_reaction *reactions;
+  double dt_chemistry_nmin; /* < 0: limit loss (m_dt.f90:34-37 default) */
+} afh_fluid_desc;
+
+/* Multigrid options, mg_t (m_af_types.f90:572-665) + coarse solver. */
+typedef struct afh_mg_desc {
+  int32_t i_phi, i_rhs, i_tmp;
+  int32_t n_cycle_down, n_cycle_up; /* 2, 2 */
+  double helmholtz_lambda;
+  int32_t coarse_mode;   /* AFH_COARSE_CYCLES */
+  int32_t coarse_cycles; /* device MG V(2,2) cycles on the level-1 grid */
+} afh_mg_desc;
+
+typedef struct afh_tree afh_tree;
+typedef struct afh_mg afh_mg;
+typedef struct afh_fluid afh_fluid;
+
+const char *afh_last_error(void);
+
+/* af_init + af_adjust_refinement result (m_af_core.f90:138-822): create the
+ * device box pool (all variables, zeroed) for this topology. device < 0
+ * keeps the current device. */
+int32_t afh_tree_create(const afh_tree_desc *desc, int32_t device,
+                        afh_tree **out);
+int32_t afh_tree_destroy(afh_tree *t);
+int32_t afh_tree_sync(afh_tree *t);
+
+/* af_set_cc_methods (m_af_core.f90:343-427): bc[6] per face, rb method,
+ * prolongation limiter used for 2-layer ghost cells (gc2_prolong_rb). */
+int32_t afh_set_cc_methods(afh_tree *t, int32_t iv, const afh_bc *bc6,
+                           int32_t rb, int32_t prolong_limiter);
+/* Update one face of the b.c. (e.g. a new voltage, field_set_voltage). */
+int32_t afh_set_bc(afh_tree *t, int32_t iv, int32_t nb, int32_t type,
+                   double value);
+
+/* Host <-> device transfers of tree%boxes(:)%cc(..., iv) / %fc(..., ivf). */
+int32_t afh_cc_put(afh_tree *t, int32_t iv, const double *host);
+int32_t afh_cc_get(afh_tree *t, int32_t iv, double *host);
+int32_t afh_fc_put(afh_tree *t, int32_t ivf, const double *host);
+int32_t afh_fc_get(afh_tree *t, int32_t ivf, double *host);
+
+/* af_gc_lvl / af_gc_tree (m_af_ghostcell.f90:25-61) */
+int32_t afh_gc_lvl(afh_tree *t, int32_t lvl, int32_t iv, int32_t corners);
+int32_t afh_gc_tree(afh_tree *t, int32_t iv, int32_t corners);
+/* af_restrict_tree (m_af_restrict.f90:50-59) */
+int32_t afh_restrict_tree(afh_tree *t, int32_t iv);
+/* af_tree_copy_cc (m_af_utils.f90) / copy_current_state (streamer.f90:639) */
+int32_t afh_tree_copy_cc(afh_tree *t, int32_t iv_from, int32_t iv_to);
+/* af_tree_maxabs_cc over leaf interiors (m_af_utils.f90:773-784) */
+int32_t afh_tree_maxabs_cc(afh_tree *t, int32_t iv, double *out);
+
+/* mg_init (m_af_multigrid.f90:43-109) + stencils; mg_fas_vcycle (185-264) */
+int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *desc, afh_mg **out);
+int32_t afh_mg_destroy(afh_mg *mg);
+int32_t afh_mg_fas_vcycle(afh_mg *mg, int32_t set_residual,
+                          int32_t highest_lvl);
+/* mg_compute_phi_gradient (m_af_multigrid.f90:1837-1879) incl. the norm */
+int32_t afh_mg_compute_phi_gradient(afh_mg *mg, int32_t i_fc, double fac,
+                                    int32_t i_norm);
+
+/* Fluid model bound to a tree (the m_fluid / m_chemistry module state). */
+int32_t afh_fluid_create(afh_tree *t, const afh_fluid_desc *desc,
+                         afh_fluid **out);
+int32_t afh_fluid_destroy(afh_fluid *f);
+/* field_set_rhs (src/m_field.f90:363-401) */
+int32_t afh_field_set_rhs(afh_fluid *f, int32_t i_rhs, int32_t s_in);
+/* flux_upwind_tree with the m_fluid flux_upwind / flux_direction callbacks
+ * (m_af_flux_schemes.f90:666-848, src/m_fluid.f90:102-227); dt_lim[2] =
+ * (CFL limit for CFL number 1, dielectric relaxation time). */
+int32_t afh_flux_upwind_tree(afh_fluid *f, int32_t s_deriv, double *dt_lim);
+/* flux_update_densities with add_source_terms / set_box_mask
+ * (m_af_flux_schemes.f90:320-436, src/m_fluid.f90:298-515); dt_lim[2] =
+ * (chemistry limit on the last step, 1e100 otherwise; energy limit). */
+int32_t afh_flux_update_densities(afh_fluid *f, double dt, int32_t s_deriv,
+                                  int32_t n_prev, const int32_t *s_prev,
+                                  const double *w_prev, int32_t s_out,
+                                  int32_t last_step, double *dt_lim);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,1495 @@
+/*
+ * ORACLE TEST INFRASTRUCTURE -- not product code. See afo.h.
+ *
+ * CPU restatement of the afivo-streamer hot path (NDIM = 3), mirroring the
+ * reference's per-box Fortran routines statement by statement, with the same
+ * floating-point evaluation order (compile with -ffp-contract=off). Paths in
+ * citations are relative to the reference root.
+ */
+#define _POSIX_C_SOURCE 200809L
+#include "afo.h"
+
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+static char g_err[512];
+static int32_t fail(int32_t code, const char *fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof g_err, fmt, ap);
+  va_end(ap);
+  return code;
+}
+const char *afo_last_error(void) { return g_err; }
+
+typedef struct {
+  int set;
+  afh_bc bc[6];
+  int rb;
+  int lim;
+} cc_method;
+
+struct afh_tree {
+  int nc, ng, nb, nlvl, nvc, nvf;
+  size_t bsz, fsz; /* doubles per box per cc var / per fc var (3 dims) */
+  afh_box_meta *boxes;
+  int *ids, *ids_off, *leaves, *leaves_off, *parents, *parents_off;
+  int cgs[3];
+  double *cc, *fc;
+  cc_method *meth; /* n_var_cell entries */
+};
+
+struct afh_mg {
+  afh_tree *t;
+  afh_mg_desc d;
+  double *lvl_c; /* per level: 7 stencil coefficients (mg_box_lpl_stencil) */
+  /* coarse solver hierarchy */
+  int n_mg;
+  int dims[16][3];
+  double *u[16], *f[16], *r[16];
+  double hc[16][3]; /* 1/h^2 per dim per MG level */
+  double cdiag[16];  /* unfolded diagonal per MG level */
+};
+
+#define AFH_CS_BOTTOM_SWEEPS 32
+
+struct afh_fluid {
+  afh_tree *t;
+  afh_fluid_desc d;
+  double *td, *chem;
+  afh_reaction reac[AFH_MAX_REACTIONS];
+};
+
+/* ---------------------------------------------------------------- tables
+ * afivo/src/m_af_types.f90:167-236 (NDIM = 3) */
+static const int child_dix[8][3] = {{0, 0, 0}, {1, 0, 0}, {0, 1, 0},
+                                    {1, 1, 0}, {0, 0, 1}, {1, 0, 1},
+                                    {0, 1, 1}, {1, 1, 1}};
+static const int child_adj_nb[6][4] = {{1, 3, 5, 7}, {2, 4, 6, 8},
+                                       {1, 2, 5, 6}, {3, 4, 7, 8},
+                                       {1, 2, 3, 4}, {5, 6, 7, 8}};
+static const int edge_dim[12] = {1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3};
+static const int edge_dir[12][3] = {
+    {0, -1, -1}, {0, 1, -1}, {0, -1, 1}, {0, 1, 1}, {-1, 0, -1}, {1, 0, -1},
+    {-1, 0, 1},  {1, 0, 1},  {-1, -1, 0}, {1, -1, 0}, {-1, 1, 0}, {1, 1, 0}};
+static const int nb_adj_edge[12][2] = {{3, 5}, {4, 5}, {3, 6}, {4, 6},
+                                       {1, 5}, {2, 5}, {1, 6}, {2, 6},
+                                       {1, 3}, {2, 3}, {1, 4}, {2, 4}};
+static const int edge_min_ix[12][3] = {
+    {0, 0, 0}, {0, 1, 0}, {0, 0, 1}, {0, 1, 1}, {0, 0, 0}, {1, 0, 0},
+    {0, 0, 1}, {1, 0, 1}, {0, 0, 0}, {1, 0, 0}, {0, 1, 0}, {1, 1, 0}};
+
+static inline int nb_dim(int nb) { return (nb - 1) / 2; } /* 0-based dim */
+static inline int nb_low(int nb) { return (nb - 1) % 2 == 0; }
+static inline int nb_pm(int nb) { return nb_low(nb) ? -1 : 1; }
+
+/* ---------------------------------------------------------------- access */
+static inline double *ccb(afh_tree *t, int iv, int id) {
+  return t->cc + ((size_t)(iv - 1) * t->nb + (size_t)(id - 1)) * t->bsz;
+}
+#define IX(t, i, j, k) ((((size_t)(k)) * (t)->ng + (size_t)(j)) * (t)->ng + (size_t)(i))
+/* fc(i,j,k,dim) with Fortran indices 1..nc+1 */
+static inline double *fcb(afh_tree *t, int ivf, int id) {
+  return t->fc + ((size_t)(ivf - 1) * t->nb + (size_t)(id - 1)) * t->fsz;
+}
+#define FX(t, d, i, j, k)                                                     \
+  ((size_t)(d) * (size_t)((t)->nc + 1) * ((t)->nc + 1) * ((t)->nc + 1) +      \
+   (((size_t)(k)-1) * ((t)->nc + 1) + ((size_t)(j)-1)) * ((t)->nc + 1) +      \
+   ((size_t)(i)-1))
+
+static inline afh_box_meta *B(afh_tree *t, int id) { return &t->boxes[id - 1]; }
+static inline int nmat(afh_tree *t, int id, int dx, int dy, int dz) {
+  return B(t, id)->neighbor_mat[(dx + 1) + 3 * (dy + 1) + 9 * (dz + 1)];
+}
+/* af_get_child_offset, m_af_types.f90:903-910 */
+static inline void child_offset(afh_tree *t, int id, int nb, int off[3]) {
+  for (int d = 0; d < 3; d++) {
+    off[d] = ((B(t, id)->ix[d] - 1) & 1) * (t->nc >> 1);
+    if (nb > 0 && nb_dim(nb) == d) off[d] -= nb_pm(nb) * t->nc;
+  }
+}
+
+/* ---------------------------------------------------------------- tree */
+int32_t afo_tree_create(const afh_tree_desc *d, int32_t device,
+                        afh_tree **out) {
+  (void)device;
+  if (!d || !out || d->n_cell < 2 || (d->n_cell & 1) || d->n_boxes < 1)
+    return fail(AFH_ERR_ARG, "afo_tree_create: bad descriptor");
+  if (d->periodic[0] || d->periodic[1] || d->periodic[2])
+    return fail(AFH_ERR_UNSUPPORTED, "periodic domains not supported");
+  afh_tree *t = calloc(1, sizeof *t);
+  t->nc = d->n_cell;
+  t->ng = d->n_cell + 2;
+  t->nb = d->n_boxes;
+  t->nlvl = d->highest_lvl;
+  t->nvc = d->n_var_cell;
+  t->nvf = d->n_var_face;
+  t->bsz = (size_t)t->ng * t->ng * t->ng;
+  t->fsz = 3 * (size_t)(t->nc + 1) * (t->nc + 1) * (t->nc + 1);
+  for (int i = 0; i < 3; i++) t->cgs[i] = d->coarse_grid_size[i];
+  t->boxes = malloc(sizeof(afh_box_meta) * t->nb);
+  memcpy(t->boxes, d->boxes, sizeof(afh_box_meta) * t->nb);
+  int n = t->nlvl + 1;
+#define CPYL(dst, dsto, src, srco)                                            \
+  t->dsto = malloc(sizeof(int) * n);                                          \
+  memcpy(t->dsto, d->srco, sizeof(int) * n);                                  \
+  t->dst = malloc(sizeof(int) * (t->dsto[t->nlvl] + 1));                      \
+  memcpy(t->dst, d->src, sizeof(int) * t->dsto[t->nlvl]);
+  CPYL(ids, ids_off, lvl_ids, lvl_ids_off)
+  CPYL(leaves, leaves_off, lvl_leaves, lvl_leaves_off)
+  CPYL(parents, parents_off, lvl_parents, lvl_parents_off)
+#undef CPYL
+  t->cc = calloc((size_t)t->nvc * t->nb * t->bsz, sizeof(double));
+  t->fc = calloc((size_t)(t->nvf > 0 ? t->nvf : 1) * t->nb * t->fsz,
+                 sizeof(double));
+  t->meth = calloc(t->nvc + 1, sizeof(cc_method));
+  if (!t->cc || !t->fc) return fail(AFH_ERR_ARG, "out of memory");
+  *out = t;
+  return AFH_OK;
+}
+
+int32_t afo_tree_destroy(afh_tree *t) {
+  if (!t) return AFH_OK;
+  free(t->boxes);
+  free(t->ids), free(t->ids_off), free(t->leaves), free(t->leaves_off);
+  free(t->parents), free(t->parents_off);
+  free(t->cc), free(t->fc), free(t->meth);
+  free(t);
+  return AFH_OK;
+}
+int32_t afo_tree_sync(afh_tree *t) {
+  (void)t;
+  return AFH_OK;
+}
+
+#define LVL_N(t, arr, l) ((t)->arr##_off[(l)] - (t)->arr##_off[(l)-1])
+#define LVL_AT(t, arr, l, i) ((t)->arr[(t)->arr##_off[(l)-1] + (i)])
+
+int32_t afo_set_cc_methods(afh_tree *t, int32_t iv, const afh_bc *bc6,
+                           int32_t rb, int32_t lim) {
+  if (iv < 1 || iv > t->nvc) return fail(AFH_ERR_ARG, "bad iv");
+  cc_method *m = &t->meth[iv];
+  m->set = 1;
+  memcpy(m->bc, bc6, sizeof m->bc);
+  m->rb = rb;
+  m->lim = lim;
+  return AFH_OK;
+}
+int32_t afo_set_bc(afh_tree *t, int32_t iv, int32_t nb, int32_t type,
+                   double value) {
+  if (iv < 1 || iv > t->nvc || nb < 1 || nb > 6) return fail(AFH_ERR_ARG, "bad arg");
+  t->meth[iv].bc[nb - 1].type = type;
+  t->meth[iv].bc[nb - 1].value = value;
+  return AFH_OK;
+}
+
+int32_t afo_cc_put(afh_tree *t, int32_t iv, const double *h) {
+  if (iv < 1 || iv > t->nvc) return fail(AFH_ERR_ARG, "bad iv");
+  memcpy(ccb(t, iv, 1), h, sizeof(double) * t->bsz * t->nb);
+  return AFH_OK;
+}
+int32_t afo_cc_get(afh_tree *t, int32_t iv, double *h) {
+  if (iv < 1 || iv > t->nvc) return fail(AFH_ERR_ARG, "bad iv");
+  memcpy(h, ccb(t, iv, 1), sizeof(double) * t->bsz * t->nb);
+  return AFH_OK;
+}
+int32_t afo_fc_put(afh_tree *t, int32_t ivf, const double *h) {
+  if (ivf < 1 || ivf > t->nvf) return fail(AFH_ERR_ARG, "bad ivf");
+  memcpy(fcb(t, ivf, 1), h, sizeof(double) * t->fsz * t->nb);
+  return AFH_OK;
+}
+int32_t afo_fc_get(afh_tree *t, int32_t ivf, double *h) {
+  if (ivf < 1 || ivf > t->nvf) return fail(AFH_ERR_ARG, "bad ivf");
+  memcpy(h, fcb(t, ivf, 1), sizeof(double) * t->fsz * t->nb);
+  return AFH_OK;
+}
+
+/* ------------------------------------------------------------ ghost cells */
+
+/* copy_from_nb, m_af_ghostcell.f90:654-669 */
+static void copy_from_nb(afh_tree *t, int id, int nb_id, const int dnb[3],
+                         const int lo[3], const int hi[3], int iv) {
+  double *c = ccb(t, iv, id), *cn = ccb(t, iv, nb_id);
+  int nc = t->nc;
+  for (int k = lo[2]; k <= hi[2]; k++)
+    for (int j = lo[1]; j <= hi[1]; j++)
+      for (int i = lo[0]; i <= hi[0]; i++)
+        c[IX(t, i, j, k)] =
+            cn[IX(t, i - dnb[0] * nc, j - dnb[1] * nc, k - dnb[2] * nc)];
+}
+
+/* bc_to_gc, m_af_ghostcell.f90:173-279 */
+static void bc_to_gc(afh_tree *t, int id, int nb, int iv, const afh_bc *bc) {
+  double c0, c1, c2;
+  int nc = t->nc, d = nb_dim(nb);
+  switch (bc->type) {
+  case AFH_BC_DIRICHLET: c0 = 2; c1 = -1; c2 = 0; break;
+  case AFH_BC_NEUMANN: c0 = B(t, id)->dr[d] * nb_pm(nb); c1 = 1; c2 = 0; break;
+  case AFH_BC_CONTINUOUS: c0 = 0; c1 = 2; c2 = -1; break;
+  default: c0 = 1; c1 = 0; c2 = 0; break; /* dirichlet_copy */
+  }
+  double *c = ccb(t, iv, id);
+  int g = nb_low(nb) ? 0 : nc + 1, x1 = nb_low(nb) ? 1 : nc,
+      x2 = nb_low(nb) ? 2 : nc - 1;
+  for (int b = 1; b <= nc; b++)
+    for (int a = 1; a <= nc; a++) {
+      int p0[3], p1[3], p2[3];
+      /* (a, b) run over the two tangential dims in index order */
+      int td0 = (d == 0) ? 1 : 0, td1 = (d == 2) ? 1 : 2;
+      p0[d] = g, p1[d] = x1, p2[d] = x2;
+      p0[td0] = p1[td0] = p2[td0] = a;
+      p0[td1] = p1[td1] = p2[td1] = b;
+      c[IX(t, p0[0], p0[1], p0[2])] =
+          c0 * bc->value + c1 * c[IX(t, p1[0], p1[1], p1[2])] +
+          c2 * c[IX(t, p2[0], p2[1], p2[2])];
+    }
+}
+
+/* mg_sides_rb, m_af_multigrid.f90:294-461 (3D) */
+static void mg_sides_rb(afh_tree *t, int id, int nb, int iv) {
+  int nc = t->nc, hnc = nc / 2, co[3];
+  int p_id = B(t, id)->parent, p_nb_id = B(t, p_id)->neighbors[nb - 1];
+  child_offset(t, id, 0, co);
+  double *cp = ccb(t, iv, p_nb_id), *c = ccb(t, iv, id);
+  int tw = hnc + 2;
+  double tmp[(64 / 2 + 2) * (64 / 2 + 2) * 4];
+  double gc[64 * 64 * 4];
+#define TMP(a, b) tmp[(b) * tw + (a)]
+#define GC(a, b) gc[((b)-1) * nc + ((a)-1)]
+  for (int b = 0; b <= hnc + 1; b++)
+    for (int a = 0; a <= hnc + 1; a++) {
+      double v = 0;
+      switch (nb) {
+      case 1: v = cp[IX(t, nc, co[1] + a, co[2] + b)]; break;
+      case 2: v = cp[IX(t, 1, co[1] + a, co[2] + b)]; break;
+      case 3: v = cp[IX(t, co[0] + a, nc, co[2] + b)]; break;
+      case 4: v = cp[IX(t, co[0] + a, 1, co[2] + b)]; break;
+      case 5: v = cp[IX(t, co[0] + a, co[1] + b, nc)]; break;
+      case 6: v = cp[IX(t, co[0] + a, co[1] + b, 1)]; break;
+      }
+      TMP(a, b) = v;
+    }
+  for (int j = 1; j <= hnc; j++)
+    for (int i = 1; i <= hnc; i++) {
+      double g1 = 0.125 * (TMP(i + 1, j) - TMP(i - 1, j));
+      double g2 = 0.125 * (TMP(i, j + 1) - TMP(i, j - 1));
+      GC(2 * i - 1, 2 * j - 1) = TMP(i, j) - g1 - g2;
+      GC(2 * i, 2 * j - 1) = TMP(i, j) + g1 - g2;
+      GC(2 * i - 1, 2 * j) = TMP(i, j) - g1 + g2;
+      GC(2 * i, 2 * j) = TMP(i, j) + g1 + g2;
+    }
+  int ix = nb_low(nb) ? 1 : nc, di = nb_low(nb) ? 1 : -1;
+  switch (nb_dim(nb)) {
+  case 0:
+    for (int k = 1; k <= nc; k++)
+      for (int j = 1; j <= nc; j++)
+        c[IX(t, ix - di, j, k)] = 0.5 * GC(j, k) + 0.75 * c[IX(t, ix, j, k)] -
+                                  0.25 * c[IX(t, ix + di, j, k)];
+    break;
+  case 1:
+    for (int k = 1; k <= nc; k++)
+      for (int i = 1; i <= nc; i++)
+        c[IX(t, i, ix - di, k)] = 0.5 * GC(i, k) + 0.75 * c[IX(t, i, ix, k)] -
+                                  0.25 * c[IX(t, i, ix + di, k)];
+    break;
+  case 2:
+    for (int j = 1; j <= nc; j++)
+      for (int i = 1; i <= nc; i++)
+        c[IX(t, i, j, ix - di)] = 0.5 * GC(i, j) + 0.75 * c[IX(t, i, j, ix)] -
+                                  0.25 * c[IX(t, i, j, ix + di)];
+    break;
+  }
+#undef TMP
+#undef GC
+}
+
+/* af_gc_interp / af_gc_interp_lim, m_af_ghostcell.f90:394-612 (3D) */
+static void gc_interp(afh_tree *t, int id, int nb, int iv, int lim) {
+  const double third = 1 / 3.0, sixth = 1 / 6.0;
+  int nc = t->nc, off[3];
+  int p_id = B(t, id)->parent, p_nb_id = B(t, p_id)->neighbors[nb - 1];
+  child_offset(t, id, nb, off);
+  double *cp = ccb(t, iv, p_nb_id), *c = ccb(t, iv, id);
+  int ix, ix_f, ix_c;
+  if (nb_low(nb)) ix = 0, ix_f = 1, ix_c = nc;
+  else ix = nc + 1, ix_f = nc, ix_c = 1;
+  for (int b = 1; b <= nc; b++) {
+    for (int a = 1; a <= nc; a++) {
+      double c1, c2, c3, cf;
+      size_t dst;
+      int a1, a2, b1, b2;
+      /* a runs over the first tangential dim, b over the second */
+      int d = nb_dim(nb);
+      int ta = (d == 0) ? 1 : 0, tb = (d == 2) ? 1 : 2;
+      a1 = off[ta] + ((a + 1) >> 1);
+      a2 = a1 + 1 - 2 * (a & 1);
+      b1 = off[tb] + ((b + 1) >> 1);
+      b2 = b1 + 1 - 2 * (b & 1);
+      if (d == 0) {
+        c1 = cp[IX(t, ix_c, a1, b1)];
+        c2 = cp[IX(t, ix_c, a2, b1)];
+        c3 = cp[IX(t, ix_c, a1, b2)];
+        cf = c[IX(t, ix_f, a, b)];
+        dst = IX(t, ix, a, b);
+      } else if (d == 1) {
+        c1 = cp[IX(t, a1, ix_c, b1)];
+        c2 = cp[IX(t, a2, ix_c, b1)];
+        c3 = cp[IX(t, a1, ix_c, b2)];
+        cf = c[IX(t, a, ix_f, b)];
+        dst = IX(t, a, ix, b);
+      } else {
+        /* case (3): c(2) uses j_c2, c(3) uses i_c2 (m_af_ghostcell.f90:479-482) */
+        c1 = cp[IX(t, a1, b1, ix_c)];
+        c2 = cp[IX(t, a1, b2, ix_c)];
+        c3 = cp[IX(t, a2, b1, ix_c)];
+        cf = c[IX(t, a, b, ix_f)];
+        dst = IX(t, a, b, ix);
+      }
+      double v = third * c1 + sixth * c2 + sixth * c3 + third * cf;
+      if (lim && v > 2 * c1) v = 2 * c1;
+      c[dst] = v;
+    }
+  }
+}
+
+/* af_edge_gc_extrap, m_af_ghostcell.f90:895-924 */
+static void edge_extrap(afh_tree *t, int id, const int lo[3], int dim, int iv) {
+  double *c = ccb(t, iv, id);
+  int o1 = dim % 3, o2 = (dim + 1) % 3; /* 1 + mod(dim, 3) with 1-based dim */
+  /* dim here is 0-based: o_dims = [1+mod(dim1,3), 1+mod(dim1+1,3)] with
+   * dim1 = dim+1 gives 0-based (dim+1)%3 and (dim+2)%3 */
+  o1 = (dim + 1) % 3;
+  o2 = (dim + 2) % 3;
+  int di[3];
+  for (int d = 0; d < 3; d++) di[d] = 1 - 2 * (lo[d] & 1);
+  di[dim] = 0;
+  int ia[3] = {lo[0], lo[1], lo[2]}, ib[3] = {lo[0], lo[1], lo[2]}, ic[3],
+      x[3] = {lo[0], lo[1], lo[2]};
+  ia[o1] += di[o1];
+  ib[o2] += di[o2];
+  for (int d = 0; d < 3; d++) ic[d] = lo[d] + di[d];
+  for (int n = 1; n <= t->nc; n++) {
+    ia[dim] = ib[dim] = ic[dim] = x[dim] = n;
+    c[IX(t, x[0], x[1], x[2])] = c[IX(t, ia[0], ia[1], ia[2])] +
+                                 c[IX(t, ib[0], ib[1], ib[2])] -
+                                 c[IX(t, ic[0], ic[1], ic[2])];
+  }
+}
+
+/* af_corner_gc_extrap, m_af_ghostcell.f90:860-889 (3D) */
+static void corner_extrap(afh_tree *t, int id, const int x[3], int iv) {
+  double *c = ccb(t, iv, id);
+  int di[3];
+  for (int d = 0; d < 3; d++) di[d] = 1 - 2 * (x[d] & 1);
+  c[IX(t, x[0], x[1], x[2])] =
+      c[IX(t, x[0], x[1] + di[1], x[2] + di[2])] +
+      c[IX(t, x[0] + di[0], x[1], x[2] + di[2])] +
+      c[IX(t, x[0] + di[0], x[1] + di[1], x[2])] -
+      2 * c[IX(t, x[0] + di[0], x[1] + di[1], x[2] + di[2])];
+}
+
+/* af_gc_box_corner, m_af_ghostcell.f90:125-170 */
+static void gc_box_corner(afh_tree *t, int id, int iv) {
+  int nc = t->nc;
+  for (int n = 0; n < 12; n++) {
+    int dim = edge_dim[n] - 1, lo[3], hi[3], dnb[3] = {0, 0, 0};
+    int nb_id = nmat(t, id, edge_dir[n][0], edge_dir[n][1], edge_dir[n][2]);
+    for (int d = 0; d < 3; d++) lo[d] = edge_min_ix[n][d] * (nc + 1);
+    lo[dim] = 1;
+    if (nb_id > 0) {
+      for (int d = 0; d < 3; d++) hi[d] = lo[d];
+      hi[dim] = nc;
+      for (int q = 0; q < 2; q++) {
+        int nb = nb_adj_edge[n][q];
+        dnb[nb_dim(nb)] += nb_pm(nb);
+      }
+      copy_from_nb(t, id, nb_id, dnb, lo, hi, iv);
+    } else {
+      edge_extrap(t, id, lo, dim, iv);
+    }
+  }
+  for (int n = 0; n < 8; n++) {
+    int dnb[3], lo[3];
+    for (int d = 0; d < 3; d++) {
+      dnb[d] = 2 * child_dix[n][d] - 1;
+      lo[d] = child_dix[n][d] * (nc + 1);
+    }
+    int nb_id = nmat(t, id, dnb[0], dnb[1], dnb[2]);
+    if (nb_id > 0) copy_from_nb(t, id, nb_id, dnb, lo, lo, iv);
+    else corner_extrap(t, id, lo, iv);
+  }
+}
+
+/* af_gc_box, m_af_ghostcell.f90:64-120 */
+static void gc_box(afh_tree *t, int id, int iv, int corners) {
+  int nc = t->nc;
+  cc_method *m = &t->meth[iv];
+  for (int nb = 1; nb <= 6; nb++) {
+    int nb_id = B(t, id)->neighbors[nb - 1];
+    if (nb_id > 0) {
+      int lo[3] = {1, 1, 1}, hi[3] = {nc, nc, nc}, dnb[3] = {0, 0, 0};
+      int d = nb_dim(nb);
+      lo[d] = hi[d] = nb_low(nb) ? 0 : nc + 1;
+      dnb[d] = nb_pm(nb);
+      copy_from_nb(t, id, nb_id, dnb, lo, hi, iv);
+    } else if (nb_id == 0) {
+      if (m->rb == AFH_RB_MG_SIDES) mg_sides_rb(t, id, nb, iv);
+      else gc_interp(t, id, nb, iv, m->rb == AFH_RB_GC_INTERP_LIM);
+    } else {
+      bc_to_gc(t, id, nb, iv, &m->bc[nb - 1]);
+    }
+  }
+  if (corners) gc_box_corner(t, id, iv);
+}
+
+static void gc_lvl(afh_tree *t, int lvl, int iv, int corners) {
+  int n = LVL_N(t, ids, lvl);
+#pragma omp parallel for schedule(static)
+  for (int i = 0; i < n; i++) gc_box(t, LVL_AT(t, ids, lvl, i), iv, corners);
+}
+
+int32_t afo_gc_lvl(afh_tree *t, int32_t lvl, int32_t iv, int32_t corners) {
+  if (lvl < 1 || lvl > t->nlvl || iv < 1 || iv > t->nvc || !t->meth[iv].set)
+    return fail(AFH_ERR_ARG, "afo_gc_lvl: bad argument / no methods");
+  gc_lvl(t, lvl, iv, corners);
+  return AFH_OK;
+}
+int32_t afo_gc_tree(afh_tree *t, int32_t iv, int32_t corners) {
+  for (int l = 1; l <= t->nlvl; l++) {
+    int32_t e = afo_gc_lvl(t, l, iv, corners);
+    if (e) return e;
+  }
+  return AFH_OK;
+}
+
+/* -------------------------------------------------------- restriction */
+
+/* af_restrict_box, m_af_restrict.f90:62-136 (3D): 0.125 * sum over the 2^3
+ * children in column-major element order */
+static void restrict_box(afh_tree *t, int c_id, int p_id, int iv) {
+  int hnc = t->nc / 2, off[3];
+  child_offset(t, c_id, 0, off);
+  double *c = ccb(t, iv, c_id), *p = ccb(t, iv, p_id);
+  for (int k = 1; k <= hnc; k++)
+    for (int j = 1; j <= hnc; j++)
+      for (int i = 1; i <= hnc; i++) {
+        int fi = 2 * i - 1, fj = 2 * j - 1, fk = 2 * k - 1;
+        double s = c[IX(t, fi, fj, fk)];
+        s += c[IX(t, fi + 1, fj, fk)];
+        s += c[IX(t, fi, fj + 1, fk)];
+        s += c[IX(t, fi + 1, fj + 1, fk)];
+        s += c[IX(t, fi, fj, fk + 1)];
+        s += c[IX(t, fi + 1, fj, fk + 1)];
+        s += c[IX(t, fi, fj + 1, fk + 1)];
+        s += c[IX(t, fi + 1, fj + 1, fk + 1)];
+        p[IX(t, off[0] + i, off[1] + j, off[2] + k)] = 0.125 * s;
+      }
+}
+
+int32_t afo_restrict_tree(afh_tree *t, int32_t iv) {
+  /* af_restrict_tree -> af_restrict_to_boxes over parents per level */
+  for (int l = t->nlvl - 1; l >= 1; l--) {
+    int n = LVL_N(t, parents, l);
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i < n; i++) {
+      int id = LVL_AT(t, parents, l, i);
+      for (int c = 0; c < 8; c++) {
+        int cid = B(t, id)->children[c];
+        if (cid > 0) restrict_box(t, cid, id, iv);
+      }
+    }
+  }
+  return AFH_OK;
+}
+
+int32_t afo_tree_copy_cc(afh_tree *t, int32_t a, int32_t b) {
+  memcpy(ccb(t, b, 1), ccb(t, a, 1), sizeof(double) * t->bsz * t->nb);
+  return AFH_OK;
+}
+
+/* af_tree_maxabs_cc over leaf interiors, m_af_utils.f90:773-784, 852-862 */
+int32_t afo_tree_maxabs_cc(afh_tree *t, int32_t iv, double *out) {
+  double mx = -HUGE_VAL;
+  int nc = t->nc;
+  for (int l = 1; l <= t->nlvl; l++)
+    for (int i = 0; i < LVL_N(t, leaves, l); i++) {
+      double *c = ccb(t, iv, LVL_AT(t, leaves, l, i));
+      for (int k = 1; k <= nc; k++)
+        for (int j = 1; j <= nc; j++)
+          for (int ii = 1; ii <= nc; ii++) {
+            double v = fabs(c[IX(t, ii, j, k)]);
+            if (v > mx) mx = v;
+          }
+    }
+  *out = mx;
+  return AFH_OK;
+}
+
+/* ------------------------------------------------------------ multigrid */
+
+/* stencil_apply_357, m_af_stencil.f90:445-457 (constant stencil) */
+static void apply_357(afh_tree *t, int id, const double *cf, int iv,
+                      int i_out) {
+  double *x = ccb(t, iv, id), *o = ccb(t, i_out, id);
+  int nc = t->nc;
+  for (int k = 1; k <= nc; k++)
+    for (int j = 1; j <= nc; j++)
+      for (int i = 1; i <= nc; i++)
+        o[IX(t, i, j, k)] =
+            cf[0] * x[IX(t, i, j, k)] + cf[1] * x[IX(t, i - 1, j, k)] +
+            cf[2] * x[IX(t, i + 1, j, k)] + cf[3] * x[IX(t, i, j - 1, k)] +
+            cf[4] * x[IX(t, i, j + 1, k)] + cf[5] * x[IX(t, i, j, k - 1)] +
+            cf[6] * x[IX(t, i, j, k + 1)];
+}
+
+/* stencil_gsrb_357, m_af_stencil.f90:938-955 (constant stencil) */
+static void gsrb_357(afh_tree *t, int id, const double *cf, int redblack,
+                     int iv, int i_rhs) {
+  double *x = ccb(t, iv, id), *r = ccb(t, i_rhs, id);
+  double inv_c1 = 1 / cf[0];
+  int nc = t->nc;
+  for (int k = 1; k <= nc; k++)
+    for (int j = 1; j <= nc; j++) {
+      int i0 = 2 - ((redblack ^ (k + j)) & 1);
+      for (int i = i0; i <= nc; i += 2)
+        x[IX(t, i, j, k)] =
+            (r[IX(t, i, j, k)] - cf[1] * x[IX(t, i - 1, j, k)] -
+             cf[2] * x[IX(t, i + 1, j, k)] - cf[3] * x[IX(t, i, j - 1, k)] -
+             cf[4] * x[IX(t, i, j + 1, k)] - cf[5] * x[IX(t, i, j, k - 1)] -
+             cf[6] * x[IX(t, i, j, k + 1)]) *
+            inv_c1;
+    }
+}
+
+/* stencil_prolong_248 with add = .true., m_af_stencil.f90:749-771 */
+static void prolong_248_add(afh_tree *t, int p_id, int c_id, int iv,
+                            int iv_to) {
+  static const double w[8] = {27 / 64.0, 9 / 64.0, 9 / 64.0, 3 / 64.0,
+                              9 / 64.0,  3 / 64.0, 3 / 64.0, 1 / 64.0};
+  int nc = t->nc, off[3];
+  child_offset(t, c_id, 0, off);
+  double *p = ccb(t, iv, p_id), *c = ccb(t, iv_to, c_id);
+  for (int k = 1; k <= nc; k++) {
+    int k1 = off[2] + ((k + 1) >> 1), k2 = k1 + 1 - 2 * (k & 1);
+    for (int j = 1; j <= nc; j++) {
+      int j1 = off[1] + ((j + 1) >> 1), j2 = j1 + 1 - 2 * (j & 1);
+      for (int i = 1; i <= nc; i++) {
+        int i1 = off[0] + ((i + 1) >> 1), i2 = i1 + 1 - 2 * (i & 1);
+        c[IX(t, i, j, k)] =
+            c[IX(t, i, j, k)] + w[0] * p[IX(t, i1, j1, k1)] +
+            w[1] * p[IX(t, i2, j1, k1)] + w[2] * p[IX(t, i1, j2, k1)] +
+            w[3] * p[IX(t, i2, j2, k1)] + w[4] * p[IX(t, i1, j1, k2)] +
+            w[5] * p[IX(t, i2, j1, k2)] + w[6] * p[IX(t, i1, j2, k2)] +
+            w[7] * p[IX(t, i2, j2, k2)];
+      }
+    }
+  }
+}
+
+static double *lvl_coeffs(afh_mg *mg, int lvl) { return mg->lvl_c + 7 * (lvl - 1); }
+
+/* residual_box, m_af_multigrid.f90:801-810 */
+static void residual_box(afh_mg *mg, int id) {
+  afh_tree *t = mg->t;
+  int nc = t->nc;
+  apply_357(t, id, lvl_coeffs(mg, B(t, id)->lvl), mg->d.i_phi, mg->d.i_tmp);
+  double *o = ccb(t, mg->d.i_tmp, id), *r = ccb(t, mg->d.i_rhs, id);
+  for (int k = 1; k <= nc; k++)
+    for (int j = 1; j <= nc; j++)
+      for (int i = 1; i <= nc; i++)
+        o[IX(t, i, j, k)] = r[IX(t, i, j, k)] - o[IX(t, i, j, k)];
+}
+
+/* gsrb_boxes, m_af_multigrid.f90:648-687 */
+int32_t afo_mg_gsrb_boxes(afh_mg *mg, int32_t lvl, int32_t up) {
+  afh_tree *t = mg->t;
+  int n_cycle = up ? mg->d.n_cycle_up : mg->d.n_cycle_down;
+  int nid = LVL_N(t, ids, lvl);
+  const double *cf = lvl_coeffs(mg, lvl);
+  for (int n = 1; n <= 2 * n_cycle; n++) {
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i < nid; i++)
+      gsrb_357(t, LVL_AT(t, ids, lvl, i), cf, n, mg->d.i_phi, mg->d.i_rhs);
+    int use_corners = up && n == 2 * n_cycle;
+    gc_lvl(t, lvl, mg->d.i_phi, use_corners);
+  }
+  return AFH_OK;
+}
+
+/* update_coarse, m_af_multigrid.f90:691-738 */
+int32_t afo_mg_update_coarse(afh_mg *mg, int32_t lvl) {
+  afh_tree *t = mg->t;
+  int nc = t->nc, nid = LVL_N(t, ids, lvl);
+  size_t bsz = t->bsz;
+  int i_phi = mg->d.i_phi, i_tmp = mg->d.i_tmp, i_rhs = mg->d.i_rhs;
+#pragma omp parallel
+  {
+    double *save = malloc(sizeof(double) * bsz);
+#pragma omp for schedule(static)
+    for (int i = 0; i < nid; i++) {
+      int id = LVL_AT(t, ids, lvl, i), p_id = B(t, id)->parent;
+      memcpy(save, ccb(t, i_tmp, id), sizeof(double) * bsz);
+      residual_box(mg, id);
+      restrict_box(t, id, p_id, i_tmp);
+      restrict_box(t, id, p_id, i_phi);
+      /* restore interior of tmp (ghosts were untouched) */
+      memcpy(ccb(t, i_tmp, id), save, sizeof(double) * bsz);
+    }
+    free(save);
+  }
+  (void)nc;
+  gc_lvl(t, lvl - 1, i_phi, 1);
+  int np = LVL_N(t, parents, lvl - 1);
+  const double *cf = lvl_coeffs(mg, lvl - 1);
+#pragma omp parallel for schedule(static)
+  for (int i = 0; i < np; i++) {
+    int id = LVL_AT(t, parents, lvl - 1, i);
+    apply_357(t, id, cf, i_phi, i_rhs);
+    double *r = ccb(t, i_rhs, id), *tm = ccb(t, i_tmp, id), *p = ccb(t, i_phi, id);
+    for (size_t q = 0; q < bsz; q++) r[q] = r[q] + tm[q];
+    for (size_t q = 0; q < bsz; q++) tm[q] = p[q];
+  }
+  return AFH_OK;
+}
+
+/* correct_children, m_af_multigrid.f90:624-646 (correct children of the
+ * parents of level lvl-1, i.e. boxes of level lvl) */
+int32_t afo_mg_correct_children(afh_mg *mg, int32_t lvl) {
+  afh_tree *t = mg->t;
+  int np = LVL_N(t, parents, lvl - 1);
+  size_t bsz = t->bsz;
+#pragma omp parallel for schedule(static)
+  for (int i = 0; i < np; i++) {
+    int id = LVL_AT(t, parents, lvl - 1, i);
+    double *tm = ccb(t, mg->d.i_tmp, id), *p = ccb(t, mg->d.i_phi, id);
+    for (size_t q = 0; q < bsz; q++) tm[q] = p[q] - tm[q];
+    for (int c = 0; c < 8; c++) {
+      int cid = B(t, id)->children[c];
+      if (cid == 0) continue;
+      prolong_248_add(t, id, cid, mg->d.i_tmp, mg->d.i_phi);
+    }
+  }
+  return AFH_OK;
+}
+
+
+/* ---- coarse-grid solver (OUR algorithm; the reference calls HYPRE PFMG,
+ * absent from the snapshot). The level-1 grid (coarse_grid_size cells) is
+ * solved by V(2,2) multigrid cycles with red-black Gauss-Seidel, boundary
+ * conditions folded into the operator exactly as stencil_handle_boundaries /
+ * coarse_solver_set_rhs_phi do (m_coarse_solver.f90:286-338, 442-491),
+ * 8-cell average restriction and trilinear (27,9,9,3,9,3,3,1)/64
+ * prolongation with ghost values reflected through the homogeneous BCs.
+ * The HIP library implements the same arithmetic in the same order. */
+#define GIX(mg, m, i, j, k)                                                   \
+  ((((size_t)(k)) * ((mg)->dims[m][1] + 2) + (size_t)(j)) *                   \
+       ((mg)->dims[m][0] + 2) +                                               \
+   (size_t)(i))
+
+static inline double cs_diag(afh_mg *mg, int m, int i, int j, int k) {
+  afh_tree *t = mg->t;
+  const afh_bc *bc = t->meth[mg->d.i_phi].bc;
+  int idx[3] = {i, j, k};
+  double d = mg->cdiag[m];
+  for (int nb = 1; nb <= 6; nb++) {
+    int dd = nb_dim(nb);
+    int at = nb_low(nb) ? (idx[dd] == 1) : (idx[dd] == mg->dims[m][dd]);
+    if (!at) continue;
+    if (bc[nb - 1].type == AFH_BC_DIRICHLET) d = d - mg->hc[m][dd];
+    else d = d + mg->hc[m][dd];
+  }
+  return d;
+}
+
+/* one red-black half sweep on MG level m */
+static void cs_gsrb(afh_mg *mg, int m, int n) {
+  double *u = mg->u[m], *f = mg->f[m];
+  int nx = mg->dims[m][0], ny = mg->dims[m][1], nz = mg->dims[m][2];
+  const double *h = mg->hc[m];
+  for (int k = 1; k <= nz; k++)
+    for (int j = 1; j <= ny; j++) {
+      int i0 = 2 - ((n ^ (k + j)) & 1);
+      for (int i = i0; i <= nx; i += 2) {
+        double s = f[GIX(mg, m, i, j, k)];
+        if (i > 1) s = s - h[0] * u[GIX(mg, m, i - 1, j, k)];
+        if (i < nx) s = s - h[0] * u[GIX(mg, m, i + 1, j, k)];
+        if (j > 1) s = s - h[1] * u[GIX(mg, m, i, j - 1, k)];
+        if (j < ny) s = s - h[1] * u[GIX(mg, m, i, j + 1, k)];
+        if (k > 1) s = s - h[2] * u[GIX(mg, m, i, j, k - 1)];
+        if (k < nz) s = s - h[2] * u[GIX(mg, m, i, j, k + 1)];
+        u[GIX(mg, m, i, j, k)] = s / cs_diag(mg, m, i, j, k);
+      }
+    }
+}
+
+/* residual on level m restricted (8-cell mean) into f[m+1]; u[m+1] = 0 */
+static void cs_residual_restrict(afh_mg *mg, int m) {
+  double *u = mg->u[m], *f = mg->f[m], *r = mg->r[m];
+  int nx = mg->dims[m][0], ny = mg->dims[m][1], nz = mg->dims[m][2];
+  const double *h = mg->hc[m];
+  for (int k = 1; k <= nz; k++)
+    for (int j = 1; j <= ny; j++)
+      for (int i = 1; i <= nx; i++) {
+        double a = cs_diag(mg, m, i, j, k) * u[GIX(mg, m, i, j, k)];
+        if (i > 1) a = a + h[0] * u[GIX(mg, m, i - 1, j, k)];
+        if (i < nx) a = a + h[0] * u[GIX(mg, m, i + 1, j, k)];
+        if (j > 1) a = a + h[1] * u[GIX(mg, m, i, j - 1, k)];
+        if (j < ny) a = a + h[1] * u[GIX(mg, m, i, j + 1, k)];
+        if (k > 1) a = a + h[2] * u[GIX(mg, m, i, j, k - 1)];
+        if (k < nz) a = a + h[2] * u[GIX(mg, m, i, j, k + 1)];
+        r[GIX(mg, m, i, j, k)] = f[GIX(mg, m, i, j, k)] - a;
+      }
+  int c = m + 1;
+  double *fc = mg->f[c], *uc = mg->u[c];
+  for (int k = 1; k <= mg->dims[c][2]; k++)
+    for (int j = 1; j <= mg->dims[c][1]; j++)
+      for (int i = 1; i <= mg->dims[c][0]; i++) {
+        int fi = 2 * i - 1, fj = 2 * j - 1, fk = 2 * k - 1;
+        double s = r[GIX(mg, m, fi, fj, fk)];
+        s += r[GIX(mg, m, fi + 1, fj, fk)];
+        s += r[GIX(mg, m, fi, fj + 1, fk)];
+        s += r[GIX(mg, m, fi + 1, fj + 1, fk)];
+        s += r[GIX(mg, m, fi, fj, fk + 1)];
+        s += r[GIX(mg, m, fi + 1, fj, fk + 1)];
+        s += r[GIX(mg, m, fi, fj + 1, fk + 1)];
+        s += r[GIX(mg, m, fi + 1, fj + 1, fk + 1)];
+        fc[GIX(mg, c, i, j, k)] = 0.125 * s;
+        uc[GIX(mg, c, i, j, k)] = 0.0;
+      }
+}
+
+/* value of u[c] at (i,j,k), reflecting through homogeneous BCs outside */
+static inline double cs_refl(afh_mg *mg, int c, int i, int j, int k) {
+  const afh_bc *bc = mg->t->meth[mg->d.i_phi].bc;
+  double s = 1.0;
+  int idx[3] = {i, j, k};
+  for (int d = 0; d < 3; d++) {
+    if (idx[d] < 1) {
+      idx[d] = 1;
+      if (bc[2 * d].type == AFH_BC_DIRICHLET) s = -s;
+    } else if (idx[d] > mg->dims[c][d]) {
+      idx[d] = mg->dims[c][d];
+      if (bc[2 * d + 1].type == AFH_BC_DIRICHLET) s = -s;
+    }
+  }
+  return s * mg->u[c][GIX(mg, c, idx[0], idx[1], idx[2])];
+}
+
+static void cs_prolong_add(afh_mg *mg, int m) {
+  static const double w[8] = {27 / 64.0, 9 / 64.0, 9 / 64.0, 3 / 64.0,
+                              9 / 64.0,  3 / 64.0, 3 / 64.0, 1 / 64.0};
+  int c = m + 1;
+  double *u = mg->u[m];
+  for (int k = 1; k <= mg->dims[m][2]; k++) {
+    int k1 = (k + 1) >> 1, k2 = k1 + 1 - 2 * (k & 1);
+    for (int j = 1; j <= mg->dims[m][1]; j++) {
+      int j1 = (j + 1) >> 1, j2 = j1 + 1 - 2 * (j & 1);
+      for (int i = 1; i <= mg->dims[m][0]; i++) {
+        int i1 = (i + 1) >> 1, i2 = i1 + 1 - 2 * (i & 1);
+        u[GIX(mg, m, i, j, k)] =
+            u[GIX(mg, m, i, j, k)] + w[0] * cs_refl(mg, c, i1, j1, k1) +
+            w[1] * cs_refl(mg, c, i2, j1, k1) + w[2] * cs_refl(mg, c, i1, j2, k1) +
+            w[3] * cs_refl(mg, c, i2, j2, k1) + w[4] * cs_refl(mg, c, i1, j1, k2) +
+            w[5] * cs_refl(mg, c, i2, j1, k2) + w[6] * cs_refl(mg, c, i1, j2, k2) +
+            w[7] * cs_refl(mg, c, i2, j2, k2);
+      }
+    }
+  }
+}
+
+static void cs_cycle(afh_mg *mg, int m) {
+  if (m == mg->n_mg - 1) {
+    for (int it = 0; it < AFH_CS_BOTTOM_SWEEPS; it++) {
+      cs_gsrb(mg, m, 1);
+      cs_gsrb(mg, m, 2);
+    }
+    return;
+  }
+  for (int s = 0; s < 2; s++) {
+    cs_gsrb(mg, m, 1);
+    cs_gsrb(mg, m, 2);
+  }
+  cs_residual_restrict(mg, m);
+  cs_cycle(mg, m + 1);
+  cs_prolong_add(mg, m);
+  for (int s = 0; s < 2; s++) {
+    cs_gsrb(mg, m, 1);
+    cs_gsrb(mg, m, 2);
+  }
+}
+
+/* solve_coarse_grid, m_af_multigrid.f90:266-291 */
+int32_t afo_mg_solve_coarse(afh_mg *mg) {
+  afh_tree *t = mg->t;
+  int nc = t->nc, nid = LVL_N(t, ids, 1);
+  const afh_bc *bc = t->meth[mg->d.i_phi].bc;
+  /* coarse_solver_set_rhs_phi: gather rhs (+ BC contributions) and phi */
+  for (int q = 0; q < nid; q++) {
+    int id = LVL_AT(t, ids, 1, q);
+    double *p = ccb(t, mg->d.i_phi, id), *r = ccb(t, mg->d.i_rhs, id);
+    int o[3];
+    for (int d = 0; d < 3; d++) o[d] = (B(t, id)->ix[d] - 1) * nc;
+    for (int k = 1; k <= nc; k++)
+      for (int j = 1; j <= nc; j++)
+        for (int i = 1; i <= nc; i++) {
+          size_t g = GIX(mg, 0, o[0] + i, o[1] + j, o[2] + k);
+          double rv = r[IX(t, i, j, k)];
+          int gi[3] = {o[0] + i, o[1] + j, o[2] + k};
+          for (int nb = 1; nb <= 6; nb++) {
+            int dd = nb_dim(nb);
+            int at = nb_low(nb) ? (gi[dd] == 1) : (gi[dd] == mg->dims[0][dd]);
+            if (!at) continue;
+            double cnb = mg->hc[0][dd], b2r;
+            if (bc[nb - 1].type == AFH_BC_DIRICHLET) b2r = -2 * cnb;
+            else b2r = -(cnb * B(t, id)->dr[dd]) * nb_pm(nb);
+            rv = rv + b2r * bc[nb - 1].value;
+          }
+          mg->f[0][g] = rv;
+          mg->u[0][g] = p[IX(t, i, j, k)];
+        }
+  }
+  for (int c = 0; c < mg->d.coarse_cycles; c++) cs_cycle(mg, 0);
+  /* coarse_solver_get_phi */
+  for (int q = 0; q < nid; q++) {
+    int id = LVL_AT(t, ids, 1, q);
+    double *p = ccb(t, mg->d.i_phi, id);
+    int o[3];
+    for (int d = 0; d < 3; d++) o[d] = (B(t, id)->ix[d] - 1) * nc;
+    for (int k = 1; k <= nc; k++)
+      for (int j = 1; j <= nc; j++)
+        for (int i = 1; i <= nc; i++)
+          p[IX(t, i, j, k)] = mg->u[0][GIX(mg, 0, o[0] + i, o[1] + j, o[2] + k)];
+  }
+  gc_lvl(t, 1, mg->d.i_phi, 1);
+  return AFH_OK;
+}
+
+/* mg_init minus HYPRE (m_af_multigrid.f90:43-109); mg_box_lpl_stencil
+ * (1227-1245): c(2:7) = 1/dr^2, c(1) = -sum(c(2:)) - lambda */
+int32_t afo_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
+  if (!t->meth[d->i_phi].set)
+    return fail(AFH_ERR_STATE, "set cc methods (bc) for phi first");
+  afh_mg *mg = calloc(1, sizeof *mg);
+  mg->t = t;
+  mg->d = *d;
+  mg->lvl_c = malloc(sizeof(double) * 7 * t->nlvl);
+  for (int l = 1; l <= t->nlvl; l++) {
+    int id = LVL_AT(t, ids, l, 0);
+    double *c = mg->lvl_c + 7 * (l - 1);
+    for (int dd = 0; dd < 3; dd++) {
+      double dr = B(t, id)->dr[dd];
+      double inv = 1 / (dr * dr);
+      c[1 + 2 * dd] = inv;
+      c[2 + 2 * dd] = inv;
+    }
+    double s = c[1];
+    for (int q = 2; q < 7; q++) s = s + c[q];
+    c[0] = -s - d->helmholtz_lambda;
+  }
+  /* coarse hierarchy */
+  int m = 0;
+  for (int dd = 0; dd < 3; dd++) mg->dims[0][dd] = t->cgs[dd];
+  mg->cdiag[0] = mg->lvl_c[0];
+  for (int dd = 0; dd < 3; dd++) mg->hc[0][dd] = mg->lvl_c[1 + 2 * dd];
+  for (;;) {
+    int *n = mg->dims[m];
+    int ok = (n[0] % 2 == 0) && (n[1] % 2 == 0) && (n[2] % 2 == 0) &&
+             n[0] >= 4 && n[1] >= 4 && n[2] >= 4 && m < 15;
+    if (!ok) break;
+    for (int dd = 0; dd < 3; dd++) {
+      mg->dims[m + 1][dd] = n[dd] / 2;
+      mg->hc[m + 1][dd] = 0.25 * mg->hc[m][dd];
+    }
+    const double *h = mg->hc[m + 1];
+    mg->cdiag[m + 1] = -(h[0] + h[0] + h[1] + h[1] + h[2] + h[2]) -
+                       d->helmholtz_lambda;
+    m++;
+  }
+  mg->n_mg = m + 1;
+  for (int q = 0; q < mg->n_mg; q++) {
+    size_t n = (size_t)(mg->dims[q][0] + 2) * (mg->dims[q][1] + 2) *
+               (mg->dims[q][2] + 2);
+    mg->u[q] = calloc(n, sizeof(double));
+    mg->f[q] = calloc(n, sizeof(double));
+    mg->r[q] = calloc(n, sizeof(double));
+  }
+  *out = mg;
+  return AFH_OK;
+}
+
+int32_t afo_mg_destroy(afh_mg *mg) {
+  if (!mg) return AFH_OK;
+  for (int q = 0; q < mg->n_mg; q++) free(mg->u[q]), free(mg->f[q]), free(mg->r[q]);
+  free(mg->lvl_c);
+  free(mg);
+  return AFH_OK;
+}
+
+/* mg_fas_vcycle, m_af_multigrid.f90:185-264 (subtract_mean = .false.) */
+int32_t afo_mg_fas_vcycle(afh_mg *mg, int32_t set_residual, int32_t hl) {
+  afh_tree *t = mg->t;
+  int max_lvl = (hl > 0) ? hl : t->nlvl;
+  for (int lvl = max_lvl; lvl >= 2; lvl--) {
+    afo_mg_gsrb_boxes(mg, lvl, 0);
+    afo_mg_update_coarse(mg, lvl);
+  }
+  afo_mg_solve_coarse(mg);
+  for (int lvl = 2; lvl <= max_lvl; lvl++) {
+    afo_mg_correct_children(mg, lvl);
+    gc_lvl(t, lvl, mg->d.i_phi, 1);
+    afo_mg_gsrb_boxes(mg, lvl, 1);
+  }
+  if (set_residual) {
+    for (int lvl = 1; lvl <= max_lvl; lvl++) {
+      int n = LVL_N(t, ids, lvl);
+#pragma omp parallel for schedule(static)
+      for (int i = 0; i < n; i++) residual_box(mg, LVL_AT(t, ids, lvl, i));
+    }
+  }
+  return AFH_OK;
+}
+
+/* mg_box_lpl_gradient + mg_box_field_norm, m_af_multigrid.f90:1882-2025 */
+int32_t afo_mg_compute_phi_gradient(afh_mg *mg, int32_t i_fc, double fac,
+                                    int32_t i_norm) {
+  afh_tree *t = mg->t;
+  int nc = t->nc;
+  for (int lvl = 1; lvl <= t->nlvl; lvl++) {
+    int n = LVL_N(t, ids, lvl);
+#pragma omp parallel for schedule(static)
+    for (int q = 0; q < n; q++) {
+      int id = LVL_AT(t, ids, lvl, q);
+      double *p = ccb(t, mg->d.i_phi, id), *f = fcb(t, i_fc, id);
+      double inv[3];
+      for (int d = 0; d < 3; d++) inv[d] = fac / B(t, id)->dr[d];
+      for (int k = 1; k <= nc; k++)
+        for (int j = 1; j <= nc; j++)
+          for (int i = 1; i <= nc + 1; i++)
+            f[FX(t, 0, i, j, k)] =
+                inv[0] * (p[IX(t, i, j, k)] - p[IX(t, i - 1, j, k)]);
+      for (int k = 1; k <= nc; k++)
+        for (int j = 1; j <= nc + 1; j++)
+          for (int i = 1; i <= nc; i++)
+            f[FX(t, 1, i, j, k)] =
+                inv[1] * (p[IX(t, i, j, k)] - p[IX(t, i, j - 1, k)]);
+      for (int k = 1; k <= nc + 1; k++)
+        for (int j = 1; j <= nc; j++)
+          for (int i = 1; i <= nc; i++)
+            f[FX(t, 2, i, j, k)] =
+                inv[2] * (p[IX(t, i, j, k)] - p[IX(t, i, j, k - 1)]);
+      if (i_norm > 0) {
+        double *o = ccb(t, i_norm, id);
+        for (int k = 1; k <= nc; k++)
+          for (int j = 1; j <= nc; j++)
+            for (int i = 1; i <= nc; i++) {
+              double a = f[FX(t, 0, i, j, k)] + f[FX(t, 0, i + 1, j, k)];
+              double b = f[FX(t, 1, i, j, k)] + f[FX(t, 1, i, j + 1, k)];
+              double c = f[FX(t, 2, i, j, k)] + f[FX(t, 2, i, j, k + 1)];
+              o[IX(t, i, j, k)] = 0.5 * sqrt(a * a + b * b + c * c);
+            }
+      }
+    }
+  }
+  return AFH_OK;
+}
+
+/* ------------------------------------------------------------ fluid */
+
+int32_t afo_fluid_create(afh_tree *t, const afh_fluid_desc *d,
+                         afh_fluid **out) {
+  if (d->n_species < 1 || d->n_species > AFH_MAX_SPECIES ||
+      d->n_reactions > AFH_MAX_REACTIONS)
+    return fail(AFH_ERR_ARG, "bad species/reaction count");
+  afh_fluid *f = calloc(1, sizeof *f);
+  f->t = t;
+  f->d = *d;
+  size_t ntd = (size_t)d->td.n_points * d->td.n_cols;
+  size_t nch = (size_t)d->chem.n_points * d->chem.n_cols;
+  f->td = malloc(sizeof(double) * (ntd ? ntd : 1));
+  f->chem = malloc(sizeof(double) * (nch ? nch : 1));
+  memcpy(f->td, d->td.rows_cols, sizeof(double) * ntd);
+  if (nch) memcpy(f->chem, d->chem.rows_cols, sizeof(double) * nch);
+  f->d.td.rows_cols = f->td;
+  f->d.chem.rows_cols = f->chem;
+  for (int r = 0; r < d->n_reactions; r++) {
+    f->reac[r] = d->reactions[r];
+    int rt = d->reactions[r].rate_type;
+    if (rt != AFH_RATE_TABULATED_FIELD && rt != AFH_RATE_CONSTANT &&
+        rt != AFH_RATE_LINEAR && rt != AFH_RATE_EXP_V1 && rt != AFH_RATE_EXP_V2)
+      return fail(AFH_ERR_UNSUPPORTED, "reaction rate type %d", rt);
+  }
+  f->d.reactions = f->reac;
+  *out = f;
+  return AFH_OK;
+}
+int32_t afo_fluid_destroy(afh_fluid *f) {
+  if (!f) return AFH_OK;
+  free(f->td), free(f->chem), free(f);
+  return AFH_OK;
+}
+
+/* LT_get_loc + LT_get_col_at_loc (linear spacing, no extrapolation),
+ * src/lookup_table_fortran/m_lookup_table.f90:330-406 */
+static inline double lt_col(const afh_lt *lt, int col, double x) {
+  double frac = (x - lt->x_min) * lt->inv_fac;
+  int low;
+  double lf;
+  if (frac <= 0) {
+    low = 1;
+    lf = 1;
+  } else if (frac >= lt->n_points - 1) {
+    low = lt->n_points - 1;
+    lf = 0;
+  } else {
+    low = (int)ceil(frac);
+    lf = low - frac;
+  }
+  const double *rc = lt->rows_cols + (size_t)(col - 1) * lt->n_points;
+  return lf * rc[low - 1] + (1 - lf) * rc[low];
+}
+
+/* field_set_rhs, src/m_field.f90:363-401 */
+int32_t afo_field_set_rhs(afh_fluid *f, int32_t i_rhs, int32_t s_in) {
+  afh_tree *t = f->t;
+  const double fac = -1.6022e-19 / 8.8541878176e-12;
+  for (int l = 1; l <= t->nlvl; l++) {
+    int n = LVL_N(t, leaves, l);
+#pragma omp parallel for schedule(static)
+    for (int q = 0; q < n; q++) {
+      int id = LVL_AT(t, leaves, l, q);
+      double *r = ccb(t, i_rhs, id);
+      for (size_t x = 0; x < t->bsz; x++) r[x] = 0.0;
+      for (int s = 0; s < f->d.n_species; s++) {
+        if (f->d.species_charge[s] == 0) continue;
+        double qq = f->d.species_charge[s] * fac;
+        double *c = ccb(t, f->d.species_iv[s] + s_in, id);
+        for (size_t x = 0; x < t->bsz; x++) r[x] = r[x] + qq * c[x];
+      }
+    }
+  }
+  return AFH_OK;
+}
+
+/* af_limiter_koren, m_af_limiters.f90:72-95; af_limiter_gminmod
+ * (120-149); vanleer (97-110); none/zero */
+static inline double limiter(int lim, double a, double b) {
+  const double third = 1 / 3.0;
+  switch (lim) {
+  case AFH_LIM_KOREN: {
+    double aa = a * a, ab = a * b;
+    if (ab <= 0) return 0;
+    if (aa <= 0.25 * ab) return 2 * a;
+    if (aa <= 2.5 * ab) return third * (b + 2 * a);
+    return 2 * b;
+  }
+  case AFH_LIM_VANLEER: {
+    double ab = a * b;
+    return ab > 0 ? 2 * ab / (a + b) : 0;
+  }
+  case AFH_LIM_NONE: return 0.5 * (a + b);
+  case AFH_LIM_ZERO: return 0.0;
+  default: {
+    double th = lim == AFH_LIM_MINMOD ? 1.0 : lim == AFH_LIM_MC ? 2.0 : 4 / 3.0;
+    if (a * b > 0) {
+      double x = fabs(th * a), y = fabs(th * b), z = fabs(0.5 * (a + b));
+      double m = x;
+      if (y < m) m = y;
+      if (z < m) m = z;
+      return copysign(m, a);
+    }
+    return 0.0;
+  }
+  }
+}
+
+/* cc2 index for the (nc+4)^3 array with indices -1..nc+2 */
+#define I2(n4, i, j, k) ((((size_t)(k) + 1) * (n4) + (size_t)(j) + 1) * (n4) + (size_t)(i) + 1)
+
+/* bc_to_gc2, m_af_ghostcell.f90:282-375 (incl. the c0 quirk for highy) */
+static void bc_to_gc2(afh_tree *t, int id, double *cc, int nb, const afh_bc *bc) {
+  int nc = t->nc, n4 = nc + 4, d = nb_dim(nb);
+  double c0, c1, c2;
+  switch (bc->type) {
+  case AFH_BC_DIRICHLET: c0 = 2; c1 = -1; c2 = c0; break;
+  case AFH_BC_NEUMANN: c0 = B(t, id)->dr[d] * nb_pm(nb); c1 = 1; c2 = 3 * c0; break;
+  default: c0 = 1; c1 = 0; c2 = c0; break;
+  }
+  if (nb == 4) c2 = c0; /* m_af_ghostcell.f90:361 uses c0 on layer 2 */
+  int g1 = nb_low(nb) ? 0 : nc + 1, g2 = nb_low(nb) ? -1 : nc + 2;
+  int x1 = nb_low(nb) ? 1 : nc, x2 = nb_low(nb) ? 2 : nc - 1;
+  int ta = (d == 0) ? 1 : 0, tb = (d == 2) ? 1 : 2;
+  for (int b = 1; b <= nc; b++)
+    for (int a = 1; a <= nc; a++) {
+      int p[3];
+      p[ta] = a, p[tb] = b;
+      p[d] = g1; size_t G1 = I2(n4, p[0], p[1], p[2]);
+      p[d] = g2; size_t G2 = I2(n4, p[0], p[1], p[2]);
+      p[d] = x1; size_t X1 = I2(n4, p[0], p[1], p[2]);
+      p[d] = x2; size_t X2 = I2(n4, p[0], p[1], p[2]);
+      cc[G1] = c0 * bc->value + c1 * cc[X1];
+      cc[G2] = c2 * bc->value + c1 * cc[X2];
+    }
+}
+
+/* gc2_prolong_rb, m_af_ghostcell.f90:753-856 (3D) */
+static void gc2_prolong_rb(afh_tree *t, int id, int nb, int iv, double *cc) {
+  int nc = t->nc, n4 = nc + 4, d = nb_dim(nb);
+  int lo[3] = {1, 1, 1}, hi[3] = {nc, nc, nc}, lo_c[3], hi_c[3], off[3];
+  lo[d] = nb_low(nb) ? -1 : nc + 1;
+  hi[d] = nb_low(nb) ? 0 : nc + 2;
+  child_offset(t, id, 0, off);
+  for (int q = 0; q < 3; q++) {
+    /* (lo+1)/2 with Fortran integer division (truncation toward zero) */
+    lo_c[q] = off[q] + (lo[q] + 1) / 2;
+    hi_c[q] = off[q] + (hi[q] + 1) / 2;
+    if (q == d) {
+      lo_c[q] -= nb_pm(nb) * nc;
+      hi_c[q] -= nb_pm(nb) * nc;
+    }
+  }
+  int p_nb_id = B(t, B(t, id)->parent)->neighbors[nb - 1];
+  double *cp = ccb(t, iv, p_nb_id);
+  int lim = t->meth[iv].lim;
+  for (int k = lo_c[2]; k <= hi_c[2]; k++) {
+    int kf = lo[2] + 2 * (k - lo_c[2]);
+    for (int j = lo_c[1]; j <= hi_c[1]; j++) {
+      int jf = lo[1] + 2 * (j - lo_c[1]);
+      for (int i = lo_c[0]; i <= hi_c[0]; i++) {
+        int fi = lo[0] + 2 * (i - lo_c[0]);
+        double f0 = cp[IX(t, i, j, k)];
+        double sa0 = cp[IX(t, i, j, k)] - cp[IX(t, i - 1, j, k)];
+        double sa1 = cp[IX(t, i, j, k)] - cp[IX(t, i, j - 1, k)];
+        double sa2 = cp[IX(t, i, j, k)] - cp[IX(t, i, j, k - 1)];
+        double sb0 = cp[IX(t, i + 1, j, k)] - cp[IX(t, i, j, k)];
+        double sb1 = cp[IX(t, i, j + 1, k)] - cp[IX(t, i, j, k)];
+        double sb2 = cp[IX(t, i, j, k + 1)] - cp[IX(t, i, j, k)];
+        double f1 = 0.25 * limiter(lim, sa0, sb0);
+        double f2 = 0.25 * limiter(lim, sa1, sb1);
+        double f3 = 0.25 * limiter(lim, sa2, sb2);
+        cc[I2(n4, fi, jf, kf)] = f0 - f1 - f2 - f3;
+        cc[I2(n4, fi, jf, kf + 1)] = f0 - f1 - f2 + f3;
+        cc[I2(n4, fi, jf + 1, kf)] = f0 - f1 + f2 - f3;
+        cc[I2(n4, fi, jf + 1, kf + 1)] = f0 - f1 + f2 + f3;
+        cc[I2(n4, fi + 1, jf, kf)] = f0 + f1 - f2 - f3;
+        cc[I2(n4, fi + 1, jf, kf + 1)] = f0 + f1 - f2 + f3;
+        cc[I2(n4, fi + 1, jf + 1, kf)] = f0 + f1 + f2 - f3;
+        cc[I2(n4, fi + 1, jf + 1, kf + 1)] = f0 + f1 + f2 + f3;
+      }
+    }
+  }
+}
+
+/* af_gc2_box, m_af_ghostcell.f90:672-744 */
+static void gc2_box(afh_tree *t, int id, int iv, double *cc) {
+  int nc = t->nc, n4 = nc + 4;
+  double *c = ccb(t, iv, id);
+  for (int k = 0; k <= nc + 1; k++)
+    for (int j = 0; j <= nc + 1; j++)
+      for (int i = 0; i <= nc + 1; i++) cc[I2(n4, i, j, k)] = c[IX(t, i, j, k)];
+  for (int nb = 1; nb <= 6; nb++) {
+    int nb_id = B(t, id)->neighbors[nb - 1], d = nb_dim(nb);
+    if (nb_id > 0) {
+      int lo[3] = {1, 1, 1}, hi[3] = {nc, nc, nc};
+      lo[d] = nb_low(nb) ? -1 : nc + 1;
+      hi[d] = nb_low(nb) ? 0 : nc + 2;
+      double *cn = ccb(t, iv, nb_id);
+      int sh = -nb_pm(nb) * nc;
+      for (int k = lo[2]; k <= hi[2]; k++)
+        for (int j = lo[1]; j <= hi[1]; j++)
+          for (int i = lo[0]; i <= hi[0]; i++) {
+            int p[3] = {i, j, k};
+            p[d] += sh;
+            cc[I2(n4, i, j, k)] = cn[IX(t, p[0], p[1], p[2])];
+          }
+    } else if (nb_id == 0) {
+      gc2_prolong_rb(t, id, nb, iv, cc);
+    } else {
+      bc_to_gc2(t, id, cc, nb, &t->meth[iv].bc[nb - 1]);
+    }
+  }
+  for (int k = 0; k <= nc + 1; k++)
+    for (int j = 0; j <= nc + 1; j++)
+      for (int i = 0; i <= nc + 1; i++) c[IX(t, i, j, k)] = cc[I2(n4, i, j, k)];
+}
+
+/* flux_upwind_box (m_af_flux_schemes.f90:715-848) with reconstruct_upwind_1d
+ * (282-303) and the m_fluid callbacks flux_direction / flux_upwind
+ * (src/m_fluid.f90:102-227) for electrons, constant N, LFA. Returns the box
+ * maxima of cfl_sum and sigma. */
+static void flux_box(afh_fluid *fl, int id, int s_deriv, double *cfl_max,
+                     double *sig_max, double *cc2, double *cfl) {
+  afh_tree *t = fl->t;
+  int nc = t->nc, n4 = nc + 4;
+  int i_e = fl->d.i_electron + s_deriv;
+  const double N_inv = 1 / fl->d.gas_number_density;
+  const double SI_to_Td = 1e21;
+  gc2_box(t, id, i_e, cc2);
+  double *ne = ccb(t, i_e, id), *E = ccb(t, fl->d.i_efld, id);
+  double *F = fcb(t, fl->d.f_flux, id), *Ef = fcb(t, fl->d.f_field, id);
+  size_t ncell = (size_t)nc * nc * nc;
+  for (size_t q = 0; q < ncell; q++) cfl[q] = 0.0;
+  double smax = -HUGE_VAL;
+  for (int d = 0; d < 3; d++) {
+    double inv_dx = 1 / B(t, id)->dr[d];
+    for (int b = 1; b <= nc; b++)
+      for (int a = 1; a <= nc; a++) {
+        /* line along dim d; (a, b) = (i, j) of the other two dims */
+        double line[64 + 4], Ecc[64 + 2], necc[64 + 2], Ex[64 + 1];
+        double v[64 + 1], dc[64 + 1], u[64 + 1];
+        for (int m = -1; m <= nc + 2; m++) {
+          int p[3];
+          if (d == 0) p[0] = m, p[1] = a, p[2] = b;
+          else if (d == 1) p[0] = a, p[1] = m, p[2] = b;
+          else p[0] = a, p[1] = b, p[2] = m;
+          line[m + 1] = cc2[I2(n4, p[0], p[1], p[2])];
+          if (m >= 0 && m <= nc + 1) {
+            Ecc[m] = E[IX(t, p[0], p[1], p[2])];
+            necc[m] = ne[IX(t, p[0], p[1], p[2])];
+          }
+          if (m >= 1 && m <= nc + 1) Ex[m - 1] = Ef[FX(t, d, p[0], p[1], p[2])];
+        }
+#define L(m) line[(m) + 1]
+        for (int fidx = 1; fidx <= nc + 1; fidx++) {
+          int pos = (-1 * Ex[fidx - 1] > 0);
+          if (pos)
+            u[fidx - 1] = L(fidx - 1) + 0.5 * limiter(fl->d.limiter,
+                                                      L(fidx) - L(fidx - 1),
+                                                      L(fidx - 1) - L(fidx - 2));
+          else
+            u[fidx - 1] = L(fidx) - 0.5 * limiter(fl->d.limiter,
+                                                  L(fidx) - L(fidx - 1),
+                                                  L(fidx + 1) - L(fidx));
+        }
+#undef L
+        for (int fidx = 1; fidx <= nc + 1; fidx++) {
+          double tfc = 0.5 * (Ecc[fidx - 1] + Ecc[fidx]) * SI_to_Td * N_inv;
+          double mu = lt_col(&fl->d.td, 1, tfc) * N_inv;
+          double dcf = lt_col(&fl->d.td, 2, tfc) * N_inv;
+          v[fidx - 1] = -mu * Ex[fidx - 1];
+          dc[fidx - 1] = dcf;
+          double flux = v[fidx - 1] * u[fidx - 1] -
+                        dcf * inv_dx * (necc[fidx] - necc[fidx - 1]);
+          double sigma = mu * u[fidx - 1];
+          if (sigma > smax) smax = sigma;
+          int p[3];
+          if (d == 0) p[0] = fidx, p[1] = a, p[2] = b;
+          else if (d == 1) p[0] = a, p[1] = fidx, p[2] = b;
+          else p[0] = a, p[1] = b, p[2] = fidx;
+          F[FX(t, d, p[0], p[1], p[2])] = flux;
+        }
+        for (int c = 1; c <= nc; c++) {
+          double mv = fmax(fabs(v[c]), fabs(v[c - 1]));
+          double md = fmax(dc[c], dc[c - 1]);
+          double term = 1.0 * mv * inv_dx + 2 * md * (inv_dx * inv_dx);
+          int p[3];
+          if (d == 0) p[0] = c, p[1] = a, p[2] = b;
+          else if (d == 1) p[0] = a, p[1] = c, p[2] = b;
+          else p[0] = a, p[1] = b, p[2] = c;
+          size_t ci = ((size_t)(p[2] - 1) * nc + (p[1] - 1)) * nc + (p[0] - 1);
+          cfl[ci] = cfl[ci] + term;
+        }
+      }
+  }
+  double cm = -HUGE_VAL;
+  for (size_t q = 0; q < ncell; q++)
+    if (cfl[q] > cm) cm = cfl[q];
+  *cfl_max = cm;
+  *sig_max = smax;
+}
+
+/* af_restrict_ref_boundary, m_af_restrict.f90:140-161 */
+static void restrict_ref_boundary(afh_tree *t, int iv) {
+  for (int l = 1; l <= t->nlvl; l++) {
+    int n = LVL_N(t, leaves, l);
+    for (int q = 0; q < n; q++) {
+      int id = LVL_AT(t, leaves, l, q), p_id = B(t, id)->parent;
+      int any = 0;
+      for (int nb = 0; nb < 6; nb++) any |= (B(t, id)->neighbors[nb] == 0);
+      if (p_id > 0 && any) restrict_box(t, id, p_id, iv);
+    }
+  }
+}
+
+/* af_consistent_fluxes / flux_from_children, m_af_core.f90:1257-1402 */
+static void consistent_fluxes(afh_tree *t, int f_ix) {
+  int nc = t->nc, nch = nc / 2;
+  for (int l = 1; l <= t->nlvl - 1; l++) {
+    int n = LVL_N(t, parents, l);
+    for (int q = 0; q < n; q++) {
+      int id = LVL_AT(t, parents, l, q);
+      for (int nb = 1; nb <= 6; nb++) {
+        int nb_id = B(t, id)->neighbors[nb - 1];
+        if (nb_id <= 0 || B(t, nb_id)->children[0] != 0) continue;
+        int d = nb_dim(nb);
+        int i = nb_low(nb) ? 1 : nc + 1, i_nb = nb_low(nb) ? nc + 1 : 1;
+        double *fn = fcb(t, f_ix, nb_id);
+        for (int ic = 0; ic < 4; ic++) {
+          int i_ch = child_adj_nb[nb - 1][ic];
+          int c_id = B(t, id)->children[i_ch - 1];
+          double *fcc = fcb(t, f_ix, c_id);
+          int ioff[3];
+          for (int x = 0; x < 3; x++) ioff[x] = nch * child_dix[i_ch - 1][x];
+          int ta = (d == 0) ? 1 : 0, tb = (d == 2) ? 1 : 2;
+          for (int bb = 1; bb <= nch; bb++)
+            for (int aa = 1; aa <= nch; aa++) {
+              int pc[3], p1[3], p2[3], p3[3], p4[3];
+              pc[d] = i_nb, pc[ta] = ioff[ta] + aa, pc[tb] = ioff[tb] + bb;
+              p1[d] = p2[d] = p3[d] = p4[d] = i;
+              p1[ta] = 2 * aa - 1, p1[tb] = 2 * bb - 1;
+              p2[ta] = 2 * aa, p2[tb] = 2 * bb - 1;
+              p3[ta] = 2 * aa - 1, p3[tb] = 2 * bb;
+              p4[ta] = 2 * aa, p4[tb] = 2 * bb;
+              fn[FX(t, d, pc[0], pc[1], pc[2])] =
+                  0.25 * (fcc[FX(t, d, p1[0], p1[1], p1[2])] +
+                          fcc[FX(t, d, p2[0], p2[1], p2[2])] +
+                          fcc[FX(t, d, p3[0], p3[1], p3[2])] +
+                          fcc[FX(t, d, p4[0], p4[1], p4[2])]);
+            }
+        }
+      }
+    }
+  }
+}
+
+/* flux_upwind_tree, m_af_flux_schemes.f90:666-712 */
+int32_t afo_flux_upwind_tree(afh_fluid *f, int32_t s_deriv, double *dt_lim) {
+  afh_tree *t = f->t;
+  int nc = t->nc;
+  restrict_ref_boundary(t, f->d.i_electron + s_deriv);
+  double cfl_max = -HUGE_VAL, sig_max = -HUGE_VAL;
+  for (int l = 1; l <= t->nlvl; l++) {
+    int n = LVL_N(t, leaves, l);
+#pragma omp parallel
+    {
+      double *cc2 = malloc(sizeof(double) * (size_t)(nc + 4) * (nc + 4) * (nc + 4));
+      double *cfl = malloc(sizeof(double) * (size_t)nc * nc * nc);
+      double lc = -HUGE_VAL, ls = -HUGE_VAL;
+#pragma omp for schedule(static)
+      for (int q = 0; q < n; q++) {
+        double c, s;
+        flux_box(f, LVL_AT(t, leaves, l, q), s_deriv, &c, &s, cc2, cfl);
+        if (c > lc) lc = c;
+        if (s > ls) ls = s;
+      }
+#pragma omp critical
+      {
+        if (lc > cfl_max) cfl_max = lc;
+        if (ls > sig_max) sig_max = ls;
+      }
+      free(cc2), free(cfl);
+    }
+  }
+  consistent_fluxes(t, f->d.f_flux);
+  /* dt_lim(1) = min over boxes of 1/maxval(cfl_sum) = 1/max(cfl_sum);
+   * other_dt(1) = eps0/(e*max(maxval(sigma),1e-100)) minimised over lines */
+  dt_lim[0] = 1 / cfl_max;
+  dt_lim[1] = 8.8541878176e-12 / (1.6022e-19 * fmax(sig_max, 1e-100));
+  return AFH_OK;
+}
+
+/* flux_update_densities (m_af_flux_schemes.f90:320-436) with
+ * add_source_terms, get_rates, get_derivatives (src/m_fluid.f90:298-466,
+ * src/m_chemistry.f90:565-688); mask is all true (set_box_mask without
+ * electrode / dielectric / plasma region). */
+int32_t afo_flux_update_densities(afh_fluid *fl, double dt, int32_t s_deriv,
+                                  int32_t n_prev, const int32_t *s_prev,
+                                  const double *w_prev, int32_t s_out,
+                                  int32_t last_step, double *dt_lim) {
+  afh_tree *t = fl->t;
+  int nc = t->nc, ns = fl->d.n_species, nr = fl->d.n_reactions;
+  double chem_min = 1e100;
+  const double eps = 1e-100;
+  for (int l = 1; l <= t->nlvl; l++) {
+    int n = LVL_N(t, leaves, l);
+#pragma omp parallel for schedule(static) reduction(min : chem_min)
+    for (int q = 0; q < n; q++) {
+      int id = LVL_AT(t, leaves, l, q);
+      double dt_dr[3];
+      for (int d = 0; d < 3; d++) dt_dr[d] = dt / B(t, id)->dr[d];
+      double *E = ccb(t, fl->d.i_efld, id);
+      double *F = fcb(t, fl->d.f_flux, id);
+      for (int k = 1; k <= nc; k++)
+        for (int j = 1; j <= nc; j++)
+          for (int i = 1; i <= nc; i++) {
+            size_t x = IX(t, i, j, k);
+            /* weighted sum of previous states */
+            for (int s = 0; s < ns; s++) {
+              int iv = fl->d.species_iv[s];
+              double tmp = 0.0;
+              for (int m = 0; m < n_prev; m++)
+                tmp = tmp + w_prev[m] * ccb(t, iv + s_prev[m], id)[x];
+              ccb(t, iv + s_out, id)[x] = tmp;
+            }
+            /* source terms */
+            double tmpN = 1 / fl->d.gas_number_density;
+            double field = 1e21 * tmpN * E[x];
+            double dens[AFH_MAX_SPECIES], der[AFH_MAX_SPECIES];
+            for (int s = 0; s < ns; s++) {
+              double v = ccb(t, fl->d.species_iv[s] + s_deriv, id)[x];
+              dens[s] = v > 0.0 ? v : 0.0; /* max(dens, 0.0_dp) */
+              der[s] = 0.0;
+            }
+            for (int r = 0; r < nr; r++) {
+              const afh_reaction *R = &fl->reac[r];
+              double c0 = R->rate_factor, rate;
+              switch (R->rate_type) {
+              case AFH_RATE_TABULATED_FIELD:
+                rate = c0 * lt_col(&fl->d.chem, R->table_col, field);
+                break;
+              case AFH_RATE_CONSTANT: rate = c0 * R->c[0]; break;
+              case AFH_RATE_LINEAR: rate = c0 * R->c[0] * (field - R->c[1]); break;
+              case AFH_RATE_EXP_V1: {
+                double z = R->c[1] / (R->c[2] + field);
+                rate = c0 * R->c[0] * exp(-(z * z));
+                break;
+              }
+              default: {
+                double z = field / R->c[1];
+                rate = c0 * R->c[0] * exp(-(z * z));
+                break;
+              }
+              }
+              double prod = 1.0;
+              for (int m = 0; m < R->n_in; m++) prod = prod * dens[R->ix_in[m] - 1];
+              rate = rate * prod;
+              for (int m = 0; m < R->n_in; m++)
+                der[R->ix_in[m] - 1] = der[R->ix_in[m] - 1] - rate;
+              for (int m = 0; m < R->n_out; m++)
+                der[R->ix_out[m] - 1] =
+                    der[R->ix_out[m] - 1] + rate * R->mult_out[m];
+            }
+            if (last_step) {
+              for (int s = 0; s < ns; s++) {
+                double a, b;
+                if (fl->d.dt_chemistry_nmin > 0) {
+                  a = dens[s] + fl->d.dt_chemistry_nmin;
+                  b = fabs(der[s]);
+                  b = b > eps ? b : eps;
+                } else {
+                  a = dens[s] > eps ? dens[s] : eps;
+                  b = -der[s] > eps ? -der[s] : eps;
+                }
+                double r = a / b;
+                if (r < chem_min) chem_min = r;
+              }
+            }
+            for (int s = 0; s < ns; s++) {
+              double *o = ccb(t, fl->d.species_iv[s] + s_out, id);
+              o[x] = o[x] + dt * der[s];
+            }
+            /* flux divergence for the electrons */
+            double *o = ccb(t, fl->d.i_electron + s_out, id);
+            o[x] = o[x] +
+                   dt_dr[0] * (F[FX(t, 0, i, j, k)] - F[FX(t, 0, i + 1, j, k)]) +
+                   dt_dr[1] * (F[FX(t, 1, i, j, k)] - F[FX(t, 1, i, j + 1, k)]) +
+                   dt_dr[2] * (F[FX(t, 2, i, j, k)] - F[FX(t, 2, i, j, k + 1)]);
+          }
+    }
+  }
+  dt_lim[0] = last_step ? chem_min : 1e100;
+  dt_lim[1] = 1e100;
+  return AFH_OK;
+}

@@ -1,0 +1,66 @@
+/*
+ * ORACLE TEST INFRASTRUCTURE -- not product code.
+ *
+ * libafo.so: a plain-C CPU restatement of the afivo-streamer hot path, used as
+ * the parity checker for the HIP library (tests/, __graft_entry__.smoke(),
+ * bench.py cpu_baseline). Same signatures as include/afivo_hip.h with the
+ * `afo_` prefix, so one Python wrapper drives either library. Each routine
+ * cites the reference routine it restates. Pinned against the golden vectors
+ * in tests/golden/ (generated from the reference's own afivo numerics, see
+ * oracle/Makefile and oracle/make_golden.py).
+ *
+ * The level-1 solve restates OUR device coarse solver (the reference calls
+ * HYPRE, absent here): a V(2,2) geometric multigrid on the coarse grid with
+ * boundary conditions folded into the operator (m_coarse_solver.f90:442-491).
+ */
+#ifndef AFO_H
+#define AFO_H
+#include "../../include/afivo_hip.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+const char *afo_last_error(void);
+int32_t afo_tree_create(const afh_tree_desc *desc, int32_t device,
+                        afh_tree **out);
+int32_t afo_tree_destroy(afh_tree *t);
+int32_t afo_tree_sync(afh_tree *t);
+int32_t afo_set_cc_methods(afh_tree *t, int32_t iv, const afh_bc *bc6,
+                           int32_t rb, int32_t prolong_limiter);
+int32_t afo_set_bc(afh_tree *t, int32_t iv, int32_t nb, int32_t type,
+                   double value);
+int32_t afo_cc_put(afh_tree *t, int32_t iv, const double *host);
+int32_t afo_cc_get(afh_tree *t, int32_t iv, double *host);
+int32_t afo_fc_put(afh_tree *t, int32_t ivf, const double *host);
+int32_t afo_fc_get(afh_tree *t, int32_t ivf, double *host);
+int32_t afo_gc_lvl(afh_tree *t, int32_t lvl, int32_t iv, int32_t corners);
+int32_t afo_gc_tree(afh_tree *t, int32_t iv, int32_t corners);
+int32_t afo_restrict_tree(afh_tree *t, int32_t iv);
+int32_t afo_tree_copy_cc(afh_tree *t, int32_t iv_from, int32_t iv_to);
+int32_t afo_tree_maxabs_cc(afh_tree *t, int32_t iv, double *out);
+int32_t afo_mg_create(afh_tree *t, const afh_mg_desc *desc, afh_mg **out);
+int32_t afo_mg_destroy(afh_mg *mg);
+int32_t afo_mg_fas_vcycle(afh_mg *mg, int32_t set_residual,
+                          int32_t highest_lvl);
+int32_t afo_mg_compute_phi_gradient(afh_mg *mg, int32_t i_fc, double fac,
+                                    int32_t i_norm);
+int32_t afo_fluid_create(afh_tree *t, const afh_fluid_desc *desc,
+                         afh_fluid **out);
+int32_t afo_fluid_destroy(afh_fluid *f);
+int32_t afo_field_set_rhs(afh_fluid *f, int32_t i_rhs, int32_t s_in);
+int32_t afo_flux_upwind_tree(afh_fluid *f, int32_t s_deriv, double *dt_lim);
+int32_t afo_flux_update_densities(afh_fluid *f, double dt, int32_t s_deriv,
+                                  int32_t n_prev, const int32_t *s_prev,
+                                  const double *w_prev, int32_t s_out,
+                                  int32_t last_step, double *dt_lim);
+/* Debug hooks: the individual V-cycle stages (for golden trace tests). */
+int32_t afo_mg_gsrb_boxes(afh_mg *mg, int32_t lvl, int32_t up);
+int32_t afo_mg_update_coarse(afh_mg *mg, int32_t lvl);
+int32_t afo_mg_solve_coarse(afh_mg *mg);
+int32_t afo_mg_correct_children(afh_mg *mg, int32_t lvl);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

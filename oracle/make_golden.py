@@ -1,0 +1,184 @@
+#!/usr/bin/env python3
+"""ORACLE TEST INFRASTRUCTURE -- pack golden vectors (build container only).
+
+Runs the golden-vector harness (oracle/_ref/golden_gen, afivo numerics compiled
+from /root/reference by oracle/Makefile) and packs its raw binary dumps into
+tests/golden/<case>.npz. Usage:
+
+    make -C oracle ref && python3 oracle/make_golden.py
+
+Array conventions in the .npz (all float64 unless noted):
+  meta_*      per-box topology, 1-based ids as in afivo (0 = no box, -1 = phys.)
+  lvl_ids_<l>, lvl_leaves_<l>, lvl_parents_<l>   int32 id lists per level
+  td_rows_cols (n_points, 4), td_xmin, td_inv_fac   transport table
+  chem_rows_cols (n_points, 2), chem_xmin, chem_inv_fac
+  <state>__<var>   cc array (n_boxes, nc+2, nc+2, nc+2) = [box][k][j][i]
+  <state>__fc_<var> fc array (n_boxes, 3, nc+1, nc+1, nc+1) = [box][dim][k][j][i]
+  trace states store only boxes that changed: <state>__<var>__ids (0-based)
+"""
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+TD_FILE = "/root/reference/transport_data/td_air_siglo_swarm.txt"
+
+# cc variable indices (1-based, hx_physics.f90)
+CC = {"e0": 1, "e1": 2, "e2": 3, "pos0": 4, "pos1": 5, "neg0": 7, "neg1": 8,
+      "phi": 10, "efld": 12, "rhs": 13, "tmp": 14}
+FC = {"flux": 1, "field": 2}
+
+CHAIN = [
+    ("init", ["e0", "pos0", "neg0", "phi"], []),
+    ("rhs", ["rhs"], []),
+    ("vcycle1", ["phi", "tmp", "rhs"], []),
+    ("vcycle2", ["phi", "tmp", "rhs"], []),
+    ("field0", ["efld"], ["field"]),
+    ("flux1", ["e0"], ["flux"]),
+    ("update1", ["e1", "pos1", "neg1"], []),
+    ("field1", ["rhs", "phi", "tmp", "efld"], ["field"]),
+    ("flux2", ["e1"], ["flux"]),
+    ("update2", ["e0", "pos0", "neg0"], []),
+]
+CASES = {
+    "uni4": {"chain": CHAIN, "trace": True},
+    "uni8": {"chain": CHAIN, "trace": False},
+    "amr4": {"chain": CHAIN[:7], "trace": False},
+}
+
+
+def read_topology(path):
+    raw = open(path, "rb").read()
+    off = 0
+
+    def take(dtype, n):
+        nonlocal off
+        a = np.frombuffer(raw, dtype=dtype, count=n, offset=off)
+        off += a.nbytes
+        return a.copy()
+
+    nc, nbox, nlvl, nvc, nvf = take(np.int32, 5)
+    out = {"nc": nc, "n_boxes": nbox, "highest_lvl": nlvl, "n_var_cell": nvc,
+           "n_var_face": nvf}
+    out["coarse_grid_size"] = take(np.int32, 3)
+    out["r_base"] = take(np.float64, 3)
+    out["dr_base"] = take(np.float64, 3)
+    lvl = np.zeros(nbox, np.int32)
+    ix = np.zeros((nbox, 3), np.int32)
+    parent = np.zeros(nbox, np.int32)
+    children = np.zeros((nbox, 8), np.int32)
+    neighbors = np.zeros((nbox, 6), np.int32)
+    nmat = np.zeros((nbox, 27), np.int32)
+    r_min = np.zeros((nbox, 3))
+    dr = np.zeros((nbox, 3))
+    for b in range(nbox):
+        lvl[b] = take(np.int32, 1)[0]
+        ix[b] = take(np.int32, 3)
+        parent[b] = take(np.int32, 1)[0]
+        children[b] = take(np.int32, 8)
+        neighbors[b] = take(np.int32, 6)
+        nmat[b] = take(np.int32, 27)
+        r_min[b] = take(np.float64, 3)
+        dr[b] = take(np.float64, 3)
+    out.update(meta_lvl=lvl, meta_ix=ix, meta_parent=parent,
+               meta_children=children, meta_neighbors=neighbors,
+               meta_neighbor_mat=nmat, meta_r_min=r_min, meta_dr=dr)
+    for lv in range(1, nlvl + 1):
+        ni, nl, npar = take(np.int32, 3)
+        out["lvl_ids_%d" % lv] = take(np.int32, ni)
+        out["lvl_leaves_%d" % lv] = take(np.int32, nl)
+        out["lvl_parents_%d" % lv] = take(np.int32, npar)
+    cv, ngas = take(np.float64, 2)
+    out["current_voltage"] = cv
+    out["gas_number_density"] = ngas
+    out["domain"] = take(np.float64, 3)
+    return out
+
+
+def read_tables(path):
+    raw = open(path, "rb").read()
+    off = 0
+    out = {}
+    for name in ("td", "chem"):
+        npts, ncol = np.frombuffer(raw, np.int32, 2, off)
+        off += 8
+        xmin, inv = np.frombuffer(raw, np.float64, 2, off)
+        off += 16
+        rc = np.frombuffer(raw, np.float64, npts * ncol, off)
+        off += rc.nbytes
+        out[name + "_rows_cols"] = rc.reshape(ncol, npts).T.copy()
+        out[name + "_xmin"] = xmin
+        out[name + "_inv_fac"] = inv
+    return out
+
+
+def read_state(path, topo):
+    nb, nc = int(topo["n_boxes"]), int(topo["nc"])
+    nvc, nvf = int(topo["n_var_cell"]), int(topo["n_var_face"])
+    a = np.fromfile(path, dtype=np.float64)
+    ncc = nb * nvc * (nc + 2) ** 3
+    cc = a[:ncc].reshape(nb, nvc, nc + 2, nc + 2, nc + 2)
+    fc = a[ncc:].reshape(nb, nvf, 3, nc + 1, nc + 1, nc + 1)
+    return cc, fc
+
+
+def pack(case, raw_dir):
+    topo = read_topology(os.path.join(raw_dir, "topology.bin"))
+    out = dict(topo)
+    out.update(read_tables(os.path.join(raw_dir, "tables.bin")))
+    # scalar logs (dt limits, residuals, thresholds)
+    for line in open(os.path.join(raw_dir, "log.txt")):
+        f = line.split()
+        if not f or f[0] in ("state",):
+            continue
+        key = "log_" + f[0] + ("_%s" % f[1] if f[0] == "field1_residual" else "")
+        vals = [float(x) for x in (f[2:] if f[0] == "field1_residual" else f[1:])]
+        out[key] = np.array(vals)
+    spec = CASES[case]
+    for name, ccv, fcv in spec["chain"]:
+        cc, fc = read_state(os.path.join(raw_dir, "state_%s.bin" % name), topo)
+        for v in ccv:
+            out["%s__%s" % (name, v)] = cc[:, CC[v] - 1].copy()
+        for v in fcv:
+            out["%s__fc_%s" % (name, v)] = fc[:, FC[v] - 1].copy()
+    if spec["trace"]:
+        logged = [l.split()[1] for l in open(os.path.join(raw_dir, "log.txt"))
+                  if l.split() and l.split()[0] == "state"]
+        seq = ["rhs"] + [s for s in logged if s.startswith("tr_")]
+        prev = read_state(os.path.join(raw_dir, "state_rhs.bin"), topo)[0]
+        order = []
+        for name in seq[1:]:
+            cc = read_state(os.path.join(raw_dir, "state_%s.bin" % name), topo)[0]
+            for v in ("phi", "rhs", "tmp"):
+                i = CC[v] - 1
+                changed = np.where(np.any(cc[:, i] != prev[:, i], axis=(1, 2, 3)))[0]
+                out["%s__%s__ids" % (name, v)] = changed.astype(np.int32)
+                out["%s__%s" % (name, v)] = cc[changed, i].copy()
+            order.append(name)
+            prev = cc
+        out["trace_order"] = np.array(order)
+    dst = os.path.join(REPO, "tests", "golden", case + ".npz")
+    np.savez_compressed(dst, **out)
+    return dst
+
+
+def main():
+    gen = os.path.join(HERE, "_ref", "golden_gen")
+    if not os.path.exists(gen):
+        sys.exit("build the harness first: make -C oracle ref")
+    for case in CASES:
+        raw = os.path.join("/tmp", "golden_raw", case)
+        os.makedirs(raw, exist_ok=True)
+        for f in os.listdir(raw):
+            os.remove(os.path.join(raw, f))
+        subprocess.run([gen, case, TD_FILE, raw], check=True,
+                       stdout=subprocess.DEVNULL)
+        dst = pack(case, raw)
+        print("%-5s -> %s (%.0f kB)" % (case, dst, os.path.getsize(dst) / 1e3))
+
+
+if __name__ == "__main__":
+    main()
