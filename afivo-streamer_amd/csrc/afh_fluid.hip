@@ -1,0 +1,660 @@
+// Drift-diffusion-reaction fluid model on the device (src/m_fluid.f90 over
+// afivo/src/m_af_flux_schemes.f90), electrons + immobile ions, LFA, constant
+// gas density.
+//
+//   k_set_rhs       field_set_rhs (src/m_field.f90:363-401)
+//   k_gc2           af_gc2_box (m_af_ghostcell.f90:672-744): 2 ghost layers of
+//                   the flux species; layer 1 is written back into the box as
+//                   the reference does, layer 2 goes to a per-box face buffer
+//   k_flux          flux_upwind_box + reconstruct_upwind_1d + Koren limiter +
+//                   the m_fluid flux_upwind / flux_direction callbacks; one
+//                   thread per cell computes the low face of each dimension
+//                   (and the high face on the last cell), plus the cell's CFL
+//                   sum; max-reductions of CFL sum and conductivity
+//   k_consistent    af_consistent_fluxes (m_af_core.f90:1257-1402)
+//   k_update        flux_update_densities + add_source_terms + get_rates +
+//                   get_derivatives (m_af_flux_schemes.f90:320-436,
+//                   src/m_fluid.f90:298-466, src/m_chemistry.f90:565-688)
+#include <algorithm>
+
+#include "afh_internal.h"
+
+namespace afh {
+
+constexpr int MAXS = AFH_MAX_SPECIES;
+constexpr int MAXPREV = 4;
+
+__device__ __forceinline__ size_t ix3(int ng, int i, int j, int k) {
+  return ((size_t)k * ng + j) * ng + i;
+}
+__device__ __forceinline__ size_t fidx(int nf, int d, int i, int j, int k) {
+  return (size_t)d * nf * nf * nf + ((size_t)(k - 1) * nf + (j - 1)) * nf +
+         (i - 1);
+}
+
+struct DevLT {
+  int n_points, n_cols;
+  double x_min, inv_fac;
+  const double *rc;
+};
+
+// LT_get_loc + LT_get_col_at_loc (m_lookup_table.f90:330-406)
+__device__ __forceinline__ double lt_col(const DevLT &lt, int col, double x) {
+  const double frac = (x - lt.x_min) * lt.inv_fac;
+  int low;
+  double lf;
+  if (frac <= 0) {
+    low = 1;
+    lf = 1;
+  } else if (frac >= lt.n_points - 1) {
+    low = lt.n_points - 1;
+    lf = 0;
+  } else {
+    low = (int)ceil(frac);
+    lf = low - frac;
+  }
+  const double *r = lt.rc + (size_t)(col - 1) * lt.n_points;
+  return lf * r[low - 1] + (1 - lf) * r[low];
+}
+
+// af_limiter_apply (m_af_limiters.f90:41-149)
+__device__ __forceinline__ double limiter(int lim, double a, double b) {
+  const double third = 1 / 3.0;
+  switch (lim) {
+  case AFH_LIM_KOREN: {
+    const double aa = a * a, ab = a * b;
+    if (ab <= 0) return 0;
+    if (aa <= 0.25 * ab) return 2 * a;
+    if (aa <= 2.5 * ab) return third * (b + 2 * a);
+    return 2 * b;
+  }
+  case AFH_LIM_VANLEER: {
+    const double ab = a * b;
+    return ab > 0 ? 2 * ab / (a + b) : 0;
+  }
+  case AFH_LIM_NONE: return 0.5 * (a + b);
+  case AFH_LIM_ZERO: return 0.0;
+  default: {
+    const double th =
+        lim == AFH_LIM_MINMOD ? 1.0 : lim == AFH_LIM_MC ? 2.0 : 4 / 3.0;
+    if (a * b > 0) {
+      double m = fabs(th * a);
+      const double y = fabs(th * b), z = fabs(0.5 * (a + b));
+      if (y < m) m = y;
+      if (z < m) m = z;
+      return copysign(m, a);
+    }
+    return 0.0;
+  }
+  }
+}
+
+// ------------------------------------------------------------ rhs
+struct RhsArgs {
+  int n;
+  const double *sp[MAXS];
+  double q[MAXS];
+};
+
+__global__ void k_set_rhs(double *__restrict__ rhs, RhsArgs A,
+                          const int32_t *__restrict__ ids, size_t bsz) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= bsz) return;
+  const size_t o = (size_t)(ids[blockIdx.y] - 1) * bsz + t;
+  double r = 0.0;
+  for (int s = 0; s < A.n; s++) r = r + A.q[s] * A.sp[s][o];
+  rhs[o] = r;
+}
+
+// ------------------------------------------------------------ gc2
+__global__ void k_gc2(double *__restrict__ v, double *__restrict__ gc2,
+                      const afh_box_meta *__restrict__ meta,
+                      const int32_t *__restrict__ ids, int nc, size_t bsz,
+                      GcArgs ga) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nc * nc) return;
+  const int id = ids[blockIdx.z];
+  const int nb = blockIdx.y + 1;
+  const int d = (nb - 1) >> 1;
+  const bool low = ((nb - 1) & 1) == 0;
+  const int ta = (d == 0) ? 1 : 0, tb = (d == 2) ? 1 : 2;
+  const int a = t % nc + 1, b = t / nc + 1;
+  const int ng = nc + 2;
+  const afh_box_meta &m = meta[id - 1];
+  double *c = v + (size_t)(id - 1) * bsz;
+  double *g2 = gc2 + ((size_t)(id - 1) * 6 + (nb - 1)) * nc * nc + t;
+  const int nb_id = m.neighbors[nb - 1];
+  int p[3];
+  p[ta] = a;
+  p[tb] = b;
+  p[d] = low ? 0 : nc + 1;
+  const size_t dst1 = ix3(ng, p[0], p[1], p[2]);
+  double l1, l2;
+  if (nb_id > 0) {
+    const double *cn = v + (size_t)(nb_id - 1) * bsz;
+    int q[3] = {p[0], p[1], p[2]};
+    q[d] = low ? nc : 1;
+    l1 = cn[ix3(ng, q[0], q[1], q[2])];
+    q[d] = low ? nc - 1 : 2;
+    l2 = cn[ix3(ng, q[0], q[1], q[2])];
+  } else if (nb_id < 0) {
+    // bc_to_gc2, incl. the c0 on layer 2 for highy (m_af_ghostcell.f90:361)
+    double c0, c1, c2;
+    const afh_bc bc = ga.bc[nb - 1];
+    switch (bc.type) {
+    case AFH_BC_DIRICHLET: c0 = 2; c1 = -1; c2 = c0; break;
+    case AFH_BC_NEUMANN: c0 = m.dr[d] * (low ? -1 : 1); c1 = 1; c2 = 3 * c0; break;
+    default: c0 = 1; c1 = 0; c2 = c0; break;
+    }
+    if (nb == 4) c2 = c0;
+    int q[3] = {p[0], p[1], p[2]};
+    q[d] = low ? 1 : nc;
+    l1 = c0 * bc.value + c1 * c[ix3(ng, q[0], q[1], q[2])];
+    q[d] = low ? 2 : nc - 1;
+    l2 = c2 * bc.value + c1 * c[ix3(ng, q[0], q[1], q[2])];
+  } else {
+    // gc2_prolong_rb: limited-slope prolongation from the parent's neighbour
+    const int hnc = nc >> 1;
+    const int p_nb_id = meta[m.parent - 1].neighbors[nb - 1];
+    const double *cp = v + (size_t)(p_nb_id - 1) * bsz;
+    int cc3[3];
+    cc3[ta] = ((m.ix[ta] - 1) & 1) * hnc + ((a + 1) >> 1);
+    cc3[tb] = ((m.ix[tb] - 1) & 1) * hnc + ((b + 1) >> 1);
+    cc3[d] = low ? nc : 1;
+    const size_t cq = ix3(ng, cc3[0], cc3[1], cc3[2]);
+    const size_t st[3] = {1, (size_t)ng, (size_t)ng * ng};
+    const double f0 = cp[cq];
+    double f[3];
+    for (int q = 0; q < 3; q++)
+      f[q] = 0.25 * limiter(ga.lim, cp[cq] - cp[cq - st[q]],
+                            cp[cq + st[q]] - cp[cq]);
+    // sign per dim: - for the first fine cell of the pair, + for the second;
+    // normal dim: layer order (-1, 0) low / (nc+1, nc+2) high
+    double s[3];
+    s[ta] = (a & 1) ? -1.0 : 1.0;
+    s[tb] = (b & 1) ? -1.0 : 1.0;
+    auto val = [&](double sn) {
+      double sg[3] = {s[0], s[1], s[2]};
+      sg[d] = sn;
+      double r = f0;
+      r = sg[0] < 0 ? r - f[0] : r + f[0];
+      r = sg[1] < 0 ? r - f[1] : r + f[1];
+      r = sg[2] < 0 ? r - f[2] : r + f[2];
+      return r;
+    };
+    // low face: layer 2 (-1) is the first cell, layer 1 (0) the second
+    l1 = val(low ? 1.0 : -1.0);
+    l2 = val(low ? -1.0 : 1.0);
+  }
+  c[dst1] = l1;
+  *g2 = l2;
+}
+
+// ------------------------------------------------------------ flux
+struct FluxArgs {
+  const double *ne;   // flux species, state s_deriv
+  const double *E;    // |E| cell centred
+  const double *Ef;   // face field
+  double *F;          // face flux
+  const double *gc2;
+  DevLT td;
+  double N_inv;
+  int lim;
+};
+
+__global__ void k_flux(FluxArgs A, const afh_box_meta *__restrict__ meta,
+                       const int32_t *__restrict__ ids, int nc, size_t bsz,
+                       size_t fsz, unsigned long long *red) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int id = ids[blockIdx.y];
+  double cfl = -HUGE_VAL, smax = -HUGE_VAL;
+  if (t < nc * nc * nc) {
+    const afh_box_meta &m = meta[id - 1];
+    const int ng = nc + 2, nf = nc + 1;
+    const int pos[3] = {t % nc + 1, (t / nc) % nc + 1, t / (nc * nc) + 1};
+    const double *ne = A.ne + (size_t)(id - 1) * bsz;
+    const double *E = A.E + (size_t)(id - 1) * bsz;
+    const double *Ef = A.Ef + (size_t)(id - 1) * fsz;
+    double *F = A.F + (size_t)(id - 1) * fsz;
+    const double SI_to_Td = 1e21;
+    cfl = 0.0;
+    for (int d = 0; d < 3; d++) {
+      const int ta = (d == 0) ? 1 : 0, tb = (d == 2) ? 1 : 2;
+      const int a = pos[ta], b = pos[tb], c = pos[d];
+      const double inv_dx = 1 / m.dr[d];
+      const size_t st = d == 0 ? 1 : d == 1 ? (size_t)ng : (size_t)ng * ng;
+      const size_t cc0 = ix3(ng, pos[0], pos[1], pos[2]);
+      auto line = [&](int mm) -> double {  // cc2 line value at index mm
+        if (mm == -1)
+          return A.gc2[((size_t)(id - 1) * 6 + 2 * d) * nc * nc +
+                       (size_t)(b - 1) * nc + (a - 1)];
+        if (mm == nc + 2)
+          return A.gc2[((size_t)(id - 1) * 6 + 2 * d + 1) * nc * nc +
+                       (size_t)(b - 1) * nc + (a - 1)];
+        return ne[cc0 + (ptrdiff_t)(mm - c) * (ptrdiff_t)st];
+      };
+      auto fpos = [&](int f) {
+        int q[3] = {pos[0], pos[1], pos[2]};
+        q[d] = f;
+        return fidx(nf, d, q[0], q[1], q[2]);
+      };
+      auto ecc = [&](int mm) { return E[cc0 + (ptrdiff_t)(mm - c) * (ptrdiff_t)st]; };
+      // transport at face f (between cells f-1, f): mu, D
+      auto transport = [&](int f, double &mu, double &dcf) {
+        const double tfc = 0.5 * (ecc(f - 1) + ecc(f)) * SI_to_Td * A.N_inv;
+        mu = lt_col(A.td, 1, tfc) * A.N_inv;
+        dcf = lt_col(A.td, 2, tfc) * A.N_inv;
+      };
+      auto face = [&](int f, double &v, double &dcf) {
+        const double ex = Ef[fpos(f)];
+        double u;
+        if (-1 * ex > 0)
+          u = line(f - 1) + 0.5 * limiter(A.lim, line(f) - line(f - 1),
+                                          line(f - 1) - line(f - 2));
+        else
+          u = line(f) - 0.5 * limiter(A.lim, line(f) - line(f - 1),
+                                      line(f + 1) - line(f));
+        double mu;
+        transport(f, mu, dcf);
+        v = -mu * ex;
+        F[fpos(f)] = v * u - dcf * inv_dx * (line(f) - line(f - 1));
+        smax = fmax(smax, mu * u);
+      };
+      double vl, dl, vh, dh;
+      face(c, vl, dl);
+      if (c == nc) {
+        face(nc + 1, vh, dh);
+      } else {
+        double mu;
+        transport(c + 1, mu, dh);
+        vh = -mu * Ef[fpos(c + 1)];
+      }
+      const double mv = fmax(fabs(vh), fabs(vl));
+      const double md = fmax(dh, dl);
+      cfl = cfl + (1.0 * mv * inv_dx + 2 * md * (inv_dx * inv_dx));
+    }
+  }
+  // block max-reduction of cfl and sigma
+  for (int o = 32; o > 0; o >>= 1) {
+    cfl = fmax(cfl, __shfl_xor(cfl, o, 64));
+    smax = fmax(smax, __shfl_xor(smax, o, 64));
+  }
+  __shared__ double r1[16], r2[16];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) r1[w] = cfl, r2[w] = smax;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int q = 1; q < (int)(blockDim.x >> 6); q++)
+      cfl = fmax(cfl, r1[q]), smax = fmax(smax, r2[q]);
+    atomicMax(&red[0], dbl_to_ord(cfl));
+    atomicMax(&red[1], dbl_to_ord(smax));
+  }
+}
+
+__constant__ int c_child_adj_nb[6][4] = {{1, 3, 5, 7}, {2, 4, 6, 8},
+                                         {1, 2, 5, 6}, {3, 4, 7, 8},
+                                         {1, 2, 3, 4}, {5, 6, 7, 8}};
+__constant__ int c_cdix[8][3] = {{0, 0, 0}, {1, 0, 0}, {0, 1, 0}, {1, 1, 0},
+                                 {0, 0, 1}, {1, 0, 1}, {0, 1, 1}, {1, 1, 1}};
+
+__global__ void k_consistent(double *__restrict__ F,
+                             const afh_box_meta *__restrict__ meta,
+                             const int32_t *__restrict__ tasks, int nc,
+                             size_t fsz) {
+  const int nch = nc >> 1;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= 4 * nch * nch) return;
+  const int task = tasks[blockIdx.y];
+  const int id = task >> 3, nb = task & 7;
+  const afh_box_meta &m = meta[id - 1];
+  const int nb_id = m.neighbors[nb - 1];
+  const int d = (nb - 1) >> 1;
+  const bool low = ((nb - 1) & 1) == 0;
+  const int ta = (d == 0) ? 1 : 0, tb = (d == 2) ? 1 : 2;
+  const int ic = t / (nch * nch), aa = t % nch + 1, bb = (t / nch) % nch + 1;
+  const int i_ch = c_child_adj_nb[nb - 1][ic];
+  const int c_id = m.children[i_ch - 1];
+  const int i = low ? 1 : nc + 1, i_nb = low ? nc + 1 : 1;
+  const int nf = nc + 1;
+  int pc[3], p1[3], p2[3], p3[3], p4[3];
+  pc[d] = i_nb;
+  pc[ta] = nch * c_cdix[i_ch - 1][ta] + aa;
+  pc[tb] = nch * c_cdix[i_ch - 1][tb] + bb;
+  p1[d] = p2[d] = p3[d] = p4[d] = i;
+  p1[ta] = 2 * aa - 1, p1[tb] = 2 * bb - 1;
+  p2[ta] = 2 * aa, p2[tb] = 2 * bb - 1;
+  p3[ta] = 2 * aa - 1, p3[tb] = 2 * bb;
+  p4[ta] = 2 * aa, p4[tb] = 2 * bb;
+  const double *fc = F + (size_t)(c_id - 1) * fsz;
+  F[(size_t)(nb_id - 1) * fsz + fidx(nf, d, pc[0], pc[1], pc[2])] =
+      0.25 * (fc[fidx(nf, d, p1[0], p1[1], p1[2])] +
+              fc[fidx(nf, d, p2[0], p2[1], p2[2])] +
+              fc[fidx(nf, d, p3[0], p3[1], p3[2])] +
+              fc[fidx(nf, d, p4[0], p4[1], p4[2])]);
+}
+
+// ------------------------------------------------------------ update
+struct DevReaction {
+  int rate_type, table_col, n_in, n_out;
+  double rate_factor, c[4];
+  int ix_in[4], ix_out[4], mult_out[4];
+};
+
+struct UpdArgs {
+  int ns, nr, n_prev, last_step, e_index;  // e_index: species slot of the flux species
+  double w_prev[MAXPREV];
+  const double *prev[MAXS][MAXPREV];
+  const double *der[MAXS];
+  double *out[MAXS];
+  const double *E;
+  const double *F;
+  const DevReaction *reac;
+  DevLT chem;
+  double inv_N;
+  double dt;
+  double dt_chemistry_nmin;
+};
+
+__global__ void k_update(UpdArgs A, const afh_box_meta *__restrict__ meta,
+                         const int32_t *__restrict__ ids, int nc, size_t bsz,
+                         size_t fsz, unsigned long long *red) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int id = ids[blockIdx.y];
+  double cmin = 1e100;
+  if (t < nc * nc * nc) {
+    const afh_box_meta &m = meta[id - 1];
+    const int i = t % nc + 1, j = (t / nc) % nc + 1, k = t / (nc * nc) + 1;
+    const int ng = nc + 2, nf = nc + 1;
+    const size_t x = (size_t)(id - 1) * bsz + ix3(ng, i, j, k);
+    double y[MAXS], der[MAXS], dens[MAXS];
+    for (int s = 0; s < A.ns; s++) {
+      double tmp = 0.0;
+      for (int q = 0; q < A.n_prev; q++) tmp = tmp + A.w_prev[q] * A.prev[s][q][x];
+      y[s] = tmp;
+      const double v = A.der[s][x];
+      dens[s] = v > 0.0 ? v : 0.0;
+      der[s] = 0.0;
+    }
+    const double field = 1e21 * A.inv_N * A.E[x];
+    for (int r = 0; r < A.nr; r++) {
+      const DevReaction &R = A.reac[r];
+      const double c0 = R.rate_factor;
+      double rate;
+      switch (R.rate_type) {
+      case AFH_RATE_TABULATED_FIELD: rate = c0 * lt_col(A.chem, R.table_col, field); break;
+      case AFH_RATE_CONSTANT: rate = c0 * R.c[0]; break;
+      case AFH_RATE_LINEAR: rate = c0 * R.c[0] * (field - R.c[1]); break;
+      case AFH_RATE_EXP_V1: {
+        const double z = R.c[1] / (R.c[2] + field);
+        rate = c0 * R.c[0] * exp(-(z * z));
+        break;
+      }
+      default: {
+        const double z = field / R.c[1];
+        rate = c0 * R.c[0] * exp(-(z * z));
+        break;
+      }
+      }
+      double prod = 1.0;
+      for (int q = 0; q < R.n_in; q++) prod = prod * dens[R.ix_in[q] - 1];
+      rate = rate * prod;
+      for (int q = 0; q < R.n_in; q++) der[R.ix_in[q] - 1] = der[R.ix_in[q] - 1] - rate;
+      for (int q = 0; q < R.n_out; q++)
+        der[R.ix_out[q] - 1] = der[R.ix_out[q] - 1] + rate * R.mult_out[q];
+    }
+    if (A.last_step) {
+      const double eps = 1e-100;
+      for (int s = 0; s < A.ns; s++) {
+        double a, b;
+        if (A.dt_chemistry_nmin > 0) {
+          a = dens[s] + A.dt_chemistry_nmin;
+          b = fabs(der[s]);
+          b = b > eps ? b : eps;
+        } else {
+          a = dens[s] > eps ? dens[s] : eps;
+          b = -der[s] > eps ? -der[s] : eps;
+        }
+        cmin = fmin(cmin, a / b);
+      }
+    }
+    for (int s = 0; s < A.ns; s++) y[s] = y[s] + A.dt * der[s];
+    const double *F = A.F + (size_t)(id - 1) * fsz;
+    const int e = A.e_index;
+    y[e] = y[e] + (A.dt / m.dr[0]) * (F[fidx(nf, 0, i, j, k)] - F[fidx(nf, 0, i + 1, j, k)]) +
+           (A.dt / m.dr[1]) * (F[fidx(nf, 1, i, j, k)] - F[fidx(nf, 1, i, j + 1, k)]) +
+           (A.dt / m.dr[2]) * (F[fidx(nf, 2, i, j, k)] - F[fidx(nf, 2, i, j, k + 1)]);
+    for (int s = 0; s < A.ns; s++) A.out[s][x] = y[s];
+  }
+  if (A.last_step) {
+    for (int o = 32; o > 0; o >>= 1) cmin = fmin(cmin, __shfl_xor(cmin, o, 64));
+    __shared__ double r1[16];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (lane == 0) r1[w] = cmin;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (int q = 1; q < (int)(blockDim.x >> 6); q++) cmin = fmin(cmin, r1[q]);
+      atomicMin(&red[0], dbl_to_ord(cmin));
+    }
+  }
+}
+
+}  // namespace afh
+
+using namespace afh;
+
+struct afh_fluid {
+  afh_tree *t = nullptr;
+  afh_fluid_desc d;
+  double *d_td = nullptr, *d_chem = nullptr;
+  DevReaction *d_reac = nullptr;
+  int e_index = -1;
+  DevLT td, chem;
+};
+
+extern "C" {
+
+int32_t afh_fluid_create(afh_tree *t, const afh_fluid_desc *d, afh_fluid **out) {
+  if (!t || !d || !out) return set_error(AFH_ERR_ARG, "afh_fluid_create: null");
+  if (d->n_species < 1 || d->n_species > MAXS || d->n_reactions < 0 ||
+      d->n_reactions > AFH_MAX_REACTIONS)
+    return set_error(AFH_ERR_ARG, "bad species/reaction count");
+  if (d->td.n_points < 2 || d->td.n_cols < 2 || !d->td.rows_cols)
+    return set_error(AFH_ERR_ARG, "transport table needs mobility + diffusion");
+  afh_fluid *f = new afh_fluid();
+  f->t = t;
+  f->d = *d;
+  for (int s = 0; s < d->n_species; s++) {
+    if (d->species_iv[s] < 1 || d->species_iv[s] > t->nvc)
+      return set_error(AFH_ERR_ARG, "bad species index");
+    if (d->species_iv[s] == d->i_electron) f->e_index = s;
+  }
+  if (f->e_index < 0) return set_error(AFH_ERR_ARG, "electron not in species list");
+  if (!t->meth[d->i_electron].set)
+    return set_error(AFH_ERR_STATE, "set cc methods for the electrons first");
+  size_t ntd = (size_t)d->td.n_points * d->td.n_cols;
+  size_t nch = (size_t)d->chem.n_points * d->chem.n_cols;
+  AFH_HIP(hipMalloc(&f->d_td, ntd * sizeof(double)));
+  AFH_HIP(hipMemcpy(f->d_td, d->td.rows_cols, ntd * sizeof(double),
+                    hipMemcpyHostToDevice));
+  AFH_HIP(hipMalloc(&f->d_chem, std::max<size_t>(1, nch) * sizeof(double)));
+  if (nch)
+    AFH_HIP(hipMemcpy(f->d_chem, d->chem.rows_cols, nch * sizeof(double),
+                      hipMemcpyHostToDevice));
+  std::vector<DevReaction> R(std::max(1, d->n_reactions));
+  for (int r = 0; r < d->n_reactions; r++) {
+    const afh_reaction &a = d->reactions[r];
+    DevReaction &b = R[r];
+    if (a.rate_type < AFH_RATE_TABULATED_FIELD || a.rate_type > AFH_RATE_EXP_V2)
+      return set_error(AFH_ERR_UNSUPPORTED, "reaction rate type %d", a.rate_type);
+    if (a.n_in < 0 || a.n_in > 4 || a.n_out < 0 || a.n_out > 4)
+      return set_error(AFH_ERR_ARG, "reaction species count");
+    b.rate_type = a.rate_type;
+    b.table_col = a.table_col;
+    b.n_in = a.n_in;
+    b.n_out = a.n_out;
+    b.rate_factor = a.rate_factor;
+    for (int q = 0; q < 4; q++) {
+      b.c[q] = a.c[q];
+      b.ix_in[q] = a.ix_in[q];
+      b.ix_out[q] = a.ix_out[q];
+      b.mult_out[q] = a.mult_out[q];
+    }
+  }
+  AFH_HIP(hipMalloc(&f->d_reac, sizeof(DevReaction) * R.size()));
+  AFH_HIP(hipMemcpy(f->d_reac, R.data(), sizeof(DevReaction) * R.size(),
+                    hipMemcpyHostToDevice));
+  f->td = DevLT{d->td.n_points, d->td.n_cols, d->td.x_min, d->td.inv_fac, f->d_td};
+  f->chem = DevLT{d->chem.n_points, d->chem.n_cols, d->chem.x_min,
+                  d->chem.inv_fac, f->d_chem};
+  *out = f;
+  return AFH_OK;
+}
+
+int32_t afh_fluid_destroy(afh_fluid *f) {
+  if (!f) return AFH_OK;
+  hipStreamSynchronize(f->t->stream);
+  hipFree(f->d_td);
+  hipFree(f->d_chem);
+  hipFree(f->d_reac);
+  delete f;
+  return AFH_OK;
+}
+
+int32_t afh_field_set_rhs(afh_fluid *f, int32_t i_rhs, int32_t s_in) {
+  if (!f) return set_error(AFH_ERR_ARG, "null fluid");
+  afh_tree *t = f->t;
+  if (i_rhs < 1 || i_rhs > t->nvc) return set_error(AFH_ERR_ARG, "bad i_rhs");
+  const double fac = -1.6022e-19 / 8.8541878176e-12;  // -UC_elem_charge/UC_eps0
+  RhsArgs A;
+  A.n = 0;
+  for (int s = 0; s < f->d.n_species; s++) {
+    if (f->d.species_charge[s] == 0) continue;
+    A.sp[A.n] = t->ccv(f->d.species_iv[s] + s_in);
+    A.q[A.n] = f->d.species_charge[s] * fac;
+    A.n++;
+  }
+  for (int l = 1; l <= t->nlvl; l++) {
+    const int n = t->leaves.n(l);
+    if (!n) continue;
+    hipLaunchKernelGGL(k_set_rhs, dim3((unsigned)((t->bsz + 255) / 256), n),
+                       dim3(256), 0, t->stream, t->ccv(i_rhs), A,
+                       t->leaves.at(l), t->bsz);
+    AFH_LAUNCH_CHECK("k_set_rhs");
+  }
+  return AFH_OK;
+}
+
+int32_t afh_flux_upwind_tree(afh_fluid *f, int32_t s_deriv, double *dt_lim) {
+  if (!f || !dt_lim) return set_error(AFH_ERR_ARG, "null argument");
+  afh_tree *t = f->t;
+  const int nc = t->nc, n3 = nc * nc * nc;
+  const int iv = f->d.i_electron + s_deriv;
+  if (iv < 1 || iv > t->nvc) return set_error(AFH_ERR_ARG, "bad s_deriv");
+  int32_t e;
+  // af_restrict_ref_boundary
+  const int nrb = t->refb.off[t->nlvl];
+  if ((e = restrict_boxes(t, t->refb.d, nrb, iv))) return e;
+  // two ghost layers, level by level (coarse write-back before fine reads)
+  for (int l = 1; l <= t->nlvl; l++) {
+    const int n = t->leaves.n(l);
+    if (!n) continue;
+    hipLaunchKernelGGL(k_gc2, dim3((nc * nc + 255) / 256, 6, n), dim3(256), 0,
+                       t->stream, t->ccv(iv), t->gc2, t->d_boxes,
+                       t->leaves.at(l), nc, t->bsz, t->gc_args(iv));
+    AFH_LAUNCH_CHECK("k_gc2");
+  }
+  unsigned long long init[2] = {host_dbl_to_ord(-HUGE_VAL), host_dbl_to_ord(-HUGE_VAL)};
+  auto *red = reinterpret_cast<unsigned long long *>(t->scratch);
+  AFH_HIP(hipMemcpyAsync(red, init, sizeof init, hipMemcpyHostToDevice, t->stream));
+  FluxArgs A;
+  A.ne = t->ccv(iv);
+  A.E = t->ccv(f->d.i_efld);
+  A.Ef = t->fcv(f->d.f_field);
+  A.F = t->fcv(f->d.f_flux);
+  A.gc2 = t->gc2;
+  A.td = f->td;
+  A.N_inv = 1 / f->d.gas_number_density;
+  A.lim = f->d.limiter;
+  for (int l = 1; l <= t->nlvl; l++) {
+    const int n = t->leaves.n(l);
+    if (!n) continue;
+    prof_begin(t, AFH_PROF_FLUX);
+    hipLaunchKernelGGL(k_flux, dim3((n3 + 255) / 256, n), dim3(256), 0,
+                       t->stream, A, t->d_boxes, t->leaves.at(l), nc, t->bsz,
+                       t->fsz, red);
+    // read n_e, |E|, 3 face fields; write 3 fluxes = 64 B/cell
+    prof_end(t, AFH_PROF_FLUX, 64.0 * n3 * n);
+    AFH_LAUNCH_CHECK("k_flux");
+  }
+  const int ntask = t->cflux.off[t->nlvl];
+  if (ntask) {
+    hipLaunchKernelGGL(k_consistent, dim3((nc * nc + 255) / 256, ntask),
+                       dim3(256), 0, t->stream, t->fcv(f->d.f_flux), t->d_boxes,
+                       t->cflux.d, nc, t->fsz);
+    AFH_LAUNCH_CHECK("k_consistent");
+  }
+  unsigned long long r[2];
+  AFH_HIP(hipMemcpyAsync(r, red, sizeof r, hipMemcpyDeviceToHost, t->stream));
+  AFH_HIP(hipStreamSynchronize(t->stream));
+  const double cfl_max = ord_to_dbl(r[0]), sig_max = ord_to_dbl(r[1]);
+  dt_lim[0] = 1 / cfl_max;
+  dt_lim[1] = 8.8541878176e-12 / (1.6022e-19 * std::max(sig_max, 1e-100));
+  return AFH_OK;
+}
+
+int32_t afh_flux_update_densities(afh_fluid *f, double dt, int32_t s_deriv,
+                                  int32_t n_prev, const int32_t *s_prev,
+                                  const double *w_prev, int32_t s_out,
+                                  int32_t last_step, double *dt_lim) {
+  if (!f || !dt_lim || n_prev < 1 || n_prev > MAXPREV || !s_prev || !w_prev)
+    return set_error(AFH_ERR_ARG, "afh_flux_update_densities: bad argument");
+  afh_tree *t = f->t;
+  const int nc = t->nc, n3 = nc * nc * nc;
+  UpdArgs A;
+  A.ns = f->d.n_species;
+  A.nr = f->d.n_reactions;
+  A.n_prev = n_prev;
+  A.last_step = last_step ? 1 : 0;
+  A.e_index = f->e_index;
+  for (int q = 0; q < n_prev; q++) A.w_prev[q] = w_prev[q];
+  for (int s = 0; s < A.ns; s++) {
+    const int iv = f->d.species_iv[s];
+    for (int q = 0; q < n_prev; q++) A.prev[s][q] = t->ccv(iv + s_prev[q]);
+    A.der[s] = t->ccv(iv + s_deriv);
+    A.out[s] = t->ccv(iv + s_out);
+  }
+  A.E = t->ccv(f->d.i_efld);
+  A.F = t->fcv(f->d.f_flux);
+  A.reac = f->d_reac;
+  A.chem = f->chem;
+  A.inv_N = 1 / f->d.gas_number_density;
+  A.dt = dt;
+  A.dt_chemistry_nmin = f->d.dt_chemistry_nmin;
+  // algorithmic bytes per cell: each distinct species state read once, the
+  // output written once, |E| and 3 fluxes read
+  int distinct = n_prev;
+  for (int q = 0; q < n_prev; q++) distinct -= (s_prev[q] == s_deriv) ? 1 : 0;
+  distinct += 1;
+  const double upd_bytes = 8.0 * (A.ns * (distinct + 1) + 4);
+  unsigned long long init = host_dbl_to_ord(1e100);
+  auto *red = reinterpret_cast<unsigned long long *>(t->scratch) + 2;
+  AFH_HIP(hipMemcpyAsync(red, &init, sizeof init, hipMemcpyHostToDevice, t->stream));
+  for (int l = 1; l <= t->nlvl; l++) {
+    const int n = t->leaves.n(l);
+    if (!n) continue;
+    prof_begin(t, AFH_PROF_UPDATE);
+    hipLaunchKernelGGL(k_update, dim3((n3 + 255) / 256, n), dim3(256), 0,
+                       t->stream, A, t->d_boxes, t->leaves.at(l), nc, t->bsz,
+                       t->fsz, red);
+    prof_end(t, AFH_PROF_UPDATE, upd_bytes * n3 * n);
+    AFH_LAUNCH_CHECK("k_update");
+  }
+  unsigned long long r;
+  AFH_HIP(hipMemcpyAsync(&r, red, sizeof r, hipMemcpyDeviceToHost, t->stream));
+  AFH_HIP(hipStreamSynchronize(t->stream));
+  dt_lim[0] = last_step ? ord_to_dbl(r) : 1e100;
+  dt_lim[1] = 1e100;
+  return AFH_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,123 @@
+// Internal declarations shared by the HIP translation units of libafivo_hip.
+//
+// Device layout (HBM):
+//   cc pool  [iv][box][k][j][i], (nc+2)^3 doubles per box, i fastest: each
+//            box of a variable is the exact image of the Fortran array
+//            box%cc(0:nc+1,0:nc+1,0:nc+1,iv), boxes contiguous per variable.
+//   fc pool  [ivf][box][dim][k][j][i], (nc+1)^3 per dim (box%fc layout).
+//   meta     afh_box_meta[n_boxes] (topology), per-level id lists.
+// All kernels evaluate floating-point expressions in the order the reference
+// Fortran writes them; the library is compiled with -ffp-contract=off so the
+// results are bitwise those of the C oracle (oracle/c/afo.c).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/afivo_hip.h"
+
+namespace afh {
+
+int32_t set_error(int32_t code, const char *fmt, ...);
+int32_t check_hip(hipError_t e, const char *what);
+#define AFH_HIP(call)                                                         \
+  do {                                                                        \
+    hipError_t _e = (call);                                                   \
+    if (_e != hipSuccess) return ::afh::check_hip(_e, #call);                 \
+  } while (0)
+#define AFH_LAUNCH_CHECK(what)                                                \
+  do {                                                                        \
+    hipError_t _e = hipGetLastError();                                        \
+    if (_e != hipSuccess) return ::afh::check_hip(_e, what);                  \
+  } while (0)
+
+struct CcMethod {
+  int set = 0;
+  afh_bc bc[6];
+  int rb = AFH_RB_GC_INTERP;
+  int lim = AFH_LIM_GMINMOD43;
+};
+
+// Per-variable methods as the kernels see them (passed by value).
+struct GcArgs {
+  afh_bc bc[6];
+  int rb;
+  int lim;
+};
+
+struct LevelList {
+  std::vector<int32_t> off;  // highest_lvl + 1 offsets
+  int32_t *d = nullptr;      // device, concatenated 1-based ids
+  int n(int lvl) const { return off[lvl] - off[lvl - 1]; }
+  const int32_t *at(int lvl) const { return d + off[lvl - 1]; }
+};
+
+}  // namespace afh
+
+struct afh_tree {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int nc = 0, ng = 0, nb = 0, nlvl = 0, nvc = 0, nvf = 0;
+  size_t bsz = 0, fsz = 0;
+  int cgs[3] = {0, 0, 0};
+  double r_base[3], dr_base[3];
+  std::vector<afh_box_meta> boxes;  // host copy
+  afh_box_meta *d_boxes = nullptr;
+  afh::LevelList ids, leaves, parents;
+  std::vector<std::vector<int32_t>> h_ids, h_leaves, h_parents;
+  // leaves next to a refinement boundary, per level (af_restrict_ref_boundary)
+  afh::LevelList refb;
+  // (parent id, nb) tasks of af_consistent_fluxes, per level
+  afh::LevelList cflux;
+  double *cc = nullptr, *fc = nullptr;
+  double *gc2 = nullptr;     // 2nd ghost layer for the flux: [box][6][nc][nc]
+  double *scratch = nullptr; // reductions etc.
+  double *h_scratch = nullptr;
+  std::vector<afh::CcMethod> meth;
+  // kernel timing (afh_profile_*)
+  int prof_class = 0;
+  std::vector<hipEvent_t> ev_pool;
+  size_t ev_used = 0;
+  double prof_bytes = 0;
+  int64_t prof_launches = 0;
+
+  double *ccv(int iv) const { return cc + (size_t)(iv - 1) * nb * bsz; }
+  double *fcv(int ivf) const { return fc + (size_t)(ivf - 1) * nb * fsz; }
+  afh::GcArgs gc_args(int iv) const {
+    afh::GcArgs a;
+    for (int n = 0; n < 6; n++) a.bc[n] = meth[iv].bc[n];
+    a.rb = meth[iv].rb;
+    a.lim = meth[iv].lim;
+    return a;
+  }
+};
+
+namespace afh {
+// Kernel timing: bracket one launch of class `kc` (no-op unless enabled).
+void prof_begin(afh_tree *t, int kc);
+void prof_end(afh_tree *t, int kc, double bytes);
+// Host launchers shared between translation units (afh_tree.hip).
+int32_t gc_lvl(afh_tree *t, int lvl, int iv, int corners);
+int32_t restrict_boxes(afh_tree *t, const int32_t *d_ids, int n, int iv);
+// Orderable encoding of doubles for atomicMax/Min on 64-bit integers.
+__device__ __forceinline__ unsigned long long dbl_to_ord(double x) {
+  unsigned long long u = __double_as_longlong(x);
+  return (u & 0x8000000000000000ull) ? ~u : (u | 0x8000000000000000ull);
+}
+inline double ord_to_dbl(unsigned long long o) {
+  unsigned long long u =
+      (o & 0x8000000000000000ull) ? (o & ~0x8000000000000000ull) : ~o;
+  double d;
+  memcpy(&d, &u, sizeof d);
+  return d;
+}
+inline unsigned long long host_dbl_to_ord(double x) {
+  unsigned long long u;
+  memcpy(&u, &x, sizeof u);
+  return (u & 0x8000000000000000ull) ? ~u : (u | 0x8000000000000000ull);
+}
+}  // namespace afh

@@ -1,0 +1,685 @@
+// FAS multigrid V-cycle over the box tree (afivo/src/m_af_multigrid.f90).
+//
+// Kernels, one launch per pass over one level (all boxes of the level):
+//   k_gsrb          stencil_gsrb_357, constant 7-point stencil (m_af_stencil.f90:938-955)
+//   k_residual      residual_box = rhs - stencil_apply_357 (m_af_multigrid.f90:801-810)
+//   k_rstr_fas      update_coarse part 1: residual of the 8 fine cells of
+//                   each parent cell + 8-cell means of residual and phi
+//                   (m_af_multigrid.f90:704-717, af_restrict_box); the child's
+//                   tmp is never written (the reference restores it)
+//   k_parent_rhs    update_coarse part 2: rhs = L phi + tmp, tmp = phi (726-736)
+//   k_corr_tmp      correct_children part 1: tmp = phi - tmp (636-637)
+//   k_prolong       stencil_prolong_248 add (m_af_stencil.f90:749-771)
+//   k_gradient      mg_box_lpl_gradient + mg_box_field_norm (1882-2025)
+// plus the level-1 coarse solver (ours; the reference calls HYPRE PFMG).
+#include <algorithm>
+
+#include "afh_internal.h"
+
+namespace afh {
+
+struct Coef {
+  double c[7];
+};
+
+constexpr int MAXMG = 16;
+constexpr int CS_BOTTOM_SWEEPS = 32;   // same constant as oracle/c/afo.c
+constexpr int CS_SMALL_CELLS = 4096;   // MG levels <= 16^3 run in one workgroup
+
+struct CsParams {
+  int n_mg;
+  int dims[MAXMG][3];
+  double hc[MAXMG][3];
+  double cdiag[MAXMG];
+  int bctype[6];
+  double *u[MAXMG], *f[MAXMG], *r[MAXMG];
+};
+
+__device__ __forceinline__ size_t ix3(int ng, int i, int j, int k) {
+  return ((size_t)k * ng + j) * ng + i;
+}
+
+// ------------------------------------------------------------ box kernels
+__global__ void k_gsrb(double *__restrict__ phi, const double *__restrict__ rhs,
+                       const int32_t *__restrict__ ids, int nc, size_t bsz,
+                       Coef cf, double inv_c1, int redblack) {
+  const int hn = nc >> 1;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= hn * nc * nc) return;
+  const int id = ids[blockIdx.y];
+  const int ih = t % hn, j = (t / hn) % nc + 1, k = t / (hn * nc) + 1;
+  const int i = 2 - ((redblack ^ (k + j)) & 1) + 2 * ih;
+  const int ng = nc + 2;
+  double *x = phi + (size_t)(id - 1) * bsz;
+  const double *r = rhs + (size_t)(id - 1) * bsz;
+  const size_t c = ix3(ng, i, j, k);
+  const size_t sj = ng, sk = (size_t)ng * ng;
+  x[c] = (r[c] - cf.c[1] * x[c - 1] - cf.c[2] * x[c + 1] - cf.c[3] * x[c - sj] -
+          cf.c[4] * x[c + sj] - cf.c[5] * x[c - sk] - cf.c[6] * x[c + sk]) *
+         inv_c1;
+}
+
+__device__ __forceinline__ double apply7(const double *x, size_t c, size_t sj,
+                                         size_t sk, const Coef &cf) {
+  return cf.c[0] * x[c] + cf.c[1] * x[c - 1] + cf.c[2] * x[c + 1] +
+         cf.c[3] * x[c - sj] + cf.c[4] * x[c + sj] + cf.c[5] * x[c - sk] +
+         cf.c[6] * x[c + sk];
+}
+
+__global__ void k_residual(const double *__restrict__ phi,
+                           const double *__restrict__ rhs,
+                           double *__restrict__ tmp,
+                           const int32_t *__restrict__ ids, int nc, size_t bsz,
+                           Coef cf) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nc * nc * nc) return;
+  const int id = ids[blockIdx.y];
+  const int i = t % nc + 1, j = (t / nc) % nc + 1, k = t / (nc * nc) + 1;
+  const int ng = nc + 2;
+  const size_t o = (size_t)(id - 1) * bsz, c = ix3(ng, i, j, k);
+  tmp[o + c] = rhs[o + c] - apply7(phi + o, c, ng, (size_t)ng * ng, cf);
+}
+
+__global__ void k_rstr_fas(double *__restrict__ phi,
+                           const double *__restrict__ rhs,
+                           double *__restrict__ tmp,
+                           const afh_box_meta *__restrict__ meta,
+                           const int32_t *__restrict__ ids, int nc, size_t bsz,
+                           Coef cf) {
+  const int hn = nc >> 1;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= hn * hn * hn) return;
+  const int id = ids[blockIdx.y];
+  const afh_box_meta &m = meta[id - 1];
+  const int i = t % hn + 1, j = (t / hn) % hn + 1, k = t / (hn * hn) + 1;
+  const int ng = nc + 2;
+  const size_t sj = ng, sk = (size_t)ng * ng;
+  const size_t o = (size_t)(id - 1) * bsz;
+  const double *x = phi + o, *r = rhs + o;
+  const int fi = 2 * i - 1, fj = 2 * j - 1, fk = 2 * k - 1;
+  size_t cs[8] = {ix3(ng, fi, fj, fk),         ix3(ng, fi + 1, fj, fk),
+                  ix3(ng, fi, fj + 1, fk),     ix3(ng, fi + 1, fj + 1, fk),
+                  ix3(ng, fi, fj, fk + 1),     ix3(ng, fi + 1, fj, fk + 1),
+                  ix3(ng, fi, fj + 1, fk + 1), ix3(ng, fi + 1, fj + 1, fk + 1)};
+  double sr = r[cs[0]] - apply7(x, cs[0], sj, sk, cf);
+  double sp = x[cs[0]];
+#pragma unroll
+  for (int q = 1; q < 8; q++) {
+    sr += r[cs[q]] - apply7(x, cs[q], sj, sk, cf);
+    sp += x[cs[q]];
+  }
+  const size_t po = (size_t)(m.parent - 1) * bsz +
+                    ix3(ng, ((m.ix[0] - 1) & 1) * hn + i,
+                        ((m.ix[1] - 1) & 1) * hn + j,
+                        ((m.ix[2] - 1) & 1) * hn + k);
+  tmp[po] = 0.125 * sr;
+  phi[po] = 0.125 * sp;
+}
+
+__global__ void k_parent_rhs(const double *__restrict__ phi,
+                             double *__restrict__ rhs, double *__restrict__ tmp,
+                             const int32_t *__restrict__ ids, int nc,
+                             size_t bsz, Coef cf) {
+  const int ng = nc + 2;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= ng * ng * ng) return;
+  const int id = ids[blockIdx.y];
+  const int i = t % ng, j = (t / ng) % ng, k = t / (ng * ng);
+  const size_t o = (size_t)(id - 1) * bsz, c = ix3(ng, i, j, k);
+  double rv = rhs[o + c];
+  if (i >= 1 && i <= nc && j >= 1 && j <= nc && k >= 1 && k <= nc)
+    rv = apply7(phi + o, c, ng, (size_t)ng * ng, cf);
+  rhs[o + c] = rv + tmp[o + c];
+  tmp[o + c] = phi[o + c];
+}
+
+__global__ void k_corr_tmp(const double *__restrict__ phi,
+                           double *__restrict__ tmp,
+                           const int32_t *__restrict__ ids, size_t bsz) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= bsz) return;
+  const size_t o = (size_t)(ids[blockIdx.y] - 1) * bsz + t;
+  tmp[o] = phi[o] - tmp[o];
+}
+
+__global__ void k_prolong(double *__restrict__ phi,
+                          const double *__restrict__ tmp,
+                          const afh_box_meta *__restrict__ meta,
+                          const int32_t *__restrict__ ids, int nc, size_t bsz) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nc * nc * nc) return;
+  const int id = ids[blockIdx.y];
+  const afh_box_meta &m = meta[id - 1];
+  const int i = t % nc + 1, j = (t / nc) % nc + 1, k = t / (nc * nc) + 1;
+  const int ng = nc + 2, hn = nc >> 1;
+  const int o0 = ((m.ix[0] - 1) & 1) * hn, o1 = ((m.ix[1] - 1) & 1) * hn,
+            o2 = ((m.ix[2] - 1) & 1) * hn;
+  const int i1 = o0 + ((i + 1) >> 1), i2 = i1 + 1 - 2 * (i & 1);
+  const int j1 = o1 + ((j + 1) >> 1), j2 = j1 + 1 - 2 * (j & 1);
+  const int k1 = o2 + ((k + 1) >> 1), k2 = k1 + 1 - 2 * (k & 1);
+  const double *p = tmp + (size_t)(m.parent - 1) * bsz;
+  const size_t c = (size_t)(id - 1) * bsz + ix3(ng, i, j, k);
+  phi[c] = phi[c] + (27 / 64.0) * p[ix3(ng, i1, j1, k1)] +
+           (9 / 64.0) * p[ix3(ng, i2, j1, k1)] +
+           (9 / 64.0) * p[ix3(ng, i1, j2, k1)] +
+           (3 / 64.0) * p[ix3(ng, i2, j2, k1)] +
+           (9 / 64.0) * p[ix3(ng, i1, j1, k2)] +
+           (3 / 64.0) * p[ix3(ng, i2, j1, k2)] +
+           (3 / 64.0) * p[ix3(ng, i1, j2, k2)] +
+           (1 / 64.0) * p[ix3(ng, i2, j2, k2)];
+}
+
+// mg_box_lpl_gradient (fc = fac/dr * (phi_i - phi_i-1)) + mg_box_field_norm
+__global__ void k_gradient(const double *__restrict__ phi,
+                           double *__restrict__ fcv, double *__restrict__ nrm,
+                           const afh_box_meta *__restrict__ meta,
+                           const int32_t *__restrict__ ids, int nc, size_t bsz,
+                           size_t fsz, double fac) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nc * nc * nc) return;
+  const int id = ids[blockIdx.y];
+  const afh_box_meta &m = meta[id - 1];
+  const int i = t % nc + 1, j = (t / nc) % nc + 1, k = t / (nc * nc) + 1;
+  const int ng = nc + 2, nf = nc + 1;
+  const double *p = phi + (size_t)(id - 1) * bsz;
+  double *f = fcv + (size_t)(id - 1) * fsz;
+  const size_t c = ix3(ng, i, j, k), sj = ng, sk = (size_t)ng * ng;
+  const double ix_ = fac / m.dr[0], iy = fac / m.dr[1], iz = fac / m.dr[2];
+  const double fxl = ix_ * (p[c] - p[c - 1]), fxh = ix_ * (p[c + 1] - p[c]);
+  const double fyl = iy * (p[c] - p[c - sj]), fyh = iy * (p[c + sj] - p[c]);
+  const double fzl = iz * (p[c] - p[c - sk]), fzh = iz * (p[c + sk] - p[c]);
+  const size_t d3 = (size_t)nf * nf * nf;
+  auto fx = [&](int d, int a, int b, int cc) {
+    return (size_t)d * d3 + ((size_t)(cc - 1) * nf + (b - 1)) * nf + (a - 1);
+  };
+  f[fx(0, i, j, k)] = fxl;
+  if (i == nc) f[fx(0, nc + 1, j, k)] = fxh;
+  f[fx(1, i, j, k)] = fyl;
+  if (j == nc) f[fx(1, i, nc + 1, k)] = fyh;
+  f[fx(2, i, j, k)] = fzl;
+  if (k == nc) f[fx(2, i, j, nc + 1)] = fzh;
+  if (nrm) {
+    const double a = fxl + fxh, b = fyl + fyh, cc = fzl + fzh;
+    nrm[(size_t)(id - 1) * bsz + c] = 0.5 * sqrt(a * a + b * b + cc * cc);
+  }
+}
+
+// ------------------------------------------------------------ coarse solver
+// Same arithmetic as oracle/c/afo.c (cs_*): BCs folded into the operator as
+// in stencil_handle_boundaries (m_coarse_solver.f90:442-491).
+__device__ __forceinline__ size_t gix(const CsParams &P, int m, int i, int j,
+                                      int k) {
+  return ((size_t)k * (P.dims[m][1] + 2) + j) * (P.dims[m][0] + 2) + i;
+}
+
+__device__ __forceinline__ double cs_diag(const CsParams &P, int m, int i,
+                                          int j, int k) {
+  const int idx[3] = {i, j, k};
+  double d = P.cdiag[m];
+  for (int nb = 1; nb <= 6; nb++) {
+    const int dd = (nb - 1) >> 1;
+    const bool low = ((nb - 1) & 1) == 0;
+    const bool at = low ? (idx[dd] == 1) : (idx[dd] == P.dims[m][dd]);
+    if (!at) continue;
+    if (P.bctype[nb - 1] == AFH_BC_DIRICHLET) d = d - P.hc[m][dd];
+    else d = d + P.hc[m][dd];
+  }
+  return d;
+}
+
+__device__ __forceinline__ void cs_gs_cell(const CsParams &P, int m, int i,
+                                           int j, int k) {
+  const int nx = P.dims[m][0], ny = P.dims[m][1], nz = P.dims[m][2];
+  double *u = P.u[m];
+  const double *h = P.hc[m];
+  double s = P.f[m][gix(P, m, i, j, k)];
+  if (i > 1) s = s - h[0] * u[gix(P, m, i - 1, j, k)];
+  if (i < nx) s = s - h[0] * u[gix(P, m, i + 1, j, k)];
+  if (j > 1) s = s - h[1] * u[gix(P, m, i, j - 1, k)];
+  if (j < ny) s = s - h[1] * u[gix(P, m, i, j + 1, k)];
+  if (k > 1) s = s - h[2] * u[gix(P, m, i, j, k - 1)];
+  if (k < nz) s = s - h[2] * u[gix(P, m, i, j, k + 1)];
+  u[gix(P, m, i, j, k)] = s / cs_diag(P, m, i, j, k);
+}
+
+__device__ __forceinline__ void cs_res_cell(const CsParams &P, int m, int i,
+                                            int j, int k) {
+  const int nx = P.dims[m][0], ny = P.dims[m][1], nz = P.dims[m][2];
+  const double *u = P.u[m];
+  const double *h = P.hc[m];
+  double a = cs_diag(P, m, i, j, k) * u[gix(P, m, i, j, k)];
+  if (i > 1) a = a + h[0] * u[gix(P, m, i - 1, j, k)];
+  if (i < nx) a = a + h[0] * u[gix(P, m, i + 1, j, k)];
+  if (j > 1) a = a + h[1] * u[gix(P, m, i, j - 1, k)];
+  if (j < ny) a = a + h[1] * u[gix(P, m, i, j + 1, k)];
+  if (k > 1) a = a + h[2] * u[gix(P, m, i, j, k - 1)];
+  if (k < nz) a = a + h[2] * u[gix(P, m, i, j, k + 1)];
+  P.r[m][gix(P, m, i, j, k)] = P.f[m][gix(P, m, i, j, k)] - a;
+}
+
+__device__ __forceinline__ void cs_rstr_cell(const CsParams &P, int c, int i,
+                                             int j, int k) {
+  const int m = c - 1;
+  const double *r = P.r[m];
+  const int fi = 2 * i - 1, fj = 2 * j - 1, fk = 2 * k - 1;
+  double s = r[gix(P, m, fi, fj, fk)];
+  s += r[gix(P, m, fi + 1, fj, fk)];
+  s += r[gix(P, m, fi, fj + 1, fk)];
+  s += r[gix(P, m, fi + 1, fj + 1, fk)];
+  s += r[gix(P, m, fi, fj, fk + 1)];
+  s += r[gix(P, m, fi + 1, fj, fk + 1)];
+  s += r[gix(P, m, fi, fj + 1, fk + 1)];
+  s += r[gix(P, m, fi + 1, fj + 1, fk + 1)];
+  P.f[c][gix(P, c, i, j, k)] = 0.125 * s;
+  P.u[c][gix(P, c, i, j, k)] = 0.0;
+}
+
+__device__ __forceinline__ double cs_refl(const CsParams &P, int c, int i,
+                                          int j, int k) {
+  double s = 1.0;
+  int idx[3] = {i, j, k};
+  for (int d = 0; d < 3; d++) {
+    if (idx[d] < 1) {
+      idx[d] = 1;
+      if (P.bctype[2 * d] == AFH_BC_DIRICHLET) s = -s;
+    } else if (idx[d] > P.dims[c][d]) {
+      idx[d] = P.dims[c][d];
+      if (P.bctype[2 * d + 1] == AFH_BC_DIRICHLET) s = -s;
+    }
+  }
+  return s * P.u[c][gix(P, c, idx[0], idx[1], idx[2])];
+}
+
+__device__ __forceinline__ void cs_prol_cell(const CsParams &P, int m, int i,
+                                             int j, int k) {
+  const int c = m + 1;
+  const int i1 = (i + 1) >> 1, i2 = i1 + 1 - 2 * (i & 1);
+  const int j1 = (j + 1) >> 1, j2 = j1 + 1 - 2 * (j & 1);
+  const int k1 = (k + 1) >> 1, k2 = k1 + 1 - 2 * (k & 1);
+  double *u = P.u[m];
+  const size_t g = gix(P, m, i, j, k);
+  u[g] = u[g] + (27 / 64.0) * cs_refl(P, c, i1, j1, k1) +
+         (9 / 64.0) * cs_refl(P, c, i2, j1, k1) +
+         (9 / 64.0) * cs_refl(P, c, i1, j2, k1) +
+         (3 / 64.0) * cs_refl(P, c, i2, j2, k1) +
+         (9 / 64.0) * cs_refl(P, c, i1, j1, k2) +
+         (3 / 64.0) * cs_refl(P, c, i2, j1, k2) +
+         (3 / 64.0) * cs_refl(P, c, i1, j2, k2) +
+         (1 / 64.0) * cs_refl(P, c, i2, j2, k2);
+}
+
+// multi-block passes over one (large, even-sized) MG level
+__global__ void k_cs_gsrb(CsParams P, int m, int n) {
+  const int nx = P.dims[m][0], ny = P.dims[m][1], nz = P.dims[m][2];
+  const int hx = nx >> 1;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= hx * ny * nz) return;
+  const int ih = t % hx, j = (t / hx) % ny + 1, k = t / (hx * ny) + 1;
+  cs_gs_cell(P, m, 2 - ((n ^ (k + j)) & 1) + 2 * ih, j, k);
+}
+__global__ void k_cs_res(CsParams P, int m) {
+  const int nx = P.dims[m][0], ny = P.dims[m][1], nz = P.dims[m][2];
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nx * ny * nz) return;
+  cs_res_cell(P, m, t % nx + 1, (t / nx) % ny + 1, t / (nx * ny) + 1);
+}
+__global__ void k_cs_rstr(CsParams P, int c) {
+  const int nx = P.dims[c][0], ny = P.dims[c][1], nz = P.dims[c][2];
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nx * ny * nz) return;
+  cs_rstr_cell(P, c, t % nx + 1, (t / nx) % ny + 1, t / (nx * ny) + 1);
+}
+__global__ void k_cs_prol(CsParams P, int m) {
+  const int nx = P.dims[m][0], ny = P.dims[m][1], nz = P.dims[m][2];
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nx * ny * nz) return;
+  cs_prol_cell(P, m, t % nx + 1, (t / nx) % ny + 1, t / (nx * ny) + 1);
+}
+
+// One workgroup runs `n_cycles` complete V-cycles starting at MG level m0
+// (all levels >= m0 are small). Every pass is followed by a barrier.
+__device__ void blk_gs(const CsParams &P, int m, int n) {
+  const int nx = P.dims[m][0], ny = P.dims[m][1], nz = P.dims[m][2];
+  const int N = nx * ny * nz;
+  for (int t = threadIdx.x; t < N; t += blockDim.x) {
+    const int i = t % nx + 1, j = (t / nx) % ny + 1, k = t / (nx * ny) + 1;
+    const int i0 = 2 - ((n ^ (k + j)) & 1);
+    if (((i - i0) & 1) == 0) cs_gs_cell(P, m, i, j, k);
+  }
+  __syncthreads();
+}
+template <typename F>
+__device__ void blk_for(const CsParams &P, int m, F f) {
+  const int nx = P.dims[m][0], ny = P.dims[m][1], nz = P.dims[m][2];
+  const int N = nx * ny * nz;
+  for (int t = threadIdx.x; t < N; t += blockDim.x)
+    f(t % nx + 1, (t / nx) % ny + 1, t / (nx * ny) + 1);
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(1024) k_cs_small(CsParams P, int m0,
+                                                   int n_cycles) {
+  const int bot = P.n_mg - 1;
+  for (int cyc = 0; cyc < n_cycles; cyc++) {
+    for (int m = m0; m < bot; m++) {
+      for (int s = 0; s < 2; s++) {
+        blk_gs(P, m, 1);
+        blk_gs(P, m, 2);
+      }
+      blk_for(P, m, [&](int i, int j, int k) { cs_res_cell(P, m, i, j, k); });
+      blk_for(P, m + 1,
+              [&](int i, int j, int k) { cs_rstr_cell(P, m + 1, i, j, k); });
+    }
+    for (int it = 0; it < CS_BOTTOM_SWEEPS; it++) {
+      blk_gs(P, bot, 1);
+      blk_gs(P, bot, 2);
+    }
+    for (int m = bot - 1; m >= m0; m--) {
+      blk_for(P, m, [&](int i, int j, int k) { cs_prol_cell(P, m, i, j, k); });
+      for (int s = 0; s < 2; s++) {
+        blk_gs(P, m, 1);
+        blk_gs(P, m, 2);
+      }
+    }
+  }
+}
+
+// coarse_solver_set_rhs_phi: gather rhs (+ folded BC values) and phi
+__global__ void k_cs_gather(CsParams P, const double *__restrict__ phi,
+                            const double *__restrict__ rhs,
+                            const afh_box_meta *__restrict__ meta,
+                            const int32_t *__restrict__ ids, int nc,
+                            size_t bsz, afh_bc b0, afh_bc b1, afh_bc b2,
+                            afh_bc b3, afh_bc b4, afh_bc b5) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nc * nc * nc) return;
+  const int id = ids[blockIdx.y];
+  const afh_box_meta &m = meta[id - 1];
+  const int i = t % nc + 1, j = (t / nc) % nc + 1, k = t / (nc * nc) + 1;
+  const int gi[3] = {(m.ix[0] - 1) * nc + i, (m.ix[1] - 1) * nc + j,
+                     (m.ix[2] - 1) * nc + k};
+  const afh_bc bc[6] = {b0, b1, b2, b3, b4, b5};
+  const size_t c = (size_t)(id - 1) * bsz + ix3(nc + 2, i, j, k);
+  double rv = rhs[c];
+  for (int nb = 1; nb <= 6; nb++) {
+    const int dd = (nb - 1) >> 1;
+    const bool low = ((nb - 1) & 1) == 0;
+    const bool at = low ? (gi[dd] == 1) : (gi[dd] == P.dims[0][dd]);
+    if (!at) continue;
+    const double cnb = P.hc[0][dd];
+    double b2r;
+    if (bc[nb - 1].type == AFH_BC_DIRICHLET) b2r = -2 * cnb;
+    else b2r = -(cnb * m.dr[dd]) * (low ? -1 : 1);
+    rv = rv + b2r * bc[nb - 1].value;
+  }
+  const size_t g = gix(P, 0, gi[0], gi[1], gi[2]);
+  P.f[0][g] = rv;
+  P.u[0][g] = phi[c];
+}
+
+__global__ void k_cs_scatter(CsParams P, double *__restrict__ phi,
+                             const afh_box_meta *__restrict__ meta,
+                             const int32_t *__restrict__ ids, int nc,
+                             size_t bsz) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nc * nc * nc) return;
+  const int id = ids[blockIdx.y];
+  const afh_box_meta &m = meta[id - 1];
+  const int i = t % nc + 1, j = (t / nc) % nc + 1, k = t / (nc * nc) + 1;
+  phi[(size_t)(id - 1) * bsz + ix3(nc + 2, i, j, k)] =
+      P.u[0][gix(P, 0, (m.ix[0] - 1) * nc + i, (m.ix[1] - 1) * nc + j,
+                 (m.ix[2] - 1) * nc + k)];
+}
+
+}  // namespace afh
+
+using namespace afh;
+
+struct afh_mg {
+  afh_tree *t = nullptr;
+  afh_mg_desc d;
+  std::vector<Coef> lvl_c;  // per tree level
+  CsParams P;
+  int small_from = 0;       // first MG level run by k_cs_small
+};
+
+static inline dim3 blocks1(size_t n, int bs = 256) {
+  return dim3((unsigned)((n + bs - 1) / bs));
+}
+
+extern "C" {
+
+int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
+  if (!t || !d || !out) return set_error(AFH_ERR_ARG, "afh_mg_create: null");
+  if (d->i_phi < 1 || d->i_phi > t->nvc || d->i_rhs < 1 || d->i_rhs > t->nvc ||
+      d->i_tmp < 1 || d->i_tmp > t->nvc)
+    return set_error(AFH_ERR_ARG, "afh_mg_create: bad variable index");
+  if (!t->meth[d->i_phi].set)
+    return set_error(AFH_ERR_STATE, "set cc methods (bc) for phi first");
+  if (d->coarse_mode != AFH_COARSE_CYCLES || d->coarse_cycles < 1)
+    return set_error(AFH_ERR_UNSUPPORTED, "coarse solver mode");
+  afh_mg *mg = new afh_mg();
+  mg->t = t;
+  mg->d = *d;
+  // mg_box_lpl_stencil: c(2:7) = 1/dr^2, c(1) = -sum(c(2:)) - lambda
+  mg->lvl_c.resize(t->nlvl);
+  for (int l = 1; l <= t->nlvl; l++) {
+    const afh_box_meta &m = t->boxes[t->h_ids[l - 1][0] - 1];
+    Coef &c = mg->lvl_c[l - 1];
+    for (int q = 0; q < 3; q++) {
+      double inv = 1 / (m.dr[q] * m.dr[q]);
+      c.c[1 + 2 * q] = inv;
+      c.c[2 + 2 * q] = inv;
+    }
+    double s = c.c[1];
+    for (int q = 2; q < 7; q++) s = s + c.c[q];
+    c.c[0] = -s - d->helmholtz_lambda;
+  }
+  // coarse hierarchy (same rule as oracle/c/afo.c afo_mg_create)
+  CsParams &P = mg->P;
+  memset(&P, 0, sizeof P);
+  int m = 0;
+  for (int q = 0; q < 3; q++) {
+    P.dims[0][q] = t->cgs[q];
+    P.hc[0][q] = mg->lvl_c[0].c[1 + 2 * q];
+  }
+  P.cdiag[0] = mg->lvl_c[0].c[0];
+  for (;;) {
+    int *n = P.dims[m];
+    bool ok = (n[0] % 2 == 0) && (n[1] % 2 == 0) && (n[2] % 2 == 0) &&
+              n[0] >= 4 && n[1] >= 4 && n[2] >= 4 && m < MAXMG - 1;
+    if (!ok) break;
+    for (int q = 0; q < 3; q++) {
+      P.dims[m + 1][q] = n[q] / 2;
+      P.hc[m + 1][q] = 0.25 * P.hc[m][q];
+    }
+    const double *h = P.hc[m + 1];
+    P.cdiag[m + 1] = -(h[0] + h[0] + h[1] + h[1] + h[2] + h[2]) -
+                     d->helmholtz_lambda;
+    m++;
+  }
+  P.n_mg = m + 1;
+  mg->small_from = P.n_mg - 1;
+  while (mg->small_from > 0) {
+    const int *n = P.dims[mg->small_from - 1];
+    if ((long)n[0] * n[1] * n[2] > CS_SMALL_CELLS) break;
+    mg->small_from--;
+  }
+  for (int q = 0; q < P.n_mg; q++) {
+    size_t n = (size_t)(P.dims[q][0] + 2) * (P.dims[q][1] + 2) * (P.dims[q][2] + 2);
+    AFH_HIP(hipMalloc(&P.u[q], n * sizeof(double)));
+    AFH_HIP(hipMalloc(&P.f[q], n * sizeof(double)));
+    AFH_HIP(hipMalloc(&P.r[q], n * sizeof(double)));
+    AFH_HIP(hipMemsetAsync(P.u[q], 0, n * sizeof(double), t->stream));
+    AFH_HIP(hipMemsetAsync(P.f[q], 0, n * sizeof(double), t->stream));
+    AFH_HIP(hipMemsetAsync(P.r[q], 0, n * sizeof(double), t->stream));
+  }
+  AFH_HIP(hipStreamSynchronize(t->stream));
+  *out = mg;
+  return AFH_OK;
+}
+
+int32_t afh_mg_destroy(afh_mg *mg) {
+  if (!mg) return AFH_OK;
+  hipStreamSynchronize(mg->t->stream);
+  for (int q = 0; q < mg->P.n_mg; q++) {
+    hipFree(mg->P.u[q]);
+    hipFree(mg->P.f[q]);
+    hipFree(mg->P.r[q]);
+  }
+  delete mg;
+  return AFH_OK;
+}
+
+static int32_t gsrb_boxes(afh_mg *mg, int lvl, bool up) {
+  afh_tree *t = mg->t;
+  const int n_cycle = up ? mg->d.n_cycle_up : mg->d.n_cycle_down;
+  const int nid = t->ids.n(lvl), nc = t->nc;
+  const Coef cf = mg->lvl_c[lvl - 1];
+  const double inv_c1 = 1 / cf.c[0];
+  const int cells = nc * nc * nc / 2;
+  for (int n = 1; n <= 2 * n_cycle; n++) {
+    prof_begin(t, AFH_PROF_GSRB);
+    hipLaunchKernelGGL(k_gsrb, dim3((cells + 255) / 256, nid), dim3(256), 0,
+                       t->stream, t->ccv(mg->d.i_phi), t->ccv(mg->d.i_rhs),
+                       t->ids.at(lvl), nc, t->bsz, cf, inv_c1, n);
+    // read phi (all), rhs (half), write phi (half) = 16 B/cell
+    prof_end(t, AFH_PROF_GSRB, 16.0 * nc * nc * nc * nid);
+    AFH_LAUNCH_CHECK("k_gsrb");
+    int32_t e = gc_lvl(t, lvl, mg->d.i_phi, up && n == 2 * n_cycle);
+    if (e) return e;
+  }
+  return AFH_OK;
+}
+
+static int32_t update_coarse(afh_mg *mg, int lvl) {
+  afh_tree *t = mg->t;
+  const int nc = t->nc, hn = nc / 2;
+  const int nid = t->ids.n(lvl);
+  hipLaunchKernelGGL(k_rstr_fas, dim3((hn * hn * hn + 255) / 256, nid),
+                     dim3(256), 0, t->stream, t->ccv(mg->d.i_phi),
+                     t->ccv(mg->d.i_rhs), t->ccv(mg->d.i_tmp), t->d_boxes,
+                     t->ids.at(lvl), nc, t->bsz, mg->lvl_c[lvl - 1]);
+  AFH_LAUNCH_CHECK("k_rstr_fas");
+  int32_t e = gc_lvl(t, lvl - 1, mg->d.i_phi, 1);
+  if (e) return e;
+  const int np = t->parents.n(lvl - 1);
+  if (np) {
+    hipLaunchKernelGGL(k_parent_rhs, dim3((unsigned)((t->bsz + 255) / 256), np),
+                       dim3(256), 0, t->stream, t->ccv(mg->d.i_phi),
+                       t->ccv(mg->d.i_rhs), t->ccv(mg->d.i_tmp),
+                       t->parents.at(lvl - 1), nc, t->bsz, mg->lvl_c[lvl - 2]);
+    AFH_LAUNCH_CHECK("k_parent_rhs");
+  }
+  return AFH_OK;
+}
+
+static int32_t correct_children(afh_mg *mg, int lvl) {
+  afh_tree *t = mg->t;
+  const int np = t->parents.n(lvl - 1), nc = t->nc;
+  if (np) {
+    hipLaunchKernelGGL(k_corr_tmp, dim3((unsigned)((t->bsz + 255) / 256), np),
+                       dim3(256), 0, t->stream, t->ccv(mg->d.i_phi),
+                       t->ccv(mg->d.i_tmp), t->parents.at(lvl - 1), t->bsz);
+    AFH_LAUNCH_CHECK("k_corr_tmp");
+  }
+  const int nid = t->ids.n(lvl);
+  hipLaunchKernelGGL(k_prolong, dim3((nc * nc * nc + 255) / 256, nid), dim3(256),
+                     0, t->stream, t->ccv(mg->d.i_phi), t->ccv(mg->d.i_tmp),
+                     t->d_boxes, t->ids.at(lvl), nc, t->bsz);
+  AFH_LAUNCH_CHECK("k_prolong");
+  return AFH_OK;
+}
+
+static int32_t solve_coarse(afh_mg *mg) {
+  afh_tree *t = mg->t;
+  CsParams &P = mg->P;
+  const afh_bc *bc = t->meth[mg->d.i_phi].bc;
+  for (int q = 0; q < 6; q++) P.bctype[q] = bc[q].type;
+  const int nc = t->nc, nid = t->ids.n(1), n3 = nc * nc * nc;
+  hipLaunchKernelGGL(k_cs_gather, dim3((n3 + 255) / 256, nid), dim3(256), 0,
+                     t->stream, P, t->ccv(mg->d.i_phi), t->ccv(mg->d.i_rhs),
+                     t->d_boxes, t->ids.at(1), nc, t->bsz, bc[0], bc[1], bc[2],
+                     bc[3], bc[4], bc[5]);
+  AFH_LAUNCH_CHECK("k_cs_gather");
+  const int s = mg->small_from;
+  if (s == 0) {
+    hipLaunchKernelGGL(k_cs_small, dim3(1), dim3(1024), 0, t->stream, P, 0,
+                       mg->d.coarse_cycles);
+    AFH_LAUNCH_CHECK("k_cs_small");
+  } else {
+    for (int cyc = 0; cyc < mg->d.coarse_cycles; cyc++) {
+      for (int m = 0; m < s; m++) {
+        const size_t N = (size_t)P.dims[m][0] * P.dims[m][1] * P.dims[m][2];
+        for (int sw = 0; sw < 2; sw++)
+          for (int n = 1; n <= 2; n++)
+            hipLaunchKernelGGL(k_cs_gsrb, blocks1(N / 2), dim3(256), 0,
+                               t->stream, P, m, n);
+        hipLaunchKernelGGL(k_cs_res, blocks1(N), dim3(256), 0, t->stream, P, m);
+        hipLaunchKernelGGL(k_cs_rstr, blocks1(N / 8), dim3(256), 0, t->stream, P,
+                           m + 1);
+      }
+      hipLaunchKernelGGL(k_cs_small, dim3(1), dim3(1024), 0, t->stream, P, s, 1);
+      for (int m = s - 1; m >= 0; m--) {
+        const size_t N = (size_t)P.dims[m][0] * P.dims[m][1] * P.dims[m][2];
+        hipLaunchKernelGGL(k_cs_prol, blocks1(N), dim3(256), 0, t->stream, P, m);
+        for (int sw = 0; sw < 2; sw++)
+          for (int n = 1; n <= 2; n++)
+            hipLaunchKernelGGL(k_cs_gsrb, blocks1(N / 2), dim3(256), 0,
+                               t->stream, P, m, n);
+      }
+    }
+    AFH_LAUNCH_CHECK("coarse solver cycle");
+  }
+  hipLaunchKernelGGL(k_cs_scatter, dim3((n3 + 255) / 256, nid), dim3(256), 0,
+                     t->stream, P, t->ccv(mg->d.i_phi), t->d_boxes,
+                     t->ids.at(1), nc, t->bsz);
+  AFH_LAUNCH_CHECK("k_cs_scatter");
+  return gc_lvl(t, 1, mg->d.i_phi, 1);
+}
+
+int32_t afh_mg_fas_vcycle(afh_mg *mg, int32_t set_residual, int32_t hl) {
+  if (!mg) return set_error(AFH_ERR_ARG, "null mg");
+  afh_tree *t = mg->t;
+  const int max_lvl = (hl > 0 && hl <= t->nlvl) ? hl : t->nlvl;
+  int32_t e;
+  for (int lvl = max_lvl; lvl >= 2; lvl--) {
+    if ((e = gsrb_boxes(mg, lvl, false))) return e;
+    if ((e = update_coarse(mg, lvl))) return e;
+  }
+  if ((e = solve_coarse(mg))) return e;
+  for (int lvl = 2; lvl <= max_lvl; lvl++) {
+    if ((e = correct_children(mg, lvl))) return e;
+    if ((e = gc_lvl(t, lvl, mg->d.i_phi, 1))) return e;
+    if ((e = gsrb_boxes(mg, lvl, true))) return e;
+  }
+  if (set_residual) {
+    const int nc = t->nc, n3 = nc * nc * nc;
+    for (int lvl = 1; lvl <= max_lvl; lvl++) {
+      hipLaunchKernelGGL(k_residual, dim3((n3 + 255) / 256, t->ids.n(lvl)),
+                         dim3(256), 0, t->stream, t->ccv(mg->d.i_phi),
+                         t->ccv(mg->d.i_rhs), t->ccv(mg->d.i_tmp),
+                         t->ids.at(lvl), nc, t->bsz, mg->lvl_c[lvl - 1]);
+      AFH_LAUNCH_CHECK("k_residual");
+    }
+  }
+  return AFH_OK;
+}
+
+int32_t afh_mg_compute_phi_gradient(afh_mg *mg, int32_t i_fc, double fac,
+                                    int32_t i_norm) {
+  if (!mg) return set_error(AFH_ERR_ARG, "null mg");
+  afh_tree *t = mg->t;
+  if (i_fc < 1 || i_fc > t->nvf || i_norm < 0 || i_norm > t->nvc)
+    return set_error(AFH_ERR_ARG, "bad variable index");
+  const int nc = t->nc, n3 = nc * nc * nc;
+  const int ntot = t->ids.off[t->nlvl];
+  hipLaunchKernelGGL(k_gradient, dim3((n3 + 255) / 256, ntot), dim3(256), 0,
+                     t->stream, t->ccv(mg->d.i_phi), t->fcv(i_fc),
+                     i_norm > 0 ? t->ccv(i_norm) : nullptr, t->d_boxes,
+                     t->ids.d, nc, t->bsz, t->fsz, fac);
+  AFH_LAUNCH_CHECK("k_gradient");
+  return AFH_OK;
+}
+
+}  // extern "C"

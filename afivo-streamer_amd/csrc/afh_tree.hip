@@ -1,0 +1,614 @@
+// Box pool, topology upload, ghost cells, restriction, reductions.
+//
+// Ghost-cell kernels restate afivo/src/m_af_ghostcell.f90 (af_gc_box 64-120,
+// copy_from_nb 654-669, bc_to_gc 173-279, af_gc_interp 394-498,
+// af_gc_interp_lim 503-612, corners/edges 125-170 + 860-924) and
+// mg_sides_rb (afivo/src/m_af_multigrid.f90:294-461). One level is filled by
+// two launches: all faces of all boxes (one thread per ghost cell), then
+// edges and corners (one workgroup per box), because edge extrapolation reads
+// face ghosts and corner extrapolation reads edge ghosts.
+#include <stdarg.h>
+#include <stdio.h>
+
+#include <algorithm>
+
+#include "afh_internal.h"
+
+namespace afh {
+
+static thread_local char g_err[512];
+
+int32_t set_error(int32_t code, const char *fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof g_err, fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+int32_t check_hip(hipError_t e, const char *what) {
+  return set_error(AFH_ERR_DEVICE, "%s: %s", what, hipGetErrorString(e));
+}
+
+static hipEvent_t next_event(afh_tree *t) {
+  if (t->ev_used == t->ev_pool.size()) {
+    hipEvent_t e;
+    hipEventCreate(&e);
+    t->ev_pool.push_back(e);
+  }
+  return t->ev_pool[t->ev_used++];
+}
+
+void prof_begin(afh_tree *t, int kc) {
+  if (t->prof_class != kc) return;
+  hipEventRecord(next_event(t), t->stream);
+}
+
+void prof_end(afh_tree *t, int kc, double bytes) {
+  if (t->prof_class != kc) return;
+  hipEventRecord(next_event(t), t->stream);
+  t->prof_bytes += bytes;
+  t->prof_launches++;
+}
+
+__device__ __forceinline__ size_t ix3(int ng, int i, int j, int k) {
+  return ((size_t)k * ng + j) * ng + i;
+}
+
+// ------------------------------------------------------------ faces
+// One thread per ghost cell of face (blockIdx.y+1) of box ids[blockIdx.z].
+__global__ void k_gc_faces(double *__restrict__ v,
+                           const afh_box_meta *__restrict__ meta,
+                           const int32_t *__restrict__ ids, int nc, size_t bsz,
+                           GcArgs ga) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nc * nc) return;
+  const int id = ids[blockIdx.z];
+  const int nb = blockIdx.y + 1;
+  const int d = (nb - 1) >> 1;
+  const bool low = ((nb - 1) & 1) == 0;
+  const int ta = (d == 0) ? 1 : 0, tb = (d == 2) ? 1 : 2;
+  const int a = t % nc + 1, b = t / nc + 1;
+  const int ng = nc + 2;
+  const afh_box_meta &m = meta[id - 1];
+  double *c = v + (size_t)(id - 1) * bsz;
+  const int nb_id = m.neighbors[nb - 1];
+  int p[3];
+  p[ta] = a;
+  p[tb] = b;
+  p[d] = low ? 0 : nc + 1;
+  const size_t dst = ix3(ng, p[0], p[1], p[2]);
+
+  if (nb_id > 0) {
+    // copy_from_nb: ghost(lo) = neighbor(lo - dnb * nc)
+    int q[3] = {p[0], p[1], p[2]};
+    q[d] = low ? nc : 1;
+    c[dst] = v[(size_t)(nb_id - 1) * bsz + ix3(ng, q[0], q[1], q[2])];
+    return;
+  }
+  const int x1 = low ? 1 : nc;
+  const int x2 = low ? 2 : nc - 1;
+  if (nb_id < 0) {
+    // bc_to_gc
+    double c0, c1, c2;
+    const afh_bc bc = ga.bc[nb - 1];
+    switch (bc.type) {
+    case AFH_BC_DIRICHLET: c0 = 2; c1 = -1; c2 = 0; break;
+    case AFH_BC_NEUMANN: c0 = m.dr[d] * (low ? -1 : 1); c1 = 1; c2 = 0; break;
+    case AFH_BC_CONTINUOUS: c0 = 0; c1 = 2; c2 = -1; break;
+    default: c0 = 1; c1 = 0; c2 = 0; break;
+    }
+    int q1[3] = {p[0], p[1], p[2]}, q2[3] = {p[0], p[1], p[2]};
+    q1[d] = x1;
+    q2[d] = x2;
+    c[dst] = c0 * bc.value + c1 * c[ix3(ng, q1[0], q1[1], q1[2])] +
+             c2 * c[ix3(ng, q2[0], q2[1], q2[2])];
+    return;
+  }
+  // refinement boundary: coarse data from the parent's neighbour
+  const int p_id = m.parent;
+  const int p_nb_id = meta[p_id - 1].neighbors[nb - 1];
+  const double *cp = v + (size_t)(p_nb_id - 1) * bsz;
+  const int hnc = nc >> 1;
+  int co[3];
+  for (int q = 0; q < 3; q++) co[q] = ((m.ix[q] - 1) & 1) * hnc;
+
+  if (ga.rb == AFH_RB_MG_SIDES) {
+    // mg_sides_rb: tmp(x, y) = coarse value next to the face, at tangential
+    // offsets co; gc = tmp +- g1 +- g2; ghost = 0.5 gc + 0.75 x_i - 0.25 x_i+d
+    const int cn = low ? nc : 1;
+    const int ii = (a + 1) >> 1, jj = (b + 1) >> 1;
+    auto tmp = [&](int x, int y) {
+      int q[3];
+      q[d] = cn;
+      q[ta] = co[ta] + x;
+      q[tb] = co[tb] + y;
+      return cp[ix3(ng, q[0], q[1], q[2])];
+    };
+    const double g1 = 0.125 * (tmp(ii + 1, jj) - tmp(ii - 1, jj));
+    const double g2 = 0.125 * (tmp(ii, jj + 1) - tmp(ii, jj - 1));
+    const double t0 = tmp(ii, jj);
+    double gcv;
+    if (a & 1) {
+      gcv = (b & 1) ? t0 - g1 - g2 : t0 - g1 + g2;
+    } else {
+      gcv = (b & 1) ? t0 + g1 - g2 : t0 + g1 + g2;
+    }
+    int q1[3] = {p[0], p[1], p[2]}, q2[3] = {p[0], p[1], p[2]};
+    q1[d] = x1;
+    q2[d] = x2;
+    c[dst] = 0.5 * gcv + 0.75 * c[ix3(ng, q1[0], q1[1], q1[2])] -
+             0.25 * c[ix3(ng, q2[0], q2[1], q2[2])];
+    return;
+  }
+  // af_gc_interp / af_gc_interp_lim; offsets on the parent's neighbour
+  const double third = 1 / 3.0, sixth = 1 / 6.0;
+  int off[3] = {co[0], co[1], co[2]};
+  off[d] -= (low ? -1 : 1) * nc;
+  const int ix_c = low ? nc : 1;
+  const int a1 = off[ta] + ((a + 1) >> 1), a2 = a1 + 1 - 2 * (a & 1);
+  const int b1 = off[tb] + ((b + 1) >> 1), b2 = b1 + 1 - 2 * (b & 1);
+  int q[3];
+  q[d] = ix_c;
+  q[ta] = a1, q[tb] = b1;
+  const double cv1 = cp[ix3(ng, q[0], q[1], q[2])];
+  double cv2, cv3;
+  if (d < 2) {
+    q[ta] = a2, q[tb] = b1;
+    cv2 = cp[ix3(ng, q[0], q[1], q[2])];
+    q[ta] = a1, q[tb] = b2;
+    cv3 = cp[ix3(ng, q[0], q[1], q[2])];
+  } else {
+    // case (3): c(2) uses j_c2 and c(3) uses i_c2 (m_af_ghostcell.f90:479-482)
+    q[ta] = a1, q[tb] = b2;
+    cv2 = cp[ix3(ng, q[0], q[1], q[2])];
+    q[ta] = a2, q[tb] = b1;
+    cv3 = cp[ix3(ng, q[0], q[1], q[2])];
+  }
+  int qf[3] = {p[0], p[1], p[2]};
+  qf[d] = x1;
+  double val = third * cv1 + sixth * cv2 + sixth * cv3 +
+               third * c[ix3(ng, qf[0], qf[1], qf[2])];
+  if (ga.rb == AFH_RB_GC_INTERP_LIM && val > 2 * cv1) val = 2 * cv1;
+  c[dst] = val;
+}
+
+// ------------------------------------------------------------ edges+corners
+__constant__ int c_edge_dim[12] = {0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2};
+__constant__ int c_edge_dir[12][3] = {
+    {0, -1, -1}, {0, 1, -1}, {0, -1, 1}, {0, 1, 1}, {-1, 0, -1}, {1, 0, -1},
+    {-1, 0, 1},  {1, 0, 1},  {-1, -1, 0}, {1, -1, 0}, {-1, 1, 0}, {1, 1, 0}};
+__constant__ int c_edge_min[12][3] = {
+    {0, 0, 0}, {0, 1, 0}, {0, 0, 1}, {0, 1, 1}, {0, 0, 0}, {1, 0, 0},
+    {0, 0, 1}, {1, 0, 1}, {0, 0, 0}, {1, 0, 0}, {0, 1, 0}, {1, 1, 0}};
+__constant__ int c_child_dix[8][3] = {{0, 0, 0}, {1, 0, 0}, {0, 1, 0},
+                                      {1, 1, 0}, {0, 0, 1}, {1, 0, 1},
+                                      {0, 1, 1}, {1, 1, 1}};
+
+__global__ void k_gc_corners(double *__restrict__ v,
+                             const afh_box_meta *__restrict__ meta,
+                             const int32_t *__restrict__ ids, int nc,
+                             size_t bsz) {
+  const int id = ids[blockIdx.x];
+  const int ng = nc + 2;
+  const afh_box_meta &m = meta[id - 1];
+  double *c = v + (size_t)(id - 1) * bsz;
+  // edges (af_gc_box_corner, first loop)
+  for (int e = threadIdx.x; e < 12 * nc; e += blockDim.x) {
+    const int n = e / nc, pos = e % nc + 1;
+    const int dim = c_edge_dim[n];
+    const int dx = c_edge_dir[n][0], dy = c_edge_dir[n][1], dz = c_edge_dir[n][2];
+    const int nb_id = m.neighbor_mat[(dx + 1) + 3 * (dy + 1) + 9 * (dz + 1)];
+    int x[3];
+    for (int q = 0; q < 3; q++) x[q] = c_edge_min[n][q] * (nc + 1);
+    x[dim] = pos;
+    if (nb_id > 0) {
+      // dnb = offsets of the two adjacent neighbours = edge direction
+      int s[3] = {x[0] - dx * nc, x[1] - dy * nc, x[2] - dz * nc};
+      c[ix3(ng, x[0], x[1], x[2])] =
+          v[(size_t)(nb_id - 1) * bsz + ix3(ng, s[0], s[1], s[2])];
+    } else {
+      // af_edge_gc_extrap
+      const int o1 = (dim + 1) % 3, o2 = (dim + 2) % 3;
+      int di[3];
+      for (int q = 0; q < 3; q++) di[q] = 1 - 2 * (x[q] & 1);
+      di[dim] = 0;
+      int ia[3] = {x[0], x[1], x[2]}, ib[3] = {x[0], x[1], x[2]};
+      ia[o1] += di[o1];
+      ib[o2] += di[o2];
+      int ic[3] = {x[0] + di[0], x[1] + di[1], x[2] + di[2]};
+      c[ix3(ng, x[0], x[1], x[2])] = c[ix3(ng, ia[0], ia[1], ia[2])] +
+                                     c[ix3(ng, ib[0], ib[1], ib[2])] -
+                                     c[ix3(ng, ic[0], ic[1], ic[2])];
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 8) {
+    const int n = threadIdx.x;
+    int dnb[3], x[3];
+    for (int q = 0; q < 3; q++) {
+      dnb[q] = 2 * c_child_dix[n][q] - 1;
+      x[q] = c_child_dix[n][q] * (nc + 1);
+    }
+    const int nb_id =
+        m.neighbor_mat[(dnb[0] + 1) + 3 * (dnb[1] + 1) + 9 * (dnb[2] + 1)];
+    if (nb_id > 0) {
+      c[ix3(ng, x[0], x[1], x[2])] =
+          v[(size_t)(nb_id - 1) * bsz +
+            ix3(ng, x[0] - dnb[0] * nc, x[1] - dnb[1] * nc, x[2] - dnb[2] * nc)];
+    } else {
+      int di[3];
+      for (int q = 0; q < 3; q++) di[q] = 1 - 2 * (x[q] & 1);
+      c[ix3(ng, x[0], x[1], x[2])] =
+          c[ix3(ng, x[0], x[1] + di[1], x[2] + di[2])] +
+          c[ix3(ng, x[0] + di[0], x[1], x[2] + di[2])] +
+          c[ix3(ng, x[0] + di[0], x[1] + di[1], x[2])] -
+          2 * c[ix3(ng, x[0] + di[0], x[1] + di[1], x[2] + di[2])];
+    }
+  }
+}
+
+int32_t gc_lvl(afh_tree *t, int lvl, int iv, int corners) {
+  const int n = t->ids.n(lvl);
+  if (n == 0) return AFH_OK;
+  const int nc = t->nc;
+  dim3 grid((nc * nc + 255) / 256, 6, n);
+  prof_begin(t, AFH_PROF_GHOST);
+  hipLaunchKernelGGL(k_gc_faces, grid, dim3(256), 0, t->stream, t->ccv(iv),
+                     t->d_boxes, t->ids.at(lvl), nc, t->bsz, t->gc_args(iv));
+  // algorithmic bytes: read one interior layer + write one ghost layer
+  prof_end(t, AFH_PROF_GHOST, 16.0 * 6 * nc * nc * n);
+  AFH_LAUNCH_CHECK("k_gc_faces");
+  if (corners) {
+    hipLaunchKernelGGL(k_gc_corners, dim3(n), dim3(256), 0, t->stream,
+                       t->ccv(iv), t->d_boxes, t->ids.at(lvl), nc, t->bsz);
+    AFH_LAUNCH_CHECK("k_gc_corners");
+  }
+  return AFH_OK;
+}
+
+// ------------------------------------------------------------ restriction
+// af_restrict_box (m_af_restrict.f90:62-136): parent octant cell = 0.125 *
+// sum of its 8 children in column-major order. One thread per parent cell.
+__global__ void k_restrict(double *__restrict__ v,
+                           const afh_box_meta *__restrict__ meta,
+                           const int32_t *__restrict__ ids, int nc,
+                           size_t bsz) {
+  const int hnc = nc >> 1;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= hnc * hnc * hnc) return;
+  const int id = ids[blockIdx.y];
+  const afh_box_meta &m = meta[id - 1];
+  const int i = t % hnc + 1, j = (t / hnc) % hnc + 1, k = t / (hnc * hnc) + 1;
+  const int ng = nc + 2;
+  const double *c = v + (size_t)(id - 1) * bsz;
+  double *p = v + (size_t)(m.parent - 1) * bsz;
+  const int fi = 2 * i - 1, fj = 2 * j - 1, fk = 2 * k - 1;
+  double s = c[ix3(ng, fi, fj, fk)];
+  s += c[ix3(ng, fi + 1, fj, fk)];
+  s += c[ix3(ng, fi, fj + 1, fk)];
+  s += c[ix3(ng, fi + 1, fj + 1, fk)];
+  s += c[ix3(ng, fi, fj, fk + 1)];
+  s += c[ix3(ng, fi + 1, fj, fk + 1)];
+  s += c[ix3(ng, fi, fj + 1, fk + 1)];
+  s += c[ix3(ng, fi + 1, fj + 1, fk + 1)];
+  const int o0 = ((m.ix[0] - 1) & 1) * hnc, o1 = ((m.ix[1] - 1) & 1) * hnc,
+            o2 = ((m.ix[2] - 1) & 1) * hnc;
+  p[ix3(ng, o0 + i, o1 + j, o2 + k)] = 0.125 * s;
+}
+
+int32_t restrict_boxes(afh_tree *t, const int32_t *d_ids, int n, int iv) {
+  if (n == 0) return AFH_OK;
+  const int hnc = t->nc / 2, cells = hnc * hnc * hnc;
+  hipLaunchKernelGGL(k_restrict, dim3((cells + 255) / 256, n), dim3(256), 0,
+                     t->stream, t->ccv(iv), t->d_boxes, d_ids, t->nc, t->bsz);
+  AFH_LAUNCH_CHECK("k_restrict");
+  return AFH_OK;
+}
+
+// ------------------------------------------------------------ reductions
+// max |x| over the interiors of the listed boxes -> atomicMax (orderable)
+__global__ void k_maxabs(const double *__restrict__ v,
+                         const int32_t *__restrict__ ids, int nc, size_t bsz,
+                         unsigned long long *out) {
+  const int ng = nc + 2;
+  const int id = ids[blockIdx.y];
+  const double *c = v + (size_t)(id - 1) * bsz;
+  const int n3 = nc * nc * nc;
+  double mx = 0.0;
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < n3;
+       t += gridDim.x * blockDim.x) {
+    const int i = t % nc + 1, j = (t / nc) % nc + 1, k = t / (nc * nc) + 1;
+    mx = fmax(mx, fabs(c[ix3(ng, i, j, k)]));
+  }
+  for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
+  __shared__ double red[16];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) red[w] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int q = 1; q < (int)(blockDim.x >> 6); q++) mx = fmax(mx, red[q]);
+    atomicMax(out, dbl_to_ord(mx));
+  }
+}
+
+}  // namespace afh
+
+using namespace afh;
+
+extern "C" {
+
+const char *afh_last_error(void) { return afh::g_err; }
+
+static int32_t upload_list(afh_tree *t, LevelList &L,
+                           const std::vector<std::vector<int32_t>> &lists) {
+  L.off.assign(lists.size() + 1, 0);
+  std::vector<int32_t> flat;
+  for (size_t l = 0; l < lists.size(); l++) {
+    flat.insert(flat.end(), lists[l].begin(), lists[l].end());
+    L.off[l + 1] = (int32_t)flat.size();
+  }
+  AFH_HIP(hipMalloc(&L.d, sizeof(int32_t) * (flat.size() + 1)));
+  if (!flat.empty())
+    AFH_HIP(hipMemcpy(L.d, flat.data(), sizeof(int32_t) * flat.size(),
+                      hipMemcpyHostToDevice));
+  return AFH_OK;
+}
+
+int32_t afh_tree_create(const afh_tree_desc *d, int32_t device,
+                        afh_tree **out) {
+  if (!d || !out || d->n_cell < 2 || (d->n_cell & 1) || d->n_boxes < 1 ||
+      d->highest_lvl < 1 || d->n_var_cell < 1)
+    return set_error(AFH_ERR_ARG, "afh_tree_create: bad descriptor");
+  if (d->n_cell > 128)
+    return set_error(AFH_ERR_UNSUPPORTED, "n_cell > 128 not supported");
+  if (d->periodic[0] || d->periodic[1] || d->periodic[2])
+    return set_error(AFH_ERR_UNSUPPORTED, "periodic domains not supported");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1)
+    return set_error(AFH_ERR_DEVICE, "no HIP device available");
+  afh_tree *t = new afh_tree();
+  if (device >= 0) {
+    AFH_HIP(hipSetDevice(device));
+    t->device = device;
+  } else {
+    AFH_HIP(hipGetDevice(&t->device));
+  }
+  AFH_HIP(hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking));
+  t->nc = d->n_cell;
+  t->ng = d->n_cell + 2;
+  t->nb = d->n_boxes;
+  t->nlvl = d->highest_lvl;
+  t->nvc = d->n_var_cell;
+  t->nvf = d->n_var_face;
+  t->bsz = (size_t)t->ng * t->ng * t->ng;
+  t->fsz = 3 * (size_t)(t->nc + 1) * (t->nc + 1) * (t->nc + 1);
+  for (int q = 0; q < 3; q++) {
+    t->cgs[q] = d->coarse_grid_size[q];
+    t->r_base[q] = d->r_base[q];
+    t->dr_base[q] = d->dr_base[q];
+  }
+  t->boxes.assign(d->boxes, d->boxes + t->nb);
+  t->meth.assign(t->nvc + 1, CcMethod());
+  auto split = [&](const int32_t *arr, const int32_t *off) {
+    std::vector<std::vector<int32_t>> v(t->nlvl);
+    for (int l = 0; l < t->nlvl; l++) v[l].assign(arr + off[l], arr + off[l + 1]);
+    return v;
+  };
+  t->h_ids = split(d->lvl_ids, d->lvl_ids_off);
+  t->h_leaves = split(d->lvl_leaves, d->lvl_leaves_off);
+  t->h_parents = split(d->lvl_parents, d->lvl_parents_off);
+  for (auto &lv : t->h_ids)
+    for (int32_t id : lv)
+      if (id < 1 || id > t->nb) return set_error(AFH_ERR_ARG, "bad box id %d", id);
+  // derived task lists
+  std::vector<std::vector<int32_t>> refb(t->nlvl), cfl(t->nlvl);
+  for (int l = 0; l < t->nlvl; l++) {
+    for (int32_t id : t->h_leaves[l]) {
+      const afh_box_meta &m = t->boxes[id - 1];
+      bool any = false;
+      for (int nb = 0; nb < 6; nb++) any |= (m.neighbors[nb] == 0);
+      if (m.parent > 0 && any) refb[l].push_back(id);
+    }
+    for (int32_t id : t->h_parents[l]) {
+      const afh_box_meta &m = t->boxes[id - 1];
+      for (int nb = 1; nb <= 6; nb++) {
+        int nb_id = m.neighbors[nb - 1];
+        if (nb_id > 0 && t->boxes[nb_id - 1].children[0] == 0)
+          cfl[l].push_back(id * 8 + nb);
+      }
+    }
+  }
+  int32_t e;
+  if ((e = upload_list(t, t->ids, t->h_ids)) ||
+      (e = upload_list(t, t->leaves, t->h_leaves)) ||
+      (e = upload_list(t, t->parents, t->h_parents)) ||
+      (e = upload_list(t, t->refb, refb)) || (e = upload_list(t, t->cflux, cfl)))
+    return e;
+  AFH_HIP(hipMalloc(&t->d_boxes, sizeof(afh_box_meta) * t->nb));
+  AFH_HIP(hipMemcpy(t->d_boxes, t->boxes.data(), sizeof(afh_box_meta) * t->nb,
+                    hipMemcpyHostToDevice));
+  size_t ncc = (size_t)t->nvc * t->nb * t->bsz;
+  size_t nfc = (size_t)std::max(1, t->nvf) * t->nb * t->fsz;
+  AFH_HIP(hipMalloc(&t->cc, ncc * sizeof(double)));
+  AFH_HIP(hipMalloc(&t->fc, nfc * sizeof(double)));
+  AFH_HIP(hipMemsetAsync(t->cc, 0, ncc * sizeof(double), t->stream));
+  AFH_HIP(hipMemsetAsync(t->fc, 0, nfc * sizeof(double), t->stream));
+  AFH_HIP(hipMalloc(&t->gc2, sizeof(double) * (size_t)t->nb * 6 * t->nc * t->nc));
+  AFH_HIP(hipMalloc(&t->scratch, 64 * sizeof(double)));
+  AFH_HIP(hipHostMalloc(&t->h_scratch, 64 * sizeof(double)));
+  AFH_HIP(hipStreamSynchronize(t->stream));
+  *out = t;
+  return AFH_OK;
+}
+
+int32_t afh_profile_enable(afh_tree *t, int32_t kclass) {
+  if (!t) return set_error(AFH_ERR_ARG, "null tree");
+  AFH_HIP(hipStreamSynchronize(t->stream));
+  t->prof_class = kclass;
+  t->ev_used = 0;
+  t->prof_bytes = 0;
+  t->prof_launches = 0;
+  return AFH_OK;
+}
+
+int32_t afh_profile_read(afh_tree *t, double *total_ms, int64_t *launches,
+                         double *bytes) {
+  if (!t || !total_ms || !launches || !bytes)
+    return set_error(AFH_ERR_ARG, "null argument");
+  AFH_HIP(hipStreamSynchronize(t->stream));
+  double ms = 0;
+  for (size_t q = 0; q + 1 < t->ev_used; q += 2) {
+    float e = 0;
+    AFH_HIP(hipEventElapsedTime(&e, t->ev_pool[q], t->ev_pool[q + 1]));
+    ms += e;
+  }
+  *total_ms = ms;
+  *launches = t->prof_launches;
+  *bytes = t->prof_bytes;
+  t->ev_used = 0;
+  t->prof_bytes = 0;
+  t->prof_launches = 0;
+  return AFH_OK;
+}
+
+int32_t afh_tree_destroy(afh_tree *t) {
+  if (!t) return AFH_OK;
+  hipStreamSynchronize(t->stream);
+  for (hipEvent_t e : t->ev_pool) hipEventDestroy(e);
+  for (LevelList *L : {&t->ids, &t->leaves, &t->parents, &t->refb, &t->cflux})
+    hipFree(L->d);
+  hipFree(t->d_boxes);
+  hipFree(t->cc);
+  hipFree(t->fc);
+  hipFree(t->gc2);
+  hipFree(t->scratch);
+  hipHostFree(t->h_scratch);
+  hipStreamDestroy(t->stream);
+  delete t;
+  return AFH_OK;
+}
+
+int32_t afh_tree_sync(afh_tree *t) {
+  AFH_HIP(hipStreamSynchronize(t->stream));
+  return AFH_OK;
+}
+
+int32_t afh_set_cc_methods(afh_tree *t, int32_t iv, const afh_bc *bc6,
+                           int32_t rb, int32_t lim) {
+  if (!t || iv < 1 || iv > t->nvc || !bc6)
+    return set_error(AFH_ERR_ARG, "afh_set_cc_methods: bad argument");
+  if (rb < AFH_RB_GC_INTERP || rb > AFH_RB_MG_SIDES)
+    return set_error(AFH_ERR_UNSUPPORTED, "refinement-boundary method %d", rb);
+  if (lim < AFH_LIM_NONE || lim > AFH_LIM_ZERO)
+    return set_error(AFH_ERR_UNSUPPORTED, "limiter %d", lim);
+  CcMethod &m = t->meth[iv];
+  m.set = 1;
+  for (int n = 0; n < 6; n++) {
+    if (bc6[n].type < AFH_BC_DIRICHLET_COPY || bc6[n].type > AFH_BC_DIRICHLET)
+      return set_error(AFH_ERR_UNSUPPORTED, "bc type %d", bc6[n].type);
+    m.bc[n] = bc6[n];
+  }
+  m.rb = rb;
+  m.lim = lim;
+  return AFH_OK;
+}
+
+int32_t afh_set_bc(afh_tree *t, int32_t iv, int32_t nb, int32_t type,
+                   double value) {
+  if (!t || iv < 1 || iv > t->nvc || nb < 1 || nb > 6)
+    return set_error(AFH_ERR_ARG, "afh_set_bc: bad argument");
+  t->meth[iv].bc[nb - 1].type = type;
+  t->meth[iv].bc[nb - 1].value = value;
+  return AFH_OK;
+}
+
+int32_t afh_cc_put(afh_tree *t, int32_t iv, const double *h) {
+  if (!t || iv < 1 || iv > t->nvc || !h)
+    return set_error(AFH_ERR_ARG, "afh_cc_put: bad argument");
+  AFH_HIP(hipMemcpyAsync(t->ccv(iv), h, sizeof(double) * t->bsz * t->nb,
+                         hipMemcpyHostToDevice, t->stream));
+  AFH_HIP(hipStreamSynchronize(t->stream));
+  return AFH_OK;
+}
+int32_t afh_cc_get(afh_tree *t, int32_t iv, double *h) {
+  if (!t || iv < 1 || iv > t->nvc || !h)
+    return set_error(AFH_ERR_ARG, "afh_cc_get: bad argument");
+  AFH_HIP(hipMemcpyAsync(h, t->ccv(iv), sizeof(double) * t->bsz * t->nb,
+                         hipMemcpyDeviceToHost, t->stream));
+  AFH_HIP(hipStreamSynchronize(t->stream));
+  return AFH_OK;
+}
+int32_t afh_fc_put(afh_tree *t, int32_t ivf, const double *h) {
+  if (!t || ivf < 1 || ivf > t->nvf || !h)
+    return set_error(AFH_ERR_ARG, "afh_fc_put: bad argument");
+  AFH_HIP(hipMemcpyAsync(t->fcv(ivf), h, sizeof(double) * t->fsz * t->nb,
+                         hipMemcpyHostToDevice, t->stream));
+  AFH_HIP(hipStreamSynchronize(t->stream));
+  return AFH_OK;
+}
+int32_t afh_fc_get(afh_tree *t, int32_t ivf, double *h) {
+  if (!t || ivf < 1 || ivf > t->nvf || !h)
+    return set_error(AFH_ERR_ARG, "afh_fc_get: bad argument");
+  AFH_HIP(hipMemcpyAsync(h, t->fcv(ivf), sizeof(double) * t->fsz * t->nb,
+                         hipMemcpyDeviceToHost, t->stream));
+  AFH_HIP(hipStreamSynchronize(t->stream));
+  return AFH_OK;
+}
+
+int32_t afh_gc_lvl(afh_tree *t, int32_t lvl, int32_t iv, int32_t corners) {
+  if (!t || lvl < 1 || lvl > t->nlvl || iv < 1 || iv > t->nvc ||
+      !t->meth[iv].set)
+    return set_error(AFH_ERR_ARG, "afh_gc_lvl: bad argument / no methods");
+  return gc_lvl(t, lvl, iv, corners);
+}
+
+int32_t afh_gc_tree(afh_tree *t, int32_t iv, int32_t corners) {
+  for (int l = 1; l <= (t ? t->nlvl : 0); l++) {
+    int32_t e = afh_gc_lvl(t, l, iv, corners);
+    if (e) return e;
+  }
+  return t ? AFH_OK : set_error(AFH_ERR_ARG, "null tree");
+}
+
+int32_t afh_restrict_tree(afh_tree *t, int32_t iv) {
+  if (!t || iv < 1 || iv > t->nvc) return set_error(AFH_ERR_ARG, "bad iv");
+  // af_restrict_tree: parents of levels highest-1..1, i.e. children of
+  // levels highest..2, coarsest last
+  for (int l = t->nlvl; l >= 2; l--) {
+    int32_t e = restrict_boxes(t, t->ids.at(l), t->ids.n(l), iv);
+    if (e) return e;
+  }
+  return AFH_OK;
+}
+
+int32_t afh_tree_copy_cc(afh_tree *t, int32_t a, int32_t b) {
+  if (!t || a < 1 || a > t->nvc || b < 1 || b > t->nvc)
+    return set_error(AFH_ERR_ARG, "bad iv");
+  AFH_HIP(hipMemcpyAsync(t->ccv(b), t->ccv(a), sizeof(double) * t->bsz * t->nb,
+                         hipMemcpyDeviceToDevice, t->stream));
+  return AFH_OK;
+}
+
+int32_t afh_tree_maxabs_cc(afh_tree *t, int32_t iv, double *out) {
+  if (!t || iv < 1 || iv > t->nvc || !out) return set_error(AFH_ERR_ARG, "bad iv");
+  unsigned long long init = host_dbl_to_ord(0.0);
+  auto *d = reinterpret_cast<unsigned long long *>(t->scratch);
+  AFH_HIP(hipMemcpyAsync(d, &init, sizeof init, hipMemcpyHostToDevice, t->stream));
+  const int nc = t->nc, n3 = nc * nc * nc;
+  int bx = std::min(64, (n3 + 255) / 256);
+  for (int l = 1; l <= t->nlvl; l++) {
+    int n = t->leaves.n(l);
+    if (!n) continue;
+    hipLaunchKernelGGL(k_maxabs, dim3(bx, n), dim3(256), 0, t->stream,
+                       t->ccv(iv), t->leaves.at(l), nc, t->bsz, d);
+    AFH_LAUNCH_CHECK("k_maxabs");
+  }
+  unsigned long long r;
+  AFH_HIP(hipMemcpyAsync(&r, d, sizeof r, hipMemcpyDeviceToHost, t->stream));
+  AFH_HIP(hipStreamSynchronize(t->stream));
+  *out = ord_to_dbl(r);
+  return AFH_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,191 @@
+#!/usr/bin/env python3
+"""Benchmark: cell-updates/s of the afivo-streamer hot path on MI355X.
+
+One step = one unit of SURVEY.md 8(d) on every leaf cell: field_set_rhs +
+max|rhs| + one FAS V(2,2)-cycle with the residual + max|residual| (the
+field_compute convergence test) + field_from_potential (gradient, |E|, |E|
+ghost cells) + flux_upwind_tree + flux_update_densities with chemistry
+(a forward-Euler sub-step, af_forward_euler), all through libafivo_hip.so.
+
+Default workload: S1-64: a uniform 3-D tree of 512 leaf boxes
+of 64^3 cells (134 M leaf cells, 585 boxes, 4 levels, 64^3 coarse grid),
+16 mm cube, electrons + M+ + M- (td_air_siglo_swarm.txt old-style model),
+Gaussian seed, -2.5 MV/m background field. Synthetic data, FP64.
+
+Multi-GPU (torchrun, one rank per GPU): every rank advances its own replica
+of the workload (no data-path collective; scaling "weak"); a barrier brackets
+the timed region and the time is the max over ranks.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "afivo-streamer_amd"))
+sys.path.insert(0, os.path.join(REPO, "tests"))
+
+CONFIGS = {
+    # name: (n_cell, coarse grid, levels, domain [m])
+    "s1-64": (64, (64, 64, 64), 4, (16e-3, 16e-3, 16e-3)),
+    "s1": (16, (16, 16, 16), 4, (16e-3, 16e-3, 16e-3)),
+}
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E peak (spec)
+
+
+def build_case(lib, config, device, coarse_cycles):
+    from afh.streamer import StreamerCase, seed_state, tables_from
+    from afh.tree import uniform_tree
+    import golden
+    nc, cgs, lvls, dom = CONFIGS[config]
+    topo = uniform_tree(nc, cgs, dom, lvls)
+    g = golden.load("uni8")  # transport/chemistry tables exported from the reference
+    td, chem = tables_from(g)
+    voltage = -dom[2] * (-2.5e6)
+    case = StreamerCase(lib, topo, td, chem, voltage, coarse_cycles=coarse_cycles,
+                        device=device)
+    seed_state(case, width=0.05 * dom[2])
+    return case
+
+
+def unit_step(case, dt):
+    """field_compute(1 V-cycle) + forward-Euler sub-step; returns dt limits."""
+    res = case.field_compute(0, n_vcycles=1)
+    d1 = case.fluid.flux_upwind_tree(0)
+    d2 = case.fluid.flux_update_densities(dt, 0, [0], [1.0], 0, True)
+    return res, d1, d2
+
+
+def cpu_baseline(config, steps=2):
+    """The C oracle (oracle/lib/libafo.so, OpenMP) on a bounded sample of the
+    same workload: the same 64^3 boxes but a 3-level tree (64 leaf boxes)."""
+    from afh import capi
+    from afh.streamer import StreamerCase, seed_state, tables_from
+    from afh.tree import uniform_tree
+    import golden
+    nc, cgs, lvls, dom = CONFIGS[config]
+    sample_lvls = 3 if config == "s1-64" else lvls
+    topo = uniform_tree(nc, cgs, dom, sample_lvls)
+    g = golden.load("uni8")
+    td, chem = tables_from(g)
+    lib = capi.oracle_library()
+    case = StreamerCase(lib, topo, td, chem, -dom[2] * (-2.5e6), coarse_cycles=8)
+    seed_state(case, width=0.05 * dom[2])
+    unit_step(case, 1e-13)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        unit_step(case, 1e-13)
+    dt = time.perf_counter() - t0
+    from afh.streamer import cells
+    ncell = cells(topo)
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    return {"value": ncell * steps / dt, "unit": "cell-updates/s",
+            "cores": threads, "kind": "port",
+            "sample": "%d steps on a %d-level uniform tree of %d leaf boxes of "
+                      "%d^3 (%d cells), C oracle OpenMP" %
+                      (steps, sample_lvls, ncell // nc ** 3, nc, ncell)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="s1-64", choices=sorted(CONFIGS))
+    ap.add_argument("--coarse-cycles", type=int, default=8)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
+        if torch.cuda.is_available():
+            torch.cuda.set_device(local)
+
+    from afh import capi
+    lib = capi.hip_library()
+    case = build_case(lib, args.config, local, args.coarse_cycles)
+    from afh.streamer import cells
+    ncell = cells(case.topo)
+    dt = 1e-13
+
+    case.field_compute(0, n_vcycles=2)  # initial potential (untimed)
+    for _ in range(args.warmup):
+        unit_step(case, dt)
+    case.tree.sync()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    # timed region: K steps; the GSRB kernel is timed with HIP events on the
+    # tree's stream (afh_profile_*) over the same region
+    lib.call("profile_enable", case.tree.h, capi.PROF_GSRB)
+    barrier()
+    case.tree.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        last = unit_step(case, dt)
+    case.tree.sync()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    import ctypes as C
+    ms, nl, by = C.c_double(), C.c_int64(), C.c_double()
+    lib.call("profile_read", case.tree.h, C.byref(ms), C.byref(nl), C.byref(by))
+
+    if dist is not None:
+        import torch
+        tt = torch.tensor([elapsed], dtype=torch.float64,
+                          device="cuda" if torch.cuda.is_available() else "cpu")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    if rank == 0:
+        avg_s = ms.value / 1e3 / max(1, nl.value)
+        bytes_per_launch = by.value / max(1, nl.value)
+        achieved = bytes_per_launch / avg_s / 1e9 if avg_s > 0 else 0.0
+        out = {
+            "metric": "cell-updates/s (fluid+MG V-cycle)",
+            "value": ncell * args.steps * world / elapsed,
+            "unit": "cell-updates/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1e3 * elapsed / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic",
+            "config": {"workload": args.config, "n_cell": CONFIGS[args.config][0],
+                       "leaf_cells_per_gpu": ncell, "boxes": int(case.topo["n_boxes"]),
+                       "levels": int(case.topo["highest_lvl"]),
+                       "coarse_cycles": args.coarse_cycles,
+                       "parallelism": "replica-per-gpu"},
+            "roofline": {"bound": "hbm", "kernel": "k_gsrb",
+                         "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": None,
+                         "avg_launch_us": avg_s * 1e6,
+                         "algorithmic_bytes_per_launch": bytes_per_launch,
+                         "launches": nl.value},
+            "last_residual": last[0][-1] if last[0] else None,
+        }
+        if not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args.config)
+        print(json.dumps(out))
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

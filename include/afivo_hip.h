@@ -227,6 +227,19 @@ int32_t afh_flux_update_densities(afh_fluid *f, double dt, int32_t s_deriv,
                                   const double *w_prev, int32_t s_out,
                                   int32_t last_step, double *dt_lim);
 
+/* Kernel timing (replaces the reference's omp_get_wtime cost buckets,
+ * src/m_streamer.f90:181-187): while enabled, every launch of the selected
+ * kernel class is bracketed by HIP events on the tree's stream;
+ * afh_profile_read returns the summed device time, the number of launches
+ * and the algorithmic HBM bytes those launches move, then resets. */
+#define AFH_PROF_GSRB 1      /* red-black Gauss-Seidel half sweep */
+#define AFH_PROF_GHOST 2     /* ghost-cell fill (faces) */
+#define AFH_PROF_FLUX 3      /* flux kernel */
+#define AFH_PROF_UPDATE 4    /* density update */
+int32_t afh_profile_enable(afh_tree *t, int32_t kclass);
+int32_t afh_profile_read(afh_tree *t, double *total_ms, int64_t *launches,
+                         double *bytes);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1493,3 +1493,14 @@ int32_t afo_flux_update_densities(afh_fluid *fl, double dt, int32_t s_deriv,
   dt_lim[1] = 1e100;
   return AFH_OK;
 }
+
+/* Kernel timing is a device concept; the oracle accepts and ignores it. */
+int32_t afo_profile_enable(afh_tree *t, int32_t kclass) {
+  (void)t, (void)kclass;
+  return AFH_OK;
+}
+int32_t afo_profile_read(afh_tree *t, double *ms, int64_t *n, double *bytes) {
+  (void)t;
+  *ms = 0, *n = 0, *bytes = 0;
+  return AFH_OK;
+}

@@ -54,6 +54,9 @@ int32_t afo_flux_update_densities(afh_fluid *f, double dt, int32_t s_deriv,
                                   int32_t n_prev, const int32_t *s_prev,
                                   const double *w_prev, int32_t s_out,
                                   int32_t last_step, double *dt_lim);
+int32_t afo_profile_enable(afh_tree *t, int32_t kclass);
+int32_t afo_profile_read(afh_tree *t, double *total_ms, int64_t *launches,
+                         double *bytes);
 /* Debug hooks: the individual V-cycle stages (for golden trace tests). */
 int32_t afo_mg_gsrb_boxes(afh_mg *mg, int32_t lvl, int32_t up);
 int32_t afo_mg_update_coarse(afh_mg *mg, int32_t lvl);
