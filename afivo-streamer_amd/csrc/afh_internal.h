@@ -78,6 +78,9 @@ struct afh_tree {
   double *scratch = nullptr; // reductions etc.
   double *h_scratch = nullptr;
   std::vector<afh::CcMethod> meth;
+  // grid spacing per level (afivo halves dr exactly per level, so every box
+  // of a level has the same bits; verified at tree creation)
+  std::vector<double> lvl_dr;  // 3 per level
   // kernel timing (afh_profile_*)
   int prof_class = 0;
   std::vector<hipEvent_t> ev_pool;

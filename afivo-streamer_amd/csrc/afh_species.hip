@@ -199,87 +199,136 @@ struct FluxArgs {
   const double *gc2;
   DevLT td;
   double N_inv;
+  double inv_dx[3];   // 1/dr per dimension of this level
   int lim;
 };
 
-__global__ void k_flux(FluxArgs A, const afh_box_meta *__restrict__ meta,
-                       const int32_t *__restrict__ ids, int nc, size_t bsz,
-                       size_t fsz, unsigned long long *red) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  const int id = ids[blockIdx.y];
-  double cfl = -HUGE_VAL, smax = -HUGE_VAL;
-  if (t < nc * nc * nc) {
-    const afh_box_meta &m = meta[id - 1];
-    const int ng = nc + 2, nf = nc + 1;
-    const int pos[3] = {t % nc + 1, (t / nc) % nc + 1, t / (nc * nc) + 1};
-    const double *ne = A.ne + (size_t)(id - 1) * bsz;
-    const double *E = A.E + (size_t)(id - 1) * bsz;
-    const double *Ef = A.Ef + (size_t)(id - 1) * fsz;
-    double *F = A.F + (size_t)(id - 1) * fsz;
-    const double SI_to_Td = 1e21;
-    cfl = 0.0;
-    for (int d = 0; d < 3; d++) {
-      const int ta = (d == 0) ? 1 : 0, tb = (d == 2) ? 1 : 2;
-      const int a = pos[ta], b = pos[tb], c = pos[d];
-      const double inv_dx = 1 / m.dr[d];
-      const size_t st = d == 0 ? 1 : d == 1 ? (size_t)ng : (size_t)ng * ng;
-      const size_t cc0 = ix3(ng, pos[0], pos[1], pos[2]);
-      auto line = [&](int mm) -> double {  // cc2 line value at index mm
-        if (mm == -1)
-          return A.gc2[((size_t)(id - 1) * 6 + 2 * d) * nc * nc +
-                       (size_t)(b - 1) * nc + (a - 1)];
-        if (mm == nc + 2)
-          return A.gc2[((size_t)(id - 1) * 6 + 2 * d + 1) * nc * nc +
-                       (size_t)(b - 1) * nc + (a - 1)];
-        return ne[cc0 + (ptrdiff_t)(mm - c) * (ptrdiff_t)st];
-      };
-      auto fpos = [&](int f) {
-        int q[3] = {pos[0], pos[1], pos[2]};
-        q[d] = f;
-        return fidx(nf, d, q[0], q[1], q[2]);
-      };
-      auto ecc = [&](int mm) { return E[cc0 + (ptrdiff_t)(mm - c) * (ptrdiff_t)st]; };
-      // transport at face f (between cells f-1, f): mu, D
-      auto transport = [&](int f, double &mu, double &dcf) {
-        const double tfc = 0.5 * (ecc(f - 1) + ecc(f)) * SI_to_Td * A.N_inv;
-        mu = lt_col(A.td, 1, tfc) * A.N_inv;
-        dcf = lt_col(A.td, 2, tfc) * A.N_inv;
-      };
-      auto face = [&](int f, double &v, double &dcf) {
-        const double ex = Ef[fpos(f)];
-        double u;
-        if (-1 * ex > 0)
-          u = line(f - 1) + 0.5 * limiter(A.lim, line(f) - line(f - 1),
-                                          line(f - 1) - line(f - 2));
-        else
-          u = line(f) - 0.5 * limiter(A.lim, line(f) - line(f - 1),
-                                      line(f + 1) - line(f));
-        double mu;
-        transport(f, mu, dcf);
-        v = -mu * ex;
-        F[fpos(f)] = v * u - dcf * inv_dx * (line(f) - line(f - 1));
-        smax = fmax(smax, mu * u);
-      };
-      double vl, dl, vh, dh;
-      face(c, vl, dl);
-      if (c == nc) {
-        face(nc + 1, vh, dh);
-      } else {
-        double mu;
-        transport(c + 1, mu, dh);
-        vh = -mu * Ef[fpos(c + 1)];
-      }
-      const double mv = fmax(fabs(vh), fabs(vl));
-      const double md = fmax(dh, dl);
-      cfl = cfl + (1.0 * mv * inv_dx + 2 * md * (inv_dx * inv_dx));
-    }
+// LT_get_col(td_tbl, td_mobility/td_diffusion, x): both columns at the same
+// location (src/m_fluid.f90:168-174, m_lookup_table.f90:330-406)
+__device__ __forceinline__ void lt_mu_dc(const DevLT &lt, double x, double &mu,
+                                         double &dc) {
+  const double frac = (x - lt.x_min) * lt.inv_fac;
+  int low;
+  double lf;
+  if (frac <= 0) {
+    low = 1;
+    lf = 1;
+  } else if (frac >= lt.n_points - 1) {
+    low = lt.n_points - 1;
+    lf = 0;
+  } else {
+    low = (int)ceil(frac);
+    lf = low - frac;
   }
-  // block max-reduction of cfl and sigma
+  const double *r = lt.rc + (low - 1);
+  mu = lf * r[0] + (1 - lf) * r[1];
+  dc = lf * r[lt.n_points] + (1 - lf) * r[lt.n_points + 1];
+}
+
+// One cell face between cells f-1 and f: upwind reconstruction with the
+// limiter (reconstruct_upwind_1d, m_af_flux_schemes.f90:282-303) and the
+// m_fluid flux_upwind callback (src/m_fluid.f90:160-205).
+__device__ __forceinline__ void face_eval(const FluxArgs &A, double Lm2,
+                                          double Lm1, double L0, double Lp1,
+                                          double Elo, double Ehi, double ex,
+                                          double inv_dx, double &v, double &dc,
+                                          double &flux, double &sigma) {
+  double u;
+  if (-1 * ex > 0)
+    u = Lm1 + 0.5 * limiter(A.lim, L0 - Lm1, Lm1 - Lm2);
+  else
+    u = L0 - 0.5 * limiter(A.lim, L0 - Lm1, Lp1 - L0);
+  const double tfc = 0.5 * (Elo + Ehi) * 1e21 * A.N_inv;
+  double mu, d;
+  lt_mu_dc(A.td, tfc, mu, d);
+  mu = mu * A.N_inv;
+  dc = d * A.N_inv;
+  v = -mu * ex;
+  flux = v * u - dc * inv_dx * (L0 - Lm1);
+  sigma = mu * u;
+}
+
+// transport only (for the CFL term of a face owned by another thread)
+__device__ __forceinline__ void face_vd(const FluxArgs &A, double Elo,
+                                        double Ehi, double ex, double &v,
+                                        double &dc) {
+  const double tfc = 0.5 * (Elo + Ehi) * 1e21 * A.N_inv;
+  double mu, d;
+  lt_mu_dc(A.td, tfc, mu, d);
+  mu = mu * A.N_inv;
+  dc = d * A.N_inv;
+  v = -mu * ex;
+}
+
+// One thread per cell. Each thread owns the low face of its cell in every
+// dimension (and the high face on the last cell of a line). The CFL sum needs
+// the velocity / diffusion of the high face too: in x it comes from the next
+// lane (__shfl_down, SHFL = lines of nc cells never straddle a wave); in y and
+// z it is recomputed (transport only, bitwise identical expression).
+template <bool SHFL>
+__global__ void __launch_bounds__(256)
+    k_flux(FluxArgs A, const int32_t *__restrict__ ids, int nc, size_t bsz,
+           size_t fsz, unsigned long long *red) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool active = t < nc * nc * nc;
+  const int tt = active ? t : 0;
+  const int id = ids[blockIdx.y];
+  const int i = tt % nc + 1, j = (tt / nc) % nc + 1, k = tt / (nc * nc) + 1;
+  const int ng = nc + 2, nf = nc + 1;
+  const double *ne = A.ne + (size_t)(id - 1) * bsz;
+  const double *E = A.E + (size_t)(id - 1) * bsz;
+  const double *Ef = A.Ef + (size_t)(id - 1) * fsz;
+  double *F = A.F + (size_t)(id - 1) * fsz;
+  const double *g2 = A.gc2 + (size_t)(id - 1) * 6 * nc * nc;
+  const int c0 = (k * ng + j) * ng + i;
+  const int fcell = ((k - 1) * nf + (j - 1)) * nf + (i - 1);
+  double cfl = 0.0, smax = -HUGE_VAL;
+#pragma unroll
+  for (int d = 0; d < 3; d++) {
+    const int st = d == 0 ? 1 : d == 1 ? ng : ng * ng;
+    const int fst = d == 0 ? 1 : d == 1 ? nf : nf * nf;
+    const int c = d == 0 ? i : d == 1 ? j : k;
+    const int a = d == 0 ? j : i, b = d == 2 ? j : k;
+    const int gq = (b - 1) * nc + (a - 1);
+    const double inv_dx = A.inv_dx[d];
+    const int fb = d * nf * nf * nf + fcell;
+    const double Lm2 = (c == 1) ? g2[(2 * d) * nc * nc + gq] : ne[c0 - 2 * st];
+    const double Lm1 = ne[c0 - st], L0 = ne[c0], Lp1 = ne[c0 + st];
+    const double Em1 = E[c0 - st], E0 = E[c0], Ep1 = E[c0 + st];
+    double vl, dl, fl, sl;
+    face_eval(A, Lm2, Lm1, L0, Lp1, Em1, E0, Ef[fb], inv_dx, vl, dl, fl, sl);
+    if (active) F[fb] = fl;
+    smax = fmax(smax, sl);
+    double vh, dh;
+    double vsh = 0, dsh = 0;
+    if (SHFL && d == 0) {
+      vsh = __shfl_down(vl, 1, 64);
+      dsh = __shfl_down(dl, 1, 64);
+    }
+    if (c == nc) {
+      const double Lp2 = g2[(2 * d + 1) * nc * nc + gq];
+      double fh, sh;
+      face_eval(A, Lm1, L0, Lp1, Lp2, E0, Ep1, Ef[fb + fst], inv_dx, vh, dh,
+                fh, sh);
+      if (active) F[fb + fst] = fh;
+      smax = fmax(smax, sh);
+    } else if (SHFL && d == 0) {
+      vh = vsh;
+      dh = dsh;
+    } else {
+      face_vd(A, E0, Ep1, Ef[fb + fst], vh, dh);
+    }
+    const double mv = fmax(fabs(vh), fabs(vl));
+    const double md = fmax(dh, dl);
+    cfl = cfl + (1.0 * mv * inv_dx + 2 * md * (inv_dx * inv_dx));
+  }
+  if (!active) cfl = smax = -HUGE_VAL;
+  // block max-reduction of the CFL sum and the conductivity
   for (int o = 32; o > 0; o >>= 1) {
     cfl = fmax(cfl, __shfl_xor(cfl, o, 64));
     smax = fmax(smax, __shfl_xor(smax, o, 64));
   }
-  __shared__ double r1[16], r2[16];
+  __shared__ double r1[4], r2[4];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   if (lane == 0) r1[w] = cfl, r2[w] = smax;
   __syncthreads();
@@ -352,27 +401,45 @@ struct UpdArgs {
   DevLT chem;
   double inv_N;
   double dt;
+  double dt_dr[3];  // dt / dr per dimension of this level
   double dt_chemistry_nmin;
 };
 
-__global__ void k_update(UpdArgs A, const afh_box_meta *__restrict__ meta,
-                         const int32_t *__restrict__ ids, int nc, size_t bsz,
-                         size_t fsz, unsigned long long *red) {
+// Register-resident species arrays indexed by runtime reaction data: the
+// select loops unroll over the compile-time species count.
+template <int NS>
+__device__ __forceinline__ double sel(const double (&a)[NS], int idx) {
+  double r = a[0];
+#pragma unroll
+  for (int s = 1; s < NS; s++) r = (s == idx) ? a[s] : r;
+  return r;
+}
+template <int NS>
+__device__ __forceinline__ void add_at(double (&a)[NS], int idx, double v) {
+#pragma unroll
+  for (int s = 0; s < NS; s++)
+    if (s == idx) a[s] = a[s] + v;
+}
+
+template <int NS>
+__global__ void __launch_bounds__(256)
+    k_update(UpdArgs A, const int32_t *__restrict__ ids, int nc, size_t bsz,
+             size_t fsz, unsigned long long *red) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   const int id = ids[blockIdx.y];
   double cmin = 1e100;
   if (t < nc * nc * nc) {
-    const afh_box_meta &m = meta[id - 1];
     const int i = t % nc + 1, j = (t / nc) % nc + 1, k = t / (nc * nc) + 1;
     const int ng = nc + 2, nf = nc + 1;
-    const size_t x = (size_t)(id - 1) * bsz + ix3(ng, i, j, k);
-    double y[MAXS], der[MAXS], dens[MAXS];
-    for (int s = 0; s < A.ns; s++) {
+    const size_t x = (size_t)(id - 1) * bsz + (size_t)((k * ng + j) * ng + i);
+    double y[NS], der[NS], dens[NS];
+#pragma unroll
+    for (int s = 0; s < NS; s++) {
       double tmp = 0.0;
       for (int q = 0; q < A.n_prev; q++) tmp = tmp + A.w_prev[q] * A.prev[s][q][x];
       y[s] = tmp;
       const double v = A.der[s][x];
-      dens[s] = v > 0.0 ? v : 0.0;
+      dens[s] = v > 0.0 ? v : 0.0;  // max(dens, 0.0_dp)
       der[s] = 0.0;
     }
     const double field = 1e21 * A.inv_N * A.E[x];
@@ -396,15 +463,16 @@ __global__ void k_update(UpdArgs A, const afh_box_meta *__restrict__ meta,
       }
       }
       double prod = 1.0;
-      for (int q = 0; q < R.n_in; q++) prod = prod * dens[R.ix_in[q] - 1];
+      for (int q = 0; q < R.n_in; q++) prod = prod * sel(dens, R.ix_in[q] - 1);
       rate = rate * prod;
-      for (int q = 0; q < R.n_in; q++) der[R.ix_in[q] - 1] = der[R.ix_in[q] - 1] - rate;
+      for (int q = 0; q < R.n_in; q++) add_at(der, R.ix_in[q] - 1, -rate);
       for (int q = 0; q < R.n_out; q++)
-        der[R.ix_out[q] - 1] = der[R.ix_out[q] - 1] + rate * R.mult_out[q];
+        add_at(der, R.ix_out[q] - 1, rate * R.mult_out[q]);
     }
     if (A.last_step) {
       const double eps = 1e-100;
-      for (int s = 0; s < A.ns; s++) {
+#pragma unroll
+      for (int s = 0; s < NS; s++) {
         double a, b;
         if (A.dt_chemistry_nmin > 0) {
           a = dens[s] + A.dt_chemistry_nmin;
@@ -417,17 +485,23 @@ __global__ void k_update(UpdArgs A, const afh_box_meta *__restrict__ meta,
         cmin = fmin(cmin, a / b);
       }
     }
-    for (int s = 0; s < A.ns; s++) y[s] = y[s] + A.dt * der[s];
+#pragma unroll
+    for (int s = 0; s < NS; s++) y[s] = y[s] + A.dt * der[s];
     const double *F = A.F + (size_t)(id - 1) * fsz;
-    const int e = A.e_index;
-    y[e] = y[e] + (A.dt / m.dr[0]) * (F[fidx(nf, 0, i, j, k)] - F[fidx(nf, 0, i + 1, j, k)]) +
-           (A.dt / m.dr[1]) * (F[fidx(nf, 1, i, j, k)] - F[fidx(nf, 1, i, j + 1, k)]) +
-           (A.dt / m.dr[2]) * (F[fidx(nf, 2, i, j, k)] - F[fidx(nf, 2, i, j, k + 1)]);
-    for (int s = 0; s < A.ns; s++) A.out[s][x] = y[s];
+    const int f0 = ((k - 1) * nf + (j - 1)) * nf + (i - 1);
+    const int d3 = nf * nf * nf;
+    const double div = A.dt_dr[0] * (F[f0] - F[f0 + 1]);
+    const double dvy = A.dt_dr[1] * (F[d3 + f0] - F[d3 + f0 + nf]);
+    const double dvz = A.dt_dr[2] * (F[2 * d3 + f0] - F[2 * d3 + f0 + nf * nf]);
+#pragma unroll
+    for (int s = 0; s < NS; s++)
+      if (s == A.e_index) y[s] = y[s] + div + dvy + dvz;
+#pragma unroll
+    for (int s = 0; s < NS; s++) A.out[s][x] = y[s];
   }
   if (A.last_step) {
     for (int o = 32; o > 0; o >>= 1) cmin = fmin(cmin, __shfl_xor(cmin, o, 64));
-    __shared__ double r1[16];
+    __shared__ double r1[4];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     if (lane == 0) r1[w] = cmin;
     __syncthreads();
@@ -436,6 +510,15 @@ __global__ void k_update(UpdArgs A, const afh_box_meta *__restrict__ meta,
       atomicMin(&red[0], dbl_to_ord(cmin));
     }
   }
+}
+
+template <int NS>
+void launch_update(const UpdArgs &A, afh_tree *t, int l,
+                          unsigned long long *red) {
+  const int nc = t->nc, n3 = nc * nc * nc;
+  hipLaunchKernelGGL(k_update<NS>, dim3((n3 + 255) / 256, t->leaves.n(l)),
+                     dim3(256), 0, t->stream, A, t->leaves.at(l), nc, t->bsz,
+                     t->fsz, red);
 }
 
 }  // namespace afh
@@ -575,13 +658,18 @@ int32_t afh_flux_upwind_tree(afh_fluid *f, int32_t s_deriv, double *dt_lim) {
   A.td = f->td;
   A.N_inv = 1 / f->d.gas_number_density;
   A.lim = f->d.limiter;
+  const bool shfl = (64 % nc) == 0;
   for (int l = 1; l <= t->nlvl; l++) {
     const int n = t->leaves.n(l);
     if (!n) continue;
+    for (int q = 0; q < 3; q++) A.inv_dx[q] = 1 / t->lvl_dr[3 * (l - 1) + q];
     prof_begin(t, AFH_PROF_FLUX);
-    hipLaunchKernelGGL(k_flux, dim3((n3 + 255) / 256, n), dim3(256), 0,
-                       t->stream, A, t->d_boxes, t->leaves.at(l), nc, t->bsz,
-                       t->fsz, red);
+    if (shfl)
+      hipLaunchKernelGGL(k_flux<true>, dim3((n3 + 255) / 256, n), dim3(256), 0,
+                         t->stream, A, t->leaves.at(l), nc, t->bsz, t->fsz, red);
+    else
+      hipLaunchKernelGGL(k_flux<false>, dim3((n3 + 255) / 256, n), dim3(256), 0,
+                         t->stream, A, t->leaves.at(l), nc, t->bsz, t->fsz, red);
     // read n_e, |E|, 3 face fields; write 3 fluxes = 64 B/cell
     prof_end(t, AFH_PROF_FLUX, 64.0 * n3 * n);
     AFH_LAUNCH_CHECK("k_flux");
@@ -609,6 +697,8 @@ int32_t afh_flux_update_densities(afh_fluid *f, double dt, int32_t s_deriv,
   if (!f || !dt_lim || n_prev < 1 || n_prev > MAXPREV || !s_prev || !w_prev)
     return set_error(AFH_ERR_ARG, "afh_flux_update_densities: bad argument");
   afh_tree *t = f->t;
+  if (f->d.n_species > 16)
+    return set_error(AFH_ERR_UNSUPPORTED, "more than 16 plasma species");
   const int nc = t->nc, n3 = nc * nc * nc;
   UpdArgs A;
   A.ns = f->d.n_species;
@@ -642,10 +732,15 @@ int32_t afh_flux_update_densities(afh_fluid *f, double dt, int32_t s_deriv,
   for (int l = 1; l <= t->nlvl; l++) {
     const int n = t->leaves.n(l);
     if (!n) continue;
+    for (int q = 0; q < 3; q++) A.dt_dr[q] = dt / t->lvl_dr[3 * (l - 1) + q];
     prof_begin(t, AFH_PROF_UPDATE);
-    hipLaunchKernelGGL(k_update, dim3((n3 + 255) / 256, n), dim3(256), 0,
-                       t->stream, A, t->d_boxes, t->leaves.at(l), nc, t->bsz,
-                       t->fsz, red);
+    switch (A.ns) {
+#define AFH_CASE(N) case N: launch_update<N>(A, t, l, red); break;
+      AFH_CASE(1) AFH_CASE(2) AFH_CASE(3) AFH_CASE(4) AFH_CASE(5) AFH_CASE(6)
+      AFH_CASE(7) AFH_CASE(8) AFH_CASE(9) AFH_CASE(10) AFH_CASE(11)
+      AFH_CASE(12) AFH_CASE(13) AFH_CASE(14) AFH_CASE(15) AFH_CASE(16)
+#undef AFH_CASE
+    }
     prof_end(t, AFH_PROF_UPDATE, upd_bytes * n3 * n);
     AFH_LAUNCH_CHECK("k_update");
   }

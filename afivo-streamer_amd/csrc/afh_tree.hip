@@ -398,9 +398,20 @@ int32_t afh_tree_create(const afh_tree_desc *d, int32_t device,
   t->h_ids = split(d->lvl_ids, d->lvl_ids_off);
   t->h_leaves = split(d->lvl_leaves, d->lvl_leaves_off);
   t->h_parents = split(d->lvl_parents, d->lvl_parents_off);
-  for (auto &lv : t->h_ids)
-    for (int32_t id : lv)
+  t->lvl_dr.assign(3 * t->nlvl, 0.0);
+  for (int l = 0; l < t->nlvl; l++) {
+    if (t->h_ids[l].empty()) return set_error(AFH_ERR_ARG, "empty level %d", l + 1);
+    for (int32_t id : t->h_ids[l]) {
       if (id < 1 || id > t->nb) return set_error(AFH_ERR_ARG, "bad box id %d", id);
+      const afh_box_meta &m = t->boxes[id - 1];
+      if (m.lvl != l + 1) return set_error(AFH_ERR_ARG, "box %d level mismatch", id);
+      for (int q = 0; q < 3; q++) {
+        if (id == t->h_ids[l][0]) t->lvl_dr[3 * l + q] = m.dr[q];
+        if (memcmp(&m.dr[q], &t->lvl_dr[3 * l + q], sizeof(double)) != 0)
+          return set_error(AFH_ERR_UNSUPPORTED, "non-uniform dr on level %d", l + 1);
+      }
+    }
+  }
   // derived task lists
   std::vector<std::vector<int32_t>> refb(t->nlvl), cfl(t->nlvl);
   for (int l = 0; l < t->nlvl; l++) {
