@@ -106,6 +106,20 @@ void prof_end(afh_tree *t, int kc, double bytes);
 // Host launchers shared between translation units (afh_tree.hip).
 int32_t gc_lvl(afh_tree *t, int lvl, int iv, int corners);
 int32_t restrict_boxes(afh_tree *t, const int32_t *d_ids, int n, int iv);
+// Sharded max/min reductions: each block folds its value into one of
+// RED_SHARDS words of a slot (no single-address contention), a one-block
+// kernel folds the shards. Slots: 0 cfl, 1 conductivity, 2 chemistry dt,
+// 3 maxabs.
+constexpr int RED_SHARDS = 1024;
+constexpr int RED_SLOTS = 8;
+int32_t red_init(afh_tree *t, int slot, double v);
+int32_t red_finish(afh_tree *t, int slot, bool is_max);
+// fetch the folded values of `n` consecutive slots starting at `slot`
+int32_t red_fetch(afh_tree *t, int slot, int n, double *out);
+__device__ __forceinline__ int red_shard() {
+  return (int)((blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) &
+               (RED_SHARDS - 1));
+}
 // Orderable encoding of doubles for atomicMax/Min on 64-bit integers.
 __device__ __forceinline__ unsigned long long dbl_to_ord(double x) {
   unsigned long long u = __double_as_longlong(x);

@@ -335,8 +335,8 @@ __global__ void __launch_bounds__(256)
   if (threadIdx.x == 0) {
     for (int q = 1; q < (int)(blockDim.x >> 6); q++)
       cfl = fmax(cfl, r1[q]), smax = fmax(smax, r2[q]);
-    atomicMax(&red[0], dbl_to_ord(cfl));
-    atomicMax(&red[1], dbl_to_ord(smax));
+    atomicMax(&red[red_shard()], dbl_to_ord(cfl));
+    atomicMax(&red[RED_SHARDS + red_shard()], dbl_to_ord(smax));
   }
 }
 
@@ -507,7 +507,7 @@ __global__ void __launch_bounds__(256)
     __syncthreads();
     if (threadIdx.x == 0) {
       for (int q = 1; q < (int)(blockDim.x >> 6); q++) cmin = fmin(cmin, r1[q]);
-      atomicMin(&red[0], dbl_to_ord(cmin));
+      atomicMin(&red[red_shard()], dbl_to_ord(cmin));
     }
   }
 }
@@ -646,9 +646,8 @@ int32_t afh_flux_upwind_tree(afh_fluid *f, int32_t s_deriv, double *dt_lim) {
                        t->leaves.at(l), nc, t->bsz, t->gc_args(iv));
     AFH_LAUNCH_CHECK("k_gc2");
   }
-  unsigned long long init[2] = {host_dbl_to_ord(-HUGE_VAL), host_dbl_to_ord(-HUGE_VAL)};
+  if ((e = red_init(t, 0, -HUGE_VAL)) || (e = red_init(t, 1, -HUGE_VAL))) return e;
   auto *red = reinterpret_cast<unsigned long long *>(t->scratch);
-  AFH_HIP(hipMemcpyAsync(red, init, sizeof init, hipMemcpyHostToDevice, t->stream));
   FluxArgs A;
   A.ne = t->ccv(iv);
   A.E = t->ccv(f->d.i_efld);
@@ -681,10 +680,10 @@ int32_t afh_flux_upwind_tree(afh_fluid *f, int32_t s_deriv, double *dt_lim) {
                        t->cflux.d, nc, t->fsz);
     AFH_LAUNCH_CHECK("k_consistent");
   }
-  unsigned long long r[2];
-  AFH_HIP(hipMemcpyAsync(r, red, sizeof r, hipMemcpyDeviceToHost, t->stream));
-  AFH_HIP(hipStreamSynchronize(t->stream));
-  const double cfl_max = ord_to_dbl(r[0]), sig_max = ord_to_dbl(r[1]);
+  if ((e = red_finish(t, 0, true)) || (e = red_finish(t, 1, true))) return e;
+  double r[2];
+  if ((e = red_fetch(t, 0, 2, r))) return e;
+  const double cfl_max = r[0], sig_max = r[1];
   dt_lim[0] = 1 / cfl_max;
   dt_lim[1] = 8.8541878176e-12 / (1.6022e-19 * std::max(sig_max, 1e-100));
   return AFH_OK;
@@ -726,9 +725,9 @@ int32_t afh_flux_update_densities(afh_fluid *f, double dt, int32_t s_deriv,
   for (int q = 0; q < n_prev; q++) distinct -= (s_prev[q] == s_deriv) ? 1 : 0;
   distinct += 1;
   const double upd_bytes = 8.0 * (A.ns * (distinct + 1) + 4);
-  unsigned long long init = host_dbl_to_ord(1e100);
-  auto *red = reinterpret_cast<unsigned long long *>(t->scratch) + 2;
-  AFH_HIP(hipMemcpyAsync(red, &init, sizeof init, hipMemcpyHostToDevice, t->stream));
+  int32_t e;
+  if ((e = red_init(t, 2, 1e100))) return e;
+  auto *red = reinterpret_cast<unsigned long long *>(t->scratch) + 2 * RED_SHARDS;
   for (int l = 1; l <= t->nlvl; l++) {
     const int n = t->leaves.n(l);
     if (!n) continue;
@@ -744,10 +743,13 @@ int32_t afh_flux_update_densities(afh_fluid *f, double dt, int32_t s_deriv,
     prof_end(t, AFH_PROF_UPDATE, upd_bytes * n3 * n);
     AFH_LAUNCH_CHECK("k_update");
   }
-  unsigned long long r;
-  AFH_HIP(hipMemcpyAsync(&r, red, sizeof r, hipMemcpyDeviceToHost, t->stream));
-  AFH_HIP(hipStreamSynchronize(t->stream));
-  dt_lim[0] = last_step ? ord_to_dbl(r) : 1e100;
+  double r = 1e100;
+  if (last_step) {
+    if ((e = red_finish(t, 2, false)) || (e = red_fetch(t, 2, 1, &r))) return e;
+  } else {
+    AFH_HIP(hipStreamSynchronize(t->stream));
+  }
+  dt_lim[0] = r;
   dt_lim[1] = 1e100;
   return AFH_OK;
 }

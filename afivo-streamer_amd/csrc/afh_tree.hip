@@ -307,7 +307,53 @@ int32_t restrict_boxes(afh_tree *t, const int32_t *d_ids, int n, int iv) {
 }
 
 // ------------------------------------------------------------ reductions
-// max |x| over the interiors of the listed boxes -> atomicMax (orderable)
+__global__ void k_red_fill(unsigned long long *r, unsigned long long v) {
+  r[blockIdx.x * blockDim.x + threadIdx.x] = v;
+}
+__global__ void k_red_fold(unsigned long long *r, unsigned long long *out,
+                           int is_max) {
+  // one block of RED_SHARDS threads; ordered integers fold like the doubles
+  __shared__ unsigned long long s[RED_SHARDS];
+  s[threadIdx.x] = r[threadIdx.x];
+  __syncthreads();
+  for (int o = RED_SHARDS / 2; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) {
+      unsigned long long a = s[threadIdx.x], b = s[threadIdx.x + o];
+      s[threadIdx.x] = is_max ? (a > b ? a : b) : (a < b ? a : b);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *out = s[0];
+}
+
+int32_t red_init(afh_tree *t, int slot, double v) {
+  auto *r = reinterpret_cast<unsigned long long *>(t->scratch);
+  hipLaunchKernelGGL(k_red_fill, dim3(RED_SHARDS / 256), dim3(256), 0,
+                     t->stream, r + (size_t)slot * RED_SHARDS,
+                     host_dbl_to_ord(v));
+  AFH_LAUNCH_CHECK("k_red_fill");
+  return AFH_OK;
+}
+int32_t red_finish(afh_tree *t, int slot, bool is_max) {
+  auto *r = reinterpret_cast<unsigned long long *>(t->scratch);
+  hipLaunchKernelGGL(k_red_fold, dim3(1), dim3(RED_SHARDS), 0, t->stream,
+                     r + (size_t)slot * RED_SHARDS,
+                     r + (size_t)RED_SLOTS * RED_SHARDS + slot, is_max ? 1 : 0);
+  AFH_LAUNCH_CHECK("k_red_fold");
+  return AFH_OK;
+}
+int32_t red_fetch(afh_tree *t, int slot, int n, double *out) {
+  auto *r = reinterpret_cast<unsigned long long *>(t->scratch);
+  auto *h = reinterpret_cast<unsigned long long *>(t->h_scratch);
+  AFH_HIP(hipMemcpyAsync(h, r + (size_t)RED_SLOTS * RED_SHARDS + slot,
+                         n * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                         t->stream));
+  AFH_HIP(hipStreamSynchronize(t->stream));
+  for (int q = 0; q < n; q++) out[q] = ord_to_dbl(h[q]);
+  return AFH_OK;
+}
+
+// max |x| over the interiors of the listed boxes -> sharded atomicMax
 __global__ void k_maxabs(const double *__restrict__ v,
                          const int32_t *__restrict__ ids, int nc, size_t bsz,
                          unsigned long long *out) {
@@ -328,7 +374,7 @@ __global__ void k_maxabs(const double *__restrict__ v,
   __syncthreads();
   if (threadIdx.x == 0) {
     for (int q = 1; q < (int)(blockDim.x >> 6); q++) mx = fmax(mx, red[q]);
-    atomicMax(out, dbl_to_ord(mx));
+    atomicMax(&out[red_shard()], dbl_to_ord(mx));
   }
 }
 
@@ -446,8 +492,8 @@ int32_t afh_tree_create(const afh_tree_desc *d, int32_t device,
   AFH_HIP(hipMemsetAsync(t->cc, 0, ncc * sizeof(double), t->stream));
   AFH_HIP(hipMemsetAsync(t->fc, 0, nfc * sizeof(double), t->stream));
   AFH_HIP(hipMalloc(&t->gc2, sizeof(double) * (size_t)t->nb * 6 * t->nc * t->nc));
-  AFH_HIP(hipMalloc(&t->scratch, 64 * sizeof(double)));
-  AFH_HIP(hipHostMalloc(&t->h_scratch, 64 * sizeof(double)));
+  AFH_HIP(hipMalloc(&t->scratch, (size_t)(RED_SLOTS + 1) * RED_SHARDS * sizeof(double)));
+  AFH_HIP(hipHostMalloc(&t->h_scratch, RED_SLOTS * sizeof(double)));
   AFH_HIP(hipStreamSynchronize(t->stream));
   *out = t;
   return AFH_OK;
@@ -603,9 +649,9 @@ int32_t afh_tree_copy_cc(afh_tree *t, int32_t a, int32_t b) {
 
 int32_t afh_tree_maxabs_cc(afh_tree *t, int32_t iv, double *out) {
   if (!t || iv < 1 || iv > t->nvc || !out) return set_error(AFH_ERR_ARG, "bad iv");
-  unsigned long long init = host_dbl_to_ord(0.0);
-  auto *d = reinterpret_cast<unsigned long long *>(t->scratch);
-  AFH_HIP(hipMemcpyAsync(d, &init, sizeof init, hipMemcpyHostToDevice, t->stream));
+  int32_t e;
+  if ((e = red_init(t, 3, 0.0))) return e;
+  auto *d = reinterpret_cast<unsigned long long *>(t->scratch) + 3 * RED_SHARDS;
   const int nc = t->nc, n3 = nc * nc * nc;
   int bx = std::min(64, (n3 + 255) / 256);
   for (int l = 1; l <= t->nlvl; l++) {
@@ -615,11 +661,8 @@ int32_t afh_tree_maxabs_cc(afh_tree *t, int32_t iv, double *out) {
                        t->ccv(iv), t->leaves.at(l), nc, t->bsz, d);
     AFH_LAUNCH_CHECK("k_maxabs");
   }
-  unsigned long long r;
-  AFH_HIP(hipMemcpyAsync(&r, d, sizeof r, hipMemcpyDeviceToHost, t->stream));
-  AFH_HIP(hipStreamSynchronize(t->stream));
-  *out = ord_to_dbl(r);
-  return AFH_OK;
+  if ((e = red_finish(t, 3, true))) return e;
+  return red_fetch(t, 3, 1, out);
 }
 
 }  // extern "C"
