@@ -32,6 +32,7 @@ struct CsParams {
   double hc[MAXMG][3];
   double cdiag[MAXMG];
   int bctype[6];
+  int halo[MAXMG];  // 1: global arrays with a ghost layer, 0: compact (LDS)
   double *u[MAXMG], *f[MAXMG], *r[MAXMG];
 };
 
@@ -209,7 +210,10 @@ __global__ void k_gradient(const double *__restrict__ phi,
 // in stencil_handle_boundaries (m_coarse_solver.f90:442-491).
 __device__ __forceinline__ size_t gix(const CsParams &P, int m, int i, int j,
                                       int k) {
-  return ((size_t)k * (P.dims[m][1] + 2) + j) * (P.dims[m][0] + 2) + i;
+  const int h = P.halo[m];
+  return ((size_t)(k - 1 + h) * (P.dims[m][1] + 2 * h) + (j - 1 + h)) *
+             (P.dims[m][0] + 2 * h) +
+         (i - 1 + h);
 }
 
 __device__ __forceinline__ double cs_diag(const CsParams &P, int m, int i,
@@ -357,9 +361,29 @@ __device__ void blk_for(const CsParams &P, int m, F f) {
   __syncthreads();
 }
 
-__global__ void __launch_bounds__(1024) k_cs_small(CsParams P, int m0,
+// The small MG levels m0..bottom live in LDS (compact layout, no ghost layer:
+// the folded operator never reads outside the grid); u and f of level m0 are
+// copied in from global memory and u copied back at the end.
+__global__ void __launch_bounds__(1024) k_cs_small(CsParams G, int m0,
                                                    int n_cycles) {
+  extern __shared__ double lds[];
+  CsParams P = G;
   const int bot = P.n_mg - 1;
+  {
+    size_t off = 0;
+    for (int m = m0; m <= bot; m++) {
+      const size_t n = (size_t)P.dims[m][0] * P.dims[m][1] * P.dims[m][2];
+      P.u[m] = lds + off;
+      P.f[m] = lds + off + n;
+      P.r[m] = lds + off + 2 * n;
+      P.halo[m] = 0;
+      off += 3 * n;
+    }
+  }
+  blk_for(P, m0, [&](int i, int j, int k) {
+    P.u[m0][gix(P, m0, i, j, k)] = G.u[m0][gix(G, m0, i, j, k)];
+    P.f[m0][gix(P, m0, i, j, k)] = G.f[m0][gix(G, m0, i, j, k)];
+  });
   for (int cyc = 0; cyc < n_cycles; cyc++) {
     for (int m = m0; m < bot; m++) {
       for (int s = 0; s < 2; s++) {
@@ -382,6 +406,9 @@ __global__ void __launch_bounds__(1024) k_cs_small(CsParams P, int m0,
       }
     }
   }
+  blk_for(P, m0, [&](int i, int j, int k) {
+    G.u[m0][gix(G, m0, i, j, k)] = P.u[m0][gix(P, m0, i, j, k)];
+  });
 }
 
 // coarse_solver_set_rhs_phi: gather rhs (+ folded BC values) and phi
@@ -441,6 +468,7 @@ struct afh_mg {
   std::vector<Coef> lvl_c;  // per tree level
   CsParams P;
   int small_from = 0;       // first MG level run by k_cs_small
+  size_t small_lds = 0;     // LDS bytes of the levels k_cs_small holds
 };
 
 static inline dim3 blocks1(size_t n, int bs = 256) {
@@ -505,6 +533,18 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
     if ((long)n[0] * n[1] * n[2] > CS_SMALL_CELLS) break;
     mg->small_from--;
   }
+  mg->small_lds = 0;
+  for (int q = 0; q < P.n_mg; q++) {
+    P.halo[q] = 1;
+    if (q >= mg->small_from)
+      mg->small_lds += 3 * sizeof(double) * (size_t)P.dims[q][0] * P.dims[q][1] *
+                       P.dims[q][2];
+  }
+  if (mg->small_lds > 160 * 1024)
+    return set_error(AFH_ERR_UNSUPPORTED, "coarse-solver LDS levels too large");
+  AFH_HIP(hipFuncSetAttribute((const void *)k_cs_small,
+                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)mg->small_lds));
   for (int q = 0; q < P.n_mg; q++) {
     size_t n = (size_t)(P.dims[q][0] + 2) * (P.dims[q][1] + 2) * (P.dims[q][2] + 2);
     AFH_HIP(hipMalloc(&P.u[q], n * sizeof(double)));
@@ -604,8 +644,8 @@ static int32_t solve_coarse(afh_mg *mg) {
   AFH_LAUNCH_CHECK("k_cs_gather");
   const int s = mg->small_from;
   if (s == 0) {
-    hipLaunchKernelGGL(k_cs_small, dim3(1), dim3(1024), 0, t->stream, P, 0,
-                       mg->d.coarse_cycles);
+    hipLaunchKernelGGL(k_cs_small, dim3(1), dim3(1024), mg->small_lds,
+                       t->stream, P, 0, mg->d.coarse_cycles);
     AFH_LAUNCH_CHECK("k_cs_small");
   } else {
     for (int cyc = 0; cyc < mg->d.coarse_cycles; cyc++) {
@@ -619,7 +659,8 @@ static int32_t solve_coarse(afh_mg *mg) {
         hipLaunchKernelGGL(k_cs_rstr, blocks1(N / 8), dim3(256), 0, t->stream, P,
                            m + 1);
       }
-      hipLaunchKernelGGL(k_cs_small, dim3(1), dim3(1024), 0, t->stream, P, s, 1);
+      hipLaunchKernelGGL(k_cs_small, dim3(1), dim3(1024), mg->small_lds,
+                         t->stream, P, s, 1);
       for (int m = s - 1; m >= 0; m--) {
         const size_t N = (size_t)P.dims[m][0] * P.dims[m][1] * P.dims[m][2];
         hipLaunchKernelGGL(k_cs_prol, blocks1(N), dim3(256), 0, t->stream, P, m);
