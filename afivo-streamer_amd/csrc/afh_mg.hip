@@ -23,7 +23,7 @@ struct Coef {
 };
 
 constexpr int MAXMG = 16;
-constexpr int CS_BOTTOM_SWEEPS = 32;   // same constant as oracle/c/afo.c
+constexpr int CS_BOTTOM_SWEEPS = 16;   // same constant as oracle/c/afo.c
 constexpr int CS_SMALL_CELLS = 4096;   // MG levels <= 16^3 run in one workgroup
 
 struct CsParams {
@@ -34,6 +34,7 @@ struct CsParams {
   int bctype[6];
   int halo[MAXMG];  // 1: global arrays with a ghost layer, 0: compact (LDS)
   double *u[MAXMG], *f[MAXMG], *r[MAXMG];
+  const double *dtab;  // [MAXMG][64][2] folded (diag, 1/diag) per class
 };
 
 __device__ __forceinline__ size_t ix3(int ng, int i, int j, int k) {
@@ -216,19 +217,20 @@ __device__ __forceinline__ size_t gix(const CsParams &P, int m, int i, int j,
          (i - 1 + h);
 }
 
+// boundary class of a cell (2 bits per dimension), index into P.dtab
+__device__ __forceinline__ int cs_class(const CsParams &P, int m, int i, int j,
+                                        int k) {
+  return (i == 1) | ((i == P.dims[m][0]) << 1) | ((j == 1) << 2) |
+         ((j == P.dims[m][1]) << 3) | ((k == 1) << 4) |
+         ((k == P.dims[m][2]) << 5);
+}
 __device__ __forceinline__ double cs_diag(const CsParams &P, int m, int i,
                                           int j, int k) {
-  const int idx[3] = {i, j, k};
-  double d = P.cdiag[m];
-  for (int nb = 1; nb <= 6; nb++) {
-    const int dd = (nb - 1) >> 1;
-    const bool low = ((nb - 1) & 1) == 0;
-    const bool at = low ? (idx[dd] == 1) : (idx[dd] == P.dims[m][dd]);
-    if (!at) continue;
-    if (P.bctype[nb - 1] == AFH_BC_DIRICHLET) d = d - P.hc[m][dd];
-    else d = d + P.hc[m][dd];
-  }
-  return d;
+  return P.dtab[(m * 64 + cs_class(P, m, i, j, k)) * 2];
+}
+__device__ __forceinline__ double cs_inv_diag(const CsParams &P, int m, int i,
+                                              int j, int k) {
+  return P.dtab[(m * 64 + cs_class(P, m, i, j, k)) * 2 + 1];
 }
 
 __device__ __forceinline__ void cs_gs_cell(const CsParams &P, int m, int i,
@@ -243,7 +245,7 @@ __device__ __forceinline__ void cs_gs_cell(const CsParams &P, int m, int i,
   if (j < ny) s = s - h[1] * u[gix(P, m, i, j + 1, k)];
   if (k > 1) s = s - h[2] * u[gix(P, m, i, j, k - 1)];
   if (k < nz) s = s - h[2] * u[gix(P, m, i, j, k + 1)];
-  u[gix(P, m, i, j, k)] = s / cs_diag(P, m, i, j, k);
+  u[gix(P, m, i, j, k)] = s * cs_inv_diag(P, m, i, j, k);
 }
 
 __device__ __forceinline__ void cs_res_cell(const CsParams &P, int m, int i,
@@ -469,7 +471,38 @@ struct afh_mg {
   CsParams P;
   int small_from = 0;       // first MG level run by k_cs_small
   size_t small_lds = 0;     // LDS bytes of the levels k_cs_small holds
+  double *d_dtab = nullptr; // device copy of h_dtab
+  std::vector<double> h_dtab;
+  int tab_bc[6] = {0, 0, 0, 0, 0, 0};
 };
+
+// (diag, 1/diag) of the folded operator per MG level and boundary class, in
+// the order of oracle/c/afo.c cs_build_table.
+static int32_t build_table(afh_mg *mg) {
+  const afh_bc *bc = mg->t->meth[mg->d.i_phi].bc;
+  CsParams &P = mg->P;
+  mg->h_dtab.assign((size_t)MAXMG * 64 * 2, 0.0);
+  for (int m = 0; m < P.n_mg; m++)
+    for (int c = 0; c < 64; c++) {
+      double d = P.cdiag[m];
+      for (int nb = 1; nb <= 6; nb++) {
+        const int dd = (nb - 1) >> 1;
+        const bool low = ((nb - 1) & 1) == 0;
+        const int at = low ? (c >> (2 * dd)) & 1 : (c >> (2 * dd + 1)) & 1;
+        if (!at) continue;
+        if (bc[nb - 1].type == AFH_BC_DIRICHLET) d = d - P.hc[m][dd];
+        else d = d + P.hc[m][dd];
+      }
+      mg->h_dtab[(m * 64 + c) * 2] = d;
+      mg->h_dtab[(m * 64 + c) * 2 + 1] = 1 / d;
+    }
+  for (int q = 0; q < 6; q++) mg->tab_bc[q] = bc[q].type;
+  AFH_HIP(hipStreamSynchronize(mg->t->stream));
+  AFH_HIP(hipMemcpy(mg->d_dtab, mg->h_dtab.data(),
+                    mg->h_dtab.size() * sizeof(double), hipMemcpyHostToDevice));
+  P.dtab = mg->d_dtab;
+  return AFH_OK;
+}
 
 static inline dim3 blocks1(size_t n, int bs = 256) {
   return dim3((unsigned)((n + bs - 1) / bs));
@@ -545,6 +578,8 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
   AFH_HIP(hipFuncSetAttribute((const void *)k_cs_small,
                               hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)mg->small_lds));
+  AFH_HIP(hipMalloc(&mg->d_dtab, (size_t)MAXMG * 64 * 2 * sizeof(double)));
+  if (int32_t e = build_table(mg)) return e;
   for (int q = 0; q < P.n_mg; q++) {
     size_t n = (size_t)(P.dims[q][0] + 2) * (P.dims[q][1] + 2) * (P.dims[q][2] + 2);
     AFH_HIP(hipMalloc(&P.u[q], n * sizeof(double)));
@@ -567,6 +602,7 @@ int32_t afh_mg_destroy(afh_mg *mg) {
     hipFree(mg->P.f[q]);
     hipFree(mg->P.r[q]);
   }
+  hipFree(mg->d_dtab);
   delete mg;
   return AFH_OK;
 }
@@ -636,6 +672,11 @@ static int32_t solve_coarse(afh_mg *mg) {
   CsParams &P = mg->P;
   const afh_bc *bc = t->meth[mg->d.i_phi].bc;
   for (int q = 0; q < 6; q++) P.bctype[q] = bc[q].type;
+  for (int q = 0; q < 6; q++)
+    if (mg->tab_bc[q] != bc[q].type) {
+      if (int32_t e = build_table(mg)) return e;
+      break;
+    }
   const int nc = t->nc, nid = t->ids.n(1), n3 = nc * nc * nc;
   hipLaunchKernelGGL(k_cs_gather, dim3((n3 + 255) / 256, nid), dim3(256), 0,
                      t->stream, P, t->ccv(mg->d.i_phi), t->ccv(mg->d.i_rhs),

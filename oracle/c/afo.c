@@ -52,9 +52,10 @@ struct afh_mg {
   double *u[16], *f[16], *r[16];
   double hc[16][3]; /* 1/h^2 per dim per MG level */
   double cdiag[16];  /* unfolded diagonal per MG level */
+  double dtab[16][64][2]; /* folded (diag, 1/diag) per boundary class */
 };
 
-#define AFH_CS_BOTTOM_SWEEPS 32
+#define AFH_CS_BOTTOM_SWEEPS 16
 
 struct afh_fluid {
   afh_tree *t;
@@ -689,19 +690,40 @@ int32_t afo_mg_correct_children(afh_mg *mg, int32_t lvl) {
        ((mg)->dims[m][0] + 2) +                                               \
    (size_t)(i))
 
-static inline double cs_diag(afh_mg *mg, int m, int i, int j, int k) {
-  afh_tree *t = mg->t;
-  const afh_bc *bc = t->meth[mg->d.i_phi].bc;
-  int idx[3] = {i, j, k};
-  double d = mg->cdiag[m];
-  for (int nb = 1; nb <= 6; nb++) {
-    int dd = nb_dim(nb);
-    int at = nb_low(nb) ? (idx[dd] == 1) : (idx[dd] == mg->dims[m][dd]);
-    if (!at) continue;
-    if (bc[nb - 1].type == AFH_BC_DIRICHLET) d = d - mg->hc[m][dd];
-    else d = d + mg->hc[m][dd];
+/* Folded diagonal of a cell: depends only on which grid faces the cell
+ * touches (class = 2 bits per dimension: at low face, at high face). The
+ * table (diag, 1/diag) per class is built once per solve. */
+static inline int cs_class(afh_mg *mg, int m, int i, int j, int k) {
+  int idx[3] = {i, j, k}, c = 0;
+  for (int d = 0; d < 3; d++) {
+    c |= (idx[d] == 1) << (2 * d);
+    c |= (idx[d] == mg->dims[m][d]) << (2 * d + 1);
   }
-  return d;
+  return c;
+}
+
+static void cs_build_table(afh_mg *mg) {
+  const afh_bc *bc = mg->t->meth[mg->d.i_phi].bc;
+  for (int m = 0; m < mg->n_mg; m++)
+    for (int c = 0; c < 64; c++) {
+      double d = mg->cdiag[m];
+      for (int nb = 1; nb <= 6; nb++) {
+        int dd = nb_dim(nb);
+        int at = nb_low(nb) ? (c >> (2 * dd)) & 1 : (c >> (2 * dd + 1)) & 1;
+        if (!at) continue;
+        if (bc[nb - 1].type == AFH_BC_DIRICHLET) d = d - mg->hc[m][dd];
+        else d = d + mg->hc[m][dd];
+      }
+      mg->dtab[m][c][0] = d;
+      mg->dtab[m][c][1] = 1 / d;
+    }
+}
+
+static inline double cs_diag(afh_mg *mg, int m, int i, int j, int k) {
+  return mg->dtab[m][cs_class(mg, m, i, j, k)][0];
+}
+static inline double cs_inv_diag(afh_mg *mg, int m, int i, int j, int k) {
+  return mg->dtab[m][cs_class(mg, m, i, j, k)][1];
 }
 
 /* one red-black half sweep on MG level m */
@@ -720,7 +742,7 @@ static void cs_gsrb(afh_mg *mg, int m, int n) {
         if (j < ny) s = s - h[1] * u[GIX(mg, m, i, j + 1, k)];
         if (k > 1) s = s - h[2] * u[GIX(mg, m, i, j, k - 1)];
         if (k < nz) s = s - h[2] * u[GIX(mg, m, i, j, k + 1)];
-        u[GIX(mg, m, i, j, k)] = s / cs_diag(mg, m, i, j, k);
+        u[GIX(mg, m, i, j, k)] = s * cs_inv_diag(mg, m, i, j, k);
       }
     }
 }
@@ -851,6 +873,7 @@ int32_t afo_mg_solve_coarse(afh_mg *mg) {
           mg->u[0][g] = p[IX(t, i, j, k)];
         }
   }
+  cs_build_table(mg);
   for (int c = 0; c < mg->d.coarse_cycles; c++) cs_cycle(mg, 0);
   /* coarse_solver_get_phi */
   for (int q = 0; q < nid; q++) {
