@@ -369,9 +369,12 @@ __device__ void blk_for(const CsParams &P, int m, F f) {
 __global__ void __launch_bounds__(1024) k_cs_small(CsParams G, int m0,
                                                    int n_cycles) {
   extern __shared__ double lds[];
-  CsParams P = G;
-  const int bot = P.n_mg - 1;
-  {
+  // the level table lives in LDS: a private copy indexed by the (dynamic)
+  // level number would be placed in scratch memory
+  __shared__ CsParams P;
+  const int bot = G.n_mg - 1;
+  if (threadIdx.x == 0) {
+    P = G;
     size_t off = 0;
     for (int m = m0; m <= bot; m++) {
       const size_t n = (size_t)P.dims[m][0] * P.dims[m][1] * P.dims[m][2];
@@ -382,6 +385,7 @@ __global__ void __launch_bounds__(1024) k_cs_small(CsParams G, int m0,
       off += 3 * n;
     }
   }
+  __syncthreads();
   blk_for(P, m0, [&](int i, int j, int k) {
     P.u[m0][gix(P, m0, i, j, k)] = G.u[m0][gix(G, m0, i, j, k)];
     P.f[m0][gix(P, m0, i, j, k)] = G.f[m0][gix(G, m0, i, j, k)];
@@ -573,7 +577,7 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
       mg->small_lds += 3 * sizeof(double) * (size_t)P.dims[q][0] * P.dims[q][1] *
                        P.dims[q][2];
   }
-  if (mg->small_lds > 160 * 1024)
+  if (mg->small_lds + sizeof(CsParams) > 160 * 1024)
     return set_error(AFH_ERR_UNSUPPORTED, "coarse-solver LDS levels too large");
   AFH_HIP(hipFuncSetAttribute((const void *)k_cs_small,
                               hipFuncAttributeMaxDynamicSharedMemorySize,
