@@ -105,6 +105,9 @@ void prof_begin(afh_tree *t, int kc);
 void prof_end(afh_tree *t, int kc, double bytes);
 // Host launchers shared between translation units (afh_tree.hip).
 int32_t gc_lvl(afh_tree *t, int lvl, int iv, int corners);
+// ghost fill of level lvl of the image v (coarse data read from vc)
+int32_t gc_lvl_ptr(afh_tree *t, int lvl, double *v, const double *vc,
+                   const GcArgs &ga, int corners);
 int32_t restrict_boxes(afh_tree *t, const int32_t *d_ids, int n, int iv);
 // Sharded max/min reductions: each block folds its value into one of
 // RED_SHARDS words of a slot (no single-address contention), a one-block
@@ -136,5 +139,100 @@ inline unsigned long long host_dbl_to_ord(double x) {
   unsigned long long u;
   memcpy(&u, &x, sizeof u);
   return (u & 0x8000000000000000ull) ? ~u : (u | 0x8000000000000000ull);
+}
+
+__device__ __forceinline__ size_t ix3(int ng, int i, int j, int k) {
+  return ((size_t)k * ng + j) * ng + i;
+}
+
+// Face ghost cell p (p[d] = 0 or nc+1, d = dim of face nb) of box m when the
+// face has no same-level neighbour (bc: the face's boundary condition, rb:
+// the refinement-boundary method): physical boundary (bc_to_gc,
+// m_af_ghostcell.f90:173-279) or refinement boundary (mg_sides_rb,
+// m_af_multigrid.f90:294-461; af_gc_interp / af_gc_interp_lim,
+// m_af_ghostcell.f90:394-612). `own(q)` returns the box's current value at
+// interior cell q; coarse data are read from v (the parent's neighbour).
+template <class Own>
+__device__ __forceinline__ double gc_face_nocopy(
+    const double *__restrict__ v, const afh_box_meta *__restrict__ meta,
+    const afh_box_meta &m, int nb, const int p[3], int a, int b, int nc,
+    size_t bsz, afh_bc bc, int rb, Own own) {
+  const int d = (nb - 1) >> 1;
+  const bool low = ((nb - 1) & 1) == 0;
+  const int ta = (d == 0) ? 1 : 0, tb = (d == 2) ? 1 : 2;
+  const int ng = nc + 2;
+  const int x1 = low ? 1 : nc;
+  const int x2 = low ? 2 : nc - 1;
+  int q1[3] = {p[0], p[1], p[2]}, q2[3] = {p[0], p[1], p[2]};
+  q1[d] = x1;
+  q2[d] = x2;
+  if (m.neighbors[nb - 1] < 0) {
+    double c0, c1, c2;
+    switch (bc.type) {
+    case AFH_BC_DIRICHLET: c0 = 2; c1 = -1; c2 = 0; break;
+    case AFH_BC_NEUMANN: c0 = m.dr[d] * (low ? -1 : 1); c1 = 1; c2 = 0; break;
+    case AFH_BC_CONTINUOUS: c0 = 0; c1 = 2; c2 = -1; break;
+    default: c0 = 1; c1 = 0; c2 = 0; break;
+    }
+    return c0 * bc.value + c1 * own(q1) + c2 * own(q2);
+  }
+  // refinement boundary: coarse data from the parent's neighbour
+  const int p_id = m.parent;
+  const int p_nb_id = meta[p_id - 1].neighbors[nb - 1];
+  const double *cp = v + (size_t)(p_nb_id - 1) * bsz;
+  const int hnc = nc >> 1;
+  int co[3];
+  for (int q = 0; q < 3; q++) co[q] = ((m.ix[q] - 1) & 1) * hnc;
+
+  if (rb == AFH_RB_MG_SIDES) {
+    // tmp(x, y) = coarse value next to the face, at tangential offsets co;
+    // gc = tmp +- g1 +- g2; ghost = 0.5 gc + 0.75 x_i - 0.25 x_i+d
+    const int cn = low ? nc : 1;
+    const int ii = (a + 1) >> 1, jj = (b + 1) >> 1;
+    auto tmp = [&](int x, int y) {
+      int q[3];
+      q[d] = cn;
+      q[ta] = co[ta] + x;
+      q[tb] = co[tb] + y;
+      return cp[ix3(ng, q[0], q[1], q[2])];
+    };
+    const double g1 = 0.125 * (tmp(ii + 1, jj) - tmp(ii - 1, jj));
+    const double g2 = 0.125 * (tmp(ii, jj + 1) - tmp(ii, jj - 1));
+    const double t0 = tmp(ii, jj);
+    double gcv;
+    if (a & 1) {
+      gcv = (b & 1) ? t0 - g1 - g2 : t0 - g1 + g2;
+    } else {
+      gcv = (b & 1) ? t0 + g1 - g2 : t0 + g1 + g2;
+    }
+    return 0.5 * gcv + 0.75 * own(q1) - 0.25 * own(q2);
+  }
+  // af_gc_interp / af_gc_interp_lim; offsets on the parent's neighbour
+  const double third = 1 / 3.0, sixth = 1 / 6.0;
+  int off[3] = {co[0], co[1], co[2]};
+  off[d] -= (low ? -1 : 1) * nc;
+  const int ix_c = low ? nc : 1;
+  const int a1 = off[ta] + ((a + 1) >> 1), a2 = a1 + 1 - 2 * (a & 1);
+  const int b1 = off[tb] + ((b + 1) >> 1), b2 = b1 + 1 - 2 * (b & 1);
+  int q[3];
+  q[d] = ix_c;
+  q[ta] = a1, q[tb] = b1;
+  const double cv1 = cp[ix3(ng, q[0], q[1], q[2])];
+  double cv2, cv3;
+  if (d < 2) {
+    q[ta] = a2, q[tb] = b1;
+    cv2 = cp[ix3(ng, q[0], q[1], q[2])];
+    q[ta] = a1, q[tb] = b2;
+    cv3 = cp[ix3(ng, q[0], q[1], q[2])];
+  } else {
+    // case (3): c(2) uses j_c2 and c(3) uses i_c2 (m_af_ghostcell.f90:479-482)
+    q[ta] = a1, q[tb] = b2;
+    cv2 = cp[ix3(ng, q[0], q[1], q[2])];
+    q[ta] = a2, q[tb] = b1;
+    cv3 = cp[ix3(ng, q[0], q[1], q[2])];
+  }
+  double val = third * cv1 + sixth * cv2 + sixth * cv3 + third * own(q1);
+  if (rb == AFH_RB_GC_INTERP_LIM && val > 2 * cv1) val = 2 * cv1;
+  return val;
 }
 }  // namespace afh

@@ -37,11 +37,18 @@ struct CsParams {
   const double *dtab;  // [MAXMG][64][2] folded (diag, 1/diag) per class
 };
 
-__device__ __forceinline__ size_t ix3(int ng, int i, int j, int k) {
-  return ((size_t)k * ng + j) * ng + i;
-}
 
 // ------------------------------------------------------------ box kernels
+// Gauss-Seidel update of cell c from its six neighbours (stencil_gsrb_357).
+__device__ __forceinline__ double gs_cell(const double *__restrict__ x,
+                                          const double *__restrict__ r,
+                                          size_t c, size_t sj, size_t sk,
+                                          const Coef &cf, double inv_c1) {
+  return (r[c] - cf.c[1] * x[c - 1] - cf.c[2] * x[c + 1] - cf.c[3] * x[c - sj] -
+          cf.c[4] * x[c + sj] - cf.c[5] * x[c - sk] - cf.c[6] * x[c + sk]) *
+         inv_c1;
+}
+
 __global__ void k_gsrb(double *__restrict__ phi, const double *__restrict__ rhs,
                        const int32_t *__restrict__ ids, int nc, size_t bsz,
                        Coef cf, double inv_c1, int redblack) {
@@ -54,11 +61,233 @@ __global__ void k_gsrb(double *__restrict__ phi, const double *__restrict__ rhs,
   const int ng = nc + 2;
   double *x = phi + (size_t)(id - 1) * bsz;
   const double *r = rhs + (size_t)(id - 1) * bsz;
-  const size_t c = ix3(ng, i, j, k);
-  const size_t sj = ng, sk = (size_t)ng * ng;
-  x[c] = (r[c] - cf.c[1] * x[c - 1] - cf.c[2] * x[c + 1] - cf.c[3] * x[c - sj] -
-          cf.c[4] * x[c + sj] - cf.c[5] * x[c - sk] - cf.c[6] * x[c + sk]) *
-         inv_c1;
+  x[ix3(ng, i, j, k)] =
+      gs_cell(x, r, ix3(ng, i, j, k), ng, (size_t)ng * ng, cf, inv_c1);
+}
+
+// ------------------------------------------------------------ fused GSRB pair
+// Half-sweeps n (odd, "red": i+j+k odd) and n+1 ("black") of gsrb_boxes
+// (m_af_multigrid.f90:741-760) in ONE pass, without the level ghost fill
+// between them; bitwise the same result as the two half-sweeps with
+// af_gc_lvl in between.
+//
+// The pair reads `src` and writes the interior of `dst` (ping-pong between
+// phi and a spare image), so every input is an old value and workgroups
+// never race. One workgroup per tile of TJ rows (j) of a box marches over
+// the k planes, holding four planes P[s-2..s+1] of its rows plus one halo
+// row on each side (and the i ghosts) in LDS. Step s:
+//   A  red cells of plane s (in-plane and k neighbours: old black values)
+//   B  the red values next to the tile that af_gc_lvl / the neighbouring
+//      tile would provide after the red half-sweep: x ghosts of the tile's
+//      rows; the halo rows (ghost row of the box, or the red cells of the
+//      adjacent tile recomputed from `src`); the z ghost planes at s = 2 and
+//      s = NC+1. A same-level neighbour's red boundary cell is recomputed
+//      from that neighbour's `src` (bitwise what its workgroup computes);
+//      physical / refinement faces use gc_face_nocopy with the box's current
+//      red and black values (coarse data from `coarse`, i.e. phi).
+//   C  black cells of plane s-1 (new red neighbours); plane s-1 of the tile
+//      is complete and written once, in full rows
+//   D  plane s+2 (prefetched into registers during the step) -> LDS
+// Each plane of phi and rhs is read once and phi is written once per pair
+// (24 B/cell algorithmic).
+template <int NC>
+struct RbGeom {
+  static constexpr int NG = NC + 2;
+  static constexpr int TJ = NC < 16 ? NC : 16;         // rows per tile
+  static constexpr int NTILE = NC / TJ;
+  static constexpr int PLT = (TJ + 2) * NG;            // LDS plane (rows j0-1..j1+1)
+  static constexpr int NT = NC * TJ >= 256 ? 256 : (NC * TJ < 64 ? 64 : NC * TJ);
+  static constexpr int CPT = (NC * TJ + NT - 1) / NT;  // columns per thread
+  static constexpr int EPT = (PLT + NT - 1) / NT;      // plane entries per thread
+};
+
+// One red ghost cell p of face nb for k_gsrb_pair. x1v / x2v: this box's
+// current values next to the face (x1 black, old; x2 red, new).
+template <int NC>
+__device__ __forceinline__ double pair_ghost(
+    const double *__restrict__ src, const double *__restrict__ coarse,
+    const double *__restrict__ rhs,
+    const afh_box_meta *__restrict__ meta, const afh_box_meta &m, int nb,
+    int p0, int p1, int p2, int a, int b, size_t bsz, const Coef &cf,
+    double inv_c1, afh_bc bc, int rb, double x1v, double x2v) {
+  constexpr int NG = NC + 2;
+  const int nb_id = m.neighbors[nb - 1];
+  const int d = (nb - 1) >> 1;
+  const bool low = ((nb - 1) & 1) == 0;
+  const int p[3] = {p0, p1, p2};
+  if (nb_id > 0) {
+    // the neighbour's red boundary cell, from its (old) black values
+    int q[3] = {p0, p1, p2};
+    q[d] = low ? NC : 1;
+    const size_t o = (size_t)(nb_id - 1) * bsz;
+    return gs_cell(src + o, rhs + o, ix3(NG, q[0], q[1], q[2]), NG,
+                   (size_t)NG * NG, cf, inv_c1);
+  }
+  const int x1 = low ? 1 : NC;
+  return gc_face_nocopy(coarse, meta, m, nb, p, a, b, NC, bsz, bc, rb,
+                        [&](const int *q) { return q[d] == x1 ? x1v : x2v; });
+}
+
+template <int NC>
+__global__ void __launch_bounds__(RbGeom<NC>::NT) __attribute__((amdgpu_waves_per_eu(4)))
+    k_gsrb_pair(const double *__restrict__ src, double *__restrict__ dst,
+                const double *__restrict__ rhs,
+                const double *__restrict__ coarse,
+                const afh_box_meta *__restrict__ meta,
+                const int32_t *__restrict__ ids, size_t bsz, Coef cf,
+                double inv_c1, GcArgs ga) {
+  using G = RbGeom<NC>;
+  constexpr int NG = G::NG, HN = NC / 2, NT = G::NT, CPT = G::CPT,
+                EPT = G::EPT, PLT = G::PLT, TJ = G::TJ;
+  constexpr size_t SK = (size_t)NG * NG;
+  __shared__ double P[4][PLT];  // planes s-2 .. s+1 at slot (plane & 3)
+  const int tid = threadIdx.x;
+  const int id = ids[blockIdx.x / G::NTILE];
+  const int j0 = (blockIdx.x % G::NTILE) * TJ + 1, j1 = j0 + TJ - 1;
+  const afh_box_meta &m = meta[id - 1];
+  const double *x = src + (size_t)(id - 1) * bsz;
+  double *y = dst + (size_t)(id - 1) * bsz;
+  const double *r = rhs + (size_t)(id - 1) * bsz;
+  const size_t t0 = (size_t)(j0 - 1) * NG;  // first LDS row in a plane
+  // tile column q of this thread: (i, j), LDS index c (row j - j0 + 1)
+  auto colof = [&](int q, int &i, int &j, int &c) {
+    const int col = tid + NT * q;
+    i = col % NC + 1;
+    j = j0 + col / NC;
+    c = (col / NC + 1) * NG + i;
+    return col < NC * TJ;
+  };
+
+  // planes 0..2 -> LDS; rhs of plane 1 -> registers
+  for (int e = tid; e < 3 * PLT; e += NT)
+    P[e / PLT][e % PLT] = x[(size_t)(e / PLT) * SK + t0 + e % PLT];
+  double r1[CPT], r2[CPT];
+#pragma unroll
+  for (int q = 0; q < CPT; q++) {
+    int i, j, c;
+    colof(q, i, j, c);
+    r1[q] = 0;
+    r2[q] = colof(q, i, j, c) ? r[SK + j * NG + i] : 0.0;
+  }
+  __syncthreads();
+
+  for (int s = 1; s <= NC + 1; s++) {
+    // prefetch plane s+2 of phi and the tile of plane s+1 of rhs
+    double nx[EPT], nr[CPT];
+#pragma unroll
+    for (int q = 0; q < EPT; q++) {
+      const int e = tid + NT * q;
+      nx[q] = (s + 2 <= NC + 1 && e < PLT) ? x[(size_t)(s + 2) * SK + t0 + e]
+                                            : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < CPT; q++) {
+      int i, j, c;
+      const bool ok = colof(q, i, j, c);
+      nr[q] = (ok && s + 1 <= NC) ? r[(size_t)(s + 1) * SK + j * NG + i] : 0.0;
+    }
+    double *Pm = P[(s - 1) & 3], *P0 = P[s & 3], *Pp = P[(s + 1) & 3];
+    double *Pmm = P[(s - 2) & 3];
+    // A: red cells of plane s
+    if (s <= NC) {
+#pragma unroll
+      for (int q = 0; q < CPT; q++) {
+        int i, j, c;
+        if (colof(q, i, j, c) && ((i + j + s) & 1))
+          P0[c] = (r2[q] - cf.c[1] * P0[c - 1] - cf.c[2] * P0[c + 1] -
+                   cf.c[3] * P0[c - NG] - cf.c[4] * P0[c + NG] -
+                   cf.c[5] * Pm[c] - cf.c[6] * Pp[c]) *
+                  inv_c1;
+      }
+    }
+    __syncthreads();
+    // B: red values around the tile
+    if (s <= NC) {
+      for (int u = tid; u < TJ + NC; u += NT) {
+        int i, j, jl;
+        double v;
+        if (u < TJ) {
+          // x ghosts of the tile's rows
+          j = j0 + u;
+          jl = u + 1;
+          i = ((j + s) & 1) ? 0 : NC + 1;
+          const int nb = i == 0 ? 1 : 2;
+          v = pair_ghost<NC>(src, coarse, rhs, meta, m, nb, i, j, s, j, s, bsz,
+                             cf, inv_c1, ga.bc[nb - 1], ga.rb,
+                             P0[jl * NG + (i == 0 ? 1 : NC)],
+                             P0[jl * NG + (i == 0 ? 2 : NC - 1)]);
+        } else {
+          // halo rows j0-1 and j1+1
+          const bool lo = u - TJ < HN;
+          j = lo ? j0 - 1 : j1 + 1;
+          jl = lo ? 0 : TJ + 1;
+          i = 2 - ((1 ^ (s + j)) & 1) + 2 * ((u - TJ) % HN);
+          if (j == 0 || j == NC + 1) {
+            const int nb = j == 0 ? 3 : 4;
+            const int l1 = j == 0 ? 1 : TJ, l2 = j == 0 ? 2 : TJ - 1;
+            v = pair_ghost<NC>(src, coarse, rhs, meta, m, nb, i, j, s, i, s,
+                               bsz, cf, inv_c1, ga.bc[nb - 1], ga.rb,
+                               P0[l1 * NG + i], P0[l2 * NG + i]);
+          } else {
+            // red cell of the adjacent tile of this box
+            v = gs_cell(x, r, ix3(NG, i, j, s), NG, SK, cf, inv_c1);
+          }
+        }
+        P0[jl * NG + i] = v;
+      }
+    }
+    if (s == 2 || s == NC + 1) {
+      // z ghost plane 0 (NC+1): x1 = plane 1 (NC), black, old;
+      // x2 = plane 2 (NC-1), red, new
+      const int nb = s == 2 ? 5 : 6, k = s == 2 ? 0 : NC + 1;
+      double *Pg = s == 2 ? Pmm : P0;
+      const double *X2 = s == 2 ? P0 : Pmm;
+#pragma unroll
+      for (int q = 0; q < CPT; q++) {
+        int i, j, c;
+        if (colof(q, i, j, c) && ((i + j + k) & 1))
+          Pg[c] = pair_ghost<NC>(src, coarse, rhs, meta, m, nb, i, j, k, i, j,
+                                 bsz, cf, inv_c1, ga.bc[nb - 1], ga.rb, Pm[c],
+                                 X2[c]);
+      }
+    }
+    __syncthreads();
+    // C: black cells of plane s-1; write the tile of plane s-1
+    if (s >= 2) {
+      const int k = s - 1;
+#pragma unroll
+      for (int q = 0; q < CPT; q++) {
+        int i, j, c;
+        if (!colof(q, i, j, c)) continue;
+        const size_t g = (size_t)k * SK + (size_t)j * NG + i;
+        if (!((i + j + k) & 1)) {
+          const double v =
+              (r1[q] - cf.c[1] * Pm[c - 1] - cf.c[2] * Pm[c + 1] -
+               cf.c[3] * Pm[c - NG] - cf.c[4] * Pm[c + NG] - cf.c[5] * Pmm[c] -
+               cf.c[6] * P0[c]) *
+              inv_c1;
+          y[g] = v;
+        } else {
+          y[g] = Pm[c];
+        }
+      }
+    }
+    __syncthreads();
+    // D: plane s+2 into the slot of plane s-2
+    if (s + 2 <= NC + 1) {
+#pragma unroll
+      for (int q = 0; q < EPT; q++) {
+        const int e = tid + NT * q;
+        if (e < PLT) P[(s + 2) & 3][e] = nx[q];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < CPT; q++) {
+      r1[q] = r2[q];
+      r2[q] = nr[q];
+    }
+    __syncthreads();
+  }
 }
 
 __device__ __forceinline__ double apply7(const double *x, size_t c, size_t sj,
@@ -478,6 +707,9 @@ struct afh_mg {
   double *d_dtab = nullptr; // device copy of h_dtab
   std::vector<double> h_dtab;
   int tab_bc[6] = {0, 0, 0, 0, 0, 0};
+  // fused GSRB pairs (k_gsrb_pair) on levels with at least fused_min boxes
+  int fused_min = 256;
+  double *alt = nullptr;  // spare image of phi (all boxes) for the ping-pong
 };
 
 // (diag, 1/diag) of the folded operator per MG level and boundary class, in
@@ -506,6 +738,10 @@ static int32_t build_table(afh_mg *mg) {
                     mg->h_dtab.size() * sizeof(double), hipMemcpyHostToDevice));
   P.dtab = mg->d_dtab;
   return AFH_OK;
+}
+
+static bool fused_nc_ok(int nc) {
+  return nc == 4 || nc == 8 || nc == 16 || nc == 32 || nc == 64;
 }
 
 static inline dim3 blocks1(size_t n, int bs = 256) {
@@ -584,6 +820,19 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
                               (int)mg->small_lds));
   AFH_HIP(hipMalloc(&mg->d_dtab, (size_t)MAXMG * 64 * 2 * sizeof(double)));
   if (int32_t e = build_table(mg)) return e;
+  // AFH_GSRB_FUSED_MIN_BOXES: smallest level (in boxes) smoothed with the
+  // fused red-black kernel; 0 disables it
+  if (const char *env = getenv("AFH_GSRB_FUSED_MIN_BOXES"))
+    mg->fused_min = atoi(env);
+  if (fused_nc_ok(t->nc) && mg->fused_min > 0) {
+    bool any = false;
+    for (int l = 2; l <= t->nlvl; l++) any |= t->ids.n(l) >= mg->fused_min;
+    if (any) {
+      AFH_HIP(hipMalloc(&mg->alt, (size_t)t->nb * t->bsz * sizeof(double)));
+      AFH_HIP(hipMemsetAsync(mg->alt, 0, (size_t)t->nb * t->bsz * sizeof(double),
+                             t->stream));
+    }
+  }
   for (int q = 0; q < P.n_mg; q++) {
     size_t n = (size_t)(P.dims[q][0] + 2) * (P.dims[q][1] + 2) * (P.dims[q][2] + 2);
     AFH_HIP(hipMalloc(&P.u[q], n * sizeof(double)));
@@ -607,27 +856,83 @@ int32_t afh_mg_destroy(afh_mg *mg) {
     hipFree(mg->P.r[q]);
   }
   hipFree(mg->d_dtab);
+  if (mg->alt) hipFree(mg->alt);
   delete mg;
   return AFH_OK;
 }
 
+}  // extern "C"
+
+template <int NC>
+static void launch_pair(afh_mg *mg, int lvl, const double *src, double *dst,
+                        const Coef &cf, double inv_c1) {
+  afh_tree *t = mg->t;
+  hipLaunchKernelGGL(k_gsrb_pair<NC>, dim3(t->ids.n(lvl) * RbGeom<NC>::NTILE),
+                     dim3(RbGeom<NC>::NT),
+                     0, t->stream, src, dst, t->ccv(mg->d.i_rhs),
+                     t->ccv(mg->d.i_phi), t->d_boxes, t->ids.at(lvl), t->bsz,
+                     cf, inv_c1, t->gc_args(mg->d.i_phi));
+}
+
+extern "C" {
+
+static int32_t gsrb_half(afh_mg *mg, int lvl, int n, bool corners) {
+  afh_tree *t = mg->t;
+  const int nid = t->ids.n(lvl), nc = t->nc;
+  const Coef cf = mg->lvl_c[lvl - 1];
+  const int cells = nc * nc * nc / 2;
+  prof_begin(t, AFH_PROF_GSRB);
+  hipLaunchKernelGGL(k_gsrb, dim3((cells + 255) / 256, nid), dim3(256), 0,
+                     t->stream, t->ccv(mg->d.i_phi), t->ccv(mg->d.i_rhs),
+                     t->ids.at(lvl), nc, t->bsz, cf, 1 / cf.c[0], n);
+  // read phi (all), rhs (half), write phi (half) = 16 B/cell
+  prof_end(t, AFH_PROF_GSRB, 16.0 * nc * nc * nc * nid);
+  AFH_LAUNCH_CHECK("k_gsrb");
+  return gc_lvl(t, lvl, mg->d.i_phi, corners);
+}
+
+// gsrb_boxes (m_af_multigrid.f90:741-760): 2 n_cycle half-sweeps, each
+// followed by a ghost fill of the level. On levels with enough boxes the
+// pairs run fused (k_gsrb_pair), alternating phi -> alt -> phi; an odd
+// number of pairs starts with one split pair.
 static int32_t gsrb_boxes(afh_mg *mg, int lvl, bool up) {
   afh_tree *t = mg->t;
   const int n_cycle = up ? mg->d.n_cycle_up : mg->d.n_cycle_down;
   const int nid = t->ids.n(lvl), nc = t->nc;
   const Coef cf = mg->lvl_c[lvl - 1];
   const double inv_c1 = 1 / cf.c[0];
-  const int cells = nc * nc * nc / 2;
-  for (int n = 1; n <= 2 * n_cycle; n++) {
+  const bool fused = mg->alt && nid >= mg->fused_min;
+  int n0 = 1;
+  if (fused && (n_cycle & 1)) {
+    if (int32_t e = gsrb_half(mg, lvl, 1, false)) return e;
+    if (int32_t e = gsrb_half(mg, lvl, 2, up && n_cycle == 1)) return e;
+    n0 = 2;
+  }
+  if (!fused) {
+    for (int n = 1; n <= 2 * n_cycle; n++)
+      if (int32_t e = gsrb_half(mg, lvl, n, up && n == 2 * n_cycle)) return e;
+    return AFH_OK;
+  }
+  double *phi = t->ccv(mg->d.i_phi);
+  const afh::GcArgs ga = t->gc_args(mg->d.i_phi);
+  for (int n = n0; n <= n_cycle; n++) {
+    const bool to_alt = ((n - n0) & 1) == 0;
+    const double *src = to_alt ? phi : mg->alt;
+    double *dst = to_alt ? mg->alt : phi;
     prof_begin(t, AFH_PROF_GSRB);
-    hipLaunchKernelGGL(k_gsrb, dim3((cells + 255) / 256, nid), dim3(256), 0,
-                       t->stream, t->ccv(mg->d.i_phi), t->ccv(mg->d.i_rhs),
-                       t->ids.at(lvl), nc, t->bsz, cf, inv_c1, n);
-    // read phi (all), rhs (half), write phi (half) = 16 B/cell
-    prof_end(t, AFH_PROF_GSRB, 16.0 * nc * nc * nc * nid);
-    AFH_LAUNCH_CHECK("k_gsrb");
-    int32_t e = gc_lvl(t, lvl, mg->d.i_phi, up && n == 2 * n_cycle);
-    if (e) return e;
+    switch (nc) {
+    case 4: launch_pair<4>(mg, lvl, src, dst, cf, inv_c1); break;
+    case 8: launch_pair<8>(mg, lvl, src, dst, cf, inv_c1); break;
+    case 16: launch_pair<16>(mg, lvl, src, dst, cf, inv_c1); break;
+    case 32: launch_pair<32>(mg, lvl, src, dst, cf, inv_c1); break;
+    default: launch_pair<64>(mg, lvl, src, dst, cf, inv_c1); break;
+    }
+    // a red+black pair reads phi and rhs and writes phi
+    // once = 24 B/cell
+    prof_end(t, AFH_PROF_GSRB, 24.0 * nc * nc * nc * nid);
+    AFH_LAUNCH_CHECK("k_gsrb_pair");
+    if (int32_t e = gc_lvl_ptr(t, lvl, dst, phi, ga, up && n == n_cycle))
+      return e;
   }
   return AFH_OK;
 }

@@ -24,9 +24,6 @@ namespace afh {
 constexpr int MAXS = AFH_MAX_SPECIES;
 constexpr int MAXPREV = 4;
 
-__device__ __forceinline__ size_t ix3(int ng, int i, int j, int k) {
-  return ((size_t)k * ng + j) * ng + i;
-}
 __device__ __forceinline__ size_t fidx(int nf, int d, int i, int j, int k) {
   return (size_t)d * nf * nf * nf + ((size_t)(k - 1) * nf + (j - 1)) * nf +
          (i - 1);

@@ -51,13 +51,11 @@ void prof_end(afh_tree *t, int kc, double bytes) {
   t->prof_launches++;
 }
 
-__device__ __forceinline__ size_t ix3(int ng, int i, int j, int k) {
-  return ((size_t)k * ng + j) * ng + i;
-}
-
 // ------------------------------------------------------------ faces
 // One thread per ghost cell of face (blockIdx.y+1) of box ids[blockIdx.z].
+// Coarse data (refinement boundaries) are read from vc.
 __global__ void k_gc_faces(double *__restrict__ v,
+                           const double *__restrict__ vc,
                            const afh_box_meta *__restrict__ meta,
                            const int32_t *__restrict__ ids, int nc, size_t bsz,
                            GcArgs ga) {
@@ -86,91 +84,10 @@ __global__ void k_gc_faces(double *__restrict__ v,
     c[dst] = v[(size_t)(nb_id - 1) * bsz + ix3(ng, q[0], q[1], q[2])];
     return;
   }
-  const int x1 = low ? 1 : nc;
-  const int x2 = low ? 2 : nc - 1;
-  if (nb_id < 0) {
-    // bc_to_gc
-    double c0, c1, c2;
-    const afh_bc bc = ga.bc[nb - 1];
-    switch (bc.type) {
-    case AFH_BC_DIRICHLET: c0 = 2; c1 = -1; c2 = 0; break;
-    case AFH_BC_NEUMANN: c0 = m.dr[d] * (low ? -1 : 1); c1 = 1; c2 = 0; break;
-    case AFH_BC_CONTINUOUS: c0 = 0; c1 = 2; c2 = -1; break;
-    default: c0 = 1; c1 = 0; c2 = 0; break;
-    }
-    int q1[3] = {p[0], p[1], p[2]}, q2[3] = {p[0], p[1], p[2]};
-    q1[d] = x1;
-    q2[d] = x2;
-    c[dst] = c0 * bc.value + c1 * c[ix3(ng, q1[0], q1[1], q1[2])] +
-             c2 * c[ix3(ng, q2[0], q2[1], q2[2])];
-    return;
-  }
-  // refinement boundary: coarse data from the parent's neighbour
-  const int p_id = m.parent;
-  const int p_nb_id = meta[p_id - 1].neighbors[nb - 1];
-  const double *cp = v + (size_t)(p_nb_id - 1) * bsz;
-  const int hnc = nc >> 1;
-  int co[3];
-  for (int q = 0; q < 3; q++) co[q] = ((m.ix[q] - 1) & 1) * hnc;
-
-  if (ga.rb == AFH_RB_MG_SIDES) {
-    // mg_sides_rb: tmp(x, y) = coarse value next to the face, at tangential
-    // offsets co; gc = tmp +- g1 +- g2; ghost = 0.5 gc + 0.75 x_i - 0.25 x_i+d
-    const int cn = low ? nc : 1;
-    const int ii = (a + 1) >> 1, jj = (b + 1) >> 1;
-    auto tmp = [&](int x, int y) {
-      int q[3];
-      q[d] = cn;
-      q[ta] = co[ta] + x;
-      q[tb] = co[tb] + y;
-      return cp[ix3(ng, q[0], q[1], q[2])];
-    };
-    const double g1 = 0.125 * (tmp(ii + 1, jj) - tmp(ii - 1, jj));
-    const double g2 = 0.125 * (tmp(ii, jj + 1) - tmp(ii, jj - 1));
-    const double t0 = tmp(ii, jj);
-    double gcv;
-    if (a & 1) {
-      gcv = (b & 1) ? t0 - g1 - g2 : t0 - g1 + g2;
-    } else {
-      gcv = (b & 1) ? t0 + g1 - g2 : t0 + g1 + g2;
-    }
-    int q1[3] = {p[0], p[1], p[2]}, q2[3] = {p[0], p[1], p[2]};
-    q1[d] = x1;
-    q2[d] = x2;
-    c[dst] = 0.5 * gcv + 0.75 * c[ix3(ng, q1[0], q1[1], q1[2])] -
-             0.25 * c[ix3(ng, q2[0], q2[1], q2[2])];
-    return;
-  }
-  // af_gc_interp / af_gc_interp_lim; offsets on the parent's neighbour
-  const double third = 1 / 3.0, sixth = 1 / 6.0;
-  int off[3] = {co[0], co[1], co[2]};
-  off[d] -= (low ? -1 : 1) * nc;
-  const int ix_c = low ? nc : 1;
-  const int a1 = off[ta] + ((a + 1) >> 1), a2 = a1 + 1 - 2 * (a & 1);
-  const int b1 = off[tb] + ((b + 1) >> 1), b2 = b1 + 1 - 2 * (b & 1);
-  int q[3];
-  q[d] = ix_c;
-  q[ta] = a1, q[tb] = b1;
-  const double cv1 = cp[ix3(ng, q[0], q[1], q[2])];
-  double cv2, cv3;
-  if (d < 2) {
-    q[ta] = a2, q[tb] = b1;
-    cv2 = cp[ix3(ng, q[0], q[1], q[2])];
-    q[ta] = a1, q[tb] = b2;
-    cv3 = cp[ix3(ng, q[0], q[1], q[2])];
-  } else {
-    // case (3): c(2) uses j_c2 and c(3) uses i_c2 (m_af_ghostcell.f90:479-482)
-    q[ta] = a1, q[tb] = b2;
-    cv2 = cp[ix3(ng, q[0], q[1], q[2])];
-    q[ta] = a2, q[tb] = b1;
-    cv3 = cp[ix3(ng, q[0], q[1], q[2])];
-  }
-  int qf[3] = {p[0], p[1], p[2]};
-  qf[d] = x1;
-  double val = third * cv1 + sixth * cv2 + sixth * cv3 +
-               third * c[ix3(ng, qf[0], qf[1], qf[2])];
-  if (ga.rb == AFH_RB_GC_INTERP_LIM && val > 2 * cv1) val = 2 * cv1;
-  c[dst] = val;
+  c[dst] = gc_face_nocopy(vc, meta, m, nb, p, a, b, nc, bsz, ga.bc[nb - 1], ga.rb,
+                          [&](const int *q) {
+                            return c[ix3(ng, q[0], q[1], q[2])];
+                          });
 }
 
 // ------------------------------------------------------------ edges+corners
@@ -248,23 +165,28 @@ __global__ void k_gc_corners(double *__restrict__ v,
   }
 }
 
-int32_t gc_lvl(afh_tree *t, int lvl, int iv, int corners) {
+int32_t gc_lvl_ptr(afh_tree *t, int lvl, double *v, const double *vc,
+                   const GcArgs &ga, int corners) {
   const int n = t->ids.n(lvl);
   if (n == 0) return AFH_OK;
   const int nc = t->nc;
   dim3 grid((nc * nc + 255) / 256, 6, n);
   prof_begin(t, AFH_PROF_GHOST);
-  hipLaunchKernelGGL(k_gc_faces, grid, dim3(256), 0, t->stream, t->ccv(iv),
-                     t->d_boxes, t->ids.at(lvl), nc, t->bsz, t->gc_args(iv));
+  hipLaunchKernelGGL(k_gc_faces, grid, dim3(256), 0, t->stream, v, vc,
+                     t->d_boxes, t->ids.at(lvl), nc, t->bsz, ga);
   // algorithmic bytes: read one interior layer + write one ghost layer
   prof_end(t, AFH_PROF_GHOST, 16.0 * 6 * nc * nc * n);
   AFH_LAUNCH_CHECK("k_gc_faces");
   if (corners) {
-    hipLaunchKernelGGL(k_gc_corners, dim3(n), dim3(256), 0, t->stream,
-                       t->ccv(iv), t->d_boxes, t->ids.at(lvl), nc, t->bsz);
+    hipLaunchKernelGGL(k_gc_corners, dim3(n), dim3(256), 0, t->stream, v,
+                       t->d_boxes, t->ids.at(lvl), nc, t->bsz);
     AFH_LAUNCH_CHECK("k_gc_corners");
   }
   return AFH_OK;
+}
+
+int32_t gc_lvl(afh_tree *t, int lvl, int iv, int corners) {
+  return gc_lvl_ptr(t, lvl, t->ccv(iv), t->ccv(iv), t->gc_args(iv), corners);
 }
 
 // ------------------------------------------------------------ restriction

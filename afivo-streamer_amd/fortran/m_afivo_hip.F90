@@ -1,0 +1,370 @@
+!> ISO_C_BINDING interface to libafivo_hip (include/afivo_hip.h).
+!>
+!> This is the layer a Fortran afivo-streamer driver uses to hand its
+!> per-timestep hot path to the MI355X library: the bind(C) types mirror the
+!> C structs field by field (same order, same padding) and every entry point
+!> keeps the C name. Nothing here depends on afivo; m_afivo_hip_tree packs an
+!> afivo tree into these types.
+!>
+!> The symbol prefix is AFH_PFX ("afh_" by default). Building with
+!> -DAFH_PFX='"afo_"' binds the same interface to the C oracle
+!> (oracle/lib/libafo.so), which the CPU tests use.
+#ifndef AFH_PFX
+#define AFH_PFX "afh_"
+#endif
+module m_afivo_hip
+  use iso_c_binding
+  implicit none
+  public
+
+  character(len=*), parameter :: afh_pfx = AFH_PFX
+
+  integer(c_int32_t), parameter :: AFH_OK = 0
+  integer(c_int32_t), parameter :: AFH_ERR_ARG = -1
+  integer(c_int32_t), parameter :: AFH_ERR_UNSUPPORTED = -2
+  integer(c_int32_t), parameter :: AFH_ERR_DEVICE = -3
+  integer(c_int32_t), parameter :: AFH_ERR_STATE = -4
+
+  ! afivo/src/m_af_types.f90:51-64
+  integer(c_int32_t), parameter :: AFH_BC_DIRICHLET = -10
+  integer(c_int32_t), parameter :: AFH_BC_NEUMANN = -11
+  integer(c_int32_t), parameter :: AFH_BC_CONTINUOUS = -12
+  integer(c_int32_t), parameter :: AFH_BC_DIRICHLET_COPY = -13
+
+  integer(c_int32_t), parameter :: AFH_RB_GC_INTERP = 1
+  integer(c_int32_t), parameter :: AFH_RB_GC_INTERP_LIM = 2
+  integer(c_int32_t), parameter :: AFH_RB_MG_SIDES = 3
+
+  integer(c_int32_t), parameter :: AFH_LIM_NONE = 1
+  integer(c_int32_t), parameter :: AFH_LIM_VANLEER = 2
+  integer(c_int32_t), parameter :: AFH_LIM_KOREN = 3
+  integer(c_int32_t), parameter :: AFH_LIM_MINMOD = 4
+  integer(c_int32_t), parameter :: AFH_LIM_MC = 5
+  integer(c_int32_t), parameter :: AFH_LIM_GMINMOD43 = 6
+  integer(c_int32_t), parameter :: AFH_LIM_ZERO = 7
+
+  integer(c_int32_t), parameter :: AFH_RATE_TABULATED_FIELD = 1
+  integer(c_int32_t), parameter :: AFH_RATE_CONSTANT = 2
+  integer(c_int32_t), parameter :: AFH_RATE_LINEAR = 3
+  integer(c_int32_t), parameter :: AFH_RATE_EXP_V1 = 4
+  integer(c_int32_t), parameter :: AFH_RATE_EXP_V2 = 5
+
+  integer(c_int32_t), parameter :: AFH_COARSE_CYCLES = 1
+  integer, parameter :: AFH_MAX_SPECIES = 32
+  integer, parameter :: AFH_MAX_REACTIONS = 128
+
+  integer(c_int32_t), parameter :: AFH_PROF_GSRB = 1
+  integer(c_int32_t), parameter :: AFH_PROF_GHOST = 2
+  integer(c_int32_t), parameter :: AFH_PROF_FLUX = 3
+  integer(c_int32_t), parameter :: AFH_PROF_UPDATE = 4
+
+  type, bind(C) :: afh_box_meta
+     integer(c_int32_t) :: lvl
+     integer(c_int32_t) :: ix(3)
+     integer(c_int32_t) :: parent
+     integer(c_int32_t) :: children(8)
+     integer(c_int32_t) :: neighbors(6)
+     integer(c_int32_t) :: neighbor_mat(27)
+     real(c_double)     :: r_min(3)
+     real(c_double)     :: dr(3)
+  end type afh_box_meta
+
+  type, bind(C) :: afh_tree_desc
+     integer(c_int32_t) :: n_cell
+     integer(c_int32_t) :: n_boxes
+     integer(c_int32_t) :: highest_lvl
+     integer(c_int32_t) :: n_var_cell
+     integer(c_int32_t) :: n_var_face
+     integer(c_int32_t) :: coarse_grid_size(3)
+     integer(c_int32_t) :: periodic(3)
+     real(c_double)     :: r_base(3)
+     real(c_double)     :: dr_base(3)
+     type(c_ptr)        :: boxes = c_null_ptr
+     type(c_ptr)        :: lvl_ids = c_null_ptr, lvl_ids_off = c_null_ptr
+     type(c_ptr)        :: lvl_leaves = c_null_ptr, lvl_leaves_off = c_null_ptr
+     type(c_ptr)        :: lvl_parents = c_null_ptr, lvl_parents_off = c_null_ptr
+  end type afh_tree_desc
+
+  type, bind(C) :: afh_bc
+     integer(c_int32_t) :: type
+     real(c_double)     :: value
+  end type afh_bc
+
+  type, bind(C) :: afh_lt
+     integer(c_int32_t) :: n_points
+     integer(c_int32_t) :: n_cols
+     real(c_double)     :: x_min
+     real(c_double)     :: inv_fac
+     type(c_ptr)        :: rows_cols = c_null_ptr
+  end type afh_lt
+
+  type, bind(C) :: afh_reaction
+     integer(c_int32_t) :: rate_type
+     integer(c_int32_t) :: table_col
+     real(c_double)     :: rate_factor
+     real(c_double)     :: c(4)
+     integer(c_int32_t) :: n_in
+     integer(c_int32_t) :: ix_in(4)
+     integer(c_int32_t) :: n_out
+     integer(c_int32_t) :: ix_out(4)
+     integer(c_int32_t) :: mult_out(4)
+  end type afh_reaction
+
+  type, bind(C) :: afh_fluid_desc
+     integer(c_int32_t) :: n_species
+     integer(c_int32_t) :: species_iv(AFH_MAX_SPECIES)
+     integer(c_int32_t) :: species_charge(AFH_MAX_SPECIES)
+     integer(c_int32_t) :: i_electron
+     integer(c_int32_t) :: i_efld
+     integer(c_int32_t) :: f_flux
+     integer(c_int32_t) :: f_field
+     integer(c_int32_t) :: limiter
+     real(c_double)     :: gas_number_density
+     type(afh_lt)       :: td
+     type(afh_lt)       :: chem
+     integer(c_int32_t) :: n_reactions
+     type(c_ptr)        :: reactions = c_null_ptr
+     real(c_double)     :: dt_chemistry_nmin
+  end type afh_fluid_desc
+
+  type, bind(C) :: afh_mg_desc
+     integer(c_int32_t) :: i_phi, i_rhs, i_tmp
+     integer(c_int32_t) :: n_cycle_down, n_cycle_up
+     real(c_double)     :: helmholtz_lambda
+     integer(c_int32_t) :: coarse_mode
+     integer(c_int32_t) :: coarse_cycles
+  end type afh_mg_desc
+
+  interface
+     function afh_last_error() bind(C, name=afh_pfx//"last_error")
+       import
+       type(c_ptr) :: afh_last_error
+     end function afh_last_error
+
+     function afh_tree_create(desc, device, out) bind(C, name=afh_pfx//"tree_create")
+       import
+       type(afh_tree_desc), intent(in) :: desc
+       integer(c_int32_t), value       :: device
+       type(c_ptr), intent(out)        :: out
+       integer(c_int32_t)              :: afh_tree_create
+     end function afh_tree_create
+
+     function afh_tree_destroy(t) bind(C, name=afh_pfx//"tree_destroy")
+       import
+       type(c_ptr), value :: t
+       integer(c_int32_t) :: afh_tree_destroy
+     end function afh_tree_destroy
+
+     function afh_tree_sync(t) bind(C, name=afh_pfx//"tree_sync")
+       import
+       type(c_ptr), value :: t
+       integer(c_int32_t) :: afh_tree_sync
+     end function afh_tree_sync
+
+     function afh_set_cc_methods(t, iv, bc6, rb, prolong_limiter) &
+          bind(C, name=afh_pfx//"set_cc_methods")
+       import
+       type(c_ptr), value              :: t
+       integer(c_int32_t), value       :: iv
+       type(afh_bc), intent(in)        :: bc6(6)
+       integer(c_int32_t), value       :: rb, prolong_limiter
+       integer(c_int32_t)              :: afh_set_cc_methods
+     end function afh_set_cc_methods
+
+     function afh_set_bc(t, iv, nb, bc_type, bc_value) bind(C, name=afh_pfx//"set_bc")
+       import
+       type(c_ptr), value        :: t
+       integer(c_int32_t), value :: iv, nb, bc_type
+       real(c_double), value     :: bc_value
+       integer(c_int32_t)        :: afh_set_bc
+     end function afh_set_bc
+
+     function afh_cc_put(t, iv, host) bind(C, name=afh_pfx//"cc_put")
+       import
+       type(c_ptr), value        :: t
+       integer(c_int32_t), value :: iv
+       real(c_double), intent(in) :: host(*)
+       integer(c_int32_t)        :: afh_cc_put
+     end function afh_cc_put
+
+     function afh_cc_get(t, iv, host) bind(C, name=afh_pfx//"cc_get")
+       import
+       type(c_ptr), value        :: t
+       integer(c_int32_t), value :: iv
+       real(c_double), intent(inout) :: host(*)
+       integer(c_int32_t)        :: afh_cc_get
+     end function afh_cc_get
+
+     function afh_fc_put(t, ivf, host) bind(C, name=afh_pfx//"fc_put")
+       import
+       type(c_ptr), value        :: t
+       integer(c_int32_t), value :: ivf
+       real(c_double), intent(in) :: host(*)
+       integer(c_int32_t)        :: afh_fc_put
+     end function afh_fc_put
+
+     function afh_fc_get(t, ivf, host) bind(C, name=afh_pfx//"fc_get")
+       import
+       type(c_ptr), value        :: t
+       integer(c_int32_t), value :: ivf
+       real(c_double), intent(inout) :: host(*)
+       integer(c_int32_t)        :: afh_fc_get
+     end function afh_fc_get
+
+     function afh_gc_lvl(t, lvl, iv, corners) bind(C, name=afh_pfx//"gc_lvl")
+       import
+       type(c_ptr), value        :: t
+       integer(c_int32_t), value :: lvl, iv, corners
+       integer(c_int32_t)        :: afh_gc_lvl
+     end function afh_gc_lvl
+
+     function afh_gc_tree(t, iv, corners) bind(C, name=afh_pfx//"gc_tree")
+       import
+       type(c_ptr), value        :: t
+       integer(c_int32_t), value :: iv, corners
+       integer(c_int32_t)        :: afh_gc_tree
+     end function afh_gc_tree
+
+     function afh_restrict_tree(t, iv) bind(C, name=afh_pfx//"restrict_tree")
+       import
+       type(c_ptr), value        :: t
+       integer(c_int32_t), value :: iv
+       integer(c_int32_t)        :: afh_restrict_tree
+     end function afh_restrict_tree
+
+     function afh_tree_copy_cc(t, iv_from, iv_to) bind(C, name=afh_pfx//"tree_copy_cc")
+       import
+       type(c_ptr), value        :: t
+       integer(c_int32_t), value :: iv_from, iv_to
+       integer(c_int32_t)        :: afh_tree_copy_cc
+     end function afh_tree_copy_cc
+
+     function afh_tree_maxabs_cc(t, iv, out) bind(C, name=afh_pfx//"tree_maxabs_cc")
+       import
+       type(c_ptr), value         :: t
+       integer(c_int32_t), value  :: iv
+       real(c_double), intent(out) :: out
+       integer(c_int32_t)         :: afh_tree_maxabs_cc
+     end function afh_tree_maxabs_cc
+
+     function afh_mg_create(t, desc, out) bind(C, name=afh_pfx//"mg_create")
+       import
+       type(c_ptr), value            :: t
+       type(afh_mg_desc), intent(in) :: desc
+       type(c_ptr), intent(out)      :: out
+       integer(c_int32_t)            :: afh_mg_create
+     end function afh_mg_create
+
+     function afh_mg_destroy(mg) bind(C, name=afh_pfx//"mg_destroy")
+       import
+       type(c_ptr), value :: mg
+       integer(c_int32_t) :: afh_mg_destroy
+     end function afh_mg_destroy
+
+     function afh_mg_fas_vcycle(mg, set_residual, highest_lvl) &
+          bind(C, name=afh_pfx//"mg_fas_vcycle")
+       import
+       type(c_ptr), value        :: mg
+       integer(c_int32_t), value :: set_residual, highest_lvl
+       integer(c_int32_t)        :: afh_mg_fas_vcycle
+     end function afh_mg_fas_vcycle
+
+     function afh_mg_compute_phi_gradient(mg, i_fc, fac, i_norm) &
+          bind(C, name=afh_pfx//"mg_compute_phi_gradient")
+       import
+       type(c_ptr), value        :: mg
+       integer(c_int32_t), value :: i_fc
+       real(c_double), value     :: fac
+       integer(c_int32_t), value :: i_norm
+       integer(c_int32_t)        :: afh_mg_compute_phi_gradient
+     end function afh_mg_compute_phi_gradient
+
+     function afh_fluid_create(t, desc, out) bind(C, name=afh_pfx//"fluid_create")
+       import
+       type(c_ptr), value               :: t
+       type(afh_fluid_desc), intent(in) :: desc
+       type(c_ptr), intent(out)         :: out
+       integer(c_int32_t)               :: afh_fluid_create
+     end function afh_fluid_create
+
+     function afh_fluid_destroy(f) bind(C, name=afh_pfx//"fluid_destroy")
+       import
+       type(c_ptr), value :: f
+       integer(c_int32_t) :: afh_fluid_destroy
+     end function afh_fluid_destroy
+
+     function afh_field_set_rhs(f, i_rhs, s_in) bind(C, name=afh_pfx//"field_set_rhs")
+       import
+       type(c_ptr), value        :: f
+       integer(c_int32_t), value :: i_rhs, s_in
+       integer(c_int32_t)        :: afh_field_set_rhs
+     end function afh_field_set_rhs
+
+     function afh_flux_upwind_tree(f, s_deriv, dt_lim) &
+          bind(C, name=afh_pfx//"flux_upwind_tree")
+       import
+       type(c_ptr), value          :: f
+       integer(c_int32_t), value   :: s_deriv
+       real(c_double), intent(out) :: dt_lim(2)
+       integer(c_int32_t)          :: afh_flux_upwind_tree
+     end function afh_flux_upwind_tree
+
+     function afh_flux_update_densities(f, dt, s_deriv, n_prev, s_prev, w_prev, &
+          s_out, last_step, dt_lim) bind(C, name=afh_pfx//"flux_update_densities")
+       import
+       type(c_ptr), value             :: f
+       real(c_double), value          :: dt
+       integer(c_int32_t), value      :: s_deriv, n_prev
+       integer(c_int32_t), intent(in) :: s_prev(*)
+       real(c_double), intent(in)     :: w_prev(*)
+       integer(c_int32_t), value      :: s_out, last_step
+       real(c_double), intent(out)    :: dt_lim(2)
+       integer(c_int32_t)             :: afh_flux_update_densities
+     end function afh_flux_update_densities
+
+     function afh_profile_enable(t, kclass) bind(C, name=afh_pfx//"profile_enable")
+       import
+       type(c_ptr), value        :: t
+       integer(c_int32_t), value :: kclass
+       integer(c_int32_t)        :: afh_profile_enable
+     end function afh_profile_enable
+
+     function afh_profile_read(t, total_ms, launches, bytes) &
+          bind(C, name=afh_pfx//"profile_read")
+       import
+       type(c_ptr), value            :: t
+       real(c_double), intent(out)   :: total_ms
+       integer(c_int64_t), intent(out) :: launches
+       real(c_double), intent(out)   :: bytes
+       integer(c_int32_t)            :: afh_profile_read
+     end function afh_profile_read
+
+     function c_strlen(s) bind(C, name="strlen")
+       import
+       type(c_ptr), value :: s
+       integer(c_size_t)  :: c_strlen
+     end function c_strlen
+  end interface
+
+contains
+
+  !> Turn a non-zero return code into `error stop`, as the reference does on
+  !> failure (e.g. m_af_stencil.f90:338), with the library's message.
+  subroutine afh_check(ierr, what)
+    integer(c_int32_t), intent(in) :: ierr
+    character(len=*), intent(in)   :: what
+    character(kind=c_char), pointer :: msg(:)
+    type(c_ptr)                     :: p
+    integer                         :: n
+    character(len=:), allocatable   :: text
+    if (ierr == AFH_OK) return
+    p = afh_last_error()
+    n = int(c_strlen(p))
+    call c_f_pointer(p, msg, [n])
+    allocate(character(len=n) :: text)
+    text = transfer(msg(1:n), text)
+    write(*, '(A,A,A,I0,A,A)') "afivo_hip: ", what, " failed (", ierr, "): ", text
+    error stop "afivo_hip call failed"
+  end subroutine afh_check
+
+end module m_afivo_hip

@@ -111,6 +111,37 @@ contains
     call table_set_column(chemtbl_fld, 2, x_data, y2)
   end subroutine hx_init_transport
 
+  !> Load td_tbl and chemtbl_fld from a tables.bin fixture (the layout
+  !> golden_gen's dump_tables writes: per table n_points, n_cols, x_min,
+  !> inv_fac, rows_cols), instead of rebuilding them from the transport-data
+  !> file with hx_init_transport.
+  subroutine hx_load_tables(path)
+    character(len=*), intent(in) :: path
+    integer                      :: u
+    open(newunit=u, file=path, access="stream", form="unformatted", &
+         status="old", action="read")
+    call read_lt(u, td_tbl)
+    call read_lt(u, chemtbl_fld)
+    close(u)
+  contains
+    subroutine read_lt(u, lt)
+      integer, intent(in)       :: u
+      type(LT_t), intent(inout) :: lt
+      integer(4)                :: np, ncol
+      integer                   :: i
+      read(u) np, ncol, lt%x_min, lt%inv_fac
+      lt%n_points = np
+      lt%n_cols = ncol
+      lt%xspacing = LT_xspacing_linear
+      lt%extrapolate_above = .false.
+      if (allocated(lt%rows_cols)) deallocate(lt%rows_cols, lt%cols_rows, lt%x)
+      allocate(lt%rows_cols(np, ncol), lt%cols_rows(ncol, np), lt%x(np))
+      read(u) lt%rows_cols
+      lt%cols_rows = transpose(lt%rows_cols)
+      lt%x = [(lt%x_min + (i - 1) / lt%inv_fac, i = 1, np)]
+    end subroutine read_lt
+  end subroutine hx_load_tables
+
   !> field_bc_homogeneous, src/m_field.f90:547-567
   subroutine hx_bc_phi(box, nb, iv, coords, bc_val, bc_type)
     type(box_t), intent(in) :: box

@@ -33,8 +33,20 @@ def oracle():
     return capi.oracle_library()
 
 
+# smoother variants: "split" = one launch per half-sweep with the level ghost
+# fill in between (the reference's sequence); "fused" = k_gsrb_pair on every
+# level (AFH_GSRB_FUSED_MIN_BOXES=1), which must give the same bits
+SMOOTHERS = {"split": "0", "fused": "1"}
+
+
+@pytest.fixture(params=sorted(SMOOTHERS))
+def smoother(request, monkeypatch):
+    monkeypatch.setenv("AFH_GSRB_FUSED_MIN_BOXES", SMOOTHERS[request.param])
+    return request.param
+
+
 @pytest.mark.parametrize("case", golden.CASES)
-def test_hip_matches_reference_golden(hip, case):
+def test_hip_matches_reference_golden(hip, case, smoother):
     report, dts, g = golden.run_golden(hip, case, isolated=True)
     bad = []
     for stage, errs in report.items():
@@ -74,6 +86,7 @@ def _assert_same(ca, cb, ivs=(), fvs=()):
 TOPOS = {
     "uni16_l3": lambda: uniform_tree(16, (16, 16, 16), (2e-3, 2e-3, 2e-3), 3),
     "uni8_l4_2x1x1": lambda: uniform_tree(8, (16, 8, 8), (2e-3, 1e-3, 1e-3), 4),
+    "uni64_l2": lambda: uniform_tree(64, (64, 64, 64), (4e-3, 4e-3, 4e-3), 2),
     "amr8": lambda: build_tree(
         8, (16, 16, 16), (2e-3, 2e-3, 2e-3), 2,
         refine=lambda lvl, r0, r1: lvl < 4 and np.all(r0 < 1.2e-3) and np.all(r1 > 0.7e-3)),
@@ -81,7 +94,7 @@ TOPOS = {
 
 
 @pytest.mark.parametrize("name", sorted(TOPOS))
-def test_hip_bitwise_equals_oracle_heun_step(hip, oracle, name):
+def test_hip_bitwise_equals_oracle_heun_step(hip, oracle, name, smoother):
     g = golden.load("uni8")
     topo = TOPOS[name]()
     ca, cb = _pair(hip, oracle, topo, g)
@@ -95,7 +108,7 @@ def test_hip_bitwise_equals_oracle_heun_step(hip, oracle, name):
                  [FV["flux"], FV["field"]])
 
 
-def test_vcycles_converge_large(hip):
+def test_vcycles_converge_large(hip, smoother):
     """Size-independent property at a larger size: each V-cycle reduces the
     max residual on the leaves by a large factor."""
     g = golden.load("uni8")
