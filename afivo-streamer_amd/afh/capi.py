@@ -120,7 +120,7 @@ SIGNATURES = {
     "profile_enable": (i32, [_VP, i32]),
     "profile_read": (i32, [_VP, P_f64, C.POINTER(C.c_int64), P_f64]),
 }
-PROF_GSRB, PROF_GHOST, PROF_FLUX, PROF_UPDATE = 1, 2, 3, 4
+PROF_GSRB, PROF_GHOST, PROF_FLUX, PROF_UPDATE, PROF_GSRB_PAIR = 1, 2, 3, 4, 5
 ORACLE_EXTRA = {
     "mg_gsrb_boxes": (i32, [_VP, i32, i32]),
     "mg_update_coarse": (i32, [_VP, i32]),

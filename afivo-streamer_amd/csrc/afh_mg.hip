@@ -919,7 +919,7 @@ static int32_t gsrb_boxes(afh_mg *mg, int lvl, bool up) {
     const bool to_alt = ((n - n0) & 1) == 0;
     const double *src = to_alt ? phi : mg->alt;
     double *dst = to_alt ? mg->alt : phi;
-    prof_begin(t, AFH_PROF_GSRB);
+    prof_begin(t, AFH_PROF_GSRB_PAIR);
     switch (nc) {
     case 4: launch_pair<4>(mg, lvl, src, dst, cf, inv_c1); break;
     case 8: launch_pair<8>(mg, lvl, src, dst, cf, inv_c1); break;
@@ -929,7 +929,7 @@ static int32_t gsrb_boxes(afh_mg *mg, int lvl, bool up) {
     }
     // a red+black pair reads phi and rhs and writes phi
     // once = 24 B/cell
-    prof_end(t, AFH_PROF_GSRB, 24.0 * nc * nc * nc * nid);
+    prof_end(t, AFH_PROF_GSRB_PAIR, 24.0 * nc * nc * nc * nid);
     AFH_LAUNCH_CHECK("k_gsrb_pair");
     if (int32_t e = gc_lvl_ptr(t, lvl, dst, phi, ga, up && n == n_cycle))
       return e;

@@ -57,6 +57,7 @@ module m_afivo_hip
   integer(c_int32_t), parameter :: AFH_PROF_GHOST = 2
   integer(c_int32_t), parameter :: AFH_PROF_FLUX = 3
   integer(c_int32_t), parameter :: AFH_PROF_UPDATE = 4
+  integer(c_int32_t), parameter :: AFH_PROF_GSRB_PAIR = 5
 
   type, bind(C) :: afh_box_meta
      integer(c_int32_t) :: lvl

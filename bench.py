@@ -89,6 +89,19 @@ def cpu_baseline(config, steps=2):
                       (steps, sample_lvls, ncell // nc ** 3, nc, ncell)}
 
 
+def pmc_traffic(config):
+    """HBM bytes per launch of the dominant kernel from the PMC passes
+    (scripts/pmc.sh -> scripts/pmc_summary.py -> profiles/*pmc*.json), or
+    None when no summary for this workload is committed."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_%s.json" % config)),
+                       reverse=True):
+        with open(path) as f:
+            d = json.load(f)
+        return d.get("hbm_bytes_per_launch")
+    return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -126,9 +139,10 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    # timed region: K steps; the GSRB kernel is timed with HIP events on the
+    # timed region: K steps; the dominant kernel (the fused red+black
+    # Gauss-Seidel pair on the leaf level) is timed with HIP events on the
     # tree's stream (afh_profile_*) over the same region
-    lib.call("profile_enable", case.tree.h, capi.PROF_GSRB)
+    lib.call("profile_enable", case.tree.h, capi.PROF_GSRB_PAIR)
     barrier()
     case.tree.sync()
     t0 = time.perf_counter()
@@ -170,10 +184,11 @@ def main():
                        "levels": int(case.topo["highest_lvl"]),
                        "coarse_cycles": args.coarse_cycles,
                        "parallelism": "replica-per-gpu"},
-            "roofline": {"bound": "hbm", "kernel": "k_gsrb",
+            "roofline": {"bound": "hbm",
+                         "kernel": "k_gsrb_pair<%d>" % CONFIGS[args.config][0],
                          "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": None,
+                         "traffic": pmc_traffic(args.config),
                          "avg_launch_us": avg_s * 1e6,
                          "algorithmic_bytes_per_launch": bytes_per_launch,
                          "launches": nl.value},

@@ -236,6 +236,7 @@ int32_t afh_flux_update_densities(afh_fluid *f, double dt, int32_t s_deriv,
 #define AFH_PROF_GHOST 2     /* ghost-cell fill (faces) */
 #define AFH_PROF_FLUX 3      /* flux kernel */
 #define AFH_PROF_UPDATE 4    /* density update */
+#define AFH_PROF_GSRB_PAIR 5 /* fused red+black Gauss-Seidel pair */
 int32_t afh_profile_enable(afh_tree *t, int32_t kclass);
 int32_t afh_profile_read(afh_tree *t, double *total_ms, int64_t *launches,
                          double *bytes);
