@@ -435,6 +435,55 @@ __global__ void k_gradient(const double *__restrict__ phi,
   }
 }
 
+// k_gradient for a compile-time box size, one level per launch: 2-D thread
+// blocks (NC x R rows) so no index divisions, and fac/dr precomputed on the
+// host (every box of a level has the same dr, so the quotient is bitwise the
+// one mg_box_lpl_gradient computes per box).
+template <int NC>
+__global__ void __launch_bounds__(256)
+    k_gradient_t(const double *__restrict__ phi, double *__restrict__ fcv,
+                 double *__restrict__ nrm, const int32_t *__restrict__ ids,
+                 size_t bsz, size_t fsz, double ix_, double iy, double iz) {
+  constexpr int R = 256 / NC < NC ? 256 / NC : NC;  // rows per block
+  constexpr int NG = NC + 2, NF = NC + 1;
+  constexpr size_t SJ = NG, SK = (size_t)NG * NG, D3 = (size_t)NF * NF * NF;
+  const int i = threadIdx.x % NC + 1;
+  const int j = (blockIdx.x % (NC / R)) * R + threadIdx.x / NC + 1;
+  const int k = blockIdx.x / (NC / R) + 1;
+  const int id = ids[blockIdx.y];
+  const double *p = phi + (size_t)(id - 1) * bsz;
+  double *f = fcv + (size_t)(id - 1) * fsz;
+  const size_t c = ((size_t)k * NG + j) * NG + i;
+  const double fxl = ix_ * (p[c] - p[c - 1]), fxh = ix_ * (p[c + 1] - p[c]);
+  const double fyl = iy * (p[c] - p[c - SJ]), fyh = iy * (p[c + SJ] - p[c]);
+  const double fzl = iz * (p[c] - p[c - SK]), fzh = iz * (p[c + SK] - p[c]);
+  const size_t fb = ((size_t)(k - 1) * NF + (j - 1)) * NF + (i - 1);
+  f[fb] = fxl;
+  if (i == NC) f[fb + 1] = fxh;
+  f[D3 + fb] = fyl;
+  if (j == NC) f[D3 + fb + NF] = fyh;
+  f[2 * D3 + fb] = fzl;
+  if (k == NC) f[2 * D3 + fb + (size_t)NF * NF] = fzh;
+  if (nrm) {
+    const double a = fxl + fxh, b = fyl + fyh, cc = fzl + fzh;
+    nrm[(size_t)(id - 1) * bsz + c] = 0.5 * sqrt(a * a + b * b + cc * cc);
+  }
+}
+
+template <int NC>
+static void launch_gradient(afh_tree *t, const double *phi, double *fcv,
+                            double *nrm, double fac) {
+  constexpr int R = 256 / NC < NC ? 256 / NC : NC;
+  for (int l = 1; l <= t->nlvl; l++) {
+    const int n = t->ids.n(l);
+    if (!n) continue;
+    const double *dr = &t->lvl_dr[3 * (l - 1)];
+    hipLaunchKernelGGL(k_gradient_t<NC>, dim3((NC / R) * NC, n), dim3(NC * R),
+                       0, t->stream, phi, fcv, nrm, t->ids.at(l), t->bsz,
+                       t->fsz, fac / dr[0], fac / dr[1], fac / dr[2]);
+  }
+}
+
 // ------------------------------------------------------------ coarse solver
 // Same arithmetic as oracle/c/afo.c (cs_*): BCs folded into the operator as
 // in stencil_handle_boundaries (m_coarse_solver.f90:442-491).
@@ -601,9 +650,13 @@ __global__ void __launch_bounds__(1024) k_cs_small(CsParams G, int m0,
   // the level table lives in LDS: a private copy indexed by the (dynamic)
   // level number would be placed in scratch memory
   __shared__ CsParams P;
+  __shared__ double s_dtab[MAXMG * 64 * 2];  // (diag, 1/diag) table in LDS
   const int bot = G.n_mg - 1;
+  for (int q = threadIdx.x; q < (bot + 1) * 128; q += blockDim.x)
+    s_dtab[q] = G.dtab[q];
   if (threadIdx.x == 0) {
     P = G;
+    P.dtab = s_dtab;
     size_t off = 0;
     for (int m = m0; m <= bot; m++) {
       const size_t n = (size_t)P.dims[m][0] * P.dims[m][1] * P.dims[m][2];
@@ -708,7 +761,8 @@ struct afh_mg {
   std::vector<double> h_dtab;
   int tab_bc[6] = {0, 0, 0, 0, 0, 0};
   // fused GSRB pairs (k_gsrb_pair) on levels with at least fused_min boxes
-  int fused_min = 256;
+  // (default: enough boxes for one workgroup per CU, 256 tiles)
+  int fused_min = 0;
   double *alt = nullptr;  // spare image of phi (all boxes) for the ping-pong
 };
 
@@ -813,7 +867,7 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
       mg->small_lds += 3 * sizeof(double) * (size_t)P.dims[q][0] * P.dims[q][1] *
                        P.dims[q][2];
   }
-  if (mg->small_lds + sizeof(CsParams) > 160 * 1024)
+  if (mg->small_lds + sizeof(CsParams) + MAXMG * 128 * sizeof(double) > 160 * 1024)
     return set_error(AFH_ERR_UNSUPPORTED, "coarse-solver LDS levels too large");
   AFH_HIP(hipFuncSetAttribute((const void *)k_cs_small,
                               hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -824,6 +878,8 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
   // fused red-black kernel; 0 disables it
   if (const char *env = getenv("AFH_GSRB_FUSED_MIN_BOXES"))
     mg->fused_min = atoi(env);
+  else if (fused_nc_ok(t->nc))
+    mg->fused_min = std::max(1, 256 / (t->nc / std::min(t->nc, 16)));
   if (fused_nc_ok(t->nc) && mg->fused_min > 0) {
     bool any = false;
     for (int l = 2; l <= t->nlvl; l++) any |= t->ids.n(l) >= mg->fused_min;
@@ -1065,10 +1121,19 @@ int32_t afh_mg_compute_phi_gradient(afh_mg *mg, int32_t i_fc, double fac,
     return set_error(AFH_ERR_ARG, "bad variable index");
   const int nc = t->nc, n3 = nc * nc * nc;
   const int ntot = t->ids.off[t->nlvl];
+  double *nrm = i_norm > 0 ? t->ccv(i_norm) : nullptr;
+  switch (nc) {
+  case 4: launch_gradient<4>(t, t->ccv(mg->d.i_phi), t->fcv(i_fc), nrm, fac); break;
+  case 8: launch_gradient<8>(t, t->ccv(mg->d.i_phi), t->fcv(i_fc), nrm, fac); break;
+  case 16: launch_gradient<16>(t, t->ccv(mg->d.i_phi), t->fcv(i_fc), nrm, fac); break;
+  case 32: launch_gradient<32>(t, t->ccv(mg->d.i_phi), t->fcv(i_fc), nrm, fac); break;
+  case 64: launch_gradient<64>(t, t->ccv(mg->d.i_phi), t->fcv(i_fc), nrm, fac); break;
+  default:
   hipLaunchKernelGGL(k_gradient, dim3((n3 + 255) / 256, ntot), dim3(256), 0,
                      t->stream, t->ccv(mg->d.i_phi), t->fcv(i_fc),
                      i_norm > 0 ? t->ccv(i_norm) : nullptr, t->d_boxes,
                      t->ids.d, nc, t->bsz, t->fsz, fac);
+  }
   AFH_LAUNCH_CHECK("k_gradient");
   return AFH_OK;
 }

@@ -337,6 +337,159 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+// Plane-marching variant of k_flux for NC in {8, 16, 32, 64}: a workgroup
+// owns a tile of TJ rows (j) of a box, one thread per (i, j) column, and
+// marches over k. Every face is evaluated once (low faces; high faces on the
+// box boundary). The CFL sum of a cell needs the transport of its high faces
+// too: x from the next lane (__shfl_down), y from the next row through LDS
+// (the tile's last row recomputes it, face_vd), z from the next plane (the
+// x+y part of the sum is carried one step). Same expressions, same operand
+// order as k_flux: bitwise identical fluxes and limits.
+template <int NC>
+struct FluxGeom {
+  static constexpr int TJ = 256 / NC < NC ? 256 / NC : NC;  // rows per tile
+  static constexpr int NT = NC * TJ;
+  static constexpr int NTILE = NC / TJ;
+};
+
+template <int NC>
+__global__ void __launch_bounds__(FluxGeom<NC>::NT)
+    k_flux_march(FluxArgs A, const int32_t *__restrict__ ids, size_t bsz,
+                 size_t fsz, unsigned long long *red) {
+  using G = FluxGeom<NC>;
+  constexpr int NG = NC + 2, NF = NC + 1, TJ = G::TJ;
+  constexpr size_t SK = (size_t)NG * NG, FSK = (size_t)NF * NF;
+  constexpr size_t FD = (size_t)NF * NF * NF;
+  __shared__ double sv[G::NT], sd[G::NT];
+  __shared__ double r1[G::NT / 64 + 1], r2[G::NT / 64 + 1];
+  const int tid = threadIdx.x;
+  const int id = ids[blockIdx.x / G::NTILE];
+  const int i = tid % NC + 1;
+  const int jr = tid / NC;  // row within the tile
+  const int j = (blockIdx.x % G::NTILE) * TJ + jr + 1;
+  const double *ne = A.ne + (size_t)(id - 1) * bsz;
+  const double *E = A.E + (size_t)(id - 1) * bsz;
+  const double *Ef = A.Ef + (size_t)(id - 1) * fsz;
+  double *F = A.F + (size_t)(id - 1) * fsz;
+  const double *g2 = A.gc2 + (size_t)(id - 1) * 6 * NC * NC;
+  const double ix = A.inv_dx[0], iy = A.inv_dx[1], iz = A.inv_dx[2];
+  const size_t cc = (size_t)j * NG + i;                    // column, plane 0
+  const size_t fcol = (size_t)(j - 1) * NF + (i - 1);      // face column
+  const int gq_z = (j - 1) * NC + (i - 1);
+  // z window of this column: ne at k-2 .. k+1, |E| at k-1, k
+  double zm2 = g2[4 * NC * NC + gq_z];  // ne(k-2) for k = 1: 2nd ghost layer
+  double zm1 = ne[cc], z0 = ne[SK + cc], zp1 = ne[2 * SK + cc];
+  double em1 = E[cc], e0 = E[SK + cc];
+  double cfl_xy = 0, vz_lo = 0, dz_lo = 0;  // previous plane's x+y sum, z-low
+  double cmax = -HUGE_VAL, smax = -HUGE_VAL;
+
+  for (int k = 1; k <= NC; k++) {
+    const size_t c0 = (size_t)k * SK + cc;
+    const size_t fb = (size_t)(k - 1) * FSK + fcol;
+    // z low face of cell k (between k-1 and k)
+    double vz, dz, fz, sz;
+    face_eval(A, zm2, zm1, z0, zp1, em1, e0, Ef[2 * FD + fb], iz, vz, dz, fz, sz);
+    F[2 * FD + fb] = fz;
+    smax = fmax(smax, sz);
+    // finish the CFL sum of cell k-1 (its z-high face is this one)
+    if (k > 1) {
+      const double mv = fmax(fabs(vz), fabs(vz_lo));
+      const double md = fmax(dz, dz_lo);
+      cmax = fmax(cmax, cfl_xy + (1.0 * mv * iz + 2 * md * (iz * iz)));
+    }
+    vz_lo = vz;
+    dz_lo = dz;
+    // x low face of cell i
+    double vx, dx, fx, sx;
+    {
+      const double Lm2 = (i == 1) ? g2[0 * NC * NC + (k - 1) * NC + (j - 1)] : ne[c0 - 2];
+      face_eval(A, Lm2, ne[c0 - 1], z0, ne[c0 + 1], E[c0 - 1], e0, Ef[fb], ix,
+                vx, dx, fx, sx);
+      F[fb] = fx;
+      smax = fmax(smax, sx);
+    }
+    double vxh = __shfl_down(vx, 1, 64), dxh = __shfl_down(dx, 1, 64);
+    if (i == NC) {
+      const double Lp2 = g2[1 * NC * NC + (k - 1) * NC + (j - 1)];
+      double fh, sh;
+      face_eval(A, ne[c0 - 1], z0, ne[c0 + 1], Lp2, e0, E[c0 + 1], Ef[fb + 1],
+                ix, vxh, dxh, fh, sh);
+      F[fb + 1] = fh;
+      smax = fmax(smax, sh);
+    }
+    // y low face of row j
+    double vy, dy, fy, sy;
+    {
+      const double Lm2 = (j == 1) ? g2[2 * NC * NC + (k - 1) * NC + (i - 1)]
+                                  : ne[c0 - 2 * NG];
+      face_eval(A, Lm2, ne[c0 - NG], z0, ne[c0 + NG], E[c0 - NG], e0,
+                Ef[FD + fb], iy, vy, dy, fy, sy);
+      F[FD + fb] = fy;
+      smax = fmax(smax, sy);
+    }
+    sv[tid] = vy;
+    sd[tid] = dy;
+    __syncthreads();
+    double vyh, dyh;
+    if (jr + 1 < TJ) {
+      vyh = sv[tid + NC];
+      dyh = sd[tid + NC];
+    } else if (j == NC) {
+      const double Lp2 = g2[3 * NC * NC + (k - 1) * NC + (i - 1)];
+      double fh, sh;
+      face_eval(A, ne[c0 - NG], z0, ne[c0 + NG], Lp2, e0, E[c0 + NG],
+                Ef[FD + fb + NF], iy, vyh, dyh, fh, sh);
+      F[FD + fb + NF] = fh;
+      smax = fmax(smax, sh);
+    } else {
+      face_vd(A, e0, E[c0 + NG], Ef[FD + fb + NF], vyh, dyh);
+    }
+    __syncthreads();  // sv/sd are rewritten next plane
+    {
+      const double mvx = fmax(fabs(vxh), fabs(vx)), mdx = fmax(dxh, dx);
+      const double mvy = fmax(fabs(vyh), fabs(vy)), mdy = fmax(dyh, dy);
+      double c = 0.0;
+      c = c + (1.0 * mvx * ix + 2 * mdx * (ix * ix));
+      c = c + (1.0 * mvy * iy + 2 * mdy * (iy * iy));
+      cfl_xy = c;
+    }
+    // advance the z window
+    const double zp2 = k + 2 <= NC + 1 ? ne[c0 + 2 * SK] : 0.0;
+    const double ep1 = E[c0 + SK];
+    if (k == NC) {
+      // z high face of the box (between NC and NC+1)
+      const double Lp2 = g2[5 * NC * NC + gq_z];
+      double vh, dh, fh, sh;
+      face_eval(A, zm1, z0, zp1, Lp2, e0, ep1,
+                Ef[2 * FD + fb + FSK], iz, vh, dh, fh, sh);
+      F[2 * FD + fb + FSK] = fh;
+      smax = fmax(smax, sh);
+      const double mv = fmax(fabs(vh), fabs(vz_lo));
+      const double md = fmax(dh, dz_lo);
+      cmax = fmax(cmax, cfl_xy + (1.0 * mv * iz + 2 * md * (iz * iz)));
+    }
+    zm2 = zm1;
+    zm1 = z0;
+    z0 = zp1;
+    zp1 = zp2;
+    em1 = e0;
+    e0 = ep1;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    cmax = fmax(cmax, __shfl_xor(cmax, o, 64));
+    smax = fmax(smax, __shfl_xor(smax, o, 64));
+  }
+  const int lane = tid & 63, w = tid >> 6;
+  if (lane == 0) r1[w] = cmax, r2[w] = smax;
+  __syncthreads();
+  if (tid == 0) {
+    for (int q = 1; q < (G::NT + 63) / 64; q++)
+      cmax = fmax(cmax, r1[q]), smax = fmax(smax, r2[q]);
+    atomicMax(&red[red_shard()], dbl_to_ord(cmax));
+    atomicMax(&red[RED_SHARDS + red_shard()], dbl_to_ord(smax));
+  }
+}
+
 __constant__ int c_child_adj_nb[6][4] = {{1, 3, 5, 7}, {2, 4, 6, 8},
                                          {1, 2, 5, 6}, {3, 4, 7, 8},
                                          {1, 2, 3, 4}, {5, 6, 7, 8}};
@@ -624,6 +777,19 @@ int32_t afh_field_set_rhs(afh_fluid *f, int32_t i_rhs, int32_t s_in) {
   return AFH_OK;
 }
 
+}  // extern "C"
+
+template <int NC>
+static void launch_flux_march(afh_tree *t, const FluxArgs &A, int l,
+                              unsigned long long *red) {
+  hipLaunchKernelGGL(k_flux_march<NC>,
+                     dim3(t->leaves.n(l) * FluxGeom<NC>::NTILE),
+                     dim3(FluxGeom<NC>::NT), 0, t->stream, A, t->leaves.at(l),
+                     t->bsz, t->fsz, red);
+}
+
+extern "C" {
+
 int32_t afh_flux_upwind_tree(afh_fluid *f, int32_t s_deriv, double *dt_lim) {
   if (!f || !dt_lim) return set_error(AFH_ERR_ARG, "null argument");
   afh_tree *t = f->t;
@@ -660,7 +826,14 @@ int32_t afh_flux_upwind_tree(afh_fluid *f, int32_t s_deriv, double *dt_lim) {
     if (!n) continue;
     for (int q = 0; q < 3; q++) A.inv_dx[q] = 1 / t->lvl_dr[3 * (l - 1) + q];
     prof_begin(t, AFH_PROF_FLUX);
-    if (shfl)
+    if (nc == 64 || nc == 32 || nc == 16 || nc == 8) {
+      switch (nc) {
+      case 8: launch_flux_march<8>(t, A, l, red); break;
+      case 16: launch_flux_march<16>(t, A, l, red); break;
+      case 32: launch_flux_march<32>(t, A, l, red); break;
+      default: launch_flux_march<64>(t, A, l, red); break;
+      }
+    } else if (shfl)
       hipLaunchKernelGGL(k_flux<true>, dim3((n3 + 255) / 256, n), dim3(256), 0,
                          t->stream, A, t->leaves.at(l), nc, t->bsz, t->fsz, red);
     else
