@@ -119,7 +119,17 @@ SIGNATURES = {
                                     i32, P_f64]),
     "profile_enable": (i32, [_VP, i32]),
     "profile_read": (i32, [_VP, P_f64, C.POINTER(C.c_int64), P_f64]),
+    "tree_set_hook": (i32, [_VP, C.c_void_p, _VP]),
+    "tree_set_stream": (i32, [_VP, _VP]),
+    "plan_create": (i32, [_VP, P_i32, i32, P_i32, C.POINTER(C.c_int64)]),
+    "plan_create_fc": (i32, [_VP, P_i32, i32, P_i32, C.POINTER(C.c_int64)]),
+    "plan_pack": (i32, [_VP, i32, i32, _VP]),
+    "plan_unpack": (i32, [_VP, i32, i32, _VP]),
 }
+HOOK_HALO, HOOK_RIMS, HOOK_RESTRICT, HOOK_MAX, HOOK_MIN, HOOK_CFLUX = 1, 2, 3, 4, 5, 6
+# int32_t (*)(void *ctx, int32_t kind, int32_t level, int32_t iv, double *vals,
+#             int32_t n)
+HOOK_FN = C.CFUNCTYPE(i32, C.c_void_p, i32, i32, i32, P_f64, i32)
 PROF_GSRB, PROF_GHOST, PROF_FLUX, PROF_UPDATE, PROF_GSRB_PAIR = 1, 2, 3, 4, 5
 ORACLE_EXTRA = {
     "mg_gsrb_boxes": (i32, [_VP, i32, i32]),

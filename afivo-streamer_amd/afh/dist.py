@@ -1,0 +1,364 @@
+"""Box sharding over ranks.
+
+Partition: a partition level Lp >= 2 is chosen (the coarsest level with at
+least one box per rank); the boxes of Lp are ordered by the Morton index of
+their position (``box%ix``) and cut into contiguous chunks of about equal
+leaf-cell weight; every descendant belongs to the rank of its Lp ancestor
+(parents and children stay together, so restriction and prolongation are
+rank-local), and the levels below Lp -- the coarse grid and its solver
+included -- are replicated: every rank computes them redundantly.
+
+Every rank allocates storage for the whole tree; the boxes of other ranks are
+replicas, refreshed by exchanges where the library's hooks say a replica is
+read after its owner wrote it (include/afivo_hip.h, AFH_HOOK_*):
+
+* HALO(l, iv): the cells of each remote neighbour (26 directions) within two
+  layers of an owned box, before a ghost-cell fill of level l;
+* RIMS(l, iv): the same regions extended over the neighbour's ghost layers,
+  after the fill (read by the fused smoother's neighbour recomputation and
+  by refinement-boundary interpolation);
+* RESTRICT(Lp, iv): the parent octants restricted from Lp into the
+  replicated level Lp-1 (all-gather);
+* MAX / MIN: all-reduce of reduction results.
+
+Transport: torch.distributed point-to-point (batch_isend_irecv) -- RCCL
+("nccl") with device buffers on the GPU, gloo with host buffers in the CPU
+tests (and for several ranks sharing one GPU, staged through the host).
+"""
+import ctypes as C
+import traceback
+
+import numpy as np
+
+from . import capi
+
+# 26 neighbour directions, neighbor_mat index (dx+1) + 3(dy+1) + 9(dz+1)
+DIRS = [(dx, dy, dz) for dz in (-1, 0, 1) for dy in (-1, 0, 1) for dx in (-1, 0, 1)
+        if (dx, dy, dz) != (0, 0, 0)]
+DEPTH = 2
+
+
+def morton3(ix):
+    """Interleaved-bit (Z-order) index of 0-based integer positions."""
+    ix = np.asarray(ix, dtype=np.int64)
+    code = np.zeros(len(ix), dtype=np.int64)
+    for b in range(20):
+        for d in range(3):
+            code |= ((ix[:, d] >> b) & 1) << (3 * b + d)
+    return code
+
+
+class Partition:
+    """Ownership of every box for n_ranks (owner -1: replicated)."""
+
+    def __init__(self, topo, n_ranks):
+        self.topo = topo
+        self.n_ranks = n_ranks
+        self.nc = int(topo["nc"])
+        self.nb = int(topo["n_boxes"])
+        self.nlvl = int(topo["highest_lvl"])
+        self.lvl = np.asarray(topo["meta_lvl"])
+        self.parent = np.asarray(topo["meta_parent"])
+        self.children = np.asarray(topo["meta_children"])
+        self.nmat = np.asarray(topo["meta_neighbor_mat"]).reshape(self.nb, 27)
+        self.ix = np.asarray(topo["meta_ix"])
+        ids = {l: np.asarray(topo["lvl_ids_%d" % l], np.int64)
+               for l in range(1, self.nlvl + 1)}
+        self.owner = np.full(self.nb, -1, np.int64)
+        self.lp = None
+        if n_ranks > 1:
+            lp = next((l for l in range(2, self.nlvl + 1) if len(ids[l]) >= n_ranks), None)
+            if lp is None:
+                raise ValueError("no level >= 2 has %d boxes to shard" % n_ranks)
+            self.lp = lp
+            # leaf-cell weight of every subtree
+            w = np.zeros(self.nb + 1, np.int64)
+            for l in range(self.nlvl, 0, -1):
+                for i in ids[l]:
+                    ch = self.children[i - 1]
+                    w[i] = 1 if ch[0] == 0 else w[ch].sum()
+            sel = ids[lp]
+            order = sel[np.argsort(morton3(self.ix[sel - 1] - 1), kind="stable")]
+            cum = np.cumsum(w[order])
+            target = cum[-1] / n_ranks
+            rk = np.minimum((np.ceil(cum / target) - 1).astype(np.int64), n_ranks - 1)
+            # every rank gets at least one box: fall back to an even split
+            if len(np.unique(rk)) < n_ranks:
+                rk = (np.arange(len(order)) * n_ranks) // len(order)
+            self.owner[order - 1] = rk
+            for l in range(lp + 1, self.nlvl + 1):
+                for i in ids[l]:
+                    self.owner[i - 1] = self.owner[self.parent[i - 1] - 1]
+        self.ids = ids
+
+    def owned(self, rank, box_ids):
+        o = self.owner[np.asarray(box_ids, np.int64) - 1]
+        return np.asarray(box_ids)[(o == rank) | (o < 0)]
+
+    def local_topology(self, rank):
+        """The topology dict with this rank's level lists."""
+        t = dict(self.topo)
+        for l in range(1, self.nlvl + 1):
+            for k in ("ids", "leaves", "parents"):
+                key = "lvl_%s_%d" % (k, l)
+                t[key] = self.owned(rank, np.asarray(self.topo[key], np.int64)).astype(np.int32)
+        return t
+
+    # ---------------------------------------------------------------- plans
+    def _region(self, b, d, rims):
+        """Cells of box b within DEPTH layers of the box in direction -d
+        (b lies at direction d of the owned box); with rims, b's ghost
+        layers are included (along d and across it)."""
+        nc = self.nc
+        lo, hi = [], []
+        for x in d:
+            if x < 0:
+                lo.append(nc - DEPTH + 1), hi.append(nc + 1 if rims else nc)
+            elif x > 0:
+                lo.append(0 if rims else 1), hi.append(DEPTH)
+            else:
+                lo.append(0 if rims else 1), hi.append(nc + 1 if rims else nc)
+        return (int(b), *lo, *hi)
+
+    def halo_regions(self, recv_rank, send_rank, level, rims):
+        """Regions of boxes owned by send_rank that recv_rank reads around its
+        boxes of `level` (sorted, duplicates and contained regions removed)."""
+        if self.lp is None or level < self.lp:
+            return []
+        regs = set()
+        for a in self.ids[level]:
+            if self.owner[a - 1] != recv_rank:
+                continue
+            for d in DIRS:
+                b = self.nmat[a - 1][(d[0] + 1) + 3 * (d[1] + 1) + 9 * (d[2] + 1)]
+                if b > 0 and self.owner[b - 1] == send_rank:
+                    regs.add(self._region(b, d, rims))
+        out = []
+        by_box = {}
+        for r in regs:
+            by_box.setdefault(r[0], []).append(r)
+        for b in sorted(by_box):
+            rs = by_box[b]
+            for r in sorted(rs):
+                inside = any(q != r and all(q[1 + k] <= r[1 + k] and r[4 + k] <= q[4 + k]
+                                            for k in range(3)) for q in rs)
+                if not inside:
+                    out.append(r)
+        return out
+
+    def cflux_regions(self, recv_rank, send_rank):
+        """Face-flux faces of recv_rank's leaves that af_consistent_fluxes
+        sets from send_rank's refined neighbours (8 ints: id, dim, lo, hi;
+        face indices), in (refined box, face) order."""
+        if self.lp is None:
+            return []
+        nc = self.nc
+        out = []
+        for l in range(1, self.nlvl + 1):
+            for p in np.asarray(self.topo["lvl_parents_%d" % l], np.int64):
+                if self.owner[p - 1] != send_rank:
+                    continue
+                for nb in range(1, 7):
+                    q = int(np.asarray(self.topo["meta_neighbors"])[p - 1][nb - 1])
+                    if q <= 0 or self.children[q - 1][0] != 0 or self.owner[q - 1] != recv_rank:
+                        continue
+                    d = (nb - 1) // 2
+                    f = nc + 1 if (nb - 1) % 2 == 0 else 1  # the neighbour's face
+                    lo, hi = [1, 1, 1], [nc, nc, nc]
+                    lo[d] = hi[d] = f
+                    out.append((q, d, *lo, *hi))
+        return out
+
+    def octant_regions(self, send_rank):
+        """Parent octants written by send_rank's boxes of Lp (into the
+        replicated level Lp-1), in box order."""
+        if self.lp is None:
+            return []
+        hnc = self.nc // 2
+        out = []
+        for c in self.ids[self.lp]:
+            if self.owner[c - 1] != send_rank:
+                continue
+            p = self.parent[c - 1]
+            co = [((self.ix[c - 1][k] - 1) & 1) * hnc for k in range(3)]
+            out.append((int(p), co[0] + 1, co[1] + 1, co[2] + 1,
+                        co[0] + hnc, co[1] + hnc, co[2] + hnc))
+        return out
+
+
+class Shard:
+    """Executes the library's exchange hooks for one rank of a sharded tree."""
+
+    def __init__(self, part, rank, backend="gloo", device=None):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist = torch, dist
+        self.part = part
+        self.rank = rank
+        self.n = part.n_ranks
+        self.backend = backend
+        self.device = device  # torch device of the library's buffers (HIP) or None
+        self.tree = None
+        self.plans = {}
+        self.n_exchanges = 0
+
+    def attach(self, tree):
+        """Register plans and the hook on a Tree built from local_topology."""
+        self.tree = tree
+        lib = tree.lib
+        part = self.part
+        peers = [q for q in range(self.n) if q != self.rank]
+        if part.lp is not None:
+            for lvl in range(part.lp, part.nlvl + 1):
+                for rims in (False, True):
+                    send, recv = {}, {}
+                    for q in peers:
+                        send[q] = self._plan(part.halo_regions(q, self.rank, lvl, rims))
+                        recv[q] = self._plan(part.halo_regions(self.rank, q, lvl, rims))
+                    self.plans[("rims" if rims else "halo", lvl)] = (send, recv)
+            self.plans[("cflux", 0)] = (
+                {q: self._plan(part.cflux_regions(q, self.rank), fc=True) for q in peers},
+                {q: self._plan(part.cflux_regions(self.rank, q), fc=True) for q in peers})
+            mine = self._plan(part.octant_regions(self.rank))
+            self.plans[("octant", part.lp)] = (
+                {q: mine for q in peers},
+                {q: self._plan(part.octant_regions(q)) for q in peers})
+        self._bufs = {}
+        self.stream = None
+        if self.device is not None and self.backend == "nccl":
+            self.stream = self.torch.cuda.Stream(device=self.device)
+            lib.call("tree_set_stream", tree.h, C.c_void_p(self.stream.cuda_stream))
+        self._cb = capi.HOOK_FN(self._hook)
+        lib.call("tree_set_hook", tree.h, C.cast(self._cb, C.c_void_p), None)
+
+    def detach(self):
+        if self.tree is not None and self.tree.h:
+            self.tree.lib.call("tree_set_hook", self.tree.h, None, None)
+
+    def _plan(self, regions, fc=False):
+        lib, t = self.tree.lib, self.tree.h
+        arr = np.ascontiguousarray(np.asarray(regions, np.int32).reshape(-1, 8 if fc else 7))
+        pid, nval = C.c_int32(), C.c_int64()
+        lib.call("plan_create_fc" if fc else "plan_create", t,
+                 arr.ctypes.data_as(capi.P_i32), len(arr), C.byref(pid), C.byref(nval))
+        return (pid.value, nval.value)
+
+    # ----------------------------------------------------------- transport
+    def _buf(self, key, n, device):
+        """Persistent exchange buffer (reused by every exchange of a plan)."""
+        torch = self.torch
+        b = self._bufs.get(key)
+        if b is None:
+            b = torch.empty(max(n, 1), dtype=torch.float64, device=device)
+            self._bufs[key] = b
+        return b[:n]
+
+    def _exchange(self, send, recv, iv):
+        torch, dist = self.torch, self.dist
+        lib, t = self.tree.lib, self.tree.h
+        peers = sorted(set(send) | set(recv))
+        if self.device is not None and self.backend == "nccl":
+            # device buffers, everything on the tree's stream: pack, RCCL
+            # send/recv (ordered after the pack, and the stream waits for
+            # them), unpack -- no host synchronisation
+            with torch.cuda.stream(self.stream):
+                ops = []
+                for q in peers:
+                    (sp, sn), (rp, rn) = send[q], recv[q]
+                    if sn:
+                        b = self._buf(("s", sp), sn, self.device)
+                        lib.call("plan_pack", t, sp, iv, C.c_void_p(b.data_ptr()))
+                        ops.append(dist.P2POp(dist.isend, b, q))
+                    if rn:
+                        ops.append(dist.P2POp(dist.irecv, self._buf(("r", rp), rn, self.device), q))
+                if ops:
+                    for r in dist.batch_isend_irecv(ops):
+                        r.wait()
+                for q in peers:
+                    rp, rn = recv[q]
+                    if rn:
+                        lib.call("plan_unpack", t, rp, iv,
+                                 C.c_void_p(self._buf(("r", rp), rn, self.device).data_ptr()))
+            self.n_exchanges += 1
+            return
+        # host transport (gloo): a device library stages through the host
+        staged = self.device is not None
+        ops = []
+        for q in peers:
+            sp, sn = send[q]
+            if sn:
+                hb = self._buf(("s", sp), sn, None)
+                if staged:
+                    db = self._buf(("ds", sp), sn, self.device)
+                    lib.call("plan_pack", t, sp, iv, C.c_void_p(db.data_ptr()))
+                    self.tree.sync()
+                    hb.copy_(db)
+                else:
+                    lib.call("plan_pack", t, sp, iv, C.c_void_p(hb.data_ptr()))
+                ops.append(dist.P2POp(dist.isend, hb, q))
+            rp, rn = recv[q]
+            if rn:
+                ops.append(dist.P2POp(dist.irecv, self._buf(("r", rp), rn, None), q))
+        if ops:
+            for r in dist.batch_isend_irecv(ops):
+                r.wait()
+        for q in peers:
+            rp, rn = recv[q]
+            if not rn:
+                continue
+            hb = self._buf(("r", rp), rn, None)
+            if staged:
+                db = self._buf(("dr", rp), rn, self.device)
+                db.copy_(hb)
+                torch.cuda.synchronize(self.device)
+                lib.call("plan_unpack", t, rp, iv, C.c_void_p(db.data_ptr()))
+                self.tree.sync()
+            else:
+                lib.call("plan_unpack", t, rp, iv, C.c_void_p(hb.data_ptr()))
+        self.n_exchanges += 1
+
+    def _reduce(self, vals, n, op):
+        torch, dist = self.torch, self.dist
+        rop = dist.ReduceOp.MAX if op == capi.HOOK_MAX else dist.ReduceOp.MIN
+        host = [vals[i] for i in range(n)]
+        if self.device is not None and self.backend == "nccl":
+            with torch.cuda.stream(self.stream):
+                x = torch.tensor(host, dtype=torch.float64, device=self.device)
+                dist.all_reduce(x, op=rop)
+                out = x.tolist()
+        else:
+            x = torch.tensor(host, dtype=torch.float64)
+            dist.all_reduce(x, op=rop)
+            out = x.tolist()
+        for i in range(n):
+            vals[i] = out[i]
+
+    def _hook(self, ctx, kind, level, iv, vals, n):
+        try:
+            if kind in (capi.HOOK_MAX, capi.HOOK_MIN):
+                self._reduce(vals, n, kind)
+            elif kind == capi.HOOK_HALO:
+                p = self.plans.get(("halo", level))
+                if p:
+                    self._exchange(p[0], p[1], iv)
+            elif kind == capi.HOOK_RIMS:
+                p = self.plans.get(("rims", level))
+                if p:
+                    self._exchange(p[0], p[1], iv)
+            elif kind == capi.HOOK_CFLUX:
+                p = self.plans.get(("cflux", 0))
+                if p:
+                    self._exchange(p[0], p[1], iv)
+            elif kind == capi.HOOK_RESTRICT:
+                p = self.plans.get(("octant", level))
+                if p:
+                    self._exchange(p[0], p[1], iv)
+            return 0
+        except Exception:  # a Python error must not unwind through C
+            traceback.print_exc()
+            return 1
+
+    # ----------------------------------------------------------- results
+    def owned_mask(self):
+        o = self.part.owner
+        return (o == self.rank) | (o < 0)

@@ -55,10 +55,15 @@ class StreamerCase:
     """One streamer simulation state on a tree, driven through `lib`."""
 
     def __init__(self, lib, topo, td, chem, voltage, n_gas=None,
-                 coarse_cycles=20, device=-1):
+                 coarse_cycles=20, device=-1, shard=None):
+        """shard: an afh.dist.Shard -- this rank's part of a sharded tree
+        (the tree is created from the rank's level lists and the exchange
+        hooks are attached); None for a single-rank tree."""
         self.lib = lib
         self.topo = topo
-        self.tree = Tree(lib, topo, N_VAR_CELL, N_VAR_FACE, device=device)
+        self.shard = shard
+        local = shard.part.local_topology(shard.rank) if shard else topo
+        self.tree = Tree(lib, local, N_VAR_CELL, N_VAR_FACE, device=device)
         t = self.tree
         neumann0 = [(capi.BC_NEUMANN, 0.0)] * 6
         for sp in ("e", "pos", "neg"):
@@ -76,6 +81,8 @@ class StreamerCase:
                            IV["e"], IV["efld"], FV["flux"], FV["field"],
                            self.n_gas, td, chem, standard_reactions())
         self.domain = np.asarray(topo["domain"], float)
+        if shard:
+            shard.attach(self.tree)
 
     @staticmethod
     def phi_bc(voltage):

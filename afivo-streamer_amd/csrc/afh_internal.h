@@ -81,14 +81,33 @@ struct afh_tree {
   // grid spacing per level (afivo halves dr exactly per level, so every box
   // of a level has the same bits; verified at tree creation)
   std::vector<double> lvl_dr;  // 3 per level
+  std::vector<int> lvl_total;  // boxes per level over all ranks (topology)
+  // level l+1 has a refinement boundary (a face without same-level neighbour)
+  std::vector<int> lvl_rb_coarse;
+  bool own_stream = true;
   // kernel timing (afh_profile_*)
   int prof_class = 0;
   std::vector<hipEvent_t> ev_pool;
   size_t ev_used = 0;
   double prof_bytes = 0;
   int64_t prof_launches = 0;
+  // box sharding (afh_tree_set_hook, afh_plan_*): exchange hook, the
+  // smoother's spare phi image (variable 0 in hooks and plans), plans
+  afh_hook_fn hook = nullptr;
+  void *hook_ctx = nullptr;
+  double *alt = nullptr;
+  struct Plan {
+    int32_t *d_reg = nullptr;  // n x 7 (id, lo[3], hi[3])
+    int64_t *d_off = nullptr;  // n + 1 value offsets
+    int n = 0, max_cells = 0;
+    int64_t n_values = 0;
+    int fc = 0;                // face-variable plan (8 ints per region)
+  };
+  std::vector<Plan> plans;
 
   double *ccv(int iv) const { return cc + (size_t)(iv - 1) * nb * bsz; }
+  // cc variable iv, or the smoother's spare image of phi for iv == 0
+  double *var(int iv) const { return iv == 0 ? alt : ccv(iv); }
   double *fcv(int ivf) const { return fc + (size_t)(ivf - 1) * nb * fsz; }
   afh::GcArgs gc_args(int iv) const {
     afh::GcArgs a;
@@ -104,10 +123,17 @@ namespace afh {
 void prof_begin(afh_tree *t, int kc);
 void prof_end(afh_tree *t, int kc, double bytes);
 // Host launchers shared between translation units (afh_tree.hip).
-int32_t gc_lvl(afh_tree *t, int lvl, int iv, int corners);
-// ghost fill of level lvl of the image v (coarse data read from vc)
-int32_t gc_lvl_ptr(afh_tree *t, int lvl, double *v, const double *vc,
-                   const GcArgs &ga, int corners);
+int32_t gc_lvl(afh_tree *t, int lvl, int iv, int corners, bool rims = false);
+// ghost fill of level lvl of variable iv (0: the spare phi image), with the
+// coarse data of refinement boundaries read from vc; calls the sharding
+// hooks: HALO before, RIMS after when `rims` (the fused smoother reads the
+// replicas' ghost cells next) or when the next level has refinement
+// boundaries (its ghost cells read this level's replicas, ghosts included)
+int32_t gc_lvl_var(afh_tree *t, int lvl, int iv, const double *vc,
+                   const GcArgs &ga, int corners, bool rims = false);
+// sharding hook (no-op without one)
+int32_t call_hook(afh_tree *t, int kind, int lvl, int iv, double *vals = nullptr,
+                  int n = 0);
 int32_t restrict_boxes(afh_tree *t, const int32_t *d_ids, int n, int iv);
 // Sharded max/min reductions: each block folds its value into one of
 // RED_SHARDS words of a slot (no single-address contention), a one-block

@@ -93,10 +93,13 @@ __global__ void k_gsrb(double *__restrict__ phi, const double *__restrict__ rhs,
 template <int NC>
 struct RbGeom {
   static constexpr int NG = NC + 2;
-  static constexpr int TJ = NC < 16 ? NC : 16;         // rows per tile
+  // one tile per box (measured on MI355X, S1-64 leaf level: 16-row tiles of
+  // 256 threads 1.06 ms per pair, whole boxes of 1024 threads 0.87 ms -- the
+  // tiles' halo rows cost more than the extra occupancy gains)
+  static constexpr int TJ = NC;                        // rows per tile
   static constexpr int NTILE = NC / TJ;
   static constexpr int PLT = (TJ + 2) * NG;            // LDS plane (rows j0-1..j1+1)
-  static constexpr int NT = NC * TJ >= 256 ? 256 : (NC * TJ < 64 ? 64 : NC * TJ);
+  static constexpr int NT = NC * TJ >= 1024 ? 1024 : (NC * TJ < 64 ? 64 : NC * TJ);
   static constexpr int CPT = (NC * TJ + NT - 1) / NT;  // columns per thread
   static constexpr int EPT = (PLT + NT - 1) / NT;      // plane entries per thread
 };
@@ -116,12 +119,21 @@ __device__ __forceinline__ double pair_ghost(
   const bool low = ((nb - 1) & 1) == 0;
   const int p[3] = {p0, p1, p2};
   if (nb_id > 0) {
-    // the neighbour's red boundary cell, from its (old) black values
+    // the neighbour's red boundary cell, from its (old) black values; its
+    // ghost cell on our side is a copy of our x1 cell, taken from here (a
+    // sharded neighbour replica need not hold that ghost)
     int q[3] = {p0, p1, p2};
     q[d] = low ? NC : 1;
     const size_t o = (size_t)(nb_id - 1) * bsz;
-    return gs_cell(src + o, rhs + o, ix3(NG, q[0], q[1], q[2]), NG,
-                   (size_t)NG * NG, cf, inv_c1);
+    const double *xn = src + o;
+    const size_t c = ix3(NG, q[0], q[1], q[2]);
+    const size_t st[3] = {1, (size_t)NG, (size_t)NG * NG};
+    double v[6] = {xn[c - 1],  xn[c + 1],  xn[c - st[1]],
+                   xn[c + st[1]], xn[c - st[2]], xn[c + st[2]]};
+    v[2 * d + (low ? 1 : 0)] = x1v;
+    return (rhs[o + c] - cf.c[1] * v[0] - cf.c[2] * v[1] - cf.c[3] * v[2] -
+            cf.c[4] * v[3] - cf.c[5] * v[4] - cf.c[6] * v[5]) *
+           inv_c1;
   }
   const int x1 = low ? 1 : NC;
   return gc_face_nocopy(coarse, meta, m, nb, p, a, b, NC, bsz, bc, rb,
@@ -879,12 +891,13 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
   if (const char *env = getenv("AFH_GSRB_FUSED_MIN_BOXES"))
     mg->fused_min = atoi(env);
   else if (fused_nc_ok(t->nc))
-    mg->fused_min = std::max(1, 256 / (t->nc / std::min(t->nc, 16)));
+    mg->fused_min = 256;  // one box per workgroup: at least one per CU
   if (fused_nc_ok(t->nc) && mg->fused_min > 0) {
     bool any = false;
-    for (int l = 2; l <= t->nlvl; l++) any |= t->ids.n(l) >= mg->fused_min;
+    for (int l = 2; l <= t->nlvl; l++) any |= t->lvl_total[l - 1] >= mg->fused_min;
     if (any) {
       AFH_HIP(hipMalloc(&mg->alt, (size_t)t->nb * t->bsz * sizeof(double)));
+      t->alt = mg->alt;
       AFH_HIP(hipMemsetAsync(mg->alt, 0, (size_t)t->nb * t->bsz * sizeof(double),
                              t->stream));
     }
@@ -912,7 +925,10 @@ int32_t afh_mg_destroy(afh_mg *mg) {
     hipFree(mg->P.r[q]);
   }
   hipFree(mg->d_dtab);
-  if (mg->alt) hipFree(mg->alt);
+  if (mg->alt) {
+    if (mg->t->alt == mg->alt) mg->t->alt = nullptr;
+    hipFree(mg->alt);
+  }
   delete mg;
   return AFH_OK;
 }
@@ -923,6 +939,7 @@ template <int NC>
 static void launch_pair(afh_mg *mg, int lvl, const double *src, double *dst,
                         const Coef &cf, double inv_c1) {
   afh_tree *t = mg->t;
+  if (t->ids.n(lvl) == 0) return;
   hipLaunchKernelGGL(k_gsrb_pair<NC>, dim3(t->ids.n(lvl) * RbGeom<NC>::NTILE),
                      dim3(RbGeom<NC>::NT),
                      0, t->stream, src, dst, t->ccv(mg->d.i_rhs),
@@ -932,19 +949,27 @@ static void launch_pair(afh_mg *mg, int lvl, const double *src, double *dst,
 
 extern "C" {
 
+// gsrb_boxes smooths level lvl with the fused pair kernel (same answer on
+// every rank of a sharded tree: decided on the level's total box count)
+static bool fused_level(const afh_mg *mg, int lvl) {
+  return mg->alt && mg->t->lvl_total[lvl - 1] >= mg->fused_min;
+}
+
 static int32_t gsrb_half(afh_mg *mg, int lvl, int n, bool corners) {
   afh_tree *t = mg->t;
   const int nid = t->ids.n(lvl), nc = t->nc;
   const Coef cf = mg->lvl_c[lvl - 1];
   const int cells = nc * nc * nc / 2;
-  prof_begin(t, AFH_PROF_GSRB);
-  hipLaunchKernelGGL(k_gsrb, dim3((cells + 255) / 256, nid), dim3(256), 0,
-                     t->stream, t->ccv(mg->d.i_phi), t->ccv(mg->d.i_rhs),
-                     t->ids.at(lvl), nc, t->bsz, cf, 1 / cf.c[0], n);
-  // read phi (all), rhs (half), write phi (half) = 16 B/cell
-  prof_end(t, AFH_PROF_GSRB, 16.0 * nc * nc * nc * nid);
-  AFH_LAUNCH_CHECK("k_gsrb");
-  return gc_lvl(t, lvl, mg->d.i_phi, corners);
+  if (nid) {
+    prof_begin(t, AFH_PROF_GSRB);
+    hipLaunchKernelGGL(k_gsrb, dim3((cells + 255) / 256, nid), dim3(256), 0,
+                       t->stream, t->ccv(mg->d.i_phi), t->ccv(mg->d.i_rhs),
+                       t->ids.at(lvl), nc, t->bsz, cf, 1 / cf.c[0], n);
+    // read phi (all), rhs (half), write phi (half) = 16 B/cell
+    prof_end(t, AFH_PROF_GSRB, 16.0 * nc * nc * nc * nid);
+    AFH_LAUNCH_CHECK("k_gsrb");
+  }
+  return gc_lvl(t, lvl, mg->d.i_phi, corners, fused_level(mg, lvl));
 }
 
 // gsrb_boxes (m_af_multigrid.f90:741-760): 2 n_cycle half-sweeps, each
@@ -957,7 +982,7 @@ static int32_t gsrb_boxes(afh_mg *mg, int lvl, bool up) {
   const int nid = t->ids.n(lvl), nc = t->nc;
   const Coef cf = mg->lvl_c[lvl - 1];
   const double inv_c1 = 1 / cf.c[0];
-  const bool fused = mg->alt && nid >= mg->fused_min;
+  const bool fused = fused_level(mg, lvl);
   int n0 = 1;
   if (fused && (n_cycle & 1)) {
     if (int32_t e = gsrb_half(mg, lvl, 1, false)) return e;
@@ -971,10 +996,13 @@ static int32_t gsrb_boxes(afh_mg *mg, int lvl, bool up) {
   }
   double *phi = t->ccv(mg->d.i_phi);
   const afh::GcArgs ga = t->gc_args(mg->d.i_phi);
+  // the pair recomputes neighbours' red boundary cells from their rhs
+  if (int32_t e = call_hook(t, AFH_HOOK_HALO, lvl, mg->d.i_rhs)) return e;
   for (int n = n0; n <= n_cycle; n++) {
     const bool to_alt = ((n - n0) & 1) == 0;
     const double *src = to_alt ? phi : mg->alt;
     double *dst = to_alt ? mg->alt : phi;
+    const int dst_iv = to_alt ? 0 : mg->d.i_phi;
     prof_begin(t, AFH_PROF_GSRB_PAIR);
     switch (nc) {
     case 4: launch_pair<4>(mg, lvl, src, dst, cf, inv_c1); break;
@@ -987,7 +1015,8 @@ static int32_t gsrb_boxes(afh_mg *mg, int lvl, bool up) {
     // once = 24 B/cell
     prof_end(t, AFH_PROF_GSRB_PAIR, 24.0 * nc * nc * nc * nid);
     AFH_LAUNCH_CHECK("k_gsrb_pair");
-    if (int32_t e = gc_lvl_ptr(t, lvl, dst, phi, ga, up && n == n_cycle))
+    (void)dst;
+    if (int32_t e = gc_lvl_var(t, lvl, dst_iv, phi, ga, up && n == n_cycle, true))
       return e;
   }
   return AFH_OK;
@@ -997,13 +1026,18 @@ static int32_t update_coarse(afh_mg *mg, int lvl) {
   afh_tree *t = mg->t;
   const int nc = t->nc, hn = nc / 2;
   const int nid = t->ids.n(lvl);
-  hipLaunchKernelGGL(k_rstr_fas, dim3((hn * hn * hn + 255) / 256, nid),
-                     dim3(256), 0, t->stream, t->ccv(mg->d.i_phi),
-                     t->ccv(mg->d.i_rhs), t->ccv(mg->d.i_tmp), t->d_boxes,
-                     t->ids.at(lvl), nc, t->bsz, mg->lvl_c[lvl - 1]);
-  AFH_LAUNCH_CHECK("k_rstr_fas");
-  int32_t e = gc_lvl(t, lvl - 1, mg->d.i_phi, 1);
-  if (e) return e;
+  if (nid) {
+    hipLaunchKernelGGL(k_rstr_fas, dim3((hn * hn * hn + 255) / 256, nid),
+                       dim3(256), 0, t->stream, t->ccv(mg->d.i_phi),
+                       t->ccv(mg->d.i_rhs), t->ccv(mg->d.i_tmp), t->d_boxes,
+                       t->ids.at(lvl), nc, t->bsz, mg->lvl_c[lvl - 1]);
+    AFH_LAUNCH_CHECK("k_rstr_fas");
+  }
+  int32_t e;
+  if ((e = call_hook(t, AFH_HOOK_RESTRICT, lvl, mg->d.i_phi)) ||
+      (e = call_hook(t, AFH_HOOK_RESTRICT, lvl, mg->d.i_tmp)))
+    return e;
+  if ((e = gc_lvl(t, lvl - 1, mg->d.i_phi, 1, fused_level(mg, lvl - 1)))) return e;
   const int np = t->parents.n(lvl - 1);
   if (np) {
     hipLaunchKernelGGL(k_parent_rhs, dim3((unsigned)((t->bsz + 255) / 256), np),
@@ -1025,10 +1059,13 @@ static int32_t correct_children(afh_mg *mg, int lvl) {
     AFH_LAUNCH_CHECK("k_corr_tmp");
   }
   const int nid = t->ids.n(lvl);
-  hipLaunchKernelGGL(k_prolong, dim3((nc * nc * nc + 255) / 256, nid), dim3(256),
-                     0, t->stream, t->ccv(mg->d.i_phi), t->ccv(mg->d.i_tmp),
-                     t->d_boxes, t->ids.at(lvl), nc, t->bsz);
-  AFH_LAUNCH_CHECK("k_prolong");
+  if (nid) {
+    hipLaunchKernelGGL(k_prolong, dim3((nc * nc * nc + 255) / 256, nid),
+                       dim3(256), 0, t->stream, t->ccv(mg->d.i_phi),
+                       t->ccv(mg->d.i_tmp), t->d_boxes, t->ids.at(lvl), nc,
+                       t->bsz);
+    AFH_LAUNCH_CHECK("k_prolong");
+  }
   return AFH_OK;
 }
 
@@ -1097,12 +1134,13 @@ int32_t afh_mg_fas_vcycle(afh_mg *mg, int32_t set_residual, int32_t hl) {
   if ((e = solve_coarse(mg))) return e;
   for (int lvl = 2; lvl <= max_lvl; lvl++) {
     if ((e = correct_children(mg, lvl))) return e;
-    if ((e = gc_lvl(t, lvl, mg->d.i_phi, 1))) return e;
+    if ((e = gc_lvl(t, lvl, mg->d.i_phi, 1, fused_level(mg, lvl)))) return e;
     if ((e = gsrb_boxes(mg, lvl, true))) return e;
   }
   if (set_residual) {
     const int nc = t->nc, n3 = nc * nc * nc;
     for (int lvl = 1; lvl <= max_lvl; lvl++) {
+      if (!t->ids.n(lvl)) continue;
       hipLaunchKernelGGL(k_residual, dim3((n3 + 255) / 256, t->ids.n(lvl)),
                          dim3(256), 0, t->stream, t->ccv(mg->d.i_phi),
                          t->ccv(mg->d.i_rhs), t->ccv(mg->d.i_tmp),

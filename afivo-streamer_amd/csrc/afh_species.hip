@@ -262,65 +262,142 @@ __device__ __forceinline__ void face_vd(const FluxArgs &A, double Elo,
 // the velocity / diffusion of the high face too: in x it comes from the next
 // lane (__shfl_down, SHFL = lines of nc cells never straddle a wave); in y and
 // z it is recomputed (transport only, bitwise identical expression).
+// Table location of LT_get_loc (m_lookup_table.f90:330-363): row `low`
+// (1-based) and weight `lf` of that row.
+__device__ __forceinline__ void lt_loc(const DevLT &lt, double x, int &low,
+                                       double &lf) {
+  const double frac = (x - lt.x_min) * lt.inv_fac;
+  if (frac <= 0) {
+    low = 1;
+    lf = 1;
+  } else if (frac >= lt.n_points - 1) {
+    low = lt.n_points - 1;
+    lf = 0;
+  } else {
+    low = (int)ceil(frac);
+    lf = low - frac;
+  }
+}
+
+// Staged form of k_flux: (1) every neighbour value the thread needs is
+// loaded up front (restrict-qualified, so the loads are issued together);
+// (2) the table rows of all faces are fetched together; (3) limiter, flux,
+// CFL. Same expressions in the same order as face_eval / face_vd, so the
+// results are bitwise those of k_flux (which issued one memory round trip per
+// face and table lookup).
 template <bool SHFL>
 __global__ void __launch_bounds__(256)
-    k_flux(FluxArgs A, const int32_t *__restrict__ ids, int nc, size_t bsz,
-           size_t fsz, unsigned long long *red) {
+    k_flux_staged(FluxArgs A, const int32_t *__restrict__ ids, int nc, size_t bsz,
+                  size_t fsz, unsigned long long *red) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   const bool active = t < nc * nc * nc;
   const int tt = active ? t : 0;
   const int id = ids[blockIdx.y];
   const int i = tt % nc + 1, j = (tt / nc) % nc + 1, k = tt / (nc * nc) + 1;
   const int ng = nc + 2, nf = nc + 1;
-  const double *ne = A.ne + (size_t)(id - 1) * bsz;
-  const double *E = A.E + (size_t)(id - 1) * bsz;
-  const double *Ef = A.Ef + (size_t)(id - 1) * fsz;
-  double *F = A.F + (size_t)(id - 1) * fsz;
-  const double *g2 = A.gc2 + (size_t)(id - 1) * 6 * nc * nc;
+  const double *__restrict__ ne = A.ne + (size_t)(id - 1) * bsz;
+  const double *__restrict__ E = A.E + (size_t)(id - 1) * bsz;
+  const double *__restrict__ Ef = A.Ef + (size_t)(id - 1) * fsz;
+  double *__restrict__ F = A.F + (size_t)(id - 1) * fsz;
+  const double *__restrict__ g2 = A.gc2 + (size_t)(id - 1) * 6 * nc * nc;
   const int c0 = (k * ng + j) * ng + i;
   const int fcell = ((k - 1) * nf + (j - 1)) * nf + (i - 1);
+  const int fd = nf * nf * nf;
+  const int cc[3] = {i, j, k};
+  const int st[3] = {1, ng, ng * ng};
+  const int fst[3] = {1, nf, nf * nf};
+  const int gq[3] = {(k - 1) * nc + (j - 1), (k - 1) * nc + (i - 1),
+                     (j - 1) * nc + (i - 1)};
+
+  // (1) loads
+  double L[3][5], Em[3], Ep[3], ex_lo[3], ex_hi[3];
+  const double L0 = ne[c0], E0 = E[c0];
+#pragma unroll
+  for (int d = 0; d < 3; d++) {
+    const int c = cc[d];
+    L[d][0] = (c == 1) ? g2[(2 * d) * nc * nc + gq[d]] : ne[c0 - 2 * st[d]];
+    L[d][1] = ne[c0 - st[d]];
+    L[d][2] = L0;
+    L[d][3] = ne[c0 + st[d]];
+    L[d][4] = (c == nc) ? g2[(2 * d + 1) * nc * nc + gq[d]] : 0.0;
+    Em[d] = E[c0 - st[d]];
+    Ep[d] = E[c0 + st[d]];
+    ex_lo[d] = Ef[d * fd + fcell];
+    ex_hi[d] = Ef[d * fd + fcell + fst[d]];
+  }
+  // (2) table rows: low face of every dimension, high face where needed
+  // (box boundary; y and z for the CFL sum; x comes from the next lane)
+  int lo_row[3], hi_row[3];
+  double lo_lf[3], hi_lf[3];
+#pragma unroll
+  for (int d = 0; d < 3; d++) {
+    lt_loc(A.td, 0.5 * (Em[d] + E0) * 1e21 * A.N_inv, lo_row[d], lo_lf[d]);
+    lt_loc(A.td, 0.5 * (E0 + Ep[d]) * 1e21 * A.N_inv, hi_row[d], hi_lf[d]);
+  }
+  const int np = A.td.n_points;
+  double lo_r[3][4], hi_r[3][4];
+#pragma unroll
+  for (int d = 0; d < 3; d++) {
+    const double *r = A.td.rc + (lo_row[d] - 1);
+    lo_r[d][0] = r[0], lo_r[d][1] = r[1], lo_r[d][2] = r[np], lo_r[d][3] = r[np + 1];
+    const bool need_hi = (cc[d] == nc) || d > 0 || !SHFL;
+    if (need_hi) {
+      const double *h = A.td.rc + (hi_row[d] - 1);
+      hi_r[d][0] = h[0], hi_r[d][1] = h[1], hi_r[d][2] = h[np], hi_r[d][3] = h[np + 1];
+    } else {
+      hi_r[d][0] = hi_r[d][1] = hi_r[d][2] = hi_r[d][3] = 0.0;
+    }
+  }
+  // (3) fluxes and CFL (face_eval / face_vd arithmetic)
   double cfl = 0.0, smax = -HUGE_VAL;
 #pragma unroll
   for (int d = 0; d < 3; d++) {
-    const int st = d == 0 ? 1 : d == 1 ? ng : ng * ng;
-    const int fst = d == 0 ? 1 : d == 1 ? nf : nf * nf;
-    const int c = d == 0 ? i : d == 1 ? j : k;
-    const int a = d == 0 ? j : i, b = d == 2 ? j : k;
-    const int gq = (b - 1) * nc + (a - 1);
     const double inv_dx = A.inv_dx[d];
-    const int fb = d * nf * nf * nf + fcell;
-    const double Lm2 = (c == 1) ? g2[(2 * d) * nc * nc + gq] : ne[c0 - 2 * st];
-    const double Lm1 = ne[c0 - st], L0 = ne[c0], Lp1 = ne[c0 + st];
-    const double Em1 = E[c0 - st], E0 = E[c0], Ep1 = E[c0 + st];
-    double vl, dl, fl, sl;
-    face_eval(A, Lm2, Lm1, L0, Lp1, Em1, E0, Ef[fb], inv_dx, vl, dl, fl, sl);
-    if (active) F[fb] = fl;
-    smax = fmax(smax, sl);
-    double vh, dh;
+    const int fb = d * fd + fcell;
+    auto finish = [&](const double rr[4], double lf, double ex, double &v,
+                      double &dc) {
+      double mu = lf * rr[0] + (1 - lf) * rr[1];
+      const double dd = lf * rr[2] + (1 - lf) * rr[3];
+      mu = mu * A.N_inv;
+      dc = dd * A.N_inv;
+      v = -mu * ex;
+      return mu;
+    };
+    auto upwind = [&](double Lm2, double Lm1, double Lc, double Lp1, double ex) {
+      if (-1 * ex > 0) return Lm1 + 0.5 * limiter(A.lim, Lc - Lm1, Lm1 - Lm2);
+      return Lc - 0.5 * limiter(A.lim, Lc - Lm1, Lp1 - Lc);
+    };
+    double vl, dl;
+    {
+      const double u = upwind(L[d][0], L[d][1], L[d][2], L[d][3], ex_lo[d]);
+      const double mu = finish(lo_r[d], lo_lf[d], ex_lo[d], vl, dl);
+      const double flux = vl * u - dl * inv_dx * (L[d][2] - L[d][1]);
+      if (active) F[fb] = flux;
+      smax = fmax(smax, mu * u);
+    }
     double vsh = 0, dsh = 0;
     if (SHFL && d == 0) {
       vsh = __shfl_down(vl, 1, 64);
       dsh = __shfl_down(dl, 1, 64);
     }
-    if (c == nc) {
-      const double Lp2 = g2[(2 * d + 1) * nc * nc + gq];
-      double fh, sh;
-      face_eval(A, Lm1, L0, Lp1, Lp2, E0, Ep1, Ef[fb + fst], inv_dx, vh, dh,
-                fh, sh);
-      if (active) F[fb + fst] = fh;
-      smax = fmax(smax, sh);
+    double vh, dh;
+    if (cc[d] == nc) {
+      const double u = upwind(L[d][1], L[d][2], L[d][3], L[d][4], ex_hi[d]);
+      const double mu = finish(hi_r[d], hi_lf[d], ex_hi[d], vh, dh);
+      const double flux = vh * u - dh * inv_dx * (L[d][3] - L[d][2]);
+      if (active) F[fb + fst[d]] = flux;
+      smax = fmax(smax, mu * u);
     } else if (SHFL && d == 0) {
       vh = vsh;
       dh = dsh;
     } else {
-      face_vd(A, E0, Ep1, Ef[fb + fst], vh, dh);
+      finish(hi_r[d], hi_lf[d], ex_hi[d], vh, dh);
     }
     const double mv = fmax(fabs(vh), fabs(vl));
     const double md = fmax(dh, dl);
     cfl = cfl + (1.0 * mv * inv_dx + 2 * md * (inv_dx * inv_dx));
   }
   if (!active) cfl = smax = -HUGE_VAL;
-  // block max-reduction of the CFL sum and the conductivity
   for (int o = 32; o > 0; o >>= 1) {
     cfl = fmax(cfl, __shfl_xor(cfl, o, 64));
     smax = fmax(smax, __shfl_xor(smax, o, 64));
@@ -337,7 +414,7 @@ __global__ void __launch_bounds__(256)
   }
 }
 
-// Plane-marching variant of k_flux for NC in {8, 16, 32, 64}: a workgroup
+// Plane-marching variant of k_flux_staged for NC in {8, 16, 32, 64}: a workgroup
 // owns a tile of TJ rows (j) of a box, one thread per (i, j) column, and
 // marches over k. Every face is evaluated once (low faces; high faces on the
 // box boundary). The CFL sum of a cell needs the transport of its high faces
@@ -582,6 +659,13 @@ __global__ void __launch_bounds__(256)
     const int i = t % nc + 1, j = (t / nc) % nc + 1, k = t / (nc * nc) + 1;
     const int ng = nc + 2, nf = nc + 1;
     const size_t x = (size_t)(id - 1) * bsz + (size_t)((k * ng + j) * ng + i);
+    // face fluxes loaded up front (their latency overlaps the chemistry)
+    const double *__restrict__ F = A.F + (size_t)(id - 1) * fsz;
+    const int f0 = ((k - 1) * nf + (j - 1)) * nf + (i - 1);
+    const int d3 = nf * nf * nf;
+    const double fx0 = F[f0], fx1 = F[f0 + 1];
+    const double fy0 = F[d3 + f0], fy1 = F[d3 + f0 + nf];
+    const double fz0 = F[2 * d3 + f0], fz1 = F[2 * d3 + f0 + nf * nf];
     double y[NS], der[NS], dens[NS];
 #pragma unroll
     for (int s = 0; s < NS; s++) {
@@ -637,12 +721,9 @@ __global__ void __launch_bounds__(256)
     }
 #pragma unroll
     for (int s = 0; s < NS; s++) y[s] = y[s] + A.dt * der[s];
-    const double *F = A.F + (size_t)(id - 1) * fsz;
-    const int f0 = ((k - 1) * nf + (j - 1)) * nf + (i - 1);
-    const int d3 = nf * nf * nf;
-    const double div = A.dt_dr[0] * (F[f0] - F[f0 + 1]);
-    const double dvy = A.dt_dr[1] * (F[d3 + f0] - F[d3 + f0 + nf]);
-    const double dvz = A.dt_dr[2] * (F[2 * d3 + f0] - F[2 * d3 + f0 + nf * nf]);
+    const double div = A.dt_dr[0] * (fx0 - fx1);
+    const double dvy = A.dt_dr[1] * (fy0 - fy1);
+    const double dvz = A.dt_dr[2] * (fz0 - fz1);
 #pragma unroll
     for (int s = 0; s < NS; s++)
       if (s == A.e_index) y[s] = y[s] + div + dvy + dvz;
@@ -682,18 +763,23 @@ struct afh_fluid {
   DevReaction *d_reac = nullptr;
   int e_index = -1;
   DevLT td, chem;
+  // AFH_FLUX_MARCH=1 selects k_flux_march (measured slower on MI355X for
+  // S1-64: 4.24 ms vs 3.78 ms for k_flux per leaf level)
+  bool march = false;
 };
 
 extern "C" {
 
 int32_t afh_fluid_create(afh_tree *t, const afh_fluid_desc *d, afh_fluid **out) {
   if (!t || !d || !out) return set_error(AFH_ERR_ARG, "afh_fluid_create: null");
+  const char *march_env = getenv("AFH_FLUX_MARCH");
   if (d->n_species < 1 || d->n_species > MAXS || d->n_reactions < 0 ||
       d->n_reactions > AFH_MAX_REACTIONS)
     return set_error(AFH_ERR_ARG, "bad species/reaction count");
   if (d->td.n_points < 2 || d->td.n_cols < 2 || !d->td.rows_cols)
     return set_error(AFH_ERR_ARG, "transport table needs mobility + diffusion");
   afh_fluid *f = new afh_fluid();
+  f->march = march_env && atoi(march_env) != 0;
   f->t = t;
   f->d = *d;
   for (int s = 0; s < d->n_species; s++) {
@@ -797,17 +883,26 @@ int32_t afh_flux_upwind_tree(afh_fluid *f, int32_t s_deriv, double *dt_lim) {
   const int iv = f->d.i_electron + s_deriv;
   if (iv < 1 || iv > t->nvc) return set_error(AFH_ERR_ARG, "bad s_deriv");
   int32_t e;
-  // af_restrict_ref_boundary
-  const int nrb = t->refb.off[t->nlvl];
-  if ((e = restrict_boxes(t, t->refb.d, nrb, iv))) return e;
+  // af_restrict_ref_boundary (per level, for the sharding hook)
+  for (int l = t->nlvl; l >= 2; l--) {
+    if ((e = restrict_boxes(t, t->refb.at(l), t->refb.n(l), iv)) ||
+        (t->hook && (e = call_hook(t, AFH_HOOK_RESTRICT, l, iv))))
+      return e;
+  }
   // two ghost layers, level by level (coarse write-back before fine reads)
   for (int l = 1; l <= t->nlvl; l++) {
+    if ((e = call_hook(t, AFH_HOOK_HALO, l, iv))) return e;
     const int n = t->leaves.n(l);
-    if (!n) continue;
-    hipLaunchKernelGGL(k_gc2, dim3((nc * nc + 255) / 256, 6, n), dim3(256), 0,
-                       t->stream, t->ccv(iv), t->gc2, t->d_boxes,
-                       t->leaves.at(l), nc, t->bsz, t->gc_args(iv));
-    AFH_LAUNCH_CHECK("k_gc2");
+    if (n) {
+      hipLaunchKernelGGL(k_gc2, dim3((nc * nc + 255) / 256, 6, n), dim3(256),
+                         0, t->stream, t->ccv(iv), t->gc2, t->d_boxes,
+                         t->leaves.at(l), nc, t->bsz, t->gc_args(iv));
+      AFH_LAUNCH_CHECK("k_gc2");
+    }
+    // k_gc2 wrote the first ghost layer back into the boxes (coarse data of
+    // the next level's refinement boundaries)
+    if (t->lvl_rb_coarse[l - 1] && (e = call_hook(t, AFH_HOOK_RIMS, l, iv)))
+      return e;
   }
   if ((e = red_init(t, 0, -HUGE_VAL)) || (e = red_init(t, 1, -HUGE_VAL))) return e;
   auto *red = reinterpret_cast<unsigned long long *>(t->scratch);
@@ -826,7 +921,7 @@ int32_t afh_flux_upwind_tree(afh_fluid *f, int32_t s_deriv, double *dt_lim) {
     if (!n) continue;
     for (int q = 0; q < 3; q++) A.inv_dx[q] = 1 / t->lvl_dr[3 * (l - 1) + q];
     prof_begin(t, AFH_PROF_FLUX);
-    if (nc == 64 || nc == 32 || nc == 16 || nc == 8) {
+    if (f->march && (nc == 64 || nc == 32 || nc == 16 || nc == 8)) {
       switch (nc) {
       case 8: launch_flux_march<8>(t, A, l, red); break;
       case 16: launch_flux_march<16>(t, A, l, red); break;
@@ -834,10 +929,10 @@ int32_t afh_flux_upwind_tree(afh_fluid *f, int32_t s_deriv, double *dt_lim) {
       default: launch_flux_march<64>(t, A, l, red); break;
       }
     } else if (shfl)
-      hipLaunchKernelGGL(k_flux<true>, dim3((n3 + 255) / 256, n), dim3(256), 0,
+      hipLaunchKernelGGL(k_flux_staged<true>, dim3((n3 + 255) / 256, n), dim3(256), 0,
                          t->stream, A, t->leaves.at(l), nc, t->bsz, t->fsz, red);
     else
-      hipLaunchKernelGGL(k_flux<false>, dim3((n3 + 255) / 256, n), dim3(256), 0,
+      hipLaunchKernelGGL(k_flux_staged<false>, dim3((n3 + 255) / 256, n), dim3(256), 0,
                          t->stream, A, t->leaves.at(l), nc, t->bsz, t->fsz, red);
     // read n_e, |E|, 3 face fields; write 3 fluxes = 64 B/cell
     prof_end(t, AFH_PROF_FLUX, 64.0 * n3 * n);
@@ -850,9 +945,11 @@ int32_t afh_flux_upwind_tree(afh_fluid *f, int32_t s_deriv, double *dt_lim) {
                        t->cflux.d, nc, t->fsz);
     AFH_LAUNCH_CHECK("k_consistent");
   }
+  if ((e = call_hook(t, AFH_HOOK_CFLUX, 0, f->d.f_flux))) return e;
   if ((e = red_finish(t, 0, true)) || (e = red_finish(t, 1, true))) return e;
   double r[2];
-  if ((e = red_fetch(t, 0, 2, r))) return e;
+  if ((e = red_fetch(t, 0, 2, r)) || (e = call_hook(t, AFH_HOOK_MAX, 0, 0, r, 2)))
+    return e;
   const double cfl_max = r[0], sig_max = r[1];
   dt_lim[0] = 1 / cfl_max;
   dt_lim[1] = 8.8541878176e-12 / (1.6022e-19 * std::max(sig_max, 1e-100));
@@ -915,7 +1012,9 @@ int32_t afh_flux_update_densities(afh_fluid *f, double dt, int32_t s_deriv,
   }
   double r = 1e100;
   if (last_step) {
-    if ((e = red_finish(t, 2, false)) || (e = red_fetch(t, 2, 1, &r))) return e;
+    if ((e = red_finish(t, 2, false)) || (e = red_fetch(t, 2, 1, &r)) ||
+        (e = call_hook(t, AFH_HOOK_MIN, 0, 0, &r, 1)))
+      return e;
   } else {
     AFH_HIP(hipStreamSynchronize(t->stream));
   }

@@ -165,28 +165,74 @@ __global__ void k_gc_corners(double *__restrict__ v,
   }
 }
 
-int32_t gc_lvl_ptr(afh_tree *t, int lvl, double *v, const double *vc,
-                   const GcArgs &ga, int corners) {
-  const int n = t->ids.n(lvl);
-  if (n == 0) return AFH_OK;
-  const int nc = t->nc;
-  dim3 grid((nc * nc + 255) / 256, 6, n);
-  prof_begin(t, AFH_PROF_GHOST);
-  hipLaunchKernelGGL(k_gc_faces, grid, dim3(256), 0, t->stream, v, vc,
-                     t->d_boxes, t->ids.at(lvl), nc, t->bsz, ga);
-  // algorithmic bytes: read one interior layer + write one ghost layer
-  prof_end(t, AFH_PROF_GHOST, 16.0 * 6 * nc * nc * n);
-  AFH_LAUNCH_CHECK("k_gc_faces");
-  if (corners) {
-    hipLaunchKernelGGL(k_gc_corners, dim3(n), dim3(256), 0, t->stream, v,
-                       t->d_boxes, t->ids.at(lvl), nc, t->bsz);
-    AFH_LAUNCH_CHECK("k_gc_corners");
-  }
+int32_t call_hook(afh_tree *t, int kind, int lvl, int iv, double *vals, int n) {
+  if (!t->hook) return AFH_OK;
+  int32_t e = t->hook(t->hook_ctx, kind, lvl, iv, vals, n);
+  if (e) return set_error(AFH_ERR_STATE, "sharding hook %d failed (%d)", kind, e);
   return AFH_OK;
 }
 
-int32_t gc_lvl(afh_tree *t, int lvl, int iv, int corners) {
-  return gc_lvl_ptr(t, lvl, t->ccv(iv), t->ccv(iv), t->gc_args(iv), corners);
+int32_t gc_lvl_var(afh_tree *t, int lvl, int iv, const double *vc,
+                   const GcArgs &ga, int corners, bool rims) {
+  const int n = t->ids.n(lvl);
+  double *v = t->var(iv);
+  int32_t e;
+  if ((e = call_hook(t, AFH_HOOK_HALO, lvl, iv))) return e;
+  if (n > 0) {
+    const int nc = t->nc;
+    dim3 grid((nc * nc + 255) / 256, 6, n);
+    prof_begin(t, AFH_PROF_GHOST);
+    hipLaunchKernelGGL(k_gc_faces, grid, dim3(256), 0, t->stream, v, vc,
+                       t->d_boxes, t->ids.at(lvl), nc, t->bsz, ga);
+    // algorithmic bytes: read one interior layer + write one ghost layer
+    prof_end(t, AFH_PROF_GHOST, 16.0 * 6 * nc * nc * n);
+    AFH_LAUNCH_CHECK("k_gc_faces");
+    if (corners) {
+      hipLaunchKernelGGL(k_gc_corners, dim3(n), dim3(256), 0, t->stream, v,
+                         t->d_boxes, t->ids.at(lvl), nc, t->bsz);
+      AFH_LAUNCH_CHECK("k_gc_corners");
+    }
+  }
+  if (rims || t->lvl_rb_coarse[lvl - 1]) return call_hook(t, AFH_HOOK_RIMS, lvl, iv);
+  return AFH_OK;
+}
+
+int32_t gc_lvl(afh_tree *t, int lvl, int iv, int corners, bool rims) {
+  return gc_lvl_var(t, lvl, iv, t->ccv(iv), t->gc_args(iv), corners, rims);
+}
+
+// ------------------------------------------------------------ plans
+// Copy the cells of a list of box regions between a variable and a packed
+// buffer (region r at off[r], i fastest). One block row per region.
+__global__ void k_plan_copy(double *__restrict__ v, double *__restrict__ buf,
+                            const int32_t *__restrict__ reg,
+                            const int64_t *__restrict__ off, int ng, size_t bsz,
+                            int unpack) {
+  const int32_t *q = reg + 7 * blockIdx.y;
+  const int nx = q[4] - q[1] + 1, ny = q[5] - q[2] + 1, nz = q[6] - q[3] + 1;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nx * ny * nz) return;
+  const int i = q[1] + t % nx, j = q[2] + (t / nx) % ny, k = q[3] + t / (nx * ny);
+  double *c = v + (size_t)(q[0] - 1) * bsz + ix3(ng, i, j, k);
+  double *b = buf + off[blockIdx.y] + t;
+  if (unpack) *c = *b;
+  else *b = *c;
+}
+
+__global__ void k_plan_copy_fc(double *__restrict__ v, double *__restrict__ buf,
+                               const int32_t *__restrict__ reg,
+                               const int64_t *__restrict__ off, int nf,
+                               size_t fsz, int unpack) {
+  const int32_t *q = reg + 8 * blockIdx.y;
+  const int nx = q[5] - q[2] + 1, ny = q[6] - q[3] + 1, nz = q[7] - q[4] + 1;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nx * ny * nz) return;
+  const int i = q[2] + t % nx, j = q[3] + (t / nx) % ny, k = q[4] + t / (nx * ny);
+  double *c = v + (size_t)(q[0] - 1) * fsz + (size_t)q[1] * nf * nf * nf +
+              ((size_t)(k - 1) * nf + (j - 1)) * nf + (i - 1);
+  double *b = buf + off[blockIdx.y] + t;
+  if (unpack) *c = *b;
+  else *b = *c;
 }
 
 // ------------------------------------------------------------ restriction
@@ -366,18 +412,37 @@ int32_t afh_tree_create(const afh_tree_desc *d, int32_t device,
   t->h_ids = split(d->lvl_ids, d->lvl_ids_off);
   t->h_leaves = split(d->lvl_leaves, d->lvl_leaves_off);
   t->h_parents = split(d->lvl_parents, d->lvl_parents_off);
+  // grid spacing per level over ALL boxes of the topology (a sharded tree
+  // lists only this rank's boxes, possibly none on some level)
   t->lvl_dr.assign(3 * t->nlvl, 0.0);
+  std::vector<int> seen(t->nlvl, 0);
+  t->lvl_total.assign(t->nlvl, 0);
+  for (int id = 1; id <= t->nb; id++) {
+    const afh_box_meta &m = t->boxes[id - 1];
+    if (m.lvl < 1) continue;  // unused id
+    if (m.lvl > t->nlvl) return set_error(AFH_ERR_ARG, "box %d level %d", id, m.lvl);
+    const int l = m.lvl - 1;
+    for (int q = 0; q < 3; q++) {
+      if (!seen[l]) t->lvl_dr[3 * l + q] = m.dr[q];
+      if (memcmp(&m.dr[q], &t->lvl_dr[3 * l + q], sizeof(double)) != 0)
+        return set_error(AFH_ERR_UNSUPPORTED, "non-uniform dr on level %d", l + 1);
+    }
+    seen[l] = 1;
+    t->lvl_total[l]++;
+  }
+  t->lvl_rb_coarse.assign(t->nlvl, 0);
+  for (int id = 1; id <= t->nb; id++) {
+    const afh_box_meta &m = t->boxes[id - 1];
+    if (m.lvl < 2) continue;
+    for (int nb = 0; nb < 6; nb++)
+      if (m.neighbors[nb] == 0) t->lvl_rb_coarse[m.lvl - 2] = 1;
+  }
   for (int l = 0; l < t->nlvl; l++) {
-    if (t->h_ids[l].empty()) return set_error(AFH_ERR_ARG, "empty level %d", l + 1);
+    if (!seen[l]) return set_error(AFH_ERR_ARG, "empty level %d", l + 1);
     for (int32_t id : t->h_ids[l]) {
       if (id < 1 || id > t->nb) return set_error(AFH_ERR_ARG, "bad box id %d", id);
-      const afh_box_meta &m = t->boxes[id - 1];
-      if (m.lvl != l + 1) return set_error(AFH_ERR_ARG, "box %d level mismatch", id);
-      for (int q = 0; q < 3; q++) {
-        if (id == t->h_ids[l][0]) t->lvl_dr[3 * l + q] = m.dr[q];
-        if (memcmp(&m.dr[q], &t->lvl_dr[3 * l + q], sizeof(double)) != 0)
-          return set_error(AFH_ERR_UNSUPPORTED, "non-uniform dr on level %d", l + 1);
-      }
+      if (t->boxes[id - 1].lvl != l + 1)
+        return set_error(AFH_ERR_ARG, "box %d level mismatch", id);
     }
   }
   // derived task lists
@@ -457,13 +522,17 @@ int32_t afh_tree_destroy(afh_tree *t) {
   for (hipEvent_t e : t->ev_pool) hipEventDestroy(e);
   for (LevelList *L : {&t->ids, &t->leaves, &t->parents, &t->refb, &t->cflux})
     hipFree(L->d);
+  for (auto &p : t->plans) {
+    hipFree(p.d_reg);
+    hipFree(p.d_off);
+  }
   hipFree(t->d_boxes);
   hipFree(t->cc);
   hipFree(t->fc);
   hipFree(t->gc2);
   hipFree(t->scratch);
   hipHostFree(t->h_scratch);
-  hipStreamDestroy(t->stream);
+  if (t->own_stream) hipStreamDestroy(t->stream);
   delete t;
   return AFH_OK;
 }
@@ -556,7 +625,7 @@ int32_t afh_restrict_tree(afh_tree *t, int32_t iv) {
   // levels highest..2, coarsest last
   for (int l = t->nlvl; l >= 2; l--) {
     int32_t e = restrict_boxes(t, t->ids.at(l), t->ids.n(l), iv);
-    if (e) return e;
+    if (e || (e = call_hook(t, AFH_HOOK_RESTRICT, l, iv))) return e;
   }
   return AFH_OK;
 }
@@ -583,8 +652,102 @@ int32_t afh_tree_maxabs_cc(afh_tree *t, int32_t iv, double *out) {
                        t->ccv(iv), t->leaves.at(l), nc, t->bsz, d);
     AFH_LAUNCH_CHECK("k_maxabs");
   }
-  if ((e = red_finish(t, 3, true))) return e;
-  return red_fetch(t, 3, 1, out);
+  if ((e = red_finish(t, 3, true)) || (e = red_fetch(t, 3, 1, out))) return e;
+  return call_hook(t, AFH_HOOK_MAX, 0, iv, out, 1);
+}
+
+int32_t afh_tree_set_stream(afh_tree *t, void *stream) {
+  if (!t) return set_error(AFH_ERR_ARG, "null tree");
+  AFH_HIP(hipStreamSynchronize(t->stream));
+  if (t->own_stream) AFH_HIP(hipStreamDestroy(t->stream));
+  t->stream = (hipStream_t)stream;
+  t->own_stream = false;
+  return AFH_OK;
+}
+
+int32_t afh_tree_set_hook(afh_tree *t, afh_hook_fn fn, void *ctx) {
+  if (!t) return set_error(AFH_ERR_ARG, "null tree");
+  t->hook = fn;
+  t->hook_ctx = ctx;
+  return AFH_OK;
+}
+
+static int32_t plan_create(afh_tree *t, const int32_t *reg, int32_t n,
+                           int32_t *plan, int64_t *n_values, int fc) {
+  if (!t || n < 0 || (n > 0 && !reg) || !plan || !n_values)
+    return set_error(AFH_ERR_ARG, "afh_plan_create: bad argument");
+  if (n > 65535) return set_error(AFH_ERR_UNSUPPORTED, "more than 65535 regions");
+  const int w = fc ? 8 : 7, lo = fc ? 2 : 1;
+  const int vmin = fc ? 1 : 0, vmax = t->nc + 1;
+  afh_tree::Plan p;
+  p.n = n;
+  p.fc = fc;
+  std::vector<int64_t> off(n + 1, 0);
+  for (int r = 0; r < n; r++) {
+    const int32_t *q = reg + w * r;
+    if (q[0] < 1 || q[0] > t->nb) return set_error(AFH_ERR_ARG, "plan: bad box id");
+    if (fc && (q[1] < 0 || q[1] > 2)) return set_error(AFH_ERR_ARG, "plan: bad dim");
+    int64_t cells = 1;
+    for (int d = 0; d < 3; d++) {
+      if (q[lo + d] < vmin || q[lo + 3 + d] > vmax || q[lo + 3 + d] < q[lo + d])
+        return set_error(AFH_ERR_ARG, "plan: bad region");
+      cells *= q[lo + 3 + d] - q[lo + d] + 1;
+    }
+    off[r + 1] = off[r] + cells;
+    p.max_cells = std::max(p.max_cells, (int)cells);
+  }
+  p.n_values = off[n];
+  AFH_HIP(hipMalloc(&p.d_reg, sizeof(int32_t) * w * std::max(n, 1)));
+  AFH_HIP(hipMalloc(&p.d_off, sizeof(int64_t) * (n + 1)));
+  if (n > 0)
+    AFH_HIP(hipMemcpy(p.d_reg, reg, sizeof(int32_t) * w * n, hipMemcpyHostToDevice));
+  AFH_HIP(hipMemcpy(p.d_off, off.data(), sizeof(int64_t) * (n + 1),
+                    hipMemcpyHostToDevice));
+  t->plans.push_back(p);
+  *plan = (int32_t)t->plans.size() - 1;
+  *n_values = p.n_values;
+  return AFH_OK;
+}
+
+int32_t afh_plan_create(afh_tree *t, const int32_t *reg, int32_t n,
+                        int32_t *plan, int64_t *n_values) {
+  return plan_create(t, reg, n, plan, n_values, 0);
+}
+
+int32_t afh_plan_create_fc(afh_tree *t, const int32_t *reg, int32_t n,
+                           int32_t *plan, int64_t *n_values) {
+  return plan_create(t, reg, n, plan, n_values, 1);
+}
+
+static int32_t plan_copy(afh_tree *t, int32_t plan, int32_t iv, double *buf,
+                         int unpack) {
+  if (!t || plan < 0 || plan >= (int)t->plans.size())
+    return set_error(AFH_ERR_ARG, "afh_plan_pack/unpack: bad plan");
+  const afh_tree::Plan &p = t->plans[plan];
+  if (p.fc ? (iv < 1 || iv > t->nvf) : (iv < 0 || iv > t->nvc || (iv == 0 && !t->alt)))
+    return set_error(AFH_ERR_ARG, "afh_plan_pack/unpack: bad variable");
+  if (p.n == 0) return AFH_OK;
+  if (p.fc) {
+    hipLaunchKernelGGL(k_plan_copy_fc, dim3((p.max_cells + 255) / 256, p.n),
+                       dim3(256), 0, t->stream, t->fcv(iv), buf, p.d_reg, p.d_off,
+                       t->nc + 1, t->fsz, unpack);
+    AFH_LAUNCH_CHECK("k_plan_copy_fc");
+    return AFH_OK;
+  }
+  hipLaunchKernelGGL(k_plan_copy, dim3((p.max_cells + 255) / 256, p.n), dim3(256),
+                     0, t->stream, t->var(iv), buf, p.d_reg, p.d_off, t->ng,
+                     t->bsz, unpack);
+  AFH_LAUNCH_CHECK("k_plan_copy");
+  return AFH_OK;
+}
+
+int32_t afh_plan_pack(afh_tree *t, int32_t plan, int32_t iv, double *buf) {
+  return plan_copy(t, plan, iv, buf, 0);
+}
+
+int32_t afh_plan_unpack(afh_tree *t, int32_t plan, int32_t iv,
+                        const double *buf) {
+  return plan_copy(t, plan, iv, const_cast<double *>(buf), 1);
 }
 
 }  // extern "C"

@@ -12,9 +12,13 @@ of 64^3 cells (134 M leaf cells, 585 boxes, 4 levels, 64^3 coarse grid),
 16 mm cube, electrons + M+ + M- (td_air_siglo_swarm.txt old-style model),
 Gaussian seed, -2.5 MV/m background field. Synthetic data, FP64.
 
-Multi-GPU (torchrun, one rank per GPU): every rank advances its own replica
-of the workload (no data-path collective; scaling "weak"); a barrier brackets
-the timed region and the time is the max over ranks.
+Multi-GPU (torchrun, one rank per GPU): the SAME tree is sharded over the
+ranks (afh.dist: Morton-ordered subtrees of the coarsest level with a box per
+rank, coarser levels replicated; halo / restriction / consistent-flux
+exchanges with RCCL on the tree's stream, all-reduced time-step limits), so
+the per-GPU work shrinks as N grows ("scaling": "strong"). A barrier
+brackets the timed region and the time is the max over ranks. `--replicas`
+runs one independent copy of the workload per GPU instead ("weak").
 """
 import argparse
 import json
@@ -36,7 +40,8 @@ CONFIGS = {
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E peak (spec)
 
 
-def build_case(lib, config, device, coarse_cycles):
+def build_case(lib, config, device, coarse_cycles, shard_ranks=None):
+    """shard_ranks = (world, rank): this rank's part of the sharded tree."""
     from afh.streamer import StreamerCase, seed_state, tables_from
     from afh.tree import uniform_tree
     import golden
@@ -45,8 +50,13 @@ def build_case(lib, config, device, coarse_cycles):
     g = golden.load("uni8")  # transport/chemistry tables exported from the reference
     td, chem = tables_from(g)
     voltage = -dom[2] * (-2.5e6)
+    shard = None
+    if shard_ranks is not None:
+        from afh.dist import Partition, Shard
+        world, rank = shard_ranks
+        shard = Shard(Partition(topo, world), rank, "nccl", device="cuda:%d" % device)
     case = StreamerCase(lib, topo, td, chem, voltage, coarse_cycles=coarse_cycles,
-                        device=device)
+                        device=device, shard=shard)
     seed_state(case, width=0.05 * dom[2])
     return case
 
@@ -110,6 +120,8 @@ def main():
     ap.add_argument("--config", default="s1-64", choices=sorted(CONFIGS))
     ap.add_argument("--coarse-cycles", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--replicas", action="store_true",
+                    help="N>1: one independent replica per GPU instead of sharding")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -125,9 +137,11 @@ def main():
 
     from afh import capi
     lib = capi.hip_library()
-    case = build_case(lib, args.config, local, args.coarse_cycles)
+    sharded = world > 1 and not args.replicas
+    case = build_case(lib, args.config, local, args.coarse_cycles,
+                      (world, rank) if sharded else None)
     from afh.streamer import cells
-    ncell = cells(case.topo)
+    ncell = cells(case.topo)  # leaf cells of the whole tree
     dt = 1e-13
 
     case.field_compute(0, n_vcycles=2)  # initial potential (untimed)
@@ -168,22 +182,23 @@ def main():
         achieved = bytes_per_launch / avg_s / 1e9 if avg_s > 0 else 0.0
         out = {
             "metric": "cell-updates/s (fluid+MG V-cycle)",
-            "value": ncell * args.steps * world / elapsed,
+            "value": ncell * args.steps * (1 if sharded else world) / elapsed,
             "unit": "cell-updates/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": 1e3 * elapsed / args.steps,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if sharded else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic",
             "config": {"workload": args.config, "n_cell": CONFIGS[args.config][0],
-                       "leaf_cells_per_gpu": ncell, "boxes": int(case.topo["n_boxes"]),
+                       "leaf_cells": ncell, "boxes": int(case.topo["n_boxes"]),
                        "levels": int(case.topo["highest_lvl"]),
                        "coarse_cycles": args.coarse_cycles,
-                       "parallelism": "replica-per-gpu"},
+                       "parallelism": ("box-shard-%d" % world) if sharded else
+                       ("replica-per-gpu" if world > 1 else "single-gpu")},
             "roofline": {"bound": "hbm",
                          "kernel": "k_gsrb_pair<%d>" % CONFIGS[args.config][0],
                          "achieved": achieved, "peak": HBM_PEAK_GBS,
@@ -194,7 +209,9 @@ def main():
                          "launches": nl.value},
             "last_residual": last[0][-1] if last[0] else None,
         }
-        if not args.no_cpu_baseline:
+        if sharded:
+            out["exchanges_per_step"] = case.shard.n_exchanges / max(1, args.steps + args.warmup + 1)
+        if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(args.config)
         print(json.dumps(out))
     if dist is not None:

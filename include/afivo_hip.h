@@ -241,6 +241,59 @@ int32_t afh_profile_enable(afh_tree *t, int32_t kclass);
 int32_t afh_profile_read(afh_tree *t, double *total_ms, int64_t *launches,
                          double *bytes);
 
+/* ---------------------------------------------------------------------------
+ * Box sharding. A sharded run creates on every rank a tree
+ * whose afh_tree_desc holds the WHOLE topology in `boxes` but only the boxes
+ * this rank computes in the level lists (lvl_ids / lvl_leaves /
+ * lvl_parents); storage is allocated for every box, and the boxes of other
+ * ranks are replicas that are valid only where an exchange refreshed them.
+ * The library calls the hook below at every point where a replica is read
+ * after its owner wrote it; the host side performs the exchange with
+ * afh_plan_pack / afh_plan_unpack and its collective library (RCCL via
+ * torch.distributed on the GPU, gloo in the CPU tests).
+ *
+ * Hook kinds (level = tree level, iv = cc variable, 0 = the smoother's spare
+ * image of phi):
+ *   AFH_HOOK_HALO      owned boxes of `level` wrote iv: refresh the replicas
+ *                      other ranks read (interior cells next to owned boxes);
+ *                      called before every ghost-cell fill of the level
+ *   AFH_HOOK_RIMS      after the ghost-cell fill: refresh replicas' ghost
+ *                      cells read by the neighbour recomputation of the fused
+ *                      smoother and by refinement-boundary interpolation
+ *   AFH_HOOK_RESTRICT  owned boxes of `level` restricted iv into their
+ *                      parents (level-1)
+ *   AFH_HOOK_MAX/MIN   reduce vals[0..n-1] over all ranks, in place
+ * A hook returns 0 on success. With no hook set (single rank) no call is
+ * made. */
+#define AFH_HOOK_HALO 1
+#define AFH_HOOK_RIMS 2
+#define AFH_HOOK_RESTRICT 3
+#define AFH_HOOK_MAX 4
+#define AFH_HOOK_MIN 5
+#define AFH_HOOK_CFLUX 6 /* af_consistent_fluxes wrote face fluxes of
+                            neighbouring leaves (iv = face variable) */
+typedef int32_t (*afh_hook_fn)(void *ctx, int32_t kind, int32_t level,
+                               int32_t iv, double *vals, int32_t n);
+int32_t afh_tree_set_hook(afh_tree *t, afh_hook_fn fn, void *ctx);
+/* Order the tree's device work on a caller-owned HIP stream (e.g. the
+ * stream the collective library uses), so that exchanges need no host
+ * synchronisation. The library no longer destroys the stream. */
+int32_t afh_tree_set_stream(afh_tree *t, void *hip_stream);
+
+/* A plan is a list of box regions: n x 7 int32 (box id, lo[3], hi[3]; cell
+ * indices 0..nc+1, inclusive). afh_plan_pack copies variable iv of the
+ * regions, in order, i fastest, into buf (device memory for libafivo_hip);
+ * afh_plan_unpack copies back. Both are ordered on the tree's stream. */
+int32_t afh_plan_create(afh_tree *t, const int32_t *regions, int32_t n,
+                        int32_t *plan, int64_t *n_values);
+/* Face-variable plan: n x 8 int32 (box id, dim 0..2, lo[3], hi[3]; face
+ * indices 1..nc+1 of box%fc(:,:,:,dim+1,ivf)); pack/unpack take ivf. */
+int32_t afh_plan_create_fc(afh_tree *t, const int32_t *regions, int32_t n,
+                           int32_t *plan, int64_t *n_values);
+int32_t afh_plan_pack(afh_tree *t, int32_t plan, int32_t iv, double *buf);
+int32_t afh_plan_unpack(afh_tree *t, int32_t plan, int32_t iv,
+                        const double *buf);
+
 #ifdef __cplusplus
 }
 #endif

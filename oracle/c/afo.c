@@ -40,7 +40,21 @@ struct afh_tree {
   int cgs[3];
   double *cc, *fc;
   cc_method *meth; /* n_var_cell entries */
+  /* box sharding (afo_tree_set_hook, afo_plan_*) */
+  afh_hook_fn hook;
+  void *hook_ctx;
+  int nplans;
+  struct afo_plan {
+    int n, fc;
+    int32_t *reg;
+    int64_t *off;
+  } *plans;
 };
+
+static int32_t hook(afh_tree *t, int kind, int lvl, int iv, double *vals, int n) {
+  if (!t->hook) return AFH_OK;
+  return t->hook(t->hook_ctx, kind, lvl, iv, vals, n) ? AFH_ERR_STATE : AFH_OK;
+}
 
 struct afh_mg {
   afh_tree *t;
@@ -158,6 +172,8 @@ int32_t afo_tree_destroy(afh_tree *t) {
   free(t->ids), free(t->ids_off), free(t->leaves), free(t->leaves_off);
   free(t->parents), free(t->parents_off);
   free(t->cc), free(t->fc), free(t->meth);
+  for (int q = 0; q < t->nplans; q++) free(t->plans[q].reg), free(t->plans[q].off);
+  free(t->plans);
   free(t);
   return AFH_OK;
 }
@@ -446,17 +462,20 @@ static void gc_box(afh_tree *t, int id, int iv, int corners) {
   if (corners) gc_box_corner(t, id, iv);
 }
 
-static void gc_lvl(afh_tree *t, int lvl, int iv, int corners) {
+/* af_gc_lvl; with sharding hooks (replicas refreshed before, their ghost
+ * cells after) */
+static int32_t gc_lvl(afh_tree *t, int lvl, int iv, int corners) {
   int n = LVL_N(t, ids, lvl);
+  if (hook(t, AFH_HOOK_HALO, lvl, iv, NULL, 0)) return AFH_ERR_STATE;
 #pragma omp parallel for schedule(static)
   for (int i = 0; i < n; i++) gc_box(t, LVL_AT(t, ids, lvl, i), iv, corners);
+  return hook(t, AFH_HOOK_RIMS, lvl, iv, NULL, 0);
 }
 
 int32_t afo_gc_lvl(afh_tree *t, int32_t lvl, int32_t iv, int32_t corners) {
   if (lvl < 1 || lvl > t->nlvl || iv < 1 || iv > t->nvc || !t->meth[iv].set)
     return fail(AFH_ERR_ARG, "afo_gc_lvl: bad argument / no methods");
-  gc_lvl(t, lvl, iv, corners);
-  return AFH_OK;
+  return gc_lvl(t, lvl, iv, corners);
 }
 int32_t afo_gc_tree(afh_tree *t, int32_t iv, int32_t corners) {
   for (int l = 1; l <= t->nlvl; l++) {
@@ -502,6 +521,7 @@ int32_t afo_restrict_tree(afh_tree *t, int32_t iv) {
         if (cid > 0) restrict_box(t, cid, id, iv);
       }
     }
+    if (hook(t, AFH_HOOK_RESTRICT, l + 1, iv, NULL, 0)) return AFH_ERR_STATE;
   }
   return AFH_OK;
 }
@@ -526,7 +546,7 @@ int32_t afo_tree_maxabs_cc(afh_tree *t, int32_t iv, double *out) {
           }
     }
   *out = mx;
-  return AFH_OK;
+  return hook(t, AFH_HOOK_MAX, 0, iv, out, 1);
 }
 
 /* ------------------------------------------------------------ multigrid */
@@ -615,7 +635,7 @@ int32_t afo_mg_gsrb_boxes(afh_mg *mg, int32_t lvl, int32_t up) {
     for (int i = 0; i < nid; i++)
       gsrb_357(t, LVL_AT(t, ids, lvl, i), cf, n, mg->d.i_phi, mg->d.i_rhs);
     int use_corners = up && n == 2 * n_cycle;
-    gc_lvl(t, lvl, mg->d.i_phi, use_corners);
+    if (gc_lvl(t, lvl, mg->d.i_phi, use_corners)) return AFH_ERR_STATE;
   }
   return AFH_OK;
 }
@@ -642,7 +662,10 @@ int32_t afo_mg_update_coarse(afh_mg *mg, int32_t lvl) {
     free(save);
   }
   (void)nc;
-  gc_lvl(t, lvl - 1, i_phi, 1);
+  if (hook(t, AFH_HOOK_RESTRICT, lvl, i_phi, NULL, 0) ||
+      hook(t, AFH_HOOK_RESTRICT, lvl, i_tmp, NULL, 0) ||
+      gc_lvl(t, lvl - 1, i_phi, 1))
+    return AFH_ERR_STATE;
   int np = LVL_N(t, parents, lvl - 1);
   const double *cf = lvl_coeffs(mg, lvl - 1);
 #pragma omp parallel for schedule(static)
@@ -886,7 +909,7 @@ int32_t afo_mg_solve_coarse(afh_mg *mg) {
         for (int i = 1; i <= nc; i++)
           p[IX(t, i, j, k)] = mg->u[0][GIX(mg, 0, o[0] + i, o[1] + j, o[2] + k)];
   }
-  gc_lvl(t, 1, mg->d.i_phi, 1);
+  if (gc_lvl(t, 1, mg->d.i_phi, 1)) return AFH_ERR_STATE;
   return AFH_OK;
 }
 
@@ -956,14 +979,14 @@ int32_t afo_mg_fas_vcycle(afh_mg *mg, int32_t set_residual, int32_t hl) {
   afh_tree *t = mg->t;
   int max_lvl = (hl > 0) ? hl : t->nlvl;
   for (int lvl = max_lvl; lvl >= 2; lvl--) {
-    afo_mg_gsrb_boxes(mg, lvl, 0);
-    afo_mg_update_coarse(mg, lvl);
+    if (afo_mg_gsrb_boxes(mg, lvl, 0) || afo_mg_update_coarse(mg, lvl))
+      return AFH_ERR_STATE;
   }
-  afo_mg_solve_coarse(mg);
+  if (afo_mg_solve_coarse(mg)) return AFH_ERR_STATE;
   for (int lvl = 2; lvl <= max_lvl; lvl++) {
     afo_mg_correct_children(mg, lvl);
-    gc_lvl(t, lvl, mg->d.i_phi, 1);
-    afo_mg_gsrb_boxes(mg, lvl, 1);
+    if (gc_lvl(t, lvl, mg->d.i_phi, 1) || afo_mg_gsrb_boxes(mg, lvl, 1))
+      return AFH_ERR_STATE;
   }
   if (set_residual) {
     for (int lvl = 1; lvl <= max_lvl; lvl++) {
@@ -1324,8 +1347,8 @@ static void flux_box(afh_fluid *fl, int id, int s_deriv, double *cfl_max,
 }
 
 /* af_restrict_ref_boundary, m_af_restrict.f90:140-161 */
-static void restrict_ref_boundary(afh_tree *t, int iv) {
-  for (int l = 1; l <= t->nlvl; l++) {
+static int32_t restrict_ref_boundary(afh_tree *t, int iv) {
+  for (int l = t->nlvl; l >= 2; l--) {
     int n = LVL_N(t, leaves, l);
     for (int q = 0; q < n; q++) {
       int id = LVL_AT(t, leaves, l, q), p_id = B(t, id)->parent;
@@ -1333,7 +1356,9 @@ static void restrict_ref_boundary(afh_tree *t, int iv) {
       for (int nb = 0; nb < 6; nb++) any |= (B(t, id)->neighbors[nb] == 0);
       if (p_id > 0 && any) restrict_box(t, id, p_id, iv);
     }
+    if (hook(t, AFH_HOOK_RESTRICT, l, iv, NULL, 0)) return AFH_ERR_STATE;
   }
+  return AFH_OK;
 }
 
 /* af_consistent_fluxes / flux_from_children, m_af_core.f90:1257-1402 */
@@ -1381,10 +1406,12 @@ static void consistent_fluxes(afh_tree *t, int f_ix) {
 int32_t afo_flux_upwind_tree(afh_fluid *f, int32_t s_deriv, double *dt_lim) {
   afh_tree *t = f->t;
   int nc = t->nc;
-  restrict_ref_boundary(t, f->d.i_electron + s_deriv);
+  if (restrict_ref_boundary(t, f->d.i_electron + s_deriv)) return AFH_ERR_STATE;
   double cfl_max = -HUGE_VAL, sig_max = -HUGE_VAL;
   for (int l = 1; l <= t->nlvl; l++) {
     int n = LVL_N(t, leaves, l);
+    if (hook(t, AFH_HOOK_HALO, l, f->d.i_electron + s_deriv, NULL, 0))
+      return AFH_ERR_STATE;
 #pragma omp parallel
     {
       double *cc2 = malloc(sizeof(double) * (size_t)(nc + 4) * (nc + 4) * (nc + 4));
@@ -1404,8 +1431,18 @@ int32_t afo_flux_upwind_tree(afh_fluid *f, int32_t s_deriv, double *dt_lim) {
       }
       free(cc2), free(cfl);
     }
+    /* the boxes' first ghost layer was written back (gc2) */
+    if (hook(t, AFH_HOOK_RIMS, l, f->d.i_electron + s_deriv, NULL, 0))
+      return AFH_ERR_STATE;
   }
   consistent_fluxes(t, f->d.f_flux);
+  if (hook(t, AFH_HOOK_CFLUX, 0, f->d.f_flux, NULL, 0)) return AFH_ERR_STATE;
+  {
+    double r[2] = {cfl_max, sig_max};
+    if (hook(t, AFH_HOOK_MAX, 0, 0, r, 2)) return AFH_ERR_STATE;
+    cfl_max = r[0];
+    sig_max = r[1];
+  }
   /* dt_lim(1) = min over boxes of 1/maxval(cfl_sum) = 1/max(cfl_sum);
    * other_dt(1) = eps0/(e*max(maxval(sigma),1e-100)) minimised over lines */
   dt_lim[0] = 1 / cfl_max;
@@ -1512,6 +1549,7 @@ int32_t afo_flux_update_densities(afh_fluid *fl, double dt, int32_t s_deriv,
           }
     }
   }
+  if (last_step && hook(t, AFH_HOOK_MIN, 0, 0, &chem_min, 1)) return AFH_ERR_STATE;
   dt_lim[0] = last_step ? chem_min : 1e100;
   dt_lim[1] = 1e100;
   return AFH_OK;
@@ -1526,4 +1564,103 @@ int32_t afo_profile_read(afh_tree *t, double *ms, int64_t *n, double *bytes) {
   (void)t;
   *ms = 0, *n = 0, *bytes = 0;
   return AFH_OK;
+}
+
+/* ---------------------------------------------------------------- sharding
+ * Host-side plans: copy the cells of box regions (id, lo[3], hi[3]) between
+ * a variable and a packed buffer, i fastest, regions in order. */
+int32_t afo_tree_set_stream(afh_tree *t, void *stream) {
+  (void)t, (void)stream; /* host library: nothing to order */
+  return AFH_OK;
+}
+
+int32_t afo_tree_set_hook(afh_tree *t, afh_hook_fn fn, void *ctx) {
+  t->hook = fn;
+  t->hook_ctx = ctx;
+  return AFH_OK;
+}
+
+static int32_t plan_create(afh_tree *t, const int32_t *reg, int32_t n,
+                           int32_t *plan, int64_t *n_values, int fc) {
+  if (n < 0 || (n > 0 && !reg) || !plan || !n_values)
+    return fail(AFH_ERR_ARG, "afo_plan_create: bad argument");
+  int w = fc ? 8 : 7, lo = fc ? 2 : 1, vmin = fc ? 1 : 0;
+  struct afo_plan p;
+  p.n = n;
+  p.fc = fc;
+  p.reg = malloc(sizeof(int32_t) * w * (n > 0 ? n : 1));
+  p.off = malloc(sizeof(int64_t) * (n + 1));
+  p.off[0] = 0;
+  for (int r = 0; r < n; r++) {
+    const int32_t *q = reg + w * r;
+    if (q[0] < 1 || q[0] > t->nb) return fail(AFH_ERR_ARG, "plan: bad box id");
+    if (fc && (q[1] < 0 || q[1] > 2)) return fail(AFH_ERR_ARG, "plan: bad dim");
+    int64_t cells = 1;
+    for (int d = 0; d < 3; d++) {
+      if (q[lo + d] < vmin || q[lo + 3 + d] > t->nc + 1 || q[lo + 3 + d] < q[lo + d])
+        return fail(AFH_ERR_ARG, "plan: bad region");
+      cells *= q[lo + 3 + d] - q[lo + d] + 1;
+    }
+    p.off[r + 1] = p.off[r] + cells;
+  }
+  if (n > 0) memcpy(p.reg, reg, sizeof(int32_t) * w * n);
+  t->plans = realloc(t->plans, sizeof(struct afo_plan) * (t->nplans + 1));
+  t->plans[t->nplans] = p;
+  *plan = t->nplans++;
+  *n_values = p.off[n];
+  return AFH_OK;
+}
+
+int32_t afo_plan_create(afh_tree *t, const int32_t *reg, int32_t n,
+                        int32_t *plan, int64_t *n_values) {
+  return plan_create(t, reg, n, plan, n_values, 0);
+}
+
+int32_t afo_plan_create_fc(afh_tree *t, const int32_t *reg, int32_t n,
+                           int32_t *plan, int64_t *n_values) {
+  return plan_create(t, reg, n, plan, n_values, 1);
+}
+
+static int32_t plan_copy(afh_tree *t, int32_t plan, int32_t iv, double *buf,
+                         int unpack) {
+  if (plan < 0 || plan >= t->nplans)
+    return fail(AFH_ERR_ARG, "afo_plan_pack/unpack: bad plan");
+  struct afo_plan *p = &t->plans[plan];
+  if (p->fc) {
+    if (iv < 1 || iv > t->nvf) return fail(AFH_ERR_ARG, "plan: bad variable");
+    for (int r = 0; r < p->n; r++) {
+      const int32_t *q = p->reg + 8 * r;
+      double *c = fcb(t, iv, q[0]), *b = buf + p->off[r];
+      for (int k = q[4]; k <= q[7]; k++)
+        for (int j = q[3]; j <= q[6]; j++)
+          for (int i = q[2]; i <= q[5]; i++) {
+            if (unpack) c[FX(t, q[1], i, j, k)] = *b;
+            else *b = c[FX(t, q[1], i, j, k)];
+            b++;
+          }
+    }
+    return AFH_OK;
+  }
+  if (iv < 1 || iv > t->nvc) return fail(AFH_ERR_ARG, "plan: bad variable");
+  for (int r = 0; r < p->n; r++) {
+    const int32_t *q = p->reg + 7 * r;
+    double *c = ccb(t, iv, q[0]), *b = buf + p->off[r];
+    for (int k = q[3]; k <= q[6]; k++)
+      for (int j = q[2]; j <= q[5]; j++)
+        for (int i = q[1]; i <= q[4]; i++) {
+          if (unpack) c[IX(t, i, j, k)] = *b;
+          else *b = c[IX(t, i, j, k)];
+          b++;
+        }
+  }
+  return AFH_OK;
+}
+
+int32_t afo_plan_pack(afh_tree *t, int32_t plan, int32_t iv, double *buf) {
+  return plan_copy(t, plan, iv, buf, 0);
+}
+
+int32_t afo_plan_unpack(afh_tree *t, int32_t plan, int32_t iv,
+                        const double *buf) {
+  return plan_copy(t, plan, iv, (double *)buf, 1);
 }

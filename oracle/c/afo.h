@@ -57,6 +57,15 @@ int32_t afo_flux_update_densities(afh_fluid *f, double dt, int32_t s_deriv,
 int32_t afo_profile_enable(afh_tree *t, int32_t kclass);
 int32_t afo_profile_read(afh_tree *t, double *total_ms, int64_t *launches,
                          double *bytes);
+int32_t afo_tree_set_hook(afh_tree *t, afh_hook_fn fn, void *ctx);
+int32_t afo_tree_set_stream(afh_tree *t, void *hip_stream);
+int32_t afo_plan_create(afh_tree *t, const int32_t *regions, int32_t n,
+                        int32_t *plan, int64_t *n_values);
+int32_t afo_plan_create_fc(afh_tree *t, const int32_t *regions, int32_t n,
+                           int32_t *plan, int64_t *n_values);
+int32_t afo_plan_pack(afh_tree *t, int32_t plan, int32_t iv, double *buf);
+int32_t afo_plan_unpack(afh_tree *t, int32_t plan, int32_t iv,
+                        const double *buf);
 /* Debug hooks: the individual V-cycle stages (for golden trace tests). */
 int32_t afo_mg_gsrb_boxes(afh_mg *mg, int32_t lvl, int32_t up);
 int32_t afo_mg_update_coarse(afh_mg *mg, int32_t lvl);
