@@ -110,6 +110,7 @@ SIGNATURES = {
     "mg_create": (i32, [_VP, C.POINTER(MgDesc), _PVP]),
     "mg_destroy": (i32, [_VP]),
     "mg_fas_vcycle": (i32, [_VP, i32, i32]),
+    "mg_fas_fmg": (i32, [_VP, i32, i32]),
     "mg_compute_phi_gradient": (i32, [_VP, i32, f64, i32]),
     "fluid_create": (i32, [_VP, C.POINTER(FluidDesc), _PVP]),
     "fluid_destroy": (i32, [_VP]),

@@ -170,6 +170,10 @@ class Multigrid:
     def fas_vcycle(self, set_residual=True, highest_lvl=0):
         self.lib.call("mg_fas_vcycle", self.h, int(set_residual), highest_lvl)
 
+    def fas_fmg(self, set_residual=True, have_guess=True):
+        """mg_fas_fmg (m_af_multigrid.f90:137-180)."""
+        self.lib.call("mg_fas_fmg", self.h, int(set_residual), int(have_guess))
+
     def compute_phi_gradient(self, i_fc, fac=-1.0, i_norm=0):
         self.lib.call("mg_compute_phi_gradient", self.h, i_fc, fac, i_norm)
 

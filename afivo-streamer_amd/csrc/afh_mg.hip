@@ -385,6 +385,17 @@ __global__ void k_corr_tmp(const double *__restrict__ phi,
   tmp[o] = phi[o] - tmp[o];
 }
 
+// FMG box operations over whole (nc+2)^3 arrays: af_box_clear_cc (src null)
+// and af_boxes_copy_cc (m_af_utils.f90)
+__global__ void k_box_copy(const double *__restrict__ src,
+                           double *__restrict__ dst,
+                           const int32_t *__restrict__ ids, size_t bsz) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= bsz) return;
+  const size_t o = (size_t)(ids[blockIdx.y] - 1) * bsz + t;
+  dst[o] = src ? src[o] : 0.0;
+}
+
 __global__ void k_prolong(double *__restrict__ phi,
                           const double *__restrict__ tmp,
                           const afh_box_meta *__restrict__ meta,
@@ -1120,6 +1131,50 @@ static int32_t solve_coarse(afh_mg *mg) {
                      t->ids.at(1), nc, t->bsz);
   AFH_LAUNCH_CHECK("k_cs_scatter");
   return gc_lvl(t, 1, mg->d.i_phi, 1);
+}
+
+static int32_t box_copy(afh_tree *t, int lvl, const double *src, double *dst) {
+  const int n = t->ids.n(lvl);
+  if (!n) return AFH_OK;
+  hipLaunchKernelGGL(k_box_copy, dim3((unsigned)((t->bsz + 255) / 256), n),
+                     dim3(256), 0, t->stream, src, dst, t->ids.at(lvl), t->bsz);
+  AFH_LAUNCH_CHECK("k_box_copy");
+  return AFH_OK;
+}
+
+// mg_fas_fmg (m_af_multigrid.f90:137-180) with set_coarse_phi_rhs (742-776)
+// and init_phi_rhs (779-799). set_coarse_phi_rhs is update_coarse without
+// restoring tmp; update_coarse's extra tmp = phi on the parents is
+// overwritten by the phi -> tmp copies below before tmp is read again.
+int32_t afh_mg_fas_fmg(afh_mg *mg, int32_t set_residual, int32_t have_guess) {
+  if (!mg) return set_error(AFH_ERR_ARG, "null mg");
+  afh_tree *t = mg->t;
+  const int nl = t->nlvl, i_phi = mg->d.i_phi;
+  double *phi = t->ccv(i_phi), *tmp = t->ccv(mg->d.i_tmp);
+  int32_t e;
+  if (have_guess) {
+    for (int lvl = nl; lvl >= 2; lvl--) {
+      if (lvl == nl && (e = gc_lvl(t, lvl, i_phi, 1, fused_level(mg, lvl)))) return e;
+      if ((e = update_coarse(mg, lvl))) return e;
+    }
+  } else {
+    for (int lvl = nl; lvl >= 2; lvl--) {
+      if ((e = box_copy(t, lvl, nullptr, phi)) ||
+          (e = restrict_boxes(t, t->ids.at(lvl), t->ids.n(lvl), mg->d.i_rhs)) ||
+          (e = call_hook(t, AFH_HOOK_RESTRICT, lvl, mg->d.i_rhs)))
+        return e;
+    }
+  }
+  if ((e = box_copy(t, 1, phi, tmp)) ||
+      (e = afh_mg_fas_vcycle(mg, set_residual && nl == 1, 1)))
+    return e;
+  for (int lvl = 2; lvl <= nl; lvl++) {
+    if ((e = box_copy(t, lvl, phi, tmp)) || (e = correct_children(mg, lvl)) ||
+        (e = gc_lvl(t, lvl, i_phi, 1, fused_level(mg, lvl))) ||
+        (e = afh_mg_fas_vcycle(mg, set_residual && lvl == nl, lvl)))
+      return e;
+  }
+  return AFH_OK;
 }
 
 int32_t afh_mg_fas_vcycle(afh_mg *mg, int32_t set_residual, int32_t hl) {

@@ -205,6 +205,10 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *desc, afh_mg **out);
 int32_t afh_mg_destroy(afh_mg *mg);
 int32_t afh_mg_fas_vcycle(afh_mg *mg, int32_t set_residual,
                           int32_t highest_lvl);
+/* mg_fas_fmg (m_af_multigrid.f90:137-180): full multigrid; have_guess = 0
+ * starts from phi = 0 on levels >= 2 (field_compute at start-up,
+ * src/m_field.f90:447-470) */
+int32_t afh_mg_fas_fmg(afh_mg *mg, int32_t set_residual, int32_t have_guess);
 /* mg_compute_phi_gradient (m_af_multigrid.f90:1837-1879) incl. the norm */
 int32_t afh_mg_compute_phi_gradient(afh_mg *mg, int32_t i_fc, double fac,
                                     int32_t i_norm);

@@ -998,6 +998,45 @@ int32_t afo_mg_fas_vcycle(afh_mg *mg, int32_t set_residual, int32_t hl) {
   return AFH_OK;
 }
 
+/* mg_fas_fmg, m_af_multigrid.f90:137-180; set_coarse_phi_rhs (742-776) is
+ * update_coarse without restoring tmp -- the extra tmp = phi on the parents
+ * is overwritten by the phi -> tmp copies below before tmp is read again;
+ * init_phi_rhs (779-799) clears phi on levels >= 2 and restricts rhs. */
+int32_t afo_mg_fas_fmg(afh_mg *mg, int32_t set_residual, int32_t have_guess) {
+  afh_tree *t = mg->t;
+  int nl = t->nlvl, i_phi = mg->d.i_phi, i_tmp = mg->d.i_tmp;
+  size_t bsz = t->bsz;
+  if (have_guess) {
+    for (int lvl = nl; lvl >= 2; lvl--) {
+      if (lvl == nl && gc_lvl(t, lvl, i_phi, 1)) return AFH_ERR_STATE;
+      if (afo_mg_update_coarse(mg, lvl)) return AFH_ERR_STATE;
+    }
+  } else {
+    for (int lvl = nl; lvl >= 2; lvl--) {
+      int n = LVL_N(t, ids, lvl);
+      for (int i = 0; i < n; i++) {
+        int id = LVL_AT(t, ids, lvl, i);
+        memset(ccb(t, i_phi, id), 0, sizeof(double) * bsz);
+        restrict_box(t, id, B(t, id)->parent, mg->d.i_rhs);
+      }
+      if (hook(t, AFH_HOOK_RESTRICT, lvl, mg->d.i_rhs, NULL, 0)) return AFH_ERR_STATE;
+    }
+  }
+  for (int lvl = 1; lvl <= nl; lvl++) {
+    int n = LVL_N(t, ids, lvl);
+    for (int i = 0; i < n; i++) {
+      int id = LVL_AT(t, ids, lvl, i);
+      memcpy(ccb(t, i_tmp, id), ccb(t, i_phi, id), sizeof(double) * bsz);
+    }
+    if (lvl > 1) {
+      afo_mg_correct_children(mg, lvl);
+      if (gc_lvl(t, lvl, i_phi, 1)) return AFH_ERR_STATE;
+    }
+    if (afo_mg_fas_vcycle(mg, set_residual && lvl == nl, lvl)) return AFH_ERR_STATE;
+  }
+  return AFH_OK;
+}
+
 /* mg_box_lpl_gradient + mg_box_field_norm, m_af_multigrid.f90:1882-2025 */
 int32_t afo_mg_compute_phi_gradient(afh_mg *mg, int32_t i_fc, double fac,
                                     int32_t i_norm) {

@@ -43,6 +43,7 @@ int32_t afo_mg_create(afh_tree *t, const afh_mg_desc *desc, afh_mg **out);
 int32_t afo_mg_destroy(afh_mg *mg);
 int32_t afo_mg_fas_vcycle(afh_mg *mg, int32_t set_residual,
                           int32_t highest_lvl);
+int32_t afo_mg_fas_fmg(afh_mg *mg, int32_t set_residual, int32_t have_guess);
 int32_t afo_mg_compute_phi_gradient(afh_mg *mg, int32_t i_fc, double fac,
                                     int32_t i_norm);
 int32_t afo_fluid_create(afh_tree *t, const afh_fluid_desc *desc,

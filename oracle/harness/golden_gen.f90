@@ -183,6 +183,17 @@ program golden_gen
   write(u_log, *) "update2_dt", dtl(3:4)
   call dump_state("update2")
 
+  ! ------------------------------------------------------------------
+  ! FAS-FMG (m_af_multigrid.f90:137-180): the start-up solve without a guess
+  ! (field_compute with have_guess = .false., m_field.f90:447-470), then with
+  ! the result as guess
+  call dump_state("fmg_in")
+  call hx_field_set_rhs(tree, 0)
+  call fmg(.false.)
+  call dump_state("fmg0")
+  call fmg(.true.)
+  call dump_state("fmg1")
+
   close(u_log)
 
 contains
@@ -231,12 +242,72 @@ contains
   end subroutine refine_amr
 
   ! ---------------- FAS V-cycle (m_af_multigrid.f90:185-264) ----------------
-  subroutine vcycle(set_residual, do_trace)
+  !> mg_fas_fmg, m_af_multigrid.f90:137-180, with set_residual = .true.
+  subroutine fmg(have_guess)
+    logical, intent(in) :: have_guess
+    integer             :: lvl, i, id, p_id
+
+    if (have_guess) then
+       do lvl = tree%highest_lvl, 2, -1
+          ! set_coarse_phi_rhs, m_af_multigrid.f90:742-776
+          if (lvl == tree%highest_lvl) call af_gc_lvl(tree, lvl, [mg%i_phi])
+          do i = 1, size(tree%lvls(lvl)%ids)
+             id = tree%lvls(lvl)%ids(i)
+             p_id = tree%boxes(id)%parent
+             call residual_box(tree%boxes(id))
+             call af_restrict_box(tree%boxes(id), tree%boxes(p_id), [mg%i_tmp], &
+                  use_geometry=.true.)
+             call af_restrict_box(tree%boxes(id), tree%boxes(p_id), [mg%i_phi], &
+                  use_geometry=.false.)
+          end do
+          call af_gc_lvl(tree, lvl-1, [mg%i_phi])
+          do i = 1, size(tree%lvls(lvl-1)%parents)
+             id = tree%lvls(lvl-1)%parents(i)
+             call af_stencil_apply_box(tree%boxes(id), mg%operator_key, &
+                  mg%i_phi, mg%i_rhs)
+             call af_box_add_cc(tree%boxes(id), mg%i_tmp, mg%i_rhs)
+          end do
+       end do
+    else
+       ! init_phi_rhs, m_af_multigrid.f90:779-799
+       do lvl = tree%highest_lvl, 2, -1
+          do i = 1, size(tree%lvls(lvl)%ids)
+             id = tree%lvls(lvl)%ids(i)
+             tree%boxes(id)%cc(:, :, :, mg%i_phi) = 0.0_dp
+             p_id = tree%boxes(id)%parent
+             call af_restrict_box(tree%boxes(id), tree%boxes(p_id), [mg%i_rhs], &
+                  use_geometry=.true.)
+          end do
+       end do
+    end if
+
+    do i = 1, size(tree%lvls(1)%ids)
+       id = tree%lvls(1)%ids(i)
+       tree%boxes(id)%cc(:, :, :, mg%i_tmp) = tree%boxes(id)%cc(:, :, :, mg%i_phi)
+    end do
+    call vcycle(1 == tree%highest_lvl, .false., 1)
+
+    do lvl = 2, tree%highest_lvl
+       do i = 1, size(tree%lvls(lvl)%ids)
+          id = tree%lvls(lvl)%ids(i)
+          tree%boxes(id)%cc(:, :, :, mg%i_tmp) = tree%boxes(id)%cc(:, :, :, mg%i_phi)
+       end do
+       call correct_children(tree%lvls(lvl-1)%parents)
+       call af_gc_lvl(tree, lvl, [mg%i_phi])
+       call vcycle(lvl == tree%highest_lvl, .false., lvl)
+    end do
+  end subroutine fmg
+
+  subroutine vcycle(set_residual, do_trace, highest)
     logical, intent(in) :: set_residual, do_trace
-    integer             :: lvl, i, id
+    integer, intent(in), optional :: highest
+    integer             :: lvl, i, id, max_lvl
     character(len=40)   :: tag
 
-    do lvl = tree%highest_lvl, 2, -1
+    max_lvl = tree%highest_lvl
+    if (present(highest)) max_lvl = highest
+
+    do lvl = max_lvl, 2, -1
        call gsrb_boxes(lvl, mg_cycle_down)
        if (do_trace) then
           write(tag, "(A,I0)") "tr_gsrb_down_", lvl
@@ -252,7 +323,7 @@ contains
     call solve_coarse_exact()
     if (do_trace) call dump_state("tr_coarse")
 
-    do lvl = 2, tree%highest_lvl
+    do lvl = 2, max_lvl
        call correct_children(tree%lvls(lvl-1)%parents)
        call af_gc_lvl(tree, lvl, [mg%i_phi])
        if (do_trace) then
@@ -267,7 +338,7 @@ contains
     end do
 
     if (set_residual) then
-       do lvl = 1, tree%highest_lvl
+       do lvl = 1, max_lvl
           do i = 1, size(tree%lvls(lvl)%ids)
              id = tree%lvls(lvl)%ids(i)
              call residual_box(tree%boxes(id))

@@ -43,10 +43,17 @@ CHAIN = [
     ("flux2", ["e1"], ["flux"]),
     ("update2", ["e0", "pos0", "neg0"], []),
 ]
+# FAS-FMG, run by the harness after the chain from the state it dumps as
+# fmg_in (so every case can replay it in isolation)
+FMG = [
+    ("fmg_in", ["e0", "pos0", "neg0", "phi", "rhs", "tmp"], []),
+    ("fmg0", ["rhs", "phi", "tmp"], []),
+    ("fmg1", ["rhs", "phi", "tmp"], []),
+]
 CASES = {
-    "uni4": {"chain": CHAIN, "trace": True},
-    "uni8": {"chain": CHAIN, "trace": False},
-    "amr4": {"chain": CHAIN[:7], "trace": False},
+    "uni4": {"chain": CHAIN + FMG, "trace": True},
+    "uni8": {"chain": CHAIN + FMG, "trace": False},
+    "amr4": {"chain": CHAIN[:7] + FMG, "trace": False},
 }
 
 

@@ -1,10 +1,12 @@
-"""Sharded tree over ranks (afh.dist) on the CPU.
+"""Sharded tree over ranks (afh.dist).
 
 world_size 2 (and 3) gloo processes each run their part of a sharded tree
-with the C oracle as the compute engine, through the same exchange hooks the
-HIP library calls; the owned boxes of all ranks, gathered, must be bitwise
-equal to a single-rank run of the same case (field solve with residual
-checks + a Heun step), and so must the time-step limits.
+-- on the CPU with the C oracle as the compute engine, on the GPU with
+libafivo_hip (2 ranks sharing the test box's GPU) -- through the exchange
+hooks the libraries call; the owned boxes of all ranks, gathered, must be
+bitwise equal to a single-rank run of the same case (FMG start-up solve,
+field solve with residual checks, a Heun step), and so must the time-step
+limits.
 """
 import os
 import socket
@@ -34,6 +36,8 @@ def _run(lib, topo, shard=None):
     c = StreamerCase(lib, topo, td, chem, float(g["current_voltage"]),
                      coarse_cycles=12, shard=shard)
     seed_state(c)
+    c.fluid.field_set_rhs(IV["rhs"], 0)
+    c.mg.fas_fmg(True, have_guess=False)  # start-up solve
     res = c.field_compute(0)
     lim = c.heun_step(1e-12)
     out = {"res": np.asarray(res), "lim": np.asarray(lim)}

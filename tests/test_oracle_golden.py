@@ -30,7 +30,7 @@ def test_oracle_matches_reference(lib, case):
     for stage, errs in report.items():
         for var, e in errs.items():
             tol = TOL_EXACT
-            if stage.startswith("vcycle") or stage == "field1":
+            if stage in golden.SOLVE_STAGES:
                 tol = TOL_PHI
             if stage.startswith("update"):
                 tol = TOL_DENS
