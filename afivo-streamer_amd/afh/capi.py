@@ -110,11 +110,13 @@ SIGNATURES = {
     "mg_create": (i32, [_VP, C.POINTER(MgDesc), _PVP]),
     "mg_destroy": (i32, [_VP]),
     "mg_fas_vcycle": (i32, [_VP, i32, i32]),
+    "mg_fas_vcycle_maxres": (i32, [_VP, i32, P_f64]),
     "mg_fas_fmg": (i32, [_VP, i32, i32]),
     "mg_compute_phi_gradient": (i32, [_VP, i32, f64, i32]),
     "fluid_create": (i32, [_VP, C.POINTER(FluidDesc), _PVP]),
     "fluid_destroy": (i32, [_VP]),
     "field_set_rhs": (i32, [_VP, i32, i32]),
+    "field_set_rhs_maxabs": (i32, [_VP, i32, i32, P_f64]),
     "flux_upwind_tree": (i32, [_VP, i32, P_f64]),
     "flux_update_densities": (i32, [_VP, f64, i32, i32, P_i32, P_f64, i32,
                                     i32, P_f64]),

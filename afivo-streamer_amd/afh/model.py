@@ -170,6 +170,12 @@ class Multigrid:
     def fas_vcycle(self, set_residual=True, highest_lvl=0):
         self.lib.call("mg_fas_vcycle", self.h, int(set_residual), highest_lvl)
 
+    def fas_vcycle_maxres(self, highest_lvl=0):
+        """mg_fas_vcycle(set_residual) + af_tree_maxabs_cc(i_tmp), fused."""
+        out = C.c_double()
+        self.lib.call("mg_fas_vcycle_maxres", self.h, highest_lvl, C.byref(out))
+        return out.value
+
     def fas_fmg(self, set_residual=True, have_guess=True):
         """mg_fas_fmg (m_af_multigrid.f90:137-180)."""
         self.lib.call("mg_fas_fmg", self.h, int(set_residual), int(have_guess))
@@ -240,6 +246,12 @@ class Fluid:
 
     def field_set_rhs(self, i_rhs, s_in):
         self.lib.call("field_set_rhs", self.h, i_rhs, s_in)
+
+    def field_set_rhs_maxabs(self, i_rhs, s_in):
+        """field_set_rhs + af_tree_maxabs_cc(i_rhs), fused; returns max|rhs|."""
+        out = C.c_double()
+        self.lib.call("field_set_rhs_maxabs", self.h, i_rhs, s_in, C.byref(out))
+        return out.value
 
     def flux_upwind_tree(self, s_deriv):
         dt = (C.c_double * 2)()

@@ -105,20 +105,22 @@ class StreamerCase:
     def field_compute(self, s_in, n_vcycles=2, max_rel_residual=1e-4,
                       check_residual=True):
         """m_field.f90:405-485 with have_guess = .true.; returns residuals."""
-        self.fluid.field_set_rhs(IV["rhs"], s_in)
         residuals = []
         threshold = None
         if check_residual:
-            max_rhs = self.tree.maxabs_cc(IV["rhs"])
+            max_rhs = self.fluid.field_set_rhs_maxabs(IV["rhs"], s_in)
             threshold = max(1e-6, max_rhs * max_rel_residual,
                             1e-10 * abs(self.voltage) /
                             (self.domain[2] * self.min_dr()))
+        else:
+            self.fluid.field_set_rhs(IV["rhs"], s_in)
         for _ in range(n_vcycles):
-            self.mg.fas_vcycle(True)
             if check_residual:
-                residuals.append(self.tree.maxabs_cc(IV["tmp"]))
+                residuals.append(self.mg.fas_vcycle_maxres())
                 if residuals[-1] < threshold:
                     break
+            else:
+                self.mg.fas_vcycle(True)
         self.field_from_potential()
         return residuals
 

@@ -154,6 +154,20 @@ __device__ __forceinline__ unsigned long long dbl_to_ord(double x) {
   unsigned long long u = __double_as_longlong(x);
   return (u & 0x8000000000000000ull) ? ~u : (u | 0x8000000000000000ull);
 }
+// Fold a per-thread max into shard red_shard() of `red` (one atomic per
+// workgroup; blockDim.x a multiple of 64, at most 1024). Every thread calls.
+__device__ __forceinline__ void block_max_to_shard(double v,
+                                                   unsigned long long *red) {
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+  __shared__ double s_red[16];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) s_red[w] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int q = 1; q < (int)(blockDim.x >> 6); q++) v = fmax(v, s_red[q]);
+    atomicMax(&red[red_shard()], dbl_to_ord(v));
+  }
+}
 inline double ord_to_dbl(unsigned long long o) {
   unsigned long long u =
       (o & 0x8000000000000000ull) ? (o & ~0x8000000000000000ull) : ~o;

@@ -309,18 +309,25 @@ __device__ __forceinline__ double apply7(const double *x, size_t c, size_t sj,
          cf.c[6] * x[c + sk];
 }
 
-__global__ void k_residual(const double *__restrict__ phi,
-                           const double *__restrict__ rhs,
-                           double *__restrict__ tmp,
-                           const int32_t *__restrict__ ids, int nc, size_t bsz,
-                           Coef cf) {
+// residual_box; with MAX (leaf boxes) the max |residual| is folded into
+// shard slots (af_tree_maxabs_cc(i_tmp) of field_compute)
+template <bool MAX>
+__global__ void __launch_bounds__(256)
+    k_residual(const double *__restrict__ phi, const double *__restrict__ rhs,
+               double *__restrict__ tmp, const int32_t *__restrict__ ids,
+               int nc, size_t bsz, Coef cf, unsigned long long *red) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= nc * nc * nc) return;
-  const int id = ids[blockIdx.y];
-  const int i = t % nc + 1, j = (t / nc) % nc + 1, k = t / (nc * nc) + 1;
-  const int ng = nc + 2;
-  const size_t o = (size_t)(id - 1) * bsz, c = ix3(ng, i, j, k);
-  tmp[o + c] = rhs[o + c] - apply7(phi + o, c, ng, (size_t)ng * ng, cf);
+  double mx = 0.0;
+  if (t < nc * nc * nc) {
+    const int id = ids[blockIdx.y];
+    const int i = t % nc + 1, j = (t / nc) % nc + 1, k = t / (nc * nc) + 1;
+    const int ng = nc + 2;
+    const size_t o = (size_t)(id - 1) * bsz, c = ix3(ng, i, j, k);
+    const double r = rhs[o + c] - apply7(phi + o, c, ng, (size_t)ng * ng, cf);
+    tmp[o + c] = r;
+    mx = fabs(r);
+  }
+  if (MAX) block_max_to_shard(mx, red);
 }
 
 __global__ void k_rstr_fas(double *__restrict__ phi,
@@ -1177,7 +1184,44 @@ int32_t afh_mg_fas_fmg(afh_mg *mg, int32_t set_residual, int32_t have_guess) {
   return AFH_OK;
 }
 
-int32_t afh_mg_fas_vcycle(afh_mg *mg, int32_t set_residual, int32_t hl) {
+}  // extern "C"
+
+// residual on every box of levels 1..max_lvl; with max_out also the leaf
+// max|residual| (reduction slot 3, as afh_tree_maxabs_cc), in the same pass
+static int32_t residual_levels(afh_mg *mg, int max_lvl, double *max_out) {
+  afh_tree *t = mg->t;
+  const int nc = t->nc, n3 = nc * nc * nc;
+  auto *red = reinterpret_cast<unsigned long long *>(t->scratch) + 3 * RED_SHARDS;
+  int32_t e;
+  if (max_out && (e = red_init(t, 3, 0.0))) return e;
+  for (int lvl = 1; lvl <= max_lvl; lvl++) {
+    const Coef &cf = mg->lvl_c[lvl - 1];
+    for (int part = 0; part < 2; part++) {
+      // part 0: leaves (max folded), part 1: parents; without max_out the
+      // level's whole id list in one launch
+      const LevelList &L = max_out ? (part ? t->parents : t->leaves) : t->ids;
+      if (!max_out && part) break;
+      const int n = L.n(lvl);
+      if (!n) continue;
+      const dim3 grid((n3 + 255) / 256, n);
+      if (max_out && !part)
+        hipLaunchKernelGGL(k_residual<true>, grid, dim3(256), 0, t->stream,
+                           t->ccv(mg->d.i_phi), t->ccv(mg->d.i_rhs),
+                           t->ccv(mg->d.i_tmp), L.at(lvl), nc, t->bsz, cf, red);
+      else
+        hipLaunchKernelGGL(k_residual<false>, grid, dim3(256), 0, t->stream,
+                           t->ccv(mg->d.i_phi), t->ccv(mg->d.i_rhs),
+                           t->ccv(mg->d.i_tmp), L.at(lvl), nc, t->bsz, cf, red);
+      AFH_LAUNCH_CHECK("k_residual");
+    }
+  }
+  if (!max_out) return AFH_OK;
+  if ((e = red_finish(t, 3, true)) || (e = red_fetch(t, 3, 1, max_out))) return e;
+  return call_hook(t, AFH_HOOK_MAX, 0, mg->d.i_tmp, max_out, 1);
+}
+
+static int32_t vcycle_impl(afh_mg *mg, int32_t set_residual, int32_t hl,
+                           double *max_res) {
   if (!mg) return set_error(AFH_ERR_ARG, "null mg");
   afh_tree *t = mg->t;
   const int max_lvl = (hl > 0 && hl <= t->nlvl) ? hl : t->nlvl;
@@ -1192,18 +1236,19 @@ int32_t afh_mg_fas_vcycle(afh_mg *mg, int32_t set_residual, int32_t hl) {
     if ((e = gc_lvl(t, lvl, mg->d.i_phi, 1, fused_level(mg, lvl)))) return e;
     if ((e = gsrb_boxes(mg, lvl, true))) return e;
   }
-  if (set_residual) {
-    const int nc = t->nc, n3 = nc * nc * nc;
-    for (int lvl = 1; lvl <= max_lvl; lvl++) {
-      if (!t->ids.n(lvl)) continue;
-      hipLaunchKernelGGL(k_residual, dim3((n3 + 255) / 256, t->ids.n(lvl)),
-                         dim3(256), 0, t->stream, t->ccv(mg->d.i_phi),
-                         t->ccv(mg->d.i_rhs), t->ccv(mg->d.i_tmp),
-                         t->ids.at(lvl), nc, t->bsz, mg->lvl_c[lvl - 1]);
-      AFH_LAUNCH_CHECK("k_residual");
-    }
-  }
+  if (set_residual) return residual_levels(mg, max_lvl, max_res);
   return AFH_OK;
+}
+
+extern "C" {
+
+int32_t afh_mg_fas_vcycle(afh_mg *mg, int32_t set_residual, int32_t hl) {
+  return vcycle_impl(mg, set_residual, hl, nullptr);
+}
+
+int32_t afh_mg_fas_vcycle_maxres(afh_mg *mg, int32_t hl, double *max_res) {
+  if (!max_res) return set_error(AFH_ERR_ARG, "null max_res");
+  return vcycle_impl(mg, 1, hl, max_res);
 }
 
 int32_t afh_mg_compute_phi_gradient(afh_mg *mg, int32_t i_fc, double fac,

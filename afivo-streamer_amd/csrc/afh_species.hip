@@ -93,14 +93,28 @@ struct RhsArgs {
   double q[MAXS];
 };
 
-__global__ void k_set_rhs(double *__restrict__ rhs, RhsArgs A,
-                          const int32_t *__restrict__ ids, size_t bsz) {
+// rhs over the whole (nc+2)^3 block (ghosts included, as DTIMES(:) in the
+// reference); with `red`, max|rhs| over the interior is folded into shard
+// slots (af_tree_maxabs_cc over leaves: set_rhs runs on leaves only).
+template <bool MAX>
+__global__ void __launch_bounds__(256)
+    k_set_rhs(double *__restrict__ rhs, RhsArgs A,
+              const int32_t *__restrict__ ids, size_t bsz, int ng,
+              unsigned long long *red) {
   const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= bsz) return;
-  const size_t o = (size_t)(ids[blockIdx.y] - 1) * bsz + t;
-  double r = 0.0;
-  for (int s = 0; s < A.n; s++) r = r + A.q[s] * A.sp[s][o];
-  rhs[o] = r;
+  double mx = 0.0;
+  if (t < bsz) {
+    const size_t o = (size_t)(ids[blockIdx.y] - 1) * bsz + t;
+    double r = 0.0;
+    for (int s = 0; s < A.n; s++) r = r + A.q[s] * A.sp[s][o];
+    rhs[o] = r;
+    if (MAX) {
+      const int tt = (int)t, i = tt % ng, j = (tt / ng) % ng, k = tt / (ng * ng);
+      if (i >= 1 && i < ng - 1 && j >= 1 && j < ng - 1 && k >= 1 && k < ng - 1)
+        mx = fabs(r);
+    }
+  }
+  if (MAX) block_max_to_shard(mx, red);
 }
 
 // ------------------------------------------------------------ gc2
@@ -837,7 +851,12 @@ int32_t afh_fluid_destroy(afh_fluid *f) {
   return AFH_OK;
 }
 
-int32_t afh_field_set_rhs(afh_fluid *f, int32_t i_rhs, int32_t s_in) {
+}  // extern "C"
+
+// field_set_rhs; with max_out, also af_tree_maxabs_cc(i_rhs) (reduction
+// slot 3, the one afh_tree_maxabs_cc uses), folded into the same pass
+static int32_t set_rhs_impl(afh_fluid *f, int32_t i_rhs, int32_t s_in,
+                            double *max_out) {
   if (!f) return set_error(AFH_ERR_ARG, "null fluid");
   afh_tree *t = f->t;
   if (i_rhs < 1 || i_rhs > t->nvc) return set_error(AFH_ERR_ARG, "bad i_rhs");
@@ -850,15 +869,36 @@ int32_t afh_field_set_rhs(afh_fluid *f, int32_t i_rhs, int32_t s_in) {
     A.q[A.n] = f->d.species_charge[s] * fac;
     A.n++;
   }
+  int32_t e;
+  auto *red = reinterpret_cast<unsigned long long *>(t->scratch) + 3 * RED_SHARDS;
+  if (max_out && (e = red_init(t, 3, 0.0))) return e;
   for (int l = 1; l <= t->nlvl; l++) {
     const int n = t->leaves.n(l);
     if (!n) continue;
-    hipLaunchKernelGGL(k_set_rhs, dim3((unsigned)((t->bsz + 255) / 256), n),
-                       dim3(256), 0, t->stream, t->ccv(i_rhs), A,
-                       t->leaves.at(l), t->bsz);
+    const dim3 grid((unsigned)((t->bsz + 255) / 256), n);
+    if (max_out)
+      hipLaunchKernelGGL(k_set_rhs<true>, grid, dim3(256), 0, t->stream,
+                         t->ccv(i_rhs), A, t->leaves.at(l), t->bsz, t->ng, red);
+    else
+      hipLaunchKernelGGL(k_set_rhs<false>, grid, dim3(256), 0, t->stream,
+                         t->ccv(i_rhs), A, t->leaves.at(l), t->bsz, t->ng, red);
     AFH_LAUNCH_CHECK("k_set_rhs");
   }
-  return AFH_OK;
+  if (!max_out) return AFH_OK;
+  if ((e = red_finish(t, 3, true)) || (e = red_fetch(t, 3, 1, max_out))) return e;
+  return call_hook(t, AFH_HOOK_MAX, 0, i_rhs, max_out, 1);
+}
+
+extern "C" {
+
+int32_t afh_field_set_rhs(afh_fluid *f, int32_t i_rhs, int32_t s_in) {
+  return set_rhs_impl(f, i_rhs, s_in, nullptr);
+}
+
+int32_t afh_field_set_rhs_maxabs(afh_fluid *f, int32_t i_rhs, int32_t s_in,
+                                 double *max_rhs) {
+  if (!max_rhs) return set_error(AFH_ERR_ARG, "null max_rhs");
+  return set_rhs_impl(f, i_rhs, s_in, max_rhs);
 }
 
 }  // extern "C"

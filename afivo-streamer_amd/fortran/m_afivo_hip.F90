@@ -270,6 +270,16 @@ module m_afivo_hip
        integer(c_int32_t)        :: afh_mg_fas_vcycle
      end function afh_mg_fas_vcycle
 
+     !> mg_fas_vcycle(set_residual) + af_tree_maxabs_cc(i_tmp), fused
+     function afh_mg_fas_vcycle_maxres(mg, highest_lvl, max_res) &
+          bind(C, name=afh_pfx//"mg_fas_vcycle_maxres")
+       import
+       type(c_ptr), value        :: mg
+       integer(c_int32_t), value :: highest_lvl
+       real(c_double), intent(out) :: max_res
+       integer(c_int32_t)        :: afh_mg_fas_vcycle_maxres
+     end function afh_mg_fas_vcycle_maxres
+
      function afh_mg_compute_phi_gradient(mg, i_fc, fac, i_norm) &
           bind(C, name=afh_pfx//"mg_compute_phi_gradient")
        import
@@ -300,6 +310,16 @@ module m_afivo_hip
        integer(c_int32_t), value :: i_rhs, s_in
        integer(c_int32_t)        :: afh_field_set_rhs
      end function afh_field_set_rhs
+
+     !> field_set_rhs + af_tree_maxabs_cc(i_rhs), fused
+     function afh_field_set_rhs_maxabs(f, i_rhs, s_in, max_rhs) &
+          bind(C, name=afh_pfx//"field_set_rhs_maxabs")
+       import
+       type(c_ptr), value        :: f
+       integer(c_int32_t), value :: i_rhs, s_in
+       real(c_double), intent(out) :: max_rhs
+       integer(c_int32_t)        :: afh_field_set_rhs_maxabs
+     end function afh_field_set_rhs_maxabs
 
      function afh_flux_upwind_tree(f, s_deriv, dt_lim) &
           bind(C, name=afh_pfx//"flux_upwind_tree")

@@ -205,6 +205,12 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *desc, afh_mg **out);
 int32_t afh_mg_destroy(afh_mg *mg);
 int32_t afh_mg_fas_vcycle(afh_mg *mg, int32_t set_residual,
                           int32_t highest_lvl);
+/* mg_fas_vcycle(set_residual = .true.) followed by af_tree_maxabs_cc(i_tmp):
+ * the V-cycle + convergence test of field_compute (src/m_field.f90:455-465),
+ * with the leaf max|residual| folded into the residual pass (no second read
+ * of tmp). Same results as the two calls. */
+int32_t afh_mg_fas_vcycle_maxres(afh_mg *mg, int32_t highest_lvl,
+                                 double *max_res);
 /* mg_fas_fmg (m_af_multigrid.f90:137-180): full multigrid; have_guess = 0
  * starts from phi = 0 on levels >= 2 (field_compute at start-up,
  * src/m_field.f90:447-470) */
@@ -219,6 +225,10 @@ int32_t afh_fluid_create(afh_tree *t, const afh_fluid_desc *desc,
 int32_t afh_fluid_destroy(afh_fluid *f);
 /* field_set_rhs (src/m_field.f90:363-401) */
 int32_t afh_field_set_rhs(afh_fluid *f, int32_t i_rhs, int32_t s_in);
+/* field_set_rhs followed by af_tree_maxabs_cc(i_rhs) (src/m_field.f90:
+ * 363-401, 419-421): the leaf max|rhs| is folded into the rhs pass. */
+int32_t afh_field_set_rhs_maxabs(afh_fluid *f, int32_t i_rhs, int32_t s_in,
+                                 double *max_rhs);
 /* flux_upwind_tree with the m_fluid flux_upwind / flux_direction callbacks
  * (m_af_flux_schemes.f90:666-848, src/m_fluid.f90:102-227); dt_lim[2] =
  * (CFL limit for CFL number 1, dielectric relaxation time). */

@@ -998,6 +998,13 @@ int32_t afo_mg_fas_vcycle(afh_mg *mg, int32_t set_residual, int32_t hl) {
   return AFH_OK;
 }
 
+/* mg_fas_vcycle(set_residual) + af_tree_maxabs_cc(i_tmp)
+ * (src/m_field.f90:455-465) */
+int32_t afo_mg_fas_vcycle_maxres(afh_mg *mg, int32_t hl, double *max_res) {
+  int32_t e = afo_mg_fas_vcycle(mg, 1, hl);
+  return e ? e : afo_tree_maxabs_cc(mg->t, mg->d.i_tmp, max_res);
+}
+
 /* mg_fas_fmg, m_af_multigrid.f90:137-180; set_coarse_phi_rhs (742-776) is
  * update_coarse without restoring tmp -- the extra tmp = phi on the parents
  * is overwritten by the phi -> tmp copies below before tmp is read again;
@@ -1156,6 +1163,13 @@ int32_t afo_field_set_rhs(afh_fluid *f, int32_t i_rhs, int32_t s_in) {
     }
   }
   return AFH_OK;
+}
+
+/* field_set_rhs + af_tree_maxabs_cc(i_rhs) (src/m_field.f90:363-401, 419) */
+int32_t afo_field_set_rhs_maxabs(afh_fluid *f, int32_t i_rhs, int32_t s_in,
+                                 double *max_rhs) {
+  int32_t e = afo_field_set_rhs(f, i_rhs, s_in);
+  return e ? e : afo_tree_maxabs_cc(f->t, i_rhs, max_rhs);
 }
 
 /* af_limiter_koren, m_af_limiters.f90:72-95; af_limiter_gminmod

@@ -43,6 +43,8 @@ int32_t afo_mg_create(afh_tree *t, const afh_mg_desc *desc, afh_mg **out);
 int32_t afo_mg_destroy(afh_mg *mg);
 int32_t afo_mg_fas_vcycle(afh_mg *mg, int32_t set_residual,
                           int32_t highest_lvl);
+int32_t afo_mg_fas_vcycle_maxres(afh_mg *mg, int32_t highest_lvl,
+                                 double *max_res);
 int32_t afo_mg_fas_fmg(afh_mg *mg, int32_t set_residual, int32_t have_guess);
 int32_t afo_mg_compute_phi_gradient(afh_mg *mg, int32_t i_fc, double fac,
                                     int32_t i_norm);
@@ -50,6 +52,8 @@ int32_t afo_fluid_create(afh_tree *t, const afh_fluid_desc *desc,
                          afh_fluid **out);
 int32_t afo_fluid_destroy(afh_fluid *f);
 int32_t afo_field_set_rhs(afh_fluid *f, int32_t i_rhs, int32_t s_in);
+int32_t afo_field_set_rhs_maxabs(afh_fluid *f, int32_t i_rhs, int32_t s_in,
+                                 double *max_rhs);
 int32_t afo_flux_upwind_tree(afh_fluid *f, int32_t s_deriv, double *dt_lim);
 int32_t afo_flux_update_densities(afh_fluid *f, double dt, int32_t s_deriv,
                                   int32_t n_prev, const int32_t *s_prev,

@@ -45,7 +45,8 @@ program dropin_heun
   character(len=256)     :: case_name, td_file
   integer                :: nc, grid(3), max_lvl, amr_lvl, i, iv, n_bad
   real(dp)               :: dom(3), r0(3), width, dt, dtl(4)
-  real(c_double)         :: dl(2)
+  real(c_double)         :: dl(2), mx_dev
+  real(dp)               :: mx_ref
 
   call get_command_argument(1, case_name)
   call get_command_argument(2, td_file)
@@ -168,6 +169,12 @@ program dropin_heun
   call hx_field_set_rhs(tree, 0)
   call afh_check(afh_field_set_rhs(fl, int(i_rhs, c_int32_t), 0_c_int32_t), "set_rhs")
   call check_cc(i_rhs, "rhs")
+  ! the fused form with the convergence test's max|rhs| (m_field.f90:419)
+  call af_tree_maxabs_cc(tree, i_rhs, mx_ref)
+  call afh_check(afh_field_set_rhs_maxabs(fl, int(i_rhs, c_int32_t), 0_c_int32_t, &
+       mx_dev), "set_rhs_maxabs")
+  call check_cc(i_rhs, "rhs (fused max)")
+  call check_dt([mx_ref], [mx_dev], "max|rhs|")
 
   ! --- field_from_potential (m_field.f90:488-505)
   call mg_compute_phi_gradient(tree, mg, f_field, -1.0_dp, i_efld)

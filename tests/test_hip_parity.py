@@ -158,3 +158,23 @@ def test_ghost_cells_exact_for_linear_field(hip):
     c.tree.gc_tree(IV["phi"])
     out = c.tree.get_cc(IV["phi"])
     assert np.max(np.abs(out - phi)) < 1e-13
+
+
+@pytest.mark.parametrize("name", ["amr8", "uni16_l3"])
+def test_fused_maxabs_equals_separate(hip, oracle, name):
+    """afh_field_set_rhs_maxabs / afh_mg_fas_vcycle_maxres (the reductions of
+    field_compute folded into the rhs and residual passes) give the values of
+    field_set_rhs + af_tree_maxabs_cc and mg_fas_vcycle + af_tree_maxabs_cc."""
+    g = golden.load("uni8")
+    ca, cb = _pair(hip, oracle, TOPOS[name](), g)
+    ma = ca.fluid.field_set_rhs_maxabs(IV["rhs"], 0)
+    cb.fluid.field_set_rhs(IV["rhs"], 0)
+    mb = cb.tree.maxabs_cc(IV["rhs"])
+    assert ma == mb and ma == ca.tree.maxabs_cc(IV["rhs"])
+    _assert_same(ca, cb, [IV["rhs"]])
+    for _ in range(2):
+        ra = ca.mg.fas_vcycle_maxres()
+        cb.mg.fas_vcycle(True)
+        rb = cb.tree.maxabs_cc(IV["tmp"])
+        assert ra == rb and ra == ca.tree.maxabs_cc(IV["tmp"])
+    _assert_same(ca, cb, [IV["phi"], IV["tmp"]])
