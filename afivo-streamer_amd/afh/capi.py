@@ -21,7 +21,7 @@ BC_DIRICHLET, BC_NEUMANN, BC_CONTINUOUS, BC_DIRICHLET_COPY = -10, -11, -12, -13
 RB_GC_INTERP, RB_GC_INTERP_LIM, RB_MG_SIDES = 1, 2, 3
 LIM_NONE, LIM_VANLEER, LIM_KOREN, LIM_MINMOD, LIM_MC, LIM_GMINMOD43, LIM_ZERO = range(1, 8)
 RATE_TABULATED_FIELD, RATE_CONSTANT, RATE_LINEAR, RATE_EXP_V1, RATE_EXP_V2 = range(1, 6)
-COARSE_CYCLES = 1
+COARSE_CYCLES, COARSE_DIRECT = 1, 2
 MAX_SPECIES = 32
 MAX_REACTIONS = 128
 
@@ -133,7 +133,7 @@ HOOK_HALO, HOOK_RIMS, HOOK_RESTRICT, HOOK_MAX, HOOK_MIN, HOOK_CFLUX = 1, 2, 3, 4
 # int32_t (*)(void *ctx, int32_t kind, int32_t level, int32_t iv, double *vals,
 #             int32_t n)
 HOOK_FN = C.CFUNCTYPE(i32, C.c_void_p, i32, i32, i32, P_f64, i32)
-PROF_GSRB, PROF_GHOST, PROF_FLUX, PROF_UPDATE, PROF_GSRB_PAIR = 1, 2, 3, 4, 5
+PROF_GSRB, PROF_GHOST, PROF_FLUX, PROF_UPDATE, PROF_GSRB_PAIR, PROF_GSRB_PAIR_TILED = 1, 2, 3, 4, 5, 6
 ORACLE_EXTRA = {
     "mg_gsrb_boxes": (i32, [_VP, i32, i32]),
     "mg_update_coarse": (i32, [_VP, i32]),

@@ -146,11 +146,16 @@ class Multigrid:
     """mg_t bound to a tree (mg_init / mg_fas_vcycle)."""
 
     def __init__(self, tree, i_phi, i_rhs, i_tmp, n_cycle_down=2, n_cycle_up=2,
-                 helmholtz_lambda=0.0, coarse_cycles=20):
+                 helmholtz_lambda=0.0, coarse_cycles=20, coarse_mode=None):
+        """coarse_mode: capi.COARSE_CYCLES (coarse_cycles MG cycles on the
+        level-1 grid) or capi.COARSE_DIRECT (exact separable solve); None
+        picks COARSE_DIRECT when coarse_cycles == 0."""
+        if coarse_mode is None:
+            coarse_mode = capi.COARSE_DIRECT if coarse_cycles == 0 else capi.COARSE_CYCLES
         self.tree = tree
         self.lib = tree.lib
         d = capi.MgDesc(i_phi, i_rhs, i_tmp, n_cycle_down, n_cycle_up,
-                        helmholtz_lambda, capi.COARSE_CYCLES, coarse_cycles)
+                        helmholtz_lambda, coarse_mode, coarse_cycles)
         self.i_phi, self.i_rhs, self.i_tmp = i_phi, i_rhs, i_tmp
         h = C.c_void_p()
         self.lib.call("mg_create", tree.h, C.byref(d), C.byref(h))

@@ -33,7 +33,8 @@ struct CsParams {
   double cdiag[MAXMG];
   int bctype[6];
   int halo[MAXMG];  // 1: global arrays with a ghost layer, 0: compact (LDS)
-  double *u[MAXMG], *f[MAXMG], *r[MAXMG];
+  int lg[MAXMG];    // log2(nx) | log2(ny) << 8 when both are powers of 2, else -1
+  double *u[MAXMG], *f[MAXMG];
   const double *dtab;  // [MAXMG][64][2] folded (diag, 1/diag) per class
 };
 
@@ -90,13 +91,14 @@ __global__ void k_gsrb(double *__restrict__ phi, const double *__restrict__ rhs,
 //   D  plane s+2 (prefetched into registers during the step) -> LDS
 // Each plane of phi and rhs is read once and phi is written once per pair
 // (24 B/cell algorithmic).
-template <int NC>
+template <int NC, int TJ_ = NC>
 struct RbGeom {
   static constexpr int NG = NC + 2;
-  // one tile per box (measured on MI355X, S1-64 leaf level: 16-row tiles of
-  // 256 threads 1.06 ms per pair, whole boxes of 1024 threads 0.87 ms -- the
-  // tiles' halo rows cost more than the extra occupancy gains)
-  static constexpr int TJ = NC;                        // rows per tile
+  // rows per tile: whole boxes on levels with a box per CU (measured on
+  // MI355X, S1-64 leaf level: 16-row tiles of 1024 threads 1.06 ms per pair,
+  // whole boxes 0.87 ms -- the tiles' halo rows cost more than the extra
+  // occupancy gains); NC/4-row tiles on levels with 64..255 boxes
+  static constexpr int TJ = TJ_;
   static constexpr int NTILE = NC / TJ;
   static constexpr int PLT = (TJ + 2) * NG;            // LDS plane (rows j0-1..j1+1)
   static constexpr int NT = NC * TJ >= 1024 ? 1024 : (NC * TJ < 64 ? 64 : NC * TJ);
@@ -140,17 +142,17 @@ __device__ __forceinline__ double pair_ghost(
                         [&](const int *q) { return q[d] == x1 ? x1v : x2v; });
 }
 
-template <int NC>
-__global__ void __launch_bounds__(RbGeom<NC>::NT) __attribute__((amdgpu_waves_per_eu(4)))
+template <int NC, int TJ>
+__global__ void __launch_bounds__((RbGeom<NC, TJ>::NT)) __attribute__((amdgpu_waves_per_eu(4)))
     k_gsrb_pair(const double *__restrict__ src, double *__restrict__ dst,
                 const double *__restrict__ rhs,
                 const double *__restrict__ coarse,
                 const afh_box_meta *__restrict__ meta,
                 const int32_t *__restrict__ ids, size_t bsz, Coef cf,
                 double inv_c1, GcArgs ga) {
-  using G = RbGeom<NC>;
+  using G = RbGeom<NC, TJ>;
   constexpr int NG = G::NG, HN = NC / 2, NT = G::NT, CPT = G::CPT,
-                EPT = G::EPT, PLT = G::PLT, TJ = G::TJ;
+                EPT = G::EPT, PLT = G::PLT;
   constexpr size_t SK = (size_t)NG * NG;
   __shared__ double P[4][PLT];  // planes s-2 .. s+1 at slot (plane & 3)
   const int tid = threadIdx.x;
@@ -556,8 +558,10 @@ __device__ __forceinline__ void cs_gs_cell(const CsParams &P, int m, int i,
   u[gix(P, m, i, j, k)] = s * cs_inv_diag(P, m, i, j, k);
 }
 
-__device__ __forceinline__ void cs_res_cell(const CsParams &P, int m, int i,
-                                            int j, int k) {
+// residual f - A u of one cell (the expression of residual_box on the folded
+// operator, same operand order as oracle/c/afo.c cs_residual_restrict)
+__device__ __forceinline__ double cs_res(const CsParams &P, int m, int i, int j,
+                                         int k) {
   const int nx = P.dims[m][0], ny = P.dims[m][1], nz = P.dims[m][2];
   const double *u = P.u[m];
   const double *h = P.hc[m];
@@ -568,22 +572,23 @@ __device__ __forceinline__ void cs_res_cell(const CsParams &P, int m, int i,
   if (j < ny) a = a + h[1] * u[gix(P, m, i, j + 1, k)];
   if (k > 1) a = a + h[2] * u[gix(P, m, i, j, k - 1)];
   if (k < nz) a = a + h[2] * u[gix(P, m, i, j, k + 1)];
-  P.r[m][gix(P, m, i, j, k)] = P.f[m][gix(P, m, i, j, k)] - a;
+  return P.f[m][gix(P, m, i, j, k)] - a;
 }
 
+// coarse cell (i, j, k) of level c = m + 1: mean of the 8 fine residuals
+// (computed here, never stored), u = 0
 __device__ __forceinline__ void cs_rstr_cell(const CsParams &P, int c, int i,
                                              int j, int k) {
   const int m = c - 1;
-  const double *r = P.r[m];
   const int fi = 2 * i - 1, fj = 2 * j - 1, fk = 2 * k - 1;
-  double s = r[gix(P, m, fi, fj, fk)];
-  s += r[gix(P, m, fi + 1, fj, fk)];
-  s += r[gix(P, m, fi, fj + 1, fk)];
-  s += r[gix(P, m, fi + 1, fj + 1, fk)];
-  s += r[gix(P, m, fi, fj, fk + 1)];
-  s += r[gix(P, m, fi + 1, fj, fk + 1)];
-  s += r[gix(P, m, fi, fj + 1, fk + 1)];
-  s += r[gix(P, m, fi + 1, fj + 1, fk + 1)];
+  double s = cs_res(P, m, fi, fj, fk);
+  s += cs_res(P, m, fi + 1, fj, fk);
+  s += cs_res(P, m, fi, fj + 1, fk);
+  s += cs_res(P, m, fi + 1, fj + 1, fk);
+  s += cs_res(P, m, fi, fj, fk + 1);
+  s += cs_res(P, m, fi + 1, fj, fk + 1);
+  s += cs_res(P, m, fi, fj + 1, fk + 1);
+  s += cs_res(P, m, fi + 1, fj + 1, fk + 1);
   P.f[c][gix(P, c, i, j, k)] = 0.125 * s;
   P.u[c][gix(P, c, i, j, k)] = 0.0;
 }
@@ -631,12 +636,7 @@ __global__ void k_cs_gsrb(CsParams P, int m, int n) {
   const int ih = t % hx, j = (t / hx) % ny + 1, k = t / (hx * ny) + 1;
   cs_gs_cell(P, m, 2 - ((n ^ (k + j)) & 1) + 2 * ih, j, k);
 }
-__global__ void k_cs_res(CsParams P, int m) {
-  const int nx = P.dims[m][0], ny = P.dims[m][1], nz = P.dims[m][2];
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= nx * ny * nz) return;
-  cs_res_cell(P, m, t % nx + 1, (t / nx) % ny + 1, t / (nx * ny) + 1);
-}
+// residual + restriction into level c (one launch)
 __global__ void k_cs_rstr(CsParams P, int c) {
   const int nx = P.dims[c][0], ny = P.dims[c][1], nz = P.dims[c][2];
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -650,83 +650,286 @@ __global__ void k_cs_prol(CsParams P, int m) {
   cs_prol_cell(P, m, t % nx + 1, (t / nx) % ny + 1, t / (nx * ny) + 1);
 }
 
-// One workgroup runs `n_cycles` complete V-cycles starting at MG level m0
-// (all levels >= m0 are small). Every pass is followed by a barrier.
-__device__ void blk_gs(const CsParams &P, int m, int n) {
-  const int nx = P.dims[m][0], ny = P.dims[m][1], nz = P.dims[m][2];
-  const int N = nx * ny * nz;
-  for (int t = threadIdx.x; t < N; t += blockDim.x) {
-    const int i = t % nx + 1, j = (t / nx) % ny + 1, k = t / (nx * ny) + 1;
-    const int i0 = 2 - ((n ^ (k + j)) & 1);
-    if (((i - i0) & 1) == 0) cs_gs_cell(P, m, i, j, k);
+// The small MG levels m0..bottom run inside ONE workgroup with u and f in
+// LDS (compact layout, no ghost layer: the folded operator never reads
+// outside the grid). Levels of more than WAVE_CELLS cells are swept by the
+// whole workgroup with a barrier after every pass; from the first level of
+// at most WAVE_CELLS cells down to the bottom and back, wave 0 works alone
+// (no workgroup barriers: a wave's LDS operations complete in order, so a
+// compiler fence is all a pass needs). Cell indices are decoded with
+// shifts when the level's nx, ny are powers of two.
+constexpr int CS_WAVE_CELLS = 512;
+
+// One small level as the LDS kernel sees it: dims, log2 dims (-1 if not
+// powers of two), stencil weights, offsets of u and f in the LDS pool.
+// Every access goes through the __shared__ pool array itself, so the
+// compiler emits LDS instructions (pointers stored in a struct would be
+// generic / flat accesses).
+struct SmLvl {
+  int nx, ny, nz, lg;
+  int uo, fo;
+  double h0, h1, h2;
+};
+
+template <bool WAVE>
+struct CsExec {
+  __device__ static int tid() { return WAVE ? (int)(threadIdx.x & 63) : (int)threadIdx.x; }
+  __device__ static int nth() { return WAVE ? 64 : (int)blockDim.x; }
+  __device__ static void sync() {
+    if (WAVE) {
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+    } else {
+      __syncthreads();
+    }
   }
-  __syncthreads();
-}
-template <typename F>
-__device__ void blk_for(const CsParams &P, int m, F f) {
-  const int nx = P.dims[m][0], ny = P.dims[m][1], nz = P.dims[m][2];
-  const int N = nx * ny * nz;
-  for (int t = threadIdx.x; t < N; t += blockDim.x)
-    f(t % nx + 1, (t / nx) % ny + 1, t / (nx * ny) + 1);
-  __syncthreads();
+};
+
+__device__ __forceinline__ int sm_cls(const SmLvl &L, int i, int j, int k) {
+  return (i == 1) | ((i == L.nx) << 1) | ((j == 1) << 2) | ((j == L.ny) << 3) |
+         ((k == 1) << 4) | ((k == L.nz) << 5);
 }
 
-// The small MG levels m0..bottom live in LDS (compact layout, no ghost layer:
-// the folded operator never reads outside the grid); u and f of level m0 are
-// copied in from global memory and u copied back at the end.
+// cs_gs_cell on a compact LDS level (same operand order)
+__device__ __forceinline__ void sm_gs_cell(double *lds, const double *dt,
+                                           const SmLvl &L, int i, int j, int k) {
+  const int c = ((k - 1) * L.ny + (j - 1)) * L.nx + (i - 1);
+  const int sy = L.nx, sz = L.nx * L.ny;
+  const double *u = lds + L.uo;
+  double s = lds[L.fo + c];
+  if (i > 1) s = s - L.h0 * u[c - 1];
+  if (i < L.nx) s = s - L.h0 * u[c + 1];
+  if (j > 1) s = s - L.h1 * u[c - sy];
+  if (j < L.ny) s = s - L.h1 * u[c + sy];
+  if (k > 1) s = s - L.h2 * u[c - sz];
+  if (k < L.nz) s = s - L.h2 * u[c + sz];
+  lds[L.uo + c] = s * dt[sm_cls(L, i, j, k) * 2 + 1];
+}
+
+// cs_res on a compact LDS level
+__device__ __forceinline__ double sm_res(const double *lds, const double *dt,
+                                         const SmLvl &L, int i, int j, int k) {
+  const int c = ((k - 1) * L.ny + (j - 1)) * L.nx + (i - 1);
+  const int sy = L.nx, sz = L.nx * L.ny;
+  const double *u = lds + L.uo;
+  double a = dt[sm_cls(L, i, j, k) * 2] * u[c];
+  if (i > 1) a = a + L.h0 * u[c - 1];
+  if (i < L.nx) a = a + L.h0 * u[c + 1];
+  if (j > 1) a = a + L.h1 * u[c - sy];
+  if (j < L.ny) a = a + L.h1 * u[c + sy];
+  if (k > 1) a = a + L.h2 * u[c - sz];
+  if (k < L.nz) a = a + L.h2 * u[c + sz];
+  return lds[L.fo + c] - a;
+}
+
+// cs_refl on a compact LDS level
+__device__ __forceinline__ double sm_refl(const double *lds, const SmLvl &C,
+                                          const int *bct, int i, int j, int k) {
+  double s = 1.0;
+  int idx[3] = {i, j, k};
+  const int dims[3] = {C.nx, C.ny, C.nz};
+#pragma unroll
+  for (int d = 0; d < 3; d++) {
+    if (idx[d] < 1) {
+      idx[d] = 1;
+      if (bct[2 * d] == AFH_BC_DIRICHLET) s = -s;
+    } else if (idx[d] > dims[d]) {
+      idx[d] = dims[d];
+      if (bct[2 * d + 1] == AFH_BC_DIRICHLET) s = -s;
+    }
+  }
+  return s * lds[C.uo + ((idx[2] - 1) * C.ny + (idx[1] - 1)) * C.nx + (idx[0] - 1)];
+}
+
+// cell t (0-based, i fastest) -> (i, j, k), 1-based
+__device__ __forceinline__ void sm_decode(const SmLvl &L, int t, int &i, int &j,
+                                          int &k) {
+  if (L.lg >= 0) {
+    const int lx = L.lg & 0xff, ly = L.lg >> 8;
+    i = (t & (L.nx - 1)) + 1;
+    j = ((t >> lx) & (L.ny - 1)) + 1;
+    k = (t >> (lx + ly)) + 1;
+  } else {
+    i = t % L.nx + 1;
+    j = (t / L.nx) % L.ny + 1;
+    k = t / (L.nx * L.ny) + 1;
+  }
+}
+
+template <bool WAVE>
+__device__ void sm_gs(double *lds, const SmLvl *lv, const double *dtab, int m,
+                      int n) {
+  using X = CsExec<WAVE>;
+  const SmLvl L = lv[m];
+  const double *dt = dtab + m * 128;
+  if ((L.nx & 1) == 0) {
+    // the cells of parity n only: nx/2 per row
+    const int hx = L.nx >> 1, N = hx * L.ny * L.nz;
+    for (int t = X::tid(); t < N; t += X::nth()) {
+      int ih, j, k;
+      if (L.lg >= 0) {
+        const int lx = (L.lg & 0xff) - 1, ly = L.lg >> 8;
+        ih = t & (hx - 1);
+        j = ((t >> lx) & (L.ny - 1)) + 1;
+        k = (t >> (lx + ly)) + 1;
+      } else {
+        ih = t % hx;
+        j = (t / hx) % L.ny + 1;
+        k = t / (hx * L.ny) + 1;
+      }
+      sm_gs_cell(lds, dt, L, 2 - ((n ^ (k + j)) & 1) + 2 * ih, j, k);
+    }
+  } else {
+    const int N = L.nx * L.ny * L.nz;
+    for (int t = X::tid(); t < N; t += X::nth()) {
+      int i, j, k;
+      sm_decode(L, t, i, j, k);
+      const int i0 = 2 - ((n ^ (k + j)) & 1);
+      if (((i - i0) & 1) == 0) sm_gs_cell(lds, dt, L, i, j, k);
+    }
+  }
+  X::sync();
+}
+
+// residual of level m restricted into level m + 1 (cs_rstr_cell order)
+template <bool WAVE>
+__device__ void sm_rstr(double *lds, const SmLvl *lv, const double *dtab, int m) {
+  using X = CsExec<WAVE>;
+  const SmLvl L = lv[m], C = lv[m + 1];
+  const double *dt = dtab + m * 128;
+  const int N = C.nx * C.ny * C.nz;
+  for (int t = X::tid(); t < N; t += X::nth()) {
+    int i, j, k;
+    sm_decode(C, t, i, j, k);
+    const int fi = 2 * i - 1, fj = 2 * j - 1, fk = 2 * k - 1;
+    double s = sm_res(lds, dt, L, fi, fj, fk);
+    s += sm_res(lds, dt, L, fi + 1, fj, fk);
+    s += sm_res(lds, dt, L, fi, fj + 1, fk);
+    s += sm_res(lds, dt, L, fi + 1, fj + 1, fk);
+    s += sm_res(lds, dt, L, fi, fj, fk + 1);
+    s += sm_res(lds, dt, L, fi + 1, fj, fk + 1);
+    s += sm_res(lds, dt, L, fi, fj + 1, fk + 1);
+    s += sm_res(lds, dt, L, fi + 1, fj + 1, fk + 1);
+    lds[C.fo + t] = 0.125 * s;
+    lds[C.uo + t] = 0.0;
+  }
+  X::sync();
+}
+
+// prolongation of level m + 1 added to level m (cs_prol_cell order)
+template <bool WAVE>
+__device__ void sm_prol(double *lds, const SmLvl *lv, const int *bct, int m) {
+  using X = CsExec<WAVE>;
+  const SmLvl L = lv[m], C = lv[m + 1];
+  const int N = L.nx * L.ny * L.nz;
+  for (int t = X::tid(); t < N; t += X::nth()) {
+    int i, j, k;
+    sm_decode(L, t, i, j, k);
+    const int i1 = (i + 1) >> 1, i2 = i1 + 1 - 2 * (i & 1);
+    const int j1 = (j + 1) >> 1, j2 = j1 + 1 - 2 * (j & 1);
+    const int k1 = (k + 1) >> 1, k2 = k1 + 1 - 2 * (k & 1);
+    lds[L.uo + t] = lds[L.uo + t] + (27 / 64.0) * sm_refl(lds, C, bct, i1, j1, k1) +
+                    (9 / 64.0) * sm_refl(lds, C, bct, i2, j1, k1) +
+                    (9 / 64.0) * sm_refl(lds, C, bct, i1, j2, k1) +
+                    (3 / 64.0) * sm_refl(lds, C, bct, i2, j2, k1) +
+                    (9 / 64.0) * sm_refl(lds, C, bct, i1, j1, k2) +
+                    (3 / 64.0) * sm_refl(lds, C, bct, i2, j1, k2) +
+                    (3 / 64.0) * sm_refl(lds, C, bct, i1, j2, k2) +
+                    (1 / 64.0) * sm_refl(lds, C, bct, i2, j2, k2);
+  }
+  X::sync();
+}
+
+template <bool WAVE>
+__device__ void sm_smooth(double *lds, const SmLvl *lv, const double *dtab,
+                          int m, int pairs) {
+  for (int s = 0; s < pairs; s++) {
+    sm_gs<WAVE>(lds, lv, dtab, m, 1);
+    sm_gs<WAVE>(lds, lv, dtab, m, 2);
+  }
+}
+
+// The small MG levels m0..bottom run inside ONE workgroup with u and f in
+// LDS (compact layout, no ghost layer: the folded operator never reads
+// outside the grid). Levels of more than CS_WAVE_CELLS cells are swept by
+// the whole workgroup with a barrier after every pass; from the first level
+// of at most CS_WAVE_CELLS cells down to the bottom and back, wave 0 works
+// alone (no workgroup barriers: a wave's LDS operations complete in order,
+// so a compiler fence is all a pass needs).
 __global__ void __launch_bounds__(1024) k_cs_small(CsParams G, int m0,
-                                                   int n_cycles) {
+                                                   int n_cycles, int wave_cells) {
   extern __shared__ double lds[];
-  // the level table lives in LDS: a private copy indexed by the (dynamic)
-  // level number would be placed in scratch memory
-  __shared__ CsParams P;
-  __shared__ double s_dtab[MAXMG * 64 * 2];  // (diag, 1/diag) table in LDS
+  __shared__ SmLvl s_lv[MAXMG];
+  __shared__ double s_dtab[MAXMG * 64 * 2];  // (diag, 1/diag) per class
+  __shared__ int s_bct[6];
   const int bot = G.n_mg - 1;
   for (int q = threadIdx.x; q < (bot + 1) * 128; q += blockDim.x)
     s_dtab[q] = G.dtab[q];
   if (threadIdx.x == 0) {
-    P = G;
-    P.dtab = s_dtab;
-    size_t off = 0;
+    int off = 0;
     for (int m = m0; m <= bot; m++) {
-      const size_t n = (size_t)P.dims[m][0] * P.dims[m][1] * P.dims[m][2];
-      P.u[m] = lds + off;
-      P.f[m] = lds + off + n;
-      P.r[m] = lds + off + 2 * n;
-      P.halo[m] = 0;
-      off += 3 * n;
+      SmLvl &L = s_lv[m];
+      L.nx = G.dims[m][0], L.ny = G.dims[m][1], L.nz = G.dims[m][2];
+      L.lg = G.lg[m];
+      L.h0 = G.hc[m][0], L.h1 = G.hc[m][1], L.h2 = G.hc[m][2];
+      const int n = L.nx * L.ny * L.nz;
+      L.uo = off;
+      L.fo = off + n;
+      off += 2 * n;
     }
+    for (int q = 0; q < 6; q++) s_bct[q] = G.bctype[q];
   }
   __syncthreads();
-  blk_for(P, m0, [&](int i, int j, int k) {
-    P.u[m0][gix(P, m0, i, j, k)] = G.u[m0][gix(G, m0, i, j, k)];
-    P.f[m0][gix(P, m0, i, j, k)] = G.f[m0][gix(G, m0, i, j, k)];
-  });
+  {
+    const SmLvl L = s_lv[m0];
+    const int N = L.nx * L.ny * L.nz;
+    for (int t = threadIdx.x; t < N; t += blockDim.x) {
+      int i, j, k;
+      sm_decode(L, t, i, j, k);
+      lds[L.uo + t] = G.u[m0][gix(G, m0, i, j, k)];
+      lds[L.fo + t] = G.f[m0][gix(G, m0, i, j, k)];
+    }
+    __syncthreads();
+  }
+  // first level handled by wave 0 alone
+  int mw = m0;
+  while (mw < bot && s_lv[mw].nx * s_lv[mw].ny * s_lv[mw].nz > wave_cells) mw++;
+  const bool wave_tail = s_lv[mw].nx * s_lv[mw].ny * s_lv[mw].nz <= wave_cells;
   for (int cyc = 0; cyc < n_cycles; cyc++) {
-    for (int m = m0; m < bot; m++) {
-      for (int s = 0; s < 2; s++) {
-        blk_gs(P, m, 1);
-        blk_gs(P, m, 2);
-      }
-      blk_for(P, m, [&](int i, int j, int k) { cs_res_cell(P, m, i, j, k); });
-      blk_for(P, m + 1,
-              [&](int i, int j, int k) { cs_rstr_cell(P, m + 1, i, j, k); });
+    for (int m = m0; m < mw; m++) {
+      sm_smooth<false>(lds, s_lv, s_dtab, m, 2);
+      sm_rstr<false>(lds, s_lv, s_dtab, m);
     }
-    for (int it = 0; it < CS_BOTTOM_SWEEPS; it++) {
-      blk_gs(P, bot, 1);
-      blk_gs(P, bot, 2);
-    }
-    for (int m = bot - 1; m >= m0; m--) {
-      blk_for(P, m, [&](int i, int j, int k) { cs_prol_cell(P, m, i, j, k); });
-      for (int s = 0; s < 2; s++) {
-        blk_gs(P, m, 1);
-        blk_gs(P, m, 2);
+    if (wave_tail) {
+      if (threadIdx.x < 64) {
+        for (int m = mw; m < bot; m++) {
+          sm_smooth<true>(lds, s_lv, s_dtab, m, 2);
+          sm_rstr<true>(lds, s_lv, s_dtab, m);
+        }
+        sm_smooth<true>(lds, s_lv, s_dtab, bot, CS_BOTTOM_SWEEPS);
+        for (int m = bot - 1; m >= mw; m--) {
+          sm_prol<true>(lds, s_lv, s_bct, m);
+          sm_smooth<true>(lds, s_lv, s_dtab, m, 2);
+        }
       }
+      __syncthreads();
+    } else {
+      sm_smooth<false>(lds, s_lv, s_dtab, bot, CS_BOTTOM_SWEEPS);  // mw == bot
+    }
+    for (int m = mw - 1; m >= m0; m--) {
+      sm_prol<false>(lds, s_lv, s_bct, m);
+      sm_smooth<false>(lds, s_lv, s_dtab, m, 2);
     }
   }
-  blk_for(P, m0, [&](int i, int j, int k) {
-    G.u[m0][gix(G, m0, i, j, k)] = P.u[m0][gix(P, m0, i, j, k)];
-  });
+  {
+    const SmLvl L = s_lv[m0];
+    const int N = L.nx * L.ny * L.nz;
+    for (int t = threadIdx.x; t < N; t += blockDim.x) {
+      int i, j, k;
+      sm_decode(L, t, i, j, k);
+      G.u[m0][gix(G, m0, i, j, k)] = lds[L.uo + t];
+    }
+  }
 }
 
 // coarse_solver_set_rhs_phi: gather rhs (+ folded BC values) and phi
@@ -776,6 +979,39 @@ __global__ void k_cs_scatter(CsParams P, double *__restrict__ phi,
                  (m.ix[2] - 1) * nc + k)];
 }
 
+// AFH_COARSE_DIRECT: one 1-D transform of the level-1 grid along dim d,
+// out(c) = sum_p M[p][c_d] in(.., p, ..) with M = Q (forward, Q^T f) or Q^T
+// (inverse, Q u^); summed in p order as oracle/c/afo.c cs_transform. With
+// `div` the forward result is divided by the eigenvalue sum (zero modes 0).
+__global__ void __launch_bounds__(256)
+    k_cs_transform(const double *__restrict__ in, int in_halo,
+                   double *__restrict__ out, int out_halo,
+                   const double *__restrict__ M, const double *__restrict__ e0,
+                   const double *__restrict__ e1, const double *__restrict__ e2,
+                   int nx, int ny, int nz, int d, int div, double lam) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nx * ny * nz) return;
+  const int i = t % nx, j = (t / nx) % ny, k = t / (nx * ny);
+  const int n = d == 0 ? nx : (d == 1 ? ny : nz);
+  const int co = d == 0 ? i : (d == 1 ? j : k);
+  // stride of dim d and the address of p = 0 in `in`
+  const int hx = nx + 2 * in_halo, hy = ny + 2 * in_halo;
+  const size_t st = d == 0 ? 1 : (d == 1 ? (size_t)hx : (size_t)hx * hy);
+  int c[3] = {i + in_halo, j + in_halo, k + in_halo};
+  c[d] = in_halo;
+  const double *src = in + ((size_t)c[2] * hy + c[1]) * hx + c[0];
+  double s = 0.0;
+  for (int p = 0; p < n; p++) s = s + M[(size_t)p * n + co] * src[p * st];
+  if (div) {
+    const double den = ((e0[i] + e1[j]) + e2[k]) - lam;
+    s = den != 0.0 ? s / den : 0.0;
+  }
+  const size_t o = out_halo
+                       ? (((size_t)k + 1) * (ny + 2) + j + 1) * (nx + 2) + i + 1
+                       : ((size_t)k * ny + j) * nx + i;
+  out[o] = s;
+}
+
 }  // namespace afh
 
 using namespace afh;
@@ -793,6 +1029,13 @@ struct afh_mg {
   // fused GSRB pairs (k_gsrb_pair) on levels with at least fused_min boxes
   // (default: enough boxes for one workgroup per CU, 256 tiles)
   int fused_min = 0;
+  bool force_tiles = false;  // AFH_GSRB_TILES
+  int wave_cells = CS_WAVE_CELLS;  // AFH_CS_WAVE_CELLS
+  // AFH_COARSE_DIRECT: eigenvectors Q and Q^T per dim, eigenvalues, work
+  double *d_q[3] = {nullptr, nullptr, nullptr}, *d_qt[3] = {nullptr, nullptr, nullptr};
+  double *d_e[3] = {nullptr, nullptr, nullptr};
+  double *w1 = nullptr, *w2 = nullptr;
+  int q_bc[6] = {0, 0, 0, 0, 0, 0};
   double *alt = nullptr;  // spare image of phi (all boxes) for the ping-pong
 };
 
@@ -824,6 +1067,51 @@ static int32_t build_table(afh_mg *mg) {
   return AFH_OK;
 }
 
+// AFH_COARSE_DIRECT tables: the folded 1-D operator of each dimension is
+// h tridiag(1, -2, 1) with end diagonals -h (Neumann) / -3h (Dirichlet),
+// diagonalised by a cosine / sine basis; same formula and operation order
+// as oracle/c/afo.c afo_cs_direct_tables.
+static void cs_direct_tables(int n, int bc_lo, int bc_hi, double h, double *q,
+                             double *e) {
+  const int dlo = bc_lo == AFH_BC_DIRICHLET, dhi = bc_hi == AFH_BC_DIRICHLET;
+  const double pi = 3.14159265358979323846;
+  for (int p = 0; p < n; p++) {
+    double th;
+    if (dlo == dhi) th = pi * (p + dlo) / n;
+    else th = pi * (p + 0.5) / n;
+    double nrm2 = 0.0;
+    for (int i = 0; i < n; i++) {
+      double v = dlo ? sin(th * (i + 0.5)) : cos(th * (i + 0.5));
+      q[i * n + p] = v;
+      nrm2 = nrm2 + v * v;
+    }
+    const double inv = 1 / sqrt(nrm2);
+    for (int i = 0; i < n; i++) q[i * n + p] = q[i * n + p] * inv;
+    e[p] = h * (2 * cos(th) - 2);
+  }
+}
+
+static int32_t build_direct(afh_mg *mg) {
+  const afh_bc *bc = mg->t->meth[mg->d.i_phi].bc;
+  AFH_HIP(hipStreamSynchronize(mg->t->stream));
+  for (int d = 0; d < 3; d++) {
+    const int n = mg->P.dims[0][d];
+    std::vector<double> q((size_t)n * n), qt((size_t)n * n), e(n);
+    cs_direct_tables(n, bc[2 * d].type, bc[2 * d + 1].type, mg->P.hc[0][d],
+                     q.data(), e.data());
+    for (int a = 0; a < n; a++)
+      for (int b = 0; b < n; b++) qt[(size_t)a * n + b] = q[(size_t)b * n + a];
+    AFH_HIP(hipMemcpy(mg->d_q[d], q.data(), sizeof(double) * n * n,
+                      hipMemcpyHostToDevice));
+    AFH_HIP(hipMemcpy(mg->d_qt[d], qt.data(), sizeof(double) * n * n,
+                      hipMemcpyHostToDevice));
+    AFH_HIP(hipMemcpy(mg->d_e[d], e.data(), sizeof(double) * n,
+                      hipMemcpyHostToDevice));
+  }
+  for (int q = 0; q < 6; q++) mg->q_bc[q] = bc[q].type;
+  return AFH_OK;
+}
+
 static bool fused_nc_ok(int nc) {
   return nc == 4 || nc == 8 || nc == 16 || nc == 32 || nc == 64;
 }
@@ -841,7 +1129,8 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
     return set_error(AFH_ERR_ARG, "afh_mg_create: bad variable index");
   if (!t->meth[d->i_phi].set)
     return set_error(AFH_ERR_STATE, "set cc methods (bc) for phi first");
-  if (d->coarse_mode != AFH_COARSE_CYCLES || d->coarse_cycles < 1)
+  if (!(d->coarse_mode == AFH_COARSE_DIRECT ||
+        (d->coarse_mode == AFH_COARSE_CYCLES && d->coarse_cycles >= 1)))
     return set_error(AFH_ERR_UNSUPPORTED, "coarse solver mode");
   afh_mg *mg = new afh_mg();
   mg->t = t;
@@ -893,8 +1182,11 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
   mg->small_lds = 0;
   for (int q = 0; q < P.n_mg; q++) {
     P.halo[q] = 1;
+    const int nx = P.dims[q][0], ny = P.dims[q][1];
+    const bool p2 = nx > 0 && ny > 0 && (nx & (nx - 1)) == 0 && (ny & (ny - 1)) == 0;
+    P.lg[q] = p2 ? (__builtin_ctz(nx) | (__builtin_ctz(ny) << 8)) : -1;
     if (q >= mg->small_from)
-      mg->small_lds += 3 * sizeof(double) * (size_t)P.dims[q][0] * P.dims[q][1] *
+      mg->small_lds += 2 * sizeof(double) * (size_t)P.dims[q][0] * P.dims[q][1] *
                        P.dims[q][2];
   }
   if (mg->small_lds + sizeof(CsParams) + MAXMG * 128 * sizeof(double) > 160 * 1024)
@@ -909,7 +1201,11 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
   if (const char *env = getenv("AFH_GSRB_FUSED_MIN_BOXES"))
     mg->fused_min = atoi(env);
   else if (fused_nc_ok(t->nc))
-    mg->fused_min = 256;  // one box per workgroup: at least one per CU
+    // whole boxes from 256 boxes (a workgroup per CU), NC/4-row tiles from
+    // 64 boxes (NC >= 32); smaller levels keep the split half-sweeps
+    mg->fused_min = t->nc >= 32 ? 64 : 256;
+  if (const char *env = getenv("AFH_GSRB_TILES")) mg->force_tiles = atoi(env) != 0;
+  if (const char *env = getenv("AFH_CS_WAVE_CELLS")) mg->wave_cells = atoi(env);
   if (fused_nc_ok(t->nc) && mg->fused_min > 0) {
     bool any = false;
     for (int l = 2; l <= t->nlvl; l++) any |= t->lvl_total[l - 1] >= mg->fused_min;
@@ -924,10 +1220,20 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
     size_t n = (size_t)(P.dims[q][0] + 2) * (P.dims[q][1] + 2) * (P.dims[q][2] + 2);
     AFH_HIP(hipMalloc(&P.u[q], n * sizeof(double)));
     AFH_HIP(hipMalloc(&P.f[q], n * sizeof(double)));
-    AFH_HIP(hipMalloc(&P.r[q], n * sizeof(double)));
     AFH_HIP(hipMemsetAsync(P.u[q], 0, n * sizeof(double), t->stream));
     AFH_HIP(hipMemsetAsync(P.f[q], 0, n * sizeof(double), t->stream));
-    AFH_HIP(hipMemsetAsync(P.r[q], 0, n * sizeof(double), t->stream));
+  }
+  if (d->coarse_mode == AFH_COARSE_DIRECT) {
+    const size_t n = (size_t)P.dims[0][0] * P.dims[0][1] * P.dims[0][2];
+    for (int q = 0; q < 3; q++) {
+      const size_t nd = P.dims[0][q];
+      AFH_HIP(hipMalloc(&mg->d_q[q], nd * nd * sizeof(double)));
+      AFH_HIP(hipMalloc(&mg->d_qt[q], nd * nd * sizeof(double)));
+      AFH_HIP(hipMalloc(&mg->d_e[q], nd * sizeof(double)));
+    }
+    AFH_HIP(hipMalloc(&mg->w1, n * sizeof(double)));
+    AFH_HIP(hipMalloc(&mg->w2, n * sizeof(double)));
+    if (int32_t e = build_direct(mg)) return e;
   }
   AFH_HIP(hipStreamSynchronize(t->stream));
   *out = mg;
@@ -940,9 +1246,11 @@ int32_t afh_mg_destroy(afh_mg *mg) {
   for (int q = 0; q < mg->P.n_mg; q++) {
     hipFree(mg->P.u[q]);
     hipFree(mg->P.f[q]);
-    hipFree(mg->P.r[q]);
   }
   hipFree(mg->d_dtab);
+  for (int q = 0; q < 3; q++) hipFree(mg->d_q[q]), hipFree(mg->d_qt[q]), hipFree(mg->d_e[q]);
+  hipFree(mg->w1);
+  hipFree(mg->w2);
   if (mg->alt) {
     if (mg->t->alt == mg->alt) mg->t->alt = nullptr;
     hipFree(mg->alt);
@@ -953,16 +1261,35 @@ int32_t afh_mg_destroy(afh_mg *mg) {
 
 }  // extern "C"
 
+template <int NC, int TJ>
+static void launch_pair_t(afh_mg *mg, int lvl, const double *src, double *dst,
+                          const Coef &cf, double inv_c1) {
+  afh_tree *t = mg->t;
+  hipLaunchKernelGGL((k_gsrb_pair<NC, TJ>),
+                     dim3(t->ids.n(lvl) * RbGeom<NC, TJ>::NTILE),
+                     dim3(RbGeom<NC, TJ>::NT), 0, t->stream, src, dst,
+                     t->ccv(mg->d.i_rhs), t->ccv(mg->d.i_phi), t->d_boxes,
+                     t->ids.at(lvl), t->bsz, cf, inv_c1,
+                     t->gc_args(mg->d.i_phi));
+}
+
+// whole boxes per workgroup, or NC/4-row tiles (NC >= 32) on levels of
+// 64..255 boxes, which fill the CUs with 4 tiles per box
+// (AFH_GSRB_TILES=1: tiles on every level, for tests)
+static bool pair_tiles(const afh_mg *mg, int lvl) {
+  const int n = mg->t->lvl_total[lvl - 1];
+  return mg->t->nc >= 32 && (mg->force_tiles || (n >= 64 && n < 256));
+}
+
 template <int NC>
 static void launch_pair(afh_mg *mg, int lvl, const double *src, double *dst,
                         const Coef &cf, double inv_c1) {
-  afh_tree *t = mg->t;
-  if (t->ids.n(lvl) == 0) return;
-  hipLaunchKernelGGL(k_gsrb_pair<NC>, dim3(t->ids.n(lvl) * RbGeom<NC>::NTILE),
-                     dim3(RbGeom<NC>::NT),
-                     0, t->stream, src, dst, t->ccv(mg->d.i_rhs),
-                     t->ccv(mg->d.i_phi), t->d_boxes, t->ids.at(lvl), t->bsz,
-                     cf, inv_c1, t->gc_args(mg->d.i_phi));
+  if (mg->t->ids.n(lvl) == 0) return;
+  if constexpr (NC >= 32) {
+    if (pair_tiles(mg, lvl))
+      return launch_pair_t<NC, NC / 4>(mg, lvl, src, dst, cf, inv_c1);
+  }
+  launch_pair_t<NC, NC>(mg, lvl, src, dst, cf, inv_c1);
 }
 
 extern "C" {
@@ -1021,7 +1348,9 @@ static int32_t gsrb_boxes(afh_mg *mg, int lvl, bool up) {
     const double *src = to_alt ? phi : mg->alt;
     double *dst = to_alt ? mg->alt : phi;
     const int dst_iv = to_alt ? 0 : mg->d.i_phi;
-    prof_begin(t, AFH_PROF_GSRB_PAIR);
+    const int pclass = (nc >= 32 && pair_tiles(mg, lvl)) ? AFH_PROF_GSRB_PAIR_TILED
+                                                          : AFH_PROF_GSRB_PAIR;
+    prof_begin(t, pclass);
     switch (nc) {
     case 4: launch_pair<4>(mg, lvl, src, dst, cf, inv_c1); break;
     case 8: launch_pair<8>(mg, lvl, src, dst, cf, inv_c1); break;
@@ -1031,7 +1360,7 @@ static int32_t gsrb_boxes(afh_mg *mg, int lvl, bool up) {
     }
     // a red+black pair reads phi and rhs and writes phi
     // once = 24 B/cell
-    prof_end(t, AFH_PROF_GSRB_PAIR, 24.0 * nc * nc * nc * nid);
+    prof_end(t, pclass, 24.0 * nc * nc * nc * nid);
     AFH_LAUNCH_CHECK("k_gsrb_pair");
     (void)dst;
     if (int32_t e = gc_lvl_var(t, lvl, dst_iv, phi, ga, up && n == n_cycle, true))
@@ -1104,9 +1433,29 @@ static int32_t solve_coarse(afh_mg *mg) {
                      bc[3], bc[4], bc[5]);
   AFH_LAUNCH_CHECK("k_cs_gather");
   const int s = mg->small_from;
-  if (s == 0) {
+  if (mg->d.coarse_mode == AFH_COARSE_DIRECT) {
+    for (int q = 0; q < 6; q++)
+      if (mg->q_bc[q] != bc[q].type) {
+        if (int32_t e = build_direct(mg)) return e;
+        break;
+      }
+    const int nx = P.dims[0][0], ny = P.dims[0][1], nz = P.dims[0][2];
+    const dim3 g = blocks1((size_t)nx * ny * nz);
+    const double lam = mg->d.helmholtz_lambda;
+    // Q^T along x, y, z (divide), then Q along z, y, x
+    struct Pass { const double *in; int ih; double *out; int oh; int d; bool fwd; int div; };
+    const Pass ps[6] = {{P.f[0], 1, mg->w1, 0, 0, true, 0}, {mg->w1, 0, mg->w2, 0, 1, true, 0},
+                        {mg->w2, 0, mg->w1, 0, 2, true, 1}, {mg->w1, 0, mg->w2, 0, 2, false, 0},
+                        {mg->w2, 0, mg->w1, 0, 1, false, 0}, {mg->w1, 0, P.u[0], 1, 0, false, 0}};
+    for (const Pass &q : ps)
+      hipLaunchKernelGGL(k_cs_transform, g, dim3(256), 0, t->stream, q.in, q.ih,
+                         q.out, q.oh, q.fwd ? mg->d_q[q.d] : mg->d_qt[q.d],
+                         mg->d_e[0], mg->d_e[1], mg->d_e[2], nx, ny, nz, q.d,
+                         q.div, lam);
+    AFH_LAUNCH_CHECK("k_cs_transform");
+  } else if (s == 0) {
     hipLaunchKernelGGL(k_cs_small, dim3(1), dim3(1024), mg->small_lds,
-                       t->stream, P, 0, mg->d.coarse_cycles);
+                       t->stream, P, 0, mg->d.coarse_cycles, mg->wave_cells);
     AFH_LAUNCH_CHECK("k_cs_small");
   } else {
     for (int cyc = 0; cyc < mg->d.coarse_cycles; cyc++) {
@@ -1116,12 +1465,11 @@ static int32_t solve_coarse(afh_mg *mg) {
           for (int n = 1; n <= 2; n++)
             hipLaunchKernelGGL(k_cs_gsrb, blocks1(N / 2), dim3(256), 0,
                                t->stream, P, m, n);
-        hipLaunchKernelGGL(k_cs_res, blocks1(N), dim3(256), 0, t->stream, P, m);
         hipLaunchKernelGGL(k_cs_rstr, blocks1(N / 8), dim3(256), 0, t->stream, P,
                            m + 1);
       }
       hipLaunchKernelGGL(k_cs_small, dim3(1), dim3(1024), mg->small_lds,
-                         t->stream, P, s, 1);
+                         t->stream, P, s, 1, mg->wave_cells);
       for (int m = s - 1; m >= 0; m--) {
         const size_t N = (size_t)P.dims[m][0] * P.dims[m][1] * P.dims[m][2];
         hipLaunchKernelGGL(k_cs_prol, blocks1(N), dim3(256), 0, t->stream, P, m);

@@ -50,6 +50,7 @@ module m_afivo_hip
   integer(c_int32_t), parameter :: AFH_RATE_EXP_V2 = 5
 
   integer(c_int32_t), parameter :: AFH_COARSE_CYCLES = 1
+  integer(c_int32_t), parameter :: AFH_COARSE_DIRECT = 2
   integer, parameter :: AFH_MAX_SPECIES = 32
   integer, parameter :: AFH_MAX_REACTIONS = 128
 

@@ -69,7 +69,7 @@ def unit_step(case, dt):
     return res, d1, d2
 
 
-def cpu_baseline(config, steps=2):
+def cpu_baseline(config, coarse_cycles, steps=2):
     """The C oracle (oracle/lib/libafo.so, OpenMP) on a bounded sample of the
     same workload: the same 64^3 boxes but a 3-level tree (64 leaf boxes)."""
     from afh import capi
@@ -82,7 +82,8 @@ def cpu_baseline(config, steps=2):
     g = golden.load("uni8")
     td, chem = tables_from(g)
     lib = capi.oracle_library()
-    case = StreamerCase(lib, topo, td, chem, -dom[2] * (-2.5e6), coarse_cycles=8)
+    case = StreamerCase(lib, topo, td, chem, -dom[2] * (-2.5e6),
+                        coarse_cycles=coarse_cycles)
     seed_state(case, width=0.05 * dom[2])
     unit_step(case, 1e-13)
     t0 = time.perf_counter()
@@ -118,7 +119,9 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="s1-64", choices=sorted(CONFIGS))
-    ap.add_argument("--coarse-cycles", type=int, default=8)
+    ap.add_argument("--coarse-cycles", type=int, default=0,
+                    help="level-1 solve: N MG cycles, or 0 = exact separable "
+                         "solve (AFH_COARSE_DIRECT)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--replicas", action="store_true",
                     help="N>1: one independent replica per GPU instead of sharding")
@@ -196,7 +199,8 @@ def main():
             "config": {"workload": args.config, "n_cell": CONFIGS[args.config][0],
                        "leaf_cells": ncell, "boxes": int(case.topo["n_boxes"]),
                        "levels": int(case.topo["highest_lvl"]),
-                       "coarse_cycles": args.coarse_cycles,
+                       "coarse_solve": ("direct" if args.coarse_cycles == 0 else
+                                        "mg%d" % args.coarse_cycles),
                        "parallelism": ("box-shard-%d" % world) if sharded else
                        ("replica-per-gpu" if world > 1 else "single-gpu")},
             "roofline": {"bound": "hbm",
@@ -212,7 +216,7 @@ def main():
         if sharded:
             out["exchanges_per_step"] = case.shard.n_exchanges / max(1, args.steps + args.warmup + 1)
         if not args.no_cpu_baseline and world == 1:
-            out["cpu_baseline"] = cpu_baseline(args.config)
+            out["cpu_baseline"] = cpu_baseline(args.config, args.coarse_cycles)
         print(json.dumps(out))
     if dist is not None:
         dist.barrier()

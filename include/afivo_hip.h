@@ -67,6 +67,8 @@ extern "C" {
 
 /* Coarse-grid solver modes (replaces HYPRE PFMG, m_coarse_solver.f90) */
 #define AFH_COARSE_CYCLES 1 /* fixed number of device MG cycles */
+#define AFH_COARSE_DIRECT 2 /* exact solve: the folded operator is separable;
+                               cosine / sine eigenbases per dimension */
 
 #define AFH_MAX_SPECIES 32
 #define AFH_MAX_REACTIONS 128
@@ -158,8 +160,9 @@ typedef struct afh_mg_desc {
   int32_t i_phi, i_rhs, i_tmp;
   int32_t n_cycle_down, n_cycle_up; /* 2, 2 */
   double helmholtz_lambda;
-  int32_t coarse_mode;   /* AFH_COARSE_CYCLES */
-  int32_t coarse_cycles; /* device MG V(2,2) cycles on the level-1 grid */
+  int32_t coarse_mode;   /* AFH_COARSE_CYCLES or AFH_COARSE_DIRECT */
+  int32_t coarse_cycles; /* AFH_COARSE_CYCLES: MG V(2,2) cycles on the
+                            level-1 grid */
 } afh_mg_desc;
 
 typedef struct afh_tree afh_tree;
@@ -250,7 +253,8 @@ int32_t afh_flux_update_densities(afh_fluid *f, double dt, int32_t s_deriv,
 #define AFH_PROF_GHOST 2     /* ghost-cell fill (faces) */
 #define AFH_PROF_FLUX 3      /* flux kernel */
 #define AFH_PROF_UPDATE 4    /* density update */
-#define AFH_PROF_GSRB_PAIR 5 /* fused red+black Gauss-Seidel pair */
+#define AFH_PROF_GSRB_PAIR 5 /* fused red+black Gauss-Seidel pair (whole boxes) */
+#define AFH_PROF_GSRB_PAIR_TILED 6 /* the same with NC/4-row tiles */
 int32_t afh_profile_enable(afh_tree *t, int32_t kclass);
 int32_t afh_profile_read(afh_tree *t, double *total_ms, int64_t *launches,
                          double *bytes);

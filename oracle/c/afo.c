@@ -67,6 +67,11 @@ struct afh_mg {
   double hc[16][3]; /* 1/h^2 per dim per MG level */
   double cdiag[16];  /* unfolded diagonal per MG level */
   double dtab[16][64][2]; /* folded (diag, 1/diag) per boundary class */
+  /* AFH_COARSE_DIRECT: per dimension the orthonormal eigenvectors q[d]
+   * (n x n, q[i*n + p] = v_p(i)) and eigenvalues e[d] of the 1-D folded
+   * operator, two work grids, and the BC types the tables were built for */
+  double *q[3], *e[3], *w1, *w2;
+  int q_bc[6];
 };
 
 #define AFH_CS_BOTTOM_SWEEPS 16
@@ -866,6 +871,96 @@ static void cs_cycle(afh_mg *mg, int m) {
   }
 }
 
+/* ---- AFH_COARSE_DIRECT: exact solve of the folded level-1 problem.
+ * The folded operator is separable, A = Tx (x) I (x) I + I (x) Ty (x) I +
+ * I (x) I (x) Tz - lambda, with T_d = h_d tridiag(1, -2, 1) whose end
+ * diagonals are -h_d (Neumann face) or -3 h_d (Dirichlet face), exactly the
+ * folding of stencil_handle_boundaries. Each T_d is diagonalised by a
+ * cosine / sine basis (DCT-II for Neumann-Neumann, DST-II for
+ * Dirichlet-Dirichlet, DCT-IV / DST-IV for mixed ends):
+ *   v_p(i) = cos|sin(theta_p (i + 1/2)) / norm,  eig_p = h (2 cos theta_p - 2)
+ * so u = Q (Lambda^-1 (Q^T f)), with Q^T and Q applied one dimension at a
+ * time as dense n x n products in a fixed summation order (the HIP library
+ * evaluates the same sums in the same order). */
+void afo_cs_direct_tables(int n, int bc_lo, int bc_hi, double h, double *q,
+                          double *e) {
+  const int dlo = bc_lo == AFH_BC_DIRICHLET, dhi = bc_hi == AFH_BC_DIRICHLET;
+  const double pi = 3.14159265358979323846;
+  for (int p = 0; p < n; p++) {
+    double th;
+    if (dlo == dhi) th = pi * (p + dlo) / n;   /* NN: p, DD: p + 1 */
+    else th = pi * (p + 0.5) / n;              /* mixed */
+    double nrm2 = 0.0;
+    for (int i = 0; i < n; i++) {
+      double v = dlo ? sin(th * (i + 0.5)) : cos(th * (i + 0.5));
+      q[i * n + p] = v;
+      nrm2 = nrm2 + v * v;
+    }
+    const double inv = 1 / sqrt(nrm2);
+    for (int i = 0; i < n; i++) q[i * n + p] = q[i * n + p] * inv;
+    e[p] = h * (2 * cos(th) - 2);
+  }
+}
+
+static void cs_direct_build(afh_mg *mg) {
+  const afh_bc *bc = mg->t->meth[mg->d.i_phi].bc;
+  for (int d = 0; d < 3; d++) {
+    int n = mg->dims[0][d];
+    afo_cs_direct_tables(n, bc[2 * d].type, bc[2 * d + 1].type, mg->hc[0][d],
+                         mg->q[d], mg->e[d]);
+  }
+  for (int q = 0; q < 6; q++) mg->q_bc[q] = bc[q].type;
+}
+
+/* one 1-D transform along dim d: out(c) = sum_p coef(c, p) in(.. p ..),
+ * coef = Q[p][c] (forward, Q^T) or Q[c][p] (inverse); in/out with a ghost
+ * layer when *_halo. With `div`, the forward result is divided by the
+ * eigenvalue sum (zero modes set to 0). */
+static void cs_transform(afh_mg *mg, const double *in, int in_halo, double *out,
+                         int out_halo, int d, int fwd, int div) {
+  const int nx = mg->dims[0][0], ny = mg->dims[0][1], nz = mg->dims[0][2];
+  const int n = mg->dims[0][d];
+  const double *q = mg->q[d];
+  const double lam = mg->d.helmholtz_lambda;
+#pragma omp parallel for schedule(static)
+  for (int k = 0; k < nz; k++)
+    for (int j = 0; j < ny; j++)
+      for (int i = 0; i < nx; i++) {
+        int c[3] = {i, j, k};
+        const int co = c[d];
+        double s = 0.0;
+        for (int p = 0; p < n; p++) {
+          c[d] = p;
+          size_t x = in_halo ? (((size_t)c[2] + 1) * (ny + 2) + c[1] + 1) * (nx + 2) + c[0] + 1
+                             : ((size_t)c[2] * ny + c[1]) * nx + c[0];
+          const double cf = fwd ? q[p * n + co] : q[co * n + p];
+          s = s + cf * in[x];
+        }
+        if (div) {
+          const double den = ((mg->e[0][i] + mg->e[1][j]) + mg->e[2][k]) - lam;
+          s = den != 0.0 ? s / den : 0.0;
+        }
+        size_t o = out_halo ? (((size_t)k + 1) * (ny + 2) + j + 1) * (nx + 2) + i + 1
+                            : ((size_t)k * ny + j) * nx + i;
+        out[o] = s;
+      }
+}
+
+static void cs_direct_solve(afh_mg *mg) {
+  const afh_bc *bc = mg->t->meth[mg->d.i_phi].bc;
+  for (int q = 0; q < 6; q++)
+    if (mg->q_bc[q] != bc[q].type) {
+      cs_direct_build(mg);
+      break;
+    }
+  cs_transform(mg, mg->f[0], 1, mg->w1, 0, 0, 1, 0);
+  cs_transform(mg, mg->w1, 0, mg->w2, 0, 1, 1, 0);
+  cs_transform(mg, mg->w2, 0, mg->w1, 0, 2, 1, 1);
+  cs_transform(mg, mg->w1, 0, mg->w2, 0, 2, 0, 0);
+  cs_transform(mg, mg->w2, 0, mg->w1, 0, 1, 0, 0);
+  cs_transform(mg, mg->w1, 0, mg->u[0], 1, 0, 0, 0);
+}
+
 /* solve_coarse_grid, m_af_multigrid.f90:266-291 */
 int32_t afo_mg_solve_coarse(afh_mg *mg) {
   afh_tree *t = mg->t;
@@ -896,8 +991,12 @@ int32_t afo_mg_solve_coarse(afh_mg *mg) {
           mg->u[0][g] = p[IX(t, i, j, k)];
         }
   }
-  cs_build_table(mg);
-  for (int c = 0; c < mg->d.coarse_cycles; c++) cs_cycle(mg, 0);
+  if (mg->d.coarse_mode == AFH_COARSE_DIRECT) {
+    cs_direct_solve(mg);
+  } else {
+    cs_build_table(mg);
+    for (int c = 0; c < mg->d.coarse_cycles; c++) cs_cycle(mg, 0);
+  }
   /* coarse_solver_get_phi */
   for (int q = 0; q < nid; q++) {
     int id = LVL_AT(t, ids, 1, q);
@@ -962,6 +1061,19 @@ int32_t afo_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
     mg->f[q] = calloc(n, sizeof(double));
     mg->r[q] = calloc(n, sizeof(double));
   }
+  if (d->coarse_mode == AFH_COARSE_DIRECT) {
+    size_t n = (size_t)mg->dims[0][0] * mg->dims[0][1] * mg->dims[0][2];
+    for (int dd = 0; dd < 3; dd++) {
+      int nd = mg->dims[0][dd];
+      mg->q[dd] = malloc(sizeof(double) * nd * nd);
+      mg->e[dd] = malloc(sizeof(double) * nd);
+    }
+    mg->w1 = malloc(sizeof(double) * n);
+    mg->w2 = malloc(sizeof(double) * n);
+    cs_direct_build(mg);
+  } else if (d->coarse_mode != AFH_COARSE_CYCLES || d->coarse_cycles < 1) {
+    return fail(AFH_ERR_UNSUPPORTED, "coarse solver mode");
+  }
   *out = mg;
   return AFH_OK;
 }
@@ -969,6 +1081,8 @@ int32_t afo_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
 int32_t afo_mg_destroy(afh_mg *mg) {
   if (!mg) return AFH_OK;
   for (int q = 0; q < mg->n_mg; q++) free(mg->u[q]), free(mg->f[q]), free(mg->r[q]);
+  for (int d = 0; d < 3; d++) free(mg->q[d]), free(mg->e[d]);
+  free(mg->w1), free(mg->w2);
   free(mg->lvl_c);
   free(mg);
   return AFH_OK;

@@ -36,18 +36,28 @@ def oracle():
 # smoother variants: "split" = one launch per half-sweep with the level ghost
 # fill in between (the reference's sequence); "fused" = k_gsrb_pair on every
 # level (AFH_GSRB_FUSED_MIN_BOXES=1), which must give the same bits
-SMOOTHERS = {"split": "0", "fused": "1"}
+# ("fused_tiles": the same with NC/4-row tiles per workgroup, the geometry of
+# levels with 64..255 boxes, AFH_GSRB_TILES=1)
+SMOOTHERS = {"split": ("0", "0"), "fused": ("1", "0"), "fused_tiles": ("1", "1")}
 
 
 @pytest.fixture(params=sorted(SMOOTHERS))
 def smoother(request, monkeypatch):
-    monkeypatch.setenv("AFH_GSRB_FUSED_MIN_BOXES", SMOOTHERS[request.param])
+    fused_min, tiles = SMOOTHERS[request.param]
+    monkeypatch.setenv("AFH_GSRB_FUSED_MIN_BOXES", fused_min)
+    monkeypatch.setenv("AFH_GSRB_TILES", tiles)
     return request.param
 
 
+# level-1 solve: 40 MG cycles, or the exact separable solve (AFH_COARSE_DIRECT)
+COARSE = {"mg": 40, "direct": 0}
+
+
+@pytest.mark.parametrize("coarse", sorted(COARSE))
 @pytest.mark.parametrize("case", golden.CASES)
-def test_hip_matches_reference_golden(hip, case, smoother):
-    report, dts, g = golden.run_golden(hip, case, isolated=True)
+def test_hip_matches_reference_golden(hip, case, smoother, coarse):
+    report, dts, g = golden.run_golden(hip, case, isolated=True,
+                                       coarse_cycles=COARSE[coarse])
     bad = []
     for stage, errs in report.items():
         for var, e in errs.items():
@@ -62,11 +72,11 @@ def test_hip_matches_reference_golden(hip, case, smoother):
     np.testing.assert_allclose(dts["flux1"], g["log_flux1_dt"], rtol=1e-15)
 
 
-def _pair(lib_a, lib_b, topo, g):
+def _pair(lib_a, lib_b, topo, g, coarse_cycles=12):
     td, chem = tables_from(g)
     v = float(g["current_voltage"])
-    ca = StreamerCase(lib_a, topo, td, chem, v, coarse_cycles=12)
-    cb = StreamerCase(lib_b, topo, td, chem, v, coarse_cycles=12)
+    ca = StreamerCase(lib_a, topo, td, chem, v, coarse_cycles=coarse_cycles)
+    cb = StreamerCase(lib_b, topo, td, chem, v, coarse_cycles=coarse_cycles)
     seed_state(ca)
     seed_state(cb)
     return ca, cb
@@ -93,11 +103,12 @@ TOPOS = {
 }
 
 
+@pytest.mark.parametrize("coarse", ["mg12", "direct"])
 @pytest.mark.parametrize("name", sorted(TOPOS))
-def test_hip_bitwise_equals_oracle_heun_step(hip, oracle, name, smoother):
+def test_hip_bitwise_equals_oracle_heun_step(hip, oracle, name, smoother, coarse):
     g = golden.load("uni8")
     topo = TOPOS[name]()
-    ca, cb = _pair(hip, oracle, topo, g)
+    ca, cb = _pair(hip, oracle, topo, g, 12 if coarse == "mg12" else 0)
     for c in (ca, cb):
         c.field_compute(0, check_residual=False)
     _assert_same(ca, cb, [IV["phi"], IV["tmp"], IV["rhs"], IV["efld"]], [FV["field"]])

@@ -23,9 +23,12 @@ def lib():
     return capi.oracle_library()
 
 
+@pytest.mark.parametrize("coarse_cycles", [40, 0])
 @pytest.mark.parametrize("case", golden.CASES)
-def test_oracle_matches_reference(lib, case):
-    report, dts, g = golden.run_golden(lib, case, isolated=True)
+def test_oracle_matches_reference(lib, case, coarse_cycles):
+    """coarse_cycles 0: the exact separable level-1 solve (AFH_COARSE_DIRECT)."""
+    report, dts, g = golden.run_golden(lib, case, isolated=True,
+                                       coarse_cycles=coarse_cycles)
     bad = []
     for stage, errs in report.items():
         for var, e in errs.items():
@@ -49,3 +52,24 @@ def test_oracle_chained_heun_step(lib):
     report, _, _ = golden.run_golden(lib, "uni8", isolated=False)
     assert report["update2"]["e0"] < 1e-8
     assert report["field1"]["phi"] < 1e-10
+
+
+@pytest.mark.parametrize("bc", [(-11, -11), (-10, -10), (-11, -10), (-10, -11)])
+def test_direct_coarse_tables_diagonalise_folded_operator(bc):
+    """The eigenbases of AFH_COARSE_DIRECT: Q orthonormal and
+    T Q = Q diag(e) for the folded 1-D operator (ends -h Neumann / -3h
+    Dirichlet, stencil_handle_boundaries)."""
+    import ctypes as C
+    lib = C.CDLL(capi.ORACLE_LIB)
+    n, h = 12, 3.0
+    q = np.zeros(n * n)
+    e = np.zeros(n)
+    lib.afo_cs_direct_tables(C.c_int(n), C.c_int(bc[0]), C.c_int(bc[1]), C.c_double(h),
+                             q.ctypes.data_as(C.POINTER(C.c_double)),
+                             e.ctypes.data_as(C.POINTER(C.c_double)))
+    Q = q.reshape(n, n)
+    T = h * (np.diag(-2 * np.ones(n)) + np.diag(np.ones(n - 1), 1) + np.diag(np.ones(n - 1), -1))
+    T[0, 0] += h if bc[0] == -11 else -h
+    T[-1, -1] += h if bc[1] == -11 else -h
+    assert np.allclose(Q.T @ Q, np.eye(n), atol=1e-13)
+    assert np.allclose(T @ Q, Q * e[None, :], atol=1e-12)
