@@ -185,6 +185,38 @@ __device__ __forceinline__ size_t ix3(int ng, int i, int j, int k) {
   return ((size_t)k * ng + j) * ng + i;
 }
 
+// Linear index t -> (i, j, k), 1-based, of an n x n x n block, i fastest.
+// n is uniform (a kernel argument): powers of two (every afivo box size in
+// practice) decode with shifts computed in scalar registers; others divide.
+__device__ __forceinline__ void cell3(int t, int n, int &i, int &j, int &k) {
+  if ((n & (n - 1)) == 0) {
+    const int ln = __builtin_ctz(n);
+    i = (t & (n - 1)) + 1;
+    j = ((t >> ln) & (n - 1)) + 1;
+    k = (t >> (2 * ln)) + 1;
+  } else {
+    i = t % n + 1;
+    j = (t / n) % n + 1;
+    k = t / (n * n) + 1;
+  }
+}
+
+// t -> (i, j, k), 0-based, of an ng^3 block (ng = nc + 2, not a power of
+// two): float quotient corrected by one step (exact for t < 2^24)
+__device__ __forceinline__ int divg(int t, int ng, float inv) {
+  int q = (int)((float)t * inv);
+  q -= (q * ng > t) ? 1 : 0;
+  q += ((q + 1) * ng <= t) ? 1 : 0;
+  return q;
+}
+__device__ __forceinline__ void cell3g(int t, int ng, int &i, int &j, int &k) {
+  const float inv = 1.0f / (float)ng;
+  const int q = divg(t, ng, inv);
+  i = t - q * ng;
+  k = divg(q, ng, inv);
+  j = q - k * ng;
+}
+
 // Face ghost cell p (p[d] = 0 or nc+1, d = dim of face nb) of box m when the
 // face has no same-level neighbour (bc: the face's boundary condition, rb:
 // the refinement-boundary method): physical boundary (bc_to_gc,

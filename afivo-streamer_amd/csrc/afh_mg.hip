@@ -57,7 +57,17 @@ __global__ void k_gsrb(double *__restrict__ phi, const double *__restrict__ rhs,
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= hn * nc * nc) return;
   const int id = ids[blockIdx.y];
-  const int ih = t % hn, j = (t / hn) % nc + 1, k = t / (hn * nc) + 1;
+  int ih, j, k;
+  if ((nc & (nc - 1)) == 0) {
+    const int ln = __builtin_ctz(nc);
+    ih = t & (hn - 1);
+    j = ((t >> (ln - 1)) & (nc - 1)) + 1;
+    k = (t >> (2 * ln - 1)) + 1;
+  } else {
+    ih = t % hn;
+    j = (t / hn) % nc + 1;
+    k = t / (hn * nc) + 1;
+  }
   const int i = 2 - ((redblack ^ (k + j)) & 1) + 2 * ih;
   const int ng = nc + 2;
   double *x = phi + (size_t)(id - 1) * bsz;
@@ -312,22 +322,46 @@ __device__ __forceinline__ double apply7(const double *x, size_t c, size_t sj,
 }
 
 // residual_box; with MAX (leaf boxes) the max |residual| is folded into
-// shard slots (af_tree_maxabs_cc(i_tmp) of field_compute)
-template <bool MAX>
+// shard slots (af_tree_maxabs_cc(i_tmp) of field_compute). Each thread
+// takes a column of K cells along k: the z neighbours are shared and all
+// loads are issued before the arithmetic (more bytes in flight per wave).
+template <bool MAX, int K>
 __global__ void __launch_bounds__(256)
     k_residual(const double *__restrict__ phi, const double *__restrict__ rhs,
                double *__restrict__ tmp, const int32_t *__restrict__ ids,
                int nc, size_t bsz, Coef cf, unsigned long long *red) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   double mx = 0.0;
-  if (t < nc * nc * nc) {
+  if (t < nc * nc * (nc / K)) {
     const int id = ids[blockIdx.y];
-    const int i = t % nc + 1, j = (t / nc) % nc + 1, k = t / (nc * nc) + 1;
+    int i, j, kq;
+    cell3(t, nc, i, j, kq);
     const int ng = nc + 2;
-    const size_t o = (size_t)(id - 1) * bsz, c = ix3(ng, i, j, k);
-    const double r = rhs[o + c] - apply7(phi + o, c, ng, (size_t)ng * ng, cf);
-    tmp[o + c] = r;
-    mx = fabs(r);
+    const size_t sj = ng, sk = (size_t)ng * ng;
+    const size_t o = (size_t)(id - 1) * bsz, c0 = ix3(ng, i, j, (kq - 1) * K + 1);
+    const double *x = phi + o;
+    double z[K + 2], xm[K], xp[K], ym[K], yp[K], r[K];
+#pragma unroll
+    for (int q = 0; q < K + 2; q++) z[q] = x[c0 + (q - 1) * sk];
+#pragma unroll
+    for (int q = 0; q < K; q++) {
+      const size_t c = c0 + q * sk;
+      xm[q] = x[c - 1];
+      xp[q] = x[c + 1];
+      ym[q] = x[c - sj];
+      yp[q] = x[c + sj];
+      r[q] = rhs[o + c];
+    }
+#pragma unroll
+    for (int q = 0; q < K; q++) {
+      // apply7 operand order
+      const double a = cf.c[0] * z[q + 1] + cf.c[1] * xm[q] + cf.c[2] * xp[q] +
+                       cf.c[3] * ym[q] + cf.c[4] * yp[q] + cf.c[5] * z[q] +
+                       cf.c[6] * z[q + 2];
+      const double v = r[q] - a;
+      tmp[o + c0 + q * sk] = v;
+      mx = fmax(mx, fabs(v));
+    }
   }
   if (MAX) block_max_to_shard(mx, red);
 }
@@ -343,7 +377,8 @@ __global__ void k_rstr_fas(double *__restrict__ phi,
   if (t >= hn * hn * hn) return;
   const int id = ids[blockIdx.y];
   const afh_box_meta &m = meta[id - 1];
-  const int i = t % hn + 1, j = (t / hn) % hn + 1, k = t / (hn * hn) + 1;
+  int i, j, k;
+  cell3(t, hn, i, j, k);
   const int ng = nc + 2;
   const size_t sj = ng, sk = (size_t)ng * ng;
   const size_t o = (size_t)(id - 1) * bsz;
@@ -376,7 +411,8 @@ __global__ void k_parent_rhs(const double *__restrict__ phi,
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= ng * ng * ng) return;
   const int id = ids[blockIdx.y];
-  const int i = t % ng, j = (t / ng) % ng, k = t / (ng * ng);
+  int i, j, k;
+  cell3g(t, ng, i, j, k);
   const size_t o = (size_t)(id - 1) * bsz, c = ix3(ng, i, j, k);
   double rv = rhs[o + c];
   if (i >= 1 && i <= nc && j >= 1 && j <= nc && k >= 1 && k <= nc)
@@ -405,31 +441,52 @@ __global__ void k_box_copy(const double *__restrict__ src,
   dst[o] = src ? src[o] : 0.0;
 }
 
-__global__ void k_prolong(double *__restrict__ phi,
-                          const double *__restrict__ tmp,
-                          const afh_box_meta *__restrict__ meta,
-                          const int32_t *__restrict__ ids, int nc, size_t bsz) {
+// stencil_prolong_248 add, a column of K cells along k per thread: the
+// K/2 + 2 parent planes the column touches are loaded once (4 values each)
+template <int K>
+__global__ void __launch_bounds__(256)
+    k_prolong(double *__restrict__ phi, const double *__restrict__ tmp,
+              const afh_box_meta *__restrict__ meta,
+              const int32_t *__restrict__ ids, int nc, size_t bsz) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= nc * nc * nc) return;
+  if (t >= nc * nc * (nc / K)) return;
   const int id = ids[blockIdx.y];
   const afh_box_meta &m = meta[id - 1];
-  const int i = t % nc + 1, j = (t / nc) % nc + 1, k = t / (nc * nc) + 1;
+  int i, j, kq;
+  cell3(t, nc, i, j, kq);
+  const int k0 = (kq - 1) * K + 1;  // odd
   const int ng = nc + 2, hn = nc >> 1;
+  const size_t sk = (size_t)ng * ng;
   const int o0 = ((m.ix[0] - 1) & 1) * hn, o1 = ((m.ix[1] - 1) & 1) * hn,
             o2 = ((m.ix[2] - 1) & 1) * hn;
   const int i1 = o0 + ((i + 1) >> 1), i2 = i1 + 1 - 2 * (i & 1);
   const int j1 = o1 + ((j + 1) >> 1), j2 = j1 + 1 - 2 * (j & 1);
-  const int k1 = o2 + ((k + 1) >> 1), k2 = k1 + 1 - 2 * (k & 1);
+  const int P = o2 + ((k0 + 1) >> 1);  // k1 of the first (odd) cell
   const double *p = tmp + (size_t)(m.parent - 1) * bsz;
-  const size_t c = (size_t)(id - 1) * bsz + ix3(ng, i, j, k);
-  phi[c] = phi[c] + (27 / 64.0) * p[ix3(ng, i1, j1, k1)] +
-           (9 / 64.0) * p[ix3(ng, i2, j1, k1)] +
-           (9 / 64.0) * p[ix3(ng, i1, j2, k1)] +
-           (3 / 64.0) * p[ix3(ng, i2, j2, k1)] +
-           (9 / 64.0) * p[ix3(ng, i1, j1, k2)] +
-           (3 / 64.0) * p[ix3(ng, i2, j1, k2)] +
-           (3 / 64.0) * p[ix3(ng, i1, j2, k2)] +
-           (1 / 64.0) * p[ix3(ng, i2, j2, k2)];
+  const size_t c = (size_t)(id - 1) * bsz + ix3(ng, i, j, k0);
+  // parent planes P-1 .. P+K/2, values at (i1,j1), (i2,j1), (i1,j2), (i2,j2)
+  double pv[K / 2 + 2][4], ph[K];
+#pragma unroll
+  for (int q = 0; q < K / 2 + 2; q++) {
+    const size_t b = ix3(ng, 0, 0, P - 1 + q);
+    pv[q][0] = p[b + (size_t)j1 * ng + i1];
+    pv[q][1] = p[b + (size_t)j1 * ng + i2];
+    pv[q][2] = p[b + (size_t)j2 * ng + i1];
+    pv[q][3] = p[b + (size_t)j2 * ng + i2];
+  }
+#pragma unroll
+  for (int q = 0; q < K; q++) ph[q] = phi[c + q * sk];
+#pragma unroll
+  for (int q = 0; q < K; q++) {
+    // cell k0+q: odd q -> (k1, k2) = planes (P+(q-1)/2, P+(q+1)/2);
+    // even q -> (P+q/2, P+q/2-1); a, b index pv from plane P-1
+    const int a = (q & 1) ? (q + 1) / 2 : q / 2 + 1;
+    const int b = (q & 1) ? (q + 3) / 2 : q / 2;
+    phi[c + q * sk] = ph[q] + (27 / 64.0) * pv[a][0] + (9 / 64.0) * pv[a][1] +
+                      (9 / 64.0) * pv[a][2] + (3 / 64.0) * pv[a][3] +
+                      (9 / 64.0) * pv[b][0] + (3 / 64.0) * pv[b][1] +
+                      (3 / 64.0) * pv[b][2] + (1 / 64.0) * pv[b][3];
+  }
 }
 
 // mg_box_lpl_gradient (fc = fac/dr * (phi_i - phi_i-1)) + mg_box_field_norm
@@ -1407,10 +1464,16 @@ static int32_t correct_children(afh_mg *mg, int lvl) {
   }
   const int nid = t->ids.n(lvl);
   if (nid) {
-    hipLaunchKernelGGL(k_prolong, dim3((nc * nc * nc + 255) / 256, nid),
-                       dim3(256), 0, t->stream, t->ccv(mg->d.i_phi),
-                       t->ccv(mg->d.i_tmp), t->d_boxes, t->ids.at(lvl), nc,
-                       t->bsz);
+    const int K = nc % 4 == 0 ? 4 : 2;
+    const dim3 grid((nc * nc * (nc / K) + 255) / 256, nid);
+    if (K == 4)
+      hipLaunchKernelGGL(k_prolong<4>, grid, dim3(256), 0, t->stream,
+                         t->ccv(mg->d.i_phi), t->ccv(mg->d.i_tmp), t->d_boxes,
+                         t->ids.at(lvl), nc, t->bsz);
+    else
+      hipLaunchKernelGGL(k_prolong<2>, grid, dim3(256), 0, t->stream,
+                         t->ccv(mg->d.i_phi), t->ccv(mg->d.i_tmp), t->d_boxes,
+                         t->ids.at(lvl), nc, t->bsz);
     AFH_LAUNCH_CHECK("k_prolong");
   }
   return AFH_OK;
@@ -1551,15 +1614,14 @@ static int32_t residual_levels(afh_mg *mg, int max_lvl, double *max_out) {
       if (!max_out && part) break;
       const int n = L.n(lvl);
       if (!n) continue;
-      const dim3 grid((n3 + 255) / 256, n);
-      if (max_out && !part)
-        hipLaunchKernelGGL(k_residual<true>, grid, dim3(256), 0, t->stream,
-                           t->ccv(mg->d.i_phi), t->ccv(mg->d.i_rhs),
-                           t->ccv(mg->d.i_tmp), L.at(lvl), nc, t->bsz, cf, red);
-      else
-        hipLaunchKernelGGL(k_residual<false>, grid, dim3(256), 0, t->stream,
-                           t->ccv(mg->d.i_phi), t->ccv(mg->d.i_rhs),
-                           t->ccv(mg->d.i_tmp), L.at(lvl), nc, t->bsz, cf, red);
+      const bool k4 = nc % 4 == 0;
+      const dim3 grid((n3 / (k4 ? 4 : 2) + 255) / 256, n);
+      const bool mx = max_out && !part;
+      auto kern = mx ? (k4 ? k_residual<true, 4> : k_residual<true, 2>)
+                     : (k4 ? k_residual<false, 4> : k_residual<false, 2>);
+      hipLaunchKernelGGL(kern, grid, dim3(256), 0, t->stream,
+                         t->ccv(mg->d.i_phi), t->ccv(mg->d.i_rhs),
+                         t->ccv(mg->d.i_tmp), L.at(lvl), nc, t->bsz, cf, red);
       AFH_LAUNCH_CHECK("k_residual");
     }
   }

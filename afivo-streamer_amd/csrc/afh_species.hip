@@ -109,7 +109,8 @@ __global__ void __launch_bounds__(256)
     for (int s = 0; s < A.n; s++) r = r + A.q[s] * A.sp[s][o];
     rhs[o] = r;
     if (MAX) {
-      const int tt = (int)t, i = tt % ng, j = (tt / ng) % ng, k = tt / (ng * ng);
+      int i, j, k;
+      cell3g((int)t, ng, i, j, k);
       if (i >= 1 && i < ng - 1 && j >= 1 && j < ng - 1 && k >= 1 && k < ng - 1)
         mx = fabs(r);
     }
@@ -129,7 +130,14 @@ __global__ void k_gc2(double *__restrict__ v, double *__restrict__ gc2,
   const int d = (nb - 1) >> 1;
   const bool low = ((nb - 1) & 1) == 0;
   const int ta = (d == 0) ? 1 : 0, tb = (d == 2) ? 1 : 2;
-  const int a = t % nc + 1, b = t / nc + 1;
+  int a, b;
+  if ((nc & (nc - 1)) == 0) {
+    a = (t & (nc - 1)) + 1;
+    b = (t >> __builtin_ctz(nc)) + 1;
+  } else {
+    a = t % nc + 1;
+    b = t / nc + 1;
+  }
   const int ng = nc + 2;
   const afh_box_meta &m = meta[id - 1];
   double *c = v + (size_t)(id - 1) * bsz;
@@ -307,7 +315,8 @@ __global__ void __launch_bounds__(256)
   const bool active = t < nc * nc * nc;
   const int tt = active ? t : 0;
   const int id = ids[blockIdx.y];
-  const int i = tt % nc + 1, j = (tt / nc) % nc + 1, k = tt / (nc * nc) + 1;
+  int i, j, k;
+  cell3(tt, nc, i, j, k);
   const int ng = nc + 2, nf = nc + 1;
   const double *__restrict__ ne = A.ne + (size_t)(id - 1) * bsz;
   const double *__restrict__ E = A.E + (size_t)(id - 1) * bsz;
@@ -670,7 +679,8 @@ __global__ void __launch_bounds__(256)
   const int id = ids[blockIdx.y];
   double cmin = 1e100;
   if (t < nc * nc * nc) {
-    const int i = t % nc + 1, j = (t / nc) % nc + 1, k = t / (nc * nc) + 1;
+    int i, j, k;
+    cell3(t, nc, i, j, k);
     const int ng = nc + 2, nf = nc + 1;
     const size_t x = (size_t)(id - 1) * bsz + (size_t)((k * ng + j) * ng + i);
     double y[NS], der[NS], dens[NS];

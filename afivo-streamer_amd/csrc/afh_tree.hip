@@ -66,7 +66,14 @@ __global__ void k_gc_faces(double *__restrict__ v,
   const int d = (nb - 1) >> 1;
   const bool low = ((nb - 1) & 1) == 0;
   const int ta = (d == 0) ? 1 : 0, tb = (d == 2) ? 1 : 2;
-  const int a = t % nc + 1, b = t / nc + 1;
+  int a, b;
+  if ((nc & (nc - 1)) == 0) {
+    a = (t & (nc - 1)) + 1;
+    b = (t >> __builtin_ctz(nc)) + 1;
+  } else {
+    a = t % nc + 1;
+    b = t / nc + 1;
+  }
   const int ng = nc + 2;
   const afh_box_meta &m = meta[id - 1];
   double *c = v + (size_t)(id - 1) * bsz;
@@ -247,7 +254,8 @@ __global__ void k_restrict(double *__restrict__ v,
   if (t >= hnc * hnc * hnc) return;
   const int id = ids[blockIdx.y];
   const afh_box_meta &m = meta[id - 1];
-  const int i = t % hnc + 1, j = (t / hnc) % hnc + 1, k = t / (hnc * hnc) + 1;
+  int i, j, k;
+  cell3(t, hnc, i, j, k);
   const int ng = nc + 2;
   const double *c = v + (size_t)(id - 1) * bsz;
   double *p = v + (size_t)(m.parent - 1) * bsz;
@@ -332,7 +340,8 @@ __global__ void k_maxabs(const double *__restrict__ v,
   double mx = 0.0;
   for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < n3;
        t += gridDim.x * blockDim.x) {
-    const int i = t % nc + 1, j = (t / nc) % nc + 1, k = t / (nc * nc) + 1;
+    int i, j, k;
+    cell3(t, nc, i, j, k);
     mx = fmax(mx, fabs(c[ix3(ng, i, j, k)]));
   }
   for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
