@@ -13,7 +13,9 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.dirname(HERE)
 REPO = os.path.dirname(PKG)
-HIP_LIB = os.path.join(PKG, "csrc", "libafivo_hip.so")
+# AFH_HIP_LIB: an alternative build of the same library (A/B timing of
+# kernel variants on one box, scripts/ab.sh)
+HIP_LIB = os.environ.get("AFH_HIP_LIB") or os.path.join(PKG, "csrc", "libafivo_hip.so")
 ORACLE_LIB = os.path.join(REPO, "oracle", "lib", "libafo.so")
 
 AFH_OK = 0

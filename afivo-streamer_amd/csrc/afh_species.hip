@@ -86,6 +86,21 @@ __device__ __forceinline__ double limiter(int lim, double a, double b) {
   }
 }
 
+// limiter with a compile-time choice (LIM = AFH_LIM_KOREN, the reference's
+// flux limiter) or the runtime switch (LIM = 0)
+template <int LIM>
+__device__ __forceinline__ double limiter_t(int lim, double a, double b) {
+  if (LIM == AFH_LIM_KOREN) {
+    const double third = 1 / 3.0;
+    const double aa = a * a, ab = a * b;
+    if (ab <= 0) return 0;
+    if (aa <= 0.25 * ab) return 2 * a;
+    if (aa <= 2.5 * ab) return third * (b + 2 * a);
+    return 2 * b;
+  }
+  return limiter(lim, a, b);
+}
+
 // ------------------------------------------------------------ rhs
 struct RhsArgs {
   int n;
@@ -306,11 +321,19 @@ __device__ __forceinline__ void lt_loc(const DevLT &lt, double x, int &low,
 // (2) the table rows of all faces are fetched together; (3) limiter, flux,
 // CFL. Same expressions in the same order as face_eval / face_vd, so the
 // results are bitwise those of k_flux (which issued one memory round trip per
-// face and table lookup).
-template <bool SHFL>
-__global__ void __launch_bounds__(256)
+// face and table lookup). The CFL sum of a cell needs the transport of its
+// high faces: x from the next lane (SHFL), y from the next row of the
+// workgroup through LDS (the workgroup's last row and the box's last row
+// evaluate it), z evaluated here.
+// minimum waves per SIMD the flux kernel is compiled for (register budget)
+#ifndef AFH_FLUX_MINW
+#define AFH_FLUX_MINW 4
+#endif
+template <bool SHFL, int LIM>
+__global__ void __launch_bounds__(256, AFH_FLUX_MINW)
     k_flux_staged(FluxArgs A, const int32_t *__restrict__ ids, int nc, size_t bsz,
                   size_t fsz, unsigned long long *red) {
+  __shared__ double s_v[256], s_d[256];
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   const bool active = t < nc * nc * nc;
   const int tt = active ? t : 0;
@@ -331,6 +354,13 @@ __global__ void __launch_bounds__(256)
   const int fst[3] = {1, nf, nf * nf};
   const int gq[3] = {(k - 1) * nc + (j - 1), (k - 1) * nc + (i - 1),
                      (j - 1) * nc + (i - 1)};
+  // y partner: the cell of the next row is in this workgroup
+  const bool y_lds = j < nc && (int)threadIdx.x + nc < (int)blockDim.x;
+  // a high face is evaluated here: box edge, or no partner to take it from
+  bool need_hi[3];
+  need_hi[0] = i == nc || !SHFL;
+  need_hi[1] = !y_lds;
+  need_hi[2] = true;
 
   // (1) loads
   double L[3][5], Em[3], Ep[3], ex_lo[3], ex_hi[3];
@@ -344,18 +374,20 @@ __global__ void __launch_bounds__(256)
     L[d][3] = ne[c0 + st[d]];
     L[d][4] = (c == nc) ? g2[(2 * d + 1) * nc * nc + gq[d]] : 0.0;
     Em[d] = E[c0 - st[d]];
-    Ep[d] = E[c0 + st[d]];
+    Ep[d] = need_hi[d] ? E[c0 + st[d]] : 0.0;
     ex_lo[d] = Ef[d * fd + fcell];
-    ex_hi[d] = Ef[d * fd + fcell + fst[d]];
+    ex_hi[d] = need_hi[d] ? Ef[d * fd + fcell + fst[d]] : 0.0;
   }
   // (2) table rows: low face of every dimension, high face where needed
-  // (box boundary; y and z for the CFL sum; x comes from the next lane)
   int lo_row[3], hi_row[3];
   double lo_lf[3], hi_lf[3];
 #pragma unroll
   for (int d = 0; d < 3; d++) {
     lt_loc(A.td, 0.5 * (Em[d] + E0) * 1e21 * A.N_inv, lo_row[d], lo_lf[d]);
-    lt_loc(A.td, 0.5 * (E0 + Ep[d]) * 1e21 * A.N_inv, hi_row[d], hi_lf[d]);
+    if (need_hi[d])
+      lt_loc(A.td, 0.5 * (E0 + Ep[d]) * 1e21 * A.N_inv, hi_row[d], hi_lf[d]);
+    else
+      hi_row[d] = 1, hi_lf[d] = 0.0;
   }
   const int np = A.td.n_points;
   double lo_r[3][4], hi_r[3][4];
@@ -363,8 +395,7 @@ __global__ void __launch_bounds__(256)
   for (int d = 0; d < 3; d++) {
     const double *r = A.td.rc + (lo_row[d] - 1);
     lo_r[d][0] = r[0], lo_r[d][1] = r[1], lo_r[d][2] = r[np], lo_r[d][3] = r[np + 1];
-    const bool need_hi = (cc[d] == nc) || d > 0 || !SHFL;
-    if (need_hi) {
+    if (need_hi[d]) {
       const double *h = A.td.rc + (hi_row[d] - 1);
       hi_r[d][0] = h[0], hi_r[d][1] = h[1], hi_r[d][2] = h[np], hi_r[d][3] = h[np + 1];
     } else {
@@ -373,51 +404,59 @@ __global__ void __launch_bounds__(256)
   }
   // (3) fluxes and CFL (face_eval / face_vd arithmetic)
   double cfl = 0.0, smax = -HUGE_VAL;
+  auto finish = [&](const double rr[4], double lf, double ex, double &v,
+                    double &dc) {
+    double mu = lf * rr[0] + (1 - lf) * rr[1];
+    const double dd = lf * rr[2] + (1 - lf) * rr[3];
+    mu = mu * A.N_inv;
+    dc = dd * A.N_inv;
+    v = -mu * ex;
+    return mu;
+  };
+  auto upwind = [&](double Lm2, double Lm1, double Lc, double Lp1, double ex) {
+    if (-1 * ex > 0) return Lm1 + 0.5 * limiter_t<LIM>(A.lim, Lc - Lm1, Lm1 - Lm2);
+    return Lc - 0.5 * limiter_t<LIM>(A.lim, Lc - Lm1, Lp1 - Lc);
+  };
+  double vl[3], dl[3];
+#pragma unroll
+  for (int d = 0; d < 3; d++) {
+    const double u = upwind(L[d][0], L[d][1], L[d][2], L[d][3], ex_lo[d]);
+    const double mu = finish(lo_r[d], lo_lf[d], ex_lo[d], vl[d], dl[d]);
+    const double flux = vl[d] * u - dl[d] * A.inv_dx[d] * (L[d][2] - L[d][1]);
+    if (active) F[d * fd + fcell] = flux;
+    smax = fmax(smax, mu * u);
+  }
+  // x partner by lane shuffle: executed by every lane (a shuffle reading an
+  // inactive lane returns 0, so never inside the divergent branch below)
+  double vsh = 0, dsh = 0;
+  if (SHFL) {
+    vsh = __shfl_down(vl[0], 1, 64);
+    dsh = __shfl_down(dl[0], 1, 64);
+  }
+  s_v[threadIdx.x] = vl[1];
+  s_d[threadIdx.x] = dl[1];
+  __syncthreads();
 #pragma unroll
   for (int d = 0; d < 3; d++) {
     const double inv_dx = A.inv_dx[d];
-    const int fb = d * fd + fcell;
-    auto finish = [&](const double rr[4], double lf, double ex, double &v,
-                      double &dc) {
-      double mu = lf * rr[0] + (1 - lf) * rr[1];
-      const double dd = lf * rr[2] + (1 - lf) * rr[3];
-      mu = mu * A.N_inv;
-      dc = dd * A.N_inv;
-      v = -mu * ex;
-      return mu;
-    };
-    auto upwind = [&](double Lm2, double Lm1, double Lc, double Lp1, double ex) {
-      if (-1 * ex > 0) return Lm1 + 0.5 * limiter(A.lim, Lc - Lm1, Lm1 - Lm2);
-      return Lc - 0.5 * limiter(A.lim, Lc - Lm1, Lp1 - Lc);
-    };
-    double vl, dl;
-    {
-      const double u = upwind(L[d][0], L[d][1], L[d][2], L[d][3], ex_lo[d]);
-      const double mu = finish(lo_r[d], lo_lf[d], ex_lo[d], vl, dl);
-      const double flux = vl * u - dl * inv_dx * (L[d][2] - L[d][1]);
-      if (active) F[fb] = flux;
-      smax = fmax(smax, mu * u);
-    }
-    double vsh = 0, dsh = 0;
-    if (SHFL && d == 0) {
-      vsh = __shfl_down(vl, 1, 64);
-      dsh = __shfl_down(dl, 1, 64);
-    }
     double vh, dh;
     if (cc[d] == nc) {
       const double u = upwind(L[d][1], L[d][2], L[d][3], L[d][4], ex_hi[d]);
       const double mu = finish(hi_r[d], hi_lf[d], ex_hi[d], vh, dh);
       const double flux = vh * u - dh * inv_dx * (L[d][3] - L[d][2]);
-      if (active) F[fb + fst[d]] = flux;
+      if (active) F[d * fd + fcell + fst[d]] = flux;
       smax = fmax(smax, mu * u);
-    } else if (SHFL && d == 0) {
+    } else if (d == 0 && SHFL) {
       vh = vsh;
       dh = dsh;
+    } else if (d == 1 && y_lds) {
+      vh = s_v[threadIdx.x + nc];
+      dh = s_d[threadIdx.x + nc];
     } else {
       finish(hi_r[d], hi_lf[d], ex_hi[d], vh, dh);
     }
-    const double mv = fmax(fabs(vh), fabs(vl));
-    const double md = fmax(dh, dl);
+    const double mv = fmax(fabs(vh), fabs(vl[d]));
+    const double md = fmax(dh, dl[d]);
     cfl = cfl + (1.0 * mv * inv_dx + 2 * md * (inv_dx * inv_dx));
   }
   if (!active) cfl = smax = -HUGE_VAL;
@@ -976,12 +1015,13 @@ int32_t afh_flux_upwind_tree(afh_fluid *f, int32_t s_deriv, double *dt_lim) {
       case 32: launch_flux_march<32>(t, A, l, red); break;
       default: launch_flux_march<64>(t, A, l, red); break;
       }
-    } else if (shfl)
-      hipLaunchKernelGGL(k_flux_staged<true>, dim3((n3 + 255) / 256, n), dim3(256), 0,
+    } else {
+      const bool koren = A.lim == AFH_LIM_KOREN;
+      auto kern = shfl ? (koren ? k_flux_staged<true, AFH_LIM_KOREN> : k_flux_staged<true, 0>)
+                       : (koren ? k_flux_staged<false, AFH_LIM_KOREN> : k_flux_staged<false, 0>);
+      hipLaunchKernelGGL(kern, dim3((n3 + 255) / 256, n), dim3(256), 0,
                          t->stream, A, t->leaves.at(l), nc, t->bsz, t->fsz, red);
-    else
-      hipLaunchKernelGGL(k_flux_staged<false>, dim3((n3 + 255) / 256, n), dim3(256), 0,
-                         t->stream, A, t->leaves.at(l), nc, t->bsz, t->fsz, red);
+    }
     // read n_e, |E|, 3 face fields; write 3 fluxes = 64 B/cell
     prof_end(t, AFH_PROF_FLUX, 64.0 * n3 * n);
     AFH_LAUNCH_CHECK("k_flux");
