@@ -680,6 +680,7 @@ struct DevReaction {
 
 struct UpdArgs {
   int ns, nr, n_prev, last_step, e_index;  // e_index: species slot of the flux species
+  int der_q;  // s_deriv == s_prev[der_q] (the derivative state is read once), or -1
   double w_prev[MAXPREV];
   const double *prev[MAXS][MAXPREV];
   const double *der[MAXS];
@@ -722,17 +723,36 @@ __global__ void __launch_bounds__(256)
     cell3(t, nc, i, j, k);
     const int ng = nc + 2, nf = nc + 1;
     const size_t x = (size_t)(id - 1) * bsz + (size_t)((k * ng + j) * ng + i);
+    // every load first (fluxes, |E|, states), then the arithmetic
+    const double *F = A.F + (size_t)(id - 1) * fsz;
+    const int f0 = ((k - 1) * nf + (j - 1)) * nf + (i - 1);
+    const int d3 = nf * nf * nf;
+    const double fx0 = F[f0], fx1 = F[f0 + 1], fy0 = F[d3 + f0], fy1 = F[d3 + f0 + nf],
+                 fz0 = F[2 * d3 + f0], fz1 = F[2 * d3 + f0 + nf * nf];
+    const double ev = A.E[x];
+    double pv[NS][MAXPREV], dv[NS];
+#pragma unroll
+    for (int s = 0; s < NS; s++) {
+#pragma unroll
+      for (int q = 0; q < MAXPREV; q++) pv[s][q] = q < A.n_prev ? A.prev[s][q][x] : 0.0;
+      dv[s] = A.der_q >= 0 ? 0.0 : A.der[s][x];
+    }
     double y[NS], der[NS], dens[NS];
 #pragma unroll
     for (int s = 0; s < NS; s++) {
       double tmp = 0.0;
-      for (int q = 0; q < A.n_prev; q++) tmp = tmp + A.w_prev[q] * A.prev[s][q][x];
+#pragma unroll
+      for (int q = 0; q < MAXPREV; q++)
+        if (q < A.n_prev) tmp = tmp + A.w_prev[q] * pv[s][q];
       y[s] = tmp;
-      const double v = A.der[s][x];
+      double v = dv[s];
+#pragma unroll
+      for (int q = 0; q < MAXPREV; q++)
+        if (q == A.der_q) v = pv[s][q];
       dens[s] = v > 0.0 ? v : 0.0;  // max(dens, 0.0_dp)
       der[s] = 0.0;
     }
-    const double field = 1e21 * A.inv_N * A.E[x];
+    const double field = 1e21 * A.inv_N * ev;
     for (int r = 0; r < A.nr; r++) {
       const DevReaction &R = A.reac[r];
       const double c0 = R.rate_factor;
@@ -777,14 +797,9 @@ __global__ void __launch_bounds__(256)
     }
 #pragma unroll
     for (int s = 0; s < NS; s++) y[s] = y[s] + A.dt * der[s];
-    // (loading the fluxes up front costs 12 VGPRs and occupancy 8 -> 6:
-    // measured slower)
-    const double *F = A.F + (size_t)(id - 1) * fsz;
-    const int f0 = ((k - 1) * nf + (j - 1)) * nf + (i - 1);
-    const int d3 = nf * nf * nf;
-    const double div = A.dt_dr[0] * (F[f0] - F[f0 + 1]);
-    const double dvy = A.dt_dr[1] * (F[d3 + f0] - F[d3 + f0 + nf]);
-    const double dvz = A.dt_dr[2] * (F[2 * d3 + f0] - F[2 * d3 + f0 + nf * nf]);
+    const double div = A.dt_dr[0] * (fx0 - fx1);
+    const double dvy = A.dt_dr[1] * (fy0 - fy1);
+    const double dvz = A.dt_dr[2] * (fz0 - fz1);
 #pragma unroll
     for (int s = 0; s < NS; s++)
       if (s == A.e_index) y[s] = y[s] + div + dvy + dvz;
@@ -1060,6 +1075,9 @@ int32_t afh_flux_update_densities(afh_fluid *f, double dt, int32_t s_deriv,
   A.n_prev = n_prev;
   A.last_step = last_step ? 1 : 0;
   A.e_index = f->e_index;
+  A.der_q = -1;
+  for (int q = 0; q < n_prev; q++)
+    if (s_prev[q] == s_deriv && A.der_q < 0) A.der_q = q;
   for (int q = 0; q < n_prev; q++) A.w_prev[q] = w_prev[q];
   for (int s = 0; s < A.ns; s++) {
     const int iv = f->d.species_iv[s];
