@@ -314,6 +314,198 @@ __global__ void __launch_bounds__((RbGeom<NC, TJ>::NT)) __attribute__((amdgpu_wa
   }
 }
 
+// Whole-box form of k_gsrb_pair with a parity mapping: in step s thread t
+// owns the same RPT (i, j) columns for the red cells of plane s (phase A)
+// and the black cells of plane s-1 (phase C) -- i = 2 ih + 1 + ((j + s) & 1)
+// -- so every lane works in both phases (the column mapping of k_gsrb_pair
+// idles half the lanes in each). Black cells are updated in place in LDS and
+// plane s-1 is then written in full rows (phase E). Same arithmetic in the
+// same order as k_gsrb_pair: bitwise identical results.
+template <int NC, int TJ = NC>
+struct RbPar {
+  static constexpr int NG = NC + 2, HN = NC / 2;
+  static constexpr int NTILE = NC / TJ;
+  static constexpr int NRED = TJ * HN;                      // red cells per tile plane
+  static constexpr int NTMAX = TJ == NC ? 1024 : 512;       // tiles: 2 workgroups per CU
+  static constexpr int NT = NRED >= NTMAX ? NTMAX : NRED;
+  static constexpr int RPT = NRED / NT;                     // red cells per thread
+  static constexpr int PL = (TJ + 2) * NG;                  // LDS plane (rows j0-1..j1+1)
+  static constexpr int EPT = (PL + NT - 1) / NT;            // plane entries per thread
+  static constexpr int OPT = (NC * TJ + NT - 1) / NT;       // stored cells per thread
+};
+
+// Parity-mapped form of k_gsrb_pair: in step s thread t owns the same RPT
+// (i, j) columns for the red cells of plane s (phase A) and the black cells
+// of plane s-1 (phase C) -- i = 2 ih + 1 + ((j + s) & 1) -- so every lane
+// works in both phases (the column mapping of k_gsrb_pair idles half the
+// lanes in each). Black cells are updated in place in LDS and plane s-1 is
+// then written in full rows (phase E). A workgroup holds TJ rows of a box
+// (TJ < NC: 512-thread workgroups, two per CU, halo rows recomputed as in
+// k_gsrb_pair). Same arithmetic in the same order as k_gsrb_pair: bitwise
+// identical results.
+template <int NC, int TJ>
+__global__ void __launch_bounds__((RbPar<NC, TJ>::NT)) __attribute__((amdgpu_waves_per_eu(4)))
+    k_gsrb_pair2(const double *__restrict__ src, double *__restrict__ dst,
+                 const double *__restrict__ rhs, const double *__restrict__ coarse,
+                 const afh_box_meta *__restrict__ meta,
+                 const int32_t *__restrict__ ids, size_t bsz, Coef cf,
+                 double inv_c1, GcArgs ga) {
+  using G = RbPar<NC, TJ>;
+  constexpr int NG = G::NG, HN = G::HN, NT = G::NT, RPT = G::RPT, PL = G::PL,
+                EPT = G::EPT, OPT = G::OPT;
+  constexpr size_t SK = (size_t)NG * NG;
+  __shared__ double P[4][PL];  // planes s-2 .. s+1 at slot (plane & 3)
+  const int tid = threadIdx.x;
+  const int id = ids[blockIdx.x / G::NTILE];
+  const int j0 = (blockIdx.x % G::NTILE) * TJ + 1, j1 = j0 + TJ - 1;
+  const afh_box_meta &m = meta[id - 1];
+  const double *x = src + (size_t)(id - 1) * bsz;
+  double *y = dst + (size_t)(id - 1) * bsz;
+  const double *r = rhs + (size_t)(id - 1) * bsz;
+  const size_t t0 = (size_t)(j0 - 1) * NG;  // first LDS row in a plane
+  // owned column q in step s: (i, j), LDS index (j - j0 + 1) * NG + i
+  auto col = [&](int q, int s, int &i, int &j) {
+    const int rr = tid + NT * q;
+    j = j0 + rr / HN;
+    i = 2 * (rr % HN) + 1 + ((j + s) & 1);
+    return (j - j0 + 1) * NG + i;
+  };
+
+  // planes 0..2 -> LDS; rhs of the red cells of plane 1
+  for (int e = tid; e < 3 * PL; e += NT)
+    P[e / PL][e % PL] = x[(size_t)(e / PL) * SK + t0 + e % PL];
+  double rR[RPT], rB[RPT];
+#pragma unroll
+  for (int q = 0; q < RPT; q++) {
+    int i, j;
+    col(q, 1, i, j);
+    rR[q] = r[SK + (size_t)j * NG + i];
+    rB[q] = 0.0;
+  }
+  __syncthreads();
+
+  for (int s = 1; s <= NC + 1; s++) {
+    // prefetch: plane s+2 of phi; rhs of plane s+1 (red, step s+1's A) and
+    // of plane s (black, step s+1's C), both at step s+1's columns
+    double nx[EPT], nR[RPT], nB[RPT];
+#pragma unroll
+    for (int e = 0; e < EPT; e++) {
+      const int xx = tid + NT * e;
+      nx[e] = (s + 2 <= NC + 1 && xx < PL) ? x[(size_t)(s + 2) * SK + t0 + xx] : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < RPT; q++) {
+      int i, j;
+      col(q, s + 1, i, j);
+      const size_t g = (size_t)j * NG + i;
+      nR[q] = s + 1 <= NC ? r[(size_t)(s + 1) * SK + g] : 0.0;
+      nB[q] = s <= NC ? r[(size_t)s * SK + g] : 0.0;
+    }
+    double *Pm = P[(s - 1) & 3], *P0 = P[s & 3], *Pp = P[(s + 1) & 3];
+    double *Pmm = P[(s - 2) & 3];
+    // A: red cells of plane s
+    if (s <= NC) {
+#pragma unroll
+      for (int q = 0; q < RPT; q++) {
+        int i, j;
+        const int c = col(q, s, i, j);
+        P0[c] = (rR[q] - cf.c[1] * P0[c - 1] - cf.c[2] * P0[c + 1] -
+                 cf.c[3] * P0[c - NG] - cf.c[4] * P0[c + NG] - cf.c[5] * Pm[c] -
+                 cf.c[6] * Pp[c]) *
+                inv_c1;
+      }
+    }
+    __syncthreads();
+    // B: red values around the tile: x ghost cells of its rows; the halo
+    // rows (ghost row of the box, or the red cells of the adjacent tile
+    // recomputed from src)
+    if (s <= NC) {
+      for (int u = tid; u < TJ + NC; u += NT) {
+        int i, j, jl;
+        double v;
+        if (u < TJ) {
+          j = j0 + u;
+          jl = u + 1;
+          i = ((j + s) & 1) ? 0 : NC + 1;
+          const int nb = i == 0 ? 1 : 2;
+          v = pair_ghost<NC>(src, coarse, rhs, meta, m, nb, i, j, s, j, s, bsz,
+                             cf, inv_c1, ga.bc[nb - 1], ga.rb,
+                             P0[jl * NG + (i == 0 ? 1 : NC)],
+                             P0[jl * NG + (i == 0 ? 2 : NC - 1)]);
+        } else {
+          const bool lo = u - TJ < HN;
+          j = lo ? j0 - 1 : j1 + 1;
+          jl = lo ? 0 : TJ + 1;
+          i = 2 - ((1 ^ (s + j)) & 1) + 2 * ((u - TJ) % HN);
+          if (j == 0 || j == NC + 1) {
+            const int nb = j == 0 ? 3 : 4;
+            const int l1 = j == 0 ? 1 : TJ, l2 = j == 0 ? 2 : TJ - 1;
+            v = pair_ghost<NC>(src, coarse, rhs, meta, m, nb, i, j, s, i, s, bsz,
+                               cf, inv_c1, ga.bc[nb - 1], ga.rb, P0[l1 * NG + i],
+                               P0[l2 * NG + i]);
+          } else {
+            v = gs_cell(x, r, ix3(NG, i, j, s), NG, SK, cf, inv_c1);
+          }
+        }
+        P0[jl * NG + i] = v;
+      }
+    }
+    if (s == 2 || s == NC + 1) {
+      // z ghost plane 0 (NC+1): red cells; x1 = plane 1 (NC), black, old;
+      // x2 = plane 2 (NC-1), red, new
+      const int nb = s == 2 ? 5 : 6, k = s == 2 ? 0 : NC + 1;
+      double *Pg = s == 2 ? Pmm : P0;
+      const double *X2 = s == 2 ? P0 : Pmm;
+#pragma unroll
+      for (int q = 0; q < RPT; q++) {
+        int i, j;
+        const int c = col(q, k, i, j);
+        Pg[c] = pair_ghost<NC>(src, coarse, rhs, meta, m, nb, i, j, k, i, j, bsz,
+                               cf, inv_c1, ga.bc[nb - 1], ga.rb, Pm[c], X2[c]);
+      }
+    }
+    __syncthreads();
+    // C: black cells of plane s-1, in place
+    if (s >= 2) {
+#pragma unroll
+      for (int q = 0; q < RPT; q++) {
+        int i, j;
+        const int c = col(q, s, i, j);
+        Pm[c] = (rB[q] - cf.c[1] * Pm[c - 1] - cf.c[2] * Pm[c + 1] -
+                 cf.c[3] * Pm[c - NG] - cf.c[4] * Pm[c + NG] - cf.c[5] * Pmm[c] -
+                 cf.c[6] * P0[c]) *
+                inv_c1;
+      }
+    }
+    __syncthreads();
+    // E: plane s-1 of the tile to dst in full rows; D: plane s+2 into the
+    // slot of plane s-2
+    if (s >= 2) {
+#pragma unroll
+      for (int q = 0; q < OPT; q++) {
+        const int e = tid + NT * q;
+        if (e < NC * TJ) {
+          const int c = (e / NC + 1) * NG + e % NC + 1;
+          y[(size_t)(s - 1) * SK + t0 + c] = Pm[c];
+        }
+      }
+    }
+    if (s + 2 <= NC + 1) {
+#pragma unroll
+      for (int e = 0; e < EPT; e++) {
+        const int xx = tid + NT * e;
+        if (xx < PL) Pmm[xx] = nx[e];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < RPT; q++) {
+      rR[q] = nR[q];
+      rB[q] = nB[q];
+    }
+    __syncthreads();
+  }
+}
+
 __device__ __forceinline__ double apply7(const double *x, size_t c, size_t sj,
                                          size_t sk, const Coef &cf) {
   return cf.c[0] * x[c] + cf.c[1] * x[c - 1] + cf.c[2] * x[c + 1] +
@@ -1087,6 +1279,8 @@ struct afh_mg {
   // (default: enough boxes for one workgroup per CU, 256 tiles)
   int fused_min = 0;
   bool force_tiles = false;  // AFH_GSRB_TILES
+  bool pair_v1 = false;      // AFH_GSRB_PAIR_V1: column-mapped whole-box kernel
+  int pair_tj = 0;           // AFH_GSRB_PAIR_TJ=32: half-box tiles (NC = 64)
   int wave_cells = CS_WAVE_CELLS;  // AFH_CS_WAVE_CELLS
   // AFH_COARSE_DIRECT: eigenvectors Q and Q^T per dim, eigenvalues, work
   double *d_q[3] = {nullptr, nullptr, nullptr}, *d_qt[3] = {nullptr, nullptr, nullptr};
@@ -1262,6 +1456,8 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
     // 64 boxes (NC >= 32); smaller levels keep the split half-sweeps
     mg->fused_min = t->nc >= 32 ? 64 : 256;
   if (const char *env = getenv("AFH_GSRB_TILES")) mg->force_tiles = atoi(env) != 0;
+  if (const char *env = getenv("AFH_GSRB_PAIR_V1")) mg->pair_v1 = atoi(env) != 0;
+  if (const char *env = getenv("AFH_GSRB_PAIR_TJ")) mg->pair_tj = atoi(env);
   if (const char *env = getenv("AFH_CS_WAVE_CELLS")) mg->wave_cells = atoi(env);
   if (fused_nc_ok(t->nc) && mg->fused_min > 0) {
     bool any = false;
@@ -1341,10 +1537,30 @@ static bool pair_tiles(const afh_mg *mg, int lvl) {
 template <int NC>
 static void launch_pair(afh_mg *mg, int lvl, const double *src, double *dst,
                         const Coef &cf, double inv_c1) {
-  if (mg->t->ids.n(lvl) == 0) return;
+  afh_tree *t = mg->t;
+  if (t->ids.n(lvl) == 0) return;
   if constexpr (NC >= 32) {
     if (pair_tiles(mg, lvl))
       return launch_pair_t<NC, NC / 4>(mg, lvl, src, dst, cf, inv_c1);
+  }
+  if constexpr (NC >= 16) {
+    if (!mg->pair_v1) {
+      if constexpr (NC == 64) {
+        if (mg->pair_tj == 32) {
+          hipLaunchKernelGGL((k_gsrb_pair2<NC, 32>), dim3(t->ids.n(lvl) * 2),
+                             dim3(RbPar<NC, 32>::NT), 0, t->stream, src, dst,
+                             t->ccv(mg->d.i_rhs), t->ccv(mg->d.i_phi), t->d_boxes,
+                             t->ids.at(lvl), t->bsz, cf, inv_c1,
+                             t->gc_args(mg->d.i_phi));
+          return;
+        }
+      }
+      hipLaunchKernelGGL((k_gsrb_pair2<NC, NC>), dim3(t->ids.n(lvl)),
+                         dim3(RbPar<NC, NC>::NT), 0, t->stream, src, dst,
+                         t->ccv(mg->d.i_rhs), t->ccv(mg->d.i_phi), t->d_boxes,
+                         t->ids.at(lvl), t->bsz, cf, inv_c1, t->gc_args(mg->d.i_phi));
+      return;
+    }
   }
   launch_pair_t<NC, NC>(mg, lvl, src, dst, cf, inv_c1);
 }

@@ -97,6 +97,10 @@ TOPOS = {
     "uni16_l3": lambda: uniform_tree(16, (16, 16, 16), (2e-3, 2e-3, 2e-3), 3),
     "uni8_l4_2x1x1": lambda: uniform_tree(8, (16, 8, 8), (2e-3, 1e-3, 1e-3), 4),
     "uni64_l2": lambda: uniform_tree(64, (64, 64, 64), (4e-3, 4e-3, 4e-3), 2),
+    "uni32_l2": lambda: uniform_tree(32, (32, 32, 32), (2e-3, 2e-3, 2e-3), 2),
+    "amr16": lambda: build_tree(
+        16, (32, 32, 32), (2e-3, 2e-3, 2e-3), 2,
+        refine=lambda lvl, r0, r1: lvl < 3 and np.all(r0 < 1.2e-3) and np.all(r1 > 0.7e-3)),
     "amr8": lambda: build_tree(
         8, (16, 16, 16), (2e-3, 2e-3, 2e-3), 2,
         refine=lambda lvl, r0, r1: lvl < 4 and np.all(r0 < 1.2e-3) and np.all(r1 > 0.7e-3)),
