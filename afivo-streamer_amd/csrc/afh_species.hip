@@ -476,61 +476,167 @@ __global__ void __launch_bounds__(256, AFH_FLUX_MINW)
   }
 }
 
-// Plane-marching variant of k_flux_staged for NC in {8, 16, 32, 64}: a workgroup
-// owns a tile of TJ rows (j) of a box, one thread per (i, j) column, and
-// marches over k. Every face is evaluated once (low faces; high faces on the
-// box boundary). The CFL sum of a cell needs the transport of its high faces
-// too: x from the next lane (__shfl_down), y from the next row through LDS
-// (the tile's last row recomputes it, face_vd), z from the next plane (the
-// x+y part of the sum is carried one step). Same expressions, same operand
-// order as k_flux: bitwise identical fluxes and limits.
+// LDS-staged plane-marching flux (NC in {16, 32, 64}): a workgroup owns TJ
+// rows of a box and marches over k. Each step stages plane k of n_e (rows
+// j0-2 .. j0+TJ+1, columns -1 .. NC+2, second ghost layers from gc2) and of
+// |E| (rows j0-1 .. j0+TJ) in LDS, double-buffered and prefetched one plane
+// ahead; the transport table (mobility, diffusion interleaved per row) lives
+// in LDS for the whole march. The z stencil comes from a register window of
+// the thread's own column. Every face is evaluated once (low faces; high
+// faces on the box boundary); the CFL sum takes the high-face transport from
+// the next lane (x), the next row through LDS (y; the tile's last row looks
+// it up) and the next plane (z: the x+y part is carried one step). The
+// per-cell global loads of k_flux_staged (~40 vector-memory instructions per
+// cell, the texture addresser ~80 % busy) become ~12. Same expressions in the
+// same operand order: bitwise identical fluxes and limits.
 template <int NC>
-struct FluxGeom {
+struct FluxLds {
   static constexpr int TJ = 256 / NC < NC ? 256 / NC : NC;  // rows per tile
-  static constexpr int NT = NC * TJ;
+  static constexpr int NT = NC * TJ;                       // 256
   static constexpr int NTILE = NC / TJ;
+  static constexpr int RW = NC + 4;                        // n_e row: i = -1 .. NC+2
+  static constexpr int NR = TJ + 4;                        // rows j0-2 .. j0+TJ+1
+  static constexpr int EW = NC + 2;                        // |E| row: i = 0 .. NC+1
+  static constexpr int ER = TJ + 2;                        // rows j0-1 .. j0+TJ
+  static constexpr int NPE = (NR * RW + NT - 1) / NT;      // staged n_e per thread
+  static constexpr int EPE = (ER * EW + NT - 1) / NT;      // staged |E| per thread
 };
+constexpr int FLUX_LDS_MAX_POINTS = 2048;  // transport table rows held in LDS
 
-template <int NC>
-__global__ void __launch_bounds__(FluxGeom<NC>::NT)
-    k_flux_march(FluxArgs A, const int32_t *__restrict__ ids, size_t bsz,
-                 size_t fsz, unsigned long long *red) {
-  using G = FluxGeom<NC>;
-  constexpr int NG = NC + 2, NF = NC + 1, TJ = G::TJ;
+template <int LIM>
+__device__ __forceinline__ double upwind_t(int lim, double Lm2, double Lm1,
+                                           double L0, double Lp1, double ex) {
+  if (-1 * ex > 0) return Lm1 + 0.5 * limiter_t<LIM>(lim, L0 - Lm1, Lm1 - Lm2);
+  return L0 - 0.5 * limiter_t<LIM>(lim, L0 - Lm1, Lp1 - L0);
+}
+
+// LT_get_loc + LT_get_col for mobility and diffusion from the interleaved LDS
+// table T[2 r] = mu N (row r+1), T[2 r + 1] = D N (lt_mu_dc order)
+__device__ __forceinline__ void lds_mu_dc(const double *T, const DevLT &lt,
+                                          double x, double &mu, double &dc) {
+  int low;
+  double lf;
+  lt_loc(lt, x, low, lf);
+  const double *r = T + 2 * (low - 1);
+  mu = lf * r[0] + (1 - lf) * r[2];
+  dc = lf * r[1] + (1 - lf) * r[3];
+}
+
+template <int NC, int LIM>
+__global__ void __launch_bounds__(256)
+    k_flux_lds(FluxArgs A, const double *__restrict__ tdi,
+               const int32_t *__restrict__ ids, size_t bsz, size_t fsz,
+               unsigned long long *red) {
+  using G = FluxLds<NC>;
+  constexpr int NG = NC + 2, NF = NC + 1, TJ = G::TJ, NT = G::NT, RW = G::RW,
+                NR = G::NR, EW = G::EW, ER = G::ER, NPE = G::NPE, EPE = G::EPE;
   constexpr size_t SK = (size_t)NG * NG, FSK = (size_t)NF * NF;
   constexpr size_t FD = (size_t)NF * NF * NF;
-  __shared__ double sv[G::NT], sd[G::NT];
-  __shared__ double r1[G::NT / 64 + 1], r2[G::NT / 64 + 1];
+  constexpr int NN = NC * NC;
+  __shared__ double T[2 * FLUX_LDS_MAX_POINTS];
+  __shared__ double SN[2][NR * RW], SE[2][ER * EW];
+  __shared__ double sv[NT], sd[NT];
+  __shared__ double r1[NT / 64], r2[NT / 64];
   const int tid = threadIdx.x;
   const int id = ids[blockIdx.x / G::NTILE];
   const int i = tid % NC + 1;
-  const int jr = tid / NC;  // row within the tile
-  const int j = (blockIdx.x % G::NTILE) * TJ + jr + 1;
+  const int jr = tid / NC;
+  const int j0 = (blockIdx.x % G::NTILE) * TJ + 1, j = j0 + jr;
   const double *ne = A.ne + (size_t)(id - 1) * bsz;
   const double *E = A.E + (size_t)(id - 1) * bsz;
   const double *Ef = A.Ef + (size_t)(id - 1) * fsz;
   double *F = A.F + (size_t)(id - 1) * fsz;
-  const double *g2 = A.gc2 + (size_t)(id - 1) * 6 * NC * NC;
+  const double *g2 = A.gc2 + (size_t)(id - 1) * 6 * NN;
   const double ix = A.inv_dx[0], iy = A.inv_dx[1], iz = A.inv_dx[2];
-  const size_t cc = (size_t)j * NG + i;                    // column, plane 0
-  const size_t fcol = (size_t)(j - 1) * NF + (i - 1);      // face column
-  const int gq_z = (j - 1) * NC + (i - 1);
-  // z window of this column: ne at k-2 .. k+1, |E| at k-1, k
-  double zm2 = g2[4 * NC * NC + gq_z];  // ne(k-2) for k = 1: 2nd ghost layer
-  double zm1 = ne[cc], z0 = ne[SK + cc], zp1 = ne[2 * SK + cc];
-  double em1 = E[cc], e0 = E[SK + cc];
-  double cfl_xy = 0, vz_lo = 0, dz_lo = 0;  // previous plane's x+y sum, z-low
+  const double N_inv = A.N_inv;
+  const int np = A.td.n_points;
+  for (int e = tid; e < 2 * np; e += NT) T[e] = tdi[e];
+
+  // staged value e of plane k: n_e (rows j0-2 .. j0+TJ+1, cols -1 .. NC+2)
+  auto ne_at = [&](int k, int e) -> double {
+    if (e >= NR * RW) return 0.0;
+    const int jj = j0 - 2 + e / RW, ii = e % RW - 1;
+    const bool jin = jj >= 0 && jj <= NC + 1, iin = ii >= 0 && ii <= NC + 1;
+    if (jin && iin) return ne[((size_t)k * NG + jj) * NG + ii];
+    if (jin && jj >= 1 && jj <= NC) {  // x second ghost layer
+      if (ii == -1) return g2[0 * NN + (k - 1) * NC + (jj - 1)];
+      if (ii == NC + 2) return g2[1 * NN + (k - 1) * NC + (jj - 1)];
+    }
+    if (iin && ii >= 1 && ii <= NC) {  // y second ghost layer
+      if (jj == -1) return g2[2 * NN + (k - 1) * NC + (ii - 1)];
+      if (jj == NC + 2) return g2[3 * NN + (k - 1) * NC + (ii - 1)];
+    }
+    return 0.0;
+  };
+  auto e_at = [&](int k, int e) -> double {
+    if (e >= ER * EW) return 0.0;
+    return E[((size_t)k * NG + (j0 - 1 + e / EW)) * NG + e % EW];
+  };
+  // own column (i, j): n_e window k-2 .. k+1 and |E| at k-1, k+1
+  const size_t cc = (size_t)j * NG + i;
+  const size_t fcol = (size_t)(j - 1) * NF + (i - 1);
+  const int gz = (j - 1) * NC + (i - 1);
+  double zm2 = g2[4 * NN + gz], zm1 = ne[cc], zp1 = ne[2 * SK + cc];
+  double em1 = E[cc];
+  // plane 1 into LDS buffer 1
+#pragma unroll
+  for (int q = 0; q < NPE; q++) {
+    const int e = tid + NT * q;
+    if (e < NR * RW) SN[1][e] = ne_at(1, e);
+  }
+#pragma unroll
+  for (int q = 0; q < EPE; q++) {
+    const int e = tid + NT * q;
+    if (e < ER * EW) SE[1][e] = e_at(1, e);
+  }
+  // face fields of plane 1
+  double exl = Ef[fcol], eyl = Ef[FD + fcol], ezl = Ef[2 * FD + fcol];
+  double exh = i == NC ? Ef[fcol + 1] : 0.0;
+  double eyh = (jr == TJ - 1) ? Ef[FD + fcol + NF] : 0.0;
+  __syncthreads();
+
+  // LDS indices of the own cell in the staged planes
+  const int cn = (jr + 2) * RW + (i + 1);  // n_e
+  const int ce = (jr + 1) * EW + i;        // |E|
+  double cfl_xy = 0, vz_lo = 0, dz_lo = 0;
   double cmax = -HUGE_VAL, smax = -HUGE_VAL;
 
   for (int k = 1; k <= NC; k++) {
-    const size_t c0 = (size_t)k * SK + cc;
+    const double *N0 = SN[k & 1], *E0p = SE[k & 1];
+    // prefetch plane k+1 (staging) and the own column / faces of step k+1
+    double pn[NPE], pe[EPE];
+    const bool more = k < NC;
+#pragma unroll
+    for (int q = 0; q < NPE; q++) pn[q] = more ? ne_at(k + 1, tid + NT * q) : 0.0;
+#pragma unroll
+    for (int q = 0; q < EPE; q++) pe[q] = more ? e_at(k + 1, tid + NT * q) : 0.0;
+    const size_t fbn = (size_t)k * FSK + fcol;  // faces of plane k+1
+    const double zp2 = k + 2 <= NC + 1 ? ne[(size_t)(k + 2) * SK + cc]
+                                       : g2[5 * NN + gz];  // k = NC: 2nd layer
+    const double ep1 = E[(size_t)(k + 1) * SK + cc];
+    double nexl = 0, neyl = 0, nezl = 0, nexh = 0, neyh = 0;
+    const double ezh = k == NC ? Ef[2 * FD + (size_t)NC * FSK + fcol] : 0.0;
+    if (more) {
+      nexl = Ef[fbn];
+      neyl = Ef[FD + fbn];
+      nezl = Ef[2 * FD + fbn];
+      if (i == NC) nexh = Ef[fbn + 1];
+      if (jr == TJ - 1) neyh = Ef[FD + fbn + NF];
+    }
     const size_t fb = (size_t)(k - 1) * FSK + fcol;
-    // z low face of cell k (between k-1 and k)
-    double vz, dz, fz, sz;
-    face_eval(A, zm2, zm1, z0, zp1, em1, e0, Ef[2 * FD + fb], iz, vz, dz, fz, sz);
-    F[2 * FD + fb] = fz;
-    smax = fmax(smax, sz);
-    // finish the CFL sum of cell k-1 (its z-high face is this one)
+    const double z0 = N0[cn], e0 = E0p[ce];
+    double mu, dcv;
+    // z low face of cell k
+    double vz, dz;
+    {
+      const double u = upwind_t<LIM>(A.lim, zm2, zm1, z0, zp1, ezl);
+      lds_mu_dc(T, A.td, 0.5 * (em1 + e0) * 1e21 * N_inv, mu, dcv);
+      mu = mu * N_inv;
+      dz = dcv * N_inv;
+      vz = -mu * ezl;
+      F[2 * FD + fb] = vz * u - dz * iz * (z0 - zm1);
+      smax = fmax(smax, mu * u);
+    }
     if (k > 1) {
       const double mv = fmax(fabs(vz), fabs(vz_lo));
       const double md = fmax(dz, dz_lo);
@@ -538,33 +644,38 @@ __global__ void __launch_bounds__(FluxGeom<NC>::NT)
     }
     vz_lo = vz;
     dz_lo = dz;
-    // x low face of cell i
-    double vx, dx, fx, sx;
+    // x low face
+    double vx, dx;
     {
-      const double Lm2 = (i == 1) ? g2[0 * NC * NC + (k - 1) * NC + (j - 1)] : ne[c0 - 2];
-      face_eval(A, Lm2, ne[c0 - 1], z0, ne[c0 + 1], E[c0 - 1], e0, Ef[fb], ix,
-                vx, dx, fx, sx);
-      F[fb] = fx;
-      smax = fmax(smax, sx);
+      const double u = upwind_t<LIM>(A.lim, N0[cn - 2], N0[cn - 1], z0, N0[cn + 1], exl);
+      lds_mu_dc(T, A.td, 0.5 * (E0p[ce - 1] + e0) * 1e21 * N_inv, mu, dcv);
+      mu = mu * N_inv;
+      dx = dcv * N_inv;
+      vx = -mu * exl;
+      F[fb] = vx * u - dx * ix * (z0 - N0[cn - 1]);
+      smax = fmax(smax, mu * u);
     }
     double vxh = __shfl_down(vx, 1, 64), dxh = __shfl_down(dx, 1, 64);
     if (i == NC) {
-      const double Lp2 = g2[1 * NC * NC + (k - 1) * NC + (j - 1)];
-      double fh, sh;
-      face_eval(A, ne[c0 - 1], z0, ne[c0 + 1], Lp2, e0, E[c0 + 1], Ef[fb + 1],
-                ix, vxh, dxh, fh, sh);
-      F[fb + 1] = fh;
-      smax = fmax(smax, sh);
+      const double u = upwind_t<LIM>(A.lim, N0[cn - 1], z0, N0[cn + 1], N0[cn + 2], exh);
+      lds_mu_dc(T, A.td, 0.5 * (e0 + E0p[ce + 1]) * 1e21 * N_inv, mu, dcv);
+      mu = mu * N_inv;
+      dxh = dcv * N_inv;
+      vxh = -mu * exh;
+      F[fb + 1] = vxh * u - dxh * ix * (N0[cn + 1] - z0);
+      smax = fmax(smax, mu * u);
     }
-    // y low face of row j
-    double vy, dy, fy, sy;
+    // y low face
+    double vy, dy;
     {
-      const double Lm2 = (j == 1) ? g2[2 * NC * NC + (k - 1) * NC + (i - 1)]
-                                  : ne[c0 - 2 * NG];
-      face_eval(A, Lm2, ne[c0 - NG], z0, ne[c0 + NG], E[c0 - NG], e0,
-                Ef[FD + fb], iy, vy, dy, fy, sy);
-      F[FD + fb] = fy;
-      smax = fmax(smax, sy);
+      const double u = upwind_t<LIM>(A.lim, N0[cn - 2 * RW], N0[cn - RW], z0,
+                                     N0[cn + RW], eyl);
+      lds_mu_dc(T, A.td, 0.5 * (E0p[ce - EW] + e0) * 1e21 * N_inv, mu, dcv);
+      mu = mu * N_inv;
+      dy = dcv * N_inv;
+      vy = -mu * eyl;
+      F[FD + fb] = vy * u - dy * iy * (z0 - N0[cn - RW]);
+      smax = fmax(smax, mu * u);
     }
     sv[tid] = vy;
     sd[tid] = dy;
@@ -574,16 +685,20 @@ __global__ void __launch_bounds__(FluxGeom<NC>::NT)
       vyh = sv[tid + NC];
       dyh = sd[tid + NC];
     } else if (j == NC) {
-      const double Lp2 = g2[3 * NC * NC + (k - 1) * NC + (i - 1)];
-      double fh, sh;
-      face_eval(A, ne[c0 - NG], z0, ne[c0 + NG], Lp2, e0, E[c0 + NG],
-                Ef[FD + fb + NF], iy, vyh, dyh, fh, sh);
-      F[FD + fb + NF] = fh;
-      smax = fmax(smax, sh);
+      const double u = upwind_t<LIM>(A.lim, N0[cn - RW], z0, N0[cn + RW],
+                                     N0[cn + 2 * RW], eyh);
+      lds_mu_dc(T, A.td, 0.5 * (e0 + E0p[ce + EW]) * 1e21 * N_inv, mu, dcv);
+      mu = mu * N_inv;
+      dyh = dcv * N_inv;
+      vyh = -mu * eyh;
+      F[FD + fb + NF] = vyh * u - dyh * iy * (N0[cn + RW] - z0);
+      smax = fmax(smax, mu * u);
     } else {
-      face_vd(A, e0, E[c0 + NG], Ef[FD + fb + NF], vyh, dyh);
+      lds_mu_dc(T, A.td, 0.5 * (e0 + E0p[ce + EW]) * 1e21 * N_inv, mu, dcv);
+      mu = mu * N_inv;
+      dyh = dcv * N_inv;
+      vyh = -mu * eyh;
     }
-    __syncthreads();  // sv/sd are rewritten next plane
     {
       const double mvx = fmax(fabs(vxh), fabs(vx)), mdx = fmax(dxh, dx);
       const double mvy = fmax(fabs(vyh), fabs(vy)), mdy = fmax(dyh, dy);
@@ -592,27 +707,37 @@ __global__ void __launch_bounds__(FluxGeom<NC>::NT)
       c = c + (1.0 * mvy * iy + 2 * mdy * (iy * iy));
       cfl_xy = c;
     }
-    // advance the z window
-    const double zp2 = k + 2 <= NC + 1 ? ne[c0 + 2 * SK] : 0.0;
-    const double ep1 = E[c0 + SK];
     if (k == NC) {
       // z high face of the box (between NC and NC+1)
-      const double Lp2 = g2[5 * NC * NC + gq_z];
-      double vh, dh, fh, sh;
-      face_eval(A, zm1, z0, zp1, Lp2, e0, ep1,
-                Ef[2 * FD + fb + FSK], iz, vh, dh, fh, sh);
-      F[2 * FD + fb + FSK] = fh;
-      smax = fmax(smax, sh);
+      const double u = upwind_t<LIM>(A.lim, zm1, z0, zp1, zp2, ezh);
+      lds_mu_dc(T, A.td, 0.5 * (e0 + ep1) * 1e21 * N_inv, mu, dcv);
+      mu = mu * N_inv;
+      const double dh = dcv * N_inv, vh = -mu * ezh;
+      F[2 * FD + fb + FSK] = vh * u - dh * iz * (zp1 - z0);
+      smax = fmax(smax, mu * u);
       const double mv = fmax(fabs(vh), fabs(vz_lo));
       const double md = fmax(dh, dz_lo);
       cmax = fmax(cmax, cfl_xy + (1.0 * mv * iz + 2 * md * (iz * iz)));
     }
+    // plane k+1 into the other buffer; advance the windows
+    if (more) {
+#pragma unroll
+      for (int q = 0; q < NPE; q++) {
+        const int e = tid + NT * q;
+        if (e < NR * RW) SN[(k + 1) & 1][e] = pn[q];
+      }
+#pragma unroll
+      for (int q = 0; q < EPE; q++) {
+        const int e = tid + NT * q;
+        if (e < ER * EW) SE[(k + 1) & 1][e] = pe[q];
+      }
+    }
     zm2 = zm1;
     zm1 = z0;
-    z0 = zp1;
     zp1 = zp2;
     em1 = e0;
-    e0 = ep1;
+    exl = nexl, eyl = neyl, ezl = nezl, exh = nexh, eyh = neyh;
+    __syncthreads();
   }
   for (int o = 32; o > 0; o >>= 1) {
     cmax = fmax(cmax, __shfl_xor(cmax, o, 64));
@@ -622,8 +747,7 @@ __global__ void __launch_bounds__(FluxGeom<NC>::NT)
   if (lane == 0) r1[w] = cmax, r2[w] = smax;
   __syncthreads();
   if (tid == 0) {
-    for (int q = 1; q < (G::NT + 63) / 64; q++)
-      cmax = fmax(cmax, r1[q]), smax = fmax(smax, r2[q]);
+    for (int q = 1; q < NT / 64; q++) cmax = fmax(cmax, r1[q]), smax = fmax(smax, r2[q]);
     atomicMax(&red[red_shard()], dbl_to_ord(cmax));
     atomicMax(&red[RED_SHARDS + red_shard()], dbl_to_ord(smax));
   }
@@ -839,23 +963,21 @@ struct afh_fluid {
   DevReaction *d_reac = nullptr;
   int e_index = -1;
   DevLT td, chem;
-  // AFH_FLUX_MARCH=1 selects k_flux_march (measured slower on MI355X for
-  // S1-64: 4.24 ms vs 3.78 ms for k_flux per leaf level)
-  bool march = false;
+  // k_flux_lds: transport table interleaved per row (mu N, D N); unset when
+  // the table does not fit LDS or AFH_FLUX_STAGED=1 selects k_flux_staged
+  double *d_tdi = nullptr;
 };
 
 extern "C" {
 
 int32_t afh_fluid_create(afh_tree *t, const afh_fluid_desc *d, afh_fluid **out) {
   if (!t || !d || !out) return set_error(AFH_ERR_ARG, "afh_fluid_create: null");
-  const char *march_env = getenv("AFH_FLUX_MARCH");
   if (d->n_species < 1 || d->n_species > MAXS || d->n_reactions < 0 ||
       d->n_reactions > AFH_MAX_REACTIONS)
     return set_error(AFH_ERR_ARG, "bad species/reaction count");
   if (d->td.n_points < 2 || d->td.n_cols < 2 || !d->td.rows_cols)
     return set_error(AFH_ERR_ARG, "transport table needs mobility + diffusion");
   afh_fluid *f = new afh_fluid();
-  f->march = march_env && atoi(march_env) != 0;
   f->t = t;
   f->d = *d;
   for (int s = 0; s < d->n_species; s++) {
@@ -875,6 +997,18 @@ int32_t afh_fluid_create(afh_tree *t, const afh_fluid_desc *d, afh_fluid **out) 
   if (nch)
     AFH_HIP(hipMemcpy(f->d_chem, d->chem.rows_cols, nch * sizeof(double),
                       hipMemcpyHostToDevice));
+  const char *staged_env = getenv("AFH_FLUX_STAGED");
+  if (d->td.n_points <= FLUX_LDS_MAX_POINTS && !(staged_env && atoi(staged_env))) {
+    const int n = d->td.n_points;
+    std::vector<double> ti(2 * (size_t)n);
+    for (int r = 0; r < n; r++) {
+      ti[2 * r] = d->td.rows_cols[r];
+      ti[2 * r + 1] = d->td.rows_cols[n + r];
+    }
+    AFH_HIP(hipMalloc(&f->d_tdi, ti.size() * sizeof(double)));
+    AFH_HIP(hipMemcpy(f->d_tdi, ti.data(), ti.size() * sizeof(double),
+                      hipMemcpyHostToDevice));
+  }
   std::vector<DevReaction> R(std::max(1, d->n_reactions));
   for (int r = 0; r < d->n_reactions; r++) {
     const afh_reaction &a = d->reactions[r];
@@ -911,6 +1045,7 @@ int32_t afh_fluid_destroy(afh_fluid *f) {
   hipFree(f->d_td);
   hipFree(f->d_chem);
   hipFree(f->d_reac);
+  hipFree(f->d_tdi);
   delete f;
   return AFH_OK;
 }
@@ -968,12 +1103,15 @@ int32_t afh_field_set_rhs_maxabs(afh_fluid *f, int32_t i_rhs, int32_t s_in,
 }  // extern "C"
 
 template <int NC>
-static void launch_flux_march(afh_tree *t, const FluxArgs &A, int l,
-                              unsigned long long *red) {
-  hipLaunchKernelGGL(k_flux_march<NC>,
-                     dim3(t->leaves.n(l) * FluxGeom<NC>::NTILE),
-                     dim3(FluxGeom<NC>::NT), 0, t->stream, A, t->leaves.at(l),
-                     t->bsz, t->fsz, red);
+static void launch_flux_lds(afh_tree *t, const FluxArgs &A, const double *tdi,
+                            int l, unsigned long long *red) {
+  const dim3 grid(t->leaves.n(l) * FluxLds<NC>::NTILE);
+  if (A.lim == AFH_LIM_KOREN)
+    hipLaunchKernelGGL((k_flux_lds<NC, AFH_LIM_KOREN>), grid, dim3(FluxLds<NC>::NT),
+                       0, t->stream, A, tdi, t->leaves.at(l), t->bsz, t->fsz, red);
+  else
+    hipLaunchKernelGGL((k_flux_lds<NC, 0>), grid, dim3(FluxLds<NC>::NT), 0,
+                       t->stream, A, tdi, t->leaves.at(l), t->bsz, t->fsz, red);
 }
 
 extern "C" {
@@ -1023,12 +1161,11 @@ int32_t afh_flux_upwind_tree(afh_fluid *f, int32_t s_deriv, double *dt_lim) {
     if (!n) continue;
     for (int q = 0; q < 3; q++) A.inv_dx[q] = 1 / t->lvl_dr[3 * (l - 1) + q];
     prof_begin(t, AFH_PROF_FLUX);
-    if (f->march && (nc == 64 || nc == 32 || nc == 16 || nc == 8)) {
+    if (f->d_tdi && (nc == 64 || nc == 32 || nc == 16)) {
       switch (nc) {
-      case 8: launch_flux_march<8>(t, A, l, red); break;
-      case 16: launch_flux_march<16>(t, A, l, red); break;
-      case 32: launch_flux_march<32>(t, A, l, red); break;
-      default: launch_flux_march<64>(t, A, l, red); break;
+      case 16: launch_flux_lds<16>(t, A, f->d_tdi, l, red); break;
+      case 32: launch_flux_lds<32>(t, A, f->d_tdi, l, red); break;
+      default: launch_flux_lds<64>(t, A, f->d_tdi, l, red); break;
       }
     } else {
       const bool koren = A.lim == AFH_LIM_KOREN;
