@@ -522,8 +522,11 @@ __device__ __forceinline__ void lds_mu_dc(const double *T, const DevLT &lt,
   dc = lf * r[1] + (1 - lf) * r[3];
 }
 
+#ifndef AFH_FLUX_LDS_MINW
+#define AFH_FLUX_LDS_MINW 4
+#endif
 template <int NC, int LIM>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256, AFH_FLUX_LDS_MINW)
     k_flux_lds(FluxArgs A, const double *__restrict__ tdi,
                const int32_t *__restrict__ ids, size_t bsz, size_t fsz,
                unsigned long long *red) {
@@ -533,7 +536,7 @@ __global__ void __launch_bounds__(256)
   constexpr size_t SK = (size_t)NG * NG, FSK = (size_t)NF * NF;
   constexpr size_t FD = (size_t)NF * NF * NF;
   constexpr int NN = NC * NC;
-  __shared__ double T[2 * FLUX_LDS_MAX_POINTS];
+  extern __shared__ double T[];  // 2 n_points (dynamic)
   __shared__ double SN[2][NR * RW], SE[2][ER * EW];
   __shared__ double sv[NT], sd[NT];
   __shared__ double r1[NT / 64], r2[NT / 64];
@@ -1106,11 +1109,12 @@ template <int NC>
 static void launch_flux_lds(afh_tree *t, const FluxArgs &A, const double *tdi,
                             int l, unsigned long long *red) {
   const dim3 grid(t->leaves.n(l) * FluxLds<NC>::NTILE);
+  const size_t lds = 2 * sizeof(double) * A.td.n_points;
   if (A.lim == AFH_LIM_KOREN)
     hipLaunchKernelGGL((k_flux_lds<NC, AFH_LIM_KOREN>), grid, dim3(FluxLds<NC>::NT),
-                       0, t->stream, A, tdi, t->leaves.at(l), t->bsz, t->fsz, red);
+                       lds, t->stream, A, tdi, t->leaves.at(l), t->bsz, t->fsz, red);
   else
-    hipLaunchKernelGGL((k_flux_lds<NC, 0>), grid, dim3(FluxLds<NC>::NT), 0,
+    hipLaunchKernelGGL((k_flux_lds<NC, 0>), grid, dim3(FluxLds<NC>::NT), lds,
                        t->stream, A, tdi, t->leaves.at(l), t->bsz, t->fsz, red);
 }
 
