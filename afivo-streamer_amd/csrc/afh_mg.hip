@@ -374,20 +374,27 @@ __global__ void __launch_bounds__((RbPar<NC, TJ>::NT)) __attribute__((amdgpu_wav
   // planes 0..2 -> LDS; rhs of the red cells of plane 1
   for (int e = tid; e < 3 * PL; e += NT)
     P[e / PL][e % PL] = x[(size_t)(e / PL) * SK + t0 + e % PL];
-  double rR[RPT], rB[RPT];
+  // rhs in registers: rR red cells of plane s, rB black cells of plane s-1,
+  // rBn black cells of plane s (step s+1). Both parities of a plane are
+  // loaded in the same step (adjacent cells 2 ih + 1, 2 ih + 2 of a row), so
+  // each rhs line is fetched once.
+  double rR[RPT], rB[RPT], rBn[RPT];
 #pragma unroll
   for (int q = 0; q < RPT; q++) {
-    int i, j;
-    col(q, 1, i, j);
-    rR[q] = r[SK + (size_t)j * NG + i];
+    const int rr = tid + NT * q;
+    const int j = j0 + rr / HN, i1 = 2 * (rr % HN) + 1;
+    const double lo = r[SK + (size_t)j * NG + i1], hi = r[SK + (size_t)j * NG + i1 + 1];
+    const bool odd = (j + 1) & 1;  // red cell of plane 1 is i1 + 1
+    rR[q] = odd ? hi : lo;
+    rBn[q] = odd ? lo : hi;
     rB[q] = 0.0;
   }
   __syncthreads();
 
   for (int s = 1; s <= NC + 1; s++) {
-    // prefetch: plane s+2 of phi; rhs of plane s+1 (red, step s+1's A) and
-    // of plane s (black, step s+1's C), both at step s+1's columns
-    double nx[EPT], nR[RPT], nB[RPT];
+    // prefetch: plane s+2 of phi; rhs of plane s+1, both parities (red for
+    // step s+1's A, black for step s+2's C)
+    double nx[EPT], nlo[RPT], nhi[RPT];
 #pragma unroll
     for (int e = 0; e < EPT; e++) {
       const int xx = tid + NT * e;
@@ -395,11 +402,11 @@ __global__ void __launch_bounds__((RbPar<NC, TJ>::NT)) __attribute__((amdgpu_wav
     }
 #pragma unroll
     for (int q = 0; q < RPT; q++) {
-      int i, j;
-      col(q, s + 1, i, j);
-      const size_t g = (size_t)j * NG + i;
-      nR[q] = s + 1 <= NC ? r[(size_t)(s + 1) * SK + g] : 0.0;
-      nB[q] = s <= NC ? r[(size_t)s * SK + g] : 0.0;
+      const int rr = tid + NT * q;
+      const int j = j0 + rr / HN, i1 = 2 * (rr % HN) + 1;
+      const size_t g = (size_t)(s + 1) * SK + (size_t)j * NG + i1;
+      nlo[q] = s + 1 <= NC ? r[g] : 0.0;
+      nhi[q] = s + 1 <= NC ? r[g + 1] : 0.0;
     }
     double *Pm = P[(s - 1) & 3], *P0 = P[s & 3], *Pp = P[(s + 1) & 3];
     double *Pmm = P[(s - 2) & 3];
@@ -499,8 +506,11 @@ __global__ void __launch_bounds__((RbPar<NC, TJ>::NT)) __attribute__((amdgpu_wav
     }
 #pragma unroll
     for (int q = 0; q < RPT; q++) {
-      rR[q] = nR[q];
-      rB[q] = nB[q];
+      const int j = j0 + (tid + NT * q) / HN;
+      const bool odd = (j + s + 1) & 1;  // red cell of plane s+1 is i1 + 1
+      rB[q] = rBn[q];
+      rR[q] = odd ? nhi[q] : nlo[q];
+      rBn[q] = odd ? nlo[q] : nhi[q];
     }
     __syncthreads();
   }
