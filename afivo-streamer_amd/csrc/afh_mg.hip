@@ -392,6 +392,56 @@ __global__ void __launch_bounds__((RbPar<NC, TJ>::NT)) __attribute__((amdgpu_wav
   __syncthreads();
 
   for (int s = 1; s <= NC + 1; s++) {
+    // B inputs first (older than the plane prefetch, so phase B waits only
+    // for them): thread u < TJ + NC owns one red ghost value of plane s. A
+    // same-level neighbour's red boundary cell (or, for tiles, the adjacent
+    // tile's red cell) is 6 neighbour values and an rhs value, loaded now;
+    // physical / refinement faces are evaluated in B (gc_face_nocopy).
+    double bl[7];
+    int b_i = 0, b_j = 0, b_jl = 0, b_nb = 0, b_rep = -1;  // b_nb 0: none
+    bool b_pre = false;
+    if (s <= NC && tid < TJ + NC) {
+      const int u = tid;
+      if (u < TJ) {
+        b_j = j0 + u;
+        b_jl = u + 1;
+        b_i = ((b_j + s) & 1) ? 0 : NC + 1;
+        b_nb = b_i == 0 ? 1 : 2;
+      } else {
+        const bool lo = u - TJ < HN;
+        b_j = lo ? j0 - 1 : j1 + 1;
+        b_jl = lo ? 0 : TJ + 1;
+        b_i = 2 - ((1 ^ (s + b_j)) & 1) + 2 * ((u - TJ) % HN);
+        b_nb = (b_j == 0 || b_j == NC + 1) ? (b_j == 0 ? 3 : 4) : 7;
+      }
+      const double *xs = nullptr, *rs = nullptr;
+      int q[3] = {b_i, b_j, s};
+      if (b_nb == 7) {
+        xs = x;
+        rs = r;
+      } else {
+        const int nb_id = m.neighbors[b_nb - 1];
+        if (nb_id > 0) {
+          const int d = (b_nb - 1) >> 1;
+          const bool low = ((b_nb - 1) & 1) == 0;
+          q[d] = low ? NC : 1;
+          xs = src + (size_t)(nb_id - 1) * bsz;
+          rs = rhs + (size_t)(nb_id - 1) * bsz;
+          b_rep = 2 * d + (low ? 1 : 0);
+        }
+      }
+      if (xs) {
+        b_pre = true;
+        const size_t c = ix3(NG, q[0], q[1], q[2]);
+        bl[0] = b_rep == 0 ? 0.0 : xs[c - 1];
+        bl[1] = b_rep == 1 ? 0.0 : xs[c + 1];
+        bl[2] = b_rep == 2 ? 0.0 : xs[c - NG];
+        bl[3] = b_rep == 3 ? 0.0 : xs[c + NG];
+        bl[4] = b_rep == 4 ? 0.0 : xs[c - SK];
+        bl[5] = b_rep == 5 ? 0.0 : xs[c + SK];
+        bl[6] = rs[c];
+      }
+    }
     // prefetch: plane s+2 of phi; rhs of plane s+1, both parities (red for
     // step s+1's A, black for step s+2's C)
     double nx[EPT], nlo[RPT], nhi[RPT];
@@ -425,37 +475,33 @@ __global__ void __launch_bounds__((RbPar<NC, TJ>::NT)) __attribute__((amdgpu_wav
     __syncthreads();
     // B: red values around the tile: x ghost cells of its rows; the halo
     // rows (ghost row of the box, or the red cells of the adjacent tile
-    // recomputed from src)
-    if (s <= NC) {
-      for (int u = tid; u < TJ + NC; u += NT) {
-        int i, j, jl;
-        double v;
-        if (u < TJ) {
-          j = j0 + u;
-          jl = u + 1;
-          i = ((j + s) & 1) ? 0 : NC + 1;
-          const int nb = i == 0 ? 1 : 2;
-          v = pair_ghost<NC>(src, coarse, rhs, meta, m, nb, i, j, s, j, s, bsz,
-                             cf, inv_c1, ga.bc[nb - 1], ga.rb,
-                             P0[jl * NG + (i == 0 ? 1 : NC)],
-                             P0[jl * NG + (i == 0 ? 2 : NC - 1)]);
-        } else {
-          const bool lo = u - TJ < HN;
-          j = lo ? j0 - 1 : j1 + 1;
-          jl = lo ? 0 : TJ + 1;
-          i = 2 - ((1 ^ (s + j)) & 1) + 2 * ((u - TJ) % HN);
-          if (j == 0 || j == NC + 1) {
-            const int nb = j == 0 ? 3 : 4;
-            const int l1 = j == 0 ? 1 : TJ, l2 = j == 0 ? 2 : TJ - 1;
-            v = pair_ghost<NC>(src, coarse, rhs, meta, m, nb, i, j, s, i, s, bsz,
-                               cf, inv_c1, ga.bc[nb - 1], ga.rb, P0[l1 * NG + i],
-                               P0[l2 * NG + i]);
-          } else {
-            v = gs_cell(x, r, ix3(NG, i, j, s), NG, SK, cf, inv_c1);
-          }
+    // recomputed from src) -- same arithmetic as pair_ghost / gs_cell
+    if (b_nb) {
+      double v;
+      if (b_pre) {
+        if (b_rep >= 0) {
+          // x1v: this box's cell next to the face (black, old)
+          const int d = b_rep >> 1;
+          int p1[3] = {b_i, b_jl, 0};
+          p1[d] = (b_rep & 1) ? (d == 0 ? 1 : 1) : (d == 0 ? NC : TJ);
+          const double x1v = P0[p1[1] * NG + p1[0]];
+          bl[b_rep] = x1v;
         }
-        P0[jl * NG + i] = v;
+        v = (bl[6] - cf.c[1] * bl[0] - cf.c[2] * bl[1] - cf.c[3] * bl[2] -
+             cf.c[4] * bl[3] - cf.c[5] * bl[4] - cf.c[6] * bl[5]) *
+            inv_c1;
+      } else if (b_nb <= 2) {
+        v = pair_ghost<NC>(src, coarse, rhs, meta, m, b_nb, b_i, b_j, s, b_j, s,
+                           bsz, cf, inv_c1, ga.bc[b_nb - 1], ga.rb,
+                           P0[b_jl * NG + (b_i == 0 ? 1 : NC)],
+                           P0[b_jl * NG + (b_i == 0 ? 2 : NC - 1)]);
+      } else {
+        const int l1 = b_j == 0 ? 1 : TJ, l2 = b_j == 0 ? 2 : TJ - 1;
+        v = pair_ghost<NC>(src, coarse, rhs, meta, m, b_nb, b_i, b_j, s, b_i, s,
+                           bsz, cf, inv_c1, ga.bc[b_nb - 1], ga.rb,
+                           P0[l1 * NG + b_i], P0[l2 * NG + b_i]);
       }
+      P0[b_jl * NG + b_i] = v;
     }
     if (s == 2 || s == NC + 1) {
       // z ghost plane 0 (NC+1): red cells; x1 = plane 1 (NC), black, old;
