@@ -74,8 +74,10 @@ class StreamerCase:
         self.voltage = voltage
         for s in (0, 1):
             t.set_cc_methods(IV["phi"] + s, self.phi_bc(voltage), capi.RB_MG_SIDES)
+        self.coarse_cycles = coarse_cycles
         self.mg = Multigrid(t, IV["phi"], IV["rhs"], IV["tmp"],
                             coarse_cycles=coarse_cycles)
+        self._mg_helm = {}
         self.n_gas = gas_number_density() if n_gas is None else n_gas
         self.fluid = Fluid(t, [IV["e"], IV["pos"], IV["neg"]], [-1, 1, -1],
                            IV["e"], IV["efld"], FV["flux"], FV["field"],
@@ -89,6 +91,16 @@ class StreamerCase:
         """field_bc_homogeneous, src/m_field.f90:547-567."""
         return [(capi.BC_NEUMANN, 0.0)] * 4 + [(capi.BC_DIRICHLET, 0.0),
                                                (capi.BC_DIRICHLET, voltage)]
+
+    def helmholtz_mg(self, lambda2):
+        """mg_t of a photoionization Helmholtz mode on phi / rhs / tmp
+        (m_photoi_helmh.f90:149-158): helmholtz_lambda = lambda^2, same
+        coarse solver as the field; created once per lambda^2."""
+        if lambda2 not in self._mg_helm:
+            self._mg_helm[lambda2] = Multigrid(
+                self.tree, IV["phi"], IV["rhs"], IV["tmp"],
+                helmholtz_lambda=lambda2, coarse_cycles=self.coarse_cycles)
+        return self._mg_helm[lambda2]
 
     def set_voltage(self, voltage):
         self.voltage = voltage

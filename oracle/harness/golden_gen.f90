@@ -41,6 +41,9 @@ program golden_gen
   integer            :: nc, grid(3), max_lvl, amr_lvl, n_dump, i
   real(dp)           :: dom(3), r0(3), width, dt, dtl(4), residuals(2)
   real(dp)           :: max_rhs, threshold
+  ! photoionization Helmholtz mode: Bourdon's second lambda at 1 bar
+  ! (src/m_photoi_helmh.f90:100), 1/m
+  real(dp), parameter :: helm_lambda = 44081.25_dp
   logical            :: trace
   integer            :: u_log
 
@@ -193,6 +196,26 @@ program golden_gen
   call dump_state("fmg0")
   call fmg(.true.)
   call dump_state("fmg1")
+
+  ! ------------------------------------------------------------------
+  ! Helmholtz FMG of a photoionization mode (photoi_helmh_compute,
+  ! src/m_photoi_helmh.f90:162-204): helmholtz_lambda = lambda^2 in the
+  ! operator (mg_box_lpl_stencil, m_af_multigrid.f90:1243), photoi_helmh_bc
+  ! (Dirichlet 0 on the z faces, Neumann 0 elsewhere = hx_bc_phi with zero
+  ! voltage), the mode starting from zero; FMG without and with guess
+  current_voltage = 0.0_dp
+  mg%helmholtz_lambda = helm_lambda**2
+  ! a new operator stencil key, as mg_init gives every mg_t of a mode
+  ! (stencils are stored once per key, m_af_multigrid.f90:1150-1154)
+  tree%n_stencil_keys_stored = tree%n_stencil_keys_stored + 1
+  mg%operator_key = tree%n_stencil_keys_stored
+  call mg_set_operators_tree(tree, mg)
+  call af_tree_clear_cc(tree, i_phi)
+  call dump_state("helm_in")
+  call fmg(.false.)
+  call dump_state("helm0")
+  call fmg(.true.)
+  call dump_state("helm1")
 
   close(u_log)
 

@@ -50,10 +50,18 @@ FMG = [
     ("fmg0", ["rhs", "phi", "tmp"], []),
     ("fmg1", ["rhs", "phi", "tmp"], []),
 ]
+# Helmholtz FMG of a photoionization mode (lambda = 44081.25 1/m), run after
+# FMG from the state dumped as helm_in
+HELM = [
+    ("helm_in", ["rhs", "phi", "tmp"], []),
+    ("helm0", ["rhs", "phi", "tmp"], []),
+    ("helm1", ["rhs", "phi", "tmp"], []),
+]
+HELM_LAMBDA = 44081.25
 CASES = {
-    "uni4": {"chain": CHAIN + FMG, "trace": True},
-    "uni8": {"chain": CHAIN + FMG, "trace": False},
-    "amr4": {"chain": CHAIN[:7] + FMG, "trace": False},
+    "uni4": {"chain": CHAIN + FMG + HELM, "trace": True},
+    "uni8": {"chain": CHAIN + FMG + HELM, "trace": False},
+    "amr4": {"chain": CHAIN[:7] + FMG + HELM, "trace": False},
 }
 
 
@@ -145,6 +153,7 @@ def pack(case, raw_dir):
         vals = [float(x) for x in (f[2:] if f[0] == "field1_residual" else f[1:])]
         out[key] = np.array(vals)
     spec = CASES[case]
+    out["helm_lambda"] = np.array(HELM_LAMBDA)
     for name, ccv, fcv in spec["chain"]:
         cc, fc = read_state(os.path.join(raw_dir, "state_%s.bin" % name), topo)
         for v in ccv:

@@ -123,17 +123,27 @@ def test_hip_bitwise_equals_oracle_heun_step(hip, oracle, name, smoother, coarse
                  [FV["flux"], FV["field"]])
 
 
+@pytest.mark.parametrize("helm", [0.0, 44081.25])
 @pytest.mark.parametrize("name", sorted(TOPOS))
-def test_hip_bitwise_equals_oracle_fmg(hip, oracle, name, smoother):
-    """mg_fas_fmg from phi = 0 and then with the result as guess."""
+def test_hip_bitwise_equals_oracle_fmg(hip, oracle, name, smoother, helm):
+    """mg_fas_fmg from phi = 0 and then with the result as guess; helm > 0:
+    a photoionization Helmholtz mode (lambda^2 in the operator, Dirichlet 0
+    on the z faces, m_photoi_helmh.f90:149-204)."""
     g = golden.load("uni8")
     ca, cb = _pair(hip, oracle, TOPOS[name](), g)
+    mgs = []
     for c in (ca, cb):
         c.fluid.field_set_rhs(IV["rhs"], 0)
-        c.mg.fas_fmg(True, have_guess=False)
+        if helm:
+            c.set_voltage(0.0)
+            mgs.append(c.helmholtz_mg(helm ** 2))
+        else:
+            mgs.append(c.mg)
+    for mg in mgs:
+        mg.fas_fmg(True, have_guess=False)
     _assert_same(ca, cb, [IV["phi"], IV["tmp"], IV["rhs"]])
-    for c in (ca, cb):
-        c.mg.fas_fmg(True, have_guess=True)
+    for mg in mgs:
+        mg.fas_fmg(True, have_guess=True)
     _assert_same(ca, cb, [IV["phi"], IV["tmp"], IV["rhs"]])
 
 
