@@ -23,6 +23,9 @@ BC_DIRICHLET, BC_NEUMANN, BC_CONTINUOUS, BC_DIRICHLET_COPY = -10, -11, -12, -13
 RB_GC_INTERP, RB_GC_INTERP_LIM, RB_MG_SIDES = 1, 2, 3
 LIM_NONE, LIM_VANLEER, LIM_KOREN, LIM_MINMOD, LIM_MC, LIM_GMINMOD43, LIM_ZERO = range(1, 8)
 RATE_TABULATED_FIELD, RATE_CONSTANT, RATE_LINEAR, RATE_EXP_V1, RATE_EXP_V2 = range(1, 6)
+RATE_K1, RATE_K3 = 6, 8
+(RATE_K4, RATE_K5, RATE_K6, RATE_K7, RATE_K8, RATE_K9, RATE_K10, RATE_K11,
+ RATE_K12, RATE_K13, RATE_K14, RATE_K15) = range(9, 21)
 COARSE_CYCLES, COARSE_DIRECT = 1, 2
 MAX_SPECIES = 32
 MAX_REACTIONS = 128
@@ -77,7 +80,8 @@ class FluidDesc(C.Structure):
                 ("i_efld", i32), ("f_flux", i32), ("f_field", i32),
                 ("limiter", i32), ("gas_number_density", f64), ("td", LT),
                 ("chem", LT), ("n_reactions", i32),
-                ("reactions", C.POINTER(Reaction)), ("dt_chemistry_nmin", f64)]
+                ("reactions", C.POINTER(Reaction)), ("dt_chemistry_nmin", f64),
+                ("gas_temperature", f64), ("td_energy_col", i32)]
 
 
 class MgDesc(C.Structure):

@@ -198,7 +198,8 @@ class Fluid:
 
     def __init__(self, tree, species_iv, species_charge, i_electron, i_efld,
                  f_flux, f_field, gas_number_density, td, chem, reactions,
-                 limiter=capi.LIM_KOREN, dt_chemistry_nmin=-1.0):
+                 limiter=capi.LIM_KOREN, dt_chemistry_nmin=-1.0,
+                 gas_temperature=300.0, td_energy_col=0):
         self.tree = tree
         self.lib = tree.lib
         d = capi.FluidDesc()
@@ -234,6 +235,8 @@ class Fluid:
         d.n_reactions = len(reactions)
         d.reactions = C.cast(arr, C.POINTER(capi.Reaction))
         d.dt_chemistry_nmin = dt_chemistry_nmin
+        d.gas_temperature = gas_temperature
+        d.td_energy_col = td_energy_col
         h = C.c_void_p()
         self.lib.call("fluid_create", tree.h, C.byref(d), C.byref(h))
         self.h = h

@@ -816,6 +816,9 @@ struct UpdArgs {
   const double *F;
   const DevReaction *reac;
   DevLT chem;
+  DevLT td;        // transport table (mean-energy column for Te)
+  int te_col;      // td_energy_eV column (1-based), 0 if absent
+  double Tg;       // gas temperature
   double inv_N;
   double dt;
   double dt_dr[3];  // dt / dr per dimension of this level
@@ -838,7 +841,66 @@ __device__ __forceinline__ void add_at(double (&a)[NS], int idx, double v) {
     if (s == idx) a[s] = a[s] + v;
 }
 
-template <int NS>
+// get_rates for one cell and one reaction, src/m_chemistry.f90:565-650
+// (operand order as there; `**2` as a product, real powers pow). Te < 0 on
+// the first call of a cell: Te = electron_eV_to_K * LT_get_col(td_tbl,
+// td_energy_eV, Td) is looked up once.
+// the temperature-dependent forms (only compiled into the update kernels of
+// reaction sets that use them: their pow / exp code raises the register
+// count)
+__device__ __forceinline__ double rate_slow(const UpdArgs &A, const DevReaction &R,
+                                         double field, double &Te) {
+  const double c0 = R.rate_factor;
+  const double *c = R.c;
+  const double Tg = A.Tg;
+  const double kB = 1.3806503e-23, eV = 1.6022e-19;  // UC_boltzmann_const, UC_elec_volt
+  const double electron_eV_to_K = 2 * eV / (3 * kB);
+  if ((R.rate_type == AFH_RATE_K1 || R.rate_type == AFH_RATE_K3) && Te < 0)
+    Te = electron_eV_to_K * lt_col(A.td, A.te_col, field);
+  switch (R.rate_type) {
+  case AFH_RATE_K1: return c0 * c[0] * pow(300 / Te, c[1]);
+  case AFH_RATE_K3: {
+    const double z = (kB / eV) * Te + c[1];
+    return c0 * (c[0] * (z * z) - c[2]) * c[3];
+  }
+  case AFH_RATE_K4: return c0 * c[0] * pow(Tg / 300, c[1]) * exp(-c[2] / Tg);
+  case AFH_RATE_K5: return c0 * c[0] * exp(-c[1] / Tg);
+  case AFH_RATE_K6: return c0 * c[0] * pow(Tg, c[1]);
+  case AFH_RATE_K7: return c0 * c[0] * pow(Tg / c[1], c[2]);
+  case AFH_RATE_K8: return c0 * c[0] * pow(300 / Tg, c[1]);
+  case AFH_RATE_K9: return c0 * c[0] * exp(-c[1] * Tg);
+  case AFH_RATE_K10: return c0 * pow(10.0, c[0] + c[1] * (Tg - 300));
+  case AFH_RATE_K11: return c0 * c[0] * pow(300 / Tg, c[1]) * exp(-c[2] / Tg);
+  case AFH_RATE_K12: return c0 * c[0] * pow(Tg, c[1]) * exp(-c[2] / Tg);
+  case AFH_RATE_K13: return c0 * c[0] * exp(-pow(c[1] / (c[2] + field), c[3]));
+  case AFH_RATE_K14: return c0 * c[0] * exp(-pow(field / c[1], c[2]));
+  default:  // AFH_RATE_K15
+    return c0 * c[0] * exp(-pow(c[1] / (kB * (Tg + field / c[2])), c[3]));
+  }
+}
+
+template <bool SLOW>
+__device__ __forceinline__ double rate_of(const UpdArgs &A, const DevReaction &R,
+                                          double field, double &Te) {
+  const double c0 = R.rate_factor;
+  const double *c = R.c;
+  switch (R.rate_type) {
+  case AFH_RATE_TABULATED_FIELD: return c0 * lt_col(A.chem, R.table_col, field);
+  case AFH_RATE_CONSTANT: return c0 * c[0];
+  case AFH_RATE_LINEAR: return c0 * c[0] * (field - c[1]);
+  case AFH_RATE_EXP_V1: {
+    const double z = c[1] / (c[2] + field);
+    return c0 * c[0] * exp(-(z * z));
+  }
+  case AFH_RATE_EXP_V2: {
+    const double z = field / c[1];
+    return c0 * c[0] * exp(-(z * z));
+  }
+  default: return SLOW ? rate_slow(A, R, field, Te) : 0.0;
+  }
+}
+
+template <int NS, bool SLOW>
 __global__ void __launch_bounds__(256)
     k_update(UpdArgs A, const int32_t *__restrict__ ids, int nc, size_t bsz,
              size_t fsz, unsigned long long *red) {
@@ -880,25 +942,10 @@ __global__ void __launch_bounds__(256)
       der[s] = 0.0;
     }
     const double field = 1e21 * A.inv_N * ev;
+    double Te = -1.0;  // electron temperature, looked up once per cell
     for (int r = 0; r < A.nr; r++) {
       const DevReaction &R = A.reac[r];
-      const double c0 = R.rate_factor;
-      double rate;
-      switch (R.rate_type) {
-      case AFH_RATE_TABULATED_FIELD: rate = c0 * lt_col(A.chem, R.table_col, field); break;
-      case AFH_RATE_CONSTANT: rate = c0 * R.c[0]; break;
-      case AFH_RATE_LINEAR: rate = c0 * R.c[0] * (field - R.c[1]); break;
-      case AFH_RATE_EXP_V1: {
-        const double z = R.c[1] / (R.c[2] + field);
-        rate = c0 * R.c[0] * exp(-(z * z));
-        break;
-      }
-      default: {
-        const double z = field / R.c[1];
-        rate = c0 * R.c[0] * exp(-(z * z));
-        break;
-      }
-      }
+      double rate = rate_of<SLOW>(A, R, field, Te);
       double prod = 1.0;
       for (int q = 0; q < R.n_in; q++) prod = prod * sel(dens, R.ix_in[q] - 1);
       rate = rate * prod;
@@ -948,11 +995,15 @@ __global__ void __launch_bounds__(256)
 
 template <int NS>
 void launch_update(const UpdArgs &A, afh_tree *t, int l,
-                          unsigned long long *red) {
+                   unsigned long long *red, bool slow) {
   const int nc = t->nc, n3 = nc * nc * nc;
-  hipLaunchKernelGGL(k_update<NS>, dim3((n3 + 255) / 256, t->leaves.n(l)),
-                     dim3(256), 0, t->stream, A, t->leaves.at(l), nc, t->bsz,
-                     t->fsz, red);
+  const dim3 grid((n3 + 255) / 256, t->leaves.n(l));
+  if (slow)
+    hipLaunchKernelGGL((k_update<NS, true>), grid, dim3(256), 0, t->stream, A,
+                       t->leaves.at(l), nc, t->bsz, t->fsz, red);
+  else
+    hipLaunchKernelGGL((k_update<NS, false>), grid, dim3(256), 0, t->stream, A,
+                       t->leaves.at(l), nc, t->bsz, t->fsz, red);
 }
 
 }  // namespace afh
@@ -969,6 +1020,7 @@ struct afh_fluid {
   // k_flux_lds: transport table interleaved per row (mu N, D N); unset when
   // the table does not fit LDS or AFH_FLUX_STAGED=1 selects k_flux_staged
   double *d_tdi = nullptr;
+  bool slow_rates = false;  // a reaction with a temperature-dependent form
 };
 
 extern "C" {
@@ -1016,8 +1068,14 @@ int32_t afh_fluid_create(afh_tree *t, const afh_fluid_desc *d, afh_fluid **out) 
   for (int r = 0; r < d->n_reactions; r++) {
     const afh_reaction &a = d->reactions[r];
     DevReaction &b = R[r];
-    if (a.rate_type < AFH_RATE_TABULATED_FIELD || a.rate_type > AFH_RATE_EXP_V2)
+    if (a.rate_type < AFH_RATE_TABULATED_FIELD || a.rate_type > AFH_RATE_K15 ||
+        a.rate_type == 7)
       return set_error(AFH_ERR_UNSUPPORTED, "reaction rate type %d", a.rate_type);
+    if (a.rate_type > AFH_RATE_EXP_V2) f->slow_rates = true;
+    if ((a.rate_type == AFH_RATE_K1 || a.rate_type == AFH_RATE_K3) &&
+        (d->td_energy_col < 1 || d->td_energy_col > d->td.n_cols))
+      return set_error(AFH_ERR_ARG, "rate type %d needs the td mean-energy column",
+                       a.rate_type);
     if (a.n_in < 0 || a.n_in > 4 || a.n_out < 0 || a.n_out > 4)
       return set_error(AFH_ERR_ARG, "reaction species count");
     b.rate_type = a.rate_type;
@@ -1230,6 +1288,9 @@ int32_t afh_flux_update_densities(afh_fluid *f, double dt, int32_t s_deriv,
   A.F = t->fcv(f->d.f_flux);
   A.reac = f->d_reac;
   A.chem = f->chem;
+  A.td = f->td;
+  A.te_col = f->d.td_energy_col;
+  A.Tg = f->d.gas_temperature;
   A.inv_N = 1 / f->d.gas_number_density;
   A.dt = dt;
   A.dt_chemistry_nmin = f->d.dt_chemistry_nmin;
@@ -1248,7 +1309,7 @@ int32_t afh_flux_update_densities(afh_fluid *f, double dt, int32_t s_deriv,
     for (int q = 0; q < 3; q++) A.dt_dr[q] = dt / t->lvl_dr[3 * (l - 1) + q];
     prof_begin(t, AFH_PROF_UPDATE);
     switch (A.ns) {
-#define AFH_CASE(N) case N: launch_update<N>(A, t, l, red); break;
+#define AFH_CASE(N) case N: launch_update<N>(A, t, l, red, f->slow_rates); break;
       AFH_CASE(1) AFH_CASE(2) AFH_CASE(3) AFH_CASE(4) AFH_CASE(5) AFH_CASE(6)
       AFH_CASE(7) AFH_CASE(8) AFH_CASE(9) AFH_CASE(10) AFH_CASE(11)
       AFH_CASE(12) AFH_CASE(13) AFH_CASE(14) AFH_CASE(15) AFH_CASE(16)

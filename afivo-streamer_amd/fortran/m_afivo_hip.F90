@@ -48,6 +48,10 @@ module m_afivo_hip
   integer(c_int32_t), parameter :: AFH_RATE_LINEAR = 3
   integer(c_int32_t), parameter :: AFH_RATE_EXP_V1 = 4
   integer(c_int32_t), parameter :: AFH_RATE_EXP_V2 = 5
+  integer(c_int32_t), parameter :: AFH_RATE_K1 = 6, AFH_RATE_K3 = 8, &
+       AFH_RATE_K4 = 9, AFH_RATE_K5 = 10, AFH_RATE_K6 = 11, AFH_RATE_K7 = 12, &
+       AFH_RATE_K8 = 13, AFH_RATE_K9 = 14, AFH_RATE_K10 = 15, AFH_RATE_K11 = 16, &
+       AFH_RATE_K12 = 17, AFH_RATE_K13 = 18, AFH_RATE_K14 = 19, AFH_RATE_K15 = 20
 
   integer(c_int32_t), parameter :: AFH_COARSE_CYCLES = 1
   integer(c_int32_t), parameter :: AFH_COARSE_DIRECT = 2
@@ -127,6 +131,8 @@ module m_afivo_hip
      integer(c_int32_t) :: n_reactions
      type(c_ptr)        :: reactions = c_null_ptr
      real(c_double)     :: dt_chemistry_nmin
+     real(c_double)     :: gas_temperature = 300.0_c_double
+     integer(c_int32_t) :: td_energy_col = 0
   end type afh_fluid_desc
 
   type, bind(C) :: afh_mg_desc

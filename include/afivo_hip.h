@@ -58,12 +58,29 @@ extern "C" {
 #define AFH_LIM_GMINMOD43 6
 #define AFH_LIM_ZERO 7
 
-/* Reaction rate types, src/m_chemistry.f90:63-104 (subset on the path) */
-#define AFH_RATE_TABULATED_FIELD 1
-#define AFH_RATE_CONSTANT 2
-#define AFH_RATE_LINEAR 3
-#define AFH_RATE_EXP_V1 4
-#define AFH_RATE_EXP_V2 5
+/* Reaction rate types, src/m_chemistry.f90:58-115 (numbers as there; Td =
+ * reduced field, Te from the transport table's mean-energy column, Tg =
+ * gas temperature). rate_tabulated_energy (0) needs the energy equation
+ * (LEA) and is not on the LFA path: rejected. */
+#define AFH_RATE_TABULATED_FIELD 1 /* c0 * table(Td) */
+#define AFH_RATE_CONSTANT 2        /* c0 c1 */
+#define AFH_RATE_LINEAR 3          /* c0 c1 (Td - c2) */
+#define AFH_RATE_EXP_V1 4          /* c0 c1 exp(-(c2 / (c3 + Td))^2) */
+#define AFH_RATE_EXP_V2 5          /* c0 c1 exp(-(Td / c2)^2) */
+#define AFH_RATE_K1 6              /* c0 c1 (300 / Te)^c2 */
+#define AFH_RATE_K3 8              /* c0 (c1 (kB/eV Te + c2)^2 - c3) c4 */
+#define AFH_RATE_K4 9              /* c0 c1 (Tg / 300)^c2 exp(-c3 / Tg) */
+#define AFH_RATE_K5 10             /* c0 c1 exp(-c2 / Tg) */
+#define AFH_RATE_K6 11             /* c0 c1 Tg^c2 */
+#define AFH_RATE_K7 12             /* c0 c1 (Tg / c2)^c3 */
+#define AFH_RATE_K8 13             /* c0 c1 (300 / Tg)^c2 */
+#define AFH_RATE_K9 14             /* c0 c1 exp(-c2 Tg) */
+#define AFH_RATE_K10 15            /* c0 10^(c1 + c2 (Tg - 300)) */
+#define AFH_RATE_K11 16            /* c0 c1 (300 / Tg)^c2 exp(-c3 / Tg) */
+#define AFH_RATE_K12 17            /* c0 c1 Tg^c2 exp(-c3 / Tg) */
+#define AFH_RATE_K13 18            /* c0 c1 exp(-(c2 / (c3 + Td))^c4) */
+#define AFH_RATE_K14 19            /* c0 c1 exp(-(Td / c2)^c3) */
+#define AFH_RATE_K15 20            /* c0 c1 exp(-(c2 / (kB (Tg + Td / c3)))^c4) */
 
 /* Coarse-grid solver modes (replaces HYPRE PFMG, m_coarse_solver.f90) */
 #define AFH_COARSE_CYCLES 1 /* fixed number of device MG cycles */
@@ -153,6 +170,9 @@ typedef struct afh_fluid_desc {
   int32_t n_reactions;
   const afh_reaction *reactions;
   double dt_chemistry_nmin; /* < 0: limit loss (m_dt.f90:34-37 default) */
+  double gas_temperature;   /* Tg (m_gas.f90:21, 300 K by default) */
+  int32_t td_energy_col;    /* mean-energy column of td (td_energy_eV,
+                               m_transport_data.f90:158), 0 if absent */
 } afh_fluid_desc;
 
 /* Multigrid options, mg_t (m_af_types.f90:572-665) + coarse solver. */

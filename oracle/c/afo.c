@@ -1223,9 +1223,11 @@ int32_t afo_fluid_create(afh_tree *t, const afh_fluid_desc *d,
   for (int r = 0; r < d->n_reactions; r++) {
     f->reac[r] = d->reactions[r];
     int rt = d->reactions[r].rate_type;
-    if (rt != AFH_RATE_TABULATED_FIELD && rt != AFH_RATE_CONSTANT &&
-        rt != AFH_RATE_LINEAR && rt != AFH_RATE_EXP_V1 && rt != AFH_RATE_EXP_V2)
+    if (rt < AFH_RATE_TABULATED_FIELD || rt > AFH_RATE_K15 || rt == 7)
       return fail(AFH_ERR_UNSUPPORTED, "reaction rate type %d", rt);
+    if ((rt == AFH_RATE_K1 || rt == AFH_RATE_K3) &&
+        (d->td_energy_col < 1 || d->td_energy_col > d->td.n_cols))
+      return fail(AFH_ERR_ARG, "rate type %d needs the td mean-energy column", rt);
   }
   f->d.reactions = f->reac;
   *out = f;
@@ -1255,6 +1257,52 @@ static inline double lt_col(const afh_lt *lt, int col, double x) {
   }
   const double *rc = lt->rows_cols + (size_t)(col - 1) * lt->n_points;
   return lf * rc[low - 1] + (1 - lf) * rc[low];
+}
+
+/* get_rates for one cell and one reaction, src/m_chemistry.f90:565-650
+ * (operand order as written there; `**2` as a product, real powers pow).
+ * *Te < 0 on the first call of a cell: Te = electron_eV_to_K *
+ * LT_get_col(td_tbl, td_energy_eV, Td) is looked up once. */
+static double rate_of(const afh_fluid *fl, const afh_reaction *R, double field,
+                      double *Te) {
+  const double c0 = R->rate_factor;
+  const double *c = R->c;
+  const double Tg = fl->d.gas_temperature;
+  const double kB = 1.3806503e-23, eV = 1.6022e-19;  /* UC_boltzmann_const, UC_elec_volt */
+  const double electron_eV_to_K = 2 * eV / (3 * kB);
+  if ((R->rate_type == AFH_RATE_K1 || R->rate_type == AFH_RATE_K3) && *Te < 0)
+    *Te = electron_eV_to_K * lt_col(&fl->d.td, fl->d.td_energy_col, field);
+  switch (R->rate_type) {
+  case AFH_RATE_TABULATED_FIELD: return c0 * lt_col(&fl->d.chem, R->table_col, field);
+  case AFH_RATE_CONSTANT: return c0 * c[0];
+  case AFH_RATE_LINEAR: return c0 * c[0] * (field - c[1]);
+  case AFH_RATE_EXP_V1: {
+    const double z = c[1] / (c[2] + field);
+    return c0 * c[0] * exp(-(z * z));
+  }
+  case AFH_RATE_EXP_V2: {
+    const double z = field / c[1];
+    return c0 * c[0] * exp(-(z * z));
+  }
+  case AFH_RATE_K1: return c0 * c[0] * pow(300 / *Te, c[1]);
+  case AFH_RATE_K3: {
+    const double z = (kB / eV) * *Te + c[1];
+    return c0 * (c[0] * (z * z) - c[2]) * c[3];
+  }
+  case AFH_RATE_K4: return c0 * c[0] * pow(Tg / 300, c[1]) * exp(-c[2] / Tg);
+  case AFH_RATE_K5: return c0 * c[0] * exp(-c[1] / Tg);
+  case AFH_RATE_K6: return c0 * c[0] * pow(Tg, c[1]);
+  case AFH_RATE_K7: return c0 * c[0] * pow(Tg / c[1], c[2]);
+  case AFH_RATE_K8: return c0 * c[0] * pow(300 / Tg, c[1]);
+  case AFH_RATE_K9: return c0 * c[0] * exp(-c[1] * Tg);
+  case AFH_RATE_K10: return c0 * pow(10.0, c[0] + c[1] * (Tg - 300));
+  case AFH_RATE_K11: return c0 * c[0] * pow(300 / Tg, c[1]) * exp(-c[2] / Tg);
+  case AFH_RATE_K12: return c0 * c[0] * pow(Tg, c[1]) * exp(-c[2] / Tg);
+  case AFH_RATE_K13: return c0 * c[0] * exp(-pow(c[1] / (c[2] + field), c[3]));
+  case AFH_RATE_K14: return c0 * c[0] * exp(-pow(field / c[1], c[2]));
+  default: /* AFH_RATE_K15 */
+    return c0 * c[0] * exp(-pow(c[1] / (kB * (Tg + field / c[2])), c[3]));
+  }
 }
 
 /* field_set_rhs, src/m_field.f90:363-401 */
@@ -1659,26 +1707,10 @@ int32_t afo_flux_update_densities(afh_fluid *fl, double dt, int32_t s_deriv,
               dens[s] = v > 0.0 ? v : 0.0; /* max(dens, 0.0_dp) */
               der[s] = 0.0;
             }
+            double Te = -1.0; /* electron temperature, looked up once */
             for (int r = 0; r < nr; r++) {
               const afh_reaction *R = &fl->reac[r];
-              double c0 = R->rate_factor, rate;
-              switch (R->rate_type) {
-              case AFH_RATE_TABULATED_FIELD:
-                rate = c0 * lt_col(&fl->d.chem, R->table_col, field);
-                break;
-              case AFH_RATE_CONSTANT: rate = c0 * R->c[0]; break;
-              case AFH_RATE_LINEAR: rate = c0 * R->c[0] * (field - R->c[1]); break;
-              case AFH_RATE_EXP_V1: {
-                double z = R->c[1] / (R->c[2] + field);
-                rate = c0 * R->c[0] * exp(-(z * z));
-                break;
-              }
-              default: {
-                double z = field / R->c[1];
-                rate = c0 * R->c[0] * exp(-(z * z));
-                break;
-              }
-              }
+              double rate = rate_of(fl, R, field, &Te);
               double prod = 1.0;
               for (int m = 0; m < R->n_in; m++) prod = prod * dens[R->ix_in[m] - 1];
               rate = rate * prod;

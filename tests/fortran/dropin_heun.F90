@@ -161,6 +161,8 @@ program dropin_heun
   fdesc%n_reactions = 2
   fdesc%reactions = c_loc(reac)
   fdesc%dt_chemistry_nmin = -1.0_dp
+  fdesc%gas_temperature = 300.0_dp
+  fdesc%td_energy_col = 0
   call afh_check(afh_fluid_create(t, fdesc, fl), "fluid_create")
 
   n_bad = 0
