@@ -126,6 +126,8 @@ SIGNATURES = {
     "flux_upwind_tree": (i32, [_VP, i32, P_f64]),
     "flux_update_densities": (i32, [_VP, f64, i32, i32, P_i32, P_f64, i32,
                                     i32, P_f64]),
+    "fluid_forward_euler": (i32, [_VP, f64, i32, i32, P_i32, P_f64, i32, i32,
+                                  i32, P_f64]),
     "profile_enable": (i32, [_VP, i32]),
     "profile_read": (i32, [_VP, P_f64, C.POINTER(C.c_int64), P_f64]),
     "tree_set_hook": (i32, [_VP, C.c_void_p, _VP]),
@@ -140,6 +142,7 @@ HOOK_HALO, HOOK_RIMS, HOOK_RESTRICT, HOOK_MAX, HOOK_MIN, HOOK_CFLUX = 1, 2, 3, 4
 #             int32_t n)
 HOOK_FN = C.CFUNCTYPE(i32, C.c_void_p, i32, i32, i32, P_f64, i32)
 PROF_GSRB, PROF_GHOST, PROF_FLUX, PROF_UPDATE, PROF_GSRB_PAIR, PROF_GSRB_PAIR_TILED = 1, 2, 3, 4, 5, 6
+PROF_FE = 7
 ORACLE_EXTRA = {
     "mg_gsrb_boxes": (i32, [_VP, i32, i32]),
     "mg_update_coarse": (i32, [_VP, i32]),

@@ -274,3 +274,16 @@ class Fluid:
                       sp.ctypes.data_as(capi.P_i32), wp.ctypes.data_as(capi.P_f64),
                       s_out, int(last_step), out)
         return out[0], out[1]
+
+    def forward_euler(self, dt, s_deriv, s_prev, w_prev, s_out, last_step,
+                      store_flux=False):
+        """flux_upwind_tree + flux_update_densities (forward_euler,
+        src/m_fluid.f90:56-70), fused on the device where the tree allows;
+        returns dt_limits(1:4)."""
+        sp = _i32(s_prev)
+        wp = np.ascontiguousarray(w_prev, dtype=np.float64)
+        out = (C.c_double * 4)()
+        self.lib.call("fluid_forward_euler", self.h, float(dt), s_deriv, len(sp),
+                      sp.ctypes.data_as(capi.P_i32), wp.ctypes.data_as(capi.P_f64),
+                      s_out, int(last_step), int(store_flux), out)
+        return out[0], out[1], out[2], out[3]

@@ -75,6 +75,9 @@ class StreamerCase:
         for s in (0, 1):
             t.set_cc_methods(IV["phi"] + s, self.phi_bc(voltage), capi.RB_MG_SIDES)
         self.coarse_cycles = coarse_cycles
+        # keep the face fluxes of the species step in FV["flux"] (the fused
+        # device step otherwise leaves them on chip)
+        self.store_flux = False
         self.mg = Multigrid(t, IV["phi"], IV["rhs"], IV["tmp"],
                             coarse_cycles=coarse_cycles)
         self._mg_helm = {}
@@ -141,10 +144,8 @@ class StreamerCase:
         """m_fluid.f90:21-99 (without the CFL/ dt_max combination)."""
         if i_step > 1:
             self.field_compute(s_deriv, **field_kw)
-        d1 = self.fluid.flux_upwind_tree(s_deriv)
-        d2 = self.fluid.flux_update_densities(dt, s_deriv, s_prev, w_prev,
-                                              s_out, i_step == n_steps)
-        return [d1[0], d1[1], d2[0], d2[1]]
+        return list(self.fluid.forward_euler(dt, s_deriv, s_prev, w_prev, s_out,
+                                             i_step == n_steps, self.store_flux))
 
     def heun_step(self, dt, **field_kw):
         """af_advance with af_heuns_method (m_af_advance.f90:160-164)."""

@@ -73,6 +73,9 @@ struct afh_tree {
   afh::LevelList refb;
   // (parent id, nb) tasks of af_consistent_fluxes, per level
   afh::LevelList cflux;
+  // af_consistent_fluxes has a task anywhere in the whole topology (all
+  // ranks): the fused forward-Euler kernel needs every face flux final
+  bool any_cflux = false;
   double *cc = nullptr, *fc = nullptr;
   double *gc2 = nullptr;     // 2nd ghost layer for the flux: [box][6][nc][nc]
   double *scratch = nullptr; // reductions etc.

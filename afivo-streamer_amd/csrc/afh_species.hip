@@ -476,6 +476,108 @@ __global__ void __launch_bounds__(256, AFH_FLUX_MINW)
   }
 }
 
+// ------------------------------------------------------------ update
+struct DevReaction {
+  int rate_type, table_col, n_in, n_out;
+  double rate_factor, c[4];
+  int ix_in[4], ix_out[4], mult_out[4];
+};
+
+struct UpdArgs {
+  int ns, nr, n_prev, last_step, e_index;  // e_index: species slot of the flux species
+  int der_q;  // s_deriv == s_prev[der_q] (the derivative state is read once), or -1
+  double w_prev[MAXPREV];
+  const double *prev[MAXS][MAXPREV];
+  const double *der[MAXS];
+  double *out[MAXS];
+  const double *E;
+  const double *F;
+  const DevReaction *reac;
+  DevLT chem;
+  DevLT td;        // transport table (mean-energy column for Te)
+  int te_col;      // td_energy_eV column (1-based), 0 if absent
+  double Tg;       // gas temperature
+  double inv_N;
+  double dt;
+  double dt_dr[3];  // dt / dr per dimension of this level
+  double dt_chemistry_nmin;
+};
+
+// Register-resident species arrays indexed by runtime reaction data: the
+// select loops unroll over the compile-time species count.
+template <int NS>
+__device__ __forceinline__ double sel(const double (&a)[NS], int idx) {
+  double r = a[0];
+#pragma unroll
+  for (int s = 1; s < NS; s++) r = (s == idx) ? a[s] : r;
+  return r;
+}
+template <int NS>
+__device__ __forceinline__ void add_at(double (&a)[NS], int idx, double v) {
+#pragma unroll
+  for (int s = 0; s < NS; s++)
+    if (s == idx) a[s] = a[s] + v;
+}
+
+// get_rates for one cell and one reaction, src/m_chemistry.f90:565-650
+// (operand order as there; `**2` as a product, real powers pow). Te < 0 on
+// the first call of a cell: Te = electron_eV_to_K * LT_get_col(td_tbl,
+// td_energy_eV, Td) is looked up once.
+// the temperature-dependent forms (only compiled into the update kernels of
+// reaction sets that use them: their pow / exp code raises the register
+// count)
+__device__ __forceinline__ double rate_slow(const UpdArgs &A, const DevReaction &R,
+                                         double field, double &Te) {
+  const double c0 = R.rate_factor;
+  const double *c = R.c;
+  const double Tg = A.Tg;
+  const double kB = 1.3806503e-23, eV = 1.6022e-19;  // UC_boltzmann_const, UC_elec_volt
+  const double electron_eV_to_K = 2 * eV / (3 * kB);
+  if ((R.rate_type == AFH_RATE_K1 || R.rate_type == AFH_RATE_K3) && Te < 0)
+    Te = electron_eV_to_K * lt_col(A.td, A.te_col, field);
+  switch (R.rate_type) {
+  case AFH_RATE_K1: return c0 * c[0] * pow(300 / Te, c[1]);
+  case AFH_RATE_K3: {
+    const double z = (kB / eV) * Te + c[1];
+    return c0 * (c[0] * (z * z) - c[2]) * c[3];
+  }
+  case AFH_RATE_K4: return c0 * c[0] * pow(Tg / 300, c[1]) * exp(-c[2] / Tg);
+  case AFH_RATE_K5: return c0 * c[0] * exp(-c[1] / Tg);
+  case AFH_RATE_K6: return c0 * c[0] * pow(Tg, c[1]);
+  case AFH_RATE_K7: return c0 * c[0] * pow(Tg / c[1], c[2]);
+  case AFH_RATE_K8: return c0 * c[0] * pow(300 / Tg, c[1]);
+  case AFH_RATE_K9: return c0 * c[0] * exp(-c[1] * Tg);
+  case AFH_RATE_K10: return c0 * pow(10.0, c[0] + c[1] * (Tg - 300));
+  case AFH_RATE_K11: return c0 * c[0] * pow(300 / Tg, c[1]) * exp(-c[2] / Tg);
+  case AFH_RATE_K12: return c0 * c[0] * pow(Tg, c[1]) * exp(-c[2] / Tg);
+  case AFH_RATE_K13: return c0 * c[0] * exp(-pow(c[1] / (c[2] + field), c[3]));
+  case AFH_RATE_K14: return c0 * c[0] * exp(-pow(field / c[1], c[2]));
+  default:  // AFH_RATE_K15
+    return c0 * c[0] * exp(-pow(c[1] / (kB * (Tg + field / c[2])), c[3]));
+  }
+}
+
+template <bool SLOW>
+__device__ __forceinline__ double rate_of(const UpdArgs &A, const DevReaction &R,
+                                          double field, double &Te) {
+  const double c0 = R.rate_factor;
+  const double *c = R.c;
+  switch (R.rate_type) {
+  case AFH_RATE_TABULATED_FIELD: return c0 * lt_col(A.chem, R.table_col, field);
+  case AFH_RATE_CONSTANT: return c0 * c[0];
+  case AFH_RATE_LINEAR: return c0 * c[0] * (field - c[1]);
+  case AFH_RATE_EXP_V1: {
+    const double z = c[1] / (c[2] + field);
+    return c0 * c[0] * exp(-(z * z));
+  }
+  case AFH_RATE_EXP_V2: {
+    const double z = field / c[1];
+    return c0 * c[0] * exp(-(z * z));
+  }
+  default: return SLOW ? rate_slow(A, R, field, Te) : 0.0;
+  }
+}
+
 // LDS-staged plane-marching flux (NC in {16, 32, 64}): a workgroup owns TJ
 // rows of a box and marches over k. Each step stages plane k of n_e (rows
 // j0-2 .. j0+TJ+1, columns -1 .. NC+2, second ghost layers from gc2) and of
@@ -798,108 +900,6 @@ __global__ void k_consistent(double *__restrict__ F,
               fc[fidx(nf, d, p4[0], p4[1], p4[2])]);
 }
 
-// ------------------------------------------------------------ update
-struct DevReaction {
-  int rate_type, table_col, n_in, n_out;
-  double rate_factor, c[4];
-  int ix_in[4], ix_out[4], mult_out[4];
-};
-
-struct UpdArgs {
-  int ns, nr, n_prev, last_step, e_index;  // e_index: species slot of the flux species
-  int der_q;  // s_deriv == s_prev[der_q] (the derivative state is read once), or -1
-  double w_prev[MAXPREV];
-  const double *prev[MAXS][MAXPREV];
-  const double *der[MAXS];
-  double *out[MAXS];
-  const double *E;
-  const double *F;
-  const DevReaction *reac;
-  DevLT chem;
-  DevLT td;        // transport table (mean-energy column for Te)
-  int te_col;      // td_energy_eV column (1-based), 0 if absent
-  double Tg;       // gas temperature
-  double inv_N;
-  double dt;
-  double dt_dr[3];  // dt / dr per dimension of this level
-  double dt_chemistry_nmin;
-};
-
-// Register-resident species arrays indexed by runtime reaction data: the
-// select loops unroll over the compile-time species count.
-template <int NS>
-__device__ __forceinline__ double sel(const double (&a)[NS], int idx) {
-  double r = a[0];
-#pragma unroll
-  for (int s = 1; s < NS; s++) r = (s == idx) ? a[s] : r;
-  return r;
-}
-template <int NS>
-__device__ __forceinline__ void add_at(double (&a)[NS], int idx, double v) {
-#pragma unroll
-  for (int s = 0; s < NS; s++)
-    if (s == idx) a[s] = a[s] + v;
-}
-
-// get_rates for one cell and one reaction, src/m_chemistry.f90:565-650
-// (operand order as there; `**2` as a product, real powers pow). Te < 0 on
-// the first call of a cell: Te = electron_eV_to_K * LT_get_col(td_tbl,
-// td_energy_eV, Td) is looked up once.
-// the temperature-dependent forms (only compiled into the update kernels of
-// reaction sets that use them: their pow / exp code raises the register
-// count)
-__device__ __forceinline__ double rate_slow(const UpdArgs &A, const DevReaction &R,
-                                         double field, double &Te) {
-  const double c0 = R.rate_factor;
-  const double *c = R.c;
-  const double Tg = A.Tg;
-  const double kB = 1.3806503e-23, eV = 1.6022e-19;  // UC_boltzmann_const, UC_elec_volt
-  const double electron_eV_to_K = 2 * eV / (3 * kB);
-  if ((R.rate_type == AFH_RATE_K1 || R.rate_type == AFH_RATE_K3) && Te < 0)
-    Te = electron_eV_to_K * lt_col(A.td, A.te_col, field);
-  switch (R.rate_type) {
-  case AFH_RATE_K1: return c0 * c[0] * pow(300 / Te, c[1]);
-  case AFH_RATE_K3: {
-    const double z = (kB / eV) * Te + c[1];
-    return c0 * (c[0] * (z * z) - c[2]) * c[3];
-  }
-  case AFH_RATE_K4: return c0 * c[0] * pow(Tg / 300, c[1]) * exp(-c[2] / Tg);
-  case AFH_RATE_K5: return c0 * c[0] * exp(-c[1] / Tg);
-  case AFH_RATE_K6: return c0 * c[0] * pow(Tg, c[1]);
-  case AFH_RATE_K7: return c0 * c[0] * pow(Tg / c[1], c[2]);
-  case AFH_RATE_K8: return c0 * c[0] * pow(300 / Tg, c[1]);
-  case AFH_RATE_K9: return c0 * c[0] * exp(-c[1] * Tg);
-  case AFH_RATE_K10: return c0 * pow(10.0, c[0] + c[1] * (Tg - 300));
-  case AFH_RATE_K11: return c0 * c[0] * pow(300 / Tg, c[1]) * exp(-c[2] / Tg);
-  case AFH_RATE_K12: return c0 * c[0] * pow(Tg, c[1]) * exp(-c[2] / Tg);
-  case AFH_RATE_K13: return c0 * c[0] * exp(-pow(c[1] / (c[2] + field), c[3]));
-  case AFH_RATE_K14: return c0 * c[0] * exp(-pow(field / c[1], c[2]));
-  default:  // AFH_RATE_K15
-    return c0 * c[0] * exp(-pow(c[1] / (kB * (Tg + field / c[2])), c[3]));
-  }
-}
-
-template <bool SLOW>
-__device__ __forceinline__ double rate_of(const UpdArgs &A, const DevReaction &R,
-                                          double field, double &Te) {
-  const double c0 = R.rate_factor;
-  const double *c = R.c;
-  switch (R.rate_type) {
-  case AFH_RATE_TABULATED_FIELD: return c0 * lt_col(A.chem, R.table_col, field);
-  case AFH_RATE_CONSTANT: return c0 * c[0];
-  case AFH_RATE_LINEAR: return c0 * c[0] * (field - c[1]);
-  case AFH_RATE_EXP_V1: {
-    const double z = c[1] / (c[2] + field);
-    return c0 * c[0] * exp(-(z * z));
-  }
-  case AFH_RATE_EXP_V2: {
-    const double z = field / c[1];
-    return c0 * c[0] * exp(-(z * z));
-  }
-  default: return SLOW ? rate_slow(A, R, field, Te) : 0.0;
-  }
-}
-
 template <int NS, bool SLOW>
 __global__ void __launch_bounds__(256)
     k_update(UpdArgs A, const int32_t *__restrict__ ids, int nc, size_t bsz,
@@ -1004,6 +1004,340 @@ void launch_update(const UpdArgs &A, afh_tree *t, int l,
   else
     hipLaunchKernelGGL((k_update<NS, false>), grid, dim3(256), 0, t->stream, A,
                        t->leaves.at(l), nc, t->bsz, t->fsz, red);
+}
+
+
+// Fused forward-Euler species step: flux_upwind_tree + flux_update_densities
+// of forward_euler (src/m_fluid.f90:56-70) when no face needs a coarse-fine
+// correction (af_consistent_fluxes has no task). k_flux_lds's plane march,
+// and at step k the six face fluxes of cell (i, j, k) are all in hand: x-hi
+// from the next lane, y-hi from the next row through LDS (the tile's last
+// row evaluates the whole face), z-hi evaluated from the register window and
+// carried as z-lo of step k + 1. The cell is then advanced with k_update's
+// expressions (states and |E| of the cell; the flux species' s_deriv value is
+// the staged n_e). Face fluxes leave the kernel only with wf; the reductions
+// are k_flux_lds's (CFL, sigma) and k_update's (chemistry, on the last step).
+// Bitwise the results of k_flux_lds + k_update: same expressions, same
+// operand order. NP = number of previous states (1 or 2).
+// NS: species slots (>= ns); NP: previous states; SD: the derivative state
+// is not one of them (der_q < 0)
+#ifndef AFH_FE_MINW
+#define AFH_FE_MINW 2
+#endif
+#ifndef AFH_FE_LATE  // issue the cell's state loads after the x / y faces
+#define AFH_FE_LATE 0
+#endif
+template <int NC, int LIM, int NS, int NP, bool SD>
+__global__ void __launch_bounds__(256, AFH_FE_MINW)
+    k_fe_lds(FluxArgs A, UpdArgs U, const double *__restrict__ tdi,
+             const int32_t *__restrict__ ids, size_t bsz, size_t fsz,
+             unsigned long long *red, int wf) {
+  using G = FluxLds<NC>;
+  constexpr int NG = NC + 2, NF = NC + 1, TJ = G::TJ, NT = G::NT, RW = G::RW,
+                NR = G::NR, EW = G::EW, ER = G::ER, NPE = G::NPE, EPE = G::EPE;
+  // box-local offsets as 32-bit ints: scalar base + vector offset loads
+  constexpr int SK = NG * NG, FSK = NF * NF, FD = NF * NF * NF;
+  constexpr int NN = NC * NC;
+  extern __shared__ double T[];  // 2 n_points (dynamic)
+  __shared__ double SN[2][NR * RW], SE[2][ER * EW];
+  __shared__ double sv[NT], sd[NT], sf[NT];
+  __shared__ double r1[NT / 64], r2[NT / 64], r3[NT / 64];
+  const int tid = threadIdx.x;
+  const int id = ids[blockIdx.x / G::NTILE];
+  const int i = tid % NC + 1;
+  const int jr = tid / NC;
+  const int j0 = (blockIdx.x % G::NTILE) * TJ + 1, j = j0 + jr;
+  const size_t boff = (size_t)(id - 1) * bsz;
+  const double *ne = A.ne + boff;
+  const double *E = A.E + boff;
+  const double *Ef = A.Ef + (size_t)(id - 1) * fsz;
+  double *F = A.F + (size_t)(id - 1) * fsz;
+  const double *g2 = A.gc2 + (size_t)(id - 1) * 6 * NN;
+  const double ix = A.inv_dx[0], iy = A.inv_dx[1], iz = A.inv_dx[2];
+  const double N_inv = A.N_inv;
+  const int np = A.td.n_points;
+  const int eix = U.e_index, dq = U.der_q, ns = U.ns;
+  for (int e = tid; e < 2 * np; e += NT) T[e] = tdi[e];
+
+  auto ne_at = [&](int k, int e) -> double {
+    if (e >= NR * RW) return 0.0;
+    const int jj = j0 - 2 + e / RW, ii = e % RW - 1;
+    const bool jin = jj >= 0 && jj <= NC + 1, iin = ii >= 0 && ii <= NC + 1;
+    if (jin && iin) return ne[(k * NG + jj) * NG + ii];
+    if (jin && jj >= 1 && jj <= NC) {
+      if (ii == -1) return g2[0 * NN + (k - 1) * NC + (jj - 1)];
+      if (ii == NC + 2) return g2[1 * NN + (k - 1) * NC + (jj - 1)];
+    }
+    if (iin && ii >= 1 && ii <= NC) {
+      if (jj == -1) return g2[2 * NN + (k - 1) * NC + (ii - 1)];
+      if (jj == NC + 2) return g2[3 * NN + (k - 1) * NC + (ii - 1)];
+    }
+    return 0.0;
+  };
+  auto e_at = [&](int k, int e) -> double {
+    if (e >= ER * EW) return 0.0;
+    return E[(k * NG + (j0 - 1 + e / EW)) * NG + e % EW];
+  };
+  const int cc = j * NG + i;
+  const int fcol = (j - 1) * NF + (i - 1);
+  const int gz = (j - 1) * NC + (i - 1);
+  // own column: n_e window k-1 .. k+1 (k = 1 here)
+  double zm1 = ne[cc], z0 = ne[SK + cc], zp1 = ne[2 * SK + cc];
+  const double zm2 = g2[4 * NN + gz];
+#pragma unroll
+  for (int q = 0; q < NPE; q++) {
+    const int e = tid + NT * q;
+    if (e < NR * RW) SN[1][e] = ne_at(1, e);
+  }
+#pragma unroll
+  for (int q = 0; q < EPE; q++) {
+    const int e = tid + NT * q;
+    if (e < ER * EW) SE[1][e] = e_at(1, e);
+  }
+  double exl = Ef[fcol], eyl = Ef[FD + fcol];
+  double exh = i == NC ? Ef[fcol + 1] : 0.0;
+  double eyh = (jr == TJ - 1) ? Ef[FD + fcol + NF] : 0.0;
+  double mu, dcv;
+  double cmax = -HUGE_VAL, smax = -HUGE_VAL, cmin = 1e100;
+  // z low face of the box (between planes 0 and 1)
+  double vz_lo, dz_lo, fz_lo;
+  {
+    const double ezl = Ef[2 * FD + fcol];
+    const double u = upwind_t<LIM>(A.lim, zm2, zm1, z0, zp1, ezl);
+    lds_mu_dc(tdi, A.td, 0.5 * (E[cc] + E[SK + cc]) * 1e21 * N_inv, mu, dcv);
+    mu = mu * N_inv;
+    dz_lo = dcv * N_inv;
+    vz_lo = -mu * ezl;
+    fz_lo = vz_lo * u - dz_lo * iz * (z0 - zm1);
+    if (wf) F[2 * FD + fcol] = fz_lo;
+    smax = fmax(smax, mu * u);
+  }
+  __syncthreads();
+
+  const int cn = (jr + 2) * RW + (i + 1);
+  const int ce = (jr + 1) * EW + i;
+
+  for (int k = 1; k <= NC; k++) {
+    const double *N0 = SN[k & 1], *E0p = SE[k & 1];
+    const bool more = k < NC;
+    // z-high face inputs, then the cell's states, then next step's faces and
+    // the staging of plane k+1 (vmcnt retires in issue order)
+    const double zp2 = k + 2 <= NC + 1 ? ne[(k + 2) * SK + cc]
+                                       : g2[5 * NN + gz];
+    const double ep1 = E[(k + 1) * SK + cc];
+    const int fbn = k * FSK + fcol;
+    const double ezh = Ef[2 * FD + fbn];
+    const int x = k * SK + cc;
+    double pv[NS][NP], dv[NS];
+    auto load_states = [&]() {
+#pragma unroll
+      for (int s = 0; s < NS; s++) {
+#pragma unroll
+        for (int q = 0; q < NP; q++)
+          pv[s][q] = (s >= ns || (!SD && s == eix && q == dq)) ? 0.0
+                                                                : (U.prev[s][q] + boff)[x];
+        dv[s] = (!SD || s >= ns || s == eix) ? 0.0 : (U.der[s] + boff)[x];
+      }
+    };
+#if !AFH_FE_LATE
+    load_states();
+#endif
+    double nexl = 0, neyl = 0, nexh = 0, neyh = 0;
+    if (more) {
+      nexl = Ef[fbn];
+      neyl = Ef[FD + fbn];
+      if (i == NC) nexh = Ef[fbn + 1];
+      if (jr == TJ - 1) neyh = Ef[FD + fbn + NF];
+    }
+    double pn[NPE], pe[EPE];
+#pragma unroll
+    for (int q = 0; q < NPE; q++) pn[q] = more ? ne_at(k + 1, tid + NT * q) : 0.0;
+#pragma unroll
+    for (int q = 0; q < EPE; q++) pe[q] = more ? e_at(k + 1, tid + NT * q) : 0.0;
+
+    const int fb = (k - 1) * FSK + fcol;
+    const double e0 = E0p[ce];
+    // x low face
+    double vx, dx, fx;
+    {
+      const double u = upwind_t<LIM>(A.lim, N0[cn - 2], N0[cn - 1], z0, N0[cn + 1], exl);
+      lds_mu_dc(T, A.td, 0.5 * (E0p[ce - 1] + e0) * 1e21 * N_inv, mu, dcv);
+      mu = mu * N_inv;
+      dx = dcv * N_inv;
+      vx = -mu * exl;
+      fx = vx * u - dx * ix * (z0 - N0[cn - 1]);
+      if (wf) F[fb] = fx;
+      smax = fmax(smax, mu * u);
+    }
+    double vxh = __shfl_down(vx, 1, 64), dxh = __shfl_down(dx, 1, 64);
+    double fxh = __shfl_down(fx, 1, 64);
+    if (i == NC) {
+      const double u = upwind_t<LIM>(A.lim, N0[cn - 1], z0, N0[cn + 1], N0[cn + 2], exh);
+      lds_mu_dc(T, A.td, 0.5 * (e0 + E0p[ce + 1]) * 1e21 * N_inv, mu, dcv);
+      mu = mu * N_inv;
+      dxh = dcv * N_inv;
+      vxh = -mu * exh;
+      fxh = vxh * u - dxh * ix * (N0[cn + 1] - z0);
+      if (wf) F[fb + 1] = fxh;
+      smax = fmax(smax, mu * u);
+    }
+    // y low face
+    double vy, dy, fy;
+    {
+      const double u = upwind_t<LIM>(A.lim, N0[cn - 2 * RW], N0[cn - RW], z0,
+                                     N0[cn + RW], eyl);
+      lds_mu_dc(T, A.td, 0.5 * (E0p[ce - EW] + e0) * 1e21 * N_inv, mu, dcv);
+      mu = mu * N_inv;
+      dy = dcv * N_inv;
+      vy = -mu * eyl;
+      fy = vy * u - dy * iy * (z0 - N0[cn - RW]);
+      if (wf) F[FD + fb] = fy;
+      smax = fmax(smax, mu * u);
+    }
+    sv[tid] = vy;
+    sd[tid] = dy;
+    sf[tid] = fy;
+    __syncthreads();
+#if AFH_FE_LATE
+    load_states();
+#endif
+    double vyh, dyh, fyh;
+    if (jr + 1 < TJ) {
+      vyh = sv[tid + NC];
+      dyh = sd[tid + NC];
+      fyh = sf[tid + NC];
+    } else {
+      // the tile's last row: the whole high face (the next tile, or the box
+      // boundary, owns it; the sigma term is counted by its owner too)
+      const double u = upwind_t<LIM>(A.lim, N0[cn - RW], z0, N0[cn + RW],
+                                     N0[cn + 2 * RW], eyh);
+      lds_mu_dc(T, A.td, 0.5 * (e0 + E0p[ce + EW]) * 1e21 * N_inv, mu, dcv);
+      mu = mu * N_inv;
+      dyh = dcv * N_inv;
+      vyh = -mu * eyh;
+      fyh = vyh * u - dyh * iy * (N0[cn + RW] - z0);
+      if (j == NC) {
+        if (wf) F[FD + fb + NF] = fyh;
+        smax = fmax(smax, mu * u);
+      }
+    }
+    // z high face (low face of cell k+1)
+    double vzh, dzh, fzh;
+    {
+      const double u = upwind_t<LIM>(A.lim, zm1, z0, zp1, zp2, ezh);
+      lds_mu_dc(T, A.td, 0.5 * (e0 + ep1) * 1e21 * N_inv, mu, dcv);
+      mu = mu * N_inv;
+      dzh = dcv * N_inv;
+      vzh = -mu * ezh;
+      fzh = vzh * u - dzh * iz * (zp1 - z0);
+      if (wf) F[2 * FD + fb + FSK] = fzh;
+      smax = fmax(smax, mu * u);
+    }
+    {
+      const double mvx = fmax(fabs(vxh), fabs(vx)), mdx = fmax(dxh, dx);
+      const double mvy = fmax(fabs(vyh), fabs(vy)), mdy = fmax(dyh, dy);
+      double c = 0.0;
+      c = c + (1.0 * mvx * ix + 2 * mdx * (ix * ix));
+      c = c + (1.0 * mvy * iy + 2 * mdy * (iy * iy));
+      const double mv = fmax(fabs(vzh), fabs(vz_lo));
+      const double md = fmax(dzh, dz_lo);
+      cmax = fmax(cmax, c + (1.0 * mv * iz + 2 * md * (iz * iz)));
+    }
+    // density update of cell (i, j, k): k_update
+    {
+      double y[NS], der[NS], dens[NS];
+#pragma unroll
+      for (int s = 0; s < NS; s++) {
+#pragma unroll
+        for (int q = 0; q < NP; q++)
+          if (!SD && s == eix && q == dq) pv[s][q] = z0;
+        if (SD && s == eix) dv[s] = z0;
+        double tmp = 0.0;
+#pragma unroll
+        for (int q = 0; q < NP; q++) tmp = tmp + U.w_prev[q] * pv[s][q];
+        y[s] = tmp;
+        double v = dv[s];
+#pragma unroll
+        for (int q = 0; q < NP; q++)
+          if (!SD && q == dq) v = pv[s][q];
+        dens[s] = v > 0.0 ? v : 0.0;
+        der[s] = 0.0;
+      }
+      const double field = 1e21 * U.inv_N * e0;
+      double Te = -1.0;
+      for (int r = 0; r < U.nr; r++) {
+        const DevReaction &R = U.reac[r];
+        double rate = rate_of<false>(U, R, field, Te);
+        double prod = 1.0;
+        for (int q = 0; q < R.n_in; q++) prod = prod * sel(dens, R.ix_in[q] - 1);
+        rate = rate * prod;
+        for (int q = 0; q < R.n_in; q++) add_at(der, R.ix_in[q] - 1, -rate);
+        for (int q = 0; q < R.n_out; q++)
+          add_at(der, R.ix_out[q] - 1, rate * R.mult_out[q]);
+      }
+      if (U.last_step) {
+        const double eps = 1e-100;
+#pragma unroll
+        for (int s = 0; s < NS; s++) {
+          if (s >= ns) break;
+          double a, b;
+          if (U.dt_chemistry_nmin > 0) {
+            a = dens[s] + U.dt_chemistry_nmin;
+            b = fabs(der[s]);
+            b = b > eps ? b : eps;
+          } else {
+            a = dens[s] > eps ? dens[s] : eps;
+            b = -der[s] > eps ? -der[s] : eps;
+          }
+          cmin = fmin(cmin, a / b);
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < NS; s++) y[s] = y[s] + U.dt * der[s];
+      const double div = U.dt_dr[0] * (fx - fxh);
+      const double dvy = U.dt_dr[1] * (fy - fyh);
+      const double dvz = U.dt_dr[2] * (fz_lo - fzh);
+#pragma unroll
+      for (int s = 0; s < NS; s++)
+        if (s == eix) y[s] = y[s] + div + dvy + dvz;
+#pragma unroll
+      for (int s = 0; s < NS; s++)
+        if (s < ns) (U.out[s] + boff)[x] = y[s];
+    }
+    if (more) {
+#pragma unroll
+      for (int q = 0; q < NPE; q++) {
+        const int e = tid + NT * q;
+        if (e < NR * RW) SN[(k + 1) & 1][e] = pn[q];
+      }
+#pragma unroll
+      for (int q = 0; q < EPE; q++) {
+        const int e = tid + NT * q;
+        if (e < ER * EW) SE[(k + 1) & 1][e] = pe[q];
+      }
+    }
+    zm1 = z0;
+    z0 = zp1;
+    zp1 = zp2;
+    vz_lo = vzh, dz_lo = dzh, fz_lo = fzh;
+    exl = nexl, eyl = neyl, exh = nexh, eyh = neyh;
+    __syncthreads();
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    cmax = fmax(cmax, __shfl_xor(cmax, o, 64));
+    smax = fmax(smax, __shfl_xor(smax, o, 64));
+    cmin = fmin(cmin, __shfl_xor(cmin, o, 64));
+  }
+  const int lane = tid & 63, w = tid >> 6;
+  if (lane == 0) r1[w] = cmax, r2[w] = smax, r3[w] = cmin;
+  __syncthreads();
+  if (tid == 0) {
+    for (int q = 1; q < NT / 64; q++)
+      cmax = fmax(cmax, r1[q]), smax = fmax(smax, r2[q]), cmin = fmin(cmin, r3[q]);
+    atomicMax(&red[red_shard()], dbl_to_ord(cmax));
+    atomicMax(&red[RED_SHARDS + red_shard()], dbl_to_ord(smax));
+    if (U.last_step) atomicMin(&red[2 * RED_SHARDS + red_shard()], dbl_to_ord(cmin));
+  }
 }
 
 }  // namespace afh
@@ -1176,14 +1510,11 @@ static void launch_flux_lds(afh_tree *t, const FluxArgs &A, const double *tdi,
                        t->stream, A, tdi, t->leaves.at(l), t->bsz, t->fsz, red);
 }
 
-extern "C" {
-
-int32_t afh_flux_upwind_tree(afh_fluid *f, int32_t s_deriv, double *dt_lim) {
-  if (!f || !dt_lim) return set_error(AFH_ERR_ARG, "null argument");
+// flux_upwind_tree before the face loop (m_af_flux_schemes.f90:666-720):
+// af_restrict_ref_boundary, then two ghost layers of the flux species
+static int32_t flux_prelude(afh_fluid *f, int iv) {
   afh_tree *t = f->t;
-  const int nc = t->nc, n3 = nc * nc * nc;
-  const int iv = f->d.i_electron + s_deriv;
-  if (iv < 1 || iv > t->nvc) return set_error(AFH_ERR_ARG, "bad s_deriv");
+  const int nc = t->nc;
   int32_t e;
   // af_restrict_ref_boundary (per level, for the sharding hook)
   for (int l = t->nlvl; l >= 2; l--) {
@@ -1206,8 +1537,11 @@ int32_t afh_flux_upwind_tree(afh_fluid *f, int32_t s_deriv, double *dt_lim) {
     if (t->lvl_rb_coarse[l - 1] && (e = call_hook(t, AFH_HOOK_RIMS, l, iv)))
       return e;
   }
-  if ((e = red_init(t, 0, -HUGE_VAL)) || (e = red_init(t, 1, -HUGE_VAL))) return e;
-  auto *red = reinterpret_cast<unsigned long long *>(t->scratch);
+  return AFH_OK;
+}
+
+static FluxArgs flux_args(afh_fluid *f, int iv) {
+  afh_tree *t = f->t;
   FluxArgs A;
   A.ne = t->ccv(iv);
   A.E = t->ccv(f->d.i_efld);
@@ -1217,6 +1551,76 @@ int32_t afh_flux_upwind_tree(afh_fluid *f, int32_t s_deriv, double *dt_lim) {
   A.td = f->td;
   A.N_inv = 1 / f->d.gas_number_density;
   A.lim = f->d.limiter;
+  return A;
+}
+
+// flux_update_densities arguments (m_af_flux_schemes.f90:320-436); bytes =
+// algorithmic HBM bytes per cell of k_update
+static int32_t upd_args(afh_fluid *f, double dt, int32_t s_deriv, int32_t n_prev,
+                        const int32_t *s_prev, const double *w_prev, int32_t s_out,
+                        int32_t last_step, UpdArgs &A, double &upd_bytes) {
+  if (n_prev < 1 || n_prev > MAXPREV || !s_prev || !w_prev)
+    return set_error(AFH_ERR_ARG, "flux_update_densities: bad previous states");
+  afh_tree *t = f->t;
+  if (f->d.n_species > 16)
+    return set_error(AFH_ERR_UNSUPPORTED, "more than 16 plasma species");
+  auto bad = [&](int s_) {
+    for (int s = 0; s < f->d.n_species; s++) {
+      const int iv = f->d.species_iv[s] + s_;
+      if (iv < 1 || iv > t->nvc) return true;
+    }
+    return false;
+  };
+  for (int q = 0; q < n_prev; q++)
+    if (bad(s_prev[q])) return set_error(AFH_ERR_ARG, "bad previous state");
+  if (bad(s_deriv) || bad(s_out)) return set_error(AFH_ERR_ARG, "bad s_deriv / s_out");
+  A.ns = f->d.n_species;
+  A.nr = f->d.n_reactions;
+  A.n_prev = n_prev;
+  A.last_step = last_step ? 1 : 0;
+  A.e_index = f->e_index;
+  A.der_q = -1;
+  for (int q = 0; q < n_prev; q++)
+    if (s_prev[q] == s_deriv && A.der_q < 0) A.der_q = q;
+  for (int q = 0; q < n_prev; q++) A.w_prev[q] = w_prev[q];
+  for (int s = 0; s < A.ns; s++) {
+    const int iv = f->d.species_iv[s];
+    for (int q = 0; q < n_prev; q++) A.prev[s][q] = t->ccv(iv + s_prev[q]);
+    A.der[s] = t->ccv(iv + s_deriv);
+    A.out[s] = t->ccv(iv + s_out);
+  }
+  A.E = t->ccv(f->d.i_efld);
+  A.F = t->fcv(f->d.f_flux);
+  A.reac = f->d_reac;
+  A.chem = f->chem;
+  A.td = f->td;
+  A.te_col = f->d.td_energy_col;
+  A.Tg = f->d.gas_temperature;
+  A.inv_N = 1 / f->d.gas_number_density;
+  A.dt = dt;
+  A.dt_chemistry_nmin = f->d.dt_chemistry_nmin;
+  // algorithmic bytes per cell: each distinct species state read once, the
+  // output written once, |E| and 3 fluxes read (SURVEY.md 8(d))
+  int distinct = n_prev;
+  for (int q = 0; q < n_prev; q++) distinct -= (s_prev[q] == s_deriv) ? 1 : 0;
+  distinct += 1;
+  upd_bytes = 8.0 * (A.ns * (distinct + 1) + 4);
+  return AFH_OK;
+}
+
+extern "C" {
+
+int32_t afh_flux_upwind_tree(afh_fluid *f, int32_t s_deriv, double *dt_lim) {
+  if (!f || !dt_lim) return set_error(AFH_ERR_ARG, "null argument");
+  afh_tree *t = f->t;
+  const int nc = t->nc, n3 = nc * nc * nc;
+  const int iv = f->d.i_electron + s_deriv;
+  if (iv < 1 || iv > t->nvc) return set_error(AFH_ERR_ARG, "bad s_deriv");
+  int32_t e;
+  if ((e = flux_prelude(f, iv))) return e;
+  if ((e = red_init(t, 0, -HUGE_VAL)) || (e = red_init(t, 1, -HUGE_VAL))) return e;
+  auto *red = reinterpret_cast<unsigned long long *>(t->scratch);
+  FluxArgs A = flux_args(f, iv);
   const bool shfl = (64 % nc) == 0;
   for (int l = 1; l <= t->nlvl; l++) {
     const int n = t->leaves.n(l);
@@ -1262,45 +1666,15 @@ int32_t afh_flux_update_densities(afh_fluid *f, double dt, int32_t s_deriv,
                                   int32_t n_prev, const int32_t *s_prev,
                                   const double *w_prev, int32_t s_out,
                                   int32_t last_step, double *dt_lim) {
-  if (!f || !dt_lim || n_prev < 1 || n_prev > MAXPREV || !s_prev || !w_prev)
-    return set_error(AFH_ERR_ARG, "afh_flux_update_densities: bad argument");
+  if (!f || !dt_lim) return set_error(AFH_ERR_ARG, "afh_flux_update_densities: null");
   afh_tree *t = f->t;
-  if (f->d.n_species > 16)
-    return set_error(AFH_ERR_UNSUPPORTED, "more than 16 plasma species");
   const int nc = t->nc, n3 = nc * nc * nc;
   UpdArgs A;
-  A.ns = f->d.n_species;
-  A.nr = f->d.n_reactions;
-  A.n_prev = n_prev;
-  A.last_step = last_step ? 1 : 0;
-  A.e_index = f->e_index;
-  A.der_q = -1;
-  for (int q = 0; q < n_prev; q++)
-    if (s_prev[q] == s_deriv && A.der_q < 0) A.der_q = q;
-  for (int q = 0; q < n_prev; q++) A.w_prev[q] = w_prev[q];
-  for (int s = 0; s < A.ns; s++) {
-    const int iv = f->d.species_iv[s];
-    for (int q = 0; q < n_prev; q++) A.prev[s][q] = t->ccv(iv + s_prev[q]);
-    A.der[s] = t->ccv(iv + s_deriv);
-    A.out[s] = t->ccv(iv + s_out);
-  }
-  A.E = t->ccv(f->d.i_efld);
-  A.F = t->fcv(f->d.f_flux);
-  A.reac = f->d_reac;
-  A.chem = f->chem;
-  A.td = f->td;
-  A.te_col = f->d.td_energy_col;
-  A.Tg = f->d.gas_temperature;
-  A.inv_N = 1 / f->d.gas_number_density;
-  A.dt = dt;
-  A.dt_chemistry_nmin = f->d.dt_chemistry_nmin;
-  // algorithmic bytes per cell: each distinct species state read once, the
-  // output written once, |E| and 3 fluxes read (SURVEY.md 8(d))
-  int distinct = n_prev;
-  for (int q = 0; q < n_prev; q++) distinct -= (s_prev[q] == s_deriv) ? 1 : 0;
-  distinct += 1;
-  const double upd_bytes = 8.0 * (A.ns * (distinct + 1) + 4);
+  double upd_bytes;
   int32_t e;
+  if ((e = upd_args(f, dt, s_deriv, n_prev, s_prev, w_prev, s_out, last_step, A,
+                    upd_bytes)))
+    return e;
   if ((e = red_init(t, 2, 1e100))) return e;
   auto *red = reinterpret_cast<unsigned long long *>(t->scratch) + 2 * RED_SHARDS;
   for (int l = 1; l <= t->nlvl; l++) {
@@ -1328,6 +1702,120 @@ int32_t afh_flux_update_densities(afh_fluid *f, double dt, int32_t s_deriv,
   }
   dt_lim[0] = r;
   dt_lim[1] = 1e100;
+  return AFH_OK;
+}
+
+}  // extern "C"
+
+// species slots of the fused kernel (runtime ns <= FE_MAX_SPECIES)
+constexpr int FE_MAX_SPECIES = 4;
+
+template <int NC, int NP, bool SD>
+static void launch_fe(afh_tree *t, const FluxArgs &A, const UpdArgs &U,
+                      const double *tdi, int l, unsigned long long *red, int wf) {
+  const dim3 grid(t->leaves.n(l) * FluxLds<NC>::NTILE);
+  const size_t lds = 2 * sizeof(double) * A.td.n_points;
+  hipLaunchKernelGGL((k_fe_lds<NC, AFH_LIM_KOREN, FE_MAX_SPECIES, NP, SD>), grid,
+                     dim3(FluxLds<NC>::NT), lds, t->stream, A, U, tdi,
+                     t->leaves.at(l), t->bsz, t->fsz, red, wf);
+}
+
+template <int NC>
+static void launch_fe_nc(afh_tree *t, const FluxArgs &A, const UpdArgs &U,
+                         const double *tdi, int l, unsigned long long *red, int wf) {
+  const bool sd = U.der_q < 0;
+  if (U.n_prev == 1)
+    sd ? launch_fe<NC, 1, true>(t, A, U, tdi, l, red, wf)
+       : launch_fe<NC, 1, false>(t, A, U, tdi, l, red, wf);
+  else
+    sd ? launch_fe<NC, 2, true>(t, A, U, tdi, l, red, wf)
+       : launch_fe<NC, 2, false>(t, A, U, tdi, l, red, wf);
+}
+
+extern "C" {
+
+int32_t afh_fluid_forward_euler(afh_fluid *f, double dt, int32_t s_deriv,
+                                int32_t n_prev, const int32_t *s_prev,
+                                const double *w_prev, int32_t s_out,
+                                int32_t last_step, int32_t store_flux,
+                                double *dt_lim) {
+  if (!f || !dt_lim) return set_error(AFH_ERR_ARG, "afh_fluid_forward_euler: null");
+  afh_tree *t = f->t;
+  const int nc = t->nc, n3 = nc * nc * nc;
+  const int iv = f->d.i_electron + s_deriv;
+  if (iv < 1 || iv > t->nvc) return set_error(AFH_ERR_ARG, "bad s_deriv");
+  UpdArgs U;
+  double upd_bytes;
+  int32_t e;
+  if ((e = upd_args(f, dt, s_deriv, n_prev, s_prev, w_prev, s_out, last_step, U,
+                    upd_bytes)))
+    return e;
+  // the fused kernel reads n_e(s_deriv) of neighbouring rows of the same box
+  // while other workgroups write the outputs: no output may alias it or |E|
+  bool alias = false;
+  for (int s = 0; s < f->d.n_species; s++) {
+    const int ivo = f->d.species_iv[s] + s_out;
+    alias |= ivo == iv || ivo == f->d.i_efld;
+  }
+  // k_fe_lds is opt-in (AFH_FE_FUSED=1): it moves 56 B/cell less than the
+  // two kernels, but at the occupancy its registers allow (2 waves per SIMD)
+  // it measured 20 % slower on S1-64 (profiles/r01_fe_ab.txt)
+  const char *fused_env = getenv("AFH_FE_FUSED");
+  const bool fused = fused_env && atoi(fused_env) && f->d_tdi &&
+                     (nc == 16 || nc == 32 || nc == 64) && !t->any_cflux &&
+                     !f->slow_rates && f->d.n_species <= FE_MAX_SPECIES &&
+                     n_prev <= 2 && !alias && f->d.limiter == AFH_LIM_KOREN;
+  if (!fused) {
+    double a[2], b[2];
+    if ((e = afh_flux_upwind_tree(f, s_deriv, a)) ||
+        (e = afh_flux_update_densities(f, dt, s_deriv, n_prev, s_prev, w_prev, s_out,
+                                       last_step, b)))
+      return e;
+    dt_lim[0] = a[0], dt_lim[1] = a[1], dt_lim[2] = b[0], dt_lim[3] = b[1];
+    return AFH_OK;
+  }
+  if ((e = flux_prelude(f, iv))) return e;
+  if ((e = red_init(t, 0, -HUGE_VAL)) || (e = red_init(t, 1, -HUGE_VAL)) ||
+      (e = red_init(t, 2, 1e100)))
+    return e;
+  auto *red = reinterpret_cast<unsigned long long *>(t->scratch);
+  const FluxArgs A0 = flux_args(f, iv);
+  // algorithmic bytes per cell: the update's states and outputs, of which
+  // n_e(s_deriv) is the flux kernel's, + |E| and the 3 face fields (40 B,
+  // the 32 B of |E| + 3 fluxes k_update would read + the 8 B of n_e), + the
+  // 3 face fluxes with store_flux
+  const double fe_bytes = upd_bytes + (store_flux ? 24.0 : 0.0);
+  for (int l = 1; l <= t->nlvl; l++) {
+    const int n = t->leaves.n(l);
+    if (!n) continue;
+    FluxArgs A = A0;
+    for (int q = 0; q < 3; q++) {
+      A.inv_dx[q] = 1 / t->lvl_dr[3 * (l - 1) + q];
+      U.dt_dr[q] = dt / t->lvl_dr[3 * (l - 1) + q];
+    }
+    prof_begin(t, AFH_PROF_FE);
+    switch (nc) {
+    case 16: launch_fe_nc<16>(t, A, U, f->d_tdi, l, red, store_flux != 0); break;
+    case 32: launch_fe_nc<32>(t, A, U, f->d_tdi, l, red, store_flux != 0); break;
+    default: launch_fe_nc<64>(t, A, U, f->d_tdi, l, red, store_flux != 0); break;
+    }
+    prof_end(t, AFH_PROF_FE, fe_bytes * n3 * n);
+    AFH_LAUNCH_CHECK("k_fe_lds");
+  }
+  if ((e = red_finish(t, 0, true)) || (e = red_finish(t, 1, true))) return e;
+  if (last_step && (e = red_finish(t, 2, false))) return e;
+  double r[3];
+  if ((e = red_fetch(t, 0, 3, r)) || (e = call_hook(t, AFH_HOOK_MAX, 0, 0, r, 2)))
+    return e;
+  if (last_step) {
+    if ((e = call_hook(t, AFH_HOOK_MIN, 0, 0, r + 2, 1))) return e;
+  } else {
+    r[2] = 1e100;
+  }
+  dt_lim[0] = 1 / r[0];
+  dt_lim[1] = 8.8541878176e-12 / (1.6022e-19 * std::max(r[1], 1e-100));
+  dt_lim[2] = r[2];
+  dt_lim[3] = 1e100;
   return AFH_OK;
 }
 

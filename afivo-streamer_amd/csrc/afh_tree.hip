@@ -454,6 +454,15 @@ int32_t afh_tree_create(const afh_tree_desc *d, int32_t device,
         return set_error(AFH_ERR_ARG, "box %d level mismatch", id);
     }
   }
+  t->any_cflux = false;
+  for (int id = 1; id <= t->nb; id++) {
+    const afh_box_meta &m = t->boxes[id - 1];
+    if (m.children[0] == 0) continue;
+    for (int nb = 0; nb < 6; nb++) {
+      const int nb_id = m.neighbors[nb];
+      if (nb_id > 0 && t->boxes[nb_id - 1].children[0] == 0) t->any_cflux = true;
+    }
+  }
   // derived task lists
   std::vector<std::vector<int32_t>> refb(t->nlvl), cfl(t->nlvl);
   for (int l = 0; l < t->nlvl; l++) {

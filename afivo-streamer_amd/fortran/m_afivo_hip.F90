@@ -63,6 +63,8 @@ module m_afivo_hip
   integer(c_int32_t), parameter :: AFH_PROF_FLUX = 3
   integer(c_int32_t), parameter :: AFH_PROF_UPDATE = 4
   integer(c_int32_t), parameter :: AFH_PROF_GSRB_PAIR = 5
+  integer(c_int32_t), parameter :: AFH_PROF_GSRB_PAIR_TILED = 6
+  integer(c_int32_t), parameter :: AFH_PROF_FE = 7
 
   type, bind(C) :: afh_box_meta
      integer(c_int32_t) :: lvl
@@ -349,6 +351,21 @@ module m_afivo_hip
        real(c_double), intent(out)    :: dt_lim(2)
        integer(c_int32_t)             :: afh_flux_update_densities
      end function afh_flux_update_densities
+
+     ! forward_euler's species part (m_fluid.f90:56-70): fused on the device
+     function afh_fluid_forward_euler(f, dt, s_deriv, n_prev, s_prev, w_prev, &
+          s_out, last_step, store_flux, dt_lim) &
+          bind(C, name=afh_pfx//"fluid_forward_euler")
+       import
+       type(c_ptr), value             :: f
+       real(c_double), value          :: dt
+       integer(c_int32_t), value      :: s_deriv, n_prev
+       integer(c_int32_t), intent(in) :: s_prev(*)
+       real(c_double), intent(in)     :: w_prev(*)
+       integer(c_int32_t), value      :: s_out, last_step, store_flux
+       real(c_double), intent(out)    :: dt_lim(4)
+       integer(c_int32_t)             :: afh_fluid_forward_euler
+     end function afh_fluid_forward_euler
 
      function afh_profile_enable(t, kclass) bind(C, name=afh_pfx//"profile_enable")
        import

@@ -61,12 +61,20 @@ def build_case(lib, config, device, coarse_cycles, shard_ranks=None):
     return case
 
 
-def unit_step(case, dt):
-    """field_compute(1 V-cycle) + forward-Euler sub-step; returns dt limits."""
-    res = case.field_compute(0, n_vcycles=1)
-    d1 = case.fluid.flux_upwind_tree(0)
-    d2 = case.fluid.flux_update_densities(dt, 0, [0], [1.0], 0, True)
-    return res, d1, d2
+def unit_step(case, dt, k):
+    """One sub-step of af_heuns_method (m_af_advance.f90:159-163), the
+    reference's default integrator: field_compute (1 V-cycle) on the
+    derivative state + forward_euler's species part (flux_upwind_tree +
+    flux_update_densities). Even k: stage 1 (state 0 -> 1); odd k: stage 2
+    (states 0, 1 -> 0, with the chemistry dt limit). Returns the residuals and
+    dt limits."""
+    if k % 2 == 0:
+        res = case.field_compute(0, n_vcycles=1)
+        d = case.fluid.forward_euler(dt, 0, [0], [1.0], 1, False)
+    else:
+        res = case.field_compute(1, n_vcycles=1)
+        d = case.fluid.forward_euler(0.5 * dt, 1, [0, 1], [0.5, 0.5], 0, True)
+    return res, d
 
 
 def cpu_baseline(config, coarse_cycles, steps=2):
@@ -85,10 +93,11 @@ def cpu_baseline(config, coarse_cycles, steps=2):
     case = StreamerCase(lib, topo, td, chem, -dom[2] * (-2.5e6),
                         coarse_cycles=coarse_cycles)
     seed_state(case, width=0.05 * dom[2])
-    unit_step(case, 1e-13)
+    unit_step(case, 1e-13, 0)
+    unit_step(case, 1e-13, 1)
     t0 = time.perf_counter()
-    for _ in range(steps):
-        unit_step(case, 1e-13)
+    for k in range(steps):
+        unit_step(case, 1e-13, k)
     dt = time.perf_counter() - t0
     from afh.streamer import cells
     ncell = cells(topo)
@@ -148,8 +157,8 @@ def main():
     dt = 1e-13
 
     case.field_compute(0, n_vcycles=2)  # initial potential (untimed)
-    for _ in range(args.warmup):
-        unit_step(case, dt)
+    for k in range(args.warmup):
+        unit_step(case, dt, k)
     case.tree.sync()
 
     def barrier():
@@ -163,8 +172,8 @@ def main():
     barrier()
     case.tree.sync()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        last = unit_step(case, dt)
+    for k in range(args.steps):
+        last = unit_step(case, dt, args.warmup + k)
     case.tree.sync()
     barrier()
     elapsed = time.perf_counter() - t0

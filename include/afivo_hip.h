@@ -264,6 +264,23 @@ int32_t afh_flux_update_densities(afh_fluid *f, double dt, int32_t s_deriv,
                                   const double *w_prev, int32_t s_out,
                                   int32_t last_step, double *dt_lim);
 
+/* The species part of forward_euler (src/m_fluid.f90:56-70):
+ * flux_upwind_tree(s_deriv) followed by flux_update_densities. When no face
+ * needs a coarse-fine correction anywhere in the topology (no
+ * af_consistent_fluxes task), the limiter is Koren, all reaction rates are
+ * field forms, n_species <= 4, n_prev <= 2 and no output state aliases
+ * n_e(s_deriv) or |E|, both can run as one fused kernel per level (opt-in,
+ * environment AFH_FE_FUSED=1; the face fluxes stay on chip and are written
+ * to f_flux only with store_flux); otherwise the two calls above run. Results are bitwise those of the two
+ * calls. dt_lim[4] = (CFL limit, dielectric relaxation limit, chemistry
+ * limit on the last step / 1e100, 1e100) -- the reference's dt_limits(1:4)
+ * before dt_cfl_number. */
+int32_t afh_fluid_forward_euler(afh_fluid *f, double dt, int32_t s_deriv,
+                                int32_t n_prev, const int32_t *s_prev,
+                                const double *w_prev, int32_t s_out,
+                                int32_t last_step, int32_t store_flux,
+                                double *dt_lim);
+
 /* Kernel timing (replaces the reference's omp_get_wtime cost buckets,
  * src/m_streamer.f90:181-187): while enabled, every launch of the selected
  * kernel class is bracketed by HIP events on the tree's stream;
@@ -275,6 +292,7 @@ int32_t afh_flux_update_densities(afh_fluid *f, double dt, int32_t s_deriv,
 #define AFH_PROF_UPDATE 4    /* density update */
 #define AFH_PROF_GSRB_PAIR 5 /* fused red+black Gauss-Seidel pair (whole boxes) */
 #define AFH_PROF_GSRB_PAIR_TILED 6 /* the same with NC/4-row tiles */
+#define AFH_PROF_FE 7        /* fused flux + density update (afh_fluid_forward_euler) */
 int32_t afh_profile_enable(afh_tree *t, int32_t kclass);
 int32_t afh_profile_read(afh_tree *t, double *total_ms, int64_t *launches,
                          double *bytes);

@@ -1754,6 +1754,25 @@ int32_t afo_flux_update_densities(afh_fluid *fl, double dt, int32_t s_deriv,
   return AFH_OK;
 }
 
+/* The species part of forward_euler (src/m_fluid.f90:56-70):
+ * flux_upwind_tree then flux_update_densities. store_flux is a device
+ * option (the face fluxes are always stored here). */
+int32_t afo_fluid_forward_euler(afh_fluid *f, double dt, int32_t s_deriv,
+                                int32_t n_prev, const int32_t *s_prev,
+                                const double *w_prev, int32_t s_out,
+                                int32_t last_step, int32_t store_flux,
+                                double *dt_lim) {
+  (void)store_flux;
+  double a[2], b[2];
+  int32_t e;
+  if ((e = afo_flux_upwind_tree(f, s_deriv, a)) ||
+      (e = afo_flux_update_densities(f, dt, s_deriv, n_prev, s_prev, w_prev, s_out,
+                                     last_step, b)))
+    return e;
+  dt_lim[0] = a[0], dt_lim[1] = a[1], dt_lim[2] = b[0], dt_lim[3] = b[1];
+  return AFH_OK;
+}
+
 /* Kernel timing is a device concept; the oracle accepts and ignores it. */
 int32_t afo_profile_enable(afh_tree *t, int32_t kclass) {
   (void)t, (void)kclass;

@@ -59,6 +59,11 @@ int32_t afo_flux_update_densities(afh_fluid *f, double dt, int32_t s_deriv,
                                   int32_t n_prev, const int32_t *s_prev,
                                   const double *w_prev, int32_t s_out,
                                   int32_t last_step, double *dt_lim);
+int32_t afo_fluid_forward_euler(afh_fluid *f, double dt, int32_t s_deriv,
+                                int32_t n_prev, const int32_t *s_prev,
+                                const double *w_prev, int32_t s_out,
+                                int32_t last_step, int32_t store_flux,
+                                double *dt_lim);
 int32_t afo_profile_enable(afh_tree *t, int32_t kclass);
 int32_t afo_profile_read(afh_tree *t, double *total_ms, int64_t *launches,
                          double *bytes);

@@ -9,7 +9,7 @@ mkdir -p gpurun_out/pmc
 CFG=${CFG:-s1-64}
 [ -x scripts/pmc_calib ] || hipcc --offload-arch=gfx950 -O3 scripts/pmc_calib.hip -o scripts/pmc_calib || exit 1
 for c in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 600 rocprofv3 --pmc $c --kernel-include-regex "${KREGEX:-k_gsrb_pair}" \
+  timeout -k 10 600 rocprofv3 --pmc $c --kernel-include-regex "${KREGEX:-k_gsrb_pair2}" \
     --output-format csv -d gpurun_out/pmc/$c -o run -- \
     python3 bench.py --config $CFG --steps 2 --warmup 0 --no-cpu-baseline > gpurun_out/pmc/$c.log 2>&1
   rc=$?; echo "pmc $c rc=$rc"

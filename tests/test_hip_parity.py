@@ -116,11 +116,41 @@ def test_hip_bitwise_equals_oracle_heun_step(hip, oracle, name, smoother, coarse
     for c in (ca, cb):
         c.field_compute(0, check_residual=False)
     _assert_same(ca, cb, [IV["phi"], IV["tmp"], IV["rhs"], IV["efld"]], [FV["field"]])
+    ca.store_flux = True  # the fused species step keeps the face fluxes
     la = ca.heun_step(1e-12, check_residual=False)
     lb = cb.heun_step(1e-12, check_residual=False)
     assert la == lb
     _assert_same(ca, cb, [IV["e"], IV["e"] + 1, IV["pos"], IV["neg"], IV["phi"]],
                  [FV["flux"], FV["field"]])
+
+
+# forward_euler species sub-steps (s_deriv, s_prev, w_prev, s_out): the two
+# Heun stages, a derivative state that is no previous state (one and two
+# previous states), and the in-place step (which must take the two-call path)
+FE_STEPS = [(0, [0], [1.0], 1), (1, [0, 1], [0.5, 0.5], 0), (1, [0], [1.0], 2),
+            (2, [0, 1], [0.25, 0.75], 1), (1, [1], [1.0], 1)]
+
+
+@pytest.mark.parametrize("fused", ["0", "1"])
+@pytest.mark.parametrize("store", [0, 1])
+@pytest.mark.parametrize("name", ["uni16_l3", "uni32_l2", "uni64_l2", "amr16"])
+def test_forward_euler_equals_oracle(hip, oracle, name, store, fused, monkeypatch):
+    """afh_fluid_forward_euler (with AFH_FE_FUSED=1: k_fe_lds on trees
+    without coarse-fine flux corrections) gives the bits of the oracle's
+    flux_upwind_tree + flux_update_densities: every species state, the dt
+    limits, and with store_flux the face fluxes."""
+    monkeypatch.setenv("AFH_FE_FUSED", fused)
+    g = golden.load("uni8")
+    ca, cb = _pair(hip, oracle, TOPOS[name](), g)
+    for c in (ca, cb):
+        c.field_compute(0, check_residual=False)
+    states = [IV[sp] + s for sp in ("e", "pos", "neg") for s in range(3)]
+    for n, (sd, sp, wp, so) in enumerate(FE_STEPS):
+        last = n % 2 == 1
+        la = ca.fluid.forward_euler(1e-12, sd, sp, wp, so, last, store_flux=store)
+        lb = cb.fluid.forward_euler(1e-12, sd, sp, wp, so, last, store_flux=store)
+        assert la == lb, (n, la, lb)
+        _assert_same(ca, cb, states, [FV["flux"]] if store else [])
 
 
 @pytest.mark.parametrize("helm", [0.0, 44081.25])
