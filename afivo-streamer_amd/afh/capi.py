@@ -119,6 +119,8 @@ SIGNATURES = {
     "mg_fas_vcycle_maxres": (i32, [_VP, i32, P_f64]),
     "mg_fas_fmg": (i32, [_VP, i32, i32]),
     "mg_compute_phi_gradient": (i32, [_VP, i32, f64, i32]),
+    "mg_set_box_stencil": (i32, [_VP, i32, P_f64, P_f64]),
+    "mg_set_box_lsf": (i32, [_VP, i32, i32, P_i32, P_f64, P_f64, i32]),
     "fluid_create": (i32, [_VP, C.POINTER(FluidDesc), _PVP]),
     "fluid_destroy": (i32, [_VP]),
     "field_set_rhs": (i32, [_VP, i32, i32]),

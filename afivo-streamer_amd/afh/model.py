@@ -181,6 +181,29 @@ class Multigrid:
         self.lib.call("mg_fas_vcycle_maxres", self.h, highest_lvl, C.byref(out))
         return out.value
 
+    def set_box_stencil(self, box_id, v, bc_correction=None):
+        """The electrode operator stencil of box `box_id` as afivo stores it
+        (mg_box_lsf_stencil): v(7, nc, nc, nc) -- here an array of shape
+        (nc, nc, nc, 7), [k][j][i][c] -- and bc_correction (nc, nc, nc) or
+        None; v = None removes it."""
+        vp = None if v is None else np.ascontiguousarray(v, dtype=np.float64)
+        bp = None if bc_correction is None else np.ascontiguousarray(
+            bc_correction, dtype=np.float64)
+        self.lib.call("mg_set_box_stencil", self.h, int(box_id),
+                      None if vp is None else vp.ctypes.data_as(capi.P_f64),
+                      None if bp is None else bp.ctypes.data_as(capi.P_f64))
+
+    def set_box_lsf(self, box_id, ix, dd, bval, i_lsf):
+        """Boundary distances of box `box_id` for mg_box_lpllsf_gradient:
+        ix (n, 3) 1-based (i, j, k), dd (n, 6), bval (nc, nc, nc) the
+        electrode potential per cell; n = 0 removes."""
+        ix = _i32(ix).reshape(-1)
+        dd = np.ascontiguousarray(dd, dtype=np.float64).reshape(-1)
+        bv = np.ascontiguousarray(bval, dtype=np.float64)
+        self.lib.call("mg_set_box_lsf", self.h, int(box_id), len(ix) // 3,
+                      ix.ctypes.data_as(capi.P_i32), dd.ctypes.data_as(capi.P_f64),
+                      bv.ctypes.data_as(capi.P_f64), int(i_lsf))
+
     def fas_fmg(self, set_residual=True, have_guess=True):
         """mg_fas_fmg (m_af_multigrid.f90:137-180)."""
         self.lib.call("mg_fas_fmg", self.h, int(set_residual), int(have_guess))

@@ -55,7 +55,7 @@ class StreamerCase:
     """One streamer simulation state on a tree, driven through `lib`."""
 
     def __init__(self, lib, topo, td, chem, voltage, n_gas=None,
-                 coarse_cycles=20, device=-1, shard=None):
+                 coarse_cycles=20, device=-1, shard=None, n_var_cell=N_VAR_CELL):
         """shard: an afh.dist.Shard -- this rank's part of a sharded tree
         (the tree is created from the rank's level lists and the exchange
         hooks are attached); None for a single-rank tree."""
@@ -63,7 +63,7 @@ class StreamerCase:
         self.topo = topo
         self.shard = shard
         local = shard.part.local_topology(shard.rank) if shard else topo
-        self.tree = Tree(lib, local, N_VAR_CELL, N_VAR_FACE, device=device)
+        self.tree = Tree(lib, local, n_var_cell, N_VAR_FACE, device=device)
         t = self.tree
         neumann0 = [(capi.BC_NEUMANN, 0.0)] * 6
         for sp in ("e", "pos", "neg"):
@@ -75,6 +75,7 @@ class StreamerCase:
         for s in (0, 1):
             t.set_cc_methods(IV["phi"] + s, self.phi_bc(voltage), capi.RB_MG_SIDES)
         self.coarse_cycles = coarse_cycles
+        self.i_lsf = 0  # level-set variable of an electrode (set_electrode)
         # keep the face fluxes of the species step in FV["flux"] (the fused
         # device step otherwise leaves them on chip)
         self.store_flux = False
@@ -104,6 +105,17 @@ class StreamerCase:
                 self.tree, IV["phi"], IV["rhs"], IV["tmp"],
                 helmholtz_lambda=lambda2, coarse_cycles=self.coarse_cycles)
         return self._mg_helm[lambda2]
+
+    def set_electrode(self, i_lsf, stencils, lsf_faces):
+        """Electrode operators (m_field.f90:255-346): the stencils afivo's
+        mg_set_operators_tree stored on the boxes the electrode crosses,
+        handed to the field multigrid. stencils: {box id: (v, bc_correction)};
+        lsf_faces: {box id: (ix, dd, bval)}."""
+        self.i_lsf = i_lsf
+        for bid, (v, bcc) in stencils.items():
+            self.mg.set_box_stencil(bid, v, bcc)
+        for bid, (ix, dd, bv) in lsf_faces.items():
+            self.mg.set_box_lsf(bid, ix, dd, bv, i_lsf)
 
     def set_voltage(self, voltage):
         self.voltage = voltage

@@ -122,6 +122,9 @@ struct afh_tree {
 };
 
 namespace afh {
+// per-level id lists -> one device array with offsets (frees L's old array)
+int32_t upload_list(afh_tree *t, LevelList &L,
+                    const std::vector<std::vector<int32_t>> &lists);
 // Kernel timing: bracket one launch of class `kc` (no-op unless enabled).
 void prof_begin(afh_tree *t, int kc);
 void prof_end(afh_tree *t, int kc, double bytes);

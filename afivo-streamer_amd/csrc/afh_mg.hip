@@ -669,6 +669,226 @@ __global__ void k_parent_rhs(const double *__restrict__ phi,
   tmp[o + c] = phi[o + c];
 }
 
+// ------------------------------------------------------------ electrode boxes
+// Boxes the electrode surface crosses carry a variable 7-point stencil
+// (mg_box_lsf_stencil, m_af_multigrid.f90:1762-1834): v(7, nc^3),
+// coefficients fastest as afivo stores them, and bc_correction(nc^3) (f times
+// the electrode potential, mg_set_operators_lvl 1156-1160); vp / bp index
+// them by box id (bp null: no correction). These kernels run on the lists of
+// such boxes only (one thread per cell; the boxes are few), the constant
+// kernels on the rest of each level.
+__device__ __forceinline__ double apply7v(const double *x, size_t c, size_t sj,
+                                          size_t sk, const double *v) {
+  return v[0] * x[c] + v[1] * x[c - 1] + v[2] * x[c + 1] + v[3] * x[c - sj] +
+         v[4] * x[c + sj] + v[5] * x[c - sk] + v[6] * x[c + sk];
+}
+
+// stencil_gsrb_357, variable branch (m_af_stencil.f90:836-841, 958-978):
+// rhs + bc_correction on every cell, the (i+j+k+redblack) even cells
+// divided by c(1), rhs - bc_correction
+__global__ void k_gsrb_v(double *__restrict__ phi, double *__restrict__ rhs,
+                         const int32_t *__restrict__ ids, int nc, size_t bsz,
+                         const double *const *__restrict__ vp,
+                         const double *const *__restrict__ bp, int redblack) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nc * nc * nc) return;
+  const int id = ids[blockIdx.y];
+  int i, j, k;
+  cell3(t, nc, i, j, k);
+  const int ng = nc + 2;
+  const size_t sj = ng, sk = (size_t)ng * ng, c = ix3(ng, i, j, k);
+  double *x = phi + (size_t)(id - 1) * bsz, *r = rhs + (size_t)(id - 1) * bsz;
+  const double *v = vp[id - 1] + 7 * (size_t)t, *b = bp[id - 1];
+  double r1 = r[c];
+  if (b) r1 = r1 + b[t];
+  if (((i + j + k + redblack) & 1) == 0)
+    x[c] = (r1 - v[1] * x[c - 1] - v[2] * x[c + 1] - v[3] * x[c - sj] -
+            v[4] * x[c + sj] - v[5] * x[c - sk] - v[6] * x[c + sk]) /
+           v[0];
+  if (b) r[c] = r1 - b[t];
+}
+
+// residual_box with the variable stencil: tmp = rhs - (L phi - bc_correction)
+template <bool MAX>
+__global__ void k_residual_v(const double *__restrict__ phi,
+                             const double *__restrict__ rhs,
+                             double *__restrict__ tmp,
+                             const int32_t *__restrict__ ids, int nc, size_t bsz,
+                             const double *const *__restrict__ vp,
+                             const double *const *__restrict__ bp,
+                             unsigned long long *red) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  double mx = 0.0;
+  if (t < nc * nc * nc) {
+    const int id = ids[blockIdx.y];
+    int i, j, k;
+    cell3(t, nc, i, j, k);
+    const int ng = nc + 2;
+    const size_t o = (size_t)(id - 1) * bsz, c = ix3(ng, i, j, k);
+    double a = apply7v(phi + o, c, ng, (size_t)ng * ng, vp[id - 1] + 7 * (size_t)t);
+    if (bp[id - 1]) a = a - bp[id - 1][t];
+    const double v = rhs[o + c] - a;
+    tmp[o + c] = v;
+    mx = fmax(mx, fabs(v));
+  }
+  if (MAX) block_max_to_shard(mx, red);
+}
+
+// k_rstr_fas for children with a variable stencil
+__global__ void k_rstr_fas_v(double *__restrict__ phi,
+                             const double *__restrict__ rhs,
+                             double *__restrict__ tmp,
+                             const afh_box_meta *__restrict__ meta,
+                             const int32_t *__restrict__ ids, int nc, size_t bsz,
+                             const double *const *__restrict__ vp,
+                             const double *const *__restrict__ bp) {
+  const int hn = nc >> 1;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= hn * hn * hn) return;
+  const int id = ids[blockIdx.y];
+  const afh_box_meta &m = meta[id - 1];
+  int i, j, k;
+  cell3(t, hn, i, j, k);
+  const int ng = nc + 2;
+  const size_t sj = ng, sk = (size_t)ng * ng;
+  const size_t o = (size_t)(id - 1) * bsz;
+  const double *x = phi + o, *r = rhs + o, *v = vp[id - 1], *b = bp[id - 1];
+  const int fi = 2 * i - 1, fj = 2 * j - 1, fk = 2 * k - 1;
+  double sr = 0.0, sp = 0.0;
+#pragma unroll
+  for (int q = 0; q < 8; q++) {
+    const int ci = fi + (q & 1), cj = fj + ((q >> 1) & 1), ck = fk + (q >> 2);
+    const size_t c = ix3(ng, ci, cj, ck);
+    const size_t cv = ((size_t)(ck - 1) * nc + (cj - 1)) * nc + (ci - 1);
+    double a = apply7v(x, c, sj, sk, v + 7 * cv);
+    if (b) a = a - b[cv];
+    const double res = r[c] - a;
+    if (q == 0) {
+      sr = res;
+      sp = x[c];
+    } else {
+      sr += res;
+      sp += x[c];
+    }
+  }
+  const size_t po = (size_t)(m.parent - 1) * bsz +
+                    ix3(ng, ((m.ix[0] - 1) & 1) * hn + i,
+                        ((m.ix[1] - 1) & 1) * hn + j,
+                        ((m.ix[2] - 1) & 1) * hn + k);
+  tmp[po] = 0.125 * sr;
+  phi[po] = 0.125 * sp;
+}
+
+// k_parent_rhs for parents with a variable stencil
+__global__ void k_parent_rhs_v(const double *__restrict__ phi,
+                               double *__restrict__ rhs, double *__restrict__ tmp,
+                               const int32_t *__restrict__ ids, int nc, size_t bsz,
+                               const double *const *__restrict__ vp,
+                               const double *const *__restrict__ bp) {
+  const int ng = nc + 2;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= ng * ng * ng) return;
+  const int id = ids[blockIdx.y];
+  int i, j, k;
+  cell3g(t, ng, i, j, k);
+  const size_t o = (size_t)(id - 1) * bsz, c = ix3(ng, i, j, k);
+  double rv = rhs[o + c];
+  if (i >= 1 && i <= nc && j >= 1 && j <= nc && k >= 1 && k <= nc) {
+    const size_t cv = ((size_t)(k - 1) * nc + (j - 1)) * nc + (i - 1);
+    rv = apply7v(phi + o, c, ng, (size_t)ng * ng, vp[id - 1] + 7 * cv);
+    if (bp[id - 1]) rv = rv - bp[id - 1][cv];
+  }
+  rhs[o + c] = rv + tmp[o + c];
+  tmp[o + c] = phi[o + c];
+}
+
+// Level-1 electrode solve: copy of phi (compact, one slot per level-1 box),
+// and max |phi - old|, max |phi| over the interiors (slots 0 and 1)
+__global__ void k_copy_compact(const double *__restrict__ phi,
+                               double *__restrict__ old,
+                               const int32_t *__restrict__ ids, size_t bsz) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= bsz) return;
+  old[(size_t)blockIdx.y * bsz + t] = phi[(size_t)(ids[blockIdx.y] - 1) * bsz + t];
+}
+
+__global__ void k_change_max(const double *__restrict__ phi,
+                             const double *__restrict__ old,
+                             const int32_t *__restrict__ ids, int nc, size_t bsz,
+                             unsigned long long *red) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  double d = 0.0, m = 0.0;
+  if (t < nc * nc * nc) {
+    int i, j, k;
+    cell3(t, nc, i, j, k);
+    const size_t c = ix3(nc + 2, i, j, k);
+    const double p = phi[(size_t)(ids[blockIdx.y] - 1) * bsz + c];
+    d = fabs(p - old[(size_t)blockIdx.y * bsz + c]);
+    m = fabs(p);
+  }
+  block_max_to_shard(d, red);
+  __syncthreads();
+  block_max_to_shard(m, red + RED_SHARDS);
+}
+
+// mg_box_lpllsf_gradient (m_af_multigrid.f90:2030-2120) on electrode leaf
+// boxes: the faces next to the boundary from the electrode potential, in the
+// order of the distance list (one thread per box: entries may share a face)
+__global__ void k_lsf_gradient(const double *__restrict__ phi,
+                               const double *__restrict__ lsf,
+                               double *__restrict__ fcv,
+                               const int32_t *__restrict__ ids, int nc, size_t bsz,
+                               size_t fsz, const int *__restrict__ cnt,
+                               const int32_t *const *__restrict__ ixp,
+                               const double *const *__restrict__ ddp,
+                               const double *const *__restrict__ bvp, double ix_,
+                               double iy, double iz) {
+  if (threadIdx.x != 0) return;
+  const int id = ids[blockIdx.x];
+  const int n = cnt[id - 1];
+  const int ng = nc + 2, nf = nc + 1;
+  const size_t d3 = (size_t)nf * nf * nf;
+  const double *p = phi + (size_t)(id - 1) * bsz, *l = lsf + (size_t)(id - 1) * bsz;
+  double *f = fcv + (size_t)(id - 1) * fsz;
+  const int32_t *X = ixp[id - 1];
+  const double *D = ddp[id - 1], *bv = bvp[id - 1];
+  auto fx = [&](int d, int a, int b, int c) {
+    return (size_t)d * d3 + ((size_t)(c - 1) * nf + (b - 1)) * nf + (a - 1);
+  };
+  for (int e = 0; e < n; e++) {
+    const int i = X[3 * e], j = X[3 * e + 1], k = X[3 * e + 2];
+    const double *dd = D + 6 * e;
+    const size_t c = ix3(ng, i, j, k);
+    if (l[c] < 0) continue;
+    const double pc = p[c], bc = bv[((size_t)(k - 1) * nc + (j - 1)) * nc + (i - 1)];
+    if (dd[0] < 1) f[fx(0, i, j, k)] = ix_ * (pc - bc) / dd[0];
+    if (dd[1] < 1) f[fx(0, i + 1, j, k)] = ix_ * (bc - pc) / dd[1];
+    if (dd[2] < 1) f[fx(1, i, j, k)] = iy * (pc - bc) / dd[2];
+    if (dd[3] < 1) f[fx(1, i, j + 1, k)] = iy * (bc - pc) / dd[3];
+    if (dd[4] < 1) f[fx(2, i, j, k)] = iz * (pc - bc) / dd[4];
+    if (dd[5] < 1) f[fx(2, i, j, k + 1)] = iz * (bc - pc) / dd[5];
+  }
+}
+
+// mg_box_field_norm (m_af_multigrid.f90:1995-2025) from the stored faces
+__global__ void k_field_norm(const double *__restrict__ fcv,
+                             double *__restrict__ nrm,
+                             const int32_t *__restrict__ ids, int nc, size_t bsz,
+                             size_t fsz) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nc * nc * nc) return;
+  const int id = ids[blockIdx.y];
+  int i, j, k;
+  cell3(t, nc, i, j, k);
+  const int nf = nc + 1;
+  const size_t d3 = (size_t)nf * nf * nf;
+  const double *f = fcv + (size_t)(id - 1) * fsz;
+  const size_t fb = ((size_t)(k - 1) * nf + (j - 1)) * nf + (i - 1);
+  const double a = f[fb] + f[fb + 1], b = f[d3 + fb] + f[d3 + fb + nf],
+               cc = f[2 * d3 + fb] + f[2 * d3 + fb + (size_t)nf * nf];
+  nrm[(size_t)(id - 1) * bsz + ix3(nc + 2, i, j, k)] = 0.5 * sqrt(a * a + b * b + cc * cc);
+}
+
 __global__ void k_corr_tmp(const double *__restrict__ phi,
                            double *__restrict__ tmp,
                            const int32_t *__restrict__ ids, size_t bsz) {
@@ -1344,6 +1564,20 @@ struct afh_mg {
   double *w1 = nullptr, *w2 = nullptr;
   int q_bc[6] = {0, 0, 0, 0, 0, 0};
   double *alt = nullptr;  // spare image of phi (all boxes) for the ping-pong
+  // electrode boxes (afh_mg_set_box_stencil / afh_mg_set_box_lsf): device
+  // arrays per box id (null: none), their device pointer tables, and the
+  // level lists split into constant- and variable-stencil boxes
+  std::vector<double *> h_vp, h_bp, h_dd, h_bv;
+  std::vector<int32_t *> h_ix;
+  std::vector<int> h_lsf_n;
+  double **d_vp = nullptr, **d_bp = nullptr, **d_dd = nullptr, **d_bv = nullptr;
+  int32_t **d_ix = nullptr;
+  int *d_lsf_n = nullptr;
+  int i_lsf = 0;
+  bool var_dirty = false, any_var = false, any_lsf = false;
+  std::vector<char> lvl_var;  // level has variable-stencil boxes
+  LevelList ids_c, ids_v, leaves_c, leaves_v, parents_c, parents_v, lsf_leaves;
+  double *cs_old = nullptr;   // level-1 electrode solve: previous phi
 };
 
 // (diag, 1/diag) of the folded operator per MG level and boundary class, in
@@ -1442,6 +1676,9 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
   afh_mg *mg = new afh_mg();
   mg->t = t;
   mg->d = *d;
+  mg->h_vp.assign(t->nb, nullptr), mg->h_bp.assign(t->nb, nullptr);
+  mg->h_dd.assign(t->nb, nullptr), mg->h_bv.assign(t->nb, nullptr);
+  mg->h_ix.assign(t->nb, nullptr), mg->h_lsf_n.assign(t->nb, 0);
   // mg_box_lpl_stencil: c(2:7) = 1/dr^2, c(1) = -sum(c(2:)) - lambda
   mg->lvl_c.resize(t->nlvl);
   for (int l = 1; l <= t->nlvl; l++) {
@@ -1564,6 +1801,14 @@ int32_t afh_mg_destroy(afh_mg *mg) {
     if (mg->t->alt == mg->alt) mg->t->alt = nullptr;
     hipFree(mg->alt);
   }
+  for (auto *v : {&mg->h_vp, &mg->h_bp, &mg->h_dd, &mg->h_bv})
+    for (double *q : *v) hipFree(q);
+  for (int32_t *q : mg->h_ix) hipFree(q);
+  hipFree(mg->d_vp), hipFree(mg->d_bp), hipFree(mg->d_dd), hipFree(mg->d_bv);
+  hipFree(mg->d_ix), hipFree(mg->d_lsf_n), hipFree(mg->cs_old);
+  for (LevelList *L : {&mg->ids_c, &mg->ids_v, &mg->leaves_c, &mg->leaves_v,
+                       &mg->parents_c, &mg->parents_v, &mg->lsf_leaves})
+    hipFree(L->d);
   delete mg;
   return AFH_OK;
 }
@@ -1626,22 +1871,81 @@ extern "C" {
 // gsrb_boxes smooths level lvl with the fused pair kernel (same answer on
 // every rank of a sharded tree: decided on the level's total box count)
 static bool fused_level(const afh_mg *mg, int lvl) {
+  if (mg->any_var && mg->lvl_var[lvl - 1]) return false;  // electrode stencils
   return mg->alt && mg->t->lvl_total[lvl - 1] >= mg->fused_min;
+}
+
+// Device tables and split level lists after afh_mg_set_box_stencil /
+// afh_mg_set_box_lsf changed them
+static int32_t prepare_var(afh_mg *mg) {
+  if (!mg->var_dirty) return AFH_OK;
+  mg->var_dirty = false;
+  afh_tree *t = mg->t;
+  const int nb = t->nb, nl = t->nlvl;
+  auto table = [&](auto **d, const auto &h) -> int32_t {
+    if (!*d) AFH_HIP(hipMalloc(d, sizeof(h[0]) * nb));
+    AFH_HIP(hipMemcpy(*d, h.data(), sizeof(h[0]) * nb, hipMemcpyHostToDevice));
+    return AFH_OK;
+  };
+  int32_t e;
+  if ((e = table(&mg->d_vp, mg->h_vp)) || (e = table(&mg->d_bp, mg->h_bp)) ||
+      (e = table(&mg->d_dd, mg->h_dd)) || (e = table(&mg->d_bv, mg->h_bv)) ||
+      (e = table(&mg->d_ix, mg->h_ix)) || (e = table(&mg->d_lsf_n, mg->h_lsf_n)))
+    return e;
+  mg->any_var = mg->any_lsf = false;
+  mg->lvl_var.assign(nl, 0);
+  for (int q = 0; q < nb; q++) {
+    if (mg->h_vp[q]) mg->any_var = true, mg->lvl_var[t->boxes[q].lvl - 1] = 1;
+    if (mg->h_lsf_n[q]) mg->any_lsf = true;
+  }
+  auto split = [&](const std::vector<std::vector<int32_t>> &src, LevelList &c,
+                   LevelList &v) -> int32_t {
+    std::vector<std::vector<int32_t>> lc(nl), lv(nl);
+    for (int l = 0; l < nl; l++)
+      for (int32_t id : src[l]) (mg->h_vp[id - 1] ? lv : lc)[l].push_back(id);
+    int32_t e2;
+    if ((e2 = upload_list(t, c, lc)) || (e2 = upload_list(t, v, lv))) return e2;
+    return AFH_OK;
+  };
+  if ((e = split(t->h_ids, mg->ids_c, mg->ids_v)) ||
+      (e = split(t->h_leaves, mg->leaves_c, mg->leaves_v)) ||
+      (e = split(t->h_parents, mg->parents_c, mg->parents_v)))
+    return e;
+  std::vector<std::vector<int32_t>> ll(nl);
+  for (int l = 0; l < nl; l++)
+    for (int32_t id : t->h_leaves[l])
+      if (mg->h_lsf_n[id - 1]) ll[l].push_back(id);
+  return upload_list(t, mg->lsf_leaves, ll);
+}
+
+// the constant-stencil part of a level list (the whole list without
+// electrode boxes)
+static const LevelList &cst(const afh_mg *mg, const LevelList &all,
+                            const LevelList &c) {
+  return mg->any_var ? c : all;
 }
 
 static int32_t gsrb_half(afh_mg *mg, int lvl, int n, bool corners) {
   afh_tree *t = mg->t;
-  const int nid = t->ids.n(lvl), nc = t->nc;
+  const LevelList &L = cst(mg, t->ids, mg->ids_c);
+  const int nid = L.n(lvl), nc = t->nc;
   const Coef cf = mg->lvl_c[lvl - 1];
   const int cells = nc * nc * nc / 2;
   if (nid) {
     prof_begin(t, AFH_PROF_GSRB);
     hipLaunchKernelGGL(k_gsrb, dim3((cells + 255) / 256, nid), dim3(256), 0,
                        t->stream, t->ccv(mg->d.i_phi), t->ccv(mg->d.i_rhs),
-                       t->ids.at(lvl), nc, t->bsz, cf, 1 / cf.c[0], n);
+                       L.at(lvl), nc, t->bsz, cf, 1 / cf.c[0], n);
     // read phi (all), rhs (half), write phi (half) = 16 B/cell
     prof_end(t, AFH_PROF_GSRB, 16.0 * nc * nc * nc * nid);
     AFH_LAUNCH_CHECK("k_gsrb");
+  }
+  const int nv = mg->any_var ? mg->ids_v.n(lvl) : 0;
+  if (nv) {
+    hipLaunchKernelGGL(k_gsrb_v, dim3((nc * nc * nc + 255) / 256, nv), dim3(256),
+                       0, t->stream, t->ccv(mg->d.i_phi), t->ccv(mg->d.i_rhs),
+                       mg->ids_v.at(lvl), nc, t->bsz, mg->d_vp, mg->d_bp, n);
+    AFH_LAUNCH_CHECK("k_gsrb_v");
   }
   return gc_lvl(t, lvl, mg->d.i_phi, corners, fused_level(mg, lvl));
 }
@@ -1701,26 +2005,44 @@ static int32_t gsrb_boxes(afh_mg *mg, int lvl, bool up) {
 static int32_t update_coarse(afh_mg *mg, int lvl) {
   afh_tree *t = mg->t;
   const int nc = t->nc, hn = nc / 2;
-  const int nid = t->ids.n(lvl);
+  const LevelList &L = cst(mg, t->ids, mg->ids_c);
+  const int nid = L.n(lvl);
   if (nid) {
     hipLaunchKernelGGL(k_rstr_fas, dim3((hn * hn * hn + 255) / 256, nid),
                        dim3(256), 0, t->stream, t->ccv(mg->d.i_phi),
                        t->ccv(mg->d.i_rhs), t->ccv(mg->d.i_tmp), t->d_boxes,
-                       t->ids.at(lvl), nc, t->bsz, mg->lvl_c[lvl - 1]);
+                       L.at(lvl), nc, t->bsz, mg->lvl_c[lvl - 1]);
     AFH_LAUNCH_CHECK("k_rstr_fas");
+  }
+  const int nv = mg->any_var ? mg->ids_v.n(lvl) : 0;
+  if (nv) {
+    hipLaunchKernelGGL(k_rstr_fas_v, dim3((hn * hn * hn + 255) / 256, nv),
+                       dim3(256), 0, t->stream, t->ccv(mg->d.i_phi),
+                       t->ccv(mg->d.i_rhs), t->ccv(mg->d.i_tmp), t->d_boxes,
+                       mg->ids_v.at(lvl), nc, t->bsz, mg->d_vp, mg->d_bp);
+    AFH_LAUNCH_CHECK("k_rstr_fas_v");
   }
   int32_t e;
   if ((e = call_hook(t, AFH_HOOK_RESTRICT, lvl, mg->d.i_phi)) ||
       (e = call_hook(t, AFH_HOOK_RESTRICT, lvl, mg->d.i_tmp)))
     return e;
   if ((e = gc_lvl(t, lvl - 1, mg->d.i_phi, 1, fused_level(mg, lvl - 1)))) return e;
-  const int np = t->parents.n(lvl - 1);
+  const LevelList &P = cst(mg, t->parents, mg->parents_c);
+  const int np = P.n(lvl - 1);
   if (np) {
     hipLaunchKernelGGL(k_parent_rhs, dim3((unsigned)((t->bsz + 255) / 256), np),
                        dim3(256), 0, t->stream, t->ccv(mg->d.i_phi),
                        t->ccv(mg->d.i_rhs), t->ccv(mg->d.i_tmp),
-                       t->parents.at(lvl - 1), nc, t->bsz, mg->lvl_c[lvl - 2]);
+                       P.at(lvl - 1), nc, t->bsz, mg->lvl_c[lvl - 2]);
     AFH_LAUNCH_CHECK("k_parent_rhs");
+  }
+  const int npv = mg->any_var ? mg->parents_v.n(lvl - 1) : 0;
+  if (npv) {
+    hipLaunchKernelGGL(k_parent_rhs_v, dim3((unsigned)((t->bsz + 255) / 256), npv),
+                       dim3(256), 0, t->stream, t->ccv(mg->d.i_phi),
+                       t->ccv(mg->d.i_rhs), t->ccv(mg->d.i_tmp),
+                       mg->parents_v.at(lvl - 1), nc, t->bsz, mg->d_vp, mg->d_bp);
+    AFH_LAUNCH_CHECK("k_parent_rhs_v");
   }
   return AFH_OK;
 }
@@ -1751,8 +2073,50 @@ static int32_t correct_children(afh_mg *mg, int lvl) {
   return AFH_OK;
 }
 
+// Level-1 solve with electrode stencils (the C oracle's solve_coarse_gs,
+// OUR algorithm; the reference hands the LSF stencils to HYPRE,
+// m_coarse_solver.f90:286-338): red-black Gauss-Seidel pairs with each box's
+// own stencil and a level ghost fill after each half-sweep until phi is
+// stationary (max change <= 4 spacing(max |phi|), after at least 11 pairs),
+// then the level's ghost cells with corners. One host check per pair: meant
+// for the small coarse grids electrode runs use.
+static int32_t solve_coarse_gs(afh_mg *mg) {
+  afh_tree *t = mg->t;
+  const int nid = t->ids.n(1), nc = t->nc, n3 = nc * nc * nc;
+  if (!mg->cs_old) AFH_HIP(hipMalloc(&mg->cs_old, sizeof(double) * t->bsz * nid));
+  auto *red = reinterpret_cast<unsigned long long *>(t->scratch);
+  double *phi = t->ccv(mg->d.i_phi);
+  int32_t e;
+  for (int it = 1; it <= 200000; it++) {
+    hipLaunchKernelGGL(k_copy_compact, dim3((unsigned)((t->bsz + 255) / 256), nid),
+                       dim3(256), 0, t->stream, phi, mg->cs_old, t->ids.at(1), t->bsz);
+    AFH_LAUNCH_CHECK("k_copy_compact");
+    for (int n = 1; n <= 2; n++)
+      if ((e = gsrb_half(mg, 1, n, false))) return e;
+    if ((e = red_init(t, 0, 0.0)) || (e = red_init(t, 1, 0.0))) return e;
+    hipLaunchKernelGGL(k_change_max, dim3((n3 + 255) / 256, nid), dim3(256), 0,
+                       t->stream, phi, mg->cs_old, t->ids.at(1), nc, t->bsz, red);
+    AFH_LAUNCH_CHECK("k_change_max");
+    double r[2];
+    if ((e = red_finish(t, 0, true)) || (e = red_finish(t, 1, true)) ||
+        (e = red_fetch(t, 0, 2, r)) ||
+        (e = call_hook(t, AFH_HOOK_MAX, 1, mg->d.i_phi, &r[0], 1)) ||
+        (e = call_hook(t, AFH_HOOK_MAX, 1, mg->d.i_phi, &r[1], 1)))
+      return e;
+    double sp = 2.2250738585072014e-308;  // Fortran spacing(max |phi|)
+    if (r[1] > 0) {
+      int ex;
+      frexp(r[1], &ex);
+      sp = ldexp(1.0, ex - 53);
+    }
+    if (r[0] <= 4 * sp && it > 10) break;
+  }
+  return gc_lvl(t, 1, mg->d.i_phi, 1);
+}
+
 static int32_t solve_coarse(afh_mg *mg) {
   afh_tree *t = mg->t;
+  if (mg->any_var && mg->lvl_var[0]) return solve_coarse_gs(mg);
   CsParams &P = mg->P;
   const afh_bc *bc = t->meth[mg->d.i_phi].bc;
   for (int q = 0; q < 6; q++) P.bctype[q] = bc[q].type;
@@ -1842,6 +2206,7 @@ int32_t afh_mg_fas_fmg(afh_mg *mg, int32_t set_residual, int32_t have_guess) {
   const int nl = t->nlvl, i_phi = mg->d.i_phi;
   double *phi = t->ccv(i_phi), *tmp = t->ccv(mg->d.i_tmp);
   int32_t e;
+  if ((e = prepare_var(mg))) return e;
   if (have_guess) {
     for (int lvl = nl; lvl >= 2; lvl--) {
       if (lvl == nl && (e = gc_lvl(t, lvl, i_phi, 1, fused_level(mg, lvl)))) return e;
@@ -1882,19 +2247,32 @@ static int32_t residual_levels(afh_mg *mg, int max_lvl, double *max_out) {
     for (int part = 0; part < 2; part++) {
       // part 0: leaves (max folded), part 1: parents; without max_out the
       // level's whole id list in one launch
-      const LevelList &L = max_out ? (part ? t->parents : t->leaves) : t->ids;
       if (!max_out && part) break;
+      const LevelList &A = max_out ? (part ? t->parents : t->leaves) : t->ids;
+      const LevelList &Lc = max_out ? (part ? mg->parents_c : mg->leaves_c) : mg->ids_c;
+      const LevelList &Lv = max_out ? (part ? mg->parents_v : mg->leaves_v) : mg->ids_v;
+      const LevelList &L = cst(mg, A, Lc);
       const int n = L.n(lvl);
-      if (!n) continue;
-      const bool k4 = nc % 4 == 0;
-      const dim3 grid((n3 / (k4 ? 4 : 2) + 255) / 256, n);
       const bool mx = max_out && !part;
-      auto kern = mx ? (k4 ? k_residual<true, 4> : k_residual<true, 2>)
-                     : (k4 ? k_residual<false, 4> : k_residual<false, 2>);
-      hipLaunchKernelGGL(kern, grid, dim3(256), 0, t->stream,
-                         t->ccv(mg->d.i_phi), t->ccv(mg->d.i_rhs),
-                         t->ccv(mg->d.i_tmp), L.at(lvl), nc, t->bsz, cf, red);
-      AFH_LAUNCH_CHECK("k_residual");
+      if (n) {
+        const bool k4 = nc % 4 == 0;
+        const dim3 grid((n3 / (k4 ? 4 : 2) + 255) / 256, n);
+        auto kern = mx ? (k4 ? k_residual<true, 4> : k_residual<true, 2>)
+                       : (k4 ? k_residual<false, 4> : k_residual<false, 2>);
+        hipLaunchKernelGGL(kern, grid, dim3(256), 0, t->stream,
+                           t->ccv(mg->d.i_phi), t->ccv(mg->d.i_rhs),
+                           t->ccv(mg->d.i_tmp), L.at(lvl), nc, t->bsz, cf, red);
+        AFH_LAUNCH_CHECK("k_residual");
+      }
+      const int nv = mg->any_var ? Lv.n(lvl) : 0;
+      if (nv) {
+        hipLaunchKernelGGL(mx ? k_residual_v<true> : k_residual_v<false>,
+                           dim3((n3 + 255) / 256, nv), dim3(256), 0, t->stream,
+                           t->ccv(mg->d.i_phi), t->ccv(mg->d.i_rhs),
+                           t->ccv(mg->d.i_tmp), Lv.at(lvl), nc, t->bsz, mg->d_vp,
+                           mg->d_bp, red);
+        AFH_LAUNCH_CHECK("k_residual_v");
+      }
     }
   }
   if (!max_out) return AFH_OK;
@@ -1908,6 +2286,7 @@ static int32_t vcycle_impl(afh_mg *mg, int32_t set_residual, int32_t hl,
   afh_tree *t = mg->t;
   const int max_lvl = (hl > 0 && hl <= t->nlvl) ? hl : t->nlvl;
   int32_t e;
+  if ((e = prepare_var(mg))) return e;
   for (int lvl = max_lvl; lvl >= 2; lvl--) {
     if ((e = gsrb_boxes(mg, lvl, false))) return e;
     if ((e = update_coarse(mg, lvl))) return e;
@@ -1955,6 +2334,79 @@ int32_t afh_mg_compute_phi_gradient(afh_mg *mg, int32_t i_fc, double fac,
                      t->ids.d, nc, t->bsz, t->fsz, fac);
   }
   AFH_LAUNCH_CHECK("k_gradient");
+  int32_t e;
+  if ((e = prepare_var(mg))) return e;
+  if (!mg->any_lsf) return AFH_OK;
+  // electrode leaf boxes: mg_box_lpllsf_gradient, then their |E| again
+  for (int l = 1; l <= t->nlvl; l++) {
+    const int n = mg->lsf_leaves.n(l);
+    if (!n) continue;
+    const double *dr = &t->lvl_dr[3 * (l - 1)];
+    hipLaunchKernelGGL(k_lsf_gradient, dim3(n), dim3(64), 0, t->stream,
+                       t->ccv(mg->d.i_phi), t->ccv(mg->i_lsf), t->fcv(i_fc),
+                       mg->lsf_leaves.at(l), nc, t->bsz, t->fsz, mg->d_lsf_n,
+                       mg->d_ix, mg->d_dd, mg->d_bv, fac / dr[0], fac / dr[1],
+                       fac / dr[2]);
+    AFH_LAUNCH_CHECK("k_lsf_gradient");
+    if (nrm) {
+      hipLaunchKernelGGL(k_field_norm, dim3((n3 + 255) / 256, n), dim3(256), 0,
+                         t->stream, t->fcv(i_fc), nrm, mg->lsf_leaves.at(l), nc,
+                         t->bsz, t->fsz);
+      AFH_LAUNCH_CHECK("k_field_norm");
+    }
+  }
+  return AFH_OK;
+}
+
+int32_t afh_mg_set_box_stencil(afh_mg *mg, int32_t id, const double *v,
+                               const double *bc_correction) {
+  if (!mg || id < 1 || id > mg->t->nb) return set_error(AFH_ERR_ARG, "bad box id");
+  afh_tree *t = mg->t;
+  const size_t n3 = (size_t)t->nc * t->nc * t->nc;
+  AFH_HIP(hipStreamSynchronize(t->stream));
+  hipFree(mg->h_vp[id - 1]), hipFree(mg->h_bp[id - 1]);
+  mg->h_vp[id - 1] = mg->h_bp[id - 1] = nullptr;
+  mg->var_dirty = true;
+  if (!v) return AFH_OK;
+  AFH_HIP(hipMalloc(&mg->h_vp[id - 1], sizeof(double) * 7 * n3));
+  AFH_HIP(hipMemcpy(mg->h_vp[id - 1], v, sizeof(double) * 7 * n3,
+                    hipMemcpyHostToDevice));
+  if (bc_correction) {
+    AFH_HIP(hipMalloc(&mg->h_bp[id - 1], sizeof(double) * n3));
+    AFH_HIP(hipMemcpy(mg->h_bp[id - 1], bc_correction, sizeof(double) * n3,
+                      hipMemcpyHostToDevice));
+  }
+  return AFH_OK;
+}
+
+int32_t afh_mg_set_box_lsf(afh_mg *mg, int32_t id, int32_t n, const int32_t *ix,
+                           const double *dd, const double *bval, int32_t i_lsf) {
+  if (!mg || id < 1 || id > mg->t->nb || n < 0)
+    return set_error(AFH_ERR_ARG, "bad box id / count");
+  afh_tree *t = mg->t;
+  const size_t n3 = (size_t)t->nc * t->nc * t->nc;
+  AFH_HIP(hipStreamSynchronize(t->stream));
+  hipFree(mg->h_ix[id - 1]), hipFree(mg->h_dd[id - 1]), hipFree(mg->h_bv[id - 1]);
+  mg->h_ix[id - 1] = nullptr, mg->h_dd[id - 1] = mg->h_bv[id - 1] = nullptr;
+  mg->h_lsf_n[id - 1] = 0;
+  mg->var_dirty = true;
+  if (n == 0) return AFH_OK;
+  if (!ix || !dd || !bval || i_lsf < 1 || i_lsf > t->nvc)
+    return set_error(AFH_ERR_ARG, "afh_mg_set_box_lsf: bad argument");
+  for (int q = 0; q < 3 * n; q++)
+    if (ix[q] < 1 || ix[q] > t->nc)
+      return set_error(AFH_ERR_ARG, "cell index out of box");
+  AFH_HIP(hipMalloc(&mg->h_ix[id - 1], sizeof(int32_t) * 3 * n));
+  AFH_HIP(hipMemcpy(mg->h_ix[id - 1], ix, sizeof(int32_t) * 3 * n,
+                    hipMemcpyHostToDevice));
+  AFH_HIP(hipMalloc(&mg->h_dd[id - 1], sizeof(double) * 6 * n));
+  AFH_HIP(hipMemcpy(mg->h_dd[id - 1], dd, sizeof(double) * 6 * n,
+                    hipMemcpyHostToDevice));
+  AFH_HIP(hipMalloc(&mg->h_bv[id - 1], sizeof(double) * n3));
+  AFH_HIP(hipMemcpy(mg->h_bv[id - 1], bval, sizeof(double) * n3,
+                    hipMemcpyHostToDevice));
+  mg->h_lsf_n[id - 1] = n;
+  mg->i_lsf = i_lsf;
   return AFH_OK;
 }
 

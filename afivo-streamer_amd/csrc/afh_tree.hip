@@ -355,16 +355,9 @@ __global__ void k_maxabs(const double *__restrict__ v,
   }
 }
 
-}  // namespace afh
-
-using namespace afh;
-
-extern "C" {
-
-const char *afh_last_error(void) { return afh::g_err; }
-
-static int32_t upload_list(afh_tree *t, LevelList &L,
-                           const std::vector<std::vector<int32_t>> &lists) {
+int32_t upload_list(afh_tree *t, LevelList &L,
+                    const std::vector<std::vector<int32_t>> &lists) {
+  if (L.d) hipFree(L.d), L.d = nullptr;
   L.off.assign(lists.size() + 1, 0);
   std::vector<int32_t> flat;
   for (size_t l = 0; l < lists.size(); l++) {
@@ -377,6 +370,15 @@ static int32_t upload_list(afh_tree *t, LevelList &L,
                       hipMemcpyHostToDevice));
   return AFH_OK;
 }
+
+}  // namespace afh
+
+using namespace afh;
+
+extern "C" {
+
+const char *afh_last_error(void) { return afh::g_err; }
+
 
 int32_t afh_tree_create(const afh_tree_desc *d, int32_t device,
                         afh_tree **out) {

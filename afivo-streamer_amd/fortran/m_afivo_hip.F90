@@ -299,6 +299,27 @@ module m_afivo_hip
        integer(c_int32_t)        :: afh_mg_compute_phi_gradient
      end function afh_mg_compute_phi_gradient
 
+     ! electrode (level-set) boxes: stencils stored by mg_set_operators_tree
+     function afh_mg_set_box_stencil(mg, id, v, bc_correction) &
+          bind(C, name=afh_pfx//"mg_set_box_stencil")
+       import
+       type(c_ptr), value        :: mg
+       integer(c_int32_t), value :: id
+       type(c_ptr), value        :: v, bc_correction   ! c_loc(...) or c_null_ptr
+       integer(c_int32_t)        :: afh_mg_set_box_stencil
+     end function afh_mg_set_box_stencil
+
+     function afh_mg_set_box_lsf(mg, id, n, ix, dd, bval, i_lsf) &
+          bind(C, name=afh_pfx//"mg_set_box_lsf")
+       import
+       type(c_ptr), value             :: mg
+       integer(c_int32_t), value      :: id, n
+       integer(c_int32_t), intent(in) :: ix(*)
+       real(c_double), intent(in)     :: dd(*), bval(*)
+       integer(c_int32_t), value      :: i_lsf
+       integer(c_int32_t)             :: afh_mg_set_box_lsf
+     end function afh_mg_set_box_lsf
+
      function afh_fluid_create(t, desc, out) bind(C, name=afh_pfx//"fluid_create")
        import
        type(c_ptr), value               :: t

@@ -25,8 +25,58 @@ module m_afivo_hip_tree
   public :: afh_put_cc_tree, afh_get_cc_tree
   public :: afh_put_fc_tree, afh_get_fc_tree
   public :: afh_bc_from_type
+  public :: afh_mg_stencils_from_af
 
 contains
+
+  !> Hand the electrode stencils mg_set_operators_tree stored on the boxes
+  !> (m_af_multigrid.f90:1133-1171) to the device multigrid `mg_h`: per box
+  !> the variable operator stencil of mg%operator_key with its bc_correction,
+  !> and the boundary distances (mg_lsf_distance_key) with
+  !> mg_lsf_boundary_value for the gradient. Call after every operator
+  !> (re)build (mg_init / mg_use / regrid) and when the electrode voltage
+  !> changes.
+  subroutine afh_mg_stencils_from_af(mg_h, tree, mg)
+    use m_af_stencil, only: af_stencil_index, stencil_variable
+    use m_coarse_solver, only: mg_lsf_boundary_value
+    type(c_ptr), intent(in)   :: mg_h
+    type(af_t), intent(in), target :: tree
+    type(mg_t), intent(in)    :: mg
+    integer                   :: id, ix, n
+    real(c_double), allocatable, target :: bval(:, :, :)
+    type(c_ptr)               :: vp, bp
+    do id = 1, tree%highest_id
+       if (.not. tree%boxes(id)%in_use) cycle
+       associate (box => tree%boxes(id))
+         vp = c_null_ptr
+         bp = c_null_ptr
+         ix = af_stencil_index(box, mg%operator_key)
+         if (ix > af_stencil_none) then
+            if (box%stencils(ix)%stype == stencil_variable) then
+               vp = c_loc(tree%boxes(id)%stencils(ix)%v)
+               if (allocated(box%stencils(ix)%bc_correction)) &
+                    bp = c_loc(tree%boxes(id)%stencils(ix)%bc_correction)
+            end if
+         end if
+         call afh_check(afh_mg_set_box_stencil(mg_h, int(id, c_int32_t), vp, bp), &
+              "mg_set_box_stencil")
+         n = 0
+         ix = af_stencil_index(box, mg_lsf_distance_key)
+         if (ix > af_stencil_none) n = size(box%stencils(ix)%sparse_ix, 2)
+         if (n > 0) then
+            bval = mg_lsf_boundary_value(box, mg)
+            call afh_check(afh_mg_set_box_lsf(mg_h, int(id, c_int32_t), &
+                 int(n, c_int32_t), int(box%stencils(ix)%sparse_ix, c_int32_t), &
+                 box%stencils(ix)%sparse_v, bval, int(mg%i_lsf, c_int32_t)), &
+                 "mg_set_box_lsf")
+         else
+            call afh_check(afh_mg_set_box_lsf(mg_h, int(id, c_int32_t), 0_c_int32_t, &
+                 [0_c_int32_t], [0.0_c_double], [0.0_c_double], 0_c_int32_t), &
+                 "mg_set_box_lsf")
+         end if
+       end associate
+    end do
+  end subroutine afh_mg_stencils_from_af
 
   !> Pack tree%boxes(1:highest_id) and tree%lvls(1:highest_lvl) into st%desc.
   subroutine afh_tree_from_af(tree, st)

@@ -242,6 +242,26 @@ int32_t afh_mg_fas_fmg(afh_mg *mg, int32_t set_residual, int32_t have_guess);
 int32_t afh_mg_compute_phi_gradient(afh_mg *mg, int32_t i_fc, double fac,
                                     int32_t i_norm);
 
+/* Electrode (level-set) boxes: the stencils mg_set_operators_tree stores on
+ * the boxes an electrode surface crosses (mg_set_operators_lvl,
+ * m_af_multigrid.f90:1133-1171), handed over per box after every operator
+ * (re)build. afh_mg_set_box_stencil: v = box%stencils(ix)%v(7, nc, nc, nc)
+ * of the operator key (mg_box_lsf_stencil, 1762-1834), bc_correction =
+ * box%stencils(ix)%bc_correction (nc^3, or NULL); v = NULL removes the
+ * box's stencil. Smoothing, residuals and the FAS restriction of such boxes
+ * use it (stencil_gsrb_357 / stencil_apply_357 variable branch,
+ * m_af_stencil.f90:459-475, 836-841, 958-978); a level-1 grid with electrode
+ * boxes is solved by Gauss-Seidel to stationarity (HYPRE gets the same
+ * stencils in the reference). afh_mg_set_box_lsf: the boundary distances
+ * (mg_lsf_distance_key: n cells, ix(3, n) 1-based, dd(6, n)) and
+ * mg_lsf_boundary_value(box) (nc^3) for mg_box_lpllsf_gradient
+ * (2030-2120) on leaf boxes; i_lsf = the level-set cc variable; n = 0
+ * removes. */
+int32_t afh_mg_set_box_stencil(afh_mg *mg, int32_t id, const double *v,
+                               const double *bc_correction);
+int32_t afh_mg_set_box_lsf(afh_mg *mg, int32_t id, int32_t n, const int32_t *ix,
+                           const double *dd, const double *bval, int32_t i_lsf);
+
 /* Fluid model bound to a tree (the m_fluid / m_chemistry module state). */
 int32_t afh_fluid_create(afh_tree *t, const afh_fluid_desc *desc,
                          afh_fluid **out);

@@ -72,6 +72,16 @@ struct afh_mg {
    * operator, two work grids, and the BC types the tables were built for */
   double *q[3], *e[3], *w1, *w2;
   int q_bc[6];
+  /* electrode (level-set) boxes, per box id - 1 (NULL / 0 = none): the
+   * variable operator stencil v(7, nc^3) and its bc_correction
+   * (mg_box_lsf_stencil + mg_set_operators_lvl), and the boundary distances
+   * of mg_box_lpllsf_gradient (n cells: ix(3, n), dd(6, n), boundary value
+   * per cell) */
+  double **vst, **vbc;
+  int *lsf_n;
+  int32_t **lsf_ix;
+  double **lsf_dd, **lsf_bv;
+  int i_lsf;
 };
 
 #define AFH_CS_BOTTOM_SWEEPS 16
@@ -590,6 +600,66 @@ static void gsrb_357(afh_tree *t, int id, const double *cf, int redblack,
     }
 }
 
+/* Cell (i, j, k) of a variable stencil v(7, nc, nc, nc) / bc_correction(nc^3) */
+static inline size_t vix(int nc, int i, int j, int k) {
+  return ((size_t)(k - 1) * nc + (size_t)(j - 1)) * nc + (size_t)(i - 1);
+}
+
+/* stencil_apply_357 with a variable stencil, then - bc_correction
+ * (m_af_stencil.f90:459-475) */
+static void apply_357_var(afh_tree *t, int id, const double *v, const double *bcc,
+                          int iv, int i_out) {
+  double *x = ccb(t, iv, id), *o = ccb(t, i_out, id);
+  int nc = t->nc;
+  for (int k = 1; k <= nc; k++)
+    for (int j = 1; j <= nc; j++)
+      for (int i = 1; i <= nc; i++) {
+        const double *c = v + 7 * vix(nc, i, j, k);
+        o[IX(t, i, j, k)] =
+            c[0] * x[IX(t, i, j, k)] + c[1] * x[IX(t, i - 1, j, k)] +
+            c[2] * x[IX(t, i + 1, j, k)] + c[3] * x[IX(t, i, j - 1, k)] +
+            c[4] * x[IX(t, i, j + 1, k)] + c[5] * x[IX(t, i, j, k - 1)] +
+            c[6] * x[IX(t, i, j, k + 1)];
+      }
+  if (bcc)
+    for (int k = 1; k <= nc; k++)
+      for (int j = 1; j <= nc; j++)
+        for (int i = 1; i <= nc; i++)
+          o[IX(t, i, j, k)] = o[IX(t, i, j, k)] - bcc[vix(nc, i, j, k)];
+}
+
+/* stencil_gsrb_357 with a variable stencil (m_af_stencil.f90:836-841,
+ * 958-978): rhs + bc_correction, the red or black cells divided by c(1),
+ * then rhs - bc_correction */
+static void gsrb_357_var(afh_tree *t, int id, const double *v, const double *bcc,
+                         int redblack, int iv, int i_rhs) {
+  double *x = ccb(t, iv, id), *r = ccb(t, i_rhs, id);
+  int nc = t->nc;
+  if (bcc)
+    for (int k = 1; k <= nc; k++)
+      for (int j = 1; j <= nc; j++)
+        for (int i = 1; i <= nc; i++)
+          r[IX(t, i, j, k)] = r[IX(t, i, j, k)] + bcc[vix(nc, i, j, k)];
+  for (int k = 1; k <= nc; k++)
+    for (int j = 1; j <= nc; j++) {
+      int i0 = 2 - ((redblack ^ (k + j)) & 1);
+      for (int i = i0; i <= nc; i += 2) {
+        const double *c = v + 7 * vix(nc, i, j, k);
+        x[IX(t, i, j, k)] =
+            (r[IX(t, i, j, k)] - c[1] * x[IX(t, i - 1, j, k)] -
+             c[2] * x[IX(t, i + 1, j, k)] - c[3] * x[IX(t, i, j - 1, k)] -
+             c[4] * x[IX(t, i, j + 1, k)] - c[5] * x[IX(t, i, j, k - 1)] -
+             c[6] * x[IX(t, i, j, k + 1)]) /
+            c[0];
+      }
+    }
+  if (bcc)
+    for (int k = 1; k <= nc; k++)
+      for (int j = 1; j <= nc; j++)
+        for (int i = 1; i <= nc; i++)
+          r[IX(t, i, j, k)] = r[IX(t, i, j, k)] - bcc[vix(nc, i, j, k)];
+}
+
 /* stencil_prolong_248 with add = .true., m_af_stencil.f90:749-771 */
 static void prolong_248_add(afh_tree *t, int p_id, int c_id, int iv,
                             int iv_to) {
@@ -617,11 +687,32 @@ static void prolong_248_add(afh_tree *t, int p_id, int c_id, int iv,
 
 static double *lvl_coeffs(afh_mg *mg, int lvl) { return mg->lvl_c + 7 * (lvl - 1); }
 
+/* mg_auto_op (af_stencil_apply_box with the operator key): the box's
+ * electrode stencil if it has one, else the level's constant stencil */
+static void apply_box(afh_mg *mg, int id, int iv, int i_out) {
+  afh_tree *t = mg->t;
+  if (mg->vst[id - 1])
+    apply_357_var(t, id, mg->vst[id - 1], mg->vbc[id - 1], iv, i_out);
+  else
+    apply_357(t, id, lvl_coeffs(mg, B(t, id)->lvl), iv, i_out);
+}
+
+/* mg_auto_gsrb (af_stencil_gsrb_box with the operator key) */
+static void gsrb_box(afh_mg *mg, int id, int redblack) {
+  afh_tree *t = mg->t;
+  if (mg->vst[id - 1])
+    gsrb_357_var(t, id, mg->vst[id - 1], mg->vbc[id - 1], redblack, mg->d.i_phi,
+                 mg->d.i_rhs);
+  else
+    gsrb_357(t, id, lvl_coeffs(mg, B(t, id)->lvl), redblack, mg->d.i_phi,
+             mg->d.i_rhs);
+}
+
 /* residual_box, m_af_multigrid.f90:801-810 */
 static void residual_box(afh_mg *mg, int id) {
   afh_tree *t = mg->t;
   int nc = t->nc;
-  apply_357(t, id, lvl_coeffs(mg, B(t, id)->lvl), mg->d.i_phi, mg->d.i_tmp);
+  apply_box(mg, id, mg->d.i_phi, mg->d.i_tmp);
   double *o = ccb(t, mg->d.i_tmp, id), *r = ccb(t, mg->d.i_rhs, id);
   for (int k = 1; k <= nc; k++)
     for (int j = 1; j <= nc; j++)
@@ -634,11 +725,9 @@ int32_t afo_mg_gsrb_boxes(afh_mg *mg, int32_t lvl, int32_t up) {
   afh_tree *t = mg->t;
   int n_cycle = up ? mg->d.n_cycle_up : mg->d.n_cycle_down;
   int nid = LVL_N(t, ids, lvl);
-  const double *cf = lvl_coeffs(mg, lvl);
   for (int n = 1; n <= 2 * n_cycle; n++) {
 #pragma omp parallel for schedule(static)
-    for (int i = 0; i < nid; i++)
-      gsrb_357(t, LVL_AT(t, ids, lvl, i), cf, n, mg->d.i_phi, mg->d.i_rhs);
+    for (int i = 0; i < nid; i++) gsrb_box(mg, LVL_AT(t, ids, lvl, i), n);
     int use_corners = up && n == 2 * n_cycle;
     if (gc_lvl(t, lvl, mg->d.i_phi, use_corners)) return AFH_ERR_STATE;
   }
@@ -672,11 +761,10 @@ int32_t afo_mg_update_coarse(afh_mg *mg, int32_t lvl) {
       gc_lvl(t, lvl - 1, i_phi, 1))
     return AFH_ERR_STATE;
   int np = LVL_N(t, parents, lvl - 1);
-  const double *cf = lvl_coeffs(mg, lvl - 1);
 #pragma omp parallel for schedule(static)
   for (int i = 0; i < np; i++) {
     int id = LVL_AT(t, parents, lvl - 1, i);
-    apply_357(t, id, cf, i_phi, i_rhs);
+    apply_box(mg, id, i_phi, i_rhs);
     double *r = ccb(t, i_rhs, id), *tm = ccb(t, i_tmp, id), *p = ccb(t, i_phi, id);
     for (size_t q = 0; q < bsz; q++) r[q] = r[q] + tm[q];
     for (size_t q = 0; q < bsz; q++) tm[q] = p[q];
@@ -961,10 +1049,60 @@ static void cs_direct_solve(afh_mg *mg) {
   cs_transform(mg, mg->w1, 0, mg->u[0], 1, 0, 0, 0);
 }
 
+/* Fortran spacing(x): the distance from |x| to the next larger double */
+static double f_spacing(double x) {
+  x = fabs(x);
+  if (x == 0) return 2.2250738585072014e-308; /* tiny(1.0_dp) */
+  int e;
+  frexp(x, &e);
+  return ldexp(1.0, e - 53);
+}
+
+/* Level-1 solve with electrode stencils (OUR algorithm; HYPRE is given the
+ * LSF stencils in the reference, m_coarse_solver.f90:286-338): red-black
+ * Gauss-Seidel pairs with the boxes' own stencils and a level ghost fill
+ * after each half-sweep, until phi is stationary (max change <= 4 spacing
+ * of max |phi|, after at least 11 pairs) -- the golden harness' exact
+ * solve -- then the level's ghost cells with corners. */
+static int32_t solve_coarse_gs(afh_mg *mg) {
+  afh_tree *t = mg->t;
+  int nc = t->nc, nid = LVL_N(t, ids, 1);
+  size_t bsz = t->bsz;
+  double *old = malloc(sizeof(double) * bsz * (nid > 0 ? nid : 1));
+  for (int it = 1; it <= 200000; it++) {
+    for (int q = 0; q < nid; q++)
+      memcpy(old + q * bsz, ccb(t, mg->d.i_phi, LVL_AT(t, ids, 1, q)),
+             sizeof(double) * bsz);
+    for (int n = 1; n <= 2; n++) {
+      for (int q = 0; q < nid; q++) gsrb_box(mg, LVL_AT(t, ids, 1, q), n);
+      if (gc_lvl(t, 1, mg->d.i_phi, 0)) return free(old), AFH_ERR_STATE;
+    }
+    double diff = 0, vmax = 0;
+    for (int q = 0; q < nid; q++) {
+      const double *p = ccb(t, mg->d.i_phi, LVL_AT(t, ids, 1, q)), *o = old + q * bsz;
+      for (int k = 1; k <= nc; k++)
+        for (int j = 1; j <= nc; j++)
+          for (int i = 1; i <= nc; i++) {
+            size_t c = IX(t, i, j, k);
+            diff = fmax(diff, fabs(p[c] - o[c]));
+            vmax = fmax(vmax, fabs(p[c]));
+          }
+    }
+    if (hook(t, AFH_HOOK_MAX, 1, mg->d.i_phi, &diff, 1) ||
+        hook(t, AFH_HOOK_MAX, 1, mg->d.i_phi, &vmax, 1))
+      return free(old), AFH_ERR_STATE;
+    if (diff <= 4 * f_spacing(vmax) && it > 10) break;
+  }
+  free(old);
+  return gc_lvl(t, 1, mg->d.i_phi, 1) ? AFH_ERR_STATE : AFH_OK;
+}
+
 /* solve_coarse_grid, m_af_multigrid.f90:266-291 */
 int32_t afo_mg_solve_coarse(afh_mg *mg) {
   afh_tree *t = mg->t;
   int nc = t->nc, nid = LVL_N(t, ids, 1);
+  for (int q = 0; q < t->nb; q++)
+    if (mg->vst[q] && B(t, q + 1)->lvl == 1) return solve_coarse_gs(mg);
   const afh_bc *bc = t->meth[mg->d.i_phi].bc;
   /* coarse_solver_set_rhs_phi: gather rhs (+ BC contributions) and phi */
   for (int q = 0; q < nid; q++) {
@@ -1021,6 +1159,12 @@ int32_t afo_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
   mg->t = t;
   mg->d = *d;
   mg->lvl_c = malloc(sizeof(double) * 7 * t->nlvl);
+  mg->vst = calloc(t->nb, sizeof(double *));
+  mg->vbc = calloc(t->nb, sizeof(double *));
+  mg->lsf_n = calloc(t->nb, sizeof(int));
+  mg->lsf_ix = calloc(t->nb, sizeof(int32_t *));
+  mg->lsf_dd = calloc(t->nb, sizeof(double *));
+  mg->lsf_bv = calloc(t->nb, sizeof(double *));
   for (int l = 1; l <= t->nlvl; l++) {
     int id = LVL_AT(t, ids, l, 0);
     double *c = mg->lvl_c + 7 * (l - 1);
@@ -1084,7 +1228,61 @@ int32_t afo_mg_destroy(afh_mg *mg) {
   for (int d = 0; d < 3; d++) free(mg->q[d]), free(mg->e[d]);
   free(mg->w1), free(mg->w2);
   free(mg->lvl_c);
+  for (int q = 0; q < mg->t->nb; q++) {
+    free(mg->vst[q]), free(mg->vbc[q]);
+    free(mg->lsf_ix[q]), free(mg->lsf_dd[q]), free(mg->lsf_bv[q]);
+  }
+  free(mg->vst), free(mg->vbc), free(mg->lsf_n);
+  free(mg->lsf_ix), free(mg->lsf_dd), free(mg->lsf_bv);
   free(mg);
+  return AFH_OK;
+}
+
+/* The electrode operator stencil of box id as mg_set_operators_lvl stored it
+ * (m_af_multigrid.f90:1133-1171): v = stencils(ix)%v(7, nc, nc, nc),
+ * bc_correction = stencils(ix)%bc_correction (NULL: none); v = NULL removes
+ * it (the level's constant stencil applies again). */
+int32_t afo_mg_set_box_stencil(afh_mg *mg, int32_t id, const double *v,
+                               const double *bc_correction) {
+  if (!mg || id < 1 || id > mg->t->nb) return fail(AFH_ERR_ARG, "bad box id");
+  size_t n3 = (size_t)mg->t->nc * mg->t->nc * mg->t->nc;
+  free(mg->vst[id - 1]), free(mg->vbc[id - 1]);
+  mg->vst[id - 1] = mg->vbc[id - 1] = NULL;
+  if (!v) return AFH_OK;
+  mg->vst[id - 1] = malloc(sizeof(double) * 7 * n3);
+  memcpy(mg->vst[id - 1], v, sizeof(double) * 7 * n3);
+  if (bc_correction) {
+    mg->vbc[id - 1] = malloc(sizeof(double) * n3);
+    memcpy(mg->vbc[id - 1], bc_correction, sizeof(double) * n3);
+  }
+  return AFH_OK;
+}
+
+/* The boundary distances of box id (mg_lsf_distance_key, sparse: ix(3, n)
+ * 1-based cell indices, dd(6, n)) and mg_lsf_boundary_value(box) (nc^3), for
+ * mg_box_lpllsf_gradient; i_lsf = the level-set cc variable. n = 0 removes. */
+int32_t afo_mg_set_box_lsf(afh_mg *mg, int32_t id, int32_t n, const int32_t *ix,
+                           const double *dd, const double *bval, int32_t i_lsf) {
+  if (!mg || id < 1 || id > mg->t->nb || n < 0)
+    return fail(AFH_ERR_ARG, "bad box id / count");
+  afh_tree *t = mg->t;
+  size_t n3 = (size_t)t->nc * t->nc * t->nc;
+  free(mg->lsf_ix[id - 1]), free(mg->lsf_dd[id - 1]), free(mg->lsf_bv[id - 1]);
+  mg->lsf_ix[id - 1] = NULL, mg->lsf_dd[id - 1] = mg->lsf_bv[id - 1] = NULL;
+  mg->lsf_n[id - 1] = 0;
+  if (n == 0) return AFH_OK;
+  if (!ix || !dd || !bval || i_lsf < 1 || i_lsf > t->nvc)
+    return fail(AFH_ERR_ARG, "afo_mg_set_box_lsf: bad argument");
+  for (int e = 0; e < 3 * n; e++)
+    if (ix[e] < 1 || ix[e] > t->nc) return fail(AFH_ERR_ARG, "cell index out of box");
+  mg->lsf_n[id - 1] = n;
+  mg->lsf_ix[id - 1] = malloc(sizeof(int32_t) * 3 * n);
+  memcpy(mg->lsf_ix[id - 1], ix, sizeof(int32_t) * 3 * n);
+  mg->lsf_dd[id - 1] = malloc(sizeof(double) * 6 * n);
+  memcpy(mg->lsf_dd[id - 1], dd, sizeof(double) * 6 * n);
+  mg->lsf_bv[id - 1] = malloc(sizeof(double) * n3);
+  memcpy(mg->lsf_bv[id - 1], bval, sizeof(double) * n3);
+  mg->i_lsf = i_lsf;
   return AFH_OK;
 }
 
@@ -1186,6 +1384,24 @@ int32_t afo_mg_compute_phi_gradient(afh_mg *mg, int32_t i_fc, double fac,
           for (int i = 1; i <= nc; i++)
             f[FX(t, 2, i, j, k)] =
                 inv[2] * (p[IX(t, i, j, k)] - p[IX(t, i, j, k - 1)]);
+      /* mg_box_lpllsf_gradient (m_af_multigrid.f90:2030-2120): electrode
+       * leaf boxes replace the faces next to the boundary, in order */
+      if (mg->lsf_n[id - 1] && B(t, id)->children[0] == 0) {
+        const double *lsf = ccb(t, mg->i_lsf, id), *bv = mg->lsf_bv[id - 1];
+        for (int e = 0; e < mg->lsf_n[id - 1]; e++) {
+          const int32_t *x = mg->lsf_ix[id - 1] + 3 * e;
+          const double *dd = mg->lsf_dd[id - 1] + 6 * e;
+          int i = x[0], j = x[1], k = x[2];
+          double pc = p[IX(t, i, j, k)], bc = bv[vix(nc, i, j, k)];
+          if (lsf[IX(t, i, j, k)] < 0) continue;
+          if (dd[0] < 1) f[FX(t, 0, i, j, k)] = inv[0] * (pc - bc) / dd[0];
+          if (dd[1] < 1) f[FX(t, 0, i + 1, j, k)] = inv[0] * (bc - pc) / dd[1];
+          if (dd[2] < 1) f[FX(t, 1, i, j, k)] = inv[1] * (pc - bc) / dd[2];
+          if (dd[3] < 1) f[FX(t, 1, i, j + 1, k)] = inv[1] * (bc - pc) / dd[3];
+          if (dd[4] < 1) f[FX(t, 2, i, j, k)] = inv[2] * (pc - bc) / dd[4];
+          if (dd[5] < 1) f[FX(t, 2, i, j, k + 1)] = inv[2] * (bc - pc) / dd[5];
+        }
+      }
       if (i_norm > 0) {
         double *o = ccb(t, i_norm, id);
         for (int k = 1; k <= nc; k++)

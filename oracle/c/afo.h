@@ -48,6 +48,10 @@ int32_t afo_mg_fas_vcycle_maxres(afh_mg *mg, int32_t highest_lvl,
 int32_t afo_mg_fas_fmg(afh_mg *mg, int32_t set_residual, int32_t have_guess);
 int32_t afo_mg_compute_phi_gradient(afh_mg *mg, int32_t i_fc, double fac,
                                     int32_t i_norm);
+int32_t afo_mg_set_box_stencil(afh_mg *mg, int32_t id, const double *v,
+                               const double *bc_correction);
+int32_t afo_mg_set_box_lsf(afh_mg *mg, int32_t id, int32_t n, const int32_t *ix,
+                           const double *dd, const double *bval, int32_t i_lsf);
 int32_t afo_fluid_create(afh_tree *t, const afh_fluid_desc *desc,
                          afh_fluid **out);
 int32_t afo_fluid_destroy(afh_fluid *f);

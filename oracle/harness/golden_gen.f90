@@ -18,8 +18,15 @@
 !> which converge to the same linear system HYPRE is given (boundary conditions
 !> folded as in stencil_handle_boundaries, m_coarse_solver.f90:442-491).
 !>
+!> Case rod8 adds a rod electrode as a level-set function (the electrode
+!> operators of m_field.f90:255-346 with field_electrode_type = rod): the
+!> reference stores its LSF stencils (mg_set_operators_tree ->
+!> store_lsf_distance_matrix / mg_box_lsf_stencil), which are dumped to lsf.bin,
+!> and the field solve (V-cycles, FMG, gradient with mg_box_lpllsf_gradient)
+!> runs through them.
+!>
 !> Usage: golden_gen <case> <td_file> <out_dir>
-!>   case = uni4 | amr4 | uni8
+!>   case = uni4 | amr4 | uni8 | rod8
 program golden_gen
 #include "cpp_macros.h"
   use m_af_types
@@ -31,6 +38,8 @@ program golden_gen
   use m_af_multigrid
   use m_af_flux_schemes
   use m_af_limiters
+  use m_coarse_solver, only: mg_lsf_boundary_value
+  use m_geometry, only: GM_dist_line
   use hx_physics
 
   implicit none
@@ -44,14 +53,20 @@ program golden_gen
   ! photoionization Helmholtz mode: Bourdon's second lambda at 1 bar
   ! (src/m_photoi_helmh.f90:100), 1/m
   real(dp), parameter :: helm_lambda = 44081.25_dp
-  logical            :: trace
-  integer            :: u_log
+  logical            :: trace, use_lsf
+  integer            :: u_log, i_lsf
+  ! rod electrode (field_rod_r0/r1/radius as fractions of the domain)
+  real(dp)           :: rod_r0(3), rod_r1(3), rod_radius
 
   call get_command_argument(1, case_name)
   call get_command_argument(2, td_file)
   call get_command_argument(3, out_dir)
 
+  use_lsf = .false.
   select case (trim(case_name))
+  case ("rod8")
+     nc = 8; grid = [8, 8, 8]; max_lvl = 2; amr_lvl = 3; trace = .false.
+     use_lsf = .true.
   case ("uni4")
      nc = 4; grid = [4, 4, 4]; max_lvl = 3; amr_lvl = 0; trace = .true.
   case ("amr4")
@@ -84,6 +99,15 @@ program golden_gen
   call af_add_fc_variable(tree, "flux_elec")
   call af_add_fc_variable(tree, "field")
   if (tree%n_var_cell /= n_cc_vars) error stop "variable layout"
+  if (use_lsf) then
+     ! the electrode's level-set variable (m_streamer.f90 adds "lsf" when
+     ! ST_use_electrode), appended after the standard layout
+     call af_add_cc_variable(tree, "lsf", ix=i_lsf)
+     tree%mg_i_lsf = i_lsf
+     rod_r0 = [0.5_dp, 0.5_dp, 1.0_dp] * dom
+     rod_r1 = [0.5_dp, 0.5_dp, 0.6_dp] * dom
+     rod_radius = 0.1_dp * dom(3)
+  end if
 
   ! Ghost-cell methods as set by streamer.f90:81-84 and m_field.f90:349-350;
   ! phi gets (sides_bc, mg_auto_rb) as in mg_init (m_af_multigrid.f90:102-105)
@@ -111,6 +135,17 @@ program golden_gen
   mg%prolongation_key = tree%n_stencil_keys_stored
   mg%initialized = .true.
   tree%mg_current_operator_mask = mg%operator_mask
+  if (use_lsf) then
+     ! field_initialize with an electrode (m_field.f90:255-346, 439-443):
+     ! rod level-set function, golden-section distances, electrode at the
+     ! applied voltage; mg_init copies tree%mg_i_lsf (m_af_multigrid.f90:77-82)
+     call af_loop_box(tree, set_lsf_box)
+     mg%i_lsf = tree%mg_i_lsf
+     mg%lsf => rod_lsf
+     mg%lsf_dist => mg_lsf_dist_gss
+     mg%lsf_length_scale = rod_radius
+     mg%lsf_boundary_value = current_voltage
+  end if
   call mg_set_operators_tree(tree, mg)
 
   call af_loop_box(tree, set_init)
@@ -123,6 +158,7 @@ program golden_gen
   call dump_topology()
   call dump_tables()
   call dump_state("init")
+  if (use_lsf) call dump_lsf()
 
   ! ------------------------------------------------------------------
   ! field_compute(tree, mg, 0, time, .true.), m_field.f90:405-485
@@ -142,6 +178,17 @@ program golden_gen
   write(u_log, *) "vcycle2_residual", residuals(2)
   call field_from_potential()
   call dump_state("field0")
+
+  if (use_lsf) then
+     ! FAS-FMG through the electrode stencils, from the potential above
+     call dump_state("fmg_in")
+     call fmg(.false.)
+     call dump_state("fmg0")
+     call fmg(.true.)
+     call dump_state("fmg1")
+     close(u_log)
+     stop
+  end if
 
   ! ------------------------------------------------------------------
   ! Heun sub-step 1: forward_euler(dt, s_deriv=0, [0], [1], s_out=1, 1, 2)
@@ -244,6 +291,64 @@ contains
        end do
     end do
   end subroutine set_init
+
+  !> rod_lsf, src/m_field.f90:626-630
+  real(dp) function rod_lsf(r)
+    real(dp), intent(in) :: r(3)
+    rod_lsf = GM_dist_line(r, rod_r0, rod_r1, 3) - rod_radius
+  end function rod_lsf
+
+  !> set_lsf_box, src/m_field.f90:608-619 (all cells, ghost cells included)
+  subroutine set_lsf_box(box)
+    type(box_t), intent(inout) :: box
+    integer                    :: IJK
+    do k = 0, box%n_cell+1
+       do j = 0, box%n_cell+1
+          do i = 0, box%n_cell+1
+             box%cc(IJK, i_lsf) = rod_lsf(af_r_cc(box, [IJK]))
+          end do
+       end do
+    end do
+  end subroutine set_lsf_box
+
+  !> The electrode stencils the reference stored (mg_set_operators_lvl,
+  !> m_af_multigrid.f90:1133-1171) per box: the variable operator stencil
+  !> v(7, nc^3) and its bc_correction (mg_box_lsf_stencil 1762-1834, f times
+  !> mg_lsf_boundary_value), and the sparse boundary distances
+  !> (store_lsf_distance_matrix 977-1097) with the boundary values, as used
+  !> by mg_box_lpllsf_gradient (2030-2120).
+  subroutine dump_lsf()
+    integer :: u, id, ix, n, has
+    open(newunit=u, file=trim(out_dir)//"/lsf.bin", &
+         access="stream", form="unformatted", status="replace")
+    do id = 1, tree%highest_id
+       associate (box => tree%boxes(id))
+         ix = af_stencil_index(box, mg%operator_key)
+         has = 0
+         if (ix > af_stencil_none) then
+            if (box%stencils(ix)%stype == stencil_variable) has = 1
+         end if
+         write(u) has
+         if (has == 1) then
+            write(u) box%stencils(ix)%v
+            has = 0
+            if (allocated(box%stencils(ix)%bc_correction)) has = 1
+            write(u) has
+            if (has == 1) write(u) box%stencils(ix)%bc_correction
+         end if
+         ix = af_stencil_index(box, mg_lsf_distance_key)
+         n = 0
+         if (ix > af_stencil_none) n = size(box%stencils(ix)%sparse_ix, 2)
+         write(u) n
+         if (n > 0) then
+            write(u) box%stencils(ix)%sparse_ix
+            write(u) box%stencils(ix)%sparse_v
+            write(u) mg_lsf_boundary_value(box, mg)
+         end if
+       end associate
+    end do
+    close(u)
+  end subroutine dump_lsf
 
   subroutine ref_amr(box, cell_flags)
     type(box_t), intent(in) :: box

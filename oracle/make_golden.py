@@ -28,7 +28,7 @@ TD_FILE = "/root/reference/transport_data/td_air_siglo_swarm.txt"
 
 # cc variable indices (1-based, hx_physics.f90)
 CC = {"e0": 1, "e1": 2, "e2": 3, "pos0": 4, "pos1": 5, "neg0": 7, "neg1": 8,
-      "phi": 10, "efld": 12, "rhs": 13, "tmp": 14}
+      "phi": 10, "efld": 12, "rhs": 13, "tmp": 14, "lsf": 15}
 FC = {"flux": 1, "field": 2}
 
 CHAIN = [
@@ -58,10 +58,23 @@ HELM = [
     ("helm1", ["rhs", "phi", "tmp"], []),
 ]
 HELM_LAMBDA = 44081.25
+# rod electrode (level-set function): the field solve through the reference's
+# LSF stencils, dumped in lsf.bin
+ROD = [
+    ("init", ["phi", "lsf"], []),
+    ("rhs", ["rhs"], []),
+    ("vcycle1", ["phi", "tmp", "rhs"], []),
+    ("vcycle2", ["phi", "tmp", "rhs"], []),
+    ("field0", ["efld"], ["field"]),
+    ("fmg_in", ["phi", "rhs", "tmp"], []),
+    ("fmg0", ["rhs", "phi", "tmp"], []),
+    ("fmg1", ["rhs", "phi", "tmp"], []),
+]
 CASES = {
     "uni4": {"chain": CHAIN + FMG + HELM, "trace": True},
     "uni8": {"chain": CHAIN + FMG + HELM, "trace": False},
     "amr4": {"chain": CHAIN[:7] + FMG + HELM, "trace": False},
+    "rod8": {"chain": ROD, "trace": False, "lsf": True},
 }
 
 
@@ -140,6 +153,50 @@ def read_state(path, topo):
     return cc, fc
 
 
+def read_lsf(path, topo):
+    """lsf.bin of golden_gen (dump_lsf): per box the variable operator
+    stencil v(7, nc^3) + bc_correction, and the sparse boundary distances
+    (sparse_ix(3, n), sparse_v(6, n)) with the boundary values.
+      lsf_v_ids (m,) 1-based box ids; lsf_v (m, nc, nc, nc, 7) [k][j][i][c];
+      lsf_bcc (m, nc, nc, nc) (zeros where lsf_bcc_has == 0)
+      lsf_d_ids, lsf_d_n (q,); lsf_d_ix (sum n, 3) int32 (i, j, k, 1-based);
+      lsf_d_dd (sum n, 6); lsf_d_bval (q, nc, nc, nc)"""
+    nb, nc = int(topo["n_boxes"]), int(topo["nc"])
+    raw = open(path, "rb").read()
+    off = 0
+
+    def take(dtype, n):
+        nonlocal off
+        a = np.frombuffer(raw, dtype=dtype, count=n, offset=off)
+        off += a.nbytes
+        return a.copy()
+
+    n3 = nc ** 3
+    v_ids, v, bcc, bcc_has = [], [], [], []
+    d_ids, d_n, d_ix, d_dd, d_bv = [], [], [], [], []
+    for b in range(nb):
+        if take(np.int32, 1)[0]:
+            v_ids.append(b + 1)
+            v.append(take(np.float64, 7 * n3).reshape(nc, nc, nc, 7))
+            has = take(np.int32, 1)[0]
+            bcc_has.append(has)
+            bcc.append(take(np.float64, n3).reshape(nc, nc, nc) if has
+                       else np.zeros((nc, nc, nc)))
+        n = take(np.int32, 1)[0]
+        if n:
+            d_ids.append(b + 1)
+            d_n.append(n)
+            d_ix.append(take(np.int32, 3 * n).reshape(n, 3))
+            d_dd.append(take(np.float64, 6 * n).reshape(n, 6))
+            d_bv.append(take(np.float64, n3).reshape(nc, nc, nc))
+    assert off == len(raw)
+    return {"lsf_v_ids": np.array(v_ids, np.int32), "lsf_v": np.array(v),
+            "lsf_bcc": np.array(bcc), "lsf_bcc_has": np.array(bcc_has, np.int32),
+            "lsf_d_ids": np.array(d_ids, np.int32), "lsf_d_n": np.array(d_n, np.int32),
+            "lsf_d_ix": np.concatenate(d_ix).astype(np.int32),
+            "lsf_d_dd": np.concatenate(d_dd), "lsf_d_bval": np.array(d_bv)}
+
+
 def pack(case, raw_dir):
     topo = read_topology(os.path.join(raw_dir, "topology.bin"))
     out = dict(topo)
@@ -154,6 +211,8 @@ def pack(case, raw_dir):
         out[key] = np.array(vals)
     spec = CASES[case]
     out["helm_lambda"] = np.array(HELM_LAMBDA)
+    if spec.get("lsf"):
+        out.update(read_lsf(os.path.join(raw_dir, "lsf.bin"), topo))
     for name, ccv, fcv in spec["chain"]:
         cc, fc = read_state(os.path.join(raw_dir, "state_%s.bin" % name), topo)
         for v in ccv:
@@ -185,7 +244,7 @@ def main():
     gen = os.path.join(HERE, "_ref", "golden_gen")
     if not os.path.exists(gen):
         sys.exit("build the harness first: make -C oracle ref")
-    for case in CASES:
+    for case in (sys.argv[1:] or CASES):
         raw = os.path.join("/tmp", "golden_raw", case)
         os.makedirs(raw, exist_ok=True)
         for f in os.listdir(raw):

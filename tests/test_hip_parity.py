@@ -69,7 +69,8 @@ def test_hip_matches_reference_golden(hip, case, smoother, coarse):
             if not e <= tol:
                 bad.append((stage, var, e, tol))
     assert not bad, bad
-    np.testing.assert_allclose(dts["flux1"], g["log_flux1_dt"], rtol=1e-15)
+    if "flux1" in dts:
+        np.testing.assert_allclose(dts["flux1"], g["log_flux1_dt"], rtol=1e-15)
 
 
 def _pair(lib_a, lib_b, topo, g, coarse_cycles=12):
@@ -233,3 +234,29 @@ def test_fused_maxabs_equals_separate(hip, oracle, name):
         rb = cb.tree.maxabs_cc(IV["tmp"])
         assert ra == rb and ra == ca.tree.maxabs_cc(IV["tmp"])
     _assert_same(ca, cb, [IV["phi"], IV["tmp"]])
+
+
+@pytest.mark.parametrize("coarse", [12, 0])
+def test_electrode_bitwise_equals_oracle(hip, oracle, smoother, coarse):
+    """The rod-electrode field solve (level-set stencils of the reference,
+    tests/golden/rod8.npz) chained: two V-cycles, the gradient with the
+    electrode faces, FMG without and with guess -- HIP == C oracle bitwise
+    (the level-1 grid holds electrode boxes: Gauss-Seidel to stationarity)."""
+    g = golden.load("rod8")
+    cases = [golden.make_case(lib, g, coarse_cycles=coarse) for lib in (hip, oracle)]
+    state = {**golden.stage_outputs(g, "init"), **golden.stage_outputs(g, "rhs")}
+    names = ["phi", "tmp", "rhs", "efld", "fc_field"]
+    for c in cases:
+        golden.upload(c, state)
+        c.mg.fas_vcycle(True)
+        c.mg.fas_vcycle(True)
+        c.field_from_potential()
+    ra, rb = (golden.download(c, names) for c in cases)
+    for n in names:
+        assert np.array_equal(ra[n], rb[n]), n
+    for c in cases:
+        c.mg.fas_fmg(True, have_guess=False)
+        c.mg.fas_fmg(True, have_guess=True)
+    ra, rb = (golden.download(c, names[:3]) for c in cases)
+    for n in names[:3]:
+        assert np.array_equal(ra[n], rb[n]), n

@@ -41,7 +41,8 @@ def test_oracle_matches_reference(lib, case, coarse_cycles):
                 bad.append((stage, var, e, tol))
     assert not bad, bad
     # dt limits (m_af_flux_schemes.f90 / m_fluid.f90)
-    np.testing.assert_allclose(dts["flux1"], g["log_flux1_dt"], rtol=1e-13)
+    if "flux1" in dts:
+        np.testing.assert_allclose(dts["flux1"], g["log_flux1_dt"], rtol=1e-13)
     if "flux2" in dts:
         np.testing.assert_allclose(dts["flux2"], g["log_flux2_dt"], rtol=1e-13)
         np.testing.assert_allclose(dts["update2"], g["log_update2_dt"], rtol=1e-13)
