@@ -321,6 +321,9 @@ __global__ void __launch_bounds__((RbGeom<NC, TJ>::NT)) __attribute__((amdgpu_wa
 // idles half the lanes in each). Black cells are updated in place in LDS and
 // plane s-1 is then written in full rows (phase E). Same arithmetic in the
 // same order as k_gsrb_pair: bitwise identical results.
+#ifndef AFH_PAIR_NB_LOADS  // 1: every neighbour value of phase B from global
+#define AFH_PAIR_NB_LOADS 0
+#endif
 template <int NC, int TJ = NC>
 struct RbPar {
   static constexpr int NG = NC + 2, HN = NC / 2;
@@ -400,6 +403,11 @@ __global__ void __launch_bounds__((RbPar<NC, TJ>::NT)) __attribute__((amdgpu_wav
     double bl[7];
     int b_i = 0, b_j = 0, b_jl = 0, b_nb = 0, b_rep = -1;  // b_nb 0: none
     bool b_pre = false;
+    // x faces: the neighbour's boundary column is a copy in this box's ghost
+    // column (the last level fill), so its rows j+-1 and planes s+-1 are read
+    // from LDS where they are interior cells of the neighbour (unchanged
+    // black values); only phi next to it and rhs come from the neighbour
+    bool b_lm = false, b_lp = false, b_zm = false, b_zp = false;
     if (s <= NC && tid < TJ + NC) {
       const int u = tid;
       if (u < TJ) {
@@ -433,12 +441,19 @@ __global__ void __launch_bounds__((RbPar<NC, TJ>::NT)) __attribute__((amdgpu_wav
       if (xs) {
         b_pre = true;
         const size_t c = ix3(NG, q[0], q[1], q[2]);
+#if !AFH_PAIR_NB_LOADS
+        const bool xg = b_rep == 0 || b_rep == 1;
+        b_lm = xg && b_j >= 2;
+        b_lp = xg && b_j <= NC - 1;
+        b_zm = xg && s >= 2;
+        b_zp = xg && s <= NC - 1;
+#endif
         bl[0] = b_rep == 0 ? 0.0 : xs[c - 1];
         bl[1] = b_rep == 1 ? 0.0 : xs[c + 1];
-        bl[2] = b_rep == 2 ? 0.0 : xs[c - NG];
-        bl[3] = b_rep == 3 ? 0.0 : xs[c + NG];
-        bl[4] = b_rep == 4 ? 0.0 : xs[c - SK];
-        bl[5] = b_rep == 5 ? 0.0 : xs[c + SK];
+        bl[2] = (b_rep == 2 || b_lm) ? 0.0 : xs[c - NG];
+        bl[3] = (b_rep == 3 || b_lp) ? 0.0 : xs[c + NG];
+        bl[4] = (b_rep == 4 || b_zm) ? 0.0 : xs[c - SK];
+        bl[5] = (b_rep == 5 || b_zp) ? 0.0 : xs[c + SK];
         bl[6] = rs[c];
       }
     }
@@ -487,6 +502,10 @@ __global__ void __launch_bounds__((RbPar<NC, TJ>::NT)) __attribute__((amdgpu_wav
           const double x1v = P0[p1[1] * NG + p1[0]];
           bl[b_rep] = x1v;
         }
+        if (b_lm) bl[2] = P0[(b_jl - 1) * NG + b_i];
+        if (b_lp) bl[3] = P0[(b_jl + 1) * NG + b_i];
+        if (b_zm) bl[4] = Pm[b_jl * NG + b_i];
+        if (b_zp) bl[5] = Pp[b_jl * NG + b_i];
         v = (bl[6] - cf.c[1] * bl[0] - cf.c[2] * bl[1] - cf.c[3] * bl[2] -
              cf.c[4] * bl[3] - cf.c[5] * bl[4] - cf.c[6] * bl[5]) *
             inv_c1;
