@@ -128,6 +128,10 @@ int32_t upload_list(afh_tree *t, LevelList &L,
 // Kernel timing: bracket one launch of class `kc` (no-op unless enabled).
 void prof_begin(afh_tree *t, int kc);
 void prof_end(afh_tree *t, int kc, double bytes);
+// or: a start / end event pair for a launch that records them itself
+// (hipExtLaunchKernelGGL; false: class not timed), then prof_count
+bool prof_ext(afh_tree *t, int kc, hipEvent_t &e0, hipEvent_t &e1);
+void prof_count(afh_tree *t, double bytes);
 // Host launchers shared between translation units (afh_tree.hip).
 int32_t gc_lvl(afh_tree *t, int lvl, int iv, int corners, bool rims = false);
 // ghost fill of level lvl of variable iv (0: the spare phi image), with the

@@ -12,6 +12,8 @@
 //   k_prolong       stencil_prolong_248 add (m_af_stencil.f90:749-771)
 //   k_gradient      mg_box_lpl_gradient + mg_box_field_norm (1882-2025)
 // plus the level-1 coarse solver (ours; the reference calls HYPRE PFMG).
+#include <hip/hip_ext.h>
+
 #include <algorithm>
 
 #include "afh_internal.h"
@@ -1834,13 +1836,25 @@ int32_t afh_mg_destroy(afh_mg *mg) {
 
 }  // extern "C"
 
+// A launch whose start / end events are written by the dispatch itself
+// (hipExtLaunchKernelGGL: the clock of rocprofv3's kernel trace, no barrier
+// packets around the kernel) when e0 is set; a plain launch otherwise.
+template <typename K, typename... A>
+static void launch_ev(K k, hipEvent_t e0, hipEvent_t e1, dim3 g, dim3 b,
+                      hipStream_t st, A... a) {
+  if (e0)
+    hipExtLaunchKernelGGL(k, g, b, 0, st, e0, e1, 0, a...);
+  else
+    hipLaunchKernelGGL(k, g, b, 0, st, a...);
+}
+
 template <int NC, int TJ>
 static void launch_pair_t(afh_mg *mg, int lvl, const double *src, double *dst,
-                          const Coef &cf, double inv_c1) {
+                          const Coef &cf, double inv_c1, hipEvent_t e0, hipEvent_t e1) {
   afh_tree *t = mg->t;
-  hipLaunchKernelGGL((k_gsrb_pair<NC, TJ>),
+  launch_ev((k_gsrb_pair<NC, TJ>), e0, e1,
                      dim3(t->ids.n(lvl) * RbGeom<NC, TJ>::NTILE),
-                     dim3(RbGeom<NC, TJ>::NT), 0, t->stream, src, dst,
+                     dim3(RbGeom<NC, TJ>::NT), t->stream, src, dst,
                      t->ccv(mg->d.i_rhs), t->ccv(mg->d.i_phi), t->d_boxes,
                      t->ids.at(lvl), t->bsz, cf, inv_c1,
                      t->gc_args(mg->d.i_phi));
@@ -1856,33 +1870,32 @@ static bool pair_tiles(const afh_mg *mg, int lvl) {
 
 template <int NC>
 static void launch_pair(afh_mg *mg, int lvl, const double *src, double *dst,
-                        const Coef &cf, double inv_c1) {
+                        const Coef &cf, double inv_c1, hipEvent_t e0, hipEvent_t e1) {
   afh_tree *t = mg->t;
   if (t->ids.n(lvl) == 0) return;
   if constexpr (NC >= 32) {
     if (pair_tiles(mg, lvl))
-      return launch_pair_t<NC, NC / 4>(mg, lvl, src, dst, cf, inv_c1);
+      return launch_pair_t<NC, NC / 4>(mg, lvl, src, dst, cf, inv_c1, e0, e1);
   }
   if constexpr (NC >= 16) {
     if (!mg->pair_v1) {
       if constexpr (NC == 64) {
         if (mg->pair_tj == 32) {
-          hipLaunchKernelGGL((k_gsrb_pair2<NC, 32>), dim3(t->ids.n(lvl) * 2),
-                             dim3(RbPar<NC, 32>::NT), 0, t->stream, src, dst,
-                             t->ccv(mg->d.i_rhs), t->ccv(mg->d.i_phi), t->d_boxes,
-                             t->ids.at(lvl), t->bsz, cf, inv_c1,
-                             t->gc_args(mg->d.i_phi));
+          launch_ev((k_gsrb_pair2<NC, 32>), e0, e1, dim3(t->ids.n(lvl) * 2),
+                    dim3(RbPar<NC, 32>::NT), t->stream, src, dst,
+                    t->ccv(mg->d.i_rhs), t->ccv(mg->d.i_phi), t->d_boxes,
+                    t->ids.at(lvl), t->bsz, cf, inv_c1, t->gc_args(mg->d.i_phi));
           return;
         }
       }
-      hipLaunchKernelGGL((k_gsrb_pair2<NC, NC>), dim3(t->ids.n(lvl)),
-                         dim3(RbPar<NC, NC>::NT), 0, t->stream, src, dst,
-                         t->ccv(mg->d.i_rhs), t->ccv(mg->d.i_phi), t->d_boxes,
-                         t->ids.at(lvl), t->bsz, cf, inv_c1, t->gc_args(mg->d.i_phi));
+      launch_ev((k_gsrb_pair2<NC, NC>), e0, e1, dim3(t->ids.n(lvl)),
+                dim3(RbPar<NC, NC>::NT), t->stream, src, dst, t->ccv(mg->d.i_rhs),
+                t->ccv(mg->d.i_phi), t->d_boxes, t->ids.at(lvl), t->bsz, cf, inv_c1,
+                t->gc_args(mg->d.i_phi));
       return;
     }
   }
-  launch_pair_t<NC, NC>(mg, lvl, src, dst, cf, inv_c1);
+  launch_pair_t<NC, NC>(mg, lvl, src, dst, cf, inv_c1, e0, e1);
 }
 
 extern "C" {
@@ -2002,17 +2015,18 @@ static int32_t gsrb_boxes(afh_mg *mg, int lvl, bool up) {
     const int dst_iv = to_alt ? 0 : mg->d.i_phi;
     const int pclass = (nc >= 32 && pair_tiles(mg, lvl)) ? AFH_PROF_GSRB_PAIR_TILED
                                                           : AFH_PROF_GSRB_PAIR;
-    prof_begin(t, pclass);
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    const bool timed = prof_ext(t, pclass, e0, e1);
     switch (nc) {
-    case 4: launch_pair<4>(mg, lvl, src, dst, cf, inv_c1); break;
-    case 8: launch_pair<8>(mg, lvl, src, dst, cf, inv_c1); break;
-    case 16: launch_pair<16>(mg, lvl, src, dst, cf, inv_c1); break;
-    case 32: launch_pair<32>(mg, lvl, src, dst, cf, inv_c1); break;
-    default: launch_pair<64>(mg, lvl, src, dst, cf, inv_c1); break;
+    case 4: launch_pair<4>(mg, lvl, src, dst, cf, inv_c1, e0, e1); break;
+    case 8: launch_pair<8>(mg, lvl, src, dst, cf, inv_c1, e0, e1); break;
+    case 16: launch_pair<16>(mg, lvl, src, dst, cf, inv_c1, e0, e1); break;
+    case 32: launch_pair<32>(mg, lvl, src, dst, cf, inv_c1, e0, e1); break;
+    default: launch_pair<64>(mg, lvl, src, dst, cf, inv_c1, e0, e1); break;
     }
     // a red+black pair reads phi and rhs and writes phi
     // once = 24 B/cell
-    prof_end(t, pclass, 24.0 * nc * nc * nc * nid);
+    if (timed) prof_count(t, 24.0 * nc * nc * nc * nid);
     AFH_LAUNCH_CHECK("k_gsrb_pair");
     (void)dst;
     if (int32_t e = gc_lvl_var(t, lvl, dst_iv, phi, ga, up && n == n_cycle, true))

@@ -44,6 +44,18 @@ void prof_begin(afh_tree *t, int kc) {
   hipEventRecord(next_event(t), t->stream);
 }
 
+bool prof_ext(afh_tree *t, int kc, hipEvent_t &e0, hipEvent_t &e1) {
+  if (t->prof_class != kc) return false;
+  e0 = next_event(t);
+  e1 = next_event(t);
+  return true;
+}
+
+void prof_count(afh_tree *t, double bytes) {
+  t->prof_bytes += bytes;
+  t->prof_launches++;
+}
+
 void prof_end(afh_tree *t, int kc, double bytes) {
   if (t->prof_class != kc) return;
   hipEventRecord(next_event(t), t->stream);

@@ -4,8 +4,9 @@
 One step = one unit of SURVEY.md 8(d) on every leaf cell: field_set_rhs +
 max|rhs| + one FAS V(2,2)-cycle with the residual + max|residual| (the
 field_compute convergence test) + field_from_potential (gradient, |E|, |E|
-ghost cells) + flux_upwind_tree + flux_update_densities with chemistry
-(a forward-Euler sub-step, af_forward_euler), all through libafivo_hip.so.
+ghost cells) + flux_upwind_tree + flux_update_densities with chemistry --
+one sub-step of af_heuns_method, stages 1 and 2 alternating (unit_step) --
+all through libafivo_hip.so.
 
 Default workload: S1-64: a uniform 3-D tree of 512 leaf boxes
 of 64^3 cells (134 M leaf cells, 585 boxes, 4 levels, 64^3 coarse grid),
