@@ -900,8 +900,14 @@ __global__ void k_consistent(double *__restrict__ F,
               fc[fidx(nf, d, p4[0], p4[1], p4[2])]);
 }
 
-template <int NS, bool SLOW>
-__global__ void __launch_bounds__(256)
+// NP: the number of previous states when known at compile time (1, 2), or
+// MAXPREV (any, A.n_prev); SD: the derivative state is no previous state
+// (A.der_q < 0) -- both only trim registers and dead loads
+#ifndef AFH_UPD_MINW  // minimum waves per SIMD of the update kernel
+#define AFH_UPD_MINW 1
+#endif
+template <int NS, bool SLOW, int NP = MAXPREV, bool SD = true>
+__global__ void __launch_bounds__(256, AFH_UPD_MINW)
     k_update(UpdArgs A, const int32_t *__restrict__ ids, int nc, size_t bsz,
              size_t fsz, unsigned long long *red) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -919,24 +925,27 @@ __global__ void __launch_bounds__(256)
     const double fx0 = F[f0], fx1 = F[f0 + 1], fy0 = F[d3 + f0], fy1 = F[d3 + f0 + nf],
                  fz0 = F[2 * d3 + f0], fz1 = F[2 * d3 + f0 + nf * nf];
     const double ev = A.E[x];
-    double pv[NS][MAXPREV], dv[NS];
+    const int n_prev = NP == MAXPREV ? A.n_prev : NP;
+    const int der_q = (NP == MAXPREV || SD) ? A.der_q : -2;  // -2: see below
+    double pv[NS][NP], dv[NS];
 #pragma unroll
     for (int s = 0; s < NS; s++) {
 #pragma unroll
-      for (int q = 0; q < MAXPREV; q++) pv[s][q] = q < A.n_prev ? A.prev[s][q][x] : 0.0;
-      dv[s] = A.der_q >= 0 ? 0.0 : A.der[s][x];
+      for (int q = 0; q < NP; q++) pv[s][q] = q < n_prev ? A.prev[s][q][x] : 0.0;
+      dv[s] = (NP != MAXPREV && !SD) || A.der_q >= 0 ? 0.0 : A.der[s][x];
     }
+    (void)der_q;
     double y[NS], der[NS], dens[NS];
 #pragma unroll
     for (int s = 0; s < NS; s++) {
       double tmp = 0.0;
 #pragma unroll
-      for (int q = 0; q < MAXPREV; q++)
-        if (q < A.n_prev) tmp = tmp + A.w_prev[q] * pv[s][q];
+      for (int q = 0; q < NP; q++)
+        if (q < n_prev) tmp = tmp + A.w_prev[q] * pv[s][q];
       y[s] = tmp;
       double v = dv[s];
 #pragma unroll
-      for (int q = 0; q < MAXPREV; q++)
+      for (int q = 0; q < NP; q++)
         if (q == A.der_q) v = pv[s][q];
       dens[s] = v > 0.0 ? v : 0.0;  // max(dens, 0.0_dp)
       der[s] = 0.0;
@@ -998,14 +1007,21 @@ void launch_update(const UpdArgs &A, afh_tree *t, int l,
                    unsigned long long *red, bool slow) {
   const int nc = t->nc, n3 = nc * nc * nc;
   const dim3 grid((n3 + 255) / 256, t->leaves.n(l));
+  const auto *ids = t->leaves.at(l);
+  const bool sd = A.der_q < 0;
   if (slow)
     hipLaunchKernelGGL((k_update<NS, true>), grid, dim3(256), 0, t->stream, A,
-                       t->leaves.at(l), nc, t->bsz, t->fsz, red);
+                       ids, nc, t->bsz, t->fsz, red);
+  else if (A.n_prev == 1 && !sd)
+    hipLaunchKernelGGL((k_update<NS, false, 1, false>), grid, dim3(256), 0,
+                       t->stream, A, ids, nc, t->bsz, t->fsz, red);
+  else if (A.n_prev == 2 && !sd)
+    hipLaunchKernelGGL((k_update<NS, false, 2, false>), grid, dim3(256), 0,
+                       t->stream, A, ids, nc, t->bsz, t->fsz, red);
   else
     hipLaunchKernelGGL((k_update<NS, false>), grid, dim3(256), 0, t->stream, A,
-                       t->leaves.at(l), nc, t->bsz, t->fsz, red);
+                       ids, nc, t->bsz, t->fsz, red);
 }
-
 
 // Fused forward-Euler species step: flux_upwind_tree + flux_update_densities
 // of forward_euler (src/m_fluid.f90:56-70) when no face needs a coarse-fine
