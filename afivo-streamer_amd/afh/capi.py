@@ -100,6 +100,8 @@ _PVP = C.POINTER(C.c_void_p)
 SIGNATURES = {
     "last_error": (C.c_char_p, []),
     "tree_create": (i32, [C.POINTER(TreeDesc), i32, _PVP]),
+    "set_cc_prolong": (i32, [_VP, i32, i32, i32]),
+    "tree_regrid": (i32, [_VP, C.POINTER(TreeDesc), _PVP]),
     "tree_destroy": (i32, [_VP]),
     "tree_sync": (i32, [_VP]),
     "set_cc_methods": (i32, [_VP, i32, C.POINTER(BC), i32, i32]),
@@ -145,6 +147,7 @@ HOOK_HALO, HOOK_RIMS, HOOK_RESTRICT, HOOK_MAX, HOOK_MIN, HOOK_CFLUX = 1, 2, 3, 4
 HOOK_FN = C.CFUNCTYPE(i32, C.c_void_p, i32, i32, i32, P_f64, i32)
 PROF_GSRB, PROF_GHOST, PROF_FLUX, PROF_UPDATE, PROF_GSRB_PAIR, PROF_GSRB_PAIR_TILED = 1, 2, 3, 4, 5, 6
 PROF_FE = 7
+PROLONG_NONE, PROLONG_LINEAR, PROLONG_LIMIT = 0, 1, 2
 ORACLE_EXTRA = {
     "mg_gsrb_boxes": (i32, [_VP, i32, i32]),
     "mg_update_coarse": (i32, [_VP, i32]),

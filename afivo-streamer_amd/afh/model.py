@@ -30,7 +30,7 @@ def _lists(topo, kind):
 class Tree:
     """af_t: topology + device box pool of n_var_cell / n_var_face variables."""
 
-    def __init__(self, lib, topo, n_var_cell, n_var_face, device=-1):
+    def __init__(self, lib, topo, n_var_cell, n_var_face, device=-1, _regrid_of=None):
         self.lib = lib
         self.topo = topo
         self.nc = int(topo["nc"])
@@ -63,8 +63,22 @@ class Tree:
             setattr(d, "lvl_%s" % k, flat.ctypes.data_as(capi.P_i32))
             setattr(d, "lvl_%s_off" % k, off.ctypes.data_as(capi.P_i32))
         h = C.c_void_p()
-        lib.call("tree_create", C.byref(d), device, C.byref(h))
+        if _regrid_of is None:
+            lib.call("tree_create", C.byref(d), device, C.byref(h))
+        else:
+            lib.call("tree_regrid", _regrid_of.h, C.byref(d), C.byref(h))
         self.h = h
+
+    def regrid(self, topo):
+        """af_adjust_refinement's data movement onto the new topology `topo`
+        (afh_tree_regrid): a new Tree; this one stays valid."""
+        return Tree(self.lib, topo, self.n_var_cell, self.n_var_face,
+                    _regrid_of=self)
+
+    def set_cc_prolong(self, iv, method, limiter=capi.LIM_GMINMOD43):
+        """tree%cc_methods(iv)%prolong (capi.PROLONG_LINEAR / PROLONG_LIMIT)
+        and prolong_limiter; iv becomes an automatic variable."""
+        self.lib.call("set_cc_prolong", self.h, iv, method, limiter)
 
     # -- lifetime
     def close(self):

@@ -40,6 +40,8 @@ struct CcMethod {
   afh_bc bc[6];
   int rb = AFH_RB_GC_INTERP;
   int lim = AFH_LIM_GMINMOD43;
+  int prolong = AFH_PROLONG_NONE;  // afh_set_cc_prolong
+  int prolong_lim = AFH_LIM_GMINMOD43;
 };
 
 // Per-variable methods as the kernels see them (passed by value).
@@ -81,6 +83,7 @@ struct afh_tree {
   double *scratch = nullptr; // reductions etc.
   double *h_scratch = nullptr;
   std::vector<afh::CcMethod> meth;
+  std::vector<int> auto_vars;  // tree%cc_auto_vars (afh_set_cc_prolong order)
   // grid spacing per level (afivo halves dr exactly per level, so every box
   // of a level has the same bits; verified at tree creation)
   std::vector<double> lvl_dr;  // 3 per level
@@ -193,6 +196,38 @@ inline unsigned long long host_dbl_to_ord(double x) {
 
 __device__ __forceinline__ size_t ix3(int ng, int i, int j, int k) {
   return ((size_t)k * ng + j) * ng + i;
+}
+
+// af_limiter_apply (m_af_limiters.f90:41-149)
+__device__ __forceinline__ double limiter(int lim, double a, double b) {
+  const double third = 1 / 3.0;
+  switch (lim) {
+  case AFH_LIM_KOREN: {
+    const double aa = a * a, ab = a * b;
+    if (ab <= 0) return 0;
+    if (aa <= 0.25 * ab) return 2 * a;
+    if (aa <= 2.5 * ab) return third * (b + 2 * a);
+    return 2 * b;
+  }
+  case AFH_LIM_VANLEER: {
+    const double ab = a * b;
+    return ab > 0 ? 2 * ab / (a + b) : 0;
+  }
+  case AFH_LIM_NONE: return 0.5 * (a + b);
+  case AFH_LIM_ZERO: return 0.0;
+  default: {
+    const double th =
+        lim == AFH_LIM_MINMOD ? 1.0 : lim == AFH_LIM_MC ? 2.0 : 4 / 3.0;
+    if (a * b > 0) {
+      double m = fabs(th * a);
+      const double y = fabs(th * b), z = fabs(0.5 * (a + b));
+      if (y < m) m = y;
+      if (z < m) m = z;
+      return copysign(m, a);
+    }
+    return 0.0;
+  }
+  }
 }
 
 // Linear index t -> (i, j, k), 1-based, of an n x n x n block, i fastest.

@@ -54,38 +54,6 @@ __device__ __forceinline__ double lt_col(const DevLT &lt, int col, double x) {
   return lf * r[low - 1] + (1 - lf) * r[low];
 }
 
-// af_limiter_apply (m_af_limiters.f90:41-149)
-__device__ __forceinline__ double limiter(int lim, double a, double b) {
-  const double third = 1 / 3.0;
-  switch (lim) {
-  case AFH_LIM_KOREN: {
-    const double aa = a * a, ab = a * b;
-    if (ab <= 0) return 0;
-    if (aa <= 0.25 * ab) return 2 * a;
-    if (aa <= 2.5 * ab) return third * (b + 2 * a);
-    return 2 * b;
-  }
-  case AFH_LIM_VANLEER: {
-    const double ab = a * b;
-    return ab > 0 ? 2 * ab / (a + b) : 0;
-  }
-  case AFH_LIM_NONE: return 0.5 * (a + b);
-  case AFH_LIM_ZERO: return 0.0;
-  default: {
-    const double th =
-        lim == AFH_LIM_MINMOD ? 1.0 : lim == AFH_LIM_MC ? 2.0 : 4 / 3.0;
-    if (a * b > 0) {
-      double m = fabs(th * a);
-      const double y = fabs(th * b), z = fabs(0.5 * (a + b));
-      if (y < m) m = y;
-      if (z < m) m = z;
-      return copysign(m, a);
-    }
-    return 0.0;
-  }
-  }
-}
-
 // limiter with a compile-time choice (LIM = AFH_LIM_KOREN, the reference's
 // flux limiter) or the runtime switch (LIM = 0)
 template <int LIM>

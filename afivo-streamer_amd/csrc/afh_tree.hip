@@ -383,6 +383,77 @@ int32_t upload_list(afh_tree *t, LevelList &L,
   return AFH_OK;
 }
 
+
+// ------------------------------------------------------------ regrid
+// af_prolong_limit / af_prolong_linear (m_af_prolong.f90:311-420, 531-679),
+// add = .false.: one thread per parent cell of the child's octant writes
+// its 8 child cells (value + 0, the child interior starting at 0)
+template <int METHOD>
+__global__ void k_prolong_new(double *__restrict__ v,
+                              const afh_box_meta *__restrict__ meta,
+                              const int32_t *__restrict__ ids, int nc, size_t bsz,
+                              int lim) {
+  const int hn = nc >> 1;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= hn * hn * hn) return;
+  const int id = ids[blockIdx.y];
+  const afh_box_meta &m = meta[id - 1];
+  int i, j, k;
+  cell3(t, hn, i, j, k);
+  const int ng = nc + 2;
+  const int ic = i + ((m.ix[0] - 1) & 1) * hn, jc = j + ((m.ix[1] - 1) & 1) * hn,
+            kc = k + ((m.ix[2] - 1) & 1) * hn;
+  const double *p = v + (size_t)(m.parent - 1) * bsz;
+  double *c = v + (size_t)(id - 1) * bsz;
+  const int fi = 2 * i - 1, fj = 2 * j - 1, fk = 2 * k - 1;
+  auto P = [&](int a, int b, int d) { return p[ix3(ng, ic + a, jc + b, kc + d)]; };
+  if (METHOD == AFH_PROLONG_LIMIT) {
+    const double f0 = P(0, 0, 0);
+    const double f1 = 0.25 * limiter(lim, f0 - P(-1, 0, 0), P(1, 0, 0) - f0);
+    const double f2 = 0.25 * limiter(lim, f0 - P(0, -1, 0), P(0, 1, 0) - f0);
+    const double f3 = 0.25 * limiter(lim, f0 - P(0, 0, -1), P(0, 0, 1) - f0);
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      double x = (q & 1) ? f0 + f1 : f0 - f1;
+      x = ((q >> 1) & 1) ? x + f2 : x - f2;
+      x = (q >> 2) ? x + f3 : x - f3;
+      c[ix3(ng, fi + (q & 1), fj + ((q >> 1) & 1), fk + (q >> 2))] = x + 0.0;
+    }
+  } else {
+    const double f1 = 1 / 64.0, f3 = 3 / 64.0, f9 = 9 / 64.0, f27 = 27 / 64.0;
+    const double f000 = f27 * P(0, 0, 0);
+    const double f00l = f9 * P(0, 0, -1), f0l0 = f9 * P(0, -1, 0), f0ll = f3 * P(0, -1, -1);
+    const double fl00 = f9 * P(-1, 0, 0), fl0l = f3 * P(-1, 0, -1), fll0 = f3 * P(-1, -1, 0);
+    const double flll = f1 * P(-1, -1, -1);
+    const double f00h = f9 * P(0, 0, 1), f0h0 = f9 * P(0, 1, 0), f0hh = f3 * P(0, 1, 1);
+    const double fh00 = f9 * P(1, 0, 0), fh0h = f3 * P(1, 0, 1), fhh0 = f3 * P(1, 1, 0);
+    const double fhhh = f1 * P(1, 1, 1);
+    const double fl0h = f3 * P(-1, 0, 1), fh0l = f3 * P(1, 0, -1), flh0 = f3 * P(-1, 1, 0);
+    const double fhl0 = f3 * P(1, -1, 0), f0lh = f3 * P(0, -1, 1), f0hl = f3 * P(0, 1, -1);
+    const double fllh = f1 * P(-1, -1, 1), flhl = f1 * P(-1, 1, -1), fhll = f1 * P(1, -1, -1);
+    const double fhhl = f1 * P(1, 1, -1), fhlh = f1 * P(1, -1, 1), flhh = f1 * P(-1, 1, 1);
+    auto W = [&](int a, int b, int d, double x) { c[ix3(ng, fi + a, fj + b, fk + d)] = x + 0.0; };
+    W(0, 0, 0, f000 + fl00 + f0l0 + f00l + fll0 + fl0l + f0ll + flll);
+    W(1, 0, 0, f000 + fh00 + f0l0 + f00l + fhl0 + fh0l + f0ll + fhll);
+    W(0, 1, 0, f000 + fl00 + f0h0 + f00l + flh0 + fl0l + f0hl + flhl);
+    W(1, 1, 0, f000 + fh00 + f0h0 + f00l + fhh0 + fh0l + f0hl + fhhl);
+    W(0, 0, 1, f000 + fl00 + f0l0 + f00h + fll0 + fl0h + f0lh + fllh);
+    W(1, 0, 1, f000 + fh00 + f0l0 + f00h + fhl0 + fh0h + f0lh + fhlh);
+    W(0, 1, 1, f000 + fl00 + f0h0 + f00h + flh0 + fl0h + f0hh + flhh);
+    W(1, 1, 1, f000 + fh00 + f0h0 + f00h + fhh0 + fh0h + f0hh + fhhh);
+  }
+}
+
+// box ids[blockIdx.y] of variable blockIdx.z: src pool -> dst pool (the two
+// pools of a regrid have different box counts, so different variable strides)
+__global__ void k_copy_boxes(const double *__restrict__ src, double *__restrict__ dst,
+                             const int32_t *__restrict__ ids, size_t per_box,
+                             size_t src_var, size_t dst_var) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= per_box) return;
+  const size_t b = (size_t)(ids[blockIdx.y] - 1) * per_box + t;
+  dst[blockIdx.z * dst_var + b] = src[blockIdx.z * src_var + b];
+}
 }  // namespace afh
 
 using namespace afh;
@@ -783,3 +854,119 @@ int32_t afh_plan_unpack(afh_tree *t, int32_t plan, int32_t iv,
 }
 
 }  // extern "C"
+
+// device id list for one launch (freed by the caller after a sync)
+static int32_t device_list(const std::vector<int32_t> &h, int32_t **d) {
+  AFH_HIP(hipMalloc(d, sizeof(int32_t) * std::max<size_t>(1, h.size())));
+  if (!h.empty())
+    AFH_HIP(hipMemcpy(*d, h.data(), sizeof(int32_t) * h.size(), hipMemcpyHostToDevice));
+  return AFH_OK;
+}
+
+extern "C" {
+
+int32_t afh_set_cc_prolong(afh_tree *t, int32_t iv, int32_t method, int32_t limiter) {
+  if (!t || iv < 1 || iv > t->nvc) return set_error(AFH_ERR_ARG, "bad variable index");
+  if (method < AFH_PROLONG_NONE || method > AFH_PROLONG_LIMIT)
+    return set_error(AFH_ERR_UNSUPPORTED, "prolongation method %d", method);
+  if (!t->meth[iv].set) return set_error(AFH_ERR_STATE, "set cc methods first");
+  if (method != AFH_PROLONG_NONE &&
+      std::find(t->auto_vars.begin(), t->auto_vars.end(), iv) == t->auto_vars.end())
+    t->auto_vars.push_back(iv);
+  t->meth[iv].prolong = method;
+  t->meth[iv].prolong_lim = limiter;
+  return AFH_OK;
+}
+
+int32_t afh_tree_regrid(afh_tree *o, const afh_tree_desc *d, afh_tree **out) {
+  if (!o || !d || !out) return set_error(AFH_ERR_ARG, "afh_tree_regrid: null");
+  if (d->n_cell != o->nc || d->n_var_cell != o->nvc || d->n_var_face != o->nvf)
+    return set_error(AFH_ERR_ARG, "afh_tree_regrid: box size / variables differ");
+  if (o->hook) return set_error(AFH_ERR_UNSUPPORTED, "regrid of a sharded tree");
+  afh_tree *t = nullptr;
+  int32_t e;
+  if ((e = afh_tree_create(d, o->device, &t))) return e;
+  t->meth = o->meth;
+  t->auto_vars = o->auto_vars;
+  const int nc = t->nc;
+  // boxes that persist: same id, level and index in both topologies
+  std::vector<char> in_old(o->nb + 1, 0), keep(t->nb + 1, 0);
+  for (const auto &L : o->h_ids)
+    for (int32_t id : L) in_old[id] = 1;
+  std::vector<int32_t> kept, rchild;
+  for (const auto &L : t->h_ids)
+    for (int32_t id : L) {
+      if (id > o->nb || !in_old[id]) continue;
+      const afh_box_meta &a = o->boxes[id - 1], &b = t->boxes[id - 1];
+      if (a.lvl != b.lvl || a.ix[0] != b.ix[0] || a.ix[1] != b.ix[1] || a.ix[2] != b.ix[2])
+        continue;
+      keep[id] = 1;
+      kept.push_back(id);
+      // auto_restrict (m_af_core.f90:826-840): the box lost its children
+      if (a.children[0] > 0 && b.children[0] == 0)
+        for (int c = 0; c < 8; c++) rchild.push_back(a.children[c]);
+    }
+  int32_t *d_list = nullptr;
+  if (!rchild.empty()) {
+    if ((e = device_list(rchild, &d_list))) return e;
+    for (int iv : o->auto_vars)
+      if ((e = restrict_boxes(o, d_list, (int)rchild.size(), iv))) return e;
+  }
+  AFH_HIP(hipStreamSynchronize(o->stream));
+  hipFree(d_list);
+  d_list = nullptr;
+  if (!kept.empty()) {
+    if ((e = device_list(kept, &d_list))) return e;
+    const unsigned n = (unsigned)kept.size();
+    hipLaunchKernelGGL(k_copy_boxes, dim3((unsigned)((t->bsz + 255) / 256), n, t->nvc),
+                       dim3(256), 0, t->stream, o->cc, t->cc, d_list, t->bsz,
+                       (size_t)o->nb * o->bsz, (size_t)t->nb * t->bsz);
+    AFH_LAUNCH_CHECK("k_copy_boxes");
+    if (t->nvf > 0) {
+      hipLaunchKernelGGL(k_copy_boxes, dim3((unsigned)((t->fsz + 255) / 256), n, t->nvf),
+                         dim3(256), 0, t->stream, o->fc, t->fc, d_list, t->fsz,
+                         (size_t)o->nb * o->fsz, (size_t)t->nb * t->fsz);
+      AFH_LAUNCH_CHECK("k_copy_boxes");
+    }
+    AFH_HIP(hipStreamSynchronize(t->stream));
+    hipFree(d_list);
+    d_list = nullptr;
+  }
+  // auto_prolong (m_af_core.f90:843-881): level by level, every automatic
+  // variable of the new boxes, then their ghost cells (corners included)
+  const int hn = nc / 2;
+  for (int l = 2; l <= t->nlvl; l++) {
+    std::vector<int32_t> add;
+    for (int32_t id : t->h_ids[l - 1])
+      if (!keep[id]) add.push_back(id);
+    if (add.empty()) continue;
+    if ((e = device_list(add, &d_list))) return e;
+    const unsigned n = (unsigned)add.size();
+    for (int iv : t->auto_vars) {
+      const CcMethod &m = t->meth[iv];
+      auto kern = m.prolong == AFH_PROLONG_LIMIT ? k_prolong_new<AFH_PROLONG_LIMIT>
+                                                 : k_prolong_new<AFH_PROLONG_LINEAR>;
+      hipLaunchKernelGGL(kern, dim3((hn * hn * hn + 255) / 256, n), dim3(256), 0,
+                         t->stream, t->ccv(iv), t->d_boxes, d_list, nc, t->bsz,
+                         m.prolong_lim);
+      AFH_LAUNCH_CHECK("k_prolong_new");
+    }
+    for (int iv : t->auto_vars) {
+      hipLaunchKernelGGL(k_gc_faces, dim3((nc * nc + 255) / 256, 6, n), dim3(256), 0,
+                         t->stream, t->ccv(iv), t->ccv(iv), t->d_boxes, d_list, nc,
+                         t->bsz, t->gc_args(iv));
+      AFH_LAUNCH_CHECK("k_gc_faces");
+      hipLaunchKernelGGL(k_gc_corners, dim3(n), dim3(256), 0, t->stream, t->ccv(iv),
+                         t->d_boxes, d_list, nc, t->bsz);
+      AFH_LAUNCH_CHECK("k_gc_corners");
+    }
+    AFH_HIP(hipStreamSynchronize(t->stream));
+    hipFree(d_list);
+    d_list = nullptr;
+  }
+  *out = t;
+  return AFH_OK;
+}
+
+}  // extern "C"
+

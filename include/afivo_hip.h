@@ -301,6 +301,24 @@ int32_t afh_fluid_forward_euler(afh_fluid *f, double dt, int32_t s_deriv,
                                 int32_t last_step, int32_t store_flux,
                                 double *dt_lim);
 
+/* Regrid (af_adjust_refinement's data movement, m_af_core.f90:697-881).
+ * afh_set_cc_prolong registers the prolongation of variable iv
+ * (tree%cc_methods(iv)%prolong / prolong_limiter, af_set_cc_methods
+ * m_af_core.f90:343-420: AFH_PROLONG_LINEAR = af_prolong_linear,
+ * AFH_PROLONG_LIMIT = af_prolong_limit with `limiter`, m_af_prolong.f90)
+ * and makes iv an automatic variable (tree%cc_auto_vars, registration
+ * order). afh_tree_regrid builds the tree of the new topology `desc` (as
+ * afivo left it after af_adjust_refinement: persisting boxes keep their ids)
+ * on the device: auto_restrict into boxes whose children were removed, the
+ * data of persisting boxes, then auto_prolong level by level (each new box
+ * prolonged from its parent, then its ghost cells, corners included). The
+ * old tree is left valid (destroy it when done). Single-rank trees. */
+#define AFH_PROLONG_NONE 0
+#define AFH_PROLONG_LINEAR 1
+#define AFH_PROLONG_LIMIT 2
+int32_t afh_set_cc_prolong(afh_tree *t, int32_t iv, int32_t method, int32_t limiter);
+int32_t afh_tree_regrid(afh_tree *old, const afh_tree_desc *desc, afh_tree **out);
+
 /* Kernel timing (replaces the reference's omp_get_wtime cost buckets,
  * src/m_streamer.f90:181-187): while enabled, every launch of the selected
  * kernel class is bracketed by HIP events on the tree's stream;

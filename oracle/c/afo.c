@@ -30,6 +30,7 @@ typedef struct {
   afh_bc bc[6];
   int rb;
   int lim;
+  int prolong, prolong_lim; /* afo_set_cc_prolong (0: not an auto variable) */
 } cc_method;
 
 struct afh_tree {
@@ -40,6 +41,7 @@ struct afh_tree {
   int cgs[3];
   double *cc, *fc;
   cc_method *meth; /* n_var_cell entries */
+  int n_auto, *auto_vars; /* tree%cc_auto_vars: prolonged / restricted on regrid */
   /* box sharding (afo_tree_set_hook, afo_plan_*) */
   afh_hook_fn hook;
   void *hook_ctx;
@@ -176,6 +178,7 @@ int32_t afo_tree_create(const afh_tree_desc *d, int32_t device,
   t->fc = calloc((size_t)(t->nvf > 0 ? t->nvf : 1) * t->nb * t->fsz,
                  sizeof(double));
   t->meth = calloc(t->nvc + 1, sizeof(cc_method));
+  t->auto_vars = calloc(t->nvc + 1, sizeof(int));
   if (!t->cc || !t->fc) return fail(AFH_ERR_ARG, "out of memory");
   *out = t;
   return AFH_OK;
@@ -186,7 +189,7 @@ int32_t afo_tree_destroy(afh_tree *t) {
   free(t->boxes);
   free(t->ids), free(t->ids_off), free(t->leaves), free(t->leaves_off);
   free(t->parents), free(t->parents_off);
-  free(t->cc), free(t->fc), free(t->meth);
+  free(t->cc), free(t->fc), free(t->meth), free(t->auto_vars);
   for (int q = 0; q < t->nplans; q++) free(t->plans[q].reg), free(t->plans[q].off);
   free(t->plans);
   free(t);
@@ -2098,3 +2101,168 @@ int32_t afo_plan_unpack(afh_tree *t, int32_t plan, int32_t iv,
                         const double *buf) {
   return plan_copy(t, plan, iv, (double *)buf, 1);
 }
+
+/* ------------------------------------------------------------ regrid */
+
+/* The prolongation of variable iv used when boxes are added
+ * (tree%cc_methods(iv)%prolong / prolong_limiter, af_set_cc_methods,
+ * m_af_core.f90:343-420); registering it makes iv an automatic variable
+ * (tree%cc_auto_vars, in registration order) that af_adjust_refinement
+ * restricts into derefined parents and prolongs into new boxes. */
+int32_t afo_set_cc_prolong(afh_tree *t, int32_t iv, int32_t method, int32_t lim) {
+  if (!t || iv < 1 || iv > t->nvc) return fail(AFH_ERR_ARG, "bad variable index");
+  if (method < AFH_PROLONG_NONE || method > AFH_PROLONG_LIMIT)
+    return fail(AFH_ERR_UNSUPPORTED, "prolongation method %d", method);
+  if (!t->meth[iv].set) return fail(AFH_ERR_STATE, "set cc methods first");
+  int known = 0;
+  for (int q = 0; q < t->n_auto; q++) known |= t->auto_vars[q] == iv;
+  if (!known && method != AFH_PROLONG_NONE) t->auto_vars[t->n_auto++] = iv;
+  t->meth[iv].prolong = method;
+  t->meth[iv].prolong_lim = lim;
+  return AFH_OK;
+}
+
+/* af_prolong_limit, m_af_prolong.f90:311-420 (3D, add = .false.: the child
+ * interior starts at 0 and each value is f0 +- f1 +- f2 +- f3 + 0) */
+static void prolong_limit(afh_tree *t, int p_id, int c_id, int iv, int lim) {
+  int nc = t->nc, hnc = nc / 2, off[3];
+  child_offset(t, c_id, 0, off);
+  const double *p = ccb(t, iv, p_id);
+  double *c = ccb(t, iv, c_id);
+  for (int k = 1; k <= nc; k++)
+    for (int j = 1; j <= nc; j++)
+      for (int i = 1; i <= nc; i++) c[IX(t, i, j, k)] = 0;
+  for (int k = 1; k <= hnc; k++)
+    for (int j = 1; j <= hnc; j++)
+      for (int i = 1; i <= hnc; i++) {
+        int ic = i + off[0], jc = j + off[1], kc = k + off[2];
+        int fi = 2 * i - 1, fj = 2 * j - 1, fk = 2 * k - 1;
+        double f0 = p[IX(t, ic, jc, kc)];
+        double a[3] = {f0 - p[IX(t, ic - 1, jc, kc)], f0 - p[IX(t, ic, jc - 1, kc)],
+                       f0 - p[IX(t, ic, jc, kc - 1)]};
+        double b[3] = {p[IX(t, ic + 1, jc, kc)] - f0, p[IX(t, ic, jc + 1, kc)] - f0,
+                       p[IX(t, ic, jc, kc + 1)] - f0};
+        double f[3];
+        for (int d = 0; d < 3; d++) f[d] = 0.25 * limiter(lim, a[d], b[d]);
+        for (int q = 0; q < 8; q++) {
+          double sx = (q & 1) ? f[0] : -f[0];
+          size_t x = IX(t, fi + (q & 1), fj + ((q >> 1) & 1), fk + (q >> 2));
+          double v = f0 + sx;
+          v = ((q >> 1) & 1) ? v + f[1] : v - f[1];
+          v = (q >> 2) ? v + f[2] : v - f[2];
+          c[x] = v + c[x];
+        }
+      }
+}
+
+/* af_prolong_linear, m_af_prolong.f90:531-679 (3D, add = .false.) */
+static void prolong_linear(afh_tree *t, int p_id, int c_id, int iv) {
+  const double f1 = 1 / 64.0, f3 = 3 / 64.0, f9 = 9 / 64.0, f27 = 27 / 64.0;
+  int nc = t->nc, hnc = nc / 2, off[3];
+  child_offset(t, c_id, 0, off);
+  const double *p = ccb(t, iv, p_id);
+  double *c = ccb(t, iv, c_id);
+  for (int k = 1; k <= nc; k++)
+    for (int j = 1; j <= nc; j++)
+      for (int i = 1; i <= nc; i++) c[IX(t, i, j, k)] = 0;
+#define P(a, b, d) p[IX(t, ic + (a), jc + (b), kc + (d))]
+  for (int k = 1; k <= hnc; k++)
+    for (int j = 1; j <= hnc; j++)
+      for (int i = 1; i <= hnc; i++) {
+        int ic = i + off[0], jc = j + off[1], kc = k + off[2];
+        int fi = 2 * i - 1, fj = 2 * j - 1, fk = 2 * k - 1;
+        double f000 = f27 * P(0, 0, 0);
+        double f00l = f9 * P(0, 0, -1), f0l0 = f9 * P(0, -1, 0), f0ll = f3 * P(0, -1, -1);
+        double fl00 = f9 * P(-1, 0, 0), fl0l = f3 * P(-1, 0, -1), fll0 = f3 * P(-1, -1, 0);
+        double flll = f1 * P(-1, -1, -1);
+        double f00h = f9 * P(0, 0, 1), f0h0 = f9 * P(0, 1, 0), f0hh = f3 * P(0, 1, 1);
+        double fh00 = f9 * P(1, 0, 0), fh0h = f3 * P(1, 0, 1), fhh0 = f3 * P(1, 1, 0);
+        double fhhh = f1 * P(1, 1, 1);
+        double fl0h = f3 * P(-1, 0, 1), fh0l = f3 * P(1, 0, -1), flh0 = f3 * P(-1, 1, 0);
+        double fhl0 = f3 * P(1, -1, 0), f0lh = f3 * P(0, -1, 1), f0hl = f3 * P(0, 1, -1);
+        double fllh = f1 * P(-1, -1, 1), flhl = f1 * P(-1, 1, -1), fhll = f1 * P(1, -1, -1);
+        double fhhl = f1 * P(1, 1, -1), fhlh = f1 * P(1, -1, 1), flhh = f1 * P(-1, 1, 1);
+        double *o;
+#define W(di, dj, dk, expr) o = &c[IX(t, fi + di, fj + dj, fk + dk)]; *o = expr + *o;
+        W(0, 0, 0, f000 + fl00 + f0l0 + f00l + fll0 + fl0l + f0ll + flll)
+        W(1, 0, 0, f000 + fh00 + f0l0 + f00l + fhl0 + fh0l + f0ll + fhll)
+        W(0, 1, 0, f000 + fl00 + f0h0 + f00l + flh0 + fl0l + f0hl + flhl)
+        W(1, 1, 0, f000 + fh00 + f0h0 + f00l + fhh0 + fh0l + f0hl + fhhl)
+        W(0, 0, 1, f000 + fl00 + f0l0 + f00h + fll0 + fl0h + f0lh + fllh)
+        W(1, 0, 1, f000 + fh00 + f0l0 + f00h + fhl0 + fh0h + f0lh + fhlh)
+        W(0, 1, 1, f000 + fl00 + f0h0 + f00h + flh0 + fl0h + f0hh + flhh)
+        W(1, 1, 1, f000 + fh00 + f0h0 + f00h + fhh0 + fh0h + f0hh + fhhh)
+#undef W
+      }
+#undef P
+}
+
+/* af_adjust_refinement's data movement (m_af_core.f90:697-822) given the new
+ * topology in `d` (box ids as afivo keeps them: a box of the old tree that
+ * is in the new level lists with the same level and index persists):
+ * auto_restrict (826-840) of every automatic variable into boxes whose
+ * children were removed, the old data of persisting boxes, then
+ * auto_prolong (843-881): level by level, each new box's automatic
+ * variables prolonged from its parent and their ghost cells filled
+ * (af_gc_box with corners). Variables without a prolongation method start at
+ * 0 in new boxes. Returns the new tree (the old one is left as it was, apart
+ * from the restricted parents). */
+int32_t afo_tree_regrid(afh_tree *o, const afh_tree_desc *d, afh_tree **out) {
+  if (!o || !d || !out) return fail(AFH_ERR_ARG, "afo_tree_regrid: null");
+  if (d->n_cell != o->nc || d->n_var_cell != o->nvc || d->n_var_face != o->nvf)
+    return fail(AFH_ERR_ARG, "afo_tree_regrid: box size / variables differ");
+  afh_tree *t;
+  int32_t e;
+  if ((e = afo_tree_create(d, -1, &t))) return e;
+  memcpy(t->meth, o->meth, sizeof(cc_method) * (o->nvc + 1));
+  t->n_auto = o->n_auto;
+  memcpy(t->auto_vars, o->auto_vars, sizeof(int) * (o->nvc + 1));
+  t->hook = o->hook, t->hook_ctx = o->hook_ctx;
+  char *in_old = calloc(o->nb + 1, 1), *keep = calloc(t->nb + 1, 1);
+  for (int q = 0; q < o->ids_off[o->nlvl]; q++) in_old[o->ids[q]] = 1;
+  for (int q = 0; q < t->ids_off[t->nlvl]; q++) {
+    int id = t->ids[q];
+    if (id <= o->nb && in_old[id] && B(o, id)->lvl == B(t, id)->lvl &&
+        B(o, id)->ix[0] == B(t, id)->ix[0] && B(o, id)->ix[1] == B(t, id)->ix[1] &&
+        B(o, id)->ix[2] == B(t, id)->ix[2])
+      keep[id] = 1;
+  }
+  /* auto_restrict: persisting boxes that lost their children */
+  for (int id = 1; id <= t->nb; id++) {
+    if (!keep[id] || B(o, id)->children[0] <= 0 || B(t, id)->children[0] != 0) continue;
+    for (int c = 0; c < 8; c++)
+      for (int q = 0; q < o->n_auto; q++)
+        restrict_box(o, B(o, id)->children[c], id, o->auto_vars[q]);
+  }
+  for (int id = 1; id <= t->nb; id++) {
+    if (!keep[id]) continue;
+    for (int iv = 1; iv <= t->nvc; iv++)
+      memcpy(ccb(t, iv, id), ccb(o, iv, id), sizeof(double) * t->bsz);
+    for (int iv = 1; iv <= t->nvf; iv++)
+      memcpy(fcb(t, iv, id), fcb(o, iv, id), sizeof(double) * t->fsz);
+  }
+  /* auto_prolong */
+  for (int l = 2; l <= t->nlvl; l++) {
+    int n = LVL_N(t, ids, l);
+    for (int q = 0; q < n; q++) {
+      int id = LVL_AT(t, ids, l, q);
+      if (keep[id]) continue;
+      for (int a = 0; a < t->n_auto; a++) {
+        int iv = t->auto_vars[a];
+        if (t->meth[iv].prolong == AFH_PROLONG_LIMIT)
+          prolong_limit(t, B(t, id)->parent, id, iv, t->meth[iv].prolong_lim);
+        else
+          prolong_linear(t, B(t, id)->parent, id, iv);
+      }
+    }
+    for (int q = 0; q < n; q++) {
+      int id = LVL_AT(t, ids, l, q);
+      if (keep[id]) continue;
+      for (int a = 0; a < t->n_auto; a++) gc_box(t, id, t->auto_vars[a], 1);
+    }
+  }
+  free(in_old), free(keep);
+  *out = t;
+  return AFH_OK;
+}
+

@@ -52,6 +52,8 @@ int32_t afo_mg_set_box_stencil(afh_mg *mg, int32_t id, const double *v,
                                const double *bc_correction);
 int32_t afo_mg_set_box_lsf(afh_mg *mg, int32_t id, int32_t n, const int32_t *ix,
                            const double *dd, const double *bval, int32_t i_lsf);
+int32_t afo_set_cc_prolong(afh_tree *t, int32_t iv, int32_t method, int32_t limiter);
+int32_t afo_tree_regrid(afh_tree *old, const afh_tree_desc *desc, afh_tree **out);
 int32_t afo_fluid_create(afh_tree *t, const afh_fluid_desc *desc,
                          afh_fluid **out);
 int32_t afo_fluid_destroy(afh_fluid *f);

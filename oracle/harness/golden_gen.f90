@@ -25,8 +25,14 @@
 !> and the field solve (V-cycles, FMG, gradient with mg_box_lpllsf_gradient)
 !> runs through them.
 !>
+!> Case regrid8 runs af_adjust_refinement (m_af_core.f90:697-822) once on
+!> an AMR tree whose densities are prolonged with af_prolong_limit (the
+!> streamer's default, m_streamer.f90:395-410): boxes near a moving point
+!> are refined, boxes far from it derefined; the topology and every variable
+!> are dumped before and after (auto_restrict / auto_prolong / af_gc_box).
+!>
 !> Usage: golden_gen <case> <td_file> <out_dir>
-!>   case = uni4 | amr4 | uni8 | rod8
+!>   case = uni4 | amr4 | uni8 | rod8 | regrid8
 program golden_gen
 #include "cpp_macros.h"
   use m_af_types
@@ -35,6 +41,7 @@ program golden_gen
   use m_af_ghostcell
   use m_af_stencil
   use m_af_restrict
+  use m_af_prolong, only: af_prolong_limit
   use m_af_multigrid
   use m_af_flux_schemes
   use m_af_limiters
@@ -53,8 +60,9 @@ program golden_gen
   ! photoionization Helmholtz mode: Bourdon's second lambda at 1 bar
   ! (src/m_photoi_helmh.f90:100), 1/m
   real(dp), parameter :: helm_lambda = 44081.25_dp
-  logical            :: trace, use_lsf
+  logical            :: trace, use_lsf, do_regrid
   integer            :: u_log, i_lsf
+  type(ref_info_t)   :: regrid_info
   ! rod electrode (field_rod_r0/r1/radius as fractions of the domain)
   real(dp)           :: rod_r0(3), rod_r1(3), rod_radius
 
@@ -63,7 +71,11 @@ program golden_gen
   call get_command_argument(3, out_dir)
 
   use_lsf = .false.
+  do_regrid = .false.
   select case (trim(case_name))
+  case ("regrid8")
+     nc = 8; grid = [8, 8, 8]; max_lvl = 2; amr_lvl = 3; trace = .false.
+     do_regrid = .true.
   case ("rod8")
      nc = 8; grid = [8, 8, 8]; max_lvl = 2; amr_lvl = 3; trace = .false.
      use_lsf = .true.
@@ -111,9 +123,19 @@ program golden_gen
 
   ! Ghost-cell methods as set by streamer.f90:81-84 and m_field.f90:349-350;
   ! phi gets (sides_bc, mg_auto_rb) as in mg_init (m_af_multigrid.f90:102-105)
-  call af_set_cc_methods(tree, i_e, af_bc_neumann_zero, af_gc_interp_lim)
-  call af_set_cc_methods(tree, i_pos, af_bc_neumann_zero, af_gc_interp_lim)
-  call af_set_cc_methods(tree, i_neg, af_bc_neumann_zero, af_gc_interp_lim)
+  if (do_regrid) then
+     ! streamer.f90:81-84 with prolong_density = limit (the default)
+     call af_set_cc_methods(tree, i_e, af_bc_neumann_zero, af_gc_interp_lim, &
+          af_prolong_limit)
+     call af_set_cc_methods(tree, i_pos, af_bc_neumann_zero, af_gc_interp_lim, &
+          af_prolong_limit)
+     call af_set_cc_methods(tree, i_neg, af_bc_neumann_zero, af_gc_interp_lim, &
+          af_prolong_limit)
+  else
+     call af_set_cc_methods(tree, i_e, af_bc_neumann_zero, af_gc_interp_lim)
+     call af_set_cc_methods(tree, i_pos, af_bc_neumann_zero, af_gc_interp_lim)
+     call af_set_cc_methods(tree, i_neg, af_bc_neumann_zero, af_gc_interp_lim)
+  end if
   call af_set_cc_methods(tree, i_efld, af_bc_neumann_zero, af_gc_interp)
   call af_set_cc_methods(tree, i_phi, hx_bc_phi, hx_rb_phi)
 
@@ -155,10 +177,21 @@ program golden_gen
 
   n_dump = 0
   open(newunit=u_log, file=trim(out_dir)//"/log.txt", status="replace")
-  call dump_topology()
+  call dump_topology("topology.bin")
   call dump_tables()
   call dump_state("init")
   if (use_lsf) call dump_lsf()
+
+  if (do_regrid) then
+     call af_gc_tree(tree, [i_efld])
+     call dump_state("regrid_in")
+     call af_adjust_refinement(tree, ref_regrid, regrid_info)
+     call dump_topology("topology_after.bin")
+     call dump_in_use("in_use_after.bin")
+     call dump_state("regrid")
+     close(u_log)
+     stop
+  end if
 
   ! ------------------------------------------------------------------
   ! field_compute(tree, mg, 0, time, .true.), m_field.f90:405-485
@@ -363,6 +396,40 @@ contains
        cell_flags = af_keep_ref
     end if
   end subroutine ref_amr
+
+  !> Regrid rule: refine (up to level 4) where cells are near r1, remove
+  !> refinement where all cells are far from it
+  subroutine ref_regrid(box, cell_flags)
+    type(box_t), intent(in) :: box
+    integer, intent(out)    :: cell_flags(DTIMES(box%n_cell))
+    integer                 :: IJK
+    real(dp)                :: r1(3), d
+    r1 = r0 + [0.35_dp, 0.0_dp, 0.0_dp] * dom
+    do k = 1, box%n_cell
+       do j = 1, box%n_cell
+          do i = 1, box%n_cell
+             d = norm2(af_r_cc(box, [IJK]) - r1)
+             if (d < 1.0_dp * width .and. box%lvl < 4) then
+                cell_flags(IJK) = af_do_ref
+             else if (d > 1.6_dp * width) then
+                cell_flags(IJK) = af_rm_ref
+             else
+                cell_flags(IJK) = af_keep_ref
+             end if
+          end do
+       end do
+    end do
+  end subroutine ref_regrid
+
+  subroutine dump_in_use(fname)
+    character(len=*), intent(in) :: fname
+    integer :: u, id
+    open(newunit=u, file=trim(out_dir)//"/"//fname, &
+         access="stream", form="unformatted", status="replace")
+    write(u) tree%highest_id
+    write(u) [(merge(1, 0, tree%boxes(id)%in_use), id = 1, tree%highest_id)]
+    close(u)
+  end subroutine dump_in_use
 
   subroutine refine_amr()
     type(ref_info_t) :: ref_info
@@ -623,9 +690,10 @@ contains
     write(u_log, *) "state ", name
   end subroutine dump_state
 
-  subroutine dump_topology()
+  subroutine dump_topology(fname)
+    character(len=*), intent(in) :: fname
     integer :: u, id, lvl
-    open(newunit=u, file=trim(out_dir)//"/topology.bin", &
+    open(newunit=u, file=trim(out_dir)//"/"//fname, &
          access="stream", form="unformatted", status="replace")
     write(u) tree%n_cell, tree%highest_id, tree%highest_lvl, &
          tree%n_var_cell, tree%n_var_face

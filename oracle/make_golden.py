@@ -70,11 +70,18 @@ ROD = [
     ("fmg0", ["rhs", "phi", "tmp"], []),
     ("fmg1", ["rhs", "phi", "tmp"], []),
 ]
+# one af_adjust_refinement (refine near a point, derefine far from it) on an
+# AMR tree; "after_" keys hold the new topology (boxes not in use: lvl 0)
+REGRID = [
+    ("regrid_in", ["e0", "pos0", "neg0", "phi", "efld"], []),
+]
+REGRID_AFTER = ("regrid", ["e0", "pos0", "neg0", "phi", "efld"])
 CASES = {
     "uni4": {"chain": CHAIN + FMG + HELM, "trace": True},
     "uni8": {"chain": CHAIN + FMG + HELM, "trace": False},
     "amr4": {"chain": CHAIN[:7] + FMG + HELM, "trace": False},
     "rod8": {"chain": ROD, "trace": False, "lsf": True},
+    "regrid8": {"chain": REGRID, "trace": False, "regrid": True},
 }
 
 
@@ -213,6 +220,18 @@ def pack(case, raw_dir):
     out["helm_lambda"] = np.array(HELM_LAMBDA)
     if spec.get("lsf"):
         out.update(read_lsf(os.path.join(raw_dir, "lsf.bin"), topo))
+    if spec.get("regrid"):
+        after = read_topology(os.path.join(raw_dir, "topology_after.bin"))
+        in_use = np.fromfile(os.path.join(raw_dir, "in_use_after.bin"), np.int32)[1:]
+        for k in ("meta_lvl", "meta_parent", "meta_children", "meta_neighbors",
+                  "meta_neighbor_mat"):
+            after[k][in_use == 0] = 0
+        for k, v in after.items():
+            out["after_" + k] = v
+        name, ccv = REGRID_AFTER
+        cc, _ = read_state(os.path.join(raw_dir, "state_%s.bin" % name), after)
+        for v in ccv:
+            out["%s__%s" % (name, v)] = cc[:, CC[v] - 1].copy()
     for name, ccv, fcv in spec["chain"]:
         cc, fc = read_state(os.path.join(raw_dir, "state_%s.bin" % name), topo)
         for v in ccv:
