@@ -91,6 +91,26 @@ class MgDesc(C.Structure):
                 ("coarse_cycles", i32)]
 
 
+MAX_REFINE_REGIONS = 8
+RM_REF, KEEP_REF, DO_REF = -1, 0, 1
+_R = MAX_REFINE_REGIONS
+
+
+class RefineDesc(C.Structure):
+    """afh_refine_desc: default_refinement's parameters (src/m_refine.f90)."""
+    _fields_ = [("i_electron", i32), ("i_efld", i32), ("td_alpha_col", i32),
+                ("td_eta_col", i32), ("use_alpha_effective", i32),
+                ("buffer_width", i32), ("adx_fac", f64), ("adx", f64),
+                ("min_dens", f64), ("derefine_dx", f64), ("max_dx", f64),
+                ("min_dx", f64), ("electrode_dx", f64), ("n_seeds", i32),
+                ("init_fac", f64), ("seed_r0", (f64 * 3) * _R),
+                ("seed_r1", (f64 * 3) * _R), ("seed_width", f64 * _R),
+                ("n_regions", i32), ("region_dr", f64 * _R),
+                ("region_rmin", (f64 * 3) * _R), ("region_rmax", (f64 * 3) * _R),
+                ("n_limits", i32), ("limit_dr", f64 * _R),
+                ("limit_rmin", (f64 * 3) * _R), ("limit_rmax", (f64 * 3) * _R)]
+
+
 assert C.sizeof(BoxMeta) == BOX_META_DTYPE.itemsize, (C.sizeof(BoxMeta),
                                                       BOX_META_DTYPE.itemsize)
 
@@ -101,6 +121,9 @@ SIGNATURES = {
     "last_error": (C.c_char_p, []),
     "tree_create": (i32, [C.POINTER(TreeDesc), i32, _PVP]),
     "set_cc_prolong": (i32, [_VP, i32, i32, i32]),
+    "refine_cell_flags": (i32, [i32, C.c_uint32, i32, i32, P_i32]),
+    "refine_flags": (i32, [_VP, C.POINTER(RefineDesc), C.POINTER(C.c_uint8),
+                           P_i32, C.POINTER(C.c_uint32)]),
     "tree_regrid": (i32, [_VP, C.POINTER(TreeDesc), _PVP]),
     "tree_destroy": (i32, [_VP]),
     "tree_sync": (i32, [_VP]),

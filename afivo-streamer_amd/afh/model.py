@@ -312,6 +312,19 @@ class Fluid:
                       s_out, int(last_step), out)
         return out[0], out[1]
 
+    def refine_flags(self, desc, electrode_box=None):
+        """default_refinement reduced per box (afh_refine_flags): (flags,
+        masks) arrays over the tree's boxes."""
+        nb = self.tree.n_boxes
+        flags = np.zeros(nb, np.int32)
+        masks = np.zeros(nb, np.uint32)
+        eb = None if electrode_box is None else np.ascontiguousarray(electrode_box, np.uint8)
+        self.lib.call("refine_flags", self.h, C.byref(desc),
+                      None if eb is None else eb.ctypes.data_as(C.POINTER(C.c_uint8)),
+                      flags.ctypes.data_as(capi.P_i32),
+                      masks.ctypes.data_as(C.POINTER(C.c_uint32)))
+        return flags, masks
+
     def forward_euler(self, dt, s_deriv, s_prev, w_prev, s_out, last_step,
                       store_flux=False):
         """flux_upwind_tree + flux_update_densities (forward_euler,

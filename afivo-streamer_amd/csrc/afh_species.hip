@@ -1324,6 +1324,133 @@ __global__ void __launch_bounds__(256, AFH_FE_MINW)
   }
 }
 
+
+// ------------------------------------------------------------ refinement
+// default_refinement (src/m_refine.f90:198-298, constant gas density) per
+// cell, reduced per box as cell_to_ref_flags (m_af_core.f90:1095-1148):
+// one workgroup per box; the box-level rules are applied per cell in the
+// reference's order. Same expressions as oracle/c/afo.c refine_cell.
+struct RefineArgs {
+  afh_refine_desc d;
+  DevLT td;
+  double N;
+  const double *ne, *E;
+  const uint8_t *elec;  // per box, or null
+};
+
+__device__ __forceinline__ double dist_line(const double r[3], const double *r0,
+                                            const double *r1) {
+  double len2 = 0, frac = 0, dv[3];
+#pragma unroll
+  for (int d = 0; d < 3; d++) len2 = len2 + (r1[d] - r0[d]) * (r1[d] - r0[d]);
+#pragma unroll
+  for (int d = 0; d < 3; d++) frac = frac + (r[d] - r0[d]) * (r1[d] - r0[d]);
+  if (frac <= 0.0) {
+#pragma unroll
+    for (int d = 0; d < 3; d++) dv[d] = r[d] - r0[d];
+  } else if (frac >= len2) {
+#pragma unroll
+    for (int d = 0; d < 3; d++) dv[d] = r[d] - r1[d];
+  } else {
+#pragma unroll
+    for (int d = 0; d < 3; d++) dv[d] = r[d] - (r0[d] + frac / len2 * (r1[d] - r0[d]));
+  }
+  return sqrt(dv[0] * dv[0] + dv[1] * dv[1] + dv[2] * dv[2]);
+}
+
+__global__ void __launch_bounds__(256)
+    k_refine_flags(RefineArgs A, const afh_box_meta *__restrict__ meta,
+                   const int32_t *__restrict__ ids, int nc, size_t bsz,
+                   int32_t *__restrict__ flags, uint32_t *__restrict__ masks) {
+  const afh_refine_desc &p = A.d;
+  const int id = ids[blockIdx.x];
+  const afh_box_meta &b = meta[id - 1];
+  __shared__ int s_do, s_keep;
+  __shared__ unsigned s_mask;
+  if (threadIdx.x == 0) s_do = 0, s_keep = 0, s_mask = 0;
+  __syncthreads();
+  double min_dx = b.dr[0], max_dx = b.dr[0];
+  for (int d = 1; d < 3; d++) {
+    if (b.dr[d] < min_dx) min_dx = b.dr[d];
+    if (b.dr[d] > max_dx) max_dx = b.dr[d];
+  }
+  const int elec = A.elec ? A.elec[id - 1] : 0;
+  const int bw = p.buffer_width, n3 = nc * nc * nc;
+  double rmin[3], rmax[3];
+  for (int d = 0; d < 3; d++) rmin[d] = b.r_min[d], rmax[d] = b.r_min[d] + b.dr[d] * nc;
+  int any_do = 0, any_keep = 0;
+  unsigned m = 0;
+  for (int t = threadIdx.x; t < n3; t += blockDim.x) {
+    int i, j, k;
+    cell3(t, nc, i, j, k);
+    const size_t x = (size_t)(id - 1) * bsz + ix3(nc + 2, i, j, k);
+    const double gas_dens = A.N;
+    const double fld = A.E[x] * 1e21 / gas_dens;
+    double alpha;
+    if (p.use_alpha_effective) {
+      alpha = (lt_col(A.td, p.td_alpha_col, p.adx_fac * fld) -
+               lt_col(A.td, p.td_eta_col, p.adx_fac * fld)) *
+              gas_dens / p.adx_fac;
+      alpha = alpha > 0.0 ? alpha : 0.0;
+    } else {
+      alpha = lt_col(A.td, p.td_alpha_col, p.adx_fac * fld) * gas_dens / p.adx_fac;
+    }
+    const double adx = max_dx * alpha, ne = A.ne[x];
+    int f;
+    if (adx > p.adx && ne > p.min_dens) f = AFH_DO_REF;
+    else if (adx < 0.125 * p.adx && max_dx < p.derefine_dx) f = AFH_RM_REF;
+    else f = AFH_KEEP_REF;
+    const double r[3] = {b.r_min[0] + (i - 0.5) * b.dr[0], b.r_min[1] + (j - 0.5) * b.dr[1],
+                         b.r_min[2] + (k - 0.5) * b.dr[2]};
+    for (int n = 0; n < p.n_seeds; n++) {
+      const double dist = dist_line(r, p.seed_r0[n], p.seed_r1[n]);
+      if (dist - p.seed_width[n] < 2 * max_dx && max_dx > p.init_fac * p.seed_width[n])
+        f = AFH_DO_REF;
+    }
+    if (elec && max_dx > p.electrode_dx) f = AFH_DO_REF;
+    for (int n = 0; n < p.n_regions; n++) {
+      bool in = max_dx > p.region_dr[n];
+      for (int d = 0; d < 3; d++)
+        in = in && rmax[d] >= p.region_rmin[n][d] && rmin[d] <= p.region_rmax[n][d];
+      if (in && i == nc / 2 && j == nc / 2 && k == nc / 2) f = AFH_DO_REF;
+    }
+    for (int n = 0; n < p.n_limits; n++) {
+      bool in = max_dx < 2 * p.limit_dr[n];
+      for (int d = 0; d < 3; d++)
+        in = in && rmin[d] >= p.limit_rmin[n][d] && rmax[d] <= p.limit_rmax[n][d];
+      if (in && f == AFH_DO_REF) f = AFH_KEEP_REF;
+    }
+    if (max_dx > p.max_dx) f = AFH_DO_REF;
+    else if (min_dx < 2 * p.min_dx && f == AFH_DO_REF) f = AFH_KEEP_REF;
+    if (f == AFH_DO_REF) {
+      any_do = 1;
+      if (bw > 0) {
+        const bool lo[3] = {i <= bw, j <= bw, k <= bw};
+        const bool hi[3] = {i > nc - bw, j > nc - bw, k > nc - bw};
+        for (int dk = -1; dk <= 1; dk++)
+          for (int dj = -1; dj <= 1; dj++)
+            for (int di = -1; di <= 1; di++) {
+              if (!di && !dj && !dk) continue;
+              const int dd[3] = {di, dj, dk};
+              bool in = true;
+              for (int d = 0; d < 3; d++)
+                in = in && (dd[d] == 0 || (dd[d] < 0 ? lo[d] : hi[d]));
+              if (in) m |= 1u << ((dk + 1) * 9 + (dj + 1) * 3 + (di + 1));
+            }
+      }
+    } else if (f == AFH_KEEP_REF) {
+      any_keep = 1;
+    }
+  }
+  if (any_do) atomicOr(&s_do, 1);
+  if (any_keep) atomicOr(&s_keep, 1);
+  if (m) atomicOr(&s_mask, m);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    flags[id - 1] = s_do ? AFH_DO_REF : s_keep ? AFH_KEEP_REF : AFH_RM_REF;
+    masks[id - 1] = s_mask;
+  }
+}
 }  // namespace afh
 
 using namespace afh;
@@ -1804,3 +1931,52 @@ int32_t afh_fluid_forward_euler(afh_fluid *f, double dt, int32_t s_deriv,
 }
 
 }  // extern "C"
+
+extern "C" {
+
+int32_t afh_refine_flags(afh_fluid *f, const afh_refine_desc *d,
+                         const uint8_t *electrode_box, int32_t *flags,
+                         uint32_t *masks) {
+  if (!f || !d || !flags || !masks) return set_error(AFH_ERR_ARG, "afh_refine_flags: null");
+  afh_tree *t = f->t;
+  if (d->n_seeds > AFH_MAX_REFINE_REGIONS || d->n_regions > AFH_MAX_REFINE_REGIONS ||
+      d->n_limits > AFH_MAX_REFINE_REGIONS || d->buffer_width < 0 ||
+      d->buffer_width > t->nc || d->i_electron < 1 || d->i_electron > t->nvc ||
+      d->i_efld < 1 || d->i_efld > t->nvc || d->td_alpha_col < 1 ||
+      d->td_alpha_col > f->td.n_cols || d->td_eta_col < 1 || d->td_eta_col > f->td.n_cols)
+    return set_error(AFH_ERR_ARG, "afh_refine_flags: bad descriptor");
+  const int nb = t->nb, nids = t->ids.off[t->nlvl];
+  int32_t *d_flags = nullptr;
+  uint32_t *d_masks = nullptr;
+  uint8_t *d_elec = nullptr;
+  AFH_HIP(hipMalloc(&d_flags, sizeof(int32_t) * nb));
+  AFH_HIP(hipMalloc(&d_masks, sizeof(uint32_t) * nb));
+  AFH_HIP(hipMemsetAsync(d_flags, 0, sizeof(int32_t) * nb, t->stream));
+  AFH_HIP(hipMemsetAsync(d_masks, 0, sizeof(uint32_t) * nb, t->stream));
+  if (electrode_box) {
+    AFH_HIP(hipMalloc(&d_elec, nb));
+    AFH_HIP(hipMemcpyAsync(d_elec, electrode_box, nb, hipMemcpyHostToDevice, t->stream));
+  }
+  RefineArgs A;
+  A.d = *d;
+  A.td = f->td;
+  A.N = f->d.gas_number_density;
+  A.ne = t->ccv(d->i_electron);
+  A.E = t->ccv(d->i_efld);
+  A.elec = d_elec;
+  if (nids > 0) {
+    hipLaunchKernelGGL(k_refine_flags, dim3(nids), dim3(256), 0, t->stream, A,
+                       t->d_boxes, t->ids.d, t->nc, t->bsz, d_flags, d_masks);
+    AFH_LAUNCH_CHECK("k_refine_flags");
+  }
+  AFH_HIP(hipMemcpyAsync(flags, d_flags, sizeof(int32_t) * nb, hipMemcpyDeviceToHost,
+                         t->stream));
+  AFH_HIP(hipMemcpyAsync(masks, d_masks, sizeof(uint32_t) * nb, hipMemcpyDeviceToHost,
+                         t->stream));
+  AFH_HIP(hipStreamSynchronize(t->stream));
+  hipFree(d_flags), hipFree(d_masks), hipFree(d_elec);
+  return AFH_OK;
+}
+
+}  // extern "C"
+

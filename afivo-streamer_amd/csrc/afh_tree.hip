@@ -970,3 +970,55 @@ int32_t afh_tree_regrid(afh_tree *o, const afh_tree_desc *d, afh_tree **out) {
 
 }  // extern "C"
 
+extern "C" {
+
+/* Cell flags with the box summary (flag, mask) of afh_refine_flags, for the
+ * driver's refinement routine (af_subr_ref) in af_adjust_refinement: a set
+ * of cells asking for refinement whose cell_to_ref_flags result
+ * (m_af_core.f90:1095-1148) is exactly (flag, mask); the other cells keep
+ * (flag >= keep) or remove (flag = remove) the refinement. Per dimension a
+ * cell index is in the low buffer slab, the high one, both or neither; one
+ * representative cell per class combination whose neighbour slabs all lie in
+ * the mask is marked when it adds a direction (or, for a box refining only
+ * away from its sides, a cell in no slab). */
+int32_t afh_refine_cell_flags(int32_t flag, uint32_t mask, int32_t nc, int32_t bw,
+                               int32_t *cf) {
+  if (nc < 1 || bw < 0 || bw > nc || !cf || flag < AFH_RM_REF || flag > AFH_DO_REF)
+    return set_error(AFH_ERR_ARG, "refine_cell_flags: bad argument");
+  const size_t n3 = (size_t)nc * nc * nc;
+  for (size_t q = 0; q < n3; q++) cf[q] = flag == AFH_RM_REF ? AFH_RM_REF : AFH_KEEP_REF;
+  if (flag != AFH_DO_REF) return mask ? set_error(AFH_ERR_ARG, "mask without refinement") : AFH_OK;
+  int rep[4]; /* class -> first index (1-based) or 0; class = lo | hi << 1 */
+  for (int c = 0; c < 4; c++) rep[c] = 0;
+  for (int i = nc; i >= 1; i--) rep[(i <= bw) | ((i > nc - bw) << 1)] = i;
+  uint32_t need = mask;
+  int placed = 0;
+  for (int pass = 0; pass < 2; pass++)
+    for (int cz = 0; cz < 4; cz++)
+      for (int cy = 0; cy < 4; cy++)
+        for (int cx = 0; cx < 4; cx++) {
+          if (!rep[cx] || !rep[cy] || !rep[cz]) continue;
+          const int cl[3] = {cx, cy, cz};
+          uint32_t mem = 0;
+          for (int dk = -1; dk <= 1; dk++)
+            for (int dj = -1; dj <= 1; dj++)
+              for (int di = -1; di <= 1; di++) {
+                if (!di && !dj && !dk) continue;
+                const int dd[3] = {di, dj, dk};
+                int in = 1;
+                for (int d = 0; d < 3; d++)
+                  in = in && (dd[d] == 0 || (cl[d] & (dd[d] < 0 ? 1 : 2)));
+                if (in) mem |= 1u << ((dk + 1) * 9 + (dj + 1) * 3 + (di + 1));
+              }
+          if ((mem & ~mask) != 0) continue;
+          /* pass 0: cells that add a direction; pass 1: any cell if none yet */
+          if (pass == 0 ? (mem & need) == 0 : placed) continue;
+          cf[((size_t)(rep[cz] - 1) * nc + (rep[cy] - 1)) * nc + (rep[cx] - 1)] = AFH_DO_REF;
+          need &= ~mem;
+          placed = 1;
+        }
+  if (need || !placed) return set_error(AFH_ERR_ARG, "refine_cell_flags: inconsistent mask");
+  return AFH_OK;
+}
+
+}  // extern "C"

@@ -118,6 +118,37 @@ module m_afivo_hip
      integer(c_int32_t) :: mult_out(4)
   end type afh_reaction
 
+  ! regrid (afh_set_cc_prolong / afh_tree_regrid / afh_refine_flags)
+  integer(c_int32_t), parameter :: AFH_PROLONG_NONE = 0, AFH_PROLONG_LINEAR = 1
+  integer(c_int32_t), parameter :: AFH_PROLONG_LIMIT = 2
+  integer(c_int32_t), parameter :: AFH_RM_REF = -1, AFH_KEEP_REF = 0, AFH_DO_REF = 1
+  integer, parameter :: AFH_MAX_REFINE_REGIONS = 8
+
+  !> default_refinement's parameters (src/m_refine.f90:10-60)
+  type, bind(C) :: afh_refine_desc
+     integer(c_int32_t) :: i_electron = 0, i_efld = 0
+     integer(c_int32_t) :: td_alpha_col = 3, td_eta_col = 4
+     integer(c_int32_t) :: use_alpha_effective = 0
+     integer(c_int32_t) :: buffer_width = 4
+     real(c_double)     :: adx_fac = 1, adx = 1, min_dens = -1e99_c_double
+     real(c_double)     :: derefine_dx = 1e-4_c_double, max_dx = 1e-3_c_double
+     real(c_double)     :: min_dx = 1e-7_c_double
+     real(c_double)     :: electrode_dx = 1e99_c_double
+     integer(c_int32_t) :: n_seeds = 0
+     real(c_double)     :: init_fac = 0.25_c_double
+     real(c_double)     :: seed_r0(3, AFH_MAX_REFINE_REGIONS) = 0
+     real(c_double)     :: seed_r1(3, AFH_MAX_REFINE_REGIONS) = 0
+     real(c_double)     :: seed_width(AFH_MAX_REFINE_REGIONS) = 0
+     integer(c_int32_t) :: n_regions = 0
+     real(c_double)     :: region_dr(AFH_MAX_REFINE_REGIONS) = 0
+     real(c_double)     :: region_rmin(3, AFH_MAX_REFINE_REGIONS) = 0
+     real(c_double)     :: region_rmax(3, AFH_MAX_REFINE_REGIONS) = 0
+     integer(c_int32_t) :: n_limits = 0
+     real(c_double)     :: limit_dr(AFH_MAX_REFINE_REGIONS) = 0
+     real(c_double)     :: limit_rmin(3, AFH_MAX_REFINE_REGIONS) = 0
+     real(c_double)     :: limit_rmax(3, AFH_MAX_REFINE_REGIONS) = 0
+  end type afh_refine_desc
+
   type, bind(C) :: afh_fluid_desc
      integer(c_int32_t) :: n_species
      integer(c_int32_t) :: species_iv(AFH_MAX_SPECIES)
@@ -319,6 +350,43 @@ module m_afivo_hip
        integer(c_int32_t), value      :: i_lsf
        integer(c_int32_t)             :: afh_mg_set_box_lsf
      end function afh_mg_set_box_lsf
+
+     function afh_set_cc_prolong(t, iv, method, limiter) &
+          bind(C, name=afh_pfx//"set_cc_prolong")
+       import
+       type(c_ptr), value        :: t
+       integer(c_int32_t), value :: iv, method, limiter
+       integer(c_int32_t)        :: afh_set_cc_prolong
+     end function afh_set_cc_prolong
+
+     ! af_adjust_refinement's data movement onto the new topology
+     function afh_tree_regrid(t, desc, out) bind(C, name=afh_pfx//"tree_regrid")
+       import
+       type(c_ptr), value             :: t
+       type(afh_tree_desc), intent(in) :: desc
+       type(c_ptr), intent(out)       :: out
+       integer(c_int32_t)             :: afh_tree_regrid
+     end function afh_tree_regrid
+
+     ! default_refinement + cell_to_ref_flags per box, on the device
+     function afh_refine_flags(f, desc, electrode_box, flags, masks) &
+          bind(C, name=afh_pfx//"refine_flags")
+       import
+       type(c_ptr), value                :: f
+       type(afh_refine_desc), intent(in) :: desc
+       type(c_ptr), value                :: electrode_box  ! c_loc(int8 array) or c_null_ptr
+       integer(c_int32_t), intent(out)   :: flags(*), masks(*)
+       integer(c_int32_t)                :: afh_refine_flags
+     end function afh_refine_flags
+
+     ! cell flags for af_adjust_refinement's ref_subr from a box summary
+     function afh_refine_cell_flags(flag, mask, nc, bw, cell_flags) &
+          bind(C, name=afh_pfx//"refine_cell_flags")
+       import
+       integer(c_int32_t), value       :: flag, mask, nc, bw
+       integer(c_int32_t), intent(out) :: cell_flags(*)
+       integer(c_int32_t)              :: afh_refine_cell_flags
+     end function afh_refine_cell_flags
 
      function afh_fluid_create(t, desc, out) bind(C, name=afh_pfx//"fluid_create")
        import

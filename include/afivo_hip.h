@@ -319,6 +319,52 @@ int32_t afh_fluid_forward_euler(afh_fluid *f, double dt, int32_t s_deriv,
 int32_t afh_set_cc_prolong(afh_tree *t, int32_t iv, int32_t method, int32_t limiter);
 int32_t afh_tree_regrid(afh_tree *old, const afh_tree_desc *desc, afh_tree **out);
 
+/* Refinement flags (default_refinement, src/m_refine.f90:198-298, reduced
+ * per box as cell_to_ref_flags does, afivo/src/m_af_core.f90:1095-1148): for
+ * every box of the tree, flags[id-1] = AFH_DO_REF if a cell asks for
+ * refinement, AFH_KEEP_REF if one asks to keep it, AFH_RM_REF if all ask for
+ * removal; masks[id-1] bit (dk+1)*9 + (dj+1)*3 + (di+1) is set when a cell
+ * within buffer_width cells of the box side towards neighbour (di,dj,dk)
+ * asks for refinement (cell_to_ref_flags' neighbour rule). The driver's
+ * refinement routine for af_adjust_refinement rebuilds the same box flags
+ * from these without the field data leaving the device. Time-dependent
+ * switches (refine_init_time, refine_regions_tstop) are the caller's: pass
+ * only the seeds / regions active now. electrode_box: per box 1 when the box
+ * is tagged mg_lsf_box (NULL: none). */
+#define AFH_RM_REF -1
+#define AFH_KEEP_REF 0
+#define AFH_DO_REF 1
+#define AFH_MAX_REFINE_REGIONS 8
+typedef struct afh_refine_desc {
+  int32_t i_electron, i_efld;        /* cc variables */
+  int32_t td_alpha_col, td_eta_col;  /* transport-table columns (td_alpha 3, td_eta 4) */
+  int32_t use_alpha_effective;       /* refine_use_alpha_effective */
+  int32_t buffer_width;              /* refine_buffer_width (cells) */
+  double adx_fac, adx, min_dens;     /* refine_adx_fac, refine_adx, refine_min_dens */
+  double derefine_dx, max_dx, min_dx; /* derefine_dx, refine_max_dx, refine_min_dx */
+  double electrode_dx;               /* current_electrode_dx */
+  int32_t n_seeds;                   /* init_conds (while global_time < refine_init_time) */
+  double init_fac;                   /* refine_init_fac */
+  double seed_r0[AFH_MAX_REFINE_REGIONS][3], seed_r1[AFH_MAX_REFINE_REGIONS][3];
+  double seed_width[AFH_MAX_REFINE_REGIONS];
+  int32_t n_regions;                 /* refine_regions_* (active ones) */
+  double region_dr[AFH_MAX_REFINE_REGIONS];
+  double region_rmin[AFH_MAX_REFINE_REGIONS][3], region_rmax[AFH_MAX_REFINE_REGIONS][3];
+  int32_t n_limits;                  /* refine_limits_* */
+  double limit_dr[AFH_MAX_REFINE_REGIONS];
+  double limit_rmin[AFH_MAX_REFINE_REGIONS][3], limit_rmax[AFH_MAX_REFINE_REGIONS][3];
+} afh_refine_desc;
+int32_t afh_refine_flags(afh_fluid *f, const afh_refine_desc *d,
+                         const uint8_t *electrode_box, int32_t *flags,
+                         uint32_t *masks);
+
+/* The cell flags a driver's refinement routine hands af_adjust_refinement
+ * for a box with summary (flag, mask) of afh_refine_flags: cell_to_ref_flags
+ * gives back exactly (flag, mask) (buffer_width bw). cell_flags: nc^3, i
+ * fastest (afivo's cell_flags(nc, nc, nc)). */
+int32_t afh_refine_cell_flags(int32_t flag, uint32_t mask, int32_t nc, int32_t bw,
+                              int32_t *cell_flags);
+
 /* Kernel timing (replaces the reference's omp_get_wtime cost buckets,
  * src/m_streamer.f90:181-187): while enabled, every launch of the selected
  * kernel class is bracketed by HIP events on the tree's stream;

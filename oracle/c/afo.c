@@ -2266,3 +2266,171 @@ int32_t afo_tree_regrid(afh_tree *o, const afh_tree_desc *d, afh_tree **out) {
   return AFH_OK;
 }
 
+/* ------------------------------------------------------------ refinement */
+
+/* GM_dist_line (src/m_geometry.f90:23-51): distance from r to the segment
+ * r0-r1 (norm2 as sqrt of the sum of squares) */
+static double dist_line(const double r[3], const double r0[3], const double r1[3]) {
+  double len2 = 0, frac = 0, dv[3];
+  for (int d = 0; d < 3; d++) len2 = len2 + (r1[d] - r0[d]) * (r1[d] - r0[d]);
+  for (int d = 0; d < 3; d++) frac = frac + (r[d] - r0[d]) * (r1[d] - r0[d]);
+  if (frac <= 0.0) {
+    for (int d = 0; d < 3; d++) dv[d] = r[d] - r0[d];
+  } else if (frac >= len2) {
+    for (int d = 0; d < 3; d++) dv[d] = r[d] - r1[d];
+  } else {
+    for (int d = 0; d < 3; d++) dv[d] = r[d] - (r0[d] + frac / len2 * (r1[d] - r0[d]));
+  }
+  return sqrt(dv[0] * dv[0] + dv[1] * dv[1] + dv[2] * dv[2]);
+}
+
+/* default_refinement for cell (i, j, k) of box id (src/m_refine.f90:198-298,
+ * constant gas density), the box-level rules applied per cell in the order
+ * the reference applies them to the whole array */
+static int refine_cell(afh_fluid *fl, const afh_refine_desc *p, int id, int elec,
+                       int i, int j, int k) {
+  afh_tree *t = fl->t;
+  const afh_box_meta *b = B(t, id);
+  int nc = t->nc;
+  double min_dx = b->dr[0], max_dx = b->dr[0];
+  for (int d = 1; d < 3; d++) {
+    if (b->dr[d] < min_dx) min_dx = b->dr[d];
+    if (b->dr[d] > max_dx) max_dx = b->dr[d];
+  }
+  size_t x = IX(t, i, j, k);
+  double gas_dens = fl->d.gas_number_density;
+  double fld = ccb(t, p->i_efld, id)[x] * 1e21 / gas_dens;  /* SI_to_Townsend */
+  double alpha;
+  if (p->use_alpha_effective) {
+    alpha = (lt_col(&fl->d.td, p->td_alpha_col, p->adx_fac * fld) -
+             lt_col(&fl->d.td, p->td_eta_col, p->adx_fac * fld)) *
+            gas_dens / p->adx_fac;
+    alpha = alpha > 0.0 ? alpha : 0.0;
+  } else {
+    alpha = lt_col(&fl->d.td, p->td_alpha_col, p->adx_fac * fld) * gas_dens / p->adx_fac;
+  }
+  double adx = max_dx * alpha, ne = ccb(t, p->i_electron, id)[x];
+  int f;
+  if (adx > p->adx && ne > p->min_dens) f = AFH_DO_REF;
+  else if (adx < 0.125 * p->adx && max_dx < p->derefine_dx) f = AFH_RM_REF;
+  else f = AFH_KEEP_REF;
+  double r[3] = {b->r_min[0] + (i - 0.5) * b->dr[0], b->r_min[1] + (j - 0.5) * b->dr[1],
+                 b->r_min[2] + (k - 0.5) * b->dr[2]};
+  for (int n = 0; n < p->n_seeds; n++) {
+    double dist = dist_line(r, p->seed_r0[n], p->seed_r1[n]);
+    if (dist - p->seed_width[n] < 2 * max_dx && max_dx > p->init_fac * p->seed_width[n])
+      f = AFH_DO_REF;
+  }
+  if (elec && max_dx > p->electrode_dx) f = AFH_DO_REF;
+  double rmin[3], rmax[3];
+  for (int d = 0; d < 3; d++) rmin[d] = b->r_min[d], rmax[d] = b->r_min[d] + b->dr[d] * nc;
+  for (int n = 0; n < p->n_regions; n++) {
+    int in = max_dx > p->region_dr[n];
+    for (int d = 0; d < 3; d++)
+      in = in && rmax[d] >= p->region_rmin[n][d] && rmin[d] <= p->region_rmax[n][d];
+    if (in && i == nc / 2 && j == nc / 2 && k == nc / 2) f = AFH_DO_REF;
+  }
+  for (int n = 0; n < p->n_limits; n++) {
+    int in = max_dx < 2 * p->limit_dr[n];
+    for (int d = 0; d < 3; d++)
+      in = in && rmin[d] >= p->limit_rmin[n][d] && rmax[d] <= p->limit_rmax[n][d];
+    if (in && f == AFH_DO_REF) f = AFH_KEEP_REF;
+  }
+  if (max_dx > p->max_dx) f = AFH_DO_REF;
+  else if (min_dx < 2 * p->min_dx && f == AFH_DO_REF) f = AFH_KEEP_REF;
+  return f;
+}
+
+int32_t afo_refine_flags(afh_fluid *fl, const afh_refine_desc *p,
+                         const uint8_t *electrode_box, int32_t *flags, uint32_t *masks) {
+  if (!fl || !p || !flags || !masks) return fail(AFH_ERR_ARG, "afo_refine_flags: null");
+  afh_tree *t = fl->t;
+  if (p->n_seeds > AFH_MAX_REFINE_REGIONS || p->n_regions > AFH_MAX_REFINE_REGIONS ||
+      p->n_limits > AFH_MAX_REFINE_REGIONS || p->buffer_width < 0 ||
+      p->buffer_width > t->nc)
+    return fail(AFH_ERR_ARG, "afo_refine_flags: bad descriptor");
+  int nc = t->nc, bw = p->buffer_width;
+  for (int q = 0; q < t->nb; q++) flags[q] = 0, masks[q] = 0;
+#pragma omp parallel for schedule(dynamic)
+  for (int q = 0; q < t->ids_off[t->nlvl]; q++) {
+    int id = t->ids[q], any_do = 0, any_keep = 0;
+    uint32_t m = 0;
+    int elec = electrode_box ? electrode_box[id - 1] : 0;
+    for (int k = 1; k <= nc; k++)
+      for (int j = 1; j <= nc; j++)
+        for (int i = 1; i <= nc; i++) {
+          int f = refine_cell(fl, p, id, elec, i, j, k);
+          if (f == AFH_DO_REF) {
+            any_do = 1;
+            if (bw > 0) {
+              /* the neighbour slabs this cell lies in (cell_to_ref_flags) */
+              int lo[3] = {i <= bw, j <= bw, k <= bw};
+              int hi[3] = {i > nc - bw, j > nc - bw, k > nc - bw};
+              for (int dk = -1; dk <= 1; dk++)
+                for (int dj = -1; dj <= 1; dj++)
+                  for (int di = -1; di <= 1; di++) {
+                    if (!di && !dj && !dk) continue;
+                    int dd[3] = {di, dj, dk}, in = 1;
+                    for (int d = 0; d < 3; d++)
+                      in = in && (dd[d] == 0 || (dd[d] < 0 ? lo[d] : hi[d]));
+                    if (in) m |= 1u << ((dk + 1) * 9 + (dj + 1) * 3 + (di + 1));
+                  }
+            }
+          } else if (f == AFH_KEEP_REF) {
+            any_keep = 1;
+          }
+        }
+    flags[id - 1] = any_do ? AFH_DO_REF : any_keep ? AFH_KEEP_REF : AFH_RM_REF;
+    masks[id - 1] = m;
+  }
+  return AFH_OK;
+}
+
+/* Cell flags with the box summary (flag, mask) of afh_refine_flags, for the
+ * driver's refinement routine (af_subr_ref) in af_adjust_refinement: a set
+ * of cells asking for refinement whose cell_to_ref_flags result
+ * (m_af_core.f90:1095-1148) is exactly (flag, mask); the other cells keep
+ * (flag >= keep) or remove (flag = remove) the refinement. Per dimension a
+ * cell index is in the low buffer slab, the high one, both or neither; one
+ * representative cell per class combination whose neighbour slabs all lie in
+ * the mask is marked when it adds a direction (or, for a box refining only
+ * away from its sides, a cell in no slab). */
+int32_t afo_refine_cell_flags(int32_t flag, uint32_t mask, int32_t nc, int32_t bw,
+                               int32_t *cf) {
+  if (nc < 1 || bw < 0 || bw > nc || !cf || flag < AFH_RM_REF || flag > AFH_DO_REF)
+    return fail(AFH_ERR_ARG, "refine_cell_flags: bad argument");
+  const size_t n3 = (size_t)nc * nc * nc;
+  for (size_t q = 0; q < n3; q++) cf[q] = flag == AFH_RM_REF ? AFH_RM_REF : AFH_KEEP_REF;
+  if (flag != AFH_DO_REF) return mask ? fail(AFH_ERR_ARG, "mask without refinement") : AFH_OK;
+  int rep[4]; /* class -> first index (1-based) or 0; class = lo | hi << 1 */
+  for (int c = 0; c < 4; c++) rep[c] = 0;
+  for (int i = nc; i >= 1; i--) rep[(i <= bw) | ((i > nc - bw) << 1)] = i;
+  uint32_t need = mask;
+  int placed = 0;
+  for (int pass = 0; pass < 2; pass++)
+    for (int cz = 0; cz < 4; cz++)
+      for (int cy = 0; cy < 4; cy++)
+        for (int cx = 0; cx < 4; cx++) {
+          if (!rep[cx] || !rep[cy] || !rep[cz]) continue;
+          const int cl[3] = {cx, cy, cz};
+          uint32_t mem = 0;
+          for (int dk = -1; dk <= 1; dk++)
+            for (int dj = -1; dj <= 1; dj++)
+              for (int di = -1; di <= 1; di++) {
+                if (!di && !dj && !dk) continue;
+                const int dd[3] = {di, dj, dk};
+                int in = 1;
+                for (int d = 0; d < 3; d++)
+                  in = in && (dd[d] == 0 || (cl[d] & (dd[d] < 0 ? 1 : 2)));
+                if (in) mem |= 1u << ((dk + 1) * 9 + (dj + 1) * 3 + (di + 1));
+              }
+          if ((mem & ~mask) != 0) continue;
+          /* pass 0: cells that add a direction; pass 1: any cell if none yet */
+          if (pass == 0 ? (mem & need) == 0 : placed) continue;
+          cf[((size_t)(rep[cz] - 1) * nc + (rep[cy] - 1)) * nc + (rep[cx] - 1)] = AFH_DO_REF;
+          need &= ~mem;
+          placed = 1;
+        }
+  if (need || !placed) return fail(AFH_ERR_ARG, "refine_cell_flags: inconsistent mask");
+  return AFH_OK;
+}

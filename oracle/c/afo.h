@@ -54,6 +54,10 @@ int32_t afo_mg_set_box_lsf(afh_mg *mg, int32_t id, int32_t n, const int32_t *ix,
                            const double *dd, const double *bval, int32_t i_lsf);
 int32_t afo_set_cc_prolong(afh_tree *t, int32_t iv, int32_t method, int32_t limiter);
 int32_t afo_tree_regrid(afh_tree *old, const afh_tree_desc *desc, afh_tree **out);
+int32_t afo_refine_flags(afh_fluid *f, const afh_refine_desc *d,
+                         const uint8_t *electrode_box, int32_t *flags, uint32_t *masks);
+int32_t afo_refine_cell_flags(int32_t flag, uint32_t mask, int32_t nc, int32_t bw,
+                              int32_t *cell_flags);
 int32_t afo_fluid_create(afh_tree *t, const afh_fluid_desc *desc,
                          afh_fluid **out);
 int32_t afo_fluid_destroy(afh_fluid *f);

@@ -47,6 +47,7 @@ program golden_gen
   use m_af_limiters
   use m_coarse_solver, only: mg_lsf_boundary_value
   use m_geometry, only: GM_dist_line
+  use m_lookup_table, only: LT_get_col
   use hx_physics
 
   implicit none
@@ -63,6 +64,15 @@ program golden_gen
   logical            :: trace, use_lsf, do_regrid
   integer            :: u_log, i_lsf
   type(ref_info_t)   :: regrid_info
+  ! default_refinement parameters of the regrid8 case (src/m_refine.f90:10-60
+  ! names), dumped with the flags
+  real(dp) :: rf_adx = 0.3_dp, rf_adx_fac = 1.0_dp, rf_min_dens = 1.0e16_dp
+  real(dp) :: rf_derefine_dx = 1.0e-4_dp, rf_max_dx = 1.0e-3_dp
+  real(dp) :: rf_min_dx = 1.0e-7_dp, rf_init_fac = 0.25_dp
+  real(dp) :: rf_seed_r0(3), rf_seed_r1(3), rf_seed_width
+  real(dp) :: rf_region_dr, rf_region_rmin(3), rf_region_rmax(3)
+  real(dp) :: rf_limit_dr, rf_limit_rmin(3), rf_limit_rmax(3)
+  integer  :: rf_buffer = 2
   ! rod electrode (field_rod_r0/r1/radius as fractions of the domain)
   real(dp)           :: rod_r0(3), rod_r1(3), rod_radius
 
@@ -183,8 +193,13 @@ program golden_gen
   if (use_lsf) call dump_lsf()
 
   if (do_regrid) then
-     call af_gc_tree(tree, [i_efld])
+     ! the field of the initial state (field_compute + field_from_potential)
+     call hx_field_set_rhs(tree, 0)
+     call vcycle(.true., .false.)
+     call vcycle(.true., .false.)
+     call field_from_potential()
      call dump_state("regrid_in")
+     call dump_refine_flags()
      call af_adjust_refinement(tree, ref_regrid, regrid_info)
      call dump_topology("topology_after.bin")
      call dump_in_use("in_use_after.bin")
@@ -420,6 +435,116 @@ contains
        end do
     end do
   end subroutine ref_regrid
+
+  !> default_refinement (src/m_refine.f90:198-298) with constant gas density,
+  !> alpha without attachment, one initial seed, one refine region and one
+  !> refine limit
+  subroutine ref_default(box, cell_flags)
+    type(box_t), intent(in) :: box
+    integer, intent(out)    :: cell_flags(DTIMES(box%n_cell))
+    integer                 :: IJK, nc
+    real(dp)                :: min_dx, max_dx, alpha, adx, fld, dist
+    real(dp)                :: rmin(3), rmax(3)
+    nc = box%n_cell
+    min_dx = minval(box%dr)
+    max_dx = maxval(box%dr)
+    do k = 1, nc
+       do j = 1, nc
+          do i = 1, nc
+             fld = box%cc(IJK, i_efld) * SI_to_Townsend / gas_number_density
+             alpha = LT_get_col(td_tbl, td_alpha, rf_adx_fac * fld) * &
+                  gas_number_density / rf_adx_fac
+             adx = max_dx * alpha
+             if (adx > rf_adx .and. box%cc(IJK, i_e) > rf_min_dens) then
+                cell_flags(IJK) = af_do_ref
+             else if (adx < 0.125_dp * rf_adx .and. max_dx < rf_derefine_dx) then
+                cell_flags(IJK) = af_rm_ref
+             else
+                cell_flags(IJK) = af_keep_ref
+             end if
+             dist = GM_dist_line(af_r_cc(box, [IJK]), rf_seed_r0, rf_seed_r1, 3)
+             if (dist - rf_seed_width < 2 * max_dx .and. &
+                  max_dx > rf_init_fac * rf_seed_width) cell_flags(IJK) = af_do_ref
+          end do
+       end do
+    end do
+    rmin = box%r_min
+    rmax = box%r_min + box%dr * box%n_cell
+    if (max_dx > rf_region_dr .and. all(rmax >= rf_region_rmin .and. &
+         rmin <= rf_region_rmax)) cell_flags(DTIMES(nc/2)) = af_do_ref
+    if (max_dx < 2 * rf_limit_dr .and. all(rmin >= rf_limit_rmin .and. &
+         rmax <= rf_limit_rmax)) where (cell_flags == af_do_ref) cell_flags = af_keep_ref
+    if (max_dx > rf_max_dx) then
+       cell_flags = af_do_ref
+    else if (min_dx < 2 * rf_min_dx) then
+       where (cell_flags == af_do_ref) cell_flags = af_keep_ref
+    end if
+  end subroutine ref_default
+
+  !> Per box: the flag cell_to_ref_flags gives the box itself
+  !> (m_af_core.f90:1111-1118) and the neighbour directions whose buffer
+  !> slab holds a refining cell (1124-1146), bit (dk+1)*9+(dj+1)*3+(di+1)
+  subroutine dump_refine_flags()
+    integer :: u, id, lvl, n, nc, IJK, di, dj, dk, ix0(3), ix1(3), f, m
+    integer :: cf(tree%n_cell, tree%n_cell, tree%n_cell)
+    integer, allocatable :: flags(:), masks(:)
+    nc = tree%n_cell
+    rf_seed_r0 = r0
+    rf_seed_r1 = r0 + [0.0_dp, 0.0_dp, 0.3_dp] * dom
+    rf_seed_width = 0.05_dp * dom(3)
+    rf_region_dr = 1.0e-4_dp
+    rf_region_rmin = [0.0_dp, 0.0_dp, 0.75_dp] * dom
+    rf_region_rmax = [0.3_dp, 0.3_dp, 1.0_dp] * dom
+    rf_limit_dr = 1.0e-4_dp
+    rf_limit_rmin = [0.5_dp, 0.5_dp, 0.0_dp] * dom
+    rf_limit_rmax = [1.0_dp, 1.0_dp, 0.5_dp] * dom
+    allocate(flags(tree%highest_id), masks(tree%highest_id))
+    flags = 0
+    masks = 0
+    do lvl = 1, tree%highest_lvl
+       do n = 1, size(tree%lvls(lvl)%ids)
+          id = tree%lvls(lvl)%ids(n)
+          call ref_default(tree%boxes(id), cf)
+          if (any(cf == af_do_ref)) then
+             f = af_do_ref
+          else if (any(cf == af_keep_ref)) then
+             f = af_keep_ref
+          else
+             f = af_rm_ref
+          end if
+          m = 0
+          do dk = -1, 1
+             do dj = -1, 1
+                do di = -1, 1
+                   if (di == 0 .and. dj == 0 .and. dk == 0) cycle
+                   ix0 = 1
+                   ix1 = nc
+                   where ([di, dj, dk] == 1)
+                      ix0 = nc - rf_buffer + 1
+                      ix1 = nc
+                   elsewhere ([di, dj, dk] == -1)
+                      ix0 = 1
+                      ix1 = rf_buffer
+                   end where
+                   if (any(cf(ix0(1):ix1(1), ix0(2):ix1(2), ix0(3):ix1(3)) &
+                        == af_do_ref)) m = ibset(m, (dk+1)*9 + (dj+1)*3 + (di+1))
+                end do
+             end do
+          end do
+          flags(id) = f
+          masks(id) = m
+       end do
+    end do
+    open(newunit=u, file=trim(out_dir)//"/refine.bin", &
+         access="stream", form="unformatted", status="replace")
+    write(u) tree%highest_id, flags, masks
+    write(u) rf_adx, rf_adx_fac, rf_min_dens, rf_derefine_dx, rf_max_dx, &
+         rf_min_dx, rf_init_fac, rf_seed_r0, rf_seed_r1, rf_seed_width, &
+         rf_region_dr, rf_region_rmin, rf_region_rmax, rf_limit_dr, &
+         rf_limit_rmin, rf_limit_rmax
+    write(u) rf_buffer
+    close(u)
+  end subroutine dump_refine_flags
 
   subroutine dump_in_use(fname)
     character(len=*), intent(in) :: fname

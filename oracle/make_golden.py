@@ -228,6 +228,12 @@ def pack(case, raw_dir):
             after[k][in_use == 0] = 0
         for k, v in after.items():
             out["after_" + k] = v
+        raw = open(os.path.join(raw_dir, "refine.bin"), "rb").read()
+        nbx = int(np.frombuffer(raw, np.int32, 1, 0)[0])
+        out["refine_flags"] = np.frombuffer(raw, np.int32, nbx, 4).copy()
+        out["refine_masks"] = np.frombuffer(raw, np.int32, nbx, 4 + 4 * nbx).copy()
+        out["refine_params"] = np.frombuffer(raw, np.float64, 28, 4 + 8 * nbx).copy()
+        out["refine_buffer"] = np.frombuffer(raw, np.int32, 1, 4 + 8 * nbx + 224).copy()
         name, ccv = REGRID_AFTER
         cc, _ = read_state(os.path.join(raw_dir, "state_%s.bin" % name), after)
         for v in ccv:
