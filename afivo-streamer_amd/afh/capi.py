@@ -56,7 +56,8 @@ class TreeDesc(C.Structure):
                 ("boxes", C.c_void_p),
                 ("lvl_ids", P_i32), ("lvl_ids_off", P_i32),
                 ("lvl_leaves", P_i32), ("lvl_leaves_off", P_i32),
-                ("lvl_parents", P_i32), ("lvl_parents_off", P_i32)]
+                ("lvl_parents", P_i32), ("lvl_parents_off", P_i32),
+                ("box_capacity", i32)]
 
 
 class BC(C.Structure):

@@ -30,7 +30,10 @@ def _lists(topo, kind):
 class Tree:
     """af_t: topology + device box pool of n_var_cell / n_var_face variables."""
 
-    def __init__(self, lib, topo, n_var_cell, n_var_face, device=-1, _regrid_of=None):
+    def __init__(self, lib, topo, n_var_cell, n_var_face, device=-1, _regrid_of=None,
+                 box_capacity=0):
+        """box_capacity: boxes the device pools hold (afivo's box_limit; 0 =
+        the topology's box count); a regrid that fits them works in place."""
         self.lib = lib
         self.topo = topo
         self.nc = int(topo["nc"])
@@ -38,6 +41,7 @@ class Tree:
         self.highest_lvl = int(topo["highest_lvl"])
         self.n_var_cell = n_var_cell
         self.n_var_face = n_var_face
+        self.box_capacity = int(box_capacity)
         nb = self.n_boxes
         meta = np.zeros(nb, capi.BOX_META_DTYPE)
         meta["lvl"] = topo["meta_lvl"]
@@ -58,6 +62,7 @@ class Tree:
         d.r_base[:] = [float(x) for x in topo["r_base"]]
         d.dr_base[:] = [float(x) for x in topo["dr_base"]]
         d.boxes = meta.ctypes.data
+        d.box_capacity = self.box_capacity
         for k in ("ids", "leaves", "parents"):
             flat, off = self._lists[k]
             setattr(d, "lvl_%s" % k, flat.ctypes.data_as(capi.P_i32))
@@ -71,9 +76,11 @@ class Tree:
 
     def regrid(self, topo):
         """af_adjust_refinement's data movement onto the new topology `topo`
-        (afh_tree_regrid): a new Tree; this one stays valid."""
+        (afh_tree_regrid): a new Tree. When the new tree fits this one's
+        pools (box_capacity) the data stay in place and this tree keeps only
+        its topology; otherwise it stays valid."""
         return Tree(self.lib, topo, self.n_var_cell, self.n_var_face,
-                    _regrid_of=self)
+                    _regrid_of=self, box_capacity=self.box_capacity)
 
     def set_cc_prolong(self, iv, method, limiter=capi.LIM_GMINMOD43):
         """tree%cc_methods(iv)%prolong (capi.PROLONG_LINEAR / PROLONG_LIMIT)

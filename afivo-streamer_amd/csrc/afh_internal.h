@@ -64,6 +64,7 @@ struct afh_tree {
   int device = 0;
   hipStream_t stream = nullptr;
   int nc = 0, ng = 0, nb = 0, nlvl = 0, nvc = 0, nvf = 0;
+  int cap = 0;  // boxes the data pools hold (variable stride), >= nb
   size_t bsz = 0, fsz = 0;
   int cgs[3] = {0, 0, 0};
   double r_base[3], dr_base[3];
@@ -111,10 +112,10 @@ struct afh_tree {
   };
   std::vector<Plan> plans;
 
-  double *ccv(int iv) const { return cc + (size_t)(iv - 1) * nb * bsz; }
+  double *ccv(int iv) const { return cc + (size_t)(iv - 1) * cap * bsz; }
   // cc variable iv, or the smoother's spare image of phi for iv == 0
   double *var(int iv) const { return iv == 0 ? alt : ccv(iv); }
-  double *fcv(int ivf) const { return fc + (size_t)(ivf - 1) * nb * fsz; }
+  double *fcv(int ivf) const { return fc + (size_t)(ivf - 1) * cap * fsz; }
   afh::GcArgs gc_args(int iv) const {
     afh::GcArgs a;
     for (int n = 0; n < 6; n++) a.bc[n] = meth[iv].bc[n];

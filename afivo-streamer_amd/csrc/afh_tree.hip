@@ -445,14 +445,15 @@ __global__ void k_prolong_new(double *__restrict__ v,
 }
 
 // box ids[blockIdx.y] of variable blockIdx.z: src pool -> dst pool (the two
-// pools of a regrid have different box counts, so different variable strides)
+// pools of a regrid may hold different box counts: different variable
+// strides); src null: zero
 __global__ void k_copy_boxes(const double *__restrict__ src, double *__restrict__ dst,
                              const int32_t *__restrict__ ids, size_t per_box,
                              size_t src_var, size_t dst_var) {
   const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= per_box) return;
   const size_t b = (size_t)(ids[blockIdx.y] - 1) * per_box + t;
-  dst[blockIdx.z * dst_var + b] = src[blockIdx.z * src_var + b];
+  dst[blockIdx.z * dst_var + b] = src ? src[blockIdx.z * src_var + b] : 0.0;
 }
 }  // namespace afh
 
@@ -463,8 +464,8 @@ extern "C" {
 const char *afh_last_error(void) { return afh::g_err; }
 
 
-int32_t afh_tree_create(const afh_tree_desc *d, int32_t device,
-                        afh_tree **out) {
+static int32_t tree_create_impl(const afh_tree_desc *d, int32_t device,
+                                afh_tree **out, afh_tree *adopt) {
   if (!d || !out || d->n_cell < 2 || (d->n_cell & 1) || d->n_boxes < 1 ||
       d->highest_lvl < 1 || d->n_var_cell < 1)
     return set_error(AFH_ERR_ARG, "afh_tree_create: bad descriptor");
@@ -486,6 +487,7 @@ int32_t afh_tree_create(const afh_tree_desc *d, int32_t device,
   t->nc = d->n_cell;
   t->ng = d->n_cell + 2;
   t->nb = d->n_boxes;
+  t->cap = std::max(d->n_boxes, d->box_capacity);
   t->nlvl = d->highest_lvl;
   t->nvc = d->n_var_cell;
   t->nvf = d->n_var_face;
@@ -575,18 +577,29 @@ int32_t afh_tree_create(const afh_tree_desc *d, int32_t device,
   AFH_HIP(hipMalloc(&t->d_boxes, sizeof(afh_box_meta) * t->nb));
   AFH_HIP(hipMemcpy(t->d_boxes, t->boxes.data(), sizeof(afh_box_meta) * t->nb,
                     hipMemcpyHostToDevice));
-  size_t ncc = (size_t)t->nvc * t->nb * t->bsz;
-  size_t nfc = (size_t)std::max(1, t->nvf) * t->nb * t->fsz;
-  AFH_HIP(hipMalloc(&t->cc, ncc * sizeof(double)));
-  AFH_HIP(hipMalloc(&t->fc, nfc * sizeof(double)));
-  AFH_HIP(hipMemsetAsync(t->cc, 0, ncc * sizeof(double), t->stream));
-  AFH_HIP(hipMemsetAsync(t->fc, 0, nfc * sizeof(double), t->stream));
-  AFH_HIP(hipMalloc(&t->gc2, sizeof(double) * (size_t)t->nb * 6 * t->nc * t->nc));
+  if (adopt) {  // afh_tree_regrid in place: the old tree's pools
+    t->cap = adopt->cap;
+    t->cc = adopt->cc, t->fc = adopt->fc, t->gc2 = adopt->gc2;
+    adopt->cc = adopt->fc = adopt->gc2 = nullptr;
+  } else {
+    size_t ncc = (size_t)t->nvc * t->cap * t->bsz;
+    size_t nfc = (size_t)std::max(1, t->nvf) * t->cap * t->fsz;
+    AFH_HIP(hipMalloc(&t->cc, ncc * sizeof(double)));
+    AFH_HIP(hipMalloc(&t->fc, nfc * sizeof(double)));
+    AFH_HIP(hipMemsetAsync(t->cc, 0, ncc * sizeof(double), t->stream));
+    AFH_HIP(hipMemsetAsync(t->fc, 0, nfc * sizeof(double), t->stream));
+    AFH_HIP(hipMalloc(&t->gc2, sizeof(double) * (size_t)t->cap * 6 * t->nc * t->nc));
+  }
   AFH_HIP(hipMalloc(&t->scratch, (size_t)(RED_SLOTS + 1) * RED_SHARDS * sizeof(double)));
   AFH_HIP(hipHostMalloc(&t->h_scratch, RED_SLOTS * sizeof(double)));
   AFH_HIP(hipStreamSynchronize(t->stream));
   *out = t;
   return AFH_OK;
+}
+
+int32_t afh_tree_create(const afh_tree_desc *d, int32_t device,
+                        afh_tree **out) {
+  return tree_create_impl(d, device, out, nullptr);
 }
 
 int32_t afh_profile_enable(afh_tree *t, int32_t kclass) {
@@ -885,27 +898,32 @@ int32_t afh_tree_regrid(afh_tree *o, const afh_tree_desc *d, afh_tree **out) {
   if (o->hook) return set_error(AFH_ERR_UNSUPPORTED, "regrid of a sharded tree");
   afh_tree *t = nullptr;
   int32_t e;
-  if ((e = afh_tree_create(d, o->device, &t))) return e;
-  t->meth = o->meth;
-  t->auto_vars = o->auto_vars;
-  const int nc = t->nc;
+  // in place when the new tree fits the old pools (box ids index them)
+  const bool in_place = std::max(d->n_boxes, d->box_capacity) <= o->cap;
+  const int nc = o->nc;
   // boxes that persist: same id, level and index in both topologies
-  std::vector<char> in_old(o->nb + 1, 0), keep(t->nb + 1, 0);
+  std::vector<char> in_old(o->nb + 1, 0), keep(d->n_boxes + 1, 0);
   for (const auto &L : o->h_ids)
     for (int32_t id : L) in_old[id] = 1;
-  std::vector<int32_t> kept, rchild;
-  for (const auto &L : t->h_ids)
-    for (int32_t id : L) {
-      if (id > o->nb || !in_old[id]) continue;
-      const afh_box_meta &a = o->boxes[id - 1], &b = t->boxes[id - 1];
-      if (a.lvl != b.lvl || a.ix[0] != b.ix[0] || a.ix[1] != b.ix[1] || a.ix[2] != b.ix[2])
+  std::vector<int32_t> kept, rchild, fresh;
+  for (int q = 0; q < d->lvl_ids_off[d->highest_lvl]; q++) {
+      const int32_t id = d->lvl_ids[q];
+      if (id < 1 || id > d->n_boxes) return set_error(AFH_ERR_ARG, "bad box id %d", id);
+      if (id > o->nb || !in_old[id]) {
+        fresh.push_back(id);
         continue;
+      }
+      const afh_box_meta &a = o->boxes[id - 1], &b = d->boxes[id - 1];
+      if (a.lvl != b.lvl || a.ix[0] != b.ix[0] || a.ix[1] != b.ix[1] || a.ix[2] != b.ix[2]) {
+        fresh.push_back(id);
+        continue;
+      }
       keep[id] = 1;
       kept.push_back(id);
       // auto_restrict (m_af_core.f90:826-840): the box lost its children
       if (a.children[0] > 0 && b.children[0] == 0)
         for (int c = 0; c < 8; c++) rchild.push_back(a.children[c]);
-    }
+  }
   int32_t *d_list = nullptr;
   if (!rchild.empty()) {
     if ((e = device_list(rchild, &d_list))) return e;
@@ -915,17 +933,38 @@ int32_t afh_tree_regrid(afh_tree *o, const afh_tree_desc *d, afh_tree **out) {
   AFH_HIP(hipStreamSynchronize(o->stream));
   hipFree(d_list);
   d_list = nullptr;
-  if (!kept.empty()) {
+  if ((e = tree_create_impl(d, o->device, &t, in_place ? o : nullptr))) return e;
+  t->meth = o->meth;
+  t->auto_vars = o->auto_vars;
+  if (in_place && !fresh.empty()) {
+    // new boxes start at 0 in every variable (af_init_box, m_af_core.f90:556-557)
+    if ((e = device_list(fresh, &d_list))) return e;
+    const unsigned n = (unsigned)fresh.size();
+    hipLaunchKernelGGL(k_copy_boxes, dim3((unsigned)((t->bsz + 255) / 256), n, t->nvc),
+                       dim3(256), 0, t->stream, nullptr, t->cc, d_list, t->bsz,
+                       (size_t)0, (size_t)t->cap * t->bsz);
+    AFH_LAUNCH_CHECK("k_copy_boxes");
+    if (t->nvf > 0) {
+      hipLaunchKernelGGL(k_copy_boxes, dim3((unsigned)((t->fsz + 255) / 256), n, t->nvf),
+                         dim3(256), 0, t->stream, nullptr, t->fc, d_list, t->fsz,
+                         (size_t)0, (size_t)t->cap * t->fsz);
+      AFH_LAUNCH_CHECK("k_copy_boxes");
+    }
+    AFH_HIP(hipStreamSynchronize(t->stream));
+    hipFree(d_list);
+    d_list = nullptr;
+  }
+  if (!in_place && !kept.empty()) {
     if ((e = device_list(kept, &d_list))) return e;
     const unsigned n = (unsigned)kept.size();
     hipLaunchKernelGGL(k_copy_boxes, dim3((unsigned)((t->bsz + 255) / 256), n, t->nvc),
                        dim3(256), 0, t->stream, o->cc, t->cc, d_list, t->bsz,
-                       (size_t)o->nb * o->bsz, (size_t)t->nb * t->bsz);
+                       (size_t)o->cap * o->bsz, (size_t)t->cap * t->bsz);
     AFH_LAUNCH_CHECK("k_copy_boxes");
     if (t->nvf > 0) {
       hipLaunchKernelGGL(k_copy_boxes, dim3((unsigned)((t->fsz + 255) / 256), n, t->nvf),
                          dim3(256), 0, t->stream, o->fc, t->fc, d_list, t->fsz,
-                         (size_t)o->nb * o->fsz, (size_t)t->nb * t->fsz);
+                         (size_t)o->cap * o->fsz, (size_t)t->cap * t->fsz);
       AFH_LAUNCH_CHECK("k_copy_boxes");
     }
     AFH_HIP(hipStreamSynchronize(t->stream));

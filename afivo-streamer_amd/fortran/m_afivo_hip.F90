@@ -91,6 +91,7 @@ module m_afivo_hip
      type(c_ptr)        :: lvl_ids = c_null_ptr, lvl_ids_off = c_null_ptr
      type(c_ptr)        :: lvl_leaves = c_null_ptr, lvl_leaves_off = c_null_ptr
      type(c_ptr)        :: lvl_parents = c_null_ptr, lvl_parents_off = c_null_ptr
+     integer(c_int32_t) :: box_capacity = 0
   end type afh_tree_desc
 
   type, bind(C) :: afh_bc

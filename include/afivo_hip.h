@@ -119,6 +119,10 @@ typedef struct afh_tree_desc {
   const int32_t *lvl_ids, *lvl_ids_off;
   const int32_t *lvl_leaves, *lvl_leaves_off;
   const int32_t *lvl_parents, *lvl_parents_off;
+  /* boxes the device data pools hold (>= n_boxes; 0: n_boxes) -- afivo's
+   * box_limit: afh_tree_regrid keeps the data in place when the new tree
+   * fits, instead of copying it into new pools */
+  int32_t box_capacity;
 } afh_tree_desc;
 
 /* One face of a physical boundary: replaces an af_subr_bc callback whose

@@ -16,9 +16,9 @@ from afh.streamer import IV, N_VAR_FACE, StreamerCase
 VARS = ["e0", "pos0", "neg0", "phi", "efld"]
 
 
-def _old_tree(lib):
+def _old_tree(lib, box_capacity=0):
     g = golden.load("regrid8")
-    t = Tree(lib, g, int(g["n_var_cell"]), N_VAR_FACE)
+    t = Tree(lib, g, int(g["n_var_cell"]), N_VAR_FACE, box_capacity=box_capacity)
     neumann0 = [(capi.BC_NEUMANN, 0.0)] * 6
     for sp in ("e", "pos", "neg"):
         for s in range(3):
@@ -38,8 +38,8 @@ def _old_tree(lib):
     return g, t
 
 
-def _regrid(lib):
-    g, t = _old_tree(lib)
+def _regrid(lib, box_capacity=0):
+    g, t = _old_tree(lib, box_capacity)
     after = {k[len("after_"):]: g[k] for k in g if k.startswith("after_")}
     t2 = t.regrid(after)
     ids = np.concatenate([np.asarray(after["lvl_ids_%d" % l]) for l in
@@ -66,8 +66,11 @@ def test_oracle_regrid_matches_reference():
 
 
 @pytest.mark.gpu
-def test_hip_regrid_matches_reference_and_oracle():
-    g, th, ids = _regrid(capi.hip_library())
+@pytest.mark.parametrize("capacity", [0, 128])
+def test_hip_regrid_matches_reference_and_oracle(capacity):
+    """capacity 0: new pools (copy); 128: the 73 new boxes fit the old
+    pools, the regrid works in place."""
+    g, th, ids = _regrid(capi.hip_library(), capacity)
     _, to, _ = _regrid(capi.oracle_library())
     for v in VARS:
         a = th.get_cc(golden.IVS[v])[ids]
