@@ -222,6 +222,8 @@ def main():
                          "algorithmic_bytes_per_launch": bytes_per_launch,
                          "launches": nl.value},
             "last_residual": last[0][-1] if last[0] else None,
+            # one FAS V(2,2)-cycle per step (SURVEY.md 8(d) reports both)
+            "vcycles_per_s": args.steps / elapsed,
         }
         if sharded:
             out["exchanges_per_step"] = case.shard.n_exchanges / max(1, args.steps + args.warmup + 1)
