@@ -82,7 +82,9 @@ class FluidDesc(C.Structure):
                 ("limiter", i32), ("gas_number_density", f64), ("td", LT),
                 ("chem", LT), ("n_reactions", i32),
                 ("reactions", C.POINTER(Reaction)), ("dt_chemistry_nmin", f64),
-                ("gas_temperature", f64), ("td_energy_col", i32)]
+                ("gas_temperature", f64), ("td_energy_col", i32),
+                ("i_gas_dens", i32), ("n_gas_species", i32),
+                ("gas_fractions", f64 * 8)]
 
 
 class MgDesc(C.Structure):

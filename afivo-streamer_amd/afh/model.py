@@ -238,12 +238,16 @@ class Multigrid:
 
 
 class Fluid:
-    """The m_fluid / m_chemistry state (LFA, constant gas density)."""
+    """The m_fluid / m_chemistry state (LFA). A variable gas density
+    (gas_constant_density = .false.) is cc variable `i_gas_dens`; the gas
+    species (densities gas_fractions * N) then come first in the reactions'
+    species indices, as in m_chemistry.f90:193-197."""
 
     def __init__(self, tree, species_iv, species_charge, i_electron, i_efld,
                  f_flux, f_field, gas_number_density, td, chem, reactions,
                  limiter=capi.LIM_KOREN, dt_chemistry_nmin=-1.0,
-                 gas_temperature=300.0, td_energy_col=0):
+                 gas_temperature=300.0, td_energy_col=0, i_gas_dens=0,
+                 gas_fractions=()):
         self.tree = tree
         self.lib = tree.lib
         d = capi.FluidDesc()
@@ -281,6 +285,9 @@ class Fluid:
         d.dt_chemistry_nmin = dt_chemistry_nmin
         d.gas_temperature = gas_temperature
         d.td_energy_col = td_energy_col
+        d.i_gas_dens = i_gas_dens
+        d.n_gas_species = len(gas_fractions)
+        d.gas_fractions[:len(gas_fractions)] = list(gas_fractions)
         h = C.c_void_p()
         self.lib.call("fluid_create", tree.h, C.byref(d), C.byref(h))
         self.h = h

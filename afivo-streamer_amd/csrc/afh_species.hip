@@ -201,6 +201,10 @@ struct FluxArgs {
   const double *gc2;
   DevLT td;
   double N_inv;
+  // variable gas density (cc variable, ghost cells filled) or null: then
+  // N_inv = 2 / (N_{f-1} + N_f) per face (src/m_fluid.f90:146-154);
+  // only k_flux_staged reads it
+  const double *Ng;
   double inv_dx[3];   // 1/dr per dimension of this level
   int lim;
 };
@@ -314,6 +318,7 @@ __global__ void __launch_bounds__(256, AFH_FLUX_MINW)
   const double *__restrict__ Ef = A.Ef + (size_t)(id - 1) * fsz;
   double *__restrict__ F = A.F + (size_t)(id - 1) * fsz;
   const double *__restrict__ g2 = A.gc2 + (size_t)(id - 1) * 6 * nc * nc;
+  const double *__restrict__ Ng = A.Ng ? A.Ng + (size_t)(id - 1) * bsz : nullptr;
   const int c0 = (k * ng + j) * ng + i;
   const int fcell = ((k - 1) * nf + (j - 1)) * nf + (i - 1);
   const int fd = nf * nf * nf;
@@ -346,14 +351,27 @@ __global__ void __launch_bounds__(256, AFH_FLUX_MINW)
     ex_lo[d] = Ef[d * fd + fcell];
     ex_hi[d] = need_hi[d] ? Ef[d * fd + fcell + fst[d]] : 0.0;
   }
+  // 1/N at the low and high face of every dimension
+  double ni_lo[3], ni_hi[3];
+  if (Ng) {
+    const double N0 = Ng[c0];
+#pragma unroll
+    for (int d = 0; d < 3; d++) {
+      ni_lo[d] = 2 / (Ng[c0 - st[d]] + N0);
+      ni_hi[d] = need_hi[d] ? 2 / (N0 + Ng[c0 + st[d]]) : A.N_inv;
+    }
+  } else {
+#pragma unroll
+    for (int d = 0; d < 3; d++) ni_lo[d] = ni_hi[d] = A.N_inv;
+  }
   // (2) table rows: low face of every dimension, high face where needed
   int lo_row[3], hi_row[3];
   double lo_lf[3], hi_lf[3];
 #pragma unroll
   for (int d = 0; d < 3; d++) {
-    lt_loc(A.td, 0.5 * (Em[d] + E0) * 1e21 * A.N_inv, lo_row[d], lo_lf[d]);
+    lt_loc(A.td, 0.5 * (Em[d] + E0) * 1e21 * ni_lo[d], lo_row[d], lo_lf[d]);
     if (need_hi[d])
-      lt_loc(A.td, 0.5 * (E0 + Ep[d]) * 1e21 * A.N_inv, hi_row[d], hi_lf[d]);
+      lt_loc(A.td, 0.5 * (E0 + Ep[d]) * 1e21 * ni_hi[d], hi_row[d], hi_lf[d]);
     else
       hi_row[d] = 1, hi_lf[d] = 0.0;
   }
@@ -372,12 +390,12 @@ __global__ void __launch_bounds__(256, AFH_FLUX_MINW)
   }
   // (3) fluxes and CFL (face_eval / face_vd arithmetic)
   double cfl = 0.0, smax = -HUGE_VAL;
-  auto finish = [&](const double rr[4], double lf, double ex, double &v,
-                    double &dc) {
+  auto finish = [&](const double rr[4], double lf, double ex, double ni,
+                    double &v, double &dc) {
     double mu = lf * rr[0] + (1 - lf) * rr[1];
     const double dd = lf * rr[2] + (1 - lf) * rr[3];
-    mu = mu * A.N_inv;
-    dc = dd * A.N_inv;
+    mu = mu * ni;
+    dc = dd * ni;
     v = -mu * ex;
     return mu;
   };
@@ -389,7 +407,7 @@ __global__ void __launch_bounds__(256, AFH_FLUX_MINW)
 #pragma unroll
   for (int d = 0; d < 3; d++) {
     const double u = upwind(L[d][0], L[d][1], L[d][2], L[d][3], ex_lo[d]);
-    const double mu = finish(lo_r[d], lo_lf[d], ex_lo[d], vl[d], dl[d]);
+    const double mu = finish(lo_r[d], lo_lf[d], ex_lo[d], ni_lo[d], vl[d], dl[d]);
     const double flux = vl[d] * u - dl[d] * A.inv_dx[d] * (L[d][2] - L[d][1]);
     if (active) F[d * fd + fcell] = flux;
     smax = fmax(smax, mu * u);
@@ -410,7 +428,7 @@ __global__ void __launch_bounds__(256, AFH_FLUX_MINW)
     double vh, dh;
     if (cc[d] == nc) {
       const double u = upwind(L[d][1], L[d][2], L[d][3], L[d][4], ex_hi[d]);
-      const double mu = finish(hi_r[d], hi_lf[d], ex_hi[d], vh, dh);
+      const double mu = finish(hi_r[d], hi_lf[d], ex_hi[d], ni_hi[d], vh, dh);
       const double flux = vh * u - dh * inv_dx * (L[d][3] - L[d][2]);
       if (active) F[d * fd + fcell + fst[d]] = flux;
       smax = fmax(smax, mu * u);
@@ -421,7 +439,7 @@ __global__ void __launch_bounds__(256, AFH_FLUX_MINW)
       vh = s_v[threadIdx.x + nc];
       dh = s_d[threadIdx.x + nc];
     } else {
-      finish(hi_r[d], hi_lf[d], ex_hi[d], vh, dh);
+      finish(hi_r[d], hi_lf[d], ex_hi[d], ni_hi[d], vh, dh);
     }
     const double mv = fmax(fabs(vh), fabs(vl[d]));
     const double md = fmax(dh, dl[d]);
@@ -469,6 +487,12 @@ struct UpdArgs {
   double dt;
   double dt_dr[3];  // dt / dr per dimension of this level
   double dt_chemistry_nmin;
+  // variable gas density (m_fluid.f90:339-348): N per cell, the gas species
+  // densities gas_frac * N occupy species slots ns .. ns+ng-1 (the host
+  // remaps the reactions' species indices, gas first in the reference)
+  const double *Ng;
+  int ng;
+  double gas_frac[AFH_MAX_GAS_SPECIES];
 };
 
 // Register-resident species arrays indexed by runtime reaction data: the
@@ -874,7 +898,7 @@ __global__ void k_consistent(double *__restrict__ F,
 #ifndef AFH_UPD_MINW  // minimum waves per SIMD of the update kernel
 #define AFH_UPD_MINW 1
 #endif
-template <int NS, bool SLOW, int NP = MAXPREV, bool SD = true>
+template <int NS, bool SLOW, int NP = MAXPREV, bool SD = true, bool GAS = false>
 __global__ void __launch_bounds__(256, AFH_UPD_MINW)
     k_update(UpdArgs A, const int32_t *__restrict__ ids, int nc, size_t bsz,
              size_t fsz, unsigned long long *red) {
@@ -903,7 +927,22 @@ __global__ void __launch_bounds__(256, AFH_UPD_MINW)
       dv[s] = (NP != MAXPREV && !SD) || A.der_q >= 0 ? 0.0 : A.der[s][x];
     }
     (void)der_q;
-    double y[NS], der[NS], dens[NS];
+    // GAS: slots NS .. NS+ng-1 hold the gas species
+    constexpr int NT = GAS ? NS + AFH_MAX_GAS_SPECIES : NS;
+    double y[NS], der[NT], dens[NT];
+    double field;
+    if (GAS) {
+      const double Nc = A.Ng[x];
+      field = 1e21 * (ev / Nc);
+#pragma unroll
+      for (int g = 0; g < NT - NS; g++) {
+        const double v = g < A.ng ? A.gas_frac[g] * Nc : 0.0;
+        dens[NS + g] = v > 0.0 ? v : 0.0;
+        der[NS + g] = 0.0;
+      }
+    } else {
+      field = 1e21 * A.inv_N * ev;
+    }
 #pragma unroll
     for (int s = 0; s < NS; s++) {
       double tmp = 0.0;
@@ -918,7 +957,6 @@ __global__ void __launch_bounds__(256, AFH_UPD_MINW)
       dens[s] = v > 0.0 ? v : 0.0;  // max(dens, 0.0_dp)
       der[s] = 0.0;
     }
-    const double field = 1e21 * A.inv_N * ev;
     double Te = -1.0;  // electron temperature, looked up once per cell
     for (int r = 0; r < A.nr; r++) {
       const DevReaction &R = A.reac[r];
@@ -933,7 +971,8 @@ __global__ void __launch_bounds__(256, AFH_UPD_MINW)
     if (A.last_step) {
       const double eps = 1e-100;
 #pragma unroll
-      for (int s = 0; s < NS; s++) {
+      for (int s = 0; s < NT; s++) {
+        if (s >= NS + (GAS ? A.ng : 0)) continue;
         double a, b;
         if (A.dt_chemistry_nmin > 0) {
           a = dens[s] + A.dt_chemistry_nmin;
@@ -977,7 +1016,10 @@ void launch_update(const UpdArgs &A, afh_tree *t, int l,
   const dim3 grid((n3 + 255) / 256, t->leaves.n(l));
   const auto *ids = t->leaves.at(l);
   const bool sd = A.der_q < 0;
-  if (slow)
+  if (A.Ng)
+    hipLaunchKernelGGL((k_update<NS, true, MAXPREV, true, true>), grid, dim3(256), 0,
+                       t->stream, A, ids, nc, t->bsz, t->fsz, red);
+  else if (slow)
     hipLaunchKernelGGL((k_update<NS, true>), grid, dim3(256), 0, t->stream, A,
                        ids, nc, t->bsz, t->fsz, red);
   else if (A.n_prev == 1 && !sd)
@@ -1486,6 +1528,10 @@ int32_t afh_fluid_create(afh_tree *t, const afh_fluid_desc *d, afh_fluid **out) 
     if (d->species_iv[s] == d->i_electron) f->e_index = s;
   }
   if (f->e_index < 0) return set_error(AFH_ERR_ARG, "electron not in species list");
+  const bool gas = d->i_gas_dens > 0;
+  const int ng = gas ? d->n_gas_species : 0;
+  if (gas && (d->i_gas_dens > t->nvc || ng < 0 || ng > AFH_MAX_GAS_SPECIES))
+    return set_error(AFH_ERR_ARG, "bad gas density variable / gas species count");
   if (!t->meth[d->i_electron].set)
     return set_error(AFH_ERR_STATE, "set cc methods for the electrons first");
   size_t ntd = (size_t)d->td.n_points * d->td.n_cols;
@@ -1498,7 +1544,8 @@ int32_t afh_fluid_create(afh_tree *t, const afh_fluid_desc *d, afh_fluid **out) 
     AFH_HIP(hipMemcpy(f->d_chem, d->chem.rows_cols, nch * sizeof(double),
                       hipMemcpyHostToDevice));
   const char *staged_env = getenv("AFH_FLUX_STAGED");
-  if (d->td.n_points <= FLUX_LDS_MAX_POINTS && !(staged_env && atoi(staged_env))) {
+  // a variable gas density takes k_flux_staged (per-face 1/N)
+  if (!gas && d->td.n_points <= FLUX_LDS_MAX_POINTS && !(staged_env && atoi(staged_env))) {
     const int n = d->td.n_points;
     std::vector<double> ti(2 * (size_t)n);
     for (int r = 0; r < n; r++) {
@@ -1528,12 +1575,21 @@ int32_t afh_fluid_create(afh_tree *t, const afh_fluid_desc *d, afh_fluid **out) 
     b.n_in = a.n_in;
     b.n_out = a.n_out;
     b.rate_factor = a.rate_factor;
+    // species indices: 1..ng gas, then the plasma species (the reference's
+    // order); the kernels keep the plasma species first, the gas after them
+    auto remap = [&](int ix) { return ix <= ng ? d->n_species + ix : ix - ng; };
     for (int q = 0; q < 4; q++) {
       b.c[q] = a.c[q];
-      b.ix_in[q] = a.ix_in[q];
-      b.ix_out[q] = a.ix_out[q];
+      b.ix_in[q] = q < a.n_in ? remap(a.ix_in[q]) : a.ix_in[q];
+      b.ix_out[q] = q < a.n_out ? remap(a.ix_out[q]) : a.ix_out[q];
       b.mult_out[q] = a.mult_out[q];
     }
+    for (int q = 0; q < a.n_in; q++)
+      if (a.ix_in[q] < 1 || a.ix_in[q] > ng + d->n_species)
+        return set_error(AFH_ERR_ARG, "reaction species index");
+    for (int q = 0; q < a.n_out; q++)
+      if (a.ix_out[q] < 1 || a.ix_out[q] > ng + d->n_species)
+        return set_error(AFH_ERR_ARG, "reaction species index");
   }
   AFH_HIP(hipMalloc(&f->d_reac, sizeof(DevReaction) * R.size()));
   AFH_HIP(hipMemcpy(f->d_reac, R.data(), sizeof(DevReaction) * R.size(),
@@ -1661,6 +1717,7 @@ static FluxArgs flux_args(afh_fluid *f, int iv) {
   A.gc2 = t->gc2;
   A.td = f->td;
   A.N_inv = 1 / f->d.gas_number_density;
+  A.Ng = f->d.i_gas_dens > 0 ? t->ccv(f->d.i_gas_dens) : nullptr;
   A.lim = f->d.limiter;
   return A;
 }
@@ -1708,6 +1765,9 @@ static int32_t upd_args(afh_fluid *f, double dt, int32_t s_deriv, int32_t n_prev
   A.te_col = f->d.td_energy_col;
   A.Tg = f->d.gas_temperature;
   A.inv_N = 1 / f->d.gas_number_density;
+  A.Ng = f->d.i_gas_dens > 0 ? t->ccv(f->d.i_gas_dens) : nullptr;
+  A.ng = f->d.i_gas_dens > 0 ? f->d.n_gas_species : 0;
+  for (int g = 0; g < AFH_MAX_GAS_SPECIES; g++) A.gas_frac[g] = f->d.gas_fractions[g];
   A.dt = dt;
   A.dt_chemistry_nmin = f->d.dt_chemistry_nmin;
   // algorithmic bytes per cell: each distinct species state read once, the

@@ -124,6 +124,7 @@ module m_afivo_hip
   integer(c_int32_t), parameter :: AFH_PROLONG_LIMIT = 2
   integer(c_int32_t), parameter :: AFH_RM_REF = -1, AFH_KEEP_REF = 0, AFH_DO_REF = 1
   integer, parameter :: AFH_MAX_REFINE_REGIONS = 8
+  integer, parameter :: AFH_MAX_GAS_SPECIES = 8
 
   !> default_refinement's parameters (src/m_refine.f90:10-60)
   type, bind(C) :: afh_refine_desc
@@ -167,6 +168,9 @@ module m_afivo_hip
      real(c_double)     :: dt_chemistry_nmin
      real(c_double)     :: gas_temperature = 300.0_c_double
      integer(c_int32_t) :: td_energy_col = 0
+     integer(c_int32_t) :: i_gas_dens = 0        ! variable gas density (0: constant)
+     integer(c_int32_t) :: n_gas_species = 0
+     real(c_double)     :: gas_fractions(AFH_MAX_GAS_SPECIES) = 0
   end type afh_fluid_desc
 
   type, bind(C) :: afh_mg_desc

@@ -88,6 +88,7 @@ extern "C" {
                                cosine / sine eigenbases per dimension */
 
 #define AFH_MAX_SPECIES 32
+#define AFH_MAX_GAS_SPECIES 8
 #define AFH_MAX_REACTIONS 128
 
 /* Topology of one box: the box_t fields the hot path reads
@@ -177,6 +178,15 @@ typedef struct afh_fluid_desc {
   double gas_temperature;   /* Tg (m_gas.f90:21, 300 K by default) */
   int32_t td_energy_col;    /* mean-energy column of td (td_energy_eV,
                                m_transport_data.f90:158), 0 if absent */
+  /* Variable gas density (gas_constant_density = .false.): cc variable of
+   * N (0: the constant gas_number_density). The flux then uses
+   * N_inv = 2 / (N_{f-1} + N_f) per face (m_fluid.f90:146-154) and the
+   * chemistry E/N per cell with gas species densities gas_fractions * N
+   * (m_fluid.f90:339-348): reactions index the gas species 1..n_gas_species
+   * first, then the plasma species (m_chemistry.f90:193-197). */
+  int32_t i_gas_dens;
+  int32_t n_gas_species;
+  double gas_fractions[AFH_MAX_GAS_SPECIES];
 } afh_fluid_desc;
 
 /* Multigrid options, mg_t (m_af_types.f90:572-665) + coarse solver. */

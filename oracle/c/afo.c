@@ -1428,9 +1428,24 @@ int32_t afo_fluid_create(afh_tree *t, const afh_fluid_desc *d,
   if (d->n_species < 1 || d->n_species > AFH_MAX_SPECIES ||
       d->n_reactions > AFH_MAX_REACTIONS)
     return fail(AFH_ERR_ARG, "bad species/reaction count");
+  if (d->i_gas_dens > 0 &&
+      (d->i_gas_dens > t->nvc || d->n_gas_species < 0 ||
+       d->n_gas_species > AFH_MAX_GAS_SPECIES))
+    return fail(AFH_ERR_ARG, "bad gas density variable / gas species count");
+  const int ng = d->i_gas_dens > 0 ? d->n_gas_species : 0;
+  for (int r = 0; r < d->n_reactions; r++) {
+    const afh_reaction *R = &d->reactions[r];
+    for (int q = 0; q < R->n_in; q++)
+      if (R->ix_in[q] < 1 || R->ix_in[q] > ng + d->n_species)
+        return fail(AFH_ERR_ARG, "reaction species index");
+    for (int q = 0; q < R->n_out; q++)
+      if (R->ix_out[q] < 1 || R->ix_out[q] > ng + d->n_species)
+        return fail(AFH_ERR_ARG, "reaction species index");
+  }
   afh_fluid *f = calloc(1, sizeof *f);
   f->t = t;
   f->d = *d;
+  if (d->i_gas_dens <= 0) f->d.n_gas_species = 0;
   size_t ntd = (size_t)d->td.n_points * d->td.n_cols;
   size_t nch = (size_t)d->chem.n_points * d->chem.n_cols;
   f->td = malloc(sizeof(double) * (ntd ? ntd : 1));
@@ -1709,6 +1724,8 @@ static void flux_box(afh_fluid *fl, int id, int s_deriv, double *cfl_max,
   gc2_box(t, id, i_e, cc2);
   double *ne = ccb(t, i_e, id), *E = ccb(t, fl->d.i_efld, id);
   double *F = fcb(t, fl->d.f_flux, id), *Ef = fcb(t, fl->d.f_field, id);
+  /* variable gas density: N_inv = 2 / (N_{f-1} + N_f) per face (m_fluid.f90:146-154) */
+  const double *Ng = fl->d.i_gas_dens > 0 ? ccb(t, fl->d.i_gas_dens, id) : NULL;
   size_t ncell = (size_t)nc * nc * nc;
   for (size_t q = 0; q < ncell; q++) cfl[q] = 0.0;
   double smax = -HUGE_VAL;
@@ -1717,7 +1734,7 @@ static void flux_box(afh_fluid *fl, int id, int s_deriv, double *cfl_max,
     for (int b = 1; b <= nc; b++)
       for (int a = 1; a <= nc; a++) {
         /* line along dim d; (a, b) = (i, j) of the other two dims */
-        double line[64 + 4], Ecc[64 + 2], necc[64 + 2], Ex[64 + 1];
+        double line[64 + 4], Ecc[64 + 2], necc[64 + 2], Ex[64 + 1], Nl[64 + 2];
         double v[64 + 1], dc[64 + 1], u[64 + 1];
         for (int m = -1; m <= nc + 2; m++) {
           int p[3];
@@ -1728,6 +1745,7 @@ static void flux_box(afh_fluid *fl, int id, int s_deriv, double *cfl_max,
           if (m >= 0 && m <= nc + 1) {
             Ecc[m] = E[IX(t, p[0], p[1], p[2])];
             necc[m] = ne[IX(t, p[0], p[1], p[2])];
+            Nl[m] = Ng ? Ng[IX(t, p[0], p[1], p[2])] : 0.0;
           }
           if (m >= 1 && m <= nc + 1) Ex[m - 1] = Ef[FX(t, d, p[0], p[1], p[2])];
         }
@@ -1745,9 +1763,10 @@ static void flux_box(afh_fluid *fl, int id, int s_deriv, double *cfl_max,
         }
 #undef L
         for (int fidx = 1; fidx <= nc + 1; fidx++) {
-          double tfc = 0.5 * (Ecc[fidx - 1] + Ecc[fidx]) * SI_to_Td * N_inv;
-          double mu = lt_col(&fl->d.td, 1, tfc) * N_inv;
-          double dcf = lt_col(&fl->d.td, 2, tfc) * N_inv;
+          const double ni = Ng ? 2 / (Nl[fidx - 1] + Nl[fidx]) : N_inv;
+          double tfc = 0.5 * (Ecc[fidx - 1] + Ecc[fidx]) * SI_to_Td * ni;
+          double mu = lt_col(&fl->d.td, 1, tfc) * ni;
+          double dcf = lt_col(&fl->d.td, 2, tfc) * ni;
           v[fidx - 1] = -mu * Ex[fidx - 1];
           dc[fidx - 1] = dcf;
           double flux = v[fidx - 1] * u[fidx - 1] -
@@ -1917,14 +1936,29 @@ int32_t afo_flux_update_densities(afh_fluid *fl, double dt, int32_t s_deriv,
                 tmp = tmp + w_prev[m] * ccb(t, iv + s_prev[m], id)[x];
               ccb(t, iv + s_out, id)[x] = tmp;
             }
-            /* source terms */
-            double tmpN = 1 / fl->d.gas_number_density;
-            double field = 1e21 * tmpN * E[x];
-            double dens[AFH_MAX_SPECIES], der[AFH_MAX_SPECIES];
+            /* source terms; with a variable gas density the gas species
+             * come first (densities gas_fractions * N) and the field is E/N
+             * per cell (m_fluid.f90:339-348) */
+            const int ng = fl->d.n_gas_species;
+            double field;
+            double dens[AFH_MAX_SPECIES + AFH_MAX_GAS_SPECIES];
+            double der[AFH_MAX_SPECIES + AFH_MAX_GAS_SPECIES];
+            if (fl->d.i_gas_dens > 0) {
+              const double Nc = ccb(t, fl->d.i_gas_dens, id)[x];
+              field = 1e21 * (E[x] / Nc);
+              for (int g = 0; g < ng; g++) {
+                double v = fl->d.gas_fractions[g] * Nc;
+                dens[g] = v > 0.0 ? v : 0.0;
+                der[g] = 0.0;
+              }
+            } else {
+              double tmpN = 1 / fl->d.gas_number_density;
+              field = 1e21 * tmpN * E[x];
+            }
             for (int s = 0; s < ns; s++) {
               double v = ccb(t, fl->d.species_iv[s] + s_deriv, id)[x];
-              dens[s] = v > 0.0 ? v : 0.0; /* max(dens, 0.0_dp) */
-              der[s] = 0.0;
+              dens[ng + s] = v > 0.0 ? v : 0.0; /* max(dens, 0.0_dp) */
+              der[ng + s] = 0.0;
             }
             double Te = -1.0; /* electron temperature, looked up once */
             for (int r = 0; r < nr; r++) {
@@ -1940,7 +1974,7 @@ int32_t afo_flux_update_densities(afh_fluid *fl, double dt, int32_t s_deriv,
                     der[R->ix_out[m] - 1] + rate * R->mult_out[m];
             }
             if (last_step) {
-              for (int s = 0; s < ns; s++) {
+              for (int s = 0; s < ng + ns; s++) {
                 double a, b;
                 if (fl->d.dt_chemistry_nmin > 0) {
                   a = dens[s] + fl->d.dt_chemistry_nmin;
@@ -1956,7 +1990,7 @@ int32_t afo_flux_update_densities(afh_fluid *fl, double dt, int32_t s_deriv,
             }
             for (int s = 0; s < ns; s++) {
               double *o = ccb(t, fl->d.species_iv[s] + s_out, id);
-              o[x] = o[x] + dt * der[s];
+              o[x] = o[x] + dt * der[ng + s];
             }
             /* flux divergence for the electrons */
             double *o = ccb(t, fl->d.i_electron + s_out, id);
