@@ -303,6 +303,12 @@ class Fluid:
         except Exception:
             pass
 
+    def electrode_species_bc(self, i_lsf, i_1pos_ion, box_ids, neumann_zero=True):
+        """electrode_species_bc over the electrode boxes (src/streamer.f90:578-636)."""
+        ids = _i32(box_ids)
+        self.lib.call("electrode_species_bc", self.h, i_lsf, i_1pos_ion,
+                      int(neumann_zero), len(ids), ids.ctypes.data_as(capi.P_i32))
+
     def field_set_rhs(self, i_rhs, s_in):
         self.lib.call("field_set_rhs", self.h, i_rhs, s_in)
 

@@ -1493,6 +1493,46 @@ __global__ void __launch_bounds__(256)
     masks[id - 1] = s_mask;
   }
 }
+// electrode_species_bc (src/streamer.f90:578-636): one thread per interior
+// cell of an electrode box. A cell with lsf < 0 is written only by its own
+// thread and its electron density is read only by cells with lsf < 0 next to
+// it -- which never use it (they average neighbours with lsf > 0) -- so the
+// in-place update is race-free and order-independent, as in the reference.
+struct ElecBcArgs {
+  double *sp[MAXS];
+  int ns;
+  const double *lsf;
+  double *ne, *ion;
+  int neumann_zero;
+};
+__global__ void __launch_bounds__(256)
+    k_electrode_bc(ElecBcArgs A, const int32_t *__restrict__ ids, int nc, size_t bsz) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nc * nc * nc) return;
+  int i, j, k;
+  cell3(t, nc, i, j, k);
+  const int ng = nc + 2;
+  const size_t b0 = (size_t)(ids[blockIdx.y] - 1) * bsz;
+  const int c = (k * ng + j) * ng + i;
+  const double *lsf = A.lsf + b0;
+  if (!(lsf[c] < 0)) return;
+  for (int s = 0; s < A.ns; s++) A.sp[s][b0 + c] = 0.0;
+  if (!A.neumann_zero) return;
+  const int nb[6] = {c - 1, c + 1, c - ng, c + ng, c - ng * ng, c + ng * ng};
+  int cnt = 0;
+  double sum = 0.0;  // sum(dens_nb, mask=(lsf_nb > 0)), in array order
+#pragma unroll
+  for (int m = 0; m < 6; m++)
+    if (lsf[nb[m]] > 0) {
+      cnt++;
+      sum = sum + A.ne[b0 + nb[m]];
+    }
+  if (cnt > 0) {
+    const double v = sum / cnt;
+    A.ne[b0 + c] = v;
+    A.ion[b0 + c] = v;
+  }
+}
 }  // namespace afh
 
 using namespace afh;
@@ -1508,6 +1548,8 @@ struct afh_fluid {
   // the table does not fit LDS or AFH_FLUX_STAGED=1 selects k_flux_staged
   double *d_tdi = nullptr;
   bool slow_rates = false;  // a reaction with a temperature-dependent form
+  int32_t *d_ids = nullptr;  // box list of afh_electrode_species_bc
+  int ids_cap = 0;
 };
 
 extern "C" {
@@ -1608,7 +1650,44 @@ int32_t afh_fluid_destroy(afh_fluid *f) {
   hipFree(f->d_chem);
   hipFree(f->d_reac);
   hipFree(f->d_tdi);
+  hipFree(f->d_ids);
   delete f;
+  return AFH_OK;
+}
+
+int32_t afh_electrode_species_bc(afh_fluid *f, int32_t i_lsf, int32_t i_1pos_ion,
+                                 int32_t neumann_zero, int32_t n_ids,
+                                 const int32_t *ids) {
+  if (!f) return set_error(AFH_ERR_ARG, "afh_electrode_species_bc: null");
+  afh_tree *t = f->t;
+  if (i_lsf < 1 || i_lsf > t->nvc || i_1pos_ion < 1 || i_1pos_ion > t->nvc ||
+      n_ids < 0 || (n_ids && !ids))
+    return set_error(AFH_ERR_ARG, "electrode_species_bc: bad argument");
+  for (int q = 0; q < n_ids; q++)
+    if (ids[q] < 1 || ids[q] > t->nb) return set_error(AFH_ERR_ARG, "bad box id");
+  if (!n_ids) return AFH_OK;
+  if (n_ids > f->ids_cap) {
+    // the previous list may still be read by a queued launch
+    AFH_HIP(hipStreamSynchronize(t->stream));
+    hipFree(f->d_ids);
+    f->d_ids = nullptr;
+    AFH_HIP(hipMalloc(&f->d_ids, sizeof(int32_t) * n_ids));
+    f->ids_cap = n_ids;
+  }
+  // pageable source: the copy is staged before the call returns
+  AFH_HIP(hipMemcpyAsync(f->d_ids, ids, sizeof(int32_t) * n_ids,
+                         hipMemcpyHostToDevice, t->stream));
+  ElecBcArgs A;
+  A.ns = f->d.n_species;
+  for (int s = 0; s < A.ns; s++) A.sp[s] = t->ccv(f->d.species_iv[s]);
+  A.lsf = t->ccv(i_lsf);
+  A.ne = t->ccv(f->d.i_electron);
+  A.ion = t->ccv(i_1pos_ion);
+  A.neumann_zero = neumann_zero ? 1 : 0;
+  const int n3 = t->nc * t->nc * t->nc;
+  hipLaunchKernelGGL(k_electrode_bc, dim3((n3 + 255) / 256, n_ids), dim3(256), 0,
+                     t->stream, A, f->d_ids, t->nc, t->bsz);
+  AFH_LAUNCH_CHECK("k_electrode_bc");
   return AFH_OK;
 }
 

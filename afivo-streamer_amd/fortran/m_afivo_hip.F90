@@ -407,6 +407,16 @@ module m_afivo_hip
        integer(c_int32_t) :: afh_fluid_destroy
      end function afh_fluid_destroy
 
+     !> electrode_species_bc (src/streamer.f90:578-636) over the mg_lsf_box boxes
+     function afh_electrode_species_bc(f, i_lsf, i_1pos_ion, neumann_zero, n_ids, ids) &
+          bind(C, name=afh_pfx//"electrode_species_bc")
+       import
+       type(c_ptr), value        :: f
+       integer(c_int32_t), value :: i_lsf, i_1pos_ion, neumann_zero, n_ids
+       integer(c_int32_t), intent(in) :: ids(*)
+       integer(c_int32_t)        :: afh_electrode_species_bc
+     end function afh_electrode_species_bc
+
      function afh_field_set_rhs(f, i_rhs, s_in) bind(C, name=afh_pfx//"field_set_rhs")
        import
        type(c_ptr), value        :: f

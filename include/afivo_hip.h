@@ -280,6 +280,16 @@ int32_t afh_mg_set_box_lsf(afh_mg *mg, int32_t id, int32_t n, const int32_t *ix,
 int32_t afh_fluid_create(afh_tree *t, const afh_fluid_desc *desc,
                          afh_fluid **out);
 int32_t afh_fluid_destroy(afh_fluid *f);
+/* electrode_species_bc over the boxes tagged mg_lsf_box (src/streamer.f90:
+ * 578-636, called per step by set_electrode_densities, 569-574): in every
+ * cell with lsf < 0 all plasma species (state 0, m_streamer.f90:242) are set
+ * to 0; with neumann_zero (bc_species => af_bc_neumann_zero), a cell next to
+ * a cell with lsf > 0 gets the mean electron density of those neighbours,
+ * copied to the first positive ion (i_1pos_ion). Reads the ghost cells of
+ * i_lsf and the electrons (the caller fills them, as in the reference). */
+int32_t afh_electrode_species_bc(afh_fluid *f, int32_t i_lsf, int32_t i_1pos_ion,
+                                 int32_t neumann_zero, int32_t n_ids,
+                                 const int32_t *ids);
 /* field_set_rhs (src/m_field.f90:363-401) */
 int32_t afh_field_set_rhs(afh_fluid *f, int32_t i_rhs, int32_t s_in);
 /* field_set_rhs followed by af_tree_maxabs_cc(i_rhs) (src/m_field.f90:

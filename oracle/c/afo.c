@@ -1473,6 +1473,43 @@ int32_t afo_fluid_destroy(afh_fluid *f) {
   return AFH_OK;
 }
 
+/* electrode_species_bc, src/streamer.f90:578-636 (3D branch) */
+int32_t afo_electrode_species_bc(afh_fluid *f, int32_t i_lsf, int32_t i_1pos_ion,
+                                 int32_t neumann_zero, int32_t n_ids,
+                                 const int32_t *ids) {
+  afh_tree *t = f->t;
+  if (i_lsf < 1 || i_lsf > t->nvc || i_1pos_ion < 1 || i_1pos_ion > t->nvc ||
+      n_ids < 0 || (n_ids && !ids))
+    return fail(AFH_ERR_ARG, "electrode_species_bc: bad argument");
+  for (int q = 0; q < n_ids; q++)
+    if (ids[q] < 1 || ids[q] > t->nb) return fail(AFH_ERR_ARG, "bad box id");
+  const int nc = t->nc;
+  for (int q = 0; q < n_ids; q++) {
+    const int id = ids[q];
+    const double *lsf = ccb(t, i_lsf, id);
+    double *ne = ccb(t, f->d.i_electron, id), *ion = ccb(t, i_1pos_ion, id);
+    for (int k = 1; k <= nc; k++)
+      for (int j = 1; j <= nc; j++)
+        for (int i = 1; i <= nc; i++) {
+          const size_t x = IX(t, i, j, k);
+          if (!(lsf[x] < 0)) continue;
+          for (int s = 0; s < f->d.n_species; s++) ccb(t, f->d.species_iv[s], id)[x] = 0.0;
+          const size_t nb[6] = {IX(t, i - 1, j, k), IX(t, i + 1, j, k), IX(t, i, j - 1, k),
+                                IX(t, i, j + 1, k), IX(t, i, j, k - 1), IX(t, i, j, k + 1)};
+          int cnt = 0;
+          for (int m = 0; m < 6; m++) cnt += lsf[nb[m]] > 0;
+          if (cnt > 0 && neumann_zero) {
+            double sum = 0.0; /* sum(dens_nb, mask=(lsf_nb > 0)) */
+            for (int m = 0; m < 6; m++)
+              if (lsf[nb[m]] > 0) sum = sum + ne[nb[m]];
+            ne[x] = sum / cnt;
+            ion[x] = ne[x];
+          }
+        }
+  }
+  return AFH_OK;
+}
+
 /* LT_get_loc + LT_get_col_at_loc (linear spacing, no extrapolation),
  * src/lookup_table_fortran/m_lookup_table.f90:330-406 */
 static inline double lt_col(const afh_lt *lt, int col, double x) {
