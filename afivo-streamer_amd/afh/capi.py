@@ -152,6 +152,8 @@ SIGNATURES = {
     "fluid_create": (i32, [_VP, C.POINTER(FluidDesc), _PVP]),
     "fluid_destroy": (i32, [_VP]),
     "electrode_species_bc": (i32, [_VP, i32, i32, i32, i32, P_i32]),
+    "fluid_set_rhs_output": (i32, [_VP, i32, i32]),
+    "fluid_rhs_maxabs": (i32, [_VP, i32, P_f64]),
     "field_set_rhs": (i32, [_VP, i32, i32]),
     "field_set_rhs_maxabs": (i32, [_VP, i32, i32, P_f64]),
     "flux_upwind_tree": (i32, [_VP, i32, P_f64]),

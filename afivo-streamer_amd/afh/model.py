@@ -309,6 +309,17 @@ class Fluid:
         self.lib.call("electrode_species_bc", self.h, i_lsf, i_1pos_ion,
                       int(neumann_zero), len(ids), ids.ctypes.data_as(capi.P_i32))
 
+    def set_rhs_output(self, i_rhs, ghosts=True):
+        """Fold field_set_rhs(i_rhs, s_out) into every density update (0: off);
+        ghosts=False leaves the rhs ghost cells alone (no solver reads them)."""
+        self.lib.call("fluid_set_rhs_output", self.h, i_rhs, int(ghosts))
+
+    def rhs_maxabs(self, s_out):
+        """max|rhs| of the rhs the last update wrote for state s_out."""
+        out = C.c_double()
+        self.lib.call("fluid_rhs_maxabs", self.h, s_out, C.byref(out))
+        return out.value
+
     def field_set_rhs(self, i_rhs, s_in):
         self.lib.call("field_set_rhs", self.h, i_rhs, s_in)
 

@@ -81,6 +81,7 @@ class StreamerCase:
         # keep the face fluxes of the species step in FV["flux"] (the fused
         # device step otherwise leaves them on chip)
         self.store_flux = False
+        self._rhs_state = None  # state whose rhs the last update wrote
         self.mg = Multigrid(t, IV["phi"], IV["rhs"], IV["tmp"],
                             coarse_cycles=coarse_cycles)
         self._mg_helm = {}
@@ -119,6 +120,13 @@ class StreamerCase:
         for bid, (ix, dd, bv) in lsf_faces.items():
             self.mg.set_box_lsf(bid, ix, dd, bv, i_lsf)
 
+    def fuse_rhs(self, on=True, ghosts=True):
+        """Fold field_set_rhs of the new state into every density update
+        (afh_fluid_set_rhs_output): the field_compute that follows reuses it."""
+        self.fluid.set_rhs_output(IV["rhs"] if on else 0, ghosts)
+        self._rhs_state = None
+        self._fused_rhs = on
+
     def set_voltage(self, voltage):
         self.voltage = voltage
         self.tree.set_bc(IV["phi"], 6, capi.BC_DIRICHLET, voltage)
@@ -136,12 +144,17 @@ class StreamerCase:
         """m_field.f90:405-485 with have_guess = .true.; returns residuals."""
         residuals = []
         threshold = None
+        fused = self._rhs_state == s_in
+        self._rhs_state = None
         if check_residual:
-            max_rhs = self.fluid.field_set_rhs_maxabs(IV["rhs"], s_in)
+            if fused:
+                max_rhs = self.fluid.rhs_maxabs(s_in)
+            else:
+                max_rhs = self.fluid.field_set_rhs_maxabs(IV["rhs"], s_in)
             threshold = max(1e-6, max_rhs * max_rel_residual,
                             1e-10 * abs(self.voltage) /
                             (self.domain[2] * self.min_dr()))
-        else:
+        elif not fused:
             self.fluid.field_set_rhs(IV["rhs"], s_in)
         for _ in range(n_vcycles):
             if check_residual:
@@ -158,8 +171,16 @@ class StreamerCase:
         """m_fluid.f90:21-99 (without the CFL/ dt_max combination)."""
         if i_step > 1:
             self.field_compute(s_deriv, **field_kw)
-        return list(self.fluid.forward_euler(dt, s_deriv, s_prev, w_prev, s_out,
-                                             i_step == n_steps, self.store_flux))
+        return list(self.species_step(dt, s_deriv, s_prev, w_prev, s_out,
+                                      i_step == n_steps))
+
+    def species_step(self, dt, s_deriv, s_prev, w_prev, s_out, last_step):
+        """forward_euler's species part (m_fluid.f90:56-70): flux_upwind_tree +
+        flux_update_densities; returns dt_limits(1:4)."""
+        lim = self.fluid.forward_euler(dt, s_deriv, s_prev, w_prev, s_out,
+                                       last_step, self.store_flux)
+        self._rhs_state = s_out if getattr(self, "_fused_rhs", False) else None
+        return lim
 
     def heun_step(self, dt, **field_kw):
         """af_advance with af_heuns_method (m_af_advance.f90:160-164)."""

@@ -1017,7 +1017,10 @@ __global__ void k_gradient(const double *__restrict__ phi,
 // blocks (NC x R rows) so no index divisions, and fac/dr precomputed on the
 // host (every box of a level has the same dr, so the quotient is bitwise the
 // one mg_box_lpl_gradient computes per box).
-template <int NC>
+// Each thread owns a column of K cells in k: the K + 2 phi values of the
+// column are loaded once (the z differences of neighbouring cells share them),
+// and every load of the column is issued before the first store.
+template <int NC, int K>
 __global__ void __launch_bounds__(256)
     k_gradient_t(const double *__restrict__ phi, double *__restrict__ fcv,
                  double *__restrict__ nrm, const int32_t *__restrict__ ids,
@@ -1027,38 +1030,59 @@ __global__ void __launch_bounds__(256)
   constexpr size_t SJ = NG, SK = (size_t)NG * NG, D3 = (size_t)NF * NF * NF;
   const int i = threadIdx.x % NC + 1;
   const int j = (blockIdx.x % (NC / R)) * R + threadIdx.x / NC + 1;
-  const int k = blockIdx.x / (NC / R) + 1;
+  const int k0 = (blockIdx.x / (NC / R)) * K + 1;
   const int id = ids[blockIdx.y];
   const double *p = phi + (size_t)(id - 1) * bsz;
   double *f = fcv + (size_t)(id - 1) * fsz;
-  const size_t c = ((size_t)k * NG + j) * NG + i;
-  const double fxl = ix_ * (p[c] - p[c - 1]), fxh = ix_ * (p[c + 1] - p[c]);
-  const double fyl = iy * (p[c] - p[c - SJ]), fyh = iy * (p[c + SJ] - p[c]);
-  const double fzl = iz * (p[c] - p[c - SK]), fzh = iz * (p[c + SK] - p[c]);
-  const size_t fb = ((size_t)(k - 1) * NF + (j - 1)) * NF + (i - 1);
-  f[fb] = fxl;
-  if (i == NC) f[fb + 1] = fxh;
-  f[D3 + fb] = fyl;
-  if (j == NC) f[D3 + fb + NF] = fyh;
-  f[2 * D3 + fb] = fzl;
-  if (k == NC) f[2 * D3 + fb + (size_t)NF * NF] = fzh;
-  if (nrm) {
-    const double a = fxl + fxh, b = fyl + fyh, cc = fzl + fzh;
-    nrm[(size_t)(id - 1) * bsz + c] = 0.5 * sqrt(a * a + b * b + cc * cc);
+  double *nb = nrm ? nrm + (size_t)(id - 1) * bsz : nullptr;
+  const size_t c0 = ((size_t)k0 * NG + j) * NG + i;
+  double pc[K + 2], xm[K], xp[K], ym[K], yp[K];
+#pragma unroll
+  for (int q = 0; q < K + 2; q++) pc[q] = p[c0 + (q - 1) * SK];
+#pragma unroll
+  for (int q = 0; q < K; q++) {
+    const size_t c = c0 + q * SK;
+    xm[q] = p[c - 1];
+    xp[q] = p[c + 1];
+    ym[q] = p[c - SJ];
+    yp[q] = p[c + SJ];
+  }
+#pragma unroll
+  for (int q = 0; q < K; q++) {
+    const int k = k0 + q;
+    const double pv = pc[q + 1];
+    const double fxl = ix_ * (pv - xm[q]), fxh = ix_ * (xp[q] - pv);
+    const double fyl = iy * (pv - ym[q]), fyh = iy * (yp[q] - pv);
+    const double fzl = iz * (pv - pc[q]), fzh = iz * (pc[q + 2] - pv);
+    const size_t fb = ((size_t)(k - 1) * NF + (j - 1)) * NF + (i - 1);
+    f[fb] = fxl;
+    if (i == NC) f[fb + 1] = fxh;
+    f[D3 + fb] = fyl;
+    if (j == NC) f[D3 + fb + NF] = fyh;
+    f[2 * D3 + fb] = fzl;
+    if (k == NC) f[2 * D3 + fb + (size_t)NF * NF] = fzh;
+    if (nb) {
+      const double a = fxl + fxh, b = fyl + fyh, cc = fzl + fzh;
+      nb[c0 + q * SK] = 0.5 * sqrt(a * a + b * b + cc * cc);
+    }
   }
 }
 
+#ifndef AFH_GRAD_K  // cells per thread column of k_gradient_t
+#define AFH_GRAD_K 4
+#endif
 template <int NC>
 static void launch_gradient(afh_tree *t, const double *phi, double *fcv,
                             double *nrm, double fac) {
   constexpr int R = 256 / NC < NC ? 256 / NC : NC;
+  constexpr int K = NC >= AFH_GRAD_K ? AFH_GRAD_K : 1;
   for (int l = 1; l <= t->nlvl; l++) {
     const int n = t->ids.n(l);
     if (!n) continue;
     const double *dr = &t->lvl_dr[3 * (l - 1)];
-    hipLaunchKernelGGL(k_gradient_t<NC>, dim3((NC / R) * NC, n), dim3(NC * R),
-                       0, t->stream, phi, fcv, nrm, t->ids.at(l), t->bsz,
-                       t->fsz, fac / dr[0], fac / dr[1], fac / dr[2]);
+    hipLaunchKernelGGL((k_gradient_t<NC, K>), dim3((NC / R) * (NC / K), n),
+                       dim3(NC * R), 0, t->stream, phi, fcv, nrm, t->ids.at(l),
+                       t->bsz, t->fsz, fac / dr[0], fac / dr[1], fac / dr[2]);
   }
 }
 

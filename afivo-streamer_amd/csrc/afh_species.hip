@@ -101,6 +101,33 @@ __global__ void __launch_bounds__(256)
   if (MAX) block_max_to_shard(mx, red);
 }
 
+// k_set_rhs on the ghost shell of a box only (the interior is written by
+// k_update with an rhs output): face blockIdx.y, one thread per cell of an
+// ng x ng face; z faces whole, y faces without the z ghost rows, x faces
+// without the y and z ghost rows, so every shell cell is written once.
+__global__ void __launch_bounds__(256)
+    k_rhs_shell(double *__restrict__ rhs, RhsArgs A,
+                const int32_t *__restrict__ ids, size_t bsz, int ng) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= ng * ng) return;
+  const int a = t % ng, b = t / ng, f = blockIdx.y, d = f >> 1;
+  const int side = (f & 1) ? ng - 1 : 0;
+  int i, j, k;
+  if (d == 2) {
+    i = a, j = b, k = side;
+  } else if (d == 1) {
+    if (b == 0 || b == ng - 1) return;
+    i = a, j = side, k = b;
+  } else {
+    if (a == 0 || a == ng - 1 || b == 0 || b == ng - 1) return;
+    i = side, j = a, k = b;
+  }
+  const size_t o = (size_t)(ids[blockIdx.z] - 1) * bsz + ((size_t)k * ng + j) * ng + i;
+  double r = 0.0;
+  for (int s = 0; s < A.n; s++) r = r + A.q[s] * A.sp[s][o];
+  rhs[o] = r;
+}
+
 // ------------------------------------------------------------ gc2
 __global__ void k_gc2(double *__restrict__ v, double *__restrict__ gc2,
                       const afh_box_meta *__restrict__ meta,
@@ -493,6 +520,12 @@ struct UpdArgs {
   const double *Ng;
   int ng;
   double gas_frac[AFH_MAX_GAS_SPECIES];
+  // field_set_rhs of the output state folded into the update (or null):
+  // rhs = sum over charged species of rq[s] * n_out[s], in species order
+  // (src/m_field.f90:363-401), max|rhs| into rhs_red
+  double *rhs;
+  double rq[MAXS];
+  unsigned long long *rhs_red;
 };
 
 // Register-resident species arrays indexed by runtime reaction data: the
@@ -904,7 +937,7 @@ __global__ void __launch_bounds__(256, AFH_UPD_MINW)
              size_t fsz, unsigned long long *red) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   const int id = ids[blockIdx.y];
-  double cmin = 1e100;
+  double cmin = 1e100, rmax = 0.0;
   if (t < nc * nc * nc) {
     int i, j, k;
     cell3(t, nc, i, j, k);
@@ -995,7 +1028,16 @@ __global__ void __launch_bounds__(256, AFH_UPD_MINW)
       if (s == A.e_index) y[s] = y[s] + div + dvy + dvz;
 #pragma unroll
     for (int s = 0; s < NS; s++) A.out[s][x] = y[s];
+    if (A.rhs) {
+      double r = 0.0;
+#pragma unroll
+      for (int s = 0; s < NS; s++)
+        if (A.rq[s] != 0.0) r = r + A.rq[s] * y[s];
+      A.rhs[x] = r;
+      rmax = fabs(r);
+    }
   }
+  if (A.rhs) block_max_to_shard(rmax, A.rhs_red);
   if (A.last_step) {
     for (int o = 32; o > 0; o >>= 1) cmin = fmin(cmin, __shfl_xor(cmin, o, 64));
     __shared__ double r1[4];
@@ -1550,6 +1592,10 @@ struct afh_fluid {
   bool slow_rates = false;  // a reaction with a temperature-dependent form
   int32_t *d_ids = nullptr;  // box list of afh_electrode_species_bc
   int ids_cap = 0;
+  // afh_fluid_set_rhs_output: the update also writes field_set_rhs(rhs_iv,
+  // s_out); rhs_state = the state it was written for (-1: none)
+  int rhs_iv = 0, rhs_state = -1;
+  bool rhs_ghosts = false;
 };
 
 extern "C" {
@@ -1691,24 +1737,52 @@ int32_t afh_electrode_species_bc(afh_fluid *f, int32_t i_lsf, int32_t i_1pos_ion
   return AFH_OK;
 }
 
+int32_t afh_fluid_set_rhs_output(afh_fluid *f, int32_t i_rhs, int32_t ghosts) {
+  if (!f) return set_error(AFH_ERR_ARG, "afh_fluid_set_rhs_output: null");
+  if (i_rhs < 0 || i_rhs > f->t->nvc) return set_error(AFH_ERR_ARG, "bad i_rhs");
+  f->rhs_iv = i_rhs;
+  f->rhs_ghosts = ghosts != 0;
+  f->rhs_state = -1;
+  return AFH_OK;
+}
+
+int32_t afh_fluid_rhs_maxabs(afh_fluid *f, int32_t s_out, double *max_rhs) {
+  if (!f || !max_rhs) return set_error(AFH_ERR_ARG, "afh_fluid_rhs_maxabs: null");
+  if (f->rhs_iv <= 0 || f->rhs_state < 0 || f->rhs_state != s_out)
+    return set_error(AFH_ERR_STATE, "no rhs output of state %d from the last update",
+                     s_out);
+  afh_tree *t = f->t;
+  int32_t e;
+  if ((e = red_fetch(t, 4, 1, max_rhs))) return e;
+  return call_hook(t, AFH_HOOK_MAX, 0, f->rhs_iv, max_rhs, 1);
+}
+
 }  // extern "C"
 
 // field_set_rhs; with max_out, also af_tree_maxabs_cc(i_rhs) (reduction
 // slot 3, the one afh_tree_maxabs_cc uses), folded into the same pass
-static int32_t set_rhs_impl(afh_fluid *f, int32_t i_rhs, int32_t s_in,
-                            double *max_out) {
-  if (!f) return set_error(AFH_ERR_ARG, "null fluid");
+// -UC_elem_charge / UC_eps0 (src/m_field.f90:377-380)
+static constexpr double RHS_FAC = -1.6022e-19 / 8.8541878176e-12;
+
+static RhsArgs rhs_args(afh_fluid *f, int32_t s_in) {
   afh_tree *t = f->t;
-  if (i_rhs < 1 || i_rhs > t->nvc) return set_error(AFH_ERR_ARG, "bad i_rhs");
-  const double fac = -1.6022e-19 / 8.8541878176e-12;  // -UC_elem_charge/UC_eps0
   RhsArgs A;
   A.n = 0;
   for (int s = 0; s < f->d.n_species; s++) {
     if (f->d.species_charge[s] == 0) continue;
     A.sp[A.n] = t->ccv(f->d.species_iv[s] + s_in);
-    A.q[A.n] = f->d.species_charge[s] * fac;
+    A.q[A.n] = f->d.species_charge[s] * RHS_FAC;
     A.n++;
   }
+  return A;
+}
+
+static int32_t set_rhs_impl(afh_fluid *f, int32_t i_rhs, int32_t s_in,
+                            double *max_out) {
+  if (!f) return set_error(AFH_ERR_ARG, "null fluid");
+  afh_tree *t = f->t;
+  if (i_rhs < 1 || i_rhs > t->nvc) return set_error(AFH_ERR_ARG, "bad i_rhs");
+  const RhsArgs A = rhs_args(f, s_in);
   int32_t e;
   auto *red = reinterpret_cast<unsigned long long *>(t->scratch) + 3 * RED_SHARDS;
   if (max_out && (e = red_init(t, 3, 0.0))) return e;
@@ -1847,6 +1921,9 @@ static int32_t upd_args(afh_fluid *f, double dt, int32_t s_deriv, int32_t n_prev
   A.Ng = f->d.i_gas_dens > 0 ? t->ccv(f->d.i_gas_dens) : nullptr;
   A.ng = f->d.i_gas_dens > 0 ? f->d.n_gas_species : 0;
   for (int g = 0; g < AFH_MAX_GAS_SPECIES; g++) A.gas_frac[g] = f->d.gas_fractions[g];
+  A.rhs = f->rhs_iv > 0 ? t->ccv(f->rhs_iv) : nullptr;
+  for (int s = 0; s < A.ns; s++) A.rq[s] = f->d.species_charge[s] * RHS_FAC;
+  A.rhs_red = reinterpret_cast<unsigned long long *>(t->scratch) + 4 * RED_SHARDS;
   A.dt = dt;
   A.dt_chemistry_nmin = f->d.dt_chemistry_nmin;
   // algorithmic bytes per cell: each distinct species state read once, the
@@ -1854,7 +1931,7 @@ static int32_t upd_args(afh_fluid *f, double dt, int32_t s_deriv, int32_t n_prev
   int distinct = n_prev;
   for (int q = 0; q < n_prev; q++) distinct -= (s_prev[q] == s_deriv) ? 1 : 0;
   distinct += 1;
-  upd_bytes = 8.0 * (A.ns * (distinct + 1) + 4);
+  upd_bytes = 8.0 * (A.ns * (distinct + 1) + 4 + (A.rhs ? 1 : 0));
   return AFH_OK;
 }
 
@@ -1926,6 +2003,8 @@ int32_t afh_flux_update_densities(afh_fluid *f, double dt, int32_t s_deriv,
                     upd_bytes)))
     return e;
   if ((e = red_init(t, 2, 1e100))) return e;
+  f->rhs_state = -1;
+  if (A.rhs && (e = red_init(t, 4, 0.0))) return e;
   auto *red = reinterpret_cast<unsigned long long *>(t->scratch) + 2 * RED_SHARDS;
   for (int l = 1; l <= t->nlvl; l++) {
     const int n = t->leaves.n(l);
@@ -1941,6 +2020,21 @@ int32_t afh_flux_update_densities(afh_fluid *f, double dt, int32_t s_deriv,
     }
     prof_end(t, AFH_PROF_UPDATE, upd_bytes * n3 * n);
     AFH_LAUNCH_CHECK("k_update");
+  }
+  if (A.rhs) {
+    // the ghost shell of rhs from the ghost cells of the new state (the
+    // update leaves them as they are), then max|rhs| folded
+    const RhsArgs R = rhs_args(f, s_out);
+    for (int l = 1; l <= t->nlvl && f->rhs_ghosts; l++) {
+      const int n = t->leaves.n(l);
+      if (!n) continue;
+      hipLaunchKernelGGL(k_rhs_shell, dim3((t->ng * t->ng + 255) / 256, 6, n),
+                         dim3(256), 0, t->stream, A.rhs, R, t->leaves.at(l),
+                         t->bsz, t->ng);
+      AFH_LAUNCH_CHECK("k_rhs_shell");
+    }
+    if ((e = red_finish(t, 4, true))) return e;
+    f->rhs_state = s_out;
   }
   double r = 1e100;
   if (last_step) {
@@ -2014,6 +2108,7 @@ int32_t afh_fluid_forward_euler(afh_fluid *f, double dt, int32_t s_deriv,
   const bool fused = fused_env && atoi(fused_env) && f->d_tdi &&
                      (nc == 16 || nc == 32 || nc == 64) && !t->any_cflux &&
                      !f->slow_rates && f->d.n_species <= FE_MAX_SPECIES &&
+                     f->rhs_iv == 0 && f->d.i_gas_dens <= 0 &&
                      n_prev <= 2 && !alias && f->d.limiter == AFH_LIM_KOREN;
   if (!fused) {
     double a[2], b[2];

@@ -407,6 +407,23 @@ module m_afivo_hip
        integer(c_int32_t) :: afh_fluid_destroy
      end function afh_fluid_destroy
 
+     !> field_set_rhs folded into the density update (0 disables)
+     function afh_fluid_set_rhs_output(f, i_rhs, ghosts) bind(C, name=afh_pfx//"fluid_set_rhs_output")
+       import
+       type(c_ptr), value        :: f
+       integer(c_int32_t), value :: i_rhs, ghosts
+       integer(c_int32_t)        :: afh_fluid_set_rhs_output
+     end function afh_fluid_set_rhs_output
+
+     !> max|rhs| of the rhs the last update wrote for state s_out
+     function afh_fluid_rhs_maxabs(f, s_out, max_rhs) bind(C, name=afh_pfx//"fluid_rhs_maxabs")
+       import
+       type(c_ptr), value        :: f
+       integer(c_int32_t), value :: s_out
+       real(c_double), intent(out) :: max_rhs
+       integer(c_int32_t)        :: afh_fluid_rhs_maxabs
+     end function afh_fluid_rhs_maxabs
+
      !> electrode_species_bc (src/streamer.f90:578-636) over the mg_lsf_box boxes
      function afh_electrode_species_bc(f, i_lsf, i_1pos_ion, neumann_zero, n_ids, ids) &
           bind(C, name=afh_pfx//"electrode_species_bc")

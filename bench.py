@@ -71,10 +71,10 @@ def unit_step(case, dt, k):
     dt limits."""
     if k % 2 == 0:
         res = case.field_compute(0, n_vcycles=1)
-        d = case.fluid.forward_euler(dt, 0, [0], [1.0], 1, False)
+        d = case.species_step(dt, 0, [0], [1.0], 1, False)
     else:
         res = case.field_compute(1, n_vcycles=1)
-        d = case.fluid.forward_euler(0.5 * dt, 1, [0, 1], [0.5, 0.5], 0, True)
+        d = case.species_step(0.5 * dt, 1, [0, 1], [0.5, 0.5], 0, True)
     return res, d
 
 
@@ -133,6 +133,9 @@ def main():
                     help="level-1 solve: N MG cycles, or 0 = exact separable "
                          "solve (AFH_COARSE_DIRECT)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-fused-rhs", action="store_true",
+                    help="separate field_set_rhs pass instead of the rhs folded "
+                         "into the density update (afh_fluid_set_rhs_output)")
     ap.add_argument("--replicas", action="store_true",
                     help="N>1: one independent replica per GPU instead of sharding")
     args = ap.parse_args()
@@ -157,6 +160,8 @@ def main():
     ncell = cells(case.topo)  # leaf cells of the whole tree
     dt = 1e-13
 
+    if not args.no_fused_rhs:
+        case.fuse_rhs(True, ghosts=False)
     case.field_compute(0, n_vcycles=2)  # initial potential (untimed)
     for k in range(args.warmup):
         unit_step(case, dt, k)
@@ -211,6 +216,7 @@ def main():
                        "levels": int(case.topo["highest_lvl"]),
                        "coarse_solve": ("direct" if args.coarse_cycles == 0 else
                                         "mg%d" % args.coarse_cycles),
+                       "fused_rhs": "interior" if not args.no_fused_rhs else False,
                        "parallelism": ("box-shard-%d" % world) if sharded else
                        ("replica-per-gpu" if world > 1 else "single-gpu")},
             "roofline": {"bound": "hbm",

@@ -287,6 +287,22 @@ int32_t afh_fluid_destroy(afh_fluid *f);
  * a cell with lsf > 0 gets the mean electron density of those neighbours,
  * copied to the first positive ion (i_1pos_ion). Reads the ghost cells of
  * i_lsf and the electrons (the caller fills them, as in the reference). */
+/* field_set_rhs folded into the density update: with i_rhs > 0, every
+ * afh_flux_update_densities / afh_fluid_forward_euler also writes
+ * rhs = field_set_rhs(i_rhs, s_out) (src/m_field.f90:363-401) -- the interior
+ * from the new densities in registers; with `ghosts` also the ghost shell,
+ * from the ghost cells of state s_out -- and folds max|rhs| over the leaf
+ * interiors. Without `ghosts` the rhs ghost cells keep their old values: no
+ * routine on the path reads them (the multigrid reads rhs on interiors
+ * only: gsrb, residual, restriction, coarse gather), and on 64^3 boxes the
+ * strided x-face shell costs as much as a third of a full rhs pass. This is the
+ * rhs the field_compute that follows the update in the reference
+ * (m_fluid.f90:51-53, streamer.f90 after af_advance) computes, provided no
+ * density of state s_out changes in between; afh_fluid_rhs_maxabs(s_out)
+ * then returns what afh_field_set_rhs_maxabs(i_rhs, s_out) would (an error
+ * if the last update did not write state s_out's rhs). i_rhs = 0 disables. */
+int32_t afh_fluid_set_rhs_output(afh_fluid *f, int32_t i_rhs, int32_t ghosts);
+int32_t afh_fluid_rhs_maxabs(afh_fluid *f, int32_t s_out, double *max_rhs);
 int32_t afh_electrode_species_bc(afh_fluid *f, int32_t i_lsf, int32_t i_1pos_ion,
                                  int32_t neumann_zero, int32_t n_ids,
                                  const int32_t *ids);

@@ -93,6 +93,8 @@ struct afh_fluid {
   afh_fluid_desc d;
   double *td, *chem;
   afh_reaction reac[AFH_MAX_REACTIONS];
+  int rhs_iv, rhs_state, rhs_ghosts; /* afo_fluid_set_rhs_output */
+  double rhs_max;
 };
 
 /* ---------------------------------------------------------------- tables
@@ -1473,6 +1475,20 @@ int32_t afo_fluid_destroy(afh_fluid *f) {
   return AFH_OK;
 }
 
+int32_t afo_fluid_set_rhs_output(afh_fluid *f, int32_t i_rhs, int32_t ghosts) {
+  if (i_rhs < 0 || i_rhs > f->t->nvc) return fail(AFH_ERR_ARG, "bad i_rhs");
+  f->rhs_iv = i_rhs;
+  f->rhs_ghosts = ghosts != 0;
+  f->rhs_state = -1;
+  return AFH_OK;
+}
+int32_t afo_fluid_rhs_maxabs(afh_fluid *f, int32_t s_out, double *max_rhs) {
+  if (f->rhs_iv <= 0 || f->rhs_state < 0 || f->rhs_state != s_out)
+    return fail(AFH_ERR_STATE, "no rhs output of state %d from the last update", s_out);
+  *max_rhs = f->rhs_max;
+  return hook(f->t, AFH_HOOK_MAX, 0, f->rhs_iv, max_rhs, 1);
+}
+
 /* electrode_species_bc, src/streamer.f90:578-636 (3D branch) */
 int32_t afo_electrode_species_bc(afh_fluid *f, int32_t i_lsf, int32_t i_1pos_ion,
                                  int32_t neumann_zero, int32_t n_ids,
@@ -2037,6 +2053,49 @@ int32_t afo_flux_update_densities(afh_fluid *fl, double dt, int32_t s_deriv,
                    dt_dr[2] * (F[FX(t, 2, i, j, k)] - F[FX(t, 2, i, j, k + 1)]);
           }
     }
+  }
+  /* field_set_rhs of the new state folded into the update (the device does
+   * it in the same pass); max|rhs| over the leaf interiors, hook deferred to
+   * afo_fluid_rhs_maxabs as on the device */
+  fl->rhs_state = -1;
+  if (fl->rhs_iv > 0 && fl->rhs_ghosts) {
+    int32_t e = afo_field_set_rhs(fl, fl->rhs_iv, s_out);
+    if (e) return e;
+  } else if (fl->rhs_iv > 0) {
+    /* interiors only, the arithmetic of afo_field_set_rhs */
+    const double fac = -1.6022e-19 / 8.8541878176e-12;
+    for (int l = 1; l <= t->nlvl; l++)
+      for (int q = 0; q < LVL_N(t, leaves, l); q++) {
+        const int id = LVL_AT(t, leaves, l, q);
+        double *r = ccb(t, fl->rhs_iv, id);
+        for (int k = 1; k <= nc; k++)
+          for (int j = 1; j <= nc; j++)
+            for (int i = 1; i <= nc; i++) {
+              const size_t x = IX(t, i, j, k);
+              double v = 0.0;
+              for (int s = 0; s < fl->d.n_species; s++) {
+                if (fl->d.species_charge[s] == 0) continue;
+                v = v + fl->d.species_charge[s] * fac *
+                            ccb(t, fl->d.species_iv[s] + s_out, id)[x];
+              }
+              r[x] = v;
+            }
+      }
+  }
+  if (fl->rhs_iv > 0) {
+    double mx = 0.0;
+    for (int l = 1; l <= t->nlvl; l++)
+      for (int q = 0; q < LVL_N(t, leaves, l); q++) {
+        const double *c = ccb(t, fl->rhs_iv, LVL_AT(t, leaves, l, q));
+        for (int k = 1; k <= nc; k++)
+          for (int j = 1; j <= nc; j++)
+            for (int i = 1; i <= nc; i++) {
+              const double v = fabs(c[IX(t, i, j, k)]);
+              if (v > mx) mx = v;
+            }
+      }
+    fl->rhs_max = mx;
+    fl->rhs_state = s_out;
   }
   if (last_step && hook(t, AFH_HOOK_MIN, 0, 0, &chem_min, 1)) return AFH_ERR_STATE;
   dt_lim[0] = last_step ? chem_min : 1e100;
