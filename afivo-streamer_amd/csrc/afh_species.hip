@@ -616,10 +616,13 @@ __device__ __forceinline__ double rate_of(const UpdArgs &A, const DevReaction &R
 // per-cell global loads of k_flux_staged (~40 vector-memory instructions per
 // cell, the texture addresser ~80 % busy) become ~12. Same expressions in the
 // same operand order: bitwise identical fluxes and limits.
-template <int NC>
+#ifndef AFH_FLUX_LDS_NT  // threads of a k_flux_lds workgroup (NC * rows)
+#define AFH_FLUX_LDS_NT 512
+#endif
+template <int NC, int NTT = AFH_FLUX_LDS_NT>
 struct FluxLds {
-  static constexpr int TJ = 256 / NC < NC ? 256 / NC : NC;  // rows per tile
-  static constexpr int NT = NC * TJ;                       // 256
+  static constexpr int TJ = NTT / NC < NC ? NTT / NC : NC;  // rows per tile
+  static constexpr int NT = NC * TJ;                       // NTT
   static constexpr int NTILE = NC / TJ;
   static constexpr int RW = NC + 4;                        // n_e row: i = -1 .. NC+2
   static constexpr int NR = TJ + 4;                        // rows j0-2 .. j0+TJ+1
@@ -653,7 +656,7 @@ __device__ __forceinline__ void lds_mu_dc(const double *T, const DevLT &lt,
 #define AFH_FLUX_LDS_MINW 4
 #endif
 template <int NC, int LIM>
-__global__ void __launch_bounds__(256, AFH_FLUX_LDS_MINW)
+__global__ void __launch_bounds__(AFH_FLUX_LDS_NT, AFH_FLUX_LDS_MINW)
     k_flux_lds(FluxArgs A, const double *__restrict__ tdi,
                const int32_t *__restrict__ ids, size_t bsz, size_t fsz,
                unsigned long long *red) {
@@ -1100,7 +1103,7 @@ __global__ void __launch_bounds__(256, AFH_FE_MINW)
     k_fe_lds(FluxArgs A, UpdArgs U, const double *__restrict__ tdi,
              const int32_t *__restrict__ ids, size_t bsz, size_t fsz,
              unsigned long long *red, int wf) {
-  using G = FluxLds<NC>;
+  using G = FluxLds<NC, 256>;
   constexpr int NG = NC + 2, NF = NC + 1, TJ = G::TJ, NT = G::NT, RW = G::RW,
                 NR = G::NR, EW = G::EW, ER = G::ER, NPE = G::NPE, EPE = G::EPE;
   // box-local offsets as 32-bit ints: scalar base + vector offset loads
@@ -2057,10 +2060,10 @@ constexpr int FE_MAX_SPECIES = 4;
 template <int NC, int NP, bool SD>
 static void launch_fe(afh_tree *t, const FluxArgs &A, const UpdArgs &U,
                       const double *tdi, int l, unsigned long long *red, int wf) {
-  const dim3 grid(t->leaves.n(l) * FluxLds<NC>::NTILE);
+  const dim3 grid(t->leaves.n(l) * FluxLds<NC, 256>::NTILE);
   const size_t lds = 2 * sizeof(double) * A.td.n_points;
   hipLaunchKernelGGL((k_fe_lds<NC, AFH_LIM_KOREN, FE_MAX_SPECIES, NP, SD>), grid,
-                     dim3(FluxLds<NC>::NT), lds, t->stream, A, U, tdi,
+                     dim3(FluxLds<NC, 256>::NT), lds, t->stream, A, U, tdi,
                      t->leaves.at(l), t->bsz, t->fsz, red, wf);
 }
 
