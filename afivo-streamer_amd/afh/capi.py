@@ -141,6 +141,8 @@ SIGNATURES = {
     "restrict_tree": (i32, [_VP, i32]),
     "tree_copy_cc": (i32, [_VP, i32, i32]),
     "tree_maxabs_cc": (i32, [_VP, i32, P_f64]),
+    "tree_sum_cc": (i32, [_VP, i32, i32, P_f64]),
+    "tree_reduce_loc": (i32, [_VP, i32, i32, P_f64, P_i32]),
     "mg_create": (i32, [_VP, C.POINTER(MgDesc), _PVP]),
     "mg_destroy": (i32, [_VP]),
     "mg_fas_vcycle": (i32, [_VP, i32, i32]),
@@ -154,6 +156,7 @@ SIGNATURES = {
     "electrode_species_bc": (i32, [_VP, i32, i32, i32, i32, P_i32]),
     "fluid_set_rhs_output": (i32, [_VP, i32, i32]),
     "fluid_rhs_maxabs": (i32, [_VP, i32, P_f64]),
+    "fluid_rhs_valid": (i32, [_VP, i32, P_i32]),
     "field_set_rhs": (i32, [_VP, i32, i32]),
     "field_set_rhs_maxabs": (i32, [_VP, i32, i32, P_f64]),
     "flux_upwind_tree": (i32, [_VP, i32, P_f64]),
@@ -171,6 +174,8 @@ SIGNATURES = {
     "plan_unpack": (i32, [_VP, i32, i32, _VP]),
 }
 HOOK_HALO, HOOK_RIMS, HOOK_RESTRICT, HOOK_MAX, HOOK_MIN, HOOK_CFLUX = 1, 2, 3, 4, 5, 6
+HOOK_SUM = 7
+RED_MAX, RED_MIN, RED_MAXABS = 1, 2, 3
 # int32_t (*)(void *ctx, int32_t kind, int32_t level, int32_t iv, double *vals,
 #             int32_t n)
 HOOK_FN = C.CFUNCTYPE(i32, C.c_void_p, i32, i32, i32, P_f64, i32)

@@ -319,7 +319,8 @@ class Shard:
 
     def _reduce(self, vals, n, op):
         torch, dist = self.torch, self.dist
-        rop = dist.ReduceOp.MAX if op == capi.HOOK_MAX else dist.ReduceOp.MIN
+        rop = {capi.HOOK_MAX: dist.ReduceOp.MAX, capi.HOOK_MIN: dist.ReduceOp.MIN,
+               capi.HOOK_SUM: dist.ReduceOp.SUM}[op]
         host = [vals[i] for i in range(n)]
         if self.device is not None and self.backend == "nccl":
             with torch.cuda.stream(self.stream):
@@ -335,7 +336,7 @@ class Shard:
 
     def _hook(self, ctx, kind, level, iv, vals, n):
         try:
-            if kind in (capi.HOOK_MAX, capi.HOOK_MIN):
+            if kind in (capi.HOOK_MAX, capi.HOOK_MIN, capi.HOOK_SUM):
                 self._reduce(vals, n, kind)
             elif kind == capi.HOOK_HALO:
                 p = self.plans.get(("halo", level))

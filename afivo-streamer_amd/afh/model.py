@@ -162,6 +162,29 @@ class Tree:
         self.lib.call("tree_maxabs_cc", self.h, iv, C.byref(out))
         return out.value
 
+    def sum_cc(self, iv, power=1):
+        """af_tree_sum_cc (m_af_utils.f90:966-1026): volume-weighted sum of
+        cc(iv)**power over the leaf interiors."""
+        out = C.c_double()
+        self.lib.call("tree_sum_cc", self.h, iv, int(power), C.byref(out))
+        return out.value
+
+    def reduce_loc(self, iv, op, with_loc=True):
+        """af_tree_max_cc / af_tree_min_cc / af_tree_maxabs_cc (op =
+        capi.RED_MAX / RED_MIN / RED_MAXABS): (value, (id, i, j, k)) -- the
+        af_loc_t of the first extremum in the reference's loop order."""
+        out = C.c_double()
+        loc = np.zeros(4, np.int32)
+        self.lib.call("tree_reduce_loc", self.h, iv, int(op), C.byref(out),
+                      loc.ctypes.data_as(capi.P_i32) if with_loc else None)
+        return out.value, (tuple(int(x) for x in loc) if with_loc else None)
+
+    def max_cc(self, iv):
+        return self.reduce_loc(iv, capi.RED_MAX, with_loc=False)[0]
+
+    def min_cc(self, iv):
+        return self.reduce_loc(iv, capi.RED_MIN, with_loc=False)[0]
+
 
 class Multigrid:
     """mg_t bound to a tree (mg_init / mg_fas_vcycle)."""
@@ -319,6 +342,13 @@ class Fluid:
         out = C.c_double()
         self.lib.call("fluid_rhs_maxabs", self.h, s_out, C.byref(out))
         return out.value
+
+    def rhs_valid(self, s_out):
+        """Whether the rhs the last update wrote for state s_out is still
+        current (afh_fluid_rhs_valid: tracked in the library)."""
+        out = C.c_int32()
+        self.lib.call("fluid_rhs_valid", self.h, s_out, C.byref(out))
+        return bool(out.value)
 
     def field_set_rhs(self, i_rhs, s_in):
         self.lib.call("field_set_rhs", self.h, i_rhs, s_in)

@@ -81,7 +81,7 @@ class StreamerCase:
         # keep the face fluxes of the species step in FV["flux"] (the fused
         # device step otherwise leaves them on chip)
         self.store_flux = False
-        self._rhs_state = None  # state whose rhs the last update wrote
+        self._fused_rhs = False  # afh_fluid_set_rhs_output active
         self.mg = Multigrid(t, IV["phi"], IV["rhs"], IV["tmp"],
                             coarse_cycles=coarse_cycles)
         self._mg_helm = {}
@@ -124,7 +124,6 @@ class StreamerCase:
         """Fold field_set_rhs of the new state into every density update
         (afh_fluid_set_rhs_output): the field_compute that follows reuses it."""
         self.fluid.set_rhs_output(IV["rhs"] if on else 0, ghosts)
-        self._rhs_state = None
         self._fused_rhs = on
 
     def set_voltage(self, voltage):
@@ -144,8 +143,8 @@ class StreamerCase:
         """m_field.f90:405-485 with have_guess = .true.; returns residuals."""
         residuals = []
         threshold = None
-        fused = self._rhs_state == s_in
-        self._rhs_state = None
+        # the library knows whether the last update's rhs of s_in is current
+        fused = self._fused_rhs and self.fluid.rhs_valid(s_in)
         if check_residual:
             if fused:
                 max_rhs = self.fluid.rhs_maxabs(s_in)
@@ -177,10 +176,8 @@ class StreamerCase:
     def species_step(self, dt, s_deriv, s_prev, w_prev, s_out, last_step):
         """forward_euler's species part (m_fluid.f90:56-70): flux_upwind_tree +
         flux_update_densities; returns dt_limits(1:4)."""
-        lim = self.fluid.forward_euler(dt, s_deriv, s_prev, w_prev, s_out,
-                                       last_step, self.store_flux)
-        self._rhs_state = s_out if getattr(self, "_fused_rhs", False) else None
-        return lim
+        return self.fluid.forward_euler(dt, s_deriv, s_prev, w_prev, s_out,
+                                        last_step, self.store_flux)
 
     def heun_step(self, dt, **field_kw):
         """af_advance with af_heuns_method (m_af_advance.f90:160-164)."""

@@ -111,6 +111,18 @@ struct afh_tree {
     int fc = 0;                // face-variable plan (8 ints per region)
   };
   std::vector<Plan> plans;
+  // afh_tree_regrid in place handed this tree's pools to the new tree: every
+  // entry point on this handle (or on a fluid / multigrid bound to it) fails
+  bool retired = false;
+  // write generation of every cc variable, bumped by the public calls that
+  // may change it (afh_fluid_rhs_valid: is a fused rhs still current?)
+  std::vector<uint64_t> gen;
+  void touch(int iv) {
+    if (iv >= 0 && iv < (int)gen.size()) gen[iv]++;
+  }
+  // per-box partial results of afh_tree_sum_cc / afh_tree_reduce_loc
+  double *d_boxred = nullptr;
+  int boxred_cap = 0;
 
   double *ccv(int iv) const { return cc + (size_t)(iv - 1) * cap * bsz; }
   // cc variable iv, or the smoother's spare image of phi for iv == 0
@@ -126,6 +138,19 @@ struct afh_tree {
 };
 
 namespace afh {
+// entry-point guard: a null or retired tree handle is an error
+inline int32_t live(const afh_tree *t, const char *what) {
+  if (!t) return set_error(AFH_ERR_ARG, "%s: null tree", what);
+  if (t->retired)
+    return set_error(AFH_ERR_STATE,
+                     "%s: tree handle retired by an in-place afh_tree_regrid", what);
+  return AFH_OK;
+}
+#define AFH_LIVE(t, what)                                                     \
+  do {                                                                        \
+    int32_t _e = ::afh::live((t), (what));                                     \
+    if (_e) return _e;                                                        \
+  } while (0)
 // per-level id lists -> one device array with offsets (frees L's old array)
 int32_t upload_list(afh_tree *t, LevelList &L,
                     const std::vector<std::vector<int32_t>> &lists);

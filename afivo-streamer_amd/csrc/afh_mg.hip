@@ -1709,7 +1709,8 @@ static inline dim3 blocks1(size_t n, int bs = 256) {
 extern "C" {
 
 int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
-  if (!t || !d || !out) return set_error(AFH_ERR_ARG, "afh_mg_create: null");
+  if (!d || !out) return set_error(AFH_ERR_ARG, "afh_mg_create: null");
+  AFH_LIVE(t, "afh_mg_create");
   if (d->i_phi < 1 || d->i_phi > t->nvc || d->i_rhs < 1 || d->i_rhs > t->nvc ||
       d->i_tmp < 1 || d->i_tmp > t->nvc)
     return set_error(AFH_ERR_ARG, "afh_mg_create: bad variable index");
@@ -2260,6 +2261,8 @@ static int32_t box_copy(afh_tree *t, int lvl, const double *src, double *dst) {
 int32_t afh_mg_fas_fmg(afh_mg *mg, int32_t set_residual, int32_t have_guess) {
   if (!mg) return set_error(AFH_ERR_ARG, "null mg");
   afh_tree *t = mg->t;
+  AFH_LIVE(t, "afh_mg_fas_fmg");
+  t->touch(mg->d.i_phi), t->touch(mg->d.i_rhs), t->touch(mg->d.i_tmp);
   const int nl = t->nlvl, i_phi = mg->d.i_phi;
   double *phi = t->ccv(i_phi), *tmp = t->ccv(mg->d.i_tmp);
   int32_t e;
@@ -2341,6 +2344,8 @@ static int32_t vcycle_impl(afh_mg *mg, int32_t set_residual, int32_t hl,
                            double *max_res) {
   if (!mg) return set_error(AFH_ERR_ARG, "null mg");
   afh_tree *t = mg->t;
+  AFH_LIVE(t, "afh_mg_fas_vcycle");
+  t->touch(mg->d.i_phi), t->touch(mg->d.i_rhs), t->touch(mg->d.i_tmp);
   const int max_lvl = (hl > 0 && hl <= t->nlvl) ? hl : t->nlvl;
   int32_t e;
   if ((e = prepare_var(mg))) return e;
@@ -2373,6 +2378,7 @@ int32_t afh_mg_compute_phi_gradient(afh_mg *mg, int32_t i_fc, double fac,
                                     int32_t i_norm) {
   if (!mg) return set_error(AFH_ERR_ARG, "null mg");
   afh_tree *t = mg->t;
+  AFH_LIVE(t, "afh_mg_compute_phi_gradient");
   if (i_fc < 1 || i_fc > t->nvf || i_norm < 0 || i_norm > t->nvc)
     return set_error(AFH_ERR_ARG, "bad variable index");
   const int nc = t->nc, n3 = nc * nc * nc;
@@ -2417,7 +2423,9 @@ int32_t afh_mg_compute_phi_gradient(afh_mg *mg, int32_t i_fc, double fac,
 
 int32_t afh_mg_set_box_stencil(afh_mg *mg, int32_t id, const double *v,
                                const double *bc_correction) {
-  if (!mg || id < 1 || id > mg->t->nb) return set_error(AFH_ERR_ARG, "bad box id");
+  if (!mg) return set_error(AFH_ERR_ARG, "null mg");
+  AFH_LIVE(mg->t, "afh_mg_set_box_stencil");
+  if (id < 1 || id > mg->t->nb) return set_error(AFH_ERR_ARG, "bad box id");
   afh_tree *t = mg->t;
   const size_t n3 = (size_t)t->nc * t->nc * t->nc;
   AFH_HIP(hipStreamSynchronize(t->stream));
@@ -2438,7 +2446,9 @@ int32_t afh_mg_set_box_stencil(afh_mg *mg, int32_t id, const double *v,
 
 int32_t afh_mg_set_box_lsf(afh_mg *mg, int32_t id, int32_t n, const int32_t *ix,
                            const double *dd, const double *bval, int32_t i_lsf) {
-  if (!mg || id < 1 || id > mg->t->nb || n < 0)
+  if (!mg) return set_error(AFH_ERR_ARG, "null mg");
+  AFH_LIVE(mg->t, "afh_mg_set_box_lsf");
+  if (id < 1 || id > mg->t->nb || n < 0)
     return set_error(AFH_ERR_ARG, "bad box id / count");
   afh_tree *t = mg->t;
   const size_t n3 = (size_t)t->nc * t->nc * t->nc;

@@ -1599,12 +1599,31 @@ struct afh_fluid {
   // s_out); rhs_state = the state it was written for (-1: none)
   int rhs_iv = 0, rhs_state = -1;
   bool rhs_ghosts = false;
+  // write generations (afh_tree::gen) of rhs_iv and of the densities of
+  // rhs_state right after the update wrote the rhs: still equal = current
+  std::vector<uint64_t> rhs_snap;
+  std::vector<int> rhs_vars(int s_out) const {
+    std::vector<int> v{rhs_iv};
+    for (int s = 0; s < d.n_species; s++) v.push_back(d.species_iv[s] + s_out);
+    return v;
+  }
+  bool rhs_current(int s_out) const {
+    if (rhs_iv <= 0 || rhs_state < 0 || rhs_state != s_out) return false;
+    const std::vector<int> v = rhs_vars(s_out);
+    for (size_t q = 0; q < v.size(); q++)
+      if (q >= rhs_snap.size() || t->gen[v[q]] != rhs_snap[q]) return false;
+    return true;
+  }
+  void touch_state(int s_) {
+    for (int s = 0; s < d.n_species; s++) t->touch(d.species_iv[s] + s_);
+  }
 };
 
 extern "C" {
 
 int32_t afh_fluid_create(afh_tree *t, const afh_fluid_desc *d, afh_fluid **out) {
-  if (!t || !d || !out) return set_error(AFH_ERR_ARG, "afh_fluid_create: null");
+  if (!d || !out) return set_error(AFH_ERR_ARG, "afh_fluid_create: null");
+  AFH_LIVE(t, "afh_fluid_create");
   if (d->n_species < 1 || d->n_species > MAXS || d->n_reactions < 0 ||
       d->n_reactions > AFH_MAX_REACTIONS)
     return set_error(AFH_ERR_ARG, "bad species/reaction count");
@@ -1709,12 +1728,15 @@ int32_t afh_electrode_species_bc(afh_fluid *f, int32_t i_lsf, int32_t i_1pos_ion
                                  const int32_t *ids) {
   if (!f) return set_error(AFH_ERR_ARG, "afh_electrode_species_bc: null");
   afh_tree *t = f->t;
+  AFH_LIVE(t, "afh_electrode_species_bc");
   if (i_lsf < 1 || i_lsf > t->nvc || i_1pos_ion < 1 || i_1pos_ion > t->nvc ||
       n_ids < 0 || (n_ids && !ids))
     return set_error(AFH_ERR_ARG, "electrode_species_bc: bad argument");
   for (int q = 0; q < n_ids; q++)
     if (ids[q] < 1 || ids[q] > t->nb) return set_error(AFH_ERR_ARG, "bad box id");
   if (!n_ids) return AFH_OK;
+  f->touch_state(0);
+  t->touch(i_1pos_ion);
   if (n_ids > f->ids_cap) {
     // the previous list may still be read by a queued launch
     AFH_HIP(hipStreamSynchronize(t->stream));
@@ -1742,6 +1764,7 @@ int32_t afh_electrode_species_bc(afh_fluid *f, int32_t i_lsf, int32_t i_1pos_ion
 
 int32_t afh_fluid_set_rhs_output(afh_fluid *f, int32_t i_rhs, int32_t ghosts) {
   if (!f) return set_error(AFH_ERR_ARG, "afh_fluid_set_rhs_output: null");
+  AFH_LIVE(f->t, "afh_fluid_set_rhs_output");
   if (i_rhs < 0 || i_rhs > f->t->nvc) return set_error(AFH_ERR_ARG, "bad i_rhs");
   f->rhs_iv = i_rhs;
   f->rhs_ghosts = ghosts != 0;
@@ -1751,13 +1774,20 @@ int32_t afh_fluid_set_rhs_output(afh_fluid *f, int32_t i_rhs, int32_t ghosts) {
 
 int32_t afh_fluid_rhs_maxabs(afh_fluid *f, int32_t s_out, double *max_rhs) {
   if (!f || !max_rhs) return set_error(AFH_ERR_ARG, "afh_fluid_rhs_maxabs: null");
-  if (f->rhs_iv <= 0 || f->rhs_state < 0 || f->rhs_state != s_out)
-    return set_error(AFH_ERR_STATE, "no rhs output of state %d from the last update",
-                     s_out);
+  AFH_LIVE(f->t, "afh_fluid_rhs_maxabs");
+  if (!f->rhs_current(s_out))
+    return set_error(AFH_ERR_STATE, "no current rhs output of state %d", s_out);
   afh_tree *t = f->t;
   int32_t e;
   if ((e = red_fetch(t, 4, 1, max_rhs))) return e;
   return call_hook(t, AFH_HOOK_MAX, 0, f->rhs_iv, max_rhs, 1);
+}
+
+int32_t afh_fluid_rhs_valid(afh_fluid *f, int32_t s_out, int32_t *valid) {
+  if (!f || !valid) return set_error(AFH_ERR_ARG, "afh_fluid_rhs_valid: null");
+  AFH_LIVE(f->t, "afh_fluid_rhs_valid");
+  *valid = f->rhs_current(s_out) ? 1 : 0;
+  return AFH_OK;
 }
 
 }  // extern "C"
@@ -1784,7 +1814,9 @@ static int32_t set_rhs_impl(afh_fluid *f, int32_t i_rhs, int32_t s_in,
                             double *max_out) {
   if (!f) return set_error(AFH_ERR_ARG, "null fluid");
   afh_tree *t = f->t;
+  AFH_LIVE(t, "afh_field_set_rhs");
   if (i_rhs < 1 || i_rhs > t->nvc) return set_error(AFH_ERR_ARG, "bad i_rhs");
+  t->touch(i_rhs);
   const RhsArgs A = rhs_args(f, s_in);
   int32_t e;
   auto *red = reinterpret_cast<unsigned long long *>(t->scratch) + 3 * RED_SHARDS;
@@ -1943,9 +1975,11 @@ extern "C" {
 int32_t afh_flux_upwind_tree(afh_fluid *f, int32_t s_deriv, double *dt_lim) {
   if (!f || !dt_lim) return set_error(AFH_ERR_ARG, "null argument");
   afh_tree *t = f->t;
+  AFH_LIVE(t, "afh_flux_upwind_tree");
   const int nc = t->nc, n3 = nc * nc * nc;
   const int iv = f->d.i_electron + s_deriv;
   if (iv < 1 || iv > t->nvc) return set_error(AFH_ERR_ARG, "bad s_deriv");
+  t->touch(iv);  // ghost layers written back
   int32_t e;
   if ((e = flux_prelude(f, iv))) return e;
   if ((e = red_init(t, 0, -HUGE_VAL)) || (e = red_init(t, 1, -HUGE_VAL))) return e;
@@ -1998,6 +2032,7 @@ int32_t afh_flux_update_densities(afh_fluid *f, double dt, int32_t s_deriv,
                                   int32_t last_step, double *dt_lim) {
   if (!f || !dt_lim) return set_error(AFH_ERR_ARG, "afh_flux_update_densities: null");
   afh_tree *t = f->t;
+  AFH_LIVE(t, "afh_flux_update_densities");
   const int nc = t->nc, n3 = nc * nc * nc;
   UpdArgs A;
   double upd_bytes;
@@ -2037,7 +2072,13 @@ int32_t afh_flux_update_densities(afh_fluid *f, double dt, int32_t s_deriv,
       AFH_LAUNCH_CHECK("k_rhs_shell");
     }
     if ((e = red_finish(t, 4, true))) return e;
+  }
+  f->touch_state(s_out);
+  if (A.rhs) {
+    t->touch(f->rhs_iv);
     f->rhs_state = s_out;
+    f->rhs_snap.clear();
+    for (int v : f->rhs_vars(s_out)) f->rhs_snap.push_back(t->gen[v]);
   }
   double r = 1e100;
   if (last_step) {
@@ -2088,6 +2129,7 @@ int32_t afh_fluid_forward_euler(afh_fluid *f, double dt, int32_t s_deriv,
                                 double *dt_lim) {
   if (!f || !dt_lim) return set_error(AFH_ERR_ARG, "afh_fluid_forward_euler: null");
   afh_tree *t = f->t;
+  AFH_LIVE(t, "afh_fluid_forward_euler");
   const int nc = t->nc, n3 = nc * nc * nc;
   const int iv = f->d.i_electron + s_deriv;
   if (iv < 1 || iv > t->nvc) return set_error(AFH_ERR_ARG, "bad s_deriv");
@@ -2122,6 +2164,9 @@ int32_t afh_fluid_forward_euler(afh_fluid *f, double dt, int32_t s_deriv,
     dt_lim[0] = a[0], dt_lim[1] = a[1], dt_lim[2] = b[0], dt_lim[3] = b[1];
     return AFH_OK;
   }
+  t->touch(iv);
+  f->touch_state(s_out);
+  f->rhs_state = -1;
   if ((e = flux_prelude(f, iv))) return e;
   if ((e = red_init(t, 0, -HUGE_VAL)) || (e = red_init(t, 1, -HUGE_VAL)) ||
       (e = red_init(t, 2, 1e100)))
@@ -2176,6 +2221,7 @@ int32_t afh_refine_flags(afh_fluid *f, const afh_refine_desc *d,
                          uint32_t *masks) {
   if (!f || !d || !flags || !masks) return set_error(AFH_ERR_ARG, "afh_refine_flags: null");
   afh_tree *t = f->t;
+  AFH_LIVE(t, "afh_refine_flags");
   if (d->n_seeds > AFH_MAX_REFINE_REGIONS || d->n_regions > AFH_MAX_REFINE_REGIONS ||
       d->n_limits > AFH_MAX_REFINE_REGIONS || d->buffer_width < 0 ||
       d->buffer_width > t->nc || d->i_electron < 1 || d->i_electron > t->nvc ||

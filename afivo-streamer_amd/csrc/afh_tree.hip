@@ -10,7 +10,11 @@
 #include <stdarg.h>
 #include <stdio.h>
 
+#include <float.h>
+#include <math.h>
+
 #include <algorithm>
+#include <cmath>
 
 #include "afh_internal.h"
 
@@ -367,6 +371,67 @@ __global__ void k_maxabs(const double *__restrict__ v,
   }
 }
 
+// af_tree_sum_cc / af_reduction_loc, per box (m_af_utils.f90:694-754,
+// 840-874, 966-1026): one workgroup per leaf box reduces its interior. The
+// sum folds each thread's cells in order, then a fixed butterfly and the
+// waves in order (deterministic); max / min keep the first cell (i fastest)
+// of the extremum, as Fortran's maxloc / minloc. The boxes are folded on the
+// host in the reference's loop order.
+__device__ __forceinline__ double ipow(double x, int n) {
+  // gfortran's real ** integer (_gfortran_pow_r8_i4): binary powering
+  double p = 1.0;
+  for (;;) {
+    if (n & 1) p *= x;
+    n >>= 1;
+    if (!n) break;
+    x *= x;
+  }
+  return p;
+}
+template <int OP>
+__global__ void k_box_reduce(const double *__restrict__ v,
+                             const int32_t *__restrict__ ids, int nc, size_t bsz,
+                             int power, double *__restrict__ out) {
+  const int ng = nc + 2, n3 = nc * nc * nc;
+  const double *c = v + (size_t)(ids[blockIdx.x] - 1) * bsz;
+  double best = OP == 0 ? 0.0 : (OP == AFH_RED_MIN ? HUGE_VAL : -HUGE_VAL);
+  int bix = 0x7fffffff;
+  for (int t = threadIdx.x; t < n3; t += blockDim.x) {
+    int i, j, k;
+    cell3(t, nc, i, j, k);
+    double x = c[ix3(ng, i, j, k)];
+    if (OP == 0) {
+      best += ipow(x, power);
+    } else {
+      if (OP == AFH_RED_MAXABS) x = fabs(x);
+      if (OP == AFH_RED_MIN ? x < best : x > best) best = x, bix = t;
+    }
+  }
+  auto comb = [&](double b, int ib) {
+    if (OP == 0) {
+      best += b;
+    } else if ((OP == AFH_RED_MIN ? b < best : b > best) || (b == best && ib < bix)) {
+      best = b, bix = ib;
+    }
+  };
+  for (int o = 32; o > 0; o >>= 1) {
+    const double b = __shfl_xor(best, o, 64);
+    const int ib = __shfl_xor(bix, o, 64);
+    comb(b, ib);
+  }
+  __shared__ double s_v[16];
+  __shared__ int s_i[16];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) s_v[w] = best, s_i[w] = bix;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    best = s_v[0], bix = s_i[0];
+    for (int q = 1; q < (int)(blockDim.x >> 6); q++) comb(s_v[q], s_i[q]);
+    out[2 * blockIdx.x] = best;
+    out[2 * blockIdx.x + 1] = (double)bix;
+  }
+}
+
 int32_t upload_list(afh_tree *t, LevelList &L,
                     const std::vector<std::vector<int32_t>> &lists) {
   if (L.d) hipFree(L.d), L.d = nullptr;
@@ -500,6 +565,7 @@ static int32_t tree_create_impl(const afh_tree_desc *d, int32_t device,
   }
   t->boxes.assign(d->boxes, d->boxes + t->nb);
   t->meth.assign(t->nvc + 1, CcMethod());
+  t->gen.assign(t->nvc + 1, 0);
   auto split = [&](const int32_t *arr, const int32_t *off) {
     std::vector<std::vector<int32_t>> v(t->nlvl);
     for (int l = 0; l < t->nlvl; l++) v[l].assign(arr + off[l], arr + off[l + 1]);
@@ -581,6 +647,7 @@ static int32_t tree_create_impl(const afh_tree_desc *d, int32_t device,
     t->cap = adopt->cap;
     t->cc = adopt->cc, t->fc = adopt->fc, t->gc2 = adopt->gc2;
     adopt->cc = adopt->fc = adopt->gc2 = nullptr;
+    adopt->retired = true;
   } else {
     size_t ncc = (size_t)t->nvc * t->cap * t->bsz;
     size_t nfc = (size_t)std::max(1, t->nvf) * t->cap * t->fsz;
@@ -603,7 +670,7 @@ int32_t afh_tree_create(const afh_tree_desc *d, int32_t device,
 }
 
 int32_t afh_profile_enable(afh_tree *t, int32_t kclass) {
-  if (!t) return set_error(AFH_ERR_ARG, "null tree");
+  AFH_LIVE(t, "afh_profile_enable");
   AFH_HIP(hipStreamSynchronize(t->stream));
   t->prof_class = kclass;
   t->ev_used = 0;
@@ -647,6 +714,7 @@ int32_t afh_tree_destroy(afh_tree *t) {
   hipFree(t->fc);
   hipFree(t->gc2);
   hipFree(t->scratch);
+  hipFree(t->d_boxred);
   hipHostFree(t->h_scratch);
   if (t->own_stream) hipStreamDestroy(t->stream);
   delete t;
@@ -654,12 +722,14 @@ int32_t afh_tree_destroy(afh_tree *t) {
 }
 
 int32_t afh_tree_sync(afh_tree *t) {
+  AFH_LIVE(t, "afh_tree_sync");
   AFH_HIP(hipStreamSynchronize(t->stream));
   return AFH_OK;
 }
 
 int32_t afh_set_cc_methods(afh_tree *t, int32_t iv, const afh_bc *bc6,
                            int32_t rb, int32_t lim) {
+  AFH_LIVE(t, "afh_set_cc_methods");
   if (!t || iv < 1 || iv > t->nvc || !bc6)
     return set_error(AFH_ERR_ARG, "afh_set_cc_methods: bad argument");
   if (rb < AFH_RB_GC_INTERP || rb > AFH_RB_MG_SIDES)
@@ -680,6 +750,7 @@ int32_t afh_set_cc_methods(afh_tree *t, int32_t iv, const afh_bc *bc6,
 
 int32_t afh_set_bc(afh_tree *t, int32_t iv, int32_t nb, int32_t type,
                    double value) {
+  AFH_LIVE(t, "afh_set_bc");
   if (!t || iv < 1 || iv > t->nvc || nb < 1 || nb > 6)
     return set_error(AFH_ERR_ARG, "afh_set_bc: bad argument");
   t->meth[iv].bc[nb - 1].type = type;
@@ -688,14 +759,17 @@ int32_t afh_set_bc(afh_tree *t, int32_t iv, int32_t nb, int32_t type,
 }
 
 int32_t afh_cc_put(afh_tree *t, int32_t iv, const double *h) {
+  AFH_LIVE(t, "afh_cc_put");
   if (!t || iv < 1 || iv > t->nvc || !h)
     return set_error(AFH_ERR_ARG, "afh_cc_put: bad argument");
+  t->touch(iv);
   AFH_HIP(hipMemcpyAsync(t->ccv(iv), h, sizeof(double) * t->bsz * t->nb,
                          hipMemcpyHostToDevice, t->stream));
   AFH_HIP(hipStreamSynchronize(t->stream));
   return AFH_OK;
 }
 int32_t afh_cc_get(afh_tree *t, int32_t iv, double *h) {
+  AFH_LIVE(t, "afh_cc_get");
   if (!t || iv < 1 || iv > t->nvc || !h)
     return set_error(AFH_ERR_ARG, "afh_cc_get: bad argument");
   AFH_HIP(hipMemcpyAsync(h, t->ccv(iv), sizeof(double) * t->bsz * t->nb,
@@ -704,6 +778,7 @@ int32_t afh_cc_get(afh_tree *t, int32_t iv, double *h) {
   return AFH_OK;
 }
 int32_t afh_fc_put(afh_tree *t, int32_t ivf, const double *h) {
+  AFH_LIVE(t, "afh_fc_put");
   if (!t || ivf < 1 || ivf > t->nvf || !h)
     return set_error(AFH_ERR_ARG, "afh_fc_put: bad argument");
   AFH_HIP(hipMemcpyAsync(t->fcv(ivf), h, sizeof(double) * t->fsz * t->nb,
@@ -712,6 +787,7 @@ int32_t afh_fc_put(afh_tree *t, int32_t ivf, const double *h) {
   return AFH_OK;
 }
 int32_t afh_fc_get(afh_tree *t, int32_t ivf, double *h) {
+  AFH_LIVE(t, "afh_fc_get");
   if (!t || ivf < 1 || ivf > t->nvf || !h)
     return set_error(AFH_ERR_ARG, "afh_fc_get: bad argument");
   AFH_HIP(hipMemcpyAsync(h, t->fcv(ivf), sizeof(double) * t->fsz * t->nb,
@@ -721,13 +797,16 @@ int32_t afh_fc_get(afh_tree *t, int32_t ivf, double *h) {
 }
 
 int32_t afh_gc_lvl(afh_tree *t, int32_t lvl, int32_t iv, int32_t corners) {
+  AFH_LIVE(t, "afh_gc_lvl");
   if (!t || lvl < 1 || lvl > t->nlvl || iv < 1 || iv > t->nvc ||
       !t->meth[iv].set)
     return set_error(AFH_ERR_ARG, "afh_gc_lvl: bad argument / no methods");
+  t->touch(iv);
   return gc_lvl(t, lvl, iv, corners);
 }
 
 int32_t afh_gc_tree(afh_tree *t, int32_t iv, int32_t corners) {
+  AFH_LIVE(t, "afh_gc_tree");
   for (int l = 1; l <= (t ? t->nlvl : 0); l++) {
     int32_t e = afh_gc_lvl(t, l, iv, corners);
     if (e) return e;
@@ -736,7 +815,9 @@ int32_t afh_gc_tree(afh_tree *t, int32_t iv, int32_t corners) {
 }
 
 int32_t afh_restrict_tree(afh_tree *t, int32_t iv) {
-  if (!t || iv < 1 || iv > t->nvc) return set_error(AFH_ERR_ARG, "bad iv");
+  AFH_LIVE(t, "afh_restrict_tree");
+  if (iv < 1 || iv > t->nvc) return set_error(AFH_ERR_ARG, "bad iv");
+  t->touch(iv);
   // af_restrict_tree: parents of levels highest-1..1, i.e. children of
   // levels highest..2, coarsest last
   for (int l = t->nlvl; l >= 2; l--) {
@@ -747,14 +828,17 @@ int32_t afh_restrict_tree(afh_tree *t, int32_t iv) {
 }
 
 int32_t afh_tree_copy_cc(afh_tree *t, int32_t a, int32_t b) {
-  if (!t || a < 1 || a > t->nvc || b < 1 || b > t->nvc)
+  AFH_LIVE(t, "afh_tree_copy_cc");
+  if (a < 1 || a > t->nvc || b < 1 || b > t->nvc)
     return set_error(AFH_ERR_ARG, "bad iv");
+  t->touch(b);
   AFH_HIP(hipMemcpyAsync(t->ccv(b), t->ccv(a), sizeof(double) * t->bsz * t->nb,
                          hipMemcpyDeviceToDevice, t->stream));
   return AFH_OK;
 }
 
 int32_t afh_tree_maxabs_cc(afh_tree *t, int32_t iv, double *out) {
+  AFH_LIVE(t, "afh_tree_maxabs_cc");
   if (!t || iv < 1 || iv > t->nvc || !out) return set_error(AFH_ERR_ARG, "bad iv");
   int32_t e;
   if ((e = red_init(t, 3, 0.0))) return e;
@@ -772,8 +856,102 @@ int32_t afh_tree_maxabs_cc(afh_tree *t, int32_t iv, double *out) {
   return call_hook(t, AFH_HOOK_MAX, 0, iv, out, 1);
 }
 
+// per-box partial results over all leaves (level order), on the host
+static int32_t box_reduce(afh_tree *t, int iv, int op, int power,
+                          std::vector<double> &res) {
+  const int nl = t->leaves.off[t->nlvl];
+  res.assign(2 * (size_t)nl, 0.0);
+  if (!nl) return AFH_OK;
+  if (nl > t->boxred_cap) {
+    AFH_HIP(hipStreamSynchronize(t->stream));
+    hipFree(t->d_boxred);
+    t->d_boxred = nullptr;
+    AFH_HIP(hipMalloc(&t->d_boxred, sizeof(double) * 2 * nl));
+    t->boxred_cap = nl;
+  }
+  const dim3 grid(nl), blk(256);
+  switch (op) {
+  case 0:
+    hipLaunchKernelGGL(k_box_reduce<0>, grid, blk, 0, t->stream, t->ccv(iv),
+                       t->leaves.d, t->nc, t->bsz, power, t->d_boxred);
+    break;
+  case AFH_RED_MAX:
+    hipLaunchKernelGGL(k_box_reduce<AFH_RED_MAX>, grid, blk, 0, t->stream,
+                       t->ccv(iv), t->leaves.d, t->nc, t->bsz, power, t->d_boxred);
+    break;
+  case AFH_RED_MIN:
+    hipLaunchKernelGGL(k_box_reduce<AFH_RED_MIN>, grid, blk, 0, t->stream,
+                       t->ccv(iv), t->leaves.d, t->nc, t->bsz, power, t->d_boxred);
+    break;
+  default:
+    hipLaunchKernelGGL(k_box_reduce<AFH_RED_MAXABS>, grid, blk, 0, t->stream,
+                       t->ccv(iv), t->leaves.d, t->nc, t->bsz, power, t->d_boxred);
+  }
+  AFH_LAUNCH_CHECK("k_box_reduce");
+  AFH_HIP(hipMemcpyAsync(res.data(), t->d_boxred, sizeof(double) * 2 * nl,
+                         hipMemcpyDeviceToHost, t->stream));
+  AFH_HIP(hipStreamSynchronize(t->stream));
+  return AFH_OK;
+}
+
+int32_t afh_tree_sum_cc(afh_tree *t, int32_t iv, int32_t power, double *out) {
+  AFH_LIVE(t, "afh_tree_sum_cc");
+  if (iv < 1 || iv > t->nvc || power < 1 || !out)
+    return set_error(AFH_ERR_ARG, "afh_tree_sum_cc: bad argument");
+  std::vector<double> res;
+  int32_t e;
+  if ((e = box_reduce(t, iv, 0, power, res))) return e;
+  // my_sum = my_sum + fac * tmp, fac = product(af_lvl_dr(tree, lvl))
+  double sum = 0.0;
+  size_t q = 0;
+  for (int l = 1; l <= t->nlvl; l++) {
+    const double *dr = &t->lvl_dr[3 * (l - 1)];
+    const double fac = dr[0] * dr[1] * dr[2];
+    for (int b = 0; b < t->leaves.n(l); b++, q++) sum = sum + fac * res[2 * q];
+  }
+  *out = sum;
+  return call_hook(t, AFH_HOOK_SUM, 0, iv, out, 1);
+}
+
+int32_t afh_tree_reduce_loc(afh_tree *t, int32_t iv, int32_t op, double *out,
+                            int32_t *loc) {
+  AFH_LIVE(t, "afh_tree_reduce_loc");
+  if (iv < 1 || iv > t->nvc || !out || op < AFH_RED_MAX || op > AFH_RED_MAXABS)
+    return set_error(AFH_ERR_ARG, "afh_tree_reduce_loc: bad argument");
+  if (t->hook && loc)
+    return set_error(AFH_ERR_UNSUPPORTED, "location of a sharded reduction");
+  std::vector<double> res;
+  int32_t e;
+  if ((e = box_reduce(t, iv, op, 1, res))) return e;
+  // af_reduction_loc: init -huge/10 (max) or huge/10 (min); a box replaces
+  // the running value when reduction(tmp, val) differs from val
+  const bool is_min = op == AFH_RED_MIN;
+  double val = (is_min ? 1 : -1) * (DBL_MAX / 10);
+  int32_t lid = -1, lix = -1;
+  size_t q = 0;
+  for (int l = 1; l <= t->nlvl; l++)
+    for (int b = 0; b < t->leaves.n(l); b++, q++) {
+      const double tmp = res[2 * q];
+      const double nv = is_min ? std::min(tmp, val) : std::max(tmp, val);
+      if (std::fabs(nv - val) > 0) {
+        val = tmp;
+        lid = t->h_leaves[l - 1][b];
+        lix = (int32_t)res[2 * q + 1];
+      }
+    }
+  *out = val;
+  if (loc) {
+    loc[0] = lid;
+    const int nc = t->nc;
+    loc[1] = lix < 0 ? -1 : lix % nc + 1;
+    loc[2] = lix < 0 ? -1 : (lix / nc) % nc + 1;
+    loc[3] = lix < 0 ? -1 : lix / (nc * nc) + 1;
+  }
+  return call_hook(t, is_min ? AFH_HOOK_MIN : AFH_HOOK_MAX, 0, iv, out, 1);
+}
+
 int32_t afh_tree_set_stream(afh_tree *t, void *stream) {
-  if (!t) return set_error(AFH_ERR_ARG, "null tree");
+  AFH_LIVE(t, "afh_tree_set_stream");
   AFH_HIP(hipStreamSynchronize(t->stream));
   if (t->own_stream) AFH_HIP(hipStreamDestroy(t->stream));
   t->stream = (hipStream_t)stream;
@@ -782,7 +960,7 @@ int32_t afh_tree_set_stream(afh_tree *t, void *stream) {
 }
 
 int32_t afh_tree_set_hook(afh_tree *t, afh_hook_fn fn, void *ctx) {
-  if (!t) return set_error(AFH_ERR_ARG, "null tree");
+  AFH_LIVE(t, "afh_tree_set_hook");
   t->hook = fn;
   t->hook_ctx = ctx;
   return AFH_OK;
@@ -790,6 +968,7 @@ int32_t afh_tree_set_hook(afh_tree *t, afh_hook_fn fn, void *ctx) {
 
 static int32_t plan_create(afh_tree *t, const int32_t *reg, int32_t n,
                            int32_t *plan, int64_t *n_values, int fc) {
+  AFH_LIVE(t, "afh_plan_create");
   if (!t || n < 0 || (n > 0 && !reg) || !plan || !n_values)
     return set_error(AFH_ERR_ARG, "afh_plan_create: bad argument");
   if (n > 65535) return set_error(AFH_ERR_UNSUPPORTED, "more than 65535 regions");
@@ -837,6 +1016,7 @@ int32_t afh_plan_create_fc(afh_tree *t, const int32_t *reg, int32_t n,
 
 static int32_t plan_copy(afh_tree *t, int32_t plan, int32_t iv, double *buf,
                          int unpack) {
+  AFH_LIVE(t, "afh_plan_pack/unpack");
   if (!t || plan < 0 || plan >= (int)t->plans.size())
     return set_error(AFH_ERR_ARG, "afh_plan_pack/unpack: bad plan");
   const afh_tree::Plan &p = t->plans[plan];
@@ -879,6 +1059,7 @@ static int32_t device_list(const std::vector<int32_t> &h, int32_t **d) {
 extern "C" {
 
 int32_t afh_set_cc_prolong(afh_tree *t, int32_t iv, int32_t method, int32_t limiter) {
+  AFH_LIVE(t, "afh_set_cc_prolong");
   if (!t || iv < 1 || iv > t->nvc) return set_error(AFH_ERR_ARG, "bad variable index");
   if (method < AFH_PROLONG_NONE || method > AFH_PROLONG_LIMIT)
     return set_error(AFH_ERR_UNSUPPORTED, "prolongation method %d", method);
@@ -893,6 +1074,7 @@ int32_t afh_set_cc_prolong(afh_tree *t, int32_t iv, int32_t method, int32_t limi
 
 int32_t afh_tree_regrid(afh_tree *o, const afh_tree_desc *d, afh_tree **out) {
   if (!o || !d || !out) return set_error(AFH_ERR_ARG, "afh_tree_regrid: null");
+  AFH_LIVE(o, "afh_tree_regrid");
   if (d->n_cell != o->nc || d->n_var_cell != o->nvc || d->n_var_face != o->nvf)
     return set_error(AFH_ERR_ARG, "afh_tree_regrid: box size / variables differ");
   if (o->hook) return set_error(AFH_ERR_UNSUPPORTED, "regrid of a sharded tree");

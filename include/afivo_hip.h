@@ -236,6 +236,23 @@ int32_t afh_restrict_tree(afh_tree *t, int32_t iv);
 int32_t afh_tree_copy_cc(afh_tree *t, int32_t iv_from, int32_t iv_to);
 /* af_tree_maxabs_cc over leaf interiors (m_af_utils.f90:773-784) */
 int32_t afh_tree_maxabs_cc(afh_tree *t, int32_t iv, double *out);
+/* af_tree_sum_cc (m_af_utils.f90:966-1026): sum over the leaf interiors of
+ * cc(iv)**power (power >= 1, evaluated as gfortran's integer power), each
+ * box weighted by the cell volume of its level, product(af_lvl_dr); boxes
+ * are folded in the reference's loop order (levels, then leaves). The
+ * output_regression_log sums (src/m_output.f90:783-837). */
+int32_t afh_tree_sum_cc(afh_tree *t, int32_t iv, int32_t power, double *out);
+/* af_tree_max_cc / af_tree_min_cc / af_tree_maxabs_cc with the location of
+ * the extremum (af_reduction_loc + box_max_cc / box_min_cc / box_maxabs_cc,
+ * m_af_utils.f90:694-874): the first cell (i fastest) of the first box in
+ * loop order holding it; loc = (box id, i, j, k), 1-based (af_loc_t), or
+ * NULL. A sharded tree reduces the value over the ranks and returns no
+ * location (loc must be NULL). */
+#define AFH_RED_MAX 1
+#define AFH_RED_MIN 2
+#define AFH_RED_MAXABS 3
+int32_t afh_tree_reduce_loc(afh_tree *t, int32_t iv, int32_t op, double *out,
+                            int32_t *loc);
 
 /* mg_init (m_af_multigrid.f90:43-109) + stencils; mg_fas_vcycle (185-264) */
 int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *desc, afh_mg **out);
@@ -280,13 +297,6 @@ int32_t afh_mg_set_box_lsf(afh_mg *mg, int32_t id, int32_t n, const int32_t *ix,
 int32_t afh_fluid_create(afh_tree *t, const afh_fluid_desc *desc,
                          afh_fluid **out);
 int32_t afh_fluid_destroy(afh_fluid *f);
-/* electrode_species_bc over the boxes tagged mg_lsf_box (src/streamer.f90:
- * 578-636, called per step by set_electrode_densities, 569-574): in every
- * cell with lsf < 0 all plasma species (state 0, m_streamer.f90:242) are set
- * to 0; with neumann_zero (bc_species => af_bc_neumann_zero), a cell next to
- * a cell with lsf > 0 gets the mean electron density of those neighbours,
- * copied to the first positive ion (i_1pos_ion). Reads the ghost cells of
- * i_lsf and the electrons (the caller fills them, as in the reference). */
 /* field_set_rhs folded into the density update: with i_rhs > 0, every
  * afh_flux_update_densities / afh_fluid_forward_euler also writes
  * rhs = field_set_rhs(i_rhs, s_out) (src/m_field.f90:363-401) -- the interior
@@ -300,9 +310,23 @@ int32_t afh_fluid_destroy(afh_fluid *f);
  * (m_fluid.f90:51-53, streamer.f90 after af_advance) computes, provided no
  * density of state s_out changes in between; afh_fluid_rhs_maxabs(s_out)
  * then returns what afh_field_set_rhs_maxabs(i_rhs, s_out) would (an error
- * if the last update did not write state s_out's rhs). i_rhs = 0 disables. */
+ * if the last update did not write state s_out's rhs). i_rhs = 0 disables.
+ * The library tracks whether that rhs is still current: any call that may
+ * change a density of the state or the rhs variable itself (another update,
+ * afh_electrode_species_bc, afh_tree_copy_cc into a density or rhs,
+ * afh_cc_put, a multigrid call with i_rhs = that variable, a regrid)
+ * invalidates it; afh_fluid_rhs_valid(s) returns 1 when the rhs of state s
+ * from the last update is current (field_compute may skip field_set_rhs). */
 int32_t afh_fluid_set_rhs_output(afh_fluid *f, int32_t i_rhs, int32_t ghosts);
 int32_t afh_fluid_rhs_maxabs(afh_fluid *f, int32_t s_out, double *max_rhs);
+int32_t afh_fluid_rhs_valid(afh_fluid *f, int32_t s_out, int32_t *valid);
+/* electrode_species_bc over the boxes tagged mg_lsf_box (src/streamer.f90:
+ * 578-636, called per step by set_electrode_densities, 569-574): in every
+ * cell with lsf < 0 all plasma species (state 0, m_streamer.f90:242) are set
+ * to 0; with neumann_zero (bc_species => af_bc_neumann_zero), a cell next to
+ * a cell with lsf > 0 gets the mean electron density of those neighbours,
+ * copied to the first positive ion (i_1pos_ion). Reads the ghost cells of
+ * i_lsf and the electrons (the caller fills them, as in the reference). */
 int32_t afh_electrode_species_bc(afh_fluid *f, int32_t i_lsf, int32_t i_1pos_ion,
                                  int32_t neumann_zero, int32_t n_ids,
                                  const int32_t *ids);
@@ -452,6 +476,7 @@ int32_t afh_profile_read(afh_tree *t, double *total_ms, int64_t *launches,
 #define AFH_HOOK_MIN 5
 #define AFH_HOOK_CFLUX 6 /* af_consistent_fluxes wrote face fluxes of
                             neighbouring leaves (iv = face variable) */
+#define AFH_HOOK_SUM 7   /* sum vals[0..n-1] over all ranks, in place */
 typedef int32_t (*afh_hook_fn)(void *ctx, int32_t kind, int32_t level,
                                int32_t iv, double *vals, int32_t n);
 int32_t afh_tree_set_hook(afh_tree *t, afh_hook_fn fn, void *ctx);

@@ -9,6 +9,7 @@
 #define _POSIX_C_SOURCE 200809L
 #include "afo.h"
 
+#include <float.h>
 #include <math.h>
 #include <stdarg.h>
 #include <stdio.h>
@@ -45,6 +46,12 @@ struct afh_tree {
   /* box sharding (afo_tree_set_hook, afo_plan_*) */
   afh_hook_fn hook;
   void *hook_ctx;
+  /* write generation per cc variable (afo_fluid_rhs_valid), as the device */
+  unsigned long long *gen;
+  /* box capacity of the pools (afh_tree_desc.box_capacity) and the in-place
+   * regrid contract of the device library: a regrid whose topology fits the
+   * capacity retires the old handle (its entry points fail) */
+  int cap, retired;
   int nplans;
   struct afo_plan {
     int n, fc;
@@ -52,6 +59,17 @@ struct afh_tree {
     int64_t *off;
   } *plans;
 };
+
+#define LIVE(t)                                                               \
+  do {                                                                        \
+    if (!(t)) return fail(AFH_ERR_ARG, "null tree");                          \
+    if ((t)->retired)                                                         \
+      return fail(AFH_ERR_STATE, "tree handle retired by an in-place regrid"); \
+  } while (0)
+
+static inline void touch(afh_tree *t, int iv) {
+  if (iv >= 0 && iv <= t->nvc) t->gen[iv]++;
+}
 
 static int32_t hook(afh_tree *t, int kind, int lvl, int iv, double *vals, int n) {
   if (!t->hook) return AFH_OK;
@@ -95,6 +113,8 @@ struct afh_fluid {
   afh_reaction reac[AFH_MAX_REACTIONS];
   int rhs_iv, rhs_state, rhs_ghosts; /* afo_fluid_set_rhs_output */
   double rhs_max;
+  /* generations of rhs_iv and the densities of rhs_state after the update */
+  unsigned long long rhs_snap[AFH_MAX_SPECIES + 1];
 };
 
 /* ---------------------------------------------------------------- tables
@@ -181,6 +201,8 @@ int32_t afo_tree_create(const afh_tree_desc *d, int32_t device,
                  sizeof(double));
   t->meth = calloc(t->nvc + 1, sizeof(cc_method));
   t->auto_vars = calloc(t->nvc + 1, sizeof(int));
+  t->gen = calloc(t->nvc + 1, sizeof(unsigned long long));
+  t->cap = d->box_capacity > t->nb ? d->box_capacity : t->nb;
   if (!t->cc || !t->fc) return fail(AFH_ERR_ARG, "out of memory");
   *out = t;
   return AFH_OK;
@@ -191,7 +213,7 @@ int32_t afo_tree_destroy(afh_tree *t) {
   free(t->boxes);
   free(t->ids), free(t->ids_off), free(t->leaves), free(t->leaves_off);
   free(t->parents), free(t->parents_off);
-  free(t->cc), free(t->fc), free(t->meth), free(t->auto_vars);
+  free(t->cc), free(t->fc), free(t->meth), free(t->auto_vars), free(t->gen);
   for (int q = 0; q < t->nplans; q++) free(t->plans[q].reg), free(t->plans[q].off);
   free(t->plans);
   free(t);
@@ -224,21 +246,26 @@ int32_t afo_set_bc(afh_tree *t, int32_t iv, int32_t nb, int32_t type,
 }
 
 int32_t afo_cc_put(afh_tree *t, int32_t iv, const double *h) {
+  LIVE(t);
   if (iv < 1 || iv > t->nvc) return fail(AFH_ERR_ARG, "bad iv");
+  touch(t, iv);
   memcpy(ccb(t, iv, 1), h, sizeof(double) * t->bsz * t->nb);
   return AFH_OK;
 }
 int32_t afo_cc_get(afh_tree *t, int32_t iv, double *h) {
+  LIVE(t);
   if (iv < 1 || iv > t->nvc) return fail(AFH_ERR_ARG, "bad iv");
   memcpy(h, ccb(t, iv, 1), sizeof(double) * t->bsz * t->nb);
   return AFH_OK;
 }
 int32_t afo_fc_put(afh_tree *t, int32_t ivf, const double *h) {
+  LIVE(t);
   if (ivf < 1 || ivf > t->nvf) return fail(AFH_ERR_ARG, "bad ivf");
   memcpy(fcb(t, ivf, 1), h, sizeof(double) * t->fsz * t->nb);
   return AFH_OK;
 }
 int32_t afo_fc_get(afh_tree *t, int32_t ivf, double *h) {
+  LIVE(t);
   if (ivf < 1 || ivf > t->nvf) return fail(AFH_ERR_ARG, "bad ivf");
   memcpy(h, fcb(t, ivf, 1), sizeof(double) * t->fsz * t->nb);
   return AFH_OK;
@@ -493,8 +520,10 @@ static int32_t gc_lvl(afh_tree *t, int lvl, int iv, int corners) {
 }
 
 int32_t afo_gc_lvl(afh_tree *t, int32_t lvl, int32_t iv, int32_t corners) {
+  LIVE(t);
   if (lvl < 1 || lvl > t->nlvl || iv < 1 || iv > t->nvc || !t->meth[iv].set)
     return fail(AFH_ERR_ARG, "afo_gc_lvl: bad argument / no methods");
+  touch(t, iv);
   return gc_lvl(t, lvl, iv, corners);
 }
 int32_t afo_gc_tree(afh_tree *t, int32_t iv, int32_t corners) {
@@ -530,6 +559,8 @@ static void restrict_box(afh_tree *t, int c_id, int p_id, int iv) {
 }
 
 int32_t afo_restrict_tree(afh_tree *t, int32_t iv) {
+  LIVE(t);
+  touch(t, iv);
   /* af_restrict_tree -> af_restrict_to_boxes over parents per level */
   for (int l = t->nlvl - 1; l >= 1; l--) {
     int n = LVL_N(t, parents, l);
@@ -547,12 +578,15 @@ int32_t afo_restrict_tree(afh_tree *t, int32_t iv) {
 }
 
 int32_t afo_tree_copy_cc(afh_tree *t, int32_t a, int32_t b) {
+  LIVE(t);
+  touch(t, b);
   memcpy(ccb(t, b, 1), ccb(t, a, 1), sizeof(double) * t->bsz * t->nb);
   return AFH_OK;
 }
 
 /* af_tree_maxabs_cc over leaf interiors, m_af_utils.f90:773-784, 852-862 */
 int32_t afo_tree_maxabs_cc(afh_tree *t, int32_t iv, double *out) {
+  LIVE(t);
   double mx = -HUGE_VAL;
   int nc = t->nc;
   for (int l = 1; l <= t->nlvl; l++)
@@ -567,6 +601,75 @@ int32_t afo_tree_maxabs_cc(afh_tree *t, int32_t iv, double *out) {
     }
   *out = mx;
   return hook(t, AFH_HOOK_MAX, 0, iv, out, 1);
+}
+
+/* gfortran's real ** integer (_gfortran_pow_r8_i4): binary powering */
+static double ipow(double x, int n) {
+  double p = 1.0;
+  for (;;) {
+    if (n & 1) p *= x;
+    n >>= 1;
+    if (!n) break;
+    x *= x;
+  }
+  return p;
+}
+
+/* af_tree_sum_cc, m_af_utils.f90:966-1026 (leaves in loop order; the per-box
+ * sum is sequential here, a fixed tree on the device: equal to rounding) */
+int32_t afo_tree_sum_cc(afh_tree *t, int32_t iv, int32_t power, double *out) {
+  LIVE(t);
+  if (iv < 1 || iv > t->nvc || power < 1) return fail(AFH_ERR_ARG, "bad argument");
+  const int nc = t->nc;
+  double my_sum = 0.0;
+  for (int l = 1; l <= t->nlvl; l++) {
+    if (LVL_N(t, ids, l) == 0) continue;
+    const afh_box_meta *m = B(t, LVL_AT(t, ids, l, 0));
+    const double fac = m->dr[0] * m->dr[1] * m->dr[2];
+    for (int q = 0; q < LVL_N(t, leaves, l); q++) {
+      const double *c = ccb(t, iv, LVL_AT(t, leaves, l, q));
+      double tmp = 0.0;
+      for (int k = 1; k <= nc; k++)
+        for (int j = 1; j <= nc; j++)
+          for (int i = 1; i <= nc; i++) tmp += ipow(c[IX(t, i, j, k)], power);
+      my_sum = my_sum + fac * tmp;
+    }
+  }
+  *out = my_sum;
+  return hook(t, AFH_HOOK_SUM, 0, iv, out, 1);
+}
+
+/* af_reduction_loc with box_max_cc / box_min_cc / box_maxabs_cc,
+ * m_af_utils.f90:694-754, 840-874 (one thread: boxes in loop order) */
+int32_t afo_tree_reduce_loc(afh_tree *t, int32_t iv, int32_t op, double *out,
+                            int32_t *loc) {
+  LIVE(t);
+  if (iv < 1 || iv > t->nvc || op < AFH_RED_MAX || op > AFH_RED_MAXABS)
+    return fail(AFH_ERR_ARG, "bad argument");
+  if (t->hook && loc) return fail(AFH_ERR_UNSUPPORTED, "location of a sharded reduction");
+  const int nc = t->nc, is_min = op == AFH_RED_MIN;
+  double val = (is_min ? 1 : -1) * (DBL_MAX / 10);
+  int lid = -1, li = -1, lj = -1, lk = -1;
+  for (int l = 1; l <= t->nlvl; l++)
+    for (int q = 0; q < LVL_N(t, leaves, l); q++) {
+      const int id = LVL_AT(t, leaves, l, q);
+      const double *c = ccb(t, iv, id);
+      /* maxloc / minloc: the first extremum, i fastest */
+      double bv = 0;
+      int bi = 0, bj = 0, bk = 0, first = 1;
+      for (int k = 1; k <= nc; k++)
+        for (int j = 1; j <= nc; j++)
+          for (int i = 1; i <= nc; i++) {
+            double x = c[IX(t, i, j, k)];
+            if (op == AFH_RED_MAXABS) x = fabs(x);
+            if (first || (is_min ? x < bv : x > bv)) bv = x, bi = i, bj = j, bk = k, first = 0;
+          }
+      const double nv = is_min ? fmin(bv, val) : fmax(bv, val);
+      if (fabs(nv - val) > 0) val = bv, lid = id, li = bi, lj = bj, lk = bk;
+    }
+  *out = val;
+  if (loc) loc[0] = lid, loc[1] = li, loc[2] = lj, loc[3] = lk;
+  return hook(t, is_min ? AFH_HOOK_MIN : AFH_HOOK_MAX, 0, iv, out, 1);
 }
 
 /* ------------------------------------------------------------ multigrid */
@@ -1293,7 +1396,9 @@ int32_t afo_mg_set_box_lsf(afh_mg *mg, int32_t id, int32_t n, const int32_t *ix,
 
 /* mg_fas_vcycle, m_af_multigrid.f90:185-264 (subtract_mean = .false.) */
 int32_t afo_mg_fas_vcycle(afh_mg *mg, int32_t set_residual, int32_t hl) {
+  LIVE(mg->t);
   afh_tree *t = mg->t;
+  touch(t, mg->d.i_phi), touch(t, mg->d.i_rhs), touch(t, mg->d.i_tmp);
   int max_lvl = (hl > 0) ? hl : t->nlvl;
   for (int lvl = max_lvl; lvl >= 2; lvl--) {
     if (afo_mg_gsrb_boxes(mg, lvl, 0) || afo_mg_update_coarse(mg, lvl))
@@ -1327,7 +1432,9 @@ int32_t afo_mg_fas_vcycle_maxres(afh_mg *mg, int32_t hl, double *max_res) {
  * is overwritten by the phi -> tmp copies below before tmp is read again;
  * init_phi_rhs (779-799) clears phi on levels >= 2 and restricts rhs. */
 int32_t afo_mg_fas_fmg(afh_mg *mg, int32_t set_residual, int32_t have_guess) {
+  LIVE(mg->t);
   afh_tree *t = mg->t;
+  touch(t, mg->d.i_phi), touch(t, mg->d.i_rhs), touch(t, mg->d.i_tmp);
   int nl = t->nlvl, i_phi = mg->d.i_phi, i_tmp = mg->d.i_tmp;
   size_t bsz = t->bsz;
   if (have_guess) {
@@ -1482,9 +1589,20 @@ int32_t afo_fluid_set_rhs_output(afh_fluid *f, int32_t i_rhs, int32_t ghosts) {
   f->rhs_state = -1;
   return AFH_OK;
 }
+static int rhs_current(afh_fluid *f, int s_out) {
+  if (f->rhs_iv <= 0 || f->rhs_state < 0 || f->rhs_state != s_out) return 0;
+  if (f->t->gen[f->rhs_iv] != f->rhs_snap[0]) return 0;
+  for (int s = 0; s < f->d.n_species; s++)
+    if (f->t->gen[f->d.species_iv[s] + s_out] != f->rhs_snap[s + 1]) return 0;
+  return 1;
+}
+int32_t afo_fluid_rhs_valid(afh_fluid *f, int32_t s_out, int32_t *valid) {
+  *valid = rhs_current(f, s_out);
+  return AFH_OK;
+}
 int32_t afo_fluid_rhs_maxabs(afh_fluid *f, int32_t s_out, double *max_rhs) {
-  if (f->rhs_iv <= 0 || f->rhs_state < 0 || f->rhs_state != s_out)
-    return fail(AFH_ERR_STATE, "no rhs output of state %d from the last update", s_out);
+  if (!rhs_current(f, s_out))
+    return fail(AFH_ERR_STATE, "no current rhs output of state %d", s_out);
   *max_rhs = f->rhs_max;
   return hook(f->t, AFH_HOOK_MAX, 0, f->rhs_iv, max_rhs, 1);
 }
@@ -1497,6 +1615,8 @@ int32_t afo_electrode_species_bc(afh_fluid *f, int32_t i_lsf, int32_t i_1pos_ion
   if (i_lsf < 1 || i_lsf > t->nvc || i_1pos_ion < 1 || i_1pos_ion > t->nvc ||
       n_ids < 0 || (n_ids && !ids))
     return fail(AFH_ERR_ARG, "electrode_species_bc: bad argument");
+  for (int s = 0; s < f->d.n_species; s++) touch(t, f->d.species_iv[s]);
+  touch(t, i_1pos_ion);
   for (int q = 0; q < n_ids; q++)
     if (ids[q] < 1 || ids[q] > t->nb) return fail(AFH_ERR_ARG, "bad box id");
   const int nc = t->nc;
@@ -1594,7 +1714,9 @@ static double rate_of(const afh_fluid *fl, const afh_reaction *R, double field,
 
 /* field_set_rhs, src/m_field.f90:363-401 */
 int32_t afo_field_set_rhs(afh_fluid *f, int32_t i_rhs, int32_t s_in) {
+  LIVE(f->t);
   afh_tree *t = f->t;
+  touch(t, i_rhs);
   const double fac = -1.6022e-19 / 8.8541878176e-12;
   for (int l = 1; l <= t->nlvl; l++) {
     int n = LVL_N(t, leaves, l);
@@ -1910,8 +2032,10 @@ static void consistent_fluxes(afh_tree *t, int f_ix) {
 
 /* flux_upwind_tree, m_af_flux_schemes.f90:666-712 */
 int32_t afo_flux_upwind_tree(afh_fluid *f, int32_t s_deriv, double *dt_lim) {
+  LIVE(f->t);
   afh_tree *t = f->t;
   int nc = t->nc;
+  touch(t, f->d.i_electron + s_deriv); /* ghost layers written back */
   if (restrict_ref_boundary(t, f->d.i_electron + s_deriv)) return AFH_ERR_STATE;
   double cfl_max = -HUGE_VAL, sig_max = -HUGE_VAL;
   for (int l = 1; l <= t->nlvl; l++) {
@@ -1964,6 +2088,7 @@ int32_t afo_flux_update_densities(afh_fluid *fl, double dt, int32_t s_deriv,
                                   int32_t n_prev, const int32_t *s_prev,
                                   const double *w_prev, int32_t s_out,
                                   int32_t last_step, double *dt_lim) {
+  LIVE(fl->t);
   afh_tree *t = fl->t;
   int nc = t->nc, ns = fl->d.n_species, nr = fl->d.n_reactions;
   double chem_min = 1e100;
@@ -2095,7 +2220,14 @@ int32_t afo_flux_update_densities(afh_fluid *fl, double dt, int32_t s_deriv,
             }
       }
     fl->rhs_max = mx;
+  }
+  for (int s = 0; s < fl->d.n_species; s++) touch(t, fl->d.species_iv[s] + s_out);
+  if (fl->rhs_iv > 0) {
+    touch(t, fl->rhs_iv);
     fl->rhs_state = s_out;
+    fl->rhs_snap[0] = t->gen[fl->rhs_iv];
+    for (int s = 0; s < fl->d.n_species; s++)
+      fl->rhs_snap[s + 1] = t->gen[fl->d.species_iv[s] + s_out];
   }
   if (last_step && hook(t, AFH_HOOK_MIN, 0, 0, &chem_min, 1)) return AFH_ERR_STATE;
   dt_lim[0] = last_step ? chem_min : 1e100;
@@ -2339,6 +2471,8 @@ static void prolong_linear(afh_tree *t, int p_id, int c_id, int iv) {
  * from the restricted parents). */
 int32_t afo_tree_regrid(afh_tree *o, const afh_tree_desc *d, afh_tree **out) {
   if (!o || !d || !out) return fail(AFH_ERR_ARG, "afo_tree_regrid: null");
+  LIVE(o);
+  const int in_place = (d->n_boxes > d->box_capacity ? d->n_boxes : d->box_capacity) <= o->cap;
   if (d->n_cell != o->nc || d->n_var_cell != o->nvc || d->n_var_face != o->nvf)
     return fail(AFH_ERR_ARG, "afo_tree_regrid: box size / variables differ");
   afh_tree *t;
@@ -2392,6 +2526,8 @@ int32_t afo_tree_regrid(afh_tree *o, const afh_tree_desc *d, afh_tree **out) {
     }
   }
   free(in_old), free(keep);
+  t->cap = in_place ? o->cap : t->cap;
+  if (in_place) o->retired = 1;
   *out = t;
   return AFH_OK;
 }

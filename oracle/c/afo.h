@@ -44,6 +44,10 @@ int32_t afo_electrode_species_bc(afh_fluid *f, int32_t i_lsf, int32_t i_1pos_ion
                                  int32_t neumann_zero, int32_t n_ids,
                                  const int32_t *ids);
 int32_t afo_tree_maxabs_cc(afh_tree *t, int32_t iv, double *out);
+int32_t afo_tree_sum_cc(afh_tree *t, int32_t iv, int32_t power, double *out);
+int32_t afo_tree_reduce_loc(afh_tree *t, int32_t iv, int32_t op, double *out,
+                            int32_t *loc);
+int32_t afo_fluid_rhs_valid(afh_fluid *f, int32_t s_out, int32_t *valid);
 int32_t afo_mg_create(afh_tree *t, const afh_mg_desc *desc, afh_mg **out);
 int32_t afo_mg_destroy(afh_mg *mg);
 int32_t afo_mg_fas_vcycle(afh_mg *mg, int32_t set_residual,

@@ -2,9 +2,12 @@
 the rhs and max|rhs| the update writes for its output state must be bitwise
 those of a separate field_set_rhs_maxabs call on that state (ghost cells
 included; without the ghost option the interiors, whose values are all the
-solver reads), for both Heun stages, on uniform and AMR trees; the Heun step
-that consumes them must be bitwise that of the unfused step. CPU: the C oracle;
-GPU: the HIP library (and HIP == oracle)."""
+solver reads), for both Heun stages, on uniform and AMR trees and on the rod
+electrode tree (level-set operators read the rhs of their boxes); the Heun
+step that consumes them must be bitwise that of the unfused step. The library
+tracks whether the fused rhs is still current (afh_fluid_rhs_valid): writing a
+density of its state invalidates it. CPU: the C oracle; GPU: the HIP library
+(and HIP == oracle)."""
 import numpy as np
 import pytest
 
@@ -19,14 +22,19 @@ TOPOS = {
     "amr8": lambda: build_tree(
         8, (16, 16, 16), (2e-3, 2e-3, 2e-3), 2,
         refine=lambda lvl, r0, r1: lvl < 4 and np.all(r0 < 1.2e-3) and np.all(r1 > 0.7e-3)),
+    # the reference's rod electrode fixture: level-set stencils on 15 boxes
+    "rod8": lambda: "rod8",
 }
 
 
 def make(lib, topo, device, fused, ghosts=True):
-    g = golden.load("uni8")
-    td, chem = tables_from(g)
-    c = StreamerCase(lib, topo, td, chem, float(g["current_voltage"]),
-                     coarse_cycles=0, device=device)
+    if isinstance(topo, str):
+        c = golden.make_case(lib, golden.load(topo), coarse_cycles=0, device=device)
+    else:
+        g = golden.load("uni8")
+        td, chem = tables_from(g)
+        c = StreamerCase(lib, topo, td, chem, float(g["current_voltage"]),
+                         coarse_cycles=0, device=device)
     seed_state(c)
     if fused:
         c.fuse_rhs(True, ghosts)
@@ -57,8 +65,13 @@ def check(lib, device, name, ghosts=True):
         assert np.array_equal(leaf_rhs(a, ghosts), leaf_rhs(b, ghosts))
         with pytest.raises(capi.AfhError):  # another state's rhs was not written
             a.fluid.rhs_maxabs(1 - s_out)
+        assert a.fluid.rhs_valid(s_out) and not a.fluid.rhs_valid(1 - s_out)
+    # any write of a density of that state makes the fused rhs stale
+    a.tree.copy_cc(IV["pos"], IV["pos"])
+    assert not a.fluid.rhs_valid(0)
+    with pytest.raises(capi.AfhError):
+        a.fluid.rhs_maxabs(0)
     # a whole Heun step through field_compute reuses the fused rhs
-    a._rhs_state = b._rhs_state = None
     for c in (a, b):
         c.field_compute(0)
     la, lb = a.heun_step(1e-12), b.heun_step(1e-12)
