@@ -84,7 +84,8 @@ class FluidDesc(C.Structure):
                 ("reactions", C.POINTER(Reaction)), ("dt_chemistry_nmin", f64),
                 ("gas_temperature", f64), ("td_energy_col", i32),
                 ("i_gas_dens", i32), ("n_gas_species", i32),
-                ("gas_fractions", f64 * 8)]
+                ("gas_fractions", f64 * 8), ("i_photo", i32),
+                ("photo_species", i32)]
 
 
 class MgDesc(C.Structure):
@@ -157,6 +158,8 @@ SIGNATURES = {
     "fluid_set_rhs_output": (i32, [_VP, i32, i32]),
     "fluid_rhs_maxabs": (i32, [_VP, i32, P_f64]),
     "fluid_rhs_valid": (i32, [_VP, i32, P_i32]),
+    "photoi_set_src": (i32, [_VP, i32, i32, f64]),
+    "photoi_helmh_compute": (i32, [C.POINTER(_VP), i32, P_f64, i32, f64, i32, P_i32]),
     "field_set_rhs": (i32, [_VP, i32, i32]),
     "field_set_rhs_maxabs": (i32, [_VP, i32, i32, P_f64]),
     "flux_upwind_tree": (i32, [_VP, i32, P_f64]),

@@ -1,0 +1,569 @@
+"""The streamer time loop over the device path (src/streamer.f90 restated).
+
+``Simulation`` is what the reference's main program does around the hot
+path, with every per-cell operation a call into the C ABI (the HIP library,
+or the C oracle for the CPU twin) and the mesh topology on the host
+(afh.amr.AfTree, af_adjust_refinement restated):
+
+* set-up: the variable registry, tables and reactions as the reference's
+  initializers left them (a case exported by oracle/_ref/export_case from a
+  .cfg, tests/golden/rtest_*.npz), af_init + set_initial_conditions
+  (streamer.f90:460-519: af_refine_up_to_lvl to refine_max_dx,
+  init_cond_set_box, then field_compute without a guess + refinement until
+  no box is added);
+* the time loop (streamer.f90:177-415): output times, step retry with
+  copy_current_state / restore_previous_state (639-668), af_advance with
+  Heun's method (m_af_advance.f90:160-164) around forward_euler
+  (m_fluid.f90:21-99), field_compute after the step, the dt update,
+  photoi_set_src every photoi_per_steps, and a regrid every refine_per_steps
+  (restrict + ghost cells of the densities, default_refinement on the device,
+  af_adjust_refinement on the host, afh_tree_regrid on the device);
+* output_regression_log (src/m_output.f90:783-837) from device reductions.
+
+Parameters the reference reads from its .cfg come from the exported case;
+routines it takes as callbacks are the library's (field_bc_homogeneous,
+af_bc_neumann_zero, photoi_helmh_bc, default_refinement).
+"""
+import math
+
+import numpy as np
+
+from . import capi
+from .amr import AfTree
+from .model import Fluid, Multigrid, Tree, photoi_helmh_compute
+
+UC_EPS0 = 8.8541878176e-12
+UC_ELEM_CHARGE = 1.6022e-19
+
+# Bourdon-3 Helmholtz photoionization modes, src/m_photoi_helmh.f90:106-118
+# (SI values; lambdas * frac_O2 * p, coeffs * (frac_O2 * p)^2)
+BOURDON3_LAMBDAS = (4147.85, 10950.93, 66755.67)
+BOURDON3_COEFFS = (1117314.935, 28692377.5, 2748842283.0)
+
+
+class Case:
+    """Accessors for an exported case (oracle/make_cases.py arrays)."""
+
+    def __init__(self, d):
+        self.d = dict(d)
+
+    def r(self, k):
+        return float(self.d[k][0])
+
+    def ra(self, k):
+        return np.asarray(self.d[k], float)
+
+    def i(self, k):
+        return int(self.d[k][0])
+
+    def ia(self, k):
+        return [int(x) for x in self.d[k]]
+
+    def s(self, k):
+        return str(self.d[k][0])
+
+    def sa(self, k):
+        return [str(x) for x in self.d[k]]
+
+    def lt(self, name):
+        n_points, n_cols = self.ia(name + "_shape")
+        rc = self.ra(name + "_rows_cols").reshape(n_cols, n_points).T
+        return {"rows_cols": rc, "x_min": self.r(name + "_xmin"),
+                "inv_fac": self.r(name + "_inv_fac")}
+
+
+def _norm2(v):
+    """gfortran's NORM2 (scaled sum of squares)."""
+    scale, ssq = 0.0, 1.0
+    for x in v:
+        if x != 0.0:
+            a = abs(x)
+            if scale < a:
+                ssq = 1.0 + ssq * (scale / a) ** 2
+                scale = a
+            else:
+                ssq = ssq + (a / scale) ** 2
+    return scale * math.sqrt(ssq)
+
+
+def _dist_vec_line(r, r0, r1):
+    """GM_dist_vec_line (src/m_geometry.f90:23-43) for an array of points r
+    (n, 3): distance vectors and fractions."""
+    d = r1 - r0
+    line_len2 = np.sum(d * d)
+    frac = np.sum((r - r0) * d, axis=1)
+    dv = np.empty_like(r)
+    lo, hi = frac <= 0.0, frac >= line_len2
+    mid = ~(lo | hi)
+    dv[lo] = r[lo] - r0
+    dv[hi] = r[hi] - r1
+    f = frac[mid] / line_len2
+    dv[mid] = r[mid] - (r0 + (frac[mid, None] / line_len2) * d)
+    out = np.zeros(len(r))
+    out[hi] = 1.0
+    out[mid] = f
+    return dv, out
+
+
+def density_line(r, r0, r1, n0, n1, width, falloff):
+    """GM_density_line (src/m_geometry.f90:53-113) at points r (n, 3)."""
+    dv, frac = _dist_vec_line(r, r0, r1)
+    dist = np.array([_norm2(v) for v in dv])
+    if falloff == "smoothstep":
+        t = dist / width - 1
+        val = np.where(dist < width, 1.0,
+                       np.where(dist < 2 * width, 1 - (3 * (t * t) - 2 * (t * t * t)), 0.0))
+    elif falloff == "gaussian":
+        val = np.exp(-(dist / width) ** 2)
+    elif falloff == "step":
+        val = np.where(dist < width, 1.0, 0.0)
+    elif falloff == "sigmoid":
+        tmp = dist / width
+        val = np.where(tmp > math.log(0.5 * np.finfo(float).max), 0.0,
+                       2 / (1 + np.exp(np.minimum(tmp, 700.0))))
+    else:
+        raise ValueError("seed_falloff %s not supported" % falloff)
+    return val * (frac * n0 + (1 - frac) * n1)
+
+
+class Simulation:
+    """One streamer simulation (src/streamer.f90) over a C-ABI library."""
+
+    def __init__(self, lib, case, device=-1, coarse_cycles=0, capacity_factor=2.0,
+                 fuse_rhs=True):
+        c = case if isinstance(case, Case) else Case(case)
+        self.c, self.lib, self.device = c, lib, device
+        self.coarse_cycles = coarse_cycles
+        self.capacity_factor = capacity_factor
+        self.fused_rhs = fuse_rhs
+        if c.s("time_integrator") != "heuns_method":
+            raise NotImplementedError("time integrator %s" % c.s("time_integrator"))
+        self.n_states = 2  # af_advance_num_steps(af_heuns_method)
+        if c.i("use_electrode") or c.i("use_dielectric") or c.i("cylindrical"):
+            raise NotImplementedError("electrode / dielectric / cylindrical cases")
+        if not c.i("gas_constant_density"):
+            raise NotImplementedError("variable gas density cases")
+        # registry (af_add_cc_variable order of the reference's modules)
+        self.cc_names = c.sa("cc_names")
+        self.n_var_cell, self.n_var_face = len(self.cc_names), len(c.sa("fc_names"))
+        (self.i_phi, self.i_electron, self.i_1pos_ion, self.i_efld, self.i_rhs,
+         self.i_tmp, self.i_photo, self.f_flux, self.f_field, _) = c.ia("ivars")
+        n_species, self.n_gas, n_reac = c.ia("n_species")
+        self.species_list = c.sa("species_list")
+        self.species_charge = c.ia("species_charge")
+        self.species_itree = c.ia("species_itree")
+        self.densities = c.ia("all_densities")
+        self.plasma = [n for n in range(n_species) if self.species_itree[n] > 0]
+        self.N = c.r("gas_number_density")
+        self.L = c.ra("domain_len")
+        self.origin = c.ra("domain_origin")
+        # field_given_by (m_field.f90:132-170): the exported voltage at t = 0
+        if c.r("current_voltage") != 0 and "table" in c.s("field_given_by"):
+            raise NotImplementedError("tabulated voltages")
+        self.voltage = c.r("current_voltage")
+        # dt parameters (m_dt.f90)
+        self.dt_max, self.dt_min = c.r("dt_max"), c.r("dt_min")
+        self.dt_safety = c.r("dt_safety_factor")
+        self.cfl = c.r("dt_cfl_number_value")
+        self.dt_growth = c.r("dt_max_growth_factor")
+        self.num_vcycles = c.i("multigrid_num_vcycles")
+        self.max_rel_res = c.r("multigrid_max_rel_residual")
+        # photoionization (m_photoi.f90, m_photoi_helmh.f90)
+        self.photoi = bool(c.i("photoi%enabled"))
+        if self.photoi:
+            if c.s("photoi%method") != "helmholtz" or c.s("photoi%source_type") != "Zheleznyak":
+                raise NotImplementedError("photoionization other than Helmholtz/Zheleznyak")
+            if c.s("photoi_helmh%author") != "Bourdon-3":
+                raise NotImplementedError("Helmholtz modes other than Bourdon-3")
+            comps = c.sa("gas_components")
+            frac_o2 = c.ra("gas_fractions")[comps.index("O2")] if "O2" in comps else 0.0
+            p = c.r("gas_pressure_value")
+            self.helm_lambdas = [lam * frac_o2 * p for lam in BOURDON3_LAMBDAS]
+            self.helm_coeffs = [cf * (frac_o2 * p) ** 2 for cf in BOURDON3_COEFFS]
+            self.helm_iv = [self.cc_names.index("helmh_%d" % (n + 1)) + 1 for n in range(3)]
+            qp = c.r("photoi%quenching_pressure")
+            self.photoi_coeff = c.r("photoi%eta") * (qp / (c.r("gas_pressure_value") + qp))
+            self.photo_species = c.i("photoi_species_index") - self.n_gas
+        self.td = c.lt("td")
+        self.chem = c.lt("chem")
+        self.reactions = []
+        for n in range(1, n_reac + 1):
+            rt, _, n_coeff, lti, _ = c.ia("reaction_%d" % n)
+            if n_coeff > 4:
+                raise NotImplementedError("rate with %d coefficients" % n_coeff)
+            shift = lambda ix: [x - self.n_gas for x in ix]  # noqa: E731
+            self.reactions.append({
+                "rate_type": rt, "table_col": lti,
+                "rate_factor": c.r("reaction_%d_factor" % n),
+                "c": list(c.ra("reaction_%d_data" % n)),
+                "ix_in": shift(c.ia("reaction_%d_in" % n)),
+                "ix_out": shift(c.ia("reaction_%d_out" % n)),
+                "mult_out": c.ia("reaction_%d_mult" % n)})
+        # init conditions (m_init_cond.f90:38-144)
+        self.background = c.r("background_density")
+        self.seeds = []
+        for n in range(len(c.ra("seed_density"))):
+            self.seeds.append({
+                "r0": c.ra("seed_rel_r0")[3 * n:3 * n + 3] * self.L + self.origin,
+                "r1": c.ra("seed_rel_r1")[3 * n:3 * n + 3] * self.L + self.origin,
+                "n0": c.ra("seed_density")[n], "n1": c.ra("seed_density2")[n],
+                "type": c.ia("seed_charge_type")[n], "width": c.ra("seed_width")[n],
+                "falloff": c.sa("seed_falloff")[n]})
+        # state (streamer.f90:107-114, initialize_modules: global_dt = dt_min)
+        self.it = 0
+        self.time = self.global_time = self.photoi_prev_time = 0.0
+        self.global_dt = self.dt = self.dt_min
+        self.n_steps_rejected = 0
+        self.frac_rejected = 0.0
+        self.output_cnt = 0
+        self.log = []
+        # mesh: af_init (streamer.f90:151-153)
+        nc = c.i("box_size")
+        self.af = AfTree(nc, self.origin + self.L, c.ia("coarse_grid_size_value"),
+                         r_min=self.origin)
+        self.tree = self.fluid = self.mg = None
+        self.helm = []
+
+    # ------------------------------------------------------------- device
+    def _capacity(self):
+        return max(64, int(self.capacity_factor * self.af.highest_id))
+
+    def _bind(self, tree):
+        """Multigrid and fluid state bound to a (new) device tree."""
+        for m in [self.mg] + self.helm:
+            if m is not None:
+                m.close()
+        if self.fluid is not None:
+            self.fluid.close()
+        self.tree = tree
+        self.mg = Multigrid(tree, self.i_phi, self.i_rhs, self.i_tmp,
+                            coarse_cycles=self.coarse_cycles)
+        self.helm = []
+        if self.photoi:
+            for iv, lam in zip(self.helm_iv, self.helm_lambdas):
+                self.helm.append(Multigrid(tree, iv, self.i_rhs, self.i_tmp,
+                                           helmholtz_lambda=lam * lam,
+                                           coarse_cycles=self.coarse_cycles))
+        c = self.c
+        td_cols = c.ia("td_cols")
+        self.fluid = Fluid(
+            tree, [self.species_itree[n] for n in self.plasma],
+            [self.species_charge[n] for n in self.plasma], self.i_electron,
+            self.i_efld, self.f_flux, self.f_field, self.N, self.td, self.chem,
+            self.reactions, dt_chemistry_nmin=c.r("dt_chemistry_nmin"),
+            gas_temperature=c.r("gas_temperature_value"),
+            td_energy_col=max(0, td_cols[4]),
+            i_photo=self.i_photo if self.photoi else 0,
+            photo_species=self.photo_species if self.photoi else 0)
+        if self.fused_rhs:
+            self.fluid.set_rhs_output(self.i_rhs, True)
+
+    def _create_tree(self):
+        t = Tree(self.lib, self.af.topology(), self.n_var_cell, self.n_var_face,
+                 device=self.device, box_capacity=self._capacity())
+        neumann0 = [(capi.BC_NEUMANN, 0.0)] * 6
+        # z faces Dirichlet 0, other faces Neumann 0 (photoi_helmh_bc)
+        helm_bc = [(capi.BC_NEUMANN, 0.0)] * 4 + [(capi.BC_DIRICHLET, 0.0)] * 2
+        if self.photoi:  # photoi_initialize (m_photoi.f90:105-106): first auto var
+            t.set_cc_methods(self.i_photo, helm_bc, capi.RB_GC_INTERP)
+            t.set_cc_prolong(self.i_photo, capi.PROLONG_LINEAR)
+            for iv in self.helm_iv:  # mg_helm(n)%sides_bc, mg_sides_rb
+                t.set_cc_methods(iv, helm_bc, capi.RB_MG_SIDES)
+        # field_initialize (m_field.f90:349-350)
+        t.set_cc_methods(self.i_efld, neumann0, capi.RB_GC_INTERP)
+        t.set_cc_prolong(self.i_efld, capi.PROLONG_LINEAR)
+        # streamer.f90:81-84: densities and their copies, af_gc_interp_lim,
+        # af_prolong_limit (prolong_density = limit), gminmod43
+        for iv in self.densities:
+            for s in range(self.n_states + 1):
+                t.set_cc_methods(iv + s, neumann0, capi.RB_GC_INTERP_LIM)
+            t.set_cc_prolong(iv, capi.PROLONG_LIMIT)
+        # phi and its copy: field_bc_homogeneous, mg_sides_rb
+        for s in (0, 1):
+            t.set_cc_methods(self.i_phi + s, self.phi_bc(), capi.RB_MG_SIDES)
+        # streamer.f90:98-104: rhs gets neumann_zero, af_gc_interp, limit
+        t.set_cc_methods(self.i_rhs, neumann0, capi.RB_GC_INTERP)
+        t.set_cc_prolong(self.i_rhs, capi.PROLONG_LIMIT)
+        return t
+
+    def phi_bc(self):
+        """field_bc_homogeneous (src/m_field.f90:547-567)."""
+        return [(capi.BC_NEUMANN, 0.0)] * 4 + [(capi.BC_DIRICHLET, 0.0),
+                                               (capi.BC_DIRICHLET, self.voltage)]
+
+    # --------------------------------------------------------- physics
+    def field_from_potential(self):
+        """m_field.f90:488-505."""
+        self.mg.compute_phi_gradient(self.f_field, -1.0, self.i_efld)
+        self.tree.gc_tree(self.i_efld)
+
+    def field_compute(self, s_in, have_guess=True):
+        """field_compute (src/m_field.f90:405-485); returns the residuals."""
+        if self.fused_rhs and self.fluid.rhs_valid(s_in):
+            max_rhs = self.fluid.rhs_maxabs(s_in)
+        else:
+            max_rhs = self.fluid.field_set_rhs_maxabs(self.i_rhs, s_in)
+        conv_fac = 1e-10
+        threshold = max(1e-6, max_rhs * self.max_rel_res,
+                        conv_fac * abs(self.voltage) / (self.L[2] * self.af.min_dr()))
+        res = []
+        if not have_guess:
+            for i in range(1, 101):
+                self.mg.fas_fmg(True, have_guess=True)
+                res.append(self.tree.maxabs_cc(self.i_tmp))
+                if res[-1] < threshold:
+                    break
+                if i > 2:
+                    ratio = min(res[-3:]) / max(res[-3:])
+                    if 0.5 < ratio < 2.0 and res[-1] < 1e8:
+                        break
+            else:
+                raise RuntimeError("No convergence in initial field computation")
+        vres = []
+        for _ in range(self.num_vcycles):
+            vres.append(self.mg.fas_vcycle_maxres())
+            if vres[-1] < threshold:
+                break
+        self.field_from_potential()
+        return res + vres
+
+    def forward_euler(self, dt, s_deriv, s_prev, w_prev, s_out, i_step, n_steps):
+        """forward_euler (src/m_fluid.f90:21-99): returns dt_lim."""
+        if i_step > 1:
+            self.field_compute(s_deriv, True)
+        lim = self.fluid.forward_euler(dt, s_deriv, s_prev, w_prev, s_out,
+                                       i_step == n_steps)
+        limits = [lim[0] * self.cfl, lim[1], lim[2], lim[3]]
+        return min(self.dt_max, min(limits))
+
+    def advance(self, dt):
+        """af_advance with af_heuns_method (m_af_advance.f90:121-214): dt_lim
+        of the last sub-step."""
+        self.forward_euler(dt, 0, [0], [1.0], 1, 1, 2)
+        dt_lim = self.forward_euler(0.5 * dt, 1, [0, 1], [0.5, 0.5], 0, 2, 2)
+        self.time = self.time + dt
+        return dt_lim
+
+    def copy_current_state(self):
+        """streamer.f90:639-651."""
+        for iv in self.densities:
+            self.tree.copy_cc(iv, iv + self.n_states)
+        self.tree.copy_cc(self.i_phi, self.i_phi + 1)
+
+    def restore_previous_state(self):
+        """streamer.f90:654-668."""
+        for iv in self.densities:
+            self.tree.copy_cc(iv + self.n_states, iv)
+        self.tree.copy_cc(self.i_phi + 1, self.i_phi)
+        self.field_from_potential()
+
+    def photoi_set_src(self):
+        """photoi_set_src (src/m_photoi.f90:140-186), Zheleznyak + Helmholtz."""
+        self.fluid.photoi_set_src(self.i_rhs, self.photoi_coeff, alpha_col=3)
+        return photoi_helmh_compute(self.helm, self.helm_coeffs, self.i_photo,
+                                    self.c.r("photoi_helmh%max_rel_residual"), 10)
+
+    # ------------------------------------------------------- refinement
+    def refine_desc(self):
+        """default_refinement's parameters (src/m_refine.f90:198-298) as of
+        global_time."""
+        c = self.c
+        d = capi.RefineDesc()
+        d.i_electron, d.i_efld = self.i_electron, self.i_efld
+        d.td_alpha_col, d.td_eta_col = 3, 4
+        d.use_alpha_effective = c.i("refine_use_alpha_effective")
+        d.buffer_width = c.i("refine_buffer_width")
+        d.adx_fac, d.adx = c.r("refine_adx_fac"), c.r("refine_adx")
+        d.min_dens, d.derefine_dx = c.r("refine_min_dens"), c.r("derefine_dx")
+        d.max_dx, d.min_dx = c.r("refine_max_dx"), c.r("refine_min_dx")
+        d.electrode_dx = c.r("refine_electrode_dx")
+        d.init_fac = c.r("refine_init_fac")
+        d.n_seeds = 0
+        if self.global_time < c.r("refine_init_time"):
+            d.n_seeds = len(self.seeds)
+            for n, sd in enumerate(self.seeds):
+                d.seed_r0[n][:] = list(sd["r0"])
+                d.seed_r1[n][:] = list(sd["r1"])
+                d.seed_width[n] = sd["width"]
+        rdr, rts = c.ra("refine_regions_dr"), c.ra("refine_regions_tstop")
+        rmin, rmax = c.ra("refine_regions_rmin"), c.ra("refine_regions_rmax")
+        k = 0
+        for n in range(len(rdr)):
+            if self.global_time <= rts[n]:
+                d.region_dr[k] = rdr[n]
+                d.region_rmin[k][:] = list(rmin[3 * n:3 * n + 3])
+                d.region_rmax[k][:] = list(rmax[3 * n:3 * n + 3])
+                k += 1
+        d.n_regions = k
+        ldr = c.ra("refine_limits_dr")
+        lmin, lmax = c.ra("refine_limits_rmin"), c.ra("refine_limits_rmax")
+        d.n_limits = len(ldr)
+        for n in range(len(ldr)):
+            d.limit_dr[n] = ldr[n]
+            d.limit_rmin[n][:] = list(lmin[3 * n:3 * n + 3])
+            d.limit_rmax[n][:] = list(lmax[3 * n:3 * n + 3])
+        return d
+
+    def adjust_refinement(self):
+        """af_adjust_refinement with default_refinement: the criterion on the
+        device, the topology on the host, the data moved by the device."""
+        flags, masks = self.fluid.refine_flags(self.refine_desc())
+
+        def fn(ids):
+            ix = np.asarray(ids, np.int64) - 1
+            return flags[ix], masks[ix]
+
+        info = self.af.adjust_refinement(fn)
+        if info.n_add or info.n_rm:
+            new = self.tree.regrid(self.af.topology())
+            old = self.tree
+            self._bind(new)
+            old.close()
+        return info
+
+    # -------------------------------------------------- initial state
+    def init_cond_set_box(self, ids, arrays):
+        """init_cond_set_box (src/m_init_cond.f90:217-291) on boxes `ids`
+        (cells 0..nc+1), into host arrays {iv: (n_boxes, ng, ng, ng)}."""
+        nc = self.af.nc
+        ng = nc + 2
+        idx = np.arange(ng) - 0.5  # af_r_cc: r_min + (i - 0.5) dr
+        ne, ni = arrays[self.i_electron], arrays[self.i_1pos_ion]
+        for b in ids:
+            rmin, dr = self.af.r_min[b], self.af.dr[b]
+            x = rmin[0] + idx * dr[0]
+            y = rmin[1] + idx * dr[1]
+            z = rmin[2] + idx * dr[2]
+            zz, yy, xx = np.meshgrid(z, y, x, indexing="ij")
+            r = np.stack([xx.ravel(), yy.ravel(), zz.ravel()], axis=1)
+            e = np.full(ng ** 3, self.background)
+            p = np.full(ng ** 3, self.background)
+            for sd in self.seeds:
+                dens = density_line(r, sd["r0"], sd["r1"], sd["n0"], sd["n1"],
+                                    sd["width"], sd["falloff"])
+                if sd["type"] == -1:
+                    e = e + dens
+                elif sd["type"] == 0:
+                    p = p + dens
+                    e = e + dens
+                elif sd["type"] == 1:
+                    p = p + dens
+                else:
+                    raise ValueError("Invalid seed_charge_type")
+            ne[b - 1] = e.reshape(ng, ng, ng)
+            ni[b - 1] = p.reshape(ng, ng, ng)
+
+    def _set_init(self, ids):
+        arrays = {iv: self.tree.get_cc(iv) for iv in (self.i_electron, self.i_1pos_ion)}
+        self.init_cond_set_box(ids, arrays)
+        for iv, a in arrays.items():
+            self.tree.put_cc(iv, a)
+
+    def set_initial_conditions(self):
+        """streamer.f90:460-519."""
+        c = self.c
+        max_dx = c.r("refine_max_dx")
+        lvl = 1
+        while lvl < 29 and not np.all(self.af.lvl_dr(lvl) <= max_dx):
+            lvl += 1
+        self.af.refine_up_to_lvl(lvl)
+        self._bind(self._create_tree())
+        all_ids = [b for l in range(1, self.af.highest_lvl + 1)
+                   for b in self.af.lvls[l]["ids"]]
+        self._set_init(all_ids)
+        for _ in range(100):
+            self.field_compute(0, have_guess=False)
+            info = self.adjust_refinement()
+            added = [b for l in sorted(info.add) for b in info.add[l]]
+            if added:
+                self._set_init(added)
+            if info.n_add == 0:
+                break
+
+    # ------------------------------------------------------------- output
+    def regression_row(self):
+        """output_regression_log (src/m_output.f90:783-837): it, time, dt,
+        then per species sum(n)/vol, sum(n^2)/vol, max(n)."""
+        vol = self.af.total_volume()
+        ns = len(self.species_list)
+        sums, sq, mx = np.zeros(ns), np.zeros(ns), np.zeros(ns)
+        for n in range(ns):
+            iv = self.species_itree[n]
+            if iv > 0:
+                sums[n] = self.tree.sum_cc(iv, 1)
+                sq[n] = self.tree.sum_cc(iv, 2)
+                mx[n] = self.tree.max_cc(iv)
+        return np.concatenate([[self.output_cnt, self.global_time, self.global_dt],
+                               sums / vol, sq / vol, mx])
+
+    def output_write(self):
+        self.log.append(self.regression_row())
+
+    # --------------------------------------------------------------- run
+    def step(self):
+        """One iteration of the main loop (streamer.f90:177-415); False at
+        the end time."""
+        c = self.c
+        self.it += 1
+        if self.time >= c.r("end_time"):
+            return False
+        output_dt = c.r("output%dt")
+        write_out = self.time + self.dt >= self.time_last_output + output_dt
+        if write_out:
+            self.dt = max(0.0, self.time_last_output + output_dt - self.time)
+        # (no pulses: field_pulse_period = huge, start_of_new_pulse is false)
+        if self.photoi and self.it % c.i("photoi%per_steps") == 0:
+            self.photoi_set_src()
+            self.photoi_prev_time = self.time
+        dt_lim = 1e100
+        for n in range(1, 11):
+            self.copy_current_state()
+            dt_lim_step = self.advance(self.dt)
+            dt_lim = min(dt_lim, dt_lim_step)
+            if self.dt <= dt_lim_step:
+                break
+            self.n_steps_rejected += 1
+            self.dt = self.dt_safety * dt_lim_step
+            self.time = self.global_time
+            write_out = False
+            self.restore_previous_state()
+        else:
+            raise RuntimeError("All time steps were rejected")
+        self.frac_rejected = 0.99 * self.frac_rejected + (0.01 if n > 1 else 0.0)
+        self.field_compute(0, True)
+        tmp = self.dt_growth if self.frac_rejected <= 0.1 else 1.0
+        self.dt = min(tmp * self.global_dt, self.dt_safety * min(dt_lim, self.dt_max))
+        self.global_dt = self.dt
+        self.global_time = self.time
+        if self.global_dt < self.dt_min:
+            raise RuntimeError("dt too small")
+        if write_out:
+            self.output_cnt += 1
+            self.time_last_output = self.global_time
+            self.output_write()
+        if self.it % c.i("refine_per_steps") == 0:
+            for iv in self.densities:
+                self.tree.restrict_tree(iv)
+                self.tree.gc_tree(iv)
+            info = self.adjust_refinement()
+            if info.n_add > 0 or info.n_rm > 0:
+                self.field_compute(0, True)
+                if self.photoi:
+                    self.photoi_set_src()
+                    self.photoi_prev_time = self.time
+        return True
+
+    def start(self):
+        self.set_initial_conditions()
+        self.output_cnt = 0
+        self.output_write()
+        self.time_last_output = self.time
+
+    def run(self, max_steps=None):
+        self.start()
+        n = 0
+        while self.step():
+            n += 1
+            if max_steps is not None and n >= max_steps:
+                break
+        return np.array(self.log)

@@ -36,6 +36,11 @@ class Tree:
         the topology's box count); a regrid that fits them works in place."""
         self.lib = lib
         self.topo = topo
+        # multigrid / fluid objects bound to this tree: closed before it, so
+        # that no library object outlives the tree it points to. Strong
+        # references: the garbage collector clears weak references before it
+        # finalizes a cycle, in any order.
+        self._deps = []
         self.nc = int(topo["nc"])
         self.n_boxes = int(topo["n_boxes"])
         self.highest_lvl = int(topo["highest_lvl"])
@@ -89,6 +94,8 @@ class Tree:
 
     # -- lifetime
     def close(self):
+        for d in list(self._deps):
+            d.close()
         if self.h:
             self.lib.call("tree_destroy", self.h)
             self.h = C.c_void_p()
@@ -204,11 +211,14 @@ class Multigrid:
         h = C.c_void_p()
         self.lib.call("mg_create", tree.h, C.byref(d), C.byref(h))
         self.h = h
+        tree._deps.append(self)
 
     def close(self):
         if self.h:
             self.lib.call("mg_destroy", self.h)
             self.h = C.c_void_p()
+        if self in self.tree._deps:
+            self.tree._deps.remove(self)
 
     def __del__(self):
         try:
@@ -270,7 +280,7 @@ class Fluid:
                  f_flux, f_field, gas_number_density, td, chem, reactions,
                  limiter=capi.LIM_KOREN, dt_chemistry_nmin=-1.0,
                  gas_temperature=300.0, td_energy_col=0, i_gas_dens=0,
-                 gas_fractions=()):
+                 gas_fractions=(), i_photo=0, photo_species=0):
         self.tree = tree
         self.lib = tree.lib
         d = capi.FluidDesc()
@@ -311,14 +321,18 @@ class Fluid:
         d.i_gas_dens = i_gas_dens
         d.n_gas_species = len(gas_fractions)
         d.gas_fractions[:len(gas_fractions)] = list(gas_fractions)
+        d.i_photo, d.photo_species = int(i_photo), int(photo_species)
         h = C.c_void_p()
         self.lib.call("fluid_create", tree.h, C.byref(d), C.byref(h))
         self.h = h
+        tree._deps.append(self)
 
     def close(self):
         if self.h:
             self.lib.call("fluid_destroy", self.h)
             self.h = C.c_void_p()
+        if self in self.tree._deps:
+            self.tree._deps.remove(self)
 
     def __del__(self):
         try:
@@ -342,6 +356,11 @@ class Fluid:
         out = C.c_double()
         self.lib.call("fluid_rhs_maxabs", self.h, s_out, C.byref(out))
         return out.value
+
+    def photoi_set_src(self, i_rhs, coeff, alpha_col=3):
+        """photoi_set_src's Zheleznyak source (photoionization_rate_from_alpha,
+        src/m_photoi.f90:217-253) into i_rhs on the leaf interiors."""
+        self.lib.call("photoi_set_src", self.h, int(i_rhs), int(alpha_col), float(coeff))
 
     def rhs_valid(self, s_out):
         """Whether the rhs the last update wrote for state s_out is still
@@ -398,3 +417,16 @@ class Fluid:
                       sp.ctypes.data_as(capi.P_i32), wp.ctypes.data_as(capi.P_f64),
                       s_out, int(last_step), int(store_flux), out)
         return out[0], out[1], out[2], out[3]
+
+
+def photoi_helmh_compute(modes, coeffs, i_photo, max_rel_res=1e-2, max_fmg=10):
+    """photoi_helmh_compute (src/m_photoi_helmh.f90:162-204) over the
+    Helmholtz multigrid modes (Multigrid objects sharing one tree); returns the
+    FMG cycles each mode took."""
+    lib = modes[0].lib
+    hs = (C.c_void_p * len(modes))(*[m.h.value for m in modes])
+    cf = np.ascontiguousarray(coeffs, dtype=np.float64)
+    n = np.zeros(len(modes), np.int32)
+    lib.call("photoi_helmh_compute", hs, len(modes), cf.ctypes.data_as(capi.P_f64),
+             int(i_photo), float(max_rel_res), int(max_fmg), n.ctypes.data_as(capi.P_i32))
+    return list(n)

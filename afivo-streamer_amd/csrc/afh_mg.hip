@@ -15,6 +15,8 @@
 #include <hip/hip_ext.h>
 
 #include <algorithm>
+#include <cfloat>
+#include <cmath>
 
 #include "afh_internal.h"
 
@@ -2474,6 +2476,66 @@ int32_t afh_mg_set_box_lsf(afh_mg *mg, int32_t id, int32_t n, const int32_t *ix,
                     hipMemcpyHostToDevice));
   mg->h_lsf_n[id - 1] = n;
   mg->i_lsf = i_lsf;
+  return AFH_OK;
+}
+
+}  // extern "C"
+
+// photoi_helmh_compute (src/m_photoi_helmh.f90:162-204): the mode loop of
+// Helmholtz FAS-FMG solves and the sum of the modes into the
+// photoionization rate
+namespace afh {
+// y -= c * x over whole boxes (ghost cells included) of the listed boxes
+__global__ void k_box_axpy(double *__restrict__ y, const double *__restrict__ x,
+                           double c, const int32_t *__restrict__ ids, size_t bsz) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= bsz) return;
+  const size_t q = (size_t)(ids[blockIdx.y] - 1) * bsz + t;
+  y[q] = y[q] - c * x[q];
+}
+}  // namespace afh
+
+extern "C" {
+
+int32_t afh_photoi_helmh_compute(afh_mg *const *modes, int32_t n_modes,
+                                 const double *coeffs, int32_t i_photo,
+                                 double max_rel_res, int32_t max_fmg,
+                                 int32_t *n_fmg) {
+  if (!modes || n_modes < 1 || !coeffs || max_fmg < 1)
+    return set_error(AFH_ERR_ARG, "afh_photoi_helmh_compute: bad argument");
+  afh_tree *t = modes[0] ? modes[0]->t : nullptr;
+  AFH_LIVE(t, "afh_photoi_helmh_compute");
+  for (int n = 0; n < n_modes; n++)
+    if (!modes[n] || modes[n]->t != t)
+      return set_error(AFH_ERR_ARG, "helmholtz modes must share one tree");
+  if (i_photo < 1 || i_photo > t->nvc) return set_error(AFH_ERR_ARG, "bad i_photo");
+  t->touch(i_photo);
+  // af_tree_clear_cc(tree, i_photo)
+  AFH_HIP(hipMemsetAsync(t->ccv(i_photo), 0, sizeof(double) * t->bsz * t->nb, t->stream));
+  double max_rhs;
+  int32_t e;
+  if ((e = afh_tree_maxabs_cc(t, modes[0]->d.i_rhs, &max_rhs))) return e;
+  max_rhs = std::max(max_rhs, std::sqrt(DBL_EPSILON));
+  for (int n = 0; n < n_modes; n++) {
+    afh_mg *mg = modes[n];
+    int i;
+    for (i = 1; i <= max_fmg; i++) {
+      double residu;
+      if ((e = afh_mg_fas_fmg(mg, 1, 1)) ||
+          (e = afh_tree_maxabs_cc(t, mg->d.i_tmp, &residu)))
+        return e;
+      if (residu / max_rhs < max_rel_res) break;
+    }
+    if (n_fmg) n_fmg[n] = std::min(i, max_fmg);
+    for (int l = 1; l <= t->nlvl; l++) {
+      const int nl = t->leaves.n(l);
+      if (!nl) continue;
+      hipLaunchKernelGGL(k_box_axpy, dim3((unsigned)((t->bsz + 255) / 256), nl),
+                         dim3(256), 0, t->stream, t->ccv(i_photo),
+                         t->ccv(mg->d.i_phi), coeffs[n], t->leaves.at(l), t->bsz);
+      AFH_LAUNCH_CHECK("k_box_axpy");
+    }
+  }
   return AFH_OK;
 }
 

@@ -526,6 +526,10 @@ struct UpdArgs {
   double *rhs;
   double rq[MAXS];
   unsigned long long *rhs_red;
+  // photoionization rate (or null), added to the electron and species
+  // slot photo_s after the chemistry limit (m_fluid.f90:435-440)
+  const double *photo;
+  int photo_s;
 };
 
 // Register-resident species arrays indexed by runtime reaction data: the
@@ -953,6 +957,7 @@ __global__ void __launch_bounds__(256, AFH_UPD_MINW)
     const double fx0 = F[f0], fx1 = F[f0 + 1], fy0 = F[d3 + f0], fy1 = F[d3 + f0 + nf],
                  fz0 = F[2 * d3 + f0], fz1 = F[2 * d3 + f0 + nf * nf];
     const double ev = A.E[x];
+    const double pho = A.photo ? A.photo[x] : 0.0;
     const int n_prev = NP == MAXPREV ? A.n_prev : NP;
     const int der_q = (NP == MAXPREV || SD) ? A.der_q : -2;  // -2: see below
     double pv[NS][NP], dv[NS];
@@ -1020,6 +1025,10 @@ __global__ void __launch_bounds__(256, AFH_UPD_MINW)
         }
         cmin = fmin(cmin, a / b);
       }
+    }
+    if (A.photo) {
+      add_at(der, A.e_index, pho);
+      add_at(der, A.photo_s, pho);
     }
 #pragma unroll
     for (int s = 0; s < NS; s++) y[s] = y[s] + A.dt * der[s];
@@ -1644,6 +1653,9 @@ int32_t afh_fluid_create(afh_tree *t, const afh_fluid_desc *d, afh_fluid **out) 
     return set_error(AFH_ERR_ARG, "bad gas density variable / gas species count");
   if (!t->meth[d->i_electron].set)
     return set_error(AFH_ERR_STATE, "set cc methods for the electrons first");
+  if (d->i_photo < 0 || d->i_photo > t->nvc ||
+      (d->i_photo > 0 && (d->photo_species < 1 || d->photo_species > d->n_species)))
+    return set_error(AFH_ERR_ARG, "bad photoionization variable / species");
   size_t ntd = (size_t)d->td.n_points * d->td.n_cols;
   size_t nch = (size_t)d->chem.n_points * d->chem.n_cols;
   AFH_HIP(hipMalloc(&f->d_td, ntd * sizeof(double)));
@@ -1961,12 +1973,14 @@ static int32_t upd_args(afh_fluid *f, double dt, int32_t s_deriv, int32_t n_prev
   A.rhs_red = reinterpret_cast<unsigned long long *>(t->scratch) + 4 * RED_SHARDS;
   A.dt = dt;
   A.dt_chemistry_nmin = f->d.dt_chemistry_nmin;
+  A.photo = f->d.i_photo > 0 ? t->ccv(f->d.i_photo) : nullptr;
+  A.photo_s = f->d.photo_species - 1;
   // algorithmic bytes per cell: each distinct species state read once, the
   // output written once, |E| and 3 fluxes read
   int distinct = n_prev;
   for (int q = 0; q < n_prev; q++) distinct -= (s_prev[q] == s_deriv) ? 1 : 0;
   distinct += 1;
-  upd_bytes = 8.0 * (A.ns * (distinct + 1) + 4 + (A.rhs ? 1 : 0));
+  upd_bytes = 8.0 * (A.ns * (distinct + 1) + 4 + (A.rhs ? 1 : 0) + (A.photo ? 1 : 0));
   return AFH_OK;
 }
 
@@ -2153,7 +2167,7 @@ int32_t afh_fluid_forward_euler(afh_fluid *f, double dt, int32_t s_deriv,
   const bool fused = fused_env && atoi(fused_env) && f->d_tdi &&
                      (nc == 16 || nc == 32 || nc == 64) && !t->any_cflux &&
                      !f->slow_rates && f->d.n_species <= FE_MAX_SPECIES &&
-                     f->rhs_iv == 0 && f->d.i_gas_dens <= 0 &&
+                     f->rhs_iv == 0 && f->d.i_gas_dens <= 0 && f->d.i_photo <= 0 &&
                      n_prev <= 2 && !alias && f->d.limiter == AFH_LIM_KOREN;
   if (!fused) {
     double a[2], b[2];
@@ -2263,3 +2277,59 @@ int32_t afh_refine_flags(afh_fluid *f, const afh_refine_desc *d,
 
 }  // extern "C"
 
+
+// photoionization_rate_from_alpha (src/m_photoi.f90:217-253): one thread per
+// leaf interior cell, operand order as there
+namespace afh {
+__global__ void k_photoi_src(double *__restrict__ rhs, const double *__restrict__ E,
+                             const double *__restrict__ ne,
+                             const double *__restrict__ Ng, double N,
+                             DevLT td, int alpha_col, double coeff,
+                             const int32_t *__restrict__ ids, int nc, size_t bsz) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nc * nc * nc) return;
+  int i, j, k;
+  cell3(t, nc, i, j, k);
+  const int ng = nc + 2;
+  const size_t x = (size_t)(ids[blockIdx.y] - 1) * bsz + (size_t)((k * ng + j) * ng + i);
+  const double fld = E[x];
+  const double gas_dens = Ng ? Ng[x] : N;
+  const double Td = fld * 1e21 / gas_dens;
+  int low;
+  double lf;
+  lt_loc(td, Td, low, lf);
+  const int np = td.n_points;
+  const double *ra = td.rc + (size_t)(alpha_col - 1) * np + (low - 1);
+  const double *rm = td.rc + (low - 1);
+  const double alpha = lf * ra[0] + (1 - lf) * ra[1];
+  const double mobility = lf * rm[0] + (1 - lf) * rm[1];
+  double tmp = fld * mobility * alpha * ne[x] * coeff;
+  if (tmp < 0) tmp = 0;
+  rhs[x] = tmp;
+}
+}  // namespace afh
+
+extern "C" {
+
+int32_t afh_photoi_set_src(afh_fluid *f, int32_t i_rhs, int32_t alpha_col, double coeff) {
+  if (!f) return set_error(AFH_ERR_ARG, "afh_photoi_set_src: null");
+  afh_tree *t = f->t;
+  AFH_LIVE(t, "afh_photoi_set_src");
+  if (i_rhs < 1 || i_rhs > t->nvc || alpha_col < 1 || alpha_col > f->td.n_cols)
+    return set_error(AFH_ERR_ARG, "afh_photoi_set_src: bad argument");
+  t->touch(i_rhs);
+  const int nc = t->nc, n3 = nc * nc * nc;
+  const double *Ng = f->d.i_gas_dens > 0 ? t->ccv(f->d.i_gas_dens) : nullptr;
+  for (int l = 1; l <= t->nlvl; l++) {
+    const int n = t->leaves.n(l);
+    if (!n) continue;
+    hipLaunchKernelGGL(k_photoi_src, dim3((n3 + 255) / 256, n), dim3(256), 0, t->stream,
+                       t->ccv(i_rhs), t->ccv(f->d.i_efld), t->ccv(f->d.i_electron), Ng,
+                       f->d.gas_number_density, f->td, alpha_col, coeff,
+                       t->leaves.at(l), nc, t->bsz);
+    AFH_LAUNCH_CHECK("k_photoi_src");
+  }
+  return AFH_OK;
+}
+
+}  // extern "C"

@@ -171,6 +171,8 @@ module m_afivo_hip
      integer(c_int32_t) :: i_gas_dens = 0        ! variable gas density (0: constant)
      integer(c_int32_t) :: n_gas_species = 0
      real(c_double)     :: gas_fractions(AFH_MAX_GAS_SPECIES) = 0
+     integer(c_int32_t) :: i_photo = 0          ! photoionization rate (0: none)
+     integer(c_int32_t) :: photo_species = 0
   end type afh_fluid_desc
 
   type, bind(C) :: afh_mg_desc

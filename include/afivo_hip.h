@@ -187,6 +187,12 @@ typedef struct afh_fluid_desc {
   int32_t i_gas_dens;
   int32_t n_gas_species;
   double gas_fractions[AFH_MAX_GAS_SPECIES];
+  /* Photoionization source (photoi_enabled, m_fluid.f90:435-440): cc
+   * variable of the photoionization rate i_photo (0: none); it is added to
+   * the electron and to species photo_species (1-based index into
+   * species_iv, photoi_species_index) after the chemistry time step limit. */
+  int32_t i_photo;
+  int32_t photo_species;
 } afh_fluid_desc;
 
 /* Multigrid options, mg_t (m_af_types.f90:572-665) + coarse solver. */
@@ -336,6 +342,24 @@ int32_t afh_field_set_rhs(afh_fluid *f, int32_t i_rhs, int32_t s_in);
  * 363-401, 419-421): the leaf max|rhs| is folded into the rhs pass. */
 int32_t afh_field_set_rhs_maxabs(afh_fluid *f, int32_t i_rhs, int32_t s_in,
                                  double *max_rhs);
+/* Photoionization (config 5; src/m_photoi.f90:140-255, m_photoi_helmh.f90:
+ * 162-204). afh_photoi_set_src: photoi_set_src's Zheleznyak source,
+ * photoionization_rate_from_alpha on the leaf interiors:
+ * rhs = max(0, |E| mu(Td) alpha(Td) n_e coeff), Td = 1e21 |E| / N, mu and
+ * alpha from the transport table (td_mobility = col 1, td_alpha = alpha_col),
+ * coeff = photoi_eta * quench_fac. */
+int32_t afh_photoi_set_src(afh_fluid *f, int32_t i_rhs, int32_t alpha_col,
+                           double coeff);
+/* photoi_helmh_compute: i_photo = 0 everywhere; max_rhs = max(max|rhs| over
+ * the leaves, sqrt(epsilon)); for each mode n (multigrid modes[n], its own
+ * phi variable, helmholtz_lambda = lambda_n^2, the source in its i_rhs) up to
+ * max_fmg FAS-FMG cycles (have_guess) until max|tmp| / max_rhs < max_rel_res;
+ * then i_photo -= coeffs[n] * phi_n on the leaves, ghost cells included.
+ * n_fmg[n] (or NULL) returns the cycles each mode took. */
+int32_t afh_photoi_helmh_compute(afh_mg *const *modes, int32_t n_modes,
+                                 const double *coeffs, int32_t i_photo,
+                                 double max_rel_res, int32_t max_fmg,
+                                 int32_t *n_fmg);
 /* flux_upwind_tree with the m_fluid flux_upwind / flux_direction callbacks
  * (m_af_flux_schemes.f90:666-848, src/m_fluid.f90:102-227); dt_lim[2] =
  * (CFL limit for CFL number 1, dielectric relaxation time). */

@@ -2166,6 +2166,13 @@ int32_t afo_flux_update_densities(afh_fluid *fl, double dt, int32_t s_deriv,
                 if (r < chem_min) chem_min = r;
               }
             }
+            /* photoionization (m_fluid.f90:435-440) */
+            if (fl->d.i_photo > 0) {
+              const double pho = ccb(t, fl->d.i_photo, id)[x];
+              for (int s = 0; s < ns; s++)
+                if (fl->d.species_iv[s] == fl->d.i_electron) der[ng + s] = der[ng + s] + pho;
+              der[ng + fl->d.photo_species - 1] = der[ng + fl->d.photo_species - 1] + pho;
+            }
             for (int s = 0; s < ns; s++) {
               double *o = ccb(t, fl->d.species_iv[s] + s_out, id);
               o[x] = o[x] + dt * der[ng + s];
@@ -2698,5 +2705,75 @@ int32_t afo_refine_cell_flags(int32_t flag, uint32_t mask, int32_t nc, int32_t b
           placed = 1;
         }
   if (need || !placed) return fail(AFH_ERR_ARG, "refine_cell_flags: inconsistent mask");
+  return AFH_OK;
+}
+
+/* photoionization_rate_from_alpha, src/m_photoi.f90:217-253 (leaf interiors) */
+int32_t afo_photoi_set_src(afh_fluid *f, int32_t i_rhs, int32_t alpha_col, double coeff) {
+  afh_tree *t = f->t;
+  LIVE(t);
+  if (i_rhs < 1 || i_rhs > t->nvc || alpha_col < 1 || alpha_col > f->d.td.n_cols)
+    return fail(AFH_ERR_ARG, "afo_photoi_set_src: bad argument");
+  touch(t, i_rhs);
+  const int nc = t->nc;
+  const afh_lt *td = &f->d.td;
+  for (int l = 1; l <= t->nlvl; l++)
+    for (int q = 0; q < LVL_N(t, leaves, l); q++) {
+      const int id = LVL_AT(t, leaves, l, q);
+      const double *E = ccb(t, f->d.i_efld, id), *ne = ccb(t, f->d.i_electron, id);
+      const double *Ng = f->d.i_gas_dens > 0 ? ccb(t, f->d.i_gas_dens, id) : NULL;
+      double *r = ccb(t, i_rhs, id);
+      for (int k = 1; k <= nc; k++)
+        for (int j = 1; j <= nc; j++)
+          for (int i = 1; i <= nc; i++) {
+            const size_t x = IX(t, i, j, k);
+            const double fld = E[x];
+            const double gas_dens = Ng ? Ng[x] : f->d.gas_number_density;
+            const double Td = fld * 1e21 / gas_dens;
+            const double alpha = lt_col(td, alpha_col, Td);
+            const double mobility = lt_col(td, 1, Td);
+            double tmp = fld * mobility * alpha * ne[x] * coeff;
+            if (tmp < 0) tmp = 0;
+            r[x] = tmp;
+          }
+    }
+  return AFH_OK;
+}
+
+/* photoi_helmh_compute, src/m_photoi_helmh.f90:162-204 */
+int32_t afo_photoi_helmh_compute(afh_mg *const *modes, int32_t n_modes,
+                                 const double *coeffs, int32_t i_photo,
+                                 double max_rel_res, int32_t max_fmg,
+                                 int32_t *n_fmg) {
+  if (!modes || n_modes < 1 || !coeffs || max_fmg < 1)
+    return fail(AFH_ERR_ARG, "afo_photoi_helmh_compute: bad argument");
+  afh_tree *t = modes[0]->t;
+  LIVE(t);
+  if (i_photo < 1 || i_photo > t->nvc) return fail(AFH_ERR_ARG, "bad i_photo");
+  touch(t, i_photo);
+  memset(ccb(t, i_photo, 1), 0, sizeof(double) * t->bsz * t->nb);
+  double max_rhs;
+  int32_t e;
+  if ((e = afo_tree_maxabs_cc(t, modes[0]->d.i_rhs, &max_rhs))) return e;
+  if (max_rhs < sqrt(DBL_EPSILON)) max_rhs = sqrt(DBL_EPSILON);
+  for (int n = 0; n < n_modes; n++) {
+    afh_mg *mg = modes[n];
+    int i;
+    for (i = 1; i <= max_fmg; i++) {
+      double residu;
+      if ((e = afo_mg_fas_fmg(mg, 1, 1)) ||
+          (e = afo_tree_maxabs_cc(t, mg->d.i_tmp, &residu)))
+        return e;
+      if (residu / max_rhs < max_rel_res) break;
+    }
+    if (n_fmg) n_fmg[n] = i < max_fmg ? i : max_fmg;
+    for (int l = 1; l <= t->nlvl; l++)
+      for (int q = 0; q < LVL_N(t, leaves, l); q++) {
+        const int id = LVL_AT(t, leaves, l, q);
+        double *y = ccb(t, i_photo, id);
+        const double *x = ccb(t, mg->d.i_phi, id);
+        for (size_t c = 0; c < t->bsz; c++) y[c] = y[c] - coeffs[n] * x[c];
+      }
+  }
   return AFH_OK;
 }

@@ -48,6 +48,11 @@ int32_t afo_tree_sum_cc(afh_tree *t, int32_t iv, int32_t power, double *out);
 int32_t afo_tree_reduce_loc(afh_tree *t, int32_t iv, int32_t op, double *out,
                             int32_t *loc);
 int32_t afo_fluid_rhs_valid(afh_fluid *f, int32_t s_out, int32_t *valid);
+int32_t afo_photoi_set_src(afh_fluid *f, int32_t i_rhs, int32_t alpha_col, double coeff);
+int32_t afo_photoi_helmh_compute(afh_mg *const *modes, int32_t n_modes,
+                                 const double *coeffs, int32_t i_photo,
+                                 double max_rel_res, int32_t max_fmg,
+                                 int32_t *n_fmg);
 int32_t afo_mg_create(afh_tree *t, const afh_mg_desc *desc, afh_mg **out);
 int32_t afo_mg_destroy(afh_mg *mg);
 int32_t afo_mg_fas_vcycle(afh_mg *mg, int32_t set_residual,

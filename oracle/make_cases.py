@@ -1,0 +1,72 @@
+#!/usr/bin/env python3
+"""ORACLE TEST INFRASTRUCTURE -- regression-case fixtures (build container only).
+
+For each of the reference's 3D regression tests (programs/standard_3d/tests/
+test_3d*.cfg, run by the reference's run_test.sh from that directory) this
+script runs oracle/_ref/export_case (the reference's own module initializers,
+compiled from /root/reference by oracle/Makefile) on the .cfg and packs what
+it printed -- configuration values, variable registry, transport table,
+parsed reactions, the field-rate lookup table, get_rates on a field grid --
+together with the numbers of the reference's committed regression log for
+that cfg (<name>_rtest.log: it, time, dt, volume-averaged sums and maxima of
+every species per output time; the expected output) into
+tests/golden/rtest_<name>.npz. Only numbers and names are stored.
+
+    make -C oracle _ref/export_case && python3 oracle/make_cases.py
+"""
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+TESTS = "/root/reference/programs/standard_3d/tests"
+CASES = ["test_3d", "test_3d_chem", "test_3d_photoi_chem"]
+
+
+def parse_dump(path):
+    out = {}
+    with open(path) as f:
+        for line in f:
+            kind, rest = line.split(":", 1)
+            parts = rest.split()
+            name, n = parts[0], int(parts[1])
+            vals = parts[2:2 + n] if kind != "s" else None
+            if kind == "r":
+                out[name] = np.array([float(v.replace("D", "E")) for v in vals], np.float64)
+            elif kind == "i":
+                out[name] = np.array([int(v) for v in vals], np.int64)
+            else:
+                toks = rest.split(None, 2)[2] if n else ""
+                if '"' in toks:
+                    items = [t for t in toks.split('"') if t.strip()]
+                else:
+                    items = toks.split()
+                out[name] = np.array(items[:n] if n else [], dtype="U64")
+    return out
+
+
+def main():
+    exe = os.path.join(HERE, "_ref", "export_case")
+    if not os.path.exists(exe):
+        sys.exit("build oracle/_ref/export_case first (make -C oracle _ref/export_case)")
+    for name in CASES:
+        dump = "/tmp/afh_export_%s.txt" % name
+        subprocess.run([exe, dump, name + ".cfg"], cwd=TESTS, check=True,
+                       stdout=subprocess.DEVNULL)
+        d = parse_dump(dump)
+        log = os.path.join(TESTS, name + "_rtest.log")
+        with open(log) as f:
+            header = f.readline().split()
+        d["rtest_columns"] = np.array(header, dtype="U64")
+        d["rtest_log"] = np.genfromtxt(log, skip_header=1)
+        out = os.path.join(REPO, "tests", "golden", "rtest_%s.npz" % name)
+        np.savez_compressed(out, **d)
+        os.remove(dump)
+        print("wrote", out, len(d), "arrays")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,151 @@
+"""The device driver's ingredients replayed through the reference's own code.
+
+Build-container only (needs /root/reference and the oracle/_ref programs that
+oracle/Makefile compiles from it; skipped elsewhere, e.g. on the GPU box):
+
+* refinement: every af_adjust_refinement call of a regression run
+  (default_refinement evaluated on the device data, afh.amr's topology) is
+  replayed by oracle/_ref/replay_refine, which loads the same electron
+  density and |E| into a tree built by the reference and calls the
+  reference's af_adjust_refinement with refine_routine => default_refinement
+  (m_af_core.f90:697-822, src/m_refine.f90:198-298); the resulting
+  topology must be ours, box id for box id, after every call;
+* species step: the state before a forward-Euler sub-step of a regression
+  run is handed to oracle/_ref/replay_step, which runs the reference's
+  forward_euler (src/m_fluid.f90:21-99: flux_upwind_tree with flux_upwind /
+  flux_direction, flux_update_densities with add_source_terms, get_rates,
+  get_derivatives and the photoionization source) on it; the new densities
+  and dt_lim must equal the C oracle's bitwise (the HIP library equals the
+  oracle bitwise in the -m gpu tests).
+"""
+import os
+import resource
+import struct
+import subprocess
+
+import numpy as np
+import pytest
+
+import golden
+from afh import capi
+from afh.driver import Simulation
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF_TESTS = "/root/reference/programs/standard_3d/tests"
+REPLAY_REFINE = os.path.join(REPO, "oracle", "_ref", "replay_refine")
+REPLAY_STEP = os.path.join(REPO, "oracle", "_ref", "replay_step")
+
+pytestmark = pytest.mark.skipif(
+    not (os.path.isdir(REF_TESTS) and os.path.exists(REPLAY_REFINE)
+         and os.path.exists(REPLAY_STEP)),
+    reason="needs the reference sources and oracle/_ref (build container)")
+
+
+def _run_ref(exe, args, name):
+    def unlimited_stack():
+        resource.setrlimit(resource.RLIMIT_STACK,
+                           (resource.RLIM_INFINITY, resource.RLIM_INFINITY))
+    env = dict(os.environ, OMP_STACKSIZE="512M", OMP_NUM_THREADS="4")
+    subprocess.run([exe] + args + [name + ".cfg"], cwd=REF_TESTS, check=True,
+                   stdout=subprocess.DEVNULL, preexec_fn=unlimited_stack, env=env)
+
+
+@pytest.mark.parametrize("name", ["test_3d", "test_3d_chem"])
+def test_refinement_replay(name, tmp_path):
+    sim = Simulation(capi.oracle_library(), golden.load("rtest_" + name))
+    rec, topo = tmp_path / "rec.bin", []
+    f = open(rec, "wb")
+    f.write(struct.pack("<i", 0))
+    n_calls = [0]
+    orig = sim.adjust_refinement
+
+    def recorded():
+        af = sim.af
+        e = sim.tree.get_cc(sim.i_electron)[:, 1:-1, 1:-1, 1:-1]
+        E = sim.tree.get_cc(sim.i_efld)[:, 1:-1, 1:-1, 1:-1]
+        f.write(struct.pack("<id", af.highest_id, sim.global_time))
+        for b in range(1, af.highest_id + 1):
+            f.write(struct.pack("<i", int(af.in_use[b])))
+            if af.in_use[b]:
+                f.write(np.ascontiguousarray(e[b - 1]).tobytes())
+                f.write(np.ascontiguousarray(E[b - 1]).tobytes())
+        info = orig()
+        topo.append((af.highest_id, [(int(af.in_use[b]), af.lvl[b], af.parent[b],
+                                      list(af.children[b]) if af.in_use[b] else None)
+                                     for b in range(1, af.highest_id + 1)]))
+        n_calls[0] += 1
+        return info
+
+    sim.adjust_refinement = recorded
+    sim.run()
+    f.seek(0)
+    f.write(struct.pack("<i", n_calls[0]))
+    f.close()
+    out = tmp_path / "rep.bin"
+    _run_ref(REPLAY_REFINE, [str(rec), str(out)], name)
+    raw, p = out.read_bytes(), 0
+    for k, (hid, boxes) in enumerate(topo):
+        rhid, _ = struct.unpack_from("<ii", raw, p)
+        p += 8
+        rows = np.frombuffer(raw, np.int32, rhid * 20, p).reshape(rhid, 20)
+        p += rhid * 80
+        assert rhid == hid, (k, rhid, hid)
+        for b, (use, lvl, parent, children) in enumerate(boxes):
+            assert rows[b, 0] == use, (k, b + 1)
+            if use:
+                assert (rows[b, 1], rows[b, 5]) == (lvl, parent), (k, b + 1)
+                assert list(rows[b, 6:14]) == children, (k, b + 1)
+    assert n_calls[0] > 40
+
+
+def replay_species_step(name, n_steps, s_deriv, s_prev, w_prev, s_out, dt, tmp_path):
+    sim = Simulation(capi.oracle_library(), golden.load("rtest_" + name))
+    sim.start()
+    while sim.it < n_steps:
+        sim.step()
+    if sim.photoi:
+        sim.photoi_set_src()
+    t, af = sim.tree, sim.af
+    hid = af.highest_id
+    used = [b for b in range(1, hid + 1) if af.in_use[b]]
+    rec = tmp_path / "step.bin"
+    with open(rec, "wb") as f:
+        f.write(struct.pack("<4i", hid, sim.n_var_cell, sim.n_var_face, af.nc))
+        for b in range(1, hid + 1):
+            ix = af.ix[b] if af.in_use[b] else (0, 0, 0)
+            f.write(struct.pack("<6i", af.parent[b], af.lvl[b], *ix, int(af.in_use[b])))
+        f.write(struct.pack("<ddii", dt, sim.time, s_deriv, len(s_prev)))
+        f.write(struct.pack("<%di" % len(s_prev), *s_prev))
+        f.write(struct.pack("<%dd" % len(w_prev), *w_prev))
+        f.write(struct.pack("<i", s_out))
+        for iv in range(1, sim.n_var_cell + 1):
+            a = t.get_cc(iv)
+            for b in used:
+                f.write(np.ascontiguousarray(a[b - 1]).tobytes())
+        for iv in range(1, sim.n_var_face + 1):
+            a = t.get_fc(iv)
+            for b in used:
+                f.write(np.ascontiguousarray(a[b - 1]).tobytes())
+    out = tmp_path / "out.bin"
+    _run_ref(REPLAY_STEP, [str(rec), str(out)], name)
+    lim = sim.fluid.forward_euler(dt, s_deriv, s_prev, w_prev, s_out, True)
+    ours = min(sim.dt_max, min(lim[0] * sim.cfl, lim[1], lim[2], lim[3]))
+    raw = out.read_bytes()
+    assert struct.unpack_from("<d", raw, 0)[0] == ours
+    ng = af.nc + 2
+    ref = np.frombuffer(raw, np.float64, offset=8).reshape(
+        sim.n_var_cell, len(used), ng, ng, ng)
+    leaves = set(af.leaves())
+    li = [k for k, b in enumerate(used) if b in leaves]
+    for iv in sim.densities:
+        mine = t.get_cc(iv + s_out)[np.array(used) - 1][li][:, 1:-1, 1:-1, 1:-1]
+        theirs = ref[iv + s_out - 1][li][:, 1:-1, 1:-1, 1:-1]
+        assert np.array_equal(mine, theirs), sim.cc_names[iv - 1]
+
+
+@pytest.mark.parametrize("name", ["test_3d", "test_3d_chem", "test_3d_photoi_chem"])
+def test_species_step_replay(name, tmp_path):
+    # Heun stage 1 on the AMR tree after 5 steps, stage 2 after 40 (the second
+    # with the photoionization source of that step)
+    replay_species_step(name, 5, 0, [0], [1.0], 1, 1e-11, tmp_path)
+    replay_species_step(name, 40, 1, [0, 1], [0.5, 0.5], 0, 2e-11, tmp_path)
