@@ -553,6 +553,24 @@ class Simulation:
                     self.photoi_prev_time = self.time
         return True
 
+    def clone(self, lib, device=-1):
+        """The same simulation state on another library (e.g. the C oracle
+        for a CPU baseline): topology, every cell and face variable, time."""
+        import copy
+        other = Simulation(lib, self.c, device=device, coarse_cycles=self.coarse_cycles,
+                           capacity_factor=self.capacity_factor, fuse_rhs=self.fused_rhs)
+        other.af = copy.deepcopy(self.af)
+        for k in ("it", "time", "global_time", "photoi_prev_time", "global_dt", "dt",
+                  "output_cnt", "time_last_output"):
+            if hasattr(self, k):
+                setattr(other, k, getattr(self, k))
+        other._bind(other._create_tree())
+        for iv in range(1, self.n_var_cell + 1):
+            other.tree.put_cc(iv, self.tree.get_cc(iv))
+        for iv in range(1, self.n_var_face + 1):
+            other.tree.put_fc(iv, self.tree.get_fc(iv))
+        return other
+
     def start(self):
         self.set_initial_conditions()
         self.output_cnt = 0

@@ -37,6 +37,12 @@ CONFIGS = {
     # name: (n_cell, coarse grid, levels, domain [m])
     "s1-64": (64, (64, 64, 64), 4, (16e-3, 16e-3, 16e-3)),
     "s1": (16, (16, 16, 16), 4, (16e-3, 16e-3, 16e-3)),
+    # BASELINE.json config 3: programs/standard_3d/streamer_3d.cfg with
+    # air_chemistry_v2 (9 species, 25 reactions), the AMR tree the reference's
+    # set_initial_conditions builds (tests/golden/case_s3.npz, exported from
+    # the reference's own initializers; afh.driver builds the tree on the
+    # device)
+    "s3": (8, None, None, (16e-3, 16e-3, 16e-3)),
 }
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E peak (spec)
 
@@ -76,6 +82,56 @@ def unit_step(case, dt, k):
         res = case.field_compute(1, n_vcycles=1)
         d = case.species_step(0.5 * dt, 1, [0, 1], [0.5, 0.5], 0, True)
     return res, d
+
+
+class DriverCase:
+    """bench adapter for an afh.driver.Simulation (config s3): the same unit
+    step -- field_compute of the derivative state (the reference's
+    field_compute: field_set_rhs + up to multigrid_num_vcycles V-cycles with
+    the residual test + field_from_potential) + forward_euler's species part,
+    Heun stages alternating."""
+
+    def __init__(self, sim):
+        self.sim = sim
+        self.tree = sim.tree
+        self.topo = sim.af.topology()
+
+    def field_compute(self, s, n_vcycles=2):
+        return self.sim.field_compute(s, True)
+
+    def species_step(self, dt, s_deriv, s_prev, w_prev, s_out, last):
+        return self.sim.fluid.forward_euler(dt, s_deriv, s_prev, w_prev, s_out, last)
+
+    def fuse_rhs(self, on=True, ghosts=False):
+        self.sim.fluid.set_rhs_output(self.sim.i_rhs if on else 0, ghosts)
+        self.sim.fused_rhs = on
+
+
+def build_driver_case(lib, device):
+    import golden
+    from afh.driver import Simulation
+    sim = Simulation(lib, golden.load("case_s3"), device=device)
+    sim.set_initial_conditions()
+    return sim
+
+
+def cpu_baseline_driver(sim, steps=2):
+    """The C oracle on the same S3 state (the tree built on the device, every
+    variable copied over), `steps` unit steps."""
+    from afh import capi
+    osim = sim.clone(capi.oracle_library())
+    case = DriverCase(osim)
+    unit_step(case, 1e-13, 0)
+    t0 = time.perf_counter()
+    for k in range(steps):
+        unit_step(case, 1e-13, k + 1)
+    dt = time.perf_counter() - t0
+    ncell = osim.af.n_leaf_cells()
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    return {"value": ncell * steps / dt, "unit": "cell-updates/s", "cores": threads,
+            "kind": "port",
+            "sample": "%d steps of the full S3 workload (%d leaf cells), C oracle "
+                      "OpenMP" % (steps, ncell)}
 
 
 def cpu_baseline(config, coarse_cycles, steps=2):
@@ -154,8 +210,14 @@ def main():
     from afh import capi
     lib = capi.hip_library()
     sharded = world > 1 and not args.replicas
-    case = build_case(lib, args.config, local, args.coarse_cycles,
-                      (world, rank) if sharded else None)
+    if args.config == "s3":
+        if sharded:
+            raise SystemExit("s3: sharding an AMR driver tree is not supported; use --replicas")
+        sim = build_driver_case(lib, local)
+        case = DriverCase(sim)
+    else:
+        case = build_case(lib, args.config, local, args.coarse_cycles,
+                          (world, rank) if sharded else None)
     from afh.streamer import cells
     ncell = cells(case.topo)  # leaf cells of the whole tree
     dt = 1e-13
@@ -220,7 +282,9 @@ def main():
                        "parallelism": ("box-shard-%d" % world) if sharded else
                        ("replica-per-gpu" if world > 1 else "single-gpu")},
             "roofline": {"bound": "hbm",
-                         "kernel": "k_gsrb_pair2<%d,%d>" % (CONFIGS[args.config][0], CONFIGS[args.config][0]),
+                         "kernel": ("k_gsrb_pair2<%d,%d>" if CONFIGS[args.config][0] >= 16
+                                    else "k_gsrb_pair<%d,%d>") % (CONFIGS[args.config][0],
+                                                                CONFIGS[args.config][0]),
                          "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": pmc_traffic(args.config),
@@ -233,8 +297,12 @@ def main():
         }
         if sharded:
             out["exchanges_per_step"] = case.shard.n_exchanges / max(1, args.steps + args.warmup + 1)
+        if args.config == "s3":
+            out["config"]["chemistry"] = "air_chemistry_v2 (9 species, 25 reactions)"
+            out["config"]["coarse_solve"] = "direct"
         if not args.no_cpu_baseline and world == 1:
-            out["cpu_baseline"] = cpu_baseline(args.config, args.coarse_cycles)
+            out["cpu_baseline"] = (cpu_baseline_driver(sim) if args.config == "s3" else
+                                   cpu_baseline(args.config, args.coarse_cycles))
         print(json.dumps(out))
     if dist is not None:
         dist.barrier()

@@ -24,6 +24,11 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 TESTS = "/root/reference/programs/standard_3d/tests"
 CASES = ["test_3d", "test_3d_chem", "test_3d_photoi_chem"]
+# BASELINE.json config 3: programs/standard_3d/streamer_3d.cfg with
+# air_chemistry_v2 (9 species, 25 reactions); no regression log
+EXTRA = {"s3": ("/root/reference/programs/standard_3d", "streamer_3d.cfg",
+                ["-input_data%file=../../transport_data/air_chemistry_v2.txt",
+                 "-input_data%old_style=f"])}
 
 
 def parse_dump(path):
@@ -63,6 +68,15 @@ def main():
         d["rtest_columns"] = np.array(header, dtype="U64")
         d["rtest_log"] = np.genfromtxt(log, skip_header=1)
         out = os.path.join(REPO, "tests", "golden", "rtest_%s.npz" % name)
+        np.savez_compressed(out, **d)
+        os.remove(dump)
+        print("wrote", out, len(d), "arrays")
+    for name, (cwd, cfg, extra) in EXTRA.items():
+        dump = "/tmp/afh_export_%s.txt" % name
+        subprocess.run([exe, dump, cfg] + extra, cwd=cwd, check=True,
+                       stdout=subprocess.DEVNULL)
+        d = parse_dump(dump)
+        out = os.path.join(REPO, "tests", "golden", "case_%s.npz" % name)
         np.savez_compressed(out, **d)
         os.remove(dump)
         print("wrote", out, len(d), "arrays")

@@ -41,12 +41,12 @@ pytestmark = pytest.mark.skipif(
     reason="needs the reference sources and oracle/_ref (build container)")
 
 
-def _run_ref(exe, args, name):
+def _run_ref(exe, args, name, cwd=REF_TESTS):
     def unlimited_stack():
         resource.setrlimit(resource.RLIMIT_STACK,
                            (resource.RLIM_INFINITY, resource.RLIM_INFINITY))
     env = dict(os.environ, OMP_STACKSIZE="512M", OMP_NUM_THREADS="4")
-    subprocess.run([exe] + args + [name + ".cfg"], cwd=REF_TESTS, check=True,
+    subprocess.run([exe] + args[:2] + [name + ".cfg"] + args[2:], cwd=cwd, check=True,
                    stdout=subprocess.DEVNULL, preexec_fn=unlimited_stack, env=env)
 
 
@@ -98,11 +98,10 @@ def test_refinement_replay(name, tmp_path):
     assert n_calls[0] > 40
 
 
-def replay_species_step(name, n_steps, s_deriv, s_prev, w_prev, s_out, dt, tmp_path):
-    sim = Simulation(capi.oracle_library(), golden.load("rtest_" + name))
-    sim.start()
-    while sim.it < n_steps:
-        sim.step()
+def _replay_state(sim, name, s_deriv, s_prev, w_prev, s_out, dt, tmp_path, cwd=REF_TESTS,
+                  cfg_args=None):
+    """Hand the state of `sim` to oracle/_ref/replay_step (the reference's
+    forward_euler) and compare its new densities and dt_lim with the oracle's."""
     if sim.photoi:
         sim.photoi_set_src()
     t, af = sim.tree, sim.af
@@ -127,7 +126,9 @@ def replay_species_step(name, n_steps, s_deriv, s_prev, w_prev, s_out, dt, tmp_p
             for b in used:
                 f.write(np.ascontiguousarray(a[b - 1]).tobytes())
     out = tmp_path / "out.bin"
-    _run_ref(REPLAY_STEP, [str(rec), str(out)], name)
+    args = cfg_args or [name + ".cfg"]
+    _run_ref(REPLAY_STEP, [str(rec), str(out)] + args[1:], args[0].replace(".cfg", ""),
+             cwd=cwd)
     lim = sim.fluid.forward_euler(dt, s_deriv, s_prev, w_prev, s_out, True)
     ours = min(sim.dt_max, min(lim[0] * sim.cfl, lim[1], lim[2], lim[3]))
     raw = out.read_bytes()
@@ -143,9 +144,31 @@ def replay_species_step(name, n_steps, s_deriv, s_prev, w_prev, s_out, dt, tmp_p
         assert np.array_equal(mine, theirs), sim.cc_names[iv - 1]
 
 
+def replay_species_step(name, n_steps, s_deriv, s_prev, w_prev, s_out, dt, tmp_path):
+    sim = Simulation(capi.oracle_library(), golden.load("rtest_" + name))
+    sim.start()
+    while sim.it < n_steps:
+        sim.step()
+    _replay_state(sim, name, s_deriv, s_prev, w_prev, s_out, dt, tmp_path)
+
+
 @pytest.mark.parametrize("name", ["test_3d", "test_3d_chem", "test_3d_photoi_chem"])
 def test_species_step_replay(name, tmp_path):
     # Heun stage 1 on the AMR tree after 5 steps, stage 2 after 40 (the second
     # with the photoionization source of that step)
     replay_species_step(name, 5, 0, [0], [1.0], 1, 1e-11, tmp_path)
     replay_species_step(name, 40, 1, [0, 1], [0.5, 0.5], 0, 2e-11, tmp_path)
+
+
+def test_species_step_replay_s3(tmp_path):
+    """BASELINE config 3 (streamer_3d.cfg + air_chemistry_v2: 9 species, 25
+    reactions) on the 10-level AMR tree set_initial_conditions builds: one
+    species step bitwise equal to the reference's forward_euler."""
+    from afh.driver import Simulation as Sim
+    sim = Sim(capi.oracle_library(), golden.load("case_s3"))
+    sim.set_initial_conditions()
+    _replay_state(sim, "s3", 0, [0], [1.0], 1, 1e-12, tmp_path,
+                  cwd="/root/reference/programs/standard_3d",
+                  cfg_args=["streamer_3d.cfg",
+                            "-input_data%file=../../transport_data/air_chemistry_v2.txt",
+                            "-input_data%old_style=f"])

@@ -83,3 +83,25 @@ def test_rtest_hip(name):
     _, olog, _ = run(capi.oracle_library(), name)
     rel = np.abs(log - olog) / np.maximum(np.abs(olog), 1e-300)
     assert rel.max() <= 1e-9, rel.max(axis=1)
+
+
+@pytest.mark.gpu
+def test_s3_hip_equals_oracle():
+    """BASELINE config 3 (streamer_3d.cfg + air_chemistry_v2, the reference's
+    set-up exported by oracle/_ref/export_case): the 10-level AMR tree
+    set_initial_conditions builds on the device (8873 boxes of 8^3), then one
+    Heun step (two forward_euler sub-steps, field solves included) on the HIP
+    library and on the C oracle from the same state. The oracle's species
+    step on this tree is bitwise the reference's forward_euler
+    (test_reference_replay.test_species_step_replay_s3)."""
+    sim = Simulation(capi.hip_library(), golden.load("case_s3"), device=0)
+    sim.set_initial_conditions()
+    assert sim.af.highest_lvl >= 5 and len(sim.af.leaves()) > 1000
+    osim = sim.clone(capi.oracle_library())
+    for s in (sim, osim):
+        s.advance(1e-12)
+        s.field_compute(0, True)
+    for iv in list(sim.densities) + [sim.i_phi, sim.i_efld]:
+        a, b = sim.tree.get_cc(iv), osim.tree.get_cc(iv)
+        rel = np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300)
+        assert rel <= 1e-12, (sim.cc_names[iv - 1], rel)
