@@ -220,6 +220,14 @@ inline unsigned long long host_dbl_to_ord(double x) {
   return (u & 0x8000000000000000ull) ? ~u : (u | 0x8000000000000000ull);
 }
 
+// Workgroup b of n -> work item: workgroups are dispatched round-robin over
+// the 8 XCDs (b % 8); this gives each XCD a contiguous run of work items
+// (bijective for any n), so neighbouring boxes of a level list share an L2.
+__device__ __forceinline__ int xcd_swizzle(int b, int n) {
+  const int q = n >> 3, r = n & 7, x = b & 7, slot = b >> 3;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + slot;
+}
+
 __device__ __forceinline__ size_t ix3(int ng, int i, int j, int k) {
   return ((size_t)k * ng + j) * ng + i;
 }

@@ -328,12 +328,13 @@ __global__ void __launch_bounds__((RbGeom<NC, TJ>::NT)) __attribute__((amdgpu_wa
 #ifndef AFH_PAIR_NB_LOADS  // 1: every neighbour value of phase B from global
 #define AFH_PAIR_NB_LOADS 0
 #endif
-template <int NC, int TJ = NC>
+template <int NC, int TJ = NC, int NTM = 0>
 struct RbPar {
   static constexpr int NG = NC + 2, HN = NC / 2;
   static constexpr int NTILE = NC / TJ;
   static constexpr int NRED = TJ * HN;                      // red cells per tile plane
-  static constexpr int NTMAX = TJ == NC ? 1024 : 512;       // tiles: 2 workgroups per CU
+  // tiles: 2 workgroups per CU
+  static constexpr int NTMAX = NTM ? NTM : (TJ == NC ? 1024 : 512);
   static constexpr int NT = NRED >= NTMAX ? NTMAX : NRED;
   static constexpr int RPT = NRED / NT;                     // red cells per thread
   static constexpr int PL = (TJ + 2) * NG;                  // LDS plane (rows j0-1..j1+1)
@@ -350,21 +351,24 @@ struct RbPar {
 // (TJ < NC: 512-thread workgroups, two per CU, halo rows recomputed as in
 // k_gsrb_pair). Same arithmetic in the same order as k_gsrb_pair: bitwise
 // identical results.
-template <int NC, int TJ>
-__global__ void __launch_bounds__((RbPar<NC, TJ>::NT)) __attribute__((amdgpu_waves_per_eu(4)))
+// DEPTH: planes of phi / rhs in flight per workgroup (1: loaded and stored
+// in the same step; 2: loaded one step earlier); NTM: workgroup size cap
+template <int NC, int TJ, int DEPTH = 2, int NTM = 0>
+__global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
     k_gsrb_pair2(const double *__restrict__ src, double *__restrict__ dst,
                  const double *__restrict__ rhs, const double *__restrict__ coarse,
                  const afh_box_meta *__restrict__ meta,
                  const int32_t *__restrict__ ids, size_t bsz, Coef cf,
                  double inv_c1, GcArgs ga) {
-  using G = RbPar<NC, TJ>;
+  using G = RbPar<NC, TJ, NTM>;
   constexpr int NG = G::NG, HN = G::HN, NT = G::NT, RPT = G::RPT, PL = G::PL,
                 EPT = G::EPT, OPT = G::OPT;
   constexpr size_t SK = (size_t)NG * NG;
   __shared__ double P[4][PL];  // planes s-2 .. s+1 at slot (plane & 3)
   const int tid = threadIdx.x;
-  const int id = ids[blockIdx.x / G::NTILE];
-  const int j0 = (blockIdx.x % G::NTILE) * TJ + 1, j1 = j0 + TJ - 1;
+  const int wg = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int id = ids[wg / G::NTILE];
+  const int j0 = (wg % G::NTILE) * TJ + 1, j1 = j0 + TJ - 1;
   const afh_box_meta &m = meta[id - 1];
   const double *x = src + (size_t)(id - 1) * bsz;
   double *y = dst + (size_t)(id - 1) * bsz;
@@ -398,85 +402,134 @@ __global__ void __launch_bounds__((RbPar<NC, TJ>::NT)) __attribute__((amdgpu_wav
   }
   __syncthreads();
 
-  for (int s = 1; s <= NC + 1; s++) {
-    // B inputs first (older than the plane prefetch, so phase B waits only
-    // for them): thread u < TJ + NC owns one red ghost value of plane s. A
-    // same-level neighbour's red boundary cell (or, for tiles, the adjacent
-    // tile's red cell) is 6 neighbour values and an rhs value, loaded now;
-    // physical / refinement faces are evaluated in B (gc_face_nocopy).
-    double bl[7];
-    int b_i = 0, b_j = 0, b_jl = 0, b_nb = 0, b_rep = -1;  // b_nb 0: none
-    bool b_pre = false;
-    // x faces: the neighbour's boundary column is a copy in this box's ghost
-    // column (the last level fill), so its rows j+-1 and planes s+-1 are read
-    // from LDS where they are interior cells of the neighbour (unchanged
-    // black values); only phi next to it and rhs come from the neighbour
-    bool b_lm = false, b_lp = false, b_zm = false, b_zp = false;
+  // B inputs (one step ahead, so phase B never waits on them): thread
+  // u < TJ + NC owns one red ghost value of plane s. A same-level
+  // neighbour's red boundary cell (or, for tiles, the adjacent tile's red
+  // cell) is 6 neighbour values and an rhs value; physical / refinement
+  // faces are evaluated in B (gc_face_nocopy).
+  // x faces: the neighbour's boundary column is a copy in this box's ghost
+  // column (the last level fill), so its rows j+-1 and planes s+-1 are read
+  // from LDS where they are interior cells of the neighbour (unchanged
+  // black values); only phi next to it and rhs come from the neighbour
+  struct BDesc {
+    int i, j, jl, nb, rep;  // nb 0: none
+    bool pre, lm, lp, zm, zp;
+    const double *xs, *rs;
+    size_t c;
+  };
+  auto bdesc = [&](int s) {
+    BDesc b;
+    b.i = b.j = b.jl = b.nb = 0;
+    b.rep = -1;
+    b.pre = b.lm = b.lp = b.zm = b.zp = false;
+    b.xs = b.rs = nullptr;
+    b.c = 0;
     if (s <= NC && tid < TJ + NC) {
       const int u = tid;
       if (u < TJ) {
-        b_j = j0 + u;
-        b_jl = u + 1;
-        b_i = ((b_j + s) & 1) ? 0 : NC + 1;
-        b_nb = b_i == 0 ? 1 : 2;
+        b.j = j0 + u;
+        b.jl = u + 1;
+        b.i = ((b.j + s) & 1) ? 0 : NC + 1;
+        b.nb = b.i == 0 ? 1 : 2;
       } else {
         const bool lo = u - TJ < HN;
-        b_j = lo ? j0 - 1 : j1 + 1;
-        b_jl = lo ? 0 : TJ + 1;
-        b_i = 2 - ((1 ^ (s + b_j)) & 1) + 2 * ((u - TJ) % HN);
-        b_nb = (b_j == 0 || b_j == NC + 1) ? (b_j == 0 ? 3 : 4) : 7;
+        b.j = lo ? j0 - 1 : j1 + 1;
+        b.jl = lo ? 0 : TJ + 1;
+        b.i = 2 - ((1 ^ (s + b.j)) & 1) + 2 * ((u - TJ) % HN);
+        b.nb = (b.j == 0 || b.j == NC + 1) ? (b.j == 0 ? 3 : 4) : 7;
       }
-      const double *xs = nullptr, *rs = nullptr;
-      int q[3] = {b_i, b_j, s};
-      if (b_nb == 7) {
-        xs = x;
-        rs = r;
+      int q[3] = {b.i, b.j, s};
+      if (b.nb == 7) {
+        b.xs = x;
+        b.rs = r;
       } else {
-        const int nb_id = m.neighbors[b_nb - 1];
+        const int nb_id = m.neighbors[b.nb - 1];
         if (nb_id > 0) {
-          const int d = (b_nb - 1) >> 1;
-          const bool low = ((b_nb - 1) & 1) == 0;
+          const int d = (b.nb - 1) >> 1;
+          const bool low = ((b.nb - 1) & 1) == 0;
           q[d] = low ? NC : 1;
-          xs = src + (size_t)(nb_id - 1) * bsz;
-          rs = rhs + (size_t)(nb_id - 1) * bsz;
-          b_rep = 2 * d + (low ? 1 : 0);
+          b.xs = src + (size_t)(nb_id - 1) * bsz;
+          b.rs = rhs + (size_t)(nb_id - 1) * bsz;
+          b.rep = 2 * d + (low ? 1 : 0);
         }
       }
-      if (xs) {
-        b_pre = true;
-        const size_t c = ix3(NG, q[0], q[1], q[2]);
+      if (b.xs) {
+        b.pre = true;
+        b.c = ix3(NG, q[0], q[1], q[2]);
 #if !AFH_PAIR_NB_LOADS
-        const bool xg = b_rep == 0 || b_rep == 1;
-        b_lm = xg && b_j >= 2;
-        b_lp = xg && b_j <= NC - 1;
-        b_zm = xg && s >= 2;
-        b_zp = xg && s <= NC - 1;
+        const bool xg = b.rep == 0 || b.rep == 1;
+        b.lm = xg && b.j >= 2;
+        b.lp = xg && b.j <= NC - 1;
+        b.zm = xg && s >= 2;
+        b.zp = xg && s <= NC - 1;
 #endif
-        bl[0] = b_rep == 0 ? 0.0 : xs[c - 1];
-        bl[1] = b_rep == 1 ? 0.0 : xs[c + 1];
-        bl[2] = (b_rep == 2 || b_lm) ? 0.0 : xs[c - NG];
-        bl[3] = (b_rep == 3 || b_lp) ? 0.0 : xs[c + NG];
-        bl[4] = (b_rep == 4 || b_zm) ? 0.0 : xs[c - SK];
-        bl[5] = (b_rep == 5 || b_zp) ? 0.0 : xs[c + SK];
-        bl[6] = rs[c];
       }
     }
-    // prefetch: plane s+2 of phi; rhs of plane s+1, both parities (red for
-    // step s+1's A, black for step s+2's C)
+    return b;
+  };
+  struct BIn {
+    double bl[7];
+  };
+  // unconditional loads (lanes without a B value read a valid dummy cell):
+  // a per-lane select around a load makes hipcc wait for each one
+  auto load_b = [&](int s) {
+    const BDesc d = bdesc(s);
+    BIn b;
+#pragma unroll
+    for (int q = 0; q < 7; q++) b.bl[q] = 0.0;
+    if (s <= NC && tid < TJ + NC) {
+      // values taken from LDS or replaced later re-read cell c (no extra
+      // cache line)
+      const double *xs = d.pre ? d.xs : x, *rs = d.pre ? d.rs : r;
+      const size_t c = d.pre ? d.c : ix3(NG, 1, j0, 1);
+      const long o2 = (d.rep == 2 || d.lm) ? 0 : -(long)NG;
+      const long o3 = (d.rep == 3 || d.lp) ? 0 : (long)NG;
+      const long o4 = (d.rep == 4 || d.zm) ? 0 : -(long)SK;
+      const long o5 = (d.rep == 5 || d.zp) ? 0 : (long)SK;
+      b.bl[0] = xs[c - 1];
+      b.bl[1] = xs[c + 1];
+      b.bl[2] = xs[c + o2];
+      b.bl[3] = xs[c + o3];
+      b.bl[4] = xs[c + o4];
+      b.bl[5] = xs[c + o5];
+      b.bl[6] = rs[c];
+    }
+    return b;
+  };
+  BIn bc = load_b(1);
+  // phi planes and rhs rows in flight: loaded in step s, consumed (LDS /
+  // rotation) in step s+1 -- two planes of each per workgroup in flight
+  struct Pf {
     double nx[EPT], nlo[RPT], nhi[RPT];
+  };
+  auto load_pf = [&](Pf &f, int kp) {  // phi plane kp, rhs plane kp - 1
+    // (clamped indices instead of per-lane guards; a plane beyond NC + 1 is
+    // never stored)
+    const int kx = kp <= NC + 1 ? kp : NC + 1, kr = kp - 1 <= NC ? kp - 1 : NC;
 #pragma unroll
     for (int e = 0; e < EPT; e++) {
       const int xx = tid + NT * e;
-      nx[e] = (s + 2 <= NC + 1 && xx < PL) ? x[(size_t)(s + 2) * SK + t0 + xx] : 0.0;
+      f.nx[e] = x[(size_t)kx * SK + t0 + (xx < PL ? xx : PL - 1)];
     }
 #pragma unroll
     for (int q = 0; q < RPT; q++) {
       const int rr = tid + NT * q;
       const int j = j0 + rr / HN, i1 = 2 * (rr % HN) + 1;
-      const size_t g = (size_t)(s + 1) * SK + (size_t)j * NG + i1;
-      nlo[q] = s + 1 <= NC ? r[g] : 0.0;
-      nhi[q] = s + 1 <= NC ? r[g + 1] : 0.0;
+      const size_t g = (size_t)kr * SK + (size_t)j * NG + i1;
+      f.nlo[q] = r[g];
+      f.nhi[q] = r[g + 1];
     }
+  };
+  Pf X0, X1;
+  if (DEPTH == 2) load_pf(X0, 3);
+
+  auto step = [&](const int s, Pf &ld, const Pf &cn) {
+    const BIn bn = load_b(s + 1);
+    load_pf(ld, s + 1 + DEPTH);
+    double *bl = bc.bl;
+    const BDesc bd = bdesc(s);
+    const int b_i = bd.i, b_j = bd.j, b_jl = bd.jl, b_nb = bd.nb, b_rep = bd.rep;
+    const bool b_pre = bd.pre, b_lm = bd.lm, b_lp = bd.lp, b_zm = bd.zm, b_zp = bd.zp;
     double *Pm = P[(s - 1) & 3], *P0 = P[s & 3], *Pp = P[(s + 1) & 3];
     double *Pmm = P[(s - 2) & 3];
     // A: red cells of plane s
@@ -504,7 +557,9 @@ __global__ void __launch_bounds__((RbPar<NC, TJ>::NT)) __attribute__((amdgpu_wav
           int p1[3] = {b_i, b_jl, 0};
           p1[d] = (b_rep & 1) ? (d == 0 ? 1 : 1) : (d == 0 ? NC : TJ);
           const double x1v = P0[p1[1] * NG + p1[0]];
-          bl[b_rep] = x1v;
+#pragma unroll
+          for (int q = 0; q < 6; q++)
+            if (q == b_rep) bl[q] = x1v;
         }
         if (b_lm) bl[2] = P0[(b_jl - 1) * NG + b_i];
         if (b_lp) bl[3] = P0[(b_jl + 1) * NG + b_i];
@@ -570,7 +625,7 @@ __global__ void __launch_bounds__((RbPar<NC, TJ>::NT)) __attribute__((amdgpu_wav
 #pragma unroll
       for (int e = 0; e < EPT; e++) {
         const int xx = tid + NT * e;
-        if (xx < PL) Pmm[xx] = nx[e];
+        if (xx < PL) Pmm[xx] = cn.nx[e];
       }
     }
 #pragma unroll
@@ -578,10 +633,19 @@ __global__ void __launch_bounds__((RbPar<NC, TJ>::NT)) __attribute__((amdgpu_wav
       const int j = j0 + (tid + NT * q) / HN;
       const bool odd = (j + s + 1) & 1;  // red cell of plane s+1 is i1 + 1
       rB[q] = rBn[q];
-      rR[q] = odd ? nhi[q] : nlo[q];
-      rBn[q] = odd ? nlo[q] : nhi[q];
+      rR[q] = odd ? cn.nhi[q] : cn.nlo[q];
+      rBn[q] = odd ? cn.nlo[q] : cn.nhi[q];
     }
+    bc = bn;
     __syncthreads();
+  };
+  if (DEPTH == 1) {
+    for (int s = 1; s <= NC + 1; s++) step(s, X0, X0);
+  } else {
+    for (int s = 1; s <= NC + 1; s += 2) {
+      step(s, X1, X0);
+      if (s + 1 <= NC + 1) step(s + 1, X0, X1);
+    }
   }
 }
 
@@ -1604,6 +1668,8 @@ struct afh_mg {
   bool force_tiles = false;  // AFH_GSRB_TILES
   bool pair_v1 = false;      // AFH_GSRB_PAIR_V1: column-mapped whole-box kernel
   int pair_tj = 0;           // AFH_GSRB_PAIR_TJ=32: half-box tiles (NC = 64)
+  int pair_depth = 1;        // AFH_GSRB_PAIR_DEPTH=2: two planes in flight (NC = 64)
+  int pair_nt = 0;           // AFH_GSRB_PAIR_NT=512: 512-thread whole-box pair (NC = 64)
   int wave_cells = CS_WAVE_CELLS;  // AFH_CS_WAVE_CELLS
   // AFH_COARSE_DIRECT: eigenvectors Q and Q^T per dim, eigenvalues, work
   double *d_q[3] = {nullptr, nullptr, nullptr}, *d_qt[3] = {nullptr, nullptr, nullptr};
@@ -1799,6 +1865,8 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
   if (const char *env = getenv("AFH_GSRB_TILES")) mg->force_tiles = atoi(env) != 0;
   if (const char *env = getenv("AFH_GSRB_PAIR_V1")) mg->pair_v1 = atoi(env) != 0;
   if (const char *env = getenv("AFH_GSRB_PAIR_TJ")) mg->pair_tj = atoi(env);
+  if (const char *env = getenv("AFH_GSRB_PAIR_DEPTH")) mg->pair_depth = atoi(env);
+  if (const char *env = getenv("AFH_GSRB_PAIR_NT")) mg->pair_nt = atoi(env);
   if (const char *env = getenv("AFH_CS_WAVE_CELLS")) mg->wave_cells = atoi(env);
   if (fused_nc_ok(t->nc) && mg->fused_min > 0) {
     bool any = false;
@@ -1895,31 +1963,40 @@ static bool pair_tiles(const afh_mg *mg, int lvl) {
   return mg->t->nc >= 32 && (mg->force_tiles || (n >= 64 && n < 256));
 }
 
+template <int NC, int TJ, int DEPTH, int NTM = 0>
+static void launch_pair2(afh_mg *mg, int lvl, const double *src, double *dst,
+                         const Coef &cf, double inv_c1, hipEvent_t e0, hipEvent_t e1) {
+  afh_tree *t = mg->t;
+  launch_ev((k_gsrb_pair2<NC, TJ, DEPTH, NTM>), e0, e1,
+            dim3(t->ids.n(lvl) * RbPar<NC, TJ, NTM>::NTILE),
+            dim3(RbPar<NC, TJ, NTM>::NT), t->stream, src, dst, t->ccv(mg->d.i_rhs),
+            t->ccv(mg->d.i_phi), t->d_boxes, t->ids.at(lvl), t->bsz, cf, inv_c1,
+            t->gc_args(mg->d.i_phi));
+}
+
 template <int NC>
 static void launch_pair(afh_mg *mg, int lvl, const double *src, double *dst,
                         const Coef &cf, double inv_c1, hipEvent_t e0, hipEvent_t e1) {
   afh_tree *t = mg->t;
   if (t->ids.n(lvl) == 0) return;
   if constexpr (NC >= 32) {
-    if (pair_tiles(mg, lvl))
-      return launch_pair_t<NC, NC / 4>(mg, lvl, src, dst, cf, inv_c1, e0, e1);
+    if (pair_tiles(mg, lvl)) {
+      if (mg->pair_v1) return launch_pair_t<NC, NC / 4>(mg, lvl, src, dst, cf, inv_c1, e0, e1);
+      return launch_pair2<NC, NC / 4, 2>(mg, lvl, src, dst, cf, inv_c1, e0, e1);
+    }
   }
   if constexpr (NC >= 16) {
     if (!mg->pair_v1) {
       if constexpr (NC == 64) {
-        if (mg->pair_tj == 32) {
-          launch_ev((k_gsrb_pair2<NC, 32>), e0, e1, dim3(t->ids.n(lvl) * 2),
-                    dim3(RbPar<NC, 32>::NT), t->stream, src, dst,
-                    t->ccv(mg->d.i_rhs), t->ccv(mg->d.i_phi), t->d_boxes,
-                    t->ids.at(lvl), t->bsz, cf, inv_c1, t->gc_args(mg->d.i_phi));
-          return;
-        }
+        if (mg->pair_tj == 32)
+          return launch_pair2<NC, 32, 2>(mg, lvl, src, dst, cf, inv_c1, e0, e1);
+        if (mg->pair_nt == 512)
+          return launch_pair2<NC, NC, 2, 512>(mg, lvl, src, dst, cf, inv_c1, e0, e1);
+        if (mg->pair_depth == 2)
+          return launch_pair2<NC, NC, 2>(mg, lvl, src, dst, cf, inv_c1, e0, e1);
+        return launch_pair2<NC, NC, 1>(mg, lvl, src, dst, cf, inv_c1, e0, e1);
       }
-      launch_ev((k_gsrb_pair2<NC, NC>), e0, e1, dim3(t->ids.n(lvl)),
-                dim3(RbPar<NC, NC>::NT), t->stream, src, dst, t->ccv(mg->d.i_rhs),
-                t->ccv(mg->d.i_phi), t->d_boxes, t->ids.at(lvl), t->bsz, cf, inv_c1,
-                t->gc_args(mg->d.i_phi));
-      return;
+      return launch_pair2<NC, NC, 2>(mg, lvl, src, dst, cf, inv_c1, e0, e1);
     }
   }
   launch_pair_t<NC, NC>(mg, lvl, src, dst, cf, inv_c1, e0, e1);
