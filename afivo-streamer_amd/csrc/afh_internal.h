@@ -303,11 +303,14 @@ __device__ __forceinline__ void cell3g(int t, int ng, int &i, int &j, int &k) {
 // m_af_multigrid.f90:294-461; af_gc_interp / af_gc_interp_lim,
 // m_af_ghostcell.f90:394-612). `own(q)` returns the box's current value at
 // interior cell q; coarse data are read from v (the parent's neighbour).
+// nb_id / drd: the face's neighbour id and the box's spacing along the
+// face normal, passed in by kernels that hold them in registers (no
+// per-lane metadata load in their hot loop).
 template <class Own>
-__device__ __forceinline__ double gc_face_nocopy(
+__device__ __forceinline__ double gc_face_nocopy_k(
     const double *__restrict__ v, const afh_box_meta *__restrict__ meta,
-    const afh_box_meta &m, int nb, const int p[3], int a, int b, int nc,
-    size_t bsz, afh_bc bc, int rb, Own own) {
+    const afh_box_meta &m, int nb, int nb_id, double drd, const int p[3], int a,
+    int b, int nc, size_t bsz, afh_bc bc, int rb, Own own) {
   const int d = (nb - 1) >> 1;
   const bool low = ((nb - 1) & 1) == 0;
   const int ta = (d == 0) ? 1 : 0, tb = (d == 2) ? 1 : 2;
@@ -317,11 +320,11 @@ __device__ __forceinline__ double gc_face_nocopy(
   int q1[3] = {p[0], p[1], p[2]}, q2[3] = {p[0], p[1], p[2]};
   q1[d] = x1;
   q2[d] = x2;
-  if (m.neighbors[nb - 1] < 0) {
+  if (nb_id < 0) {
     double c0, c1, c2;
     switch (bc.type) {
     case AFH_BC_DIRICHLET: c0 = 2; c1 = -1; c2 = 0; break;
-    case AFH_BC_NEUMANN: c0 = m.dr[d] * (low ? -1 : 1); c1 = 1; c2 = 0; break;
+    case AFH_BC_NEUMANN: c0 = drd * (low ? -1 : 1); c1 = 1; c2 = 0; break;
     case AFH_BC_CONTINUOUS: c0 = 0; c1 = 2; c2 = -1; break;
     default: c0 = 1; c1 = 0; c2 = 0; break;
     }
@@ -385,5 +388,14 @@ __device__ __forceinline__ double gc_face_nocopy(
   double val = third * cv1 + sixth * cv2 + sixth * cv3 + third * own(q1);
   if (rb == AFH_RB_GC_INTERP_LIM && val > 2 * cv1) val = 2 * cv1;
   return val;
+}
+
+template <class Own>
+__device__ __forceinline__ double gc_face_nocopy(
+    const double *__restrict__ v, const afh_box_meta *__restrict__ meta,
+    const afh_box_meta &m, int nb, const int p[3], int a, int b, int nc,
+    size_t bsz, afh_bc bc, int rb, Own own) {
+  return gc_face_nocopy_k(v, meta, m, nb, m.neighbors[nb - 1], m.dr[(nb - 1) >> 1], p,
+                          a, b, nc, bsz, bc, rb, own);
 }
 }  // namespace afh

@@ -123,14 +123,13 @@ struct RbGeom {
 // One red ghost cell p of face nb for k_gsrb_pair. x1v / x2v: this box's
 // current values next to the face (x1 black, old; x2 red, new).
 template <int NC>
-__device__ __forceinline__ double pair_ghost(
+__device__ __forceinline__ double pair_ghost_k(
     const double *__restrict__ src, const double *__restrict__ coarse,
     const double *__restrict__ rhs,
     const afh_box_meta *__restrict__ meta, const afh_box_meta &m, int nb,
-    int p0, int p1, int p2, int a, int b, size_t bsz, const Coef &cf,
-    double inv_c1, afh_bc bc, int rb, double x1v, double x2v) {
+    int nb_id, double drd, int p0, int p1, int p2, int a, int b, size_t bsz,
+    const Coef &cf, double inv_c1, afh_bc bc, int rb, double x1v, double x2v) {
   constexpr int NG = NC + 2;
-  const int nb_id = m.neighbors[nb - 1];
   const int d = (nb - 1) >> 1;
   const bool low = ((nb - 1) & 1) == 0;
   const int p[3] = {p0, p1, p2};
@@ -152,8 +151,20 @@ __device__ __forceinline__ double pair_ghost(
            inv_c1;
   }
   const int x1 = low ? 1 : NC;
-  return gc_face_nocopy(coarse, meta, m, nb, p, a, b, NC, bsz, bc, rb,
-                        [&](const int *q) { return q[d] == x1 ? x1v : x2v; });
+  return gc_face_nocopy_k(coarse, meta, m, nb, nb_id, drd, p, a, b, NC, bsz, bc, rb,
+                          [&](const int *q) { return q[d] == x1 ? x1v : x2v; });
+}
+
+template <int NC>
+__device__ __forceinline__ double pair_ghost(
+    const double *__restrict__ src, const double *__restrict__ coarse,
+    const double *__restrict__ rhs,
+    const afh_box_meta *__restrict__ meta, const afh_box_meta &m, int nb,
+    int p0, int p1, int p2, int a, int b, size_t bsz, const Coef &cf,
+    double inv_c1, afh_bc bc, int rb, double x1v, double x2v) {
+  return pair_ghost_k<NC>(src, coarse, rhs, meta, m, nb, m.neighbors[nb - 1],
+                          m.dr[(nb - 1) >> 1], p0, p1, p2, a, b, bsz, cf, inv_c1, bc,
+                          rb, x1v, x2v);
 }
 
 template <int NC, int TJ>
@@ -340,6 +351,7 @@ struct RbPar {
   static constexpr int PL = (TJ + 2) * NG;                  // LDS plane (rows j0-1..j1+1)
   static constexpr int EPT = (PL + NT - 1) / NT;            // plane entries per thread
   static constexpr int OPT = (NC * TJ + NT - 1) / NT;       // stored cells per thread
+  static constexpr int OPTF = (NG * TJ + NT - 1) / NT;      // same, rows with x ghosts
 };
 
 // Parity-mapped form of k_gsrb_pair: in step s thread t owns the same RPT
@@ -353,7 +365,10 @@ struct RbPar {
 // identical results.
 // DEPTH: planes of phi / rhs in flight per workgroup (1: loaded and stored
 // in the same step; 2: loaded one step earlier); NTM: workgroup size cap
-template <int NC, int TJ, int DEPTH = 2, int NTM = 0>
+// FR: store plane rows whole, x ghost cells included (one contiguous run per
+// tile plane, no partially written cache lines; the level fill after the
+// pair rewrites every ghost cell of dst)
+template <int NC, int TJ, int DEPTH = 2, int NTM = 0, bool FR = true, bool P3 = true>
 __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
     k_gsrb_pair2(const double *__restrict__ src, double *__restrict__ dst,
                  const double *__restrict__ rhs, const double *__restrict__ coarse,
@@ -370,6 +385,30 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
   const int id = ids[wg / G::NTILE];
   const int j0 = (wg % G::NTILE) * TJ + 1, j1 = j0 + TJ - 1;
   const afh_box_meta &m = meta[id - 1];
+  // the box's neighbour ids and spacings, wave-uniform, read once: per-lane
+  // metadata loads in the loop would wait for the plane prefetch (vmcnt(0))
+  // (separate scalars, not an array: a selected array element becomes a
+  // scratch load)
+  const int nb1 = m.neighbors[0], nb2 = m.neighbors[1], nb3 = m.neighbors[2],
+            nb4 = m.neighbors[3], nb5 = m.neighbors[4], nb6 = m.neighbors[5];
+  const double dr0 = m.dr[0], dr1 = m.dr[1], dr2 = m.dr[2];
+  auto nbid = [&](int nb) {
+    return nb == 1 ? nb1 : nb == 2 ? nb2 : nb == 3 ? nb3 : nb == 4 ? nb4 : nb == 5 ? nb5 : nb6;
+  };
+  auto drof = [&](int nb) {
+    const int d = (nb - 1) >> 1;
+    return d == 0 ? dr0 : d == 1 ? dr1 : dr2;
+  };
+  // the face's boundary condition, selected the same way (a per-lane index
+  // into the kernel-argument array would be a scratch copy)
+  auto bcof = [&](int nb) {
+    afh_bc b;
+    b.type = nb == 1 ? ga.bc[0].type : nb == 2 ? ga.bc[1].type : nb == 3 ? ga.bc[2].type
+           : nb == 4 ? ga.bc[3].type : nb == 5 ? ga.bc[4].type : ga.bc[5].type;
+    b.value = nb == 1 ? ga.bc[0].value : nb == 2 ? ga.bc[1].value : nb == 3 ? ga.bc[2].value
+            : nb == 4 ? ga.bc[3].value : nb == 5 ? ga.bc[4].value : ga.bc[5].value;
+    return b;
+  };
   const double *x = src + (size_t)(id - 1) * bsz;
   double *y = dst + (size_t)(id - 1) * bsz;
   const double *r = rhs + (size_t)(id - 1) * bsz;
@@ -443,7 +482,7 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
         b.xs = x;
         b.rs = r;
       } else {
-        const int nb_id = m.neighbors[b.nb - 1];
+        const int nb_id = nbid(b.nb);
         if (nb_id > 0) {
           const int d = (b.nb - 1) >> 1;
           const bool low = ((b.nb - 1) & 1) == 0;
@@ -523,6 +562,30 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
   Pf X0, X1;
   if (DEPTH == 2) load_pf(X0, 3);
 
+  // E: plane k of the tile to dst (in full rows with FR)
+  auto store_plane = [&](const int k, const double *Pk) {
+    if (FR) {
+#pragma unroll
+      for (int q = 0; q < G::OPTF; q++) {
+        const int e = tid + NT * q;
+        if (e < NG * TJ) y[(size_t)k * SK + t0 + NG + e] = Pk[NG + e];
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < OPT; q++) {
+        const int e = tid + NT * q;
+        if (e < NC * TJ) {
+          const int c = (e / NC + 1) * NG + e % NC + 1;
+          y[(size_t)k * SK + t0 + c] = Pk[c];
+        }
+      }
+    }
+  };
+  // Step s. P3 (three barriers): A (red cells of plane s) with E of plane
+  // s-2 | B (red ghosts of plane s: they are first read by C of step s+1)
+  // with C (black cells of plane s-1) | D. At s = 2 and NC+1 the z ghost
+  // plane is written between B and C (C reads it; it reads the black cells
+  // C updates). Otherwise A | B | C | E, D.
   auto step = [&](const int s, Pf &ld, const Pf &cn) {
     const BIn bn = load_b(s + 1);
     load_pf(ld, s + 1 + DEPTH);
@@ -544,6 +607,7 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
                 inv_c1;
       }
     }
+    if (P3 && s >= 3) store_plane(s - 2, Pmm);
     __syncthreads();
     // B: red values around the tile: x ghost cells of its rows; the halo
     // rows (ghost row of the box, or the red cells of the adjacent tile
@@ -569,15 +633,15 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
              cf.c[4] * bl[3] - cf.c[5] * bl[4] - cf.c[6] * bl[5]) *
             inv_c1;
       } else if (b_nb <= 2) {
-        v = pair_ghost<NC>(src, coarse, rhs, meta, m, b_nb, b_i, b_j, s, b_j, s,
-                           bsz, cf, inv_c1, ga.bc[b_nb - 1], ga.rb,
-                           P0[b_jl * NG + (b_i == 0 ? 1 : NC)],
-                           P0[b_jl * NG + (b_i == 0 ? 2 : NC - 1)]);
+        v = pair_ghost_k<NC>(src, coarse, rhs, meta, m, b_nb, nbid(b_nb), drof(b_nb),
+                             b_i, b_j, s, b_j, s, bsz, cf, inv_c1, bcof(b_nb), ga.rb,
+                             P0[b_jl * NG + (b_i == 0 ? 1 : NC)],
+                             P0[b_jl * NG + (b_i == 0 ? 2 : NC - 1)]);
       } else {
         const int l1 = b_j == 0 ? 1 : TJ, l2 = b_j == 0 ? 2 : TJ - 1;
-        v = pair_ghost<NC>(src, coarse, rhs, meta, m, b_nb, b_i, b_j, s, b_i, s,
-                           bsz, cf, inv_c1, ga.bc[b_nb - 1], ga.rb,
-                           P0[l1 * NG + b_i], P0[l2 * NG + b_i]);
+        v = pair_ghost_k<NC>(src, coarse, rhs, meta, m, b_nb, nbid(b_nb), drof(b_nb),
+                             b_i, b_j, s, b_i, s, bsz, cf, inv_c1, bcof(b_nb), ga.rb,
+                             P0[l1 * NG + b_i], P0[l2 * NG + b_i]);
       }
       P0[b_jl * NG + b_i] = v;
     }
@@ -591,11 +655,13 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
       for (int q = 0; q < RPT; q++) {
         int i, j;
         const int c = col(q, k, i, j);
-        Pg[c] = pair_ghost<NC>(src, coarse, rhs, meta, m, nb, i, j, k, i, j, bsz,
-                               cf, inv_c1, ga.bc[nb - 1], ga.rb, Pm[c], X2[c]);
+        Pg[c] = pair_ghost_k<NC>(src, coarse, rhs, meta, m, nb, s == 2 ? nb5 : nb6, dr2,
+                                 i, j, k, i, j, bsz, cf, inv_c1,
+                                 s == 2 ? ga.bc[4] : ga.bc[5], ga.rb, Pm[c], X2[c]);
       }
+      if (P3) __syncthreads();
     }
-    __syncthreads();
+    if (!P3) __syncthreads();
     // C: black cells of plane s-1, in place
     if (s >= 2) {
 #pragma unroll
@@ -609,18 +675,8 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
       }
     }
     __syncthreads();
-    // E: plane s-1 of the tile to dst in full rows; D: plane s+2 into the
-    // slot of plane s-2
-    if (s >= 2) {
-#pragma unroll
-      for (int q = 0; q < OPT; q++) {
-        const int e = tid + NT * q;
-        if (e < NC * TJ) {
-          const int c = (e / NC + 1) * NG + e % NC + 1;
-          y[(size_t)(s - 1) * SK + t0 + c] = Pm[c];
-        }
-      }
-    }
+    // E (without P3): plane s-1; D: plane s+2 into the slot of plane s-2
+    if (!P3 && s >= 2) store_plane(s - 1, Pm);
     if (s + 2 <= NC + 1) {
 #pragma unroll
       for (int e = 0; e < EPT; e++) {
@@ -647,6 +703,7 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
       if (s + 1 <= NC + 1) step(s + 1, X0, X1);
     }
   }
+  if (P3) store_plane(NC, P[NC & 3]);
 }
 
 __device__ __forceinline__ double apply7(const double *x, size_t c, size_t sj,
@@ -1670,6 +1727,8 @@ struct afh_mg {
   int pair_tj = 0;           // AFH_GSRB_PAIR_TJ=32: half-box tiles (NC = 64)
   int pair_depth = 1;        // AFH_GSRB_PAIR_DEPTH=2: two planes in flight (NC = 64)
   int pair_nt = 0;           // AFH_GSRB_PAIR_NT=512: 512-thread whole-box pair (NC = 64)
+  bool pair_fr = true;       // AFH_GSRB_PAIR_FR=0: interior-only row stores (NC = 64)
+  bool pair_p3 = true;       // AFH_GSRB_PAIR_P3=0: four barriers per plane (NC = 64)
   int wave_cells = CS_WAVE_CELLS;  // AFH_CS_WAVE_CELLS
   // AFH_COARSE_DIRECT: eigenvectors Q and Q^T per dim, eigenvalues, work
   double *d_q[3] = {nullptr, nullptr, nullptr}, *d_qt[3] = {nullptr, nullptr, nullptr};
@@ -1867,6 +1926,8 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
   if (const char *env = getenv("AFH_GSRB_PAIR_TJ")) mg->pair_tj = atoi(env);
   if (const char *env = getenv("AFH_GSRB_PAIR_DEPTH")) mg->pair_depth = atoi(env);
   if (const char *env = getenv("AFH_GSRB_PAIR_NT")) mg->pair_nt = atoi(env);
+  if (const char *env = getenv("AFH_GSRB_PAIR_FR")) mg->pair_fr = atoi(env) != 0;
+  if (const char *env = getenv("AFH_GSRB_PAIR_P3")) mg->pair_p3 = atoi(env) != 0;
   if (const char *env = getenv("AFH_CS_WAVE_CELLS")) mg->wave_cells = atoi(env);
   if (fused_nc_ok(t->nc) && mg->fused_min > 0) {
     bool any = false;
@@ -1963,11 +2024,11 @@ static bool pair_tiles(const afh_mg *mg, int lvl) {
   return mg->t->nc >= 32 && (mg->force_tiles || (n >= 64 && n < 256));
 }
 
-template <int NC, int TJ, int DEPTH, int NTM = 0>
+template <int NC, int TJ, int DEPTH, int NTM = 0, bool FR = true, bool P3 = true>
 static void launch_pair2(afh_mg *mg, int lvl, const double *src, double *dst,
                          const Coef &cf, double inv_c1, hipEvent_t e0, hipEvent_t e1) {
   afh_tree *t = mg->t;
-  launch_ev((k_gsrb_pair2<NC, TJ, DEPTH, NTM>), e0, e1,
+  launch_ev((k_gsrb_pair2<NC, TJ, DEPTH, NTM, FR, P3>), e0, e1,
             dim3(t->ids.n(lvl) * RbPar<NC, TJ, NTM>::NTILE),
             dim3(RbPar<NC, TJ, NTM>::NT), t->stream, src, dst, t->ccv(mg->d.i_rhs),
             t->ccv(mg->d.i_phi), t->d_boxes, t->ids.at(lvl), t->bsz, cf, inv_c1,
@@ -1994,6 +2055,11 @@ static void launch_pair(afh_mg *mg, int lvl, const double *src, double *dst,
           return launch_pair2<NC, NC, 2, 512>(mg, lvl, src, dst, cf, inv_c1, e0, e1);
         if (mg->pair_depth == 2)
           return launch_pair2<NC, NC, 2>(mg, lvl, src, dst, cf, inv_c1, e0, e1);
+        if (!mg->pair_fr)
+          return launch_pair2<NC, NC, 1, 0, false>(mg, lvl, src, dst, cf, inv_c1, e0, e1);
+        if (!mg->pair_p3)
+          return launch_pair2<NC, NC, 1, 0, true, false>(mg, lvl, src, dst, cf, inv_c1, e0,
+                                                         e1);
         return launch_pair2<NC, NC, 1>(mg, lvl, src, dst, cf, inv_c1, e0, e1);
       }
       return launch_pair2<NC, NC, 2>(mg, lvl, src, dst, cf, inv_c1, e0, e1);
