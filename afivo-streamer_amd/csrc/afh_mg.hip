@@ -368,7 +368,8 @@ struct RbPar {
 // FR: store plane rows whole, x ghost cells included (one contiguous run per
 // tile plane, no partially written cache lines; the level fill after the
 // pair rewrites every ghost cell of dst)
-template <int NC, int TJ, int DEPTH = 2, int NTM = 0, bool FR = true, bool P3 = true>
+template <int NC, int TJ, int DEPTH = 2, int NTM = 0, bool FR = true, bool P3 = true,
+          bool SP = true>
 __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
     k_gsrb_pair2(const double *__restrict__ src, double *__restrict__ dst,
                  const double *__restrict__ rhs, const double *__restrict__ coarse,
@@ -380,6 +381,15 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
                 EPT = G::EPT, OPT = G::OPT;
   constexpr size_t SK = (size_t)NG * NG;
   __shared__ double P[4][PL];  // planes s-2 .. s+1 at slot (plane & 3)
+  // LDS row layout. SP (split parity): each row holds its even-i cells, then
+  // its odd-i cells, so the red (black) cells the lanes of a row update and
+  // all their neighbours are unit-stride in LDS (no bank conflicts); the
+  // plane image is permuted on its way in (D) and out (E).
+  constexpr int HG = NG / 2;
+  auto L = [](int jl, int i) {
+    return jl * NG + (SP ? ((i & 1) ? HG + (i >> 1) : (i >> 1)) : i);
+  };
+  auto perm = [&](int e) { return L(e / NG, e % NG); };  // plane entry -> LDS
   const int tid = threadIdx.x;
   const int wg = xcd_swizzle(blockIdx.x, gridDim.x);
   const int id = ids[wg / G::NTILE];
@@ -418,12 +428,12 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
     const int rr = tid + NT * q;
     j = j0 + rr / HN;
     i = 2 * (rr % HN) + 1 + ((j + s) & 1);
-    return (j - j0 + 1) * NG + i;
+    return L(j - j0 + 1, i);
   };
 
   // planes 0..2 -> LDS; rhs of the red cells of plane 1
   for (int e = tid; e < 3 * PL; e += NT)
-    P[e / PL][e % PL] = x[(size_t)(e / PL) * SK + t0 + e % PL];
+    P[e / PL][perm(e % PL)] = x[(size_t)(e / PL) * SK + t0 + e % PL];
   // rhs in registers: rR red cells of plane s, rB black cells of plane s-1,
   // rBn black cells of plane s (step s+1). Both parities of a plane are
   // loaded in the same step (adjacent cells 2 ih + 1, 2 ih + 2 of a row), so
@@ -568,7 +578,7 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
 #pragma unroll
       for (int q = 0; q < G::OPTF; q++) {
         const int e = tid + NT * q;
-        if (e < NG * TJ) y[(size_t)k * SK + t0 + NG + e] = Pk[NG + e];
+        if (e < NG * TJ) y[(size_t)k * SK + t0 + NG + e] = Pk[perm(NG + e)];
       }
     } else {
 #pragma unroll
@@ -576,7 +586,7 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
         const int e = tid + NT * q;
         if (e < NC * TJ) {
           const int c = (e / NC + 1) * NG + e % NC + 1;
-          y[(size_t)k * SK + t0 + c] = Pk[c];
+          y[(size_t)k * SK + t0 + c] = Pk[L(e / NC + 1, e % NC + 1)];
         }
       }
     }
@@ -601,7 +611,8 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
       for (int q = 0; q < RPT; q++) {
         int i, j;
         const int c = col(q, s, i, j);
-        P0[c] = (rR[q] - cf.c[1] * P0[c - 1] - cf.c[2] * P0[c + 1] -
+        const int cm = L(j - j0 + 1, i - 1), cp = L(j - j0 + 1, i + 1);
+        P0[c] = (rR[q] - cf.c[1] * P0[cm] - cf.c[2] * P0[cp] -
                  cf.c[3] * P0[c - NG] - cf.c[4] * P0[c + NG] - cf.c[5] * Pm[c] -
                  cf.c[6] * Pp[c]) *
                 inv_c1;
@@ -620,30 +631,30 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
           const int d = b_rep >> 1;
           int p1[3] = {b_i, b_jl, 0};
           p1[d] = (b_rep & 1) ? (d == 0 ? 1 : 1) : (d == 0 ? NC : TJ);
-          const double x1v = P0[p1[1] * NG + p1[0]];
+          const double x1v = P0[L(p1[1], p1[0])];
 #pragma unroll
           for (int q = 0; q < 6; q++)
             if (q == b_rep) bl[q] = x1v;
         }
-        if (b_lm) bl[2] = P0[(b_jl - 1) * NG + b_i];
-        if (b_lp) bl[3] = P0[(b_jl + 1) * NG + b_i];
-        if (b_zm) bl[4] = Pm[b_jl * NG + b_i];
-        if (b_zp) bl[5] = Pp[b_jl * NG + b_i];
+        if (b_lm) bl[2] = P0[L(b_jl - 1, b_i)];
+        if (b_lp) bl[3] = P0[L(b_jl + 1, b_i)];
+        if (b_zm) bl[4] = Pm[L(b_jl, b_i)];
+        if (b_zp) bl[5] = Pp[L(b_jl, b_i)];
         v = (bl[6] - cf.c[1] * bl[0] - cf.c[2] * bl[1] - cf.c[3] * bl[2] -
              cf.c[4] * bl[3] - cf.c[5] * bl[4] - cf.c[6] * bl[5]) *
             inv_c1;
       } else if (b_nb <= 2) {
         v = pair_ghost_k<NC>(src, coarse, rhs, meta, m, b_nb, nbid(b_nb), drof(b_nb),
                              b_i, b_j, s, b_j, s, bsz, cf, inv_c1, bcof(b_nb), ga.rb,
-                             P0[b_jl * NG + (b_i == 0 ? 1 : NC)],
-                             P0[b_jl * NG + (b_i == 0 ? 2 : NC - 1)]);
+                             P0[L(b_jl, b_i == 0 ? 1 : NC)],
+                             P0[L(b_jl, b_i == 0 ? 2 : NC - 1)]);
       } else {
         const int l1 = b_j == 0 ? 1 : TJ, l2 = b_j == 0 ? 2 : TJ - 1;
         v = pair_ghost_k<NC>(src, coarse, rhs, meta, m, b_nb, nbid(b_nb), drof(b_nb),
                              b_i, b_j, s, b_i, s, bsz, cf, inv_c1, bcof(b_nb), ga.rb,
-                             P0[l1 * NG + b_i], P0[l2 * NG + b_i]);
+                             P0[L(l1, b_i)], P0[L(l2, b_i)]);
       }
-      P0[b_jl * NG + b_i] = v;
+      P0[L(b_jl, b_i)] = v;
     }
     if (s == 2 || s == NC + 1) {
       // z ghost plane 0 (NC+1): red cells; x1 = plane 1 (NC), black, old;
@@ -668,7 +679,8 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
       for (int q = 0; q < RPT; q++) {
         int i, j;
         const int c = col(q, s, i, j);
-        Pm[c] = (rB[q] - cf.c[1] * Pm[c - 1] - cf.c[2] * Pm[c + 1] -
+        const int cm = L(j - j0 + 1, i - 1), cp = L(j - j0 + 1, i + 1);
+        Pm[c] = (rB[q] - cf.c[1] * Pm[cm] - cf.c[2] * Pm[cp] -
                  cf.c[3] * Pm[c - NG] - cf.c[4] * Pm[c + NG] - cf.c[5] * Pmm[c] -
                  cf.c[6] * P0[c]) *
                 inv_c1;
@@ -681,7 +693,7 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
 #pragma unroll
       for (int e = 0; e < EPT; e++) {
         const int xx = tid + NT * e;
-        if (xx < PL) Pmm[xx] = cn.nx[e];
+        if (xx < PL) Pmm[perm(xx)] = cn.nx[e];
       }
     }
 #pragma unroll
@@ -1729,6 +1741,7 @@ struct afh_mg {
   int pair_nt = 0;           // AFH_GSRB_PAIR_NT=512: 512-thread whole-box pair (NC = 64)
   bool pair_fr = true;       // AFH_GSRB_PAIR_FR=0: interior-only row stores (NC = 64)
   bool pair_p3 = true;       // AFH_GSRB_PAIR_P3=0: four barriers per plane (NC = 64)
+  bool pair_sp = true;       // AFH_GSRB_PAIR_SP=0: natural LDS row order (NC = 64)
   int wave_cells = CS_WAVE_CELLS;  // AFH_CS_WAVE_CELLS
   // AFH_COARSE_DIRECT: eigenvectors Q and Q^T per dim, eigenvalues, work
   double *d_q[3] = {nullptr, nullptr, nullptr}, *d_qt[3] = {nullptr, nullptr, nullptr};
@@ -1928,6 +1941,7 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
   if (const char *env = getenv("AFH_GSRB_PAIR_NT")) mg->pair_nt = atoi(env);
   if (const char *env = getenv("AFH_GSRB_PAIR_FR")) mg->pair_fr = atoi(env) != 0;
   if (const char *env = getenv("AFH_GSRB_PAIR_P3")) mg->pair_p3 = atoi(env) != 0;
+  if (const char *env = getenv("AFH_GSRB_PAIR_SP")) mg->pair_sp = atoi(env) != 0;
   if (const char *env = getenv("AFH_CS_WAVE_CELLS")) mg->wave_cells = atoi(env);
   if (fused_nc_ok(t->nc) && mg->fused_min > 0) {
     bool any = false;
@@ -2024,11 +2038,12 @@ static bool pair_tiles(const afh_mg *mg, int lvl) {
   return mg->t->nc >= 32 && (mg->force_tiles || (n >= 64 && n < 256));
 }
 
-template <int NC, int TJ, int DEPTH, int NTM = 0, bool FR = true, bool P3 = true>
+template <int NC, int TJ, int DEPTH, int NTM = 0, bool FR = true, bool P3 = true,
+          bool SP = true>
 static void launch_pair2(afh_mg *mg, int lvl, const double *src, double *dst,
                          const Coef &cf, double inv_c1, hipEvent_t e0, hipEvent_t e1) {
   afh_tree *t = mg->t;
-  launch_ev((k_gsrb_pair2<NC, TJ, DEPTH, NTM, FR, P3>), e0, e1,
+  launch_ev((k_gsrb_pair2<NC, TJ, DEPTH, NTM, FR, P3, SP>), e0, e1,
             dim3(t->ids.n(lvl) * RbPar<NC, TJ, NTM>::NTILE),
             dim3(RbPar<NC, TJ, NTM>::NT), t->stream, src, dst, t->ccv(mg->d.i_rhs),
             t->ccv(mg->d.i_phi), t->d_boxes, t->ids.at(lvl), t->bsz, cf, inv_c1,
@@ -2051,12 +2066,21 @@ static void launch_pair(afh_mg *mg, int lvl, const double *src, double *dst,
       if constexpr (NC == 64) {
         if (mg->pair_tj == 32)
           return launch_pair2<NC, 32, 2>(mg, lvl, src, dst, cf, inv_c1, e0, e1);
+        if (mg->pair_nt == 512 && !mg->pair_sp)
+          return launch_pair2<NC, NC, 2, 512, true, true, false>(mg, lvl, src, dst, cf, inv_c1,
+                                                                 e0, e1);
         if (mg->pair_nt == 512)
           return launch_pair2<NC, NC, 2, 512>(mg, lvl, src, dst, cf, inv_c1, e0, e1);
+        if (mg->pair_depth == 2 && !mg->pair_sp)
+          return launch_pair2<NC, NC, 2, 0, true, true, false>(mg, lvl, src, dst, cf, inv_c1,
+                                                               e0, e1);
         if (mg->pair_depth == 2)
           return launch_pair2<NC, NC, 2>(mg, lvl, src, dst, cf, inv_c1, e0, e1);
         if (!mg->pair_fr)
           return launch_pair2<NC, NC, 1, 0, false>(mg, lvl, src, dst, cf, inv_c1, e0, e1);
+        if (!mg->pair_sp)
+          return launch_pair2<NC, NC, 1, 0, true, true, false>(mg, lvl, src, dst, cf, inv_c1,
+                                                               e0, e1);
         if (!mg->pair_p3)
           return launch_pair2<NC, NC, 1, 0, true, false>(mg, lvl, src, dst, cf, inv_c1, e0,
                                                          e1);
