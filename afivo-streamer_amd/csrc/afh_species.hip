@@ -33,6 +33,7 @@ struct DevLT {
   int n_points, n_cols;
   double x_min, inv_fac;
   const double *rc;
+  const double *rm = nullptr;  // row-major copy [row][col] (chemistry table)
 };
 
 // LT_get_loc + LT_get_col_at_loc (m_lookup_table.f90:330-406)
@@ -532,20 +533,32 @@ struct UpdArgs {
   int photo_s;
 };
 
-// Register-resident species arrays indexed by runtime reaction data: the
-// select loops unroll over the compile-time species count.
+// Register-resident species arrays indexed by runtime reaction data (the
+// index is wave-uniform): direct indexing (VGPR index mode,
+// s_set_gpr_idx_on), or with AFH_UPD_SELECT=1 a select over every species.
+#ifndef AFH_UPD_SELECT
+#define AFH_UPD_SELECT 0
+#endif
 template <int NS>
 __device__ __forceinline__ double sel(const double (&a)[NS], int idx) {
+#if AFH_UPD_SELECT
   double r = a[0];
 #pragma unroll
   for (int s = 1; s < NS; s++) r = (s == idx) ? a[s] : r;
   return r;
+#else
+  return a[idx];
+#endif
 }
 template <int NS>
 __device__ __forceinline__ void add_at(double (&a)[NS], int idx, double v) {
+#if AFH_UPD_SELECT
 #pragma unroll
   for (int s = 0; s < NS; s++)
     if (s == idx) a[s] = a[s] + v;
+#else
+  a[idx] = a[idx] + v;
+#endif
 }
 
 // get_rates for one cell and one reaction, src/m_chemistry.f90:565-650
@@ -586,13 +599,26 @@ __device__ __forceinline__ double rate_slow(const UpdArgs &A, const DevReaction 
   }
 }
 
+// Tabulated rates of one cell: the table location (low, lf) depends only on
+// the field, so it is found once per cell (lt_loc) and every tabulated
+// reaction reads its column from the two rows of a row-major copy of the
+// table (one or two cache lines per cell instead of two per reaction); same
+// expression as LT_get_col_at_loc, bitwise.
+__device__ __forceinline__ double lt_at_rm(const DevLT &lt, int col, int low, double lf) {
+  const double *r = lt.rm + (size_t)(low - 1) * lt.n_cols + (col - 1);
+  return lf * r[0] + (1 - lf) * r[lt.n_cols];
+}
+
 template <bool SLOW>
 __device__ __forceinline__ double rate_of(const UpdArgs &A, const DevReaction &R,
-                                          double field, double &Te) {
+                                          double field, double &Te, int low = -1,
+                                          double lf = 0.0) {
   const double c0 = R.rate_factor;
   const double *c = R.c;
   switch (R.rate_type) {
-  case AFH_RATE_TABULATED_FIELD: return c0 * lt_col(A.chem, R.table_col, field);
+  case AFH_RATE_TABULATED_FIELD:
+    return c0 * (low > 0 ? lt_at_rm(A.chem, R.table_col, low, lf)
+                         : lt_col(A.chem, R.table_col, field));
   case AFH_RATE_CONSTANT: return c0 * c[0];
   case AFH_RATE_LINEAR: return c0 * c[0] * (field - c[1]);
   case AFH_RATE_EXP_V1: {
@@ -999,9 +1025,12 @@ __global__ void __launch_bounds__(256, AFH_UPD_MINW)
       der[s] = 0.0;
     }
     double Te = -1.0;  // electron temperature, looked up once per cell
+    int clow = -1;
+    double clf = 0.0;
+    if (A.chem.rm) lt_loc(A.chem, field, clow, clf);
     for (int r = 0; r < A.nr; r++) {
       const DevReaction &R = A.reac[r];
-      double rate = rate_of<SLOW>(A, R, field, Te);
+      double rate = rate_of<SLOW>(A, R, field, Te, clow, clf);
       double prod = 1.0;
       for (int q = 0; q < R.n_in; q++) prod = prod * sel(dens, R.ix_in[q] - 1);
       rate = rate * prod;
@@ -1073,6 +1102,12 @@ void launch_update(const UpdArgs &A, afh_tree *t, int l,
   if (A.Ng)
     hipLaunchKernelGGL((k_update<NS, true, MAXPREV, true, true>), grid, dim3(256), 0,
                        t->stream, A, ids, nc, t->bsz, t->fsz, red);
+  else if (slow && A.n_prev == 1 && !sd)
+    hipLaunchKernelGGL((k_update<NS, true, 1, false>), grid, dim3(256), 0, t->stream, A,
+                       ids, nc, t->bsz, t->fsz, red);
+  else if (slow && A.n_prev == 2 && !sd)
+    hipLaunchKernelGGL((k_update<NS, true, 2, false>), grid, dim3(256), 0, t->stream, A,
+                       ids, nc, t->bsz, t->fsz, red);
   else if (slow)
     hipLaunchKernelGGL((k_update<NS, true>), grid, dim3(256), 0, t->stream, A,
                        ids, nc, t->bsz, t->fsz, red);
@@ -1594,7 +1629,7 @@ using namespace afh;
 struct afh_fluid {
   afh_tree *t = nullptr;
   afh_fluid_desc d;
-  double *d_td = nullptr, *d_chem = nullptr;
+  double *d_td = nullptr, *d_chem = nullptr, *d_chem_rm = nullptr;
   DevReaction *d_reac = nullptr;
   int e_index = -1;
   DevLT td, chem;
@@ -1662,9 +1697,16 @@ int32_t afh_fluid_create(afh_tree *t, const afh_fluid_desc *d, afh_fluid **out) 
   AFH_HIP(hipMemcpy(f->d_td, d->td.rows_cols, ntd * sizeof(double),
                     hipMemcpyHostToDevice));
   AFH_HIP(hipMalloc(&f->d_chem, std::max<size_t>(1, nch) * sizeof(double)));
-  if (nch)
+  if (nch) {
     AFH_HIP(hipMemcpy(f->d_chem, d->chem.rows_cols, nch * sizeof(double),
                       hipMemcpyHostToDevice));
+    const int np = d->chem.n_points, ncol = d->chem.n_cols;
+    std::vector<double> rm(nch);
+    for (int c = 0; c < ncol; c++)
+      for (int r = 0; r < np; r++) rm[(size_t)r * ncol + c] = d->chem.rows_cols[(size_t)c * np + r];
+    AFH_HIP(hipMalloc(&f->d_chem_rm, nch * sizeof(double)));
+    AFH_HIP(hipMemcpy(f->d_chem_rm, rm.data(), nch * sizeof(double), hipMemcpyHostToDevice));
+  }
   const char *staged_env = getenv("AFH_FLUX_STAGED");
   // a variable gas density takes k_flux_staged (per-face 1/N)
   if (!gas && d->td.n_points <= FLUX_LDS_MAX_POINTS && !(staged_env && atoi(staged_env))) {
@@ -1718,7 +1760,7 @@ int32_t afh_fluid_create(afh_tree *t, const afh_fluid_desc *d, afh_fluid **out) 
                     hipMemcpyHostToDevice));
   f->td = DevLT{d->td.n_points, d->td.n_cols, d->td.x_min, d->td.inv_fac, f->d_td};
   f->chem = DevLT{d->chem.n_points, d->chem.n_cols, d->chem.x_min,
-                  d->chem.inv_fac, f->d_chem};
+                  d->chem.inv_fac, f->d_chem, f->d_chem_rm};
   *out = f;
   return AFH_OK;
 }
@@ -1728,6 +1770,7 @@ int32_t afh_fluid_destroy(afh_fluid *f) {
   hipStreamSynchronize(f->t->stream);
   hipFree(f->d_td);
   hipFree(f->d_chem);
+  hipFree(f->d_chem_rm);
   hipFree(f->d_reac);
   hipFree(f->d_tdi);
   hipFree(f->d_ids);

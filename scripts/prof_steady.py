@@ -3,8 +3,8 @@
 trace (--kernel-trace --output-format csv).
 
 The timed region of `bench.py --steps K` is the last K unit steps; each step
-ends with the species update (k_update), so the window starts right after
-the (K+1)-th last k_update. Reports per step: kernel time by kernel, launch
+ends with the species update (k_update, one launch per leaf level), so the
+window starts right after the (K+1)-th last run of k_update launches. Reports per step: kernel time by kernel, launch
 count, busy time, the gaps between consecutive kernels (launch overhead and
 host synchronisation) and the span; and, for the S1-64 leaf level (largest
 launch of each kernel), average duration, algorithmic bytes (DESIGN.md
@@ -50,8 +50,10 @@ def main(path, k_steps, out):
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     upd = [i for i, r in enumerate(rows) if "k_update" in r["Kernel_Name"]]
-    start = upd[-(k_steps + 1)] + 1
-    win = rows[start:upd[-1] + 1]
+    # a step ends with the update of every leaf level (consecutive launches)
+    ends = [i for n, i in enumerate(upd) if n + 1 == len(upd) or upd[n + 1] != i + 1]
+    start = ends[-(k_steps + 1)] + 1
+    win = rows[start:ends[-1] + 1]
     st = [int(r["Start_Timestamp"]) for r in win]
     en = [int(r["End_Timestamp"]) for r in win]
     busy = sum(e - s for s, e in zip(st, en))

@@ -105,3 +105,30 @@ def test_s3_hip_equals_oracle():
         a, b = sim.tree.get_cc(iv), osim.tree.get_cc(iv)
         rel = np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300)
         assert rel <= 1e-12, (sim.cc_names[iv - 1], rel)
+
+
+@pytest.mark.gpu
+def test_s3_species_step_hip_equals_oracle():
+    """One forward_euler species step (flux + air_chemistry_v2 update, both
+    Heun stages) on the S3 tree, HIP against the C oracle (whose step is the
+    reference's forward_euler bitwise, test_reference_replay): the fluxes and
+    dt limits bitwise; the densities to 1e-13 relative -- the temperature
+    forms of air_chemistry_v2 call pow / exp, whose device (ocml) and host
+    (glibc) results may differ in the last ulp."""
+    sim = Simulation(capi.hip_library(), golden.load("case_s3"), device=0)
+    sim.set_initial_conditions()
+    osim = sim.clone(capi.oracle_library())
+    lims = []
+    for s in (sim, osim):
+        a = s.fluid.forward_euler(1e-12, 0, [0], [1.0], 1, False)
+        b = s.fluid.forward_euler(5e-13, 1, [0, 1], [0.5, 0.5], 0, True)
+        lims.append((list(a), list(b)))
+    assert lims[0][0][:2] == lims[1][0][:2] and lims[0][1][:2] == lims[1][1][:2]
+    assert np.allclose(lims[0][1], lims[1][1], rtol=1e-13, atol=0)
+    for iv in range(1, sim.n_var_face + 1):
+        assert np.array_equal(sim.tree.get_fc(iv), osim.tree.get_fc(iv))
+    for iv in sim.densities:
+        for st in (0, 1):
+            a, b = sim.tree.get_cc(iv + st), osim.tree.get_cc(iv + st)
+            rel = np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300)
+            assert rel <= 1e-13, (sim.cc_names[iv + st - 1], rel)
