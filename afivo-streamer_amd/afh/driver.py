@@ -571,6 +571,68 @@ class Simulation:
             other.tree.put_fc(iv, self.tree.get_fc(iv))
         return other
 
+    # ------------------------------------------------------- .dat files
+    def write_dat(self, name):
+        """af_write_tree(tree, name, write_sim_data) as the streamer's output
+        does (m_af_output.f90:41-194, streamer.f90:521-536): the topology of
+        the host tree, every cell and face variable from the device, the
+        simulation record appended; writes name + ".dat". The global
+        reaction rates and J.E integrals (ST_global_rates / JdotE, outputs of
+        the reference's analysis module, not computed here) are written as
+        zeros."""
+        from .datfile import DatTree, sim_data_bytes
+        t = DatTree.from_aftree(self.af, self.cc_names, self.c.sa("fc_names"))
+        used = [b for b in range(1, self.af.highest_id + 1) if self.af.in_use[b]]
+        for iv in range(1, self.n_var_cell + 1):
+            a = self.tree.get_cc(iv)
+            for b in used:
+                t.boxes[b].cc[iv] = a[b - 1]
+        for iv in range(1, self.n_var_face + 1):
+            a = self.tree.get_fc(iv)
+            for b in used:
+                t.boxes[b].fc[iv] = a[b - 1]
+        t.other = sim_data_bytes(self.it, self.output_cnt, self.time, self.global_time,
+                                 self.photoi_prev_time, self.global_dt,
+                                 np.zeros(len(self.reactions)), 0.0, self.frac_rejected)
+        t.write(name + ".dat")
+        return t
+
+    def restart(self, path):
+        """restart_from_file (streamer.f90:117-138): af_read_tree with
+        read_sim_data, the consistency checks, then the device tree built
+        from the file's topology and data (box ids as stored)."""
+        from .datfile import DatTree, parse_sim_data
+        t = DatTree.read(path)
+        if t.n_cell != self.af.nc:
+            raise ValueError("restart_from_file: incompatible box size")
+        if t.n_var_cell != self.n_var_cell:
+            raise ValueError("restart_from_file: incompatible variable list")
+        if t.other is None:
+            raise ValueError("af_read_tree: other data is not present")
+        d = parse_sim_data(t.other, len(self.reactions))
+        self.af = t.aftree()
+        self._bind(self._create_tree())
+        nb = self.tree.n_boxes
+        for iv in range(1, self.n_var_cell + 1):
+            a = np.zeros(self.tree.cc_shape)
+            if t.cc_write_binary[iv - 1]:
+                for b, box in t.boxes.items():
+                    a[b - 1] = box.cc[iv]
+            self.tree.put_cc(iv, a[:nb])
+        for iv in range(1, self.n_var_face + 1):
+            a = np.zeros(self.tree.fc_shape)
+            if t.fc_write_binary[iv - 1]:
+                for b, box in t.boxes.items():
+                    a[b - 1] = box.fc[iv]
+            self.tree.put_fc(iv, a[:nb])
+        self.it, self.output_cnt = d["it"], d["output_cnt"]
+        self.time, self.global_time = d["time"], d["global_time"]
+        self.photoi_prev_time, self.global_dt = d["photoi_prev_time"], d["global_dt"]
+        self.frac_rejected = d["fraction_steps_rejected"]
+        self.dt = self.global_dt
+        self.time_last_output = self.time  # streamer.f90:172
+        return t
+
     def start(self):
         self.set_initial_conditions()
         self.output_cnt = 0
