@@ -122,6 +122,12 @@ module m_afivo_hip
   ! regrid (afh_set_cc_prolong / afh_tree_regrid / afh_refine_flags)
   integer(c_int32_t), parameter :: AFH_PROLONG_NONE = 0, AFH_PROLONG_LINEAR = 1
   integer(c_int32_t), parameter :: AFH_PROLONG_LIMIT = 2
+  ! afh_tree_reduce_loc operations
+  integer(c_int32_t), parameter :: AFH_RED_MAX = 1, AFH_RED_MIN = 2, AFH_RED_MAXABS = 3
+  ! exchange hook kinds (afh_tree_set_hook)
+  integer(c_int32_t), parameter :: AFH_HOOK_HALO = 1, AFH_HOOK_RIMS = 2, &
+       AFH_HOOK_RESTRICT = 3, AFH_HOOK_MAX = 4, AFH_HOOK_MIN = 5, AFH_HOOK_CFLUX = 6, &
+       AFH_HOOK_SUM = 7
   integer(c_int32_t), parameter :: AFH_RM_REF = -1, AFH_KEEP_REF = 0, AFH_DO_REF = 1
   integer, parameter :: AFH_MAX_REFINE_REGIONS = 8
   integer, parameter :: AFH_MAX_GAS_SPECIES = 8
@@ -317,6 +323,36 @@ module m_afivo_hip
        integer(c_int32_t)        :: afh_mg_fas_vcycle
      end function afh_mg_fas_vcycle
 
+     !> mg_fas_fmg (m_af_multigrid.f90:137-180)
+     function afh_mg_fas_fmg(mg, set_residual, have_guess) &
+          bind(C, name=afh_pfx//"mg_fas_fmg")
+       import
+       type(c_ptr), value        :: mg
+       integer(c_int32_t), value :: set_residual, have_guess
+       integer(c_int32_t)        :: afh_mg_fas_fmg
+     end function afh_mg_fas_fmg
+
+     !> af_tree_sum_cc (m_af_utils.f90:966-1026)
+     function afh_tree_sum_cc(t, iv, power, out) bind(C, name=afh_pfx//"tree_sum_cc")
+       import
+       type(c_ptr), value          :: t
+       integer(c_int32_t), value   :: iv, power
+       real(c_double), intent(out) :: out
+       integer(c_int32_t)          :: afh_tree_sum_cc
+     end function afh_tree_sum_cc
+
+     !> af_tree_max_cc / min_cc / maxabs_cc with location (af_reduction_loc,
+     !> m_af_utils.f90:694-874); loc = [id, i, j, k]
+     function afh_tree_reduce_loc(t, iv, op, out, loc) &
+          bind(C, name=afh_pfx//"tree_reduce_loc")
+       import
+       type(c_ptr), value              :: t
+       integer(c_int32_t), value       :: iv, op
+       real(c_double), intent(out)     :: out
+       integer(c_int32_t), intent(out) :: loc(4)
+       integer(c_int32_t)              :: afh_tree_reduce_loc
+     end function afh_tree_reduce_loc
+
      !> mg_fas_vcycle(set_residual) + af_tree_maxabs_cc(i_tmp), fused
      function afh_mg_fas_vcycle_maxres(mg, highest_lvl, max_res) &
           bind(C, name=afh_pfx//"mg_fas_vcycle_maxres")
@@ -425,6 +461,91 @@ module m_afivo_hip
        real(c_double), intent(out) :: max_rhs
        integer(c_int32_t)        :: afh_fluid_rhs_maxabs
      end function afh_fluid_rhs_maxabs
+
+     !> 1 when the rhs of state s_out from the last update is current
+     function afh_fluid_rhs_valid(f, s_out, valid) bind(C, name=afh_pfx//"fluid_rhs_valid")
+       import
+       type(c_ptr), value              :: f
+       integer(c_int32_t), value       :: s_out
+       integer(c_int32_t), intent(out) :: valid
+       integer(c_int32_t)              :: afh_fluid_rhs_valid
+     end function afh_fluid_rhs_valid
+
+     !> photoi_set_src, Zheleznyak source (src/m_photoi.f90:140-186)
+     function afh_photoi_set_src(f, i_rhs, alpha_col, coeff) &
+          bind(C, name=afh_pfx//"photoi_set_src")
+       import
+       type(c_ptr), value        :: f
+       integer(c_int32_t), value :: i_rhs, alpha_col
+       real(c_double), value     :: coeff
+       integer(c_int32_t)        :: afh_photoi_set_src
+     end function afh_photoi_set_src
+
+     !> photoi_helmh_compute (src/m_photoi_helmh.f90:162-204); modes: the
+     !> Helmholtz multigrid handles, one per mode
+     function afh_photoi_helmh_compute(modes, n_modes, coeffs, i_photo, max_rel_res, &
+          max_fmg, n_fmg) bind(C, name=afh_pfx//"photoi_helmh_compute")
+       import
+       type(c_ptr), intent(in)         :: modes(*)
+       integer(c_int32_t), value       :: n_modes, i_photo, max_fmg
+       real(c_double), intent(in)      :: coeffs(*)
+       real(c_double), value           :: max_rel_res
+       integer(c_int32_t), intent(out) :: n_fmg
+       integer(c_int32_t)              :: afh_photoi_helmh_compute
+     end function afh_photoi_helmh_compute
+
+     !> order the tree's device work on a caller-owned HIP stream
+     function afh_tree_set_stream(t, stream) bind(C, name=afh_pfx//"tree_set_stream")
+       import
+       type(c_ptr), value :: t, stream
+       integer(c_int32_t) :: afh_tree_set_stream
+     end function afh_tree_set_stream
+
+     !> exchange hook of a sharded tree (afh_hook_fn: a bind(C) function
+     !> (ctx, kind, level, iv, vals, n) -> int32)
+     function afh_tree_set_hook(t, fn, ctx) bind(C, name=afh_pfx//"tree_set_hook")
+       import
+       type(c_ptr), value    :: t, ctx
+       type(c_funptr), value :: fn
+       integer(c_int32_t)    :: afh_tree_set_hook
+     end function afh_tree_set_hook
+
+     !> region plans for exchanges: n x 7 (cc) / n x 8 (fc) int32 regions
+     function afh_plan_create(t, regions, n, plan, n_values) &
+          bind(C, name=afh_pfx//"plan_create")
+       import
+       type(c_ptr), value              :: t
+       integer(c_int32_t), intent(in)  :: regions(*)
+       integer(c_int32_t), value       :: n
+       integer(c_int32_t), intent(out) :: plan
+       integer(c_int64_t), intent(out) :: n_values
+       integer(c_int32_t)              :: afh_plan_create
+     end function afh_plan_create
+
+     function afh_plan_create_fc(t, regions, n, plan, n_values) &
+          bind(C, name=afh_pfx//"plan_create_fc")
+       import
+       type(c_ptr), value              :: t
+       integer(c_int32_t), intent(in)  :: regions(*)
+       integer(c_int32_t), value       :: n
+       integer(c_int32_t), intent(out) :: plan
+       integer(c_int64_t), intent(out) :: n_values
+       integer(c_int32_t)              :: afh_plan_create_fc
+     end function afh_plan_create_fc
+
+     function afh_plan_pack(t, plan, iv, buf) bind(C, name=afh_pfx//"plan_pack")
+       import
+       type(c_ptr), value        :: t, buf
+       integer(c_int32_t), value :: plan, iv
+       integer(c_int32_t)        :: afh_plan_pack
+     end function afh_plan_pack
+
+     function afh_plan_unpack(t, plan, iv, buf) bind(C, name=afh_pfx//"plan_unpack")
+       import
+       type(c_ptr), value        :: t, buf
+       integer(c_int32_t), value :: plan, iv
+       integer(c_int32_t)        :: afh_plan_unpack
+     end function afh_plan_unpack
 
      !> electrode_species_bc (src/streamer.f90:578-636) over the mg_lsf_box boxes
      function afh_electrode_species_bc(f, i_lsf, i_1pos_ion, neumann_zero, n_ids, ids) &

@@ -7,13 +7,17 @@
 !> state: by the reference afivo routines (with the m_fluid callbacks restated
 !> in oracle/harness/hx_physics.f90), and through the shim
 !> (afh_field_set_rhs, afh_mg_compute_phi_gradient + afh_gc_tree,
-!> afh_flux_upwind_tree, afh_flux_update_densities). The device results are
-!> downloaded into the afivo boxes' layout and must be bitwise equal.
+!> afh_flux_upwind_tree, afh_flux_update_densities, the tree reductions). The
+!> device results are downloaded into the afivo boxes' layout and must be
+!> bitwise equal. FMG and V-cycle run through the shim as well (dumped and
+!> compared across the two builds, see below).
 !>
 !> Built twice: against libafivo_hip.so (AFH_PFX "afh_", GPU) and against the
 !> C oracle libafo.so (AFH_PFX "afo_", CPU tests).
 !>
-!> Usage: dropin_heun <uni8|amr4> <tables.bin>  prints "DROPIN OK" on success
+!> Usage: dropin_heun <uni8|amr4> <tables.bin> [dump]  prints "DROPIN OK" on
+!> success; with [dump], phi and the residual after an FMG + V-cycle through
+!> the shim are written there (stream, float64, afh_cc_get layout)
 !> (tables.bin: the transport/chemistry tables of the golden fixture, in the
 !> layout of golden_gen's dump_tables; tests/test_dropin.py writes it)
 program dropin_heun
@@ -45,8 +49,10 @@ program dropin_heun
   character(len=256)     :: case_name, td_file
   integer                :: nc, grid(3), max_lvl, amr_lvl, i, iv, n_bad
   real(dp)               :: dom(3), r0(3), width, dt, dtl(4)
-  real(c_double)         :: dl(2), mx_dev
-  real(dp)               :: mx_ref
+  real(c_double)         :: dl(2), mx_dev, s_dev
+  real(dp)               :: mx_ref, s_ref
+  type(af_loc_t)         :: loc_ref
+  character(len=512)     :: dump_file
 
   call get_command_argument(1, case_name)
   call get_command_argument(2, td_file)
@@ -230,6 +236,36 @@ program dropin_heun
      call check_cc(species_itree(i), "species (2)")
   end do
 
+  ! --- tree reductions through the shim against the reference's
+  ! af_tree_sum_cc (to 1e-13: its OpenMP partial sums are thread-order
+  ! dependent) and af_tree_max_cc / min_cc / maxabs_cc with location
+  ! (m_af_utils.f90:758-1026), on the species state both now hold
+  do i = 1, 2
+     call af_tree_sum_cc(tree, i_e, s_ref, i)
+     call afh_check(afh_tree_sum_cc(t, int(i_e, c_int32_t), int(i, c_int32_t), &
+          s_dev), "sum_cc")
+     write(*, '(A,I0,2ES24.16)') "  sum_cc power ", i, s_ref, s_dev
+     if (abs(s_ref - s_dev) > 1e-13_dp * abs(s_ref)) n_bad = n_bad + 1
+  end do
+  call af_tree_max_cc(tree, i_pos, mx_ref, loc_ref)
+  call check_loc(AFH_RED_MAX, i_pos, "max_cc")
+  call af_tree_min_cc(tree, i_neg, mx_ref, loc_ref)
+  call check_loc(AFH_RED_MIN, i_neg, "min_cc")
+  call af_tree_maxabs_cc(tree, i_e, mx_ref, loc_ref)
+  call check_loc(AFH_RED_MAXABS, i_e, "maxabs_cc")
+
+  ! --- FAS-FMG and a V-cycle through the shim (m_af_multigrid.f90:137-264).
+  ! The reference's own V-cycle calls HYPRE (absent), so phi and the
+  ! residual are written to argument 3 and tests/test_dropin.py compares the
+  ! oracle-bound and the device-bound builds.
+  if (command_argument_count() >= 3) then
+     call get_command_argument(3, dump_file)
+     call afh_check(afh_field_set_rhs(fl, int(i_rhs, c_int32_t), 0_c_int32_t), "set_rhs")
+     call afh_check(afh_mg_fas_fmg(dmg, 1_c_int32_t, 1_c_int32_t), "fmg")
+     call afh_check(afh_mg_fas_vcycle(dmg, 1_c_int32_t, 0_c_int32_t), "vcycle")
+     call dump_cc([i_phi, i_tmp])
+  end if
+
   call afh_check(afh_fluid_destroy(fl), "fluid_destroy")
   call afh_check(afh_mg_destroy(dmg), "mg_destroy")
   call afh_check(afh_tree_destroy(t), "tree_destroy")
@@ -292,6 +328,31 @@ contains
     write(*, '(A,A,A,ES10.3)') "  ", what, " max|diff| = ", d
     if (d /= 0) n_bad = n_bad + 1
   end subroutine check_fc
+
+  subroutine check_loc(op, iv, what)
+    integer(c_int32_t), intent(in) :: op
+    integer, intent(in)            :: iv
+    character(len=*), intent(in)   :: what
+    integer(c_int32_t)             :: dloc(4)
+    call afh_check(afh_tree_reduce_loc(t, int(iv, c_int32_t), op, mx_dev, dloc), what)
+    write(*, '(A,A,2ES24.16,8I5)') "  ", what, mx_ref, mx_dev, loc_ref%id, loc_ref%ix, dloc
+    if (mx_ref /= mx_dev .or. loc_ref%id /= dloc(1) .or. &
+         any(loc_ref%ix /= dloc(2:4))) n_bad = n_bad + 1
+  end subroutine check_loc
+
+  subroutine dump_cc(ivs)
+    integer, intent(in)         :: ivs(:)
+    real(c_double), allocatable :: buf(:, :, :, :)
+    integer                     :: u, n
+    allocate(buf(nc+2, nc+2, nc+2, tree%highest_id))
+    open(newunit=u, file=trim(dump_file), access="stream", form="unformatted", &
+         status="replace")
+    do n = 1, size(ivs)
+       call afh_check(afh_cc_get(t, int(ivs(n), c_int32_t), buf), "cc_get")
+       write(u) buf
+    end do
+    close(u)
+  end subroutine dump_cc
 
   subroutine check_dt(a, b, what)
     real(dp), intent(in)         :: a(:), b(:)

@@ -41,18 +41,25 @@ def _run(variant, case, tmp_path):
     if not os.path.exists(exe):
         pytest.skip("drop-in driver not built (oracle/Makefile dropin needs "
                     "the reference sources)")
-    out = subprocess.run([exe, case, _tables(tmp_path)], capture_output=True,
-                         text=True, timeout=300)
+    dump = str(tmp_path / ("mg_%s.bin" % variant))
+    out = subprocess.run([exe, case, _tables(tmp_path), dump], capture_output=True,
+                         text=True, timeout=300, env=dict(os.environ, OMP_NUM_THREADS="4"))
     assert out.returncode == 0 and "DROPIN OK" in out.stdout, out.stdout + out.stderr
-    return out.stdout
+    return out.stdout, np.fromfile(dump, np.float64)
 
 
 @pytest.mark.parametrize("case", ["uni8", "amr4"])
 def test_dropin_oracle(case, tmp_path):
-    _run("afo", case, tmp_path)
+    _, mg = _run("afo", case, tmp_path)
+    assert mg.size and np.all(np.isfinite(mg))
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", ["uni8", "amr4"])
 def test_dropin_hip(case, tmp_path):
-    _run("afh", case, tmp_path)
+    """The device-bound build: every stage bitwise against the reference
+    routines, and FMG + V-cycle through the shim bitwise equal to the
+    oracle-bound build's (the oracle build runs on the host CPU)."""
+    _, mg = _run("afh", case, tmp_path)
+    _, ref = _run("afo", case, tmp_path)
+    assert np.array_equal(mg, ref)
