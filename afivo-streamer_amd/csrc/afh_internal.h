@@ -117,6 +117,9 @@ struct afh_tree {
   // write generation of every cc variable, bumped by the public calls that
   // may change it (afh_fluid_rhs_valid: is a fused rhs still current?)
   std::vector<uint64_t> gen;
+  // bumped by afh_set_cc_methods / afh_set_cc_prolong: graphs captured with
+  // the old boundary values are replayed no more
+  uint64_t meth_gen = 0;
   void touch(int iv) {
     if (iv >= 0 && iv < (int)gen.size()) gen[iv]++;
   }

@@ -17,6 +17,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <map>
 
 #include "afh_internal.h"
 
@@ -1760,6 +1761,15 @@ struct afh_mg {
   int *d_lsf_n = nullptr;
   int i_lsf = 0;
   bool var_dirty = false, any_var = false, any_lsf = false;
+  // V-cycles captured as hipGraphs (launch amortisation), one per (highest
+  // level, set_residual, max|res|) variant; AFH_GRAPHS=0 disables them
+  struct Graph {
+    hipGraphExec_t exec = nullptr;
+    uint64_t meth_gen = 0;
+    bool warm = false;  // one eager call done (tables built, spare image allocated)
+  };
+  std::map<int, Graph> graphs;
+  bool use_graphs = true;
   std::vector<char> lvl_var;  // level has variable-stencil boxes
   LevelList ids_c, ids_v, leaves_c, leaves_v, parents_c, parents_v, lsf_leaves;
   double *cs_old = nullptr;   // level-1 electrode solve: previous phi
@@ -1942,6 +1952,7 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
   if (const char *env = getenv("AFH_GSRB_PAIR_FR")) mg->pair_fr = atoi(env) != 0;
   if (const char *env = getenv("AFH_GSRB_PAIR_P3")) mg->pair_p3 = atoi(env) != 0;
   if (const char *env = getenv("AFH_GSRB_PAIR_SP")) mg->pair_sp = atoi(env) != 0;
+  if (const char *env = getenv("AFH_GRAPHS")) mg->use_graphs = atoi(env) != 0;
   if (const char *env = getenv("AFH_CS_WAVE_CELLS")) mg->wave_cells = atoi(env);
   if (fused_nc_ok(t->nc) && mg->fused_min > 0) {
     bool any = false;
@@ -1980,6 +1991,8 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
 int32_t afh_mg_destroy(afh_mg *mg) {
   if (!mg) return AFH_OK;
   hipStreamSynchronize(mg->t->stream);
+  for (auto &g : mg->graphs)
+    if (g.second.exec) hipGraphExecDestroy(g.second.exec);
   for (int q = 0; q < mg->P.n_mg; q++) {
     hipFree(mg->P.u[q]);
     hipFree(mg->P.f[q]);
@@ -2106,6 +2119,9 @@ static bool fused_level(const afh_mg *mg, int lvl) {
 static int32_t prepare_var(afh_mg *mg) {
   if (!mg->var_dirty) return AFH_OK;
   mg->var_dirty = false;
+  for (auto &g : mg->graphs)
+    if (g.second.exec) hipGraphExecDestroy(g.second.exec);
+  mg->graphs.clear();
   afh_tree *t = mg->t;
   const int nb = t->nb, nl = t->nlvl;
   auto table = [&](auto **d, const auto &h) -> int32_t {
@@ -2465,7 +2481,8 @@ int32_t afh_mg_fas_fmg(afh_mg *mg, int32_t set_residual, int32_t have_guess) {
 
 // residual on every box of levels 1..max_lvl; with max_out also the leaf
 // max|residual| (reduction slot 3, as afh_tree_maxabs_cc), in the same pass
-static int32_t residual_levels(afh_mg *mg, int max_lvl, double *max_out) {
+// (device work only; residual_fetch reads the maximum)
+static int32_t residual_levels(afh_mg *mg, int max_lvl, bool max_out) {
   afh_tree *t = mg->t;
   const int nc = t->nc, n3 = nc * nc * nc;
   auto *red = reinterpret_cast<unsigned long long *>(t->scratch) + 3 * RED_SHARDS;
@@ -2505,8 +2522,71 @@ static int32_t residual_levels(afh_mg *mg, int max_lvl, double *max_out) {
     }
   }
   if (!max_out) return AFH_OK;
-  if ((e = red_finish(t, 3, true)) || (e = red_fetch(t, 3, 1, max_out))) return e;
-  return call_hook(t, AFH_HOOK_MAX, 0, mg->d.i_tmp, max_out, 1);
+  return red_finish(t, 3, true);
+}
+
+static int32_t residual_fetch(afh_mg *mg, double *max_out) {
+  int32_t e;
+  if ((e = red_fetch(mg->t, 3, 1, max_out))) return e;
+  return call_hook(mg->t, AFH_HOOK_MAX, 0, mg->d.i_tmp, max_out, 1);
+}
+
+// the device work of one V-cycle (everything but reading max|res|)
+static int32_t vcycle_body(afh_mg *mg, int32_t set_residual, int max_lvl, bool max_out) {
+  afh_tree *t = mg->t;
+  int32_t e;
+  for (int lvl = max_lvl; lvl >= 2; lvl--) {
+    if ((e = gsrb_boxes(mg, lvl, false))) return e;
+    if ((e = update_coarse(mg, lvl))) return e;
+  }
+  if ((e = solve_coarse(mg))) return e;
+  for (int lvl = 2; lvl <= max_lvl; lvl++) {
+    if ((e = correct_children(mg, lvl))) return e;
+    if ((e = gc_lvl(t, lvl, mg->d.i_phi, 1, fused_level(mg, lvl)))) return e;
+    if ((e = gsrb_boxes(mg, lvl, true))) return e;
+  }
+  if (set_residual) return residual_levels(mg, max_lvl, max_out);
+  return AFH_OK;
+}
+
+// Replays a captured V-cycle when it can: no sharding hook (its collectives
+// run on the host), no kernel timing, no electrode coarse solve (it reads
+// the device every pair). The first call of a variant runs eagerly (tables,
+// spare image); a change of boundary conditions drops the graph.
+static int32_t vcycle_graph(afh_mg *mg, int32_t set_residual, int max_lvl, bool max_out,
+                            bool &done) {
+  afh_tree *t = mg->t;
+  done = false;
+  if (!mg->use_graphs || t->hook || t->prof_class || (mg->any_var && mg->lvl_var[0]))
+    return AFH_OK;
+  const int key = (max_lvl << 2) | (set_residual ? 2 : 0) | (max_out ? 1 : 0);
+  afh_mg::Graph &g = mg->graphs[key];
+  if (g.exec && g.meth_gen != t->meth_gen) {
+    hipGraphExecDestroy(g.exec);
+    g = afh_mg::Graph();
+  }
+  if (!g.warm) {
+    g.warm = true;
+    return AFH_OK;  // this call runs eagerly
+  }
+  if (!g.exec) {
+    hipGraph_t graph;
+    AFH_HIP(hipStreamBeginCapture(t->stream, hipStreamCaptureModeThreadLocal));
+    const int32_t e = vcycle_body(mg, set_residual, max_lvl, max_out);
+    const hipError_t ce = hipStreamEndCapture(t->stream, &graph);
+    if (e) {
+      if (ce == hipSuccess) hipGraphDestroy(graph);
+      return e;
+    }
+    AFH_HIP(ce);
+    const hipError_t ie = hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0);
+    hipGraphDestroy(graph);
+    AFH_HIP(ie);
+    g.meth_gen = t->meth_gen;
+  }
+  AFH_HIP(hipGraphLaunch(g.exec, t->stream));
+  done = true;
+  return AFH_OK;
 }
 
 static int32_t vcycle_impl(afh_mg *mg, int32_t set_residual, int32_t hl,
@@ -2518,18 +2598,11 @@ static int32_t vcycle_impl(afh_mg *mg, int32_t set_residual, int32_t hl,
   const int max_lvl = (hl > 0 && hl <= t->nlvl) ? hl : t->nlvl;
   int32_t e;
   if ((e = prepare_var(mg))) return e;
-  for (int lvl = max_lvl; lvl >= 2; lvl--) {
-    if ((e = gsrb_boxes(mg, lvl, false))) return e;
-    if ((e = update_coarse(mg, lvl))) return e;
-  }
-  if ((e = solve_coarse(mg))) return e;
-  for (int lvl = 2; lvl <= max_lvl; lvl++) {
-    if ((e = correct_children(mg, lvl))) return e;
-    if ((e = gc_lvl(t, lvl, mg->d.i_phi, 1, fused_level(mg, lvl)))) return e;
-    if ((e = gsrb_boxes(mg, lvl, true))) return e;
-  }
-  if (set_residual) return residual_levels(mg, max_lvl, max_res);
-  return AFH_OK;
+  bool done;
+  const bool max_out = set_residual && max_res;
+  if ((e = vcycle_graph(mg, set_residual, max_lvl, max_out, done))) return e;
+  if (!done && (e = vcycle_body(mg, set_residual, max_lvl, max_out))) return e;
+  return max_out ? residual_fetch(mg, max_res) : AFH_OK;
 }
 
 extern "C" {

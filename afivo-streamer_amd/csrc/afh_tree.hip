@@ -738,6 +738,7 @@ int32_t afh_set_cc_methods(afh_tree *t, int32_t iv, const afh_bc *bc6,
     return set_error(AFH_ERR_UNSUPPORTED, "limiter %d", lim);
   CcMethod &m = t->meth[iv];
   m.set = 1;
+  t->meth_gen++;
   for (int n = 0; n < 6; n++) {
     if (bc6[n].type < AFH_BC_DIRICHLET_COPY || bc6[n].type > AFH_BC_DIRICHLET)
       return set_error(AFH_ERR_UNSUPPORTED, "bc type %d", bc6[n].type);
@@ -1059,6 +1060,7 @@ static int32_t device_list(const std::vector<int32_t> &h, int32_t **d) {
 extern "C" {
 
 int32_t afh_set_cc_prolong(afh_tree *t, int32_t iv, int32_t method, int32_t limiter) {
+  if (t) t->meth_gen++;
   AFH_LIVE(t, "afh_set_cc_prolong");
   if (!t || iv < 1 || iv > t->nvc) return set_error(AFH_ERR_ARG, "bad variable index");
   if (method < AFH_PROLONG_NONE || method > AFH_PROLONG_LIMIT)

@@ -194,8 +194,13 @@ def main():
                          "into the density update (afh_fluid_set_rhs_output)")
     ap.add_argument("--replicas", action="store_true",
                     help="N>1: one independent replica per GPU instead of sharding")
+    ap.add_argument("--graphs", choices=("auto", "on", "off"), default="auto",
+                    help="V-cycles replayed as captured hipGraphs (auto: on for the "
+                         "small-box configs s1 / s3, whose steps are launch-bound)")
     args = ap.parse_args()
 
+    if args.graphs == "off":
+        os.environ["AFH_GRAPHS"] = "0"  # read by afh_mg_create
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -233,10 +238,15 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    # timed region: K steps; the dominant kernel (the fused red+black
+    # timed region: K steps. The dominant kernel (the fused red+black
     # Gauss-Seidel pair on the leaf level) is timed with HIP events on the
-    # tree's stream (afh_profile_*) over the same region
-    lib.call("profile_enable", case.tree.h, capi.PROF_GSRB_PAIR)
+    # tree's stream (afh_profile_*) over the same region -- unless V-cycles
+    # are replayed as hipGraphs (kernel timing needs eager launches): then
+    # over two eager unit steps right after the timed region
+    import ctypes as C
+    graphs = args.graphs == "on" or (args.graphs == "auto" and args.config != "s1-64")
+    if not graphs:
+        lib.call("profile_enable", case.tree.h, capi.PROF_GSRB_PAIR)
     barrier()
     case.tree.sync()
     t0 = time.perf_counter()
@@ -245,7 +255,11 @@ def main():
     case.tree.sync()
     barrier()
     elapsed = time.perf_counter() - t0
-    import ctypes as C
+    if graphs:
+        lib.call("profile_enable", case.tree.h, capi.PROF_GSRB_PAIR)
+        for k in range(2):
+            unit_step(case, dt, args.warmup + args.steps + k)
+        case.tree.sync()
     ms, nl, by = C.c_double(), C.c_int64(), C.c_double()
     lib.call("profile_read", case.tree.h, C.byref(ms), C.byref(nl), C.byref(by))
 
@@ -279,6 +293,7 @@ def main():
                        "coarse_solve": ("direct" if args.coarse_cycles == 0 else
                                         "mg%d" % args.coarse_cycles),
                        "fused_rhs": "interior" if not args.no_fused_rhs else False,
+                       "vcycle_graphs": graphs,
                        "parallelism": ("box-shard-%d" % world) if sharded else
                        ("replica-per-gpu" if world > 1 else "single-gpu")},
             "roofline": {"bound": "hbm",
@@ -290,7 +305,9 @@ def main():
                          "traffic": pmc_traffic(args.config),
                          "avg_launch_us": avg_s * 1e6,
                          "algorithmic_bytes_per_launch": bytes_per_launch,
-                         "launches": nl.value},
+                         "launches": nl.value,
+                         "timed_over": ("2 eager unit steps after the timed region"
+                                        if graphs else "the timed region")},
             "last_residual": last[0][-1] if last[0] else None,
             # one FAS V(2,2)-cycle per step (SURVEY.md 8(d) reports both)
             "vcycles_per_s": args.steps / elapsed,
