@@ -30,7 +30,7 @@ ALG = {
     "void afh::k_prolong<4>": (20, LEAF),
     "afh::k_corr_tmp": (24, PARENT),
     "afh::k_parent_rhs": (24, PARENT),
-    "void afh::k_gradient_t<64, 4>": (40, LEAF + PARENT + 9 * 64 ** 3),
+    "void afh::k_gradient_t<64, 4>": (40, LEAF),
     "void afh::k_flux_lds<64, 3>": (64 + 192 / 64, LEAF),
     "void afh::k_update<3, false, 1": (8 * 3 * 2 + 32, LEAF),
     "void afh::k_update<3, false, 2": (8 * 3 * 3 + 32, LEAF),
