@@ -719,6 +719,190 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
   if (P3) store_plane(NC, P[NC & 3]);
 }
 
+// Whole-box form of the fused pair for small boxes (NC <= 16): the box, its
+// ghost layer included, sits in LDS ((NC+2)^3 doubles, 47 KB at NC = 16), so
+// the pair is four phases over the whole box -- A all red cells | B the red
+// face ghosts the level fill would produce after the red sweep (same
+// arithmetic as k_gsrb_pair2's B: a same-level neighbour's boundary cell
+// recomputed from its old values, its loads issued at the start; physical
+// and refinement faces through gc_face_nocopy) | C all black cells | the
+// whole block stored contiguously -- instead of a plane march of NC+1 steps
+// with three barriers each, which leaves small boxes latency-bound. The
+// stored ghost cells are rewritten by the level fill after the pair; edge
+// and corner ghosts are src's, unchanged by the pair. Bitwise the split
+// half-sweeps.
+template <int NC>
+struct RbBox {
+  static constexpr int NG = NC + 2, HN = NC / 2;
+  static constexpr int NRED = NC * NC * HN;                  // red cells per box
+  static constexpr int NT = NRED >= 512 ? 512 : (NRED < 64 ? 64 : NRED);
+  static constexpr int RPT = (NRED + NT - 1) / NT;           // red cells per thread
+  static constexpr int NGH = 3 * NC * NC;                    // red face ghosts
+  static constexpr int GPT = (NGH + NT - 1) / NT;            // ghosts per thread
+};
+
+template <int NC>
+__global__ void __launch_bounds__(RbBox<NC>::NT)
+    k_gsrb_pair_box(const double *__restrict__ src, double *__restrict__ dst,
+                    const double *__restrict__ rhs, const double *__restrict__ coarse,
+                    const afh_box_meta *__restrict__ meta,
+                    const int32_t *__restrict__ ids, size_t bsz, Coef cf,
+                    double inv_c1, GcArgs ga) {
+  using G = RbBox<NC>;
+  constexpr int NG = G::NG, HN = G::HN, NT = G::NT, RPT = G::RPT, GPT = G::GPT;
+  constexpr int SK = NG * NG, NB = NG * NG * NG;
+  __shared__ double P[NB];
+  const int tid = threadIdx.x;
+  const int id = ids[xcd_swizzle(blockIdx.x, gridDim.x)];
+  const afh_box_meta &m = meta[id - 1];
+  const int nb1 = m.neighbors[0], nb2 = m.neighbors[1], nb3 = m.neighbors[2],
+            nb4 = m.neighbors[3], nb5 = m.neighbors[4], nb6 = m.neighbors[5];
+  const double dr0 = m.dr[0], dr1 = m.dr[1], dr2 = m.dr[2];
+  auto nbid = [&](int nb) {
+    return nb == 1 ? nb1 : nb == 2 ? nb2 : nb == 3 ? nb3 : nb == 4 ? nb4 : nb == 5 ? nb5 : nb6;
+  };
+  auto bcof = [&](int nb) {
+    afh_bc b;
+    b.type = nb == 1 ? ga.bc[0].type : nb == 2 ? ga.bc[1].type : nb == 3 ? ga.bc[2].type
+           : nb == 4 ? ga.bc[3].type : nb == 5 ? ga.bc[4].type : ga.bc[5].type;
+    b.value = nb == 1 ? ga.bc[0].value : nb == 2 ? ga.bc[1].value : nb == 3 ? ga.bc[2].value
+            : nb == 4 ? ga.bc[3].value : nb == 5 ? ga.bc[4].value : ga.bc[5].value;
+    return b;
+  };
+  const double *x = src + (size_t)(id - 1) * bsz;
+  double *y = dst + (size_t)(id - 1) * bsz;
+  const double *r = rhs + (size_t)(id - 1) * bsz;
+
+  // red cell q of this thread: row (j, k), i = 2 ih + 1 + ((j + k) & 1);
+  // the black cell of the same pair of columns is the other parity
+  auto cell = [&](int q, bool red, int &i, int &j, int &k) {
+    const int rr = tid + NT * q;
+    const int ih = rr % HN, row = rr / HN;
+    j = row % NC + 1;
+    k = row / NC + 1;
+    i = 2 * ih + 1 + (((j + k) & 1) ^ (red ? 0 : 1));
+    return rr < G::NRED;
+  };
+  // face ghost u: face nb = u / (NC^2 / 2) + 1, (a, b) its in-face indices,
+  // red parity
+  auto ghost = [&](int u, int &nb, int p[3]) {
+    const int per = NC * HN;
+    nb = u / per + 1;
+    const int w = u % per, d = (nb - 1) >> 1;
+    const int ta = d == 0 ? 1 : 0, tb = d == 2 ? 1 : 2;
+    const int bb = w / HN + 1, ah = w % HN;
+    p[d] = ((nb - 1) & 1) ? NC + 1 : 0;
+    p[tb] = bb;
+    // red: p[0] + p[1] + p[2] odd
+    p[ta] = 2 * ah + 1 + ((p[d] + bb) & 1);
+  };
+
+  // global loads first: the box image, rhs of the thread's cells, and the
+  // neighbour values of the same-level face ghosts
+  for (int e = tid; e < NB; e += NT) P[e] = x[e];
+  double rR[RPT], rB[RPT];
+#pragma unroll
+  for (int q = 0; q < RPT; q++) {
+    int i, j, k;
+    const bool ok = cell(q, true, i, j, k);
+    rR[q] = ok ? r[(size_t)(k * NG + j) * NG + i] : 0.0;
+    int i2, j2, k2;
+    cell(q, false, i2, j2, k2);
+    rB[q] = ok ? r[(size_t)(k2 * NG + j2) * NG + i2] : 0.0;
+  }
+  double bl[GPT][7];
+  int brep[GPT];
+  bool bpre[GPT];
+#pragma unroll
+  for (int g = 0; g < GPT; g++) {
+    const int u = tid + NT * g;
+    brep[g] = -1;
+    bpre[g] = false;
+#pragma unroll
+    for (int q = 0; q < 7; q++) bl[g][q] = 0.0;
+    if (u < G::NGH) {
+      int nb, p[3];
+      ghost(u, nb, p);
+      const int nid = nbid(nb);
+      if (nid > 0) {
+        const int d = (nb - 1) >> 1;
+        const bool low = ((nb - 1) & 1) == 0;
+        int q3[3] = {p[0], p[1], p[2]};
+        q3[d] = low ? NC : 1;
+        const double *xs = src + (size_t)(nid - 1) * bsz;
+        const size_t c = ix3(NG, q3[0], q3[1], q3[2]);
+        bpre[g] = true;
+        brep[g] = 2 * d + (low ? 1 : 0);
+        bl[g][0] = xs[c - 1];
+        bl[g][1] = xs[c + 1];
+        bl[g][2] = xs[c - NG];
+        bl[g][3] = xs[c + NG];
+        bl[g][4] = xs[c - SK];
+        bl[g][5] = xs[c + SK];
+        bl[g][6] = rhs[(size_t)(nid - 1) * bsz + c];
+      }
+    }
+  }
+  __syncthreads();
+  // A: red cells
+#pragma unroll
+  for (int q = 0; q < RPT; q++) {
+    int i, j, k;
+    if (!cell(q, true, i, j, k)) continue;
+    const int c = (k * NG + j) * NG + i;
+    P[c] = (rR[q] - cf.c[1] * P[c - 1] - cf.c[2] * P[c + 1] - cf.c[3] * P[c - NG] -
+            cf.c[4] * P[c + NG] - cf.c[5] * P[c - SK] - cf.c[6] * P[c + SK]) *
+           inv_c1;
+  }
+  __syncthreads();
+  // B: red face ghosts
+#pragma unroll
+  for (int g = 0; g < GPT; g++) {
+    const int u = tid + NT * g;
+    if (u >= G::NGH) continue;
+    int nb, p[3];
+    ghost(u, nb, p);
+    const int d = (nb - 1) >> 1;
+    const bool low = ((nb - 1) & 1) == 0;
+    int q1[3] = {p[0], p[1], p[2]}, q2[3] = {p[0], p[1], p[2]};
+    q1[d] = low ? 1 : NC;
+    q2[d] = low ? 2 : NC - 1;
+    const double x1v = P[ix3(NG, q1[0], q1[1], q1[2])];  // black, old
+    double v;
+    if (bpre[g]) {
+      double b[7];
+#pragma unroll
+      for (int q = 0; q < 7; q++) b[q] = bl[g][q];
+#pragma unroll
+      for (int q = 0; q < 6; q++)
+        if (q == brep[g]) b[q] = x1v;
+      v = (b[6] - cf.c[1] * b[0] - cf.c[2] * b[1] - cf.c[3] * b[2] - cf.c[4] * b[3] -
+           cf.c[5] * b[4] - cf.c[6] * b[5]) *
+          inv_c1;
+    } else {
+      const double x2v = P[ix3(NG, q2[0], q2[1], q2[2])];  // red, new
+      const int ta = d == 0 ? 1 : 0, tb = d == 2 ? 1 : 2;
+      v = pair_ghost_k<NC>(src, coarse, rhs, meta, m, nb, nbid(nb),
+                           d == 0 ? dr0 : d == 1 ? dr1 : dr2, p[0], p[1], p[2], p[ta],
+                           p[tb], bsz, cf, inv_c1, bcof(nb), ga.rb, x1v, x2v);
+    }
+    P[ix3(NG, p[0], p[1], p[2])] = v;
+  }
+  __syncthreads();
+  // C: black cells
+#pragma unroll
+  for (int q = 0; q < RPT; q++) {
+    int i, j, k;
+    if (!cell(q, false, i, j, k)) continue;
+    const int c = (k * NG + j) * NG + i;
+    P[c] = (rB[q] - cf.c[1] * P[c - 1] - cf.c[2] * P[c + 1] - cf.c[3] * P[c - NG] -
+            cf.c[4] * P[c + NG] - cf.c[5] * P[c - SK] - cf.c[6] * P[c + SK]) *
+           inv_c1;
+  }
+  __syncthreads();
+  for (int e = tid; e < NB; e += NT) y[e] = P[e];
+}
+
 __device__ __forceinline__ double apply7(const double *x, size_t c, size_t sj,
                                          size_t sk, const Coef &cf) {
   return cf.c[0] * x[c] + cf.c[1] * x[c - 1] + cf.c[2] * x[c + 1] +
@@ -1743,6 +1927,7 @@ struct afh_mg {
   bool pair_fr = true;       // AFH_GSRB_PAIR_FR=0: interior-only row stores (NC = 64)
   bool pair_p3 = true;       // AFH_GSRB_PAIR_P3=0: four barriers per plane (NC = 64)
   bool pair_sp = true;       // AFH_GSRB_PAIR_SP=0: natural LDS row order (NC = 64)
+  bool pair_box = true;      // AFH_GSRB_PAIR_BOX=0: plane-marching pair for NC <= 16
   int wave_cells = CS_WAVE_CELLS;  // AFH_CS_WAVE_CELLS
   // AFH_COARSE_DIRECT: eigenvectors Q and Q^T per dim, eigenvalues, work
   double *d_q[3] = {nullptr, nullptr, nullptr}, *d_qt[3] = {nullptr, nullptr, nullptr};
@@ -1953,6 +2138,7 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
   if (const char *env = getenv("AFH_GSRB_PAIR_P3")) mg->pair_p3 = atoi(env) != 0;
   if (const char *env = getenv("AFH_GSRB_PAIR_SP")) mg->pair_sp = atoi(env) != 0;
   if (const char *env = getenv("AFH_GRAPHS")) mg->use_graphs = atoi(env) != 0;
+  if (const char *env = getenv("AFH_GSRB_PAIR_BOX")) mg->pair_box = atoi(env) != 0;
   if (const char *env = getenv("AFH_CS_WAVE_CELLS")) mg->wave_cells = atoi(env);
   if (fused_nc_ok(t->nc) && mg->fused_min > 0) {
     bool any = false;
@@ -2068,6 +2254,14 @@ static void launch_pair(afh_mg *mg, int lvl, const double *src, double *dst,
                         const Coef &cf, double inv_c1, hipEvent_t e0, hipEvent_t e1) {
   afh_tree *t = mg->t;
   if (t->ids.n(lvl) == 0) return;
+  if constexpr (NC <= 16) {
+    if (mg->pair_box) {
+      launch_ev((k_gsrb_pair_box<NC>), e0, e1, dim3(t->ids.n(lvl)), dim3(RbBox<NC>::NT),
+                t->stream, src, dst, t->ccv(mg->d.i_rhs), t->ccv(mg->d.i_phi), t->d_boxes,
+                t->ids.at(lvl), t->bsz, cf, inv_c1, t->gc_args(mg->d.i_phi));
+      return;
+    }
+  }
   if constexpr (NC >= 32) {
     if (pair_tiles(mg, lvl)) {
       if (mg->pair_v1) return launch_pair_t<NC, NC / 4>(mg, lvl, src, dst, cf, inv_c1, e0, e1);

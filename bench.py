@@ -297,9 +297,10 @@ def main():
                        "parallelism": ("box-shard-%d" % world) if sharded else
                        ("replica-per-gpu" if world > 1 else "single-gpu")},
             "roofline": {"bound": "hbm",
-                         "kernel": ("k_gsrb_pair2<%d,%d>" if CONFIGS[args.config][0] >= 16
-                                    else "k_gsrb_pair<%d,%d>") % (CONFIGS[args.config][0],
-                                                                CONFIGS[args.config][0]),
+                         "kernel": ("k_gsrb_pair2<%d,%d>" % (CONFIGS[args.config][0],
+                                                             CONFIGS[args.config][0])
+                                    if CONFIGS[args.config][0] > 16 else
+                                    "k_gsrb_pair_box<%d>" % CONFIGS[args.config][0]),
                          "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": pmc_traffic(args.config),
