@@ -369,8 +369,11 @@ struct RbPar {
 // FR: store plane rows whole, x ghost cells included (one contiguous run per
 // tile plane, no partially written cache lines; the level fill after the
 // pair rewrites every ghost cell of dst)
+// KS: the k planes split into KS chunks, one workgroup each (levels with
+// too few boxes to fill the chip): a chunk recomputes the red cells of the
+// plane below it (as tiles recompute halo rows) and stores its own planes
 template <int NC, int TJ, int DEPTH = 2, int NTM = 0, bool FR = true, bool P3 = true,
-          bool SP = true>
+          bool SP = true, int KS = 1>
 __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
     k_gsrb_pair2(const double *__restrict__ src, double *__restrict__ dst,
                  const double *__restrict__ rhs, const double *__restrict__ coarse,
@@ -392,9 +395,13 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
   };
   auto perm = [&](int e) { return L(e / NG, e % NG); };  // plane entry -> LDS
   const int tid = threadIdx.x;
-  const int wg = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int wgs = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int chunk = wgs % KS, wg = wgs / KS;
   const int id = ids[wg / G::NTILE];
   const int j0 = (wg % G::NTILE) * TJ + 1, j1 = j0 + TJ - 1;
+  constexpr int KC = NC / KS;
+  const int k0 = chunk * KC + 1, k1 = k0 + KC - 1;  // planes this workgroup stores
+  const int s0 = chunk == 0 ? 1 : k0 - 1;            // first step
   const afh_box_meta &m = meta[id - 1];
   // the box's neighbour ids and spacings, wave-uniform, read once: per-lane
   // metadata loads in the loop would wait for the plane prefetch (vmcnt(0))
@@ -432,9 +439,11 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
     return L(j - j0 + 1, i);
   };
 
-  // planes 0..2 -> LDS; rhs of the red cells of plane 1
-  for (int e = tid; e < 3 * PL; e += NT)
-    P[e / PL][perm(e % PL)] = x[(size_t)(e / PL) * SK + t0 + e % PL];
+  // planes s0-1 .. s0+1 -> LDS; rhs of the red cells of plane s0
+  for (int e = tid; e < 3 * PL; e += NT) {
+    const int pl = s0 - 1 + e / PL;
+    P[pl & 3][perm(e % PL)] = x[(size_t)pl * SK + t0 + e % PL];
+  }
   // rhs in registers: rR red cells of plane s, rB black cells of plane s-1,
   // rBn black cells of plane s (step s+1). Both parities of a plane are
   // loaded in the same step (adjacent cells 2 ih + 1, 2 ih + 2 of a row), so
@@ -444,8 +453,9 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
   for (int q = 0; q < RPT; q++) {
     const int rr = tid + NT * q;
     const int j = j0 + rr / HN, i1 = 2 * (rr % HN) + 1;
-    const double lo = r[SK + (size_t)j * NG + i1], hi = r[SK + (size_t)j * NG + i1 + 1];
-    const bool odd = (j + 1) & 1;  // red cell of plane 1 is i1 + 1
+    const double lo = r[(size_t)s0 * SK + (size_t)j * NG + i1],
+                 hi = r[(size_t)s0 * SK + (size_t)j * NG + i1 + 1];
+    const bool odd = (j + s0) & 1;  // red cell of plane s0 is i1 + 1
     rR[q] = odd ? hi : lo;
     rBn[q] = odd ? lo : hi;
     rB[q] = 0.0;
@@ -474,7 +484,7 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
     b.pre = b.lm = b.lp = b.zm = b.zp = false;
     b.xs = b.rs = nullptr;
     b.c = 0;
-    if (s <= NC && tid < TJ + NC) {
+    if (s >= k0 && s <= k1 && tid < TJ + NC) {
       const int u = tid;
       if (u < TJ) {
         b.j = j0 + u;
@@ -527,7 +537,7 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
     BIn b;
 #pragma unroll
     for (int q = 0; q < 7; q++) b.bl[q] = 0.0;
-    if (s <= NC && tid < TJ + NC) {
+    if (s >= k0 && s <= k1 && tid < TJ + NC) {
       // values taken from LDS or replaced later re-read cell c (no extra
       // cache line)
       const double *xs = d.pre ? d.xs : x, *rs = d.pre ? d.rs : r;
@@ -546,7 +556,7 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
     }
     return b;
   };
-  BIn bc = load_b(1);
+  BIn bc = load_b(s0);
   // phi planes and rhs rows in flight: loaded in step s, consumed (LDS /
   // rotation) in step s+1 -- two planes of each per workgroup in flight
   struct Pf {
@@ -571,7 +581,7 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
     }
   };
   Pf X0, X1;
-  if (DEPTH == 2) load_pf(X0, 3);
+  if (DEPTH == 2) load_pf(X0, s0 + 2);
 
   // E: plane k of the tile to dst (in full rows with FR)
   auto store_plane = [&](const int k, const double *Pk) {
@@ -619,7 +629,7 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
                 inv_c1;
       }
     }
-    if (P3 && s >= 3) store_plane(s - 2, Pmm);
+    if (P3 && s - 2 >= k0 && s - 2 < k1) store_plane(s - 2, Pmm);
     __syncthreads();
     // B: red values around the tile: x ghost cells of its rows; the halo
     // rows (ghost row of the box, or the red cells of the adjacent tile
@@ -675,7 +685,7 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
     }
     if (!P3) __syncthreads();
     // C: black cells of plane s-1, in place
-    if (s >= 2) {
+    if (s - 1 >= k0 && s - 1 <= k1) {
 #pragma unroll
       for (int q = 0; q < RPT; q++) {
         int i, j;
@@ -689,8 +699,8 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
     }
     __syncthreads();
     // E (without P3): plane s-1; D: plane s+2 into the slot of plane s-2
-    if (!P3 && s >= 2) store_plane(s - 1, Pm);
-    if (s + 2 <= NC + 1) {
+    if (!P3 && s - 1 >= k0 && s - 1 <= k1) store_plane(s - 1, Pm);
+    if (s + 2 <= NC + 1 && s + 2 <= k1 + 2) {
 #pragma unroll
       for (int e = 0; e < EPT; e++) {
         const int xx = tid + NT * e;
@@ -709,14 +719,14 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
     __syncthreads();
   };
   if (DEPTH == 1) {
-    for (int s = 1; s <= NC + 1; s++) step(s, X0, X0);
+    for (int s = s0; s <= k1 + 1; s++) step(s, X0, X0);
   } else {
-    for (int s = 1; s <= NC + 1; s += 2) {
+    for (int s = s0; s <= k1 + 1; s += 2) {
       step(s, X1, X0);
-      if (s + 1 <= NC + 1) step(s + 1, X0, X1);
+      if (s + 1 <= k1 + 1) step(s + 1, X0, X1);
     }
   }
-  if (P3) store_plane(NC, P[NC & 3]);
+  if (P3) store_plane(k1, P[k1 & 3]);
 }
 
 // Whole-box form of the fused pair for small boxes (NC <= 16): the box, its
@@ -1928,6 +1938,8 @@ struct afh_mg {
   bool pair_p3 = true;       // AFH_GSRB_PAIR_P3=0: four barriers per plane (NC = 64)
   bool pair_sp = true;       // AFH_GSRB_PAIR_SP=0: natural LDS row order (NC = 64)
   bool pair_box = true;      // AFH_GSRB_PAIR_BOX=0: plane-marching pair for NC <= 16
+  int pair_ks = 4;           // AFH_GSRB_PAIR_KS: k chunks on 64..255-box levels (NC = 64;
+                             // 4 whole-box chunks, 44 quarter-box tiles x 4, 0 tiles)
   int wave_cells = CS_WAVE_CELLS;  // AFH_CS_WAVE_CELLS
   // AFH_COARSE_DIRECT: eigenvectors Q and Q^T per dim, eigenvalues, work
   double *d_q[3] = {nullptr, nullptr, nullptr}, *d_qt[3] = {nullptr, nullptr, nullptr};
@@ -2139,6 +2151,7 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
   if (const char *env = getenv("AFH_GSRB_PAIR_SP")) mg->pair_sp = atoi(env) != 0;
   if (const char *env = getenv("AFH_GRAPHS")) mg->use_graphs = atoi(env) != 0;
   if (const char *env = getenv("AFH_GSRB_PAIR_BOX")) mg->pair_box = atoi(env) != 0;
+  if (const char *env = getenv("AFH_GSRB_PAIR_KS")) mg->pair_ks = atoi(env);
   if (const char *env = getenv("AFH_CS_WAVE_CELLS")) mg->wave_cells = atoi(env);
   if (fused_nc_ok(t->nc) && mg->fused_min > 0) {
     bool any = false;
@@ -2238,12 +2251,12 @@ static bool pair_tiles(const afh_mg *mg, int lvl) {
 }
 
 template <int NC, int TJ, int DEPTH, int NTM = 0, bool FR = true, bool P3 = true,
-          bool SP = true>
+          bool SP = true, int KS = 1>
 static void launch_pair2(afh_mg *mg, int lvl, const double *src, double *dst,
                          const Coef &cf, double inv_c1, hipEvent_t e0, hipEvent_t e1) {
   afh_tree *t = mg->t;
-  launch_ev((k_gsrb_pair2<NC, TJ, DEPTH, NTM, FR, P3, SP>), e0, e1,
-            dim3(t->ids.n(lvl) * RbPar<NC, TJ, NTM>::NTILE),
+  launch_ev((k_gsrb_pair2<NC, TJ, DEPTH, NTM, FR, P3, SP, KS>), e0, e1,
+            dim3(t->ids.n(lvl) * RbPar<NC, TJ, NTM>::NTILE * KS),
             dim3(RbPar<NC, TJ, NTM>::NT), t->stream, src, dst, t->ccv(mg->d.i_rhs),
             t->ccv(mg->d.i_phi), t->d_boxes, t->ids.at(lvl), t->bsz, cf, inv_c1,
             t->gc_args(mg->d.i_phi));
@@ -2265,6 +2278,15 @@ static void launch_pair(afh_mg *mg, int lvl, const double *src, double *dst,
   if constexpr (NC >= 32) {
     if (pair_tiles(mg, lvl)) {
       if (mg->pair_v1) return launch_pair_t<NC, NC / 4>(mg, lvl, src, dst, cf, inv_c1, e0, e1);
+      if constexpr (NC == 64) {
+        // too few boxes for the chip: split the march over k
+        if (mg->pair_ks == 4)
+          return launch_pair2<NC, NC, 1, 0, true, true, true, 4>(mg, lvl, src, dst, cf,
+                                                                 inv_c1, e0, e1);
+        if (mg->pair_ks == 44)
+          return launch_pair2<NC, NC / 4, 1, 0, true, true, true, 4>(mg, lvl, src, dst, cf,
+                                                                     inv_c1, e0, e1);
+      }
       return launch_pair2<NC, NC / 4, 2>(mg, lvl, src, dst, cf, inv_c1, e0, e1);
     }
   }
