@@ -175,7 +175,20 @@ SIGNATURES = {
     "plan_create_fc": (i32, [_VP, P_i32, i32, P_i32, C.POINTER(C.c_int64)]),
     "plan_pack": (i32, [_VP, i32, i32, _VP]),
     "plan_unpack": (i32, [_VP, i32, i32, _VP]),
+    # native box sharding
+    "dist_partition": (i32, [C.POINTER(TreeDesc), i32, P_i32, P_i32]),
+    "dist_plan": (i32, [C.POINTER(TreeDesc), P_i32, i32, i32, i32, i32, P_i32, i32, P_i32]),
+    "tree_create_sharded": (i32, [C.POINTER(TreeDesc), P_i32, i32, i32, _PVP]),
+    "dist_group_create": (i32, [i32, _PVP]),
+    "dist_group_destroy": (i32, [_VP]),
+    "dist_rccl_unique_id": (i32, [_VP]),
+    "dist_rccl_comm": (i32, [_VP, i32, i32, i32, _PVP]),
+    "dist_rccl_comm_destroy": (i32, [_VP]),
+    "dist_create": (i32, [_VP, C.POINTER(TreeDesc), P_i32, i32, i32, i32, _VP, _PVP]),
+    "dist_destroy": (i32, [_VP]),
+    "dist_stats": (i32, [_VP, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
 }
+DIST_LOCAL, DIST_RCCL = 1, 2
 HOOK_HALO, HOOK_RIMS, HOOK_RESTRICT, HOOK_MAX, HOOK_MIN, HOOK_CFLUX = 1, 2, 3, 4, 5, 6
 HOOK_SUM = 7
 RED_MAX, RED_MIN, RED_MAXABS = 1, 2, 3

@@ -48,6 +48,20 @@ def morton3(ix):
     return code
 
 
+def local_topology(topo, owner, rank):
+    """The topology dict with rank's level lists: its own boxes and the
+    replicated ones (owner -1); what afh_tree_create_sharded builds."""
+    owner = np.asarray(owner)
+    t = dict(topo)
+    for l in range(1, int(topo["highest_lvl"]) + 1):
+        for k in ("ids", "leaves", "parents"):
+            key = "lvl_%s_%d" % (k, l)
+            ids = np.asarray(topo[key], np.int64)
+            o = owner[ids - 1]
+            t[key] = ids[(o == rank) | (o < 0)].astype(np.int32)
+    return t
+
+
 class Partition:
     """Ownership of every box for n_ranks (owner -1: replicated)."""
 
@@ -97,12 +111,7 @@ class Partition:
 
     def local_topology(self, rank):
         """The topology dict with this rank's level lists."""
-        t = dict(self.topo)
-        for l in range(1, self.nlvl + 1):
-            for k in ("ids", "leaves", "parents"):
-                key = "lvl_%s_%d" % (k, l)
-                t[key] = self.owned(rank, np.asarray(self.topo[key], np.int64)).astype(np.int32)
-        return t
+        return local_topology(self.topo, self.owner, rank)
 
     # ---------------------------------------------------------------- plans
     def _region(self, b, d, rims):
@@ -201,6 +210,12 @@ class Shard:
         self.tree = None
         self.plans = {}
         self.n_exchanges = 0
+
+    def make_tree(self, lib, topo, n_var_cell, n_var_face, device=-1, box_capacity=0):
+        """This rank's Tree: storage for the whole tree, its level lists."""
+        from .model import Tree
+        return Tree(lib, self.part.local_topology(self.rank), n_var_cell, n_var_face,
+                    device=device, box_capacity=box_capacity)
 
     def attach(self, tree):
         """Register plans and the hook on a Tree built from local_topology."""
@@ -363,3 +378,110 @@ class Shard:
     def owned_mask(self):
         o = self.part.owner
         return (o == self.rank) | (o < 0)
+
+
+# ---------------------------------------------------------------- native
+class NativeGroup:
+    """afh_dist_group: the ranks of one process sharing a sharded tree
+    (AFH_DIST_LOCAL; one thread per rank)."""
+
+    def __init__(self, lib, n_ranks):
+        self.lib = lib
+        self.n_ranks = n_ranks
+        h = C.c_void_p()
+        lib.call("dist_group_create", n_ranks, C.byref(h))
+        self.h = h
+
+    def close(self):
+        if self.h:
+            self.lib.call("dist_group_destroy", self.h)
+            self.h = C.c_void_p()
+
+
+def rccl_comm(lib, rank, n_ranks, device):
+    """An RCCL communicator for the library's AFH_DIST_RCCL transport; the
+    unique id travels over the torch.distributed process group."""
+    uid = (C.c_uint8 * 128)()
+    if rank == 0:
+        lib.call("dist_rccl_unique_id", C.cast(uid, C.c_void_p))
+    if n_ranks > 1:
+        import torch
+        import torch.distributed as tdist
+        t = torch.tensor(list(uid), dtype=torch.uint8)
+        tdist.broadcast(t, src=0)
+        uid = (C.c_uint8 * 128)(*t.tolist())
+    comm = C.c_void_p()
+    lib.call("dist_rccl_comm", C.cast(uid, C.c_void_p), rank, n_ranks, device, C.byref(comm))
+    return comm
+
+
+class NativeShard:
+    """One rank of a tree sharded by the library itself (afh_dist_*): the
+    partition, the plans and the exchange hook are native; no Python runs
+    during a step. Same interface as Shard (make_tree / attach / detach).
+
+    transport: capi.DIST_LOCAL with `group` (a NativeGroup; ranks are
+    threads of this process) or capi.DIST_RCCL with `comm` (rccl_comm)."""
+
+    def __init__(self, lib, topo, n_ranks, rank, transport=capi.DIST_LOCAL, group=None,
+                 comm=None):
+        from .model import tree_desc
+        self.lib = lib
+        self.topo = topo
+        self.n = n_ranks
+        self.rank = rank
+        self.transport = transport
+        self.link = group.h if transport == capi.DIST_LOCAL else comm
+        self._desc, self._keep = tree_desc(topo, 1, 1)
+        self.owner = np.zeros(int(topo["n_boxes"]), np.int32)
+        lp = C.c_int32()
+        lib.call("dist_partition", C.byref(self._desc), n_ranks,
+                 self.owner.ctypes.data_as(capi.P_i32), C.byref(lp))
+        self.lp = lp.value or None
+        self.tree = None
+        self.h = C.c_void_p()
+
+    def plan(self, kind, level, recv_rank, send_rank):
+        """The regions one exchange moves (afh_dist_plan), n x 7 (x 8 CFLUX)."""
+        n = C.c_int32()
+        pown = self.owner.ctypes.data_as(capi.P_i32)
+        self.lib.call("dist_plan", C.byref(self._desc), pown, kind, level, recv_rank,
+                      send_rank, None, 0, C.byref(n))
+        w = 8 if kind == capi.HOOK_CFLUX else 7
+        out = np.zeros((n.value, w), np.int32)
+        self.lib.call("dist_plan", C.byref(self._desc), pown, kind, level, recv_rank,
+                      send_rank, out.ctypes.data_as(capi.P_i32), n.value, C.byref(n))
+        return out
+
+    def local_topology(self):
+        return local_topology(self.topo, self.owner, self.rank)
+
+    def make_tree(self, lib, topo, n_var_cell, n_var_face, device=-1, box_capacity=0):
+        from .model import Tree
+        return Tree(lib, self.local_topology(), n_var_cell, n_var_face, device=device,
+                    box_capacity=box_capacity, shard_of=(topo, self.owner, self.rank))
+
+    def attach(self, tree):
+        self.tree = tree
+        h = C.c_void_p()
+        self.lib.call("dist_create", tree.h, C.byref(self._desc),
+                      self.owner.ctypes.data_as(capi.P_i32), self.rank, self.n,
+                      self.transport, self.link, C.byref(h))
+        self.h = h
+
+    def detach(self):
+        if self.h:
+            self.lib.call("dist_destroy", self.h)
+            self.h = C.c_void_p()
+
+    def stats(self):
+        n, b = C.c_int64(), C.c_int64()
+        self.lib.call("dist_stats", self.h, C.byref(n), C.byref(b))
+        return n.value, b.value
+
+    @property
+    def n_exchanges(self):
+        return self.stats()[0]
+
+    def owned_mask(self):
+        return (self.owner == self.rank) | (self.owner < 0)

@@ -27,13 +27,39 @@ def _lists(topo, kind):
     return _i32(flat), off
 
 
+def tree_desc(topo, n_var_cell, n_var_face, box_capacity=0):
+    """afh_tree_desc of a topology dict; returns (desc, arrays it points to)."""
+    nb = int(topo["n_boxes"])
+    meta = np.zeros(nb, capi.BOX_META_DTYPE)
+    for k in ("lvl", "ix", "parent", "children", "neighbors", "neighbor_mat", "r_min", "dr"):
+        meta[k] = topo["meta_" + k]
+    lists = {k: _lists(topo, k) for k in ("ids", "leaves", "parents")}
+    d = capi.TreeDesc()
+    d.n_cell, d.n_boxes, d.highest_lvl = int(topo["nc"]), nb, int(topo["highest_lvl"])
+    d.n_var_cell, d.n_var_face = n_var_cell, n_var_face
+    d.coarse_grid_size[:] = [int(x) for x in topo["coarse_grid_size"]]
+    d.periodic[:] = [0, 0, 0]
+    d.r_base[:] = [float(x) for x in topo["r_base"]]
+    d.dr_base[:] = [float(x) for x in topo["dr_base"]]
+    d.boxes = meta.ctypes.data
+    d.box_capacity = int(box_capacity)
+    for k in ("ids", "leaves", "parents"):
+        flat, off = lists[k]
+        setattr(d, "lvl_%s" % k, flat.ctypes.data_as(capi.P_i32))
+        setattr(d, "lvl_%s_off" % k, off.ctypes.data_as(capi.P_i32))
+    return d, (meta, lists)
+
+
 class Tree:
     """af_t: topology + device box pool of n_var_cell / n_var_face variables."""
 
     def __init__(self, lib, topo, n_var_cell, n_var_face, device=-1, _regrid_of=None,
-                 box_capacity=0):
+                 box_capacity=0, shard_of=None):
         """box_capacity: boxes the device pools hold (afivo's box_limit; 0 =
-        the topology's box count); a regrid that fits them works in place."""
+        the topology's box count); a regrid that fits them works in place.
+        shard_of: (full topology, owner, rank) -- the library builds this
+        rank's part of a sharded tree (afh_tree_create_sharded); `topo` is
+        then that rank's view (afh.dist.local_topology)."""
         self.lib = lib
         self.topo = topo
         # multigrid / fluid objects bound to this tree: closed before it, so
@@ -47,33 +73,16 @@ class Tree:
         self.n_var_cell = n_var_cell
         self.n_var_face = n_var_face
         self.box_capacity = int(box_capacity)
-        nb = self.n_boxes
-        meta = np.zeros(nb, capi.BOX_META_DTYPE)
-        meta["lvl"] = topo["meta_lvl"]
-        meta["ix"] = topo["meta_ix"]
-        meta["parent"] = topo["meta_parent"]
-        meta["children"] = topo["meta_children"]
-        meta["neighbors"] = topo["meta_neighbors"]
-        meta["neighbor_mat"] = topo["meta_neighbor_mat"]
-        meta["r_min"] = topo["meta_r_min"]
-        meta["dr"] = topo["meta_dr"]
-        self._meta = meta
-        self._lists = {k: _lists(topo, k) for k in ("ids", "leaves", "parents")}
-        d = capi.TreeDesc()
-        d.n_cell, d.n_boxes, d.highest_lvl = self.nc, nb, self.highest_lvl
-        d.n_var_cell, d.n_var_face = n_var_cell, n_var_face
-        d.coarse_grid_size[:] = [int(x) for x in topo["coarse_grid_size"]]
-        d.periodic[:] = [0, 0, 0]
-        d.r_base[:] = [float(x) for x in topo["r_base"]]
-        d.dr_base[:] = [float(x) for x in topo["dr_base"]]
-        d.boxes = meta.ctypes.data
-        d.box_capacity = self.box_capacity
-        for k in ("ids", "leaves", "parents"):
-            flat, off = self._lists[k]
-            setattr(d, "lvl_%s" % k, flat.ctypes.data_as(capi.P_i32))
-            setattr(d, "lvl_%s_off" % k, off.ctypes.data_as(capi.P_i32))
+        d, self._keep = tree_desc(topo, n_var_cell, n_var_face, self.box_capacity)
         h = C.c_void_p()
-        if _regrid_of is None:
+        if shard_of is not None:
+            # this rank's boxes of the full tree (afh_tree_create_sharded)
+            full, self._keep_full = tree_desc(shard_of[0], n_var_cell, n_var_face,
+                                              self.box_capacity)
+            owner = np.ascontiguousarray(shard_of[1], np.int32)
+            lib.call("tree_create_sharded", C.byref(full), owner.ctypes.data_as(capi.P_i32),
+                     int(shard_of[2]), device, C.byref(h))
+        elif _regrid_of is None:
             lib.call("tree_create", C.byref(d), device, C.byref(h))
         else:
             lib.call("tree_regrid", _regrid_of.h, C.byref(d), C.byref(h))

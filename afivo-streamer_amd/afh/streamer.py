@@ -57,15 +57,18 @@ class StreamerCase:
     def __init__(self, lib, topo, td, chem, voltage, n_gas=None,
                  coarse_cycles=20, device=-1, shard=None, n_var_cell=N_VAR_CELL,
                  box_capacity=0):
-        """shard: an afh.dist.Shard -- this rank's part of a sharded tree
+        """shard: an afh.dist.Shard or NativeShard -- this rank's part of a sharded tree
         (the tree is created from the rank's level lists and the exchange
         hooks are attached); None for a single-rank tree."""
         self.lib = lib
         self.topo = topo
         self.shard = shard
-        local = shard.part.local_topology(shard.rank) if shard else topo
-        self.tree = Tree(lib, local, n_var_cell, N_VAR_FACE, device=device,
-                         box_capacity=box_capacity)
+        if shard:
+            self.tree = shard.make_tree(lib, topo, n_var_cell, N_VAR_FACE, device=device,
+                                        box_capacity=box_capacity)
+        else:
+            self.tree = Tree(lib, topo, n_var_cell, N_VAR_FACE, device=device,
+                             box_capacity=box_capacity)
         t = self.tree
         neumann0 = [(capi.BC_NEUMANN, 0.0)] * 6
         for sp in ("e", "pos", "neg"):

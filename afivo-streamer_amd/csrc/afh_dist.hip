@@ -1,0 +1,343 @@
+// Native box sharding: the partition, the exchange plans
+// and the exchange hook inside the library, so a driver in any language
+// shards a tree without a collective library of its own.
+//
+// Partition (as afivo-streamer_amd/afh/dist.py states it, the tests compare
+// the two): the partition level Lp is the coarsest level >= 2 with a box per
+// rank; its boxes, in Morton order of box%ix, are cut into contiguous chunks
+// of equal leaf-cell weight; descendants follow their Lp ancestor; levels
+// below Lp are replicated (owner -1).
+//
+// Plans: for every exchange the library's hooks request (HALO / RIMS per
+// level, CFLUX, RESTRICT), the regions this rank sends to and receives from
+// every peer, packed and unpacked by afh_plan_pack / afh_plan_unpack on the
+// tree's stream.
+//
+// Transports: AFH_DIST_LOCAL -- the ranks are threads of one process (one
+// tree each, on one or several GPUs): pack, a group barrier, peer copies of
+// the peers' packed buffers, unpack, a barrier; AFH_DIST_RCCL -- one rank per
+// process: grouped ncclSend / ncclRecv on the tree's stream (no host
+// synchronisation) and ncclAllReduce for the reductions.
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <array>
+#include <cmath>
+#include <condition_variable>
+#include <map>
+#include <mutex>
+#include <set>
+#include <tuple>
+
+#include "afh_internal.h"
+
+using namespace afh;
+
+#include "afh_dist_core.h"
+
+using namespace afhd;
+
+struct afh_dist;
+
+struct afh_dist_group {
+  int n;
+  Barrier bar;
+  std::vector<afh_dist *> rank;
+  std::vector<std::array<double, 16>> vals;
+  explicit afh_dist_group(int n_) : n(n_), bar(n_), rank(n_, nullptr), vals(n_) {}
+};
+
+struct afh_dist {
+  afh_tree *t = nullptr;
+  int rank = 0, n = 1, transport = 0, device = 0;
+  afh_dist_group *group = nullptr;
+  ncclComm_t comm = nullptr;
+  struct Side {
+    int32_t plan = -1;
+    int64_t n = 0;
+    double *buf = nullptr;
+  };
+  struct Plan {
+    std::vector<Side> send, recv;  // per peer
+  };
+  std::map<std::pair<int, int>, Plan> plans;  // (hook kind, level)
+  double *d_red = nullptr;
+  int64_t n_exchanges = 0, bytes = 0;
+};
+
+namespace {
+
+using Key = std::pair<int, int>;  // (hook kind, level)
+
+int32_t exchange(afh_dist *d, const Key &key, int iv) {
+  auto it = d->plans.find(key);
+  if (it == d->plans.end()) return AFH_OK;
+  const afh_dist::Plan &p = it->second;
+  afh_tree *t = d->t;
+  int32_t e = AFH_OK;
+  for (int q = 0; q < d->n && !e; q++)
+    if (p.send[q].n) e = afh_plan_pack(t, p.send[q].plan, iv, p.send[q].buf);
+  if (d->transport == AFH_DIST_RCCL) {
+    if (e) return e;
+    if (ncclGroupStart() != ncclSuccess) return set_error(AFH_ERR_DEVICE, "ncclGroupStart");
+    for (int q = 0; q < d->n && !e; q++) {
+      if (p.send[q].n &&
+          ncclSend(p.send[q].buf, p.send[q].n, ncclDouble, q, d->comm, t->stream) != ncclSuccess)
+        e = set_error(AFH_ERR_DEVICE, "ncclSend");
+      if (!e && p.recv[q].n &&
+          ncclRecv(p.recv[q].buf, p.recv[q].n, ncclDouble, q, d->comm, t->stream) != ncclSuccess)
+        e = set_error(AFH_ERR_DEVICE, "ncclRecv");
+    }
+    if (ncclGroupEnd() != ncclSuccess && !e) e = set_error(AFH_ERR_DEVICE, "ncclGroupEnd");
+    if (e) return e;
+  } else {
+    // every rank's packs complete, then each copies the peers' packed
+    // buffers; nobody packs again before every peer has copied. The
+    // barriers are passed on every path, so a failing rank cannot strand
+    // its peers.
+    if (!e && hipStreamSynchronize(t->stream) != hipSuccess)
+      e = set_error(AFH_ERR_DEVICE, "stream sync");
+    d->group->bar.wait();
+    for (int q = 0; q < d->n && !e; q++) {
+      if (!p.recv[q].n) continue;
+      const afh_dist *peer = d->group->rank[q];
+      const afh_dist::Side &src = peer->plans.at(key).send[d->rank];
+      if (src.n != p.recv[q].n)
+        e = set_error(AFH_ERR_STATE, "exchange %d/%d: rank %d sends %lld values, rank %d "
+                      "expects %lld", key.first, key.second, q, (long long)src.n, d->rank,
+                      (long long)p.recv[q].n);
+      else if (hipMemcpyPeerAsync(p.recv[q].buf, d->device, src.buf, peer->device,
+                                  sizeof(double) * src.n, t->stream) != hipSuccess)
+        e = set_error(AFH_ERR_DEVICE, "peer copy");
+    }
+    if (!e && hipStreamSynchronize(t->stream) != hipSuccess)
+      e = set_error(AFH_ERR_DEVICE, "stream sync");
+    d->group->bar.wait();
+    if (e) return e;
+  }
+  for (int q = 0; q < d->n && !e; q++)
+    if (p.recv[q].n) e = afh_plan_unpack(t, p.recv[q].plan, iv, p.recv[q].buf);
+  if (e) return e;
+  d->n_exchanges++;
+  for (int q = 0; q < d->n; q++) d->bytes += 8 * (p.send[q].n + p.recv[q].n);
+  return AFH_OK;
+}
+
+int32_t reduce(afh_dist *d, int kind, double *vals, int n) {
+  if (n > 16) return set_error(AFH_ERR_ARG, "reduction of %d values", n);
+  if (d->transport == AFH_DIST_RCCL) {
+    afh_tree *t = d->t;
+    const ncclRedOp_t op = kind == AFH_HOOK_MAX ? ncclMax : kind == AFH_HOOK_MIN ? ncclMin : ncclSum;
+    AFH_HIP(hipMemcpyAsync(d->d_red, vals, sizeof(double) * n, hipMemcpyHostToDevice, t->stream));
+    if (ncclAllReduce(d->d_red, d->d_red, n, ncclDouble, op, d->comm, t->stream) != ncclSuccess)
+      return set_error(AFH_ERR_DEVICE, "ncclAllReduce");
+    AFH_HIP(hipMemcpyAsync(vals, d->d_red, sizeof(double) * n, hipMemcpyDeviceToHost, t->stream));
+    AFH_HIP(hipStreamSynchronize(t->stream));
+    return AFH_OK;
+  }
+  afh_dist_group *g = d->group;
+  for (int k = 0; k < n; k++) g->vals[d->rank][k] = vals[k];
+  g->bar.wait();
+  for (int k = 0; k < n; k++) {
+    double v = g->vals[0][k];  // rank order: the same result on every rank
+    for (int q = 1; q < d->n; q++) {
+      const double w = g->vals[q][k];
+      v = kind == AFH_HOOK_MAX ? std::max(v, w) : kind == AFH_HOOK_MIN ? std::min(v, w) : v + w;
+    }
+    vals[k] = v;
+  }
+  g->bar.wait();
+  return AFH_OK;
+}
+
+int32_t dist_hook(void *ctx, int32_t kind, int32_t level, int32_t iv, double *vals, int32_t n) {
+  afh_dist *d = static_cast<afh_dist *>(ctx);
+  switch (kind) {
+  case AFH_HOOK_MAX:
+  case AFH_HOOK_MIN:
+  case AFH_HOOK_SUM: return reduce(d, kind, vals, n);
+  case AFH_HOOK_CFLUX: return exchange(d, Key(kind, 0), iv);
+  default: return exchange(d, Key(kind, level), iv);
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t afh_dist_partition(const afh_tree_desc *desc, int32_t n_ranks, int32_t *owner,
+                           int32_t *lp) {
+  if (!desc || !owner || n_ranks < 1) return set_error(AFH_ERR_ARG, "afh_dist_partition");
+  const Topo t = topo_of(desc);
+  std::vector<int32_t> own;
+  const int l = partition(t, n_ranks, own);
+  if (l < 0) return set_error(AFH_ERR_ARG, "no level >= 2 has %d boxes to shard", n_ranks);
+  std::copy(own.begin(), own.end(), owner);
+  if (lp) *lp = l;
+  return AFH_OK;
+}
+
+int32_t afh_dist_plan(const afh_tree_desc *desc, const int32_t *owner, int32_t kind,
+                      int32_t level, int32_t recv_rank, int32_t send_rank, int32_t *regions,
+                      int32_t cap, int32_t *n) {
+  if (!desc || !owner || !n) return set_error(AFH_ERR_ARG, "afh_dist_plan");
+  const Topo t = topo_of(desc);
+  const std::vector<int32_t> own(owner, owner + t.nb);
+  const auto rs = plan_regions(t, own, first_owned_level(t, owner), kind, level, recv_rank,
+                               send_rank);
+  const int w = kind == AFH_HOOK_CFLUX ? 8 : 7;
+  *n = (int32_t)rs.size();
+  if (regions) {
+    if ((int)rs.size() > cap) return set_error(AFH_ERR_ARG, "afh_dist_plan: %d regions > cap %d",
+                                               (int)rs.size(), cap);
+    for (size_t k = 0; k < rs.size(); k++)
+      for (int c = 0; c < w; c++) regions[k * w + c] = rs[k][c];
+  }
+  return AFH_OK;
+}
+
+int32_t afh_tree_create_sharded(const afh_tree_desc *desc, const int32_t *owner, int32_t rank,
+                                int32_t device, afh_tree **out) {
+  if (!desc || !owner || !out) return set_error(AFH_ERR_ARG, "afh_tree_create_sharded");
+  const Topo t = topo_of(desc);
+  std::vector<int32_t> lists[3], offs[3];
+  const std::vector<std::vector<int32_t>> *src[3] = {&t.ids, &t.leaves, &t.parents};
+  for (int k = 0; k < 3; k++) {
+    offs[k].push_back(0);
+    for (int l = 0; l < t.nlvl; l++) {
+      for (int32_t i : (*src[k])[l])
+        if (owner[i - 1] == rank || owner[i - 1] < 0) lists[k].push_back(i);
+      offs[k].push_back((int32_t)lists[k].size());
+    }
+  }
+  afh_tree_desc d = *desc;
+  d.lvl_ids = lists[0].data(), d.lvl_ids_off = offs[0].data();
+  d.lvl_leaves = lists[1].data(), d.lvl_leaves_off = offs[1].data();
+  d.lvl_parents = lists[2].data(), d.lvl_parents_off = offs[2].data();
+  return afh_tree_create(&d, device, out);
+}
+
+int32_t afh_dist_group_create(int32_t n_ranks, afh_dist_group **out) {
+  if (n_ranks < 1 || !out) return set_error(AFH_ERR_ARG, "afh_dist_group_create");
+  *out = new afh_dist_group(n_ranks);
+  return AFH_OK;
+}
+
+int32_t afh_dist_group_destroy(afh_dist_group *g) {
+  delete g;
+  return AFH_OK;
+}
+
+int32_t afh_dist_rccl_unique_id(void *id) {
+  if (!id) return set_error(AFH_ERR_ARG, "null id");
+  ncclUniqueId u;
+  if (ncclGetUniqueId(&u) != ncclSuccess) return set_error(AFH_ERR_DEVICE, "ncclGetUniqueId");
+  memcpy(id, &u, sizeof(u));
+  return AFH_OK;
+}
+
+int32_t afh_dist_rccl_comm(const void *id, int32_t rank, int32_t n_ranks, int32_t device,
+                           void **comm) {
+  if (!id || !comm) return set_error(AFH_ERR_ARG, "afh_dist_rccl_comm");
+  AFH_HIP(hipSetDevice(device));
+  ncclUniqueId u;
+  memcpy(&u, id, sizeof(u));
+  ncclComm_t c;
+  if (ncclCommInitRank(&c, n_ranks, u, rank) != ncclSuccess)
+    return set_error(AFH_ERR_DEVICE, "ncclCommInitRank");
+  *comm = c;
+  return AFH_OK;
+}
+
+int32_t afh_dist_rccl_comm_destroy(void *comm) {
+  if (comm) ncclCommDestroy(static_cast<ncclComm_t>(comm));
+  return AFH_OK;
+}
+
+int32_t afh_dist_create(afh_tree *t, const afh_tree_desc *desc, const int32_t *owner,
+                        int32_t rank, int32_t n_ranks, int32_t transport, void *group_or_comm,
+                        afh_dist **out) {
+  if (!t || !desc || !owner || !out || rank < 0 || rank >= n_ranks || !group_or_comm)
+    return set_error(AFH_ERR_ARG, "afh_dist_create");
+  AFH_LIVE(t, "afh_dist_create");
+  if (transport != AFH_DIST_LOCAL && transport != AFH_DIST_RCCL)
+    return set_error(AFH_ERR_UNSUPPORTED, "transport %d", transport);
+  const Topo tp = topo_of(desc);
+  if (tp.nb != t->nb || tp.nc != t->nc) return set_error(AFH_ERR_ARG, "topology mismatch");
+  const std::vector<int32_t> own(owner, owner + tp.nb);
+  const int lp = first_owned_level(tp, owner);
+  afh_dist *d = new afh_dist;
+  d->t = t, d->rank = rank, d->n = n_ranks, d->transport = transport;
+  hipGetDevice(&d->device);
+  if (transport == AFH_DIST_LOCAL) {
+    d->group = static_cast<afh_dist_group *>(group_or_comm);
+    if (d->group->n != n_ranks) {
+      delete d;
+      return set_error(AFH_ERR_ARG, "group of %d ranks, n_ranks %d", d->group->n, n_ranks);
+    }
+  } else {
+    d->comm = static_cast<ncclComm_t>(group_or_comm);
+  }
+  auto add = [&](int kind, int level) -> int32_t {
+    afh_dist::Plan p;
+    p.send.resize(n_ranks), p.recv.resize(n_ranks);
+    const bool fc = kind == AFH_HOOK_CFLUX;
+    for (int q = 0; q < n_ranks; q++) {
+      if (q == rank) continue;
+      for (int side = 0; side < 2; side++) {
+        const auto rs = side == 0 ? plan_regions(tp, own, lp, kind, level, q, rank)
+                                  : plan_regions(tp, own, lp, kind, level, rank, q);
+        afh_dist::Side &sd = side == 0 ? p.send[q] : p.recv[q];
+        if (rs.empty()) continue;
+        std::vector<int32_t> flat;
+        for (const Region &r : rs) flat.insert(flat.end(), r.begin(), r.begin() + (fc ? 8 : 7));
+        int32_t e = fc ? afh_plan_create_fc(t, flat.data(), (int32_t)rs.size(), &sd.plan, &sd.n)
+                       : afh_plan_create(t, flat.data(), (int32_t)rs.size(), &sd.plan, &sd.n);
+        if (e) return e;
+        if (sd.n && hipMalloc(&sd.buf, sizeof(double) * sd.n) != hipSuccess)
+          return set_error(AFH_ERR_DEVICE, "exchange buffer");
+      }
+    }
+    d->plans[Key(kind, level)] = std::move(p);
+    return AFH_OK;
+  };
+  int32_t e = AFH_OK;
+  if (lp) {
+    for (int l = lp; l <= tp.nlvl && !e; l++)
+      if (!(e = add(AFH_HOOK_HALO, l))) e = add(AFH_HOOK_RIMS, l);
+    if (!e) e = add(AFH_HOOK_CFLUX, 0);
+    if (!e) e = add(AFH_HOOK_RESTRICT, lp);
+  }
+  if (!e && transport == AFH_DIST_RCCL && hipMalloc(&d->d_red, 16 * sizeof(double)) != hipSuccess)
+    e = set_error(AFH_ERR_DEVICE, "reduction buffer");
+  if (!e) e = afh_tree_set_hook(t, dist_hook, d);
+  if (e) {
+    afh_dist_destroy(d);
+    return e;
+  }
+  if (transport == AFH_DIST_LOCAL) d->group->rank[rank] = d;
+  *out = d;
+  return AFH_OK;
+}
+
+int32_t afh_dist_destroy(afh_dist *d) {
+  if (!d) return AFH_OK;
+  if (d->t && !d->t->retired && d->t->hook_ctx == d) afh_tree_set_hook(d->t, nullptr, nullptr);
+  if (d->t) hipStreamSynchronize(d->t->stream);
+  for (auto &kv : d->plans)
+    for (auto *v : {&kv.second.send, &kv.second.recv})
+      for (auto &sd : *v) hipFree(sd.buf);
+  hipFree(d->d_red);
+  if (d->group && d->group->rank[d->rank] == d) d->group->rank[d->rank] = nullptr;
+  delete d;
+  return AFH_OK;
+}
+
+int32_t afh_dist_stats(afh_dist *d, int64_t *n_exchanges, int64_t *bytes) {
+  if (!d) return set_error(AFH_ERR_ARG, "null dist");
+  if (n_exchanges) *n_exchanges = d->n_exchanges;
+  if (bytes) *bytes = d->bytes;
+  return AFH_OK;
+}
+
+}  // extern "C"

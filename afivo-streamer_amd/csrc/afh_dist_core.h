@@ -1,0 +1,228 @@
+// Native box sharding: the partition and the exchange plans (host code
+// shared by libafivo_hip (afh_dist.hip) and the C oracle's CPU twin
+// (oracle/c/afo_dist.cpp), which runs the same sharded semantics on host
+// buffers). The Python reference these restate: afivo-streamer_amd/afh/dist.py
+// (Partition); tests/test_dist_native.py compares them.
+#pragma once
+#include <stdint.h>
+
+#include <algorithm>
+#include <array>
+#include <cmath>
+#include <condition_variable>
+#include <map>
+#include <mutex>
+#include <set>
+#include <vector>
+
+#include "../../include/afivo_hip.h"
+
+namespace afhd {
+
+using Region = std::array<int32_t, 8>;  // cc: id, lo[3], hi[3] (7 used); fc: id, dim, lo, hi
+
+constexpr int DEPTH = 2;  // halo layers (dist.py DEPTH)
+
+struct Topo {
+  int nc, nb, nlvl;
+  const afh_box_meta *m;
+  std::vector<std::vector<int32_t>> ids, leaves, parents;  // per level 1..nlvl (index l-1)
+};
+
+inline Topo topo_of(const afh_tree_desc *d) {
+  Topo t;
+  t.nc = d->n_cell, t.nb = d->n_boxes, t.nlvl = d->highest_lvl, t.m = d->boxes;
+  auto lists = [&](const int32_t *a, const int32_t *off) {
+    std::vector<std::vector<int32_t>> v(t.nlvl);
+    for (int l = 0; l < t.nlvl; l++) v[l].assign(a + off[l], a + off[l + 1]);
+    return v;
+  };
+  t.ids = lists(d->lvl_ids, d->lvl_ids_off);
+  t.leaves = lists(d->lvl_leaves, d->lvl_leaves_off);
+  t.parents = lists(d->lvl_parents, d->lvl_parents_off);
+  return t;
+}
+
+inline int64_t morton3(const int32_t ix[3]) {
+  int64_t code = 0;
+  for (int b = 0; b < 20; b++)
+    for (int d = 0; d < 3; d++) code |= (int64_t)(((ix[d] - 1) >> b) & 1) << (3 * b + d);
+  return code;
+}
+
+// Partition.__init__ (afh/dist.py)
+inline int partition(const Topo &t, int n, std::vector<int32_t> &owner) {
+  owner.assign(t.nb, -1);
+  if (n <= 1) return 0;
+  int lp = 0;
+  for (int l = 2; l <= t.nlvl; l++)
+    if ((int)t.ids[l - 1].size() >= n) {
+      lp = l;
+      break;
+    }
+  if (!lp) return -1;
+  std::vector<int64_t> w(t.nb + 1, 0);
+  for (int l = t.nlvl; l >= 1; l--)
+    for (int32_t i : t.ids[l - 1]) {
+      const int32_t *ch = t.m[i - 1].children;
+      if (ch[0] == 0) {
+        w[i] = 1;
+      } else {
+        int64_t s = 0;
+        for (int c = 0; c < 8; c++) s += w[ch[c]];
+        w[i] = s;
+      }
+    }
+  std::vector<int32_t> order = t.ids[lp - 1];
+  std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) {
+    return morton3(t.m[a - 1].ix) < morton3(t.m[b - 1].ix);
+  });
+  const int no = (int)order.size();
+  std::vector<int64_t> cum(no);
+  int64_t s = 0;
+  for (int q = 0; q < no; q++) cum[q] = (s += w[order[q]]);
+  const double target = (double)cum[no - 1] / n;
+  std::vector<int64_t> rk(no);
+  for (int q = 0; q < no; q++) {
+    const int64_t r = (int64_t)std::ceil((double)cum[q] / target) - 1;
+    rk[q] = std::min<int64_t>(r, n - 1);
+  }
+  std::set<int64_t> used(rk.begin(), rk.end());
+  if ((int)used.size() < n)
+    for (int q = 0; q < no; q++) rk[q] = ((int64_t)q * n) / no;
+  for (int q = 0; q < no; q++) owner[order[q] - 1] = (int32_t)rk[q];
+  for (int l = lp + 1; l <= t.nlvl; l++)
+    for (int32_t i : t.ids[l - 1]) owner[i - 1] = owner[t.m[i - 1].parent - 1];
+  return lp;
+}
+
+// Partition._region: cells of box b within DEPTH layers, b at direction d
+inline Region region(const Topo &t, int32_t b, const int d[3], bool rims) {
+  Region r{};
+  r[0] = b;
+  for (int k = 0; k < 3; k++) {
+    int lo, hi;
+    if (d[k] < 0)
+      lo = t.nc - DEPTH + 1, hi = rims ? t.nc + 1 : t.nc;
+    else if (d[k] > 0)
+      lo = rims ? 0 : 1, hi = DEPTH;
+    else
+      lo = rims ? 0 : 1, hi = rims ? t.nc + 1 : t.nc;
+    r[1 + k] = lo, r[4 + k] = hi;
+  }
+  return r;
+}
+
+// Partition.halo_regions
+inline std::vector<Region> halo_regions(const Topo &t, const std::vector<int32_t> &owner, int lp,
+                                 int recv, int send, int level, bool rims) {
+  std::vector<Region> out;
+  if (!lp || level < lp) return out;
+  std::set<Region> regs;
+  for (int32_t a : t.ids[level - 1]) {
+    if (owner[a - 1] != recv) continue;
+    for (int dz = -1; dz <= 1; dz++)
+      for (int dy = -1; dy <= 1; dy++)
+        for (int dx = -1; dx <= 1; dx++) {
+          if (!dx && !dy && !dz) continue;
+          const int b = t.m[a - 1].neighbor_mat[(dx + 1) + 3 * (dy + 1) + 9 * (dz + 1)];
+          const int d[3] = {dx, dy, dz};
+          if (b > 0 && owner[b - 1] == send) regs.insert(region(t, b, d, rims));
+        }
+  }
+  std::map<int32_t, std::vector<Region>> by_box;
+  for (const Region &r : regs) by_box[r[0]].push_back(r);
+  for (auto &kv : by_box) {
+    auto &rs = kv.second;
+    std::sort(rs.begin(), rs.end());
+    for (const Region &r : rs) {
+      bool inside = false;
+      for (const Region &q : rs)
+        if (q != r && q[1] <= r[1] && q[2] <= r[2] && q[3] <= r[3] && r[4] <= q[4] &&
+            r[5] <= q[5] && r[6] <= q[6])
+          inside = true;
+      if (!inside) out.push_back(r);
+    }
+  }
+  return out;
+}
+
+// Partition.cflux_regions (8 ints: id, dim, lo, hi; face indices)
+inline std::vector<Region> cflux_regions(const Topo &t, const std::vector<int32_t> &owner, int lp,
+                                  int recv, int send) {
+  std::vector<Region> out;
+  if (!lp) return out;
+  for (int l = 1; l <= t.nlvl; l++)
+    for (int32_t p : t.parents[l - 1]) {
+      if (owner[p - 1] != send) continue;
+      for (int nb = 1; nb <= 6; nb++) {
+        const int q = t.m[p - 1].neighbors[nb - 1];
+        if (q <= 0 || t.m[q - 1].children[0] != 0 || owner[q - 1] != recv) continue;
+        const int d = (nb - 1) / 2;
+        const int f = (nb - 1) % 2 == 0 ? t.nc + 1 : 1;
+        int lo[3] = {1, 1, 1}, hi[3] = {t.nc, t.nc, t.nc};
+        lo[d] = hi[d] = f;
+        out.push_back(Region{q, d, lo[0], lo[1], lo[2], hi[0], hi[1], hi[2]});
+      }
+    }
+  return out;
+}
+
+// Partition.octant_regions: parent octants written by send's boxes of Lp
+inline std::vector<Region> octant_regions(const Topo &t, const std::vector<int32_t> &owner, int lp,
+                                   int send) {
+  std::vector<Region> out;
+  if (!lp) return out;
+  const int h = t.nc / 2;
+  for (int32_t c : t.ids[lp - 1]) {
+    if (owner[c - 1] != send) continue;
+    const afh_box_meta &m = t.m[c - 1];
+    int co[3];
+    for (int k = 0; k < 3; k++) co[k] = ((m.ix[k] - 1) & 1) * h;
+    out.push_back(Region{m.parent, co[0] + 1, co[1] + 1, co[2] + 1, co[0] + h, co[1] + h,
+                         co[2] + h, 0});
+  }
+  return out;
+}
+
+inline std::vector<Region> plan_regions(const Topo &t, const std::vector<int32_t> &owner, int lp,
+                                 int kind, int level, int recv, int send) {
+  switch (kind) {
+  case AFH_HOOK_HALO: return halo_regions(t, owner, lp, recv, send, level, false);
+  case AFH_HOOK_RIMS: return halo_regions(t, owner, lp, recv, send, level, true);
+  case AFH_HOOK_CFLUX: return cflux_regions(t, owner, lp, recv, send);
+  case AFH_HOOK_RESTRICT: return level == lp ? octant_regions(t, owner, lp, send)
+                                             : std::vector<Region>();
+  default: return {};
+  }
+}
+
+// A reusable barrier for the threads of an AFH_DIST_LOCAL group
+struct Barrier {
+  std::mutex mu;
+  std::condition_variable cv;
+  int n, waiting = 0;
+  uint64_t gen = 0;
+  explicit Barrier(int n_) : n(n_) {}
+  void wait() {
+    std::unique_lock<std::mutex> lk(mu);
+    const uint64_t g = gen;
+    if (++waiting == n) {
+      waiting = 0;
+      gen++;
+      cv.notify_all();
+    } else {
+      cv.wait(lk, [&] { return gen != g; });
+    }
+  }
+};
+
+// the partition level: the first level with an owned (non-replicated) box
+inline int first_owned_level(const Topo &t, const int32_t *owner) {
+  for (int l = 1; l <= t.nlvl; l++)
+    for (int32_t i : t.ids[l - 1])
+      if (owner[i - 1] >= 0) return l;
+  return 0;
+}
+
+}  // namespace afhd

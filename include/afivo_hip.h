@@ -523,6 +523,46 @@ int32_t afh_plan_pack(afh_tree *t, int32_t plan, int32_t iv, double *buf);
 int32_t afh_plan_unpack(afh_tree *t, int32_t plan, int32_t iv,
                         const double *buf);
 
+/* ---- Native box sharding -------------------------------
+ * The partition, the exchange plans and the exchange hook inside the library
+ * (the Python hook of afh/dist.py is the reference these restate; the tests
+ * compare them), so a driver in any language shards a tree:
+ *   owner <- afh_dist_partition(full desc, n_ranks)  (box id b: owner[b-1],
+ *            -1 = replicated coarse level, *lp = the partition level)
+ *   afh_tree_create_sharded(full desc, owner, rank, device, &t)  (this
+ *            rank's boxes in the level lists; storage for the whole tree)
+ *   afh_dist_create(t, full desc, owner, rank, n_ranks, transport, x, &d)
+ * Transports: AFH_DIST_LOCAL -- the ranks are threads of one process (one
+ * tree each, on one GPU or several; x = an afh_dist_group shared by the
+ * ranks): pack, group barrier, peer copies, unpack; AFH_DIST_RCCL -- one
+ * rank per process (x = an RCCL communicator, afh_dist_rccl_comm): grouped
+ * ncclSend / ncclRecv on the tree's stream, ncclAllReduce for reductions.
+ * afh_dist_plan returns the regions one exchange moves from send_rank to
+ * recv_rank (n x 7 int32, n x 8 for AFH_HOOK_CFLUX; regions may be null to
+ * query n). */
+#define AFH_DIST_LOCAL 1
+#define AFH_DIST_RCCL 2
+typedef struct afh_dist afh_dist;
+typedef struct afh_dist_group afh_dist_group;
+int32_t afh_dist_partition(const afh_tree_desc *desc, int32_t n_ranks, int32_t *owner,
+                           int32_t *lp);
+int32_t afh_dist_plan(const afh_tree_desc *desc, const int32_t *owner, int32_t kind,
+                      int32_t level, int32_t recv_rank, int32_t send_rank, int32_t *regions,
+                      int32_t cap, int32_t *n);
+int32_t afh_tree_create_sharded(const afh_tree_desc *desc, const int32_t *owner, int32_t rank,
+                                int32_t device, afh_tree **out);
+int32_t afh_dist_group_create(int32_t n_ranks, afh_dist_group **out);
+int32_t afh_dist_group_destroy(afh_dist_group *g);
+int32_t afh_dist_rccl_unique_id(void *id128);
+int32_t afh_dist_rccl_comm(const void *id128, int32_t rank, int32_t n_ranks, int32_t device,
+                           void **comm);
+int32_t afh_dist_rccl_comm_destroy(void *comm);
+int32_t afh_dist_create(afh_tree *t, const afh_tree_desc *desc, const int32_t *owner,
+                        int32_t rank, int32_t n_ranks, int32_t transport, void *group_or_comm,
+                        afh_dist **out);
+int32_t afh_dist_destroy(afh_dist *d);
+int32_t afh_dist_stats(afh_dist *d, int64_t *n_exchanges, int64_t *bytes);
+
 #ifdef __cplusplus
 }
 #endif

@@ -25,6 +25,10 @@ static int32_t fail(int32_t code, const char *fmt, ...) {
   return code;
 }
 const char *afo_last_error(void) { return g_err; }
+/* error setter for the C++ part of the oracle (c/afo_dist.cpp) */
+__attribute__((visibility("hidden"))) int32_t afo_fail_msg(int32_t code, const char *msg) {
+  return fail(code, "%s", msg);
+}
 
 typedef struct {
   int set;

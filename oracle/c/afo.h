@@ -106,6 +106,27 @@ int32_t afo_mg_update_coarse(afh_mg *mg, int32_t lvl);
 int32_t afo_mg_solve_coarse(afh_mg *mg);
 int32_t afo_mg_correct_children(afh_mg *mg, int32_t lvl);
 
+/* native box sharding: the CPU twin of afh_dist_* (c/afo_dist.cpp);
+ * AFH_DIST_LOCAL only (ranks are threads), the RCCL entry points refuse */
+int32_t afo_dist_partition(const afh_tree_desc *desc, int32_t n_ranks, int32_t *owner,
+                           int32_t *lp);
+int32_t afo_dist_plan(const afh_tree_desc *desc, const int32_t *owner, int32_t kind,
+                      int32_t level, int32_t recv_rank, int32_t send_rank, int32_t *regions,
+                      int32_t cap, int32_t *n);
+int32_t afo_tree_create_sharded(const afh_tree_desc *desc, const int32_t *owner, int32_t rank,
+                                int32_t device, afh_tree **out);
+int32_t afo_dist_group_create(int32_t n_ranks, afh_dist_group **out);
+int32_t afo_dist_group_destroy(afh_dist_group *g);
+int32_t afo_dist_rccl_unique_id(void *id128);
+int32_t afo_dist_rccl_comm(const void *id128, int32_t rank, int32_t n_ranks, int32_t device,
+                           void **comm);
+int32_t afo_dist_rccl_comm_destroy(void *comm);
+int32_t afo_dist_create(afh_tree *t, const afh_tree_desc *desc, const int32_t *owner,
+                        int32_t rank, int32_t n_ranks, int32_t transport, void *group_or_comm,
+                        afh_dist **out);
+int32_t afo_dist_destroy(afh_dist *d);
+int32_t afo_dist_stats(afh_dist *d, int64_t *n_exchanges, int64_t *bytes);
+
 #ifdef __cplusplus
 }
 #endif

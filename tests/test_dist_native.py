@@ -1,0 +1,153 @@
+"""Native box sharding (afh_dist_*): the library partitions
+the tree, builds the exchange plans and runs the exchange hook itself.
+
+* The native partition and plans (afivo-streamer_amd/csrc/afh_dist_core.h,
+  compiled into both libafivo_hip and the oracle) equal the Python statement
+  of them (afh.dist.Partition) -- host code, checked on the CPU for both
+  libraries.
+* Ranks as threads of one process (AFH_DIST_LOCAL): the owned boxes of all
+  ranks, gathered, are bitwise equal to a single-rank run (FMG start-up
+  solve, field solve, a Heun step, time-step limits) -- the oracle's CPU twin
+  here, libafivo_hip with 2 and 3 ranks on the test box's GPU.
+* AFH_DIST_RCCL with one rank on the GPU (two ranks cannot share one GPU in
+  an RCCL communicator): the reductions go through ncclAllReduce and the
+  result is bitwise the unsharded run. Multi-rank RCCL is unmeasured here.
+"""
+import ctypes as C
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pytest
+
+from afh import capi
+from afh.dist import NativeGroup, NativeShard, Partition, rccl_comm
+from test_dist import TOPOS, _run
+
+KINDS = [capi.HOOK_HALO, capi.HOOK_RIMS, capi.HOOK_CFLUX, capi.HOOK_RESTRICT]
+
+
+def _python_regions(part, kind, level, recv, send):
+    if kind == capi.HOOK_HALO:
+        r = part.halo_regions(recv, send, level, False)
+    elif kind == capi.HOOK_RIMS:
+        r = part.halo_regions(recv, send, level, True)
+    elif kind == capi.HOOK_CFLUX:
+        r = part.cflux_regions(recv, send)
+    else:
+        r = part.octant_regions(send) if level == part.lp else []
+    w = 8 if kind == capi.HOOK_CFLUX else 7
+    return np.asarray(r, np.int32).reshape(-1, w)
+
+
+@pytest.mark.parametrize("libname", ["oracle", "hip"])
+@pytest.mark.parametrize("name,world", [("uni8_l3", 2), ("amr8", 2), ("amr8", 3),
+                                        ("uni8_l3", 5)])
+def test_native_partition_and_plans_equal_python(libname, name, world):
+    lib = capi.oracle_library() if libname == "oracle" else capi.hip_library()
+    topo = TOPOS[name]()
+    part = Partition(topo, world)
+    sh = NativeShard(lib, topo, world, 0, transport=capi.DIST_LOCAL,
+                     group=type("G", (), {"h": None})())
+    np.testing.assert_array_equal(sh.owner, part.owner)
+    assert sh.lp == part.lp
+    n_regions = 0
+    for kind in KINDS:
+        levels = [0] if kind == capi.HOOK_CFLUX else range(1, part.nlvl + 1)
+        for level in levels:
+            for recv in range(world):
+                for send in range(world):
+                    if recv == send:
+                        continue
+                    got = sh.plan(kind, level, recv, send)
+                    want = _python_regions(part, kind, level, recv, send)
+                    np.testing.assert_array_equal(got, want, err_msg=str((kind, level, recv, send)))
+                    n_regions += len(got)
+    assert n_regions > 0
+
+
+def test_native_partition_refuses_too_many_ranks():
+    lib = capi.oracle_library()
+    topo = TOPOS["uni8_l3"]()
+    with pytest.raises(capi.AfhError, match="no level"):
+        NativeShard(lib, topo, 10 ** 4, 0, group=type("G", (), {"h": None})())
+
+
+def test_native_tree_create_sharded_matches_local_topology():
+    """afh_tree_create_sharded == tree_create on the Python local view: the
+    sharded trees' reductions see only their own leaves."""
+    from afh.model import Tree
+    lib = capi.oracle_library()
+    topo = TOPOS["amr8"]()
+    part = Partition(topo, 2)
+    sh = NativeShard(lib, topo, 2, 1, group=type("G", (), {"h": None})())
+    a = sh.make_tree(lib, topo, 4, 1)
+    b = Tree(lib, part.local_topology(1), 4, 1)
+    rng = np.random.default_rng(0)
+    x = rng.random(a.cc_shape)
+    a.put_cc(2, x)
+    b.put_cc(2, x)
+    assert a.sum_cc(2) == b.sum_cc(2)
+    assert a.maxabs_cc(2) == b.maxabs_cc(2)
+    a.close()
+    b.close()
+
+
+def _run_threads(lib, name, world, device=-1):
+    topo = TOPOS[name]()
+    group = NativeGroup(lib, world)
+    shards = [NativeShard(lib, topo, world, r, group=group) for r in range(world)]
+    try:
+        with ThreadPoolExecutor(world) as ex:
+            futs = [ex.submit(_run, lib, topo, shards[r]) for r in range(world)]
+            parts = [f.result() for f in futs]
+    finally:
+        group.close()
+    return shards, parts
+
+
+def _compare(ref, shards, parts):
+    for p in parts:
+        np.testing.assert_array_equal(p["lim"], ref["lim"])
+        np.testing.assert_array_equal(p["res"], ref["res"])
+    for key in ref:
+        if key in ("res", "lim"):
+            continue
+        merged = np.array(ref[key], copy=True)
+        merged[:] = np.nan
+        for sh, p in zip(shards, parts):
+            mine = sh.owned_mask()
+            merged[mine] = p[key][mine]
+        assert not np.isnan(merged).any(), key
+        bad = np.argwhere(merged != ref[key])
+        assert len(bad) == 0, (key, bad[:5], np.max(np.abs(merged - ref[key])))
+
+
+@pytest.mark.parametrize("name,world", [("uni8_l3", 2), ("amr8", 3)])
+def test_native_sharded_oracle_threads_bitwise(name, world):
+    lib = capi.oracle_library()
+    ref = _run(lib, TOPOS[name]())
+    shards, parts = _run_threads(lib, name, world)
+    _compare(ref, shards, parts)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,world", [("uni8_l3", 2), ("amr8", 2), ("amr8", 3)])
+def test_native_sharded_hip_local_bitwise(name, world):
+    lib = capi.hip_library()
+    ref = _run(lib, TOPOS[name]())
+    shards, parts = _run_threads(lib, name, world)
+    _compare(ref, shards, parts)
+
+
+@pytest.mark.gpu
+def test_native_rccl_single_rank_bitwise():
+    lib = capi.hip_library()
+    topo = TOPOS["amr8"]()
+    ref = _run(lib, topo)
+    comm = rccl_comm(lib, 0, 1, 0)
+    try:
+        sh = NativeShard(lib, topo, 1, 0, transport=capi.DIST_RCCL, comm=comm)
+        out = _run(lib, topo, sh)
+    finally:
+        lib.call("dist_rccl_comm_destroy", comm)
+    _compare(ref, [sh], [out])
