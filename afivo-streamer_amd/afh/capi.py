@@ -178,6 +178,7 @@ SIGNATURES = {
     # native box sharding
     "dist_partition": (i32, [C.POINTER(TreeDesc), i32, P_i32, P_i32]),
     "dist_plan": (i32, [C.POINTER(TreeDesc), P_i32, i32, i32, i32, i32, P_i32, i32, P_i32]),
+    "dist_local_ids": (i32, [C.POINTER(TreeDesc), P_i32, i32, P_i32, i32, P_i32]),
     "tree_create_sharded": (i32, [C.POINTER(TreeDesc), P_i32, i32, i32, _PVP]),
     "dist_group_create": (i32, [i32, _PVP]),
     "dist_group_destroy": (i32, [_VP]),

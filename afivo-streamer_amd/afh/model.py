@@ -75,13 +75,23 @@ class Tree:
         self.box_capacity = int(box_capacity)
         d, self._keep = tree_desc(topo, n_var_cell, n_var_face, self.box_capacity)
         h = C.c_void_p()
+        # sharded: the global id of every stored box, in local-id order (the
+        # library stores only the boxes the rank reads, plus one unused id)
+        self.global_ids = None
         if shard_of is not None:
             # this rank's boxes of the full tree (afh_tree_create_sharded)
-            full, self._keep_full = tree_desc(shard_of[0], n_var_cell, n_var_face,
-                                              self.box_capacity)
+            full, self._keep_full = tree_desc(shard_of[0], n_var_cell, n_var_face)
             owner = np.ascontiguousarray(shard_of[1], np.int32)
-            lib.call("tree_create_sharded", C.byref(full), owner.ctypes.data_as(capi.P_i32),
-                     int(shard_of[2]), device, C.byref(h))
+            pown, rank = owner.ctypes.data_as(capi.P_i32), int(shard_of[2])
+            n = C.c_int32()
+            lib.call("dist_local_ids", C.byref(full), pown, rank, None, 0, C.byref(n))
+            gids = np.zeros(n.value, np.int32)
+            lib.call("dist_local_ids", C.byref(full), pown, rank,
+                     gids.ctypes.data_as(capi.P_i32), n.value, C.byref(n))
+            self.global_ids = gids
+            self.n_global = self.n_boxes
+            self.n_boxes = n.value + 1
+            lib.call("tree_create_sharded", C.byref(full), pown, rank, device, C.byref(h))
         elif _regrid_of is None:
             lib.call("tree_create", C.byref(d), device, C.byref(h))
         else:
@@ -140,25 +150,51 @@ class Tree:
     def set_bc(self, iv, nb, bc_type, value):
         self.lib.call("set_bc", self.h, iv, nb, bc_type, float(value))
 
+    def local_id(self, box_id):
+        """The library's id of global box id (0: a sharded tree does not store it)."""
+        if self.global_ids is None:
+            return int(box_id)
+        k = int(np.searchsorted(self.global_ids, box_id))
+        return k + 1 if k < len(self.global_ids) and self.global_ids[k] == box_id else 0
+
+    def _to_local(self, a):
+        """A whole-tree array -> the stored boxes (the unused last id NaN)."""
+        if self.global_ids is None or a.shape[0] == self.n_boxes:
+            return a
+        assert a.shape[0] == self.n_global, (a.shape, self.n_global)
+        out = np.full((self.n_boxes,) + a.shape[1:], np.nan)
+        out[:-1] = a[self.global_ids - 1]
+        return out
+
+    def _to_global(self, a):
+        """Stored boxes -> a whole-tree array (NaN where not stored)."""
+        if self.global_ids is None:
+            return a
+        out = np.full((self.n_global,) + a.shape[1:], np.nan)
+        out[self.global_ids - 1] = a[:-1]
+        return out
+
     def put_cc(self, iv, arr):
-        a = np.ascontiguousarray(arr, dtype=np.float64)
+        """Whole-tree array (n_boxes, ng, ng, ng); a sharded tree takes the
+        whole tree's array (or its stored boxes', local_shape)."""
+        a = np.ascontiguousarray(self._to_local(np.asarray(arr, np.float64)))
         assert a.shape == self.cc_shape, (a.shape, self.cc_shape)
         self.lib.call("cc_put", self.h, iv, a.ctypes.data_as(capi.P_f64))
 
     def get_cc(self, iv):
         a = np.empty(self.cc_shape)
         self.lib.call("cc_get", self.h, iv, a.ctypes.data_as(capi.P_f64))
-        return a
+        return self._to_global(a)
 
     def put_fc(self, ivf, arr):
-        a = np.ascontiguousarray(arr, dtype=np.float64)
+        a = np.ascontiguousarray(self._to_local(np.asarray(arr, np.float64)))
         assert a.shape == self.fc_shape
         self.lib.call("fc_put", self.h, ivf, a.ctypes.data_as(capi.P_f64))
 
     def get_fc(self, ivf):
         a = np.empty(self.fc_shape)
         self.lib.call("fc_get", self.h, ivf, a.ctypes.data_as(capi.P_f64))
-        return a
+        return self._to_global(a)
 
     # -- afivo tree operations
     def gc_lvl(self, lvl, iv, corners=True):

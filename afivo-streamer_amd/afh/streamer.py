@@ -116,12 +116,17 @@ class StreamerCase:
         """Electrode operators (m_field.f90:255-346): the stencils afivo's
         mg_set_operators_tree stored on the boxes the electrode crosses,
         handed to the field multigrid. stencils: {box id: (v, bc_correction)};
-        lsf_faces: {box id: (ix, dd, bval)}."""
+        lsf_faces: {box id: (ix, dd, bval)} (global ids; a sharded tree takes
+        those of the boxes it stores)."""
         self.i_lsf = i_lsf
         for bid, (v, bcc) in stencils.items():
-            self.mg.set_box_stencil(bid, v, bcc)
+            lid = self.tree.local_id(bid)
+            if lid:
+                self.mg.set_box_stencil(lid, v, bcc)
         for bid, (ix, dd, bv) in lsf_faces.items():
-            self.mg.set_box_lsf(bid, ix, dd, bv, i_lsf)
+            lid = self.tree.local_id(bid)
+            if lid:
+                self.mg.set_box_lsf(lid, ix, dd, bv, i_lsf)
 
     def fuse_rhs(self, on=True, ghosts=True):
         """Fold field_set_rhs of the new state into every density update

@@ -196,25 +196,55 @@ int32_t afh_dist_plan(const afh_tree_desc *desc, const int32_t *owner, int32_t k
   return AFH_OK;
 }
 
+int32_t afh_dist_local_ids(const afh_tree_desc *desc, const int32_t *owner, int32_t rank,
+                          int32_t *ids, int32_t cap, int32_t *n) {
+  if (!desc || !owner || !n) return set_error(AFH_ERR_ARG, "afh_dist_local_ids");
+  const Topo t = topo_of(desc);
+  const auto v = local_boxes(t, std::vector<int32_t>(owner, owner + t.nb), rank);
+  *n = (int32_t)v.size();
+  if (ids) {
+    if ((int)v.size() > cap)
+      return set_error(AFH_ERR_ARG, "afh_dist_local_ids: %d boxes > cap %d", (int)v.size(), cap);
+    std::copy(v.begin(), v.end(), ids);
+  }
+  return AFH_OK;
+}
+
 int32_t afh_tree_create_sharded(const afh_tree_desc *desc, const int32_t *owner, int32_t rank,
                                 int32_t device, afh_tree **out) {
   if (!desc || !owner || !out) return set_error(AFH_ERR_ARG, "afh_tree_create_sharded");
   const Topo t = topo_of(desc);
-  std::vector<int32_t> lists[3], offs[3];
-  const std::vector<std::vector<int32_t>> *src[3] = {&t.ids, &t.leaves, &t.parents};
-  for (int k = 0; k < 3; k++) {
-    offs[k].push_back(0);
-    for (int l = 0; l < t.nlvl; l++) {
-      for (int32_t i : (*src[k])[l])
-        if (owner[i - 1] == rank || owner[i - 1] < 0) lists[k].push_back(i);
-      offs[k].push_back((int32_t)lists[k].size());
+  Compact c;
+  compact(t, desc, std::vector<int32_t>(owner, owner + t.nb), rank, c);
+  int32_t e = afh_tree_create(&c.desc, device, out);
+  if (e) return e;
+  // the choices every rank must make alike (which exchanges a ghost-cell
+  // fill requests, the smoother per level) follow the whole topology, as in
+  // an unsharded tree, not this rank's boxes
+  afh_tree *tr = *out;
+  // the unused id reads as NaN in every variable: a kernel that reaches a
+  // box the rank does not store fails the parity tests loudly
+  for (int iv = 1; iv <= tr->nvc; iv++)
+    AFH_HIP(hipMemsetAsync(tr->ccv(iv) + (size_t)(tr->nb - 1) * tr->bsz, 0xff,
+                           sizeof(double) * tr->bsz, tr->stream));
+  for (int iv = 1; iv <= tr->nvf; iv++)
+    AFH_HIP(hipMemsetAsync(tr->fcv(iv) + (size_t)(tr->nb - 1) * tr->fsz, 0xff,
+                           sizeof(double) * tr->fsz, tr->stream));
+  AFH_HIP(hipStreamSynchronize(tr->stream));
+  tr->lvl_total.assign(t.nlvl, 0);
+  tr->lvl_rb_coarse.assign(t.nlvl, 0);
+  tr->any_cflux = false;
+  for (int id = 1; id <= t.nb; id++) {
+    const afh_box_meta &m = t.m[id - 1];
+    if (m.lvl < 1) continue;
+    tr->lvl_total[m.lvl - 1]++;
+    for (int q = 0; q < 6; q++) {
+      if (m.lvl >= 2 && m.neighbors[q] == 0) tr->lvl_rb_coarse[m.lvl - 2] = 1;
+      if (m.children[0] && m.neighbors[q] > 0 && t.m[m.neighbors[q] - 1].children[0] == 0)
+        tr->any_cflux = true;
     }
   }
-  afh_tree_desc d = *desc;
-  d.lvl_ids = lists[0].data(), d.lvl_ids_off = offs[0].data();
-  d.lvl_leaves = lists[1].data(), d.lvl_leaves_off = offs[1].data();
-  d.lvl_parents = lists[2].data(), d.lvl_parents_off = offs[2].data();
-  return afh_tree_create(&d, device, out);
+  return AFH_OK;
 }
 
 int32_t afh_dist_group_create(int32_t n_ranks, afh_dist_group **out) {
@@ -263,9 +293,15 @@ int32_t afh_dist_create(afh_tree *t, const afh_tree_desc *desc, const int32_t *o
   if (transport != AFH_DIST_LOCAL && transport != AFH_DIST_RCCL)
     return set_error(AFH_ERR_UNSUPPORTED, "transport %d", transport);
   const Topo tp = topo_of(desc);
-  if (tp.nb != t->nb || tp.nc != t->nc) return set_error(AFH_ERR_ARG, "topology mismatch");
   const std::vector<int32_t> own(owner, owner + tp.nb);
   const int lp = first_owned_level(tp, owner);
+  // region box ids -> the rank's compacted ids (afh_tree_create_sharded)
+  const auto local = local_boxes(tp, own, rank);
+  if ((int)local.size() + 1 != t->nb || tp.nc != t->nc)
+    return set_error(AFH_ERR_ARG, "afh_dist_create: the tree is not rank %d's part of this "
+                     "topology (afh_tree_create_sharded)", rank);
+  std::vector<int32_t> g2l(tp.nb + 1, 0);
+  for (size_t k = 0; k < local.size(); k++) g2l[local[k]] = (int32_t)k + 1;
   afh_dist *d = new afh_dist;
   d->t = t, d->rank = rank, d->n = n_ranks, d->transport = transport;
   hipGetDevice(&d->device);
@@ -290,7 +326,10 @@ int32_t afh_dist_create(afh_tree *t, const afh_tree_desc *desc, const int32_t *o
         afh_dist::Side &sd = side == 0 ? p.send[q] : p.recv[q];
         if (rs.empty()) continue;
         std::vector<int32_t> flat;
-        for (const Region &r : rs) flat.insert(flat.end(), r.begin(), r.begin() + (fc ? 8 : 7));
+        for (const Region &r : rs) {
+          flat.insert(flat.end(), r.begin(), r.begin() + (fc ? 8 : 7));
+          flat[flat.size() - (fc ? 8 : 7)] = g2l[r[0]];
+        }
         int32_t e = fc ? afh_plan_create_fc(t, flat.data(), (int32_t)rs.size(), &sd.plan, &sd.n)
                        : afh_plan_create(t, flat.data(), (int32_t)rs.size(), &sd.plan, &sd.n);
         if (e) return e;

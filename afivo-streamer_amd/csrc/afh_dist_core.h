@@ -225,4 +225,92 @@ inline int first_owned_level(const Topo &t, const int32_t *owner) {
   return 0;
 }
 
+// The boxes a rank stores (owned-box allocation): its own boxes, the
+// replicated levels below Lp, every box an exchange plan of the rank names
+// (as sender or receiver: halo / rim replicas, the faces it writes for the
+// consistent fluxes, the parents of the restriction) and, on a level where
+// that leaves none, one box of the level (its grid spacing). Ascending
+// global ids; the local id of ids[k] is k + 1.
+inline std::vector<int32_t> local_boxes(const Topo &t, const std::vector<int32_t> &owner,
+                                        int rank) {
+  int lp = 0, n = 1;
+  for (int l = 1; l <= t.nlvl && !lp; l++)
+    for (int32_t i : t.ids[l - 1])
+      if (owner[i - 1] >= 0) {
+        lp = l;
+        break;
+      }
+  for (int32_t o : owner) n = std::max(n, o + 1);
+  std::vector<char> keep(t.nb + 1, 0);
+  for (int i = 1; i <= t.nb; i++) keep[i] = owner[i - 1] == rank || owner[i - 1] < 0;
+  auto add = [&](const std::vector<Region> &rs) {
+    for (const Region &r : rs) keep[r[0]] = 1;
+  };
+  if (lp)
+    for (int q = 0; q < n; q++) {
+      if (q == rank) continue;
+      for (int l = lp; l <= t.nlvl; l++) {
+        add(plan_regions(t, owner, lp, AFH_HOOK_RIMS, l, rank, q));
+        add(plan_regions(t, owner, lp, AFH_HOOK_RIMS, l, q, rank));
+      }
+      add(plan_regions(t, owner, lp, AFH_HOOK_CFLUX, 0, rank, q));
+      add(plan_regions(t, owner, lp, AFH_HOOK_CFLUX, 0, q, rank));
+      add(plan_regions(t, owner, lp, AFH_HOOK_RESTRICT, lp, rank, q));
+      add(plan_regions(t, owner, lp, AFH_HOOK_RESTRICT, lp, q, rank));
+    }
+  for (int l = 1; l <= t.nlvl; l++) {
+    bool any = false;
+    for (int32_t i : t.ids[l - 1]) any |= keep[i] != 0;
+    if (!any && !t.ids[l - 1].empty()) keep[t.ids[l - 1][0]] = 1;
+  }
+  std::vector<int32_t> ids;
+  for (int i = 1; i <= t.nb; i++)
+    if (keep[i]) ids.push_back(i);
+  return ids;
+}
+
+// A rank's compacted tree: the boxes of local_boxes renumbered 1..n, and a
+// last, unused id (level 0, no data anyone reads) that stands for every box
+// a stored box names but the rank does not store.
+struct Compact {
+  std::vector<int32_t> ids, g2l;  // local -> global (ids[k] = global id of k+1); global -> local
+  std::vector<afh_box_meta> meta;
+  std::vector<int32_t> lists[3], offs[3];
+  afh_tree_desc desc;
+};
+
+inline void compact(const Topo &t, const afh_tree_desc *full, const std::vector<int32_t> &owner,
+                    int rank, Compact &c) {
+  c.ids = local_boxes(t, owner, rank);
+  const int n = (int)c.ids.size(), absent = n + 1;
+  c.g2l.assign(t.nb + 1, 0);
+  for (int k = 0; k < n; k++) c.g2l[c.ids[k]] = k + 1;
+  auto map = [&](int32_t g) { return g <= 0 ? g : c.g2l[g] ? c.g2l[g] : absent; };
+  c.meta.assign(n + 1, afh_box_meta{});
+  for (int k = 0; k < n; k++) {
+    afh_box_meta m = t.m[c.ids[k] - 1];
+    m.parent = map(m.parent);
+    for (int q = 0; q < 8; q++) m.children[q] = map(m.children[q]);
+    for (int q = 0; q < 6; q++) m.neighbors[q] = map(m.neighbors[q]);
+    for (int q = 0; q < 27; q++) m.neighbor_mat[q] = map(m.neighbor_mat[q]);
+    c.meta[k] = m;
+  }
+  const std::vector<std::vector<int32_t>> *src[3] = {&t.ids, &t.leaves, &t.parents};
+  for (int k = 0; k < 3; k++) {
+    c.lists[k].clear(), c.offs[k].assign(1, 0);
+    for (int l = 0; l < t.nlvl; l++) {
+      for (int32_t i : (*src[k])[l])
+        if (owner[i - 1] == rank || owner[i - 1] < 0) c.lists[k].push_back(c.g2l[i]);
+      c.offs[k].push_back((int32_t)c.lists[k].size());
+    }
+  }
+  c.desc = *full;
+  c.desc.n_boxes = n + 1;
+  c.desc.box_capacity = 0;
+  c.desc.boxes = c.meta.data();
+  c.desc.lvl_ids = c.lists[0].data(), c.desc.lvl_ids_off = c.offs[0].data();
+  c.desc.lvl_leaves = c.lists[1].data(), c.desc.lvl_leaves_off = c.offs[1].data();
+  c.desc.lvl_parents = c.lists[2].data(), c.desc.lvl_parents_off = c.offs[2].data();
+}
+
 }  // namespace afhd

@@ -48,7 +48,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E peak (spec)
 
 
 def build_case(lib, config, device, coarse_cycles, shard_ranks=None):
-    """shard_ranks = (world, rank): this rank's part of the sharded tree."""
+    """shard_ranks = (world, rank, "native" | "python"): this rank's part of
+    the sharded tree."""
     from afh.streamer import StreamerCase, seed_state, tables_from
     from afh.tree import uniform_tree
     import golden
@@ -59,9 +60,17 @@ def build_case(lib, config, device, coarse_cycles, shard_ranks=None):
     voltage = -dom[2] * (-2.5e6)
     shard = None
     if shard_ranks is not None:
-        from afh.dist import Partition, Shard
-        world, rank = shard_ranks
-        shard = Shard(Partition(topo, world), rank, "nccl", device="cuda:%d" % device)
+        world, rank, kind = shard_ranks
+        if kind == "native":
+            # the library's own sharding: owned-box storage, exchanges as
+            # RCCL send/recv on the tree's stream, no Python in the step
+            from afh import capi
+            from afh.dist import NativeShard, rccl_comm
+            shard = NativeShard(lib, topo, world, rank, transport=capi.DIST_RCCL,
+                                comm=rccl_comm(lib, rank, world, device))
+        else:
+            from afh.dist import Partition, Shard
+            shard = Shard(Partition(topo, world), rank, "nccl", device="cuda:%d" % device)
     case = StreamerCase(lib, topo, td, chem, voltage, coarse_cycles=coarse_cycles,
                         device=device, shard=shard)
     seed_state(case, width=0.05 * dom[2])
@@ -194,6 +203,9 @@ def main():
                          "into the density update (afh_fluid_set_rhs_output)")
     ap.add_argument("--replicas", action="store_true",
                     help="N>1: one independent replica per GPU instead of sharding")
+    ap.add_argument("--shard", choices=("native", "python"), default="native",
+                    help="N>1 sharding: the library's (afh_dist, RCCL transport, owned-box "
+                         "storage) or the Python hook over torch.distributed (afh.dist.Shard)")
     ap.add_argument("--graphs", choices=("auto", "on", "off"), default="auto",
                     help="V-cycles replayed as captured hipGraphs (auto: on for the "
                          "small-box configs s1 / s3, whose steps are launch-bound)")
@@ -222,7 +234,7 @@ def main():
         case = DriverCase(sim)
     else:
         case = build_case(lib, args.config, local, args.coarse_cycles,
-                          (world, rank) if sharded else None)
+                          (world, rank, args.shard) if sharded else None)
     from afh.streamer import cells
     ncell = cells(case.topo)  # leaf cells of the whole tree
     dt = 1e-13
@@ -294,7 +306,7 @@ def main():
                                         "mg%d" % args.coarse_cycles),
                        "fused_rhs": "interior" if not args.no_fused_rhs else False,
                        "vcycle_graphs": graphs,
-                       "parallelism": ("box-shard-%d" % world) if sharded else
+                       "parallelism": ("box-shard-%d-%s" % (world, args.shard)) if sharded else
                        ("replica-per-gpu" if world > 1 else "single-gpu")},
             "roofline": {"bound": "hbm",
                          "kernel": ("k_gsrb_pair2<%d,%d>" % (CONFIGS[args.config][0],

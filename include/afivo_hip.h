@@ -529,8 +529,12 @@ int32_t afh_plan_unpack(afh_tree *t, int32_t plan, int32_t iv,
  * compare them), so a driver in any language shards a tree:
  *   owner <- afh_dist_partition(full desc, n_ranks)  (box id b: owner[b-1],
  *            -1 = replicated coarse level, *lp = the partition level)
- *   afh_tree_create_sharded(full desc, owner, rank, device, &t)  (this
- *            rank's boxes in the level lists; storage for the whole tree)
+ *   afh_tree_create_sharded(full desc, owner, rank, device, &t)  (storage
+ *            only for the boxes this rank reads: its own, the replicated
+ *            levels and the replicas its exchanges name; renumbered 1..n in
+ *            ascending global id, afh_dist_local_ids gives the global ids,
+ *            plus one unused id n+1 standing for every box not stored;
+ *            cc/fc arrays and box ids in calls on t are local)
  *   afh_dist_create(t, full desc, owner, rank, n_ranks, transport, x, &d)
  * Transports: AFH_DIST_LOCAL -- the ranks are threads of one process (one
  * tree each, on one GPU or several; x = an afh_dist_group shared by the
@@ -549,6 +553,8 @@ int32_t afh_dist_partition(const afh_tree_desc *desc, int32_t n_ranks, int32_t *
 int32_t afh_dist_plan(const afh_tree_desc *desc, const int32_t *owner, int32_t kind,
                       int32_t level, int32_t recv_rank, int32_t send_rank, int32_t *regions,
                       int32_t cap, int32_t *n);
+int32_t afh_dist_local_ids(const afh_tree_desc *desc, const int32_t *owner, int32_t rank,
+                          int32_t *ids, int32_t cap, int32_t *n);
 int32_t afh_tree_create_sharded(const afh_tree_desc *desc, const int32_t *owner, int32_t rank,
                                 int32_t device, afh_tree **out);
 int32_t afh_dist_group_create(int32_t n_ranks, afh_dist_group **out);

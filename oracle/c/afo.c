@@ -212,6 +212,13 @@ int32_t afo_tree_create(const afh_tree_desc *d, int32_t device,
   return AFH_OK;
 }
 
+/* sharded trees (c/afo_dist.cpp): box id's data read as NaN in every
+ * variable (the unused id standing for boxes a rank does not store) */
+__attribute__((visibility("hidden"))) void afo_poison_box(afh_tree *t, int id) {
+  for (int iv = 1; iv <= t->nvc; iv++) memset(ccb(t, iv, id), 0xff, sizeof(double) * t->bsz);
+  for (int iv = 1; iv <= t->nvf; iv++) memset(fcb(t, iv, id), 0xff, sizeof(double) * t->fsz);
+}
+
 int32_t afo_tree_destroy(afh_tree *t) {
   if (!t) return AFH_OK;
   free(t->boxes);

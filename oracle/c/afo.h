@@ -113,6 +113,8 @@ int32_t afo_dist_partition(const afh_tree_desc *desc, int32_t n_ranks, int32_t *
 int32_t afo_dist_plan(const afh_tree_desc *desc, const int32_t *owner, int32_t kind,
                       int32_t level, int32_t recv_rank, int32_t send_rank, int32_t *regions,
                       int32_t cap, int32_t *n);
+int32_t afo_dist_local_ids(const afh_tree_desc *desc, const int32_t *owner, int32_t rank,
+                          int32_t *ids, int32_t cap, int32_t *n);
 int32_t afo_tree_create_sharded(const afh_tree_desc *desc, const int32_t *owner, int32_t rank,
                                 int32_t device, afh_tree **out);
 int32_t afo_dist_group_create(int32_t n_ranks, afh_dist_group **out);

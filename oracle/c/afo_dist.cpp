@@ -21,6 +21,7 @@
 #include "../../afivo-streamer_amd/csrc/afh_dist_core.h"
 
 extern "C" int32_t afo_fail_msg(int32_t code, const char *msg);
+extern "C" void afo_poison_box(afh_tree *t, int id);
 
 using namespace afhd;
 
@@ -156,25 +157,29 @@ int32_t afo_dist_plan(const afh_tree_desc *desc, const int32_t *owner, int32_t k
   return AFH_OK;
 }
 
+int32_t afo_dist_local_ids(const afh_tree_desc *desc, const int32_t *owner, int32_t rank,
+                          int32_t *ids, int32_t cap, int32_t *n) {
+  if (!desc || !owner || !n) return fail(AFH_ERR_ARG, "afo_dist_local_ids");
+  const Topo t = topo_of(desc);
+  const auto v = local_boxes(t, std::vector<int32_t>(owner, owner + t.nb), rank);
+  *n = (int32_t)v.size();
+  if (ids) {
+    if ((int)v.size() > cap)
+      return fail(AFH_ERR_ARG, "afo_dist_local_ids: %d boxes > cap %d", (int)v.size(), cap);
+    std::copy(v.begin(), v.end(), ids);
+  }
+  return AFH_OK;
+}
+
 int32_t afo_tree_create_sharded(const afh_tree_desc *desc, const int32_t *owner, int32_t rank,
                                 int32_t device, afh_tree **out) {
   if (!desc || !owner || !out) return fail(AFH_ERR_ARG, "afo_tree_create_sharded");
   const Topo t = topo_of(desc);
-  std::vector<int32_t> lists[3], offs[3];
-  const std::vector<std::vector<int32_t>> *src[3] = {&t.ids, &t.leaves, &t.parents};
-  for (int k = 0; k < 3; k++) {
-    offs[k].push_back(0);
-    for (int l = 0; l < t.nlvl; l++) {
-      for (int32_t i : (*src[k])[l])
-        if (owner[i - 1] == rank || owner[i - 1] < 0) lists[k].push_back(i);
-      offs[k].push_back((int32_t)lists[k].size());
-    }
-  }
-  afh_tree_desc d = *desc;
-  d.lvl_ids = lists[0].data(), d.lvl_ids_off = offs[0].data();
-  d.lvl_leaves = lists[1].data(), d.lvl_leaves_off = offs[1].data();
-  d.lvl_parents = lists[2].data(), d.lvl_parents_off = offs[2].data();
-  return afo_tree_create(&d, device, out);
+  Compact c;
+  compact(t, desc, std::vector<int32_t>(owner, owner + t.nb), rank, c);
+  const int32_t e = afo_tree_create(&c.desc, device, out);
+  if (!e) afo_poison_box(*out, c.desc.n_boxes);
+  return e;
 }
 
 int32_t afo_dist_group_create(int32_t n_ranks, afh_dist_group **out) {
@@ -210,6 +215,9 @@ int32_t afo_dist_create(afh_tree *t, const afh_tree_desc *desc, const int32_t *o
   const Topo tp = topo_of(desc);
   const std::vector<int32_t> own(owner, owner + tp.nb);
   const int lp = first_owned_level(tp, owner);
+  const auto local = local_boxes(tp, own, rank);
+  std::vector<int32_t> g2l(tp.nb + 1, 0);
+  for (size_t k = 0; k < local.size(); k++) g2l[local[k]] = (int32_t)k + 1;
   afh_dist *d = new afh_dist;
   d->t = t, d->rank = rank, d->n = n_ranks, d->group = g;
   auto add = [&](int kind, int level) -> int32_t {
@@ -224,7 +232,10 @@ int32_t afo_dist_create(afh_tree *t, const afh_tree_desc *desc, const int32_t *o
         afh_dist::Side &sd = side == 0 ? p.send[q] : p.recv[q];
         if (rs.empty()) continue;
         std::vector<int32_t> flat;
-        for (const Region &r : rs) flat.insert(flat.end(), r.begin(), r.begin() + (fc ? 8 : 7));
+        for (const Region &r : rs) {
+          flat.insert(flat.end(), r.begin(), r.begin() + (fc ? 8 : 7));
+          flat[flat.size() - (fc ? 8 : 7)] = g2l[r[0]];
+        }
         const int32_t e = fc ? afo_plan_create_fc(t, flat.data(), (int32_t)rs.size(), &sd.plan, &sd.n)
                              : afo_plan_create(t, flat.data(), (int32_t)rs.size(), &sd.plan, &sd.n);
         if (e) return e;

@@ -7,8 +7,11 @@ the tree, builds the exchange plans and runs the exchange hook itself.
   libraries.
 * Ranks as threads of one process (AFH_DIST_LOCAL): the owned boxes of all
   ranks, gathered, are bitwise equal to a single-rank run (FMG start-up
-  solve, field solve, a Heun step, time-step limits) -- the oracle's CPU twin
-  here, libafivo_hip with 2 and 3 ranks on the test box's GPU.
+  solve, field solve, a Heun step, time-step limits; on the rod-electrode
+  AMR tree also the level-set operators and a Helmholtz FMG) -- the oracle's
+  CPU twin here, libafivo_hip with 2 and 3 ranks on the test box's GPU. Each
+  rank stores only the boxes it reads (afh_tree_create_sharded); the unused
+  id that stands for the others reads as NaN, so a stray read would show.
 * AFH_DIST_RCCL with one rank on the GPU (two ranks cannot share one GPU in
   an RCCL communicator): the reductions go through ncclAllReduce and the
   result is bitwise the unsharded run. Multi-rank RCCL is unmeasured here.
@@ -20,8 +23,10 @@ import numpy as np
 import pytest
 
 from afh import capi
+import golden
 from afh.dist import NativeGroup, NativeShard, Partition, rccl_comm
-from test_dist import TOPOS, _run
+from afh.streamer import FV, IV
+from test_dist import CC_VARS, TOPOS, _run
 
 KINDS = [capi.HOOK_HALO, capi.HOOK_RIMS, capi.HOOK_CFLUX, capi.HOOK_RESTRICT]
 
@@ -83,22 +88,64 @@ def test_native_tree_create_sharded_matches_local_topology():
     a = sh.make_tree(lib, topo, 4, 1)
     b = Tree(lib, part.local_topology(1), 4, 1)
     rng = np.random.default_rng(0)
-    x = rng.random(a.cc_shape)
+    x = rng.random(b.cc_shape)  # whole-tree array; a stores only its boxes
     a.put_cc(2, x)
     b.put_cc(2, x)
     assert a.sum_cc(2) == b.sum_cc(2)
     assert a.maxabs_cc(2) == b.maxabs_cc(2)
+    # owned-box allocation: fewer stored boxes than the tree has, every
+    # owned and replicated box among them, and the rest read back as NaN
+    assert a.n_boxes - 1 < a.n_global
+    mine = sh.owned_mask()
+    assert np.all(np.isin(np.nonzero(mine)[0] + 1, a.global_ids))
+    y = a.get_cc(2)
+    np.testing.assert_array_equal(y[mine], x[mine])
+    absent = np.setdiff1d(np.arange(1, a.n_global + 1), a.global_ids)
+    assert len(absent) and np.isnan(y[absent - 1]).all()
     a.close()
     b.close()
 
 
+def _run_rod(lib, topo, shard=None):
+    """Config 4's shape: the reference's rod-electrode AMR tree
+    (tests/golden/rod8.npz, level-set stencils) -- two V-cycles, the
+    gradient, FMG without and with guess, a Heun step, then a
+    photoionization Helmholtz mode's FMG (m_photoi_helmh.f90:149-204)."""
+    g = golden.load("rod8")
+    c = golden.make_case(lib, g, coarse_cycles=12, shard=shard)
+    golden.upload(c, {**golden.stage_outputs(g, "init"), **golden.stage_outputs(g, "rhs")})
+    c.mg.fas_vcycle(True)
+    c.mg.fas_vcycle(True)
+    c.field_from_potential()
+    c.mg.fas_fmg(True, have_guess=False)
+    c.mg.fas_fmg(True, have_guess=True)
+    out = {"lim": np.asarray(c.heun_step(1e-12)), "res": np.zeros(0)}
+    for iv in CC_VARS:
+        out["cc%d" % iv] = c.tree.get_cc(iv)
+    c.set_voltage(0.0)
+    c.fluid.field_set_rhs(IV["rhs"], 0)
+    c.helmholtz_mg(44081.25 ** 2).fas_fmg(True, have_guess=False)
+    out["helm_phi"] = c.tree.get_cc(IV["phi"])
+    out["fc_field"] = c.tree.get_fc(FV["field"])
+    if shard is not None:
+        shard.detach()
+    return out
+
+
+RUNS = {"uni8_l3": _run, "amr8": _run, "rod8": _run_rod}
+
+
+def _topo(name):
+    return golden.load("rod8") if name == "rod8" else TOPOS[name]()
+
+
 def _run_threads(lib, name, world, device=-1):
-    topo = TOPOS[name]()
+    topo = _topo(name)
     group = NativeGroup(lib, world)
     shards = [NativeShard(lib, topo, world, r, group=group) for r in range(world)]
     try:
         with ThreadPoolExecutor(world) as ex:
-            futs = [ex.submit(_run, lib, topo, shards[r]) for r in range(world)]
+            futs = [ex.submit(RUNS[name], lib, topo, shards[r]) for r in range(world)]
             parts = [f.result() for f in futs]
     finally:
         group.close()
@@ -122,19 +169,20 @@ def _compare(ref, shards, parts):
         assert len(bad) == 0, (key, bad[:5], np.max(np.abs(merged - ref[key])))
 
 
-@pytest.mark.parametrize("name,world", [("uni8_l3", 2), ("amr8", 3)])
+@pytest.mark.parametrize("name,world", [("uni8_l3", 2), ("amr8", 3), ("rod8", 2)])
 def test_native_sharded_oracle_threads_bitwise(name, world):
     lib = capi.oracle_library()
-    ref = _run(lib, TOPOS[name]())
+    ref = RUNS[name](lib, _topo(name))
     shards, parts = _run_threads(lib, name, world)
     _compare(ref, shards, parts)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,world", [("uni8_l3", 2), ("amr8", 2), ("amr8", 3)])
+@pytest.mark.parametrize("name,world", [("uni8_l3", 2), ("amr8", 2), ("amr8", 3),
+                                        ("rod8", 2), ("rod8", 3)])
 def test_native_sharded_hip_local_bitwise(name, world):
     lib = capi.hip_library()
-    ref = _run(lib, TOPOS[name]())
+    ref = RUNS[name](lib, _topo(name))
     shards, parts = _run_threads(lib, name, world)
     _compare(ref, shards, parts)
 
