@@ -128,6 +128,8 @@ module m_afivo_hip
   integer(c_int32_t), parameter :: AFH_HOOK_HALO = 1, AFH_HOOK_RIMS = 2, &
        AFH_HOOK_RESTRICT = 3, AFH_HOOK_MAX = 4, AFH_HOOK_MIN = 5, AFH_HOOK_CFLUX = 6, &
        AFH_HOOK_SUM = 7
+  ! afh_dist_create transports
+  integer(c_int32_t), parameter :: AFH_DIST_LOCAL = 1, AFH_DIST_RCCL = 2
   integer(c_int32_t), parameter :: AFH_RM_REF = -1, AFH_KEEP_REF = 0, AFH_DO_REF = 1
   integer, parameter :: AFH_MAX_REFINE_REGIONS = 8
   integer, parameter :: AFH_MAX_GAS_SPECIES = 8
@@ -546,6 +548,111 @@ module m_afivo_hip
        integer(c_int32_t), value :: plan, iv
        integer(c_int32_t)        :: afh_plan_unpack
      end function afh_plan_unpack
+
+     !> native box sharding (include/afivo_hip.h, afh_dist_*): the library
+     !> partitions the tree, stores a rank's boxes and runs the exchanges.
+     !> With MPI, rank 0 calls afh_dist_rccl_unique_id, broadcasts the 128
+     !> bytes (MPI_Bcast), every rank calls afh_dist_rccl_comm and then
+     !> afh_dist_create(..., AFH_DIST_RCCL, comm, d).
+     function afh_dist_partition(desc, n_ranks, owner, lp) &
+          bind(C, name=afh_pfx//"dist_partition")
+       import
+       type(afh_tree_desc), intent(in) :: desc
+       integer(c_int32_t), value       :: n_ranks
+       integer(c_int32_t), intent(out) :: owner(*), lp
+       integer(c_int32_t)              :: afh_dist_partition
+     end function afh_dist_partition
+
+     function afh_dist_plan(desc, owner, kind, level, recv_rank, send_rank, regions, cap, n) &
+          bind(C, name=afh_pfx//"dist_plan")
+       import
+       type(afh_tree_desc), intent(in) :: desc
+       integer(c_int32_t), intent(in)  :: owner(*)
+       integer(c_int32_t), value       :: kind, level, recv_rank, send_rank, cap
+       type(c_ptr), value              :: regions
+       integer(c_int32_t), intent(out) :: n
+       integer(c_int32_t)              :: afh_dist_plan
+     end function afh_dist_plan
+
+     !> the global ids of the boxes rank stores (local id k = ids(k))
+     function afh_dist_local_ids(desc, owner, rank, ids, cap, n) &
+          bind(C, name=afh_pfx//"dist_local_ids")
+       import
+       type(afh_tree_desc), intent(in) :: desc
+       integer(c_int32_t), intent(in)  :: owner(*)
+       integer(c_int32_t), value       :: rank, cap
+       type(c_ptr), value              :: ids
+       integer(c_int32_t), intent(out) :: n
+       integer(c_int32_t)              :: afh_dist_local_ids
+     end function afh_dist_local_ids
+
+     function afh_tree_create_sharded(desc, owner, rank, device, out) &
+          bind(C, name=afh_pfx//"tree_create_sharded")
+       import
+       type(afh_tree_desc), intent(in) :: desc
+       integer(c_int32_t), intent(in)  :: owner(*)
+       integer(c_int32_t), value       :: rank, device
+       type(c_ptr), intent(out)        :: out
+       integer(c_int32_t)              :: afh_tree_create_sharded
+     end function afh_tree_create_sharded
+
+     function afh_dist_group_create(n_ranks, out) bind(C, name=afh_pfx//"dist_group_create")
+       import
+       integer(c_int32_t), value :: n_ranks
+       type(c_ptr), intent(out)  :: out
+       integer(c_int32_t)        :: afh_dist_group_create
+     end function afh_dist_group_create
+
+     function afh_dist_group_destroy(g) bind(C, name=afh_pfx//"dist_group_destroy")
+       import
+       type(c_ptr), value :: g
+       integer(c_int32_t) :: afh_dist_group_destroy
+     end function afh_dist_group_destroy
+
+     function afh_dist_rccl_unique_id(id128) bind(C, name=afh_pfx//"dist_rccl_unique_id")
+       import
+       type(c_ptr), value :: id128
+       integer(c_int32_t) :: afh_dist_rccl_unique_id
+     end function afh_dist_rccl_unique_id
+
+     function afh_dist_rccl_comm(id128, rank, n_ranks, device, comm) &
+          bind(C, name=afh_pfx//"dist_rccl_comm")
+       import
+       type(c_ptr), value        :: id128
+       integer(c_int32_t), value :: rank, n_ranks, device
+       type(c_ptr), intent(out)  :: comm
+       integer(c_int32_t)        :: afh_dist_rccl_comm
+     end function afh_dist_rccl_comm
+
+     function afh_dist_rccl_comm_destroy(comm) bind(C, name=afh_pfx//"dist_rccl_comm_destroy")
+       import
+       type(c_ptr), value :: comm
+       integer(c_int32_t) :: afh_dist_rccl_comm_destroy
+     end function afh_dist_rccl_comm_destroy
+
+     function afh_dist_create(t, desc, owner, rank, n_ranks, transport, group_or_comm, out) &
+          bind(C, name=afh_pfx//"dist_create")
+       import
+       type(c_ptr), value              :: t, group_or_comm
+       type(afh_tree_desc), intent(in) :: desc
+       integer(c_int32_t), intent(in)  :: owner(*)
+       integer(c_int32_t), value       :: rank, n_ranks, transport
+       type(c_ptr), intent(out)        :: out
+       integer(c_int32_t)              :: afh_dist_create
+     end function afh_dist_create
+
+     function afh_dist_destroy(d) bind(C, name=afh_pfx//"dist_destroy")
+       import
+       type(c_ptr), value :: d
+       integer(c_int32_t) :: afh_dist_destroy
+     end function afh_dist_destroy
+
+     function afh_dist_stats(d, n_exchanges, bytes) bind(C, name=afh_pfx//"dist_stats")
+       import
+       type(c_ptr), value              :: d
+       integer(c_int64_t), intent(out) :: n_exchanges, bytes
+       integer(c_int32_t)              :: afh_dist_stats
+     end function afh_dist_stats
 
      !> electrode_species_bc (src/streamer.f90:578-636) over the mg_lsf_box boxes
      function afh_electrode_species_bc(f, i_lsf, i_1pos_ion, neumann_zero, n_ids, ids) &
