@@ -223,6 +223,30 @@ inline unsigned long long host_dbl_to_ord(double x) {
   return (u & 0x8000000000000000ull) ? ~u : (u | 0x8000000000000000ull);
 }
 
+// A store of a kernel's output, streaming (nontemporal: no reuse expected
+// before eviction) when NT. The big per-level outputs are read back only by
+// the next kernel, from HBM anyway (a leaf level is GBs, the L2 + MALL a few
+// hundred MB). Per-kernel-class switches (-DAFH_NT_*=0 for plain stores),
+// measured with scripts/grad_ab.py / scripts/ab_bench.sh: S1-64 14.1-14.9
+// -> 13.9 ms/step over three alternating rounds:
+#ifndef AFH_NT_FLUX
+#define AFH_NT_FLUX 1
+#endif
+#ifndef AFH_NT_UPD
+#define AFH_NT_UPD 1
+#endif
+#ifndef AFH_NT_PAIR
+#define AFH_NT_PAIR 1
+#endif
+#ifndef AFH_NT_MG
+#define AFH_NT_MG 1
+#endif
+template <bool NT>
+__device__ __forceinline__ void st_nt(double *p, double v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
 // Workgroup b of n -> work item: workgroups are dispatched round-robin over
 // the 8 XCDs (b % 8); this gives each XCD a contiguous run of work items
 // (bijective for any n), so neighbouring boxes of a level list share an L2.

@@ -589,7 +589,7 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
 #pragma unroll
       for (int q = 0; q < G::OPTF; q++) {
         const int e = tid + NT * q;
-        if (e < NG * TJ) y[(size_t)k * SK + t0 + NG + e] = Pk[perm(NG + e)];
+        if (e < NG * TJ) st_nt<AFH_NT_PAIR>(y + ((size_t)k * SK + t0 + NG + e), Pk[perm(NG + e)]);
       }
     } else {
 #pragma unroll
@@ -597,7 +597,7 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
         const int e = tid + NT * q;
         if (e < NC * TJ) {
           const int c = (e / NC + 1) * NG + e % NC + 1;
-          y[(size_t)k * SK + t0 + c] = Pk[L(e / NC + 1, e % NC + 1)];
+          st_nt<AFH_NT_PAIR>(y + ((size_t)k * SK + t0 + c), Pk[L(e / NC + 1, e % NC + 1)]);
         }
       }
     }
@@ -958,7 +958,7 @@ __global__ void __launch_bounds__(256)
                        cf.c[3] * ym[q] + cf.c[4] * yp[q] + cf.c[5] * z[q] +
                        cf.c[6] * z[q + 2];
       const double v = r[q] - a;
-      tmp[o + c0 + q * sk] = v;
+      st_nt<AFH_NT_MG>(tmp + (o + c0 + q * sk), v);
       mx = fmax(mx, fabs(v));
     }
   }
@@ -1301,10 +1301,11 @@ __global__ void __launch_bounds__(256)
     // even q -> (P+q/2, P+q/2-1); a, b index pv from plane P-1
     const int a = (q & 1) ? (q + 1) / 2 : q / 2 + 1;
     const int b = (q & 1) ? (q + 3) / 2 : q / 2;
-    phi[c + q * sk] = ph[q] + (27 / 64.0) * pv[a][0] + (9 / 64.0) * pv[a][1] +
-                      (9 / 64.0) * pv[a][2] + (3 / 64.0) * pv[a][3] +
-                      (9 / 64.0) * pv[b][0] + (3 / 64.0) * pv[b][1] +
-                      (3 / 64.0) * pv[b][2] + (1 / 64.0) * pv[b][3];
+    st_nt<AFH_NT_MG>(phi + (c + q * sk),
+                     ph[q] + (27 / 64.0) * pv[a][0] + (9 / 64.0) * pv[a][1] +
+                         (9 / 64.0) * pv[a][2] + (3 / 64.0) * pv[a][3] +
+                         (9 / 64.0) * pv[b][0] + (3 / 64.0) * pv[b][1] +
+                         (3 / 64.0) * pv[b][2] + (1 / 64.0) * pv[b][3]);
   }
 }
 
@@ -1350,7 +1351,7 @@ __global__ void k_gradient(const double *__restrict__ phi,
 // Each thread owns a column of K cells in k: the K + 2 phi values of the
 // column are loaded once (the z differences of neighbouring cells share them),
 // and every load of the column is issued before the first store.
-template <int NC, int K>
+template <int NC, int K, bool NT = false>
 __global__ void __launch_bounds__(256)
     k_gradient_t(const double *__restrict__ phi, double *__restrict__ fcv,
                  double *__restrict__ nrm, const int32_t *__restrict__ ids,
@@ -1385,15 +1386,15 @@ __global__ void __launch_bounds__(256)
     const double fyl = iy * (pv - ym[q]), fyh = iy * (yp[q] - pv);
     const double fzl = iz * (pv - pc[q]), fzh = iz * (pc[q + 2] - pv);
     const size_t fb = ((size_t)(k - 1) * NF + (j - 1)) * NF + (i - 1);
-    f[fb] = fxl;
-    if (i == NC) f[fb + 1] = fxh;
-    f[D3 + fb] = fyl;
-    if (j == NC) f[D3 + fb + NF] = fyh;
-    f[2 * D3 + fb] = fzl;
-    if (k == NC) f[2 * D3 + fb + (size_t)NF * NF] = fzh;
+    st_nt<NT>(f + fb, fxl);
+    if (i == NC) st_nt<NT>(f + fb + 1, fxh);
+    st_nt<NT>(f + D3 + fb, fyl);
+    if (j == NC) st_nt<NT>(f + D3 + fb + NF, fyh);
+    st_nt<NT>(f + 2 * D3 + fb, fzl);
+    if (k == NC) st_nt<NT>(f + 2 * D3 + fb + (size_t)NF * NF, fzh);
     if (nb) {
       const double a = fxl + fxh, b = fyl + fyh, cc = fzl + fzh;
-      nb[c0 + q * SK] = 0.5 * sqrt(a * a + b * b + cc * cc);
+      st_nt<NT>(nb + c0 + q * SK, 0.5 * sqrt(a * a + b * b + cc * cc));
     }
   }
 }
@@ -1403,16 +1404,21 @@ __global__ void __launch_bounds__(256)
 #endif
 template <int NC>
 static void launch_gradient(afh_tree *t, const double *phi, double *fcv,
-                            double *nrm, double fac) {
+                            double *nrm, double fac, bool nt) {
   constexpr int R = 256 / NC < NC ? 256 / NC : NC;
   constexpr int K = NC >= AFH_GRAD_K ? AFH_GRAD_K : 1;
   for (int l = 1; l <= t->nlvl; l++) {
     const int n = t->ids.n(l);
     if (!n) continue;
     const double *dr = &t->lvl_dr[3 * (l - 1)];
-    hipLaunchKernelGGL((k_gradient_t<NC, K>), dim3((NC / R) * (NC / K), n),
-                       dim3(NC * R), 0, t->stream, phi, fcv, nrm, t->ids.at(l),
-                       t->bsz, t->fsz, fac / dr[0], fac / dr[1], fac / dr[2]);
+    if (nt)
+      hipLaunchKernelGGL((k_gradient_t<NC, K, true>), dim3((NC / R) * (NC / K), n),
+                         dim3(NC * R), 0, t->stream, phi, fcv, nrm, t->ids.at(l),
+                         t->bsz, t->fsz, fac / dr[0], fac / dr[1], fac / dr[2]);
+    else
+      hipLaunchKernelGGL((k_gradient_t<NC, K>), dim3((NC / R) * (NC / K), n),
+                         dim3(NC * R), 0, t->stream, phi, fcv, nrm, t->ids.at(l),
+                         t->bsz, t->fsz, fac / dr[0], fac / dr[1], fac / dr[2]);
   }
 }
 
@@ -1938,6 +1944,8 @@ struct afh_mg {
   bool pair_p3 = true;       // AFH_GSRB_PAIR_P3=0: four barriers per plane (NC = 64)
   bool pair_sp = true;       // AFH_GSRB_PAIR_SP=0: natural LDS row order (NC = 64)
   bool pair_box = true;      // AFH_GSRB_PAIR_BOX=0: plane-marching pair for NC <= 16
+  bool grad_nt = true;       // AFH_GRAD_NT: the gradient's face fields and |E| stored
+                             // nontemporal (streaming): -9 % on S1-64 (scripts/grad_ab.py)
   int pair_ks = 4;           // AFH_GSRB_PAIR_KS: k chunks on 64..255-box levels (NC = 64;
                              // 4 whole-box chunks, 44 quarter-box tiles x 4, 0 tiles)
   int wave_cells = CS_WAVE_CELLS;  // AFH_CS_WAVE_CELLS
@@ -2152,6 +2160,7 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
   if (const char *env = getenv("AFH_GRAPHS")) mg->use_graphs = atoi(env) != 0;
   if (const char *env = getenv("AFH_GSRB_PAIR_BOX")) mg->pair_box = atoi(env) != 0;
   if (const char *env = getenv("AFH_GSRB_PAIR_KS")) mg->pair_ks = atoi(env);
+  if (const char *env = getenv("AFH_GRAD_NT")) mg->grad_nt = atoi(env) != 0;
   if (const char *env = getenv("AFH_CS_WAVE_CELLS")) mg->wave_cells = atoi(env);
   if (fused_nc_ok(t->nc) && mg->fused_min > 0) {
     bool any = false;
@@ -2843,11 +2852,11 @@ int32_t afh_mg_compute_phi_gradient(afh_mg *mg, int32_t i_fc, double fac,
   const int ntot = t->ids.off[t->nlvl];
   double *nrm = i_norm > 0 ? t->ccv(i_norm) : nullptr;
   switch (nc) {
-  case 4: launch_gradient<4>(t, t->ccv(mg->d.i_phi), t->fcv(i_fc), nrm, fac); break;
-  case 8: launch_gradient<8>(t, t->ccv(mg->d.i_phi), t->fcv(i_fc), nrm, fac); break;
-  case 16: launch_gradient<16>(t, t->ccv(mg->d.i_phi), t->fcv(i_fc), nrm, fac); break;
-  case 32: launch_gradient<32>(t, t->ccv(mg->d.i_phi), t->fcv(i_fc), nrm, fac); break;
-  case 64: launch_gradient<64>(t, t->ccv(mg->d.i_phi), t->fcv(i_fc), nrm, fac); break;
+  case 4: launch_gradient<4>(t, t->ccv(mg->d.i_phi), t->fcv(i_fc), nrm, fac, mg->grad_nt); break;
+  case 8: launch_gradient<8>(t, t->ccv(mg->d.i_phi), t->fcv(i_fc), nrm, fac, mg->grad_nt); break;
+  case 16: launch_gradient<16>(t, t->ccv(mg->d.i_phi), t->fcv(i_fc), nrm, fac, mg->grad_nt); break;
+  case 32: launch_gradient<32>(t, t->ccv(mg->d.i_phi), t->fcv(i_fc), nrm, fac, mg->grad_nt); break;
+  case 64: launch_gradient<64>(t, t->ccv(mg->d.i_phi), t->fcv(i_fc), nrm, fac, mg->grad_nt); break;
   default:
   hipLaunchKernelGGL(k_gradient, dim3((n3 + 255) / 256, ntot), dim3(256), 0,
                      t->stream, t->ccv(mg->d.i_phi), t->fcv(i_fc),

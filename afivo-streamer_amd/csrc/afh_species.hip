@@ -797,7 +797,7 @@ __global__ void __launch_bounds__(AFH_FLUX_LDS_NT, AFH_FLUX_LDS_MINW)
       mu = mu * N_inv;
       dz = dcv * N_inv;
       vz = -mu * ezl;
-      F[2 * FD + fb] = vz * u - dz * iz * (z0 - zm1);
+      st_nt<AFH_NT_FLUX>(F + (2 * FD + fb), vz * u - dz * iz * (z0 - zm1));
       smax = fmax(smax, mu * u);
     }
     if (k > 1) {
@@ -815,7 +815,7 @@ __global__ void __launch_bounds__(AFH_FLUX_LDS_NT, AFH_FLUX_LDS_MINW)
       mu = mu * N_inv;
       dx = dcv * N_inv;
       vx = -mu * exl;
-      F[fb] = vx * u - dx * ix * (z0 - N0[cn - 1]);
+      st_nt<AFH_NT_FLUX>(F + (fb), vx * u - dx * ix * (z0 - N0[cn - 1]));
       smax = fmax(smax, mu * u);
     }
     double vxh = __shfl_down(vx, 1, 64), dxh = __shfl_down(dx, 1, 64);
@@ -825,7 +825,7 @@ __global__ void __launch_bounds__(AFH_FLUX_LDS_NT, AFH_FLUX_LDS_MINW)
       mu = mu * N_inv;
       dxh = dcv * N_inv;
       vxh = -mu * exh;
-      F[fb + 1] = vxh * u - dxh * ix * (N0[cn + 1] - z0);
+      st_nt<AFH_NT_FLUX>(F + (fb + 1), vxh * u - dxh * ix * (N0[cn + 1] - z0));
       smax = fmax(smax, mu * u);
     }
     // y low face
@@ -837,7 +837,7 @@ __global__ void __launch_bounds__(AFH_FLUX_LDS_NT, AFH_FLUX_LDS_MINW)
       mu = mu * N_inv;
       dy = dcv * N_inv;
       vy = -mu * eyl;
-      F[FD + fb] = vy * u - dy * iy * (z0 - N0[cn - RW]);
+      st_nt<AFH_NT_FLUX>(F + (FD + fb), vy * u - dy * iy * (z0 - N0[cn - RW]));
       smax = fmax(smax, mu * u);
     }
     sv[tid] = vy;
@@ -854,7 +854,7 @@ __global__ void __launch_bounds__(AFH_FLUX_LDS_NT, AFH_FLUX_LDS_MINW)
       mu = mu * N_inv;
       dyh = dcv * N_inv;
       vyh = -mu * eyh;
-      F[FD + fb + NF] = vyh * u - dyh * iy * (N0[cn + RW] - z0);
+      st_nt<AFH_NT_FLUX>(F + (FD + fb + NF), vyh * u - dyh * iy * (N0[cn + RW] - z0));
       smax = fmax(smax, mu * u);
     } else {
       lds_mu_dc(T, A.td, 0.5 * (e0 + E0p[ce + EW]) * 1e21 * N_inv, mu, dcv);
@@ -876,7 +876,7 @@ __global__ void __launch_bounds__(AFH_FLUX_LDS_NT, AFH_FLUX_LDS_MINW)
       lds_mu_dc(T, A.td, 0.5 * (e0 + ep1) * 1e21 * N_inv, mu, dcv);
       mu = mu * N_inv;
       const double dh = dcv * N_inv, vh = -mu * ezh;
-      F[2 * FD + fb + FSK] = vh * u - dh * iz * (zp1 - z0);
+      st_nt<AFH_NT_FLUX>(F + (2 * FD + fb + FSK), vh * u - dh * iz * (zp1 - z0));
       smax = fmax(smax, mu * u);
       const double mv = fmax(fabs(vh), fabs(vz_lo));
       const double md = fmax(dh, dz_lo);
@@ -1068,13 +1068,13 @@ __global__ void __launch_bounds__(256, AFH_UPD_MINW)
     for (int s = 0; s < NS; s++)
       if (s == A.e_index) y[s] = y[s] + div + dvy + dvz;
 #pragma unroll
-    for (int s = 0; s < NS; s++) A.out[s][x] = y[s];
+    for (int s = 0; s < NS; s++) st_nt<AFH_NT_UPD>(A.out[s] + x, y[s]);
     if (A.rhs) {
       double r = 0.0;
 #pragma unroll
       for (int s = 0; s < NS; s++)
         if (A.rq[s] != 0.0) r = r + A.rq[s] * y[s];
-      A.rhs[x] = r;
+      st_nt<AFH_NT_UPD>(A.rhs + x, r);
       rmax = fabs(r);
     }
   }
