@@ -255,6 +255,21 @@ __device__ __forceinline__ int xcd_swizzle(int b, int n) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + slot;
 }
 
+// A 2-D grid (the blocks of a box in x, the boxes of a level list in y)
+// remapped by xcd_swizzle: the blocks of a box run on one XCD, in order, so
+// the planes and rows that neighbouring blocks both read meet in one L2.
+// Used where it measured faster (k_gradient_t -8 %; k_flux_lds's 1-D tiles
+// -1 %); k_update, k_residual, k_prolong and k_rstr_fas measured 2-8 %
+// slower with it (scripts/ab_kernels.sh) and keep the hardware order.
+struct Blk {
+  int x, y;
+};
+__device__ __forceinline__ Blk xcd_block() {
+  const int gx = gridDim.x;
+  const int w = xcd_swizzle(blockIdx.y * gx + blockIdx.x, gx * gridDim.y);
+  return {w % gx, w / gx};
+}
+
 __device__ __forceinline__ size_t ix3(int ng, int i, int j, int k) {
   return ((size_t)k * ng + j) * ng + i;
 }

@@ -1359,10 +1359,11 @@ __global__ void __launch_bounds__(256)
   constexpr int R = 256 / NC < NC ? 256 / NC : NC;  // rows per block
   constexpr int NG = NC + 2, NF = NC + 1;
   constexpr size_t SJ = NG, SK = (size_t)NG * NG, D3 = (size_t)NF * NF * NF;
+  const Blk B = xcd_block();
   const int i = threadIdx.x % NC + 1;
-  const int j = (blockIdx.x % (NC / R)) * R + threadIdx.x / NC + 1;
-  const int k0 = (blockIdx.x / (NC / R)) * K + 1;
-  const int id = ids[blockIdx.y];
+  const int j = (B.x % (NC / R)) * R + threadIdx.x / NC + 1;
+  const int k0 = (B.x / (NC / R)) * K + 1;
+  const int id = ids[B.y];
   const double *p = phi + (size_t)(id - 1) * bsz;
   double *f = fcv + (size_t)(id - 1) * fsz;
   double *nb = nrm ? nrm + (size_t)(id - 1) * bsz : nullptr;

@@ -701,10 +701,11 @@ __global__ void __launch_bounds__(AFH_FLUX_LDS_NT, AFH_FLUX_LDS_MINW)
   __shared__ double sv[NT], sd[NT];
   __shared__ double r1[NT / 64], r2[NT / 64];
   const int tid = threadIdx.x;
-  const int id = ids[blockIdx.x / G::NTILE];
+  const int wg = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int id = ids[wg / G::NTILE];
   const int i = tid % NC + 1;
   const int jr = tid / NC;
-  const int j0 = (blockIdx.x % G::NTILE) * TJ + 1, j = j0 + jr;
+  const int j0 = (wg % G::NTILE) * TJ + 1, j = j0 + jr;
   const double *ne = A.ne + (size_t)(id - 1) * bsz;
   const double *E = A.E + (size_t)(id - 1) * bsz;
   const double *Ef = A.Ef + (size_t)(id - 1) * fsz;
