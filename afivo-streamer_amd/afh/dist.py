@@ -398,6 +398,17 @@ class NativeGroup:
             self.h = C.c_void_p()
 
 
+def broadcast_bytes(data, src=0):
+    """Rank src's bytes on every rank of the torch.distributed group (a device
+    tensor under the nccl backend, which carries no host tensors)."""
+    import torch
+    import torch.distributed as tdist
+    dev = "cuda" if tdist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor(list(data), dtype=torch.uint8, device=dev)
+    tdist.broadcast(t, src=src)
+    return bytes(t.cpu().tolist())
+
+
 def rccl_comm(lib, rank, n_ranks, device):
     """An RCCL communicator for the library's AFH_DIST_RCCL transport; the
     unique id travels over the torch.distributed process group."""
@@ -405,11 +416,7 @@ def rccl_comm(lib, rank, n_ranks, device):
     if rank == 0:
         lib.call("dist_rccl_unique_id", C.cast(uid, C.c_void_p))
     if n_ranks > 1:
-        import torch
-        import torch.distributed as tdist
-        t = torch.tensor(list(uid), dtype=torch.uint8)
-        tdist.broadcast(t, src=0)
-        uid = (C.c_uint8 * 128)(*t.tolist())
+        uid = (C.c_uint8 * 128)(*broadcast_bytes(bytes(uid)))
     comm = C.c_void_p()
     lib.call("dist_rccl_comm", C.cast(uid, C.c_void_p), rank, n_ranks, device, C.byref(comm))
     return comm

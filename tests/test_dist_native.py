@@ -187,6 +187,33 @@ def test_native_sharded_hip_local_bitwise(name, world):
     _compare(ref, shards, parts)
 
 
+def _bcast_worker(rank, world, port, outdir):
+    import os
+    import torch.distributed as dist
+    from afh.dist import broadcast_bytes
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        data = bytes(range(128)) if rank == 0 else bytes(128)
+        got = broadcast_bytes(data)
+        with open(os.path.join(outdir, "r%d" % rank), "wb") as f:
+            f.write(got)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_unique_id_broadcast_gloo(tmp_path):
+    """The RCCL unique id (128 bytes) reaches every rank over the process
+    group (rccl_comm; gloo here, device tensors under nccl)."""
+    import torch.multiprocessing as mp
+    from test_dist import _free_port
+    mp.start_processes(_bcast_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2,
+                       start_method="spawn", join=True)
+    for r in range(2):
+        assert (tmp_path / ("r%d" % r)).read_bytes() == bytes(range(128))
+
+
 @pytest.mark.gpu
 def test_native_rccl_single_rank_bitwise():
     lib = capi.hip_library()
