@@ -2471,6 +2471,10 @@ static int32_t gsrb_boxes(afh_mg *mg, int lvl, bool up) {
   return AFH_OK;
 }
 
+#ifndef AFH_RES_K  // cells per thread column of k_residual (8, 4 or 2)
+#define AFH_RES_K 4
+#endif
+
 static int32_t update_coarse(afh_mg *mg, int lvl) {
   afh_tree *t = mg->t;
   const int nc = t->nc, hn = nc / 2;
@@ -2727,10 +2731,12 @@ static int32_t residual_levels(afh_mg *mg, int max_lvl, bool max_out) {
       const int n = L.n(lvl);
       const bool mx = max_out && !part;
       if (n) {
-        const bool k4 = nc % 4 == 0;
-        const dim3 grid((n3 / (k4 ? 4 : 2) + 255) / 256, n);
-        auto kern = mx ? (k4 ? k_residual<true, 4> : k_residual<true, 2>)
-                       : (k4 ? k_residual<false, 4> : k_residual<false, 2>);
+        const int kc = nc % AFH_RES_K == 0 ? AFH_RES_K : nc % 4 == 0 ? 4 : 2;
+        const dim3 grid((n3 / kc + 255) / 256, n);
+        auto kern = mx ? (kc == 8 ? k_residual<true, 8> : kc == 4 ? k_residual<true, 4>
+                                                                  : k_residual<true, 2>)
+                       : (kc == 8 ? k_residual<false, 8> : kc == 4 ? k_residual<false, 4>
+                                                                   : k_residual<false, 2>);
         hipLaunchKernelGGL(kern, grid, dim3(256), 0, t->stream,
                            t->ccv(mg->d.i_phi), t->ccv(mg->d.i_rhs),
                            t->ccv(mg->d.i_tmp), L.at(lvl), nc, t->bsz, cf, red);
