@@ -130,9 +130,12 @@ class Simulation:
     """One streamer simulation (src/streamer.f90) over a C-ABI library."""
 
     def __init__(self, lib, case, device=-1, coarse_cycles=0, capacity_factor=2.0,
-                 fuse_rhs=True):
+                 fuse_rhs=True, user=None):
+        """user: the program's m_user hooks (afh.users), e.g. the gas density
+        function and initial conditions of programs/3d_sprite."""
         c = case if isinstance(case, Case) else Case(case)
         self.c, self.lib, self.device = c, lib, device
+        self.user = user
         self.coarse_cycles = coarse_cycles
         self.capacity_factor = capacity_factor
         self.fused_rhs = fuse_rhs
@@ -141,10 +144,18 @@ class Simulation:
         self.n_states = 2  # af_advance_num_steps(af_heuns_method)
         if c.i("use_electrode") or c.i("use_dielectric") or c.i("cylindrical"):
             raise NotImplementedError("electrode / dielectric / cylindrical cases")
-        if not c.i("gas_constant_density"):
-            raise NotImplementedError("variable gas density cases")
         # registry (af_add_cc_variable order of the reference's modules)
         self.cc_names = c.sa("cc_names")
+        # gas density given by a function (streamer.f90:86-95 with
+        # user_gas_density, m_gas.f90:146-148): the cc variable "M", set on
+        # every cell of a box (ghosts included) when the box is created
+        # (set_gas_density_from_user_function, streamer.f90:672-681)
+        self.i_gas_dens = 0
+        if not c.i("gas_constant_density"):
+            if user is None or not hasattr(user, "gas_density"):
+                raise NotImplementedError("a variable gas density needs the user's gas_density")
+            self.i_gas_dens = list(self.cc_names).index("M") + 1
+            self.gas_fractions = list(c.ra("gas_fractions"))
         self.n_var_cell, self.n_var_face = len(self.cc_names), len(c.sa("fc_names"))
         (self.i_phi, self.i_electron, self.i_1pos_ion, self.i_efld, self.i_rhs,
          self.i_tmp, self.i_photo, self.f_flux, self.f_field, _) = c.ia("ivars")
@@ -191,7 +202,11 @@ class Simulation:
             rt, _, n_coeff, lti, _ = c.ia("reaction_%d" % n)
             if n_coeff > 4:
                 raise NotImplementedError("rate with %d coefficients" % n_coeff)
-            shift = lambda ix: [x - self.n_gas for x in ix]  # noqa: E731
+            # constant N: the gas species are folded into the rate factors
+            # (m_chemistry.f90:1086-1099) and leave the index space; variable
+            # N: they stay first, the library gives them gas_fractions * N
+            shift = ((lambda ix: [x - self.n_gas for x in ix]) if not self.i_gas_dens
+                     else (lambda ix: list(ix)))
             self.reactions.append({
                 "rate_type": rt, "table_col": lti,
                 "rate_factor": c.r("reaction_%d_factor" % n),
@@ -254,7 +269,9 @@ class Simulation:
             gas_temperature=c.r("gas_temperature_value"),
             td_energy_col=max(0, td_cols[4]),
             i_photo=self.i_photo if self.photoi else 0,
-            photo_species=self.photo_species if self.photoi else 0)
+            photo_species=self.photo_species if self.photoi else 0,
+            i_gas_dens=self.i_gas_dens,
+            gas_fractions=self.gas_fractions if self.i_gas_dens else ())
         if self.fused_rhs:
             self.fluid.set_rhs_output(self.i_rhs, True)
 
@@ -419,6 +436,8 @@ class Simulation:
             old = self.tree
             self._bind(new)
             old.close()
+            if self.i_gas_dens and info.n_add:  # m_af_core.f90:866-869
+                self._set_gas([b for l in sorted(info.add) for b in info.add[l]])
         return info
 
     # -------------------------------------------------- initial state
@@ -453,9 +472,33 @@ class Simulation:
             ne[b - 1] = e.reshape(ng, ng, ng)
             ni[b - 1] = p.reshape(ng, ng, ng)
 
+    def box_cells(self, b):
+        """af_r_cc of every cell 0..nc+1 of box b, (ng^3, 3), i fastest."""
+        ng = self.af.nc + 2
+        idx = np.arange(ng) - 0.5
+        rmin, dr = self.af.r_min[b], self.af.dr[b]
+        zz, yy, xx = np.meshgrid(rmin[2] + idx * dr[2], rmin[1] + idx * dr[1],
+                                 rmin[0] + idx * dr[0], indexing="ij")
+        return np.stack([xx.ravel(), yy.ravel(), zz.ravel()], axis=1)
+
+    def _set_gas(self, ids):
+        """set_gas_density_from_user_function (streamer.f90:672-681) on boxes ids."""
+        ng = self.af.nc + 2
+        a = self.tree.get_cc(self.i_gas_dens)
+        for b in ids:
+            a[b - 1] = self.user.gas_density(self.box_cells(b)).reshape(ng, ng, ng)
+        self.tree.put_cc(self.i_gas_dens, a)
+
     def _set_init(self, ids):
         arrays = {iv: self.tree.get_cc(iv) for iv in (self.i_electron, self.i_1pos_ion)}
         self.init_cond_set_box(ids, arrays)
+        if self.user is not None and hasattr(self.user, "initial_conditions"):
+            # user_initial_conditions after init_cond_set_box (streamer.f90:472-475)
+            ng = self.af.nc + 2
+            for b in ids:
+                ne, ni = self.user.initial_conditions(self, self.box_cells(b))
+                arrays[self.i_electron][b - 1] = ne.reshape(ng, ng, ng)
+                arrays[self.i_1pos_ion][b - 1] = ni.reshape(ng, ng, ng)
         for iv, a in arrays.items():
             self.tree.put_cc(iv, a)
 
@@ -470,6 +513,8 @@ class Simulation:
         self._bind(self._create_tree())
         all_ids = [b for l in range(1, self.af.highest_lvl + 1)
                    for b in self.af.lvls[l]["ids"]]
+        if self.i_gas_dens:
+            self._set_gas(all_ids)
         self._set_init(all_ids)
         for _ in range(100):
             self.field_compute(0, have_guess=False)
@@ -558,7 +603,8 @@ class Simulation:
         for a CPU baseline): topology, every cell and face variable, time."""
         import copy
         other = Simulation(lib, self.c, device=device, coarse_cycles=self.coarse_cycles,
-                           capacity_factor=self.capacity_factor, fuse_rhs=self.fused_rhs)
+                           capacity_factor=self.capacity_factor, fuse_rhs=self.fused_rhs,
+                           user=self.user)
         other.af = copy.deepcopy(self.af)
         for k in ("it", "time", "global_time", "photoi_prev_time", "global_dt", "dt",
                   "output_cnt", "time_last_output"):

@@ -1458,7 +1458,7 @@ __global__ void __launch_bounds__(256, AFH_FE_MINW)
 
 
 // ------------------------------------------------------------ refinement
-// default_refinement (src/m_refine.f90:198-298, constant gas density) per
+// default_refinement (src/m_refine.f90:198-298; N per cell with a variable gas density) per
 // cell, reduced per box as cell_to_ref_flags (m_af_core.f90:1095-1148):
 // one workgroup per box; the box-level rules are applied per cell in the
 // reference's order. Same expressions as oracle/c/afo.c refine_cell.
@@ -1467,6 +1467,7 @@ struct RefineArgs {
   DevLT td;
   double N;
   const double *ne, *E;
+  const double *Ng;     // gas density per cell (variable N), or null
   const uint8_t *elec;  // per box, or null
 };
 
@@ -1516,7 +1517,7 @@ __global__ void __launch_bounds__(256)
     int i, j, k;
     cell3(t, nc, i, j, k);
     const size_t x = (size_t)(id - 1) * bsz + ix3(nc + 2, i, j, k);
-    const double gas_dens = A.N;
+    const double gas_dens = A.Ng ? A.Ng[x] : A.N;  // m_refine.f90:219-223
     const double fld = A.E[x] * 1e21 / gas_dens;
     double alpha;
     if (p.use_alpha_effective) {
@@ -2302,6 +2303,7 @@ int32_t afh_refine_flags(afh_fluid *f, const afh_refine_desc *d,
   A.d = *d;
   A.td = f->td;
   A.N = f->d.gas_number_density;
+  A.Ng = f->d.i_gas_dens > 0 ? t->ccv(f->d.i_gas_dens) : nullptr;
   A.ne = t->ccv(d->i_electron);
   A.E = t->ccv(d->i_efld);
   A.elec = d_elec;

@@ -43,7 +43,14 @@ CONFIGS = {
     # the reference's own initializers; afh.driver builds the tree on the
     # device)
     "s3": (8, None, None, (16e-3, 16e-3, 16e-3)),
+    # BASELINE.json config 5: programs/3d_sprite/sprite_3d.cfg -- sprite
+    # chemistry (10 species, 12 reactions), the exponential atmosphere of its
+    # m_user.f90 as a variable gas density, Helmholtz photoionization every
+    # photoi%per_steps time steps, the 8-level AMR tree of 8^3 boxes its
+    # initial refinement builds (tests/golden/case_s5.npz, afh.users.Sprite3D)
+    "s5": (8, None, None, (5e3, 5e3, 20e3)),
 }
+DRIVER_CONFIGS = ("s3", "s5")
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E peak (spec)
 
 
@@ -84,6 +91,8 @@ def unit_step(case, dt, k):
     flux_update_densities). Even k: stage 1 (state 0 -> 1); odd k: stage 2
     (states 0, 1 -> 0, with the chemistry dt limit). Returns the residuals and
     dt limits."""
+    if hasattr(case, "pre_step"):
+        case.pre_step(k)
     if k % 2 == 0:
         res = case.field_compute(0, n_vcycles=1)
         d = case.species_step(dt, 0, [0], [1.0], 1, False)
@@ -111,21 +120,30 @@ class DriverCase:
     def species_step(self, dt, s_deriv, s_prev, w_prev, s_out, last):
         return self.sim.fluid.forward_euler(dt, s_deriv, s_prev, w_prev, s_out, last)
 
+    def pre_step(self, k):
+        """photoi_set_src every photoi%per_steps time steps (streamer.f90:
+        230-234), i.e. every 2 * per_steps unit steps."""
+        sim = self.sim
+        if sim.photoi and k % (2 * sim.c.i("photoi%per_steps")) == 0:
+            sim.photoi_set_src()
+
     def fuse_rhs(self, on=True, ghosts=False):
         self.sim.fluid.set_rhs_output(self.sim.i_rhs if on else 0, ghosts)
         self.sim.fused_rhs = on
 
 
-def build_driver_case(lib, device):
+def build_driver_case(lib, device, config="s3"):
     import golden
     from afh.driver import Simulation
-    sim = Simulation(lib, golden.load("case_s3"), device=device)
+    from afh.users import USERS
+    sim = Simulation(lib, golden.load("case_" + config), device=device,
+                     user=USERS.get(config))
     sim.set_initial_conditions()
     return sim
 
 
-def cpu_baseline_driver(sim, steps=2):
-    """The C oracle on the same S3 state (the tree built on the device, every
+def cpu_baseline_driver(sim, steps=2, config="s3"):
+    """The C oracle on the same S3 / S5 state (the tree built on the device, every
     variable copied over), `steps` unit steps."""
     from afh import capi
     osim = sim.clone(capi.oracle_library())
@@ -139,8 +157,8 @@ def cpu_baseline_driver(sim, steps=2):
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     return {"value": ncell * steps / dt, "unit": "cell-updates/s", "cores": threads,
             "kind": "port",
-            "sample": "%d steps of the full S3 workload (%d leaf cells), C oracle "
-                      "OpenMP" % (steps, ncell)}
+            "sample": "%d steps of the full %s workload (%d leaf cells), C oracle "
+                      "OpenMP" % (steps, config.upper(), ncell)}
 
 
 def cpu_baseline(config, coarse_cycles, steps=2):
@@ -227,10 +245,11 @@ def main():
     from afh import capi
     lib = capi.hip_library()
     sharded = world > 1 and not args.replicas
-    if args.config == "s3":
+    if args.config in DRIVER_CONFIGS:
         if sharded:
-            raise SystemExit("s3: sharding an AMR driver tree is not supported; use --replicas")
-        sim = build_driver_case(lib, local)
+            raise SystemExit("%s: sharding an AMR driver tree is not supported; use --replicas"
+                             % args.config)
+        sim = build_driver_case(lib, local, args.config)
         case = DriverCase(sim)
     else:
         case = build_case(lib, args.config, local, args.coarse_cycles,
@@ -330,8 +349,15 @@ def main():
         if args.config == "s3":
             out["config"]["chemistry"] = "air_chemistry_v2 (9 species, 25 reactions)"
             out["config"]["coarse_solve"] = "direct"
+        if args.config == "s5":
+            out["config"]["chemistry"] = "sprite_chemistry_v0 (10 species, 12 reactions)"
+            out["config"]["gas_density"] = "variable (3d_sprite m_user: 2.5e25 exp(-z/7.2 km))"
+            out["config"]["photoionization"] = ("Helmholtz Bourdon-3, every %d time steps"
+                                                % sim.c.i("photoi%per_steps"))
+            out["config"]["coarse_solve"] = "direct"
         if not args.no_cpu_baseline and world == 1:
-            out["cpu_baseline"] = (cpu_baseline_driver(sim) if args.config == "s3" else
+            out["cpu_baseline"] = (cpu_baseline_driver(sim, config=args.config)
+                                   if args.config in DRIVER_CONFIGS else
                                    cpu_baseline(args.config, args.coarse_cycles))
         print(json.dumps(out))
     if dist is not None:

@@ -2582,7 +2582,9 @@ static int refine_cell(afh_fluid *fl, const afh_refine_desc *p, int id, int elec
     if (b->dr[d] > max_dx) max_dx = b->dr[d];
   }
   size_t x = IX(t, i, j, k);
-  double gas_dens = fl->d.gas_number_density;
+  /* m_refine.f90:219-223: the cell's gas density when it varies */
+  double gas_dens = fl->d.i_gas_dens > 0 ? ccb(t, fl->d.i_gas_dens, id)[x]
+                                         : fl->d.gas_number_density;
   double fld = ccb(t, p->i_efld, id)[x] * 1e21 / gas_dens;  /* SI_to_Townsend */
   double alpha;
   if (p->use_alpha_effective) {

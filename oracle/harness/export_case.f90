@@ -1,3 +1,4 @@
+#include "cpp_macros.h"
 !> ORACLE TEST INFRASTRUCTURE (build container only).
 !>
 !> export_case: set up the reference's streamer modules from a .cfg file exactly
@@ -36,6 +37,7 @@ program export_case
   use m_table_data
   use m_model
   use m_lookup_table
+  use m_user_methods
   implicit none
 
   type(CFG_t) :: cfg
@@ -46,11 +48,16 @@ program export_case
   real(dp), allocatable :: flds(:), rates(:, :)
   real(dp) :: out_dt = 1.0e-10_dp
   logical  :: out_rtest = .false.
+  character(len=32) :: user_gas = ""
 
   call get_command_argument(1, out_file)
   ! CFG_update_from_arguments skips nothing: shift the output file away by
   ! reading the remaining arguments ourselves
   call read_cfg_args(cfg)
+  ! --user-gas=sprite: programs/3d_sprite's user_initialize sets
+  ! user_gas_density (3d_sprite/m_user.f90:24-30), which makes gas_initialize
+  ! register the gas density variable "M" (m_gas.f90:146-148)
+  if (user_gas == "sprite") user_gas_density => sprite_gas_density
 
   ! initialize_modules (src/streamer.f90:429-458)
   call model_initialize(cfg)
@@ -188,13 +195,25 @@ program export_case
 
 contains
 
+  !> gas_density of programs/3d_sprite/m_user.f90:34-40 (exponential
+  !> atmosphere, scale height 7.2 km)
+  pure real(dp) function sprite_gas_density(box, IJK)
+    type(box_t), intent(in) :: box
+    integer, intent(in)     :: IJK
+    real(dp)                :: rr(NDIM)
+    rr = af_r_cc(box, [IJK])
+    sprite_gas_density = 2.5e25_dp * exp(-rr(NDIM) / 7.2e3_dp)
+  end function sprite_gas_density
+
   subroutine read_cfg_args(cfg)
     type(CFG_t), intent(inout) :: cfg
     integer :: n, ix
     character(len=1024) :: arg
     do n = 2, command_argument_count()
        call get_command_argument(n, arg)
-       if (arg(1:1) == '-') then
+       if (arg(1:11) == "--user-gas=") then
+          user_gas = trim(arg(12:))
+       else if (arg(1:1) == '-') then
           ix = index(arg, '=')
           call CFG_update_from_line(cfg, trim(arg(2:)))
        else

@@ -20,7 +20,7 @@
 !> unresolved (--unresolved-symbols=ignore-in-object-files) instead of
 !> providing anything in their place.
 !>
-!> Usage: replay_step <record_file> <out_file> <cfg> [-key=value ...]
+!> Usage: replay_step <record_file> <out_file> <cfg> [-key=value ...] [--user-gas=sprite]
 !> Record (stream, little endian): int32 highest_id, n_var_cell, n_var_face,
 !> nc; per id: int32 parent, lvl, ix(3), in_use; float64 dt, time; int32
 !> s_deriv, n_prev, s_prev(n_prev); float64 w_prev(n_prev); int32 s_out;
@@ -43,6 +43,7 @@ program replay_step
   use m_table_data
   use m_model
   use m_fluid
+  use m_user_methods
   implicit none
 
   type(CFG_t)        :: cfg
@@ -60,7 +61,12 @@ program replay_step
   call get_command_argument(2, out_file)
   do n = 3, command_argument_count()
      call get_command_argument(n, arg)
-     if (arg(1:1) == '-') then
+     if (arg(1:11) == "--user-gas=") then
+        ! programs/3d_sprite's user_initialize (m_user.f90:24-30): the gas
+        ! density "M" is a cc variable (m_gas.f90:146-148); its values come
+        ! from the record
+        if (trim(arg(12:)) == "sprite") user_gas_density => sprite_gas_density
+     else if (arg(1:1) == '-') then
         call CFG_update_from_line(cfg, trim(arg(2:)))
      else
         call CFG_read_file(cfg, trim(arg))
@@ -155,6 +161,15 @@ program replay_step
   close(uo)
 
 contains
+
+  !> gas_density of programs/3d_sprite/m_user.f90:34-40
+  pure real(dp) function sprite_gas_density(box, IJK)
+    type(box_t), intent(in) :: box
+    integer, intent(in)     :: IJK
+    real(dp)                :: rr(NDIM)
+    rr = af_r_cc(box, [IJK])
+    sprite_gas_density = 2.5e25_dp * exp(-rr(NDIM) / 7.2e3_dp)
+  end function sprite_gas_density
 
   !> Refine the boxes the record lists as parents
   subroutine refine_as_recorded(box, cell_flags)

@@ -12,7 +12,7 @@ that cfg (<name>_rtest.log: it, time, dt, volume-averaged sums and maxima of
 every species per output time; the expected output) into
 tests/golden/rtest_<name>.npz. Only numbers and names are stored.
 
-    make -C oracle _ref/export_case && python3 oracle/make_cases.py
+    make -C oracle _ref/export_case && python3 oracle/make_cases.py [name ...]
 """
 import os
 import subprocess
@@ -28,7 +28,12 @@ CASES = ["test_3d", "test_3d_chem", "test_3d_photoi_chem"]
 # air_chemistry_v2 (9 species, 25 reactions); no regression log
 EXTRA = {"s3": ("/root/reference/programs/standard_3d", "streamer_3d.cfg",
                 ["-input_data%file=../../transport_data/air_chemistry_v2.txt",
-                 "-input_data%old_style=f"])}
+                 "-input_data%old_style=f"]),
+         # BASELINE.json config 5: programs/3d_sprite/sprite_3d.cfg
+         # (sprite_chemistry_v0, Helmholtz photoionization, the gas density
+         # of its m_user.f90: an exponential atmosphere, so the "M" variable)
+         "s5": ("/root/reference/programs/3d_sprite", "sprite_3d.cfg",
+                ["--user-gas=sprite"])}
 
 
 def parse_dump(path):
@@ -57,7 +62,10 @@ def main():
     exe = os.path.join(HERE, "_ref", "export_case")
     if not os.path.exists(exe):
         sys.exit("build oracle/_ref/export_case first (make -C oracle _ref/export_case)")
+    only = set(sys.argv[1:])
     for name in CASES:
+        if only and name not in only:
+            continue
         dump = "/tmp/afh_export_%s.txt" % name
         subprocess.run([exe, dump, name + ".cfg"], cwd=TESTS, check=True,
                        stdout=subprocess.DEVNULL)
@@ -72,6 +80,8 @@ def main():
         os.remove(dump)
         print("wrote", out, len(d), "arrays")
     for name, (cwd, cfg, extra) in EXTRA.items():
+        if only and name not in only:
+            continue
         dump = "/tmp/afh_export_%s.txt" % name
         subprocess.run([exe, dump, cfg] + extra, cwd=cwd, check=True,
                        stdout=subprocess.DEVNULL)

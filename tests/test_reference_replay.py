@@ -172,3 +172,23 @@ def test_species_step_replay_s3(tmp_path):
                   cfg_args=["streamer_3d.cfg",
                             "-input_data%file=../../transport_data/air_chemistry_v2.txt",
                             "-input_data%old_style=f"])
+
+
+def test_species_step_replay_s5(tmp_path):
+    """BASELINE config 5 (programs/3d_sprite/sprite_3d.cfg: sprite_chemistry_v0,
+    Helmholtz photoionization, the exponential atmosphere of its m_user.f90 as
+    the gas density variable "M"): after the initial refinement and three time
+    steps, Heun stages 1 and 2 -- with the photoionization source -- bitwise
+    equal to the reference's forward_euler with a variable gas density (1/N
+    per face, E/N and gas species densities per cell)."""
+    from afh.driver import Simulation as Sim
+    from afh.users import Sprite3D
+    sim = Sim(capi.oracle_library(), golden.load("case_s5"), user=Sprite3D)
+    sim.start()
+    for _ in range(3):
+        sim.step()
+    args = ["sprite_3d.cfg", "--user-gas=sprite"]
+    cwd = "/root/reference/programs/3d_sprite"
+    _replay_state(sim, "s5", 0, [0], [1.0], 1, 1e-12, tmp_path, cwd=cwd, cfg_args=args)
+    _replay_state(sim, "s5", 1, [0, 1], [0.5, 0.5], 0, 5e-13, tmp_path, cwd=cwd,
+                  cfg_args=args)

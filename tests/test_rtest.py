@@ -132,3 +132,45 @@ def test_s3_species_step_hip_equals_oracle():
             a, b = sim.tree.get_cc(iv + st), osim.tree.get_cc(iv + st)
             rel = np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300)
             assert rel <= 1e-13, (sim.cc_names[iv + st - 1], rel)
+
+
+@pytest.mark.gpu
+def test_s5_sprite_hip_equals_oracle():
+    """BASELINE config 5 (sprite_3d.cfg: variable gas density, sprite
+    chemistry, Helmholtz photoionization) on the device driver: after the
+    initial refinement and three steps on the GPU, the same state on the C
+    oracle (whose species step is the reference's forward_euler bitwise,
+    test_reference_replay) -- the photoionization source to 1e-12; Heun
+    stage 1 with fluxes and CFL / dielectric limits bitwise, stage 2 (on
+    stage-1 densities that may differ in the last ulp: exp in the rate forms,
+    ocml vs glibc) to 1e-12, densities to 1e-12; the refinement flags (E/N
+    per cell) equal."""
+    from afh.users import Sprite3D
+    sim = Simulation(capi.hip_library(), golden.load("case_s5"), device=0, user=Sprite3D)
+    sim.start()
+    for _ in range(3):
+        sim.step()
+    assert sim.af.highest_lvl >= 6
+    osim = sim.clone(capi.oracle_library())
+    for s in (sim, osim):
+        s.photoi_set_src()
+    a, b = sim.tree.get_cc(sim.i_photo), osim.tree.get_cc(osim.i_photo)
+    assert np.max(np.abs(a - b)) <= 1e-12 * np.max(np.abs(b))
+    x = [s.fluid.forward_euler(1e-12, 0, [0], [1.0], 1, False) for s in (sim, osim)]
+    assert list(x[0])[:2] == list(x[1])[:2]
+    for iv in range(1, sim.n_var_face + 1):  # stage 1 reads state 0: identical inputs
+        assert np.array_equal(sim.tree.get_fc(iv), osim.tree.get_fc(iv))
+    # stage 2 reads state 1, whose densities may differ in the last ulp
+    y = [s.fluid.forward_euler(5e-13, 1, [0, 1], [0.5, 0.5], 0, True) for s in (sim, osim)]
+    assert np.allclose(list(y[0]), list(y[1]), rtol=1e-12, atol=0)
+    for iv in range(1, sim.n_var_face + 1):
+        a, b = sim.tree.get_fc(iv), osim.tree.get_fc(iv)
+        assert np.max(np.abs(a - b)) <= 1e-12 * np.max(np.abs(b))
+    for iv in sim.densities:
+        for st in (0, 1):
+            a, b = sim.tree.get_cc(iv + st), osim.tree.get_cc(iv + st)
+            rel = np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300)
+            assert rel <= 1e-12, (sim.cc_names[iv + st - 1], rel)
+    fa = sim.fluid.refine_flags(sim.refine_desc())
+    fb = osim.fluid.refine_flags(osim.refine_desc())
+    assert np.array_equal(fa[0], fb[0]) and np.array_equal(fa[1], fb[1])
