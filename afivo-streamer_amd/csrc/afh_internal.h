@@ -102,7 +102,10 @@ struct afh_tree {
   // smoother's spare phi image (variable 0 in hooks and plans), plans
   afh_hook_fn hook = nullptr;
   void *hook_ctx = nullptr;
+  // shared by every multigrid on the tree (one stream: the image is only
+  // live inside one fused pair); freed with the last of them
   double *alt = nullptr;
+  int alt_refs = 0;
   struct Plan {
     int32_t *d_reg = nullptr;  // n x 7 (id, lo[3], hi[3])
     int64_t *d_off = nullptr;  // n + 1 value offsets

@@ -2167,10 +2167,14 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
     bool any = false;
     for (int l = 2; l <= t->nlvl; l++) any |= t->lvl_total[l - 1] >= mg->fused_min;
     if (any) {
-      AFH_HIP(hipMalloc(&mg->alt, (size_t)t->nb * t->bsz * sizeof(double)));
-      t->alt = mg->alt;
-      AFH_HIP(hipMemsetAsync(mg->alt, 0, (size_t)t->nb * t->bsz * sizeof(double),
-                             t->stream));
+      // one spare image per tree: the level fills after a pair fill t->alt
+      if (!t->alt) {
+        AFH_HIP(hipMalloc(&t->alt, (size_t)t->nb * t->bsz * sizeof(double)));
+        AFH_HIP(hipMemsetAsync(t->alt, 0, (size_t)t->nb * t->bsz * sizeof(double),
+                               t->stream));
+      }
+      t->alt_refs++;
+      mg->alt = t->alt;
     }
   }
   for (int q = 0; q < P.n_mg; q++) {
@@ -2210,9 +2214,9 @@ int32_t afh_mg_destroy(afh_mg *mg) {
   for (int q = 0; q < 3; q++) hipFree(mg->d_q[q]), hipFree(mg->d_qt[q]), hipFree(mg->d_e[q]);
   hipFree(mg->w1);
   hipFree(mg->w2);
-  if (mg->alt) {
-    if (mg->t->alt == mg->alt) mg->t->alt = nullptr;
-    hipFree(mg->alt);
+  if (mg->alt && --mg->t->alt_refs == 0) {
+    hipFree(mg->t->alt);
+    mg->t->alt = nullptr;
   }
   for (auto *v : {&mg->h_vp, &mg->h_bp, &mg->h_dd, &mg->h_bv})
     for (double *q : *v) hipFree(q);

@@ -178,6 +178,32 @@ def test_hip_bitwise_equals_oracle_fmg(hip, oracle, name, smoother, helm):
     _assert_same(ca, cb, [IV["phi"], IV["tmp"], IV["rhs"]])
 
 
+@pytest.mark.parametrize("name", ["uni8_l4_2x1x1", "uni16_l3"])
+def test_multigrids_sharing_a_tree(hip, oracle, name, smoother):
+    """Several multigrids on one tree (the field solver and the Helmholtz
+    photoionization modes): each one's fused pairs and the level fills that
+    follow them use the tree's one spare image, whichever was created last
+    (a per-multigrid image left the fills of the earlier ones filling
+    another's). Interleaved FMGs, bitwise the oracle."""
+    g = golden.load("uni8")
+    ca, cb = _pair(hip, oracle, TOPOS[name](), g)
+    mgs = []
+    for c in (ca, cb):
+        c.fluid.field_set_rhs(IV["rhs"], 0)
+        c.set_voltage(0.0)
+        mgs.append([c.mg, c.helmholtz_mg(1e6), c.helmholtz_mg(4e8)])
+    for rnd in range(2):
+        for k in (0, 2, 1):
+            for m in mgs:
+                m[k].fas_fmg(True, have_guess=rnd > 0)
+            _assert_same(ca, cb, [IV["phi"], IV["tmp"], IV["rhs"]])
+    mgs[0][2].close()  # the last-created one goes first
+    mgs[1][2].close()
+    for m in mgs:
+        m[1].fas_fmg(True, have_guess=True)
+    _assert_same(ca, cb, [IV["phi"], IV["tmp"], IV["rhs"]])
+
+
 def test_vcycles_converge_large(hip, smoother):
     """Size-independent property at a larger size: each V-cycle reduces the
     max residual on the leaves by a large factor."""
