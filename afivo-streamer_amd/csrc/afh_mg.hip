@@ -1002,6 +1002,86 @@ __global__ void k_rstr_fas(double *__restrict__ phi,
   phi[po] = 0.125 * sp;
 }
 
+// k_rstr_fas with each thread marching a column of K coarse cells (2K fine
+// planes) along k: the 2x2 fine centre values of each plane are loaded once
+// and serve as the z neighbours of the planes above and below (the one-cell
+// form re-read the fine planes around every coarse plane from other blocks,
+// 1.67x the algorithmic bytes in the PMC counters). Same operand order as
+// k_rstr_fas / apply7: bitwise the same parent values.
+template <int K>
+__global__ void __launch_bounds__(256)
+    k_rstr_fas_col(double *__restrict__ phi, const double *__restrict__ rhs,
+                   double *__restrict__ tmp, const afh_box_meta *__restrict__ meta,
+                   const int32_t *__restrict__ ids, int nc, size_t bsz, Coef cf) {
+  const int hn = nc >> 1;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= hn * hn * (hn / K)) return;
+  const int id = ids[blockIdx.y];
+  const afh_box_meta &m = meta[id - 1];
+  int i, j, kq;
+  cell3(t, hn, i, j, kq);
+  const int k0 = (kq - 1) * K + 1;  // first coarse plane of the column
+  const int ng = nc + 2;
+  const size_t sj = ng;
+  const size_t o = (size_t)(id - 1) * bsz;
+  const double *x = phi + o, *r = rhs + o;
+  const int fi = 2 * i - 1, fj = 2 * j - 1, f0 = 2 * k0 - 1;
+  // centre values c[p][a + 2 b] of fine plane f0 - 1 + p at (fi + a, fj + b)
+  double c[2 * K + 2][4];
+#pragma unroll
+  for (int p = 0; p < 2 * K + 2; p++) {
+    const size_t b = ix3(ng, fi, fj, f0 - 1 + p);
+    c[p][0] = x[b];
+    c[p][1] = x[b + 1];
+    c[p][2] = x[b + sj];
+    c[p][3] = x[b + sj + 1];
+  }
+  const size_t pb = (size_t)(m.parent - 1) * bsz;
+  const int pi = ((m.ix[0] - 1) & 1) * hn + i, pj = ((m.ix[1] - 1) & 1) * hn + j,
+            pk = ((m.ix[2] - 1) & 1) * hn;
+#pragma unroll
+  for (int q = 0; q < K; q++) {
+    double sr = 0.0, sp = 0.0;
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const int p = 2 * q + 1 + h;  // fine plane f0 - 1 + p
+      const size_t b = ix3(ng, fi, fj, f0 - 1 + p);
+      // x neighbours (fi - 1, fi + 2) and y neighbours (fj - 1, fj + 2)
+      const double xm0 = x[b - 1], xp0 = x[b + 2];
+      const double xm1 = x[b + sj - 1], xp1 = x[b + sj + 2];
+      const double ym0 = x[b - sj], ym1 = x[b - sj + 1];
+      const double yp0 = x[b + 2 * sj], yp1 = x[b + 2 * sj + 1];
+      const double r0 = r[b], r1 = r[b + 1], r2 = r[b + sj], r3 = r[b + sj + 1];
+      const double *z = c[p], *zm = c[p - 1], *zp = c[p + 1];
+      // cells (fi, fj), (fi+1, fj), (fi, fj+1), (fi+1, fj+1) of this plane
+      const double a0 = cf.c[0] * z[0] + cf.c[1] * xm0 + cf.c[2] * z[1] + cf.c[3] * ym0 +
+                        cf.c[4] * z[2] + cf.c[5] * zm[0] + cf.c[6] * zp[0];
+      const double a1 = cf.c[0] * z[1] + cf.c[1] * z[0] + cf.c[2] * xp0 + cf.c[3] * ym1 +
+                        cf.c[4] * z[3] + cf.c[5] * zm[1] + cf.c[6] * zp[1];
+      const double a2 = cf.c[0] * z[2] + cf.c[1] * xm1 + cf.c[2] * z[3] + cf.c[3] * z[0] +
+                        cf.c[4] * yp0 + cf.c[5] * zm[2] + cf.c[6] * zp[2];
+      const double a3 = cf.c[0] * z[3] + cf.c[1] * z[2] + cf.c[2] * xp1 + cf.c[3] * z[1] +
+                        cf.c[4] * yp1 + cf.c[5] * zm[3] + cf.c[6] * zp[3];
+      if (h == 0) {
+        sr = r0 - a0;
+        sp = z[0];
+      } else {
+        sr += r0 - a0;
+        sp += z[0];
+      }
+      sr += r1 - a1;
+      sp += z[1];
+      sr += r2 - a2;
+      sp += z[2];
+      sr += r3 - a3;
+      sp += z[3];
+    }
+    const size_t po = pb + ix3(ng, pi, pj, pk + k0 + q);
+    tmp[po] = 0.125 * sr;
+    phi[po] = 0.125 * sp;
+  }
+}
+
 __global__ void k_parent_rhs(const double *__restrict__ phi,
                              double *__restrict__ rhs, double *__restrict__ tmp,
                              const int32_t *__restrict__ ids, int nc,
@@ -1947,6 +2027,7 @@ struct afh_mg {
   bool pair_box = true;      // AFH_GSRB_PAIR_BOX=0: plane-marching pair for NC <= 16
   bool grad_nt = true;       // AFH_GRAD_NT: the gradient's face fields and |E| stored
                              // nontemporal (streaming): -9 % on S1-64 (scripts/grad_ab.py)
+  bool rstr_col = true;       // AFH_RSTR_COL=0: one coarse cell per thread (k_rstr_fas)
   int pair_ks = 4;           // AFH_GSRB_PAIR_KS: k chunks on 64..255-box levels (NC = 64;
                              // 4 whole-box chunks, 44 quarter-box tiles x 4, 0 tiles)
   int wave_cells = CS_WAVE_CELLS;  // AFH_CS_WAVE_CELLS
@@ -2159,6 +2240,7 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
   if (const char *env = getenv("AFH_GSRB_PAIR_P3")) mg->pair_p3 = atoi(env) != 0;
   if (const char *env = getenv("AFH_GSRB_PAIR_SP")) mg->pair_sp = atoi(env) != 0;
   if (const char *env = getenv("AFH_GRAPHS")) mg->use_graphs = atoi(env) != 0;
+  if (const char *env = getenv("AFH_RSTR_COL")) mg->rstr_col = atoi(env) != 0;
   if (const char *env = getenv("AFH_GSRB_PAIR_BOX")) mg->pair_box = atoi(env) != 0;
   if (const char *env = getenv("AFH_GSRB_PAIR_KS")) mg->pair_ks = atoi(env);
   if (const char *env = getenv("AFH_GRAD_NT")) mg->grad_nt = atoi(env) != 0;
@@ -2475,6 +2557,9 @@ static int32_t gsrb_boxes(afh_mg *mg, int lvl, bool up) {
   return AFH_OK;
 }
 
+#ifndef AFH_RSTR_K  // coarse cells per thread column of k_rstr_fas_col
+#define AFH_RSTR_K 2
+#endif
 #ifndef AFH_RES_K  // cells per thread column of k_residual (8, 4 or 2)
 #define AFH_RES_K 4
 #endif
@@ -2485,10 +2570,17 @@ static int32_t update_coarse(afh_mg *mg, int lvl) {
   const LevelList &L = cst(mg, t->ids, mg->ids_c);
   const int nid = L.n(lvl);
   if (nid) {
-    hipLaunchKernelGGL(k_rstr_fas, dim3((hn * hn * hn + 255) / 256, nid),
-                       dim3(256), 0, t->stream, t->ccv(mg->d.i_phi),
-                       t->ccv(mg->d.i_rhs), t->ccv(mg->d.i_tmp), t->d_boxes,
-                       L.at(lvl), nc, t->bsz, mg->lvl_c[lvl - 1]);
+    constexpr int RK = AFH_RSTR_K;
+    if (mg->rstr_col && hn % RK == 0)
+      hipLaunchKernelGGL(k_rstr_fas_col<RK>, dim3((hn * hn * (hn / RK) + 255) / 256, nid),
+                         dim3(256), 0, t->stream, t->ccv(mg->d.i_phi),
+                         t->ccv(mg->d.i_rhs), t->ccv(mg->d.i_tmp), t->d_boxes,
+                         L.at(lvl), nc, t->bsz, mg->lvl_c[lvl - 1]);
+    else
+      hipLaunchKernelGGL(k_rstr_fas, dim3((hn * hn * hn + 255) / 256, nid),
+                         dim3(256), 0, t->stream, t->ccv(mg->d.i_phi),
+                         t->ccv(mg->d.i_rhs), t->ccv(mg->d.i_tmp), t->d_boxes,
+                         L.at(lvl), nc, t->bsz, mg->lvl_c[lvl - 1]);
     AFH_LAUNCH_CHECK("k_rstr_fas");
   }
   const int nv = mg->any_var ? mg->ids_v.n(lvl) : 0;
