@@ -28,7 +28,7 @@ import math
 
 import numpy as np
 
-from . import capi
+from . import capi, electrode
 from .amr import AfTree
 from .model import Fluid, Multigrid, Tree, photoi_helmh_compute
 
@@ -73,17 +73,8 @@ class Case:
 
 
 def _norm2(v):
-    """gfortran's NORM2 (scaled sum of squares)."""
-    scale, ssq = 0.0, 1.0
-    for x in v:
-        if x != 0.0:
-            a = abs(x)
-            if scale < a:
-                ssq = 1.0 + ssq * (scale / a) ** 2
-                scale = a
-            else:
-                ssq = ssq + (a / scale) ** 2
-    return scale * math.sqrt(ssq)
+    """NORM2 as the reference's Fortran runtime computes it (afh.electrode.norm2)."""
+    return float(electrode.norm2(np.asarray(v, float)[None])[0])
 
 
 def _dist_vec_line(r, r0, r1):
@@ -108,7 +99,7 @@ def _dist_vec_line(r, r0, r1):
 def density_line(r, r0, r1, n0, n1, width, falloff):
     """GM_density_line (src/m_geometry.f90:53-113) at points r (n, 3)."""
     dv, frac = _dist_vec_line(r, r0, r1)
-    dist = np.array([_norm2(v) for v in dv])
+    dist = electrode.norm2(dv)
     if falloff == "smoothstep":
         t = dist / width - 1
         val = np.where(dist < width, 1.0,
@@ -142,8 +133,27 @@ class Simulation:
         if c.s("time_integrator") != "heuns_method":
             raise NotImplementedError("time integrator %s" % c.s("time_integrator"))
         self.n_states = 2  # af_advance_num_steps(af_heuns_method)
-        if c.i("use_electrode") or c.i("use_dielectric") or c.i("cylindrical"):
-            raise NotImplementedError("electrode / dielectric / cylindrical cases")
+        if c.i("use_dielectric") or c.i("cylindrical"):
+            raise NotImplementedError("dielectric / cylindrical cases")
+        # electrode (m_field.f90:196-346): a rod or sphere as level-set
+        # function; its operators are computed on the host per box
+        # (afh.electrode, mg_set_operators_tree) and handed to the library
+        self.lsf = None
+        if c.i("use_electrode"):
+            kind = c.s("field_electrode_type")
+            L0, o0 = c.ra("domain_len"), c.ra("domain_origin")
+            r0 = o0 + c.ra("field_rod_r0") * L0
+            r1 = o0 + c.ra("field_rod_r1") * L0
+            if kind == "rod":
+                self.lsf = electrode.RodLSF(r0, r1, c.r("field_rod_radius"))
+            elif kind == "sphere":
+                self.lsf = electrode.SphereLSF(r0, c.r("field_rod_radius"))
+            else:
+                raise NotImplementedError("electrode type %s" % kind)
+            if c.i("photoi%enabled"):
+                raise NotImplementedError("Helmholtz photoionization with an electrode")
+            self.electrode_grounded = bool(c.i("field_electrode_grounded"))
+            self._ops = {}  # box geometry -> box_operators (tags persist)
         # registry (af_add_cc_variable order of the reference's modules)
         self.cc_names = c.sa("cc_names")
         # gas density given by a function (streamer.f90:86-95 with
@@ -158,7 +168,7 @@ class Simulation:
             self.gas_fractions = list(c.ra("gas_fractions"))
         self.n_var_cell, self.n_var_face = len(self.cc_names), len(c.sa("fc_names"))
         (self.i_phi, self.i_electron, self.i_1pos_ion, self.i_efld, self.i_rhs,
-         self.i_tmp, self.i_photo, self.f_flux, self.f_field, _) = c.ia("ivars")
+         self.i_tmp, self.i_photo, self.f_flux, self.f_field, self.i_lsf) = c.ia("ivars")
         n_species, self.n_gas, n_reac = c.ia("n_species")
         self.species_list = c.sa("species_list")
         self.species_charge = c.ia("species_charge")
@@ -274,6 +284,46 @@ class Simulation:
             gas_fractions=self.gas_fractions if self.i_gas_dens else ())
         if self.fused_rhs:
             self.fluid.set_rhs_output(self.i_rhs, True)
+        if self.lsf is not None:
+            self._set_electrode()
+
+    def lsf_boundary_value(self):
+        """mg%lsf_boundary_value (m_field.f90:439-443)."""
+        return 0.0 if self.electrode_grounded else self.voltage
+
+    def _set_electrode(self):
+        """set_lsf_box on every box (cells 0..nc+1, m_field.f90:608-619) and
+        the operators of mg_set_operators_tree (m_af_multigrid.f90:
+        1133-1205): box tags and stencils, computed once per box (afivo
+        keeps them with the box), bc_correction with the current electrode
+        potential; the electrode boxes for refine_electrode_dx and
+        electrode_species_bc."""
+        nc, ng = self.af.nc, self.af.nc + 2
+        lsf = np.zeros((self.tree.n_boxes, ng, ng, ng))
+        bv = self.lsf_boundary_value()
+        self.electrode_ids = []
+        self.electrode_box = np.zeros(self.tree.n_boxes, np.uint8)
+        used = [b for b in range(1, self.af.highest_id + 1) if self.af.in_use[b]]
+        r = np.stack([electrode.cell_centers(self.af.r_min[b], self.af.dr[b], nc, 0, nc + 1)
+                      for b in used])
+        lsf[np.asarray(used) - 1] = self.lsf(r)
+        key = {b: (tuple(self.af.r_min[b]), tuple(self.af.dr[b])) for b in used}
+        new = [b for b in used if key[b] not in self._ops]
+        ops = electrode.boxes_operators(
+            self.lsf, [(lsf[b - 1][1:-1, 1:-1, 1:-1], self.af.r_min[b], self.af.dr[b])
+                       for b in new], nc, 1.0)
+        for b, op in zip(new, ops):
+            self._ops[key[b]] = op
+        for b in used:
+            op = self._ops[key[b]]
+            if op is None:
+                continue
+            v, fb, ix, dd = op  # fb: f times 1
+            self.electrode_ids.append(b)
+            self.electrode_box[b - 1] = 1
+            self.mg.set_box_stencil(b, v, fb * bv)
+            self.mg.set_box_lsf(b, ix, dd, np.full((nc, nc, nc), bv), self.i_lsf)
+        self.tree.put_cc(self.i_lsf, lsf)
 
     def _create_tree(self):
         t = Tree(self.lib, self.af.topology(), self.n_var_cell, self.n_var_face,
@@ -320,7 +370,8 @@ class Simulation:
             max_rhs = self.fluid.rhs_maxabs(s_in)
         else:
             max_rhs = self.fluid.field_set_rhs_maxabs(self.i_rhs, s_in)
-        conv_fac = 1e-10
+        # with an electrode the initial convergence test is less strict
+        conv_fac = 1e-8 if self.lsf is not None else 1e-10
         threshold = max(1e-6, max_rhs * self.max_rel_res,
                         conv_fac * abs(self.voltage) / (self.L[2] * self.af.min_dr()))
         res = []
@@ -424,7 +475,8 @@ class Simulation:
     def adjust_refinement(self):
         """af_adjust_refinement with default_refinement: the criterion on the
         device, the topology on the host, the data moved by the device."""
-        flags, masks = self.fluid.refine_flags(self.refine_desc())
+        flags, masks = self.fluid.refine_flags(
+            self.refine_desc(), self.electrode_box if self.lsf is not None else None)
 
         def fn(ids):
             ix = np.asarray(ids, np.int64) - 1
@@ -560,6 +612,10 @@ class Simulation:
         if self.photoi and self.it % c.i("photoi%per_steps") == 0:
             self.photoi_set_src()
             self.photoi_prev_time = self.time
+        if self.lsf is not None:  # set_electrode_densities (streamer.f90:244-246)
+            self.fluid.electrode_species_bc(
+                self.i_lsf, self.i_1pos_ion, self.electrode_ids,
+                c.s("species_boundary_condition") == "neumann_zero")
         dt_lim = 1e100
         for n in range(1, 11):
             self.copy_current_state()

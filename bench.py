@@ -49,8 +49,13 @@ CONFIGS = {
     # photoi%per_steps time steps, the 8-level AMR tree of 8^3 boxes its
     # initial refinement builds (tests/golden/case_s5.npz, afh.users.Sprite3D)
     "s5": (8, None, None, (5e3, 5e3, 20e3)),
+    # BASELINE.json config 4 on one device: config 3 with the grounded rod
+    # electrode of SURVEY 8(d) S4 (tests/golden/case_s4.npz): level-set
+    # stencils on the boxes the rod crosses (afh.electrode), the electrode's
+    # species boundary condition every time step, 5 levels of 8^3 boxes
+    "s4": (8, None, None, (16e-3, 16e-3, 16e-3)),
 }
-DRIVER_CONFIGS = ("s3", "s5")
+DRIVER_CONFIGS = ("s3", "s4", "s5")
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E peak (spec)
 
 
@@ -126,6 +131,10 @@ class DriverCase:
         sim = self.sim
         if sim.photoi and k % (2 * sim.c.i("photoi%per_steps")) == 0:
             sim.photoi_set_src()
+        if sim.lsf is not None and k % 2 == 0:  # set_electrode_densities
+            sim.fluid.electrode_species_bc(
+                sim.i_lsf, sim.i_1pos_ion, sim.electrode_ids,
+                sim.c.s("species_boundary_condition") == "neumann_zero")
 
     def fuse_rhs(self, on=True, ghosts=False):
         self.sim.fluid.set_rhs_output(self.sim.i_rhs if on else 0, ghosts)
@@ -293,6 +302,18 @@ def main():
         case.tree.sync()
     ms, nl, by = C.c_double(), C.c_int64(), C.c_double()
     lib.call("profile_read", case.tree.h, C.byref(ms), C.byref(nl), C.byref(by))
+    kname = ("k_gsrb_pair2<%d,%d>" % (CONFIGS[args.config][0], CONFIGS[args.config][0])
+             if CONFIGS[args.config][0] > 16 else "k_gsrb_pair_box<%d>" % CONFIGS[args.config][0])
+    if nl.value == 0:
+        # no level runs the fused pair (too few boxes per level, or
+        # electrode stencils): the split half-sweep k_gsrb is the smoother
+        kname = "k_gsrb (half-sweep, 16 B/cell)"
+        graphs = True
+        lib.call("profile_enable", case.tree.h, capi.PROF_GSRB)
+        for k in range(2):
+            unit_step(case, dt, args.warmup + args.steps + 2 + k)
+        case.tree.sync()
+        lib.call("profile_read", case.tree.h, C.byref(ms), C.byref(nl), C.byref(by))
 
     if dist is not None:
         import torch
@@ -328,10 +349,7 @@ def main():
                        "parallelism": ("box-shard-%d-%s" % (world, args.shard)) if sharded else
                        ("replica-per-gpu" if world > 1 else "single-gpu")},
             "roofline": {"bound": "hbm",
-                         "kernel": ("k_gsrb_pair2<%d,%d>" % (CONFIGS[args.config][0],
-                                                             CONFIGS[args.config][0])
-                                    if CONFIGS[args.config][0] > 16 else
-                                    "k_gsrb_pair_box<%d>" % CONFIGS[args.config][0]),
+                         "kernel": kname,
                          "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": pmc_traffic(args.config),
@@ -349,6 +367,11 @@ def main():
         if args.config == "s3":
             out["config"]["chemistry"] = "air_chemistry_v2 (9 species, 25 reactions)"
             out["config"]["coarse_solve"] = "direct"
+        if args.config == "s4":
+            out["config"]["chemistry"] = "air_chemistry_v2 (9 species, 25 reactions)"
+            out["config"]["electrode"] = ("grounded rod (0.5,0.5,0)-(0.5,0.5,0.15) L, r = 1 mm, "
+                                          "%d electrode boxes" % len(sim.electrode_ids))
+            out["config"]["coarse_solve"] = "electrode level 1: red-black GS to stationarity"
         if args.config == "s5":
             out["config"]["chemistry"] = "sprite_chemistry_v0 (10 species, 12 reactions)"
             out["config"]["gas_density"] = "variable (3d_sprite m_user: 2.5e25 exp(-z/7.2 km))"

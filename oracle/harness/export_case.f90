@@ -110,6 +110,9 @@ program export_case
   call put_l("use_electrode"); call put_l("use_dielectric"); call put_l("cylindrical")
   call put_s("prolong_density"); call put_s("species_boundary_condition")
   call put_l("input_data%old_style")
+  ! electrode (m_field.f90:196-230; relative coordinates, as in the cfg)
+  call put_s("field_electrode_type"); call put_l("field_electrode_grounded")
+  call put_ra("field_rod_r0"); call put_ra("field_rod_r1"); call put_r("field_rod_radius")
 
   ! derived module state
   write(u, "(A,1X,I0,*(1X,ES25.17E3))") "r:dt_cfl_number_value", 1, dt_cfl_number

@@ -29,6 +29,17 @@ CASES = ["test_3d", "test_3d_chem", "test_3d_photoi_chem"]
 EXTRA = {"s3": ("/root/reference/programs/standard_3d", "streamer_3d.cfg",
                 ["-input_data%file=../../transport_data/air_chemistry_v2.txt",
                  "-input_data%old_style=f"]),
+         # BASELINE.json config 4: config 3 with the rod electrode of
+         # SURVEY.md 8(d) S4 (the geometry of the reference's own
+         # standard_2d/tests/test_2d_pos_electrode.cfg: a grounded rod from
+         # the z = 0 plane to 0.15 L, radius 1 mm), refined to 2e-4 m at
+         # the electrode and to no less than 1e-4 m (5 levels of 8^3 boxes)
+         "s4": ("/root/reference/programs/standard_3d", "streamer_3d.cfg",
+                ["-input_data%file=../../transport_data/air_chemistry_v2.txt",
+                 "-input_data%old_style=f", "-use_electrode=T",
+                 "-field_electrode_grounded=T", "-field_rod_r0=0.5 0.5 0.0",
+                 "-field_rod_r1=0.5 0.5 0.15", "-field_rod_radius=1e-3",
+                 "-refine_electrode_dx=2e-4", "-refine_min_dx=1e-4"]),
          # BASELINE.json config 5: programs/3d_sprite/sprite_3d.cfg
          # (sprite_chemistry_v0, Helmholtz photoionization, the gas density
          # of its m_user.f90: an exponential atmosphere, so the "M" variable)

@@ -13,5 +13,5 @@ else
   for f in $(git ls-tree --name-only $rev afivo-streamer_amd/csrc/ include/); do git show $rev:$f > $src/$f; done
 fi
 make -s -C $src/afivo-streamer_amd/csrc -j8 HIPFLAGS_EXTRA="$*" >/dev/null
-mkdir -p ab/$name && cp $src/afivo-streamer_amd/csrc/libafivo_hip.so ab/$name/
-echo "ab/$name/libafivo_hip.so"
+mkdir -p abv/$name && cp $src/afivo-streamer_amd/csrc/libafivo_hip.so abv/$name/
+echo "abv/$name/libafivo_hip.so"

@@ -22,20 +22,25 @@ LEAF = 512 * 64 ** 3          # S1-64 leaf cells
 PARENT = 64 * 64 ** 3         # S1-64 level-3 boxes (parents of the leaves)
 # kernel (name prefix up to '(') -> (algorithmic bytes per cell, cells)
 ALG = {
+    "void afh::k_gsrb_pair2<64, 64, 1, 0, true, true, true, 1>": (24, LEAF),
+    "void afh::k_gsrb_pair2<64, 64, 1, 0, true, true, true, 4>": (24, PARENT),
     "void afh::k_gsrb_pair2<64, 64": (24, LEAF),
     "void afh::k_gsrb_pair2<64, 16": (24, PARENT),
     "void afh::k_residual<true, 4>": (24, LEAF),
     "void afh::k_residual<false, 4>": (24, PARENT),
     "afh::k_rstr_fas": (18, LEAF),
+    "void afh::k_rstr_fas_col<2>": (18, LEAF),
     "void afh::k_prolong<4>": (20, LEAF),
     "afh::k_corr_tmp": (24, PARENT),
     "afh::k_parent_rhs": (24, PARENT),
     "void afh::k_gradient_t<64, 4>": (40, LEAF),
+    "void afh::k_gradient_t<64, 4, true>": (40, LEAF),
     "void afh::k_flux_lds<64, 3>": (64 + 192 / 64, LEAF),
     "void afh::k_update<3, false, 1": (8 * 3 * 2 + 32, LEAF),
     "void afh::k_update<3, false, 2": (8 * 3 * 3 + 32, LEAF),
     "afh::k_gc_faces": (96 / 64, LEAF),
     "afh::k_gc2": (2 * 96 / 64, LEAF),
+    "void afh::k_set_rhs<true>": (32, LEAF),
 }
 
 

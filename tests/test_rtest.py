@@ -174,3 +174,58 @@ def test_s5_sprite_hip_equals_oracle():
     fa = sim.fluid.refine_flags(sim.refine_desc())
     fb = osim.fluid.refine_flags(osim.refine_desc())
     assert np.array_equal(fa[0], fb[0]) and np.array_equal(fa[1], fb[1])
+
+
+def _s4_checks(sim):
+    """The electrode of config 4 as the set-up leaves it: boxes tagged,
+    a grounded rod (phi ~ 0 inside it, leaf interiors), refined to
+    refine_electrode_dx around it."""
+    assert len(sim.electrode_ids) > 10
+    lsf, phi = sim.tree.get_cc(sim.i_lsf), sim.tree.get_cc(sim.i_phi)
+    inner = (slice(None),) + (slice(1, -1),) * 3
+    leaves = np.asarray(sim.af.leaves()) - 1
+    li, lp = lsf[leaves][inner], phi[leaves][inner]
+    assert np.max(np.abs(lp[li < 0])) < 1e-3 * abs(sim.voltage)
+    assert np.min(lp[li > 0]) > -1e-3 * abs(sim.voltage)
+    dx = min(float(np.max(sim.af.dr[b])) for b in sim.electrode_ids if b - 1 in set(leaves))
+    assert dx <= sim.c.r("refine_electrode_dx")
+
+
+def test_s4_electrode_oracle():
+    """BASELINE config 4 on one device (streamer_3d.cfg + air_chemistry_v2
+    with the grounded rod of SURVEY 8(d) S4, exported by oracle/make_cases.py)
+    through the driver on the C oracle: the host electrode operators
+    (afh.electrode, pinned to the reference's own stencils in
+    test_electrode_ops) in the set-up's field solves and two time steps."""
+    sim = Simulation(capi.oracle_library(), golden.load("case_s4"))
+    sim.start()
+    _s4_checks(sim)
+    for _ in range(2):
+        sim.step()
+    assert np.all(np.isfinite(sim.log[-1]))
+
+
+@pytest.mark.gpu
+def test_s4_electrode_hip_equals_oracle():
+    """Config 4 on the GPU: the set-up (electrode field solves on the device,
+    level-set stencils, electrode refinement) on the HIP library, then the
+    same state on the C oracle; two Heun steps with electrode_species_bc
+    and field solves through the electrode stencils on both: densities,
+    potential and field to 1e-12 relative (the air_chemistry_v2 rate forms'
+    pow / exp may differ in the last ulp between ocml and glibc), the
+    refinement flags equal."""
+    sim = Simulation(capi.hip_library(), golden.load("case_s4"), device=0)
+    sim.start()
+    _s4_checks(sim)
+    osim = sim.clone(capi.oracle_library())
+    for s in (sim, osim):
+        s.fluid.electrode_species_bc(s.i_lsf, s.i_1pos_ion, s.electrode_ids, True)
+        s.advance(1e-12)
+        s.field_compute(0, True)
+    for iv in list(sim.densities) + [sim.i_phi, sim.i_efld]:
+        a, b = sim.tree.get_cc(iv), osim.tree.get_cc(iv)
+        rel = np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300)
+        assert rel <= 1e-12, (sim.cc_names[iv - 1], rel)
+    fa = sim.fluid.refine_flags(sim.refine_desc(), sim.electrode_box)
+    fb = osim.fluid.refine_flags(osim.refine_desc(), osim.electrode_box)
+    assert np.array_equal(fa[0], fb[0]) and np.array_equal(fa[1], fb[1])
