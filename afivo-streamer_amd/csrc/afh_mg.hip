@@ -2027,6 +2027,8 @@ struct afh_mg {
   bool pair_box = true;      // AFH_GSRB_PAIR_BOX=0: plane-marching pair for NC <= 16
   bool grad_nt = true;       // AFH_GRAD_NT: the gradient's face fields and |E| stored
                              // nontemporal (streaming): -9 % on S1-64 (scripts/grad_ab.py)
+  bool cs_fused = true;       // AFH_CS_FUSED=0: the electrode coarse solve launch per pair
+  int *cs_iters = nullptr;     // pairs the last k_cs_electrode took
   bool rstr_col = true;       // AFH_RSTR_COL=0: one coarse cell per thread (k_rstr_fas)
   int pair_ks = 4;           // AFH_GSRB_PAIR_KS: k chunks on 64..255-box levels (NC = 64;
                              // 4 whole-box chunks, 44 quarter-box tiles x 4, 0 tiles)
@@ -2241,6 +2243,8 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
   if (const char *env = getenv("AFH_GSRB_PAIR_SP")) mg->pair_sp = atoi(env) != 0;
   if (const char *env = getenv("AFH_GRAPHS")) mg->use_graphs = atoi(env) != 0;
   if (const char *env = getenv("AFH_RSTR_COL")) mg->rstr_col = atoi(env) != 0;
+  if (const char *env = getenv("AFH_CS_FUSED")) mg->cs_fused = atoi(env) != 0;
+  AFH_HIP(hipMalloc(&mg->cs_iters, sizeof(int)));
   if (const char *env = getenv("AFH_GSRB_PAIR_BOX")) mg->pair_box = atoi(env) != 0;
   if (const char *env = getenv("AFH_GSRB_PAIR_KS")) mg->pair_ks = atoi(env);
   if (const char *env = getenv("AFH_GRAD_NT")) mg->grad_nt = atoi(env) != 0;
@@ -2305,6 +2309,7 @@ int32_t afh_mg_destroy(afh_mg *mg) {
   for (int32_t *q : mg->h_ix) hipFree(q);
   hipFree(mg->d_vp), hipFree(mg->d_bp), hipFree(mg->d_dd), hipFree(mg->d_bv);
   hipFree(mg->d_ix), hipFree(mg->d_lsf_n), hipFree(mg->cs_old);
+  hipFree(mg->cs_iters);
   for (LevelList *L : {&mg->ids_c, &mg->ids_v, &mg->leaves_c, &mg->leaves_v,
                        &mg->parents_c, &mg->parents_v, &mg->lsf_leaves})
     hipFree(L->d);
@@ -2649,9 +2654,155 @@ static int32_t correct_children(afh_mg *mg, int lvl) {
 // stationary (max change <= 4 spacing(max |phi|), after at least 11 pairs),
 // then the level's ghost cells with corners. One host check per pair: meant
 // for the small coarse grids electrode runs use.
+// The same iteration for a level 1 of one box with six physical faces (the
+// usual electrode case: coarse grid = one box) in one workgroup: the box and
+// its rhs in LDS, each pair = two k_gsrb_v half sweeps (rhs + bc_correction,
+// parity update, rhs = (rhs + bc) - bc), each followed by the face fill of
+// gc_face_nocopy's physical branch (no corners), then max |change| and
+// max |phi| over the interior and the same stopping test -- all on the
+// device, no host round trip per pair. Every wave leaves the loop at the
+// same test (block-uniform), bounded by the host loop's 200000 pairs.
+// Bitwise the launch-per-pair form.
+extern "C++" {
+template <int NC>
+__global__ void __launch_bounds__(1024)
+    k_cs_electrode(double *__restrict__ x, double *__restrict__ r,
+                   const double *__restrict__ v, const double *__restrict__ b,
+                   GcArgs ga, double dr0, double dr1, double dr2,
+                   int *__restrict__ iters) {
+  constexpr int NG = NC + 2, N3 = NC * NC * NC, G3 = NG * NG * NG;
+  constexpr int SJ = NG, SK = NG * NG;
+  __shared__ double X[G3], R[N3];
+  __shared__ double s_d[16], s_m[16];
+  const int tid = threadIdx.x, nt = blockDim.x;
+  for (int e = tid; e < G3; e += nt) X[e] = x[e];
+  for (int e = tid; e < N3; e += nt) {
+    const int i = e % NC + 1, j = (e / NC) % NC + 1, k = e / (NC * NC) + 1;
+    R[e] = r[ix3(NG, i, j, k)];
+  }
+  __syncthreads();
+  constexpr int CPT = (N3 + 1023) / 1024;  // cells per thread (<= 4 at NC 16)
+  double old[CPT];
+  int it;
+  for (it = 1; it <= 200000; it++) {
+#pragma unroll
+    for (int q = 0; q < CPT; q++) {
+      const int e = tid + q * nt;
+      if (e < N3) {
+        const int i = e % NC + 1, j = (e / NC) % NC + 1, k = e / (NC * NC) + 1;
+        old[q] = X[ix3(NG, i, j, k)];
+      }
+    }
+    for (int n = 1; n <= 2; n++) {
+      for (int e = tid; e < N3; e += nt) {
+        const int i = e % NC + 1, j = (e / NC) % NC + 1, k = e / (NC * NC) + 1;
+        const int c = ix3(NG, i, j, k);
+        const double *w = v + 7 * (size_t)e;
+        double r1 = R[e];
+        if (b) r1 = r1 + b[e];
+        if (((i + j + k + n) & 1) == 0)
+          X[c] = (r1 - w[1] * X[c - 1] - w[2] * X[c + 1] - w[3] * X[c - SJ] -
+                  w[4] * X[c + SJ] - w[5] * X[c - SK] - w[6] * X[c + SK]) /
+                 w[0];
+        if (b) R[e] = r1 - b[e];
+      }
+      __syncthreads();
+      // face ghosts (physical boundaries; gc_face_nocopy_k, nb_id < 0)
+      for (int e = tid; e < 6 * NC * NC; e += nt) {
+        const int nb = e / (NC * NC) + 1, ab = e % (NC * NC);
+        const int d = (nb - 1) >> 1;
+        const bool low = ((nb - 1) & 1) == 0;
+        const int ta = d == 0 ? 1 : 0, tb = d == 2 ? 1 : 2;
+        int p[3], q1[3];
+        p[ta] = ab % NC + 1;
+        p[tb] = ab / NC + 1;
+        p[d] = low ? 0 : NC + 1;
+        q1[0] = p[0], q1[1] = p[1], q1[2] = p[2];
+        q1[d] = low ? 1 : NC;
+        const afh_bc bc = ga.bc[nb - 1];
+        const double drd = d == 0 ? dr0 : d == 1 ? dr1 : dr2;
+        double c0, c1;
+        switch (bc.type) {
+        case AFH_BC_DIRICHLET: c0 = 2; c1 = -1; break;
+        case AFH_BC_NEUMANN: c0 = drd * (low ? -1 : 1); c1 = 1; break;
+        default: c0 = 1; c1 = 0; break;
+        }
+        X[ix3(NG, p[0], p[1], p[2])] = c0 * bc.value + c1 * X[ix3(NG, q1[0], q1[1], q1[2])];
+      }
+      __syncthreads();
+    }
+    double dm = 0.0, mm = 0.0;
+#pragma unroll
+    for (int q = 0; q < CPT; q++) {
+      const int e = tid + q * nt;
+      if (e < N3) {
+        const int i = e % NC + 1, j = (e / NC) % NC + 1, k = e / (NC * NC) + 1;
+        const double pv = X[ix3(NG, i, j, k)];
+        dm = fmax(dm, fabs(pv - old[q]));
+        mm = fmax(mm, fabs(pv));
+      }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      dm = fmax(dm, __shfl_xor(dm, o, 64));
+      mm = fmax(mm, __shfl_xor(mm, o, 64));
+    }
+    if ((tid & 63) == 0) s_d[tid >> 6] = dm, s_m[tid >> 6] = mm;
+    __syncthreads();
+    dm = s_d[0], mm = s_m[0];
+    for (int w = 1; w < (nt >> 6); w++) dm = fmax(dm, s_d[w]), mm = fmax(mm, s_m[w]);
+    __syncthreads();  // s_d / s_m reused by the next pair
+    double sp = 2.2250738585072014e-308;  // Fortran spacing(max |phi|)
+    if (mm > 0) {
+      int ex;
+      frexp(mm, &ex);
+      sp = ldexp(1.0, ex - 53);
+    }
+    if (dm <= 4 * sp && it > 10) break;
+  }
+  for (int e = tid; e < G3; e += nt) x[e] = X[e];
+  for (int e = tid; e < N3; e += nt) {
+    const int i = e % NC + 1, j = (e / NC) % NC + 1, k = e / (NC * NC) + 1;
+    r[ix3(NG, i, j, k)] = R[e];
+  }
+  if (tid == 0) iters[0] = it;
+}
+}  // extern "C++"
+
+// whether the electrode coarse solve runs as k_cs_electrode (one level-1 box
+// with an electrode stencil and six physical faces, no sharding hook)
+static bool cs_electrode_fused(const afh_mg *mg) {
+  const afh_tree *t = mg->t;
+  if (t->ids.n(1) != 1 || t->hook || (t->nc != 8 && t->nc != 16) || !mg->cs_fused)
+    return false;
+  const int id = t->h_ids[0][0];
+  bool phys = mg->h_vp[id - 1] != nullptr;
+  for (int q = 0; q < 6; q++) phys = phys && t->boxes[id - 1].neighbors[q] < 0;
+  return phys;
+}
+
 static int32_t solve_coarse_gs(afh_mg *mg) {
   afh_tree *t = mg->t;
   const int nid = t->ids.n(1), nc = t->nc, n3 = nc * nc * nc;
+  if (cs_electrode_fused(mg)) {
+    const int id = t->h_ids[0][0];
+    const afh_box_meta &m = t->boxes[id - 1];
+    {
+      double *phi = t->ccv(mg->d.i_phi) + (size_t)(id - 1) * t->bsz;
+      double *rhs = t->ccv(mg->d.i_rhs) + (size_t)(id - 1) * t->bsz;
+      int *iters = mg->cs_iters;
+      const int nt = n3 >= 1024 ? 1024 : n3;
+      if (nc == 8)
+        hipLaunchKernelGGL(k_cs_electrode<8>, dim3(1), dim3(nt), 0, t->stream, phi, rhs,
+                           mg->h_vp[id - 1], mg->h_bp[id - 1], t->gc_args(mg->d.i_phi),
+                           m.dr[0], m.dr[1], m.dr[2], iters);
+      else
+        hipLaunchKernelGGL(k_cs_electrode<16>, dim3(1), dim3(nt), 0, t->stream, phi, rhs,
+                           mg->h_vp[id - 1], mg->h_bp[id - 1], t->gc_args(mg->d.i_phi),
+                           m.dr[0], m.dr[1], m.dr[2], iters);
+      AFH_LAUNCH_CHECK("k_cs_electrode");
+      return gc_lvl(t, 1, mg->d.i_phi, 1);
+    }
+  }
   if (!mg->cs_old) AFH_HIP(hipMalloc(&mg->cs_old, sizeof(double) * t->bsz * nid));
   auto *red = reinterpret_cast<unsigned long long *>(t->scratch);
   double *phi = t->ccv(mg->d.i_phi);
@@ -2885,7 +3036,8 @@ static int32_t vcycle_graph(afh_mg *mg, int32_t set_residual, int max_lvl, bool 
                             bool &done) {
   afh_tree *t = mg->t;
   done = false;
-  if (!mg->use_graphs || t->hook || t->prof_class || (mg->any_var && mg->lvl_var[0]))
+  if (!mg->use_graphs || t->hook || t->prof_class ||
+      (mg->any_var && mg->lvl_var[0] && !cs_electrode_fused(mg)))
     return AFH_OK;
   const int key = (max_lvl << 2) | (set_residual ? 2 : 0) | (max_out ? 1 : 0);
   afh_mg::Graph &g = mg->graphs[key];
