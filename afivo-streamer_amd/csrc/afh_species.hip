@@ -962,6 +962,9 @@ __global__ void k_consistent(double *__restrict__ F,
 // NP: the number of previous states when known at compile time (1, 2), or
 // MAXPREV (any, A.n_prev); SD: the derivative state is no previous state
 // (A.der_q < 0) -- both only trim registers and dead loads
+#ifndef AFH_UPD_KC  // cells per thread column of k_update (1, 2, 4)
+#define AFH_UPD_KC 1
+#endif
 #ifndef AFH_UPD_MINW  // minimum waves per SIMD of the update kernel
 #define AFH_UPD_MINW 1
 #endif
@@ -972,9 +975,16 @@ __global__ void __launch_bounds__(256, AFH_UPD_MINW)
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   const int id = ids[blockIdx.y];
   double cmin = 1e100, rmax = 0.0;
-  if (t < nc * nc * nc) {
-    int i, j, k;
-    cell3(t, nc, i, j, k);
+  // KC cells along k per thread: the z flux between two of them is loaded
+  // once (the high face of cell k is the low face of cell k + 1)
+  constexpr int KC = AFH_UPD_KC;
+  double fz_carry = 0.0;
+#pragma unroll 1
+  for (int kc = 0; kc < KC; kc++)
+  if (t < nc * nc * (nc / KC)) {
+    int i, j, kq;
+    cell3(t, nc, i, j, kq);
+    const int k = (kq - 1) * KC + 1 + kc;
     const int ng = nc + 2, nf = nc + 1;
     const size_t x = (size_t)(id - 1) * bsz + (size_t)((k * ng + j) * ng + i);
     // every load first (fluxes, |E|, states), then the arithmetic
@@ -982,7 +992,8 @@ __global__ void __launch_bounds__(256, AFH_UPD_MINW)
     const int f0 = ((k - 1) * nf + (j - 1)) * nf + (i - 1);
     const int d3 = nf * nf * nf;
     const double fx0 = F[f0], fx1 = F[f0 + 1], fy0 = F[d3 + f0], fy1 = F[d3 + f0 + nf],
-                 fz0 = F[2 * d3 + f0], fz1 = F[2 * d3 + f0 + nf * nf];
+                 fz0 = kc ? fz_carry : F[2 * d3 + f0], fz1 = F[2 * d3 + f0 + nf * nf];
+    fz_carry = fz1;
     const double ev = A.E[x];
     const double pho = A.photo ? A.photo[x] : 0.0;
     const int n_prev = NP == MAXPREV ? A.n_prev : NP;
@@ -1076,7 +1087,7 @@ __global__ void __launch_bounds__(256, AFH_UPD_MINW)
       for (int s = 0; s < NS; s++)
         if (A.rq[s] != 0.0) r = r + A.rq[s] * y[s];
       st_nt<AFH_NT_UPD>(A.rhs + x, r);
-      rmax = fabs(r);
+      rmax = fmax(rmax, fabs(r));
     }
   }
   if (A.rhs) block_max_to_shard(rmax, A.rhs_red);
@@ -1097,7 +1108,7 @@ template <int NS>
 void launch_update(const UpdArgs &A, afh_tree *t, int l,
                    unsigned long long *red, bool slow) {
   const int nc = t->nc, n3 = nc * nc * nc;
-  const dim3 grid((n3 + 255) / 256, t->leaves.n(l));
+  const dim3 grid((n3 / AFH_UPD_KC + 255) / 256, t->leaves.n(l));
   const auto *ids = t->leaves.at(l);
   const bool sd = A.der_q < 0;
   if (A.Ng)
@@ -2031,10 +2042,12 @@ static int32_t upd_args(afh_fluid *f, double dt, int32_t s_deriv, int32_t n_prev
 
 extern "C" {
 
-int32_t afh_flux_upwind_tree(afh_fluid *f, int32_t s_deriv, double *dt_lim) {
-  if (!f || !dt_lim) return set_error(AFH_ERR_ARG, "null argument");
+}  // extern "C"
+
+// flux_upwind_tree's device work up to the folded CFL / sigma maxima
+// (reduction slots 0, 1); the caller fetches them
+static int32_t flux_tree_dev(afh_fluid *f, int32_t s_deriv) {
   afh_tree *t = f->t;
-  AFH_LIVE(t, "afh_flux_upwind_tree");
   const int nc = t->nc, n3 = nc * nc * nc;
   const int iv = f->d.i_electron + s_deriv;
   if (iv < 1 || iv > t->nvc) return set_error(AFH_ERR_ARG, "bad s_deriv");
@@ -2075,23 +2088,42 @@ int32_t afh_flux_upwind_tree(afh_fluid *f, int32_t s_deriv, double *dt_lim) {
     AFH_LAUNCH_CHECK("k_consistent");
   }
   if ((e = call_hook(t, AFH_HOOK_CFLUX, 0, f->d.f_flux))) return e;
-  if ((e = red_finish(t, 0, true)) || (e = red_finish(t, 1, true))) return e;
-  double r[2];
-  if ((e = red_fetch(t, 0, 2, r)) || (e = call_hook(t, AFH_HOOK_MAX, 0, 0, r, 2)))
-    return e;
+  if ((e = red_finish(t, 0, true))) return e;
+  return red_finish(t, 1, true);
+}
+
+// dt_lim(1:2) of flux_upwind_tree from the folded maxima
+static void flux_dt_limits(const double r[2], double *dt_lim) {
   const double cfl_max = r[0], sig_max = r[1];
   dt_lim[0] = 1 / cfl_max;
   dt_lim[1] = 8.8541878176e-12 / (1.6022e-19 * std::max(sig_max, 1e-100));
+}
+
+extern "C" {
+
+int32_t afh_flux_upwind_tree(afh_fluid *f, int32_t s_deriv, double *dt_lim) {
+  if (!f || !dt_lim) return set_error(AFH_ERR_ARG, "null argument");
+  afh_tree *t = f->t;
+  AFH_LIVE(t, "afh_flux_upwind_tree");
+  const int iv = f->d.i_electron + s_deriv;
+  if (iv < 1 || iv > t->nvc) return set_error(AFH_ERR_ARG, "bad s_deriv");
+  int32_t e;
+  double r[2];
+  if ((e = flux_tree_dev(f, s_deriv)) || (e = red_fetch(t, 0, 2, r)) ||
+      (e = call_hook(t, AFH_HOOK_MAX, 0, 0, r, 2)))
+    return e;
+  flux_dt_limits(r, dt_lim);
   return AFH_OK;
 }
 
-int32_t afh_flux_update_densities(afh_fluid *f, double dt, int32_t s_deriv,
-                                  int32_t n_prev, const int32_t *s_prev,
-                                  const double *w_prev, int32_t s_out,
-                                  int32_t last_step, double *dt_lim) {
-  if (!f || !dt_lim) return set_error(AFH_ERR_ARG, "afh_flux_update_densities: null");
+}  // extern "C"
+
+// flux_update_densities' device work; on the last step the chemistry dt
+// minimum folded into reduction slot 2 for the caller to fetch
+static int32_t update_dev(afh_fluid *f, double dt, int32_t s_deriv, int32_t n_prev,
+                          const int32_t *s_prev, const double *w_prev, int32_t s_out,
+                          int32_t last_step) {
   afh_tree *t = f->t;
-  AFH_LIVE(t, "afh_flux_update_densities");
   const int nc = t->nc, n3 = nc * nc * nc;
   UpdArgs A;
   double upd_bytes;
@@ -2139,10 +2171,23 @@ int32_t afh_flux_update_densities(afh_fluid *f, double dt, int32_t s_deriv,
     f->rhs_snap.clear();
     for (int v : f->rhs_vars(s_out)) f->rhs_snap.push_back(t->gen[v]);
   }
+  return last_step ? red_finish(t, 2, false) : AFH_OK;
+}
+
+extern "C" {
+
+int32_t afh_flux_update_densities(afh_fluid *f, double dt, int32_t s_deriv,
+                                  int32_t n_prev, const int32_t *s_prev,
+                                  const double *w_prev, int32_t s_out,
+                                  int32_t last_step, double *dt_lim) {
+  if (!f || !dt_lim) return set_error(AFH_ERR_ARG, "afh_flux_update_densities: null");
+  afh_tree *t = f->t;
+  AFH_LIVE(t, "afh_flux_update_densities");
+  int32_t e;
+  if ((e = update_dev(f, dt, s_deriv, n_prev, s_prev, w_prev, s_out, last_step))) return e;
   double r = 1e100;
   if (last_step) {
-    if ((e = red_finish(t, 2, false)) || (e = red_fetch(t, 2, 1, &r)) ||
-        (e = call_hook(t, AFH_HOOK_MIN, 0, 0, &r, 1)))
+    if ((e = red_fetch(t, 2, 1, &r)) || (e = call_hook(t, AFH_HOOK_MIN, 0, 0, &r, 1)))
       return e;
   } else {
     AFH_HIP(hipStreamSynchronize(t->stream));
@@ -2215,12 +2260,17 @@ int32_t afh_fluid_forward_euler(afh_fluid *f, double dt, int32_t s_deriv,
                      f->rhs_iv == 0 && f->d.i_gas_dens <= 0 && f->d.i_photo <= 0 &&
                      n_prev <= 2 && !alias && f->d.limiter == AFH_LIM_KOREN;
   if (!fused) {
-    double a[2], b[2];
-    if ((e = afh_flux_upwind_tree(f, s_deriv, a)) ||
-        (e = afh_flux_update_densities(f, dt, s_deriv, n_prev, s_prev, w_prev, s_out,
-                                       last_step, b)))
+    // flux and update back to back on the stream, one fetch of the three
+    // limits (the flux maxima are not needed before the update)
+    double r[3] = {0.0, 0.0, 1e100};
+    if ((e = flux_tree_dev(f, s_deriv)) ||
+        (e = update_dev(f, dt, s_deriv, n_prev, s_prev, w_prev, s_out, last_step)) ||
+        (e = red_fetch(t, 0, last_step ? 3 : 2, r)) ||
+        (e = call_hook(t, AFH_HOOK_MAX, 0, 0, r, 2)) ||
+        (last_step && (e = call_hook(t, AFH_HOOK_MIN, 0, 0, r + 2, 1))))
       return e;
-    dt_lim[0] = a[0], dt_lim[1] = a[1], dt_lim[2] = b[0], dt_lim[3] = b[1];
+    flux_dt_limits(r, dt_lim);
+    dt_lim[2] = r[2], dt_lim[3] = 1e100;
     return AFH_OK;
   }
   t->touch(iv);
