@@ -106,6 +106,11 @@ struct afh_tree {
   // live inside one fused pair); freed with the last of them
   double *alt = nullptr;
   int alt_refs = 0;
+  // level face fills: six faces per thread (k_gc_faces6) or one thread per
+  // ghost cell (k_gc_faces). Default (-1): k_gc_faces6 for boxes up to 16^3
+  // (S1 leaf fill 13.5 -> 11.8 us); at 64^3 it measured 134 -> 129 us per
+  // fill but the step no faster, so k_gc_faces stays (AFH_GC_FACES6=0/1)
+  int gc_faces6 = -1;
   struct Plan {
     int32_t *d_reg = nullptr;  // n x 7 (id, lo[3], hi[3])
     int64_t *d_off = nullptr;  // n + 1 value offsets

@@ -113,6 +113,55 @@ __global__ void k_gc_faces(double *__restrict__ v,
                           });
 }
 
+// The six faces of a box by one thread per (a, b): the six ghost values are
+// loaded (neighbour copies, or gc_face_nocopy's boundary / refinement
+// values, which read only interior and coarse cells) before the six stores,
+// six independent chains per thread instead of one. Same values as
+// k_gc_faces.
+__global__ void __launch_bounds__(256)
+    k_gc_faces6(double *__restrict__ v, const double *__restrict__ vc,
+                const afh_box_meta *__restrict__ meta, const int32_t *__restrict__ ids,
+                int nc, size_t bsz, GcArgs ga) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nc * nc) return;
+  const int id = ids[blockIdx.y];
+  int a, b;
+  if ((nc & (nc - 1)) == 0) {
+    a = (t & (nc - 1)) + 1;
+    b = (t >> __builtin_ctz(nc)) + 1;
+  } else {
+    a = t % nc + 1;
+    b = t / nc + 1;
+  }
+  const int ng = nc + 2;
+  const afh_box_meta &m = meta[id - 1];
+  double *c = v + (size_t)(id - 1) * bsz;
+  double val[6];
+  size_t dst[6];
+#pragma unroll
+  for (int nb = 1; nb <= 6; nb++) {
+    const int d = (nb - 1) >> 1;
+    const bool low = ((nb - 1) & 1) == 0;
+    const int ta = (d == 0) ? 1 : 0, tb = (d == 2) ? 1 : 2;
+    int p[3];
+    p[ta] = a;
+    p[tb] = b;
+    p[d] = low ? 0 : nc + 1;
+    dst[nb - 1] = ix3(ng, p[0], p[1], p[2]);
+    const int nb_id = m.neighbors[nb - 1];
+    if (nb_id > 0) {
+      int q[3] = {p[0], p[1], p[2]};
+      q[d] = low ? nc : 1;
+      val[nb - 1] = v[(size_t)(nb_id - 1) * bsz + ix3(ng, q[0], q[1], q[2])];
+    } else {
+      val[nb - 1] = gc_face_nocopy(vc, meta, m, nb, p, a, b, nc, bsz, ga.bc[nb - 1], ga.rb,
+                                   [&](const int *q) { return c[ix3(ng, q[0], q[1], q[2])]; });
+    }
+  }
+#pragma unroll
+  for (int nb = 0; nb < 6; nb++) c[dst[nb]] = val[nb];
+}
+
 // ------------------------------------------------------------ edges+corners
 __constant__ int c_edge_dim[12] = {0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2};
 __constant__ int c_edge_dir[12][3] = {
@@ -203,10 +252,13 @@ int32_t gc_lvl_var(afh_tree *t, int lvl, int iv, const double *vc,
   if ((e = call_hook(t, AFH_HOOK_HALO, lvl, iv))) return e;
   if (n > 0) {
     const int nc = t->nc;
-    dim3 grid((nc * nc + 255) / 256, 6, n);
     prof_begin(t, AFH_PROF_GHOST);
-    hipLaunchKernelGGL(k_gc_faces, grid, dim3(256), 0, t->stream, v, vc,
-                       t->d_boxes, t->ids.at(lvl), nc, t->bsz, ga);
+    if (t->gc_faces6 == 1 || (t->gc_faces6 < 0 && nc <= 16))
+      hipLaunchKernelGGL(k_gc_faces6, dim3((nc * nc + 255) / 256, n), dim3(256), 0,
+                         t->stream, v, vc, t->d_boxes, t->ids.at(lvl), nc, t->bsz, ga);
+    else
+      hipLaunchKernelGGL(k_gc_faces, dim3((nc * nc + 255) / 256, 6, n), dim3(256), 0,
+                         t->stream, v, vc, t->d_boxes, t->ids.at(lvl), nc, t->bsz, ga);
     // algorithmic bytes: read one interior layer + write one ghost layer
     prof_end(t, AFH_PROF_GHOST, 16.0 * 6 * nc * nc * n);
     AFH_LAUNCH_CHECK("k_gc_faces");
@@ -542,6 +594,8 @@ static int32_t tree_create_impl(const afh_tree_desc *d, int32_t device,
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1)
     return set_error(AFH_ERR_DEVICE, "no HIP device available");
   afh_tree *t = new afh_tree();
+  if (const char *env = getenv("AFH_GC_FACES6")) t->gc_faces6 = atoi(env) != 0;
+  else t->gc_faces6 = -1;  // by box size
   if (device >= 0) {
     AFH_HIP(hipSetDevice(device));
     t->device = device;
