@@ -2227,12 +2227,16 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
   if (int32_t e = build_table(mg)) return e;
   // AFH_GSRB_FUSED_MIN_BOXES: smallest level (in boxes) smoothed with the
   // fused red-black kernel; 0 disables it
+  if (const char *env = getenv("AFH_GSRB_PAIR_BOX")) mg->pair_box = atoi(env) != 0;
   if (const char *env = getenv("AFH_GSRB_FUSED_MIN_BOXES"))
     mg->fused_min = atoi(env);
   else if (fused_nc_ok(t->nc))
     // whole boxes from 256 boxes (a workgroup per CU), NC/4-row tiles from
-    // 64 boxes (NC >= 32); smaller levels keep the split half-sweeps
-    mg->fused_min = t->nc >= 32 ? 64 : 256;
+    // 64 boxes (NC >= 32); smaller levels keep the split half-sweeps. Boxes
+    // up to 16^3 (k_gsrb_pair_box) fuse on every level: on the small levels
+    // the launches, not the bytes, cost (S1 0.768 -> 0.737 ms/step, S3
+    // 2.57 -> 2.54 ms/step, scripts/env_bench_ab.sh)
+    mg->fused_min = t->nc >= 32 ? 64 : (t->nc <= 16 && mg->pair_box ? 1 : 256);
   if (const char *env = getenv("AFH_GSRB_TILES")) mg->force_tiles = atoi(env) != 0;
   if (const char *env = getenv("AFH_GSRB_PAIR_V1")) mg->pair_v1 = atoi(env) != 0;
   if (const char *env = getenv("AFH_GSRB_PAIR_TJ")) mg->pair_tj = atoi(env);
@@ -2540,8 +2544,11 @@ static int32_t gsrb_boxes(afh_mg *mg, int lvl, bool up) {
     const double *src = to_alt ? phi : mg->alt;
     double *dst = to_alt ? mg->alt : phi;
     const int dst_iv = to_alt ? 0 : mg->d.i_phi;
+    // the bench's roofline times the big levels (>= 256 boxes, or tiles);
+    // small-level pairs of small boxes are launch-bound and not timed
     const int pclass = (nc >= 32 && pair_tiles(mg, lvl)) ? AFH_PROF_GSRB_PAIR_TILED
-                                                          : AFH_PROF_GSRB_PAIR;
+                       : (nc >= 32 || t->lvl_total[lvl - 1] >= 256) ? AFH_PROF_GSRB_PAIR
+                                                                     : -1;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     const bool timed = prof_ext(t, pclass, e0, e1);
     switch (nc) {
