@@ -2234,10 +2234,10 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
     // whole boxes from 256 boxes (a workgroup per CU), NC/4-row tiles from
     // 64 boxes (NC >= 32); smaller levels keep the split half-sweeps.
     // (AFH_GSRB_FUSED_MIN_BOXES=1 fuses every level: S1 0.768 -> 0.737
-    // ms/step, S3 2.57 -> 2.54, scripts/env_bench_ab.sh; but the device
-    // regression run test_3d then left the oracle's rows at 1.2 ns (2e-4),
-    // so some small AMR level's fused pair is not bitwise its split form:
-    // not the default until that is found)
+    // ms/step, S3 2.57 -> 2.54, scripts/env_bench_ab.sh; but one device
+    // regression run of test_3d with it left the oracle's rows at 1.2 ns,
+    // unexplained -- V-cycles, FMGs and field solves on that run's trees
+    // are bitwise the split form, scripts/fused_small_debug.py)
     mg->fused_min = t->nc >= 32 ? 64 : 256;
   if (const char *env = getenv("AFH_GSRB_TILES")) mg->force_tiles = atoi(env) != 0;
   if (const char *env = getenv("AFH_GSRB_PAIR_V1")) mg->pair_v1 = atoi(env) != 0;
