@@ -12,11 +12,16 @@ from afh import capi
 from afh.driver import Simulation
 
 
+# argv: the B run's settings (default AFH_GSRB_FUSED_MIN_BOXES=1)
+B_ENV = [a.split("=", 1) for a in sys.argv[1:]] or [["AFH_GSRB_FUSED_MIN_BOXES", "1"]]
+
+
 def env(on):
-    if on:
-        os.environ["AFH_GSRB_FUSED_MIN_BOXES"] = "1"
-    else:
-        os.environ.pop("AFH_GSRB_FUSED_MIN_BOXES", None)
+    for k, v in B_ENV:
+        if on:
+            os.environ[k] = v
+        else:
+            os.environ.pop(k, None)
 
 
 S = Simulation(capi.hip_library(), golden.load("rtest_test_3d"), device=0)
@@ -45,6 +50,7 @@ def each(fn):
     env(False)
 
 
+print("B:", B_ENV, "level boxes", [len(S.af.lvls[l]["ids"]) for l in range(1, S.af.highest_lvl + 1)], flush=True)
 cmp("cloned at step 65")
 each(lambda s: s.copy_current_state())
 each(lambda s: s.advance(s.dt))
@@ -57,6 +63,7 @@ for s in sims:
         s.tree.gc_tree(iv)
 each(lambda s: s.adjust_refinement())
 cmp("after regrid")
+print("level boxes after regrid", [len(sims[0].af.lvls[l]["ids"]) for l in range(1, sims[0].af.highest_lvl + 1)], flush=True)
 each(lambda s: s.field_compute(0, True))
 cmp("after field_compute 2")
 each(lambda s: s.field_compute(0, True))
