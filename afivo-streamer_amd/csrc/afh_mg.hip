@@ -2027,6 +2027,13 @@ struct afh_mg {
   bool pair_box = true;      // AFH_GSRB_PAIR_BOX=0: plane-marching pair for NC <= 16
   bool grad_nt = true;       // AFH_GRAD_NT: the gradient's face fields and |E| stored
                              // nontemporal (streaming): -9 % on S1-64 (scripts/grad_ab.py)
+  // t->gen[i_phi] when this multigrid last left phi's ghost cells current
+  // (a V-cycle over all levels, or an FMG fill); anything else that writes
+  // phi bumps the generation. The fused pair needs current ghost cells on
+  // entry (phase B takes a same-level neighbour's boundary column from this
+  // box's ghost column), so a V-cycle that finds them stale (after a regrid,
+  // an upload, a copy) smooths its top level with split half-sweeps first
+  uint64_t phi_gc_gen = UINT64_MAX;
   bool cs_fused = true;       // AFH_CS_FUSED=0: the electrode coarse solve launch per pair
   int *cs_iters = nullptr;     // pairs the last k_cs_electrode took
   bool rstr_col = true;       // AFH_RSTR_COL=0: one coarse cell per thread (k_rstr_fas)
@@ -2519,13 +2526,14 @@ static int32_t gsrb_half(afh_mg *mg, int lvl, int n, bool corners) {
 // followed by a ghost fill of the level. On levels with enough boxes the
 // pairs run fused (k_gsrb_pair), alternating phi -> alt -> phi; an odd
 // number of pairs starts with one split pair.
-static int32_t gsrb_boxes(afh_mg *mg, int lvl, bool up) {
+static int32_t gsrb_boxes(afh_mg *mg, int lvl, bool up, bool stale_ghosts = false) {
   afh_tree *t = mg->t;
   const int n_cycle = up ? mg->d.n_cycle_up : mg->d.n_cycle_down;
   const int nid = t->ids.n(lvl), nc = t->nc;
   const Coef cf = mg->lvl_c[lvl - 1];
   const double inv_c1 = 1 / cf.c[0];
-  const bool fused = fused_level(mg, lvl);
+  // stale ghost cells on entry: the split half-sweeps, as the reference
+  const bool fused = fused_level(mg, lvl) && !stale_ghosts;
   int n0 = 1;
   if (fused && (n_cycle & 1)) {
     if (int32_t e = gsrb_half(mg, lvl, 1, false)) return e;
@@ -2956,9 +2964,10 @@ int32_t afh_mg_fas_fmg(afh_mg *mg, int32_t set_residual, int32_t have_guess) {
     return e;
   for (int lvl = 2; lvl <= nl; lvl++) {
     if ((e = box_copy(t, lvl, phi, tmp)) || (e = correct_children(mg, lvl)) ||
-        (e = gc_lvl(t, lvl, i_phi, 1, fused_level(mg, lvl))) ||
-        (e = afh_mg_fas_vcycle(mg, set_residual && lvl == nl, lvl)))
+        (e = gc_lvl(t, lvl, i_phi, 1, fused_level(mg, lvl))))
       return e;
+    mg->phi_gc_gen = t->gen[i_phi];  // the cycle's top level was just filled
+    if ((e = afh_mg_fas_vcycle(mg, set_residual && lvl == nl, lvl))) return e;
   }
   return AFH_OK;
 }
@@ -3020,11 +3029,12 @@ static int32_t residual_fetch(afh_mg *mg, double *max_out) {
 }
 
 // the device work of one V-cycle (everything but reading max|res|)
-static int32_t vcycle_body(afh_mg *mg, int32_t set_residual, int max_lvl, bool max_out) {
+static int32_t vcycle_body(afh_mg *mg, int32_t set_residual, int max_lvl, bool max_out,
+                           bool top_stale) {
   afh_tree *t = mg->t;
   int32_t e;
   for (int lvl = max_lvl; lvl >= 2; lvl--) {
-    if ((e = gsrb_boxes(mg, lvl, false))) return e;
+    if ((e = gsrb_boxes(mg, lvl, false, top_stale && lvl == max_lvl))) return e;
     if ((e = update_coarse(mg, lvl))) return e;
   }
   if ((e = solve_coarse(mg))) return e;
@@ -3042,13 +3052,14 @@ static int32_t vcycle_body(afh_mg *mg, int32_t set_residual, int max_lvl, bool m
 // the device every pair). The first call of a variant runs eagerly (tables,
 // spare image); a change of boundary conditions drops the graph.
 static int32_t vcycle_graph(afh_mg *mg, int32_t set_residual, int max_lvl, bool max_out,
-                            bool &done) {
+                            bool top_stale, bool &done) {
   afh_tree *t = mg->t;
   done = false;
   if (!mg->use_graphs || t->hook || t->prof_class ||
       (mg->any_var && mg->lvl_var[0] && !cs_electrode_fused(mg)))
     return AFH_OK;
-  const int key = (max_lvl << 2) | (set_residual ? 2 : 0) | (max_out ? 1 : 0);
+  const int key = (max_lvl << 3) | (top_stale ? 4 : 0) | (set_residual ? 2 : 0) |
+                  (max_out ? 1 : 0);
   afh_mg::Graph &g = mg->graphs[key];
   if (g.exec && g.meth_gen != t->meth_gen) {
     hipGraphExecDestroy(g.exec);
@@ -3061,7 +3072,7 @@ static int32_t vcycle_graph(afh_mg *mg, int32_t set_residual, int max_lvl, bool 
   if (!g.exec) {
     hipGraph_t graph;
     AFH_HIP(hipStreamBeginCapture(t->stream, hipStreamCaptureModeThreadLocal));
-    const int32_t e = vcycle_body(mg, set_residual, max_lvl, max_out);
+    const int32_t e = vcycle_body(mg, set_residual, max_lvl, max_out, top_stale);
     const hipError_t ce = hipStreamEndCapture(t->stream, &graph);
     if (e) {
       if (ce == hipSuccess) hipGraphDestroy(graph);
@@ -3083,14 +3094,17 @@ static int32_t vcycle_impl(afh_mg *mg, int32_t set_residual, int32_t hl,
   if (!mg) return set_error(AFH_ERR_ARG, "null mg");
   afh_tree *t = mg->t;
   AFH_LIVE(t, "afh_mg_fas_vcycle");
+  const bool top_stale = mg->phi_gc_gen != t->gen[mg->d.i_phi];
   t->touch(mg->d.i_phi), t->touch(mg->d.i_rhs), t->touch(mg->d.i_tmp);
   const int max_lvl = (hl > 0 && hl <= t->nlvl) ? hl : t->nlvl;
   int32_t e;
   if ((e = prepare_var(mg))) return e;
   bool done;
   const bool max_out = set_residual && max_res;
-  if ((e = vcycle_graph(mg, set_residual, max_lvl, max_out, done))) return e;
-  if (!done && (e = vcycle_body(mg, set_residual, max_lvl, max_out))) return e;
+  if ((e = vcycle_graph(mg, set_residual, max_lvl, max_out, top_stale, done))) return e;
+  if (!done && (e = vcycle_body(mg, set_residual, max_lvl, max_out, top_stale))) return e;
+  // the up leg filled every level's ghost cells (corners on the last fill)
+  if (max_lvl == t->nlvl) mg->phi_gc_gen = t->gen[mg->d.i_phi];
   return max_out ? residual_fetch(mg, max_res) : AFH_OK;
 }
 
