@@ -2239,13 +2239,11 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
     mg->fused_min = atoi(env);
   else if (fused_nc_ok(t->nc))
     // whole boxes from 256 boxes (a workgroup per CU), NC/4-row tiles from
-    // 64 boxes (NC >= 32); smaller levels keep the split half-sweeps.
-    // (AFH_GSRB_FUSED_MIN_BOXES=1 fuses every level: S1 0.768 -> 0.737
-    // ms/step, S3 2.57 -> 2.54, scripts/env_bench_ab.sh; but one device
-    // regression run of test_3d with it left the oracle's rows at 1.2 ns,
-    // unexplained -- V-cycles, FMGs and field solves on that run's trees
-    // are bitwise the split form, scripts/fused_small_debug.py)
-    mg->fused_min = t->nc >= 32 ? 64 : 256;
+    // 64 boxes (NC >= 32). Boxes up to 16^3 (k_gsrb_pair_box) fuse on every
+    // level: the small levels are launch-bound (S1 0.768 -> 0.737 ms/step,
+    // S3 2.57 -> 2.54, scripts/env_bench_ab.sh); bitwise the split form
+    // (test_3d every row, scripts/rtest_determinism.py)
+    mg->fused_min = t->nc >= 32 ? 64 : (t->nc <= 16 && mg->pair_box ? 1 : 256);
   if (const char *env = getenv("AFH_GSRB_TILES")) mg->force_tiles = atoi(env) != 0;
   if (const char *env = getenv("AFH_GSRB_PAIR_V1")) mg->pair_v1 = atoi(env) != 0;
   if (const char *env = getenv("AFH_GSRB_PAIR_TJ")) mg->pair_tj = atoi(env);
