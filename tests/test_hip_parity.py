@@ -204,6 +204,33 @@ def test_multigrids_sharing_a_tree(hip, oracle, name, smoother):
     _assert_same(ca, cb, [IV["phi"], IV["tmp"], IV["rhs"]])
 
 
+@pytest.mark.parametrize("name", ["amr8", "uni16_l3"])
+def test_vcycle_from_stale_ghost_cells(hip, oracle, name, smoother):
+    """A V-cycle whose phi has stale ghost cells (as after a regrid: afivo
+    neither prolongs nor fills phi) runs its top level's first leg split, as
+    the reference does: the fused pair's phase B would take this box's stale
+    ghost column for the neighbour's boundary column. Seeded phi with zero
+    ghost cells, uploaded; then V-cycles and an upload between them, bitwise
+    the oracle."""
+    g = golden.load("uni8")
+    ca, cb = _pair(hip, oracle, TOPOS[name](), g)
+    rng = np.random.default_rng(7)
+    phi = rng.standard_normal(ca.tree.get_cc(IV["phi"]).shape) * 1e3
+    phi[:, 0, :, :] = phi[:, -1, :, :] = 0.0
+    phi[:, :, 0, :] = phi[:, :, -1, :] = 0.0
+    phi[:, :, :, 0] = phi[:, :, :, -1] = 0.0
+    for c in (ca, cb):
+        c.fluid.field_set_rhs(IV["rhs"], 0)
+        c.tree.put_cc(IV["phi"], phi)
+        c.mg.fas_vcycle(True)
+        c.mg.fas_vcycle(True)
+    _assert_same(ca, cb, [IV["phi"], IV["tmp"]])
+    for c in (ca, cb):
+        c.tree.put_cc(IV["phi"], phi)
+        c.mg.fas_vcycle(True)
+    _assert_same(ca, cb, [IV["phi"], IV["tmp"]])
+
+
 def test_vcycles_converge_large(hip, smoother):
     """Size-independent property at a larger size: each V-cycle reduces the
     max residual on the leaves by a large factor."""
