@@ -78,18 +78,24 @@ int32_t exchange(afh_dist *d, const Key &key, int iv) {
   for (int q = 0; q < d->n && !e; q++)
     if (p.send[q].n) e = afh_plan_pack(t, p.send[q].plan, iv, p.send[q].buf);
   if (d->transport == AFH_DIST_RCCL) {
-    if (e) return e;
-    if (ncclGroupStart() != ncclSuccess) return set_error(AFH_ERR_DEVICE, "ncclGroupStart");
-    for (int q = 0; q < d->n && !e; q++) {
+    // the grouped send/recv is posted even after a failed pack (the buffer
+    // then carries stale values), so the peers' matching calls complete and
+    // every rank reports an error instead of some of them hanging
+    const int32_t e_pack = e;
+    bool posted = ncclGroupStart() == ncclSuccess;
+    for (int q = 0; q < d->n && posted; q++) {
       if (p.send[q].n &&
           ncclSend(p.send[q].buf, p.send[q].n, ncclDouble, q, d->comm, t->stream) != ncclSuccess)
-        e = set_error(AFH_ERR_DEVICE, "ncclSend");
-      if (!e && p.recv[q].n &&
+        posted = false;
+      if (posted && p.recv[q].n &&
           ncclRecv(p.recv[q].buf, p.recv[q].n, ncclDouble, q, d->comm, t->stream) != ncclSuccess)
-        e = set_error(AFH_ERR_DEVICE, "ncclRecv");
+        posted = false;
     }
-    if (ncclGroupEnd() != ncclSuccess && !e) e = set_error(AFH_ERR_DEVICE, "ncclGroupEnd");
-    if (e) return e;
+    if (ncclGroupEnd() != ncclSuccess) posted = false;
+    if (!posted)
+      return set_error(AFH_ERR_DEVICE, "exchange %d/%d: posting the RCCL send/recv failed",
+                       key.first, key.second);
+    if (e_pack) return e_pack;
   } else {
     // every rank's packs complete, then each copies the peers' packed
     // buffers; nobody packs again before every peer has copied. The
@@ -231,6 +237,11 @@ int32_t afh_tree_create_sharded(const afh_tree_desc *desc, const int32_t *owner,
     AFH_HIP(hipMemsetAsync(tr->fcv(iv) + (size_t)(tr->nb - 1) * tr->fsz, 0xff,
                            sizeof(double) * tr->fsz, tr->stream));
   AFH_HIP(hipStreamSynchronize(tr->stream));
+  // a replicated leaf (levels below the partition level) is summed by rank 0
+  // only, so the SUM all-reduce counts it once
+  tr->sum_skip.assign(tr->nb, 0);
+  if (rank != 0)
+    for (size_t k = 0; k < c.ids.size(); k++) tr->sum_skip[k] = owner[c.ids[k] - 1] < 0;
   tr->lvl_total.assign(t.nlvl, 0);
   tr->lvl_rb_coarse.assign(t.nlvl, 0);
   tr->any_cflux = false;

@@ -134,6 +134,10 @@ struct afh_tree {
   // per-box partial results of afh_tree_sum_cc / afh_tree_reduce_loc
   double *d_boxred = nullptr;
   int boxred_cap = 0;
+  // sharded tree: boxes whose leaf sum another rank contributes (the
+  // replicated levels below the partition level count on rank 0 only);
+  // empty on an unsharded tree
+  std::vector<char> sum_skip;
 
   double *ccv(int iv) const { return cc + (size_t)(iv - 1) * cap * bsz; }
   // cc variable iv, or the smoother's spare image of phi for iv == 0

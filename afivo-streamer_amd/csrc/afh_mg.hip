@@ -3059,9 +3059,12 @@ static int32_t vcycle_graph(afh_mg *mg, int32_t set_residual, int max_lvl, bool 
   const int key = (max_lvl << 3) | (top_stale ? 4 : 0) | (set_residual ? 2 : 0) |
                   (max_out ? 1 : 0);
   afh_mg::Graph &g = mg->graphs[key];
-  if (g.exec && g.meth_gen != t->meth_gen) {
-    hipGraphExecDestroy(g.exec);
+  if (g.meth_gen != t->meth_gen) {
+    // new boundary values or types since the warm call / capture: run
+    // eagerly once more (rebuilds the coarse-solve tables outside capture)
+    if (g.exec) hipGraphExecDestroy(g.exec);
     g = afh_mg::Graph();
+    g.meth_gen = t->meth_gen;
   }
   if (!g.warm) {
     g.warm = true;
@@ -3080,7 +3083,6 @@ static int32_t vcycle_graph(afh_mg *mg, int32_t set_residual, int max_lvl, bool 
     const hipError_t ie = hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0);
     hipGraphDestroy(graph);
     AFH_HIP(ie);
-    g.meth_gen = t->meth_gen;
   }
   AFH_HIP(hipGraphLaunch(g.exec, t->stream));
   done = true;

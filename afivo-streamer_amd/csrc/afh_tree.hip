@@ -808,6 +808,11 @@ int32_t afh_set_bc(afh_tree *t, int32_t iv, int32_t nb, int32_t type,
   AFH_LIVE(t, "afh_set_bc");
   if (!t || iv < 1 || iv > t->nvc || nb < 1 || nb > 6)
     return set_error(AFH_ERR_ARG, "afh_set_bc: bad argument");
+  if (type < AFH_BC_DIRICHLET_COPY || type > AFH_BC_DIRICHLET)
+    return set_error(AFH_ERR_UNSUPPORTED, "bc type %d", type);
+  // captured V-cycles hold the boundary values (and the coarse-solve tables
+  // the types): drop them, as afh_set_cc_methods does
+  t->meth_gen++;
   t->meth[iv].bc[nb - 1].type = type;
   t->meth[iv].bc[nb - 1].value = value;
   return AFH_OK;
@@ -962,7 +967,9 @@ int32_t afh_tree_sum_cc(afh_tree *t, int32_t iv, int32_t power, double *out) {
   for (int l = 1; l <= t->nlvl; l++) {
     const double *dr = &t->lvl_dr[3 * (l - 1)];
     const double fac = dr[0] * dr[1] * dr[2];
-    for (int b = 0; b < t->leaves.n(l); b++, q++) sum = sum + fac * res[2 * q];
+    for (int b = 0; b < t->leaves.n(l); b++, q++)
+      if (t->sum_skip.empty() || !t->sum_skip[t->h_leaves[l - 1][b] - 1])
+        sum = sum + fac * res[2 * q];
   }
   *out = sum;
   return call_hook(t, AFH_HOOK_SUM, 0, iv, out, 1);
@@ -1098,6 +1105,12 @@ int32_t afh_plan_pack(afh_tree *t, int32_t plan, int32_t iv, double *buf) {
 
 int32_t afh_plan_unpack(afh_tree *t, int32_t plan, int32_t iv,
                         const double *buf) {
+  // a caller unpacking into phi or a species state: ghost cells and a fused
+  // rhs derived from the old values are no longer current (the hook path
+  // runs inside calls that touch the variable themselves)
+  if (t && !t->retired && t->plans.size() > (size_t)std::max(plan, 0) &&
+      !t->plans[plan].fc && iv > 0)
+    t->touch(iv);
   return plan_copy(t, plan, iv, const_cast<double *>(buf), 1);
 }
 

@@ -62,6 +62,9 @@ struct afh_tree {
     int32_t *reg;
     int64_t *off;
   } *plans;
+  /* sharded tree: leaves another rank sums (replicated levels count on rank
+   * 0 only, as the device library); NULL on an unsharded tree */
+  unsigned char *sum_skip;
 };
 
 #define LIVE(t)                                                               \
@@ -214,6 +217,13 @@ int32_t afo_tree_create(const afh_tree_desc *d, int32_t device,
 
 /* sharded trees (c/afo_dist.cpp): box id's data read as NaN in every
  * variable (the unused id standing for boxes a rank does not store) */
+__attribute__((visibility("hidden"))) void afo_set_sum_skip(afh_tree *t,
+                                                           const unsigned char *skip) {
+  free(t->sum_skip);
+  t->sum_skip = (unsigned char *)malloc((size_t)t->nb);
+  memcpy(t->sum_skip, skip, (size_t)t->nb);
+}
+
 __attribute__((visibility("hidden"))) void afo_poison_box(afh_tree *t, int id) {
   for (int iv = 1; iv <= t->nvc; iv++) memset(ccb(t, iv, id), 0xff, sizeof(double) * t->bsz);
   for (int iv = 1; iv <= t->nvf; iv++) memset(fcb(t, iv, id), 0xff, sizeof(double) * t->fsz);
@@ -225,6 +235,7 @@ int32_t afo_tree_destroy(afh_tree *t) {
   free(t->ids), free(t->ids_off), free(t->leaves), free(t->leaves_off);
   free(t->parents), free(t->parents_off);
   free(t->cc), free(t->fc), free(t->meth), free(t->auto_vars), free(t->gen);
+  free(t->sum_skip);
   for (int q = 0; q < t->nplans; q++) free(t->plans[q].reg), free(t->plans[q].off);
   free(t->plans);
   free(t);
@@ -638,6 +649,7 @@ int32_t afo_tree_sum_cc(afh_tree *t, int32_t iv, int32_t power, double *out) {
     const afh_box_meta *m = B(t, LVL_AT(t, ids, l, 0));
     const double fac = m->dr[0] * m->dr[1] * m->dr[2];
     for (int q = 0; q < LVL_N(t, leaves, l); q++) {
+      if (t->sum_skip && t->sum_skip[LVL_AT(t, leaves, l, q) - 1]) continue;
       const double *c = ccb(t, iv, LVL_AT(t, leaves, l, q));
       double tmp = 0.0;
       for (int k = 1; k <= nc; k++)
@@ -2379,6 +2391,7 @@ int32_t afo_plan_pack(afh_tree *t, int32_t plan, int32_t iv, double *buf) {
 
 int32_t afo_plan_unpack(afh_tree *t, int32_t plan, int32_t iv,
                         const double *buf) {
+  if (t && plan >= 0 && plan < t->nplans && !t->plans[plan].fc && iv > 0) touch(t, iv);
   return plan_copy(t, plan, iv, (double *)buf, 1);
 }
 

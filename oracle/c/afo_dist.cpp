@@ -22,6 +22,7 @@
 
 extern "C" int32_t afo_fail_msg(int32_t code, const char *msg);
 extern "C" void afo_poison_box(afh_tree *t, int id);
+extern "C" void afo_set_sum_skip(afh_tree *t, const unsigned char *skip);
 
 using namespace afhd;
 
@@ -178,8 +179,14 @@ int32_t afo_tree_create_sharded(const afh_tree_desc *desc, const int32_t *owner,
   Compact c;
   compact(t, desc, std::vector<int32_t>(owner, owner + t.nb), rank, c);
   const int32_t e = afo_tree_create(&c.desc, device, out);
-  if (!e) afo_poison_box(*out, c.desc.n_boxes);
-  return e;
+  if (e) return e;
+  afo_poison_box(*out, c.desc.n_boxes);
+  // a replicated leaf is summed by rank 0 only (the SUM reduction counts it once)
+  std::vector<unsigned char> skip(c.desc.n_boxes, 0);
+  if (rank != 0)
+    for (size_t k = 0; k < c.ids.size(); k++) skip[k] = owner[c.ids[k] - 1] < 0;
+  afo_set_sum_skip(*out, skip.data());
+  return AFH_OK;
 }
 
 int32_t afo_dist_group_create(int32_t n_ranks, afh_dist_group **out) {

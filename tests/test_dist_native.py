@@ -106,6 +106,69 @@ def test_native_tree_create_sharded_matches_local_topology():
     b.close()
 
 
+def _sum_topo():
+    """Leaves below the partition level: one of the eight level-1 boxes is
+    refined, so with two ranks level 2 is the partition level and the seven
+    level-1 leaves are replicated on both ranks."""
+    from afh.tree import build_tree
+    return build_tree(8, (16, 16, 16), (2e-3, 2e-3, 2e-3), 1,
+                      refine=lambda lvl, r0, r1: lvl < 2 and np.all(r1 <= 1e-3 + 1e-12))
+
+
+def _sharded_sums(lib, device=-1):
+    topo = _sum_topo()
+    world = 2
+    rng = np.random.default_rng(3)
+    from afh.model import Tree
+    ref_tree = Tree(lib, topo, 2, 1, device=device)
+    x = rng.random(ref_tree.cc_shape)
+    ref_tree.put_cc(1, x)
+    ref = [ref_tree.sum_cc(1), ref_tree.sum_cc(1, 2), ref_tree.maxabs_cc(1)]
+    ref_tree.close()
+    group = NativeGroup(lib, world)
+    shards = [NativeShard(lib, topo, world, r, group=group) for r in range(world)]
+    assert shards[0].lp == 2 and int(np.sum(shards[0].owner < 0)) == 8
+    repl_leaves = [b for b in topo["lvl_leaves_1"]]
+    assert len(repl_leaves) == 7
+
+    def rank(r):
+        t = shards[r].make_tree(lib, topo, 2, 1, device=device)
+        shards[r].attach(t)
+        t.put_cc(1, x)
+        out = [t.sum_cc(1), t.sum_cc(1, 2), t.maxabs_cc(1)]
+        shards[r].detach()
+        t.close()
+        return out
+
+    try:
+        with ThreadPoolExecutor(world) as ex:
+            parts = list(ex.map(rank, range(world)))
+    finally:
+        group.close()
+    return ref, parts
+
+
+def _check_sums(ref, parts):
+    for p in parts:
+        assert p == parts[0]  # every rank holds the same all-reduced value
+        # the sum over ranks regroups the additions: equal to rounding; a
+        # replicated leaf counted twice would be off by ~7/36 of the total
+        np.testing.assert_allclose(p[:2], ref[:2], rtol=1e-13)
+        assert p[2] == ref[2]
+
+
+def test_sharded_sum_counts_replicated_leaves_once_oracle():
+    """af_tree_sum_cc on a sharded tree (the SUM all-reduce): the leaves of
+    the replicated levels below the partition level count once, as on a
+    single rank -- the oracle's twin, thread ranks."""
+    _check_sums(*_sharded_sums(capi.oracle_library()))
+
+
+@pytest.mark.gpu
+def test_sharded_sum_counts_replicated_leaves_once_hip():
+    _check_sums(*_sharded_sums(capi.hip_library(), device=0))
+
+
 def _run_rod(lib, topo, shard=None):
     """Config 4's shape: the reference's rod-electrode AMR tree
     (tests/golden/rod8.npz, level-set stencils) -- two V-cycles, the

@@ -1,7 +1,7 @@
 """V-cycles replayed as captured hipGraphs (launch amortisation in
 afh_mg_fas_vcycle*): bitwise the eager launches, across regrids (new trees,
-new graphs) and boundary-condition changes (afh_set_cc_methods drops the
-captured graph)."""
+new graphs) and boundary-condition changes (afh_set_cc_methods and
+afh_set_bc drop the captured graph)."""
 import os
 
 import numpy as np
@@ -25,6 +25,19 @@ def _run(graphs, steps=6):
         sim.voltage *= 1.25
         sim.tree.set_cc_methods(sim.i_phi, sim.phi_bc(), capi.RB_MG_SIDES)
         res = sim.field_compute(0, True)
+        res += sim.field_compute(0, True)
+        # the same through afh_set_bc (field_set_voltage's route,
+        # INTEGRATION.md): a value change, then a type change (the coarse
+        # solve's tables follow the types) and back
+        sim.voltage *= 0.5
+        sim.tree.set_bc(sim.i_phi, 6, capi.BC_DIRICHLET, sim.voltage)
+        res += sim.field_compute(0, True)
+        res += sim.field_compute(0, True)
+        sim.tree.set_bc(sim.i_phi, 1, capi.BC_DIRICHLET, 0.0)
+        res += sim.field_compute(0, True)
+        res += sim.field_compute(0, True)
+        sim.tree.set_bc(sim.i_phi, 1, capi.BC_NEUMANN, 0.0)
+        res += sim.field_compute(0, True)
         res += sim.field_compute(0, True)
     finally:
         if old is None:
