@@ -92,7 +92,7 @@ class MgDesc(C.Structure):
     _fields_ = [("i_phi", i32), ("i_rhs", i32), ("i_tmp", i32),
                 ("n_cycle_down", i32), ("n_cycle_up", i32),
                 ("helmholtz_lambda", f64), ("coarse_mode", i32),
-                ("coarse_cycles", i32)]
+                ("coarse_cycles", i32), ("coarse_tol", f64)]
 
 
 MAX_REFINE_REGIONS = 8
@@ -149,6 +149,7 @@ SIGNATURES = {
     "mg_fas_vcycle": (i32, [_VP, i32, i32]),
     "mg_fas_vcycle_maxres": (i32, [_VP, i32, P_f64]),
     "mg_fas_fmg": (i32, [_VP, i32, i32]),
+    "mg_coarse_iterations": (i32, [_VP, P_i32]),
     "mg_compute_phi_gradient": (i32, [_VP, i32, f64, i32]),
     "mg_set_box_stencil": (i32, [_VP, i32, P_f64, P_f64]),
     "mg_set_box_lsf": (i32, [_VP, i32, i32, P_i32, P_f64, P_f64, i32]),

@@ -121,13 +121,17 @@ class Simulation:
     """One streamer simulation (src/streamer.f90) over a C-ABI library."""
 
     def __init__(self, lib, case, device=-1, coarse_cycles=0, capacity_factor=2.0,
-                 fuse_rhs=True, user=None):
+                 fuse_rhs=True, user=None, coarse_tol=0.0):
         """user: the program's m_user hooks (afh.users), e.g. the gas density
-        function and initial conditions of programs/3d_sprite."""
+        function and initial conditions of programs/3d_sprite.
+        coarse_cycles / coarse_tol: the level-1 solve (0: exact; else at most
+        coarse_cycles MG cycles, stopped at |r| < coarse_tol |b| when
+        coarse_tol > 0 -- HYPRE PFMG's rule, the reference's solver)."""
         c = case if isinstance(case, Case) else Case(case)
         self.c, self.lib, self.device = c, lib, device
         self.user = user
         self.coarse_cycles = coarse_cycles
+        self.coarse_tol = coarse_tol
         self.capacity_factor = capacity_factor
         self.fused_rhs = fuse_rhs
         if c.s("time_integrator") != "heuns_method":
@@ -262,13 +266,14 @@ class Simulation:
             self.fluid.close()
         self.tree = tree
         self.mg = Multigrid(tree, self.i_phi, self.i_rhs, self.i_tmp,
-                            coarse_cycles=self.coarse_cycles)
+                            coarse_cycles=self.coarse_cycles, coarse_tol=self.coarse_tol)
         self.helm = []
         if self.photoi:
             for iv, lam in zip(self.helm_iv, self.helm_lambdas):
                 self.helm.append(Multigrid(tree, iv, self.i_rhs, self.i_tmp,
                                            helmholtz_lambda=lam * lam,
-                                           coarse_cycles=self.coarse_cycles))
+                                           coarse_cycles=self.coarse_cycles,
+                                           coarse_tol=self.coarse_tol))
         c = self.c
         td_cols = c.ia("td_cols")
         self.fluid = Fluid(
@@ -336,6 +341,11 @@ class Simulation:
             t.set_cc_prolong(self.i_photo, capi.PROLONG_LINEAR)
             for iv in self.helm_iv:  # mg_helm(n)%sides_bc, mg_sides_rb
                 t.set_cc_methods(iv, helm_bc, capi.RB_MG_SIDES)
+                # mg_init (m_af_multigrid.f90:102-105) sets the methods without
+                # a prolongation argument: af_prolong_linear, and the mode's
+                # phi becomes an auto variable (prolonged into new boxes,
+                # m_af_core.f90:387-391, 420-425, 842-881)
+                t.set_cc_prolong(iv, capi.PROLONG_LINEAR)
         # field_initialize (m_field.f90:349-350)
         t.set_cc_methods(self.i_efld, neumann0, capi.RB_GC_INTERP)
         t.set_cc_prolong(self.i_efld, capi.PROLONG_LINEAR)
@@ -345,9 +355,14 @@ class Simulation:
             for s in range(self.n_states + 1):
                 t.set_cc_methods(iv + s, neumann0, capi.RB_GC_INTERP_LIM)
             t.set_cc_prolong(iv, capi.PROLONG_LIMIT)
-        # phi and its copy: field_bc_homogeneous, mg_sides_rb
+        # phi and its copy: field_bc_homogeneous, mg_sides_rb; mg_init
+        # (m_af_multigrid.f90:102-105) makes phi (not its copy) an auto
+        # variable with af_prolong_linear: new boxes get phi prolonged from
+        # their parent and their ghost cells filled (auto_prolong,
+        # m_af_core.f90:842-881), the guess of the field solve after a regrid
         for s in (0, 1):
             t.set_cc_methods(self.i_phi + s, self.phi_bc(), capi.RB_MG_SIDES)
+        t.set_cc_prolong(self.i_phi, capi.PROLONG_LINEAR)
         # streamer.f90:98-104: rhs gets neumann_zero, af_gc_interp, limit
         t.set_cc_methods(self.i_rhs, neumann0, capi.RB_GC_INTERP)
         t.set_cc_prolong(self.i_rhs, capi.PROLONG_LIMIT)
@@ -659,6 +674,7 @@ class Simulation:
         for a CPU baseline): topology, every cell and face variable, time."""
         import copy
         other = Simulation(lib, self.c, device=device, coarse_cycles=self.coarse_cycles,
+                           coarse_tol=self.coarse_tol,
                            capacity_factor=self.capacity_factor, fuse_rhs=self.fused_rhs,
                            user=self.user)
         other.af = copy.deepcopy(self.af)

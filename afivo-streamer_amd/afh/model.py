@@ -242,16 +242,19 @@ class Multigrid:
     """mg_t bound to a tree (mg_init / mg_fas_vcycle)."""
 
     def __init__(self, tree, i_phi, i_rhs, i_tmp, n_cycle_down=2, n_cycle_up=2,
-                 helmholtz_lambda=0.0, coarse_cycles=20, coarse_mode=None):
+                 helmholtz_lambda=0.0, coarse_cycles=20, coarse_mode=None,
+                 coarse_tol=0.0):
         """coarse_mode: capi.COARSE_CYCLES (coarse_cycles MG cycles on the
         level-1 grid) or capi.COARSE_DIRECT (exact separable solve); None
-        picks COARSE_DIRECT when coarse_cycles == 0."""
+        picks COARSE_DIRECT when coarse_cycles == 0. coarse_tol > 0 (cycles
+        only): HYPRE PFMG's stopping rule, |r|_2 < coarse_tol |b|_2 within at
+        most coarse_cycles cycles."""
         if coarse_mode is None:
             coarse_mode = capi.COARSE_DIRECT if coarse_cycles == 0 else capi.COARSE_CYCLES
         self.tree = tree
         self.lib = tree.lib
         d = capi.MgDesc(i_phi, i_rhs, i_tmp, n_cycle_down, n_cycle_up,
-                        helmholtz_lambda, coarse_mode, coarse_cycles)
+                        helmholtz_lambda, coarse_mode, coarse_cycles, coarse_tol)
         self.i_phi, self.i_rhs, self.i_tmp = i_phi, i_rhs, i_tmp
         h = C.c_void_p()
         self.lib.call("mg_create", tree.h, C.byref(d), C.byref(h))
@@ -306,6 +309,12 @@ class Multigrid:
     def fas_fmg(self, set_residual=True, have_guess=True):
         """mg_fas_fmg (m_af_multigrid.f90:137-180)."""
         self.lib.call("mg_fas_fmg", self.h, int(set_residual), int(have_guess))
+
+    def coarse_iterations(self):
+        """Level-1 cycles of the last coarse solve (PFMG's GetNumIteration)."""
+        n = C.c_int32()
+        self.lib.call("mg_coarse_iterations", self.h, C.byref(n))
+        return n.value
 
     def compute_phi_gradient(self, i_fc, fac=-1.0, i_norm=0):
         self.lib.call("mg_compute_phi_gradient", self.h, i_fc, fac, i_norm)

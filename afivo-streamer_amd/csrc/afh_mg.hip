@@ -1562,6 +1562,33 @@ __device__ __forceinline__ double cs_res(const CsParams &P, int m, int i, int j,
   return P.f[m][gix(P, m, i, j, k)] - a;
 }
 
+// per-workgroup partial sums of r^2 (res) or f^2 over MG level 0 (the
+// stopping rule of the multi-launch coarse cycles; summed on the host in
+// workgroup order)
+__global__ void k_cs_norm2(CsParams P, int res, double *__restrict__ part) {
+  __shared__ double s_part[4];
+  const int nx = P.dims[0][0], ny = P.dims[0][1], nz = P.dims[0][2];
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  double v = 0.0;
+  if (t < nx * ny * nz) {
+    const int i = t % nx + 1, j = (t / nx) % ny + 1, k = t / (nx * ny) + 1;
+    const double x = res ? cs_res(P, 0, i, j, k) : P.f[0][gix(P, 0, i, j, k)];
+    v = x * x;
+  }
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+  if ((threadIdx.x & 63) == 0) s_part[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = ((s_part[0] + s_part[1]) + s_part[2]) + s_part[3];
+}
+
+// u = 0 on MG level 0 (PFMG with a zero rhs)
+__global__ void k_cs_zero(CsParams P) {
+  const int nx = P.dims[0][0], ny = P.dims[0][1], nz = P.dims[0][2];
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nx * ny * nz) return;
+  P.u[0][gix(P, 0, t % nx + 1, (t / nx) % ny + 1, t / (nx * ny) + 1)] = 0.0;
+}
+
 // coarse cell (i, j, k) of level c = m + 1: mean of the 8 fine residuals
 // (computed here, never stored), u = 0
 __device__ __forceinline__ void cs_rstr_cell(const CsParams &P, int c, int i,
@@ -1843,9 +1870,26 @@ __device__ void sm_smooth(double *lds, const SmLvl *lv, const double *dtab,
 // of at most CS_WAVE_CELLS cells down to the bottom and back, wave 0 works
 // alone (no workgroup barriers: a wave's LDS operations complete in order,
 // so a compiler fence is all a pass needs).
+// sum of v over the workgroup, the same value in every thread (wave
+// shuffles, then the waves' partials in order)
+__device__ double cs_block_sum(double v, double *part) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = v;
+  __syncthreads();
+  double s = 0.0;
+  for (int q = 0; q < (int)(blockDim.x >> 6); q++) s += part[q];
+  return s;
+}
+
+// tol2 > 0: HYPRE PFMG's stopping rule on level m0 = 0 (|r|^2 < tol2 |b|^2
+// after a cycle, at most n_cycles; b = 0 gives u = 0); the cycles run go to
+// *cycles_out (when set)
 __global__ void __launch_bounds__(1024) k_cs_small(CsParams G, int m0,
-                                                   int n_cycles, int wave_cells) {
+                                                   int n_cycles, int wave_cells,
+                                                   double tol2, int *cycles_out) {
   extern __shared__ double lds[];
+  __shared__ double s_part[16];
   __shared__ SmLvl s_lv[MAXMG];
   __shared__ double s_dtab[MAXMG * 64 * 2];  // (diag, 1/diag) per class
   __shared__ int s_bct[6];
@@ -1882,7 +1926,21 @@ __global__ void __launch_bounds__(1024) k_cs_small(CsParams G, int m0,
   int mw = m0;
   while (mw < bot && s_lv[mw].nx * s_lv[mw].ny * s_lv[mw].nz > wave_cells) mw++;
   const bool wave_tail = s_lv[mw].nx * s_lv[mw].ny * s_lv[mw].nz <= wave_cells;
-  for (int cyc = 0; cyc < n_cycles; cyc++) {
+  double bb = 0.0;
+  if (tol2 > 0) {
+    const SmLvl L = s_lv[m0];
+    const int N = L.nx * L.ny * L.nz;
+    double p = 0.0;
+    for (int t = threadIdx.x; t < N; t += blockDim.x) p += lds[L.fo + t] * lds[L.fo + t];
+    bb = cs_block_sum(p, s_part);
+    if (bb == 0.0) {
+      for (int t = threadIdx.x; t < N; t += blockDim.x) lds[L.uo + t] = 0.0;
+      __syncthreads();
+      n_cycles = 0;
+    }
+  }
+  int cyc = 0;
+  while (cyc < n_cycles) {
     for (int m = m0; m < mw; m++) {
       sm_smooth<false>(lds, s_lv, s_dtab, m, 2);
       sm_rstr<false>(lds, s_lv, s_dtab, m);
@@ -1907,7 +1965,21 @@ __global__ void __launch_bounds__(1024) k_cs_small(CsParams G, int m0,
       sm_prol<false>(lds, s_lv, s_bct, m);
       sm_smooth<false>(lds, s_lv, s_dtab, m, 2);
     }
+    cyc++;
+    if (tol2 > 0) {
+      const SmLvl L = s_lv[m0];
+      const double *dt = s_dtab + m0 * 128;
+      double p = 0.0;
+      for (int t = threadIdx.x; t < L.nx * L.ny * L.nz; t += blockDim.x) {
+        int i, j, k;
+        sm_decode(L, t, i, j, k);
+        const double r = sm_res(lds, dt, L, i, j, k);
+        p += r * r;
+      }
+      if (cs_block_sum(p, s_part) / bb < tol2) break;  // the same in every thread
+    }
   }
+  if (cycles_out && threadIdx.x == 0) *cycles_out = cyc;
   {
     const SmLvl L = s_lv[m0];
     const int N = L.nx * L.ny * L.nz;
@@ -2036,6 +2108,13 @@ struct afh_mg {
   uint64_t phi_gc_gen = UINT64_MAX;
   bool cs_fused = true;       // AFH_CS_FUSED=0: the electrode coarse solve launch per pair
   int *cs_iters = nullptr;     // pairs the last k_cs_electrode took
+  // level-1 cycles of the last coarse solve (afh_mg_coarse_iterations): on
+  // the device when k_cs_small applied the stopping rule, else on the host
+  int *d_cycles = nullptr;
+  int cycles_host = 0;
+  bool cycles_on_dev = false;
+  double *d_norm = nullptr;   // k_cs_norm2 partial sums
+  std::vector<double> h_norm;
   bool rstr_col = true;       // AFH_RSTR_COL=0: one coarse cell per thread (k_rstr_fas)
   int pair_ks = 4;           // AFH_GSRB_PAIR_KS: k chunks on 64..255-box levels (NC = 64;
                              // 4 whole-box chunks, 44 quarter-box tiles x 4, 0 tiles)
@@ -2165,6 +2244,8 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
   if (!(d->coarse_mode == AFH_COARSE_DIRECT ||
         (d->coarse_mode == AFH_COARSE_CYCLES && d->coarse_cycles >= 1)))
     return set_error(AFH_ERR_UNSUPPORTED, "coarse solver mode");
+  if (!(d->coarse_tol >= 0.0))
+    return set_error(AFH_ERR_ARG, "afh_mg_create: coarse_tol %g", d->coarse_tol);
   afh_mg *mg = new afh_mg();
   mg->t = t;
   mg->d = *d;
@@ -2256,6 +2337,7 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
   if (const char *env = getenv("AFH_RSTR_COL")) mg->rstr_col = atoi(env) != 0;
   if (const char *env = getenv("AFH_CS_FUSED")) mg->cs_fused = atoi(env) != 0;
   AFH_HIP(hipMalloc(&mg->cs_iters, sizeof(int)));
+  AFH_HIP(hipMalloc(&mg->d_cycles, sizeof(int)));
   if (const char *env = getenv("AFH_GSRB_PAIR_BOX")) mg->pair_box = atoi(env) != 0;
   if (const char *env = getenv("AFH_GSRB_PAIR_KS")) mg->pair_ks = atoi(env);
   if (const char *env = getenv("AFH_GRAD_NT")) mg->grad_nt = atoi(env) != 0;
@@ -2321,6 +2403,8 @@ int32_t afh_mg_destroy(afh_mg *mg) {
   hipFree(mg->d_vp), hipFree(mg->d_bp), hipFree(mg->d_dd), hipFree(mg->d_bv);
   hipFree(mg->d_ix), hipFree(mg->d_lsf_n), hipFree(mg->cs_old);
   hipFree(mg->cs_iters);
+  hipFree(mg->d_cycles);
+  hipFree(mg->d_norm);
   for (LevelList *L : {&mg->ids_c, &mg->ids_v, &mg->leaves_c, &mg->leaves_v,
                        &mg->parents_c, &mg->parents_v, &mg->lsf_leaves})
     hipFree(L->d);
@@ -2887,12 +2971,43 @@ static int32_t solve_coarse(afh_mg *mg) {
                          mg->d_e[0], mg->d_e[1], mg->d_e[2], nx, ny, nz, q.d,
                          q.div, lam);
     AFH_LAUNCH_CHECK("k_cs_transform");
+    mg->cycles_host = 0, mg->cycles_on_dev = false;
   } else if (s == 0) {
-    hipLaunchKernelGGL(k_cs_small, dim3(1), dim3(1024), mg->small_lds,
-                       t->stream, P, 0, mg->d.coarse_cycles, mg->wave_cells);
+    const double tol2 = mg->d.coarse_tol > 0 ? mg->d.coarse_tol * mg->d.coarse_tol : 0.0;
+    hipLaunchKernelGGL(k_cs_small, dim3(1), dim3(1024), mg->small_lds, t->stream, P, 0,
+                       mg->d.coarse_cycles, mg->wave_cells, tol2, mg->d_cycles);
     AFH_LAUNCH_CHECK("k_cs_small");
+    mg->cycles_host = mg->d.coarse_cycles, mg->cycles_on_dev = tol2 > 0;
   } else {
-    for (int cyc = 0; cyc < mg->d.coarse_cycles; cyc++) {
+    // with the stopping rule: |b|^2 first, |r|^2 after every cycle, read on
+    // the host (no graph capture then, vcycle_graph)
+    const bool tol = mg->d.coarse_tol > 0;
+    const int n0 = P.dims[0][0] * P.dims[0][1] * P.dims[0][2], nblk = (n0 + 255) / 256;
+    auto norm2 = [&](int res, double &out) -> int32_t {
+      if (!mg->d_norm) AFH_HIP(hipMalloc(&mg->d_norm, sizeof(double) * nblk));
+      mg->h_norm.resize(nblk);
+      hipLaunchKernelGGL(k_cs_norm2, dim3(nblk), dim3(256), 0, t->stream, P, res, mg->d_norm);
+      AFH_LAUNCH_CHECK("k_cs_norm2");
+      AFH_HIP(hipMemcpyAsync(mg->h_norm.data(), mg->d_norm, sizeof(double) * nblk,
+                             hipMemcpyDeviceToHost, t->stream));
+      AFH_HIP(hipStreamSynchronize(t->stream));
+      out = 0.0;
+      for (double v : mg->h_norm) out += v;
+      return AFH_OK;
+    };
+    double bb = 0.0;
+    int n_cyc = mg->d.coarse_cycles;
+    if (tol) {
+      if (int32_t e = norm2(0, bb)) return e;
+      if (bb == 0.0) {
+        hipLaunchKernelGGL(k_cs_zero, dim3(nblk), dim3(256), 0, t->stream, P);
+        AFH_LAUNCH_CHECK("k_cs_zero");
+        n_cyc = 0;
+      }
+    }
+    const double eps = tol ? mg->d.coarse_tol * mg->d.coarse_tol : 0.0;
+    int done = 0;
+    for (int cyc = 0; cyc < n_cyc; cyc++) {
       for (int m = 0; m < s; m++) {
         const size_t N = (size_t)P.dims[m][0] * P.dims[m][1] * P.dims[m][2];
         for (int sw = 0; sw < 2; sw++)
@@ -2903,7 +3018,7 @@ static int32_t solve_coarse(afh_mg *mg) {
                            m + 1);
       }
       hipLaunchKernelGGL(k_cs_small, dim3(1), dim3(1024), mg->small_lds,
-                         t->stream, P, s, 1, mg->wave_cells);
+                         t->stream, P, s, 1, mg->wave_cells, 0.0, (int *)nullptr);
       for (int m = s - 1; m >= 0; m--) {
         const size_t N = (size_t)P.dims[m][0] * P.dims[m][1] * P.dims[m][2];
         hipLaunchKernelGGL(k_cs_prol, blocks1(N), dim3(256), 0, t->stream, P, m);
@@ -2912,8 +3027,15 @@ static int32_t solve_coarse(afh_mg *mg) {
             hipLaunchKernelGGL(k_cs_gsrb, blocks1(N / 2), dim3(256), 0,
                                t->stream, P, m, n);
       }
+      done = cyc + 1;
+      if (tol) {
+        double rr;
+        if (int32_t e = norm2(1, rr)) return e;
+        if (rr / bb < eps) break;
+      }
     }
     AFH_LAUNCH_CHECK("coarse solver cycle");
+    mg->cycles_host = done, mg->cycles_on_dev = false;
   }
   hipLaunchKernelGGL(k_cs_scatter, dim3((n3 + 255) / 256, nid), dim3(256), 0,
                      t->stream, P, t->ccv(mg->d.i_phi), t->d_boxes,
@@ -3053,8 +3175,11 @@ static int32_t vcycle_graph(afh_mg *mg, int32_t set_residual, int max_lvl, bool 
                             bool top_stale, bool &done) {
   afh_tree *t = mg->t;
   done = false;
+  // (the multi-launch coarse cycles with a stopping rule read the device
+  // every cycle too)
   if (!mg->use_graphs || t->hook || t->prof_class ||
-      (mg->any_var && mg->lvl_var[0] && !cs_electrode_fused(mg)))
+      (mg->any_var && mg->lvl_var[0] && !cs_electrode_fused(mg)) ||
+      (mg->d.coarse_mode == AFH_COARSE_CYCLES && mg->d.coarse_tol > 0 && mg->small_from > 0))
     return AFH_OK;
   const int key = (max_lvl << 3) | (top_stale ? 4 : 0) | (set_residual ? 2 : 0) |
                   (max_out ? 1 : 0);
@@ -3117,6 +3242,20 @@ int32_t afh_mg_fas_vcycle(afh_mg *mg, int32_t set_residual, int32_t hl) {
 int32_t afh_mg_fas_vcycle_maxres(afh_mg *mg, int32_t hl, double *max_res) {
   if (!max_res) return set_error(AFH_ERR_ARG, "null max_res");
   return vcycle_impl(mg, 1, hl, max_res);
+}
+
+int32_t afh_mg_coarse_iterations(afh_mg *mg, int32_t *n) {
+  if (!mg || !n) return set_error(AFH_ERR_ARG, "afh_mg_coarse_iterations: null");
+  AFH_LIVE(mg->t, "afh_mg_coarse_iterations");
+  *n = mg->cycles_host;
+  if (mg->cycles_on_dev) {
+    int v = 0;
+    AFH_HIP(hipMemcpyAsync(&v, mg->d_cycles, sizeof(int), hipMemcpyDeviceToHost,
+                           mg->t->stream));
+    AFH_HIP(hipStreamSynchronize(mg->t->stream));
+    *n = v;
+  }
+  return AFH_OK;
 }
 
 int32_t afh_mg_compute_phi_gradient(afh_mg *mg, int32_t i_fc, double fac,

@@ -189,6 +189,7 @@ module m_afivo_hip
      real(c_double)     :: helmholtz_lambda
      integer(c_int32_t) :: coarse_mode
      integer(c_int32_t) :: coarse_cycles
+     real(c_double)     :: coarse_tol = 0   ! PFMG's stopping rule (0: fixed cycles)
   end type afh_mg_desc
 
   interface
@@ -333,6 +334,14 @@ module m_afivo_hip
        integer(c_int32_t), value :: set_residual, have_guess
        integer(c_int32_t)        :: afh_mg_fas_fmg
      end function afh_mg_fas_fmg
+
+     !> HYPRE_StructPFMGGetNumIteration (m_coarse_solver.f90:433-435)
+     function afh_mg_coarse_iterations(mg, n) bind(C, name=afh_pfx//"mg_coarse_iterations")
+       import
+       type(c_ptr), value              :: mg
+       integer(c_int32_t), intent(out) :: n
+       integer(c_int32_t)              :: afh_mg_coarse_iterations
+     end function afh_mg_coarse_iterations
 
      !> af_tree_sum_cc (m_af_utils.f90:966-1026)
      function afh_tree_sum_cc(t, iv, power, out) bind(C, name=afh_pfx//"tree_sum_cc")

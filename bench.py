@@ -215,6 +215,23 @@ def pmc_traffic(config):
     return None
 
 
+def write_topology(case, config, path):
+    """Boxes, leaves and parents per level, the box size and the species
+    counts of the benchmarked tree (scripts/prof_steady.py)."""
+    topo = case.topo
+    nl = int(topo["highest_lvl"])
+    cnt = lambda kind: [len(topo["lvl_%s_%d" % (kind, l)]) for l in range(1, nl + 1)]  # noqa: E731
+    if isinstance(case, DriverCase):
+        charges = [case.sim.species_charge[n] for n in case.sim.plasma]
+    else:
+        charges = [-1, 1, -1]  # e, M+, M-
+    with open(path, "w") as f:
+        json.dump({"config": config, "nc": int(topo["nc"]), "ids": cnt("ids"),
+                   "leaves": cnt("leaves"), "parents": cnt("parents"),
+                   "n_species": len(charges),
+                   "n_charged": sum(1 for q in charges if q != 0)}, f)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -321,6 +338,10 @@ def main():
                           device="cuda" if torch.cuda.is_available() else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
+
+    if rank == 0 and os.environ.get("AFH_BENCH_TOPO"):
+        # the run's topology for scripts/prof_steady.py's byte model
+        write_topology(case, args.config, os.environ["AFH_BENCH_TOPO"])
 
     if rank == 0:
         avg_s = ms.value / 1e3 / max(1, nl.value)

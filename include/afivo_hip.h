@@ -202,7 +202,13 @@ typedef struct afh_mg_desc {
   double helmholtz_lambda;
   int32_t coarse_mode;   /* AFH_COARSE_CYCLES or AFH_COARSE_DIRECT */
   int32_t coarse_cycles; /* AFH_COARSE_CYCLES: MG V(2,2) cycles on the
-                            level-1 grid */
+                            level-1 grid (at most, with coarse_tol) */
+  /* AFH_COARSE_CYCLES: stop once the level-1 residual's 2-norm is below
+   * coarse_tol times the (boundary-folded) rhs's, as HYPRE PFMG's
+   * SetTol does (m_coarse_solver.f90:408-414, 433-435; tolerance 1e-6 and
+   * at most 50 iterations by default, m_af_types.f90:560-565); a zero rhs
+   * gives phi = 0 there. 0: always coarse_cycles cycles. */
+  double coarse_tol;
 } afh_mg_desc;
 
 typedef struct afh_tree afh_tree;
@@ -275,6 +281,10 @@ int32_t afh_mg_fas_vcycle_maxres(afh_mg *mg, int32_t highest_lvl,
  * starts from phi = 0 on levels >= 2 (field_compute at start-up,
  * src/m_field.f90:447-470) */
 int32_t afh_mg_fas_fmg(afh_mg *mg, int32_t set_residual, int32_t have_guess);
+/* HYPRE_StructPFMGGetNumIteration (m_coarse_solver.f90:433-435): level-1
+ * cycles of the last coarse solve (AFH_COARSE_CYCLES; 0 for the direct
+ * solve); synchronises the tree's stream. */
+int32_t afh_mg_coarse_iterations(afh_mg *mg, int32_t *n);
 /* mg_compute_phi_gradient (m_af_multigrid.f90:1837-1879) incl. the norm */
 int32_t afh_mg_compute_phi_gradient(afh_mg *mg, int32_t i_fc, double fac,
                                     int32_t i_norm);

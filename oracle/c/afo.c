@@ -109,6 +109,7 @@ struct afh_mg {
   int32_t **lsf_ix;
   double **lsf_dd, **lsf_bv;
   int i_lsf;
+  int cs_iters; /* level-1 cycles of the last coarse solve */
 };
 
 #define AFH_CS_BOTTOM_SWEEPS 16
@@ -994,6 +995,36 @@ static void cs_gsrb(afh_mg *mg, int m, int n) {
     }
 }
 
+/* f - A u at cell (i, j, k) of MG level m (cs_residual_restrict's order) */
+static double cs_res_cell(afh_mg *mg, int m, int i, int j, int k) {
+  const double *u = mg->u[m];
+  int nx = mg->dims[m][0], ny = mg->dims[m][1], nz = mg->dims[m][2];
+  const double *h = mg->hc[m];
+  double a = cs_diag(mg, m, i, j, k) * u[GIX(mg, m, i, j, k)];
+  if (i > 1) a = a + h[0] * u[GIX(mg, m, i - 1, j, k)];
+  if (i < nx) a = a + h[0] * u[GIX(mg, m, i + 1, j, k)];
+  if (j > 1) a = a + h[1] * u[GIX(mg, m, i, j - 1, k)];
+  if (j < ny) a = a + h[1] * u[GIX(mg, m, i, j + 1, k)];
+  if (k > 1) a = a + h[2] * u[GIX(mg, m, i, j, k - 1)];
+  if (k < nz) a = a + h[2] * u[GIX(mg, m, i, j, k + 1)];
+  return mg->f[m][GIX(mg, m, i, j, k)] - a;
+}
+
+/* HYPRE's hypre_StructInnerProd of the residual (res = 1) or of the rhs
+ * with itself on the level-1 grid, cells i fastest (the device sums in
+ * another order: equal to rounding, which only matters for a stopping test
+ * that falls within rounding of the tolerance) */
+static double cs_norm2(afh_mg *mg, int res) {
+  double s = 0.0;
+  for (int k = 1; k <= mg->dims[0][2]; k++)
+    for (int j = 1; j <= mg->dims[0][1]; j++)
+      for (int i = 1; i <= mg->dims[0][0]; i++) {
+        const double v = res ? cs_res_cell(mg, 0, i, j, k) : mg->f[0][GIX(mg, 0, i, j, k)];
+        s = s + v * v;
+      }
+  return s;
+}
+
 /* residual on level m restricted (8-cell mean) into f[m+1]; u[m+1] = 0 */
 static void cs_residual_restrict(afh_mg *mg, int m) {
   double *u = mg->u[m], *f = mg->f[m], *r = mg->r[m];
@@ -1262,9 +1293,29 @@ int32_t afo_mg_solve_coarse(afh_mg *mg) {
   }
   if (mg->d.coarse_mode == AFH_COARSE_DIRECT) {
     cs_direct_solve(mg);
+    mg->cs_iters = 0;
+  } else if (mg->d.coarse_tol > 0) {
+    /* HYPRE PFMG's stopping rule (pfmg_solve: r.r / b.b < tol^2, at most
+     * max_iter cycles; b = 0 gives x = 0), with our V(2,2) cycles */
+    cs_build_table(mg);
+    const double bb = cs_norm2(mg, 0), eps = mg->d.coarse_tol * mg->d.coarse_tol;
+    int c = 0;
+    if (bb == 0.0) {
+      for (int k = 1; k <= mg->dims[0][2]; k++)
+        for (int j = 1; j <= mg->dims[0][1]; j++)
+          for (int i = 1; i <= mg->dims[0][0]; i++) mg->u[0][GIX(mg, 0, i, j, k)] = 0.0;
+    } else {
+      while (c < mg->d.coarse_cycles) {
+        cs_cycle(mg, 0);
+        c++;
+        if (cs_norm2(mg, 1) / bb < eps) break;
+      }
+    }
+    mg->cs_iters = c;
   } else {
     cs_build_table(mg);
     for (int c = 0; c < mg->d.coarse_cycles; c++) cs_cycle(mg, 0);
+    mg->cs_iters = mg->d.coarse_cycles;
   }
   /* coarse_solver_get_phi */
   for (int q = 0; q < nid; q++) {
@@ -1350,6 +1401,12 @@ int32_t afo_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
     return fail(AFH_ERR_UNSUPPORTED, "coarse solver mode");
   }
   *out = mg;
+  return AFH_OK;
+}
+
+int32_t afo_mg_coarse_iterations(afh_mg *mg, int32_t *n) {
+  if (!mg || !n) return fail(AFH_ERR_ARG, "afo_mg_coarse_iterations: null");
+  *n = mg->cs_iters;
   return AFH_OK;
 }
 

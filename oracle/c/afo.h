@@ -60,6 +60,7 @@ int32_t afo_mg_fas_vcycle(afh_mg *mg, int32_t set_residual,
 int32_t afo_mg_fas_vcycle_maxres(afh_mg *mg, int32_t highest_lvl,
                                  double *max_res);
 int32_t afo_mg_fas_fmg(afh_mg *mg, int32_t set_residual, int32_t have_guess);
+int32_t afo_mg_coarse_iterations(afh_mg *mg, int32_t *n);
 int32_t afo_mg_compute_phi_gradient(afh_mg *mg, int32_t i_fc, double fac,
                                     int32_t i_norm);
 int32_t afo_mg_set_box_stencil(afh_mg *mg, int32_t id, const double *v,

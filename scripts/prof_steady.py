@@ -3,58 +3,101 @@
 trace (--kernel-trace --output-format csv).
 
 The timed region of `bench.py --steps K` is the last K unit steps; each step
-ends with the species update (k_update, one launch per leaf level), so the
-window starts right after the (K+1)-th last run of k_update launches. Reports per step: kernel time by kernel, launch
-count, busy time, the gaps between consecutive kernels (launch overhead and
-host synchronisation) and the span; and, for the S1-64 leaf level (largest
-launch of each kernel), average duration, algorithmic bytes (DESIGN.md
-table) and the fraction of the 8 TB/s HBM peak.
+ends with the species update (k_update / k_fe_lds, one launch per leaf
+level), so the window starts right after the (K+1)-th last run of update
+launches. Reports per step: kernel time by kernel, launch count, busy time,
+the gaps between consecutive kernels (launch overhead and host
+synchronisation) and the span; and for the largest launch of each kernel
+its average duration, its algorithmic bytes and the fraction of the 8 TB/s
+HBM peak.
 
-Usage: prof_steady.py <run_kernel_trace.csv> <K> <out.json> [config]
+Algorithmic bytes follow SURVEY.md 8(d): bytes per cell
+of the pass x the cells of the launch. The cells come from the run's own
+topology, which bench.py writes when AFH_BENCH_TOPO names a file: per level
+the number of boxes, leaves and parents, the box size and the species
+counts. The largest launch of a kernel is taken to cover the level with the
+most boxes of the list the kernel runs over (all boxes, leaves or parents;
+the k-split / tiled pair only runs on levels of 64..255 boxes).
+
+Usage: prof_steady.py <run_kernel_trace.csv> <K> <out.json> <topo.json>
 """
 import collections
 import csv
 import json
+import re
 import sys
 
 PEAK = 8e12
-LEAF = 512 * 64 ** 3          # S1-64 leaf cells
-PARENT = 64 * 64 ** 3         # S1-64 level-3 boxes (parents of the leaves)
-# kernel (name prefix up to '(') -> (algorithmic bytes per cell, cells)
-ALG = {
-    "void afh::k_gsrb_pair2<64, 64, 1, 0, true, true, true, 1>": (24, LEAF),
-    "void afh::k_gsrb_pair2<64, 64, 1, 0, true, true, true, 4>": (24, PARENT),
-    "void afh::k_gsrb_pair2<64, 64": (24, LEAF),
-    "void afh::k_gsrb_pair2<64, 16": (24, PARENT),
-    "void afh::k_residual<true, 4>": (24, LEAF),
-    "void afh::k_residual<false, 4>": (24, PARENT),
-    "afh::k_rstr_fas": (18, LEAF),
-    "void afh::k_rstr_fas_col<2>": (18, LEAF),
-    "void afh::k_prolong<4>": (20, LEAF),
-    "afh::k_corr_tmp": (24, PARENT),
-    "afh::k_parent_rhs": (24, PARENT),
-    "void afh::k_gradient_t<64, 4>": (40, LEAF),
-    "void afh::k_gradient_t<64, 4, true>": (40, LEAF),
-    "void afh::k_flux_lds<64, 3>": (64 + 192 / 64, LEAF),
-    "void afh::k_update<3, false, 1": (8 * 3 * 2 + 32, LEAF),
-    "void afh::k_update<3, false, 2": (8 * 3 * 3 + 32, LEAF),
-    "afh::k_gc_faces": (96 / 64, LEAF),
-    "afh::k_gc2": (2 * 96 / 64, LEAF),
-    "void afh::k_set_rhs<true>": (32, LEAF),
-}
+
+
+def rules(topo):
+    """[(name regex, bytes per cell, list, level filter)]; first match wins."""
+    nc = topo["nc"]
+    nq = topo.get("n_charged", topo.get("n_species", 3))
+    small = lambda n: 64 <= n < 256  # noqa: E731  k-split / tiled pair levels
+    # the split half-sweep: levels below the fused pair's 64 boxes (nc >= 32),
+    # or a stale top level (any)
+    split = (lambda n: n < 64) if nc >= 32 else None
+
+    def upd(m):
+        ns, np_ = int(m.group(1)), int(m.group(2) or 2)
+        return 8 * ns * ((np_ if np_ in (1, 2) else 2) + 1) + 32
+
+    return [
+        (r"k_gsrb_pair2<64, 64, 1, 0, true, true, true, 4>", 24, "ids", small),
+        (r"k_gsrb_pair", 24, "ids", None),
+        (r"k_gsrb_v", 16, "ids", None),
+        (r"k_gsrb\(", 16, "ids", split),
+        (r"k_residual<true", 24, "leaves", None),
+        (r"k_residual<false", 24, "parents", None),
+        (r"k_rstr_fas", 18, "ids", None),
+        (r"k_prolong<", 20, "ids", None),
+        (r"k_corr_tmp", 24, "parents", None),
+        (r"k_parent_rhs", 24, "parents", None),
+        (r"k_gradient", 40, "all", None),
+        (r"k_flux_lds|k_flux_staged", 64 + 192 / nc, "leaves", None),
+        (r"k_update<(\d+), \w+(?:, (\d+))?", upd, "leaves", None),
+        (r"k_gc_faces", 96 / nc, "ids", None),
+        (r"k_gc2", 192 / nc, "leaves", None),
+        (r"k_set_rhs<", 8 * (nq + 1), "leaves", None),
+    ]
+
+
+def largest(topo, lst, filt):
+    if lst == "all":
+        return sum(topo["ids"])
+    counts = [n for n, tot in zip(topo[lst], topo["ids"]) if filt is None or filt(tot)]
+    return max(counts) if counts else 0
 
 
 def key(name):
-    for k in ALG:
-        if name.startswith(k):
-            return k
-    return name.split("(")[0]
+    """Kernel name without the argument list."""
+    depth = 0
+    for i, ch in enumerate(name):
+        if ch == "<":
+            depth += 1
+        elif ch == ">":
+            depth -= 1
+        elif ch == "(" and depth == 0:
+            return name[:i]
+    return name
 
 
-def main(path, k_steps, out):
+def algorithmic(name, topo):
+    for pat, b, lst, filt in rules(topo):
+        m = re.search(pat, name)
+        if m:
+            per_cell = b(m) if callable(b) else b
+            return per_cell * topo["nc"] ** 3 * largest(topo, lst, filt)
+    return None
+
+
+def main(path, k_steps, out, topo_path):
+    topo = json.load(open(topo_path))
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    upd = [i for i, r in enumerate(rows) if "k_update" in r["Kernel_Name"]]
+    upd = [i for i, r in enumerate(rows)
+           if "k_update" in r["Kernel_Name"] or "k_fe_lds" in r["Kernel_Name"]]
     # a step ends with the update of every leaf level (consecutive launches)
     ends = [i for n, i in enumerate(upd) if n + 1 == len(upd) or upd[n + 1] != i + 1]
     start = ends[-(k_steps + 1)] + 1
@@ -80,26 +123,33 @@ def main(path, k_steps, out):
         ent = {"kernel": k, "launches_per_step": n / k_steps,
                "us_per_step": tot / k_steps, "share": tot * 1e3 / busy,
                "largest_launch_avg_us": avg}
-        if k in ALG:
-            b = ALG[k][0] * ALG[k][1]
+        b = algorithmic(k, topo)
+        if b:
             ent.update({"algorithmic_bytes": b, "achieved_TBps": b / (avg * 1e-6) / 1e12,
                         "frac_of_8TBps": b / (avg * 1e-6) / PEAK})
         table.append(ent)
-    res = {"steps": k_steps, "launches_per_step": len(win) / k_steps,
+    res = {"config": topo.get("config"), "nc": topo["nc"],
+           "leaf_cells": topo["nc"] ** 3 * sum(topo["leaves"]),
+           "boxes_per_level": topo["ids"], "leaves_per_level": topo["leaves"],
+           "steps": k_steps, "launches_per_step": len(win) / k_steps,
            "span_ms_per_step": span / 1e6 / k_steps,
            "busy_ms_per_step": busy / 1e6 / k_steps,
-           "gap_ms_per_step": gaps / 1e6 / k_steps, "kernels": table}
+           "gap_ms_per_step": gaps / 1e6 / k_steps,
+           "gap_share": gaps / span if span else 0.0, "kernels": table}
     json.dump(res, open(out, "w"), indent=1)
-    print("per step: %.3f ms span, %.3f ms busy, %.3f ms gaps, %.0f launches" %
+    print("per step: %.3f ms span, %.3f ms busy, %.3f ms gaps (%.0f %%), %.0f launches" %
           (res["span_ms_per_step"], res["busy_ms_per_step"], res["gap_ms_per_step"],
-           res["launches_per_step"]))
-    for e in table[:16]:
-        print("%-34s %5.1f/step %8.1f us/step %5.1f%%  leaf %8.1f us %s" % (
-            e["kernel"][:34], e["launches_per_step"], e["us_per_step"], 100 * e["share"],
+           100 * res["gap_share"], res["launches_per_step"]))
+    for e in table[:18]:
+        print("%-40s %5.1f/step %8.1f us/step %5.1f%%  largest %8.1f us %s" % (
+            e["kernel"][:40], e["launches_per_step"], e["us_per_step"], 100 * e["share"],
             e["largest_launch_avg_us"],
             ("%.2f TB/s frac %.3f" % (e["achieved_TBps"], e["frac_of_8TBps"]))
             if "achieved_TBps" in e else ""))
+    bad = [e["kernel"] for e in table if e.get("frac_of_8TBps", 0) > 1]
+    if bad:
+        print("WARNING: fraction above 1 (byte model wrong) for", bad)
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], int(sys.argv[2]), sys.argv[3])
+    main(sys.argv[1], int(sys.argv[2]), sys.argv[3], sys.argv[4])

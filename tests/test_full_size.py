@@ -56,6 +56,44 @@ def test_full_size_deterministic_and_contracting(hip):
         assert np.array_equal(a, b), v
 
 
+def _s1_run(lib):
+    """BASELINE config 2 (S1): the bench's own S1 workload --
+    512 leaf boxes of 16^3, 585 boxes, 4 levels, 2.1 M leaf cells, the rhs
+    folded into the density update -- the initial field solve and two unit
+    steps (Heun stages 1 and 2)."""
+    import bench
+    from afh.streamer import IV
+    c = bench.build_case(lib, "s1", 0, 0)
+    c.fuse_rhs(True, ghosts=False)
+    out = {"res0": c.field_compute(0, n_vcycles=2)}
+    for k in range(2):
+        out["step%d" % k] = bench.unit_step(c, 1e-13, k)
+    for v in ("e", "pos", "neg", "phi", "efld", "rhs"):
+        out[v] = c.tree.get_cc(IV[v])
+        out[v + "1"] = c.tree.get_cc(IV[v] + 1) if v in ("e", "pos", "neg") else None
+    c.tree.close()
+    return out
+
+
+@pytest.mark.parametrize("graphs", ["1", "0"])
+def test_s1_config2_bitwise_equals_oracle(hip, graphs, monkeypatch):
+    """Config 2 at its full size, HIP == C oracle bitwise: every species
+    state, phi, |E| and rhs, the residuals and the dt limits; V-cycles
+    replayed as captured graphs and launched eagerly."""
+    from afh import capi
+    monkeypatch.setenv("AFH_GRAPHS", graphs)
+    a = _s1_run(hip)
+    b = _s1_run(capi.oracle_library())
+    assert a.keys() == b.keys()
+    for k in a:
+        if a[k] is None:
+            continue
+        if isinstance(a[k], np.ndarray):
+            assert np.array_equal(a[k], b[k]), (k, np.nanmax(np.abs(a[k] - b[k])))
+        else:
+            assert a[k] == b[k], (k, a[k], b[k])
+
+
 def test_full_size_flux_update_conserves_electrons(hip):
     import bench
     from afh.model import Fluid

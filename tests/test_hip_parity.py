@@ -207,7 +207,8 @@ def test_multigrids_sharing_a_tree(hip, oracle, name, smoother):
 @pytest.mark.parametrize("name", ["amr8", "uni16_l3"])
 def test_vcycle_from_stale_ghost_cells(hip, oracle, name, smoother):
     """A V-cycle whose phi has stale ghost cells (as after a regrid: afivo
-    neither prolongs nor fills phi) runs its top level's first leg split, as
+    fills the ghost cells of the new boxes only, not those of their
+    neighbours) runs its top level's first leg split, as
     the reference does: the fused pair's phase B would take this box's stale
     ghost column for the neighbour's boundary column. Seeded phi with zero
     ghost cells, uploaded; then V-cycles and an upload between them, bitwise

@@ -11,21 +11,24 @@ own initializers (tests/golden/rtest_*.npz, oracle/make_cases.py), AMR set-up,
 photoionization every 5 steps -- over the C oracle (CPU) and the HIP library
 (GPU), and compares against those committed rows.
 
-What is expected, and why:
-* rows 0-2 of test_3d (0 - 0.4 ns) and rows 0-1 of the chemistry cases match
-  within compare_logs' own tolerance;
-* rows up to 1.2 ns (test_3d: up to 1.4 ns) within 5e-5: the reference's
-  level-1 solve is HYPRE PFMG to a relative residual of 1e-6 (absent from the
-  snapshot, its result unpinned); the field solve of field_compute stops at
-  a residual of 1e-4 max|rhs|, so the solution depends on that solver at the
-  1e-5 level (an inexact one-cycle coarse solve moves the rows by ~8e-6);
-* later rows: the streamer head's alpha*dx approaches refine_adx = 1.5 and
-  reaches it within 0.3 % at 1.3 ns (step 44, 1.4966): the refinement that
-  follows happens at a step the reference evidently did not take at the same
-  time, after which sums agree within 1 % and maxima within 20 %.
-Independently of the logs, test_reference_replay pins the two ingredients on
-identical data to the reference's own code: every af_adjust_refinement call
-(topology id for id) and the species step (bitwise).
+What is expected, and why (profiles/r03_rtest_coarse_sensitivity.json,
+scripts/rtest_coarse_sensitivity.py):
+* the reference's level-1 solve is HYPRE PFMG stopped at a relative residual
+  of 1e-6 (afivo/src/m_coarse_solver.f90:393-439; HYPRE is absent from the
+  snapshot) and field_compute stops at a residual of 1e-4 max|rhs|, so the
+  rows depend on the coarse solver at the 1e-5 level: the same runs with the
+  level-1 solve exact or stopped at 1e-8 ... 1e-4 differ by up to 1.2e-5;
+* with PFMG's stopping rule (coarse_tol 1e-6, at most 50 cycles) test_3d
+  matches every row within compare_logs' own tolerance (max 8.9e-6); the
+  chemistry cases every row within 3e-5;
+* with the exact level-1 solve (the driver's default) every row of every
+  case is within 4e-5.
+Until round 3 the rows diverged by 1e-3 .. 2e-2 after 1.4 ns: the field
+solve after the first regrid (level 6 created at step 46) started from
+phi = 0 in the new boxes, because the driver did not make phi an auto
+variable as mg_init does (m_af_multigrid.f90:102-105: af_set_cc_methods
+without a prolongation method, so af_prolong_linear into every new box,
+m_af_core.f90:387-391, 420-425, 842-881).
 """
 import numpy as np
 import pytest
@@ -35,52 +38,58 @@ from afh import capi
 from afh.driver import Simulation
 
 CASES = ["test_3d", "test_3d_chem", "test_3d_photoi_chem"]
-# rows within compare_logs' tolerance, and the last row (0.2 ns each) before
-# the first refinement-timing divergence
-STRICT = {"test_3d": 3, "test_3d_chem": 2, "test_3d_photoi_chem": 2}
-LAST_CLOSE = {"test_3d": 7, "test_3d_chem": 6, "test_3d_photoi_chem": 6}
+# level-1 solves: (max cycles, tolerance) -- exact (AFH_COARSE_DIRECT), and
+# HYPRE PFMG's stopping rule with our V(2,2) cycles
+EXACT, PFMG = (0, 0.0), (50, 1e-6)
+# bound on every row's relative deviation from the reference, per level-1
+# solve: compare_logs' 1e-5 where the table shows it met, else the bound the
+# table justifies (measured max + the 1.2e-5 coarse-solve spread, rounded up)
+BOUND = {("test_3d", PFMG): 1e-5, ("test_3d", EXACT): 2.5e-5,
+         ("test_3d_chem", PFMG): 5e-5, ("test_3d_chem", EXACT): 5e-5,
+         ("test_3d_photoi_chem", PFMG): 5e-5, ("test_3d_photoi_chem", EXACT): 5e-5}
 
 
 def load(name):
     return golden.load("rtest_" + name)
 
 
-def run(lib, name, device=-1):
+def run(lib, name, device=-1, solve=EXACT):
     d = load(name)
-    sim = Simulation(lib, d, device=device)
+    sim = Simulation(lib, d, device=device, coarse_cycles=solve[0], coarse_tol=solve[1])
     return sim, sim.run(), d["rtest_log"]
 
 
-def check_against_reference(name, log, ref):
+def check_against_reference(name, log, ref, solve=EXACT):
     assert log.shape == ref.shape, (log.shape, ref.shape)
     # it and time columns exactly (output times are hit exactly)
     assert np.array_equal(log[:, 0], ref[:, 0])
     assert np.allclose(log[:, 1], ref[:, 1], rtol=1e-12, atol=0)
-    # compare_logs.py tolerance (rtol 1e-5, atol 1e-8)
-    n = STRICT[name]
-    assert np.all(np.isclose(log[:n], ref[:n], rtol=1e-5, atol=1e-8))
-    k = LAST_CLOSE[name] + 1
-    assert np.all(np.isclose(log[:k], ref[:k], rtol=5e-5, atol=1e-8))
-    ns = (log.shape[1] - 3) // 3
-    sums = slice(3, 3 + 2 * ns)
-    assert np.all(np.isclose(log[k:, sums], ref[k:, sums], rtol=1e-2, atol=1e-8))
-    assert np.all(np.isclose(log[k:, 3 + 2 * ns:], ref[k:, 3 + 2 * ns:], rtol=0.2, atol=1e-8))
+    # every row, compare_logs.py's atol 1e-8 and the case's rtol
+    rtol = BOUND[(name, solve)]
+    bad = ~np.isclose(log, ref, rtol=rtol, atol=1e-8)
+    assert not bad.any(), (rtol, np.argwhere(bad)[:5],
+                           np.max(np.abs(log - ref) / np.maximum(np.abs(ref), 1e-300)))
 
 
+SOLVES = {"exact": EXACT, "pfmg": PFMG}
+
+
+@pytest.mark.parametrize("solve", sorted(SOLVES))
 @pytest.mark.parametrize("name", CASES)
-def test_rtest_oracle(name):
-    _, log, ref = run(capi.oracle_library(), name)
-    check_against_reference(name, log, ref)
+def test_rtest_oracle(name, solve):
+    _, log, ref = run(capi.oracle_library(), name, solve=SOLVES[solve])
+    check_against_reference(name, log, ref, SOLVES[solve])
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("solve", sorted(SOLVES))
 @pytest.mark.parametrize("name", CASES)
-def test_rtest_hip(name):
+def test_rtest_hip(name, solve):
     """The device time loop: the reference rows as above, and the oracle's
     rows (same algorithms on the CPU) to 1e-9."""
-    sim, log, ref = run(capi.hip_library(), name, device=0)
-    check_against_reference(name, log, ref)
-    _, olog, _ = run(capi.oracle_library(), name)
+    sim, log, ref = run(capi.hip_library(), name, device=0, solve=SOLVES[solve])
+    check_against_reference(name, log, ref, SOLVES[solve])
+    _, olog, _ = run(capi.oracle_library(), name, solve=SOLVES[solve])
     rel = np.abs(log - olog) / np.maximum(np.abs(olog), 1e-300)
     assert rel.max() <= 1e-9, rel.max(axis=1)
 
