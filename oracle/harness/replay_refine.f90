@@ -12,9 +12,15 @@
 !> refine_buffer_width, and the resulting topology is written out.
 !> Usage: replay_refine <record_file> <out_file> <cfg> [-key=value ...]
 !> Record: int32 n_calls, then per call: int32 n_boxes, float64 global_time,
-!> then per box id 1..n_boxes: int32 in_use, and (in use) float64 e(nc^3),
-!> E(nc^3), i fastest. Output per call: int32 highest_id, highest_lvl, then per
-!> id 1..highest_id: in_use, lvl, ix(3), parent, children(8), neighbors(6).
+!> int32 full, then per box id 1..n_boxes: int32 in_use, and (in use) either
+!> float64 e(nc^3), E(nc^3), i fastest (full = 0), or every cc variable of
+!> the box with its ghost cells, cc(0:nc+1, 0:nc+1, 0:nc+1, n_var_cell)
+!> (full = 1: the whole state af_adjust_refinement moves). Output per call:
+!> int32 highest_id, highest_lvl, then per id 1..highest_id: in_use, lvl,
+!> ix(3), parent, children(8), neighbors(6); after a full call also the
+!> auto variables (int32 n, iv(n)), the number of added boxes, and per
+!> added box its id and every cc variable with ghost cells (the data
+!> auto_prolong / auto_restrict left, m_af_core.f90:825-881).
 #include "cpp_macros.h"
 program replay_refine
   use m_config
@@ -36,9 +42,10 @@ program replay_refine
   type(af_t)         :: tree
   type(ref_info_t)   :: ref_info
   character(len=512) :: rec_file, out_file, arg
-  integer            :: ur, uo, n_calls, call_ix, nb, id, in_use, nc, lvl, n
+  integer            :: ur, uo, n_calls, call_ix, nb, id, in_use, nc, lvl, n, full
+  integer            :: n_add, i
   real(dp)           :: t_glob
-  real(dp), allocatable :: buf(:)
+  real(dp), allocatable :: buf(:), fbuf(:, :, :, :)
 
   call get_command_argument(1, rec_file)
   call get_command_argument(2, out_file)
@@ -72,6 +79,12 @@ program replay_refine
           call af_set_cc_methods(tree, n, af_bc_neumann_zero, af_gc_interp, &
           ST_prolongation_method)
   end do
+  ! mg_init's methods for phi (m_af_multigrid.f90:61, 102-105; mg_init
+  ! itself needs HYPRE): no prolongation argument, so af_prolong_linear and
+  ! phi an auto variable; mg_auto_rb (private there) is mg_sides_rb for
+  ! boxes without a variable-epsilon tag (926-940), phi_rb below
+  if (.not. tree%has_cc_method(mg%i_phi)) &
+       call af_set_cc_methods(tree, mg%i_phi, mg%sides_bc, phi_rb)
 
   call af_init(tree, ST_box_size, ST_domain_origin + ST_domain_len, &
        ST_coarse_grid_size, periodic=ST_periodic, coord=af_xyz, &
@@ -83,17 +96,21 @@ program replay_refine
 
   nc = tree%n_cell
   allocate(buf(nc**3))
+  allocate(fbuf(0:nc+1, 0:nc+1, 0:nc+1, tree%n_var_cell))
   open(newunit=ur, file=trim(rec_file), access="stream", form="unformatted", &
        action="read")
   open(newunit=uo, file=trim(out_file), access="stream", form="unformatted", &
        action="write", status="replace")
   read(ur) n_calls
   do call_ix = 1, n_calls
-     read(ur) nb, t_glob
+     read(ur) nb, t_glob, full
      global_time = t_glob
      do id = 1, nb
         read(ur) in_use
-        if (in_use /= 0) then
+        if (in_use /= 0 .and. full /= 0) then
+           read(ur) fbuf
+           if (id <= tree%highest_id) tree%boxes(id)%cc = fbuf
+        else if (in_use /= 0) then
            read(ur) buf
            ! a box the reference tree does not have (after a disagreement)
            if (id <= tree%highest_id) &
@@ -103,6 +120,8 @@ program replay_refine
                 tree%boxes(id)%cc(1:nc, 1:nc, 1:nc, i_electric_fld) = reshape(buf, [nc, nc, nc])
         end if
      end do
+     ! the applied voltage field_compute last set (phi's boundary values)
+     call field_set_voltage(tree, global_time)
      call af_adjust_refinement(tree, refine_routine, ref_info, refine_buffer_width)
      write(uo) tree%highest_id, tree%highest_lvl
      do id = 1, tree%highest_id
@@ -110,7 +129,27 @@ program replay_refine
           write(uo) merge(1, 0, b%in_use), b%lvl, b%ix, b%parent, b%children, b%neighbors
         end associate
      end do
+     if (full /= 0) then
+        write(uo) size(tree%cc_auto_vars), tree%cc_auto_vars
+        n_add = 0
+        do lvl = 1, size(ref_info%lvls)
+           n_add = n_add + size(ref_info%lvls(lvl)%add)
+        end do
+        write(uo) n_add
+        do lvl = 1, size(ref_info%lvls)
+           do i = 1, size(ref_info%lvls(lvl)%add)
+              id = ref_info%lvls(lvl)%add(i)
+              write(uo) id, tree%boxes(id)%cc
+           end do
+        end do
+     end if
   end do
   close(ur)
   close(uo)
+contains
+  subroutine phi_rb(boxes, id, nb, iv, op_mask)
+    type(box_t), intent(inout) :: boxes(:)
+    integer, intent(in)        :: id, nb, iv, op_mask
+    call mg_sides_rb(boxes, id, nb, iv)
+  end subroutine phi_rb
 end program replay_refine
