@@ -82,6 +82,11 @@ struct afh_tree {
   double *cc = nullptr, *fc = nullptr;
   double *gc2 = nullptr;     // 2nd ghost layer for the flux: [box][6][nc][nc]
   double *scratch = nullptr; // reductions etc.
+  // reduction slots (red_init / red_finish): a fold leaves the slot's shards
+  // at its canonical start value, so the next red_init with that value needs
+  // no fill launch
+  uint64_t red_canon[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  bool red_ready[8] = {false, false, false, false, false, false, false, false};
   double *h_scratch = nullptr;
   std::vector<afh::CcMethod> meth;
   std::vector<int> auto_vars;  // tree%cc_auto_vars (afh_set_cc_prolong order)
@@ -111,6 +116,9 @@ struct afh_tree {
   // (S1 leaf fill 13.5 -> 11.8 us); at 64^3 it measured 134 -> 129 us per
   // fill but the step no faster, so k_gc_faces stays (AFH_GC_FACES6=0/1)
   int gc_faces6 = -1;
+  // boxes up to 16^3: faces, edges and corners of a level in one launch
+  // (k_gc_box, AFH_GC_BOX=0 for the two-launch form)
+  bool gc_box = true;
   struct Plan {
     int32_t *d_reg = nullptr;  // n x 7 (id, lo[3], hi[3])
     int64_t *d_off = nullptr;  // n + 1 value offsets
@@ -185,6 +193,9 @@ int32_t gc_lvl(afh_tree *t, int lvl, int iv, int corners, bool rims = false);
 // boundaries (its ghost cells read this level's replicas, ghosts included)
 int32_t gc_lvl_var(afh_tree *t, int lvl, int iv, const double *vc,
                    const GcArgs &ga, int corners, bool rims = false);
+// edges and corners only of level lvl (k_gc_corners), for a level whose
+// faces a producer kernel filled (the fused pair's pushed faces)
+int32_t gc_lvl_corners(afh_tree *t, int lvl, int iv);
 // sharding hook (no-op without one)
 int32_t call_hook(afh_tree *t, int kind, int lvl, int iv, double *vals = nullptr,
                   int n = 0);

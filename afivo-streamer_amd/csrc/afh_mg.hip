@@ -751,7 +751,18 @@ struct RbBox {
   static constexpr int GPT = (NGH + NT - 1) / NT;            // ghosts per thread
 };
 
-template <int NC>
+//
+// PUSH: the level fill after the pair is done by the pair itself. The box
+// stores its interior, edges and corners, and the face ghosts the fill
+// would give: a same-level neighbour's ghost layer facing this box gets this
+// box's new boundary cells (copy_from_nb seen from the other side), a
+// physical / refinement face of this box its gc_face_nocopy value from the
+// new interior and the coarse data. Nobody else writes those cells (each
+// face ghost of dst has exactly one writer: the box, or its same-level
+// neighbour), and every box of the level is in the launch; so dst ends as
+// pair + k_gc_faces would leave it (edges and corners: src's, as without
+// corners; k_gc_corners follows when the fill wants them).
+template <int NC, bool PUSH = false>
 __global__ void __launch_bounds__(RbBox<NC>::NT)
     k_gsrb_pair_box(const double *__restrict__ src, double *__restrict__ dst,
                     const double *__restrict__ rhs, const double *__restrict__ coarse,
@@ -910,7 +921,41 @@ __global__ void __launch_bounds__(RbBox<NC>::NT)
            inv_c1;
   }
   __syncthreads();
-  for (int e = tid; e < NB; e += NT) y[e] = P[e];
+  if constexpr (!PUSH) {
+    for (int e = tid; e < NB; e += NT) y[e] = P[e];
+  } else {
+    // interior, edges and corners (not the six face ghost layers)
+    for (int e = tid; e < NB; e += NT) {
+      const int i = e % NG, j = (e / NG) % NG, k = e / SK;
+      const int nout = (i == 0 || i == NG - 1) + (j == 0 || j == NG - 1) + (k == 0 || k == NG - 1);
+      if (nout != 1) y[e] = P[e];
+    }
+    // face ghosts: pushed into the same-level neighbour, or this box's own
+    for (int u = tid; u < 6 * NC * NC; u += NT) {
+      const int nb = u / (NC * NC) + 1, w = u % (NC * NC);
+      const int a = w % NC + 1, b = w / NC + 1;
+      const int d = (nb - 1) >> 1;
+      const bool low = ((nb - 1) & 1) == 0;
+      const int ta = (d == 0) ? 1 : 0, tb = (d == 2) ? 1 : 2;
+      int p[3];
+      p[ta] = a;
+      p[tb] = b;
+      p[d] = low ? 0 : NC + 1;
+      int q1[3] = {p[0], p[1], p[2]};
+      q1[d] = low ? 1 : NC;
+      const double x1v = P[ix3(NG, q1[0], q1[1], q1[2])];
+      const int nid = nbid(nb);
+      if (nid > 0) {
+        int q[3] = {p[0], p[1], p[2]};
+        q[d] = low ? NC + 1 : 0;  // the neighbour's ghost facing this box
+        dst[(size_t)(nid - 1) * bsz + ix3(NG, q[0], q[1], q[2])] = x1v;
+      } else {
+        y[ix3(NG, p[0], p[1], p[2])] = gc_face_nocopy_k(
+            coarse, meta, m, nb, nid, d == 0 ? dr0 : d == 1 ? dr1 : dr2, p, a, b, NC, bsz,
+            bcof(nb), ga.rb, [&](const int *q) { return P[ix3(NG, q[0], q[1], q[2])]; });
+      }
+    }
+  }
 }
 
 __device__ __forceinline__ double apply7(const double *x, size_t c, size_t sj,
@@ -1435,7 +1480,8 @@ template <int NC, int K, bool NT = false>
 __global__ void __launch_bounds__(256)
     k_gradient_t(const double *__restrict__ phi, double *__restrict__ fcv,
                  double *__restrict__ nrm, const int32_t *__restrict__ ids,
-                 size_t bsz, size_t fsz, double ix_, double iy, double iz) {
+                 size_t bsz, size_t fsz, const afh_box_meta *__restrict__ meta,
+                 double fac) {
   constexpr int R = 256 / NC < NC ? 256 / NC : NC;  // rows per block
   constexpr int NG = NC + 2, NF = NC + 1;
   constexpr size_t SJ = NG, SK = (size_t)NG * NG, D3 = (size_t)NF * NF * NF;
@@ -1444,6 +1490,10 @@ __global__ void __launch_bounds__(256)
   const int j = (B.x % (NC / R)) * R + threadIdx.x / NC + 1;
   const int k0 = (B.x / (NC / R)) * K + 1;
   const int id = ids[B.y];
+  // fac / dr per dimension (every box of a level has its level's dr bits):
+  // all levels in one launch
+  const double ix_ = fac / meta[id - 1].dr[0], iy = fac / meta[id - 1].dr[1],
+               iz = fac / meta[id - 1].dr[2];
   const double *p = phi + (size_t)(id - 1) * bsz;
   double *f = fcv + (size_t)(id - 1) * fsz;
   double *nb = nrm ? nrm + (size_t)(id - 1) * bsz : nullptr;
@@ -1488,18 +1538,17 @@ static void launch_gradient(afh_tree *t, const double *phi, double *fcv,
                             double *nrm, double fac, bool nt) {
   constexpr int R = 256 / NC < NC ? 256 / NC : NC;
   constexpr int K = NC >= AFH_GRAD_K ? AFH_GRAD_K : 1;
-  for (int l = 1; l <= t->nlvl; l++) {
-    const int n = t->ids.n(l);
-    if (!n) continue;
-    const double *dr = &t->lvl_dr[3 * (l - 1)];
+  const int ntot = t->ids.off[t->nlvl];  // every box of every level
+  for (int o = 0; o < ntot; o += 65535) {  // grid.y limit
+    const int n = std::min(65535, ntot - o);
     if (nt)
       hipLaunchKernelGGL((k_gradient_t<NC, K, true>), dim3((NC / R) * (NC / K), n),
-                         dim3(NC * R), 0, t->stream, phi, fcv, nrm, t->ids.at(l),
-                         t->bsz, t->fsz, fac / dr[0], fac / dr[1], fac / dr[2]);
+                         dim3(NC * R), 0, t->stream, phi, fcv, nrm, t->ids.d + o, t->bsz,
+                         t->fsz, t->d_boxes, fac);
     else
       hipLaunchKernelGGL((k_gradient_t<NC, K>), dim3((NC / R) * (NC / K), n),
-                         dim3(NC * R), 0, t->stream, phi, fcv, nrm, t->ids.at(l),
-                         t->bsz, t->fsz, fac / dr[0], fac / dr[1], fac / dr[2]);
+                         dim3(NC * R), 0, t->stream, phi, fcv, nrm, t->ids.d + o, t->bsz,
+                         t->fsz, t->d_boxes, fac);
   }
 }
 
@@ -2071,6 +2120,80 @@ __global__ void __launch_bounds__(256)
   out[o] = s;
 }
 
+// AFH_COARSE_DIRECT on a level-1 grid of at most CS_SMALL_CELLS cells (S1's
+// 16^3, the 8^3 of streamer_3d.cfg) in ONE workgroup: k_cs_gather's folded
+// rhs, the six k_cs_transform passes and k_cs_scatter, the grid held in LDS
+// (compact, i fastest) -- the same sums in the same order, one launch
+// instead of eight.
+__global__ void __launch_bounds__(1024)
+    k_cs_direct_small(CsParams P, double *__restrict__ phi, const double *__restrict__ rhs,
+                      const afh_box_meta *__restrict__ meta, const int32_t *__restrict__ ids,
+                      int nid, int nc, size_t bsz, afh_bc b0, afh_bc b1, afh_bc b2,
+                      afh_bc b3, afh_bc b4, afh_bc b5, const double *__restrict__ q0,
+                      const double *__restrict__ q1, const double *__restrict__ q2,
+                      const double *__restrict__ qt0, const double *__restrict__ qt1,
+                      const double *__restrict__ qt2, const double *__restrict__ e0,
+                      const double *__restrict__ e1, const double *__restrict__ e2,
+                      double lam) {
+  __shared__ double A[CS_SMALL_CELLS], B[CS_SMALL_CELLS];
+  const int nx = P.dims[0][0], ny = P.dims[0][1], nz = P.dims[0][2];
+  const int N = nx * ny * nz, n3 = nc * nc * nc;
+  const afh_bc bc[6] = {b0, b1, b2, b3, b4, b5};
+  for (int u = threadIdx.x; u < nid * n3; u += blockDim.x) {
+    const int id = ids[u / n3], t = u % n3;
+    const afh_box_meta &m = meta[id - 1];
+    const int i = t % nc + 1, j = (t / nc) % nc + 1, k = t / (nc * nc) + 1;
+    const int gi[3] = {(m.ix[0] - 1) * nc + i, (m.ix[1] - 1) * nc + j,
+                       (m.ix[2] - 1) * nc + k};
+    double rv = rhs[(size_t)(id - 1) * bsz + ix3(nc + 2, i, j, k)];
+    for (int nb = 1; nb <= 6; nb++) {
+      const int dd = (nb - 1) >> 1;
+      const bool low = ((nb - 1) & 1) == 0;
+      const bool at = low ? (gi[dd] == 1) : (gi[dd] == P.dims[0][dd]);
+      if (!at) continue;
+      const double cnb = P.hc[0][dd];
+      double b2r;
+      if (bc[nb - 1].type == AFH_BC_DIRICHLET) b2r = -2 * cnb;
+      else b2r = -(cnb * m.dr[dd]) * (low ? -1 : 1);
+      rv = rv + b2r * bc[nb - 1].value;
+    }
+    A[((gi[2] - 1) * ny + (gi[1] - 1)) * nx + (gi[0] - 1)] = rv;
+  }
+  __syncthreads();
+  // Q^T along x, y, z (divide), then Q along z, y, x: A -> B -> A -> B -> A -> B -> A
+  const double *Ms[6] = {q0, q1, q2, qt2, qt1, qt0};
+  const int ds[6] = {0, 1, 2, 2, 1, 0};
+  for (int ps = 0; ps < 6; ps++) {
+    const double *in = (ps & 1) ? B : A;
+    double *out = (ps & 1) ? A : B;
+    const int d = ds[ps], n = d == 0 ? nx : (d == 1 ? ny : nz);
+    const int st = d == 0 ? 1 : (d == 1 ? nx : nx * ny);
+    const double *M = Ms[ps];
+    for (int t = threadIdx.x; t < N; t += blockDim.x) {
+      const int i = t % nx, j = (t / nx) % ny, k = t / (nx * ny);
+      const int co = d == 0 ? i : (d == 1 ? j : k);
+      const double *src = in + (t - co * st);
+      double s = 0.0;
+      for (int p = 0; p < n; p++) s = s + M[p * n + co] * src[p * st];
+      if (ps == 2) {
+        const double den = ((e0[i] + e1[j]) + e2[k]) - lam;
+        s = den != 0.0 ? s / den : 0.0;
+      }
+      out[t] = s;
+    }
+    __syncthreads();
+  }
+  // the sixth pass wrote A
+  for (int u = threadIdx.x; u < nid * n3; u += blockDim.x) {
+    const int id = ids[u / n3], t = u % n3;
+    const afh_box_meta &m = meta[id - 1];
+    const int i = t % nc + 1, j = (t / nc) % nc + 1, k = t / (nc * nc) + 1;
+    phi[(size_t)(id - 1) * bsz + ix3(nc + 2, i, j, k)] =
+        A[(((m.ix[2] - 1) * nc + k - 1) * ny + (m.ix[1] - 1) * nc + j - 1) * nx +
+          (m.ix[0] - 1) * nc + i - 1];
+  }
+}
+
 }  // namespace afh
 
 using namespace afh;
@@ -2110,6 +2233,10 @@ struct afh_mg {
   int *cs_iters = nullptr;     // pairs the last k_cs_electrode took
   // level-1 cycles of the last coarse solve (afh_mg_coarse_iterations): on
   // the device when k_cs_small applied the stopping rule, else on the host
+  // AFH_CS_DIRECT_SMALL: the direct solve of a level-1 grid of at most
+  // CS_SMALL_CELLS cells in one workgroup (k_cs_direct_small), default on
+  bool cs_direct_small = true;
+  bool pair_push = true;  // AFH_PAIR_PUSH: the small-box pair fills the faces
   int *d_cycles = nullptr;
   int cycles_host = 0;
   bool cycles_on_dev = false;
@@ -2336,6 +2463,8 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
   if (const char *env = getenv("AFH_GRAPHS")) mg->use_graphs = atoi(env) != 0;
   if (const char *env = getenv("AFH_RSTR_COL")) mg->rstr_col = atoi(env) != 0;
   if (const char *env = getenv("AFH_CS_FUSED")) mg->cs_fused = atoi(env) != 0;
+  if (const char *env = getenv("AFH_CS_DIRECT_SMALL")) mg->cs_direct_small = atoi(env) != 0;
+  if (const char *env = getenv("AFH_PAIR_PUSH")) mg->pair_push = atoi(env) != 0;
   AFH_HIP(hipMalloc(&mg->cs_iters, sizeof(int)));
   AFH_HIP(hipMalloc(&mg->d_cycles, sizeof(int)));
   if (const char *env = getenv("AFH_GSRB_PAIR_BOX")) mg->pair_box = atoi(env) != 0;
@@ -2458,6 +2587,13 @@ static void launch_pair2(afh_mg *mg, int lvl, const double *src, double *dst,
             t->gc_args(mg->d.i_phi));
 }
 
+// the small-box pair fills the level's faces itself (k_gsrb_pair_box PUSH)
+// unless the tree is sharded (a replica's ghosts are its owner's to fill,
+// through the exchange hooks) or AFH_PAIR_PUSH=0
+static bool pair_push(const afh_mg *mg) {
+  return mg->pair_push && mg->pair_box && mg->t->nc <= 16 && !mg->t->hook;
+}
+
 template <int NC>
 static void launch_pair(afh_mg *mg, int lvl, const double *src, double *dst,
                         const Coef &cf, double inv_c1, hipEvent_t e0, hipEvent_t e1) {
@@ -2465,9 +2601,15 @@ static void launch_pair(afh_mg *mg, int lvl, const double *src, double *dst,
   if (t->ids.n(lvl) == 0) return;
   if constexpr (NC <= 16) {
     if (mg->pair_box) {
-      launch_ev((k_gsrb_pair_box<NC>), e0, e1, dim3(t->ids.n(lvl)), dim3(RbBox<NC>::NT),
-                t->stream, src, dst, t->ccv(mg->d.i_rhs), t->ccv(mg->d.i_phi), t->d_boxes,
-                t->ids.at(lvl), t->bsz, cf, inv_c1, t->gc_args(mg->d.i_phi));
+      if (pair_push(mg))
+        launch_ev((k_gsrb_pair_box<NC, true>), e0, e1, dim3(t->ids.n(lvl)),
+                  dim3(RbBox<NC>::NT), t->stream, src, dst, t->ccv(mg->d.i_rhs),
+                  t->ccv(mg->d.i_phi), t->d_boxes, t->ids.at(lvl), t->bsz, cf, inv_c1,
+                  t->gc_args(mg->d.i_phi));
+      else
+        launch_ev((k_gsrb_pair_box<NC>), e0, e1, dim3(t->ids.n(lvl)), dim3(RbBox<NC>::NT),
+                  t->stream, src, dst, t->ccv(mg->d.i_rhs), t->ccv(mg->d.i_phi), t->d_boxes,
+                  t->ids.at(lvl), t->bsz, cf, inv_c1, t->gc_args(mg->d.i_phi));
       return;
     }
   }
@@ -2655,8 +2797,13 @@ static int32_t gsrb_boxes(afh_mg *mg, int lvl, bool up, bool stale_ghosts = fals
     if (timed) prof_count(t, 24.0 * nc * nc * nc * nid);
     AFH_LAUNCH_CHECK("k_gsrb_pair");
     (void)dst;
-    if (int32_t e = gc_lvl_var(t, lvl, dst_iv, phi, ga, up && n == n_cycle, true))
+    if (pair_push(mg)) {
+      // the pair filled the faces; edges and corners on the leg's last pair
+      if (up && n == n_cycle)
+        if (int32_t e = gc_lvl_corners(t, lvl, dst_iv)) return e;
+    } else if (int32_t e = gc_lvl_var(t, lvl, dst_iv, phi, ga, up && n == n_cycle, true)) {
       return e;
+    }
   }
   return AFH_OK;
 }
@@ -2945,6 +3092,24 @@ static int32_t solve_coarse(afh_mg *mg) {
       break;
     }
   const int nc = t->nc, nid = t->ids.n(1), n3 = nc * nc * nc;
+  if (mg->d.coarse_mode == AFH_COARSE_DIRECT && mg->cs_direct_small &&
+      (long)P.dims[0][0] * P.dims[0][1] * P.dims[0][2] <= CS_SMALL_CELLS) {
+    for (int q = 0; q < 6; q++)
+      if (mg->q_bc[q] != bc[q].type) {
+        if (int32_t e = build_direct(mg)) return e;
+        break;
+      }
+    if (nid)
+      hipLaunchKernelGGL(k_cs_direct_small, dim3(1), dim3(1024), 0, t->stream, P,
+                         t->ccv(mg->d.i_phi), t->ccv(mg->d.i_rhs), t->d_boxes, t->ids.at(1),
+                         nid, nc, t->bsz, bc[0], bc[1], bc[2], bc[3], bc[4], bc[5],
+                         mg->d_q[0], mg->d_q[1], mg->d_q[2], mg->d_qt[0], mg->d_qt[1],
+                         mg->d_qt[2], mg->d_e[0], mg->d_e[1], mg->d_e[2],
+                         mg->d.helmholtz_lambda);
+    AFH_LAUNCH_CHECK("k_cs_direct_small");
+    mg->cycles_host = 0, mg->cycles_on_dev = false;
+    return gc_lvl(t, 1, mg->d.i_phi, 1);
+  }
   hipLaunchKernelGGL(k_cs_gather, dim3((n3 + 255) / 256, nid), dim3(256), 0,
                      t->stream, P, t->ccv(mg->d.i_phi), t->ccv(mg->d.i_rhs),
                      t->d_boxes, t->ids.at(1), nc, t->bsz, bc[0], bc[1], bc[2],

@@ -237,6 +237,99 @@ __global__ void k_gc_corners(double *__restrict__ v,
   }
 }
 
+// A small box's whole fill in one workgroup (NC <= 16: NC^2 threads, one
+// per (a, b)): the six faces as k_gc_faces6, then -- with corners -- the
+// edges and corners as k_gc_corners, behind workgroup barriers (edge
+// extrapolation reads this box's face ghosts, corner extrapolation its edge
+// ghosts). One launch per level fill instead of two; the same values.
+template <int NC>
+__global__ void __launch_bounds__(NC * NC)
+    k_gc_box(double *__restrict__ v, const double *__restrict__ vc,
+             const afh_box_meta *__restrict__ meta, const int32_t *__restrict__ ids,
+             size_t bsz, GcArgs ga, int corners) {
+  constexpr int NG = NC + 2;
+  const int t = threadIdx.x;
+  const int id = ids[blockIdx.x];
+  const int a = t % NC + 1, b = t / NC + 1;
+  const afh_box_meta &m = meta[id - 1];
+  double *c = v + (size_t)(id - 1) * bsz;
+  {
+    double val[6];
+    int dst[6];
+#pragma unroll
+    for (int nb = 1; nb <= 6; nb++) {
+      const int d = (nb - 1) >> 1;
+      const bool low = ((nb - 1) & 1) == 0;
+      const int ta = (d == 0) ? 1 : 0, tb = (d == 2) ? 1 : 2;
+      int p[3];
+      p[ta] = a;
+      p[tb] = b;
+      p[d] = low ? 0 : NC + 1;
+      dst[nb - 1] = ix3(NG, p[0], p[1], p[2]);
+      const int nb_id = m.neighbors[nb - 1];
+      if (nb_id > 0) {
+        int q[3] = {p[0], p[1], p[2]};
+        q[d] = low ? NC : 1;
+        val[nb - 1] = v[(size_t)(nb_id - 1) * bsz + ix3(NG, q[0], q[1], q[2])];
+      } else {
+        val[nb - 1] = gc_face_nocopy(vc, meta, m, nb, p, a, b, NC, bsz, ga.bc[nb - 1], ga.rb,
+                                     [&](const int *q) { return c[ix3(NG, q[0], q[1], q[2])]; });
+      }
+    }
+#pragma unroll
+    for (int nb = 0; nb < 6; nb++) c[dst[nb]] = val[nb];
+  }
+  if (!corners) return;
+  __syncthreads();
+  for (int e = t; e < 12 * NC; e += NC * NC) {
+    const int n = e / NC, pos = e % NC + 1;
+    const int dim = c_edge_dim[n];
+    const int dx = c_edge_dir[n][0], dy = c_edge_dir[n][1], dz = c_edge_dir[n][2];
+    const int nb_id = m.neighbor_mat[(dx + 1) + 3 * (dy + 1) + 9 * (dz + 1)];
+    int x[3];
+    for (int q = 0; q < 3; q++) x[q] = c_edge_min[n][q] * (NC + 1);
+    x[dim] = pos;
+    if (nb_id > 0) {
+      int s[3] = {x[0] - dx * NC, x[1] - dy * NC, x[2] - dz * NC};
+      c[ix3(NG, x[0], x[1], x[2])] = v[(size_t)(nb_id - 1) * bsz + ix3(NG, s[0], s[1], s[2])];
+    } else {
+      const int o1 = (dim + 1) % 3, o2 = (dim + 2) % 3;
+      int di[3];
+      for (int q = 0; q < 3; q++) di[q] = 1 - 2 * (x[q] & 1);
+      di[dim] = 0;
+      int ia[3] = {x[0], x[1], x[2]}, ib[3] = {x[0], x[1], x[2]};
+      ia[o1] += di[o1];
+      ib[o2] += di[o2];
+      int ic[3] = {x[0] + di[0], x[1] + di[1], x[2] + di[2]};
+      c[ix3(NG, x[0], x[1], x[2])] = c[ix3(NG, ia[0], ia[1], ia[2])] +
+                                     c[ix3(NG, ib[0], ib[1], ib[2])] -
+                                     c[ix3(NG, ic[0], ic[1], ic[2])];
+    }
+  }
+  __syncthreads();
+  if (t < 8) {
+    const int n = t;
+    int dnb[3], x[3];
+    for (int q = 0; q < 3; q++) {
+      dnb[q] = 2 * c_child_dix[n][q] - 1;
+      x[q] = c_child_dix[n][q] * (NC + 1);
+    }
+    const int nb_id = m.neighbor_mat[(dnb[0] + 1) + 3 * (dnb[1] + 1) + 9 * (dnb[2] + 1)];
+    if (nb_id > 0) {
+      c[ix3(NG, x[0], x[1], x[2])] =
+          v[(size_t)(nb_id - 1) * bsz +
+            ix3(NG, x[0] - dnb[0] * NC, x[1] - dnb[1] * NC, x[2] - dnb[2] * NC)];
+    } else {
+      int di[3];
+      for (int q = 0; q < 3; q++) di[q] = 1 - 2 * (x[q] & 1);
+      c[ix3(NG, x[0], x[1], x[2])] = c[ix3(NG, x[0], x[1] + di[1], x[2] + di[2])] +
+                                     c[ix3(NG, x[0] + di[0], x[1], x[2] + di[2])] +
+                                     c[ix3(NG, x[0] + di[0], x[1] + di[1], x[2])] -
+                                     2 * c[ix3(NG, x[0] + di[0], x[1] + di[1], x[2] + di[2])];
+    }
+  }
+}
+
 int32_t call_hook(afh_tree *t, int kind, int lvl, int iv, double *vals, int n) {
   if (!t->hook) return AFH_OK;
   int32_t e = t->hook(t->hook_ctx, kind, lvl, iv, vals, n);
@@ -253,22 +346,46 @@ int32_t gc_lvl_var(afh_tree *t, int lvl, int iv, const double *vc,
   if (n > 0) {
     const int nc = t->nc;
     prof_begin(t, AFH_PROF_GHOST);
-    if (t->gc_faces6 == 1 || (t->gc_faces6 < 0 && nc <= 16))
-      hipLaunchKernelGGL(k_gc_faces6, dim3((nc * nc + 255) / 256, n), dim3(256), 0,
-                         t->stream, v, vc, t->d_boxes, t->ids.at(lvl), nc, t->bsz, ga);
-    else
-      hipLaunchKernelGGL(k_gc_faces, dim3((nc * nc + 255) / 256, 6, n), dim3(256), 0,
-                         t->stream, v, vc, t->d_boxes, t->ids.at(lvl), nc, t->bsz, ga);
-    // algorithmic bytes: read one interior layer + write one ghost layer
-    prof_end(t, AFH_PROF_GHOST, 16.0 * 6 * nc * nc * n);
-    AFH_LAUNCH_CHECK("k_gc_faces");
-    if (corners) {
-      hipLaunchKernelGGL(k_gc_corners, dim3(n), dim3(256), 0, t->stream, v,
-                         t->d_boxes, t->ids.at(lvl), nc, t->bsz);
-      AFH_LAUNCH_CHECK("k_gc_corners");
+    if (t->gc_box && (nc == 4 || nc == 8 || nc == 16)) {
+      const int cr = corners ? 1 : 0;
+      if (nc == 4)
+        hipLaunchKernelGGL(k_gc_box<4>, dim3(n), dim3(16), 0, t->stream, v, vc, t->d_boxes,
+                           t->ids.at(lvl), t->bsz, ga, cr);
+      else if (nc == 8)
+        hipLaunchKernelGGL(k_gc_box<8>, dim3(n), dim3(64), 0, t->stream, v, vc, t->d_boxes,
+                           t->ids.at(lvl), t->bsz, ga, cr);
+      else
+        hipLaunchKernelGGL(k_gc_box<16>, dim3(n), dim3(256), 0, t->stream, v, vc, t->d_boxes,
+                           t->ids.at(lvl), t->bsz, ga, cr);
+      prof_end(t, AFH_PROF_GHOST, 16.0 * 6 * nc * nc * n);
+      AFH_LAUNCH_CHECK("k_gc_box");
+    } else {
+      if (t->gc_faces6 == 1 || (t->gc_faces6 < 0 && nc <= 16))
+        hipLaunchKernelGGL(k_gc_faces6, dim3((nc * nc + 255) / 256, n), dim3(256), 0,
+                           t->stream, v, vc, t->d_boxes, t->ids.at(lvl), nc, t->bsz, ga);
+      else
+        hipLaunchKernelGGL(k_gc_faces, dim3((nc * nc + 255) / 256, 6, n), dim3(256), 0,
+                           t->stream, v, vc, t->d_boxes, t->ids.at(lvl), nc, t->bsz, ga);
+      // algorithmic bytes: read one interior layer + write one ghost layer
+      prof_end(t, AFH_PROF_GHOST, 16.0 * 6 * nc * nc * n);
+      AFH_LAUNCH_CHECK("k_gc_faces");
+      if (corners) {
+        hipLaunchKernelGGL(k_gc_corners, dim3(n), dim3(256), 0, t->stream, v,
+                           t->d_boxes, t->ids.at(lvl), nc, t->bsz);
+        AFH_LAUNCH_CHECK("k_gc_corners");
+      }
     }
   }
   if (rims || t->lvl_rb_coarse[lvl - 1]) return call_hook(t, AFH_HOOK_RIMS, lvl, iv);
+  return AFH_OK;
+}
+
+int32_t gc_lvl_corners(afh_tree *t, int lvl, int iv) {
+  const int n = t->ids.n(lvl);
+  if (!n) return AFH_OK;
+  hipLaunchKernelGGL(k_gc_corners, dim3(n), dim3(256), 0, t->stream, t->var(iv), t->d_boxes,
+                     t->ids.at(lvl), t->nc, t->bsz);
+  AFH_LAUNCH_CHECK("k_gc_corners");
   return AFH_OK;
 }
 
@@ -355,10 +472,12 @@ __global__ void k_red_fill(unsigned long long *r, unsigned long long v) {
   r[blockIdx.x * blockDim.x + threadIdx.x] = v;
 }
 __global__ void k_red_fold(unsigned long long *r, unsigned long long *out,
-                           int is_max) {
-  // one block of RED_SHARDS threads; ordered integers fold like the doubles
+                           int is_max, unsigned long long reset) {
+  // one block of RED_SHARDS threads; ordered integers fold like the doubles;
+  // the shards are left at `reset` for the slot's next use
   __shared__ unsigned long long s[RED_SHARDS];
   s[threadIdx.x] = r[threadIdx.x];
+  r[threadIdx.x] = reset;
   __syncthreads();
   for (int o = RED_SHARDS / 2; o > 0; o >>= 1) {
     if ((int)threadIdx.x < o) {
@@ -370,20 +489,31 @@ __global__ void k_red_fold(unsigned long long *r, unsigned long long *out,
   if (threadIdx.x == 0) *out = s[0];
 }
 
+// Each slot has a canonical start value (red_canon, set at tree creation);
+// a fold resets the shards to it, so a red_init with that value finds them
+// ready and launches nothing (V-cycle graphs captured in that state replay
+// in it: every fold in them re-arms the slot). Another start value fills.
 int32_t red_init(afh_tree *t, int slot, double v) {
+  const unsigned long long o = host_dbl_to_ord(v);
+  if (t->red_ready[slot] && o == t->red_canon[slot]) {
+    t->red_ready[slot] = false;
+    return AFH_OK;
+  }
   auto *r = reinterpret_cast<unsigned long long *>(t->scratch);
   hipLaunchKernelGGL(k_red_fill, dim3(RED_SHARDS / 256), dim3(256), 0,
-                     t->stream, r + (size_t)slot * RED_SHARDS,
-                     host_dbl_to_ord(v));
+                     t->stream, r + (size_t)slot * RED_SHARDS, o);
   AFH_LAUNCH_CHECK("k_red_fill");
+  t->red_ready[slot] = false;
   return AFH_OK;
 }
 int32_t red_finish(afh_tree *t, int slot, bool is_max) {
   auto *r = reinterpret_cast<unsigned long long *>(t->scratch);
   hipLaunchKernelGGL(k_red_fold, dim3(1), dim3(RED_SHARDS), 0, t->stream,
                      r + (size_t)slot * RED_SHARDS,
-                     r + (size_t)RED_SLOTS * RED_SHARDS + slot, is_max ? 1 : 0);
+                     r + (size_t)RED_SLOTS * RED_SHARDS + slot, is_max ? 1 : 0,
+                     (unsigned long long)t->red_canon[slot]);
   AFH_LAUNCH_CHECK("k_red_fold");
+  t->red_ready[slot] = true;
   return AFH_OK;
 }
 int32_t red_fetch(afh_tree *t, int slot, int n, double *out) {
@@ -594,6 +724,7 @@ static int32_t tree_create_impl(const afh_tree_desc *d, int32_t device,
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1)
     return set_error(AFH_ERR_DEVICE, "no HIP device available");
   afh_tree *t = new afh_tree();
+  if (const char *env = getenv("AFH_GC_BOX")) t->gc_box = atoi(env) != 0;
   if (const char *env = getenv("AFH_GC_FACES6")) t->gc_faces6 = atoi(env) != 0;
   else t->gc_faces6 = -1;  // by box size
   if (device >= 0) {
@@ -713,6 +844,16 @@ static int32_t tree_create_impl(const afh_tree_desc *d, int32_t device,
   }
   AFH_HIP(hipMalloc(&t->scratch, (size_t)(RED_SLOTS + 1) * RED_SHARDS * sizeof(double)));
   AFH_HIP(hipHostMalloc(&t->h_scratch, RED_SLOTS * sizeof(double)));
+  // canonical start values of the reduction slots: the flux maxima (0, 1),
+  // the chemistry time-step minimum (2), max|x| (3, 4)
+  static_assert(RED_SLOTS == 8, "red_canon / red_ready sizes");
+  const double canon[RED_SLOTS] = {-HUGE_VAL, -HUGE_VAL, 1e100, 0.0, 0.0, 0.0, 0.0, 0.0};
+  for (int q = 0; q < RED_SLOTS; q++) {
+    t->red_canon[q] = host_dbl_to_ord(canon[q]);
+    t->red_ready[q] = false;
+    if (int32_t e2 = red_init(t, q, canon[q])) return e2;
+    t->red_ready[q] = true;
+  }
   AFH_HIP(hipStreamSynchronize(t->stream));
   *out = t;
   return AFH_OK;
