@@ -156,6 +156,16 @@ int32_t reduce(afh_dist *d, int kind, double *vals, int n) {
   return AFH_OK;
 }
 
+// RCCL: all-reduce n ordered keys (dbl_to_ord: max / min of the keys is that
+// of the doubles) in place on the tree's stream
+int32_t dist_dev_reduce(void *ctx, int kind, unsigned long long *keys, int n) {
+  afh_dist *d = static_cast<afh_dist *>(ctx);
+  if (ncclAllReduce(keys, keys, n, ncclUint64, kind == AFH_HOOK_MIN ? ncclMin : ncclMax,
+                    d->comm, d->t->stream) != ncclSuccess)
+    return set_error(AFH_ERR_DEVICE, "ncclAllReduce (device keys)");
+  return AFH_OK;
+}
+
 int32_t dist_hook(void *ctx, int32_t kind, int32_t level, int32_t iv, double *vals, int32_t n) {
   afh_dist *d = static_cast<afh_dist *>(ctx);
   switch (kind) {
@@ -361,6 +371,7 @@ int32_t afh_dist_create(afh_tree *t, const afh_tree_desc *desc, const int32_t *o
   if (!e && transport == AFH_DIST_RCCL && hipMalloc(&d->d_red, 16 * sizeof(double)) != hipSuccess)
     e = set_error(AFH_ERR_DEVICE, "reduction buffer");
   if (!e) e = afh_tree_set_hook(t, dist_hook, d);
+  if (!e && transport == AFH_DIST_RCCL) t->dev_reduce = dist_dev_reduce;
   if (e) {
     afh_dist_destroy(d);
     return e;
@@ -372,7 +383,10 @@ int32_t afh_dist_create(afh_tree *t, const afh_tree_desc *desc, const int32_t *o
 
 int32_t afh_dist_destroy(afh_dist *d) {
   if (!d) return AFH_OK;
-  if (d->t && !d->t->retired && d->t->hook_ctx == d) afh_tree_set_hook(d->t, nullptr, nullptr);
+  if (d->t && !d->t->retired && d->t->hook_ctx == d) {
+    afh_tree_set_hook(d->t, nullptr, nullptr);
+    d->t->dev_reduce = nullptr;
+  }
   if (d->t) hipStreamSynchronize(d->t->stream);
   for (auto &kv : d->plans)
     for (auto *v : {&kv.second.send, &kv.second.recv})

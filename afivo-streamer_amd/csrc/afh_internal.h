@@ -107,6 +107,10 @@ struct afh_tree {
   // smoother's spare phi image (variable 0 in hooks and plans), plans
   afh_hook_fn hook = nullptr;
   void *hook_ctx = nullptr;
+  // sharded over RCCL (afh_dist_create): MAX / MIN of the reduction slots are
+  // all-reduced on the device, on the ordered keys in place (stream-ordered,
+  // no host round trip); the one fetch afterwards reads the global value
+  int32_t (*dev_reduce)(void *ctx, int kind, unsigned long long *keys, int n) = nullptr;
   // shared by every multigrid on the tree (one stream: the image is only
   // live inside one fused pair); freed with the last of them
   double *alt = nullptr;
@@ -210,6 +214,11 @@ int32_t red_init(afh_tree *t, int slot, double v);
 int32_t red_finish(afh_tree *t, int slot, bool is_max);
 // fetch the folded values of `n` consecutive slots starting at `slot`
 int32_t red_fetch(afh_tree *t, int slot, int n, double *out);
+// the folded values of slots slot .. slot+n_max-1 (maxima) and the next
+// n_min (minima), reduced over the ranks of a sharded tree: on the device
+// before the fetch (dev_reduce), or through the host hook after it
+int32_t red_reduce_fetch(afh_tree *t, int slot, int n_max, int n_min, double *out,
+                         int iv = 0, int level = 0);
 __device__ __forceinline__ int red_shard() {
   return (int)((blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) &
                (RED_SHARDS - 1));

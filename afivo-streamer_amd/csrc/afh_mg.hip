@@ -2570,9 +2570,13 @@ static void launch_pair_t(afh_mg *mg, int lvl, const double *src, double *dst,
 // whole boxes per workgroup, or NC/4-row tiles (NC >= 32) on levels of
 // 64..255 boxes, which fill the CUs with 4 tiles per box
 // (AFH_GSRB_TILES=1: tiles on every level, for tests)
+// The geometry follows the boxes THIS rank smooths (the variants are bitwise
+// alike and exchange the same data, so ranks need not agree on it): a rank
+// of a sharded tree with fewer than 256 boxes of a level (S1-64 on 8 GPUs:
+// 64 leaf boxes each) splits them, instead of leaving most CUs idle.
 static bool pair_tiles(const afh_mg *mg, int lvl) {
-  const int n = mg->t->lvl_total[lvl - 1];
-  return mg->t->nc >= 32 && (mg->force_tiles || (n >= 64 && n < 256));
+  const int n = mg->t->ids.n(lvl);
+  return mg->t->nc >= 32 && (mg->force_tiles || n < 256);
 }
 
 template <int NC, int TJ, int DEPTH, int NTM = 0, bool FR = true, bool P3 = true,
@@ -3065,9 +3069,7 @@ static int32_t solve_coarse_gs(afh_mg *mg) {
     AFH_LAUNCH_CHECK("k_change_max");
     double r[2];
     if ((e = red_finish(t, 0, true)) || (e = red_finish(t, 1, true)) ||
-        (e = red_fetch(t, 0, 2, r)) ||
-        (e = call_hook(t, AFH_HOOK_MAX, 1, mg->d.i_phi, &r[0], 1)) ||
-        (e = call_hook(t, AFH_HOOK_MAX, 1, mg->d.i_phi, &r[1], 1)))
+        (e = red_reduce_fetch(t, 0, 2, 0, r, mg->d.i_phi, 1)))
       return e;
     double sp = 2.2250738585072014e-308;  // Fortran spacing(max |phi|)
     if (r[1] > 0) {
@@ -3308,9 +3310,7 @@ static int32_t residual_levels(afh_mg *mg, int max_lvl, bool max_out) {
 }
 
 static int32_t residual_fetch(afh_mg *mg, double *max_out) {
-  int32_t e;
-  if ((e = red_fetch(mg->t, 3, 1, max_out))) return e;
-  return call_hook(mg->t, AFH_HOOK_MAX, 0, mg->d.i_tmp, max_out, 1);
+  return red_reduce_fetch(mg->t, 3, 1, 0, max_out, mg->d.i_tmp);
 }
 
 // the device work of one V-cycle (everything but reading max|res|)

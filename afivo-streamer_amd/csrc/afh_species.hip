@@ -16,8 +16,11 @@
 //                   get_derivatives (m_af_flux_schemes.f90:320-436,
 //                   src/m_fluid.f90:298-466, src/m_chemistry.f90:565-688)
 #include <algorithm>
+#include <type_traits>
+#include <utility>
 
 #include "afh_internal.h"
+#include "afh_networks.h"
 
 namespace afh {
 
@@ -633,6 +636,100 @@ __device__ __forceinline__ double rate_of(const UpdArgs &A, const DevReaction &R
   }
 }
 
+// Compiled reaction networks (afh_networks.h, scripts/gen_networks.py): the
+// reaction loop of get_rates / get_derivatives unrolled at compile time, so
+// the rate form is a constant, not a per-reaction switch, and every species
+// index is a register number, not a run-time index into the state arrays
+// (the generic loop pays both per reaction and cell). The coefficients are
+// still read from A.reac. Same expressions in the same order as rate_of and
+// the generic loop: bitwise the same derivatives.
+template <int T, bool SLOW>
+__device__ __forceinline__ double rate_t(const UpdArgs &A, const DevReaction &R, double field,
+                                         double &Te, int low, double lf) {
+  const double c0 = R.rate_factor;
+  const double *c = R.c;
+  if constexpr (T == AFH_RATE_TABULATED_FIELD) {
+    return c0 * (low > 0 ? lt_at_rm(A.chem, R.table_col, low, lf)
+                         : lt_col(A.chem, R.table_col, field));
+  } else if constexpr (T == AFH_RATE_CONSTANT) {
+    return c0 * c[0];
+  } else if constexpr (T == AFH_RATE_LINEAR) {
+    return c0 * c[0] * (field - c[1]);
+  } else if constexpr (T == AFH_RATE_EXP_V1) {
+    const double z = c[1] / (c[2] + field);
+    return c0 * c[0] * exp(-(z * z));
+  } else if constexpr (T == AFH_RATE_EXP_V2) {
+    const double z = field / c[1];
+    return c0 * c[0] * exp(-(z * z));
+  } else {
+    static_assert(SLOW, "temperature-dependent rate form in a fast update");
+    return rate_slow(A, R, field, Te);
+  }
+}
+
+// a temperature-dependent rate form in network NET (afh_fluid::slow_rates)
+template <class NET>
+constexpr bool net_slow() {
+  for (int r = 0; r < NET::NR; r++)
+    if (NET::type[r] > AFH_RATE_EXP_V2) return true;
+  return false;
+}
+
+// dens / der slot of 1-based reference species index ix (afh_fluid_create's
+// remap: gas species after the plasma species)
+template <class NET>
+constexpr int net_slot(int ix) {
+  return ix <= NET::NG ? NET::NS + ix - 1 : ix - NET::NG - 1;
+}
+
+template <class NET, bool SLOW, int R, int NT>
+__device__ __forceinline__ void net_one(const UpdArgs &A, double field, double &Te, int clow,
+                                        double clf, const double (&dens)[NT], double (&der)[NT]) {
+  constexpr int NI = NET::n_in[R], NO = NET::n_out[R];
+  const DevReaction &X = A.reac[R];
+  double rate = rate_t<NET::type[R], SLOW>(A, X, field, Te, clow, clf);
+  double prod = 1.0;
+  if constexpr (NI > 0) prod = prod * dens[net_slot<NET>(NET::ix_in[R][0])];
+  if constexpr (NI > 1) prod = prod * dens[net_slot<NET>(NET::ix_in[R][1])];
+  if constexpr (NI > 2) prod = prod * dens[net_slot<NET>(NET::ix_in[R][2])];
+  if constexpr (NI > 3) prod = prod * dens[net_slot<NET>(NET::ix_in[R][3])];
+  rate = rate * prod;
+  if constexpr (NI > 0) der[net_slot<NET>(NET::ix_in[R][0])] += -rate;
+  if constexpr (NI > 1) der[net_slot<NET>(NET::ix_in[R][1])] += -rate;
+  if constexpr (NI > 2) der[net_slot<NET>(NET::ix_in[R][2])] += -rate;
+  if constexpr (NI > 3) der[net_slot<NET>(NET::ix_in[R][3])] += -rate;
+  if constexpr (NO > 0) der[net_slot<NET>(NET::ix_out[R][0])] += rate * NET::mult[R][0];
+  if constexpr (NO > 1) der[net_slot<NET>(NET::ix_out[R][1])] += rate * NET::mult[R][1];
+  if constexpr (NO > 2) der[net_slot<NET>(NET::ix_out[R][2])] += rate * NET::mult[R][2];
+  if constexpr (NO > 3) der[net_slot<NET>(NET::ix_out[R][3])] += rate * NET::mult[R][3];
+}
+
+template <class NET, bool SLOW, int NT, size_t... R>
+__device__ __forceinline__ void net_all(const UpdArgs &A, double field, double &Te, int clow,
+                                        double clf, const double (&dens)[NT], double (&der)[NT],
+                                        std::index_sequence<R...>) {
+  (net_one<NET, SLOW, (int)R, NT>(A, field, Te, clow, clf, dens, der), ...);
+}
+
+// does the fluid's reaction list have network NET's structure?
+template <class NET>
+static bool net_matches(const afh_fluid_desc *d) {
+  const bool gas = d->i_gas_dens > 0;
+  if (d->n_species != NET::NS || d->n_reactions != NET::NR || gas != (NET::GAS != 0) ||
+      (gas && d->n_gas_species != NET::NG))
+    return false;
+  for (int r = 0; r < NET::NR; r++) {
+    const afh_reaction &a = d->reactions[r];
+    if (a.rate_type != NET::type[r] || a.n_in != NET::n_in[r] || a.n_out != NET::n_out[r])
+      return false;
+    for (int q = 0; q < a.n_in; q++)
+      if (a.ix_in[q] != NET::ix_in[r][q]) return false;
+    for (int q = 0; q < a.n_out; q++)
+      if (a.ix_out[q] != NET::ix_out[r][q] || a.mult_out[q] != NET::mult[r][q]) return false;
+  }
+  return true;
+}
+
 // LDS-staged plane-marching flux (NC in {16, 32, 64}): a workgroup owns TJ
 // rows of a box and marches over k. Each step stages plane k of n_e (rows
 // j0-2 .. j0+TJ+1, columns -1 .. NC+2, second ghost layers from gc2) and of
@@ -968,7 +1065,8 @@ __global__ void k_consistent(double *__restrict__ F,
 #ifndef AFH_UPD_MINW  // minimum waves per SIMD of the update kernel
 #define AFH_UPD_MINW 1
 #endif
-template <int NS, bool SLOW, int NP = MAXPREV, bool SD = true, bool GAS = false>
+template <int NS, bool SLOW, int NP = MAXPREV, bool SD = true, bool GAS = false,
+          class NET = void>
 __global__ void __launch_bounds__(256, AFH_UPD_MINW)
     k_update(UpdArgs A, const int32_t *__restrict__ ids, int nc, size_t bsz,
              size_t fsz, unsigned long long *red) {
@@ -1040,15 +1138,20 @@ __global__ void __launch_bounds__(256, AFH_UPD_MINW)
     int clow = -1;
     double clf = 0.0;
     if (A.chem.rm) lt_loc(A.chem, field, clow, clf);
-    for (int r = 0; r < A.nr; r++) {
-      const DevReaction &R = A.reac[r];
-      double rate = rate_of<SLOW>(A, R, field, Te, clow, clf);
-      double prod = 1.0;
-      for (int q = 0; q < R.n_in; q++) prod = prod * sel(dens, R.ix_in[q] - 1);
-      rate = rate * prod;
-      for (int q = 0; q < R.n_in; q++) add_at(der, R.ix_in[q] - 1, -rate);
-      for (int q = 0; q < R.n_out; q++)
-        add_at(der, R.ix_out[q] - 1, rate * R.mult_out[q]);
+    if constexpr (!std::is_void<NET>::value) {
+      net_all<NET, SLOW>(A, field, Te, clow, clf, dens, der,
+                         std::make_index_sequence<NET::NR>{});
+    } else {
+      for (int r = 0; r < A.nr; r++) {
+        const DevReaction &R = A.reac[r];
+        double rate = rate_of<SLOW>(A, R, field, Te, clow, clf);
+        double prod = 1.0;
+        for (int q = 0; q < R.n_in; q++) prod = prod * sel(dens, R.ix_in[q] - 1);
+        rate = rate * prod;
+        for (int q = 0; q < R.n_in; q++) add_at(der, R.ix_in[q] - 1, -rate);
+        for (int q = 0; q < R.n_out; q++)
+          add_at(der, R.ix_out[q] - 1, rate * R.mult_out[q]);
+      }
     }
     if (A.last_step) {
       const double eps = 1e-100;
@@ -1104,13 +1207,52 @@ __global__ void __launch_bounds__(256, AFH_UPD_MINW)
   }
 }
 
+// the update of a compiled network (NET::NS == NS): the variants of
+// launch_update's generic dispatch
+template <int NS, class NET>
+static bool launch_update_net(const UpdArgs &A, afh_tree *t, const dim3 &grid,
+                              const int32_t *ids, unsigned long long *red, bool slow) {
+  if constexpr (NET::NS != NS) {
+    return false;
+  } else {
+    constexpr bool SL = net_slow<NET>();
+    const int nc = t->nc;
+    const bool sd = A.der_q < 0;
+    if (NET::GAS != (A.Ng != nullptr) || slow != SL) return false;
+    if constexpr (NET::GAS) {
+      hipLaunchKernelGGL((k_update<NS, SL, MAXPREV, true, true, NET>), grid, dim3(256), 0,
+                         t->stream, A, ids, nc, t->bsz, t->fsz, red);
+    } else {
+      if (A.n_prev == 1 && !sd)
+        hipLaunchKernelGGL((k_update<NS, SL, 1, false, false, NET>), grid, dim3(256), 0,
+                           t->stream, A, ids, nc, t->bsz, t->fsz, red);
+      else if (A.n_prev == 2 && !sd)
+        hipLaunchKernelGGL((k_update<NS, SL, 2, false, false, NET>), grid, dim3(256), 0,
+                           t->stream, A, ids, nc, t->bsz, t->fsz, red);
+      else
+        hipLaunchKernelGGL((k_update<NS, SL, MAXPREV, true, false, NET>), grid, dim3(256),
+                           0, t->stream, A, ids, nc, t->bsz, t->fsz, red);
+    }
+    return true;
+  }
+}
+
 template <int NS>
 void launch_update(const UpdArgs &A, afh_tree *t, int l,
-                   unsigned long long *red, bool slow) {
+                   unsigned long long *red, bool slow, int net = 0) {
   const int nc = t->nc, n3 = nc * nc * nc;
   const dim3 grid((n3 / AFH_UPD_KC + 255) / 256, t->leaves.n(l));
   const auto *ids = t->leaves.at(l);
   const bool sd = A.der_q < 0;
+  switch (net) {
+#define AFH_NET_CASE(K, NET) \
+  case K:                   \
+    if (launch_update_net<NS, net::NET>(A, t, grid, ids, red, slow)) return; \
+    break;
+    AFH_NETWORKS(AFH_NET_CASE)
+#undef AFH_NET_CASE
+  default: break;
+  }
   if (A.Ng)
     hipLaunchKernelGGL((k_update<NS, true, MAXPREV, true, true>), grid, dim3(256), 0,
                        t->stream, A, ids, nc, t->bsz, t->fsz, red);
@@ -1650,6 +1792,9 @@ struct afh_fluid {
   // the table does not fit LDS or AFH_FLUX_STAGED=1 selects k_flux_staged
   double *d_tdi = nullptr;
   bool slow_rates = false;  // a reaction with a temperature-dependent form
+  // compiled network of the reaction list (afh_networks.h, 1-based; 0: the
+  // generic loop); AFH_UPD_NET=0 forces the generic loop, =2 requires a match
+  int net = 0;
   int32_t *d_ids = nullptr;  // box list of afh_electrode_species_bc
   int ids_cap = 0;
   // afh_fluid_set_rhs_output: the update also writes field_set_rhs(rhs_iv,
@@ -1768,6 +1913,18 @@ int32_t afh_fluid_create(afh_tree *t, const afh_fluid_desc *d, afh_fluid **out) 
       if (a.ix_out[q] < 1 || a.ix_out[q] > ng + d->n_species)
         return set_error(AFH_ERR_ARG, "reaction species index");
   }
+  {
+    const char *env = getenv("AFH_UPD_NET");
+    if (!(env && atoi(env) == 0)) {
+#define AFH_NET_MATCH(K, NET) \
+  if (!f->net && net_matches<net::NET>(d)) f->net = K;
+      AFH_NETWORKS(AFH_NET_MATCH)
+#undef AFH_NET_MATCH
+    }
+    // AFH_UPD_NET=2 (tests): a compiled network must match
+    if (env && atoi(env) == 2 && !f->net)
+      return set_error(AFH_ERR_UNSUPPORTED, "no compiled reaction network matches");
+  }
   AFH_HIP(hipMalloc(&f->d_reac, sizeof(DevReaction) * R.size()));
   AFH_HIP(hipMemcpy(f->d_reac, R.data(), sizeof(DevReaction) * R.size(),
                     hipMemcpyHostToDevice));
@@ -1845,10 +2002,7 @@ int32_t afh_fluid_rhs_maxabs(afh_fluid *f, int32_t s_out, double *max_rhs) {
   AFH_LIVE(f->t, "afh_fluid_rhs_maxabs");
   if (!f->rhs_current(s_out))
     return set_error(AFH_ERR_STATE, "no current rhs output of state %d", s_out);
-  afh_tree *t = f->t;
-  int32_t e;
-  if ((e = red_fetch(t, 4, 1, max_rhs))) return e;
-  return call_hook(t, AFH_HOOK_MAX, 0, f->rhs_iv, max_rhs, 1);
+  return red_reduce_fetch(f->t, 4, 1, 0, max_rhs, f->rhs_iv);
 }
 
 int32_t afh_fluid_rhs_valid(afh_fluid *f, int32_t s_out, int32_t *valid) {
@@ -1902,8 +2056,8 @@ static int32_t set_rhs_impl(afh_fluid *f, int32_t i_rhs, int32_t s_in,
     AFH_LAUNCH_CHECK("k_set_rhs");
   }
   if (!max_out) return AFH_OK;
-  if ((e = red_finish(t, 3, true)) || (e = red_fetch(t, 3, 1, max_out))) return e;
-  return call_hook(t, AFH_HOOK_MAX, 0, i_rhs, max_out, 1);
+  if ((e = red_finish(t, 3, true))) return e;
+  return red_reduce_fetch(t, 3, 1, 0, max_out, i_rhs);
 }
 
 extern "C" {
@@ -2109,9 +2263,7 @@ int32_t afh_flux_upwind_tree(afh_fluid *f, int32_t s_deriv, double *dt_lim) {
   if (iv < 1 || iv > t->nvc) return set_error(AFH_ERR_ARG, "bad s_deriv");
   int32_t e;
   double r[2];
-  if ((e = flux_tree_dev(f, s_deriv)) || (e = red_fetch(t, 0, 2, r)) ||
-      (e = call_hook(t, AFH_HOOK_MAX, 0, 0, r, 2)))
-    return e;
+  if ((e = flux_tree_dev(f, s_deriv)) || (e = red_reduce_fetch(t, 0, 2, 0, r))) return e;
   flux_dt_limits(r, dt_lim);
   return AFH_OK;
 }
@@ -2141,7 +2293,7 @@ static int32_t update_dev(afh_fluid *f, double dt, int32_t s_deriv, int32_t n_pr
     for (int q = 0; q < 3; q++) A.dt_dr[q] = dt / t->lvl_dr[3 * (l - 1) + q];
     prof_begin(t, AFH_PROF_UPDATE);
     switch (A.ns) {
-#define AFH_CASE(N) case N: launch_update<N>(A, t, l, red, f->slow_rates); break;
+#define AFH_CASE(N) case N: launch_update<N>(A, t, l, red, f->slow_rates, f->net); break;
       AFH_CASE(1) AFH_CASE(2) AFH_CASE(3) AFH_CASE(4) AFH_CASE(5) AFH_CASE(6)
       AFH_CASE(7) AFH_CASE(8) AFH_CASE(9) AFH_CASE(10) AFH_CASE(11)
       AFH_CASE(12) AFH_CASE(13) AFH_CASE(14) AFH_CASE(15) AFH_CASE(16)
@@ -2187,8 +2339,7 @@ int32_t afh_flux_update_densities(afh_fluid *f, double dt, int32_t s_deriv,
   if ((e = update_dev(f, dt, s_deriv, n_prev, s_prev, w_prev, s_out, last_step))) return e;
   double r = 1e100;
   if (last_step) {
-    if ((e = red_fetch(t, 2, 1, &r)) || (e = call_hook(t, AFH_HOOK_MIN, 0, 0, &r, 1)))
-      return e;
+    if ((e = red_reduce_fetch(t, 2, 0, 1, &r))) return e;
   } else {
     AFH_HIP(hipStreamSynchronize(t->stream));
   }
@@ -2265,9 +2416,7 @@ int32_t afh_fluid_forward_euler(afh_fluid *f, double dt, int32_t s_deriv,
     double r[3] = {0.0, 0.0, 1e100};
     if ((e = flux_tree_dev(f, s_deriv)) ||
         (e = update_dev(f, dt, s_deriv, n_prev, s_prev, w_prev, s_out, last_step)) ||
-        (e = red_fetch(t, 0, last_step ? 3 : 2, r)) ||
-        (e = call_hook(t, AFH_HOOK_MAX, 0, 0, r, 2)) ||
-        (last_step && (e = call_hook(t, AFH_HOOK_MIN, 0, 0, r + 2, 1))))
+        (e = red_reduce_fetch(t, 0, 2, last_step ? 1 : 0, r)))
       return e;
     flux_dt_limits(r, dt_lim);
     dt_lim[2] = r[2], dt_lim[3] = 1e100;
@@ -2306,14 +2455,8 @@ int32_t afh_fluid_forward_euler(afh_fluid *f, double dt, int32_t s_deriv,
   }
   if ((e = red_finish(t, 0, true)) || (e = red_finish(t, 1, true))) return e;
   if (last_step && (e = red_finish(t, 2, false))) return e;
-  double r[3];
-  if ((e = red_fetch(t, 0, 3, r)) || (e = call_hook(t, AFH_HOOK_MAX, 0, 0, r, 2)))
-    return e;
-  if (last_step) {
-    if ((e = call_hook(t, AFH_HOOK_MIN, 0, 0, r + 2, 1))) return e;
-  } else {
-    r[2] = 1e100;
-  }
+  double r[3] = {0.0, 0.0, 1e100};
+  if ((e = red_reduce_fetch(t, 0, 2, last_step ? 1 : 0, r))) return e;
   dt_lim[0] = 1 / r[0];
   dt_lim[1] = 8.8541878176e-12 / (1.6022e-19 * std::max(r[1], 1e-100));
   dt_lim[2] = r[2];

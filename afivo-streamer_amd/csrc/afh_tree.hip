@@ -527,6 +527,22 @@ int32_t red_fetch(afh_tree *t, int slot, int n, double *out) {
   return AFH_OK;
 }
 
+int32_t red_reduce_fetch(afh_tree *t, int slot, int n_max, int n_min, double *out, int iv,
+                         int level) {
+  int32_t e;
+  if (t->hook && t->dev_reduce) {
+    auto *keys = reinterpret_cast<unsigned long long *>(t->scratch) +
+                 (size_t)RED_SLOTS * RED_SHARDS + slot;
+    if (n_max && (e = t->dev_reduce(t->hook_ctx, AFH_HOOK_MAX, keys, n_max))) return e;
+    if (n_min && (e = t->dev_reduce(t->hook_ctx, AFH_HOOK_MIN, keys + n_max, n_min))) return e;
+    return red_fetch(t, slot, n_max + n_min, out);
+  }
+  if ((e = red_fetch(t, slot, n_max + n_min, out))) return e;
+  if (n_max && (e = call_hook(t, AFH_HOOK_MAX, level, iv, out, n_max))) return e;
+  if (n_min && (e = call_hook(t, AFH_HOOK_MIN, level, iv, out + n_max, n_min))) return e;
+  return AFH_OK;
+}
+
 // max |x| over the interiors of the listed boxes -> sharded atomicMax
 __global__ void k_maxabs(const double *__restrict__ v,
                          const int32_t *__restrict__ ids, int nc, size_t bsz,
@@ -1053,8 +1069,8 @@ int32_t afh_tree_maxabs_cc(afh_tree *t, int32_t iv, double *out) {
                        t->ccv(iv), t->leaves.at(l), nc, t->bsz, d);
     AFH_LAUNCH_CHECK("k_maxabs");
   }
-  if ((e = red_finish(t, 3, true)) || (e = red_fetch(t, 3, 1, out))) return e;
-  return call_hook(t, AFH_HOOK_MAX, 0, iv, out, 1);
+  if ((e = red_finish(t, 3, true))) return e;
+  return red_reduce_fetch(t, 3, 1, 0, out, iv);
 }
 
 // per-box partial results over all leaves (level order), on the host
@@ -1166,6 +1182,7 @@ int32_t afh_tree_set_hook(afh_tree *t, afh_hook_fn fn, void *ctx) {
   AFH_LIVE(t, "afh_tree_set_hook");
   t->hook = fn;
   t->hook_ctx = ctx;
+  t->dev_reduce = nullptr;  // the library's RCCL transport sets its own
   return AFH_OK;
 }
 

@@ -13,5 +13,6 @@ rc=$?; echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_gpu.log
 for v in AFH_GC_BOX AFH_PAIR_PUSH AFH_CS_DIRECT_SMALL; do
   CFG=s1 REPS=2 bash scripts/env_bench_ab.sh $v "0 1" || exit $?
 done
-CFG=s3 REPS=2 bash scripts/env_bench_ab.sh AFH_GC_BOX,AFH_PAIR_PUSH,AFH_CS_DIRECT_SMALL "0 1" || exit $?
+CFG=s3 REPS=2 bash scripts/env_bench_ab.sh AFH_GC_BOX,AFH_PAIR_PUSH,AFH_CS_DIRECT_SMALL,AFH_UPD_NET "0 1" || exit $?
+CFG=s3 REPS=2 bash scripts/env_bench_ab.sh AFH_UPD_NET "0 1" || exit $?
 CFG=s1-64 REPS=1 bash scripts/env_bench_ab.sh AFH_GC_BOX "1" || exit $?

@@ -1,0 +1,77 @@
+"""Round-3 launch fusions, each bitwise its unfused form (run-time switches
+read at tree / multigrid / fluid creation):
+
+* AFH_GC_BOX: a small box's level fill (faces, edges, corners) in one
+  workgroup (k_gc_box) vs k_gc_faces6 + k_gc_corners;
+* AFH_PAIR_PUSH: the small-box fused red-black pair writes the level's face
+  ghosts itself (k_gsrb_pair_box PUSH) vs the pair + a level fill;
+* AFH_CS_DIRECT_SMALL: the exact level-1 solve of a grid up to 16^3 in one
+  workgroup (k_cs_direct_small) vs gather + six transforms + scatter;
+* AFH_UPD_NET: the compiled reaction network (afh_networks.h, k_update's
+  unrolled reaction loop) vs the generic loop -- on the S3 tree with
+  air_chemistry_v2 (9 species, 25 reactions) and on S1's old-style model.
+
+The fused forms are also what every other GPU test runs (they are the
+defaults); these tests pin them to the unfused forms on full workloads.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _s1(monkeypatch, env):
+    import bench
+    from afh import capi
+    from afh.streamer import IV
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    c = bench.build_case(capi.hip_library(), "s1", 0, 0)
+    c.fuse_rhs(True, ghosts=False)
+    out = {"res0": c.field_compute(0, n_vcycles=2)}
+    for k in range(4):
+        out["step%d" % k] = bench.unit_step(c, 1e-13, k)
+    for v in ("e", "pos", "neg", "phi", "efld", "rhs", "tmp"):
+        out[v] = c.tree.get_cc(IV[v])
+    c.tree.close()
+    return out
+
+
+def _same(a, b):
+    for k in a:
+        if isinstance(a[k], np.ndarray):
+            assert np.array_equal(a[k], b[k]), (k, np.nanmax(np.abs(a[k] - b[k])))
+        else:
+            assert a[k] == b[k], (k, a[k], b[k])
+
+
+@pytest.mark.parametrize("switch", ["AFH_GC_BOX", "AFH_PAIR_PUSH", "AFH_CS_DIRECT_SMALL",
+                                    "AFH_UPD_NET"])
+def test_s1_fusion_bitwise(switch, monkeypatch):
+    """Config 2 (S1: 512 leaf boxes of 16^3, 4 levels): field solve and four
+    unit steps with the fusion on and off."""
+    # AFH_UPD_NET=2: the compiled network must match (S1's old-style model)
+    a = _s1(monkeypatch, {switch: "2" if switch == "AFH_UPD_NET" else "1"})
+    b = _s1(monkeypatch, {switch: "0"})
+    _same(a, b)
+
+
+def test_s3_compiled_network_bitwise(monkeypatch):
+    """Config 3's chemistry: the species step on the S3 tree with the
+    compiled air_chemistry_v2 network, bitwise the generic reaction loop
+    (both Heun stages, the chemistry time-step limit)."""
+    import golden
+    from afh import capi
+    from afh.driver import Simulation
+    outs = []
+    for net in ("2", "0"):  # 2: the compiled network must match
+        monkeypatch.setenv("AFH_UPD_NET", net)
+        sim = Simulation(capi.hip_library(), golden.load("case_s3"), device=0)
+        sim.set_initial_conditions()
+        lims = [list(sim.fluid.forward_euler(1e-12, 0, [0], [1.0], 1, False)),
+                list(sim.fluid.forward_euler(5e-13, 1, [0, 1], [0.5, 0.5], 0, True))]
+        states = [sim.tree.get_cc(iv + s) for iv in sim.densities for s in (0, 1)]
+        outs.append((lims, states))
+    assert outs[0][0] == outs[1][0]
+    for x, y in zip(outs[0][1], outs[1][1]):
+        assert np.array_equal(x, y)
