@@ -386,11 +386,23 @@ class NativeGroup:
     (AFH_DIST_LOCAL; one thread per rank)."""
 
     def __init__(self, lib, n_ranks):
+        import threading
         self.lib = lib
         self.n_ranks = n_ranks
         h = C.c_void_p()
         lib.call("dist_group_create", n_ranks, C.byref(h))
         self.h = h
+        # host-side all-gather of Python objects among the thread ranks
+        self._barrier = threading.Barrier(n_ranks)
+        self._slots = [None] * n_ranks
+
+    def allgather(self, rank, obj):
+        """Every thread rank's obj, in rank order (a collective of the group)."""
+        self._slots[rank] = obj
+        self._barrier.wait()
+        out = list(self._slots)
+        self._barrier.wait()
+        return out
 
     def close(self):
         if self.h:
@@ -438,6 +450,7 @@ class NativeShard:
         self.n = n_ranks
         self.rank = rank
         self.transport = transport
+        self.group, self.comm = group, comm
         self.link = group.h if transport == capi.DIST_LOCAL else comm
         self._desc, self._keep = tree_desc(topo, 1, 1)
         self.owner = np.zeros(int(topo["n_boxes"]), np.int32)
@@ -480,6 +493,23 @@ class NativeShard:
         if self.h:
             self.lib.call("dist_destroy", self.h)
             self.h = C.c_void_p()
+
+    def renew(self, topo):
+        """A shard of a new topology (after a regrid) over the same ranks and
+        transport: a fresh partition."""
+        return NativeShard(self.lib, topo, self.n, self.rank, self.transport,
+                           group=self.group, comm=self.comm)
+
+    def allgather(self, obj):
+        """Every rank's obj, in rank order: the thread ranks' group, or the
+        torch.distributed process group (RCCL transport: one rank per
+        process)."""
+        if self.transport == capi.DIST_LOCAL:
+            return self.group.allgather(self.rank, obj)
+        import torch.distributed as tdist
+        out = [None] * self.n
+        tdist.all_gather_object(out, obj)
+        return out
 
     def stats(self):
         n, b = C.c_int64(), C.c_int64()

@@ -252,6 +252,7 @@ class Simulation:
                          r_min=self.origin)
         self.tree = self.fluid = self.mg = None
         self.helm = []
+        self.shard = None  # shard_over
 
     # ------------------------------------------------------------- device
     def _capacity(self):
@@ -304,10 +305,11 @@ class Simulation:
         potential; the electrode boxes for refine_electrode_dx and
         electrode_species_bc."""
         nc, ng = self.af.nc, self.af.nc + 2
-        lsf = np.zeros((self.tree.n_boxes, ng, ng, ng))
+        n_glob = self._n_global()
+        lsf = np.zeros((n_glob, ng, ng, ng))
         bv = self.lsf_boundary_value()
         self.electrode_ids = []
-        self.electrode_box = np.zeros(self.tree.n_boxes, np.uint8)
+        self.electrode_box = np.zeros(n_glob, np.uint8)
         used = [b for b in range(1, self.af.highest_id + 1) if self.af.in_use[b]]
         r = np.stack([electrode.cell_centers(self.af.r_min[b], self.af.dr[b], nc, 0, nc + 1)
                       for b in used])
@@ -324,15 +326,113 @@ class Simulation:
             if op is None:
                 continue
             v, fb, ix, dd = op  # fb: f times 1
-            self.electrode_ids.append(b)
             self.electrode_box[b - 1] = 1
-            self.mg.set_box_stencil(b, v, fb * bv)
-            self.mg.set_box_lsf(b, ix, dd, np.full((nc, nc, nc), bv), self.i_lsf)
+            # a sharded tree: the boxes it stores, by their library ids;
+            # electrode_species_bc on the boxes it computes
+            lid = self.tree.local_id(b)
+            if not lid:
+                continue
+            if self.shard is None or self._computes(b):
+                self.electrode_ids.append(lid)
+            self.mg.set_box_stencil(lid, v, fb * bv)
+            self.mg.set_box_lsf(lid, ix, dd, np.full((nc, nc, nc), bv), self.i_lsf)
         self.tree.put_cc(self.i_lsf, lsf)
 
     def _create_tree(self):
         t = Tree(self.lib, self.af.topology(), self.n_var_cell, self.n_var_face,
                  device=self.device, box_capacity=self._capacity())
+        return self._set_methods(t)
+
+    def _n_global(self):
+        """Boxes of the whole tree (a sharded tree stores only some)."""
+        t = self.tree
+        return t.n_global if t.global_ids is not None else t.n_boxes
+
+    def _computes(self, b):
+        """This rank computes box b (owns it, or it is on a replicated level)."""
+        sh = self.shard
+        owner = sh.owner if hasattr(sh, "owner") else sh.part.owner
+        o = int(owner[b - 1])
+        return o < 0 or o == sh.rank
+
+    def shard_over(self, shard):
+        """Continue the run sharded over ranks (afh.dist.NativeShard, or the
+        Python Shard): this rank's part of the current tree -- the boxes it
+        owns, the replicated levels and the replicas its exchanges refresh --
+        is created from the current topology and filled with the current
+        data of every variable, the multigrids and the fluid are bound to it
+        and the shard's exchange hook is attached. Every rank must hold the
+        same state before (e.g. the same deterministic set-up). Refinement is
+        not sharded: adjust_refinement then raises."""
+        topo = self.af.topology()
+        full = self.tree
+        t = self._set_methods(shard.make_tree(self.lib, topo, self.n_var_cell,
+                                              self.n_var_face, device=self.device))
+        for iv in range(1, self.n_var_cell + 1):
+            t.put_cc(iv, full.get_cc(iv))
+        for iv in range(1, self.n_var_face + 1):
+            t.put_fc(iv, full.get_fc(iv))
+        self.shard = shard
+        self._bind(t)
+        shard.attach(t)
+        full.close()
+        return t
+
+    def _gather_full(self):
+        """The whole tree on this rank: every rank's computed boxes (owned,
+        and the replicated levels from rank 0), gathered through the shard's
+        host all-gather, in a new single-rank tree."""
+        sh = self.shard
+        owner = np.asarray(sh.owner)
+        t = self._create_tree()
+        for kind, n_var in (("cc", self.n_var_cell), ("fc", self.n_var_face)):
+            get = getattr(self.tree, "get_" + kind)
+            for iv in range(1, n_var + 1):
+                a = get(iv)
+                mine = np.nonzero((owner == sh.rank) | ((owner < 0) & (sh.rank == 0)))[0]
+                parts = sh.allgather((mine, a[mine]))
+                for ids, vals in parts:
+                    a[ids] = vals
+                getattr(t, "put_" + kind)(iv, a)
+        return t
+
+    def _adjust_refinement_sharded(self):
+        """af_adjust_refinement of a sharded run: the whole tree is gathered
+        on every rank, refined there as a single-rank run does (the same
+        flags, topology and data movement on every rank: bitwise the
+        single-rank run), and sharded again with a fresh partition of the new
+        topology, so the load balance follows the refinement."""
+        import copy
+        sh = self.shard
+        # the refinement flags of the computed boxes decide first, on a copy
+        # of the host topology: most calls change nothing and move no data
+        t = self.tree
+        eb = (None if self.lsf is None else
+              np.append(self.electrode_box[t.global_ids - 1], 0).astype(np.uint8))
+        flags, masks = self.fluid.refine_flags(self.refine_desc(), eb)
+        owner = np.asarray(sh.owner)
+        mine = np.nonzero((owner == sh.rank) | ((owner < 0) & (sh.rank == 0)))[0]
+        lid = np.searchsorted(t.global_ids, mine + 1)
+        gf = np.zeros(len(owner), np.int32)
+        gm = np.zeros(len(owner), np.uint32)
+        for ids, f, m in sh.allgather((mine, flags[lid], masks[lid])):
+            gf[ids], gm[ids] = f, m
+        probe = copy.deepcopy(self.af)
+        info = probe.adjust_refinement(
+            lambda ids: (gf[np.asarray(ids, np.int64) - 1], gm[np.asarray(ids, np.int64) - 1]))
+        if not (info.n_add or info.n_rm):
+            return info
+        full = self._gather_full()
+        old = self.tree
+        sh.detach()
+        self.shard = None
+        self._bind(full)
+        old.close()
+        info = self.adjust_refinement()
+        self.shard_over(sh.renew(self.af.topology()))
+        return info
+
+    def _set_methods(self, t):
         neumann0 = [(capi.BC_NEUMANN, 0.0)] * 6
         # z faces Dirichlet 0, other faces Neumann 0 (photoi_helmh_bc)
         helm_bc = [(capi.BC_NEUMANN, 0.0)] * 4 + [(capi.BC_DIRICHLET, 0.0)] * 2
@@ -490,6 +590,8 @@ class Simulation:
     def adjust_refinement(self):
         """af_adjust_refinement with default_refinement: the criterion on the
         device, the topology on the host, the data moved by the device."""
+        if self.shard is not None:
+            return self._adjust_refinement_sharded()
         flags, masks = self.fluid.refine_flags(
             self.refine_desc(), self.electrode_box if self.lsf is not None else None)
 

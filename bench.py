@@ -116,8 +116,15 @@ class DriverCase:
 
     def __init__(self, sim):
         self.sim = sim
-        self.tree = sim.tree
         self.topo = sim.af.topology()
+
+    @property
+    def tree(self):
+        return self.sim.tree
+
+    @property
+    def shard(self):
+        return self.sim.shard
 
     def field_compute(self, s, n_vcycles=2):
         return self.sim.field_compute(s, True)
@@ -272,10 +279,14 @@ def main():
     lib = capi.hip_library()
     sharded = world > 1 and not args.replicas
     if args.config in DRIVER_CONFIGS:
-        if sharded:
-            raise SystemExit("%s: sharding an AMR driver tree is not supported; use --replicas"
-                             % args.config)
         sim = build_driver_case(lib, local, args.config)
+        if sharded:
+            # every rank built the same AMR tree (the set-up is deterministic);
+            # its part of it continues sharded, exchanges over RCCL
+            from afh.dist import NativeShard, rccl_comm
+            sim.shard_over(NativeShard(lib, sim.af.topology(), world, rank,
+                                       transport=capi.DIST_RCCL,
+                                       comm=rccl_comm(lib, rank, world, local)))
         case = DriverCase(sim)
     else:
         case = build_case(lib, args.config, local, args.coarse_cycles,
