@@ -148,6 +148,8 @@ SIGNATURES = {
     "mg_destroy": (i32, [_VP]),
     "mg_fas_vcycle": (i32, [_VP, i32, i32]),
     "mg_fas_vcycle_maxres": (i32, [_VP, i32, P_f64]),
+    "mg_fas_vcycle_fold": (i32, [_VP, i32]),
+    "tree_fetch_reduced": (i32, [_VP, i32, P_i32, P_f64]),
     "mg_fas_fmg": (i32, [_VP, i32, i32]),
     "mg_coarse_iterations": (i32, [_VP, P_i32]),
     "mg_compute_phi_gradient": (i32, [_VP, i32, f64, i32]),
@@ -168,6 +170,8 @@ SIGNATURES = {
                                     i32, P_f64]),
     "fluid_forward_euler": (i32, [_VP, f64, i32, i32, P_i32, P_f64, i32, i32,
                                   i32, P_f64]),
+    "fluid_forward_euler_fold": (i32, [_VP, f64, i32, i32, P_i32, P_f64, i32, i32, i32]),
+    "fluid_fetch_step": (i32, [_VP, i32, i32, P_i32, P_f64, P_f64]),
     "profile_enable": (i32, [_VP, i32]),
     "profile_read": (i32, [_VP, P_f64, C.POINTER(C.c_int64), P_f64]),
     "tree_set_hook": (i32, [_VP, C.c_void_p, _VP]),
@@ -194,6 +198,8 @@ DIST_LOCAL, DIST_RCCL = 1, 2
 HOOK_HALO, HOOK_RIMS, HOOK_RESTRICT, HOOK_MAX, HOOK_MIN, HOOK_CFLUX = 1, 2, 3, 4, 5, 6
 HOOK_SUM = 7
 RED_MAX, RED_MIN, RED_MAXABS = 1, 2, 3
+# deferred reduction slots (afh_tree_fetch_reduced, afh_fluid_fetch_step)
+SLOT_MAXRES, SLOT_RHS = 3, 4
 # int32_t (*)(void *ctx, int32_t kind, int32_t level, int32_t iv, double *vals,
 #             int32_t n)
 HOOK_FN = C.CFUNCTYPE(i32, C.c_void_p, i32, i32, i32, P_f64, i32)

@@ -25,6 +25,7 @@ routines it takes as callbacks are the library's (field_bc_homogeneous,
 af_bc_neumann_zero, photoi_helmh_bc, default_refinement).
 """
 import math
+import os
 
 import numpy as np
 
@@ -134,6 +135,9 @@ class Simulation:
         self.coarse_tol = coarse_tol
         self.capacity_factor = capacity_factor
         self.fused_rhs = fuse_rhs
+        # field_compute reads max|rhs| with the first residual (AFH_DEFER=0:
+        # before the V-cycle, as the reference orders it; for A/B runs)
+        self._defer_ok = os.environ.get("AFH_DEFER", "1") != "0"
         if c.s("time_integrator") != "heuns_method":
             raise NotImplementedError("time integrator %s" % c.s("time_integrator"))
         self.n_states = 2  # af_advance_num_steps(af_heuns_method)
@@ -480,9 +484,19 @@ class Simulation:
         self.tree.gc_tree(self.i_efld)
 
     def field_compute(self, s_in, have_guess=True):
-        """field_compute (src/m_field.f90:405-485); returns the residuals."""
+        """field_compute (src/m_field.f90:405-485); returns the residuals.
+
+        With the rhs folded into the last update (fused_rhs) and a guess, the
+        first V-cycle runs before max|rhs| is read, and both maxima come back
+        in one transfer (the threshold is first used after that V-cycle)."""
+        vres = []
         if self.fused_rhs and self.fluid.rhs_valid(s_in):
-            max_rhs = self.fluid.rhs_maxabs(s_in)
+            if have_guess and self.num_vcycles >= 1 and self._defer_ok:
+                self.mg.fas_vcycle_fold()
+                r0, max_rhs = self.tree.fetch_reduced(capi.SLOT_MAXRES, capi.SLOT_RHS)
+                vres.append(r0)
+            else:
+                max_rhs = self.fluid.rhs_maxabs(s_in)
         else:
             max_rhs = self.fluid.field_set_rhs_maxabs(self.i_rhs, s_in)
         # with an electrode the initial convergence test is less strict
@@ -502,11 +516,8 @@ class Simulation:
                         break
             else:
                 raise RuntimeError("No convergence in initial field computation")
-        vres = []
-        for _ in range(self.num_vcycles):
+        while len(vres) < self.num_vcycles and not (vres and vres[-1] < threshold):
             vres.append(self.mg.fas_vcycle_maxres())
-            if vres[-1] < threshold:
-                break
         self.field_from_potential()
         return res + vres
 

@@ -214,6 +214,14 @@ class Tree:
         self.lib.call("tree_maxabs_cc", self.h, iv, C.byref(out))
         return out.value
 
+    def fetch_reduced(self, *slots):
+        """The |x| maxima folded on the device by the deferred entry points
+        (capi.SLOT_MAXRES, capi.SLOT_RHS), read in one transfer."""
+        sl = _i32(slots)
+        out = (C.c_double * len(sl))()
+        self.lib.call("tree_fetch_reduced", self.h, len(sl), sl.ctypes.data_as(capi.P_i32), out)
+        return list(out)
+
     def sum_cc(self, iv, power=1):
         """af_tree_sum_cc (m_af_utils.f90:966-1026): volume-weighted sum of
         cc(iv)**power over the leaf interiors."""
@@ -282,6 +290,12 @@ class Multigrid:
         out = C.c_double()
         self.lib.call("mg_fas_vcycle_maxres", self.h, highest_lvl, C.byref(out))
         return out.value
+
+    def fas_vcycle_fold(self, highest_lvl=0):
+        """fas_vcycle_maxres without reading the maximum: it stays folded in
+        capi.SLOT_MAXRES (Tree.fetch_reduced, Fluid.fetch_step) and the call
+        does not wait for the device."""
+        self.lib.call("mg_fas_vcycle_fold", self.h, highest_lvl)
 
     def set_box_stencil(self, box_id, v, bc_correction=None):
         """The electrode operator stencil of box `box_id` as afivo stores it
@@ -471,6 +485,26 @@ class Fluid:
                       sp.ctypes.data_as(capi.P_i32), wp.ctypes.data_as(capi.P_f64),
                       s_out, int(last_step), int(store_flux), out)
         return out[0], out[1], out[2], out[3]
+
+    def forward_euler_fold(self, dt, s_deriv, s_prev, w_prev, s_out, last_step,
+                           store_flux=False):
+        """forward_euler without reading the limits (fetch_step reads them);
+        does not wait for the device."""
+        sp = _i32(s_prev)
+        wp = np.ascontiguousarray(w_prev, dtype=np.float64)
+        self.lib.call("fluid_forward_euler_fold", self.h, float(dt), s_deriv, len(sp),
+                      sp.ctypes.data_as(capi.P_i32), wp.ctypes.data_as(capi.P_f64),
+                      s_out, int(last_step), int(store_flux))
+
+    def fetch_step(self, last_step, *extra_slots):
+        """(dt_limits(1:4) of the last forward_euler_fold, [extra slot
+        values]) in one transfer."""
+        sl = _i32(extra_slots) if extra_slots else np.zeros(1, np.int32)
+        lim = (C.c_double * 4)()
+        ext = (C.c_double * max(1, len(extra_slots)))()
+        self.lib.call("fluid_fetch_step", self.h, int(last_step), len(extra_slots),
+                      sl.ctypes.data_as(capi.P_i32), lim, ext)
+        return (lim[0], lim[1], lim[2], lim[3]), list(ext)[:len(extra_slots)]
 
 
 def photoi_helmh_compute(modes, coeffs, i_photo, max_rel_res=1e-2, max_fmg=10):

@@ -8,6 +8,7 @@ field_compute (m_field.f90:405-485), forward_euler (m_fluid.f90:21-99) and a
 Heun step (af_advance, afivo/src/m_af_advance.f90:160-164).
 """
 import math
+import os
 
 import numpy as np
 
@@ -85,6 +86,10 @@ class StreamerCase:
         # device step otherwise leaves them on chip)
         self.store_flux = False
         self._fused_rhs = False  # afh_fluid_set_rhs_output active
+        # field_compute(defer=True): the residual list the next species_step
+        # fills (AFH_DEFER=0 turns deferral off, for A/B runs)
+        self._deferred_res = None
+        self._defer_ok = os.environ.get("AFH_DEFER", "1") != "0"
         self.mg = Multigrid(t, IV["phi"], IV["rhs"], IV["tmp"],
                             coarse_cycles=coarse_cycles)
         self._mg_helm = {}
@@ -147,12 +152,24 @@ class StreamerCase:
         self.tree.gc_tree(IV["efld"])
 
     def field_compute(self, s_in, n_vcycles=2, max_rel_residual=1e-4,
-                      check_residual=True):
-        """m_field.f90:405-485 with have_guess = .true.; returns residuals."""
+                      check_residual=True, defer=False):
+        """m_field.f90:405-485 with have_guess = .true.; returns residuals.
+
+        defer (one V-cycle, whose convergence test decides nothing): the
+        residual stays folded on the device and the returned list is filled
+        by the next species_step, which reads it with the step's limits in one
+        transfer; nothing here waits for the device."""
         residuals = []
         threshold = None
         # the library knows whether the last update's rhs of s_in is current
         fused = self._fused_rhs and self.fluid.rhs_valid(s_in)
+        if defer and n_vcycles == 1 and check_residual and self._defer_ok:
+            if not fused:
+                self.fluid.field_set_rhs(IV["rhs"], s_in)
+            self.mg.fas_vcycle_fold()
+            self.field_from_potential()
+            self._deferred_res = residuals
+            return residuals
         if check_residual:
             if fused:
                 max_rhs = self.fluid.rhs_maxabs(s_in)
@@ -184,6 +201,13 @@ class StreamerCase:
     def species_step(self, dt, s_deriv, s_prev, w_prev, s_out, last_step):
         """forward_euler's species part (m_fluid.f90:56-70): flux_upwind_tree +
         flux_update_densities; returns dt_limits(1:4)."""
+        if self._deferred_res is not None:
+            res, self._deferred_res = self._deferred_res, None
+            self.fluid.forward_euler_fold(dt, s_deriv, s_prev, w_prev, s_out,
+                                          last_step, self.store_flux)
+            lim, (max_res,) = self.fluid.fetch_step(last_step, capi.SLOT_MAXRES)
+            res.append(max_res)
+            return lim
         return self.fluid.forward_euler(dt, s_deriv, s_prev, w_prev, s_out,
                                         last_step, self.store_flux)
 

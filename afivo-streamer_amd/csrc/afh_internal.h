@@ -217,6 +217,8 @@ int32_t red_fetch(afh_tree *t, int slot, int n, double *out);
 // the folded values of slots slot .. slot+n_max-1 (maxima) and the next
 // n_min (minima), reduced over the ranks of a sharded tree: on the device
 // before the fetch (dev_reduce), or through the host hook after it
+// several folded slots in one transfer (sharded: all-reduced first)
+int32_t red_fetch_slots(afh_tree *t, int n, const int32_t *slots, double *out);
 int32_t red_reduce_fetch(afh_tree *t, int slot, int n_max, int n_min, double *out,
                          int iv = 0, int level = 0);
 __device__ __forceinline__ int red_shard() {

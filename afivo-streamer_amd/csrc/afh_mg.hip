@@ -3054,7 +3054,8 @@ static int32_t solve_coarse_gs(afh_mg *mg) {
     }
   }
   if (!mg->cs_old) AFH_HIP(hipMalloc(&mg->cs_old, sizeof(double) * t->bsz * nid));
-  auto *red = reinterpret_cast<unsigned long long *>(t->scratch);
+  // slots 6, 7: the step's deferred limits (0..2) stay as they are
+  auto *red = reinterpret_cast<unsigned long long *>(t->scratch) + 6 * RED_SHARDS;
   double *phi = t->ccv(mg->d.i_phi);
   int32_t e;
   for (int it = 1; it <= 200000; it++) {
@@ -3063,13 +3064,13 @@ static int32_t solve_coarse_gs(afh_mg *mg) {
     AFH_LAUNCH_CHECK("k_copy_compact");
     for (int n = 1; n <= 2; n++)
       if ((e = gsrb_half(mg, 1, n, false))) return e;
-    if ((e = red_init(t, 0, 0.0)) || (e = red_init(t, 1, 0.0))) return e;
+    if ((e = red_init(t, 6, 0.0)) || (e = red_init(t, 7, 0.0))) return e;
     hipLaunchKernelGGL(k_change_max, dim3((n3 + 255) / 256, nid), dim3(256), 0,
                        t->stream, phi, mg->cs_old, t->ids.at(1), nc, t->bsz, red);
     AFH_LAUNCH_CHECK("k_change_max");
     double r[2];
-    if ((e = red_finish(t, 0, true)) || (e = red_finish(t, 1, true)) ||
-        (e = red_reduce_fetch(t, 0, 2, 0, r, mg->d.i_phi, 1)))
+    if ((e = red_finish(t, 6, true)) || (e = red_finish(t, 7, true)) ||
+        (e = red_reduce_fetch(t, 6, 2, 0, r, mg->d.i_phi, 1)))
       return e;
     double sp = 2.2250738585072014e-308;  // Fortran spacing(max |phi|)
     if (r[1] > 0) {
@@ -3379,7 +3380,9 @@ static int32_t vcycle_graph(afh_mg *mg, int32_t set_residual, int max_lvl, bool 
   return AFH_OK;
 }
 
-static int32_t vcycle_impl(afh_mg *mg, int32_t set_residual, int32_t hl,
+// max_out: the leaf max|residual| folded into AFH_SLOT_MAXRES, read into
+// max_res when given
+static int32_t vcycle_impl(afh_mg *mg, int32_t set_residual, int32_t hl, bool max_out,
                            double *max_res) {
   if (!mg) return set_error(AFH_ERR_ARG, "null mg");
   afh_tree *t = mg->t;
@@ -3390,23 +3393,27 @@ static int32_t vcycle_impl(afh_mg *mg, int32_t set_residual, int32_t hl,
   int32_t e;
   if ((e = prepare_var(mg))) return e;
   bool done;
-  const bool max_out = set_residual && max_res;
+  max_out = max_out && set_residual;
   if ((e = vcycle_graph(mg, set_residual, max_lvl, max_out, top_stale, done))) return e;
   if (!done && (e = vcycle_body(mg, set_residual, max_lvl, max_out, top_stale))) return e;
   // the up leg filled every level's ghost cells (corners on the last fill)
   if (max_lvl == t->nlvl) mg->phi_gc_gen = t->gen[mg->d.i_phi];
-  return max_out ? residual_fetch(mg, max_res) : AFH_OK;
+  return max_out && max_res ? residual_fetch(mg, max_res) : AFH_OK;
 }
 
 extern "C" {
 
 int32_t afh_mg_fas_vcycle(afh_mg *mg, int32_t set_residual, int32_t hl) {
-  return vcycle_impl(mg, set_residual, hl, nullptr);
+  return vcycle_impl(mg, set_residual, hl, false, nullptr);
 }
 
 int32_t afh_mg_fas_vcycle_maxres(afh_mg *mg, int32_t hl, double *max_res) {
   if (!max_res) return set_error(AFH_ERR_ARG, "null max_res");
-  return vcycle_impl(mg, 1, hl, max_res);
+  return vcycle_impl(mg, 1, hl, true, max_res);
+}
+
+int32_t afh_mg_fas_vcycle_fold(afh_mg *mg, int32_t hl) {
+  return vcycle_impl(mg, 1, hl, true, nullptr);
 }
 
 int32_t afh_mg_coarse_iterations(afh_mg *mg, int32_t *n) {

@@ -2377,14 +2377,40 @@ static void launch_fe_nc(afh_tree *t, const FluxArgs &A, const UpdArgs &U,
 
 extern "C" {
 
-int32_t afh_fluid_forward_euler(afh_fluid *f, double dt, int32_t s_deriv,
-                                int32_t n_prev, const int32_t *s_prev,
-                                const double *w_prev, int32_t s_out,
-                                int32_t last_step, int32_t store_flux,
-                                double *dt_lim) {
-  if (!f || !dt_lim) return set_error(AFH_ERR_ARG, "afh_fluid_forward_euler: null");
+}  // extern "C"
+
+// forward_euler's limits from the folded slots (CFL, sigma; the chemistry
+// minimum on the last step) plus `n_extra` more slots, one transfer
+static int32_t fetch_step(afh_fluid *f, int32_t last_step, int n_extra, const int32_t *extra,
+                          double *dt_lim, double *extra_out) {
+  int32_t slots[RED_SLOTS];
+  double r[RED_SLOTS];
+  int n = 0;
+  slots[n++] = AFH_SLOT_CFL;
+  slots[n++] = AFH_SLOT_SIGMA;
+  if (last_step) slots[n++] = AFH_SLOT_CHEM;
+  if (n_extra < 0 || n_extra > 2)
+    return set_error(AFH_ERR_ARG, "afh_fluid_fetch_step: %d extra slots", n_extra);
+  for (int q = 0; q < n_extra; q++) {
+    if (extra[q] != AFH_SLOT_MAXRES && extra[q] != AFH_SLOT_RHS)
+      return set_error(AFH_ERR_ARG, "afh_fluid_fetch_step: slot %d", extra[q]);
+    slots[n++] = extra[q];
+  }
+  int32_t e;
+  if ((e = red_fetch_slots(f->t, n, slots, r))) return e;
+  flux_dt_limits(r, dt_lim);
+  dt_lim[2] = last_step ? r[2] : 1e100;
+  dt_lim[3] = 1e100;
+  for (int q = 0; q < n_extra; q++) extra_out[q] = r[n - n_extra + q];
+  return AFH_OK;
+}
+
+// forward_euler's device work: flux_upwind_tree + flux_update_densities (or
+// the fused kernel), the limits folded into slots 0..2 for fetch_step
+static int32_t fe_dev(afh_fluid *f, double dt, int32_t s_deriv, int32_t n_prev,
+                      const int32_t *s_prev, const double *w_prev, int32_t s_out,
+                      int32_t last_step, int32_t store_flux) {
   afh_tree *t = f->t;
-  AFH_LIVE(t, "afh_fluid_forward_euler");
   const int nc = t->nc, n3 = nc * nc * nc;
   const int iv = f->d.i_electron + s_deriv;
   if (iv < 1 || iv > t->nvc) return set_error(AFH_ERR_ARG, "bad s_deriv");
@@ -2411,16 +2437,10 @@ int32_t afh_fluid_forward_euler(afh_fluid *f, double dt, int32_t s_deriv,
                      f->rhs_iv == 0 && f->d.i_gas_dens <= 0 && f->d.i_photo <= 0 &&
                      n_prev <= 2 && !alias && f->d.limiter == AFH_LIM_KOREN;
   if (!fused) {
-    // flux and update back to back on the stream, one fetch of the three
-    // limits (the flux maxima are not needed before the update)
-    double r[3] = {0.0, 0.0, 1e100};
-    if ((e = flux_tree_dev(f, s_deriv)) ||
-        (e = update_dev(f, dt, s_deriv, n_prev, s_prev, w_prev, s_out, last_step)) ||
-        (e = red_reduce_fetch(t, 0, 2, last_step ? 1 : 0, r)))
-      return e;
-    flux_dt_limits(r, dt_lim);
-    dt_lim[2] = r[2], dt_lim[3] = 1e100;
-    return AFH_OK;
+    // flux and update back to back on the stream (the flux maxima are not
+    // needed before the update)
+    if ((e = flux_tree_dev(f, s_deriv))) return e;
+    return update_dev(f, dt, s_deriv, n_prev, s_prev, w_prev, s_out, last_step);
   }
   t->touch(iv);
   f->touch_state(s_out);
@@ -2454,14 +2474,39 @@ int32_t afh_fluid_forward_euler(afh_fluid *f, double dt, int32_t s_deriv,
     AFH_LAUNCH_CHECK("k_fe_lds");
   }
   if ((e = red_finish(t, 0, true)) || (e = red_finish(t, 1, true))) return e;
-  if (last_step && (e = red_finish(t, 2, false))) return e;
-  double r[3] = {0.0, 0.0, 1e100};
-  if ((e = red_reduce_fetch(t, 0, 2, last_step ? 1 : 0, r))) return e;
-  dt_lim[0] = 1 / r[0];
-  dt_lim[1] = 8.8541878176e-12 / (1.6022e-19 * std::max(r[1], 1e-100));
-  dt_lim[2] = r[2];
-  dt_lim[3] = 1e100;
-  return AFH_OK;
+  return last_step ? red_finish(t, 2, false) : AFH_OK;
+}
+
+extern "C" {
+
+int32_t afh_fluid_forward_euler(afh_fluid *f, double dt, int32_t s_deriv,
+                                int32_t n_prev, const int32_t *s_prev,
+                                const double *w_prev, int32_t s_out,
+                                int32_t last_step, int32_t store_flux,
+                                double *dt_lim) {
+  if (!f || !dt_lim) return set_error(AFH_ERR_ARG, "afh_fluid_forward_euler: null");
+  AFH_LIVE(f->t, "afh_fluid_forward_euler");
+  int32_t e;
+  if ((e = fe_dev(f, dt, s_deriv, n_prev, s_prev, w_prev, s_out, last_step, store_flux)))
+    return e;
+  return fetch_step(f, last_step, 0, nullptr, dt_lim, nullptr);
+}
+
+int32_t afh_fluid_forward_euler_fold(afh_fluid *f, double dt, int32_t s_deriv,
+                                     int32_t n_prev, const int32_t *s_prev,
+                                     const double *w_prev, int32_t s_out,
+                                     int32_t last_step, int32_t store_flux) {
+  if (!f) return set_error(AFH_ERR_ARG, "afh_fluid_forward_euler_fold: null");
+  AFH_LIVE(f->t, "afh_fluid_forward_euler_fold");
+  return fe_dev(f, dt, s_deriv, n_prev, s_prev, w_prev, s_out, last_step, store_flux);
+}
+
+int32_t afh_fluid_fetch_step(afh_fluid *f, int32_t last_step, int32_t n_extra,
+                             const int32_t *extra_slots, double *dt_lim, double *extra) {
+  if (!f || !dt_lim || (n_extra > 0 && (!extra_slots || !extra)))
+    return set_error(AFH_ERR_ARG, "afh_fluid_fetch_step: null");
+  AFH_LIVE(f->t, "afh_fluid_fetch_step");
+  return fetch_step(f, last_step, n_extra, extra_slots, dt_lim, extra);
 }
 
 }  // extern "C"

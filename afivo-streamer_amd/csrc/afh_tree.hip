@@ -543,6 +543,54 @@ int32_t red_reduce_fetch(afh_tree *t, int slot, int n_max, int n_min, double *ou
   return AFH_OK;
 }
 
+// Any folded slots in one transfer (the deferred reductions of a step):
+// with a device all-reduce, each run of consecutive slots of one kind is
+// all-reduced in place first; with a host hook, each kind's values are
+// reduced in one call after the fetch. Slot AFH_SLOT_CHEM is a minimum,
+// every other slot a maximum.
+int32_t red_fetch_slots(afh_tree *t, int n, const int32_t *slots, double *out) {
+  if (n < 1 || n > RED_SLOTS) return set_error(AFH_ERR_ARG, "fetch of %d slots", n);
+  int lo = RED_SLOTS, hi = -1;
+  for (int q = 0; q < n; q++) {
+    if (slots[q] < 0 || slots[q] >= RED_SLOTS)
+      return set_error(AFH_ERR_ARG, "bad reduction slot %d", slots[q]);
+    lo = std::min(lo, (int)slots[q]), hi = std::max(hi, (int)slots[q]);
+  }
+  auto is_min = [](int s) { return s == AFH_SLOT_CHEM; };
+  auto *keys = reinterpret_cast<unsigned long long *>(t->scratch) +
+               (size_t)RED_SLOTS * RED_SHARDS;
+  int32_t e;
+  if (t->hook && t->dev_reduce) {
+    bool want[RED_SLOTS] = {};
+    for (int q = 0; q < n; q++) want[slots[q]] = true;
+    for (int s = lo; s <= hi;) {
+      if (!want[s]) { s++; continue; }
+      int r = s + 1;
+      while (r <= hi && want[r] && is_min(r) == is_min(s)) r++;
+      if ((e = t->dev_reduce(t->hook_ctx, is_min(s) ? AFH_HOOK_MIN : AFH_HOOK_MAX, keys + s,
+                             r - s)))
+        return e;
+      s = r;
+    }
+  }
+  double v[RED_SLOTS];
+  if ((e = red_fetch(t, lo, hi - lo + 1, v))) return e;
+  for (int q = 0; q < n; q++) out[q] = v[slots[q] - lo];
+  if (t->hook && !t->dev_reduce) {
+    for (int kind = 0; kind < 2; kind++) {
+      double w[RED_SLOTS];
+      int m = 0;
+      for (int q = 0; q < n; q++)
+        if (is_min(slots[q]) == (kind == 1)) w[m++] = out[q];
+      if (m && (e = call_hook(t, kind ? AFH_HOOK_MIN : AFH_HOOK_MAX, 0, 0, w, m))) return e;
+      m = 0;
+      for (int q = 0; q < n; q++)
+        if (is_min(slots[q]) == (kind == 1)) out[q] = w[m++];
+    }
+  }
+  return AFH_OK;
+}
+
 // max |x| over the interiors of the listed boxes -> sharded atomicMax
 __global__ void k_maxabs(const double *__restrict__ v,
                          const int32_t *__restrict__ ids, int nc, size_t bsz,
@@ -1167,6 +1215,16 @@ int32_t afh_tree_reduce_loc(afh_tree *t, int32_t iv, int32_t op, double *out,
     loc[3] = lix < 0 ? -1 : lix / (nc * nc) + 1;
   }
   return call_hook(t, is_min ? AFH_HOOK_MIN : AFH_HOOK_MAX, 0, iv, out, 1);
+}
+
+int32_t afh_tree_fetch_reduced(afh_tree *t, int32_t n, const int32_t *slots, double *out) {
+  if (!t || !slots || !out) return set_error(AFH_ERR_ARG, "afh_tree_fetch_reduced: null");
+  AFH_LIVE(t, "afh_tree_fetch_reduced");
+  if (n < 1 || n > 2) return set_error(AFH_ERR_ARG, "afh_tree_fetch_reduced: %d slots", n);
+  for (int q = 0; q < n; q++)
+    if (slots[q] != AFH_SLOT_MAXRES && slots[q] != AFH_SLOT_RHS)
+      return set_error(AFH_ERR_ARG, "afh_tree_fetch_reduced: slot %d", slots[q]);
+  return red_fetch_slots(t, n, slots, out);
 }
 
 int32_t afh_tree_set_stream(afh_tree *t, void *stream) {

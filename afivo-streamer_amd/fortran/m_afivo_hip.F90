@@ -124,6 +124,9 @@ module m_afivo_hip
   integer(c_int32_t), parameter :: AFH_PROLONG_LIMIT = 2
   ! afh_tree_reduce_loc operations
   integer(c_int32_t), parameter :: AFH_RED_MAX = 1, AFH_RED_MIN = 2, AFH_RED_MAXABS = 3
+  ! deferred reduction slots (afh_tree_fetch_reduced, afh_fluid_fetch_step)
+  integer(c_int32_t), parameter :: AFH_SLOT_CFL = 0, AFH_SLOT_SIGMA = 1, &
+       AFH_SLOT_CHEM = 2, AFH_SLOT_MAXRES = 3, AFH_SLOT_RHS = 4
   ! exchange hook kinds (afh_tree_set_hook)
   integer(c_int32_t), parameter :: AFH_HOOK_HALO = 1, AFH_HOOK_RIMS = 2, &
        AFH_HOOK_RESTRICT = 3, AFH_HOOK_MAX = 4, AFH_HOOK_MIN = 5, AFH_HOOK_CFLUX = 6, &
@@ -373,6 +376,25 @@ module m_afivo_hip
        real(c_double), intent(out) :: max_res
        integer(c_int32_t)        :: afh_mg_fas_vcycle_maxres
      end function afh_mg_fas_vcycle_maxres
+
+     ! the same with max|residual| left folded in AFH_SLOT_MAXRES
+     function afh_mg_fas_vcycle_fold(mg, highest_lvl) &
+          bind(C, name=afh_pfx//"mg_fas_vcycle_fold")
+       import
+       type(c_ptr), value        :: mg
+       integer(c_int32_t), value :: highest_lvl
+       integer(c_int32_t)        :: afh_mg_fas_vcycle_fold
+     end function afh_mg_fas_vcycle_fold
+
+     function afh_tree_fetch_reduced(t, n, slots, vals) &
+          bind(C, name=afh_pfx//"tree_fetch_reduced")
+       import
+       type(c_ptr), value             :: t
+       integer(c_int32_t), value      :: n
+       integer(c_int32_t), intent(in) :: slots(*)
+       real(c_double), intent(out)    :: vals(*)
+       integer(c_int32_t)             :: afh_tree_fetch_reduced
+     end function afh_tree_fetch_reduced
 
      function afh_mg_compute_phi_gradient(mg, i_fc, fac, i_norm) &
           bind(C, name=afh_pfx//"mg_compute_phi_gradient")
@@ -726,6 +748,29 @@ module m_afivo_hip
        real(c_double), intent(out)    :: dt_lim(4)
        integer(c_int32_t)             :: afh_fluid_forward_euler
      end function afh_fluid_forward_euler
+
+     function afh_fluid_forward_euler_fold(f, dt, s_deriv, n_prev, s_prev, w_prev, &
+          s_out, last_step, store_flux) &
+          bind(C, name=afh_pfx//"fluid_forward_euler_fold")
+       import
+       type(c_ptr), value             :: f
+       real(c_double), value          :: dt
+       integer(c_int32_t), value      :: s_deriv, n_prev
+       integer(c_int32_t), intent(in) :: s_prev(*)
+       real(c_double), intent(in)     :: w_prev(*)
+       integer(c_int32_t), value      :: s_out, last_step, store_flux
+       integer(c_int32_t)             :: afh_fluid_forward_euler_fold
+     end function afh_fluid_forward_euler_fold
+
+     function afh_fluid_fetch_step(f, last_step, n_extra, extra_slots, dt_lim, extra) &
+          bind(C, name=afh_pfx//"fluid_fetch_step")
+       import
+       type(c_ptr), value             :: f
+       integer(c_int32_t), value      :: last_step, n_extra
+       integer(c_int32_t), intent(in) :: extra_slots(*)
+       real(c_double), intent(out)    :: dt_lim(4), extra(*)
+       integer(c_int32_t)             :: afh_fluid_fetch_step
+     end function afh_fluid_fetch_step
 
      function afh_profile_enable(t, kclass) bind(C, name=afh_pfx//"profile_enable")
        import

@@ -98,11 +98,13 @@ def unit_step(case, dt, k):
     dt limits."""
     if hasattr(case, "pre_step"):
         case.pre_step(k)
+    # defer: the V-cycle's residual is read with the species step's limits,
+    # one host synchronisation per sub-step (afh_mg_fas_vcycle_fold)
     if k % 2 == 0:
-        res = case.field_compute(0, n_vcycles=1)
+        res = case.field_compute(0, n_vcycles=1, defer=True)
         d = case.species_step(dt, 0, [0], [1.0], 1, False)
     else:
-        res = case.field_compute(1, n_vcycles=1)
+        res = case.field_compute(1, n_vcycles=1, defer=True)
         d = case.species_step(0.5 * dt, 1, [0, 1], [0.5, 0.5], 0, True)
     return res, d
 
@@ -126,7 +128,7 @@ class DriverCase:
     def shard(self):
         return self.sim.shard
 
-    def field_compute(self, s, n_vcycles=2):
+    def field_compute(self, s, n_vcycles=2, defer=False):
         return self.sim.field_compute(s, True)
 
     def species_step(self, dt, s_deriv, s_prev, w_prev, s_out, last):

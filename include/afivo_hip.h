@@ -246,6 +246,20 @@ int32_t afh_gc_tree(afh_tree *t, int32_t iv, int32_t corners);
 int32_t afh_restrict_tree(afh_tree *t, int32_t iv);
 /* af_tree_copy_cc (m_af_utils.f90) / copy_current_state (streamer.f90:639) */
 int32_t afh_tree_copy_cc(afh_tree *t, int32_t iv_from, int32_t iv_to);
+/* Deferred reductions. The device work of a step folds its maxima and
+ * minima into reduction slots on the device; the *_fold entry points leave
+ * them there and return without waiting, and afh_tree_fetch_reduced reads
+ * any of them in one transfer -- one host synchronisation per step instead
+ * of one per reduction. A slot holds its last fold until the next operation
+ * that uses it. Sharded trees reduce over ranks in the fetch. */
+#define AFH_SLOT_CFL 0    /* flux_upwind_tree: max CFL sum (dt_lim(1) = 1 / v) */
+#define AFH_SLOT_SIGMA 1  /* flux_upwind_tree: max conductivity */
+#define AFH_SLOT_CHEM 2   /* density update, last step: min chemistry dt (a minimum) */
+#define AFH_SLOT_MAXRES 3 /* V-cycle with residual: leaf max|residual| */
+#define AFH_SLOT_RHS 4    /* density update with the rhs output: max|rhs| */
+/* the |x| maxima AFH_SLOT_MAXRES and AFH_SLOT_RHS (n <= 2); the limits are
+ * read by afh_fluid_fetch_step */
+int32_t afh_tree_fetch_reduced(afh_tree *t, int32_t n, const int32_t *slots, double *out);
 /* af_tree_maxabs_cc over leaf interiors (m_af_utils.f90:773-784) */
 int32_t afh_tree_maxabs_cc(afh_tree *t, int32_t iv, double *out);
 /* af_tree_sum_cc (m_af_utils.f90:966-1026): sum over the leaf interiors of
@@ -277,6 +291,12 @@ int32_t afh_mg_fas_vcycle(afh_mg *mg, int32_t set_residual,
  * of tmp). Same results as the two calls. */
 int32_t afh_mg_fas_vcycle_maxres(afh_mg *mg, int32_t highest_lvl,
                                  double *max_res);
+/* afh_mg_fas_vcycle_maxres without reading the maximum: it stays folded in
+ * reduction slot AFH_SLOT_MAXRES (afh_tree_fetch_reduced,
+ * afh_fluid_fetch_step) and the call returns without waiting for the device.
+ * field_compute with one V-cycle (multigrid_num_vcycles = 1) needs the
+ * residual only after the step. */
+int32_t afh_mg_fas_vcycle_fold(afh_mg *mg, int32_t highest_lvl);
 /* mg_fas_fmg (m_af_multigrid.f90:137-180): full multigrid; have_guess = 0
  * starts from phi = 0 on levels >= 2 (field_compute at start-up,
  * src/m_field.f90:447-470) */
@@ -398,6 +418,17 @@ int32_t afh_fluid_forward_euler(afh_fluid *f, double dt, int32_t s_deriv,
                                 const double *w_prev, int32_t s_out,
                                 int32_t last_step, int32_t store_flux,
                                 double *dt_lim);
+/* afh_fluid_forward_euler without reading the limits (slots AFH_SLOT_CFL,
+ * _SIGMA and, on the last step, _CHEM); returns without waiting. */
+int32_t afh_fluid_forward_euler_fold(afh_fluid *f, double dt, int32_t s_deriv,
+                                     int32_t n_prev, const int32_t *s_prev,
+                                     const double *w_prev, int32_t s_out,
+                                     int32_t last_step, int32_t store_flux);
+/* dt_lim[4] of the last afh_fluid_forward_euler_fold, as
+ * afh_fluid_forward_euler returns them, plus n_extra more slots
+ * (AFH_SLOT_MAXRES, AFH_SLOT_RHS; n_extra <= 2) into extra -- one transfer. */
+int32_t afh_fluid_fetch_step(afh_fluid *f, int32_t last_step, int32_t n_extra,
+                             const int32_t *extra_slots, double *dt_lim, double *extra);
 
 /* Regrid (af_adjust_refinement's data movement, m_af_core.f90:697-881).
  * afh_set_cc_prolong registers the prolongation of variable iv

@@ -65,6 +65,10 @@ struct afh_tree {
   /* sharded tree: leaves another rank sums (replicated levels count on rank
    * 0 only, as the device library); NULL on an unsharded tree */
   unsigned char *sum_skip;
+  /* the deferred reductions (afo_*_fold): the last value of each slot --
+   * the limits (0..2) already reduced over ranks, the |x| maxima (3, 4) this
+   * rank's, reduced when they are read */
+  double slot[8];
 };
 
 #define LIVE(t)                                                               \
@@ -608,8 +612,14 @@ int32_t afo_tree_copy_cc(afh_tree *t, int32_t a, int32_t b) {
 }
 
 /* af_tree_maxabs_cc over leaf interiors, m_af_utils.f90:773-784, 852-862 */
+static double maxabs_local(afh_tree *t, int32_t iv);
 int32_t afo_tree_maxabs_cc(afh_tree *t, int32_t iv, double *out) {
   LIVE(t);
+  *out = maxabs_local(t, iv);
+  return hook(t, AFH_HOOK_MAX, 0, iv, out, 1);
+}
+
+static double maxabs_local(afh_tree *t, int32_t iv) {
   double mx = -HUGE_VAL;
   int nc = t->nc;
   for (int l = 1; l <= t->nlvl; l++)
@@ -622,8 +632,7 @@ int32_t afo_tree_maxabs_cc(afh_tree *t, int32_t iv, double *out) {
             if (v > mx) mx = v;
           }
     }
-  *out = mx;
-  return hook(t, AFH_HOOK_MAX, 0, iv, out, 1);
+  return mx;
 }
 
 /* gfortran's real ** integer (_gfortran_pow_r8_i4): binary powering */
@@ -1507,6 +1516,25 @@ int32_t afo_mg_fas_vcycle_maxres(afh_mg *mg, int32_t hl, double *max_res) {
   return e ? e : afo_tree_maxabs_cc(mg->t, mg->d.i_tmp, max_res);
 }
 
+/* afh_mg_fas_vcycle_fold: the maximum kept for afo_tree_fetch_reduced */
+int32_t afo_mg_fas_vcycle_fold(afh_mg *mg, int32_t hl) {
+  int32_t e = afo_mg_fas_vcycle(mg, 1, hl);
+  if (!e) mg->t->slot[AFH_SLOT_MAXRES] = maxabs_local(mg->t, mg->d.i_tmp);
+  return e;
+}
+
+/* the |x| maxima only (the limits are read by afo_fluid_fetch_step) */
+int32_t afo_tree_fetch_reduced(afh_tree *t, int32_t n, const int32_t *slots, double *out) {
+  LIVE(t);
+  if (n < 1 || n > 2) return fail(AFH_ERR_ARG, "fetch of %d slots", n);
+  for (int q = 0; q < n; q++) {
+    if (slots[q] != AFH_SLOT_MAXRES && slots[q] != AFH_SLOT_RHS)
+      return fail(AFH_ERR_ARG, "bad reduction slot %d", slots[q]);
+    out[q] = t->slot[slots[q]];
+  }
+  return hook(t, AFH_HOOK_MAX, 0, 0, out, n);
+}
+
 /* mg_fas_fmg, m_af_multigrid.f90:137-180; set_coarse_phi_rhs (742-776) is
  * update_coarse without restoring tmp -- the extra tmp = phi on the parents
  * is overwritten by the phi -> tmp copies below before tmp is read again;
@@ -2307,6 +2335,7 @@ int32_t afo_flux_update_densities(afh_fluid *fl, double dt, int32_t s_deriv,
             }
       }
     fl->rhs_max = mx;
+    t->slot[AFH_SLOT_RHS] = mx;
   }
   for (int s = 0; s < fl->d.n_species; s++) touch(t, fl->d.species_iv[s] + s_out);
   if (fl->rhs_iv > 0) {
@@ -2339,6 +2368,31 @@ int32_t afo_fluid_forward_euler(afh_fluid *f, double dt, int32_t s_deriv,
     return e;
   dt_lim[0] = a[0], dt_lim[1] = a[1], dt_lim[2] = b[0], dt_lim[3] = b[1];
   return AFH_OK;
+}
+
+/* afh_fluid_forward_euler_fold / afh_fluid_fetch_step: the limits kept on
+ * the tree until they are read (slots 0..2 hold dt_lim(1:3)) */
+int32_t afo_fluid_forward_euler_fold(afh_fluid *f, double dt, int32_t s_deriv,
+                                     int32_t n_prev, const int32_t *s_prev,
+                                     const double *w_prev, int32_t s_out,
+                                     int32_t last_step, int32_t store_flux) {
+  double lim[4];
+  int32_t e = afo_fluid_forward_euler(f, dt, s_deriv, n_prev, s_prev, w_prev, s_out,
+                                      last_step, store_flux, lim);
+  if (e) return e;
+  for (int q = 0; q < 3; q++) f->t->slot[q] = lim[q];
+  return AFH_OK;
+}
+
+int32_t afo_fluid_fetch_step(afh_fluid *f, int32_t last_step, int32_t n_extra,
+                             const int32_t *extra_slots, double *dt_lim, double *extra) {
+  afh_tree *t = f->t;
+  LIVE(t);
+  if (n_extra < 0 || n_extra > 2) return fail(AFH_ERR_ARG, "%d extra slots", n_extra);
+  dt_lim[0] = t->slot[0], dt_lim[1] = t->slot[1];
+  dt_lim[2] = last_step ? t->slot[2] : 1e100;
+  dt_lim[3] = 1e100;
+  return n_extra ? afo_tree_fetch_reduced(t, n_extra, extra_slots, extra) : AFH_OK;
 }
 
 /* Kernel timing is a device concept; the oracle accepts and ignores it. */

@@ -59,6 +59,8 @@ int32_t afo_mg_fas_vcycle(afh_mg *mg, int32_t set_residual,
                           int32_t highest_lvl);
 int32_t afo_mg_fas_vcycle_maxres(afh_mg *mg, int32_t highest_lvl,
                                  double *max_res);
+int32_t afo_mg_fas_vcycle_fold(afh_mg *mg, int32_t highest_lvl);
+int32_t afo_tree_fetch_reduced(afh_tree *t, int32_t n, const int32_t *slots, double *out);
 int32_t afo_mg_fas_fmg(afh_mg *mg, int32_t set_residual, int32_t have_guess);
 int32_t afo_mg_coarse_iterations(afh_mg *mg, int32_t *n);
 int32_t afo_mg_compute_phi_gradient(afh_mg *mg, int32_t i_fc, double fac,
@@ -89,6 +91,12 @@ int32_t afo_fluid_forward_euler(afh_fluid *f, double dt, int32_t s_deriv,
                                 const double *w_prev, int32_t s_out,
                                 int32_t last_step, int32_t store_flux,
                                 double *dt_lim);
+int32_t afo_fluid_forward_euler_fold(afh_fluid *f, double dt, int32_t s_deriv,
+                                     int32_t n_prev, const int32_t *s_prev,
+                                     const double *w_prev, int32_t s_out,
+                                     int32_t last_step, int32_t store_flux);
+int32_t afo_fluid_fetch_step(afh_fluid *f, int32_t last_step, int32_t n_extra,
+                             const int32_t *extra_slots, double *dt_lim, double *extra);
 int32_t afo_profile_enable(afh_tree *t, int32_t kclass);
 int32_t afo_profile_read(afh_tree *t, double *total_ms, int64_t *launches,
                          double *bytes);
