@@ -176,6 +176,30 @@ class Partition:
                     lo, hi = [1, 1, 1], [nc, nc, nc]
                     lo[d] = hi[d] = f
                     out.append((q, d, *lo, *hi))
+        # a replicated refined box whose children are sharded: the face
+        # quarter each child covers on the replicated coarse neighbour goes
+        # from the child's owner to every other rank
+        h = nc // 2
+        nbs = np.asarray(self.topo["meta_neighbors"])
+        for l in range(1, self.nlvl + 1):
+            for p in np.asarray(self.topo["lvl_parents_%d" % l], np.int64):
+                if self.owner[p - 1] >= 0 or recv_rank == send_rank:
+                    continue
+                for nb in range(1, 7):
+                    q = int(nbs[p - 1][nb - 1])
+                    if q <= 0 or self.children[q - 1][0] != 0 or self.owner[q - 1] >= 0:
+                        continue
+                    d, side = (nb - 1) // 2, (nb - 1) % 2
+                    f = nc + 1 if side == 0 else 1
+                    for ch in range(8):
+                        c = int(self.children[p - 1][ch])
+                        cd = (ch & 1, (ch >> 1) & 1, (ch >> 2) & 1)
+                        if cd[d] != side or c <= 0 or self.owner[c - 1] != send_rank:
+                            continue
+                        lo = [h * cd[k] + 1 for k in range(3)]
+                        hi = [h * cd[k] + h for k in range(3)]
+                        lo[d] = hi[d] = f
+                        out.append((q, d, *lo, *hi))
         return out
 
     def octant_regions(self, send_rank):

@@ -165,6 +165,30 @@ inline std::vector<Region> cflux_regions(const Topo &t, const std::vector<int32_
         out.push_back(Region{q, d, lo[0], lo[1], lo[2], hi[0], hi[1], hi[2]});
       }
     }
+  // a replicated refined box whose children are sharded (the level below
+  // Lp): every rank computes the coarse leaf neighbour's face, but only the
+  // owner of a child has that child's fluxes -- the face quarter each child
+  // covers goes from the child's owner to every other rank
+  const int h = t.nc / 2;
+  for (int l = 1; l <= t.nlvl; l++)
+    for (int32_t p : t.parents[l - 1]) {
+      if (owner[p - 1] >= 0) continue;
+      for (int nb = 1; nb <= 6; nb++) {
+        const int q = t.m[p - 1].neighbors[nb - 1];
+        if (q <= 0 || t.m[q - 1].children[0] != 0 || owner[q - 1] >= 0 || recv == send) continue;
+        const int d = (nb - 1) / 2, side = (nb - 1) % 2;  // side 0: q below p
+        const int f = side == 0 ? t.nc + 1 : 1;
+        for (int ch = 0; ch < 8; ch++) {
+          const int c = t.m[p - 1].children[ch];
+          const int cd[3] = {ch & 1, (ch >> 1) & 1, (ch >> 2) & 1};  // af_child_dix
+          if (cd[d] != side || c <= 0 || owner[c - 1] != send) continue;
+          int lo[3], hi[3];
+          for (int k = 0; k < 3; k++) lo[k] = h * cd[k] + 1, hi[k] = h * cd[k] + h;
+          lo[d] = hi[d] = f;
+          out.push_back(Region{q, d, lo[0], lo[1], lo[2], hi[0], hi[1], hi[2]});
+        }
+      }
+    }
   return out;
 }
 

@@ -123,6 +123,10 @@ struct afh_tree {
   // boxes up to 16^3: faces, edges and corners of a level in one launch
   // (k_gc_box, AFH_GC_BOX=0 for the two-launch form)
   bool gc_box = true;
+  // independent per-box work of every leaf level in one launch where the
+  // kernel reads the box's level data from its meta record (flux of small
+  // boxes, density update, residual; AFH_ALL_LVL=0: one launch per level)
+  bool all_lvl_launch = true;
   struct Plan {
     int32_t *d_reg = nullptr;  // n x 7 (id, lo[3], hi[3])
     int64_t *d_off = nullptr;  // n + 1 value offsets

@@ -973,11 +973,15 @@ template <bool MAX, int K>
 __global__ void __launch_bounds__(256)
     k_residual(const double *__restrict__ phi, const double *__restrict__ rhs,
                double *__restrict__ tmp, const int32_t *__restrict__ ids,
-               int nc, size_t bsz, Coef cf, unsigned long long *red) {
+               int nc, size_t bsz, Coef cf0, unsigned long long *red,
+               const Coef *__restrict__ cft = nullptr,
+               const afh_box_meta *__restrict__ meta = nullptr) {
+  // cft: boxes of several levels, the level's coefficients from the table
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   double mx = 0.0;
   if (t < nc * nc * (nc / K)) {
     const int id = ids[blockIdx.y];
+    const Coef cf = cft ? cft[meta[id - 1].lvl - 1] : cf0;
     int i, j, kq;
     cell3(t, nc, i, j, kq);
     const int ng = nc + 2;
@@ -2241,6 +2245,7 @@ struct afh_mg {
   int cycles_host = 0;
   bool cycles_on_dev = false;
   double *d_norm = nullptr;   // k_cs_norm2 partial sums
+  Coef *d_lvl_c = nullptr;    // lvl_c on the device (residual of every level in one launch)
   std::vector<double> h_norm;
   bool rstr_col = true;       // AFH_RSTR_COL=0: one coarse cell per thread (k_rstr_fas)
   int pair_ks = 4;           // AFH_GSRB_PAIR_KS: k chunks on 64..255-box levels (NC = 64;
@@ -2393,6 +2398,9 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
     for (int q = 2; q < 7; q++) s = s + c.c[q];
     c.c[0] = -s - d->helmholtz_lambda;
   }
+  AFH_HIP(hipMalloc(&mg->d_lvl_c, sizeof(Coef) * t->nlvl));
+  AFH_HIP(hipMemcpy(mg->d_lvl_c, mg->lvl_c.data(), sizeof(Coef) * t->nlvl,
+                    hipMemcpyHostToDevice));
   // coarse hierarchy (same rule as oracle/c/afo.c afo_mg_create)
   CsParams &P = mg->P;
   memset(&P, 0, sizeof P);
@@ -2534,6 +2542,7 @@ int32_t afh_mg_destroy(afh_mg *mg) {
   hipFree(mg->cs_iters);
   hipFree(mg->d_cycles);
   hipFree(mg->d_norm);
+  hipFree(mg->d_lvl_c);
   for (LevelList *L : {&mg->ids_c, &mg->ids_v, &mg->leaves_c, &mg->leaves_v,
                        &mg->parents_c, &mg->parents_v, &mg->lsf_leaves})
     hipFree(L->d);
@@ -3271,6 +3280,9 @@ static int32_t residual_levels(afh_mg *mg, int max_lvl, bool max_out) {
   auto *red = reinterpret_cast<unsigned long long *>(t->scratch) + 3 * RED_SHARDS;
   int32_t e;
   if (max_out && (e = red_init(t, 3, 0.0))) return e;
+  // the constant-coefficient boxes of every level in one launch per part
+  // (the level's coefficients from d_lvl_c): levels do not interact here
+  const bool all_lvls = t->all_lvl_launch;
   for (int lvl = 1; lvl <= max_lvl; lvl++) {
     const Coef &cf = mg->lvl_c[lvl - 1];
     for (int part = 0; part < 2; part++) {
@@ -3281,7 +3293,9 @@ static int32_t residual_levels(afh_mg *mg, int max_lvl, bool max_out) {
       const LevelList &Lc = max_out ? (part ? mg->parents_c : mg->leaves_c) : mg->ids_c;
       const LevelList &Lv = max_out ? (part ? mg->parents_v : mg->leaves_v) : mg->ids_v;
       const LevelList &L = cst(mg, A, Lc);
-      const int n = L.n(lvl);
+      const int n_all = L.off[max_lvl] - L.off[0];
+      const bool one = all_lvls && n_all <= 65535;
+      const int n = one ? (lvl == 1 ? n_all : 0) : L.n(lvl);
       const bool mx = max_out && !part;
       if (n) {
         const int kc = nc % AFH_RES_K == 0 ? AFH_RES_K : nc % 4 == 0 ? 4 : 2;
@@ -3292,7 +3306,8 @@ static int32_t residual_levels(afh_mg *mg, int max_lvl, bool max_out) {
                                                                    : k_residual<false, 2>);
         hipLaunchKernelGGL(kern, grid, dim3(256), 0, t->stream,
                            t->ccv(mg->d.i_phi), t->ccv(mg->d.i_rhs),
-                           t->ccv(mg->d.i_tmp), L.at(lvl), nc, t->bsz, cf, red);
+                           t->ccv(mg->d.i_tmp), L.at(lvl), nc, t->bsz, cf, red,
+                           one ? mg->d_lvl_c : nullptr, one ? t->d_boxes : nullptr);
         AFH_LAUNCH_CHECK("k_residual");
       }
       const int nv = mg->any_var ? Lv.n(lvl) : 0;

@@ -238,6 +238,9 @@ struct FluxArgs {
   const double *Ng;
   double inv_dx[3];   // 1/dr per dimension of this level
   int lim;
+  // all leaf levels in one launch (k_flux_staged): the box's 1/dr from its
+  // meta record (the same doubles as the level's, afh_tree_create checks)
+  const afh_box_meta *meta;
 };
 
 // LT_get_col(td_tbl, td_mobility/td_diffusion, x): both columns at the same
@@ -353,6 +356,9 @@ __global__ void __launch_bounds__(256, AFH_FLUX_MINW)
   const int c0 = (k * ng + j) * ng + i;
   const int fcell = ((k - 1) * nf + (j - 1)) * nf + (i - 1);
   const int fd = nf * nf * nf;
+  double idx[3];
+#pragma unroll
+  for (int d = 0; d < 3; d++) idx[d] = A.meta ? 1 / A.meta[id - 1].dr[d] : A.inv_dx[d];
   const int cc[3] = {i, j, k};
   const int st[3] = {1, ng, ng * ng};
   const int fst[3] = {1, nf, nf * nf};
@@ -439,7 +445,7 @@ __global__ void __launch_bounds__(256, AFH_FLUX_MINW)
   for (int d = 0; d < 3; d++) {
     const double u = upwind(L[d][0], L[d][1], L[d][2], L[d][3], ex_lo[d]);
     const double mu = finish(lo_r[d], lo_lf[d], ex_lo[d], ni_lo[d], vl[d], dl[d]);
-    const double flux = vl[d] * u - dl[d] * A.inv_dx[d] * (L[d][2] - L[d][1]);
+    const double flux = vl[d] * u - dl[d] * idx[d] * (L[d][2] - L[d][1]);
     if (active) F[d * fd + fcell] = flux;
     smax = fmax(smax, mu * u);
   }
@@ -455,7 +461,7 @@ __global__ void __launch_bounds__(256, AFH_FLUX_MINW)
   __syncthreads();
 #pragma unroll
   for (int d = 0; d < 3; d++) {
-    const double inv_dx = A.inv_dx[d];
+    const double inv_dx = idx[d];
     double vh, dh;
     if (cc[d] == nc) {
       const double u = upwind(L[d][1], L[d][2], L[d][3], L[d][4], ex_hi[d]);
@@ -517,6 +523,8 @@ struct UpdArgs {
   double inv_N;
   double dt;
   double dt_dr[3];  // dt / dr per dimension of this level
+  // all leaf levels in one launch: dt / dr from the box's meta record
+  const afh_box_meta *meta;
   double dt_chemistry_nmin;
   // variable gas density (m_fluid.f90:339-348): N per cell, the gas species
   // densities gas_frac * N occupy species slots ns .. ns+ng-1 (the host
@@ -1176,9 +1184,12 @@ __global__ void __launch_bounds__(256, AFH_UPD_MINW)
     }
 #pragma unroll
     for (int s = 0; s < NS; s++) y[s] = y[s] + A.dt * der[s];
-    const double div = A.dt_dr[0] * (fx0 - fx1);
-    const double dvy = A.dt_dr[1] * (fy0 - fy1);
-    const double dvz = A.dt_dr[2] * (fz0 - fz1);
+    double dtr[3];
+#pragma unroll
+    for (int d = 0; d < 3; d++) dtr[d] = A.meta ? A.dt / A.meta[id - 1].dr[d] : A.dt_dr[d];
+    const double div = dtr[0] * (fx0 - fx1);
+    const double dvy = dtr[1] * (fy0 - fy1);
+    const double dvz = dtr[2] * (fz0 - fz1);
 #pragma unroll
     for (int s = 0; s < NS; s++)
       if (s == A.e_index) y[s] = y[s] + div + dvy + dvz;
@@ -1238,10 +1249,11 @@ static bool launch_update_net(const UpdArgs &A, afh_tree *t, const dim3 &grid,
 }
 
 template <int NS>
-void launch_update(const UpdArgs &A, afh_tree *t, int l,
+void launch_update(const UpdArgs &A, afh_tree *t, int l, int n_boxes,
                    unsigned long long *red, bool slow, int net = 0) {
+  // boxes leaves.at(l) .. + n_boxes (one level, or every level from 1)
   const int nc = t->nc, n3 = nc * nc * nc;
-  const dim3 grid((n3 / AFH_UPD_KC + 255) / 256, t->leaves.n(l));
+  const dim3 grid((n3 / AFH_UPD_KC + 255) / 256, n_boxes);
   const auto *ids = t->leaves.at(l);
   const bool sd = A.der_q < 0;
   switch (net) {
@@ -2129,6 +2141,7 @@ static FluxArgs flux_args(afh_fluid *f, int iv) {
   A.N_inv = 1 / f->d.gas_number_density;
   A.Ng = f->d.i_gas_dens > 0 ? t->ccv(f->d.i_gas_dens) : nullptr;
   A.lim = f->d.limiter;
+  A.meta = nullptr;
   return A;
 }
 
@@ -2185,6 +2198,7 @@ static int32_t upd_args(afh_fluid *f, double dt, int32_t s_deriv, int32_t n_prev
   A.dt_chemistry_nmin = f->d.dt_chemistry_nmin;
   A.photo = f->d.i_photo > 0 ? t->ccv(f->d.i_photo) : nullptr;
   A.photo_s = f->d.photo_species - 1;
+  A.meta = nullptr;
   // algorithmic bytes per cell: each distinct species state read once, the
   // output written once, |E| and 3 fluxes read
   int distinct = n_prev;
@@ -2212,12 +2226,17 @@ static int32_t flux_tree_dev(afh_fluid *f, int32_t s_deriv) {
   auto *red = reinterpret_cast<unsigned long long *>(t->scratch);
   FluxArgs A = flux_args(f, iv);
   const bool shfl = (64 % nc) == 0;
+  const bool lds = f->d_tdi && (nc == 64 || nc == 32 || nc == 16);
+  // the staged kernel takes each box's 1/dr from its meta record: every leaf
+  // level in one launch (small boxes: one launch instead of one per level)
+  const bool all_lvls = !lds && t->all_lvl_launch && t->leaves.off[t->nlvl] <= 65535;
   for (int l = 1; l <= t->nlvl; l++) {
-    const int n = t->leaves.n(l);
+    const int n = all_lvls ? (l == 1 ? t->leaves.off[t->nlvl] : 0) : t->leaves.n(l);
     if (!n) continue;
     for (int q = 0; q < 3; q++) A.inv_dx[q] = 1 / t->lvl_dr[3 * (l - 1) + q];
+    if (all_lvls) A.meta = t->d_boxes;
     prof_begin(t, AFH_PROF_FLUX);
-    if (f->d_tdi && (nc == 64 || nc == 32 || nc == 16)) {
+    if (lds) {
       switch (nc) {
       case 16: launch_flux_lds<16>(t, A, f->d_tdi, l, red); break;
       case 32: launch_flux_lds<32>(t, A, f->d_tdi, l, red); break;
@@ -2287,13 +2306,16 @@ static int32_t update_dev(afh_fluid *f, double dt, int32_t s_deriv, int32_t n_pr
   f->rhs_state = -1;
   if (A.rhs && (e = red_init(t, 4, 0.0))) return e;
   auto *red = reinterpret_cast<unsigned long long *>(t->scratch) + 2 * RED_SHARDS;
+  // dt / dr from each box's meta record: every leaf level in one launch
+  const bool all_lvls = t->all_lvl_launch && t->leaves.off[t->nlvl] <= 65535;
+  if (all_lvls) A.meta = t->d_boxes;
   for (int l = 1; l <= t->nlvl; l++) {
-    const int n = t->leaves.n(l);
+    const int n = all_lvls ? (l == 1 ? t->leaves.off[t->nlvl] : 0) : t->leaves.n(l);
     if (!n) continue;
     for (int q = 0; q < 3; q++) A.dt_dr[q] = dt / t->lvl_dr[3 * (l - 1) + q];
     prof_begin(t, AFH_PROF_UPDATE);
     switch (A.ns) {
-#define AFH_CASE(N) case N: launch_update<N>(A, t, l, red, f->slow_rates, f->net); break;
+#define AFH_CASE(N) case N: launch_update<N>(A, t, l, n, red, f->slow_rates, f->net); break;
       AFH_CASE(1) AFH_CASE(2) AFH_CASE(3) AFH_CASE(4) AFH_CASE(5) AFH_CASE(6)
       AFH_CASE(7) AFH_CASE(8) AFH_CASE(9) AFH_CASE(10) AFH_CASE(11)
       AFH_CASE(12) AFH_CASE(13) AFH_CASE(14) AFH_CASE(15) AFH_CASE(16)

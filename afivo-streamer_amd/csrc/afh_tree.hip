@@ -789,6 +789,7 @@ static int32_t tree_create_impl(const afh_tree_desc *d, int32_t device,
     return set_error(AFH_ERR_DEVICE, "no HIP device available");
   afh_tree *t = new afh_tree();
   if (const char *env = getenv("AFH_GC_BOX")) t->gc_box = atoi(env) != 0;
+  if (const char *env = getenv("AFH_ALL_LVL")) t->all_lvl_launch = atoi(env) != 0;
   if (const char *env = getenv("AFH_GC_FACES6")) t->gc_faces6 = atoi(env) != 0;
   else t->gc_faces6 = -1;  // by box size
   if (device >= 0) {

@@ -15,6 +15,7 @@ for v in AFH_GC_BOX AFH_PAIR_PUSH AFH_CS_DIRECT_SMALL; do
 done
 CFG=s3 REPS=2 bash scripts/env_bench_ab.sh AFH_GC_BOX,AFH_PAIR_PUSH,AFH_CS_DIRECT_SMALL,AFH_UPD_NET "0 1" || exit $?
 CFG=s3 REPS=2 bash scripts/env_bench_ab.sh AFH_UPD_NET "0 1" || exit $?
+CFG=s3 REPS=2 bash scripts/env_bench_ab.sh AFH_ALL_LVL "0 1" || exit $?
 CFG=s1 REPS=2 bash scripts/env_bench_ab.sh AFH_DEFER "0 1" || exit $?
 CFG=s3 REPS=2 bash scripts/env_bench_ab.sh AFH_DEFER "0 1" || exit $?
 CFG=s1-64 REPS=1 bash scripts/env_bench_ab.sh AFH_GC_BOX "1" || exit $?

@@ -10,7 +10,9 @@ single-rank run bitwise, and so do the time-step limits.
 Cases: the regression test with Helmholtz photoionization and chemistry
 (test_3d_photoi_chem), BASELINE config 4's rod electrode (level-set
 stencils, electrode coarse solve) and config 5's sprite (variable gas
-density, photoionization). The C oracle's CPU twin here; libafivo_hip on
+density, photoionization; level-1 leaves next to refined level-1 boxes, so
+the consistent fluxes of replicated coarse leaves come from the ranks that
+own the fine children). The C oracle's CPU twin here; libafivo_hip on
 the GPU.
 """
 from concurrent.futures import ThreadPoolExecutor
@@ -77,7 +79,7 @@ def _run(lib, name, world, device=-1):
                                                        np.nanmax(np.abs(got[used] - want[used])))
 
 
-@pytest.mark.parametrize("name,world", [("photoi_chem", 2), ("s4_rod", 2)])
+@pytest.mark.parametrize("name,world", [("photoi_chem", 2), ("s4_rod", 2), ("s5_sprite", 2)])
 def test_sharded_driver_oracle_threads_bitwise(name, world):
     _run(capi.oracle_library(), name, world)
 

@@ -9,7 +9,10 @@ read at tree / multigrid / fluid creation):
   workgroup (k_cs_direct_small) vs gather + six transforms + scatter;
 * AFH_UPD_NET: the compiled reaction network (afh_networks.h, k_update's
   unrolled reaction loop) vs the generic loop -- on the S3 tree with
-  air_chemistry_v2 (9 species, 25 reactions) and on S1's old-style model.
+  air_chemistry_v2 (9 species, 25 reactions) and on S1's old-style model;
+* AFH_ALL_LVL: the small-box flux, the density update and the residual of
+  every level in one launch (the box's grid spacing / coefficients from its
+  level) vs one launch per level -- on the S3 tree (8 leaf levels).
 
 The fused forms are also what every other GPU test runs (they are the
 defaults); these tests pin them to the unfused forms on full workloads.
@@ -46,7 +49,7 @@ def _same(a, b):
 
 
 @pytest.mark.parametrize("switch", ["AFH_GC_BOX", "AFH_PAIR_PUSH", "AFH_CS_DIRECT_SMALL",
-                                    "AFH_UPD_NET"])
+                                    "AFH_UPD_NET", "AFH_ALL_LVL"])
 def test_s1_fusion_bitwise(switch, monkeypatch):
     """Config 2 (S1: 512 leaf boxes of 16^3, 4 levels): field solve and four
     unit steps with the fusion on and off."""
@@ -54,6 +57,25 @@ def test_s1_fusion_bitwise(switch, monkeypatch):
     a = _s1(monkeypatch, {switch: "2" if switch == "AFH_UPD_NET" else "1"})
     b = _s1(monkeypatch, {switch: "0"})
     _same(a, b)
+
+
+def test_s3_all_level_launches_bitwise(monkeypatch):
+    """Config 3: two unit steps (field solve with its residuals, flux,
+    update with the chemistry limit) with every leaf level in one launch and
+    with one launch per level."""
+    import bench
+    from afh import capi
+    outs = []
+    for v in ("1", "0"):
+        monkeypatch.setenv("AFH_ALL_LVL", v)
+        case = bench.DriverCase(bench.build_driver_case(capi.hip_library(), 0, "s3"))
+        case.fuse_rhs(True, ghosts=False)
+        res = [bench.unit_step(case, 1e-13, k) for k in range(2)]
+        sim = case.sim
+        outs.append((res, [sim.tree.get_cc(iv) for iv in range(1, sim.n_var_cell + 1)]))
+    assert outs[0][0] == outs[1][0]
+    for x, y in zip(outs[0][1], outs[1][1]):
+        assert np.array_equal(x, y, equal_nan=True)
 
 
 def test_s3_compiled_network_bitwise(monkeypatch):
