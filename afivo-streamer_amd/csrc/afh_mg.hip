@@ -2387,10 +2387,12 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
   // mg_box_lpl_stencil: c(2:7) = 1/dr^2, c(1) = -sum(c(2:)) - lambda
   mg->lvl_c.resize(t->nlvl);
   for (int l = 1; l <= t->nlvl; l++) {
-    const afh_box_meta &m = t->boxes[t->h_ids[l - 1][0] - 1];
+    // the level's spacing over the whole topology (a rank of a sharded tree
+    // may compute no box of a level)
+    const double *dr = &t->lvl_dr[3 * (l - 1)];
     Coef &c = mg->lvl_c[l - 1];
     for (int q = 0; q < 3; q++) {
-      double inv = 1 / (m.dr[q] * m.dr[q]);
+      double inv = 1 / (dr[q] * dr[q]);
       c.c[1 + 2 * q] = inv;
       c.c[2 + 2 * q] = inv;
     }

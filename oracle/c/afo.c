@@ -1357,7 +1357,12 @@ int32_t afo_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
   mg->lsf_dd = calloc(t->nb, sizeof(double *));
   mg->lsf_bv = calloc(t->nb, sizeof(double *));
   for (int l = 1; l <= t->nlvl; l++) {
-    int id = LVL_AT(t, ids, l, 0);
+    /* a box of the level (a rank of a sharded tree may compute none of its
+     * boxes, but stores one) */
+    int id = 0;
+    for (int b = 1; b <= t->nb && !id; b++)
+      if (B(t, b)->lvl == l) id = b;
+    if (!id) return fail(AFH_ERR_ARG, "no box on level %d", l);
     double *c = mg->lvl_c + 7 * (l - 1);
     for (int dd = 0; dd < 3; dd++) {
       double dr = B(t, id)->dr[dd];
