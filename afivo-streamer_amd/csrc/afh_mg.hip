@@ -30,6 +30,7 @@ struct Coef {
 constexpr int MAXMG = 16;
 constexpr int CS_BOTTOM_SWEEPS = 16;   // same constant as oracle/c/afo.c
 constexpr int CS_SMALL_CELLS = 4096;   // MG levels <= 16^3 run in one workgroup
+constexpr int CS_DS_N = 16;            // k_cs_direct_small: LDS matrices up to 16 x 16
 
 struct CsParams {
   int n_mg;
@@ -2140,6 +2141,7 @@ __global__ void __launch_bounds__(1024)
                       const double *__restrict__ e1, const double *__restrict__ e2,
                       double lam) {
   __shared__ double A[CS_SMALL_CELLS], B[CS_SMALL_CELLS];
+  __shared__ double Ml[6][CS_DS_N * CS_DS_N];
   const int nx = P.dims[0][0], ny = P.dims[0][1], nz = P.dims[0][2];
   const int N = nx * ny * nz, n3 = nc * nc * nc;
   const afh_bc bc[6] = {b0, b1, b2, b3, b4, b5};
@@ -2163,22 +2165,41 @@ __global__ void __launch_bounds__(1024)
     }
     A[((gi[2] - 1) * ny + (gi[1] - 1)) * nx + (gi[0] - 1)] = rv;
   }
-  __syncthreads();
   // Q^T along x, y, z (divide), then Q along z, y, x: A -> B -> A -> B -> A -> B -> A
   const double *Ms[6] = {q0, q1, q2, qt2, qt1, qt0};
   const int ds[6] = {0, 1, 2, 2, 1, 0};
+  // grids of at most 16 cells per dimension: the six matrices in LDS and
+  // each output's 2 x n operands loaded before its (ordered) sum, so the
+  // loads overlap instead of each product waiting for its own
+  const bool small = nx <= CS_DS_N && ny <= CS_DS_N && nz <= CS_DS_N;
+  if (small)
+    for (int ps = 0; ps < 6; ps++) {
+      const int d = ds[ps], n = d == 0 ? nx : (d == 1 ? ny : nz);
+      for (int u = threadIdx.x; u < n * n; u += blockDim.x) Ml[ps][u] = Ms[ps][u];
+    }
+  __syncthreads();
   for (int ps = 0; ps < 6; ps++) {
     const double *in = (ps & 1) ? B : A;
     double *out = (ps & 1) ? A : B;
     const int d = ds[ps], n = d == 0 ? nx : (d == 1 ? ny : nz);
     const int st = d == 0 ? 1 : (d == 1 ? nx : nx * ny);
-    const double *M = Ms[ps];
+    const double *M = small ? Ml[ps] : Ms[ps];
     for (int t = threadIdx.x; t < N; t += blockDim.x) {
       const int i = t % nx, j = (t / nx) % ny, k = t / (nx * ny);
       const int co = d == 0 ? i : (d == 1 ? j : k);
       const double *src = in + (t - co * st);
       double s = 0.0;
-      for (int p = 0; p < n; p++) s = s + M[p * n + co] * src[p * st];
+      if (small) {
+        double mv[CS_DS_N], xv[CS_DS_N];
+#pragma unroll
+        for (int p = 0; p < CS_DS_N; p++)
+          if (p < n) mv[p] = M[p * n + co], xv[p] = src[p * st];
+#pragma unroll
+        for (int p = 0; p < CS_DS_N; p++)
+          if (p < n) s = s + mv[p] * xv[p];
+      } else {
+        for (int p = 0; p < n; p++) s = s + M[p * n + co] * src[p * st];
+      }
       if (ps == 2) {
         const double den = ((e0[i] + e1[j]) + e2[k]) - lam;
         s = den != 0.0 ? s / den : 0.0;

@@ -17,7 +17,10 @@ topology, which bench.py writes when AFH_BENCH_TOPO names a file: per level
 the number of boxes, leaves and parents, the box size and the species
 counts. The largest launch of a kernel is taken to cover the level with the
 most boxes of the list the kernel runs over (all boxes, leaves or parents;
-the k-split / tiled pair only runs on levels of 64..255 boxes).
+the k-split / tiled pair only runs on levels of 64..255 boxes); a kernel
+whose grid is (box cells, boxes) -- the update, the small-box flux and the
+residual, which may cover every leaf level in one launch -- takes its boxes
+from the launch's grid.
 
 Usage: prof_steady.py <run_kernel_trace.csv> <K> <out.json> <topo.json>
 """
@@ -83,12 +86,18 @@ def key(name):
     return name
 
 
-def algorithmic(name, topo):
+# kernels whose grid is (cells of a box, boxes): one launch may cover every
+# leaf level (AFH_ALL_LVL), so the boxes are read from the launch's grid
+BOX_GRID = re.compile(r"k_update<|k_flux_staged|k_residual<")
+
+
+def algorithmic(name, topo, grid_y=1):
     for pat, b, lst, filt in rules(topo):
         m = re.search(pat, name)
         if m:
             per_cell = b(m) if callable(b) else b
-            return per_cell * topo["nc"] ** 3 * largest(topo, lst, filt)
+            boxes = grid_y if BOX_GRID.search(name) and grid_y > 1 else largest(topo, lst, filt)
+            return per_cell * topo["nc"] ** 3 * boxes
     return None
 
 
@@ -114,16 +123,17 @@ def main(path, k_steps, out, topo_path):
         g = int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
         per[k][0] += 1
         per[k][1] += d
-        per[k][2].append((g, d))
+        per[k][2].append((g, d, int(r["Grid_Size_Y"])))
     table = []
     for k, (n, tot, lst) in sorted(per.items(), key=lambda kv: -kv[1][1]):
-        gmax = max(g for g, _ in lst)
-        big = [d for g, d in lst if g == gmax]
+        gmax = max(g for g, _, _ in lst)
+        big = [d for g, d, _ in lst if g == gmax]
+        gy = max(y for g, _, y in lst if g == gmax)
         avg = sum(big) / len(big)
         ent = {"kernel": k, "launches_per_step": n / k_steps,
                "us_per_step": tot / k_steps, "share": tot * 1e3 / busy,
                "largest_launch_avg_us": avg}
-        b = algorithmic(k, topo)
+        b = algorithmic(k, topo, gy)
         if b:
             ent.update({"algorithmic_bytes": b, "achieved_TBps": b / (avg * 1e-6) / 1e12,
                         "frac_of_8TBps": b / (avg * 1e-6) / PEAK})
