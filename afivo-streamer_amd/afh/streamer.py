@@ -198,9 +198,19 @@ class StreamerCase:
         return list(self.species_step(dt, s_deriv, s_prev, w_prev, s_out,
                                       i_step == n_steps))
 
-    def species_step(self, dt, s_deriv, s_prev, w_prev, s_out, last_step):
+    def species_step(self, dt, s_deriv, s_prev, w_prev, s_out, last_step, fetch=True):
         """forward_euler's species part (m_fluid.f90:56-70): flux_upwind_tree +
-        flux_update_densities; returns dt_limits(1:4)."""
+        flux_update_densities; returns dt_limits(1:4).
+
+        fetch=False: the limits stay folded on the device and nothing is
+        returned (None). af_advance overwrites dt_lim in every sub-step
+        (m_af_advance.f90:160-164, m_fluid.f90:97-98), so the limits of a
+        Heun step's first sub-step are never read; a deferred V-cycle
+        residual stays pending too (it is overwritten by the next one)."""
+        if not fetch:
+            self.fluid.forward_euler_fold(dt, s_deriv, s_prev, w_prev, s_out,
+                                          last_step, self.store_flux)
+            return None
         if self._deferred_res is not None:
             res, self._deferred_res = self._deferred_res, None
             self.fluid.forward_euler_fold(dt, s_deriv, s_prev, w_prev, s_out,

@@ -100,9 +100,12 @@ def unit_step(case, dt, k):
         case.pre_step(k)
     # defer: the V-cycle's residual is read with the species step's limits,
     # one host synchronisation per sub-step (afh_mg_fas_vcycle_fold)
+    # stage 1's dt limits are never read (af_advance keeps the last
+    # sub-step's, m_af_advance.f90:160-164): they stay on the device and the
+    # host synchronises once per time step, after stage 2
     if k % 2 == 0:
         res = case.field_compute(0, n_vcycles=1, defer=True)
-        d = case.species_step(dt, 0, [0], [1.0], 1, False)
+        d = case.species_step(dt, 0, [0], [1.0], 1, False, fetch=False)
     else:
         res = case.field_compute(1, n_vcycles=1, defer=True)
         d = case.species_step(0.5 * dt, 1, [0, 1], [0.5, 0.5], 0, True)
@@ -131,7 +134,10 @@ class DriverCase:
     def field_compute(self, s, n_vcycles=2, defer=False):
         return self.sim.field_compute(s, True)
 
-    def species_step(self, dt, s_deriv, s_prev, w_prev, s_out, last):
+    def species_step(self, dt, s_deriv, s_prev, w_prev, s_out, last, fetch=True):
+        if not fetch:
+            self.sim.fluid.forward_euler_fold(dt, s_deriv, s_prev, w_prev, s_out, last)
+            return None
         return self.sim.fluid.forward_euler(dt, s_deriv, s_prev, w_prev, s_out, last)
 
     def pre_step(self, k):

@@ -27,7 +27,11 @@ def _unit_steps(lib, monkeypatch, defer, config, device, n=4):
     c.fuse_rhs(True, ghosts=False)
     out = [c.field_compute(0, n_vcycles=2)]
     for k in range(n):
-        out.append(bench.unit_step(c, 1e-13, k))
+        res, lim = bench.unit_step(c, 1e-13, k)
+        # a Heun step's first sub-step fetches nothing (its limits are never
+        # read, m_af_advance.f90:160-164): its V-cycle residual stays on the
+        # device when deferred
+        out.append((res if k % 2 else None, lim))
     state = [c.tree.get_cc(iv) for iv in range(1, c.tree.n_var_cell + 1)]
     c.tree.close()
     return out, state
@@ -69,7 +73,7 @@ def test_unit_step_deferred_oracle(monkeypatch, tiny):
     b = _unit_steps(lib, monkeypatch, False, tiny, -1)
     _same(a, b)
     # the deferred residual list was filled by the species step
-    assert all(len(res) == 1 for res, _ in a[0][1:])
+    assert all(len(res) == 1 for res, _ in a[0][2::2])
 
 
 def test_driver_deferred_oracle(monkeypatch):
