@@ -17,6 +17,8 @@ REPO = os.path.dirname(PKG)
 # kernel variants on one box, scripts/ab.sh)
 HIP_LIB = os.environ.get("AFH_HIP_LIB") or os.path.join(PKG, "csrc", "libafivo_hip.so")
 ORACLE_LIB = os.path.join(REPO, "oracle", "lib", "libafo.so")
+# the NDIM = 2 build (BASELINE config 1; include/afivo_hip_2d.h)
+HIP_LIB_2D = os.path.join(PKG, "csrc", "libafivo_hip_2d.so")
 
 AFH_OK = 0
 BC_DIRICHLET, BC_NEUMANN, BC_CONTINUOUS, BC_DIRICHLET_COPY = -10, -11, -12, -13
@@ -221,7 +223,9 @@ class AfhError(RuntimeError):
 class Library:
     """A loaded C-ABI library; call functions without their prefix."""
 
-    def __init__(self, path, prefix, extra=None):
+    def __init__(self, path, prefix, extra=None, only=None):
+        """only: the entry points the library implements (a subset of
+        SIGNATURES; the 2-D build's, include/afivo_hip_2d.h)."""
         if not os.path.exists(path):
             raise AfhError("shared library not built: %s" % path)
         self.path = path
@@ -230,6 +234,8 @@ class Library:
         sigs = dict(SIGNATURES)
         if extra:
             sigs.update(extra)
+        if only is not None:
+            sigs = {n: sigs[n] for n in only}
         self.fn = {}
         for name, (res, args) in sigs.items():
             f = getattr(self.lib, prefix + name)
@@ -258,6 +264,15 @@ def hip_library():
     return _loaded["hip"]
 
 
+def hip_library_2d():
+    """The NDIM = 2 product library (the entry points of afivo_hip_2d.h).
+    Raises if it was not built -- no CPU fallback."""
+    if "hip2d" not in _loaded:
+        only = [n[len("afh_"):] for n in header_symbols("afivo_hip_2d.h")]
+        _loaded["hip2d"] = Library(HIP_LIB_2D, "afh_", only=only)
+    return _loaded["hip2d"]
+
+
 def oracle_library():
     """The test oracle (oracle/lib/libafo.so)."""
     if "oracle" not in _loaded:
@@ -265,8 +280,8 @@ def oracle_library():
     return _loaded["oracle"]
 
 
-def header_symbols():
-    """Every afh_* function declared in include/afivo_hip.h."""
+def header_symbols(header="afivo_hip.h"):
+    """Every afh_* function declared in include/<header>."""
     import re
-    src = open(os.path.join(REPO, "include", "afivo_hip.h")).read()
+    src = open(os.path.join(REPO, "include", header)).read()
     return sorted(set(re.findall(r"\b(afh_[a-z_0-9]+)\s*\(", src)))

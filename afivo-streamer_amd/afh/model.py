@@ -28,19 +28,27 @@ def _lists(topo, kind):
 
 
 def tree_desc(topo, n_var_cell, n_var_face, box_capacity=0):
-    """afh_tree_desc of a topology dict; returns (desc, arrays it points to)."""
+    """afh_tree_desc of a topology dict; returns (desc, arrays it points to).
+    A 2-D topology (topo["ndim"] == 2: ix / r_min / dr of 2, children and
+    neighbors of 4, a 3 x 3 neighbor_mat) fills the leading entries of the
+    3-D-sized fields (include/afivo_hip_2d.h)."""
     nb = int(topo["n_boxes"])
     meta = np.zeros(nb, capi.BOX_META_DTYPE)
     for k in ("lvl", "ix", "parent", "children", "neighbors", "neighbor_mat", "r_min", "dr"):
-        meta[k] = topo["meta_" + k]
+        v = np.asarray(topo["meta_" + k])
+        if v.ndim == 2 and v.shape[1] < meta[k].shape[1]:
+            meta[k][:, :v.shape[1]] = v
+        else:
+            meta[k] = v
     lists = {k: _lists(topo, k) for k in ("ids", "leaves", "parents")}
+    pad = lambda a, fill: [x for x in a] + [fill] * (3 - len(a))  # noqa: E731
     d = capi.TreeDesc()
     d.n_cell, d.n_boxes, d.highest_lvl = int(topo["nc"]), nb, int(topo["highest_lvl"])
     d.n_var_cell, d.n_var_face = n_var_cell, n_var_face
-    d.coarse_grid_size[:] = [int(x) for x in topo["coarse_grid_size"]]
+    d.coarse_grid_size[:] = pad([int(x) for x in topo["coarse_grid_size"]], 1)
     d.periodic[:] = [0, 0, 0]
-    d.r_base[:] = [float(x) for x in topo["r_base"]]
-    d.dr_base[:] = [float(x) for x in topo["dr_base"]]
+    d.r_base[:] = pad([float(x) for x in topo["r_base"]], 0.0)
+    d.dr_base[:] = pad([float(x) for x in topo["dr_base"]], 0.0)
     d.boxes = meta.ctypes.data
     d.box_capacity = int(box_capacity)
     for k in ("ids", "leaves", "parents"):
@@ -68,6 +76,7 @@ class Tree:
         # finalizes a cycle, in any order.
         self._deps = []
         self.nc = int(topo["nc"])
+        self.ndim = int(topo.get("ndim", 3))
         self.n_boxes = int(topo["n_boxes"])
         self.highest_lvl = int(topo["highest_lvl"])
         self.n_var_cell = n_var_cell
@@ -131,19 +140,17 @@ class Tree:
     # -- methods / data
     @property
     def cc_shape(self):
-        n = self.nc + 2
-        return (self.n_boxes, n, n, n)
+        return (self.n_boxes,) + (self.nc + 2,) * self.ndim
 
     @property
     def fc_shape(self):
-        n = self.nc + 1
-        return (self.n_boxes, 3, n, n, n)
+        return (self.n_boxes, self.ndim) + (self.nc + 1,) * self.ndim
 
     def set_cc_methods(self, iv, bc, rb=capi.RB_GC_INTERP,
                        prolong_limiter=capi.LIM_GMINMOD43):
-        """af_set_cc_methods; bc is a list of 6 (type, value) pairs."""
+        """af_set_cc_methods; bc is a list of 2 ndim (type, value) pairs."""
         arr = (capi.BC * 6)()
-        for n, (t, v) in enumerate(bc):
+        for n, (t, v) in enumerate(bc[:2 * self.ndim]):
             arr[n].type, arr[n].value = int(t), float(v)
         self.lib.call("set_cc_methods", self.h, iv, arr, rb, prolong_limiter)
 

@@ -71,7 +71,8 @@ class StreamerCase:
             self.tree = Tree(lib, topo, n_var_cell, N_VAR_FACE, device=device,
                              box_capacity=box_capacity)
         t = self.tree
-        neumann0 = [(capi.BC_NEUMANN, 0.0)] * 6
+        self.ndim = t.ndim
+        neumann0 = [(capi.BC_NEUMANN, 0.0)] * (2 * self.ndim)
         for sp in ("e", "pos", "neg"):
             for s in range(3):
                 t.set_cc_methods(IV[sp] + s, neumann0, capi.RB_GC_INTERP_LIM,
@@ -79,7 +80,7 @@ class StreamerCase:
         t.set_cc_methods(IV["efld"], neumann0, capi.RB_GC_INTERP)
         self.voltage = voltage
         for s in (0, 1):
-            t.set_cc_methods(IV["phi"] + s, self.phi_bc(voltage), capi.RB_MG_SIDES)
+            t.set_cc_methods(IV["phi"] + s, self.phi_bc(voltage, self.ndim), capi.RB_MG_SIDES)
         self.coarse_cycles = coarse_cycles
         self.i_lsf = 0  # level-set variable of an electrode (set_electrode)
         # keep the face fluxes of the species step in FV["flux"] (the fused
@@ -89,7 +90,8 @@ class StreamerCase:
         # field_compute(defer=True): the residual list the next species_step
         # fills (AFH_DEFER=0 turns deferral off, for A/B runs)
         self._deferred_res = None
-        self._defer_ok = os.environ.get("AFH_DEFER", "1") != "0"
+        # (the 2-D library has no deferred entry points, afivo_hip_2d.h)
+        self._defer_ok = os.environ.get("AFH_DEFER", "1") != "0" and self.ndim == 3
         self.mg = Multigrid(t, IV["phi"], IV["rhs"], IV["tmp"],
                             coarse_cycles=coarse_cycles)
         self._mg_helm = {}
@@ -102,10 +104,11 @@ class StreamerCase:
             shard.attach(self.tree)
 
     @staticmethod
-    def phi_bc(voltage):
-        """field_bc_homogeneous, src/m_field.f90:547-567."""
-        return [(capi.BC_NEUMANN, 0.0)] * 4 + [(capi.BC_DIRICHLET, 0.0),
-                                               (capi.BC_DIRICHLET, voltage)]
+    def phi_bc(voltage, ndim=3):
+        """field_bc_homogeneous, src/m_field.f90:547-567: Dirichlet 0 / V on
+        the faces of the last dimension, Neumann 0 elsewhere."""
+        return [(capi.BC_NEUMANN, 0.0)] * (2 * ndim - 2) + [(capi.BC_DIRICHLET, 0.0),
+                                                              (capi.BC_DIRICHLET, voltage)]
 
     def helmholtz_mg(self, lambda2):
         """mg_t of a photoionization Helmholtz mode on phi / rhs / tmp
@@ -141,7 +144,7 @@ class StreamerCase:
 
     def set_voltage(self, voltage):
         self.voltage = voltage
-        self.tree.set_bc(IV["phi"], 6, capi.BC_DIRICHLET, voltage)
+        self.tree.set_bc(IV["phi"], 2 * self.ndim, capi.BC_DIRICHLET, voltage)
 
     def min_dr(self):
         return float(np.min(self.topo["meta_dr"]))
@@ -177,7 +180,7 @@ class StreamerCase:
                 max_rhs = self.fluid.field_set_rhs_maxabs(IV["rhs"], s_in)
             threshold = max(1e-6, max_rhs * max_rel_residual,
                             1e-10 * abs(self.voltage) /
-                            (self.domain[2] * self.min_dr()))
+                            (self.domain[-1] * self.min_dr()))
         elif not fused:
             self.fluid.field_set_rhs(IV["rhs"], s_in)
         for _ in range(n_vcycles):
@@ -207,6 +210,10 @@ class StreamerCase:
         (m_af_advance.f90:160-164, m_fluid.f90:97-98), so the limits of a
         Heun step's first sub-step are never read; a deferred V-cycle
         residual stays pending too (it is overwritten by the next one)."""
+        if not fetch and self.ndim == 2:
+            self.fluid.forward_euler(dt, s_deriv, s_prev, w_prev, s_out, last_step,
+                                     self.store_flux)
+            return None
         if not fetch:
             self.fluid.forward_euler_fold(dt, s_deriv, s_prev, w_prev, s_out,
                                           last_step, self.store_flux)
@@ -247,6 +254,8 @@ def gaussian_seed(topo, r0, width, n0=5e18, bg=1e15):
 def seed_state(case, r0=None, width=None):
     """S1-style seed: n_e = n_+ = 1e15 + 5e18 exp(-|r-r0|^2/w^2), n_- = 1e14,
     phi = linear background."""
+    if case.ndim == 2:
+        return _seed_state_2d(case, r0, width)
     topo = case.topo
     dom = np.asarray(topo["domain"], float)
     r0 = 0.5 * dom if r0 is None else np.asarray(r0)
@@ -264,4 +273,27 @@ def seed_state(case, r0=None, width=None):
 
 def cells(topo):
     return sum(len(topo["lvl_leaves_%d" % l]) for l in
-               range(1, int(topo["highest_lvl"]) + 1)) * int(topo["nc"]) ** 3
+               range(1, int(topo["highest_lvl"]) + 1)) * int(topo["nc"]) ** int(topo.get("ndim", 3))
+
+
+def _seed_state_2d(case, r0=None, width=None):
+    """seed_state on a 2-D tree (the same seed, the field along y)."""
+    topo = case.topo
+    dom = np.asarray(topo["domain"], float)
+    r0 = 0.5 * dom if r0 is None else np.asarray(r0)
+    width = 0.025 * dom[-1] if width is None else width
+    nc = int(topo["nc"])
+    idx = np.arange(nc + 2) - 0.5
+    r_min, dr = topo["meta_r_min"], topo["meta_dr"]
+    x = r_min[:, 0, None] + idx[None, :] * dr[:, 0, None]
+    y = r_min[:, 1, None] + idx[None, :] * dr[:, 1, None]
+    d2 = ((x - r0[0]) ** 2)[:, None, :] + ((y - r0[1]) ** 2)[:, :, None]
+    ne = 1e15 + 5e18 * np.exp(-d2 / width ** 2)
+    t = case.tree
+    t.put_cc(IV["e"], ne)
+    t.put_cc(IV["pos"], ne)
+    t.put_cc(IV["neg"], np.full(ne.shape, 1e14))
+    phi = np.broadcast_to(case.voltage * (y / dom[1])[:, :, None], ne.shape)
+    t.put_cc(IV["phi"], np.ascontiguousarray(phi))
+    t.gc_tree(IV["phi"])
+    return ne

@@ -193,9 +193,85 @@ def uniform_tree(n_cell, coarse_grid_size, domain, max_lvl):
     return build_tree(n_cell, coarse_grid_size, domain, max_lvl)
 
 
+def uniform_tree_2d(n_cell, coarse_grid_size, domain, max_lvl):
+    """The 2-D topology af_init + af_refine_up_to_lvl build with NDIM = 2
+    (m_af_core.f90:138-340; children in af_child_dix order (0,0), (1,0),
+    (0,1), (1,1), m_af_types.f90:134): ids level by level, the level-1 boxes
+    i fastest, children in parent-id order. topo["ndim"] = 2; neighbors
+    (lowx, highx, lowy, highy), neighbor_mat(-1:1, -1:1) i fastest, -1 =
+    physical boundary, as in the reference's 2-D box_t."""
+    nc = int(n_cell)
+    cgs = np.array(coarse_grid_size, np.int64)
+    nbox0 = cgs // nc
+    assert np.all(nbox0 * nc == cgs), "coarse_grid_size must be a multiple of n_cell"
+    domain = np.asarray(domain, float)
+    dr_base = domain / cgs
+    cdix = np.array([[0, 0], [1, 0], [0, 1], [1, 1]], np.int32)
+    key2id, lvl, ix, parent, children = {}, [], [], [], []
+
+    def add(l, p, par):
+        key2id[(l, tuple(int(v) for v in p))] = len(lvl) + 1
+        lvl.append(l), ix.append(np.asarray(p, np.int32)), parent.append(par)
+        children.append(np.zeros(4, np.int32))
+        return len(lvl)
+
+    for j in range(1, nbox0[1] + 1):
+        for i in range(1, nbox0[0] + 1):
+            add(1, (i, j), 0)
+    for l in range(1, max_lvl):
+        for bid in [b for b in range(1, len(lvl) + 1) if lvl[b - 1] == l]:
+            for c in range(4):
+                children[bid - 1][c] = add(l + 1, 2 * ix[bid - 1] - 1 + cdix[c], bid)
+    nb = len(lvl)
+    out = {"nc": np.int32(nc), "n_boxes": np.int32(nb), "ndim": np.int32(2),
+           "highest_lvl": np.int32(max_lvl), "coarse_grid_size": cgs.astype(np.int32),
+           "r_base": np.zeros(2), "dr_base": dr_base, "domain": domain}
+    lv, ixa = np.array(lvl, np.int32), np.array(ix, np.int32)
+    nbs = np.zeros((nb, 4), np.int32)
+    nmat = np.zeros((nb, 9), np.int32)
+    r_min, dr = np.zeros((nb, 2)), np.zeros((nb, 2))
+    ndix = np.array([[-1, 0], [1, 0], [0, -1], [0, 1]])
+    for b in range(nb):
+        l, p = int(lv[b]), ixa[b]
+        n = nbox0 * 2 ** (l - 1)
+        inside = lambda q: bool(np.all(q >= 1) and np.all(q <= n))  # noqa: E731
+        for m in range(4):
+            q = p + ndix[m]
+            nbs[b, m] = key2id.get((l, tuple(int(v) for v in q)), 0) if inside(q) else -1
+        for dy in (-1, 0, 1):
+            for dx in (-1, 0, 1):
+                q = p + (dx, dy)
+                # a diagonal outside the domain: -1 on level 1, 0 (no box)
+                # below, where afivo finds it through the parent's neighbours
+                out_v = -1 if l == 1 or dx == 0 or dy == 0 else 0
+                nmat[b, (dx + 1) + 3 * (dy + 1)] = (
+                    key2id.get((l, tuple(int(v) for v in q)), 0) if inside(q) else out_v)
+    # r_min / dr accumulated from the parent as afivo does (add_children)
+    for b in range(nb):
+        if parent[b] > 0:
+            pb = parent[b] - 1
+            c = list(children[pb]).index(b + 1)
+            dr[b] = 0.5 * dr[pb]
+            r_min[b] = r_min[pb] + 0.5 * dr[pb] * cdix[c] * nc
+        else:
+            dr[b] = dr_base
+            r_min[b] = (ixa[b] - 1) * nc * dr_base
+    ch = np.array(children, np.int32)
+    out.update(meta_lvl=lv, meta_ix=ixa, meta_parent=np.array(parent, np.int32),
+               meta_children=ch, meta_neighbors=nbs, meta_neighbor_mat=nmat,
+               meta_r_min=r_min, meta_dr=dr)
+    for l in range(1, max_lvl + 1):
+        ids = np.where(lv == l)[0] + 1
+        has_ch = ch[ids - 1, 0] > 0
+        out["lvl_ids_%d" % l] = ids.astype(np.int32)
+        out["lvl_leaves_%d" % l] = ids[~has_ch].astype(np.int32)
+        out["lvl_parents_%d" % l] = ids[has_ch].astype(np.int32)
+    return out
+
+
 def leaf_cells(topo):
     nc = int(topo["nc"])
     n = 0
     for l in range(1, int(topo["highest_lvl"]) + 1):
         n += len(topo["lvl_leaves_%d" % l])
-    return n * nc ** 3
+    return n * nc ** int(topo.get("ndim", 3))

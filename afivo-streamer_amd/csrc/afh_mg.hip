@@ -30,8 +30,12 @@ struct Coef {
 constexpr int MAXMG = 16;
 constexpr int CS_BOTTOM_SWEEPS = 16;   // same constant as oracle/c/afo.c
 constexpr int CS_SMALL_CELLS = 4096;   // MG levels <= 16^3 run in one workgroup
-constexpr int CS_DS_N = 16;            // k_cs_direct_small: at most 16 cells per dimension
-constexpr int CS_DS_CELLS = (CS_DS_N + 1) * CS_DS_N * CS_DS_N;  // rows padded to nx + 1
+constexpr int CS_DS_N = 16;            // k_cs_direct_small: LDS matrices up to 16 x 16
+// k_cs_direct_small serves level-1 grids up to 1024 cells (S3's 8^3: 15 us,
+// against ~25 us for the eight launches of k_cs_gather / k_cs_transform /
+// k_cs_scatter); S1's 16^3 runs those (one workgroup took 63 us there, the
+// multi-launch form is 0.60 against 0.64 ms per step: profiles/r03_ab_fusions.txt)
+constexpr int CS_DS_CELLS = 1024;
 
 struct CsParams {
   int n_mg;
@@ -2126,16 +2130,11 @@ __global__ void __launch_bounds__(256)
   out[o] = s;
 }
 
-// AFH_COARSE_DIRECT on a level-1 grid of at most 16 cells per dimension
-// (S1's 16^3, the 8^3 of streamer_3d.cfg) in ONE workgroup: k_cs_gather's
-// folded rhs, the six k_cs_transform passes and k_cs_scatter, the grid held
-// in LDS -- the same sums in the same order, one launch instead of eight.
-// A pass works on lines along its dimension: a work item is one line and a
-// group of up to four outputs of it, and every wave takes one output group,
-// so the matrix entries are wave-uniform (scalar loads, no LDS traffic) and
-// a line's inputs are read from LDS once per group instead of once per
-// output. Rows are padded to nx + 1 doubles so that the x pass's lines (one
-// per lane, a row apart) do not fall into one LDS bank.
+// AFH_COARSE_DIRECT on a level-1 grid of at most CS_DS_CELLS cells (the 8^3
+// of streamer_3d.cfg) in ONE workgroup: k_cs_gather's folded
+// rhs, the six k_cs_transform passes and k_cs_scatter, the grid held in LDS
+// (compact, i fastest) -- the same sums in the same order, one launch
+// instead of eight.
 __global__ void __launch_bounds__(1024)
     k_cs_direct_small(CsParams P, double *__restrict__ phi, const double *__restrict__ rhs,
                       const afh_box_meta *__restrict__ meta, const int32_t *__restrict__ ids,
@@ -2146,9 +2145,10 @@ __global__ void __launch_bounds__(1024)
                       const double *__restrict__ qt2, const double *__restrict__ e0,
                       const double *__restrict__ e1, const double *__restrict__ e2,
                       double lam) {
-  __shared__ double A[CS_DS_CELLS], B[CS_DS_CELLS];
+  __shared__ double A[CS_SMALL_CELLS], B[CS_SMALL_CELLS];
+  __shared__ double Ml[6][CS_DS_N * CS_DS_N];
   const int nx = P.dims[0][0], ny = P.dims[0][1], nz = P.dims[0][2];
-  const int px = nx + 1, pl = px * ny, n3 = nc * nc * nc;
+  const int N = nx * ny * nz, n3 = nc * nc * nc;
   const afh_bc bc[6] = {b0, b1, b2, b3, b4, b5};
   for (int u = threadIdx.x; u < nid * n3; u += blockDim.x) {
     const int id = ids[u / n3], t = u % n3;
@@ -2168,50 +2168,48 @@ __global__ void __launch_bounds__(1024)
       else b2r = -(cnb * m.dr[dd]) * (low ? -1 : 1);
       rv = rv + b2r * bc[nb - 1].value;
     }
-    A[(gi[2] - 1) * pl + (gi[1] - 1) * px + (gi[0] - 1)] = rv;
+    A[((gi[2] - 1) * ny + (gi[1] - 1)) * nx + (gi[0] - 1)] = rv;
   }
-  __syncthreads();
   // Q^T along x, y, z (divide), then Q along z, y, x: A -> B -> A -> B -> A -> B -> A
   const double *Ms[6] = {q0, q1, q2, qt2, qt1, qt0};
   const int ds[6] = {0, 1, 2, 2, 1, 0};
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+  // grids of at most 16 cells per dimension: the six matrices in LDS and
+  // each output's 2 x n operands loaded before its (ordered) sum, so the
+  // loads overlap instead of each product waiting for its own
+  const bool small = nx <= CS_DS_N && ny <= CS_DS_N && nz <= CS_DS_N;
+  if (small)
+    for (int ps = 0; ps < 6; ps++) {
+      const int d = ds[ps], n = d == 0 ? nx : (d == 1 ? ny : nz);
+      for (int u = threadIdx.x; u < n * n; u += blockDim.x) Ml[ps][u] = Ms[ps][u];
+    }
+  __syncthreads();
   for (int ps = 0; ps < 6; ps++) {
     const double *in = (ps & 1) ? B : A;
     double *out = (ps & 1) ? A : B;
-    const int d = ds[ps];
-    const int n = d == 0 ? nx : (d == 1 ? ny : nz);
-    // the line's two other coordinates: (a, b) = (j, k), (i, k) or (i, j)
-    const int na = d == 0 ? ny : nx;
-    const int nlines = (d == 0 ? ny * nz : (d == 1 ? nx * nz : nx * ny));
-    const int st = d == 0 ? 1 : (d == 1 ? px : pl);
-    const int ng = (n + 3) >> 2;                // output groups of four
-    const int nchunk = ((nlines + 63) >> 6) * ng;
-    const double *M = Ms[ps];
-    for (int c = wave; c < nchunk; c += nw) {
-      const int g = __builtin_amdgcn_readfirstlane(c % ng);
-      const int line = (c / ng) * 64 + lane;
-      if (line >= nlines) continue;
-      const int a = line % na, b = line / na;
-      const int base = d == 0 ? b * pl + a * px : (d == 1 ? b * pl + a : b * px + a);
-      double x[CS_DS_N];
-#pragma unroll
-      for (int p = 0; p < CS_DS_N; p++)
-        if (p < n) x[p] = in[base + p * st];
-#pragma unroll
-      for (int r = 0; r < 4; r++) {
-        const int co = g * 4 + r;
-        if (co >= n) break;
-        double s = 0.0;
+    const int d = ds[ps], n = d == 0 ? nx : (d == 1 ? ny : nz);
+    const int st = d == 0 ? 1 : (d == 1 ? nx : nx * ny);
+    const double *M = small ? Ml[ps] : Ms[ps];
+    for (int t = threadIdx.x; t < N; t += blockDim.x) {
+      const int i = t % nx, j = (t / nx) % ny, k = t / (nx * ny);
+      const int co = d == 0 ? i : (d == 1 ? j : k);
+      const double *src = in + (t - co * st);
+      double s = 0.0;
+      if (small) {
+        double mv[CS_DS_N], xv[CS_DS_N];
 #pragma unroll
         for (int p = 0; p < CS_DS_N; p++)
-          if (p < n) s = s + M[p * n + co] * x[p];
-        if (ps == 2) {
-          const int i = d == 0 ? co : a, j = d == 1 ? co : (d == 0 ? a : b), k = d == 2 ? co : b;
-          const double den = ((e0[i] + e1[j]) + e2[k]) - lam;
-          s = den != 0.0 ? s / den : 0.0;
-        }
-        out[base + co * st] = s;
+          if (p < n) mv[p] = M[p * n + co], xv[p] = src[p * st];
+#pragma unroll
+        for (int p = 0; p < CS_DS_N; p++)
+          if (p < n) s = s + mv[p] * xv[p];
+      } else {
+        for (int p = 0; p < n; p++) s = s + M[p * n + co] * src[p * st];
       }
+      if (ps == 2) {
+        const double den = ((e0[i] + e1[j]) + e2[k]) - lam;
+        s = den != 0.0 ? s / den : 0.0;
+      }
+      out[t] = s;
     }
     __syncthreads();
   }
@@ -2221,7 +2219,7 @@ __global__ void __launch_bounds__(1024)
     const afh_box_meta &m = meta[id - 1];
     const int i = t % nc + 1, j = (t / nc) % nc + 1, k = t / (nc * nc) + 1;
     phi[(size_t)(id - 1) * bsz + ix3(nc + 2, i, j, k)] =
-        A[((m.ix[2] - 1) * nc + k - 1) * pl + ((m.ix[1] - 1) * nc + j - 1) * px +
+        A[(((m.ix[2] - 1) * nc + k - 1) * ny + (m.ix[1] - 1) * nc + j - 1) * nx +
           (m.ix[0] - 1) * nc + i - 1];
   }
 }
@@ -2266,7 +2264,7 @@ struct afh_mg {
   // level-1 cycles of the last coarse solve (afh_mg_coarse_iterations): on
   // the device when k_cs_small applied the stopping rule, else on the host
   // AFH_CS_DIRECT_SMALL: the direct solve of a level-1 grid of at most
-  // 16 cells per dimension in one workgroup (k_cs_direct_small), default on
+  // CS_DS_CELLS cells in one workgroup (k_cs_direct_small), default on
   bool cs_direct_small = true;
   bool pair_push = true;  // AFH_PAIR_PUSH: the small-box pair fills the faces
   int *d_cycles = nullptr;
@@ -3135,7 +3133,7 @@ static int32_t solve_coarse(afh_mg *mg) {
     }
   const int nc = t->nc, nid = t->ids.n(1), n3 = nc * nc * nc;
   if (mg->d.coarse_mode == AFH_COARSE_DIRECT && mg->cs_direct_small &&
-      P.dims[0][0] <= CS_DS_N && P.dims[0][1] <= CS_DS_N && P.dims[0][2] <= CS_DS_N) {
+      (long)P.dims[0][0] * P.dims[0][1] * P.dims[0][2] <= CS_DS_CELLS) {
     for (int q = 0; q < 6; q++)
       if (mg->q_bc[q] != bc[q].type) {
         if (int32_t e = build_direct(mg)) return e;

@@ -54,6 +54,11 @@ CONFIGS = {
     # stencils on the boxes the rod crosses (afh.electrode), the electrode's
     # species boundary condition every time step, 5 levels of 8^3 boxes
     "s4": (8, None, None, (16e-3, 16e-3, 16e-3)),
+    # BASELINE.json config 1 (programs/standard_2d, streamer_2d.cfg's box size
+    # and domain) on the 2-D build (libafivo_hip_2d.so): 8^2 boxes, one
+    # level-1 box, uniformly refined to level 8 (128 x 128 leaf boxes, 1024^2
+    # cells), the old-style 3-species model; the unit step as for s1
+    "2d": (8, (8, 8), 8, (32e-3, 32e-3)),
 }
 DRIVER_CONFIGS = ("s3", "s4", "s5")
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E peak (spec)
@@ -66,10 +71,14 @@ def build_case(lib, config, device, coarse_cycles, shard_ranks=None):
     from afh.tree import uniform_tree
     import golden
     nc, cgs, lvls, dom = CONFIGS[config]
-    topo = uniform_tree(nc, cgs, dom, lvls)
+    if len(dom) == 2:
+        from afh.tree import uniform_tree_2d
+        topo = uniform_tree_2d(nc, cgs, dom, lvls)
+    else:
+        topo = uniform_tree(nc, cgs, dom, lvls)
     g = golden.load("uni8")  # transport/chemistry tables exported from the reference
     td, chem = tables_from(g)
-    voltage = -dom[2] * (-2.5e6)
+    voltage = -dom[-1] * (-2.5e6)
     shard = None
     if shard_ranks is not None:
         world, rank, kind = shard_ranks
@@ -85,7 +94,7 @@ def build_case(lib, config, device, coarse_cycles, shard_ranks=None):
             shard = Shard(Partition(topo, world), rank, "nccl", device="cuda:%d" % device)
     case = StreamerCase(lib, topo, td, chem, voltage, coarse_cycles=coarse_cycles,
                         device=device, shard=shard)
-    seed_state(case, width=0.05 * dom[2])
+    seed_state(case, width=0.05 * dom[-1])
     return case
 
 
@@ -284,8 +293,11 @@ def main():
             torch.cuda.set_device(local)
 
     from afh import capi
-    lib = capi.hip_library()
+    two_d = len(CONFIGS[args.config][3]) == 2
+    lib = capi.hip_library_2d() if two_d else capi.hip_library()
     sharded = world > 1 and not args.replicas
+    if two_d and sharded:
+        raise SystemExit("the 2-D build does not shard (--replicas runs one per GPU)")
     if args.config in DRIVER_CONFIGS:
         sim = build_driver_case(lib, local, args.config)
         if sharded:
@@ -303,7 +315,7 @@ def main():
     ncell = cells(case.topo)  # leaf cells of the whole tree
     dt = 1e-13
 
-    if not args.no_fused_rhs:
+    if not args.no_fused_rhs and not two_d:
         case.fuse_rhs(True, ghosts=False)
     case.field_compute(0, n_vcycles=2)  # initial potential (untimed)
     for k in range(args.warmup):
@@ -321,7 +333,9 @@ def main():
     # over two eager unit steps right after the timed region
     import ctypes as C
     graphs = args.graphs == "on" or (args.graphs == "auto" and args.config != "s1-64")
-    if not graphs:
+    if two_d:
+        graphs = False  # (no graphs, no kernel timing in the 2-D build)
+    elif not graphs:
         lib.call("profile_enable", case.tree.h, capi.PROF_GSRB_PAIR)
     barrier()
     case.tree.sync()
@@ -337,10 +351,11 @@ def main():
             unit_step(case, dt, args.warmup + args.steps + k)
         case.tree.sync()
     ms, nl, by = C.c_double(), C.c_int64(), C.c_double()
-    lib.call("profile_read", case.tree.h, C.byref(ms), C.byref(nl), C.byref(by))
+    if not two_d:
+        lib.call("profile_read", case.tree.h, C.byref(ms), C.byref(nl), C.byref(by))
     kname = ("k_gsrb_pair2<%d,%d>" % (CONFIGS[args.config][0], CONFIGS[args.config][0])
              if CONFIGS[args.config][0] > 16 else "k_gsrb_pair_box<%d>" % CONFIGS[args.config][0])
-    if nl.value == 0:
+    if nl.value == 0 and not two_d:
         # no level runs the fused pair (too few boxes per level, or
         # electrode stencils): the split half-sweep k_gsrb is the smoother
         kname = "k_gsrb (half-sweep, 16 B/cell)"
@@ -402,6 +417,13 @@ def main():
             # one FAS V(2,2)-cycle per step (SURVEY.md 8(d) reports both)
             "vcycles_per_s": args.steps / elapsed,
         }
+        if two_d:
+            # the 2-D build has no kernel timing (afivo_hip_2d.h): no roofline
+            # line; the config is BASELINE's plumbing case, not a bench target
+            out["roofline"] = None
+            out["config"]["coarse_solve"] = "direct"
+            out["config"]["ndim"] = 2
+            out["config"]["fused_rhs"] = False
         if sharded:
             out["exchanges_per_step"] = case.shard.n_exchanges / max(1, args.steps + args.warmup + 1)
         if args.config == "s3":
@@ -418,7 +440,7 @@ def main():
             out["config"]["photoionization"] = ("Helmholtz Bourdon-3, every %d time steps"
                                                 % sim.c.i("photoi%per_steps"))
             out["config"]["coarse_solve"] = "direct"
-        if not args.no_cpu_baseline and world == 1:
+        if not args.no_cpu_baseline and world == 1 and not two_d:
             out["cpu_baseline"] = (cpu_baseline_driver(sim, config=args.config)
                                    if args.config in DRIVER_CONFIGS else
                                    cpu_baseline(args.config, args.coarse_cycles))

@@ -85,7 +85,9 @@ CASES = {
 }
 
 
-def read_topology(path):
+def read_topology(path, ndim=3):
+    """ndim = 2: the 2-D harness' topology (golden_gen2d.f90): ix (n, 2),
+    children (n, 4), neighbors (n, 4), neighbor_mat (n, 9), r_min / dr (n, 2)."""
     raw = open(path, "rb").read()
     off = 0
 
@@ -98,26 +100,27 @@ def read_topology(path):
     nc, nbox, nlvl, nvc, nvf = take(np.int32, 5)
     out = {"nc": nc, "n_boxes": nbox, "highest_lvl": nlvl, "n_var_cell": nvc,
            "n_var_face": nvf}
-    out["coarse_grid_size"] = take(np.int32, 3)
-    out["r_base"] = take(np.float64, 3)
-    out["dr_base"] = take(np.float64, 3)
+    d = ndim
+    out["coarse_grid_size"] = take(np.int32, d)
+    out["r_base"] = take(np.float64, d)
+    out["dr_base"] = take(np.float64, d)
     lvl = np.zeros(nbox, np.int32)
-    ix = np.zeros((nbox, 3), np.int32)
+    ix = np.zeros((nbox, d), np.int32)
     parent = np.zeros(nbox, np.int32)
-    children = np.zeros((nbox, 8), np.int32)
-    neighbors = np.zeros((nbox, 6), np.int32)
-    nmat = np.zeros((nbox, 27), np.int32)
-    r_min = np.zeros((nbox, 3))
-    dr = np.zeros((nbox, 3))
+    children = np.zeros((nbox, 2 ** d), np.int32)
+    neighbors = np.zeros((nbox, 2 * d), np.int32)
+    nmat = np.zeros((nbox, 3 ** d), np.int32)
+    r_min = np.zeros((nbox, d))
+    dr = np.zeros((nbox, d))
     for b in range(nbox):
         lvl[b] = take(np.int32, 1)[0]
-        ix[b] = take(np.int32, 3)
+        ix[b] = take(np.int32, d)
         parent[b] = take(np.int32, 1)[0]
-        children[b] = take(np.int32, 8)
-        neighbors[b] = take(np.int32, 6)
-        nmat[b] = take(np.int32, 27)
-        r_min[b] = take(np.float64, 3)
-        dr[b] = take(np.float64, 3)
+        children[b] = take(np.int32, 2 ** d)
+        neighbors[b] = take(np.int32, 2 * d)
+        nmat[b] = take(np.int32, 3 ** d)
+        r_min[b] = take(np.float64, d)
+        dr[b] = take(np.float64, d)
     out.update(meta_lvl=lvl, meta_ix=ix, meta_parent=parent,
                meta_children=children, meta_neighbors=neighbors,
                meta_neighbor_mat=nmat, meta_r_min=r_min, meta_dr=dr)
@@ -129,7 +132,9 @@ def read_topology(path):
     cv, ngas = take(np.float64, 2)
     out["current_voltage"] = cv
     out["gas_number_density"] = ngas
-    out["domain"] = take(np.float64, 3)
+    out["domain"] = take(np.float64, d)
+    if d == 2:
+        out["ndim"] = np.int32(2)
     return out
 
 
@@ -153,10 +158,11 @@ def read_tables(path):
 def read_state(path, topo):
     nb, nc = int(topo["n_boxes"]), int(topo["nc"])
     nvc, nvf = int(topo["n_var_cell"]), int(topo["n_var_face"])
+    d = int(topo.get("ndim", 3))
     a = np.fromfile(path, dtype=np.float64)
-    ncc = nb * nvc * (nc + 2) ** 3
-    cc = a[:ncc].reshape(nb, nvc, nc + 2, nc + 2, nc + 2)
-    fc = a[ncc:].reshape(nb, nvf, 3, nc + 1, nc + 1, nc + 1)
+    ncc = nb * nvc * (nc + 2) ** d
+    cc = a[:ncc].reshape((nb, nvc) + (nc + 2,) * d)
+    fc = a[ncc:].reshape((nb, nvf, d) + (nc + 1,) * d)
     return cc, fc
 
 
@@ -204,8 +210,17 @@ def read_lsf(path, topo):
             "lsf_d_dd": np.concatenate(d_dd), "lsf_d_bval": np.array(d_bv)}
 
 
+# BASELINE config 1, the reference's 2-D build (oracle/_ref/2d/golden_gen2d):
+# arrays are [box][j][i] (cc) and [box][dim][j][i] (fc)
+CASES_2D = {
+    "uni2d": {"chain": CHAIN + FMG + HELM, "trace": False, "ndim": 2},
+    "amr2d": {"chain": CHAIN + FMG + HELM, "trace": False, "ndim": 2},
+}
+
+
 def pack(case, raw_dir):
-    topo = read_topology(os.path.join(raw_dir, "topology.bin"))
+    spec = CASES_2D[case] if case in CASES_2D else CASES[case]
+    topo = read_topology(os.path.join(raw_dir, "topology.bin"), spec.get("ndim", 3))
     out = dict(topo)
     out.update(read_tables(os.path.join(raw_dir, "tables.bin")))
     # scalar logs (dt limits, residuals, thresholds)
@@ -216,7 +231,6 @@ def pack(case, raw_dir):
         key = "log_" + f[0] + ("_%s" % f[1] if f[0] == "field1_residual" else "")
         vals = [float(x) for x in (f[2:] if f[0] == "field1_residual" else f[1:])]
         out[key] = np.array(vals)
-    spec = CASES[case]
     out["helm_lambda"] = np.array(HELM_LAMBDA)
     if spec.get("lsf"):
         out.update(read_lsf(os.path.join(raw_dir, "lsf.bin"), topo))
@@ -269,13 +283,14 @@ def main():
     gen = os.path.join(HERE, "_ref", "golden_gen")
     if not os.path.exists(gen):
         sys.exit("build the harness first: make -C oracle ref")
-    for case in (sys.argv[1:] or CASES):
+    gen2d = os.path.join(HERE, "_ref", "2d", "golden_gen2d")
+    for case in (sys.argv[1:] or list(CASES) + list(CASES_2D)):
         raw = os.path.join("/tmp", "golden_raw", case)
         os.makedirs(raw, exist_ok=True)
         for f in os.listdir(raw):
             os.remove(os.path.join(raw, f))
-        subprocess.run([gen, case, TD_FILE, raw], check=True,
-                       stdout=subprocess.DEVNULL)
+        subprocess.run([gen2d if case in CASES_2D else gen, case, TD_FILE, raw],
+                       check=True, stdout=subprocess.DEVNULL)
         dst = pack(case, raw)
         print("%-5s -> %s (%.0f kB)" % (case, dst, os.path.getsize(dst) / 1e3))
 

@@ -5,8 +5,9 @@ read at tree / multigrid / fluid creation):
   workgroup (k_gc_box) vs k_gc_faces6 + k_gc_corners;
 * AFH_PAIR_PUSH: the small-box fused red-black pair writes the level's face
   ghosts itself (k_gsrb_pair_box PUSH) vs the pair + a level fill;
-* AFH_CS_DIRECT_SMALL: the exact level-1 solve of a grid up to 16^3 in one
-  workgroup (k_cs_direct_small) vs gather + six transforms + scatter;
+* AFH_CS_DIRECT_SMALL: the exact level-1 solve of a grid up to 1024 cells
+  in one workgroup (k_cs_direct_small) vs gather + six transforms + scatter
+  (on an 8^3 level-1 grid, streamer_3d.cfg's; S1's 16^3 runs the launches);
 * AFH_UPD_NET: the compiled reaction network (afh_networks.h, k_update's
   unrolled reaction loop) vs the generic loop -- on the S3 tree with
   air_chemistry_v2 (9 species, 25 reactions) and on S1's old-style model;
@@ -23,13 +24,13 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def _s1(monkeypatch, env):
+def _s1(monkeypatch, env, config="s1"):
     import bench
     from afh import capi
     from afh.streamer import IV
     for k, v in env.items():
         monkeypatch.setenv(k, v)
-    c = bench.build_case(capi.hip_library(), "s1", 0, 0)
+    c = bench.build_case(capi.hip_library(), config, 0, 0)
     c.fuse_rhs(True, ghosts=False)
     out = {"res0": c.field_compute(0, n_vcycles=2)}
     for k in range(4):
@@ -56,6 +57,16 @@ def test_s1_fusion_bitwise(switch, monkeypatch):
     # AFH_UPD_NET=2: the compiled network must match (S1's old-style model)
     a = _s1(monkeypatch, {switch: "2" if switch == "AFH_UPD_NET" else "1"})
     b = _s1(monkeypatch, {switch: "0"})
+    _same(a, b)
+
+
+def test_direct_small_bitwise_8cubed(monkeypatch):
+    """k_cs_direct_small on an 8^3 level-1 grid (one box, 3 levels of 8^3
+    boxes): field solve and four unit steps, one workgroup vs the launches."""
+    import bench
+    monkeypatch.setitem(bench.CONFIGS, "c8", (8, (8, 8, 8), 3, (8e-3, 8e-3, 8e-3)))
+    a = _s1(monkeypatch, {"AFH_CS_DIRECT_SMALL": "1"}, "c8")
+    b = _s1(monkeypatch, {"AFH_CS_DIRECT_SMALL": "0"}, "c8")
     _same(a, b)
 
 
