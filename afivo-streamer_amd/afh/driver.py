@@ -138,6 +138,12 @@ class Simulation:
         # field_compute reads max|rhs| with the first residual (AFH_DEFER=0:
         # before the V-cycle, as the reference orders it; for A/B runs)
         self._defer_ok = os.environ.get("AFH_DEFER", "1") != "0"
+        # the flux takes the face field from phi (afh_fluid_set_field_source):
+        # the gradient then writes |E| only; not with an electrode (its
+        # boxes' gradient is mg_box_lpllsf_gradient). AFH_FACES_FROM_PHI=0
+        # stores and reads the face field, as the reference does (A/B runs)
+        self._faces_from_phi_ok = os.environ.get("AFH_FACES_FROM_PHI", "1") != "0"
+        self.faces_from_phi = False
         if c.s("time_integrator") != "heuns_method":
             raise NotImplementedError("time integrator %s" % c.s("time_integrator"))
         self.n_states = 2  # af_advance_num_steps(af_heuns_method)
@@ -294,6 +300,9 @@ class Simulation:
             gas_fractions=self.gas_fractions if self.i_gas_dens else ())
         if self.fused_rhs:
             self.fluid.set_rhs_output(self.i_rhs, True)
+        self.faces_from_phi = self._faces_from_phi_ok and self.lsf is None
+        if self.faces_from_phi:
+            self.fluid.set_field_source(self.i_phi, -1.0)
         if self.lsf is not None:
             self._set_electrode()
 
@@ -479,8 +488,10 @@ class Simulation:
 
     # --------------------------------------------------------- physics
     def field_from_potential(self):
-        """m_field.f90:488-505."""
-        self.mg.compute_phi_gradient(self.f_field, -1.0, self.i_efld)
+        """m_field.f90:488-505 (with faces_from_phi the face field is not
+        stored: the flux evaluates it from phi)."""
+        self.mg.compute_phi_gradient(0 if self.faces_from_phi else self.f_field, -1.0,
+                                     self.i_efld)
         self.tree.gc_tree(self.i_efld)
 
     def field_compute(self, s_in, have_guess=True):
@@ -812,6 +823,10 @@ class Simulation:
         the reference's analysis module, not computed here) are written as
         zeros."""
         from .datfile import DatTree, sim_data_bytes
+        if self.faces_from_phi:
+            # the face field the reference stores: mg_box_lpl_gradient of the
+            # potential the last field_from_potential used (phi unchanged since)
+            self.mg.compute_phi_gradient(self.f_field, -1.0, 0)
         t = DatTree.from_aftree(self.af, self.cc_names, self.c.sa("fc_names"))
         used = [b for b in range(1, self.af.highest_id + 1) if self.af.in_use[b]]
         for iv in range(1, self.n_var_cell + 1):

@@ -146,9 +146,12 @@ class Tree:
     def fc_shape(self):
         return (self.n_boxes, self.ndim) + (self.nc + 1,) * self.ndim
 
-    def set_cc_methods(self, iv, bc, rb=capi.RB_GC_INTERP,
-                       prolong_limiter=capi.LIM_GMINMOD43):
-        """af_set_cc_methods; bc is a list of 2 ndim (type, value) pairs."""
+    def set_cc_methods(self, iv, bc, rb=capi.RB_GC_INTERP, prolong_limiter=None):
+        """af_set_cc_methods; bc is a list of 2 ndim (type, value) pairs. The
+        default prolong_limiter is af_set_cc_methods' own: MC in 2-D,
+        gminmod43 in 3-D (m_af_core.f90:399-408)."""
+        if prolong_limiter is None:
+            prolong_limiter = capi.LIM_MC if self.ndim < 3 else capi.LIM_GMINMOD43
         arr = (capi.BC * 6)()
         for n, (t, v) in enumerate(bc[:2 * self.ndim]):
             arr[n].type, arr[n].value = int(t), float(v)
@@ -425,6 +428,12 @@ class Fluid:
         """Fold field_set_rhs(i_rhs, s_out) into every density update (0: off);
         ghosts=False leaves the rhs ghost cells alone (no solver reads them)."""
         self.lib.call("fluid_set_rhs_output", self.h, i_rhs, int(ghosts))
+
+    def set_field_source(self, i_phi, fac=-1.0):
+        """The flux evaluates the face field from the potential i_phi
+        (fac / dr * (phi_f - phi_{f-1}), mg_box_lpl_gradient) instead of
+        reading f_field; 0 restores f_field (afh_fluid_set_field_source)."""
+        self.lib.call("fluid_set_field_source", self.h, i_phi, float(fac))
 
     def rhs_maxabs(self, s_out):
         """max|rhs| of the rhs the last update wrote for state s_out."""

@@ -75,8 +75,9 @@ class StreamerCase:
         neumann0 = [(capi.BC_NEUMANN, 0.0)] * (2 * self.ndim)
         for sp in ("e", "pos", "neg"):
             for s in range(3):
-                t.set_cc_methods(IV[sp] + s, neumann0, capi.RB_GC_INTERP_LIM,
-                                 capi.LIM_GMINMOD43)
+                # the default prolong_limiter (streamer.f90:81-84 passes
+                # none): MC in 2-D, gminmod43 in 3-D
+                t.set_cc_methods(IV[sp] + s, neumann0, capi.RB_GC_INTERP_LIM)
         t.set_cc_methods(IV["efld"], neumann0, capi.RB_GC_INTERP)
         self.voltage = voltage
         for s in (0, 1):
@@ -87,6 +88,7 @@ class StreamerCase:
         # device step otherwise leaves them on chip)
         self.store_flux = False
         self._fused_rhs = False  # afh_fluid_set_rhs_output active
+        self._faces_from_phi = False  # afh_fluid_set_field_source active
         # field_compute(defer=True): the residual list the next species_step
         # fills (AFH_DEFER=0 turns deferral off, for A/B runs)
         self._deferred_res = None
@@ -142,6 +144,12 @@ class StreamerCase:
         self.fluid.set_rhs_output(IV["rhs"] if on else 0, ghosts)
         self._fused_rhs = on
 
+    def faces_from_phi(self, on=True):
+        """The flux evaluates the face field from phi (afh_fluid_set_field_source)
+        and field_from_potential stores |E| only (not with an electrode)."""
+        self.fluid.set_field_source(IV["phi"] if on else 0, -1.0)
+        self._faces_from_phi = on
+
     def set_voltage(self, voltage):
         self.voltage = voltage
         self.tree.set_bc(IV["phi"], 2 * self.ndim, capi.BC_DIRICHLET, voltage)
@@ -151,7 +159,8 @@ class StreamerCase:
 
     def field_from_potential(self):
         """m_field.f90:488-505."""
-        self.mg.compute_phi_gradient(FV["field"], -1.0, IV["efld"])
+        self.mg.compute_phi_gradient(0 if self._faces_from_phi else FV["field"], -1.0,
+                                     IV["efld"])
         self.tree.gc_tree(IV["efld"])
 
     def field_compute(self, s_in, n_vcycles=2, max_rel_residual=1e-4,

@@ -845,7 +845,7 @@ struct Meth {
   int set = 0;
   afh_bc bc[4];
   int rb = AFH_RB_GC_INTERP;
-  int lim = AFH_LIM_GMINMOD43;
+  int lim = AFH_LIM_MC;  // af_set_cc_methods default in 2-D (m_af_core.f90:401-402)
 };
 
 }  // namespace afh2

@@ -1486,7 +1486,7 @@ __global__ void k_gradient(const double *__restrict__ phi,
 // Each thread owns a column of K cells in k: the K + 2 phi values of the
 // column are loaded once (the z differences of neighbouring cells share them),
 // and every load of the column is issued before the first store.
-template <int NC, int K, bool NT = false>
+template <int NC, int K, bool NT = false, bool FC = true>
 __global__ void __launch_bounds__(256)
     k_gradient_t(const double *__restrict__ phi, double *__restrict__ fcv,
                  double *__restrict__ nrm, const int32_t *__restrict__ ids,
@@ -1527,12 +1527,14 @@ __global__ void __launch_bounds__(256)
     const double fyl = iy * (pv - ym[q]), fyh = iy * (yp[q] - pv);
     const double fzl = iz * (pv - pc[q]), fzh = iz * (pc[q + 2] - pv);
     const size_t fb = ((size_t)(k - 1) * NF + (j - 1)) * NF + (i - 1);
-    st_nt<NT>(f + fb, fxl);
-    if (i == NC) st_nt<NT>(f + fb + 1, fxh);
-    st_nt<NT>(f + D3 + fb, fyl);
-    if (j == NC) st_nt<NT>(f + D3 + fb + NF, fyh);
-    st_nt<NT>(f + 2 * D3 + fb, fzl);
-    if (k == NC) st_nt<NT>(f + 2 * D3 + fb + (size_t)NF * NF, fzh);
+    if (FC) {  // (without FC: the norm only, afh_fluid_set_field_source)
+      st_nt<NT>(f + fb, fxl);
+      if (i == NC) st_nt<NT>(f + fb + 1, fxh);
+      st_nt<NT>(f + D3 + fb, fyl);
+      if (j == NC) st_nt<NT>(f + D3 + fb + NF, fyh);
+      st_nt<NT>(f + 2 * D3 + fb, fzl);
+      if (k == NC) st_nt<NT>(f + 2 * D3 + fb + (size_t)NF * NF, fzh);
+    }
     if (nb) {
       const double a = fxl + fxh, b = fyl + fyh, cc = fzl + fzh;
       st_nt<NT>(nb + c0 + q * SK, 0.5 * sqrt(a * a + b * b + cc * cc));
@@ -1551,14 +1553,10 @@ static void launch_gradient(afh_tree *t, const double *phi, double *fcv,
   const int ntot = t->ids.off[t->nlvl];  // every box of every level
   for (int o = 0; o < ntot; o += 65535) {  // grid.y limit
     const int n = std::min(65535, ntot - o);
-    if (nt)
-      hipLaunchKernelGGL((k_gradient_t<NC, K, true>), dim3((NC / R) * (NC / K), n),
-                         dim3(NC * R), 0, t->stream, phi, fcv, nrm, t->ids.d + o, t->bsz,
-                         t->fsz, t->d_boxes, fac);
-    else
-      hipLaunchKernelGGL((k_gradient_t<NC, K>), dim3((NC / R) * (NC / K), n),
-                         dim3(NC * R), 0, t->stream, phi, fcv, nrm, t->ids.d + o, t->bsz,
-                         t->fsz, t->d_boxes, fac);
+    auto kern = fcv ? (nt ? k_gradient_t<NC, K, true> : k_gradient_t<NC, K>)
+                    : (nt ? k_gradient_t<NC, K, true, false> : k_gradient_t<NC, K, false, false>);
+    hipLaunchKernelGGL(kern, dim3((NC / R) * (NC / K), n), dim3(NC * R), 0, t->stream, phi,
+                       fcv, nrm, t->ids.d + o, t->bsz, t->fsz, t->d_boxes, fac);
   }
 }
 
@@ -3478,26 +3476,32 @@ int32_t afh_mg_compute_phi_gradient(afh_mg *mg, int32_t i_fc, double fac,
   if (!mg) return set_error(AFH_ERR_ARG, "null mg");
   afh_tree *t = mg->t;
   AFH_LIVE(t, "afh_mg_compute_phi_gradient");
-  if (i_fc < 1 || i_fc > t->nvf || i_norm < 0 || i_norm > t->nvc)
+  if (i_fc < 0 || i_fc > t->nvf || i_norm < 0 || i_norm > t->nvc)
     return set_error(AFH_ERR_ARG, "bad variable index");
+  int32_t e;
+  if ((e = prepare_var(mg))) return e;
+  // i_fc = 0: the norm only (the flux evaluates the face field from phi,
+  // afh_fluid_set_field_source); electrode boxes need the face field
+  if (i_fc == 0 && (i_norm == 0 || mg->any_lsf))
+    return set_error(AFH_ERR_ARG, "i_fc = 0 needs i_norm and no electrode boxes");
   const int nc = t->nc, n3 = nc * nc * nc;
   const int ntot = t->ids.off[t->nlvl];
   double *nrm = i_norm > 0 ? t->ccv(i_norm) : nullptr;
+  double *fcv = i_fc > 0 ? t->fcv(i_fc) : nullptr;
   switch (nc) {
-  case 4: launch_gradient<4>(t, t->ccv(mg->d.i_phi), t->fcv(i_fc), nrm, fac, mg->grad_nt); break;
-  case 8: launch_gradient<8>(t, t->ccv(mg->d.i_phi), t->fcv(i_fc), nrm, fac, mg->grad_nt); break;
-  case 16: launch_gradient<16>(t, t->ccv(mg->d.i_phi), t->fcv(i_fc), nrm, fac, mg->grad_nt); break;
-  case 32: launch_gradient<32>(t, t->ccv(mg->d.i_phi), t->fcv(i_fc), nrm, fac, mg->grad_nt); break;
-  case 64: launch_gradient<64>(t, t->ccv(mg->d.i_phi), t->fcv(i_fc), nrm, fac, mg->grad_nt); break;
+  case 4: launch_gradient<4>(t, t->ccv(mg->d.i_phi), fcv, nrm, fac, mg->grad_nt); break;
+  case 8: launch_gradient<8>(t, t->ccv(mg->d.i_phi), fcv, nrm, fac, mg->grad_nt); break;
+  case 16: launch_gradient<16>(t, t->ccv(mg->d.i_phi), fcv, nrm, fac, mg->grad_nt); break;
+  case 32: launch_gradient<32>(t, t->ccv(mg->d.i_phi), fcv, nrm, fac, mg->grad_nt); break;
+  case 64: launch_gradient<64>(t, t->ccv(mg->d.i_phi), fcv, nrm, fac, mg->grad_nt); break;
   default:
+  if (!fcv) return set_error(AFH_ERR_UNSUPPORTED, "i_fc = 0: box size %d", nc);
   hipLaunchKernelGGL(k_gradient, dim3((n3 + 255) / 256, ntot), dim3(256), 0,
                      t->stream, t->ccv(mg->d.i_phi), t->fcv(i_fc),
                      i_norm > 0 ? t->ccv(i_norm) : nullptr, t->d_boxes,
                      t->ids.d, nc, t->bsz, t->fsz, fac);
   }
   AFH_LAUNCH_CHECK("k_gradient");
-  int32_t e;
-  if ((e = prepare_var(mg))) return e;
   if (!mg->any_lsf) return AFH_OK;
   // electrode leaf boxes: mg_box_lpllsf_gradient, then their |E| again
   for (int l = 1; l <= t->nlvl; l++) {

@@ -228,6 +228,13 @@ struct FluxArgs {
   const double *ne;   // flux species, state s_deriv
   const double *E;    // |E| cell centred
   const double *Ef;   // face field
+  // face field from the potential (afh_fluid_set_field_source): with phi
+  // set, the kernels evaluate mg_box_lpl_gradient's face value
+  // fac / dr * (phi_f - phi_{f-1}) themselves instead of reading Ef
+  // (m_af_multigrid.f90:1882-1900): the same expression, bitwise
+  const double *phi;
+  double fac;
+  double gfac[3];     // fac / dr per dimension of this level
   double *F;          // face flux
   const double *gc2;
   DevLT td;
@@ -335,7 +342,7 @@ __device__ __forceinline__ void lt_loc(const DevLT &lt, double x, int &low,
 #ifndef AFH_FLUX_MINW
 #define AFH_FLUX_MINW 4
 #endif
-template <bool SHFL, int LIM>
+template <bool SHFL, int LIM, bool PHI = false>
 __global__ void __launch_bounds__(256, AFH_FLUX_MINW)
     k_flux_staged(FluxArgs A, const int32_t *__restrict__ ids, int nc, size_t bsz,
                   size_t fsz, unsigned long long *red) {
@@ -356,9 +363,14 @@ __global__ void __launch_bounds__(256, AFH_FLUX_MINW)
   const int c0 = (k * ng + j) * ng + i;
   const int fcell = ((k - 1) * nf + (j - 1)) * nf + (i - 1);
   const int fd = nf * nf * nf;
-  double idx[3];
+  double idx[3], gf[3];
 #pragma unroll
-  for (int d = 0; d < 3; d++) idx[d] = A.meta ? 1 / A.meta[id - 1].dr[d] : A.inv_dx[d];
+  for (int d = 0; d < 3; d++) {
+    idx[d] = A.meta ? 1 / A.meta[id - 1].dr[d] : A.inv_dx[d];
+    if (PHI) gf[d] = A.meta ? A.fac / A.meta[id - 1].dr[d] : A.gfac[d];
+  }
+  const double *__restrict__ ph = PHI ? A.phi + (size_t)(id - 1) * bsz : nullptr;
+  const double P0 = PHI ? ph[c0] : 0.0;
   const int cc[3] = {i, j, k};
   const int st[3] = {1, ng, ng * ng};
   const int fst[3] = {1, nf, nf * nf};
@@ -385,8 +397,13 @@ __global__ void __launch_bounds__(256, AFH_FLUX_MINW)
     L[d][4] = (c == nc) ? g2[(2 * d + 1) * nc * nc + gq[d]] : 0.0;
     Em[d] = E[c0 - st[d]];
     Ep[d] = need_hi[d] ? E[c0 + st[d]] : 0.0;
-    ex_lo[d] = Ef[d * fd + fcell];
-    ex_hi[d] = need_hi[d] ? Ef[d * fd + fcell + fst[d]] : 0.0;
+    if (PHI) {
+      ex_lo[d] = gf[d] * (P0 - ph[c0 - st[d]]);
+      ex_hi[d] = need_hi[d] ? gf[d] * (ph[c0 + st[d]] - P0) : 0.0;
+    } else {
+      ex_lo[d] = Ef[d * fd + fcell];
+      ex_hi[d] = need_hi[d] ? Ef[d * fd + fcell + fst[d]] : 0.0;
+    }
   }
   // 1/N at the low and high face of every dimension
   double ni_lo[3], ni_hi[3];
@@ -790,7 +807,7 @@ __device__ __forceinline__ void lds_mu_dc(const double *T, const DevLT &lt,
 #ifndef AFH_FLUX_LDS_MINW
 #define AFH_FLUX_LDS_MINW 4
 #endif
-template <int NC, int LIM>
+template <int NC, int LIM, bool PHI = false>
 __global__ void __launch_bounds__(AFH_FLUX_LDS_NT, AFH_FLUX_LDS_MINW)
     k_flux_lds(FluxArgs A, const double *__restrict__ tdi,
                const int32_t *__restrict__ ids, size_t bsz, size_t fsz,
@@ -858,10 +875,24 @@ __global__ void __launch_bounds__(AFH_FLUX_LDS_NT, AFH_FLUX_LDS_MINW)
     const int e = tid + NT * q;
     if (e < ER * EW) SE[1][e] = e_at(1, e);
   }
-  // face fields of plane 1
-  double exl = Ef[fcol], eyl = Ef[FD + fcol], ezl = Ef[2 * FD + fcol];
-  double exh = i == NC ? Ef[fcol + 1] : 0.0;
-  double eyh = (jr == TJ - 1) ? Ef[FD + fcol + NF] : 0.0;
+  // face fields of plane 1 (PHI: from the potential, k_gradient_t's
+  // expressions; pk = phi of the own cell in the current plane)
+  const double *ph = PHI ? A.phi + (size_t)(id - 1) * bsz : nullptr;
+  const double gfx = A.gfac[0], gfy = A.gfac[1], gfz = A.gfac[2];
+  double exl, eyl, ezl, exh, eyh, pk = 0.0;
+  if (PHI) {
+    const size_t c1 = SK + cc;
+    pk = ph[c1];
+    exl = gfx * (pk - ph[c1 - 1]);
+    eyl = gfy * (pk - ph[c1 - NG]);
+    ezl = gfz * (pk - ph[cc]);
+    exh = i == NC ? gfx * (ph[c1 + 1] - pk) : 0.0;
+    eyh = (jr == TJ - 1) ? gfy * (ph[c1 + NG] - pk) : 0.0;
+  } else {
+    exl = Ef[fcol], eyl = Ef[FD + fcol], ezl = Ef[2 * FD + fcol];
+    exh = i == NC ? Ef[fcol + 1] : 0.0;
+    eyh = (jr == TJ - 1) ? Ef[FD + fcol + NF] : 0.0;
+  }
   __syncthreads();
 
   // LDS indices of the own cell in the staged planes
@@ -883,14 +914,30 @@ __global__ void __launch_bounds__(AFH_FLUX_LDS_NT, AFH_FLUX_LDS_MINW)
     const double zp2 = k + 2 <= NC + 1 ? ne[(size_t)(k + 2) * SK + cc]
                                        : g2[5 * NN + gz];  // k = NC: 2nd layer
     const double ep1 = E[(size_t)(k + 1) * SK + cc];
-    double nexl = 0, neyl = 0, nezl = 0, nexh = 0, neyh = 0;
-    const double ezh = k == NC ? Ef[2 * FD + (size_t)NC * FSK + fcol] : 0.0;
-    if (more) {
-      nexl = Ef[fbn];
-      neyl = Ef[FD + fbn];
-      nezl = Ef[2 * FD + fbn];
-      if (i == NC) nexh = Ef[fbn + 1];
-      if (jr == TJ - 1) neyh = Ef[FD + fbn + NF];
+    // (PHI: the potential of plane k+1 is prefetched raw -- own cell, x-1,
+    // y-1, and x+1 / y+1 on the last column / row -- and the face fields
+    // are formed where the window advances, below)
+    double nexl = 0, neyl = 0, nezl = 0, nexh = 0, neyh = 0, npk = 0;
+    double ezh;
+    if (PHI) {
+      const size_t cn1 = (size_t)(k + 1) * SK + cc;  // own cell, plane k+1
+      ezh = k == NC ? gfz * (ph[cn1] - pk) : 0.0;
+      if (more) {
+        npk = ph[cn1];
+        nexl = ph[cn1 - 1];
+        neyl = ph[cn1 - NG];
+        if (i == NC) nexh = ph[cn1 + 1];
+        if (jr == TJ - 1) neyh = ph[cn1 + NG];
+      }
+    } else {
+      ezh = k == NC ? Ef[2 * FD + (size_t)NC * FSK + fcol] : 0.0;
+      if (more) {
+        nexl = Ef[fbn];
+        neyl = Ef[FD + fbn];
+        nezl = Ef[2 * FD + fbn];
+        if (i == NC) nexh = Ef[fbn + 1];
+        if (jr == TJ - 1) neyh = Ef[FD + fbn + NF];
+      }
     }
     const size_t fb = (size_t)(k - 1) * FSK + fcol;
     const double z0 = N0[cn], e0 = E0p[ce];
@@ -1005,7 +1052,18 @@ __global__ void __launch_bounds__(AFH_FLUX_LDS_NT, AFH_FLUX_LDS_MINW)
     zm1 = z0;
     zp1 = zp2;
     em1 = e0;
-    exl = nexl, eyl = neyl, ezl = nezl, exh = nexh, eyh = neyh;
+    if (PHI) {
+      if (more) {
+        exl = gfx * (npk - nexl);
+        eyl = gfy * (npk - neyl);
+        ezl = gfz * (npk - pk);
+        exh = i == NC ? gfx * (nexh - npk) : 0.0;
+        eyh = (jr == TJ - 1) ? gfy * (neyh - npk) : 0.0;
+      }
+      pk = npk;
+    } else {
+      exl = nexl, eyl = neyl, ezl = nezl, exh = nexh, eyh = neyh;
+    }
     __syncthreads();
   }
   for (int o = 32; o > 0; o >>= 1) {
@@ -1813,6 +1871,11 @@ struct afh_fluid {
   // s_out); rhs_state = the state it was written for (-1: none)
   int rhs_iv = 0, rhs_state = -1;
   bool rhs_ghosts = false;
+  // afh_fluid_set_field_source: the flux evaluates the face field from the
+  // potential phi_iv (fac / dr * (phi_f - phi_{f-1})) instead of reading
+  // f_field (0: read f_field)
+  int phi_iv = 0;
+  double phi_fac = -1.0;
   // write generations (afh_tree::gen) of rhs_iv and of the densities of
   // rhs_state right after the update wrote the rhs: still equal = current
   std::vector<uint64_t> rhs_snap;
@@ -2009,6 +2072,15 @@ int32_t afh_fluid_set_rhs_output(afh_fluid *f, int32_t i_rhs, int32_t ghosts) {
   return AFH_OK;
 }
 
+int32_t afh_fluid_set_field_source(afh_fluid *f, int32_t i_phi, double fac) {
+  if (!f) return set_error(AFH_ERR_ARG, "afh_fluid_set_field_source: null");
+  AFH_LIVE(f->t, "afh_fluid_set_field_source");
+  if (i_phi < 0 || i_phi > f->t->nvc) return set_error(AFH_ERR_ARG, "bad i_phi");
+  f->phi_iv = i_phi;
+  f->phi_fac = fac;
+  return AFH_OK;
+}
+
 int32_t afh_fluid_rhs_maxabs(afh_fluid *f, int32_t s_out, double *max_rhs) {
   if (!f || !max_rhs) return set_error(AFH_ERR_ARG, "afh_fluid_rhs_maxabs: null");
   AFH_LIVE(f->t, "afh_fluid_rhs_maxabs");
@@ -2091,12 +2163,11 @@ static void launch_flux_lds(afh_tree *t, const FluxArgs &A, const double *tdi,
                             int l, unsigned long long *red) {
   const dim3 grid(t->leaves.n(l) * FluxLds<NC>::NTILE);
   const size_t lds = 2 * sizeof(double) * A.td.n_points;
-  if (A.lim == AFH_LIM_KOREN)
-    hipLaunchKernelGGL((k_flux_lds<NC, AFH_LIM_KOREN>), grid, dim3(FluxLds<NC>::NT),
-                       lds, t->stream, A, tdi, t->leaves.at(l), t->bsz, t->fsz, red);
-  else
-    hipLaunchKernelGGL((k_flux_lds<NC, 0>), grid, dim3(FluxLds<NC>::NT), lds,
-                       t->stream, A, tdi, t->leaves.at(l), t->bsz, t->fsz, red);
+  const bool koren = A.lim == AFH_LIM_KOREN;
+  auto kern = A.phi ? (koren ? k_flux_lds<NC, AFH_LIM_KOREN, true> : k_flux_lds<NC, 0, true>)
+                    : (koren ? k_flux_lds<NC, AFH_LIM_KOREN> : k_flux_lds<NC, 0>);
+  hipLaunchKernelGGL(kern, grid, dim3(FluxLds<NC>::NT), lds, t->stream, A, tdi,
+                     t->leaves.at(l), t->bsz, t->fsz, red);
 }
 
 // flux_upwind_tree before the face loop (m_af_flux_schemes.f90:666-720):
@@ -2135,6 +2206,8 @@ static FluxArgs flux_args(afh_fluid *f, int iv) {
   A.ne = t->ccv(iv);
   A.E = t->ccv(f->d.i_efld);
   A.Ef = t->fcv(f->d.f_field);
+  A.phi = f->phi_iv > 0 ? t->ccv(f->phi_iv) : nullptr;
+  A.fac = f->phi_fac;
   A.F = t->fcv(f->d.f_flux);
   A.gc2 = t->gc2;
   A.td = f->td;
@@ -2233,7 +2306,10 @@ static int32_t flux_tree_dev(afh_fluid *f, int32_t s_deriv) {
   for (int l = 1; l <= t->nlvl; l++) {
     const int n = all_lvls ? (l == 1 ? t->leaves.off[t->nlvl] : 0) : t->leaves.n(l);
     if (!n) continue;
-    for (int q = 0; q < 3; q++) A.inv_dx[q] = 1 / t->lvl_dr[3 * (l - 1) + q];
+    for (int q = 0; q < 3; q++) {
+      A.inv_dx[q] = 1 / t->lvl_dr[3 * (l - 1) + q];
+      A.gfac[q] = A.fac / t->lvl_dr[3 * (l - 1) + q];  // fac / box%dr, bitwise
+    }
     if (all_lvls) A.meta = t->d_boxes;
     prof_begin(t, AFH_PROF_FLUX);
     if (lds) {
@@ -2244,8 +2320,13 @@ static int32_t flux_tree_dev(afh_fluid *f, int32_t s_deriv) {
       }
     } else {
       const bool koren = A.lim == AFH_LIM_KOREN;
-      auto kern = shfl ? (koren ? k_flux_staged<true, AFH_LIM_KOREN> : k_flux_staged<true, 0>)
-                       : (koren ? k_flux_staged<false, AFH_LIM_KOREN> : k_flux_staged<false, 0>);
+      auto kern =
+          A.phi ? (shfl ? (koren ? k_flux_staged<true, AFH_LIM_KOREN, true>
+                                 : k_flux_staged<true, 0, true>)
+                        : (koren ? k_flux_staged<false, AFH_LIM_KOREN, true>
+                                 : k_flux_staged<false, 0, true>))
+                : (shfl ? (koren ? k_flux_staged<true, AFH_LIM_KOREN> : k_flux_staged<true, 0>)
+                        : (koren ? k_flux_staged<false, AFH_LIM_KOREN> : k_flux_staged<false, 0>));
       hipLaunchKernelGGL(kern, dim3((n3 + 255) / 256, n), dim3(256), 0,
                          t->stream, A, t->leaves.at(l), nc, t->bsz, t->fsz, red);
     }
@@ -2455,7 +2536,7 @@ static int32_t fe_dev(afh_fluid *f, double dt, int32_t s_deriv, int32_t n_prev,
   const char *fused_env = getenv("AFH_FE_FUSED");
   const bool fused = fused_env && atoi(fused_env) && f->d_tdi &&
                      (nc == 16 || nc == 32 || nc == 64) && !t->any_cflux &&
-                     !f->slow_rates && f->d.n_species <= FE_MAX_SPECIES &&
+                     !f->slow_rates && f->d.n_species <= FE_MAX_SPECIES && f->phi_iv == 0 &&
                      f->rhs_iv == 0 && f->d.i_gas_dens <= 0 && f->d.i_photo <= 0 &&
                      n_prev <= 2 && !alias && f->d.limiter == AFH_LIM_KOREN;
   if (!fused) {

@@ -486,6 +486,15 @@ module m_afivo_hip
        integer(c_int32_t)        :: afh_fluid_set_rhs_output
      end function afh_fluid_set_rhs_output
 
+     !> face field of the flux from the potential i_phi (0: read f_field)
+     function afh_fluid_set_field_source(f, i_phi, fac) bind(C, name=afh_pfx//"fluid_set_field_source")
+       import
+       type(c_ptr), value        :: f
+       integer(c_int32_t), value :: i_phi
+       real(c_double), value     :: fac
+       integer(c_int32_t)        :: afh_fluid_set_field_source
+     end function afh_fluid_set_field_source
+
      !> max|rhs| of the rhs the last update wrote for state s_out
      function afh_fluid_rhs_maxabs(f, s_out, max_rhs) bind(C, name=afh_pfx//"fluid_rhs_maxabs")
        import

@@ -269,6 +269,10 @@ def main():
     ap.add_argument("--no-fused-rhs", action="store_true",
                     help="separate field_set_rhs pass instead of the rhs folded "
                          "into the density update (afh_fluid_set_rhs_output)")
+    ap.add_argument("--stored-face-field", action="store_true",
+                    help="the gradient stores the face field and the flux reads it, as "
+                         "the reference does, instead of the flux evaluating it from phi "
+                         "(afh_fluid_set_field_source)")
     ap.add_argument("--replicas", action="store_true",
                     help="N>1: one independent replica per GPU instead of sharding")
     ap.add_argument("--shard", choices=("native", "python"), default="native",
@@ -317,6 +321,15 @@ def main():
 
     if not args.no_fused_rhs and not two_d:
         case.fuse_rhs(True, ghosts=False)
+    if args.config in DRIVER_CONFIGS:
+        if args.stored_face_field and case.sim.faces_from_phi:
+            raise SystemExit("--stored-face-field: set AFH_FACES_FROM_PHI=0 for the driver configs")
+        faces_from_phi = case.sim.faces_from_phi
+    else:
+        faces_from_phi = (not args.stored_face_field and not two_d and
+                          os.environ.get("AFH_FACES_FROM_PHI", "1") != "0")
+        if faces_from_phi:
+            case.faces_from_phi(True)
     case.field_compute(0, n_vcycles=2)  # initial potential (untimed)
     for k in range(args.warmup):
         unit_step(case, dt, k)
@@ -400,6 +413,7 @@ def main():
                        "coarse_solve": ("direct" if args.coarse_cycles == 0 else
                                         "mg%d" % args.coarse_cycles),
                        "fused_rhs": "interior" if not args.no_fused_rhs else False,
+                       "face_field": "from phi in the flux" if faces_from_phi else "stored",
                        "vcycle_graphs": graphs,
                        "parallelism": ("box-shard-%d-%s" % (world, args.shard)) if sharded else
                        ("replica-per-gpu" if world > 1 else "single-gpu")},

@@ -305,7 +305,10 @@ int32_t afh_mg_fas_fmg(afh_mg *mg, int32_t set_residual, int32_t have_guess);
  * cycles of the last coarse solve (AFH_COARSE_CYCLES; 0 for the direct
  * solve); synchronises the tree's stream. */
 int32_t afh_mg_coarse_iterations(afh_mg *mg, int32_t *n);
-/* mg_compute_phi_gradient (m_af_multigrid.f90:1837-1879) incl. the norm */
+/* mg_compute_phi_gradient (m_af_multigrid.f90:1837-1879) incl. the norm.
+ * i_fc = 0 computes the norm i_norm only, on trees without electrode boxes:
+ * for a fluid whose flux takes the face field from the potential
+ * (afh_fluid_set_field_source), which never reads a stored face field. */
 int32_t afh_mg_compute_phi_gradient(afh_mg *mg, int32_t i_fc, double fac,
                                     int32_t i_norm);
 
@@ -355,6 +358,21 @@ int32_t afh_fluid_destroy(afh_fluid *f);
  * from the last update is current (field_compute may skip field_set_rhs). */
 int32_t afh_fluid_set_rhs_output(afh_fluid *f, int32_t i_rhs, int32_t ghosts);
 int32_t afh_fluid_rhs_maxabs(afh_fluid *f, int32_t s_out, double *max_rhs);
+/* Face field from the potential: with i_phi > 0 the flux
+ * (afh_flux_upwind_tree, afh_fluid_forward_euler) evaluates the face field of
+ * every face as mg_box_lpl_gradient does, fac / dr * (phi_f - phi_{f-1})
+ * (m_af_multigrid.f90:1882-1900; fac = -1 in field_from_potential,
+ * src/m_field.f90:488-505), from phi's interior and ghost cells, instead of
+ * reading f_field -- the same expression on the same values, so the fluxes
+ * are bitwise those from the stored face field, as long as phi and its
+ * ghost cells are the ones the gradient saw (field_from_potential is followed
+ * by the flux with phi untouched in m_fluid.f90 / af_advance). The stored
+ * face field is then neither written (afh_mg_compute_phi_gradient with
+ * i_fc = 0) nor read: 24 B per cell less in each of the gradient and the
+ * flux pass. Not for electrode boxes (mg_box_lpllsf_gradient) or dielectric
+ * surface corrections of the face field. i_phi = 0 (the default): read
+ * f_field. */
+int32_t afh_fluid_set_field_source(afh_fluid *f, int32_t i_phi, double fac);
 int32_t afh_fluid_rhs_valid(afh_fluid *f, int32_t s_out, int32_t *valid);
 /* electrode_species_bc over the boxes tagged mg_lsf_box (src/streamer.f90:
  * 578-636, called per step by set_electrode_densities, 569-574): in every

@@ -124,6 +124,8 @@ struct afh_fluid {
   double *td, *chem;
   afh_reaction reac[AFH_MAX_REACTIONS];
   int rhs_iv, rhs_state, rhs_ghosts; /* afo_fluid_set_rhs_output */
+  int phi_iv;     /* afo_fluid_set_field_source (0: read f_field) */
+  double phi_fac;
   double rhs_max;
   /* generations of rhs_iv and the densities of rhs_state after the update */
   unsigned long long rhs_snap[AFH_MAX_SPECIES + 1];
@@ -1586,12 +1588,23 @@ int32_t afo_mg_compute_phi_gradient(afh_mg *mg, int32_t i_fc, double fac,
                                     int32_t i_norm) {
   afh_tree *t = mg->t;
   int nc = t->nc;
+  if (i_fc < 0 || i_fc > t->nvf || i_norm < 0 || i_norm > t->nvc)
+    return fail(AFH_ERR_ARG, "bad variable index");
+  /* i_fc = 0: the norm only (afo_fluid_set_field_source); the face values
+   * go through a per-box scratch array */
+  if (i_fc == 0) {
+    int lsf = 0;
+    for (int q = 0; q < t->nb; q++) lsf |= mg->lsf_n && mg->lsf_n[q] != 0;
+    if (i_norm == 0 || lsf)
+      return fail(AFH_ERR_ARG, "i_fc = 0 needs i_norm and no electrode boxes");
+  }
   for (int lvl = 1; lvl <= t->nlvl; lvl++) {
     int n = LVL_N(t, ids, lvl);
 #pragma omp parallel for schedule(static)
     for (int q = 0; q < n; q++) {
       int id = LVL_AT(t, ids, lvl, q);
-      double *p = ccb(t, mg->d.i_phi, id), *f = fcb(t, i_fc, id);
+      double *scratch = i_fc == 0 ? malloc(sizeof(double) * t->fsz) : NULL;
+      double *p = ccb(t, mg->d.i_phi, id), *f = i_fc ? fcb(t, i_fc, id) : scratch;
       double inv[3];
       for (int d = 0; d < 3; d++) inv[d] = fac / B(t, id)->dr[d];
       for (int k = 1; k <= nc; k++)
@@ -1638,6 +1651,7 @@ int32_t afo_mg_compute_phi_gradient(afh_mg *mg, int32_t i_fc, double fac,
               o[IX(t, i, j, k)] = 0.5 * sqrt(a * a + b * b + c * c);
             }
       }
+      free(scratch);
     }
   }
   return AFH_OK;
@@ -1692,6 +1706,13 @@ int32_t afo_fluid_create(afh_tree *t, const afh_fluid_desc *d,
 int32_t afo_fluid_destroy(afh_fluid *f) {
   if (!f) return AFH_OK;
   free(f->td), free(f->chem), free(f);
+  return AFH_OK;
+}
+
+int32_t afo_fluid_set_field_source(afh_fluid *f, int32_t i_phi, double fac) {
+  if (i_phi < 0 || i_phi > f->t->nvc) return fail(AFH_ERR_ARG, "bad i_phi");
+  f->phi_iv = i_phi;
+  f->phi_fac = fac;
   return AFH_OK;
 }
 
@@ -2011,7 +2032,11 @@ static void flux_box(afh_fluid *fl, int id, int s_deriv, double *cfl_max,
   const double SI_to_Td = 1e21;
   gc2_box(t, id, i_e, cc2);
   double *ne = ccb(t, i_e, id), *E = ccb(t, fl->d.i_efld, id);
-  double *F = fcb(t, fl->d.f_flux, id), *Ef = fcb(t, fl->d.f_field, id);
+  double *F = fcb(t, fl->d.f_flux, id);
+  /* the face field: stored (f_field), or mg_box_lpl_gradient's value from
+   * the potential (afo_fluid_set_field_source) */
+  const double *Ef = fl->phi_iv ? NULL : fcb(t, fl->d.f_field, id);
+  const double *Pp = fl->phi_iv ? ccb(t, fl->phi_iv, id) : NULL;
   /* variable gas density: N_inv = 2 / (N_{f-1} + N_f) per face (m_fluid.f90:146-154) */
   const double *Ng = fl->d.i_gas_dens > 0 ? ccb(t, fl->d.i_gas_dens, id) : NULL;
   size_t ncell = (size_t)nc * nc * nc;
@@ -2035,7 +2060,16 @@ static void flux_box(afh_fluid *fl, int id, int s_deriv, double *cfl_max,
             necc[m] = ne[IX(t, p[0], p[1], p[2])];
             Nl[m] = Ng ? Ng[IX(t, p[0], p[1], p[2])] : 0.0;
           }
-          if (m >= 1 && m <= nc + 1) Ex[m - 1] = Ef[FX(t, d, p[0], p[1], p[2])];
+          if (m >= 1 && m <= nc + 1) {
+            if (Pp) {
+              int pm[3] = {p[0], p[1], p[2]};
+              pm[d] -= 1;
+              Ex[m - 1] = (fl->phi_fac / B(t, id)->dr[d]) *
+                          (Pp[IX(t, p[0], p[1], p[2])] - Pp[IX(t, pm[0], pm[1], pm[2])]);
+            } else {
+              Ex[m - 1] = Ef[FX(t, d, p[0], p[1], p[2])];
+            }
+          }
         }
 #define L(m) line[(m) + 1]
         for (int fidx = 1; fidx <= nc + 1; fidx++) {

@@ -160,6 +160,10 @@ def _replay_state(sim, name, s_deriv, s_prev, w_prev, s_out, dt, tmp_path, cwd=R
     if sim.photoi:
         sim.photoi_set_src()
     t, af = sim.tree, sim.af
+    if sim.faces_from_phi:
+        # our flux forms the face field from phi; the reference's
+        # forward_euler reads the stored one (the same values)
+        sim.mg.compute_phi_gradient(sim.f_field, -1.0, 0)
     hid = af.highest_id
     used = [b for b in range(1, hid + 1) if af.in_use[b]]
     rec = tmp_path / "step.bin"
