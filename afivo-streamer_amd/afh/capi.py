@@ -30,6 +30,7 @@ RATE_K1, RATE_K3 = 6, 8
  RATE_K12, RATE_K13, RATE_K14, RATE_K15) = range(9, 21)
 COARSE_CYCLES, COARSE_DIRECT = 1, 2
 MAX_SPECIES = 32
+MAX_IONS = 8
 MAX_REACTIONS = 128
 
 i32 = C.c_int32
@@ -87,7 +88,9 @@ class FluidDesc(C.Structure):
                 ("gas_temperature", f64), ("td_energy_col", i32),
                 ("i_gas_dens", i32), ("n_gas_species", i32),
                 ("gas_fractions", f64 * 8), ("i_photo", i32),
-                ("photo_species", i32)]
+                ("photo_species", i32), ("n_ions", i32),
+                ("ion_species", i32 * MAX_IONS), ("f_ion_flux", i32 * MAX_IONS),
+                ("ion_mobility", f64 * MAX_IONS)]
 
 
 class MgDesc(C.Structure):

@@ -189,6 +189,21 @@ class Simulation:
         self.species_itree = c.ia("species_itree")
         self.densities = c.ia("all_densities")
         self.plasma = [n for n in range(n_species) if self.species_itree[n] > 0]
+        # mobile ions (input_data%mobile_ions): flux species 2.. after the
+        # electrons (m_streamer.f90:253-282), as (plasma species index
+        # (1-based), flux face variable, scaled mobility) for the fluid
+        self.ions = []
+        n_ions = c.i("n_mobile_ions") if "n_mobile_ions" in c.d else 0
+        if n_ions:
+            fs, fv = c.ia("flux_species"), c.ia("flux_variables")
+            mob = c.ra("ion_mobilities")
+            if len(fs) != 1 + n_ions or fs[0] != self.i_electron:
+                raise NotImplementedError("electron energy equation")
+            if c.r("ion_se_yield") > 0:
+                raise NotImplementedError("secondary emission from ions (ion_se_yield)")
+            plasma_iv = [self.species_itree[n] for n in self.plasma]
+            for q in range(n_ions):
+                self.ions.append((plasma_iv.index(fs[1 + q]) + 1, fv[1 + q], float(mob[q])))
         self.N = c.r("gas_number_density")
         self.L = c.ra("domain_len")
         self.origin = c.ra("domain_origin")
@@ -297,7 +312,8 @@ class Simulation:
             i_photo=self.i_photo if self.photoi else 0,
             photo_species=self.photo_species if self.photoi else 0,
             i_gas_dens=self.i_gas_dens,
-            gas_fractions=self.gas_fractions if self.i_gas_dens else ())
+            gas_fractions=self.gas_fractions if self.i_gas_dens else (),
+            ions=self.ions)
         if self.fused_rhs:
             self.fluid.set_rhs_output(self.i_rhs, True)
         self.faces_from_phi = self._faces_from_phi_ok and self.lsf is None

@@ -358,7 +358,9 @@ class Fluid:
                  f_flux, f_field, gas_number_density, td, chem, reactions,
                  limiter=capi.LIM_KOREN, dt_chemistry_nmin=-1.0,
                  gas_temperature=300.0, td_energy_col=0, i_gas_dens=0,
-                 gas_fractions=(), i_photo=0, photo_species=0):
+                 gas_fractions=(), i_photo=0, photo_species=0, ions=()):
+        """ions: the mobile ions, [(species index (1-based into species_iv),
+        face flux variable, mobility x N)] (afh_fluid_desc n_ions ...)."""
         self.tree = tree
         self.lib = tree.lib
         d = capi.FluidDesc()
@@ -400,6 +402,9 @@ class Fluid:
         d.n_gas_species = len(gas_fractions)
         d.gas_fractions[:len(gas_fractions)] = list(gas_fractions)
         d.i_photo, d.photo_species = int(i_photo), int(photo_species)
+        d.n_ions = len(ions)  # (more than AFH_MAX_IONS: the library refuses it)
+        for q, (sp, fv, mob) in enumerate(ions[:capi.MAX_IONS]):
+            d.ion_species[q], d.f_ion_flux[q], d.ion_mobility[q] = int(sp), int(fv), float(mob)
         h = C.c_void_p()
         self.lib.call("fluid_create", tree.h, C.byref(d), C.byref(h))
         self.h = h

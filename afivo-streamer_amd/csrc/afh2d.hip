@@ -1480,8 +1480,9 @@ int32_t afh_fluid_create(afh_tree *t, const afh_fluid_desc *d, afh_fluid **out) 
   if (!t || !d || !out) return set_error(AFH_ERR_ARG, "afh_fluid_create: null");
   if (d->n_species < 1 || d->n_species > AFH_MAX_SPECIES)
     return set_error(AFH_ERR_ARG, "afh_fluid_create: n_species");
-  if (d->i_gas_dens || d->i_photo)
-    return set_error(AFH_ERR_UNSUPPORTED, "2-D: variable gas density / photoionization");
+  if (d->i_gas_dens || d->i_photo || d->n_ions)
+    return set_error(AFH_ERR_UNSUPPORTED,
+                     "2-D: variable gas density / photoionization / mobile ions");
   for (int r = 0; r < d->n_reactions; r++) {
     const int ty = d->reactions[r].rate_type;
     if (ty != AFH_RATE_TABULATED_FIELD && ty != AFH_RATE_CONSTANT && ty != AFH_RATE_LINEAR &&

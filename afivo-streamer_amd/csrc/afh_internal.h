@@ -123,6 +123,9 @@ struct afh_tree {
   // boxes up to 16^3: faces, edges and corners of a level in one launch
   // (k_gc_box, AFH_GC_BOX=0 for the two-launch form)
   bool gc_box = true;
+  // k_gc_faces pairs same-level x interfaces (one thread copies both ghost
+  // values; AFH_GC_XPAIR=0 for one thread per ghost value)
+  int gc_xpair = 0;
   // independent per-box work of every leaf level in one launch where the
   // kernel reads the box's level data from its meta record (flux of small
   // boxes, density update, residual; AFH_ALL_LVL=0: one launch per level)

@@ -2226,6 +2226,9 @@ __global__ void __launch_bounds__(1024)
 
 using namespace afh;
 
+#ifndef AFH_RSTR_K  // coarse cells per thread column of k_rstr_fas_col
+#define AFH_RSTR_K 2
+#endif
 struct afh_mg {
   afh_tree *t = nullptr;
   afh_mg_desc d;
@@ -2272,6 +2275,7 @@ struct afh_mg {
   Coef *d_lvl_c = nullptr;    // lvl_c on the device (residual of every level in one launch)
   std::vector<double> h_norm;
   bool rstr_col = true;       // AFH_RSTR_COL=0: one coarse cell per thread (k_rstr_fas)
+  int rstr_k = AFH_RSTR_K;     // coarse cells per column (AFH_RSTR_K=2|4 at run time)
   int pair_ks = 4;           // AFH_GSRB_PAIR_KS: k chunks on 64..255-box levels (NC = 64;
                              // 4 whole-box chunks, 44 quarter-box tiles x 4, 0 tiles)
   int wave_cells = CS_WAVE_CELLS;  // AFH_CS_WAVE_CELLS
@@ -2496,6 +2500,7 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
   if (const char *env = getenv("AFH_GSRB_PAIR_SP")) mg->pair_sp = atoi(env) != 0;
   if (const char *env = getenv("AFH_GRAPHS")) mg->use_graphs = atoi(env) != 0;
   if (const char *env = getenv("AFH_RSTR_COL")) mg->rstr_col = atoi(env) != 0;
+  if (const char *env = getenv("AFH_RSTR_K")) mg->rstr_k = atoi(env) == 4 ? 4 : 2;
   if (const char *env = getenv("AFH_CS_FUSED")) mg->cs_fused = atoi(env) != 0;
   if (const char *env = getenv("AFH_CS_DIRECT_SMALL")) mg->cs_direct_small = atoi(env) != 0;
   if (const char *env = getenv("AFH_PAIR_PUSH")) mg->pair_push = atoi(env) != 0;
@@ -2847,9 +2852,6 @@ static int32_t gsrb_boxes(afh_mg *mg, int lvl, bool up, bool stale_ghosts = fals
   return AFH_OK;
 }
 
-#ifndef AFH_RSTR_K  // coarse cells per thread column of k_rstr_fas_col
-#define AFH_RSTR_K 2
-#endif
 #ifndef AFH_RES_K  // cells per thread column of k_residual (8, 4 or 2)
 #define AFH_RES_K 4
 #endif
@@ -2860,9 +2862,16 @@ static int32_t update_coarse(afh_mg *mg, int lvl) {
   const LevelList &L = cst(mg, t->ids, mg->ids_c);
   const int nid = L.n(lvl);
   if (nid) {
-    constexpr int RK = AFH_RSTR_K;
-    if (mg->rstr_col && hn % RK == 0)
-      hipLaunchKernelGGL(k_rstr_fas_col<RK>, dim3((hn * hn * (hn / RK) + 255) / 256, nid),
+    // column length (AFH_RSTR_K = 2 or 4): a column reads 2K + 2 fine planes
+    // for 2K; K = 4 halves that excess at twice the centre registers
+    const int RK = mg->rstr_k;
+    if (mg->rstr_col && RK == 4 && hn % 4 == 0)
+      hipLaunchKernelGGL(k_rstr_fas_col<4>, dim3((hn * hn * (hn / 4) + 255) / 256, nid),
+                         dim3(256), 0, t->stream, t->ccv(mg->d.i_phi),
+                         t->ccv(mg->d.i_rhs), t->ccv(mg->d.i_tmp), t->d_boxes,
+                         L.at(lvl), nc, t->bsz, mg->lvl_c[lvl - 1]);
+    else if (mg->rstr_col && hn % 2 == 0)
+      hipLaunchKernelGGL(k_rstr_fas_col<2>, dim3((hn * hn * (hn / 2) + 255) / 256, nid),
                          dim3(256), 0, t->stream, t->ccv(mg->d.i_phi),
                          t->ccv(mg->d.i_rhs), t->ccv(mg->d.i_tmp), t->d_boxes,
                          L.at(lvl), nc, t->bsz, mg->lvl_c[lvl - 1]);

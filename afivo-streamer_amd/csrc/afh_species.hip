@@ -236,6 +236,10 @@ struct FluxArgs {
   double fac;
   double gfac[3];     // fac / dr per dimension of this level
   double *F;          // face flux
+  // with mobile ions: the electrons' mu u per face (their share of the
+  // dielectric relaxation sum, m_fluid.f90:196, 207-214) is stored here for
+  // k_flux_ion, which folds the maximum of the sum (null: folded here)
+  double *sig;
   const double *gc2;
   DevLT td;
   double N_inv;
@@ -465,6 +469,7 @@ __global__ void __launch_bounds__(256, AFH_FLUX_MINW)
     const double flux = vl[d] * u - dl[d] * idx[d] * (L[d][2] - L[d][1]);
     if (active) F[d * fd + fcell] = flux;
     smax = fmax(smax, mu * u);
+    if (A.sig && active) A.sig[(size_t)(id - 1) * fsz + d * fd + fcell] = mu * u;
   }
   // x partner by lane shuffle: executed by every lane (a shuffle reading an
   // inactive lane returns 0, so never inside the divergent branch below)
@@ -486,6 +491,7 @@ __global__ void __launch_bounds__(256, AFH_FLUX_MINW)
       const double flux = vh * u - dh * inv_dx * (L[d][3] - L[d][2]);
       if (active) F[d * fd + fcell + fst[d]] = flux;
       smax = fmax(smax, mu * u);
+      if (A.sig && active) A.sig[(size_t)(id - 1) * fsz + d * fd + fcell + fst[d]] = mu * u;
     } else if (d == 0 && SHFL) {
       vh = vsh;
       dh = dsh;
@@ -500,6 +506,7 @@ __global__ void __launch_bounds__(256, AFH_FLUX_MINW)
     cfl = cfl + (1.0 * mv * inv_dx + 2 * md * (inv_dx * inv_dx));
   }
   if (!active) cfl = smax = -HUGE_VAL;
+  if (A.sig) smax = -HUGE_VAL;  // k_flux_ion folds the sum
   for (int o = 32; o > 0; o >>= 1) {
     cfl = fmax(cfl, __shfl_xor(cfl, o, 64));
     smax = fmax(smax, __shfl_xor(smax, o, 64));
@@ -512,6 +519,90 @@ __global__ void __launch_bounds__(256, AFH_FLUX_MINW)
     for (int q = 1; q < (int)(blockDim.x >> 6); q++)
       cfl = fmax(cfl, r1[q]), smax = fmax(smax, r2[q]);
     atomicMax(&red[red_shard()], dbl_to_ord(cfl));
+    atomicMax(&red[RED_SHARDS + red_shard()], dbl_to_ord(smax));
+  }
+}
+
+// ------------------------------------------------------------ mobile ions
+// The ion part of the m_fluid flux_upwind callback (src/m_fluid.f90:207-214)
+// for every face of a leaf: mu = mobility N_inv, v = sign(q) mu E_f, flux =
+// v u_f with u_f reconstruct_upwind_1d's Koren-limited upwind value along
+// sign(q) E_f (flux_direction, m_fluid.f90:216-232; the second ghost layer
+// of each ion from its own gc2 buffer); sigma = the electrons' mu u_f (from
+// k_flux_staged) + mu u_f of each ion in flux-species order, its maximum
+// folded into slot 1 (the dielectric relaxation limit). One thread per
+// cell: the low face of each dimension, the high face on the box's last
+// cell. Same expressions as the reference's array statements, bitwise.
+struct IonArgs {
+  int n;
+  const double *ni[AFH_MAX_IONS];   // ion densities, state s_deriv
+  double *F[AFH_MAX_IONS];          // their face fluxes
+  const double *gc2[AFH_MAX_IONS];  // their second ghost layers [box][6][nc][nc]
+  double mob[AFH_MAX_IONS];         // mobility x N (the reference's scaled value)
+  double sgn[AFH_MAX_IONS];         // flux_species_charge_sign
+};
+
+template <int LIM, bool PHI>
+__global__ void __launch_bounds__(256)
+    k_flux_ion(FluxArgs A, IonArgs I, const int32_t *__restrict__ ids, int nc, size_t bsz,
+               size_t fsz, unsigned long long *red) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool active = t < nc * nc * nc;
+  const int tt = active ? t : 0;
+  const int id = ids[blockIdx.y];
+  int i, j, k;
+  cell3(tt, nc, i, j, k);
+  const int ng = nc + 2, nf = nc + 1;
+  const size_t ob = (size_t)(id - 1) * bsz, of = (size_t)(id - 1) * fsz;
+  const double *__restrict__ Ef = A.Ef + of;
+  const double *__restrict__ ph = PHI ? A.phi + ob : nullptr;
+  const double *__restrict__ Ng = A.Ng ? A.Ng + ob : nullptr;
+  const int c0 = (k * ng + j) * ng + i;
+  const int fcell = ((k - 1) * nf + (j - 1)) * nf + (i - 1);
+  const int fd = nf * nf * nf, nn = nc * nc;
+  const int cc[3] = {i, j, k};
+  const int st[3] = {1, ng, ng * ng};
+  const int fst[3] = {1, nf, nf * nf};
+  const int gq[3] = {(k - 1) * nc + (j - 1), (k - 1) * nc + (i - 1), (j - 1) * nc + (i - 1)};
+  double smax = -HUGE_VAL;
+  for (int d = 0; d < 3; d++) {
+    const double gf = PHI ? (A.meta ? A.fac / A.meta[id - 1].dr[d] : A.gfac[d]) : 0.0;
+    for (int hi = 0; hi < 2; hi++) {
+      if (hi && cc[d] != nc) continue;
+      const int fi = d * fd + fcell + (hi ? fst[d] : 0);
+      const int cl = c0 - st[d] + (hi ? st[d] : 0);  // cell f-1; cl + st[d] is cell f
+      const double ex = PHI ? gf * (ph[cl + st[d]] - ph[cl]) : Ef[fi];
+      const double ni = Ng ? 2 / (Ng[cl] + Ng[cl + st[d]]) : A.N_inv;
+      double sigma = A.sig[of + fi];
+      for (int n = 0; n < I.n; n++) {
+        const double *L = I.ni[n] + ob;
+        const double *g2 = I.gc2[n] + (size_t)(id - 1) * 6 * nn;
+        const double Lm1 = L[cl], L0 = L[cl + st[d]];
+        // L(f-2): second ghost layer below the box's first cell
+        const double Lm2 = (!hi && cc[d] == 1) ? g2[(2 * d) * nn + gq[d]] : L[cl - st[d]];
+        // L(f+1): second ghost layer above the box's last cell
+        const double Lp1 = hi ? g2[(2 * d + 1) * nn + gq[d]] : L[cl + 2 * st[d]];
+        double u;
+        if (I.sgn[n] * ex > 0)
+          u = Lm1 + 0.5 * limiter_t<LIM>(A.lim, L0 - Lm1, Lm1 - Lm2);
+        else
+          u = L0 - 0.5 * limiter_t<LIM>(A.lim, L0 - Lm1, Lp1 - L0);
+        const double mu = I.mob[n] * ni;
+        const double v = I.sgn[n] * mu * ex;
+        if (active) I.F[n][of + fi] = v * u;
+        sigma = sigma + mu * u;
+      }
+      smax = fmax(smax, sigma);
+    }
+  }
+  if (!active) smax = -HUGE_VAL;
+  for (int o = 32; o > 0; o >>= 1) smax = fmax(smax, __shfl_xor(smax, o, 64));
+  __shared__ double r2[4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) r2[w] = smax;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int q = 1; q < (int)(blockDim.x >> 6); q++) smax = fmax(smax, r2[q]);
     atomicMax(&red[RED_SHARDS + red_shard()], dbl_to_ord(smax));
   }
 }
@@ -559,6 +650,11 @@ struct UpdArgs {
   // slot photo_s after the chemistry limit (m_fluid.f90:435-440)
   const double *photo;
   int photo_s;
+  // mobile ions: species slot and face flux of each (their flux divergence
+  // is added as the electrons', flux_update_densities over i_cc_flux)
+  int n_ion;
+  int ion_s[AFH_MAX_IONS];
+  const double *Fion[AFH_MAX_IONS];
 };
 
 // Register-resident species arrays indexed by runtime reaction data (the
@@ -1251,6 +1347,16 @@ __global__ void __launch_bounds__(256, AFH_UPD_MINW)
 #pragma unroll
     for (int s = 0; s < NS; s++)
       if (s == A.e_index) y[s] = y[s] + div + dvy + dvz;
+    for (int n = 0; n < A.n_ion; n++) {
+      const double *G = A.Fion[n] + (size_t)(id - 1) * fsz;
+      const double gx0 = G[f0], gx1 = G[f0 + 1], gy0 = G[d3 + f0], gy1 = G[d3 + f0 + nf],
+                   gz0 = G[2 * d3 + f0], gz1 = G[2 * d3 + f0 + nf * nf];
+      const double ix_ = dtr[0] * (gx0 - gx1), iy_ = dtr[1] * (gy0 - gy1),
+                   iz_ = dtr[2] * (gz0 - gz1);
+#pragma unroll
+      for (int s = 0; s < NS; s++)
+        if (s == A.ion_s[n]) y[s] = y[s] + ix_ + iy_ + iz_;
+    }
 #pragma unroll
     for (int s = 0; s < NS; s++) st_nt<AFH_NT_UPD>(A.out[s] + x, y[s]);
     if (A.rhs) {
@@ -1876,6 +1982,9 @@ struct afh_fluid {
   // f_field (0: read f_field)
   int phi_iv = 0;
   double phi_fac = -1.0;
+  // mobile ions: second ghost layers of each ion [ion][box][6][nc][nc] and
+  // the electrons' mu u per face (k_flux_staged -> k_flux_ion)
+  double *d_gc2_ion = nullptr, *d_sig = nullptr;
   // write generations (afh_tree::gen) of rhs_iv and of the densities of
   // rhs_state right after the update wrote the rhs: still equal = current
   std::vector<uint64_t> rhs_snap;
@@ -1940,9 +2049,27 @@ int32_t afh_fluid_create(afh_tree *t, const afh_fluid_desc *d, afh_fluid **out) 
     AFH_HIP(hipMalloc(&f->d_chem_rm, nch * sizeof(double)));
     AFH_HIP(hipMemcpy(f->d_chem_rm, rm.data(), nch * sizeof(double), hipMemcpyHostToDevice));
   }
+  if (d->n_ions < 0 || d->n_ions > AFH_MAX_IONS)
+    return set_error(AFH_ERR_ARG, "bad mobile ion count");
+  for (int q = 0; q < d->n_ions; q++) {
+    const int sp = d->ion_species[q];
+    if (sp < 1 || sp > d->n_species || sp - 1 == f->e_index || d->species_charge[sp - 1] == 0)
+      return set_error(AFH_ERR_ARG, "mobile ion %d: bad species", q + 1);
+    if (d->f_ion_flux[q] < 1 || d->f_ion_flux[q] > t->nvf || d->f_ion_flux[q] == d->f_flux)
+      return set_error(AFH_ERR_ARG, "mobile ion %d: bad flux variable", q + 1);
+    if (!t->meth[d->species_iv[sp - 1]].set)
+      return set_error(AFH_ERR_STATE, "set cc methods for mobile ion %d first", q + 1);
+  }
+  if (d->n_ions > 0) {
+    AFH_HIP(hipMalloc(&f->d_gc2_ion,
+                      sizeof(double) * d->n_ions * (size_t)t->cap * 6 * t->nc * t->nc));
+    AFH_HIP(hipMalloc(&f->d_sig, sizeof(double) * (size_t)t->cap * t->fsz));
+  }
   const char *staged_env = getenv("AFH_FLUX_STAGED");
-  // a variable gas density takes k_flux_staged (per-face 1/N)
-  if (!gas && d->td.n_points <= FLUX_LDS_MAX_POINTS && !(staged_env && atoi(staged_env))) {
+  // a variable gas density takes k_flux_staged (per-face 1/N); so do mobile
+  // ions (k_flux_staged hands the electrons' mu u to k_flux_ion)
+  if (!gas && d->n_ions == 0 && d->td.n_points <= FLUX_LDS_MAX_POINTS &&
+      !(staged_env && atoi(staged_env))) {
     const int n = d->td.n_points;
     std::vector<double> ti(2 * (size_t)n);
     for (int r = 0; r < n; r++) {
@@ -2019,6 +2146,8 @@ int32_t afh_fluid_destroy(afh_fluid *f) {
   hipFree(f->d_reac);
   hipFree(f->d_tdi);
   hipFree(f->d_ids);
+  hipFree(f->d_gc2_ion);
+  hipFree(f->d_sig);
   delete f;
   return AFH_OK;
 }
@@ -2172,7 +2301,7 @@ static void launch_flux_lds(afh_tree *t, const FluxArgs &A, const double *tdi,
 
 // flux_upwind_tree before the face loop (m_af_flux_schemes.f90:666-720):
 // af_restrict_ref_boundary, then two ghost layers of the flux species
-static int32_t flux_prelude(afh_fluid *f, int iv) {
+static int32_t flux_prelude(afh_fluid *f, int iv, double *gc2) {
   afh_tree *t = f->t;
   const int nc = t->nc;
   int32_t e;
@@ -2188,7 +2317,7 @@ static int32_t flux_prelude(afh_fluid *f, int iv) {
     const int n = t->leaves.n(l);
     if (n) {
       hipLaunchKernelGGL(k_gc2, dim3((nc * nc + 255) / 256, 6, n), dim3(256),
-                         0, t->stream, t->ccv(iv), t->gc2, t->d_boxes,
+                         0, t->stream, t->ccv(iv), gc2, t->d_boxes,
                          t->leaves.at(l), nc, t->bsz, t->gc_args(iv));
       AFH_LAUNCH_CHECK("k_gc2");
     }
@@ -2208,6 +2337,7 @@ static FluxArgs flux_args(afh_fluid *f, int iv) {
   A.Ef = t->fcv(f->d.f_field);
   A.phi = f->phi_iv > 0 ? t->ccv(f->phi_iv) : nullptr;
   A.fac = f->phi_fac;
+  A.sig = f->d.n_ions > 0 ? f->d_sig : nullptr;
   A.F = t->fcv(f->d.f_flux);
   A.gc2 = t->gc2;
   A.td = f->td;
@@ -2271,6 +2401,11 @@ static int32_t upd_args(afh_fluid *f, double dt, int32_t s_deriv, int32_t n_prev
   A.dt_chemistry_nmin = f->d.dt_chemistry_nmin;
   A.photo = f->d.i_photo > 0 ? t->ccv(f->d.i_photo) : nullptr;
   A.photo_s = f->d.photo_species - 1;
+  A.n_ion = f->d.n_ions;
+  for (int q = 0; q < AFH_MAX_IONS; q++) {
+    A.ion_s[q] = q < A.n_ion ? f->d.ion_species[q] - 1 : -1;
+    A.Fion[q] = q < A.n_ion ? t->fcv(f->d.f_ion_flux[q]) : nullptr;
+  }
   A.meta = nullptr;
   // algorithmic bytes per cell: each distinct species state read once, the
   // output written once, |E| and 3 fluxes read
@@ -2294,7 +2429,14 @@ static int32_t flux_tree_dev(afh_fluid *f, int32_t s_deriv) {
   if (iv < 1 || iv > t->nvc) return set_error(AFH_ERR_ARG, "bad s_deriv");
   t->touch(iv);  // ghost layers written back
   int32_t e;
-  if ((e = flux_prelude(f, iv))) return e;
+  if ((e = flux_prelude(f, iv, t->gc2))) return e;
+  // every flux species (af_restrict_ref_boundary and af_gc2_box over i_cc)
+  const size_t g2sz = (size_t)t->cap * 6 * nc * nc;
+  for (int n = 0; n < f->d.n_ions; n++) {
+    const int ivn = f->d.species_iv[f->d.ion_species[n] - 1] + s_deriv;
+    t->touch(ivn);
+    if ((e = flux_prelude(f, ivn, f->d_gc2_ion + n * g2sz))) return e;
+  }
   if ((e = red_init(t, 0, -HUGE_VAL)) || (e = red_init(t, 1, -HUGE_VAL))) return e;
   auto *red = reinterpret_cast<unsigned long long *>(t->scratch);
   FluxArgs A = flux_args(f, iv);
@@ -2333,15 +2475,37 @@ static int32_t flux_tree_dev(afh_fluid *f, int32_t s_deriv) {
     // read n_e, |E|, 3 face fields; write 3 fluxes = 64 B/cell
     prof_end(t, AFH_PROF_FLUX, 64.0 * n3 * n);
     AFH_LAUNCH_CHECK("k_flux");
+    if (f->d.n_ions > 0) {
+      IonArgs I;
+      I.n = f->d.n_ions;
+      for (int q = 0; q < I.n; q++) {
+        const int sp = f->d.ion_species[q] - 1;
+        I.ni[q] = t->ccv(f->d.species_iv[sp] + s_deriv);
+        I.F[q] = t->fcv(f->d.f_ion_flux[q]);
+        I.gc2[q] = f->d_gc2_ion + q * g2sz;
+        I.mob[q] = f->d.ion_mobility[q];
+        I.sgn[q] = f->d.species_charge[sp] > 0 ? 1.0 : -1.0;
+      }
+      const bool koren = A.lim == AFH_LIM_KOREN;
+      auto kern = A.phi ? (koren ? k_flux_ion<AFH_LIM_KOREN, true> : k_flux_ion<0, true>)
+                        : (koren ? k_flux_ion<AFH_LIM_KOREN, false> : k_flux_ion<0, false>);
+      hipLaunchKernelGGL(kern, dim3((n3 + 255) / 256, n), dim3(256), 0, t->stream, A, I,
+                         t->leaves.at(l), nc, t->bsz, t->fsz, red);
+      AFH_LAUNCH_CHECK("k_flux_ion");
+    }
   }
+  // af_consistent_fluxes over every flux variable (i_flux)
   const int ntask = t->cflux.off[t->nlvl];
-  if (ntask) {
-    hipLaunchKernelGGL(k_consistent, dim3((nc * nc + 255) / 256, ntask),
-                       dim3(256), 0, t->stream, t->fcv(f->d.f_flux), t->d_boxes,
-                       t->cflux.d, nc, t->fsz);
-    AFH_LAUNCH_CHECK("k_consistent");
+  for (int q = -1; q < f->d.n_ions; q++) {
+    const int fv = q < 0 ? f->d.f_flux : f->d.f_ion_flux[q];
+    if (ntask) {
+      hipLaunchKernelGGL(k_consistent, dim3((nc * nc + 255) / 256, ntask),
+                         dim3(256), 0, t->stream, t->fcv(fv), t->d_boxes,
+                         t->cflux.d, nc, t->fsz);
+      AFH_LAUNCH_CHECK("k_consistent");
+    }
+    if ((e = call_hook(t, AFH_HOOK_CFLUX, 0, fv))) return e;
   }
-  if ((e = call_hook(t, AFH_HOOK_CFLUX, 0, f->d.f_flux))) return e;
   if ((e = red_finish(t, 0, true))) return e;
   return red_finish(t, 1, true);
 }
@@ -2548,7 +2712,7 @@ static int32_t fe_dev(afh_fluid *f, double dt, int32_t s_deriv, int32_t n_prev,
   t->touch(iv);
   f->touch_state(s_out);
   f->rhs_state = -1;
-  if ((e = flux_prelude(f, iv))) return e;
+  if ((e = flux_prelude(f, iv, t->gc2))) return e;
   if ((e = red_init(t, 0, -HUGE_VAL)) || (e = red_init(t, 1, -HUGE_VAL)) ||
       (e = red_init(t, 2, 1e100)))
     return e;

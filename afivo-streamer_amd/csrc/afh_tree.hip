@@ -74,7 +74,7 @@ __global__ void k_gc_faces(double *__restrict__ v,
                            const double *__restrict__ vc,
                            const afh_box_meta *__restrict__ meta,
                            const int32_t *__restrict__ ids, int nc, size_t bsz,
-                           GcArgs ga) {
+                           GcArgs ga, int xpair) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= nc * nc) return;
   const int id = ids[blockIdx.z];
@@ -101,6 +101,24 @@ __global__ void k_gc_faces(double *__restrict__ v,
   const size_t dst = ix3(ng, p[0], p[1], p[2]);
 
   if (nb_id > 0) {
+    if (xpair && d == 0 && meta[nb_id - 1].lvl > 0) {
+      // x interface with a stored same-level box, copied both ways by the
+      // low-x thread of the box on its high side: its own ghost (0, a, b)
+      // and the neighbour's ghost (nc+1, a, b) sit in the lines of the two
+      // interior values it reads (row start of this box, row end of the
+      // neighbour), so each line is read once and written back once instead
+      // of being fetched by two faces. (The sentinel id of a sharded tree,
+      // level 0, stands for boxes the rank does not store: never written.)
+      // xpair: ids is every stored box of the level (a whole-level fill),
+      // so every such interface has its low-x thread in the launch
+      if (!low) return;  // the neighbour's low-x thread copies this one
+      double *cn = v + (size_t)(nb_id - 1) * bsz;
+      const size_t sa = ix3(ng, nc, a, b), sb = ix3(ng, 1, a, b);
+      const double va = cn[sa], vb = c[sb];
+      c[dst] = va;
+      cn[sa + 1] = vb;
+      return;
+    }
     // copy_from_nb: ghost(lo) = neighbor(lo - dnb * nc)
     int q[3] = {p[0], p[1], p[2]};
     q[d] = low ? nc : 1;
@@ -365,7 +383,8 @@ int32_t gc_lvl_var(afh_tree *t, int lvl, int iv, const double *vc,
                            t->stream, v, vc, t->d_boxes, t->ids.at(lvl), nc, t->bsz, ga);
       else
         hipLaunchKernelGGL(k_gc_faces, dim3((nc * nc + 255) / 256, 6, n), dim3(256), 0,
-                           t->stream, v, vc, t->d_boxes, t->ids.at(lvl), nc, t->bsz, ga);
+                           t->stream, v, vc, t->d_boxes, t->ids.at(lvl), nc, t->bsz, ga,
+                           t->gc_xpair);
       // algorithmic bytes: read one interior layer + write one ghost layer
       prof_end(t, AFH_PROF_GHOST, 16.0 * 6 * nc * nc * n);
       AFH_LAUNCH_CHECK("k_gc_faces");
@@ -792,6 +811,7 @@ static int32_t tree_create_impl(const afh_tree_desc *d, int32_t device,
   if (const char *env = getenv("AFH_ALL_LVL")) t->all_lvl_launch = atoi(env) != 0;
   if (const char *env = getenv("AFH_GC_FACES6")) t->gc_faces6 = atoi(env) != 0;
   else t->gc_faces6 = -1;  // by box size
+  if (const char *env = getenv("AFH_GC_XPAIR")) t->gc_xpair = atoi(env) != 0;
   if (device >= 0) {
     AFH_HIP(hipSetDevice(device));
     t->device = device;
@@ -1461,7 +1481,7 @@ int32_t afh_tree_regrid(afh_tree *o, const afh_tree_desc *d, afh_tree **out) {
     for (int iv : t->auto_vars) {
       hipLaunchKernelGGL(k_gc_faces, dim3((nc * nc + 255) / 256, 6, n), dim3(256), 0,
                          t->stream, t->ccv(iv), t->ccv(iv), t->d_boxes, d_list, nc,
-                         t->bsz, t->gc_args(iv));
+                         t->bsz, t->gc_args(iv), 0);  // new boxes only: no pairing
       AFH_LAUNCH_CHECK("k_gc_faces");
       hipLaunchKernelGGL(k_gc_corners, dim3(n), dim3(256), 0, t->stream, t->ccv(iv),
                          t->d_boxes, d_list, nc, t->bsz);

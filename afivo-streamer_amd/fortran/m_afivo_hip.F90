@@ -136,6 +136,7 @@ module m_afivo_hip
   integer(c_int32_t), parameter :: AFH_RM_REF = -1, AFH_KEEP_REF = 0, AFH_DO_REF = 1
   integer, parameter :: AFH_MAX_REFINE_REGIONS = 8
   integer, parameter :: AFH_MAX_GAS_SPECIES = 8
+  integer, parameter :: AFH_MAX_IONS = 8
 
   !> default_refinement's parameters (src/m_refine.f90:10-60)
   type, bind(C) :: afh_refine_desc
@@ -184,6 +185,10 @@ module m_afivo_hip
      real(c_double)     :: gas_fractions(AFH_MAX_GAS_SPECIES) = 0
      integer(c_int32_t) :: i_photo = 0          ! photoionization rate (0: none)
      integer(c_int32_t) :: photo_species = 0
+     integer(c_int32_t) :: n_ions = 0              ! mobile ions (0: electrons only)
+     integer(c_int32_t) :: ion_species(AFH_MAX_IONS) = 0
+     integer(c_int32_t) :: f_ion_flux(AFH_MAX_IONS) = 0
+     real(c_double)     :: ion_mobility(AFH_MAX_IONS) = 0
   end type afh_fluid_desc
 
   type, bind(C) :: afh_mg_desc

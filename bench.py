@@ -239,7 +239,7 @@ def pmc_traffic(config):
     return None
 
 
-def write_topology(case, config, path):
+def write_topology(case, config, path, faces_from_phi=False):
     """Boxes, leaves and parents per level, the box size and the species
     counts of the benchmarked tree (scripts/prof_steady.py)."""
     topo = case.topo
@@ -253,7 +253,8 @@ def write_topology(case, config, path):
         json.dump({"config": config, "nc": int(topo["nc"]), "ids": cnt("ids"),
                    "leaves": cnt("leaves"), "parents": cnt("parents"),
                    "n_species": len(charges),
-                   "n_charged": sum(1 for q in charges if q != 0)}, f)
+                   "n_charged": sum(1 for q in charges if q != 0),
+                   "faces_from_phi": bool(faces_from_phi)}, f)
 
 
 def main():
@@ -388,7 +389,7 @@ def main():
 
     if rank == 0 and os.environ.get("AFH_BENCH_TOPO"):
         # the run's topology for scripts/prof_steady.py's byte model
-        write_topology(case, args.config, os.environ["AFH_BENCH_TOPO"])
+        write_topology(case, args.config, os.environ["AFH_BENCH_TOPO"], faces_from_phi)
 
     if rank == 0:
         avg_s = ms.value / 1e3 / max(1, nl.value)

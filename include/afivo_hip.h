@@ -89,6 +89,7 @@ extern "C" {
 
 #define AFH_MAX_SPECIES 32
 #define AFH_MAX_GAS_SPECIES 8
+#define AFH_MAX_IONS 8
 #define AFH_MAX_REACTIONS 128
 
 /* Topology of one box: the box_t fields the hot path reads
@@ -193,6 +194,20 @@ typedef struct afh_fluid_desc {
    * species_iv, photoi_species_index) after the chemistry time step limit. */
   int32_t i_photo;
   int32_t photo_species;
+  /* Mobile ions (input_data%mobile_ions / ion_mobilities,
+   * m_transport_data.f90:195-215; flux species 2.. of m_streamer.f90:
+   * 253-282): n_ions plasma species (1-based index into species_iv) that
+   * move with the field. Each has the face flux variable f_ion_flux and the
+   * mobility times the gas density the reference scales it to
+   * (ion_mobilities * 1e5 / (k_B 300 K)); its flux is
+   * sign(q) mu N_inv E_f u_f with the Koren-limited upwind value u_f
+   * (upwind along sign(q) E_f, no diffusion), its mu u_f adds to the
+   * electrons' in the dielectric relaxation limit, and its CFL is ignored
+   * (m_fluid.f90:207-214). 0: electrons only. */
+  int32_t n_ions;
+  int32_t ion_species[AFH_MAX_IONS];
+  int32_t f_ion_flux[AFH_MAX_IONS];
+  double ion_mobility[AFH_MAX_IONS];
 } afh_fluid_desc;
 
 /* Multigrid options, mg_t (m_af_types.f90:572-665) + coarse solver. */

@@ -1668,6 +1668,16 @@ int32_t afo_fluid_create(afh_tree *t, const afh_fluid_desc *d,
       (d->i_gas_dens > t->nvc || d->n_gas_species < 0 ||
        d->n_gas_species > AFH_MAX_GAS_SPECIES))
     return fail(AFH_ERR_ARG, "bad gas density variable / gas species count");
+  if (d->n_ions < 0 || d->n_ions > AFH_MAX_IONS)
+    return fail(AFH_ERR_ARG, "bad mobile ion count");
+  for (int q = 0; q < d->n_ions; q++) {
+    const int sp = d->ion_species[q];
+    if (sp < 1 || sp > d->n_species || d->species_iv[sp - 1] == d->i_electron ||
+        d->species_charge[sp - 1] == 0)
+      return fail(AFH_ERR_ARG, "mobile ion: bad species");
+    if (d->f_ion_flux[q] < 1 || d->f_ion_flux[q] > t->nvf || d->f_ion_flux[q] == d->f_flux)
+      return fail(AFH_ERR_ARG, "mobile ion: bad flux variable");
+  }
   const int ng = d->i_gas_dens > 0 ? d->n_gas_species : 0;
   for (int r = 0; r < d->n_reactions; r++) {
     const afh_reaction *R = &d->reactions[r];
@@ -2023,14 +2033,28 @@ static void gc2_box(afh_tree *t, int id, int iv, double *cc) {
  * (282-303) and the m_fluid callbacks flux_direction / flux_upwind
  * (src/m_fluid.f90:102-227) for electrons, constant N, LFA. Returns the box
  * maxima of cfl_sum and sigma. */
+/* value m (-1 .. nc+2) of the line along dim d at (a, b) of an enlarged box */
+static double line_at(const double *cc2, int n4, int d, int a, int b, int m) {
+  int p[3];
+  if (d == 0) p[0] = m, p[1] = a, p[2] = b;
+  else if (d == 1) p[0] = a, p[1] = m, p[2] = b;
+  else p[0] = a, p[1] = b, p[2] = m;
+  return cc2[I2(n4, p[0], p[1], p[2])];
+}
+
 static void flux_box(afh_fluid *fl, int id, int s_deriv, double *cfl_max,
-                     double *sig_max, double *cc2, double *cfl) {
+                     double *sig_max, double *cc2, double *cfl, double *cc2i) {
   afh_tree *t = fl->t;
   int nc = t->nc, n4 = nc + 4;
   int i_e = fl->d.i_electron + s_deriv;
   const double N_inv = 1 / fl->d.gas_number_density;
   const double SI_to_Td = 1e21;
   gc2_box(t, id, i_e, cc2);
+  /* mobile ions (flux species 2.., m_streamer.f90:253-282): their own two
+   * ghost layers (af_gc2_box over every flux species) */
+  const size_t n4c = (size_t)n4 * n4 * n4;
+  for (int q = 0; q < fl->d.n_ions; q++)
+    gc2_box(t, id, fl->d.species_iv[fl->d.ion_species[q] - 1] + s_deriv, cc2i + q * n4c);
   double *ne = ccb(t, i_e, id), *E = ccb(t, fl->d.i_efld, id);
   double *F = fcb(t, fl->d.f_flux, id);
   /* the face field: stored (f_field), or mg_box_lpl_gradient's value from
@@ -2094,11 +2118,30 @@ static void flux_box(afh_fluid *fl, int id, int s_deriv, double *cfl_max,
           double flux = v[fidx - 1] * u[fidx - 1] -
                         dcf * inv_dx * (necc[fidx] - necc[fidx - 1]);
           double sigma = mu * u[fidx - 1];
-          if (sigma > smax) smax = sigma;
           int p[3];
           if (d == 0) p[0] = fidx, p[1] = a, p[2] = b;
           else if (d == 1) p[0] = a, p[1] = fidx, p[2] = b;
           else p[0] = a, p[1] = b, p[2] = fidx;
+          /* ion fluxes (m_fluid.f90:207-214): mu = mobility N_inv,
+           * v = sign mu E_x, flux = v u; sigma = sigma + mu u */
+          for (int q = 0; q < fl->d.n_ions; q++) {
+            const double *c2 = cc2i + q * n4c;
+            const double sg = fl->d.species_charge[fl->d.ion_species[q] - 1] > 0 ? 1.0 : -1.0;
+            const double Lm2 = line_at(c2, n4, d, a, b, fidx - 2);
+            const double Lm1 = line_at(c2, n4, d, a, b, fidx - 1);
+            const double L0 = line_at(c2, n4, d, a, b, fidx);
+            const double Lp1 = line_at(c2, n4, d, a, b, fidx + 1);
+            double ui;
+            if (sg * Ex[fidx - 1] > 0)
+              ui = Lm1 + 0.5 * limiter(fl->d.limiter, L0 - Lm1, Lm1 - Lm2);
+            else
+              ui = L0 - 0.5 * limiter(fl->d.limiter, L0 - Lm1, Lp1 - L0);
+            const double mui = fl->d.ion_mobility[q] * ni;
+            const double vi = sg * mui * Ex[fidx - 1];
+            fcb(t, fl->d.f_ion_flux[q], id)[FX(t, d, p[0], p[1], p[2])] = vi * ui;
+            sigma = sigma + mui * ui;
+          }
+          if (sigma > smax) smax = sigma;
           F[FX(t, d, p[0], p[1], p[2])] = flux;
         }
         for (int c = 1; c <= nc; c++) {
@@ -2184,20 +2227,31 @@ int32_t afo_flux_upwind_tree(afh_fluid *f, int32_t s_deriv, double *dt_lim) {
   int nc = t->nc;
   touch(t, f->d.i_electron + s_deriv); /* ghost layers written back */
   if (restrict_ref_boundary(t, f->d.i_electron + s_deriv)) return AFH_ERR_STATE;
+  for (int q = 0; q < f->d.n_ions; q++) {
+    const int iv = f->d.species_iv[f->d.ion_species[q] - 1] + s_deriv;
+    touch(t, iv);
+    if (restrict_ref_boundary(t, iv)) return AFH_ERR_STATE;
+  }
   double cfl_max = -HUGE_VAL, sig_max = -HUGE_VAL;
   for (int l = 1; l <= t->nlvl; l++) {
     int n = LVL_N(t, leaves, l);
     if (hook(t, AFH_HOOK_HALO, l, f->d.i_electron + s_deriv, NULL, 0))
       return AFH_ERR_STATE;
+    for (int q = 0; q < f->d.n_ions; q++)
+      if (hook(t, AFH_HOOK_HALO, l, f->d.species_iv[f->d.ion_species[q] - 1] + s_deriv,
+               NULL, 0))
+        return AFH_ERR_STATE;
 #pragma omp parallel
     {
       double *cc2 = malloc(sizeof(double) * (size_t)(nc + 4) * (nc + 4) * (nc + 4));
+      double *cc2i = malloc(sizeof(double) * (size_t)(nc + 4) * (nc + 4) * (nc + 4) *
+                            (f->d.n_ions > 0 ? f->d.n_ions : 1));
       double *cfl = malloc(sizeof(double) * (size_t)nc * nc * nc);
       double lc = -HUGE_VAL, ls = -HUGE_VAL;
 #pragma omp for schedule(static)
       for (int q = 0; q < n; q++) {
         double c, s;
-        flux_box(f, LVL_AT(t, leaves, l, q), s_deriv, &c, &s, cc2, cfl);
+        flux_box(f, LVL_AT(t, leaves, l, q), s_deriv, &c, &s, cc2, cfl, cc2i);
         if (c > lc) lc = c;
         if (s > ls) ls = s;
       }
@@ -2206,14 +2260,23 @@ int32_t afo_flux_upwind_tree(afh_fluid *f, int32_t s_deriv, double *dt_lim) {
         if (lc > cfl_max) cfl_max = lc;
         if (ls > sig_max) sig_max = ls;
       }
-      free(cc2), free(cfl);
+      free(cc2), free(cfl), free(cc2i);
     }
     /* the boxes' first ghost layer was written back (gc2) */
     if (hook(t, AFH_HOOK_RIMS, l, f->d.i_electron + s_deriv, NULL, 0))
       return AFH_ERR_STATE;
+    for (int q = 0; q < f->d.n_ions; q++)
+      if (hook(t, AFH_HOOK_RIMS, l, f->d.species_iv[f->d.ion_species[q] - 1] + s_deriv,
+               NULL, 0))
+        return AFH_ERR_STATE;
   }
+  /* af_consistent_fluxes over every flux variable */
   consistent_fluxes(t, f->d.f_flux);
   if (hook(t, AFH_HOOK_CFLUX, 0, f->d.f_flux, NULL, 0)) return AFH_ERR_STATE;
+  for (int q = 0; q < f->d.n_ions; q++) {
+    consistent_fluxes(t, f->d.f_ion_flux[q]);
+    if (hook(t, AFH_HOOK_CFLUX, 0, f->d.f_ion_flux[q], NULL, 0)) return AFH_ERR_STATE;
+  }
   {
     double r[2] = {cfl_max, sig_max};
     if (hook(t, AFH_HOOK_MAX, 0, 0, r, 2)) return AFH_ERR_STATE;
@@ -2330,6 +2393,15 @@ int32_t afo_flux_update_densities(afh_fluid *fl, double dt, int32_t s_deriv,
                    dt_dr[0] * (F[FX(t, 0, i, j, k)] - F[FX(t, 0, i + 1, j, k)]) +
                    dt_dr[1] * (F[FX(t, 1, i, j, k)] - F[FX(t, 1, i, j + 1, k)]) +
                    dt_dr[2] * (F[FX(t, 2, i, j, k)] - F[FX(t, 2, i, j, k + 1)]);
+            /* and for the mobile ions (i_cc_flux 2..) */
+            for (int q = 0; q < fl->d.n_ions; q++) {
+              const double *G = fcb(t, fl->d.f_ion_flux[q], id);
+              double *oi = ccb(t, fl->d.species_iv[fl->d.ion_species[q] - 1] + s_out, id);
+              oi[x] = oi[x] +
+                      dt_dr[0] * (G[FX(t, 0, i, j, k)] - G[FX(t, 0, i + 1, j, k)]) +
+                      dt_dr[1] * (G[FX(t, 1, i, j, k)] - G[FX(t, 1, i, j + 1, k)]) +
+                      dt_dr[2] * (G[FX(t, 2, i, j, k)] - G[FX(t, 2, i, j, k + 1)]);
+            }
           }
     }
   }

@@ -132,6 +132,14 @@ program export_case
   write(u, "(A,1X,I0,*(1X,I0))") "i:td_cols", 5, td_mobility, td_diffusion, &
        td_alpha, td_eta, td_energy_eV
   write(u, "(A,1X,I0,*(1X,I0))") "i:n_mobile_ions", 1, transport_data_ions%n_mobile_ions
+  ! flux species (m_streamer.f90:253-282): the electrons, then the mobile
+  ! ions with their scaled mobilities (m_transport_data.f90:195-215)
+  write(u, "(A,1X,I0,*(1X,I0))") "i:flux_species", flux_num_species, flux_species
+  write(u, "(A,1X,I0,*(1X,I0))") "i:flux_variables", flux_num_species, flux_variables
+  write(u, "(A,1X,I0,*(1X,I0))") "i:flux_species_charge_sign", flux_num_species, &
+       flux_species_charge_sign
+  write(u, "(A,1X,I0,*(1X,ES25.17E3))") "r:ion_mobilities", &
+       transport_data_ions%n_mobile_ions, transport_data_ions%mobilities
   write(u, "(A,1X,I0,*(1X,ES25.17E3))") "r:ion_se_yield", 1, ion_se_yield
 
   ! variable registry (af_add_cc_variable order)

@@ -24,6 +24,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 TESTS = "/root/reference/programs/standard_3d/tests"
 CASES = ["test_3d", "test_3d_chem", "test_3d_photoi_chem"]
+ION_ARGS = ["-input_data%mobile_ions=N2_plus O2_plus O2_min",
+            "-input_data%ion_mobilities=1e-2 2e-2 1.5e-2"]
 # BASELINE.json config 3: programs/standard_3d/streamer_3d.cfg with
 # air_chemistry_v2 (9 species, 25 reactions); no regression log
 EXTRA = {"s3": ("/root/reference/programs/standard_3d", "streamer_3d.cfg",
@@ -44,7 +46,13 @@ EXTRA = {"s3": ("/root/reference/programs/standard_3d", "streamer_3d.cfg",
          # (sprite_chemistry_v0, Helmholtz photoionization, the gas density
          # of its m_user.f90: an exponential atmosphere, so the "M" variable)
          "s5": ("/root/reference/programs/3d_sprite", "sprite_3d.cfg",
-                ["--user-gas=sprite"])}
+                ["--user-gas=sprite"]),
+         # mobile ions (input_data%mobile_ions / ion_mobilities, flux species
+         # 2.. of m_streamer.f90:253-282): test_3d_chem with three of its ions
+         # made mobile, at the 1e-2 m^2/Vs of the reference's own
+         # standard_2d/tests/test_cyl_ion_motion.cfg (far above real ion
+         # mobilities, so the ion fluxes matter within a step)
+         "ions": (TESTS, "test_3d_chem.cfg", ION_ARGS)}
 
 
 def parse_dump(path):

@@ -37,6 +37,7 @@ def rules(topo):
     """[(name regex, bytes per cell, list, level filter)]; first match wins."""
     nc = topo["nc"]
     nq = topo.get("n_charged", topo.get("n_species", 3))
+    phi = topo.get("faces_from_phi", False)
     small = lambda n: 64 <= n < 256  # noqa: E731  k-split / tiled pair levels
     # the split half-sweep: levels below the fused pair's 64 boxes (nc >= 32),
     # or a stale top level (any)
@@ -57,8 +58,11 @@ def rules(topo):
         (r"k_prolong<", 20, "ids", None),
         (r"k_corr_tmp", 24, "parents", None),
         (r"k_parent_rhs", 24, "parents", None),
-        (r"k_gradient", 40, "all", None),
-        (r"k_flux_lds|k_flux_staged", 64 + 192 / nc, "leaves", None),
+        # with the face field formed in the flux (faces_from_phi): the
+        # gradient reads phi and writes |E|; the flux reads phi instead of
+        # three face fields
+        (r"k_gradient", 16 if phi else 40, "all", None),
+        (r"k_flux_lds|k_flux_staged", (48 if phi else 64) + 192 / nc, "leaves", None),
         (r"k_update<(\d+), \w+(?:, (\d+))?", upd, "leaves", None),
         (r"k_gc_faces", 96 / nc, "ids", None),
         (r"k_gc2", 192 / nc, "leaves", None),

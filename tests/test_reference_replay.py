@@ -251,3 +251,26 @@ def test_species_step_replay_s5(tmp_path):
     _replay_state(sim, "s5", 0, [0], [1.0], 1, 1e-12, tmp_path, cwd=cwd, cfg_args=args)
     _replay_state(sim, "s5", 1, [0, 1], [0.5, 0.5], 0, 5e-13, tmp_path, cwd=cwd,
                   cfg_args=args)
+
+
+ION_ARGS = ["test_3d_chem.cfg", "-input_data%mobile_ions=N2_plus O2_plus O2_min",
+            "-input_data%ion_mobilities=1e-2 2e-2 1.5e-2"]
+
+
+def test_species_step_replay_mobile_ions(tmp_path):
+    """Mobile ions (input_data%mobile_ions / ion_mobilities; flux species 2..
+    of m_streamer.f90:253-282, their fluxes in m_fluid.f90:207-214): test_3d_chem
+    with N2+, O2+ and O2- mobile (tests/golden/case_ions.npz, oracle/
+    make_cases.py). After the initial refinement and three time steps, Heun
+    stages 1 and 2 bitwise equal to the reference's forward_euler: every
+    density -- the ions' now with their flux divergence -- and dt_lim, whose
+    dielectric relaxation term sums the ions' mu u with the electrons' per
+    face."""
+    sim = Simulation(capi.oracle_library(), golden.load("case_ions"))
+    assert [q[1] for q in sim.ions] == [3, 4, 5]
+    sim.start()
+    for _ in range(3):
+        sim.step()
+    _replay_state(sim, "ions", 0, [0], [1.0], 1, 1e-12, tmp_path, cfg_args=ION_ARGS)
+    _replay_state(sim, "ions", 1, [0, 1], [0.5, 0.5], 0, 5e-13, tmp_path,
+                  cfg_args=ION_ARGS)
