@@ -2226,8 +2226,11 @@ __global__ void __launch_bounds__(1024)
 
 using namespace afh;
 
+#ifndef AFH_RES_K  // cells per thread column of k_residual (8, 4 or 2)
+#define AFH_RES_K 4
+#endif
 #ifndef AFH_RSTR_K  // coarse cells per thread column of k_rstr_fas_col
-#define AFH_RSTR_K 2
+#define AFH_RSTR_K 4
 #endif
 struct afh_mg {
   afh_tree *t = nullptr;
@@ -2276,6 +2279,7 @@ struct afh_mg {
   std::vector<double> h_norm;
   bool rstr_col = true;       // AFH_RSTR_COL=0: one coarse cell per thread (k_rstr_fas)
   int rstr_k = AFH_RSTR_K;     // coarse cells per column (AFH_RSTR_K=2|4 at run time)
+  int res_k = AFH_RES_K;       // residual cells per column (AFH_RES_K=2|4|8 at run time)
   int pair_ks = 4;           // AFH_GSRB_PAIR_KS: k chunks on 64..255-box levels (NC = 64;
                              // 4 whole-box chunks, 44 quarter-box tiles x 4, 0 tiles)
   int wave_cells = CS_WAVE_CELLS;  // AFH_CS_WAVE_CELLS
@@ -2501,6 +2505,8 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
   if (const char *env = getenv("AFH_GRAPHS")) mg->use_graphs = atoi(env) != 0;
   if (const char *env = getenv("AFH_RSTR_COL")) mg->rstr_col = atoi(env) != 0;
   if (const char *env = getenv("AFH_RSTR_K")) mg->rstr_k = atoi(env) == 4 ? 4 : 2;
+  if (const char *env = getenv("AFH_RES_K"))
+    mg->res_k = atoi(env) == 8 ? 8 : atoi(env) == 2 ? 2 : 4;
   if (const char *env = getenv("AFH_CS_FUSED")) mg->cs_fused = atoi(env) != 0;
   if (const char *env = getenv("AFH_CS_DIRECT_SMALL")) mg->cs_direct_small = atoi(env) != 0;
   if (const char *env = getenv("AFH_PAIR_PUSH")) mg->pair_push = atoi(env) != 0;
@@ -2852,9 +2858,6 @@ static int32_t gsrb_boxes(afh_mg *mg, int lvl, bool up, bool stale_ghosts = fals
   return AFH_OK;
 }
 
-#ifndef AFH_RES_K  // cells per thread column of k_residual (8, 4 or 2)
-#define AFH_RES_K 4
-#endif
 
 static int32_t update_coarse(afh_mg *mg, int lvl) {
   afh_tree *t = mg->t;
@@ -3333,7 +3336,7 @@ static int32_t residual_levels(afh_mg *mg, int max_lvl, bool max_out) {
       const int n = one ? (lvl == 1 ? n_all : 0) : L.n(lvl);
       const bool mx = max_out && !part;
       if (n) {
-        const int kc = nc % AFH_RES_K == 0 ? AFH_RES_K : nc % 4 == 0 ? 4 : 2;
+        const int kc = nc % mg->res_k == 0 ? mg->res_k : nc % 4 == 0 ? 4 : 2;
         const dim3 grid((n3 / kc + 255) / 256, n);
         auto kern = mx ? (kc == 8 ? k_residual<true, 8> : kc == 4 ? k_residual<true, 4>
                                                                   : k_residual<true, 2>)

@@ -4,7 +4,7 @@
 # profiles at HEAD (face field from phi) for S1-64 and S1.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_hip_parity.py tests/test_graphs.py tests/test_full_size.py tests/test_dist_native.py tests/test_face_field.py -m gpu -x -v \
+AFH_GC_XPAIR=1 timeout -k 10 600 python -u -m pytest tests/test_ions.py tests/test_graphs.py -m gpu -x -v \
   --timeout 300 --timeout-method thread > gpurun_out/pytest_i.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -n 3 gpurun_out/pytest_i.log; [ $rc -eq 0 ] || exit $rc
 CFG=s1-64 REPS=2 bash scripts/env_bench_ab.sh AFH_GC_XPAIR "0 1" || exit $?

@@ -11,9 +11,9 @@ pinned to the reference's own forward_euler on it by
 tests/test_reference_replay.py::test_species_step_replay_mobile_ions.
 CPU: the descriptor is validated the same way by both libraries. GPU: the
 HIP driver's state after three steps, handed to the oracle: Heun stage 1
-(fluxes of every species, the CFL and dielectric limits, the densities)
-bitwise; stage 2 as test_rtest's S5 (rate forms with exp: ocml vs glibc in
-the last ulp of stage-1 densities) to 1e-12."""
+fluxes of every species and the CFL and dielectric limits bitwise, the
+densities to 1e-13 (rate forms with exp: ocml vs glibc in the last ulp);
+stage 2 as test_rtest's S5 to 1e-12."""
 import numpy as np
 import pytest
 
@@ -74,9 +74,11 @@ def test_hip_mobile_ions_equal_oracle():
         a, b = sim.tree.get_fc(fv)[leaves], osim.tree.get_fc(fv)[leaves]
         assert np.array_equal(a, b), fv
         assert np.max(np.abs(a)) > 0
+    # the densities: the rate forms with exp (air_chemistry_small_v1: O- + O2
+    # + M -> O3- + M, c1 exp(-(Td/c2)^2)) may differ in the last ulp
     for iv in sim.densities:
-        assert np.array_equal(sim.tree.get_cc(iv + 1), osim.tree.get_cc(iv + 1)), \
-            sim.cc_names[iv - 1]
+        a, b = sim.tree.get_cc(iv + 1), osim.tree.get_cc(iv + 1)
+        assert np.max(np.abs(a - b)) <= 1e-13 * np.max(np.abs(b)), sim.cc_names[iv - 1]
     y = [s.fluid.forward_euler(5e-13, 1, [0, 1], [0.5, 0.5], 0, True) for s in (sim, osim)]
     assert np.allclose(list(y[0]), list(y[1]), rtol=1e-12, atol=0)
     for iv in sim.densities:
