@@ -125,7 +125,7 @@ struct afh_tree {
   bool gc_box = true;
   // k_gc_faces pairs same-level x interfaces (one thread copies both ghost
   // values; AFH_GC_XPAIR=0 for one thread per ghost value)
-  int gc_xpair = 1;
+  int gc_xpair = 0;
   // independent per-box work of every leaf level in one launch where the
   // kernel reads the box's level data from its meta record (flux of small
   // boxes, density update, residual; AFH_ALL_LVL=0: one launch per level)

@@ -2280,6 +2280,7 @@ struct afh_mg {
   bool rstr_col = true;       // AFH_RSTR_COL=0: one coarse cell per thread (k_rstr_fas)
   int rstr_k = AFH_RSTR_K;     // coarse cells per column (AFH_RSTR_K=2|4 at run time)
   int res_k = AFH_RES_K;       // residual cells per column (AFH_RES_K=2|4|8 at run time)
+  int rstr_bs = 256;           // k_rstr_fas_col workgroup size (AFH_RSTR_BS=128|256)
   int pair_ks = 4;           // AFH_GSRB_PAIR_KS: k chunks on 64..255-box levels (NC = 64;
                              // 4 whole-box chunks, 44 quarter-box tiles x 4, 0 tiles)
   int wave_cells = CS_WAVE_CELLS;  // AFH_CS_WAVE_CELLS
@@ -2505,6 +2506,7 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
   if (const char *env = getenv("AFH_GRAPHS")) mg->use_graphs = atoi(env) != 0;
   if (const char *env = getenv("AFH_RSTR_COL")) mg->rstr_col = atoi(env) != 0;
   if (const char *env = getenv("AFH_RSTR_K")) mg->rstr_k = atoi(env) == 4 ? 4 : 2;
+  if (const char *env = getenv("AFH_RSTR_BS")) mg->rstr_bs = atoi(env) == 128 ? 128 : 256;
   if (const char *env = getenv("AFH_RES_K"))
     mg->res_k = atoi(env) == 8 ? 8 : atoi(env) == 2 ? 2 : 4;
   if (const char *env = getenv("AFH_CS_FUSED")) mg->cs_fused = atoi(env) != 0;
@@ -2867,15 +2869,18 @@ static int32_t update_coarse(afh_mg *mg, int lvl) {
   if (nid) {
     // column length (AFH_RSTR_K = 2 or 4): a column reads 2K + 2 fine planes
     // for 2K; K = 4 halves that excess at twice the centre registers
-    const int RK = mg->rstr_k;
+    // (workgroup size AFH_RSTR_BS: with 128 the blocks of neighbouring
+    // columns along k are 8 apart in dispatch order, i.e. on the same XCD,
+    // whose L2 then holds the fine plane both read)
+    const int RK = mg->rstr_k, BS = mg->rstr_bs;
     if (mg->rstr_col && RK == 4 && hn % 4 == 0)
-      hipLaunchKernelGGL(k_rstr_fas_col<4>, dim3((hn * hn * (hn / 4) + 255) / 256, nid),
-                         dim3(256), 0, t->stream, t->ccv(mg->d.i_phi),
+      hipLaunchKernelGGL(k_rstr_fas_col<4>, dim3((hn * hn * (hn / 4) + BS - 1) / BS, nid),
+                         dim3(BS), 0, t->stream, t->ccv(mg->d.i_phi),
                          t->ccv(mg->d.i_rhs), t->ccv(mg->d.i_tmp), t->d_boxes,
                          L.at(lvl), nc, t->bsz, mg->lvl_c[lvl - 1]);
     else if (mg->rstr_col && hn % 2 == 0)
-      hipLaunchKernelGGL(k_rstr_fas_col<2>, dim3((hn * hn * (hn / 2) + 255) / 256, nid),
-                         dim3(256), 0, t->stream, t->ccv(mg->d.i_phi),
+      hipLaunchKernelGGL(k_rstr_fas_col<2>, dim3((hn * hn * (hn / 2) + BS - 1) / BS, nid),
+                         dim3(BS), 0, t->stream, t->ccv(mg->d.i_phi),
                          t->ccv(mg->d.i_rhs), t->ccv(mg->d.i_tmp), t->d_boxes,
                          L.at(lvl), nc, t->bsz, mg->lvl_c[lvl - 1]);
     else

@@ -371,7 +371,10 @@ __global__ void __launch_bounds__(256, AFH_FLUX_MINW)
 #pragma unroll
   for (int d = 0; d < 3; d++) {
     idx[d] = A.meta ? 1 / A.meta[id - 1].dr[d] : A.inv_dx[d];
-    if (PHI) gf[d] = A.meta ? A.fac / A.meta[id - 1].dr[d] : A.gfac[d];
+    // fac / dr; for fac = -1 (field_from_potential) that is -(1 / dr)
+    // bitwise (IEEE division rounds symmetrically): no second division
+    if (PHI)
+      gf[d] = !A.meta ? A.gfac[d] : A.fac == -1.0 ? -idx[d] : A.fac / A.meta[id - 1].dr[d];
   }
   const double *__restrict__ ph = PHI ? A.phi + (size_t)(id - 1) * bsz : nullptr;
   const double P0 = PHI ? ph[c0] : 0.0;
@@ -566,7 +569,8 @@ __global__ void __launch_bounds__(256)
   const int gq[3] = {(k - 1) * nc + (j - 1), (k - 1) * nc + (i - 1), (j - 1) * nc + (i - 1)};
   double smax = -HUGE_VAL;
   for (int d = 0; d < 3; d++) {
-    const double gf = PHI ? (A.meta ? A.fac / A.meta[id - 1].dr[d] : A.gfac[d]) : 0.0;
+    const double gf = !PHI ? 0.0 : !A.meta ? A.gfac[d]
+                    : A.fac == -1.0 ? -(1 / A.meta[id - 1].dr[d]) : A.fac / A.meta[id - 1].dr[d];
     for (int hi = 0; hi < 2; hi++) {
       if (hi && cc[d] != nc) continue;
       const int fi = d * fd + fcell + (hi ? fst[d] : 0);
@@ -2305,11 +2309,19 @@ static int32_t flux_prelude(afh_fluid *f, int iv, double *gc2) {
   afh_tree *t = f->t;
   const int nc = t->nc;
   int32_t e;
-  // af_restrict_ref_boundary (per level, for the sharding hook)
-  for (int l = t->nlvl; l >= 2; l--) {
-    if ((e = restrict_boxes(t, t->refb.at(l), t->refb.n(l), iv)) ||
-        (t->hook && (e = call_hook(t, AFH_HOOK_RESTRICT, l, iv))))
+  // af_restrict_ref_boundary: only leaves are restricted and their parents
+  // are no leaves, so the levels are independent -- one launch over the
+  // refinement-boundary leaves of levels 2.. (contiguous in the level list);
+  // per level with the sharding hook, which exchanges after each
+  if (!t->hook && t->nlvl >= 2) {
+    if ((e = restrict_boxes(t, t->refb.at(2), t->refb.off[t->nlvl] - t->refb.off[1], iv)))
       return e;
+  } else {
+    for (int l = t->nlvl; l >= 2; l--) {
+      if ((e = restrict_boxes(t, t->refb.at(l), t->refb.n(l), iv)) ||
+          (t->hook && (e = call_hook(t, AFH_HOOK_RESTRICT, l, iv))))
+        return e;
+    }
   }
   // two ghost layers, level by level (coarse write-back before fine reads)
   for (int l = 1; l <= t->nlvl; l++) {
