@@ -378,8 +378,15 @@ struct RbPar {
 // KS: the k planes split into KS chunks, one workgroup each (levels with
 // too few boxes to fill the chip): a chunk recomputes the red cells of the
 // plane below it (as tiles recompute halo rows) and stores its own planes
+// NTL: the streamed plane and rhs loads non-temporal (they are used once;
+// the lines phase B reads from neighbouring boxes should stay in L2)
+template <bool NTL>
+__device__ __forceinline__ double ld_nt(const double *p) {
+  if constexpr (NTL) return __builtin_nontemporal_load(p);
+  else return *p;
+}
 template <int NC, int TJ, int DEPTH = 2, int NTM = 0, bool FR = true, bool P3 = true,
-          bool SP = true, int KS = 1>
+          bool SP = true, int KS = 1, bool NTL = false>
 __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
     k_gsrb_pair2(const double *__restrict__ src, double *__restrict__ dst,
                  const double *__restrict__ rhs, const double *__restrict__ coarse,
@@ -575,15 +582,15 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
 #pragma unroll
     for (int e = 0; e < EPT; e++) {
       const int xx = tid + NT * e;
-      f.nx[e] = x[(size_t)kx * SK + t0 + (xx < PL ? xx : PL - 1)];
+      f.nx[e] = ld_nt<NTL>(x + ((size_t)kx * SK + t0 + (xx < PL ? xx : PL - 1)));
     }
 #pragma unroll
     for (int q = 0; q < RPT; q++) {
       const int rr = tid + NT * q;
       const int j = j0 + rr / HN, i1 = 2 * (rr % HN) + 1;
       const size_t g = (size_t)kr * SK + (size_t)j * NG + i1;
-      f.nlo[q] = r[g];
-      f.nhi[q] = r[g + 1];
+      f.nlo[q] = ld_nt<NTL>(r + g);
+      f.nhi[q] = ld_nt<NTL>(r + g + 1);
     }
   };
   Pf X0, X1;
