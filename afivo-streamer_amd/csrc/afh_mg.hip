@@ -2288,6 +2288,7 @@ struct afh_mg {
   int rstr_k = AFH_RSTR_K;     // coarse cells per column (AFH_RSTR_K=2|4 at run time)
   int res_k = AFH_RES_K;       // residual cells per column (AFH_RES_K=2|4|8 at run time)
   int rstr_bs = 256;           // k_rstr_fas_col workgroup size (AFH_RSTR_BS=128|256)
+  bool pair_ntl = false;       // AFH_GSRB_PAIR_NTL: non-temporal plane loads in the 64^3 pair
   int pair_ks = 4;           // AFH_GSRB_PAIR_KS: k chunks on 64..255-box levels (NC = 64;
                              // 4 whole-box chunks, 44 quarter-box tiles x 4, 0 tiles)
   int wave_cells = CS_WAVE_CELLS;  // AFH_CS_WAVE_CELLS
@@ -2513,6 +2514,7 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
   if (const char *env = getenv("AFH_GRAPHS")) mg->use_graphs = atoi(env) != 0;
   if (const char *env = getenv("AFH_RSTR_COL")) mg->rstr_col = atoi(env) != 0;
   if (const char *env = getenv("AFH_RSTR_K")) mg->rstr_k = atoi(env) == 4 ? 4 : 2;
+  if (const char *env = getenv("AFH_GSRB_PAIR_NTL")) mg->pair_ntl = atoi(env) != 0;
   if (const char *env = getenv("AFH_RSTR_BS")) mg->rstr_bs = atoi(env) == 128 ? 128 : 256;
   if (const char *env = getenv("AFH_RES_K"))
     mg->res_k = atoi(env) == 8 ? 8 : atoi(env) == 2 ? 2 : 4;
@@ -2635,11 +2637,11 @@ static bool pair_tiles(const afh_mg *mg, int lvl) {
 }
 
 template <int NC, int TJ, int DEPTH, int NTM = 0, bool FR = true, bool P3 = true,
-          bool SP = true, int KS = 1>
+          bool SP = true, int KS = 1, bool NTL = false>
 static void launch_pair2(afh_mg *mg, int lvl, const double *src, double *dst,
                          const Coef &cf, double inv_c1, hipEvent_t e0, hipEvent_t e1) {
   afh_tree *t = mg->t;
-  launch_ev((k_gsrb_pair2<NC, TJ, DEPTH, NTM, FR, P3, SP, KS>), e0, e1,
+  launch_ev((k_gsrb_pair2<NC, TJ, DEPTH, NTM, FR, P3, SP, KS, NTL>), e0, e1,
             dim3(t->ids.n(lvl) * RbPar<NC, TJ, NTM>::NTILE * KS),
             dim3(RbPar<NC, TJ, NTM>::NT), t->stream, src, dst, t->ccv(mg->d.i_rhs),
             t->ccv(mg->d.i_phi), t->d_boxes, t->ids.at(lvl), t->bsz, cf, inv_c1,
@@ -2710,6 +2712,9 @@ static void launch_pair(afh_mg *mg, int lvl, const double *src, double *dst,
         if (!mg->pair_p3)
           return launch_pair2<NC, NC, 1, 0, true, false>(mg, lvl, src, dst, cf, inv_c1, e0,
                                                          e1);
+        if (mg->pair_ntl)
+          return launch_pair2<NC, NC, 1, 0, true, true, true, 1, true>(mg, lvl, src, dst, cf,
+                                                                       inv_c1, e0, e1);
         return launch_pair2<NC, NC, 1>(mg, lvl, src, dst, cf, inv_c1, e0, e1);
       }
       return launch_pair2<NC, NC, 2>(mg, lvl, src, dst, cf, inv_c1, e0, e1);
