@@ -239,7 +239,7 @@ def pmc_traffic(config):
     return None
 
 
-def write_topology(case, config, path, faces_from_phi=False):
+def write_topology(case, config, path, faces_from_phi=False, fused_rhs=False):
     """Boxes, leaves and parents per level, the box size and the species
     counts of the benchmarked tree (scripts/prof_steady.py)."""
     topo = case.topo
@@ -254,7 +254,8 @@ def write_topology(case, config, path, faces_from_phi=False):
                    "leaves": cnt("leaves"), "parents": cnt("parents"),
                    "n_species": len(charges),
                    "n_charged": sum(1 for q in charges if q != 0),
-                   "faces_from_phi": bool(faces_from_phi)}, f)
+                   "faces_from_phi": bool(faces_from_phi),
+                   "fused_rhs": bool(fused_rhs)}, f)
 
 
 def main():
@@ -389,7 +390,8 @@ def main():
 
     if rank == 0 and os.environ.get("AFH_BENCH_TOPO"):
         # the run's topology for scripts/prof_steady.py's byte model
-        write_topology(case, args.config, os.environ["AFH_BENCH_TOPO"], faces_from_phi)
+        write_topology(case, args.config, os.environ["AFH_BENCH_TOPO"], faces_from_phi,
+                       not args.no_fused_rhs and not two_d)
 
     if rank == 0:
         avg_s = ms.value / 1e3 / max(1, nl.value)

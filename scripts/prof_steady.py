@@ -38,14 +38,16 @@ def rules(topo):
     nc = topo["nc"]
     nq = topo.get("n_charged", topo.get("n_species", 3))
     phi = topo.get("faces_from_phi", False)
+    rhs = topo.get("fused_rhs", False)
     small = lambda n: 64 <= n < 256  # noqa: E731  k-split / tiled pair levels
     # the split half-sweep: levels below the fused pair's 64 boxes (nc >= 32),
     # or a stale top level (any)
     split = (lambda n: n < 64) if nc >= 32 else None
 
     def upd(m):
+        # + the rhs of the new state when field_set_rhs is folded in
         ns, np_ = int(m.group(1)), int(m.group(2) or 2)
-        return 8 * ns * ((np_ if np_ in (1, 2) else 2) + 1) + 32
+        return 8 * ns * ((np_ if np_ in (1, 2) else 2) + 1) + 32 + (8 if rhs else 0)
 
     return [
         (r"k_gsrb_pair2<64, 64, 1, 0, true, true, true, 4>", 24, "ids", small),
