@@ -33,8 +33,9 @@ constexpr int CS_SMALL_CELLS = 4096;   // MG levels <= 16^3 run in one workgroup
 constexpr int CS_DS_N = 16;            // k_cs_direct_small: LDS matrices up to 16 x 16
 // k_cs_direct_small serves level-1 grids up to 1024 cells (S3's 8^3: 15 us,
 // against ~25 us for the eight launches of k_cs_gather / k_cs_transform /
-// k_cs_scatter); S1's 16^3 runs those (one workgroup took 63 us there, the
-// multi-launch form is 0.60 against 0.64 ms per step: profiles/r03_ab_fusions.txt)
+// k_cs_scatter); S1's 16^3 runs those: one workgroup is latency-bound there
+// (one wave per SIMD), 0.573 against 0.551 ms per step with one thread per
+// grid line (profiles/r03_ab_cs_direct_lines.txt; AFH_CS_DS_CELLS=4096 for A/B)
 constexpr int CS_DS_CELLS = 1024;
 
 struct CsParams {
@@ -2178,9 +2179,6 @@ __global__ void __launch_bounds__(1024)
   // Q^T along x, y, z (divide), then Q along z, y, x: A -> B -> A -> B -> A -> B -> A
   const double *Ms[6] = {q0, q1, q2, qt2, qt1, qt0};
   const int ds[6] = {0, 1, 2, 2, 1, 0};
-  // grids of at most 16 cells per dimension: the six matrices in LDS and
-  // each output's 2 x n operands loaded before its (ordered) sum, so the
-  // loads overlap instead of each product waiting for its own
   const bool small = nx <= CS_DS_N && ny <= CS_DS_N && nz <= CS_DS_N;
   if (small)
     for (int ps = 0; ps < 6; ps++) {
@@ -2188,35 +2186,65 @@ __global__ void __launch_bounds__(1024)
       for (int u = threadIdx.x; u < n * n; u += blockDim.x) Ml[ps][u] = Ms[ps][u];
     }
   __syncthreads();
-  for (int ps = 0; ps < 6; ps++) {
-    const double *in = (ps & 1) ? B : A;
-    double *out = (ps & 1) ? A : B;
-    const int d = ds[ps], n = d == 0 ? nx : (d == 1 ? ny : nz);
-    const int st = d == 0 ? 1 : (d == 1 ? nx : nx * ny);
-    const double *M = small ? Ml[ps] : Ms[ps];
-    for (int t = threadIdx.x; t < N; t += blockDim.x) {
-      const int i = t % nx, j = (t / nx) % ny, k = t / (nx * ny);
-      const int co = d == 0 ? i : (d == 1 ? j : k);
-      const double *src = in + (t - co * st);
-      double s = 0.0;
-      if (small) {
-        double mv[CS_DS_N], xv[CS_DS_N];
+  if (small) {
+    // grids of at most 16 cells per dimension: one thread per grid line
+    // holds the line's n values in registers and forms its n outputs, each
+    // the ordered sum over p of M[p][c] x[p] with the matrix entries
+    // wave-uniform (scalar loads): per output no LDS traffic but the store,
+    // instead of 2 n LDS reads (the LDS throughput bound this pass before)
+    for (int ps = 0; ps < 6; ps++) {
+      const double *in = (ps & 1) ? B : A;
+      double *out = (ps & 1) ? A : B;
+      const int d = ds[ps], n = d == 0 ? nx : (d == 1 ? ny : nz);
+      const int st = d == 0 ? 1 : (d == 1 ? nx : nx * ny);
+      const double *M = Ml[ps];  // uniform addresses: LDS broadcast reads
+      const int nl = N / n;
+      for (int l = threadIdx.x; l < nl; l += blockDim.x) {
+        // the line's cell 0 along d
+        const int base = d == 0 ? l * nx : d == 1 ? (l / nx) * nx * ny + l % nx : l;
+        double x[CS_DS_N];
 #pragma unroll
-        for (int p = 0; p < CS_DS_N; p++)
-          if (p < n) mv[p] = M[p * n + co], xv[p] = src[p * st];
+        for (int p = 0; p < CS_DS_N; p++) x[p] = p < n ? in[base + p * st] : 0.0;
 #pragma unroll
-        for (int p = 0; p < CS_DS_N; p++)
-          if (p < n) s = s + mv[p] * xv[p];
-      } else {
-        for (int p = 0; p < n; p++) s = s + M[p * n + co] * src[p * st];
+        for (int c = 0; c < CS_DS_N; c++) {
+          if (c < n) {
+            double sum = 0.0;
+#pragma unroll
+            for (int p = 0; p < CS_DS_N; p++)
+              if (p < n) sum = sum + M[p * n + c] * x[p];
+            const int o = base + c * st;
+            if (ps == 2) {
+              const int i = o % nx, j = (o / nx) % ny, k = o / (nx * ny);
+              const double den = ((e0[i] + e1[j]) + e2[k]) - lam;
+              sum = den != 0.0 ? sum / den : 0.0;
+            }
+            out[o] = sum;
+          }
+        }
       }
-      if (ps == 2) {
-        const double den = ((e0[i] + e1[j]) + e2[k]) - lam;
-        s = den != 0.0 ? s / den : 0.0;
-      }
-      out[t] = s;
+      __syncthreads();
     }
-    __syncthreads();
+  } else {
+    for (int ps = 0; ps < 6; ps++) {
+      const double *in = (ps & 1) ? B : A;
+      double *out = (ps & 1) ? A : B;
+      const int d = ds[ps], n = d == 0 ? nx : (d == 1 ? ny : nz);
+      const int st = d == 0 ? 1 : (d == 1 ? nx : nx * ny);
+      const double *M = Ms[ps];
+      for (int t = threadIdx.x; t < N; t += blockDim.x) {
+        const int i = t % nx, j = (t / nx) % ny, k = t / (nx * ny);
+        const int co = d == 0 ? i : (d == 1 ? j : k);
+        const double *src = in + (t - co * st);
+        double sum = 0.0;
+        for (int p = 0; p < n; p++) sum = sum + M[p * n + co] * src[p * st];
+        if (ps == 2) {
+          const double den = ((e0[i] + e1[j]) + e2[k]) - lam;
+          sum = den != 0.0 ? sum / den : 0.0;
+        }
+        out[t] = sum;
+      }
+      __syncthreads();
+    }
   }
   // the sixth pass wrote A
   for (int u = threadIdx.x; u < nid * n3; u += blockDim.x) {
@@ -2277,6 +2305,7 @@ struct afh_mg {
   // AFH_CS_DIRECT_SMALL: the direct solve of a level-1 grid of at most
   // CS_DS_CELLS cells in one workgroup (k_cs_direct_small), default on
   bool cs_direct_small = true;
+  int cs_ds_cells = CS_DS_CELLS;  // AFH_CS_DS_CELLS: its size limit (at most CS_SMALL_CELLS)
   bool pair_push = true;  // AFH_PAIR_PUSH: the small-box pair fills the faces
   int *d_cycles = nullptr;
   int cycles_host = 0;
@@ -2520,6 +2549,8 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
     mg->res_k = atoi(env) == 8 ? 8 : atoi(env) == 2 ? 2 : 4;
   if (const char *env = getenv("AFH_CS_FUSED")) mg->cs_fused = atoi(env) != 0;
   if (const char *env = getenv("AFH_CS_DIRECT_SMALL")) mg->cs_direct_small = atoi(env) != 0;
+  if (const char *env = getenv("AFH_CS_DS_CELLS"))
+    mg->cs_ds_cells = std::min(CS_SMALL_CELLS, std::max(0, atoi(env)));
   if (const char *env = getenv("AFH_PAIR_PUSH")) mg->pair_push = atoi(env) != 0;
   AFH_HIP(hipMalloc(&mg->cs_iters, sizeof(int)));
   AFH_HIP(hipMalloc(&mg->d_cycles, sizeof(int)));
@@ -3160,7 +3191,7 @@ static int32_t solve_coarse(afh_mg *mg) {
     }
   const int nc = t->nc, nid = t->ids.n(1), n3 = nc * nc * nc;
   if (mg->d.coarse_mode == AFH_COARSE_DIRECT && mg->cs_direct_small &&
-      (long)P.dims[0][0] * P.dims[0][1] * P.dims[0][2] <= CS_DS_CELLS) {
+      (long)P.dims[0][0] * P.dims[0][1] * P.dims[0][2] <= mg->cs_ds_cells) {
     for (int q = 0; q < 6; q++)
       if (mg->q_bc[q] != bc[q].type) {
         if (int32_t e = build_direct(mg)) return e;

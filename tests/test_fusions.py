@@ -70,6 +70,20 @@ def test_direct_small_bitwise_8cubed(monkeypatch):
     _same(a, b)
 
 
+@pytest.mark.parametrize("config", ["s1", "c16x8"])
+def test_direct_small_bitwise_lines(config, monkeypatch):
+    """k_cs_direct_small, one thread per grid line (the line in registers,
+    the matrix entries wave-uniform), on S1's 16^3 level-1 grid
+    (AFH_CS_DS_CELLS=4096 lets it take the 4096 cells) and on a 16 x 8 x 8
+    level-1 grid of two boxes (lines of different lengths per dimension):
+    bitwise the gather + six transforms + scatter."""
+    import bench
+    monkeypatch.setitem(bench.CONFIGS, "c16x8", (8, (16, 8, 8), 3, (16e-3, 8e-3, 8e-3)))
+    a = _s1(monkeypatch, {"AFH_CS_DIRECT_SMALL": "1", "AFH_CS_DS_CELLS": "4096"}, config)
+    b = _s1(monkeypatch, {"AFH_CS_DIRECT_SMALL": "0"}, config)
+    _same(a, b)
+
+
 def test_s3_all_level_launches_bitwise(monkeypatch):
     """Config 3: two unit steps (field solve with its residuals, flux,
     update with the chemistry limit) with every leaf level in one launch and
