@@ -219,6 +219,7 @@ constexpr int RED_SHARDS = 1024;
 constexpr int RED_SLOTS = 8;
 int32_t red_init(afh_tree *t, int slot, double v);
 int32_t red_finish(afh_tree *t, int slot, bool is_max);
+int32_t red_finish_n(afh_tree *t, int n, const int *slots, const bool *is_max);
 // fetch the folded values of `n` consecutive slots starting at `slot`
 int32_t red_fetch(afh_tree *t, int slot, int n, double *out);
 // the folded values of slots slot .. slot+n_max-1 (maxima) and the next

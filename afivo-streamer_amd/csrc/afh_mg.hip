@@ -3164,7 +3164,9 @@ static int32_t solve_coarse_gs(afh_mg *mg) {
                        t->stream, phi, mg->cs_old, t->ids.at(1), nc, t->bsz, red);
     AFH_LAUNCH_CHECK("k_change_max");
     double r[2];
-    if ((e = red_finish(t, 6, true)) || (e = red_finish(t, 7, true)) ||
+    const int slots[2] = {6, 7};
+    const bool mx[2] = {true, true};
+    if ((e = red_finish_n(t, 2, slots, mx)) ||
         (e = red_reduce_fetch(t, 6, 2, 0, r, mg->d.i_phi, 1)))
       return e;
     double sp = 2.2250738585072014e-308;  // Fortran spacing(max |phi|)

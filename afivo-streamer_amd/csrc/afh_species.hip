@@ -2518,8 +2518,11 @@ static int32_t flux_tree_dev(afh_fluid *f, int32_t s_deriv) {
     }
     if ((e = call_hook(t, AFH_HOOK_CFLUX, 0, fv))) return e;
   }
-  if ((e = red_finish(t, 0, true))) return e;
-  return red_finish(t, 1, true);
+  {
+    const int slots[2] = {0, 1};
+    const bool mx[2] = {true, true};
+    return red_finish_n(t, 2, slots, mx);
+  }
 }
 
 // dt_lim(1:2) of flux_upwind_tree from the folded maxima
@@ -2593,7 +2596,6 @@ static int32_t update_dev(afh_fluid *f, double dt, int32_t s_deriv, int32_t n_pr
                          t->bsz, t->ng);
       AFH_LAUNCH_CHECK("k_rhs_shell");
     }
-    if ((e = red_finish(t, 4, true))) return e;
   }
   f->touch_state(s_out);
   if (A.rhs) {
@@ -2602,7 +2604,12 @@ static int32_t update_dev(afh_fluid *f, double dt, int32_t s_deriv, int32_t n_pr
     f->rhs_snap.clear();
     for (int v : f->rhs_vars(s_out)) f->rhs_snap.push_back(t->gen[v]);
   }
-  return last_step ? red_finish(t, 2, false) : AFH_OK;
+  // max|rhs| (slot 4) and the chemistry limit (slot 2) in one fold launch
+  int slots[2], n_fold = 0;
+  bool mx[2];
+  if (A.rhs) slots[n_fold] = 4, mx[n_fold++] = true;
+  if (last_step) slots[n_fold] = 2, mx[n_fold++] = false;
+  return n_fold ? red_finish_n(t, n_fold, slots, mx) : AFH_OK;
 }
 
 extern "C" {
@@ -2752,8 +2759,9 @@ static int32_t fe_dev(afh_fluid *f, double dt, int32_t s_deriv, int32_t n_prev,
     prof_end(t, AFH_PROF_FE, fe_bytes * n3 * n);
     AFH_LAUNCH_CHECK("k_fe_lds");
   }
-  if ((e = red_finish(t, 0, true)) || (e = red_finish(t, 1, true))) return e;
-  return last_step ? red_finish(t, 2, false) : AFH_OK;
+  const int slots[3] = {0, 1, 2};
+  const bool mx[3] = {true, true, false};
+  return red_finish_n(t, last_step ? 3 : 2, slots, mx);
 }
 
 extern "C" {

@@ -490,13 +490,21 @@ int32_t restrict_boxes(afh_tree *t, const int32_t *d_ids, int n, int iv) {
 __global__ void k_red_fill(unsigned long long *r, unsigned long long v) {
   r[blockIdx.x * blockDim.x + threadIdx.x] = v;
 }
-__global__ void k_red_fold(unsigned long long *r, unsigned long long *out,
-                           int is_max, unsigned long long reset) {
-  // one block of RED_SHARDS threads; ordered integers fold like the doubles;
-  // the shards are left at `reset` for the slot's next use
+// Slots folded by one launch of k_red_fold: block b folds slots[b]
+struct RedFold {
+  int slot[RED_SLOTS];
+  int is_max[RED_SLOTS];
+  unsigned long long reset[RED_SLOTS];
+};
+__global__ void k_red_fold(unsigned long long *red, RedFold F) {
+  // one block of RED_SHARDS threads per slot; ordered integers fold like the
+  // doubles; the shards are left at `reset` for the slot's next use
   __shared__ unsigned long long s[RED_SHARDS];
+  const int slot = F.slot[blockIdx.x], is_max = F.is_max[blockIdx.x];
+  unsigned long long *r = red + (size_t)slot * RED_SHARDS;
+  unsigned long long *out = red + (size_t)RED_SLOTS * RED_SHARDS + slot;
   s[threadIdx.x] = r[threadIdx.x];
-  r[threadIdx.x] = reset;
+  r[threadIdx.x] = F.reset[blockIdx.x];
   __syncthreads();
   for (int o = RED_SHARDS / 2; o > 0; o >>= 1) {
     if ((int)threadIdx.x < o) {
@@ -526,13 +534,23 @@ int32_t red_init(afh_tree *t, int slot, double v) {
   return AFH_OK;
 }
 int32_t red_finish(afh_tree *t, int slot, bool is_max) {
+  const int slots[1] = {slot};
+  const bool mx[1] = {is_max};
+  return red_finish_n(t, 1, slots, mx);
+}
+// n slots folded in one launch (one block each)
+int32_t red_finish_n(afh_tree *t, int n, const int *slots, const bool *is_max) {
+  if (n < 1 || n > RED_SLOTS) return set_error(AFH_ERR_ARG, "fold of %d slots", n);
+  RedFold F;
+  for (int q = 0; q < n; q++) {
+    F.slot[q] = slots[q];
+    F.is_max[q] = is_max[q] ? 1 : 0;
+    F.reset[q] = (unsigned long long)t->red_canon[slots[q]];
+  }
   auto *r = reinterpret_cast<unsigned long long *>(t->scratch);
-  hipLaunchKernelGGL(k_red_fold, dim3(1), dim3(RED_SHARDS), 0, t->stream,
-                     r + (size_t)slot * RED_SHARDS,
-                     r + (size_t)RED_SLOTS * RED_SHARDS + slot, is_max ? 1 : 0,
-                     (unsigned long long)t->red_canon[slot]);
+  hipLaunchKernelGGL(k_red_fold, dim3(n), dim3(RED_SHARDS), 0, t->stream, r, F);
   AFH_LAUNCH_CHECK("k_red_fold");
-  t->red_ready[slot] = true;
+  for (int q = 0; q < n; q++) t->red_ready[slots[q]] = true;
   return AFH_OK;
 }
 int32_t red_fetch(afh_tree *t, int slot, int n, double *out) {

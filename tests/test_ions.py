@@ -55,6 +55,14 @@ def test_case_declares_three_mobile_ions():
     assert names == ["N2+", "O2+", "O2-"] or names == ["N2_plus", "O2_plus", "O2_min"], names
 
 
+def test_cases_without_mobile_ions():
+    """Cases exported before the flux-species fields (and configs without
+    mobile ions) give an electrons-only fluid."""
+    for name in ("rtest_test_3d", "case_s3"):
+        sim = Simulation(capi.oracle_library(), golden.load(name))
+        assert sim.ions == []
+
+
 @pytest.mark.gpu
 def test_hip_refuses_bad_ion_lists():
     bad_ion_fluids(capi.hip_library(), device=0)
