@@ -88,8 +88,11 @@ def test_oracle_norm_only_gradient_refused_with_electrode():
     c = golden.make_case(lib, golden.load("rod8"), coarse_cycles=0)
     with pytest.raises(capi.AfhError):
         c.mg.compute_phi_gradient(0, -1.0, IV["efld"])
+    c = make(lib, TOPOS["uni8_l3"](), -1, True)
     with pytest.raises(capi.AfhError):  # the norm only needs a norm
-        make(lib, TOPOS["uni8_l3"](), -1, True).mg.compute_phi_gradient(0, -1.0, 0)
+        c.mg.compute_phi_gradient(0, -1.0, 0)
+    with pytest.raises(capi.AfhError):  # no such potential variable
+        c.fluid.set_field_source(c.tree.n_var_cell + 1, -1.0)
 
 
 @pytest.mark.gpu
