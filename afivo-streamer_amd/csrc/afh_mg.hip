@@ -2314,7 +2314,7 @@ struct afh_mg {
   Coef *d_lvl_c = nullptr;    // lvl_c on the device (residual of every level in one launch)
   std::vector<double> h_norm;
   bool rstr_col = true;       // AFH_RSTR_COL=0: one coarse cell per thread (k_rstr_fas)
-  int rstr_k = AFH_RSTR_K;     // coarse cells per column (AFH_RSTR_K=2|4 at run time)
+  int rstr_k = AFH_RSTR_K;     // coarse cells per column (AFH_RSTR_K=2|4|8 at run time)
   int res_k = AFH_RES_K;       // residual cells per column (AFH_RES_K=2|4|8 at run time)
   int rstr_bs = 256;           // k_rstr_fas_col workgroup size (AFH_RSTR_BS=128|256)
   bool pair_ntl = false;       // AFH_GSRB_PAIR_NTL: non-temporal plane loads in the 64^3 pair
@@ -2542,7 +2542,10 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
   if (const char *env = getenv("AFH_GSRB_PAIR_SP")) mg->pair_sp = atoi(env) != 0;
   if (const char *env = getenv("AFH_GRAPHS")) mg->use_graphs = atoi(env) != 0;
   if (const char *env = getenv("AFH_RSTR_COL")) mg->rstr_col = atoi(env) != 0;
-  if (const char *env = getenv("AFH_RSTR_K")) mg->rstr_k = atoi(env) == 4 ? 4 : 2;
+  if (const char *env = getenv("AFH_RSTR_K")) {
+    const int k = atoi(env);
+    mg->rstr_k = k == 8 ? 8 : k == 4 ? 4 : 2;
+  }
   if (const char *env = getenv("AFH_GSRB_PAIR_NTL")) mg->pair_ntl = atoi(env) != 0;
   if (const char *env = getenv("AFH_RSTR_BS")) mg->rstr_bs = atoi(env) == 128 ? 128 : 256;
   if (const char *env = getenv("AFH_RES_K"))
@@ -2910,13 +2913,19 @@ static int32_t update_coarse(afh_mg *mg, int lvl) {
   const LevelList &L = cst(mg, t->ids, mg->ids_c);
   const int nid = L.n(lvl);
   if (nid) {
-    // column length (AFH_RSTR_K = 2 or 4): a column reads 2K + 2 fine planes
-    // for 2K; K = 4 halves that excess at twice the centre registers
+    // column length (AFH_RSTR_K = 2, 4 or 8): a column reads 2K + 2 fine
+    // planes for 2K; each doubling of K halves that excess at twice the
+    // centre registers
     // (workgroup size AFH_RSTR_BS: with 128 the blocks of neighbouring
     // columns along k are 8 apart in dispatch order, i.e. on the same XCD,
     // whose L2 then holds the fine plane both read)
     const int RK = mg->rstr_k, BS = mg->rstr_bs;
-    if (mg->rstr_col && RK == 4 && hn % 4 == 0)
+    if (mg->rstr_col && RK == 8 && hn % 8 == 0)
+      hipLaunchKernelGGL(k_rstr_fas_col<8>, dim3((hn * hn * (hn / 8) + BS - 1) / BS, nid),
+                         dim3(BS), 0, t->stream, t->ccv(mg->d.i_phi),
+                         t->ccv(mg->d.i_rhs), t->ccv(mg->d.i_tmp), t->d_boxes,
+                         L.at(lvl), nc, t->bsz, mg->lvl_c[lvl - 1]);
+    else if (mg->rstr_col && RK >= 4 && hn % 4 == 0)
       hipLaunchKernelGGL(k_rstr_fas_col<4>, dim3((hn * hn * (hn / 4) + BS - 1) / BS, nid),
                          dim3(BS), 0, t->stream, t->ccv(mg->d.i_phi),
                          t->ccv(mg->d.i_rhs), t->ccv(mg->d.i_tmp), t->d_boxes,

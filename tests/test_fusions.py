@@ -60,6 +60,18 @@ def test_s1_fusion_bitwise(switch, monkeypatch):
     _same(a, b)
 
 
+@pytest.mark.parametrize("k", ["2", "8"])
+def test_s1_restriction_columns_bitwise(k, monkeypatch):
+    """k_rstr_fas_col with columns of 2 and 8 coarse cells (S1's 16^3 boxes:
+    one column per (i, j) at 8) against the default 4 and the one-cell form
+    (AFH_RSTR_COL=0): the same operand order, so bitwise."""
+    a = _s1(monkeypatch, {"AFH_RSTR_K": k})
+    b = _s1(monkeypatch, {"AFH_RSTR_K": "4"})
+    _same(a, b)
+    c = _s1(monkeypatch, {"AFH_RSTR_COL": "0"})
+    _same(a, c)
+
+
 def test_direct_small_bitwise_8cubed(monkeypatch):
     """k_cs_direct_small on an 8^3 level-1 grid (one box, 3 levels of 8^3
     boxes): field solve and four unit steps, one workgroup vs the launches."""
