@@ -50,7 +50,7 @@ def rules(topo):
         return 8 * ns * ((np_ if np_ in (1, 2) else 2) + 1) + 32 + (8 if rhs else 0)
 
     return [
-        (r"k_gsrb_pair2<64, 64, 1, 0, true, true, true, 4>", 24, "ids", small),
+        (r"k_gsrb_pair2<64, 64, 1, 0, true, true, true, 4[,>]", 24, "ids", small),
         (r"k_gsrb_pair", 24, "ids", None),
         (r"k_gsrb_v", 16, "ids", None),
         (r"k_gsrb\(", 16, "ids", split),
