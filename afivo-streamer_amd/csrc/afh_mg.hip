@@ -2261,8 +2261,8 @@ __global__ void __launch_bounds__(1024)
 
 using namespace afh;
 
-#ifndef AFH_RES_K  // cells per thread column of k_residual (8, 4 or 2)
-#define AFH_RES_K 4
+#ifndef AFH_RES_K  // cells per thread column of k_residual (8, 4 or 2; 0: 8 on
+#define AFH_RES_K 0  // boxes of 32^3 and up, 4 below)
 #endif
 #ifndef AFH_RSTR_K  // coarse cells per thread column of k_rstr_fas_col
 #define AFH_RSTR_K 4
@@ -3395,7 +3395,10 @@ static int32_t residual_levels(afh_mg *mg, int max_lvl, bool max_out) {
       const int n = one ? (lvl == 1 ? n_all : 0) : L.n(lvl);
       const bool mx = max_out && !part;
       if (n) {
-        const int kc = nc % mg->res_k == 0 ? mg->res_k : nc % 4 == 0 ? 4 : 2;
+        // columns of 8 on the large boxes: 693 against 728 us per 64^3 leaf
+        // launch (profiles/r03_ab_res_k.txt); small boxes keep their threads
+        const int rk = mg->res_k ? mg->res_k : nc >= 32 ? 8 : 4;
+        const int kc = nc % rk == 0 ? rk : nc % 4 == 0 ? 4 : 2;
         const dim3 grid((n3 / kc + 255) / 256, n);
         auto kern = mx ? (kc == 8 ? k_residual<true, 8> : kc == 4 ? k_residual<true, 4>
                                                                   : k_residual<true, 2>)

@@ -72,6 +72,13 @@ def test_s1_restriction_columns_bitwise(k, monkeypatch):
     _same(a, c)
 
 
+@pytest.mark.parametrize("k", ["2", "8"])
+def test_s1_residual_columns_bitwise(k, monkeypatch):
+    """k_residual with columns of 2 and 8 cells against 4 (S1's 16^3 boxes):
+    the residuals and their maximum are per-cell values, so bitwise."""
+    _same(_s1(monkeypatch, {"AFH_RES_K": k}), _s1(monkeypatch, {"AFH_RES_K": "4"}))
+
+
 def test_direct_small_bitwise_8cubed(monkeypatch):
     """k_cs_direct_small on an 8^3 level-1 grid (one box, 3 levels of 8^3
     boxes): field solve and four unit steps, one workgroup vs the launches."""
