@@ -2986,9 +2986,18 @@ static int32_t correct_children(afh_mg *mg, int lvl) {
   }
   const int nid = t->ids.n(lvl);
   if (nid) {
-    const int K = nc % 4 == 0 ? 4 : 2;
+    // column length 4; AFH_PROLONG_K=8 where nc allows: the launch is
+    // faster (195 against 223 us on S1-64) but the pair after it slower,
+    // 13.32 against 12.57-12.60 ms per step (profiles/r03_ab_prolong_k.txt)
+    static const int env_k = getenv("AFH_PROLONG_K") ? atoi(getenv("AFH_PROLONG_K")) : 0;
+    const int want = env_k ? env_k : 4;
+    const int K = want == 8 && nc % 8 == 0 ? 8 : nc % 4 == 0 ? 4 : 2;
     const dim3 grid((nc * nc * (nc / K) + 255) / 256, nid);
-    if (K == 4)
+    if (K == 8)
+      hipLaunchKernelGGL(k_prolong<8>, grid, dim3(256), 0, t->stream,
+                         t->ccv(mg->d.i_phi), t->ccv(mg->d.i_tmp), t->d_boxes,
+                         t->ids.at(lvl), nc, t->bsz);
+    else if (K == 4)
       hipLaunchKernelGGL(k_prolong<4>, grid, dim3(256), 0, t->stream,
                          t->ccv(mg->d.i_phi), t->ccv(mg->d.i_tmp), t->d_boxes,
                          t->ids.at(lvl), nc, t->bsz);

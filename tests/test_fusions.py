@@ -79,6 +79,11 @@ def test_s1_residual_columns_bitwise(k, monkeypatch):
     _same(_s1(monkeypatch, {"AFH_RES_K": k}), _s1(monkeypatch, {"AFH_RES_K": "4"}))
 
 
+def test_s1_prolong_columns_bitwise(monkeypatch):
+    """k_prolong with columns of 8 cells (AFH_PROLONG_K=8) against 4."""
+    _same(_s1(monkeypatch, {"AFH_PROLONG_K": "8"}), _s1(monkeypatch, {"AFH_PROLONG_K": "4"}))
+
+
 def test_direct_small_bitwise_8cubed(monkeypatch):
     """k_cs_direct_small on an 8^3 level-1 grid (one box, 3 levels of 8^3
     boxes): field solve and four unit steps, one workgroup vs the launches."""
