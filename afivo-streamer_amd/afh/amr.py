@@ -46,6 +46,40 @@ CHILD_ADJ_NB = ((0, 2, 4, 6), (1, 3, 5, 7), (0, 1, 4, 5), (2, 3, 6, 7),
                 (0, 1, 2, 3), (4, 5, 6, 7))  # 0-based af_child_adj_nb
 
 
+class _Dim:
+    """afivo's per-NDIM constants (m_af_types.f90:114-236): child offsets,
+    neighbour offsets, af_neighb_rev, af_child_adj_nb, the neighbor_mat
+    directions in KJI_DO(-1,1) order (k outer, i inner)."""
+
+    def __init__(self, ndim):
+        self.ndim = ndim
+        self.n_children = 2 ** ndim
+        self.n_neighbors = 2 * ndim
+        self.n_mat = 3 ** ndim
+        self.center = (self.n_mat - 1) // 2
+        if ndim == 3:
+            self.child_dix, self.neighb_dix = CHILD_DIX, NEIGHB_DIX
+            self.neighb_rev, self.child_adj_nb = NEIGHB_REV, CHILD_ADJ_NB
+            self.dirs = [(di, dj, dk) for dk in (-1, 0, 1) for dj in (-1, 0, 1)
+                         for di in (-1, 0, 1)]
+        elif ndim == 2:
+            self.child_dix = ((0, 0), (1, 0), (0, 1), (1, 1))
+            self.neighb_dix = ((-1, 0), (1, 0), (0, -1), (0, 1))
+            self.neighb_rev = (1, 0, 3, 2)
+            self.child_adj_nb = ((0, 2), (1, 3), (0, 1), (2, 3))
+            self.dirs = [(di, dj) for dj in (-1, 0, 1) for di in (-1, 0, 1)]
+        else:
+            raise ValueError("NDIM = %d not supported" % ndim)
+
+    def nmat_index(self, d):
+        """Index of neighbor_mat(d) in the flat 3^NDIM list (i fastest)."""
+        return sum((d[q] + 1) * 3 ** q for q in range(self.ndim))
+
+    def ix_to_ichild(self, ix):
+        """af_ix_to_ichild (m_af_types.f90:1012-1023), 0-based."""
+        return sum((1 - (ix[q] & 1)) << q for q in range(self.ndim))
+
+
 def nmat_index(di, dj, dk):
     """Index of neighbor_mat(di, dj, dk) in a flat 27-list (i fastest)."""
     return (di + 1) + 3 * (dj + 1) + 9 * (dk + 1)
@@ -54,10 +88,6 @@ def nmat_index(di, dj, dk):
 def ix_to_ichild(ix):
     """af_ix_to_ichild (m_af_types.f90:1012-1023), 0-based."""
     return (1 - (ix[0] & 1)) + 2 * (1 - (ix[1] & 1)) + 4 * (1 - (ix[2] & 1))
-
-
-# the 26 neighbour directions in KJI_DO(-1,1) order (k outer, i inner)
-_DIRS = [(di, dj, dk) for dk in (-1, 0, 1) for dj in (-1, 0, 1) for di in (-1, 0, 1)]
 
 
 class RefInfo:
@@ -77,23 +107,27 @@ class RefInfo:
 
 
 class AfTree:
-    """The af_t topology (m_af_types.f90:326-393) of a 3D Cartesian tree."""
+    """The af_t topology (m_af_types.f90:326-393) of a Cartesian tree, NDIM = 3
+    (the default) or 2 (len(grid_size) == 2: afivo/lib_2d, BASELINE config 1)."""
 
-    def __init__(self, n_cell, r_max, grid_size, periodic=(False, False, False),
-                 r_min=(0.0, 0.0, 0.0), box_limit=10 ** 7):
+    def __init__(self, n_cell, r_max, grid_size, periodic=None, r_min=None,
+                 box_limit=10 ** 7):
         nc = int(n_cell)
         if nc < 2 or nc % 2:
             raise ValueError("n_cell should be even and >= 2")
         grid_size = [int(g) for g in grid_size]
+        nd = len(grid_size)
+        self.D = _Dim(nd)
+        self.ndim = nd
         if any(g < nc or g % nc for g in grid_size):
             raise ValueError("coarse_grid_size must be a multiple of n_cell")
         self.nc = nc
-        self.r_base = np.asarray(r_min, float)
-        self.domain = np.asarray(r_max, float)
+        self.r_base = np.zeros(nd) if r_min is None else np.asarray(r_min, float)[:nd]
+        self.domain = np.asarray(r_max, float)[:nd]
         # dr_base = (r_max - r_min) / grid_size (af_init, 174)
         self.dr_base = (self.domain - self.r_base) / np.asarray(grid_size, float)
         self.coarse_grid_size = grid_size
-        self.periodic = tuple(bool(p) for p in periodic)
+        self.periodic = tuple(bool(p) for p in (periodic or (False,) * nd))
         self.box_limit = int(box_limit)
         # per-box records, indexed by id (index 0 unused)
         self.lvl, self.ix, self.parent = [0], [None], [0]
@@ -123,38 +157,41 @@ class AfTree:
         return self.children[bid][0] > NO_BOX
 
     def _set_coarse_grid(self):
-        """af_set_coarse_grid (m_af_core.f90:206-340), NDIM = 3."""
+        """af_set_coarse_grid (m_af_core.f90:206-340)."""
+        D, nd = self.D, self.ndim
         nx = [g // self.nc for g in self.coarse_grid_size]
 
-        def index(i, j, k):  # create_index_array (436-501)
-            q = [i, j, k]
-            for d in range(3):
+        def index(q):  # create_index_array (436-501)
+            q = list(q)
+            for d in range(nd):
                 if q[d] < 1 or q[d] > nx[d]:
                     if not self.periodic[d]:
                         return PHYS_BOUNDARY
                     q[d] = nx[d] if q[d] < 1 else 1
-            return (q[2] - 1) * nx[1] * nx[0] + (q[1] - 1) * nx[0] + q[0]
+            bid, stride = 0, 1
+            for d in range(nd):
+                bid += (q[d] - 1) * stride
+                stride *= nx[d]
+            return bid + 1
 
-        n = nx[0] * nx[1] * nx[2]
+        n = int(np.prod(nx))
         ids = self.get_free_ids(n)
         self.lvls[1]["ids"] = list(ids)
         self.lvls[1]["leaves"] = list(ids)
-        for k in range(1, nx[2] + 1):
-            for j in range(1, nx[1] + 1):
-                for i in range(1, nx[0] + 1):
-                    bid = index(i, j, k)
-                    self.lvl[bid] = 1
-                    self.ix[bid] = (i, j, k)
-                    self.dr[bid] = self.dr_base.copy()
-                    self.r_min[bid] = self.r_base + (np.array([i, j, k]) - 1) * \
-                        self.dr_base * self.nc
-                    self.parent[bid] = NO_BOX
-                    self.children[bid] = [NO_BOX] * 8
-                    self.neighbors[bid] = [index(i + d[0], j + d[1], k + d[2])
-                                           for d in NEIGHB_DIX]
-                    self.nmat[bid] = [index(i + di, j + dj, k + dk)
-                                      for (di, dj, dk) in _DIRS]
-                    self.in_use[bid] = True
+        # box ids i fastest (KJI order)
+        for q in np.ndindex(*reversed(nx)):
+            ixq = tuple(int(x) + 1 for x in reversed(q))
+            bid = index(ixq)
+            self.lvl[bid] = 1
+            self.ix[bid] = ixq
+            self.dr[bid] = self.dr_base.copy()
+            self.r_min[bid] = self.r_base + (np.array(ixq) - 1) * self.dr_base * self.nc
+            self.parent[bid] = NO_BOX
+            self.children[bid] = [NO_BOX] * D.n_children
+            self.neighbors[bid] = [index([ixq[d] + dd[d] for d in range(nd)])
+                                   for dd in D.neighb_dix]
+            self.nmat[bid] = [index([ixq[d] + dd[d] for d in range(nd)]) for dd in D.dirs]
+            self.in_use[bid] = True
         self.highest_lvl = 1
 
     def get_free_ids(self, n):
@@ -173,75 +210,78 @@ class AfTree:
     # ------------------------------------------------------- connectivity
     def _find_neighb(self, bid, dix):
         """find_neighb (m_af_core.f90:636-661)."""
+        D, nd = self.D, self.ndim
         p_id = self.parent[bid]
-        c_ix = ix_to_ichild(self.ix[bid])
-        low = CHILD_DIX[c_ix]
-        dix_c = [dix[d] if ((dix[d] == -1) == (low[d] == 0)) else 0 for d in range(3)]
-        p_nb = self.nmat[p_id][nmat_index(*dix_c)]
+        low = D.child_dix[D.ix_to_ichild(self.ix[bid])]
+        dix_c = [dix[d] if ((dix[d] == -1) == (low[d] == 0)) else 0 for d in range(nd)]
+        p_nb = self.nmat[p_id][D.nmat_index(dix_c)]
         if p_nb <= NO_BOX:
             return p_nb
-        q = [self.ix[bid][d] + dix[d] for d in range(3)]
-        return self.children[p_nb][ix_to_ichild(q)]
+        q = [self.ix[bid][d] + dix[d] for d in range(nd)]
+        return self.children[p_nb][D.ix_to_ichild(q)]
 
     def _set_neighbs(self, bid):
         """set_neighbs (m_af_core.f90:595-633)."""
+        D = self.D
         nm = self.nmat[bid]
-        for (di, dj, dk) in _DIRS:
-            m = nmat_index(di, dj, dk)
+        for dd in D.dirs:
+            m = D.nmat_index(dd)
             if nm[m] == NO_BOX:
-                nb_id = self._find_neighb(bid, (di, dj, dk))
+                nb_id = self._find_neighb(bid, dd)
                 if nb_id > NO_BOX:
                     nm[m] = nb_id
-                    self.nmat[nb_id][nmat_index(-di, -dj, -dk)] = bid
+                    self.nmat[nb_id][D.nmat_index([-x for x in dd])] = bid
         nbs = self.neighbors[bid]
-        for nb in range(6):
+        for nb in range(D.n_neighbors):
             if nbs[nb] == NO_BOX:
-                nb_id = nm[nmat_index(*NEIGHB_DIX[nb])]
+                nb_id = nm[D.nmat_index(D.neighb_dix[nb])]
                 if nb_id > NO_BOX:
                     nbs[nb] = nb_id
-                    self.neighbors[nb_id][NEIGHB_REV[nb]] = bid
+                    self.neighbors[nb_id][D.neighb_rev[nb]] = bid
 
     def _add_children(self, bid, c_ids):
         """add_children (m_af_core.f90:1188-1233)."""
+        D, nd = self.D, self.ndim
         self.children[bid] = list(c_ids)
         base = [2 * x - 1 for x in self.ix[bid]]
-        for c in range(8):
+        for c in range(D.n_children):
             cid = c_ids[c]
-            dix = CHILD_DIX[c]
-            self.ix[cid] = tuple(base[d] + dix[d] for d in range(3))
+            dix = D.child_dix[c]
+            self.ix[cid] = tuple(base[d] + dix[d] for d in range(nd))
             self.lvl[cid] = self.lvl[bid] + 1
             self.parent[cid] = bid
-            self.children[cid] = [NO_BOX] * 8
-            self.neighbors[cid] = [NO_BOX] * 6
-            nm = [NO_BOX] * 27
-            nm[nmat_index(0, 0, 0)] = cid
+            self.children[cid] = [NO_BOX] * D.n_children
+            self.neighbors[cid] = [NO_BOX] * D.n_neighbors
+            nm = [NO_BOX] * D.n_mat
+            nm[D.center] = cid
             self.nmat[cid] = nm
             self.dr[cid] = 0.5 * self.dr[bid]
             self.r_min[cid] = self.r_min[bid] + 0.5 * self.dr[bid] * \
                 np.asarray(dix, float) * self.nc
-        for nb in range(6):
+        for nb in range(D.n_neighbors):
             pnb = self.neighbors[bid][nb]
             if pnb < NO_BOX:  # physical boundary
-                for c in CHILD_ADJ_NB[nb]:
+                for c in D.child_adj_nb[nb]:
                     cid = c_ids[c]
                     self.neighbors[cid][nb] = pnb
-                    self.nmat[cid][nmat_index(*NEIGHB_DIX[nb])] = pnb
+                    self.nmat[cid][D.nmat_index(D.neighb_dix[nb])] = pnb
         for cid in c_ids:  # af_init_box: data zeroed on the device
             self.in_use[cid] = True
 
     def _remove_children(self, bid):
         """remove_children (m_af_core.f90:1151-1185)."""
+        D = self.D
         for cid in self.children[bid]:
-            for nb in range(6):
+            for nb in range(D.n_neighbors):
                 nb_id = self.neighbors[cid][nb]
                 if nb_id > NO_BOX:
-                    self.neighbors[nb_id][NEIGHB_REV[nb]] = NO_BOX
-            for (di, dj, dk) in _DIRS:
-                nb_id = self.nmat[cid][nmat_index(di, dj, dk)]
+                    self.neighbors[nb_id][D.neighb_rev[nb]] = NO_BOX
+            for dd in D.dirs:
+                nb_id = self.nmat[cid][D.nmat_index(dd)]
                 if nb_id > NO_BOX:
-                    self.nmat[nb_id][nmat_index(-di, -dj, -dk)] = NO_BOX
+                    self.nmat[nb_id][D.nmat_index([-x for x in dd])] = NO_BOX
             self.in_use[cid] = False  # af_deactivate_box
-        self.children[bid] = [NO_BOX] * 8
+        self.children[bid] = [NO_BOX] * D.n_children
 
     def _set_leaves_parents(self, lvl):
         """set_leaves_parents (m_af_core.f90:504-535)."""
@@ -262,14 +302,15 @@ class AfTree:
             ref[bid] = max(ref[bid], RM_REF)
         if mask:
             nm = self.nmat[bid]
-            for m in range(27):
-                if (mask >> m) & 1 and m != 13:
+            for m in range(self.D.n_mat):
+                if (mask >> m) & 1 and m != self.D.center:
                     nb_id = nm[m]
                     if nb_id > NO_BOX:
                         ref[nb_id] = DO_REF
 
     def _consistent_ref_flags(self, flags_fn):
         """consistent_ref_flags (m_af_core.f90:929-1013), without ref_links."""
+        D = self.D
         ref = [_UNSET] * (self.highest_id + 1)
         ids, parents_of = [], []
         for lvl in range(1, self.highest_lvl + 1):
@@ -277,7 +318,7 @@ class AfTree:
                 ids.append(bid)
                 if self.lvl[bid] > 1:
                     p = self.parent[bid]
-                    c = ix_to_ichild(self.ix[bid])
+                    c = D.ix_to_ichild(self.ix[bid])
                     if all(self.has_children(self.children[p][q]) for q in range(c)):
                         parents_of.append((len(ids) - 1, p))
         # the refinement routine for every box it is called on, in one call
@@ -299,17 +340,18 @@ class AfTree:
 
     def _ensure_two_one_balance(self, ref):
         """ensure_two_one_balance (m_af_core.f90:1016-1057)."""
+        n_nb = self.D.n_neighbors
         for lvl in range(self.highest_lvl, 0, -1):
             for bid in self.lvls[lvl]["leaves"]:
                 if ref[bid] in (DO_REF, REFINE):
                     ref[bid] = REFINE
-                    for nb in range(6):
+                    for nb in range(n_nb):
                         if self.neighbors[bid][nb] == NO_BOX:
                             p_nb = self.neighbors[self.parent[bid]][nb]
                             if p_nb > NO_BOX:  # always, in a balanced tree
                                 ref[p_nb] = REFINE
                 elif ref[bid] == RM_REF:
-                    for nb in range(6):
+                    for nb in range(n_nb):
                         nb_id = self.neighbors[bid][nb]
                         if nb_id > NO_BOX and (self.has_children(nb_id) or
                                                ref[nb_id] > KEEP_REF):
@@ -345,7 +387,7 @@ class AfTree:
                 if bid > n_ref:
                     continue  # a newly added box
                 if ref[bid] == REFINE:
-                    c_ids = self.get_free_ids(8)
+                    c_ids = self.get_free_ids(self.D.n_children)
                     self._add_children(bid, c_ids)
                     add += self.children[bid]
                 elif ref[bid] == DEREFINE:
@@ -393,7 +435,8 @@ class AfTree:
         return self.dr_base * 0.5 ** (lvl - 1)
 
     def total_volume(self):
-        """af_total_volume (m_af_utils.f90): the coarse boxes' volume."""
+        """af_total_volume (m_af_utils.f90): the coarse boxes' volume (area
+        in 2-D)."""
         v = 0.0
         for bid in self.lvls[1]["ids"]:
             v += float(np.prod(self.dr[bid] * self.nc))
@@ -405,21 +448,24 @@ class AfTree:
 
     def topology(self):
         """The topology dict the device tree is created from (afh/tree.py
-        conventions; ids not in use have level 0)."""
+        conventions; ids not in use have level 0; a 2-D tree has ndim = 2)."""
+        D, nd = self.D, self.ndim
         nb = self.highest_id
         out = {"nc": np.int32(self.nc), "n_boxes": np.int32(nb),
                "highest_lvl": np.int32(self.highest_lvl),
                "coarse_grid_size": np.array(self.coarse_grid_size, np.int32),
                "r_base": self.r_base.copy(), "dr_base": self.dr_base.copy(),
                "domain": self.domain.copy()}
+        if nd != 3:
+            out["ndim"] = np.int32(nd)
         lvl = np.zeros(nb, np.int32)
-        ix = np.zeros((nb, 3), np.int32)
+        ix = np.zeros((nb, nd), np.int32)
         parent = np.zeros(nb, np.int32)
-        children = np.zeros((nb, 8), np.int32)
-        neighbors = np.zeros((nb, 6), np.int32)
-        nmat = np.zeros((nb, 27), np.int32)
-        r_min = np.zeros((nb, 3))
-        dr = np.zeros((nb, 3))
+        children = np.zeros((nb, D.n_children), np.int32)
+        neighbors = np.zeros((nb, D.n_neighbors), np.int32)
+        nmat = np.zeros((nb, D.n_mat), np.int32)
+        r_min = np.zeros((nb, nd))
+        dr = np.zeros((nb, nd))
         for b in range(1, nb + 1):
             if not self.in_use[b]:
                 continue
@@ -445,4 +491,4 @@ class AfTree:
         return [b for l in range(1, self.highest_lvl + 1) for b in self.lvls[l]["leaves"]]
 
     def n_leaf_cells(self):
-        return len(self.leaves()) * self.nc ** 3
+        return len(self.leaves()) * self.nc ** self.ndim

@@ -257,6 +257,11 @@ class Library:
     def symbols(self):
         return [self.prefix + n for n in self.fn]
 
+    def has(self, name):
+        """Whether the library implements entry point `name` (the 2-D build
+        exports a subset, include/afivo_hip_2d.h)."""
+        return name in self.fn
+
 
 _loaded = {}
 

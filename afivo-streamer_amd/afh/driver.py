@@ -134,7 +134,12 @@ class Simulation:
         self.coarse_cycles = coarse_cycles
         self.coarse_tol = coarse_tol
         self.capacity_factor = capacity_factor
-        self.fused_rhs = fuse_rhs
+        # NDIM: the exported coarse grid has one entry per dimension (2: the
+        # reference's 2-D build, programs/standard_2d, on libafivo_hip_2d.so)
+        self.ndim = len(c.ia("coarse_grid_size_value"))
+        # the rhs folded into the density update and the face field formed
+        # from phi are entry points of the 3-D library only
+        self.fused_rhs = fuse_rhs and lib.has("fluid_set_rhs_output")
         # field_compute reads max|rhs| with the first residual (AFH_DEFER=0:
         # before the V-cycle, as the reference orders it; for A/B runs)
         self._defer_ok = os.environ.get("AFH_DEFER", "1") != "0"
@@ -142,7 +147,8 @@ class Simulation:
         # the gradient then writes |E| only; not with an electrode (its
         # boxes' gradient is mg_box_lpllsf_gradient). AFH_FACES_FROM_PHI=0
         # stores and reads the face field, as the reference does (A/B runs)
-        self._faces_from_phi_ok = os.environ.get("AFH_FACES_FROM_PHI", "1") != "0"
+        self._faces_from_phi_ok = (os.environ.get("AFH_FACES_FROM_PHI", "1") != "0" and
+                                   lib.has("fluid_set_field_source"))
         self.faces_from_phi = False
         if c.s("time_integrator") != "heuns_method":
             raise NotImplementedError("time integrator %s" % c.s("time_integrator"))
@@ -256,10 +262,11 @@ class Simulation:
         # init conditions (m_init_cond.f90:38-144)
         self.background = c.r("background_density")
         self.seeds = []
+        nd = self.ndim
         for n in range(len(c.ra("seed_density"))):
             self.seeds.append({
-                "r0": c.ra("seed_rel_r0")[3 * n:3 * n + 3] * self.L + self.origin,
-                "r1": c.ra("seed_rel_r1")[3 * n:3 * n + 3] * self.L + self.origin,
+                "r0": c.ra("seed_rel_r0")[nd * n:nd * n + nd] * self.L + self.origin,
+                "r1": c.ra("seed_rel_r1")[nd * n:nd * n + nd] * self.L + self.origin,
                 "n0": c.ra("seed_density")[n], "n1": c.ra("seed_density2")[n],
                 "type": c.ia("seed_charge_type")[n], "width": c.ra("seed_width")[n],
                 "falloff": c.sa("seed_falloff")[n]})
@@ -498,9 +505,10 @@ class Simulation:
         return t
 
     def phi_bc(self):
-        """field_bc_homogeneous (src/m_field.f90:547-567)."""
-        return [(capi.BC_NEUMANN, 0.0)] * 4 + [(capi.BC_DIRICHLET, 0.0),
-                                               (capi.BC_DIRICHLET, self.voltage)]
+        """field_bc_homogeneous (src/m_field.f90:547-567): Dirichlet 0 and
+        the voltage on the faces normal to the last dimension."""
+        return [(capi.BC_NEUMANN, 0.0)] * (2 * self.ndim - 2) + [
+            (capi.BC_DIRICHLET, 0.0), (capi.BC_DIRICHLET, self.voltage)]
 
     # --------------------------------------------------------- physics
     def field_from_potential(self):
@@ -529,7 +537,7 @@ class Simulation:
         # with an electrode the initial convergence test is less strict
         conv_fac = 1e-8 if self.lsf is not None else 1e-10
         threshold = max(1e-6, max_rhs * self.max_rel_res,
-                        conv_fac * abs(self.voltage) / (self.L[2] * self.af.min_dr()))
+                        conv_fac * abs(self.voltage) / (self.L[-1] * self.af.min_dr()))
         res = []
         if not have_guess:
             for i in range(1, 101):
@@ -599,12 +607,17 @@ class Simulation:
         d.max_dx, d.min_dx = c.r("refine_max_dx"), c.r("refine_min_dx")
         d.electrode_dx = c.r("refine_electrode_dx")
         d.init_fac = c.r("refine_init_fac")
+        nd = self.ndim
+
+        def v3(a, n):  # entry n of a list of nd-vectors, as the 3-slot field
+            return [float(x) for x in a[nd * n:nd * n + nd]] + [0.0] * (3 - nd)
+
         d.n_seeds = 0
         if self.global_time < c.r("refine_init_time"):
             d.n_seeds = len(self.seeds)
             for n, sd in enumerate(self.seeds):
-                d.seed_r0[n][:] = list(sd["r0"])
-                d.seed_r1[n][:] = list(sd["r1"])
+                d.seed_r0[n][:] = v3(sd["r0"], 0)
+                d.seed_r1[n][:] = v3(sd["r1"], 0)
                 d.seed_width[n] = sd["width"]
         rdr, rts = c.ra("refine_regions_dr"), c.ra("refine_regions_tstop")
         rmin, rmax = c.ra("refine_regions_rmin"), c.ra("refine_regions_rmax")
@@ -612,8 +625,8 @@ class Simulation:
         for n in range(len(rdr)):
             if self.global_time <= rts[n]:
                 d.region_dr[k] = rdr[n]
-                d.region_rmin[k][:] = list(rmin[3 * n:3 * n + 3])
-                d.region_rmax[k][:] = list(rmax[3 * n:3 * n + 3])
+                d.region_rmin[k][:] = v3(rmin, n)
+                d.region_rmax[k][:] = v3(rmax, n)
                 k += 1
         d.n_regions = k
         ldr = c.ra("refine_limits_dr")
@@ -621,8 +634,8 @@ class Simulation:
         d.n_limits = len(ldr)
         for n in range(len(ldr)):
             d.limit_dr[n] = ldr[n]
-            d.limit_rmin[n][:] = list(lmin[3 * n:3 * n + 3])
-            d.limit_rmax[n][:] = list(lmax[3 * n:3 * n + 3])
+            d.limit_rmin[n][:] = v3(lmin, n)
+            d.limit_rmax[n][:] = v3(lmax, n)
         return d
 
     def adjust_refinement(self):
@@ -651,19 +664,13 @@ class Simulation:
     def init_cond_set_box(self, ids, arrays):
         """init_cond_set_box (src/m_init_cond.f90:217-291) on boxes `ids`
         (cells 0..nc+1), into host arrays {iv: (n_boxes, ng, ng, ng)}."""
-        nc = self.af.nc
-        ng = nc + 2
-        idx = np.arange(ng) - 0.5  # af_r_cc: r_min + (i - 0.5) dr
+        ng = self.af.nc + 2
+        shape = (ng,) * self.ndim
         ne, ni = arrays[self.i_electron], arrays[self.i_1pos_ion]
         for b in ids:
-            rmin, dr = self.af.r_min[b], self.af.dr[b]
-            x = rmin[0] + idx * dr[0]
-            y = rmin[1] + idx * dr[1]
-            z = rmin[2] + idx * dr[2]
-            zz, yy, xx = np.meshgrid(z, y, x, indexing="ij")
-            r = np.stack([xx.ravel(), yy.ravel(), zz.ravel()], axis=1)
-            e = np.full(ng ** 3, self.background)
-            p = np.full(ng ** 3, self.background)
+            r = self.box_cells(b)
+            e = np.full(len(r), self.background)
+            p = np.full(len(r), self.background)
             for sd in self.seeds:
                 dens = density_line(r, sd["r0"], sd["r1"], sd["n0"], sd["n1"],
                                     sd["width"], sd["falloff"])
@@ -676,24 +683,25 @@ class Simulation:
                     p = p + dens
                 else:
                     raise ValueError("Invalid seed_charge_type")
-            ne[b - 1] = e.reshape(ng, ng, ng)
-            ni[b - 1] = p.reshape(ng, ng, ng)
+            ne[b - 1] = e.reshape(shape)
+            ni[b - 1] = p.reshape(shape)
 
     def box_cells(self, b):
-        """af_r_cc of every cell 0..nc+1 of box b, (ng^3, 3), i fastest."""
+        """af_r_cc (r_min + (i - 0.5) dr) of every cell 0..nc+1 of box b,
+        (ng^NDIM, NDIM), i fastest."""
         ng = self.af.nc + 2
         idx = np.arange(ng) - 0.5
         rmin, dr = self.af.r_min[b], self.af.dr[b]
-        zz, yy, xx = np.meshgrid(rmin[2] + idx * dr[2], rmin[1] + idx * dr[1],
-                                 rmin[0] + idx * dr[0], indexing="ij")
-        return np.stack([xx.ravel(), yy.ravel(), zz.ravel()], axis=1)
+        axes = [rmin[d] + idx * dr[d] for d in reversed(range(self.ndim))]
+        g = np.meshgrid(*axes, indexing="ij")
+        return np.stack([a.ravel() for a in reversed(g)], axis=1)
 
     def _set_gas(self, ids):
         """set_gas_density_from_user_function (streamer.f90:672-681) on boxes ids."""
         ng = self.af.nc + 2
         a = self.tree.get_cc(self.i_gas_dens)
         for b in ids:
-            a[b - 1] = self.user.gas_density(self.box_cells(b)).reshape(ng, ng, ng)
+            a[b - 1] = self.user.gas_density(self.box_cells(b)).reshape((ng,) * self.ndim)
         self.tree.put_cc(self.i_gas_dens, a)
 
     def _set_init(self, ids):
@@ -701,11 +709,11 @@ class Simulation:
         self.init_cond_set_box(ids, arrays)
         if self.user is not None and hasattr(self.user, "initial_conditions"):
             # user_initial_conditions after init_cond_set_box (streamer.f90:472-475)
-            ng = self.af.nc + 2
+            shape = (self.af.nc + 2,) * self.ndim
             for b in ids:
                 ne, ni = self.user.initial_conditions(self, self.box_cells(b))
-                arrays[self.i_electron][b - 1] = ne.reshape(ng, ng, ng)
-                arrays[self.i_1pos_ion][b - 1] = ni.reshape(ng, ng, ng)
+                arrays[self.i_electron][b - 1] = ne.reshape(shape)
+                arrays[self.i_1pos_ion][b - 1] = ni.reshape(shape)
         for iv, a in arrays.items():
             self.tree.put_cc(iv, a)
 

@@ -115,9 +115,13 @@ class Tree:
         return Tree(self.lib, topo, self.n_var_cell, self.n_var_face,
                     _regrid_of=self, box_capacity=self.box_capacity)
 
-    def set_cc_prolong(self, iv, method, limiter=capi.LIM_GMINMOD43):
+    def set_cc_prolong(self, iv, method, limiter=None):
         """tree%cc_methods(iv)%prolong (capi.PROLONG_LINEAR / PROLONG_LIMIT)
-        and prolong_limiter; iv becomes an automatic variable."""
+        and prolong_limiter; iv becomes an automatic variable. The default
+        limiter is af_set_cc_methods' own: MC in 2-D, gminmod43 in 3-D
+        (m_af_core.f90:399-408)."""
+        if limiter is None:
+            limiter = capi.LIM_MC if self.ndim < 3 else capi.LIM_GMINMOD43
         self.lib.call("set_cc_prolong", self.h, iv, method, limiter)
 
     # -- lifetime

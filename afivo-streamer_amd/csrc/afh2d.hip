@@ -846,6 +846,8 @@ struct Meth {
   afh_bc bc[4];
   int rb = AFH_RB_GC_INTERP;
   int lim = AFH_LIM_MC;  // af_set_cc_methods default in 2-D (m_af_core.f90:401-402)
+  int prolong = AFH_PROLONG_NONE;  // afh_set_cc_prolong
+  int prolong_lim = AFH_LIM_MC;
 };
 
 }  // namespace afh2
@@ -865,7 +867,9 @@ struct afh_tree {
   double *cc = nullptr, *fc = nullptr, *gc2 = nullptr;
   unsigned long long *red = nullptr, *red_out = nullptr, *h_red = nullptr;
   std::vector<Meth> meth;
+  std::vector<int> auto_vars;  // tree%cc_auto_vars (afh_set_cc_prolong order)
   std::vector<double> lvl_dr;  // 2 per level
+  double *d_boxred = nullptr;  // per-leaf (value, cell) of afh_tree_sum_cc / reduce_loc
   double *ccv(int iv) const { return cc + (size_t)(iv - 1) * nb * bsz; }
   double *fcv(int ivf) const { return fc + (size_t)(ivf - 1) * nb * fsz; }
   Bc4 bc4(int iv) const {
@@ -973,8 +977,8 @@ int32_t afh_tree_create(const afh_tree_desc *desc, int32_t device, afh_tree **ou
   if (nc < 2 || nc % 2 || desc->n_boxes < 1 || desc->highest_lvl < 1 ||
       desc->n_var_cell < 1 || desc->n_var_face < 0)
     return set_error(AFH_ERR_ARG, "afh_tree_create: bad sizes");
-  if (desc->box_capacity > desc->n_boxes)
-    return set_error(AFH_ERR_UNSUPPORTED, "2-D: box_capacity (in-place regrid) not built");
+  // box_capacity (the 3-D in-place regrid) is accepted and not used: a 2-D
+  // regrid copies the persisting boxes into the new tree's pools
   if (device >= 0) H2(hipSetDevice(device));
   afh_tree *t = new afh_tree();
   H2(hipGetDevice(&t->device));
@@ -1055,7 +1059,7 @@ int32_t afh_tree_destroy(afh_tree *t) {
   for (LevelList *L : {&t->ids, &t->leaves, &t->parents, &t->refb, &t->children_of, &t->cflux})
     free_list(*L);
   hipFree(t->d_boxes), hipFree(t->cc), hipFree(t->fc), hipFree(t->gc2);
-  hipFree(t->red), hipFree(t->red_out), hipHostFree(t->h_red);
+  hipFree(t->red), hipFree(t->red_out), hipHostFree(t->h_red), hipFree(t->d_boxred);
   hipStreamDestroy(t->stream);
   delete t;
   return AFH_OK;
@@ -1687,6 +1691,477 @@ int32_t afh_fluid_forward_euler(afh_fluid *f, double dt, int32_t s_deriv, int32_
   int32_t e;
   if ((e = flux_tree(f, s_deriv, dt_lim))) return e;
   return update(f, dt, s_deriv, n_prev, s_prev, w_prev, s_out, last_step, dt_lim + 2);
+}
+
+}  // extern "C"
+
+// ============================================================ regrid, refinement, sums
+namespace afh2 {
+
+// af_prolong_limit / af_prolong_linear, NDIM = 2 (m_af_prolong.f90:311-420,
+// 531-679) with add = .false.: one thread per parent cell of the child's
+// quadrant writes its 4 child cells (value + 0: the child interior is zeroed
+// first, so -0 becomes +0 as in the reference)
+template <int METHOD>
+__global__ void __launch_bounds__(NT)
+    k2_prolong_new(double *__restrict__ v, const afh_box_meta *__restrict__ meta,
+                   const int32_t *__restrict__ ids, int nc, int bsz, int lim) {
+  const int hn = nc >> 1;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= hn * hn) return;
+  const int id = ids[blockIdx.y];
+  const afh_box_meta &m = meta[id - 1];
+  const int i = t % hn + 1, j = t / hn + 1, ng = nc + 2;
+  const int ic = i + ((m.ix[0] - 1) & 1) * hn, jc = j + ((m.ix[1] - 1) & 1) * hn;
+  const double *p = v + (size_t)(m.parent - 1) * bsz;
+  double *c = v + (size_t)(id - 1) * bsz;
+  const int fi = 2 * i - 1, fj = 2 * j - 1;
+  auto P = [&](int a, int b) { return p[ix2(ng, ic + a, jc + b)]; };
+  if (METHOD == AFH_PROLONG_LIMIT) {
+    const double f0 = P(0, 0);
+    const double f1 = 0.25 * limiter(lim, P(0, 0) - P(-1, 0), P(1, 0) - P(0, 0));
+    const double f2 = 0.25 * limiter(lim, P(0, 0) - P(0, -1), P(0, 1) - P(0, 0));
+    c[ix2(ng, fi, fj)] = f0 - f1 - f2 + 0.0;
+    c[ix2(ng, fi + 1, fj)] = f0 + f1 - f2 + 0.0;
+    c[ix2(ng, fi, fj + 1)] = f0 - f1 + f2 + 0.0;
+    c[ix2(ng, fi + 1, fj + 1)] = f0 + f1 + f2 + 0.0;
+  } else {
+    const double f1 = 1 / 16.0, f3 = 3 / 16.0, f9 = 9 / 16.0;
+    const double f0 = f9 * P(0, 0);
+    const double flx = f3 * P(-1, 0), fhx = f3 * P(1, 0);
+    const double fly = f3 * P(0, -1), fhy = f3 * P(0, 1);
+    const double fll = f1 * P(-1, -1), fhl = f1 * P(1, -1);
+    const double flh = f1 * P(-1, 1), fhh = f1 * P(1, 1);
+    c[ix2(ng, fi, fj)] = f0 + flx + fly + fll + 0.0;
+    c[ix2(ng, fi + 1, fj)] = f0 + fhx + fly + fhl + 0.0;
+    c[ix2(ng, fi, fj + 1)] = f0 + flx + fhy + flh + 0.0;
+    c[ix2(ng, fi + 1, fj + 1)] = f0 + fhx + fhy + fhh + 0.0;
+  }
+}
+
+// boxes ids[blockIdx.y] of variable blockIdx.z from one pool to another (the
+// pools of a regrid hold different box counts: different variable strides)
+__global__ void __launch_bounds__(NT)
+    k2_copy_boxes(const double *__restrict__ src, double *__restrict__ dst,
+                  const int32_t *__restrict__ ids, int per_box, size_t src_var,
+                  size_t dst_var) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= per_box) return;
+  const size_t b = (size_t)(ids[blockIdx.y] - 1) * per_box + t;
+  dst[blockIdx.z * dst_var + b] = src[blockIdx.z * src_var + b];
+}
+
+// NORM2 as the Fortran runtime the reference is built with evaluates it
+// (afh.electrode.norm2): the largest |x| so far m, s = sum (x / m)^2 without
+// m's own term, element by element; m sqrt(s + 1)
+__device__ __forceinline__ double norm2_rt(const double *x, int n) {
+  double m = 0.0, s = 0.0;
+  for (int q = 0; q < n; q++) {
+    const double a = fabs(x[q]);
+    if (m == 0.0) {
+      m = a;
+    } else if (a > m) {
+      double u = m / a;
+      u = u * u;
+      s = s * u + u;
+      m = a;
+    } else {
+      const double u = a / m;
+      s = s + u * u;
+    }
+  }
+  return m * sqrt(s + 1.0);
+}
+
+// GM_dist_line (src/m_geometry.f90:21-51), n_dim = 2
+__device__ __forceinline__ double dist_line2(const double r[2], const double *r0,
+                                             const double *r1) {
+  const double d0 = r1[0] - r0[0], d1 = r1[1] - r0[1];
+  const double len2 = d0 * d0 + d1 * d1;
+  const double frac = (r[0] - r0[0]) * d0 + (r[1] - r0[1]) * d1;
+  double dv[2];
+  if (frac <= 0.0) {
+    dv[0] = r[0] - r0[0], dv[1] = r[1] - r0[1];
+  } else if (frac >= len2) {
+    dv[0] = r[0] - r1[0], dv[1] = r[1] - r1[1];
+  } else {
+    dv[0] = r[0] - (r0[0] + frac / len2 * d0);
+    dv[1] = r[1] - (r0[1] + frac / len2 * d1);
+  }
+  return norm2_rt(dv, 2);
+}
+
+struct RefineArgs2 {
+  afh_refine_desc d;
+  DevLT td;
+  double N;
+  const double *ne, *E;
+};
+
+// default_refinement (src/m_refine.f90:198-298), NDIM = 2, per cell, reduced
+// per box as cell_to_ref_flags does (m_af_core.f90:1095-1148): flag = do if
+// any cell asks for refinement, else keep if any keeps, else remove; mask bit
+// (dj+1)*3 + (di+1) when a cell within buffer_width of the side towards the
+// neighbour (di, dj) asks for refinement. One workgroup per box.
+__global__ void __launch_bounds__(NT)
+    k2_refine_flags(RefineArgs2 A, const afh_box_meta *__restrict__ meta,
+                    const int32_t *__restrict__ ids, int nc, int bsz,
+                    int32_t *__restrict__ flags, uint32_t *__restrict__ masks) {
+  const afh_refine_desc &p = A.d;
+  const int id = ids[blockIdx.x];
+  const afh_box_meta &b = meta[id - 1];
+  __shared__ int s_do, s_keep;
+  __shared__ unsigned s_mask;
+  if (threadIdx.x == 0) s_do = 0, s_keep = 0, s_mask = 0;
+  __syncthreads();
+  const double min_dx = b.dr[0] < b.dr[1] ? b.dr[0] : b.dr[1];
+  const double max_dx = b.dr[0] > b.dr[1] ? b.dr[0] : b.dr[1];
+  const int bw = p.buffer_width;
+  double rmin[2], rmax[2];
+  for (int d = 0; d < 2; d++) rmin[d] = b.r_min[d], rmax[d] = b.r_min[d] + b.dr[d] * nc;
+  int any_do = 0, any_keep = 0;
+  unsigned msk = 0;
+  for (int t = threadIdx.x; t < nc * nc; t += blockDim.x) {
+    const int i = t % nc + 1, j = t / nc + 1;
+    const size_t x = (size_t)(id - 1) * bsz + ix2(nc + 2, i, j);
+    const double gas_dens = A.N;
+    const double fld = A.E[x] * 1e21 / gas_dens;
+    double alpha;
+    if (p.use_alpha_effective) {
+      alpha = (lt_col(A.td, p.td_alpha_col, p.adx_fac * fld) -
+               lt_col(A.td, p.td_eta_col, p.adx_fac * fld)) *
+              gas_dens / p.adx_fac;
+      alpha = alpha > 0.0 ? alpha : 0.0;
+    } else {
+      alpha = lt_col(A.td, p.td_alpha_col, p.adx_fac * fld) * gas_dens / p.adx_fac;
+    }
+    const double adx = max_dx * alpha, ne = A.ne[x];
+    int f;
+    if (adx > p.adx && ne > p.min_dens) f = AFH_DO_REF;
+    else if (adx < 0.125 * p.adx && max_dx < p.derefine_dx) f = AFH_RM_REF;
+    else f = AFH_KEEP_REF;
+    // af_r_cc: r_min + (i - 0.5) dr
+    const double r[2] = {b.r_min[0] + (i - 0.5) * b.dr[0], b.r_min[1] + (j - 0.5) * b.dr[1]};
+    for (int n = 0; n < p.n_seeds; n++) {
+      const double dist = dist_line2(r, p.seed_r0[n], p.seed_r1[n]);
+      if (dist - p.seed_width[n] < 2 * max_dx && max_dx > p.init_fac * p.seed_width[n])
+        f = AFH_DO_REF;
+    }
+    for (int n = 0; n < p.n_regions; n++) {
+      bool in = max_dx > p.region_dr[n];
+      for (int d = 0; d < 2; d++)
+        in = in && rmax[d] >= p.region_rmin[n][d] && rmin[d] <= p.region_rmax[n][d];
+      if (in && i == nc / 2 && j == nc / 2) f = AFH_DO_REF;
+    }
+    for (int n = 0; n < p.n_limits; n++) {
+      bool in = max_dx < 2 * p.limit_dr[n];
+      for (int d = 0; d < 2; d++)
+        in = in && rmin[d] >= p.limit_rmin[n][d] && rmax[d] <= p.limit_rmax[n][d];
+      if (in && f == AFH_DO_REF) f = AFH_KEEP_REF;
+    }
+    if (max_dx > p.max_dx) f = AFH_DO_REF;
+    else if (min_dx < 2 * p.min_dx && f == AFH_DO_REF) f = AFH_KEEP_REF;
+    if (f == AFH_DO_REF) {
+      any_do = 1;
+      if (bw > 0) {
+        const bool lo[2] = {i <= bw, j <= bw}, hi[2] = {i > nc - bw, j > nc - bw};
+        for (int dj = -1; dj <= 1; dj++)
+          for (int di = -1; di <= 1; di++) {
+            if (!di && !dj) continue;
+            const int dd[2] = {di, dj};
+            bool in = true;
+            for (int d = 0; d < 2; d++) in = in && (dd[d] == 0 || (dd[d] < 0 ? lo[d] : hi[d]));
+            if (in) msk |= 1u << ((dj + 1) * 3 + (di + 1));
+          }
+      }
+    } else if (f == AFH_KEEP_REF) {
+      any_keep = 1;
+    }
+  }
+  if (any_do) atomicOr(&s_do, 1);
+  if (any_keep) atomicOr(&s_keep, 1);
+  if (msk) atomicOr(&s_mask, msk);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    flags[id - 1] = s_do ? AFH_DO_REF : s_keep ? AFH_KEEP_REF : AFH_RM_REF;
+    masks[id - 1] = s_mask;
+  }
+}
+
+// gfortran's real ** integer (_gfortran_pow_r8_i4): binary powering
+__device__ __forceinline__ double ipow2(double x, int n) {
+  double p = 1.0;
+  for (;;) {
+    if (n & 1) p *= x;
+    n >>= 1;
+    if (!n) break;
+    x *= x;
+  }
+  return p;
+}
+
+// Per leaf box (one thread each; 2-D boxes are small): OP 0 the sum of
+// cc(1:nc, 1:nc)**power in the Fortran element order (j outer, i inner);
+// AFH_RED_MAX / MIN / MAXABS the extremum and its first cell (i fastest)
+template <int OP>
+__global__ void __launch_bounds__(NT)
+    k2_box_reduce(const double *__restrict__ v, const int32_t *__restrict__ ids, int nl,
+                  int nc, int bsz, int power, double *__restrict__ out) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= nl) return;
+  const double *c = v + (size_t)(ids[q] - 1) * bsz;
+  const int ng = nc + 2;
+  double best = OP == 0 ? 0.0 : (OP == AFH_RED_MIN ? HUGE_VAL : -HUGE_VAL);
+  int bix = -1;
+  for (int j = 1; j <= nc; j++)
+    for (int i = 1; i <= nc; i++) {
+      double x = c[ix2(ng, i, j)];
+      if (OP == 0) {
+        best = best + ipow2(x, power);
+      } else {
+        if (OP == AFH_RED_MAXABS) x = fabs(x);
+        if (bix < 0 || (OP == AFH_RED_MIN ? x < best : x > best))
+          best = x, bix = (j - 1) * nc + (i - 1);
+      }
+    }
+  out[2 * q] = best;
+  out[2 * q + 1] = (double)bix;
+}
+
+static int32_t device_list(const std::vector<int32_t> &h, int32_t **d) {
+  H2(hipMalloc(d, sizeof(int32_t) * std::max<size_t>(1, h.size())));
+  if (!h.empty())
+    H2(hipMemcpy(*d, h.data(), sizeof(int32_t) * h.size(), hipMemcpyHostToDevice));
+  return AFH_OK;
+}
+
+static int32_t box_reduce(afh_tree *t, int iv, int op, int power, std::vector<double> &res) {
+  const int nl = t->leaves.off[t->nlvl];
+  res.assign(2 * (size_t)nl, 0.0);
+  if (!nl) return AFH_OK;
+  if (!t->d_boxred) H2(hipMalloc(&t->d_boxred, sizeof(double) * 2 * t->nb));
+  const dim3 grid((nl + NT - 1) / NT), blk(NT);
+  const double *v = t->ccv(iv);
+  switch (op) {
+  case 0:
+    hipLaunchKernelGGL(k2_box_reduce<0>, grid, blk, 0, t->stream, v, t->leaves.d, nl, t->nc,
+                       t->bsz, power, t->d_boxred);
+    break;
+  case AFH_RED_MAX:
+    hipLaunchKernelGGL(k2_box_reduce<AFH_RED_MAX>, grid, blk, 0, t->stream, v, t->leaves.d, nl,
+                       t->nc, t->bsz, power, t->d_boxred);
+    break;
+  case AFH_RED_MIN:
+    hipLaunchKernelGGL(k2_box_reduce<AFH_RED_MIN>, grid, blk, 0, t->stream, v, t->leaves.d, nl,
+                       t->nc, t->bsz, power, t->d_boxred);
+    break;
+  default:
+    hipLaunchKernelGGL(k2_box_reduce<AFH_RED_MAXABS>, grid, blk, 0, t->stream, v, t->leaves.d,
+                       nl, t->nc, t->bsz, power, t->d_boxred);
+  }
+  H2_LAUNCH("k2_box_reduce");
+  H2(hipMemcpyAsync(res.data(), t->d_boxred, sizeof(double) * 2 * nl, hipMemcpyDeviceToHost,
+                    t->stream));
+  H2(hipStreamSynchronize(t->stream));
+  return AFH_OK;
+}
+
+}  // namespace afh2
+
+extern "C" {
+
+int32_t afh_set_cc_prolong(afh_tree *t, int32_t iv, int32_t method, int32_t limiter) {
+  if (int32_t e = check_iv(t, iv, "afh_set_cc_prolong")) return e;
+  if (method < AFH_PROLONG_NONE || method > AFH_PROLONG_LIMIT)
+    return set_error(AFH_ERR_UNSUPPORTED, "prolongation method %d", method);
+  if (!t->meth[iv].set) return set_error(AFH_ERR_STATE, "set cc methods first");
+  if (method != AFH_PROLONG_NONE &&
+      std::find(t->auto_vars.begin(), t->auto_vars.end(), iv) == t->auto_vars.end())
+    t->auto_vars.push_back(iv);
+  t->meth[iv].prolong = method;
+  t->meth[iv].prolong_lim = limiter;
+  return AFH_OK;
+}
+
+// af_adjust_refinement's data movement (m_af_core.f90:697-881) onto the new
+// topology: auto_restrict into boxes whose children go, the data of the
+// boxes that persist (same id, level and index), then auto_prolong level by
+// level (every automatic variable of the new boxes from their parents, then
+// their ghost cells, corners included). The old tree stays valid.
+int32_t afh_tree_regrid(afh_tree *o, const afh_tree_desc *d, afh_tree **out) {
+  if (!o || !d || !out) return set_error(AFH_ERR_ARG, "afh_tree_regrid: null");
+  if (d->n_cell != o->nc || d->n_var_cell != o->nvc || d->n_var_face != o->nvf)
+    return set_error(AFH_ERR_ARG, "afh_tree_regrid: box size / variables differ");
+  std::vector<char> in_old(o->nb + 1, 0), keep(d->n_boxes + 1, 0);
+  for (const auto &L : o->h_ids)
+    for (int32_t id : L) in_old[id] = 1;
+  std::vector<int32_t> kept, rchild;
+  for (int q = 0; q < d->lvl_ids_off[d->highest_lvl]; q++) {
+    const int32_t id = d->lvl_ids[q];
+    if (id < 1 || id > d->n_boxes) return set_error(AFH_ERR_ARG, "bad box id %d", id);
+    if (id > o->nb || !in_old[id]) continue;
+    const afh_box_meta &a = o->boxes[id - 1], &b = d->boxes[id - 1];
+    if (a.lvl != b.lvl || a.ix[0] != b.ix[0] || a.ix[1] != b.ix[1]) continue;
+    keep[id] = 1;
+    kept.push_back(id);
+    // auto_restrict (m_af_core.f90:826-840): the box lost its children
+    if (a.children[0] > 0 && b.children[0] == 0)
+      for (int c = 0; c < 4; c++) rchild.push_back(a.children[c]);
+  }
+  int32_t *d_list = nullptr;
+  int32_t e;
+  const int nc = o->nc;
+  if (!rchild.empty()) {
+    if ((e = device_list(rchild, &d_list))) return e;
+    for (int iv : o->auto_vars) {
+      hipLaunchKernelGGL(k2_restrict, grid2(nc * nc / 4, (int)rchild.size()), dim3(NT), 0,
+                         o->stream, o->ccv(iv), o->d_boxes, d_list, nc, o->bsz);
+      H2_LAUNCH("k2_restrict");
+    }
+    H2(hipStreamSynchronize(o->stream));
+    hipFree(d_list);
+    d_list = nullptr;
+  }
+  afh_tree *t = nullptr;
+  if ((e = afh_tree_create(d, o->device, &t))) return e;
+  t->meth = o->meth;
+  t->auto_vars = o->auto_vars;
+  if (!kept.empty()) {
+    if ((e = device_list(kept, &d_list))) return e;
+    const unsigned n = (unsigned)kept.size();
+    hipLaunchKernelGGL(k2_copy_boxes, dim3((unsigned)((t->bsz + NT - 1) / NT), n, t->nvc),
+                       dim3(NT), 0, t->stream, o->cc, t->cc, d_list, t->bsz,
+                       (size_t)o->nb * o->bsz, (size_t)t->nb * t->bsz);
+    H2_LAUNCH("k2_copy_boxes");
+    if (t->nvf > 0) {
+      hipLaunchKernelGGL(k2_copy_boxes, dim3((unsigned)((t->fsz + NT - 1) / NT), n, t->nvf),
+                         dim3(NT), 0, t->stream, o->fc, t->fc, d_list, t->fsz,
+                         (size_t)o->nb * o->fsz, (size_t)t->nb * t->fsz);
+      H2_LAUNCH("k2_copy_boxes");
+    }
+    H2(hipStreamSynchronize(t->stream));
+    hipFree(d_list);
+    d_list = nullptr;
+  }
+  const int hn = nc / 2;
+  for (int l = 2; l <= t->nlvl; l++) {
+    std::vector<int32_t> add;
+    for (int32_t id : t->h_ids[l - 1])
+      if (!keep[id]) add.push_back(id);
+    if (add.empty()) continue;
+    if ((e = device_list(add, &d_list))) return e;
+    const int n = (int)add.size();
+    for (int iv : t->auto_vars) {
+      const Meth &m = t->meth[iv];
+      auto kern = m.prolong == AFH_PROLONG_LIMIT ? k2_prolong_new<AFH_PROLONG_LIMIT>
+                                                 : k2_prolong_new<AFH_PROLONG_LINEAR>;
+      hipLaunchKernelGGL(kern, grid2(hn * hn, n), dim3(NT), 0, t->stream, t->ccv(iv),
+                         t->d_boxes, d_list, nc, t->bsz, m.prolong_lim);
+      H2_LAUNCH("k2_prolong_new");
+    }
+    // af_gc_box of every new box (sides, then corners) once all are prolonged
+    for (int iv : t->auto_vars) {
+      hipLaunchKernelGGL(k2_gc, grid2(4 * nc, n), dim3(NT), 0, t->stream, t->ccv(iv),
+                         t->d_boxes, d_list, nc, t->bsz, t->bc4(iv));
+      H2_LAUNCH("k2_gc");
+      hipLaunchKernelGGL(k2_corners, dim3((4 * n + NT - 1) / NT), dim3(NT), 0, t->stream,
+                         t->ccv(iv), t->d_boxes, d_list, n, nc, t->bsz);
+      H2_LAUNCH("k2_corners");
+    }
+    H2(hipStreamSynchronize(t->stream));
+    hipFree(d_list);
+    d_list = nullptr;
+  }
+  *out = t;
+  return AFH_OK;
+}
+
+int32_t afh_refine_flags(afh_fluid *f, const afh_refine_desc *d, const uint8_t *electrode_box,
+                         int32_t *flags, uint32_t *masks) {
+  if (!f || !d || !flags || !masks) return set_error(AFH_ERR_ARG, "afh_refine_flags: null");
+  afh_tree *t = f->t;
+  if (electrode_box) return set_error(AFH_ERR_UNSUPPORTED, "2-D: electrodes");
+  if (d->n_seeds > AFH_MAX_REFINE_REGIONS || d->n_regions > AFH_MAX_REFINE_REGIONS ||
+      d->n_limits > AFH_MAX_REFINE_REGIONS || d->buffer_width < 0 ||
+      d->buffer_width > t->nc || d->i_electron < 1 || d->i_electron > t->nvc ||
+      d->i_efld < 1 || d->i_efld > t->nvc || d->td_alpha_col < 1 ||
+      d->td_alpha_col > f->d.td.n_cols || d->td_eta_col < 1 || d->td_eta_col > f->d.td.n_cols)
+    return set_error(AFH_ERR_ARG, "afh_refine_flags: bad descriptor");
+  const int nb = t->nb, nids = t->ids.off[t->nlvl];
+  int32_t *d_flags = nullptr;
+  uint32_t *d_masks = nullptr;
+  H2(hipMalloc(&d_flags, sizeof(int32_t) * nb));
+  H2(hipMalloc(&d_masks, sizeof(uint32_t) * nb));
+  H2(hipMemsetAsync(d_flags, 0, sizeof(int32_t) * nb, t->stream));
+  H2(hipMemsetAsync(d_masks, 0, sizeof(uint32_t) * nb, t->stream));
+  RefineArgs2 A;
+  A.d = *d;
+  A.td = dev_lt(f->d.td, f->d_td);
+  A.N = f->d.gas_number_density;
+  A.ne = t->ccv(d->i_electron);
+  A.E = t->ccv(d->i_efld);
+  if (nids > 0) {
+    hipLaunchKernelGGL(k2_refine_flags, dim3(nids), dim3(NT), 0, t->stream, A, t->d_boxes,
+                       t->ids.d, t->nc, t->bsz, d_flags, d_masks);
+    H2_LAUNCH("k2_refine_flags");
+  }
+  H2(hipMemcpyAsync(flags, d_flags, sizeof(int32_t) * nb, hipMemcpyDeviceToHost, t->stream));
+  H2(hipMemcpyAsync(masks, d_masks, sizeof(uint32_t) * nb, hipMemcpyDeviceToHost, t->stream));
+  H2(hipStreamSynchronize(t->stream));
+  hipFree(d_flags), hipFree(d_masks);
+  return AFH_OK;
+}
+
+// af_tree_sum_cc (m_af_utils.f90:966-1026), Cartesian: per leaf the sum of
+// cc**power, then my_sum = my_sum + fac * tmp in the reference's loop order
+// (levels, then leaves), fac = product(af_lvl_dr)
+int32_t afh_tree_sum_cc(afh_tree *t, int32_t iv, int32_t power, double *out) {
+  if (int32_t e = check_iv(t, iv, "afh_tree_sum_cc")) return e;
+  if (power < 1 || !out) return set_error(AFH_ERR_ARG, "afh_tree_sum_cc: bad argument");
+  std::vector<double> res;
+  if (int32_t e = box_reduce(t, iv, 0, power, res)) return e;
+  double sum = 0.0;
+  size_t q = 0;
+  for (int l = 1; l <= t->nlvl; l++) {
+    const double fac = t->lvl_dr[2 * (l - 1)] * t->lvl_dr[2 * (l - 1) + 1];
+    for (int b = 0; b < t->leaves.n(l); b++, q++) sum = sum + fac * res[2 * q];
+  }
+  *out = sum;
+  return AFH_OK;
+}
+
+// af_tree_max_cc / min_cc / maxabs_cc with af_reduction_loc (m_af_utils.f90:
+// 694-874): loc = (box id, i, j, 0), the first cell of the first box in loop
+// order holding the extremum
+int32_t afh_tree_reduce_loc(afh_tree *t, int32_t iv, int32_t op, double *out, int32_t *loc) {
+  if (int32_t e = check_iv(t, iv, "afh_tree_reduce_loc")) return e;
+  if (!out || op < AFH_RED_MAX || op > AFH_RED_MAXABS)
+    return set_error(AFH_ERR_ARG, "afh_tree_reduce_loc: bad argument");
+  std::vector<double> res;
+  if (int32_t e = box_reduce(t, iv, op, 1, res)) return e;
+  const bool is_min = op == AFH_RED_MIN;
+  double val = (is_min ? 1 : -1) * (1.7976931348623157e308 / 10);
+  int32_t lid = -1, lix = -1;
+  size_t q = 0;
+  for (int l = 1; l <= t->nlvl; l++)
+    for (int b = 0; b < t->leaves.n(l); b++, q++) {
+      const double tmp = res[2 * q];
+      const double nv = is_min ? std::min(tmp, val) : std::max(tmp, val);
+      if (std::fabs(nv - val) > 0) {
+        val = tmp;
+        lid = t->h_leaves[l - 1][b];
+        lix = (int32_t)res[2 * q + 1];
+      }
+    }
+  *out = val;
+  if (loc) {
+    const int nc = t->nc;
+    loc[0] = lid;
+    loc[1] = lix < 0 ? -1 : lix % nc + 1;
+    loc[2] = lix < 0 ? -1 : lix / nc + 1;
+    loc[3] = 0;
+  }
+  return AFH_OK;
 }
 
 }  // extern "C"

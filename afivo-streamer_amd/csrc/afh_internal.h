@@ -24,6 +24,11 @@ namespace afh {
 
 int32_t set_error(int32_t code, const char *fmt, ...);
 int32_t check_hip(hipError_t e, const char *what);
+// Data pools (cc, fc, gc2, the spare image): hipMalloc, or with
+// AFH_POOL_CONTIG=1 hipExtMallocWithFlags(hipDeviceMallocContiguous) (falls
+// back to hipMalloc if the runtime refuses); AFH_LOG_POOLS=1 prints each
+// pool's address and its offsets modulo 4 KiB / 64 KiB / 2 MiB to stderr.
+int32_t pool_alloc(void **p, size_t bytes, const char *what);
 #define AFH_HIP(call)                                                         \
   do {                                                                        \
     hipError_t _e = (call);                                                   \

@@ -2316,6 +2316,7 @@ struct afh_mg {
   bool rstr_col = true;       // AFH_RSTR_COL=0: one coarse cell per thread (k_rstr_fas)
   int rstr_k = AFH_RSTR_K;     // coarse cells per column (AFH_RSTR_K=2|4|8 at run time)
   int res_k = AFH_RES_K;       // residual cells per column (AFH_RES_K=2|4|8 at run time)
+  int prolong_k = 4;           // prolongation cells per column (AFH_PROLONG_K=2|4|8)
   int rstr_bs = 256;           // k_rstr_fas_col workgroup size (AFH_RSTR_BS=128|256)
   bool pair_ntl = false;       // AFH_GSRB_PAIR_NTL: non-temporal plane loads in the 64^3 pair
   int pair_ks = 4;           // AFH_GSRB_PAIR_KS: k chunks on 64..255-box levels (NC = 64;
@@ -2550,6 +2551,8 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
   if (const char *env = getenv("AFH_RSTR_BS")) mg->rstr_bs = atoi(env) == 128 ? 128 : 256;
   if (const char *env = getenv("AFH_RES_K"))
     mg->res_k = atoi(env) == 8 ? 8 : atoi(env) == 2 ? 2 : 4;
+  if (const char *env = getenv("AFH_PROLONG_K"))
+    mg->prolong_k = atoi(env) == 8 ? 8 : atoi(env) == 2 ? 2 : 4;
   if (const char *env = getenv("AFH_CS_FUSED")) mg->cs_fused = atoi(env) != 0;
   if (const char *env = getenv("AFH_CS_DIRECT_SMALL")) mg->cs_direct_small = atoi(env) != 0;
   if (const char *env = getenv("AFH_CS_DS_CELLS"))
@@ -2567,7 +2570,9 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
     if (any) {
       // one spare image per tree: the level fills after a pair fill t->alt
       if (!t->alt) {
-        AFH_HIP(hipMalloc(&t->alt, (size_t)t->nb * t->bsz * sizeof(double)));
+        if (int32_t e2 = pool_alloc((void **)&t->alt, (size_t)t->nb * t->bsz * sizeof(double),
+                                    "alt"))
+          return e2;
         AFH_HIP(hipMemsetAsync(t->alt, 0, (size_t)t->nb * t->bsz * sizeof(double),
                                t->stream));
       }
@@ -2989,9 +2994,8 @@ static int32_t correct_children(afh_mg *mg, int lvl) {
     // column length 4; AFH_PROLONG_K=8 where nc allows: the launch is
     // faster (195 against 223 us on S1-64) but the pair after it slower,
     // 13.32 against 12.57-12.60 ms per step (profiles/r03_ab_prolong_k.txt)
-    static const int env_k = getenv("AFH_PROLONG_K") ? atoi(getenv("AFH_PROLONG_K")) : 0;
-    const int want = env_k ? env_k : 4;
-    const int K = want == 8 && nc % 8 == 0 ? 8 : nc % 4 == 0 ? 4 : 2;
+    const int want = mg->prolong_k;
+    const int K = want == 8 && nc % 8 == 0 ? 8 : want >= 4 && nc % 4 == 0 ? 4 : 2;
     const dim3 grid((nc * nc * (nc / K) + 255) / 256, nid);
     if (K == 8)
       hipLaunchKernelGGL(k_prolong<8>, grid, dim3(256), 0, t->stream,

@@ -34,6 +34,29 @@ int32_t check_hip(hipError_t e, const char *what) {
   return set_error(AFH_ERR_DEVICE, "%s: %s", what, hipGetErrorString(e));
 }
 
+int32_t pool_alloc(void **p, size_t bytes, const char *what) {
+  static const bool contig = getenv("AFH_POOL_CONTIG") && atoi(getenv("AFH_POOL_CONTIG"));
+  static const bool log = getenv("AFH_LOG_POOLS") && atoi(getenv("AFH_LOG_POOLS"));
+  bool got_contig = false;
+  *p = nullptr;
+  if (contig) {
+    if (hipExtMallocWithFlags(p, bytes, hipDeviceMallocContiguous) == hipSuccess) {
+      got_contig = true;
+    } else {
+      (void)hipGetLastError();
+      *p = nullptr;
+    }
+  }
+  if (!*p) AFH_HIP(hipMalloc(p, bytes));
+  if (log) {
+    const uintptr_t a = (uintptr_t)*p;
+    fprintf(stderr, "afh_pool %s %p bytes %zu mod4K %zu mod64K %zu mod2M %zu contig %d\n",
+            what, *p, bytes, (size_t)(a & 4095), (size_t)(a & 65535),
+            (size_t)(a & ((1u << 21) - 1)), (int)got_contig);
+  }
+  return AFH_OK;
+}
+
 static hipEvent_t next_event(afh_tree *t) {
   if (t->ev_used == t->ev_pool.size()) {
     hipEvent_t e;
@@ -939,11 +962,13 @@ static int32_t tree_create_impl(const afh_tree_desc *d, int32_t device,
   } else {
     size_t ncc = (size_t)t->nvc * t->cap * t->bsz;
     size_t nfc = (size_t)std::max(1, t->nvf) * t->cap * t->fsz;
-    AFH_HIP(hipMalloc(&t->cc, ncc * sizeof(double)));
-    AFH_HIP(hipMalloc(&t->fc, nfc * sizeof(double)));
+    if (int32_t e2 = pool_alloc((void **)&t->cc, ncc * sizeof(double), "cc")) return e2;
+    if (int32_t e2 = pool_alloc((void **)&t->fc, nfc * sizeof(double), "fc")) return e2;
     AFH_HIP(hipMemsetAsync(t->cc, 0, ncc * sizeof(double), t->stream));
     AFH_HIP(hipMemsetAsync(t->fc, 0, nfc * sizeof(double), t->stream));
-    AFH_HIP(hipMalloc(&t->gc2, sizeof(double) * (size_t)t->cap * 6 * t->nc * t->nc));
+    if (int32_t e2 = pool_alloc((void **)&t->gc2,
+                                sizeof(double) * (size_t)t->cap * 6 * t->nc * t->nc, "gc2"))
+      return e2;
   }
   AFH_HIP(hipMalloc(&t->scratch, (size_t)(RED_SLOTS + 1) * RED_SHARDS * sizeof(double)));
   AFH_HIP(hipHostMalloc(&t->h_scratch, RED_SLOTS * sizeof(double)));

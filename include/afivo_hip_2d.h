@@ -29,7 +29,11 @@
  * flux_update_densities with the field-dependent rate forms). Not built in
  * 2-D (AFH_ERR_UNSUPPORTED or not exported): cylindrical coordinates
  * (af_cyl), electrodes / level sets, variable gas density, photoionization,
- * the temperature rate forms, regrid, sharding, deferred reductions.
+ * the temperature rate forms, sharding, deferred reductions. Built in round 4
+ * for the 2-D time loop (afh.driver over this library, programs/standard_2d/
+ * tests/test_2d_rtest.log): the device regrid with the prolongation of the
+ * automatic variables, default_refinement's flags, and the regression-log
+ * sums and extrema.
  */
 #ifndef AFIVO_HIP_2D_H
 #define AFIVO_HIP_2D_H
@@ -71,6 +75,20 @@ int32_t afh_flux_upwind_tree(afh_fluid *f, int32_t s_deriv, double *dt_lim);
 int32_t afh_flux_update_densities(afh_fluid *f, double dt, int32_t s_deriv, int32_t n_prev,
                                   const int32_t *s_prev, const double *w_prev,
                                   int32_t s_out, int32_t last_step, double *dt_lim);
+/* the device regrid (af_adjust_refinement's data movement, round 4): the
+ * persisting boxes are copied into the new tree's pools (box_capacity is not
+ * used in 2-D) */
+int32_t afh_set_cc_prolong(afh_tree *t, int32_t iv, int32_t method, int32_t limiter);
+int32_t afh_tree_regrid(afh_tree *old, const afh_tree_desc *desc, afh_tree **out);
+/* default_refinement reduced per box; masks use the 2-D bit (dj+1)*3 + (di+1);
+ * the seeds' / regions' first two coordinates; electrode_box must be NULL */
+int32_t afh_refine_flags(afh_fluid *f, const afh_refine_desc *d,
+                         const uint8_t *electrode_box, int32_t *flags,
+                         uint32_t *masks);
+/* the output_regression_log reductions; loc = (id, i, j, 0) */
+int32_t afh_tree_sum_cc(afh_tree *t, int32_t iv, int32_t power, double *out);
+int32_t afh_tree_reduce_loc(afh_tree *t, int32_t iv, int32_t op, double *out,
+                            int32_t *loc);
 /* store_flux is ignored: the 2-D species step always stores the face fluxes */
 int32_t afh_fluid_forward_euler(afh_fluid *f, double dt, int32_t s_deriv, int32_t n_prev,
                                 const int32_t *s_prev, const double *w_prev, int32_t s_out,

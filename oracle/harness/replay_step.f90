@@ -27,6 +27,9 @@
 !> then every cc variable of every box in use ((nc+2)^3, i fastest) and every
 !> fc variable ((nc+1)^3 x 3).
 !> Output: float64 dt_lim, then every cc variable of every box in use.
+!> NDIM = 2 (oracle/Makefile _ref/2d/replay_step): the same record with the
+!> 2-D box shapes ((nc+2)^2 per cc variable, (nc+1)^2 x 2 per fc variable);
+!> ix keeps three entries, the third unused.
 #include "cpp_macros.h"
 program replay_step
   use m_config
@@ -101,6 +104,7 @@ program replay_step
   if (nvc /= tree%n_var_cell .or. nvf /= tree%n_var_face) &
        error stop "record: variable registry differs"
   allocate(parent(hid), blvl(hid), bix(3, hid), in_use(hid))
+  ! (bix(1:NDIM, :) is the box index; a 2-D record leaves bix(3, :) at 0)
   do id = 1, hid
      read(ur) parent(id), blvl(id), bix(:, id), in_use(id)
   end do
@@ -119,7 +123,7 @@ program replay_step
      if (in_use(id) == 0) cycle
      do n = 1, tree%highest_id
         if (tree%boxes(n)%in_use .and. tree%boxes(n)%lvl == blvl(id)) then
-           if (all(tree%boxes(n)%ix == bix(:, id))) then
+           if (all(tree%boxes(n)%ix == bix(1:NDIM, id))) then
               rid(id) = n
               exit
            end if
@@ -135,12 +139,12 @@ program replay_step
   read(ur) s_prev, w_prev, s_out
   do iv = 1, nvc
      do id = 1, hid
-        if (in_use(id) /= 0) read(ur) tree%boxes(rid(id))%cc(:, :, :, iv)
+        if (in_use(id) /= 0) read(ur) tree%boxes(rid(id))%cc(DTIMES(:), iv)
      end do
   end do
   do iv = 1, nvf
      do id = 1, hid
-        if (in_use(id) /= 0) read(ur) tree%boxes(rid(id))%fc(:, :, :, :, iv)
+        if (in_use(id) /= 0) read(ur) tree%boxes(rid(id))%fc(DTIMES(:), :, iv)
      end do
   end do
   close(ur)
@@ -155,7 +159,7 @@ program replay_step
   write(uo) dt_lim
   do iv = 1, nvc
      do id = 1, hid
-        if (in_use(id) /= 0) write(uo) tree%boxes(rid(id))%cc(:, :, :, iv)
+        if (in_use(id) /= 0) write(uo) tree%boxes(rid(id))%cc(DTIMES(:), iv)
      end do
   end do
   close(uo)
@@ -180,7 +184,7 @@ contains
     has_child = .false.
     do c = 1, hid
        if (in_use(c) /= 0 .and. blvl(c) == box%lvl + 1) then
-          if (all((bix(:, c) + 1) / 2 == box%ix)) then
+          if (all((bix(1:NDIM, c) + 1) / 2 == box%ix)) then
              has_child = .true.
              exit
           end if

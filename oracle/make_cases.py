@@ -13,6 +13,11 @@ every species per output time; the expected output) into
 tests/golden/rtest_<name>.npz. Only numbers and names are stored.
 
     make -C oracle _ref/export_case && python3 oracle/make_cases.py [name ...]
+
+The 2-D cases (BASELINE config 1: programs/standard_2d) use the NDIM = 2
+build of the same harness (make -C oracle _ref/2d/export_case):
+tests/golden/rtest_test_2d.npz (tests/test_2d.cfg with its regression log)
+and tests/golden/case_s2d.npz (streamer_2d.cfg itself: air_chemistry_v1).
 """
 import os
 import subprocess
@@ -55,6 +60,11 @@ EXTRA = {"s3": ("/root/reference/programs/standard_3d", "streamer_3d.cfg",
          "ions": (TESTS, "test_3d_chem.cfg", ION_ARGS)}
 
 
+TESTS_2D = "/root/reference/programs/standard_2d/tests"
+CASES_2D = ["test_2d"]
+EXTRA_2D = {"s2d": ("/root/reference/programs/standard_2d", "streamer_2d.cfg", [])}
+
+
 def parse_dump(path):
     out = {}
     with open(path) as f:
@@ -78,18 +88,24 @@ def parse_dump(path):
 
 
 def main():
-    exe = os.path.join(HERE, "_ref", "export_case")
-    if not os.path.exists(exe):
-        sys.exit("build oracle/_ref/export_case first (make -C oracle _ref/export_case)")
     only = set(sys.argv[1:])
-    for name in CASES:
+    run(os.path.join(HERE, "_ref", "export_case"), TESTS, CASES, EXTRA, only)
+    run(os.path.join(HERE, "_ref", "2d", "export_case"), TESTS_2D, CASES_2D, EXTRA_2D, only)
+
+
+def run(exe, tests, cases, extra_cases, only):
+    if only and not (only & (set(cases) | set(extra_cases))):
+        return
+    if not os.path.exists(exe):
+        sys.exit("build %s first (make -C oracle %s)" % (exe, os.path.relpath(exe, HERE)))
+    for name in cases:
         if only and name not in only:
             continue
         dump = "/tmp/afh_export_%s.txt" % name
-        subprocess.run([exe, dump, name + ".cfg"], cwd=TESTS, check=True,
+        subprocess.run([exe, dump, name + ".cfg"], cwd=tests, check=True,
                        stdout=subprocess.DEVNULL)
         d = parse_dump(dump)
-        log = os.path.join(TESTS, name + "_rtest.log")
+        log = os.path.join(tests, name + "_rtest.log")
         with open(log) as f:
             header = f.readline().split()
         d["rtest_columns"] = np.array(header, dtype="U64")
@@ -98,7 +114,7 @@ def main():
         np.savez_compressed(out, **d)
         os.remove(dump)
         print("wrote", out, len(d), "arrays")
-    for name, (cwd, cfg, extra) in EXTRA.items():
+    for name, (cwd, cfg, extra) in extra_cases.items():
         if only and name not in only:
             continue
         dump = "/tmp/afh_export_%s.txt" % name

@@ -11,10 +11,11 @@ for rep in $(seq ${REPS:-2}); do
     envs=()
     [ "$v" = default ] || IFS=',' read -ra envs <<< "$v"
     env "${envs[@]}" timeout -k 10 400 python3 bench.py --config ${CFG:-s1-64} --steps ${STEPS:-10} \
-      --warmup 2 --no-cpu-baseline > gpurun_out/envsets/$tag.log 2>&1 || { tail -3 gpurun_out/envsets/$tag.log; exit 1; }
+      --warmup ${WARMUP:-2} --no-cpu-baseline > gpurun_out/envsets/$tag.log 2>&1 || { tail -3 gpurun_out/envsets/$tag.log; exit 1; }
     python3 -c "
 import json
 d = json.loads([l for l in open('gpurun_out/envsets/$tag.log') if l.startswith('{')][-1])
-print('%-52s %.3f ms/step  %.3f G  frac %.3f' % ('$tag', d['ms_per_step'], d['value'] / 1e9, d['roofline']['frac']), flush=True)"
+r = d['roofline'] or {}
+print('%-52s %.3f ms/step  %.3f G  frac %.3f  pair %.1f us' % ('$tag', d['ms_per_step'], d['value'] / 1e9, r.get('frac', 0), r.get('avg_launch_us', 0)), flush=True)"
   done
 done

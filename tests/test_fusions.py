@@ -79,9 +79,11 @@ def test_s1_residual_columns_bitwise(k, monkeypatch):
     _same(_s1(monkeypatch, {"AFH_RES_K": k}), _s1(monkeypatch, {"AFH_RES_K": "4"}))
 
 
-def test_s1_prolong_columns_bitwise(monkeypatch):
-    """k_prolong with columns of 8 cells (AFH_PROLONG_K=8) against 4."""
-    _same(_s1(monkeypatch, {"AFH_PROLONG_K": "8"}), _s1(monkeypatch, {"AFH_PROLONG_K": "4"}))
+@pytest.mark.parametrize("k", ["2", "8"])
+def test_s1_prolong_columns_bitwise(k, monkeypatch):
+    """k_prolong with columns of 2 and 8 cells (AFH_PROLONG_K, read when the
+    multigrid is created) against 4."""
+    _same(_s1(monkeypatch, {"AFH_PROLONG_K": k}), _s1(monkeypatch, {"AFH_PROLONG_K": "4"}))
 
 
 def test_direct_small_bitwise_8cubed(monkeypatch):
