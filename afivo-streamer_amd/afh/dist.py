@@ -1,25 +1,36 @@
 """Box sharding over ranks.
 
-Partition: a partition level Lp >= 2 is chosen (the coarsest level with at
-least one box per rank); the boxes of Lp are ordered by the Morton index of
-their position (``box%ix``) and cut into contiguous chunks of about equal
-leaf-cell weight; every descendant belongs to the rank of its Lp ancestor
-(parents and children stay together, so restriction and prolongation are
-rank-local), and the levels below Lp -- the coarse grid and its solver
-included -- are replicated: every rank computes them redundantly.
+Partition (round 4: a weighted Morton split of a partition frontier). The
+frontier starts as the boxes of level 2 (level 1 -- the coarse grid and its
+solver -- is replicated on every rank). Its boxes are ordered by the Morton
+index of their lower corner at the finest level's resolution (a Z-order
+walk over boxes of several levels, which cover disjoint blocks) and cut into
+contiguous chunks of about equal leaf weight (the leaf boxes of the subtree:
+the species step and the finest V-cycle work). While the heaviest rank
+carries more than (1 + TOL) of the mean, or the frontier has fewer boxes than
+ranks, the heaviest refined frontier box is replaced by its children and
+becomes replicated. Every descendant belongs to the rank of its frontier
+ancestor, so restriction and prolongation stay rank-local below the
+frontier; the replicated boxes above it (ancestors of frontier boxes, never
+leaves, except level-1 leaves) are computed by every rank. On a uniform tree
+the first frontier (level 2 or the first level with a box per rank) is
+already balanced, so the split is the round-3 one.
 
 Every rank allocates storage for the whole tree; the boxes of other ranks are
 replicas, refreshed by exchanges where the library's hooks say a replica is
 read after its owner wrote it (include/afivo_hip.h, AFH_HOOK_*):
 
 * HALO(l, iv): the cells of each remote neighbour (26 directions) within two
-  layers of an owned box, before a ghost-cell fill of level l;
+  layers of a box the rank computes (owned or replicated), before a
+  ghost-cell fill of level l;
 * RIMS(l, iv): the same regions extended over the neighbour's ghost layers,
   after the fill (read by the fused smoother's neighbour recomputation and
   by refinement-boundary interpolation);
-* RESTRICT(Lp, iv): the parent octants restricted from Lp into the
-  replicated level Lp-1 (all-gather);
-* MAX / MIN: all-reduce of reduction results.
+* RESTRICT(l, iv): the parent octants restricted from owned boxes of level l
+  into their replicated parents (all-gather);
+* CFLUX: the face fluxes af_consistent_fluxes copies from a refined box's
+  children into a coarse leaf neighbour on another rank;
+* MAX / MIN / SUM: all-reduce of reduction results.
 
 Transport: torch.distributed point-to-point (batch_isend_irecv) -- RCCL
 ("nccl") with device buffers on the GPU, gloo with host buffers in the CPU
@@ -36,13 +47,17 @@ from . import capi
 DIRS = [(dx, dy, dz) for dz in (-1, 0, 1) for dy in (-1, 0, 1) for dx in (-1, 0, 1)
         if (dx, dy, dz) != (0, 0, 0)]
 DEPTH = 2
+# the frontier is refined while the heaviest rank carries more than
+# (100 + TOL_PCT) % of the mean leaf weight (afh_dist_core.h TOL_PCT)
+TOL_PCT = 10
+MORTON_BITS = 21  # per dimension (int64 codes)
 
 
 def morton3(ix):
     """Interleaved-bit (Z-order) index of 0-based integer positions."""
     ix = np.asarray(ix, dtype=np.int64)
     code = np.zeros(len(ix), dtype=np.int64)
-    for b in range(20):
+    for b in range(MORTON_BITS):
         for d in range(3):
             code |= ((ix[:, d] >> b) & 1) << (3 * b + d)
     return code
@@ -81,29 +96,61 @@ class Partition:
         self.owner = np.full(self.nb, -1, np.int64)
         self.lp = None
         if n_ranks > 1:
-            lp = next((l for l in range(2, self.nlvl + 1) if len(ids[l]) >= n_ranks), None)
-            if lp is None:
-                raise ValueError("no level >= 2 has %d boxes to shard" % n_ranks)
-            self.lp = lp
-            # leaf-cell weight of every subtree
-            w = np.zeros(self.nb + 1, np.int64)
-            for l in range(self.nlvl, 0, -1):
-                for i in ids[l]:
-                    ch = self.children[i - 1]
-                    w[i] = 1 if ch[0] == 0 else w[ch].sum()
-            sel = ids[lp]
-            order = sel[np.argsort(morton3(self.ix[sel - 1] - 1), kind="stable")]
-            cum = np.cumsum(w[order])
-            target = cum[-1] / n_ranks
-            rk = np.minimum((np.ceil(cum / target) - 1).astype(np.int64), n_ranks - 1)
-            # every rank gets at least one box: fall back to an even split
-            if len(np.unique(rk)) < n_ranks:
-                rk = (np.arange(len(order)) * n_ranks) // len(order)
-            self.owner[order - 1] = rk
-            for l in range(lp + 1, self.nlvl + 1):
-                for i in ids[l]:
-                    self.owner[i - 1] = self.owner[self.parent[i - 1] - 1]
+            self._partition(ids, n_ranks)
         self.ids = ids
+
+    def _partition(self, ids, n):
+        """The weighted Morton split of the partition frontier (module
+        docstring); afh_dist_core.h partition() is the same algorithm."""
+        nlvl = self.nlvl
+        # leaf weight of every subtree
+        w = np.zeros(self.nb + 1, np.int64)
+        for l in range(nlvl, 0, -1):
+            for i in ids[l]:
+                ch = self.children[i - 1]
+                w[i] = 1 if ch[0] == 0 else w[ch].sum()
+        if nlvl < 2:
+            raise ValueError("no level >= 2 has enough boxes to shard over %d ranks" % n)
+        roots = [int(i) for i in ids[2]]
+
+        def code(b):  # Morton index of the lower corner at the finest resolution
+            sh = nlvl - int(self.lvl[b - 1])
+            return int(morton3((self.ix[b - 1][None] - 1) << sh)[0])
+
+        def split(rs):
+            order = sorted(rs, key=code)
+            ww = w[np.asarray(order, np.int64)]
+            cum = np.cumsum(ww)
+            target = cum[-1] / n
+            rk = np.minimum((np.ceil(cum / target) - 1).astype(np.int64), n - 1)
+            ok = len(np.unique(rk)) == n
+            loads = np.bincount(rk, weights=ww, minlength=n).astype(np.int64)
+            return order, rk, ok, int(loads.max()), int(cum[-1])
+
+        while True:
+            if len(roots) >= n:
+                order, rk, ok, mx, total = split(roots)
+                if ok and mx * n * 100 <= (100 + TOL_PCT) * total:
+                    break
+            cand = [r for r in roots if self.children[r - 1][0] > 0]
+            if not cand:
+                if len(roots) < n:
+                    raise ValueError("no level >= 2 has enough boxes to shard over %d ranks" % n)
+                break
+            h = max(cand, key=lambda r: (w[r], -r))  # heaviest, then lowest id
+            roots.remove(h)
+            roots += [int(c) for c in self.children[h - 1]]
+        order, rk, ok, _, _ = split(roots)
+        # every rank gets at least one frontier box: fall back to an even split
+        if not ok:
+            rk = (np.arange(len(order)) * n) // len(order)
+        self.owner[np.asarray(order, np.int64) - 1] = rk
+        for l in range(3, nlvl + 1):
+            for i in ids[l]:
+                p = self.parent[i - 1]
+                if self.owner[p - 1] >= 0:
+                    self.owner[i - 1] = self.owner[p - 1]
+        self.lp = min(int(self.lvl[r - 1]) for r in roots)
 
     def owned(self, rank, box_ids):
         o = self.owner[np.asarray(box_ids, np.int64) - 1]
@@ -136,7 +183,8 @@ class Partition:
             return []
         regs = set()
         for a in self.ids[level]:
-            if self.owner[a - 1] != recv_rank:
+            # the boxes recv_rank computes: its own and the replicated ones
+            if self.owner[a - 1] != recv_rank and self.owner[a - 1] >= 0:
                 continue
             for d in DIRS:
                 b = self.nmat[a - 1][(d[0] + 1) + 3 * (d[1] + 1) + 9 * (d[2] + 1)]
@@ -177,8 +225,9 @@ class Partition:
                     lo[d] = hi[d] = f
                     out.append((q, d, *lo, *hi))
         # a replicated refined box whose children are sharded: the face
-        # quarter each child covers on the replicated coarse neighbour goes
-        # from the child's owner to every other rank
+        # quarter each child covers on the coarse leaf neighbour goes from
+        # the child's owner to the neighbour's owner (every other rank when
+        # the neighbour is replicated)
         h = nc // 2
         nbs = np.asarray(self.topo["meta_neighbors"])
         for l in range(1, self.nlvl + 1):
@@ -187,7 +236,9 @@ class Partition:
                     continue
                 for nb in range(1, 7):
                     q = int(nbs[p - 1][nb - 1])
-                    if q <= 0 or self.children[q - 1][0] != 0 or self.owner[q - 1] >= 0:
+                    if q <= 0 or self.children[q - 1][0] != 0:
+                        continue
+                    if self.owner[q - 1] >= 0 and self.owner[q - 1] != recv_rank:
                         continue
                     d, side = (nb - 1) // 2, (nb - 1) % 2
                     f = nc + 1 if side == 0 else 1
@@ -202,17 +253,29 @@ class Partition:
                         out.append((q, d, *lo, *hi))
         return out
 
-    def octant_regions(self, send_rank):
-        """Parent octants written by send_rank's boxes of Lp (into the
-        replicated level Lp-1), in box order."""
+    def restrict_levels(self):
+        """Levels with an owned box whose parent is replicated (a RESTRICT
+        exchange after their restriction)."""
         if self.lp is None:
             return []
+        return [l for l in range(max(2, self.lp), self.nlvl + 1)
+                if any(self.owner[c - 1] >= 0 and self.owner[self.parent[c - 1] - 1] < 0
+                       for c in self.ids[l])]
+
+    def octant_regions(self, send_rank, level=None):
+        """Parent octants written by send_rank's boxes of `level` (default
+        Lp) into their replicated parents, in box order."""
+        if self.lp is None:
+            return []
+        level = self.lp if level is None else level
         hnc = self.nc // 2
         out = []
-        for c in self.ids[self.lp]:
+        for c in self.ids[level]:
             if self.owner[c - 1] != send_rank:
                 continue
             p = self.parent[c - 1]
+            if self.owner[p - 1] >= 0:
+                continue
             co = [((self.ix[c - 1][k] - 1) & 1) * hnc for k in range(3)]
             out.append((int(p), co[0] + 1, co[1] + 1, co[2] + 1,
                         co[0] + hnc, co[1] + hnc, co[2] + hnc))
@@ -258,10 +321,11 @@ class Shard:
             self.plans[("cflux", 0)] = (
                 {q: self._plan(part.cflux_regions(q, self.rank), fc=True) for q in peers},
                 {q: self._plan(part.cflux_regions(self.rank, q), fc=True) for q in peers})
-            mine = self._plan(part.octant_regions(self.rank))
-            self.plans[("octant", part.lp)] = (
-                {q: mine for q in peers},
-                {q: self._plan(part.octant_regions(q)) for q in peers})
+            for lvl in part.restrict_levels():
+                mine = self._plan(part.octant_regions(self.rank, lvl))
+                self.plans[("octant", lvl)] = (
+                    {q: mine for q in peers},
+                    {q: self._plan(part.octant_regions(q, lvl)) for q in peers})
         self._bufs = {}
         self.stream = None
         if self.device is not None and self.backend == "nccl":

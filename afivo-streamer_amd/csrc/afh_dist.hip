@@ -3,10 +3,10 @@
 // shards a tree without a collective library of its own.
 //
 // Partition (as afivo-streamer_amd/afh/dist.py states it, the tests compare
-// the two): the partition level Lp is the coarsest level >= 2 with a box per
-// rank; its boxes, in Morton order of box%ix, are cut into contiguous chunks
-// of equal leaf-cell weight; descendants follow their Lp ancestor; levels
-// below Lp are replicated (owner -1).
+// the two): a weighted Morton split of a partition frontier, refined until
+// the heaviest rank carries at most 110 % of the mean leaf weight
+// (afh_dist_core.h partition()); descendants follow their frontier box; the
+// frontier's ancestors and level 1 are replicated (owner -1).
 //
 // Plans: for every exchange the library's hooks request (HALO / RIMS per
 // level, CFLUX, RESTRICT), the regions this rank sends to and receives from
@@ -187,7 +187,9 @@ int32_t afh_dist_partition(const afh_tree_desc *desc, int32_t n_ranks, int32_t *
   const Topo t = topo_of(desc);
   std::vector<int32_t> own;
   const int l = partition(t, n_ranks, own);
-  if (l < 0) return set_error(AFH_ERR_ARG, "no level >= 2 has %d boxes to shard", n_ranks);
+  if (l < 0)
+    return set_error(AFH_ERR_ARG, "no level >= 2 has enough boxes to shard over %d ranks",
+                     n_ranks);
   std::copy(own.begin(), own.end(), owner);
   if (lp) *lp = l;
   return AFH_OK;
@@ -366,7 +368,8 @@ int32_t afh_dist_create(afh_tree *t, const afh_tree_desc *desc, const int32_t *o
     for (int l = lp; l <= tp.nlvl && !e; l++)
       if (!(e = add(AFH_HOOK_HALO, l))) e = add(AFH_HOOK_RIMS, l);
     if (!e) e = add(AFH_HOOK_CFLUX, 0);
-    if (!e) e = add(AFH_HOOK_RESTRICT, lp);
+    for (int l : restrict_levels(tp, own, lp))
+      if (!e) e = add(AFH_HOOK_RESTRICT, l);
   }
   if (!e && transport == AFH_DIST_RCCL && hipMalloc(&d->d_red, 16 * sizeof(double)) != hipSuccess)
     e = set_error(AFH_ERR_DEVICE, "reduction buffer");

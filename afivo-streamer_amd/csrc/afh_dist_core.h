@@ -22,6 +22,8 @@ namespace afhd {
 using Region = std::array<int32_t, 8>;  // cc: id, lo[3], hi[3] (7 used); fc: id, dim, lo, hi
 
 constexpr int DEPTH = 2;  // halo layers (dist.py DEPTH)
+constexpr int TOL_PCT = 10;  // frontier refined while max load > (100 + TOL_PCT) % of the mean
+constexpr int MORTON_BITS = 21;
 
 struct Topo {
   int nc, nb, nlvl;
@@ -43,24 +45,27 @@ inline Topo topo_of(const afh_tree_desc *d) {
   return t;
 }
 
-inline int64_t morton3(const int32_t ix[3]) {
+// Z-order index of the box's lower corner at `shift` levels finer
+inline int64_t morton3(const int32_t ix[3], int shift = 0) {
   int64_t code = 0;
-  for (int b = 0; b < 20; b++)
-    for (int d = 0; d < 3; d++) code |= (int64_t)(((ix[d] - 1) >> b) & 1) << (3 * b + d);
+  for (int b = 0; b < MORTON_BITS; b++)
+    for (int d = 0; d < 3; d++)
+      code |= (int64_t)((((int64_t)(ix[d] - 1) << shift) >> b) & 1) << (3 * b + d);
   return code;
 }
 
-// Partition.__init__ (afh/dist.py)
+// Partition._partition (afh/dist.py): the weighted Morton split of a
+// partition frontier. The frontier starts as level 2 (level 1 replicated);
+// its boxes, in Z-order of their lower corners at the finest resolution, are
+// cut into chunks of about equal leaf weight; while the heaviest rank carries
+// more than (100 + TOL_PCT) % of the mean (or the frontier has fewer boxes
+// than ranks), its heaviest refined box is replaced by its children and
+// becomes replicated. Descendants follow their frontier box. Returns the
+// first level with an owned box, or -1.
 inline int partition(const Topo &t, int n, std::vector<int32_t> &owner) {
   owner.assign(t.nb, -1);
   if (n <= 1) return 0;
-  int lp = 0;
-  for (int l = 2; l <= t.nlvl; l++)
-    if ((int)t.ids[l - 1].size() >= n) {
-      lp = l;
-      break;
-    }
-  if (!lp) return -1;
+  if (t.nlvl < 2) return -1;
   std::vector<int64_t> w(t.nb + 1, 0);
   for (int l = t.nlvl; l >= 1; l--)
     for (int32_t i : t.ids[l - 1]) {
@@ -73,26 +78,57 @@ inline int partition(const Topo &t, int n, std::vector<int32_t> &owner) {
         w[i] = s;
       }
     }
-  std::vector<int32_t> order = t.ids[lp - 1];
-  std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) {
-    return morton3(t.m[a - 1].ix) < morton3(t.m[b - 1].ix);
-  });
-  const int no = (int)order.size();
-  std::vector<int64_t> cum(no);
-  int64_t s = 0;
-  for (int q = 0; q < no; q++) cum[q] = (s += w[order[q]]);
-  const double target = (double)cum[no - 1] / n;
-  std::vector<int64_t> rk(no);
-  for (int q = 0; q < no; q++) {
-    const int64_t r = (int64_t)std::ceil((double)cum[q] / target) - 1;
-    rk[q] = std::min<int64_t>(r, n - 1);
+  std::vector<int32_t> roots = t.ids[1];
+  auto code = [&](int32_t b) { return morton3(t.m[b - 1].ix, t.nlvl - t.m[b - 1].lvl); };
+  std::vector<int32_t> order;
+  std::vector<int64_t> rk;
+  // chunks of the frontier; true when every rank gets a box
+  auto split = [&](int64_t &mx, int64_t &total) {
+    order = roots;
+    std::vector<int64_t> key(t.nb + 1, 0);
+    for (int32_t b : order) key[b] = code(b);
+    std::stable_sort(order.begin(), order.end(),
+                     [&](int32_t a, int32_t b) { return key[a] < key[b]; });
+    const int no = (int)order.size();
+    std::vector<int64_t> cum(no);
+    int64_t s = 0;
+    for (int q = 0; q < no; q++) cum[q] = (s += w[order[q]]);
+    total = s;
+    const double target = (double)s / n;
+    rk.assign(no, 0);
+    std::vector<int64_t> load(n, 0);
+    for (int q = 0; q < no; q++) {
+      const int64_t r = (int64_t)std::ceil((double)cum[q] / target) - 1;
+      rk[q] = std::min<int64_t>(r, n - 1);
+      load[rk[q]] += w[order[q]];
+    }
+    mx = *std::max_element(load.begin(), load.end());
+    return (int)std::set<int64_t>(rk.begin(), rk.end()).size() == n;
+  };
+  int64_t mx = 0, total = 0;
+  for (;;) {
+    if ((int)roots.size() >= n && split(mx, total) && mx * n * 100 <= (100 + TOL_PCT) * total)
+      break;
+    int32_t h = 0;
+    for (int32_t r : roots)
+      if (t.m[r - 1].children[0] > 0 && (!h || w[r] > w[h] || (w[r] == w[h] && r < h))) h = r;
+    if (!h) {
+      if ((int)roots.size() < n) return -1;
+      break;
+    }
+    roots.erase(std::find(roots.begin(), roots.end(), h));
+    for (int c = 0; c < 8; c++) roots.push_back(t.m[h - 1].children[c]);
   }
-  std::set<int64_t> used(rk.begin(), rk.end());
-  if ((int)used.size() < n)
-    for (int q = 0; q < no; q++) rk[q] = ((int64_t)q * n) / no;
-  for (int q = 0; q < no; q++) owner[order[q] - 1] = (int32_t)rk[q];
-  for (int l = lp + 1; l <= t.nlvl; l++)
-    for (int32_t i : t.ids[l - 1]) owner[i - 1] = owner[t.m[i - 1].parent - 1];
+  if (!split(mx, total))  // every rank gets a frontier box: an even split
+    for (size_t q = 0; q < order.size(); q++) rk[q] = ((int64_t)q * n) / (int64_t)order.size();
+  for (size_t q = 0; q < order.size(); q++) owner[order[q] - 1] = (int32_t)rk[q];
+  for (int l = 3; l <= t.nlvl; l++)
+    for (int32_t i : t.ids[l - 1]) {
+      const int32_t p = t.m[i - 1].parent;
+      if (owner[p - 1] >= 0) owner[i - 1] = owner[p - 1];
+    }
+  int lp = t.nlvl;
+  for (int32_t r : roots) lp = std::min(lp, t.m[r - 1].lvl);
   return lp;
 }
 
@@ -120,7 +156,8 @@ inline std::vector<Region> halo_regions(const Topo &t, const std::vector<int32_t
   if (!lp || level < lp) return out;
   std::set<Region> regs;
   for (int32_t a : t.ids[level - 1]) {
-    if (owner[a - 1] != recv) continue;
+    // the boxes recv computes: its own and the replicated ones
+    if (owner[a - 1] != recv && owner[a - 1] >= 0) continue;
     for (int dz = -1; dz <= 1; dz++)
       for (int dy = -1; dy <= 1; dy++)
         for (int dx = -1; dx <= 1; dx++) {
@@ -165,17 +202,18 @@ inline std::vector<Region> cflux_regions(const Topo &t, const std::vector<int32_
         out.push_back(Region{q, d, lo[0], lo[1], lo[2], hi[0], hi[1], hi[2]});
       }
     }
-  // a replicated refined box whose children are sharded (the level below
-  // Lp): every rank computes the coarse leaf neighbour's face, but only the
-  // owner of a child has that child's fluxes -- the face quarter each child
-  // covers goes from the child's owner to every other rank
+  // a replicated refined box whose children are sharded: only the owner of
+  // a child has that child's fluxes -- the face quarter each child covers on
+  // the coarse leaf neighbour goes from the child's owner to the neighbour's
+  // owner (to every other rank when the neighbour is replicated)
   const int h = t.nc / 2;
   for (int l = 1; l <= t.nlvl; l++)
     for (int32_t p : t.parents[l - 1]) {
       if (owner[p - 1] >= 0) continue;
       for (int nb = 1; nb <= 6; nb++) {
         const int q = t.m[p - 1].neighbors[nb - 1];
-        if (q <= 0 || t.m[q - 1].children[0] != 0 || owner[q - 1] >= 0 || recv == send) continue;
+        if (q <= 0 || t.m[q - 1].children[0] != 0 || recv == send) continue;
+        if (owner[q - 1] >= 0 && owner[q - 1] != recv) continue;
         const int d = (nb - 1) / 2, side = (nb - 1) % 2;  // side 0: q below p
         const int f = side == 0 ? t.nc + 1 : 1;
         for (int ch = 0; ch < 8; ch++) {
@@ -192,20 +230,36 @@ inline std::vector<Region> cflux_regions(const Topo &t, const std::vector<int32_
   return out;
 }
 
-// Partition.octant_regions: parent octants written by send's boxes of Lp
+// Partition.octant_regions: parent octants written by send's boxes of
+// `level` into their replicated parents
 inline std::vector<Region> octant_regions(const Topo &t, const std::vector<int32_t> &owner, int lp,
-                                   int send) {
+                                   int send, int level) {
   std::vector<Region> out;
-  if (!lp) return out;
+  if (!lp || level < 2 || level > t.nlvl) return out;
   const int h = t.nc / 2;
-  for (int32_t c : t.ids[lp - 1]) {
+  for (int32_t c : t.ids[level - 1]) {
     if (owner[c - 1] != send) continue;
     const afh_box_meta &m = t.m[c - 1];
+    if (owner[m.parent - 1] >= 0) continue;
     int co[3];
     for (int k = 0; k < 3; k++) co[k] = ((m.ix[k] - 1) & 1) * h;
     out.push_back(Region{m.parent, co[0] + 1, co[1] + 1, co[2] + 1, co[0] + h, co[1] + h,
                          co[2] + h, 0});
   }
+  return out;
+}
+
+// Partition.restrict_levels: levels with an owned box whose parent is
+// replicated (a RESTRICT exchange follows their restriction)
+inline std::vector<int> restrict_levels(const Topo &t, const std::vector<int32_t> &owner, int lp) {
+  std::vector<int> out;
+  if (!lp) return out;
+  for (int l = std::max(2, lp); l <= t.nlvl; l++)
+    for (int32_t c : t.ids[l - 1])
+      if (owner[c - 1] >= 0 && owner[t.m[c - 1].parent - 1] < 0) {
+        out.push_back(l);
+        break;
+      }
   return out;
 }
 
@@ -215,8 +269,7 @@ inline std::vector<Region> plan_regions(const Topo &t, const std::vector<int32_t
   case AFH_HOOK_HALO: return halo_regions(t, owner, lp, recv, send, level, false);
   case AFH_HOOK_RIMS: return halo_regions(t, owner, lp, recv, send, level, true);
   case AFH_HOOK_CFLUX: return cflux_regions(t, owner, lp, recv, send);
-  case AFH_HOOK_RESTRICT: return level == lp ? octant_regions(t, owner, lp, send)
-                                             : std::vector<Region>();
+  case AFH_HOOK_RESTRICT: return octant_regions(t, owner, lp, send, level);
   default: return {};
   }
 }
@@ -279,8 +332,10 @@ inline std::vector<int32_t> local_boxes(const Topo &t, const std::vector<int32_t
       }
       add(plan_regions(t, owner, lp, AFH_HOOK_CFLUX, 0, rank, q));
       add(plan_regions(t, owner, lp, AFH_HOOK_CFLUX, 0, q, rank));
-      add(plan_regions(t, owner, lp, AFH_HOOK_RESTRICT, lp, rank, q));
-      add(plan_regions(t, owner, lp, AFH_HOOK_RESTRICT, lp, q, rank));
+      for (int l : restrict_levels(t, owner, lp)) {
+        add(plan_regions(t, owner, lp, AFH_HOOK_RESTRICT, l, rank, q));
+        add(plan_regions(t, owner, lp, AFH_HOOK_RESTRICT, l, q, rank));
+      }
     }
   for (int l = 1; l <= t.nlvl; l++) {
     bool any = false;

@@ -163,7 +163,10 @@ struct afh_tree {
   // empty on an unsharded tree
   std::vector<char> sum_skip;
 
-  double *ccv(int iv) const { return cc + (size_t)(iv - 1) * cap * bsz; }
+  // cc variable stride (doubles): cap * bsz, plus AFH_POOL_PAD bytes
+  size_t vstride = 0;
+  double *alt_base = nullptr;  // allocation of alt (alt = alt_base + AFH_ALT_OFF)
+  double *ccv(int iv) const { return cc + (size_t)(iv - 1) * vstride; }
   // cc variable iv, or the smoother's spare image of phi for iv == 0
   double *var(int iv) const { return iv == 0 ? alt : ccv(iv); }
   double *fcv(int ivf) const { return fc + (size_t)(ivf - 1) * cap * fsz; }

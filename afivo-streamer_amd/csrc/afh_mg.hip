@@ -2570,9 +2570,13 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
     if (any) {
       // one spare image per tree: the level fills after a pair fill t->alt
       if (!t->alt) {
-        if (int32_t e2 = pool_alloc((void **)&t->alt, (size_t)t->nb * t->bsz * sizeof(double),
-                                    "alt"))
+        // AFH_ALT_OFF: the spare image starts that many bytes into its
+        // allocation (placement experiments)
+        const size_t off = getenv("AFH_ALT_OFF") ? (size_t)atoll(getenv("AFH_ALT_OFF")) / 8 : 0;
+        if (int32_t e2 = pool_alloc((void **)&t->alt_base,
+                                    ((size_t)t->nb * t->bsz + off) * sizeof(double), "alt"))
           return e2;
+        t->alt = t->alt_base + off;
         AFH_HIP(hipMemsetAsync(t->alt, 0, (size_t)t->nb * t->bsz * sizeof(double),
                                t->stream));
       }
@@ -2618,8 +2622,8 @@ int32_t afh_mg_destroy(afh_mg *mg) {
   hipFree(mg->w1);
   hipFree(mg->w2);
   if (mg->alt && --mg->t->alt_refs == 0) {
-    hipFree(mg->t->alt);
-    mg->t->alt = nullptr;
+    hipFree(mg->t->alt_base);
+    mg->t->alt = mg->t->alt_base = nullptr;
   }
   for (auto *v : {&mg->h_vp, &mg->h_bp, &mg->h_dd, &mg->h_bv})
     for (double *q : *v) hipFree(q);

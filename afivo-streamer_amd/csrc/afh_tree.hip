@@ -956,11 +956,16 @@ static int32_t tree_create_impl(const afh_tree_desc *d, int32_t device,
                     hipMemcpyHostToDevice));
   if (adopt) {  // afh_tree_regrid in place: the old tree's pools
     t->cap = adopt->cap;
+    t->vstride = adopt->vstride;
     t->cc = adopt->cc, t->fc = adopt->fc, t->gc2 = adopt->gc2;
     adopt->cc = adopt->fc = adopt->gc2 = nullptr;
     adopt->retired = true;
   } else {
-    size_t ncc = (size_t)t->nvc * t->cap * t->bsz;
+    // AFH_POOL_PAD: bytes between cc variables (placement experiments:
+    // the relative offsets of the streams a kernel reads in HBM)
+    const size_t pad = getenv("AFH_POOL_PAD") ? (size_t)atoll(getenv("AFH_POOL_PAD")) / 8 : 0;
+    t->vstride = (size_t)t->cap * t->bsz + pad;
+    size_t ncc = (size_t)t->nvc * t->vstride;
     size_t nfc = (size_t)std::max(1, t->nvf) * t->cap * t->fsz;
     if (int32_t e2 = pool_alloc((void **)&t->cc, ncc * sizeof(double), "cc")) return e2;
     if (int32_t e2 = pool_alloc((void **)&t->fc, nfc * sizeof(double), "fc")) return e2;
@@ -1473,7 +1478,7 @@ int32_t afh_tree_regrid(afh_tree *o, const afh_tree_desc *d, afh_tree **out) {
     const unsigned n = (unsigned)fresh.size();
     hipLaunchKernelGGL(k_copy_boxes, dim3((unsigned)((t->bsz + 255) / 256), n, t->nvc),
                        dim3(256), 0, t->stream, nullptr, t->cc, d_list, t->bsz,
-                       (size_t)0, (size_t)t->cap * t->bsz);
+                       (size_t)0, t->vstride);
     AFH_LAUNCH_CHECK("k_copy_boxes");
     if (t->nvf > 0) {
       hipLaunchKernelGGL(k_copy_boxes, dim3((unsigned)((t->fsz + 255) / 256), n, t->nvf),
@@ -1490,7 +1495,7 @@ int32_t afh_tree_regrid(afh_tree *o, const afh_tree_desc *d, afh_tree **out) {
     const unsigned n = (unsigned)kept.size();
     hipLaunchKernelGGL(k_copy_boxes, dim3((unsigned)((t->bsz + 255) / 256), n, t->nvc),
                        dim3(256), 0, t->stream, o->cc, t->cc, d_list, t->bsz,
-                       (size_t)o->cap * o->bsz, (size_t)t->cap * t->bsz);
+                       o->vstride, t->vstride);
     AFH_LAUNCH_CHECK("k_copy_boxes");
     if (t->nvf > 0) {
       hipLaunchKernelGGL(k_copy_boxes, dim3((unsigned)((t->fsz + 255) / 256), n, t->nvf),

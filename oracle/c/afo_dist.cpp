@@ -133,7 +133,8 @@ int32_t afo_dist_partition(const afh_tree_desc *desc, int32_t n_ranks, int32_t *
   const Topo t = topo_of(desc);
   std::vector<int32_t> own;
   const int l = partition(t, n_ranks, own);
-  if (l < 0) return fail(AFH_ERR_ARG, "no level >= 2 has %d boxes to shard", n_ranks);
+  if (l < 0)
+    return fail(AFH_ERR_ARG, "no level >= 2 has enough boxes to shard over %d ranks", n_ranks);
   std::copy(own.begin(), own.end(), owner);
   if (lp) *lp = l;
   return AFH_OK;
@@ -257,7 +258,8 @@ int32_t afo_dist_create(afh_tree *t, const afh_tree_desc *desc, const int32_t *o
     for (int l = lp; l <= tp.nlvl && !e; l++)
       if (!(e = add(AFH_HOOK_HALO, l))) e = add(AFH_HOOK_RIMS, l);
     if (!e) e = add(AFH_HOOK_CFLUX, 0);
-    if (!e) e = add(AFH_HOOK_RESTRICT, lp);
+    for (int l : restrict_levels(tp, own, lp))
+      if (!e) e = add(AFH_HOOK_RESTRICT, l);
   }
   if (!e) e = afo_tree_set_hook(t, dist_hook, d);
   if (e) {

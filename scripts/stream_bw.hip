@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 __global__ void copy8(const double *__restrict__ a, double *__restrict__ b, size_t n) {
@@ -52,12 +53,27 @@ double timeit(F f) {
   return t[t.size() / 2] * 1e-3;
 }
 
+// STREAM_CONTIG=1: the three arrays in one hipDeviceMallocContiguous
+// allocation; STREAM_GAP (bytes): extra bytes between them
 int main() {
   const size_t n = (size_t)1 << 27;  // 1 GiB per array of doubles
   double *a, *b, *c;
-  hipMalloc(&a, n * 8);
-  hipMalloc(&b, n * 8);
-  hipMalloc(&c, n * 8);
+  const char *ce = getenv("STREAM_CONTIG");
+  if (ce && atoi(ce)) {
+    const size_t gap = getenv("STREAM_GAP") ? (size_t)atoll(getenv("STREAM_GAP")) / 8 : 0;
+    double *base = nullptr;
+    if (hipExtMallocWithFlags((void **)&base, (3 * (n + gap)) * 8, hipDeviceMallocContiguous) !=
+        hipSuccess) {
+      printf("contiguous allocation refused\n");
+      return 1;
+    }
+    a = base, b = base + n + gap, c = base + 2 * (n + gap);
+    printf("contiguous, gap %zu B\n", gap * 8);
+  } else {
+    hipMalloc(&a, n * 8);
+    hipMalloc(&b, n * 8);
+    hipMalloc(&c, n * 8);
+  }
   hipMemset(a, 0, n * 8);
   hipMemset(b, 0, n * 8);
   hipMemset(c, 0, n * 8);

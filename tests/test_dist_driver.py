@@ -56,6 +56,11 @@ def _run(lib, name, world, device=-1):
     for sim, sh in zip(clones, shards):
         sim.shard_over(sh)
     assert shards[0].lp is not None
+    if world == 8:  # a mixed frontier: some level holds replicated and owned boxes
+        o = shards[0].owner
+        lv = base.af.topology()["meta_lvl"]
+        assert any((o[lv == l] < 0).any() and (o[lv == l] >= 0).any()
+                   for l in range(2, base.af.highest_lvl + 1))
     owned = [int(np.sum(sh.owner == r)) for r, sh in enumerate(shards)]
     assert min(owned) > 0, owned
     try:
@@ -79,14 +84,18 @@ def _run(lib, name, world, device=-1):
                                                        np.nanmax(np.abs(got[used] - want[used])))
 
 
-@pytest.mark.parametrize("name,world", [("photoi_chem", 2), ("s4_rod", 2), ("s5_sprite", 2)])
+@pytest.mark.parametrize("name,world", [("photoi_chem", 2), ("s4_rod", 2), ("s5_sprite", 2),
+                                        ("s5_sprite", 8), ("s4_rod", 8)])
 def test_sharded_driver_oracle_threads_bitwise(name, world):
+    # 8 ranks: the partition frontier spans several levels (replicated
+    # parents next to owned boxes of the same level, owned boxes restricted
+    # into replicated parents on several levels)
     _run(capi.oracle_library(), name, world)
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name,world", [("photoi_chem", 2), ("photoi_chem", 3),
-                                        ("s4_rod", 2), ("s5_sprite", 2)])
+                                        ("s4_rod", 2), ("s5_sprite", 2), ("s5_sprite", 8)])
 def test_sharded_driver_hip_threads_bitwise(name, world):
     _run(capi.hip_library(), name, world, device=0)
 

@@ -39,7 +39,7 @@ def _python_regions(part, kind, level, recv, send):
     elif kind == capi.HOOK_CFLUX:
         r = part.cflux_regions(recv, send)
     else:
-        r = part.octant_regions(send) if level == part.lp else []
+        r = part.octant_regions(send, level) if level in part.restrict_levels() else []
     w = 8 if kind == capi.HOOK_CFLUX else 7
     return np.asarray(r, np.int32).reshape(-1, w)
 
