@@ -398,8 +398,9 @@ class Simulation:
         is created from the current topology and filled with the current
         data of every variable, the multigrids and the fluid are bound to it
         and the shard's exchange hook is attached. Every rank must hold the
-        same state before (e.g. the same deterministic set-up). Refinement is
-        not sharded: adjust_refinement then raises."""
+        same state before (e.g. the same deterministic set-up). A refinement
+        of the sharded run (adjust_refinement) needs the library's own
+        sharding (afh.dist.NativeShard); with the Python Shard it raises."""
         topo = self.af.topology()
         full = self.tree
         t = self._set_methods(shard.make_tree(self.lib, topo, self.n_var_cell,
@@ -440,6 +441,9 @@ class Simulation:
         topology, so the load balance follows the refinement."""
         import copy
         sh = self.shard
+        if not hasattr(sh, "renew"):
+            raise NotImplementedError("refinement of a run sharded by the Python Shard "
+                                      "(afh.dist.Shard); use afh.dist.NativeShard")
         # the refinement flags of the computed boxes decide first, on a copy
         # of the host topology: most calls change nothing and move no data
         t = self.tree

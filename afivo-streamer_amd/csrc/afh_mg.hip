@@ -20,6 +20,9 @@
 #include <map>
 
 #include "afh_internal.h"
+#include "afh_cs_direct.h"
+
+#include <mutex>
 
 namespace afh {
 
@@ -2351,6 +2354,14 @@ struct afh_mg {
   std::vector<char> lvl_var;  // level has variable-stencil boxes
   LevelList ids_c, ids_v, leaves_c, leaves_v, parents_c, parents_v, lsf_leaves;
   double *cs_old = nullptr;   // level-1 electrode solve: previous phi
+  // AFH_CS_ELEC_DIRECT (default on): the one-box electrode level-1 solve as
+  // x = A^-1 ((rhs + bcc) - g) (afh_cs_direct.h); host copy of the level-1
+  // box's stencil, the device inverse and g, and what they were built from
+  bool csd_on = true, csd_ok = false;
+  std::vector<double> h_v1;
+  int h_v1_id = 0;
+  uint64_t v1_gen = 1, csd_v_gen = 0, csd_meth_gen = UINT64_MAX;
+  double *d_csd_ainv = nullptr, *d_csd_g = nullptr;
 };
 
 // (diag, 1/diag) of the folded operator per MG level and boundary class, in
@@ -2554,6 +2565,7 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
   if (const char *env = getenv("AFH_PROLONG_K"))
     mg->prolong_k = atoi(env) == 8 ? 8 : atoi(env) == 2 ? 2 : 4;
   if (const char *env = getenv("AFH_CS_FUSED")) mg->cs_fused = atoi(env) != 0;
+  if (const char *env = getenv("AFH_CS_ELEC_DIRECT")) mg->csd_on = atoi(env) != 0;
   if (const char *env = getenv("AFH_CS_DIRECT_SMALL")) mg->cs_direct_small = atoi(env) != 0;
   if (const char *env = getenv("AFH_CS_DS_CELLS"))
     mg->cs_ds_cells = std::min(CS_SMALL_CELLS, std::max(0, atoi(env)));
@@ -2621,6 +2633,7 @@ int32_t afh_mg_destroy(afh_mg *mg) {
   for (int q = 0; q < 3; q++) hipFree(mg->d_q[q]), hipFree(mg->d_qt[q]), hipFree(mg->d_e[q]);
   hipFree(mg->w1);
   hipFree(mg->w2);
+  hipFree(mg->d_csd_ainv), hipFree(mg->d_csd_g);
   if (mg->alt && --mg->t->alt_refs == 0) {
     hipFree(mg->t->alt_base);
     mg->t->alt = mg->t->alt_base = nullptr;
@@ -3151,9 +3164,115 @@ static bool cs_electrode_fused(const afh_mg *mg) {
   return phys;
 }
 
+// The one-box electrode level-1 solve as a dense product (afh_cs_direct.h):
+// x = A^-1 ((rhs + bcc) - g), one thread per row of A^-1, the columns in
+// order; A^-1 stored column-major, so a wave's loads of one column are
+// contiguous. Bitwise the C oracle's loop.
+__global__ void __launch_bounds__(64)
+    k_cs_elec_direct(double *__restrict__ x, const double *__restrict__ r,
+                     const double *__restrict__ bcc, const double *__restrict__ ainv_t,
+                     const double *__restrict__ g) {
+  constexpr int NC = AFH_CSD_NC, NG = NC + 2, N = AFH_CSD_N;
+  __shared__ double B[N];
+  for (int e = threadIdx.x; e < N; e += blockDim.x) {
+    const int i = e % NC + 1, j = (e / NC) % NC + 1, k = e / (NC * NC) + 1;
+    double rv = r[ix3(NG, i, j, k)];
+    if (bcc) rv = rv + bcc[e];
+    B[e] = rv - g[e];
+  }
+  __syncthreads();
+  const int row = blockIdx.x * blockDim.x + threadIdx.x;
+  double acc = 0.0;
+  for (int c = 0; c < N; c++) acc = acc + ainv_t[(size_t)c * N + row] * B[c];
+  const int i = row % NC + 1, j = (row / NC) % NC + 1, k = row / (NC * NC) + 1;
+  x[ix3(NG, i, j, k)] = acc;
+}
+
+namespace {
+// A^-1 and g of the recent level-1 operators (a regrid creates new
+// multigrids with the same level-1 stencil): keyed by the stencil, the
+// boundary conditions and the spacing; shared by the thread ranks
+struct CsdEntry {
+  std::vector<double> v, ainv, g;
+  afh_bc bc[6];
+  double dr[3];
+  bool singular;
+};
+std::mutex csd_mu;
+std::vector<CsdEntry> csd_cache;
+}  // namespace
+
+// Before a V-cycle / FMG (outside any graph capture): whether the level-1
+// solve is the direct one, and its device tables current
+static int32_t prepare_cs_direct(afh_mg *mg) {
+  afh_tree *t = mg->t;
+  mg->csd_ok = false;
+  // a level 1 of one 8^3 box with an electrode stencil and six physical
+  // faces, no sharding hook (the oracle's solve_coarse_direct: the same test)
+  if (!mg->csd_on || t->nc != AFH_CSD_NC || !(mg->any_var && mg->lvl_var[0]) ||
+      t->ids.n(1) != 1 || t->hook || mg->h_v1_id != t->h_ids[0][0] ||
+      !mg->h_vp[mg->h_v1_id - 1])
+    return AFH_OK;
+  for (int q = 0; q < 6; q++)
+    if (t->boxes[mg->h_v1_id - 1].neighbors[q] >= 0) return AFH_OK;
+  if (mg->csd_v_gen == mg->v1_gen && mg->csd_meth_gen == t->meth_gen && mg->d_csd_ainv) {
+    mg->csd_ok = true;
+    return AFH_OK;
+  }
+  const afh_box_meta &m = t->boxes[mg->h_v1_id - 1];
+  const afh_bc *bc = t->meth[mg->d.i_phi].bc;
+  const CsdEntry *hit = nullptr;
+  std::lock_guard<std::mutex> lk(csd_mu);
+  for (const CsdEntry &c : csd_cache)
+    if (c.v == mg->h_v1 && !memcmp(c.bc, bc, sizeof c.bc) && !memcmp(c.dr, m.dr, sizeof c.dr))
+      hit = &c;
+  if (!hit) {
+    CsdEntry c;
+    c.v = mg->h_v1;
+    memcpy(c.bc, bc, sizeof c.bc);
+    memcpy(c.dr, m.dr, sizeof c.dr);
+    c.ainv.assign((size_t)AFH_CSD_N * AFH_CSD_N, 0.0);
+    c.g.assign(AFH_CSD_N, 0.0);
+    std::vector<double> work((size_t)2 * AFH_CSD_N * AFH_CSD_N);
+    c.singular = afh_csd_build(c.v.data(), c.bc, c.dr, c.ainv.data(), c.g.data(), work.data()) != 0;
+    if (csd_cache.size() >= 4) csd_cache.erase(csd_cache.begin());
+    csd_cache.push_back(std::move(c));
+    hit = &csd_cache.back();
+  }
+  if (hit->singular) return AFH_OK;  // the iteration stays
+  if (!mg->d_csd_ainv) {
+    AFH_HIP(hipMalloc(&mg->d_csd_ainv, sizeof(double) * AFH_CSD_N * AFH_CSD_N));
+    AFH_HIP(hipMalloc(&mg->d_csd_g, sizeof(double) * AFH_CSD_N));
+  }
+  AFH_HIP(hipStreamSynchronize(t->stream));
+  AFH_HIP(hipMemcpy(mg->d_csd_ainv, hit->ainv.data(), sizeof(double) * hit->ainv.size(),
+                    hipMemcpyHostToDevice));
+  AFH_HIP(hipMemcpy(mg->d_csd_g, hit->g.data(), sizeof(double) * AFH_CSD_N,
+                    hipMemcpyHostToDevice));
+  mg->csd_v_gen = mg->v1_gen;
+  mg->csd_meth_gen = t->meth_gen;
+  mg->csd_ok = true;
+  return AFH_OK;
+}
+
+static int32_t prepare_all(afh_mg *mg) {
+  if (int32_t e = prepare_var(mg)) return e;
+  return prepare_cs_direct(mg);
+}
+
 static int32_t solve_coarse_gs(afh_mg *mg) {
   afh_tree *t = mg->t;
   const int nid = t->ids.n(1), nc = t->nc, n3 = nc * nc * nc;
+  if (mg->csd_ok) {
+    const int id = t->h_ids[0][0];
+    hipLaunchKernelGGL(k_cs_elec_direct, dim3(AFH_CSD_N / 64), dim3(64), 0, t->stream,
+                       t->ccv(mg->d.i_phi) + (size_t)(id - 1) * t->bsz,
+                       t->ccv(mg->d.i_rhs) + (size_t)(id - 1) * t->bsz, mg->h_bp[id - 1],
+                       mg->d_csd_ainv, mg->d_csd_g);
+    AFH_LAUNCH_CHECK("k_cs_elec_direct");
+    mg->cycles_host = 1, mg->cycles_on_dev = false;
+    return gc_lvl(t, 1, mg->d.i_phi, 1);
+  }
   if (cs_electrode_fused(mg)) {
     const int id = t->h_ids[0][0];
     const afh_box_meta &m = t->boxes[id - 1];
@@ -3356,7 +3475,7 @@ int32_t afh_mg_fas_fmg(afh_mg *mg, int32_t set_residual, int32_t have_guess) {
   const int nl = t->nlvl, i_phi = mg->d.i_phi;
   double *phi = t->ccv(i_phi), *tmp = t->ccv(mg->d.i_tmp);
   int32_t e;
-  if ((e = prepare_var(mg))) return e;
+  if ((e = prepare_all(mg))) return e;
   if (have_guess) {
     for (int lvl = nl; lvl >= 2; lvl--) {
       if (lvl == nl && (e = gc_lvl(t, lvl, i_phi, 1, fused_level(mg, lvl)))) return e;
@@ -3476,7 +3595,7 @@ static int32_t vcycle_graph(afh_mg *mg, int32_t set_residual, int max_lvl, bool 
   // (the multi-launch coarse cycles with a stopping rule read the device
   // every cycle too)
   if (!mg->use_graphs || t->hook || t->prof_class ||
-      (mg->any_var && mg->lvl_var[0] && !cs_electrode_fused(mg)) ||
+      (mg->any_var && mg->lvl_var[0] && !cs_electrode_fused(mg) && !mg->csd_ok) ||
       (mg->d.coarse_mode == AFH_COARSE_CYCLES && mg->d.coarse_tol > 0 && mg->small_from > 0))
     return AFH_OK;
   const int key = (max_lvl << 3) | (top_stale ? 4 : 0) | (set_residual ? 2 : 0) |
@@ -3523,7 +3642,7 @@ static int32_t vcycle_impl(afh_mg *mg, int32_t set_residual, int32_t hl, bool ma
   t->touch(mg->d.i_phi), t->touch(mg->d.i_rhs), t->touch(mg->d.i_tmp);
   const int max_lvl = (hl > 0 && hl <= t->nlvl) ? hl : t->nlvl;
   int32_t e;
-  if ((e = prepare_var(mg))) return e;
+  if ((e = prepare_all(mg))) return e;
   bool done;
   max_out = max_out && set_residual;
   if ((e = vcycle_graph(mg, set_residual, max_lvl, max_out, top_stale, done))) return e;
@@ -3570,7 +3689,7 @@ int32_t afh_mg_compute_phi_gradient(afh_mg *mg, int32_t i_fc, double fac,
   if (i_fc < 0 || i_fc > t->nvf || i_norm < 0 || i_norm > t->nvc)
     return set_error(AFH_ERR_ARG, "bad variable index");
   int32_t e;
-  if ((e = prepare_var(mg))) return e;
+  if ((e = prepare_all(mg))) return e;
   // i_fc = 0: the norm only (the flux evaluates the face field from phi,
   // afh_fluid_set_field_source); electrode boxes need the face field
   if (i_fc == 0 && (i_norm == 0 || mg->any_lsf))
@@ -3626,6 +3745,11 @@ int32_t afh_mg_set_box_stencil(afh_mg *mg, int32_t id, const double *v,
   hipFree(mg->h_vp[id - 1]), hipFree(mg->h_bp[id - 1]);
   mg->h_vp[id - 1] = mg->h_bp[id - 1] = nullptr;
   mg->var_dirty = true;
+  if (t->boxes[id - 1].lvl == 1) {  // the level-1 solve's host copy
+    mg->v1_gen++;
+    if (v) mg->h_v1.assign(v, v + 7 * n3), mg->h_v1_id = id;
+    else if (mg->h_v1_id == id) mg->h_v1.clear(), mg->h_v1_id = 0;
+  }
   if (!v) return AFH_OK;
   AFH_HIP(hipMalloc(&mg->h_vp[id - 1], sizeof(double) * 7 * n3));
   AFH_HIP(hipMemcpy(mg->h_vp[id - 1], v, sizeof(double) * 7 * n3,

@@ -111,7 +111,9 @@ def unit_step(case, dt, k):
     # one host synchronisation per sub-step (afh_mg_fas_vcycle_fold)
     # stage 1's dt limits are never read (af_advance keeps the last
     # sub-step's, m_af_advance.f90:160-164): they stay on the device and the
-    # host synchronises once per time step, after stage 2
+    # host synchronises once per time step, after stage 2. So is stage 1's
+    # V-cycle residual: the returned list is empty for stage 1 (the JSON
+    # line's last_residual is stage 2's)
     if k % 2 == 0:
         res = case.field_compute(0, n_vcycles=1, defer=True)
         d = case.species_step(dt, 0, [0], [1.0], 1, False, fetch=False)
@@ -355,8 +357,11 @@ def main():
     barrier()
     case.tree.sync()
     t0 = time.perf_counter()
+    last_res = None
     for k in range(args.steps):
         last = unit_step(case, dt, args.warmup + k)
+        if last[0]:
+            last_res = last[0]  # (stage 1 returns no residual: deferred)
     case.tree.sync()
     barrier()
     elapsed = time.perf_counter() - t0
@@ -430,7 +435,7 @@ def main():
                          "launches": nl.value,
                          "timed_over": ("2 eager unit steps after the timed region"
                                         if graphs else "the timed region")},
-            "last_residual": last[0][-1] if last[0] else None,
+            "last_residual": last_res[-1] if last_res else None,
             # one FAS V(2,2)-cycle per step (SURVEY.md 8(d) reports both)
             "vcycles_per_s": args.steps / elapsed,
         }

@@ -8,6 +8,7 @@
  */
 #define _POSIX_C_SOURCE 200809L
 #include "afo.h"
+#include "../../afivo-streamer_amd/csrc/afh_cs_direct.h"
 
 #include <float.h>
 #include <math.h>
@@ -1237,10 +1238,79 @@ static double f_spacing(double x) {
  * after each half-sweep, until phi is stationary (max change <= 4 spacing
  * of max |phi|, after at least 11 pairs) -- the golden harness' exact
  * solve -- then the level's ghost cells with corners. */
+/* The one-box electrode level-1 solve as a dense product (afh_cs_direct.h,
+ * the library's AFH_CS_ELEC_DIRECT, default on): a level 1 of one box of
+ * 8^3 with an electrode stencil and six physical faces. The inverse of the
+ * last operator is kept (a regrid makes new multigrids with the same
+ * level-1 stencil). Returns 1 when it does not apply (the iteration runs). */
+static struct {
+  double *v, *ainv, *g;
+  afh_bc bc[6];
+  double dr[3];
+  int valid, singular;
+} csd_last;
+
+static int solve_coarse_direct(afh_mg *mg) {
+  afh_tree *t = mg->t;
+  const char *env = getenv("AFH_CS_ELEC_DIRECT");
+  if ((env && !atoi(env)) || t->nc != AFH_CSD_NC || LVL_N(t, ids, 1) != 1 ||
+      t->hook)
+    return 1;
+  const int id = LVL_AT(t, ids, 1, 0);
+  const afh_box_meta *m = B(t, id);
+  if (!mg->vst[id - 1]) return 1;
+  for (int q = 0; q < 6; q++)
+    if (m->neighbors[q] >= 0) return 1;
+  const afh_bc *bc = t->meth[mg->d.i_phi].bc;
+  const size_t n = AFH_CSD_N;
+  if (!csd_last.valid || memcmp(csd_last.v, mg->vst[id - 1], sizeof(double) * 7 * n) ||
+      memcmp(csd_last.bc, bc, sizeof csd_last.bc) ||
+      memcmp(csd_last.dr, m->dr, sizeof csd_last.dr)) {
+    if (!csd_last.v) {
+      csd_last.v = malloc(sizeof(double) * 7 * n);
+      csd_last.ainv = malloc(sizeof(double) * n * n);
+      csd_last.g = malloc(sizeof(double) * n);
+    }
+    memcpy(csd_last.v, mg->vst[id - 1], sizeof(double) * 7 * n);
+    memcpy(csd_last.bc, bc, sizeof csd_last.bc);
+    memcpy(csd_last.dr, m->dr, sizeof csd_last.dr);
+    double *work = malloc(sizeof(double) * 2 * n * n);
+    csd_last.singular = afh_csd_build(csd_last.v, csd_last.bc, csd_last.dr, csd_last.ainv,
+                                      csd_last.g, work);
+    free(work);
+    csd_last.valid = 1;
+  }
+  if (csd_last.singular) return 1;
+  double b[AFH_CSD_N];
+  const double *r = ccb(t, mg->d.i_rhs, id), *bcc = mg->vbc[id - 1];
+  double *x = ccb(t, mg->d.i_phi, id);
+  const int nc = AFH_CSD_NC;
+  for (int e = 0; e < (int)n; e++) {
+    const int i = e % nc + 1, j = (e / nc) % nc + 1, k = e / (nc * nc) + 1;
+    double rv = r[IX(t, i, j, k)];
+    if (bcc) rv = rv + bcc[e];
+    b[e] = rv - csd_last.g[e];
+  }
+#pragma omp parallel for schedule(static)
+  for (int row = 0; row < (int)n; row++) {
+    double acc = 0.0;
+    for (size_t c = 0; c < n; c++) acc = acc + csd_last.ainv[c * n + row] * b[c];
+    const int i = row % nc + 1, j = (row / nc) % nc + 1, k = row / (nc * nc) + 1;
+    x[IX(t, i, j, k)] = acc;
+  }
+  mg->cs_iters = 1;
+  return gc_lvl(t, 1, mg->d.i_phi, 1) ? -1 : 0;
+}
+
 static int32_t solve_coarse_gs(afh_mg *mg) {
   afh_tree *t = mg->t;
   int nc = t->nc, nid = LVL_N(t, ids, 1);
   size_t bsz = t->bsz;
+  {
+    const int rc = solve_coarse_direct(mg);
+    if (rc == 0) return AFH_OK;
+    if (rc < 0) return AFH_ERR_STATE;
+  }
   double *old = malloc(sizeof(double) * bsz * (nid > 0 ? nid : 1));
   for (int it = 1; it <= 200000; it++) {
     for (int q = 0; q < nid; q++)

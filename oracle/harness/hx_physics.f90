@@ -5,14 +5,19 @@
 !> (/root/reference/afivo/src, see oracle/Makefile), and used to generate the
 !> fixtures in tests/golden/.
 !>
-!> The streamer modules (src/m_fluid.f90, m_field.f90, m_chemistry.f90,
-!> m_transport_data.f90) cannot be compiled here: all of them `use m_af_all`,
-!> which pulls m_af_output -> m_write_silo and the Silo library (absent). The
-!> afivo numerics they drive ARE compiled from the reference. The physics
-!> callbacks below are therefore restatements of the reference callbacks,
-!> restricted to the branches the hot path takes in configs 1-3 (LFA model,
-!> constant gas density, no energy equation, no dielectric, no photoi, no ion
-!> mobility, old-style transport data), each citing the lines it follows.
+!> The golden-vector harnesses (golden_gen.f90, golden_gen2d.f90) link only the
+!> afivo numerics compiled from the reference, not the streamer modules: they
+!> re-sequence mg_fas_vcycle around a level-1 solve of their own, because the
+!> reference's solve_coarse_grid calls HYPRE, which is absent. The physics
+!> callbacks below are restatements of the reference callbacks for that
+!> harness, restricted to the branches the hot path takes in configs 1-3 (LFA
+!> model, constant gas density, no energy equation, no dielectric, no photoi,
+!> no ion mobility, old-style transport data), each citing the lines it
+!> follows. (The streamer modules themselves DO compile here since round 2 --
+!> oracle/Makefile _ref/full and _ref/full2d, with silo_f9x.inc taken from the
+!> bundled Silo tarball -- and pin these restatements: replay_step runs the
+!> reference's own forward_euler on recorded states, tests/
+!> test_reference_replay.py and tests/test_2d_replay.py.)
 module hx_physics
 #include "cpp_macros.h"
   use m_af_types
