@@ -589,15 +589,44 @@ class NativeShard:
                            group=self.group, comm=self.comm)
 
     def allgather(self, obj):
-        """Every rank's obj, in rank order: the thread ranks' group, or the
-        torch.distributed process group (RCCL transport: one rank per
-        process)."""
+        """Every rank's obj, in rank order: the thread ranks' group (objects
+        shared in-process), or the torch.distributed process group (RCCL
+        transport: one rank per process; small host objects only)."""
         if self.transport == capi.DIST_LOCAL:
             return self.group.allgather(self.rank, obj)
         import torch.distributed as tdist
         out = [None] * self.n
         tdist.all_gather_object(out, obj)
         return out
+
+    def allgather_rows(self, ids, rows):
+        """Every rank's (ids, rows) -- int box ids and float64 rows of equal
+        width -- in rank order, as numeric collectives: the thread ranks'
+        group in-process; with the RCCL transport two all_gathers of device
+        tensors (the counts, then the rows padded to the longest), no pickling
+        of data."""
+        ids = np.ascontiguousarray(ids, np.int64)
+        rows = np.ascontiguousarray(rows, np.float64).reshape(len(ids), -1)
+        if self.transport == capi.DIST_LOCAL:
+            return self.group.allgather(self.rank, (ids, rows))
+        import torch
+        import torch.distributed as tdist
+        dev = "cuda" if tdist.get_backend() == "nccl" else "cpu"
+        n = torch.tensor([len(ids)], dtype=torch.int64, device=dev)
+        counts = [torch.zeros_like(n) for _ in range(self.n)]
+        tdist.all_gather(counts, n)
+        counts = [int(c.item()) for c in counts]
+        m, w = max(counts), rows.shape[1]
+        pid = torch.zeros(max(m, 1), dtype=torch.int64, device=dev)
+        pid[:len(ids)] = torch.from_numpy(ids).to(dev)
+        prow = torch.zeros((max(m, 1), w), dtype=torch.float64, device=dev)
+        prow[:len(ids)] = torch.from_numpy(rows).to(dev)
+        gid = [torch.zeros_like(pid) for _ in range(self.n)]
+        grow = [torch.zeros_like(prow) for _ in range(self.n)]
+        tdist.all_gather(gid, pid)
+        tdist.all_gather(grow, prow)
+        return [(gid[q][:counts[q]].cpu().numpy(), grow[q][:counts[q]].cpu().numpy())
+                for q in range(self.n)]
 
     def stats(self):
         n, b = C.c_int64(), C.c_int64()

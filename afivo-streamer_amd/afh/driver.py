@@ -417,20 +417,26 @@ class Simulation:
 
     def _gather_full(self):
         """The whole tree on this rank: every rank's computed boxes (owned,
-        and the replicated levels from rank 0), gathered through the shard's
-        host all-gather, in a new single-rank tree."""
+        and the replicated ones from rank 0) with every cell and face
+        variable, in one numeric all-gather (NativeShard.allgather_rows), in
+        a new single-rank tree."""
         sh = self.shard
         owner = np.asarray(sh.owner)
         t = self._create_tree()
-        for kind, n_var in (("cc", self.n_var_cell), ("fc", self.n_var_face)):
-            get = getattr(self.tree, "get_" + kind)
-            for iv in range(1, n_var + 1):
-                a = get(iv)
-                mine = np.nonzero((owner == sh.rank) | ((owner < 0) & (sh.rank == 0)))[0]
-                parts = sh.allgather((mine, a[mine]))
-                for ids, vals in parts:
-                    a[ids] = vals
-                getattr(t, "put_" + kind)(iv, a)
+        mine = np.nonzero((owner == sh.rank) | ((owner < 0) & (sh.rank == 0)))[0]
+        cc = [self.tree.get_cc(iv) for iv in range(1, self.n_var_cell + 1)]
+        fc = [self.tree.get_fc(iv) for iv in range(1, self.n_var_face + 1)]
+        rows = np.concatenate([a[mine].reshape(len(mine), -1) for a in cc + fc], axis=1)
+        for ids, vals in sh.allgather_rows(mine, rows):
+            off = 0
+            for a in cc + fc:
+                w = int(np.prod(a.shape[1:]))
+                a[ids] = vals[:, off:off + w].reshape((len(ids),) + a.shape[1:])
+                off += w
+        for iv, a in enumerate(cc, 1):
+            t.put_cc(iv, a)
+        for iv, a in enumerate(fc, 1):
+            t.put_fc(iv, a)
         return t
 
     def _adjust_refinement_sharded(self):
@@ -455,8 +461,10 @@ class Simulation:
         lid = np.searchsorted(t.global_ids, mine + 1)
         gf = np.zeros(len(owner), np.int32)
         gm = np.zeros(len(owner), np.uint32)
-        for ids, f, m in sh.allgather((mine, flags[lid], masks[lid])):
-            gf[ids], gm[ids] = f, m
+        # (flags and masks as exact float64 rows of a numeric all-gather)
+        fm = np.stack([flags[lid], masks[lid]], axis=1).astype(np.float64)
+        for ids, v in sh.allgather_rows(mine, fm):
+            gf[ids], gm[ids] = v[:, 0].astype(np.int32), v[:, 1].astype(np.uint32)
         probe = copy.deepcopy(self.af)
         info = probe.adjust_refinement(
             lambda ids: (gf[np.asarray(ids, np.int64) - 1], gm[np.asarray(ids, np.int64) - 1]))

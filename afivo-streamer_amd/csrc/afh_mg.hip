@@ -2322,6 +2322,7 @@ struct afh_mg {
   int prolong_k = 4;           // prolongation cells per column (AFH_PROLONG_K=2|4|8)
   int rstr_bs = 256;           // k_rstr_fas_col workgroup size (AFH_RSTR_BS=128|256)
   bool pair_ntl = false;       // AFH_GSRB_PAIR_NTL: non-temporal plane loads in the 64^3 pair
+  int pair_ks_leaf = 1;      // AFH_PAIR_KS_LEAF (experiment)
   int pair_ks = 4;           // AFH_GSRB_PAIR_KS: k chunks on 64..255-box levels (NC = 64;
                              // 4 whole-box chunks, 44 quarter-box tiles x 4, 0 tiles)
   int wave_cells = CS_WAVE_CELLS;  // AFH_CS_WAVE_CELLS
@@ -2574,6 +2575,7 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
   AFH_HIP(hipMalloc(&mg->d_cycles, sizeof(int)));
   if (const char *env = getenv("AFH_GSRB_PAIR_BOX")) mg->pair_box = atoi(env) != 0;
   if (const char *env = getenv("AFH_GSRB_PAIR_KS")) mg->pair_ks = atoi(env);
+  if (const char *env = getenv("AFH_PAIR_KS_LEAF")) mg->pair_ks_leaf = atoi(env);
   if (const char *env = getenv("AFH_GRAD_NT")) mg->grad_nt = atoi(env) != 0;
   if (const char *env = getenv("AFH_CS_WAVE_CELLS")) mg->wave_cells = atoi(env);
   if (fused_nc_ok(t->nc) && mg->fused_min > 0) {
@@ -2771,6 +2773,15 @@ static void launch_pair(afh_mg *mg, int lvl, const double *src, double *dst,
         if (mg->pair_ntl)
           return launch_pair2<NC, NC, 1, 0, true, true, true, 1, true>(mg, lvl, src, dst, cf,
                                                                        inv_c1, e0, e1);
+        // AFH_PAIR_KS_LEAF=2|4: the k-split march on the leaf level too
+        // (workgroups of one box start at different planes: an experiment
+        // on the placement sensitivity of the lock-stepped plane streams)
+        if (mg->pair_ks_leaf == 2)
+          return launch_pair2<NC, NC, 1, 0, true, true, true, 2>(mg, lvl, src, dst, cf,
+                                                                 inv_c1, e0, e1);
+        if (mg->pair_ks_leaf == 4)
+          return launch_pair2<NC, NC, 1, 0, true, true, true, 4>(mg, lvl, src, dst, cf,
+                                                                 inv_c1, e0, e1);
         return launch_pair2<NC, NC, 1>(mg, lvl, src, dst, cf, inv_c1, e0, e1);
       }
       return launch_pair2<NC, NC, 2>(mg, lvl, src, dst, cf, inv_c1, e0, e1);

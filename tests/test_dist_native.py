@@ -289,3 +289,41 @@ def test_native_rccl_single_rank_bitwise():
     finally:
         lib.call("dist_rccl_comm_destroy", comm)
     _compare(ref, [sh], [out])
+
+
+def _rows_worker(rank, world, port, outdir):
+    import os
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # the RCCL transport's path of NativeShard.allgather_rows (torch
+        # collectives; gloo here, device tensors under nccl)
+        sh = type("S", (), {"transport": capi.DIST_RCCL, "n": world, "rank": rank})()
+        ids = np.arange(rank + 1) * 10 + rank
+        rows = np.arange((rank + 1) * 3, dtype=np.float64).reshape(rank + 1, 3) + 0.5 * rank
+        got = NativeShard.allgather_rows(sh, ids, rows)
+        np.savez(os.path.join(outdir, "r%d.npz" % rank),
+                 **{"ids%d" % q: g[0] for q, g in enumerate(got)},
+                 **{"rows%d" % q: g[1] for q, g in enumerate(got)})
+    finally:
+        dist.destroy_process_group()
+
+
+def test_allgather_rows_gloo(tmp_path):
+    """The numeric all-gather a sharded regrid gathers boxes with (ragged
+    counts, padded rows): every rank receives every rank's ids and rows
+    exactly."""
+    import torch.multiprocessing as mp
+    from test_dist import _free_port
+    world = 3
+    mp.start_processes(_rows_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world,
+                       start_method="spawn", join=True)
+    for r in range(world):
+        d = np.load(tmp_path / ("r%d.npz" % r))
+        for q in range(world):
+            np.testing.assert_array_equal(d["ids%d" % q], np.arange(q + 1) * 10 + q)
+            np.testing.assert_array_equal(
+                d["rows%d" % q],
+                np.arange((q + 1) * 3, dtype=np.float64).reshape(q + 1, 3) + 0.5 * q)
