@@ -326,6 +326,7 @@ class Simulation:
         self.faces_from_phi = self._faces_from_phi_ok and self.lsf is None
         if self.faces_from_phi:
             self.fluid.set_field_source(self.i_phi, -1.0)
+            self.mg.set_gradient_output(self.i_efld, -1.0)
         if self.lsf is not None:
             self._set_electrode()
 

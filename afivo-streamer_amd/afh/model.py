@@ -344,6 +344,12 @@ class Multigrid:
         self.lib.call("mg_coarse_iterations", self.h, C.byref(n))
         return n.value
 
+    def set_gradient_output(self, i_norm, fac=-1.0):
+        """afh_mg_set_gradient_output: the final residual pass of every later
+        V-cycle also stores |E| into i_norm (0: off); compute_phi_gradient(0,
+        fac, i_norm) after it then launches nothing."""
+        self.lib.call("mg_set_gradient_output", self.h, int(i_norm), float(fac))
+
     def compute_phi_gradient(self, i_fc, fac=-1.0, i_norm=0):
         self.lib.call("mg_compute_phi_gradient", self.h, i_fc, fac, i_norm)
 

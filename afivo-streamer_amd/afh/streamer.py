@@ -148,6 +148,10 @@ class StreamerCase:
         """The flux evaluates the face field from phi (afh_fluid_set_field_source)
         and field_from_potential stores |E| only (not with an electrode)."""
         self.fluid.set_field_source(IV["phi"] if on else 0, -1.0)
+        if self.lib.has("mg_set_gradient_output"):
+            # |E| from the V-cycle's residual pass (field_from_potential's
+            # gradient then has nothing left to do)
+            self.mg.set_gradient_output(IV["efld"] if on else 0, -1.0)
         self._faces_from_phi = on
 
     def set_voltage(self, voltage):

@@ -986,13 +986,17 @@ __device__ __forceinline__ double apply7(const double *x, size_t c, size_t sj,
 // shard slots (af_tree_maxabs_cc(i_tmp) of field_compute). Each thread
 // takes a column of K cells along k: the z neighbours are shared and all
 // loads are issued before the arithmetic (more bytes in flight per wave).
-template <bool MAX, int K>
+// GRAD (afh_mg_set_gradient_output): the same phi values also give |E| of
+// field_from_potential's gradient (k_gradient_t's expressions, fac / dr of
+// the box), stored in nrm -- one read of phi for both.
+template <bool MAX, int K, bool GRAD = false>
 __global__ void __launch_bounds__(256)
     k_residual(const double *__restrict__ phi, const double *__restrict__ rhs,
                double *__restrict__ tmp, const int32_t *__restrict__ ids,
                int nc, size_t bsz, Coef cf0, unsigned long long *red,
                const Coef *__restrict__ cft = nullptr,
-               const afh_box_meta *__restrict__ meta = nullptr) {
+               const afh_box_meta *__restrict__ meta = nullptr,
+               double *__restrict__ nrm = nullptr, double gfac = 0.0) {
   // cft: boxes of several levels, the level's coefficients from the table
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   double mx = 0.0;
@@ -1026,6 +1030,19 @@ __global__ void __launch_bounds__(256)
       const double v = r[q] - a;
       st_nt<AFH_NT_MG>(tmp + (o + c0 + q * sk), v);
       mx = fmax(mx, fabs(v));
+    }
+    if constexpr (GRAD) {
+      const afh_box_meta &mb = meta[id - 1];
+      const double gx = gfac / mb.dr[0], gy = gfac / mb.dr[1], gz = gfac / mb.dr[2];
+#pragma unroll
+      for (int q = 0; q < K; q++) {
+        const double pv = z[q + 1];
+        const double fxl = gx * (pv - xm[q]), fxh = gx * (xp[q] - pv);
+        const double fyl = gy * (pv - ym[q]), fyh = gy * (yp[q] - pv);
+        const double fzl = gz * (pv - z[q]), fzh = gz * (z[q + 2] - pv);
+        const double a = fxl + fxh, b = fyl + fyh, c = fzl + fzh;
+        st_nt<AFH_NT_MG>(nrm + (o + c0 + q * sk), 0.5 * sqrt(a * a + b * b + c * c));
+      }
     }
   }
   if (MAX) block_max_to_shard(mx, red);
@@ -2363,6 +2380,12 @@ struct afh_mg {
   int h_v1_id = 0;
   uint64_t v1_gen = 1, csd_v_gen = 0, csd_meth_gen = UINT64_MAX;
   double *d_csd_ainv = nullptr, *d_csd_g = nullptr;
+  // afh_mg_set_gradient_output: |E| (cc variable grad_iv, factor grad_fac)
+  // from the final residual pass; the generations of phi and |E| it left
+  // them at (afh_mg_compute_phi_gradient then skips its own pass)
+  int grad_iv = 0;
+  double grad_fac = -1.0;
+  uint64_t grad_phi_gen = UINT64_MAX, grad_norm_gen = UINT64_MAX;
 };
 
 // (diag, 1/diag) of the folded operator per MG level and boundary class, in
@@ -3518,6 +3541,12 @@ int32_t afh_mg_fas_fmg(afh_mg *mg, int32_t set_residual, int32_t have_guess) {
 // residual on every box of levels 1..max_lvl; with max_out also the leaf
 // max|residual| (reduction slot 3, as afh_tree_maxabs_cc), in the same pass
 // (device work only; residual_fetch reads the maximum)
+// the final residual pass of a V-cycle also writes |E| (afh_mg_set_gradient_
+// output): V-cycles over the whole tree, constant stencils only
+static bool grad_fused(const afh_mg *mg, int max_lvl) {
+  return mg->grad_iv > 0 && !mg->any_var && max_lvl == mg->t->nlvl;
+}
+
 static int32_t residual_levels(afh_mg *mg, int max_lvl, bool max_out) {
   afh_tree *t = mg->t;
   const int nc = t->nc, n3 = nc * nc * nc;
@@ -3547,14 +3576,22 @@ static int32_t residual_levels(afh_mg *mg, int max_lvl, bool max_out) {
         const int rk = mg->res_k ? mg->res_k : nc >= 32 ? 8 : 4;
         const int kc = nc % rk == 0 ? rk : nc % 4 == 0 ? 4 : 2;
         const dim3 grid((n3 / kc + 255) / 256, n);
-        auto kern = mx ? (kc == 8 ? k_residual<true, 8> : kc == 4 ? k_residual<true, 4>
+        const bool gr = grad_fused(mg, max_lvl);
+        auto kern = gr ? (mx ? (kc == 8 ? k_residual<true, 8, true>
+                                        : kc == 4 ? k_residual<true, 4, true>
+                                                  : k_residual<true, 2, true>)
+                             : (kc == 8 ? k_residual<false, 8, true>
+                                        : kc == 4 ? k_residual<false, 4, true>
+                                                  : k_residual<false, 2, true>))
+                  : mx ? (kc == 8 ? k_residual<true, 8> : kc == 4 ? k_residual<true, 4>
                                                                   : k_residual<true, 2>)
                        : (kc == 8 ? k_residual<false, 8> : kc == 4 ? k_residual<false, 4>
                                                                    : k_residual<false, 2>);
         hipLaunchKernelGGL(kern, grid, dim3(256), 0, t->stream,
                            t->ccv(mg->d.i_phi), t->ccv(mg->d.i_rhs),
                            t->ccv(mg->d.i_tmp), L.at(lvl), nc, t->bsz, cf, red,
-                           one ? mg->d_lvl_c : nullptr, one ? t->d_boxes : nullptr);
+                           one ? mg->d_lvl_c : nullptr, (one || gr) ? t->d_boxes : nullptr,
+                           gr ? t->ccv(mg->grad_iv) : nullptr, mg->grad_fac);
         AFH_LAUNCH_CHECK("k_residual");
       }
       const int nv = mg->any_var ? Lv.n(lvl) : 0;
@@ -3660,6 +3697,11 @@ static int32_t vcycle_impl(afh_mg *mg, int32_t set_residual, int32_t hl, bool ma
   if (!done && (e = vcycle_body(mg, set_residual, max_lvl, max_out, top_stale))) return e;
   // the up leg filled every level's ghost cells (corners on the last fill)
   if (max_lvl == t->nlvl) mg->phi_gc_gen = t->gen[mg->d.i_phi];
+  if (set_residual && grad_fused(mg, max_lvl)) {  // |E| of this phi is stored
+    t->touch(mg->grad_iv);
+    mg->grad_phi_gen = t->gen[mg->d.i_phi];
+    mg->grad_norm_gen = t->gen[mg->grad_iv];
+  }
   return max_out && max_res ? residual_fetch(mg, max_res) : AFH_OK;
 }
 
@@ -3676,6 +3718,17 @@ int32_t afh_mg_fas_vcycle_maxres(afh_mg *mg, int32_t hl, double *max_res) {
 
 int32_t afh_mg_fas_vcycle_fold(afh_mg *mg, int32_t hl) {
   return vcycle_impl(mg, 1, hl, true, nullptr);
+}
+
+int32_t afh_mg_set_gradient_output(afh_mg *mg, int32_t i_norm, double fac) {
+  if (!mg) return set_error(AFH_ERR_ARG, "null mg");
+  AFH_LIVE(mg->t, "afh_mg_set_gradient_output");
+  if (i_norm < 0 || i_norm > mg->t->nvc) return set_error(AFH_ERR_ARG, "bad variable index");
+  mg->grad_iv = i_norm;
+  mg->grad_fac = fac;
+  mg->grad_phi_gen = mg->grad_norm_gen = UINT64_MAX;
+  mg->t->meth_gen++;  // captured V-cycles baked the residual kernel in
+  return AFH_OK;
 }
 
 int32_t afh_mg_coarse_iterations(afh_mg *mg, int32_t *n) {
@@ -3705,6 +3758,11 @@ int32_t afh_mg_compute_phi_gradient(afh_mg *mg, int32_t i_fc, double fac,
   // afh_fluid_set_field_source); electrode boxes need the face field
   if (i_fc == 0 && (i_norm == 0 || mg->any_lsf))
     return set_error(AFH_ERR_ARG, "i_fc = 0 needs i_norm and no electrode boxes");
+  // the last V-cycle's residual pass stored this |E| of this phi already
+  // (afh_mg_set_gradient_output; neither changed since)
+  if (i_fc == 0 && i_norm == mg->grad_iv && fac == mg->grad_fac && !mg->any_var &&
+      mg->grad_phi_gen == t->gen[mg->d.i_phi] && mg->grad_norm_gen == t->gen[i_norm])
+    return AFH_OK;
   const int nc = t->nc, n3 = nc * nc * nc;
   const int ntot = t->ids.off[t->nlvl];
   double *nrm = i_norm > 0 ? t->ccv(i_norm) : nullptr;

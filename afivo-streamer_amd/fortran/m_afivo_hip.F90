@@ -351,6 +351,16 @@ module m_afivo_hip
        integer(c_int32_t)              :: afh_mg_coarse_iterations
      end function afh_mg_coarse_iterations
 
+     !> field_from_potential's |E| folded into the V-cycle's residual pass
+     function afh_mg_set_gradient_output(mg, i_norm, fac) &
+          bind(C, name=afh_pfx//"mg_set_gradient_output")
+       import
+       type(c_ptr), value        :: mg
+       integer(c_int32_t), value :: i_norm
+       real(c_double), value     :: fac
+       integer(c_int32_t)        :: afh_mg_set_gradient_output
+     end function afh_mg_set_gradient_output
+
      !> af_tree_sum_cc (m_af_utils.f90:966-1026)
      function afh_tree_sum_cc(t, iv, power, out) bind(C, name=afh_pfx//"tree_sum_cc")
        import

@@ -326,6 +326,14 @@ int32_t afh_mg_coarse_iterations(afh_mg *mg, int32_t *n);
  * (afh_fluid_set_field_source), which never reads a stored face field. */
 int32_t afh_mg_compute_phi_gradient(afh_mg *mg, int32_t i_fc, double fac,
                                     int32_t i_norm);
+/* field_from_potential's |E| folded into the V-cycle: from now on the final
+ * residual pass of a V-cycle over the whole tree (set_residual) also stores
+ * |E| = afh_mg_compute_phi_gradient's norm with factor fac into cc variable
+ * i_norm (0: off), from the same reads of phi; a following
+ * afh_mg_compute_phi_gradient(mg, 0, fac, i_norm) then finds it current (phi
+ * and |E| unchanged since) and launches nothing. Same values bitwise.
+ * Constant-stencil trees only (with electrode stencils it stays off). */
+int32_t afh_mg_set_gradient_output(afh_mg *mg, int32_t i_norm, double fac);
 
 /* Electrode (level-set) boxes: the stencils mg_set_operators_tree stores on
  * the boxes an electrode surface crosses (mg_set_operators_lvl,

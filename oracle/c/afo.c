@@ -1490,6 +1490,16 @@ int32_t afo_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
   return AFH_OK;
 }
 
+/* afh_mg_set_gradient_output: the library folds |E| into the V-cycle's
+ * residual pass; the values are those of mg_compute_phi_gradient, which the
+ * oracle computes in full every time */
+int32_t afo_mg_set_gradient_output(afh_mg *mg, int32_t i_norm, double fac) {
+  (void)fac;
+  if (!mg || i_norm < 0 || i_norm > mg->t->nvc)
+    return fail(AFH_ERR_ARG, "afo_mg_set_gradient_output: bad argument");
+  return AFH_OK;
+}
+
 int32_t afo_mg_coarse_iterations(afh_mg *mg, int32_t *n) {
   if (!mg || !n) return fail(AFH_ERR_ARG, "afo_mg_coarse_iterations: null");
   *n = mg->cs_iters;

@@ -54,6 +54,9 @@ def rules(topo):
         (r"k_gsrb_pair", 24, "ids", None),
         (r"k_gsrb_v", 16, "ids", None),
         (r"k_gsrb\(", 16, "ids", split),
+        # with |E| folded in (afh_mg_set_gradient_output): + 8 B written
+        (r"k_residual<true, \d, true", 32, "leaves", None),
+        (r"k_residual<false, \d, true", 32, "parents", None),
         (r"k_residual<true", 24, "leaves", None),
         (r"k_residual<false", 24, "parents", None),
         (r"k_rstr_fas", 18, "ids", None),

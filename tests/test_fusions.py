@@ -148,3 +148,30 @@ def test_s3_compiled_network_bitwise(monkeypatch):
     assert outs[0][0] == outs[1][0]
     for x, y in zip(outs[0][1], outs[1][1]):
         assert np.array_equal(x, y)
+
+
+@pytest.mark.parametrize("config", ["s1", "c32"])
+def test_gradient_folded_into_residual_bitwise(config, monkeypatch):
+    """afh_mg_set_gradient_output: |E| from the V-cycle's final residual pass
+    (one read of phi for both) against field_from_potential's own gradient
+    pass -- the field solve and four unit steps (16^3 and 32^3 boxes: residual
+    columns of 4 and 8), every variable bitwise."""
+    import bench
+    from afh import capi
+    from afh.streamer import IV
+    monkeypatch.setitem(bench.CONFIGS, "c32", (32, (32, 32, 32), 3, (8e-3, 8e-3, 8e-3)))
+    outs = []
+    for fold in (True, False):
+        c = bench.build_case(capi.hip_library(), config, 0, 0)
+        c.fuse_rhs(True, ghosts=False)
+        c.faces_from_phi(True)
+        if not fold:
+            c.mg.set_gradient_output(0)
+        out = {"res0": c.field_compute(0, n_vcycles=2)}
+        for k in range(4):
+            out["step%d" % k] = bench.unit_step(c, 1e-13, k)
+        for v in ("e", "pos", "neg", "phi", "efld", "rhs", "tmp"):
+            out[v] = c.tree.get_cc(IV[v])
+        c.tree.close()
+        outs.append(out)
+    _same(outs[0], outs[1])
