@@ -3242,9 +3242,10 @@ static int32_t prepare_cs_direct(afh_mg *mg) {
   afh_tree *t = mg->t;
   mg->csd_ok = false;
   // a level 1 of one 8^3 box with an electrode stencil and six physical
-  // faces, no sharding hook (the oracle's solve_coarse_direct: the same test)
+  // faces (the oracle's solve_coarse_direct: the same test); a sharded tree
+  // too -- level 1 is replicated, every rank solves it alike, no collective
   if (!mg->csd_on || t->nc != AFH_CSD_NC || !(mg->any_var && mg->lvl_var[0]) ||
-      t->ids.n(1) != 1 || t->hook || mg->h_v1_id != t->h_ids[0][0] ||
+      t->ids.n(1) != 1 || mg->h_v1_id != t->h_ids[0][0] ||
       !mg->h_vp[mg->h_v1_id - 1])
     return AFH_OK;
   for (int q = 0; q < 6; q++)

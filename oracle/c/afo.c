@@ -1253,9 +1253,9 @@ static struct {
 static int solve_coarse_direct(afh_mg *mg) {
   afh_tree *t = mg->t;
   const char *env = getenv("AFH_CS_ELEC_DIRECT");
-  if ((env && !atoi(env)) || t->nc != AFH_CSD_NC || LVL_N(t, ids, 1) != 1 ||
-      t->hook)
-    return 1;
+  /* (a sharded tree too: level 1 is replicated, every rank solves it alike
+     without a collective) */
+  if ((env && !atoi(env)) || t->nc != AFH_CSD_NC || LVL_N(t, ids, 1) != 1) return 1;
   const int id = LVL_AT(t, ids, 1, 0);
   const afh_box_meta *m = B(t, id);
   if (!mg->vst[id - 1]) return 1;
