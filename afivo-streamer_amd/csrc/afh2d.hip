@@ -870,6 +870,13 @@ struct afh_tree {
   std::vector<int> auto_vars;  // tree%cc_auto_vars (afh_set_cc_prolong order)
   std::vector<double> lvl_dr;  // 2 per level
   double *d_boxred = nullptr;  // per-leaf (value, cell) of afh_tree_sum_cc / reduce_loc
+  // kernel timing (afh_profile_enable/read, as in libafivo_hip): HIP events
+  // around every launch of one kernel class on the tree's stream
+  int prof_class = 0;
+  std::vector<hipEvent_t> ev_pool;
+  size_t ev_used = 0;
+  double prof_bytes = 0;
+  int64_t prof_launches = 0;
   double *ccv(int iv) const { return cc + (size_t)(iv - 1) * nb * bsz; }
   double *fcv(int ivf) const { return fc + (size_t)(ivf - 1) * nb * fsz; }
   Bc4 bc4(int iv) const {
@@ -917,6 +924,23 @@ static int32_t upload_list(LevelList &L, const std::vector<std::vector<int32_t>>
     H2(hipMemcpy(L.d, flat.data(), flat.size() * sizeof(int32_t), hipMemcpyHostToDevice));
   }
   return AFH_OK;
+}
+
+static void prof_mark(afh_tree *t, int kc) {
+  if (t->prof_class != kc) return;
+  if (t->ev_used == t->ev_pool.size()) {
+    hipEvent_t e;
+    hipEventCreate(&e);
+    t->ev_pool.push_back(e);
+  }
+  hipEventRecord(t->ev_pool[t->ev_used++], t->stream);
+}
+
+static void prof_end(afh_tree *t, int kc, double bytes) {
+  if (t->prof_class != kc) return;
+  prof_mark(t, kc);
+  t->prof_bytes += bytes;
+  t->prof_launches++;
 }
 
 static void free_list(LevelList &L) {
@@ -1060,6 +1084,7 @@ int32_t afh_tree_destroy(afh_tree *t) {
     free_list(*L);
   hipFree(t->d_boxes), hipFree(t->cc), hipFree(t->fc), hipFree(t->gc2);
   hipFree(t->red), hipFree(t->red_out), hipHostFree(t->h_red), hipFree(t->d_boxred);
+  for (hipEvent_t e : t->ev_pool) hipEventDestroy(e);
   hipStreamDestroy(t->stream);
   delete t;
   return AFH_OK;
@@ -1068,6 +1093,38 @@ int32_t afh_tree_destroy(afh_tree *t) {
 int32_t afh_tree_sync(afh_tree *t) {
   if (!t) return set_error(AFH_ERR_ARG, "afh_tree_sync: null");
   H2(hipStreamSynchronize(t->stream));
+  return AFH_OK;
+}
+
+int32_t afh_profile_enable(afh_tree *t, int32_t kclass) {
+  if (!t) return set_error(AFH_ERR_ARG, "afh_profile_enable: null");
+  if (kclass != 0 && kclass != AFH_PROF_GSRB && kclass != AFH_PROF_FLUX)
+    return set_error(AFH_ERR_UNSUPPORTED, "afh_profile_enable: class %d (2-D: GSRB, FLUX)",
+                     kclass);
+  H2(hipStreamSynchronize(t->stream));
+  t->prof_class = kclass;
+  t->ev_used = 0;
+  t->prof_bytes = 0;
+  t->prof_launches = 0;
+  return AFH_OK;
+}
+
+int32_t afh_profile_read(afh_tree *t, double *total_ms, int64_t *launches, double *bytes) {
+  if (!t || !total_ms || !launches || !bytes)
+    return set_error(AFH_ERR_ARG, "afh_profile_read: null argument");
+  H2(hipStreamSynchronize(t->stream));
+  double ms = 0;
+  for (size_t q = 0; q + 1 < t->ev_used; q += 2) {
+    float e = 0;
+    H2(hipEventElapsedTime(&e, t->ev_pool[q], t->ev_pool[q + 1]));
+    ms += e;
+  }
+  *total_ms = ms;
+  *launches = t->prof_launches;
+  *bytes = t->prof_bytes;
+  t->ev_used = 0;
+  t->prof_bytes = 0;
+  t->prof_launches = 0;
   return AFH_OK;
 }
 
@@ -1297,10 +1354,12 @@ static int32_t gsrb_boxes(afh_mg *mg, int lvl, bool up) {
   const int nc_ = up ? mg->d.n_cycle_up : mg->d.n_cycle_down;
   for (int s = 1; s <= 2 * nc_; s++) {
     if (n) {
+      prof_mark(t, AFH_PROF_GSRB);
       hipLaunchKernelGGL(k2_gsrb, grid2(t->nc * t->nc / 2, n), dim3(NT), 0, t->stream,
                          t->ccv(mg->d.i_phi), t->ccv(mg->d.i_rhs), t->ids.at(lvl), t->nc,
                          t->bsz, mg->lvl_c[lvl - 1], s);
       H2_LAUNCH("k2_gsrb");
+      prof_end(t, AFH_PROF_GSRB, 16.0 * t->nc * t->nc * n);
     }
     if (int32_t e = gc_lvl(t, lvl, mg->d.i_phi, up && s == 2 * nc_)) return e;
   }
@@ -1600,9 +1659,12 @@ static int32_t flux_tree(afh_fluid *f, int32_t s_deriv, double *dt_lim) {
     hipLaunchKernelGGL(k2_gc2, grid2(4 * nc, n), dim3(NT), 0, t->stream, t->ccv(iv), t->gc2,
                        t->d_boxes, t->leaves.at(l), nc, t->bsz, t->bc4(iv));
     H2_LAUNCH("k2_gc2");
+    prof_mark(t, AFH_PROF_FLUX);
     hipLaunchKernelGGL(k2_flux, grid2(nc * nc, n), dim3(NT), 0, t->stream, A,
                        t->leaves.at(l), t->d_boxes, nc, t->bsz, t->fsz, t->red);
     H2_LAUNCH("k2_flux");
+    // ne and |E| read, two face fields read and two fluxes written per cell
+    prof_end(t, AFH_PROF_FLUX, 48.0 * nc * nc * n);
   }
   // af_consistent_fluxes
   const int ntask = t->cflux.off.back();

@@ -351,7 +351,10 @@ def main():
     import ctypes as C
     graphs = args.graphs == "on" or (args.graphs == "auto" and args.config != "s1-64")
     if two_d:
-        graphs = False  # (no graphs, no kernel timing in the 2-D build)
+        # no graphs in the 2-D build; its smoother is the split half sweep
+        # k2_gsrb on every level (one thread per cell pair of 8^2 boxes)
+        graphs = False
+        lib.call("profile_enable", case.tree.h, capi.PROF_GSRB)
     elif not graphs:
         lib.call("profile_enable", case.tree.h, capi.PROF_GSRB_PAIR)
     barrier()
@@ -371,10 +374,11 @@ def main():
             unit_step(case, dt, args.warmup + args.steps + k)
         case.tree.sync()
     ms, nl, by = C.c_double(), C.c_int64(), C.c_double()
-    if not two_d:
-        lib.call("profile_read", case.tree.h, C.byref(ms), C.byref(nl), C.byref(by))
+    lib.call("profile_read", case.tree.h, C.byref(ms), C.byref(nl), C.byref(by))
     kname = ("k_gsrb_pair2<%d,%d>" % (CONFIGS[args.config][0], CONFIGS[args.config][0])
              if CONFIGS[args.config][0] > 16 else "k_gsrb_pair_box<%d>" % CONFIGS[args.config][0])
+    if two_d:
+        kname = "k2_gsrb (half sweep, all levels, 16 B/cell)"
     if nl.value == 0 and not two_d:
         # no level runs the fused pair (too few boxes per level, or
         # electrode stencils): the split half-sweep k_gsrb is the smoother
@@ -440,9 +444,8 @@ def main():
             "vcycles_per_s": args.steps / elapsed,
         }
         if two_d:
-            # the 2-D build has no kernel timing (afivo_hip_2d.h): no roofline
-            # line; the config is BASELINE's plumbing case, not a bench target
-            out["roofline"] = None
+            # BASELINE's CPU-runnable case, not the headline: its roofline
+            # line is the half-sweep smoother over all levels
             out["config"]["coarse_solve"] = "direct"
             out["config"]["ndim"] = 2
             out["config"]["fused_rhs"] = False
@@ -455,7 +458,10 @@ def main():
             out["config"]["chemistry"] = "air_chemistry_v2 (9 species, 25 reactions)"
             out["config"]["electrode"] = ("grounded rod (0.5,0.5,0)-(0.5,0.5,0.15) L, r = 1 mm, "
                                           "%d electrode boxes" % len(sim.electrode_ids))
-            out["config"]["coarse_solve"] = "electrode level 1: red-black GS to stationarity"
+            out["config"]["coarse_solve"] = (
+                "electrode level 1: red-black GS to stationarity"
+                if os.environ.get("AFH_CS_ELEC_DIRECT", "1") == "0" else
+                "electrode level 1: dense inverse product (one 8^3 box)")
         if args.config == "s5":
             out["config"]["chemistry"] = "sprite_chemistry_v0 (10 species, 12 reactions)"
             out["config"]["gas_density"] = "variable (3d_sprite m_user: 2.5e25 exp(-z/7.2 km))"
