@@ -115,7 +115,7 @@ def main(path, k_steps, out, topo_path):
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     upd = [i for i, r in enumerate(rows)
-           if "k_update" in r["Kernel_Name"] or "k_fe_lds" in r["Kernel_Name"]]
+           if re.search(r"k2?_update|k_fe_lds", r["Kernel_Name"])]
     # a step ends with the update of every leaf level (consecutive launches)
     ends = [i for n, i in enumerate(upd) if n + 1 == len(upd) or upd[n + 1] != i + 1]
     start = ends[-(k_steps + 1)] + 1
