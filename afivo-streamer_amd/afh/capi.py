@@ -157,6 +157,7 @@ SIGNATURES = {
     "tree_fetch_reduced": (i32, [_VP, i32, P_i32, P_f64]),
     "mg_fas_fmg": (i32, [_VP, i32, i32]),
     "mg_coarse_iterations": (i32, [_VP, P_i32]),
+    "mg_graph_stats": (i32, [_VP, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
     "mg_set_gradient_output": (i32, [_VP, i32, f64]),
     "mg_compute_phi_gradient": (i32, [_VP, i32, f64, i32]),
     "mg_set_box_stencil": (i32, [_VP, i32, P_f64, P_f64]),

@@ -285,15 +285,30 @@ class Simulation:
         self.tree = self.fluid = self.mg = None
         self.helm = []
         self.shard = None  # shard_over
+        # V-cycles replayed from hipGraphs (of them segmented, sharded), over
+        # every multigrid this run has bound (afh_mg_graph_stats)
+        self.graph_replays = [0, 0]
 
     # ------------------------------------------------------------- device
     def _capacity(self):
         return max(64, int(self.capacity_factor * self.af.highest_id))
 
+    def graph_stats(self):
+        """(V-cycles replayed from hipGraphs, of them segmented) over this
+        run's multigrids, the bound ones included."""
+        tot = list(self.graph_replays)
+        for m in [self.mg] + self.helm:
+            if m is not None and m.lib.has("mg_graph_stats"):
+                tot = [a + b for a, b in zip(tot, m.graph_stats())]
+        return tuple(tot)
+
     def _bind(self, tree):
         """Multigrid and fluid state bound to a (new) device tree."""
         for m in [self.mg] + self.helm:
             if m is not None:
+                if m.lib.has("mg_graph_stats"):
+                    self.graph_replays = [a + b for a, b in
+                                          zip(self.graph_replays, m.graph_stats())]
                 m.close()
         if self.fluid is not None:
             self.fluid.close()

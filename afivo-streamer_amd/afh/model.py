@@ -344,6 +344,12 @@ class Multigrid:
         self.lib.call("mg_coarse_iterations", self.h, C.byref(n))
         return n.value
 
+    def graph_stats(self):
+        """(V-cycles replayed from hipGraphs, of them segmented) -- diagnostics."""
+        r, s = C.c_int64(), C.c_int64()
+        self.lib.call("mg_graph_stats", self.h, C.byref(r), C.byref(s))
+        return r.value, s.value
+
     def set_gradient_output(self, i_norm, fac=-1.0):
         """afh_mg_set_gradient_output: the final residual pass of every later
         V-cycle also stores |E| into i_norm (0: off); compute_phi_gradient(0,

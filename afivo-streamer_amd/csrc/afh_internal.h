@@ -16,6 +16,7 @@
 #include <string.h>
 
 #include <string>
+#include <array>
 #include <vector>
 
 #include "../../include/afivo_hip.h"
@@ -116,6 +117,16 @@ struct afh_tree {
   // all-reduced on the device, on the ordered keys in place (stream-ordered,
   // no host round trip); the one fetch afterwards reads the global value
   int32_t (*dev_reduce)(void *ctx, int kind, unsigned long long *keys, int n) = nullptr;
+  // segmented capture of a sharded V-cycle (afh_mg.hip vcycle_graph): while
+  // seg_rec is set the stream is capturing, and call_hook ends the capture at
+  // each exchange, records the exchange and begins the next segment; a
+  // reduction (host values) marks the recording unusable
+  struct SegRec {
+    std::vector<hipGraph_t> graphs;
+    std::vector<std::array<int32_t, 3>> ops;  // (kind, level, iv) after graphs[k]
+    bool bad = false;
+  };
+  SegRec *seg_rec = nullptr;
   // shared by every multigrid on the tree (one stream: the image is only
   // live inside one fused pair); freed with the last of them
   double *alt = nullptr;

@@ -2366,9 +2366,24 @@ struct afh_mg {
     hipGraphExec_t exec = nullptr;
     uint64_t meth_gen = 0;
     bool warm = false;  // one eager call done (tables built, spare image allocated)
+    // sharded (a hook): the V-cycle as segments between its exchanges, each
+    // replayed as a graph, the exchange (ops[k]) run after segs[k]
+    std::vector<hipGraphExec_t> segs;
+    std::vector<std::array<int32_t, 3>> ops;
+    bool eager_only = false;  // the recording met a reduction
+    void release() {
+      if (exec) hipGraphExecDestroy(exec);
+      for (hipGraphExec_t s : segs)
+        if (s) hipGraphExecDestroy(s);
+      exec = nullptr;
+      segs.clear();
+      ops.clear();
+    }
   };
   std::map<int, Graph> graphs;
   bool use_graphs = true;
+  bool seg_graphs = true;  // sharded V-cycles as segment graphs (AFH_SEG_GRAPHS=0: eager)
+  int64_t n_replays = 0, n_seg_replays = 0;  // afh_mg_graph_stats
   std::vector<char> lvl_var;  // level has variable-stencil boxes
   LevelList ids_c, ids_v, leaves_c, leaves_v, parents_c, parents_v, lsf_leaves;
   double *cs_old = nullptr;   // level-1 electrode solve: previous phi
@@ -2577,6 +2592,7 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
   if (const char *env = getenv("AFH_GSRB_PAIR_P3")) mg->pair_p3 = atoi(env) != 0;
   if (const char *env = getenv("AFH_GSRB_PAIR_SP")) mg->pair_sp = atoi(env) != 0;
   if (const char *env = getenv("AFH_GRAPHS")) mg->use_graphs = atoi(env) != 0;
+  if (const char *env = getenv("AFH_SEG_GRAPHS")) mg->seg_graphs = atoi(env) != 0;
   if (const char *env = getenv("AFH_RSTR_COL")) mg->rstr_col = atoi(env) != 0;
   if (const char *env = getenv("AFH_RSTR_K")) {
     const int k = atoi(env);
@@ -2648,8 +2664,7 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
 int32_t afh_mg_destroy(afh_mg *mg) {
   if (!mg) return AFH_OK;
   hipStreamSynchronize(mg->t->stream);
-  for (auto &g : mg->graphs)
-    if (g.second.exec) hipGraphExecDestroy(g.second.exec);
+  for (auto &g : mg->graphs) g.second.release();
   for (int q = 0; q < mg->P.n_mg; q++) {
     hipFree(mg->P.u[q]);
     hipFree(mg->P.f[q]);
@@ -2827,8 +2842,7 @@ static bool fused_level(const afh_mg *mg, int lvl) {
 static int32_t prepare_var(afh_mg *mg) {
   if (!mg->var_dirty) return AFH_OK;
   mg->var_dirty = false;
-  for (auto &g : mg->graphs)
-    if (g.second.exec) hipGraphExecDestroy(g.second.exec);
+  for (auto &g : mg->graphs) g.second.release();
   mg->graphs.clear();
   afh_tree *t = mg->t;
   const int nb = t->nb, nl = t->nlvl;
@@ -3633,17 +3647,68 @@ static int32_t vcycle_body(afh_mg *mg, int32_t set_residual, int max_lvl, bool m
   return AFH_OK;
 }
 
-// Replays a captured V-cycle when it can: no sharding hook (its collectives
-// run on the host), no kernel timing, no electrode coarse solve (it reads
-// the device every pair). The first call of a variant runs eagerly (tables,
-// spare image); a change of boundary conditions drops the graph.
+// A sharded V-cycle (a hook) as segments: the device work between two
+// exchanges is captured as one graph, the exchange itself (host-driven:
+// pack, the transport, unpack) is recorded and run between the replays of
+// its neighbouring segments. Every rank records and replays the same
+// sequence of exchanges, in the eager order.
+static int32_t vcycle_segments(afh_mg *mg, afh_mg::Graph &g, int32_t set_residual,
+                               int max_lvl, bool max_out, bool top_stale, bool &done) {
+  afh_tree *t = mg->t;
+  if (g.segs.empty()) {
+    afh_tree::SegRec rec;
+    AFH_HIP(hipStreamBeginCapture(t->stream, hipStreamCaptureModeThreadLocal));
+    t->seg_rec = &rec;
+    int32_t e = vcycle_body(mg, set_residual, max_lvl, max_out, top_stale);
+    t->seg_rec = nullptr;
+    hipGraph_t last = nullptr;
+    const hipError_t ce = hipStreamEndCapture(t->stream, &last);
+    if (ce == hipSuccess) rec.graphs.push_back(last);
+    if (!e && ce != hipSuccess) e = set_error(AFH_ERR_DEVICE, "segment capture failed");
+    for (size_t k = 0; k < rec.graphs.size() && !e; k++) {
+      size_t nn = 0;
+      hipGraphExec_t x = nullptr;
+      if (hipGraphGetNodes(rec.graphs[k], nullptr, &nn) != hipSuccess ||
+          (nn && hipGraphInstantiate(&x, rec.graphs[k], nullptr, nullptr, 0) != hipSuccess))
+        e = set_error(AFH_ERR_DEVICE, "segment instantiation failed");
+      g.segs.push_back(x);  // (an empty segment replays as nothing)
+    }
+    for (hipGraph_t gr : rec.graphs)
+      if (gr) hipGraphDestroy(gr);
+    if (rec.bad) {
+      // (a reduction on the way: this variant stays eager)
+      g.release();
+      g.eager_only = true;
+      return AFH_OK;
+    }
+    if (e) {
+      g.release();
+      return e;
+    }
+    g.ops = rec.ops;
+  }
+  for (size_t k = 0; k < g.segs.size(); k++) {
+    if (g.segs[k]) AFH_HIP(hipGraphLaunch(g.segs[k], t->stream));
+    if (k < g.ops.size())
+      if (int32_t e = call_hook(t, g.ops[k][0], g.ops[k][1], g.ops[k][2])) return e;
+  }
+  mg->n_replays++, mg->n_seg_replays++;
+  done = true;
+  return AFH_OK;
+}
+
+// Replays a captured V-cycle when it can: no kernel timing, no electrode
+// coarse solve that reads the device every pair; sharded, as segments
+// between the exchanges (vcycle_segments). The first call of a variant runs
+// eagerly (tables, spare image); a change of boundary conditions drops the
+// graph.
 static int32_t vcycle_graph(afh_mg *mg, int32_t set_residual, int max_lvl, bool max_out,
                             bool top_stale, bool &done) {
   afh_tree *t = mg->t;
   done = false;
   // (the multi-launch coarse cycles with a stopping rule read the device
   // every cycle too)
-  if (!mg->use_graphs || t->hook || t->prof_class ||
+  if (!mg->use_graphs || (t->hook && !mg->seg_graphs) || t->prof_class ||
       (mg->any_var && mg->lvl_var[0] && !cs_electrode_fused(mg) && !mg->csd_ok) ||
       (mg->d.coarse_mode == AFH_COARSE_CYCLES && mg->d.coarse_tol > 0 && mg->small_from > 0))
     return AFH_OK;
@@ -3653,7 +3718,7 @@ static int32_t vcycle_graph(afh_mg *mg, int32_t set_residual, int max_lvl, bool 
   if (g.meth_gen != t->meth_gen) {
     // new boundary values or types since the warm call / capture: run
     // eagerly once more (rebuilds the coarse-solve tables outside capture)
-    if (g.exec) hipGraphExecDestroy(g.exec);
+    g.release();
     g = afh_mg::Graph();
     g.meth_gen = t->meth_gen;
   }
@@ -3661,6 +3726,8 @@ static int32_t vcycle_graph(afh_mg *mg, int32_t set_residual, int max_lvl, bool 
     g.warm = true;
     return AFH_OK;  // this call runs eagerly
   }
+  if (g.eager_only) return AFH_OK;
+  if (t->hook) return vcycle_segments(mg, g, set_residual, max_lvl, max_out, top_stale, done);
   if (!g.exec) {
     hipGraph_t graph;
     AFH_HIP(hipStreamBeginCapture(t->stream, hipStreamCaptureModeThreadLocal));
@@ -3676,6 +3743,7 @@ static int32_t vcycle_graph(afh_mg *mg, int32_t set_residual, int max_lvl, bool 
     AFH_HIP(ie);
   }
   AFH_HIP(hipGraphLaunch(g.exec, t->stream));
+  mg->n_replays++;
   done = true;
   return AFH_OK;
 }
@@ -3729,6 +3797,13 @@ int32_t afh_mg_set_gradient_output(afh_mg *mg, int32_t i_norm, double fac) {
   mg->grad_fac = fac;
   mg->grad_phi_gen = mg->grad_norm_gen = UINT64_MAX;
   mg->t->meth_gen++;  // captured V-cycles baked the residual kernel in
+  return AFH_OK;
+}
+
+int32_t afh_mg_graph_stats(afh_mg *mg, int64_t *replays, int64_t *segmented) {
+  if (!mg || !replays || !segmented) return set_error(AFH_ERR_ARG, "afh_mg_graph_stats: null");
+  *replays = mg->n_replays;
+  *segmented = mg->n_seg_replays;
   return AFH_OK;
 }
 

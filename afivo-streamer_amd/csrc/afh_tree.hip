@@ -373,6 +373,20 @@ __global__ void __launch_bounds__(NC * NC)
 
 int32_t call_hook(afh_tree *t, int kind, int lvl, int iv, double *vals, int n) {
   if (!t->hook) return AFH_OK;
+  if (afh_tree::SegRec *r = t->seg_rec) {
+    // inside a segmented capture: the exchange runs between the segments'
+    // replays; a reduction needs host values now and cannot be deferred
+    if (vals || kind == AFH_HOOK_MAX || kind == AFH_HOOK_MIN || kind == AFH_HOOK_SUM) {
+      r->bad = true;
+      return set_error(AFH_ERR_STATE, "reduction inside a captured V-cycle");
+    }
+    hipGraph_t g = nullptr;
+    AFH_HIP(hipStreamEndCapture(t->stream, &g));
+    r->graphs.push_back(g);
+    r->ops.push_back({kind, lvl, iv});
+    AFH_HIP(hipStreamBeginCapture(t->stream, hipStreamCaptureModeThreadLocal));
+    return AFH_OK;
+  }
   int32_t e = t->hook(t->hook_ctx, kind, lvl, iv, vals, n);
   if (e) return set_error(AFH_ERR_STATE, "sharding hook %d failed (%d)", kind, e);
   return AFH_OK;
@@ -1310,6 +1324,7 @@ int32_t afh_tree_set_hook(afh_tree *t, afh_hook_fn fn, void *ctx) {
   t->hook = fn;
   t->hook_ctx = ctx;
   t->dev_reduce = nullptr;  // the library's RCCL transport sets its own
+  t->meth_gen++;            // captured V-cycles recorded the old exchanges
   return AFH_OK;
 }
 

@@ -351,6 +351,15 @@ module m_afivo_hip
        integer(c_int32_t)              :: afh_mg_coarse_iterations
      end function afh_mg_coarse_iterations
 
+     !> diagnostics: V-cycles replayed from graphs (of them, segmented)
+     function afh_mg_graph_stats(mg, replays, segmented) &
+          bind(C, name=afh_pfx//"mg_graph_stats")
+       import
+       type(c_ptr), value              :: mg
+       integer(c_int64_t), intent(out) :: replays, segmented
+       integer(c_int32_t)              :: afh_mg_graph_stats
+     end function afh_mg_graph_stats
+
      !> field_from_potential's |E| folded into the V-cycle's residual pass
      function afh_mg_set_gradient_output(mg, i_norm, fac) &
           bind(C, name=afh_pfx//"mg_set_gradient_output")

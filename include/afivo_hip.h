@@ -320,6 +320,11 @@ int32_t afh_mg_fas_fmg(afh_mg *mg, int32_t set_residual, int32_t have_guess);
  * cycles of the last coarse solve (AFH_COARSE_CYCLES; 0 for the direct
  * solve); synchronises the tree's stream. */
 int32_t afh_mg_coarse_iterations(afh_mg *mg, int32_t *n);
+/* Diagnostics (no reference counterpart): V-cycles replayed from captured
+ * hipGraphs so far, and of those the sharded ones replayed as segments
+ * between their exchanges (AFH_GRAPHS, AFH_SEG_GRAPHS). The oracle replays
+ * nothing and returns 0, 0. */
+int32_t afh_mg_graph_stats(afh_mg *mg, int64_t *replays, int64_t *segmented);
 /* mg_compute_phi_gradient (m_af_multigrid.f90:1837-1879) incl. the norm.
  * i_fc = 0 computes the norm i_norm only, on trees without electrode boxes:
  * for a fluid whose flux takes the face field from the potential

@@ -1500,6 +1500,12 @@ int32_t afo_mg_set_gradient_output(afh_mg *mg, int32_t i_norm, double fac) {
   return AFH_OK;
 }
 
+int32_t afo_mg_graph_stats(afh_mg *mg, int64_t *replays, int64_t *segmented) {
+  if (!mg || !replays || !segmented) return fail(AFH_ERR_ARG, "afo_mg_graph_stats: null");
+  *replays = *segmented = 0;
+  return AFH_OK;
+}
+
 int32_t afo_mg_coarse_iterations(afh_mg *mg, int32_t *n) {
   if (!mg || !n) return fail(AFH_ERR_ARG, "afo_mg_coarse_iterations: null");
   *n = mg->cs_iters;

@@ -64,6 +64,7 @@ int32_t afo_mg_fas_vcycle_fold(afh_mg *mg, int32_t highest_lvl);
 int32_t afo_tree_fetch_reduced(afh_tree *t, int32_t n, const int32_t *slots, double *out);
 int32_t afo_mg_fas_fmg(afh_mg *mg, int32_t set_residual, int32_t have_guess);
 int32_t afo_mg_coarse_iterations(afh_mg *mg, int32_t *n);
+int32_t afo_mg_graph_stats(afh_mg *mg, int64_t *replays, int64_t *segmented);
 int32_t afo_mg_set_gradient_output(afh_mg *mg, int32_t i_norm, double fac);
 int32_t afo_mg_compute_phi_gradient(afh_mg *mg, int32_t i_fc, double fac,
                                     int32_t i_norm);

@@ -124,6 +124,11 @@ def _run_loop(lib, world, n_steps, device=-1):
 
     with ThreadPoolExecutor(world) as ex:
         outs = list(ex.map(loop, clones))
+    if device >= 0:
+        # the sharded V-cycles ran as segment graphs between their exchanges
+        # (afh_mg.hip vcycle_segments), all ranks alike
+        segs = [sim.graph_stats()[1] for sim in clones]
+        assert segs[0] > 0 and len(set(segs)) == 1, segs
     for _ in range(n_steps):
         base.step()
     ref = np.array(base.log)
