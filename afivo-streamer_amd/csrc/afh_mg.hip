@@ -975,6 +975,206 @@ __global__ void __launch_bounds__(RbBox<NC>::NT)
   }
 }
 
+// correct_children's prolongation (stencil_prolong_248 add, k_prolong's
+// expressions) for a small box in one workgroup, followed by the face fill
+// the level's ghost fill would do, pushed like k_gsrb_pair_box<PUSH>: a
+// same-level neighbour's ghost layer facing this box gets the corrected
+// boundary cells, a physical / refinement face of this box its
+// gc_face_nocopy value from the corrected interior and the coarse data.
+// Edges and corners are left as they were: the up leg's pairs do not read
+// them, and its last pair is followed by k_gc_corners. Replaces k_prolong +
+// k_gc_box on levels smoothed by pushing pairs (one launch instead of two;
+// the fill no longer re-reads the box). Same values.
+template <int NC>
+__global__ void __launch_bounds__(RbBox<NC>::NT)
+    k_prolong_box(double *__restrict__ phi, const double *__restrict__ tmp,
+                  const afh_box_meta *__restrict__ meta, const int32_t *__restrict__ ids,
+                  size_t bsz, GcArgs ga) {
+  constexpr int NG = NC + 2, NT = RbBox<NC>::NT, HN = NC / 2;
+  __shared__ double P[NG * NG * NG];
+  const int tid = threadIdx.x;
+  const int id = ids[xcd_swizzle(blockIdx.x, gridDim.x)];
+  const afh_box_meta &m = meta[id - 1];
+  double *y = phi + (size_t)(id - 1) * bsz;
+  const double *pp = tmp + (size_t)(m.parent - 1) * bsz;
+  const int o0 = ((m.ix[0] - 1) & 1) * HN, o1 = ((m.ix[1] - 1) & 1) * HN,
+            o2 = ((m.ix[2] - 1) & 1) * HN;
+  for (int e = tid; e < NC * NC * NC; e += NT) {
+    const int i = e % NC + 1, j = (e / NC) % NC + 1, k = e / (NC * NC) + 1;
+    const int i1 = o0 + ((i + 1) >> 1), i2 = i1 + 1 - 2 * (i & 1);
+    const int j1 = o1 + ((j + 1) >> 1), j2 = j1 + 1 - 2 * (j & 1);
+    const int k1 = o2 + ((k + 1) >> 1), k2 = k1 + 1 - 2 * (k & 1);
+    const int c = ix3(NG, i, j, k);
+    const double *a = pp + ix3(NG, 0, 0, k1), *b = pp + ix3(NG, 0, 0, k2);
+    const double v = y[c] + (27 / 64.0) * a[j1 * NG + i1] + (9 / 64.0) * a[j1 * NG + i2] +
+                     (9 / 64.0) * a[j2 * NG + i1] + (3 / 64.0) * a[j2 * NG + i2] +
+                     (9 / 64.0) * b[j1 * NG + i1] + (3 / 64.0) * b[j1 * NG + i2] +
+                     (3 / 64.0) * b[j2 * NG + i1] + (1 / 64.0) * b[j2 * NG + i2];
+    P[c] = v;
+    y[c] = v;
+  }
+  __syncthreads();
+  for (int u = tid; u < 6 * NC * NC; u += NT) {
+    const int nb = u / (NC * NC) + 1, w = u % (NC * NC);
+    const int a = w % NC + 1, b = w / NC + 1;
+    const int d = (nb - 1) >> 1;
+    const bool low = ((nb - 1) & 1) == 0;
+    const int ta = (d == 0) ? 1 : 0, tb = (d == 2) ? 1 : 2;
+    int p[3];
+    p[ta] = a;
+    p[tb] = b;
+    p[d] = low ? 0 : NC + 1;
+    const int nid = m.neighbors[nb - 1];
+    if (nid > 0) {
+      int q1[3] = {p[0], p[1], p[2]}, q[3] = {p[0], p[1], p[2]};
+      q1[d] = low ? 1 : NC;
+      q[d] = low ? NC + 1 : 0;  // the neighbour's ghost facing this box
+      phi[(size_t)(nid - 1) * bsz + ix3(NG, q[0], q[1], q[2])] = P[ix3(NG, q1[0], q1[1], q1[2])];
+    } else {
+      y[ix3(NG, p[0], p[1], p[2])] = gc_face_nocopy_k(
+          phi, meta, m, nb, nid, m.dr[d], p, a, b, NC, bsz, ga.bc[nb - 1], ga.rb,
+          [&](const int *q) { return P[ix3(NG, q[0], q[1], q[2])]; });
+    }
+  }
+}
+
+__device__ __forceinline__ double apply7(const double *x, size_t c, size_t sj, size_t sk,
+                                         const Coef &cf);
+
+// update_coarse's restriction (k_rstr_fas's expressions) of one small fine
+// box into its octant of the parent, followed by the parent's face ghosts
+// that octant determines, pushed like k_prolong_box: the parent's
+// same-level neighbour's ghost layer facing it gets the new boundary values,
+// a physical / refinement face of the parent its gc_face_nocopy value (from
+// x1, x2 of the octant and the coarser level's data, which this launch does
+// not change). Each octant covers three of the parent's faces; every face
+// ghost the level fill would rewrite after the restriction has exactly one
+// writer. Ghosts facing unchanged boxes keep their values: only valid when
+// the level's ghosts were filled since phi last changed (the caller checks).
+template <int NC>
+__global__ void __launch_bounds__(NC >= 16 ? 512 : 64)
+    k_rstr_box(double *__restrict__ phi, const double *__restrict__ rhs,
+               double *__restrict__ tmp, const afh_box_meta *__restrict__ meta,
+               const int32_t *__restrict__ ids, size_t bsz, Coef cf, GcArgs ga) {
+  constexpr int NG = NC + 2, HN = NC / 2, NT = NC >= 16 ? 512 : 64;
+  constexpr int SJ = NG, SK = NG * NG;
+  __shared__ double Q[HN * HN * HN];
+  const int tid = threadIdx.x;
+  const int id = ids[xcd_swizzle(blockIdx.x, gridDim.x)];
+  const afh_box_meta &m = meta[id - 1];
+  const afh_box_meta &pm = meta[m.parent - 1];
+  const double *x = phi + (size_t)(id - 1) * bsz, *r = rhs + (size_t)(id - 1) * bsz;
+  const int o[3] = {((m.ix[0] - 1) & 1) * HN, ((m.ix[1] - 1) & 1) * HN,
+                    ((m.ix[2] - 1) & 1) * HN};
+  const size_t pb = (size_t)(m.parent - 1) * bsz;
+  for (int e = tid; e < HN * HN * HN; e += NT) {
+    const int i = e % HN + 1, j = (e / HN) % HN + 1, k = e / (HN * HN) + 1;
+    const int fi = 2 * i - 1, fj = 2 * j - 1, fk = 2 * k - 1;
+    const size_t cs[8] = {ix3(NG, fi, fj, fk),         ix3(NG, fi + 1, fj, fk),
+                          ix3(NG, fi, fj + 1, fk),     ix3(NG, fi + 1, fj + 1, fk),
+                          ix3(NG, fi, fj, fk + 1),     ix3(NG, fi + 1, fj, fk + 1),
+                          ix3(NG, fi, fj + 1, fk + 1), ix3(NG, fi + 1, fj + 1, fk + 1)};
+    double sr = r[cs[0]] - apply7(x, cs[0], SJ, SK, cf);
+    double sp = x[cs[0]];
+#pragma unroll
+    for (int q = 1; q < 8; q++) {
+      sr += r[cs[q]] - apply7(x, cs[q], SJ, SK, cf);
+      sp += x[cs[q]];
+    }
+    const size_t po = pb + ix3(NG, o[0] + i, o[1] + j, o[2] + k);
+    tmp[po] = 0.125 * sr;
+    phi[po] = 0.125 * sp;
+    Q[e] = 0.125 * sp;
+  }
+  __syncthreads();
+  auto own = [&](const int *q) {
+    return Q[((q[2] - o[2] - 1) * HN + (q[1] - o[1] - 1)) * HN + (q[0] - o[0] - 1)];
+  };
+  for (int u = tid; u < 3 * HN * HN; u += NT) {
+    const int d = u / (HN * HN), w = u % (HN * HN);
+    const bool low = o[d] == 0;
+    const int nb = 2 * d + (low ? 1 : 2);
+    const int ta = (d == 0) ? 1 : 0, tb = (d == 2) ? 1 : 2;
+    int p[3];
+    p[ta] = o[ta] + w % HN + 1;
+    p[tb] = o[tb] + w / HN + 1;
+    p[d] = low ? 0 : NC + 1;
+    const int nid = pm.neighbors[nb - 1];
+    if (nid > 0) {
+      int q1[3] = {p[0], p[1], p[2]}, q[3] = {p[0], p[1], p[2]};
+      q1[d] = low ? 1 : NC;
+      q[d] = low ? NC + 1 : 0;  // the neighbour's ghost facing the parent
+      phi[(size_t)(nid - 1) * bsz + ix3(NG, q[0], q[1], q[2])] = own(q1);
+    } else {
+      phi[pb + ix3(NG, p[0], p[1], p[2])] =
+          gc_face_nocopy_k(phi, meta, pm, nb, nid, pm.dr[d], p, p[ta], p[tb], NC, bsz,
+                           ga.bc[nb - 1], ga.rb, own);
+    }
+  }
+}
+
+// the edges and corners of a box from its face ghosts and its diagonal
+// neighbours (k_gc_corners' loops, for the calling workgroup's box; the
+// edge table arithmetically: edge n runs along n / 4, its sign bits r = n % 4
+// over the two other dimensions in increasing order)
+__device__ __forceinline__ void box_edges_corners(double *__restrict__ v,
+                                                  const afh_box_meta &m, int id, int nc,
+                                                  size_t bsz, int tid, int nt) {
+  const int ng = nc + 2;
+  double *c = v + (size_t)(id - 1) * bsz;
+  for (int e = tid; e < 12 * nc; e += nt) {
+    const int n = e / nc, pos = e % nc + 1;
+    const int dim = n >> 2, r = n & 3;
+    const int oa = dim == 0 ? 1 : 0, ob = dim == 2 ? 1 : 2;
+    int dir[3] = {0, 0, 0}, x[3];
+    dir[oa] = (r & 1) ? 1 : -1;
+    dir[ob] = (r & 2) ? 1 : -1;
+    x[dim] = pos;
+    x[oa] = (r & 1) ? nc + 1 : 0;
+    x[ob] = (r & 2) ? nc + 1 : 0;
+    const int nb_id = m.neighbor_mat[(dir[0] + 1) + 3 * (dir[1] + 1) + 9 * (dir[2] + 1)];
+    if (nb_id > 0) {
+      c[ix3(ng, x[0], x[1], x[2])] =
+          v[(size_t)(nb_id - 1) * bsz +
+            ix3(ng, x[0] - dir[0] * nc, x[1] - dir[1] * nc, x[2] - dir[2] * nc)];
+    } else {
+      const int o1 = (dim + 1) % 3, o2 = (dim + 2) % 3;
+      int di[3];
+      for (int q = 0; q < 3; q++) di[q] = 1 - 2 * (x[q] & 1);
+      di[dim] = 0;
+      int ia[3] = {x[0], x[1], x[2]}, ib[3] = {x[0], x[1], x[2]};
+      ia[o1] += di[o1];
+      ib[o2] += di[o2];
+      c[ix3(ng, x[0], x[1], x[2])] = c[ix3(ng, ia[0], ia[1], ia[2])] +
+                                     c[ix3(ng, ib[0], ib[1], ib[2])] -
+                                     c[ix3(ng, x[0] + di[0], x[1] + di[1], x[2] + di[2])];
+    }
+  }
+  __syncthreads();
+  if (tid < 8) {
+    int dnb[3], x[3];
+    for (int q = 0; q < 3; q++) {
+      const int b = (tid >> q) & 1;
+      dnb[q] = 2 * b - 1;
+      x[q] = b * (nc + 1);
+    }
+    const int nb_id = m.neighbor_mat[(dnb[0] + 1) + 3 * (dnb[1] + 1) + 9 * (dnb[2] + 1)];
+    if (nb_id > 0) {
+      c[ix3(ng, x[0], x[1], x[2])] =
+          v[(size_t)(nb_id - 1) * bsz +
+            ix3(ng, x[0] - dnb[0] * nc, x[1] - dnb[1] * nc, x[2] - dnb[2] * nc)];
+    } else {
+      int di[3];
+      for (int q = 0; q < 3; q++) di[q] = 1 - 2 * (x[q] & 1);
+      c[ix3(ng, x[0], x[1], x[2])] = c[ix3(ng, x[0], x[1] + di[1], x[2] + di[2])] +
+                                     c[ix3(ng, x[0] + di[0], x[1], x[2] + di[2])] +
+                                     c[ix3(ng, x[0] + di[0], x[1] + di[1], x[2])] -
+                                     2 * c[ix3(ng, x[0] + di[0], x[1] + di[1], x[2] + di[2])];
+    }
+  }
+  __syncthreads();
+}
+
 __device__ __forceinline__ double apply7(const double *x, size_t c, size_t sj,
                                          size_t sk, const Coef &cf) {
   return cf.c[0] * x[c] + cf.c[1] * x[c - 1] + cf.c[2] * x[c + 1] +
@@ -1181,6 +1381,32 @@ __global__ void k_parent_rhs(const double *__restrict__ phi,
     rv = apply7(phi + o, c, ng, (size_t)ng * ng, cf);
   rhs[o + c] = rv + tmp[o + c];
   tmp[o + c] = phi[o + c];
+}
+
+// After k_rstr_box (faces pushed): a parent box's edges and corners, then
+// its k_parent_rhs, in one workgroup per parent. The level's leaves keep
+// their edges and corners until the up leg's k_gc_corners: nothing reads
+// them before (the 7-point operators, the restriction and the pushing pairs
+// read faces only; the prolongation reads parents' edges, set here).
+template <int NT>
+__global__ void __launch_bounds__(NT)
+    k_parent_rhs_box(double *__restrict__ phi, double *__restrict__ rhs,
+                     double *__restrict__ tmp, const afh_box_meta *__restrict__ meta,
+                     const int32_t *__restrict__ ids, int nc, size_t bsz, Coef cf) {
+  const int id = ids[xcd_swizzle(blockIdx.x, gridDim.x)];
+  box_edges_corners(phi, meta[id - 1], id, nc, bsz, threadIdx.x, NT);
+  const int ng = nc + 2;
+  const size_t o = (size_t)(id - 1) * bsz;
+  for (int t = threadIdx.x; t < ng * ng * ng; t += NT) {
+    int i, j, k;
+    cell3g(t, ng, i, j, k);
+    const size_t c = ix3(ng, i, j, k);
+    double rv = rhs[o + c];
+    if (i >= 1 && i <= nc && j >= 1 && j <= nc && k >= 1 && k <= nc)
+      rv = apply7(phi + o, c, ng, (size_t)ng * ng, cf);
+    rhs[o + c] = rv + tmp[o + c];
+    tmp[o + c] = phi[o + c];
+  }
 }
 
 // ------------------------------------------------------------ electrode boxes
@@ -2318,6 +2544,7 @@ struct afh_mg {
   // box's ghost column), so a V-cycle that finds them stale (after a regrid,
   // an upload, a copy) smooths its top level with split half-sweeps first
   uint64_t phi_gc_gen = UINT64_MAX;
+  uint64_t phi_gc_meth = UINT64_MAX;  // t->meth_gen of that fill (boundary values)
   bool cs_fused = true;       // AFH_CS_FUSED=0: the electrode coarse solve launch per pair
   int *cs_iters = nullptr;     // pairs the last k_cs_electrode took
   // level-1 cycles of the last coarse solve (afh_mg_coarse_iterations): on
@@ -2327,6 +2554,8 @@ struct afh_mg {
   bool cs_direct_small = true;
   int cs_ds_cells = CS_DS_CELLS;  // AFH_CS_DS_CELLS: its size limit (at most CS_SMALL_CELLS)
   bool pair_push = true;  // AFH_PAIR_PUSH: the small-box pair fills the faces
+  bool prolong_push = true;  // AFH_PROLONG_PUSH: so does the small-box correction
+  bool rstr_push = true;     // AFH_RSTR_PUSH: and the small-box restriction
   int *d_cycles = nullptr;
   int cycles_host = 0;
   bool cycles_on_dev = false;
@@ -2610,6 +2839,8 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
   if (const char *env = getenv("AFH_CS_DS_CELLS"))
     mg->cs_ds_cells = std::min(CS_SMALL_CELLS, std::max(0, atoi(env)));
   if (const char *env = getenv("AFH_PAIR_PUSH")) mg->pair_push = atoi(env) != 0;
+  if (const char *env = getenv("AFH_PROLONG_PUSH")) mg->prolong_push = atoi(env) != 0;
+  if (const char *env = getenv("AFH_RSTR_PUSH")) mg->rstr_push = atoi(env) != 0;
   AFH_HIP(hipMalloc(&mg->cs_iters, sizeof(int)));
   AFH_HIP(hipMalloc(&mg->d_cycles, sizeof(int)));
   if (const char *env = getenv("AFH_GSRB_PAIR_BOX")) mg->pair_box = atoi(env) != 0;
@@ -2977,11 +3208,53 @@ static int32_t gsrb_boxes(afh_mg *mg, int lvl, bool up, bool stale_ghosts = fals
 }
 
 
-static int32_t update_coarse(afh_mg *mg, int lvl) {
+// The restriction into level lvl-1 pushes that level's faces (k_rstr_box)
+// and the parents' edges and corners come with their rhs (k_parent_rhs_box),
+// instead of a full level fill between the two: small boxes smoothed by the
+// pushing pair, no electrode stencils, and ghost cells valid on entry (the
+// fill keeps the ghosts facing boxes the restriction does not change).
+// AFH_RSTR_PUSH=0: off.
+static bool rstr_push(const afh_mg *mg, int lvl, bool ghosts_valid) {
+  const int nc = mg->t->nc;
+  return ghosts_valid && mg->rstr_push && pair_push(mg) && !mg->any_var &&
+         (nc == 4 || nc == 8 || nc == 16) && fused_level(mg, lvl - 1);
+}
+
+static int32_t update_coarse(afh_mg *mg, int lvl, bool ghosts_valid = false) {
   afh_tree *t = mg->t;
   const int nc = t->nc, hn = nc / 2;
   const LevelList &L = cst(mg, t->ids, mg->ids_c);
   const int nid = L.n(lvl);
+  if (rstr_push(mg, lvl, ghosts_valid)) {
+    const GcArgs ga = t->gc_args(mg->d.i_phi);
+    const Coef cf = mg->lvl_c[lvl - 1];
+    double *phi = t->ccv(mg->d.i_phi), *rhs = t->ccv(mg->d.i_rhs), *tmp = t->ccv(mg->d.i_tmp);
+    if (nid) {
+      if (nc == 4)
+        hipLaunchKernelGGL(k_rstr_box<4>, dim3(nid), dim3(64), 0, t->stream, phi, rhs, tmp,
+                           t->d_boxes, L.at(lvl), t->bsz, cf, ga);
+      else if (nc == 8)
+        hipLaunchKernelGGL(k_rstr_box<8>, dim3(nid), dim3(64), 0, t->stream, phi, rhs, tmp,
+                           t->d_boxes, L.at(lvl), t->bsz, cf, ga);
+      else
+        hipLaunchKernelGGL(k_rstr_box<16>, dim3(nid), dim3(512), 0, t->stream, phi, rhs, tmp,
+                           t->d_boxes, L.at(lvl), t->bsz, cf, ga);
+      AFH_LAUNCH_CHECK("k_rstr_box");
+    }
+    const int np = t->parents.n(lvl - 1);
+    if (np) {
+      if (nc == 16)
+        hipLaunchKernelGGL(k_parent_rhs_box<512>, dim3(np), dim3(512), 0, t->stream, phi, rhs,
+                           tmp, t->d_boxes, t->parents.at(lvl - 1), nc, t->bsz,
+                           mg->lvl_c[lvl - 2]);
+      else
+        hipLaunchKernelGGL(k_parent_rhs_box<256>, dim3(np), dim3(256), 0, t->stream, phi,
+                           rhs, tmp, t->d_boxes, t->parents.at(lvl - 1), nc, t->bsz,
+                           mg->lvl_c[lvl - 2]);
+      AFH_LAUNCH_CHECK("k_parent_rhs_box");
+    }
+    return AFH_OK;
+  }
   if (nid) {
     // column length (AFH_RSTR_K = 2, 4 or 8): a column reads 2K + 2 fine
     // planes for 2K; each doubling of K halves that excess at twice the
@@ -3045,6 +3318,14 @@ static int32_t update_coarse(afh_mg *mg, int lvl) {
   return AFH_OK;
 }
 
+// the correction of level lvl also fills its faces (k_prolong_box): small
+// boxes whose level the pushing pair smooths next (AFH_PROLONG_PUSH=0: off)
+static bool prolong_push(const afh_mg *mg, int lvl) {
+  const int nc = mg->t->nc;
+  return mg->prolong_push && pair_push(mg) && (nc == 4 || nc == 8 || nc == 16) &&
+         fused_level(mg, lvl);
+}
+
 static int32_t correct_children(afh_mg *mg, int lvl) {
   afh_tree *t = mg->t;
   const int np = t->parents.n(lvl - 1), nc = t->nc;
@@ -3055,7 +3336,22 @@ static int32_t correct_children(afh_mg *mg, int lvl) {
     AFH_LAUNCH_CHECK("k_corr_tmp");
   }
   const int nid = t->ids.n(lvl);
-  if (nid) {
+  if (nid && prolong_push(mg, lvl)) {
+    const GcArgs ga = t->gc_args(mg->d.i_phi);
+    if (nc == 4)
+      hipLaunchKernelGGL(k_prolong_box<4>, dim3(nid), dim3(RbBox<4>::NT), 0, t->stream,
+                         t->ccv(mg->d.i_phi), t->ccv(mg->d.i_tmp), t->d_boxes, t->ids.at(lvl),
+                         t->bsz, ga);
+    else if (nc == 8)
+      hipLaunchKernelGGL(k_prolong_box<8>, dim3(nid), dim3(RbBox<8>::NT), 0, t->stream,
+                         t->ccv(mg->d.i_phi), t->ccv(mg->d.i_tmp), t->d_boxes, t->ids.at(lvl),
+                         t->bsz, ga);
+    else
+      hipLaunchKernelGGL(k_prolong_box<16>, dim3(nid), dim3(RbBox<16>::NT), 0, t->stream,
+                         t->ccv(mg->d.i_phi), t->ccv(mg->d.i_tmp), t->d_boxes, t->ids.at(lvl),
+                         t->bsz, ga);
+    AFH_LAUNCH_CHECK("k_prolong_box");
+  } else if (nid) {
     // column length 4; AFH_PROLONG_K=8 where nc allows: the launch is
     // faster (195 against 223 us on S1-64) but the pair after it slower,
     // 13.32 against 12.57-12.60 ms per step (profiles/r03_ab_prolong_k.txt)
@@ -3546,6 +3842,7 @@ int32_t afh_mg_fas_fmg(afh_mg *mg, int32_t set_residual, int32_t have_guess) {
         (e = gc_lvl(t, lvl, i_phi, 1, fused_level(mg, lvl))))
       return e;
     mg->phi_gc_gen = t->gen[i_phi];  // the cycle's top level was just filled
+    mg->phi_gc_meth = t->meth_gen;
     if ((e = afh_mg_fas_vcycle(mg, set_residual && lvl == nl, lvl))) return e;
   }
   return AFH_OK;
@@ -3635,12 +3932,19 @@ static int32_t vcycle_body(afh_mg *mg, int32_t set_residual, int max_lvl, bool m
   int32_t e;
   for (int lvl = max_lvl; lvl >= 2; lvl--) {
     if ((e = gsrb_boxes(mg, lvl, false, top_stale && lvl == max_lvl))) return e;
-    if ((e = update_coarse(mg, lvl))) return e;
+    // (ghosts of the levels below valid: phi and the boundary conditions
+    // unchanged since a V-cycle over the whole tree filled them)
+    if ((e = update_coarse(mg, lvl, !top_stale && max_lvl == t->nlvl &&
+                                        mg->phi_gc_meth == t->meth_gen)))
+      return e;
   }
   if ((e = solve_coarse(mg))) return e;
   for (int lvl = 2; lvl <= max_lvl; lvl++) {
     if ((e = correct_children(mg, lvl))) return e;
-    if ((e = gc_lvl(t, lvl, mg->d.i_phi, 1, fused_level(mg, lvl)))) return e;
+    // (a pushing correction filled the faces, and the pushing pairs read no
+    // edges or corners: k_gc_corners follows the leg's last pair)
+    if (!prolong_push(mg, lvl) && (e = gc_lvl(t, lvl, mg->d.i_phi, 1, fused_level(mg, lvl))))
+      return e;
     if ((e = gsrb_boxes(mg, lvl, true))) return e;
   }
   if (set_residual) return residual_levels(mg, max_lvl, max_out);
@@ -3765,7 +4069,7 @@ static int32_t vcycle_impl(afh_mg *mg, int32_t set_residual, int32_t hl, bool ma
   if ((e = vcycle_graph(mg, set_residual, max_lvl, max_out, top_stale, done))) return e;
   if (!done && (e = vcycle_body(mg, set_residual, max_lvl, max_out, top_stale))) return e;
   // the up leg filled every level's ghost cells (corners on the last fill)
-  if (max_lvl == t->nlvl) mg->phi_gc_gen = t->gen[mg->d.i_phi];
+  if (max_lvl == t->nlvl) mg->phi_gc_gen = t->gen[mg->d.i_phi], mg->phi_gc_meth = t->meth_gen;
   if (set_residual && grad_fused(mg, max_lvl)) {  // |E| of this phi is stored
     t->touch(mg->grad_iv);
     mg->grad_phi_gen = t->gen[mg->d.i_phi];

@@ -15,6 +15,16 @@ read at tree / multigrid / fluid creation):
   every level in one launch (the box's grid spacing / coefficients from its
   level) vs one launch per level -- on the S3 tree (8 leaf levels).
 
+Round 4:
+
+* AFH_PROLONG_PUSH: the small-box correction (k_prolong_box) fills the
+  level's faces itself vs k_prolong + a level fill;
+* AFH_RSTR_PUSH: the small-box restriction pushes the coarse level's faces
+  (k_rstr_box) and the parents' edges, corners and rhs come in one launch
+  (k_parent_rhs_box) vs k_rstr_fas_col + a level fill + k_parent_rhs --
+  on S1, on a tree of 8^3 boxes and on the S3 and S5 AMR trees (refinement
+  boundaries on every level, physical faces).
+
 The fused forms are also what every other GPU test runs (they are the
 defaults); these tests pin them to the unfused forms on full workloads.
 """
@@ -50,7 +60,8 @@ def _same(a, b):
 
 
 @pytest.mark.parametrize("switch", ["AFH_GC_BOX", "AFH_PAIR_PUSH", "AFH_CS_DIRECT_SMALL",
-                                    "AFH_UPD_NET", "AFH_ALL_LVL"])
+                                    "AFH_UPD_NET", "AFH_ALL_LVL", "AFH_PROLONG_PUSH",
+                                    "AFH_RSTR_PUSH"])
 def test_s1_fusion_bitwise(switch, monkeypatch):
     """Config 2 (S1: 512 leaf boxes of 16^3, 4 levels): field solve and four
     unit steps with the fusion on and off."""
@@ -122,6 +133,33 @@ def test_s3_all_level_launches_bitwise(monkeypatch):
         case = bench.DriverCase(bench.build_driver_case(capi.hip_library(), 0, "s3"))
         case.fuse_rhs(True, ghosts=False)
         res = [bench.unit_step(case, 1e-13, k) for k in range(2)]
+        sim = case.sim
+        outs.append((res, [sim.tree.get_cc(iv) for iv in range(1, sim.n_var_cell + 1)]))
+    assert outs[0][0] == outs[1][0]
+    for x, y in zip(outs[0][1], outs[1][1]):
+        assert np.array_equal(x, y, equal_nan=True)
+
+
+@pytest.mark.parametrize("switch", ["AFH_PROLONG_PUSH", "AFH_RSTR_PUSH"])
+def test_push_bitwise_8cubed(switch, monkeypatch):
+    import bench
+    monkeypatch.setitem(bench.CONFIGS, "c8", (8, (8, 8, 8), 3, (8e-3, 8e-3, 8e-3)))
+    _same(_s1(monkeypatch, {switch: "1"}, "c8"), _s1(monkeypatch, {switch: "0"}, "c8"))
+
+
+@pytest.mark.parametrize("config", ["s3", "s5"])
+def test_push_bitwise_amr(config, monkeypatch):
+    """Configs 3 and 5: four unit steps (field solves, flux, update) with
+    the pushing correction and restriction on and both off."""
+    import bench
+    from afh import capi
+    outs = []
+    for v in ("1", "0"):
+        monkeypatch.setenv("AFH_PROLONG_PUSH", v)
+        monkeypatch.setenv("AFH_RSTR_PUSH", v)
+        case = bench.DriverCase(bench.build_driver_case(capi.hip_library(), 0, config))
+        case.fuse_rhs(True, ghosts=False)
+        res = [bench.unit_step(case, 1e-13, k) for k in range(4)]
         sim = case.sim
         outs.append((res, [sim.tree.get_cc(iv) for iv in range(1, sim.n_var_cell + 1)]))
     assert outs[0][0] == outs[1][0]
