@@ -77,6 +77,57 @@ def local_topology(topo, owner, rank):
     return t
 
 
+def compact_topology(topo, present, space):
+    """The topology dict of the boxes `present` (global ids) renumbered by
+    their position in `space` (sorted global ids, a superset shared by
+    several such trees: a box keeps its id in each), plus one unused id
+    (len(space) + 1) that every reference to a box outside `present` points
+    to -- the convention of afh_tree_create_sharded. Ids of `space` not
+    present are holes (level 0)."""
+    space = np.asarray(space, np.int64)
+    present = np.asarray(sorted(set(int(b) for b in present)), np.int64)
+    n = len(space)
+    unused = n + 1
+    nb = int(topo["n_boxes"])
+    g2c = np.zeros(nb + 2, np.int64)
+    pos = np.searchsorted(space, present)
+    g2c[present] = pos + 1
+    inset = np.zeros(nb + 2, bool)
+    inset[present] = True
+
+    def remap(a):
+        a = np.asarray(a, np.int64)
+        out = a.copy()
+        pos_ = a > 0
+        ok = np.zeros_like(pos_)
+        ok[pos_] = inset[a[pos_]]
+        out[pos_ & ok] = g2c[a[pos_ & ok]]
+        out[pos_ & ~ok] = unused
+        return out.astype(np.int32)
+
+    out = {k: v for k, v in topo.items() if not k.startswith(("meta_", "lvl_"))}
+    out["n_boxes"] = np.int32(n + 1)
+    rows = pos  # compact index (0-based) of each present box
+    src = present - 1
+    for key in ("meta_lvl", "meta_ix", "meta_r_min", "meta_dr"):
+        a = np.asarray(topo[key])
+        b = np.zeros((n + 1,) + a.shape[1:], a.dtype)
+        b[rows] = a[src]
+        out[key] = b
+    for key in ("meta_parent", "meta_children", "meta_neighbors", "meta_neighbor_mat"):
+        a = np.asarray(topo[key])
+        b = np.zeros((n + 1,) + a.shape[1:], np.int32)
+        b[rows] = remap(a[src])
+        out[key] = b
+    for l in range(1, int(topo["highest_lvl"]) + 1):
+        for k in ("ids", "leaves", "parents"):
+            key = "lvl_%s_%d" % (k, l)
+            ids = np.asarray(topo[key], np.int64)
+            ids = ids[inset[ids]]
+            out[key] = g2c[ids].astype(np.int32)
+    return out
+
+
 class Partition:
     """Ownership of every box for n_ranks (owner -1: replicated)."""
 
@@ -564,6 +615,17 @@ class NativeShard:
     def local_topology(self):
         return local_topology(self.topo, self.owner, self.rank)
 
+    def local_ids(self, rank):
+        """Global ids of the boxes rank stores (afh_dist_local_ids: owned,
+        replicated, replicas), sorted."""
+        n = C.c_int32()
+        pown = self.owner.ctypes.data_as(capi.P_i32)
+        self.lib.call("dist_local_ids", C.byref(self._desc), pown, rank, None, 0, C.byref(n))
+        out = np.zeros(n.value, np.int32)
+        self.lib.call("dist_local_ids", C.byref(self._desc), pown, rank,
+                      out.ctypes.data_as(capi.P_i32), n.value, C.byref(n))
+        return out
+
     def make_tree(self, lib, topo, n_var_cell, n_var_face, device=-1, box_capacity=0):
         from .model import Tree
         return Tree(lib, self.local_topology(), n_var_cell, n_var_face, device=device,
@@ -627,6 +689,47 @@ class NativeShard:
         tdist.all_gather(grow, prow)
         return [(gid[q][:counts[q]].cpu().numpy(), grow[q][:counts[q]].cpu().numpy())
                 for q in range(self.n)]
+
+    def exchange_rows(self, sends):
+        """Point to point: sends = {rank q: (ids, rows)} (int box ids, float64
+        rows of equal width); returns {rank q: (ids, rows)} received from q.
+        The thread ranks hand over arrays in-process; with the RCCL transport
+        the counts go in one all_gather and the data in batched send/recv of
+        device tensors (only the pairs that exchange rows)."""
+        norm = {}
+        for q, (ids, rows) in sends.items():
+            ids = np.ascontiguousarray(ids, np.int64)
+            norm[q] = (ids, np.ascontiguousarray(rows, np.float64).reshape(len(ids), -1))
+        if self.transport == capi.DIST_LOCAL:
+            every = self.group.allgather(self.rank, norm)
+            return {q: every[q][self.rank] for q in range(self.n)
+                    if q != self.rank and self.rank in every[q]}
+        import torch
+        import torch.distributed as tdist
+        dev = "cuda" if tdist.get_backend() == "nccl" else "cpu"
+        mine = torch.zeros((self.n, 2), dtype=torch.int64, device=dev)
+        for q, (ids, rows) in norm.items():
+            mine[q, 0], mine[q, 1] = len(ids), rows.shape[1]
+        counts = [torch.zeros_like(mine) for _ in range(self.n)]
+        tdist.all_gather(counts, mine)
+        counts = [c.cpu().numpy() for c in counts]
+        ops, bufs = [], {}
+        for q, (ids, rows) in norm.items():
+            if len(ids):
+                ops.append(tdist.P2POp(tdist.isend, torch.from_numpy(ids).to(dev), q))
+                ops.append(tdist.P2POp(tdist.isend, torch.from_numpy(rows).to(dev), q))
+        for q in range(self.n):
+            m, w = counts[q][self.rank]
+            if q != self.rank and m:
+                bi = torch.zeros(int(m), dtype=torch.int64, device=dev)
+                br = torch.zeros((int(m), int(w)), dtype=torch.float64, device=dev)
+                bufs[q] = (bi, br)
+                ops.append(tdist.P2POp(tdist.irecv, bi, q))
+                ops.append(tdist.P2POp(tdist.irecv, br, q))
+        if ops:
+            for r in tdist.batch_isend_irecv(ops):
+                r.wait()
+        return {q: (bi.cpu().numpy(), br.cpu().numpy()) for q, (bi, br) in bufs.items()}
 
     def stats(self):
         n, b = C.c_int64(), C.c_int64()

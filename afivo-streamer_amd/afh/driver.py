@@ -456,11 +456,15 @@ class Simulation:
         return t
 
     def _adjust_refinement_sharded(self):
-        """af_adjust_refinement of a sharded run: the whole tree is gathered
-        on every rank, refined there as a single-rank run does (the same
-        flags, topology and data movement on every rank: bitwise the
-        single-rank run), and sharded again with a fresh partition of the new
-        topology, so the load balance follows the refinement."""
+        """af_adjust_refinement of a sharded run. The refinement flags of
+        the computed boxes are all-gathered and every rank decides the same
+        new topology on a copy of the host tree; the new tree is sharded with
+        a fresh partition (the load balance follows the refinement), and
+        each rank builds its part of it from the boxes it needs
+        (_regrid_rank_local: only boxes whose data live on another rank
+        travel, point to point). AFH_REGRID_GATHER=1: the round-3 form, the
+        whole tree gathered on every rank and regridded as a single rank
+        does. Both are bitwise the single-rank run."""
         import copy
         sh = self.shard
         if not hasattr(sh, "renew"):
@@ -486,6 +490,8 @@ class Simulation:
             lambda ids: (gf[np.asarray(ids, np.int64) - 1], gm[np.asarray(ids, np.int64) - 1]))
         if not (info.n_add or info.n_rm):
             return info
+        if os.environ.get("AFH_REGRID_GATHER", "0") != "1":
+            return self._regrid_rank_local(probe, info)
         full = self._gather_full()
         old = self.tree
         sh.detach()
@@ -494,6 +500,141 @@ class Simulation:
         old.close()
         info = self.adjust_refinement()
         self.shard_over(sh.renew(self.af.topology()))
+        return info
+
+    def _regrid_sources(self, old, new, owner_new, sh_new, rank):
+        """The boxes rank's regrid reads: W, the new tree's boxes it stores
+        closed over what afh_tree_regrid reads to create them (a new box's
+        parent, its same-level neighbours for the ghost fill, the parent's
+        neighbours for refinement-boundary faces, recursively through new
+        boxes), and the old boxes behind W (W's persisting boxes, and the
+        removed children of those that lose them, for auto_restrict)."""
+        nb_old, nb_new = int(old["n_boxes"]), int(new["n_boxes"])
+        lo, ln = np.asarray(old["meta_lvl"]), np.asarray(new["meta_lvl"])
+        xo, xn = np.asarray(old["meta_ix"]), np.asarray(new["meta_ix"])
+        par = np.asarray(new["meta_parent"])
+        nmat = np.asarray(new["meta_neighbor_mat"])
+        cho, chn = np.asarray(old["meta_children"]), np.asarray(new["meta_children"])
+
+        def kept(b):
+            return (b <= nb_old and lo[b - 1] > 0 and lo[b - 1] == ln[b - 1] and
+                    np.array_equal(xo[b - 1], xn[b - 1]))
+
+        W = set(int(b) for b in sh_new.local_ids(rank))
+        stack = [b for b in W if not kept(b)]
+        while stack:
+            b = stack.pop()
+            p = int(par[b - 1])
+            cand = [p] + [int(c) for c in nmat[b - 1]]
+            if p > 0:
+                cand += [int(c) for c in nmat[p - 1]]
+            for c in cand:
+                if 0 < c <= nb_new and ln[c - 1] > 0 and c not in W:
+                    W.add(c)
+                    if not kept(c):
+                        stack.append(c)
+        W_old = set()
+        for b in W:
+            if kept(b):
+                W_old.add(b)
+                if cho[b - 1][0] > 0 and chn[b - 1][0] == 0:
+                    W_old.update(int(c) for c in cho[b - 1])
+        return sorted(W), sorted(W_old)
+
+    def _regrid_rank_local(self, probe, info):
+        """This rank's part of the refined tree without a whole-tree gather:
+        (1) every rank computes, for every rank, the new boxes it stores and
+        the old boxes behind them (_regrid_sources); (2) the old owner of
+        each such box sends it (every cell and face variable, ghost cells
+        included) to the ranks that need it, point to point
+        (NativeShard.exchange_rows; replicated boxes and a rank's own are
+        local); (3) the old boxes go into a small tree of the old topology,
+        afh_tree_regrid moves them onto the new topology -- auto_restrict,
+        the persisting boxes, the new boxes prolonged and their ghost cells
+        filled level by level, exactly the single-rank data movement -- and
+        (4) this rank's boxes of the new partition are copied from it into
+        the new sharded tree. Both small trees number their boxes by one id
+        space (dist.compact_topology), so a persisting box keeps its id."""
+        from .dist import compact_topology
+        sh = self.shard
+        old_topo, new_topo = self.af.topology(), probe.topology()
+        sh2 = sh.renew(new_topo)
+        owner_old = np.asarray(sh.owner)
+        me, n = sh.rank, sh.n
+        src = [self._regrid_sources(old_topo, new_topo, sh2.owner, sh2, q) for q in range(n)]
+        # (2) the rows this rank sends: its owned boxes other ranks read
+        t_old = self.tree
+        cc = [t_old.get_cc_local(iv) for iv in range(1, self.n_var_cell + 1)]
+        fc = [t_old.get_fc_local(iv) for iv in range(1, self.n_var_face + 1)]
+
+        def rows_of(gids):
+            lid = np.array([t_old.local_id(b) for b in gids], np.int64) - 1
+            return np.concatenate([a[lid].reshape(len(lid), -1) for a in cc + fc], axis=1)
+
+        sends = {}
+        for q in range(n):
+            if q == me:
+                continue
+            ids = [b for b in src[q][1] if owner_old[b - 1] == me]
+            if ids:
+                sends[q] = (np.asarray(ids, np.int64), rows_of(ids))
+        got = sh.exchange_rows(sends)
+        self.regrid_rows_received = sum(len(v[0]) for v in got.values())
+        # (3) the old boxes behind this rank's part, in a tree of their own
+        W, W_old = src[me]
+        space = sorted(set(W) | set(W_old))
+        pos = {b: k for k, b in enumerate(space)}
+        t_ow = self._set_methods(Tree(self.lib, compact_topology(old_topo, W_old, space),
+                                      self.n_var_cell, self.n_var_face, device=self.device))
+        local = [b for b in W_old if owner_old[b - 1] == me or owner_old[b - 1] < 0]
+        data = [np.full((len(space) + 1,) + a.shape[1:], np.nan) for a in cc + fc]
+        if local:
+            rl = rows_of(local)
+            k = np.array([pos[b] for b in local])
+            off = 0
+            for d in data:
+                w = int(np.prod(d.shape[1:]))
+                d[k] = rl[:, off:off + w].reshape((len(k),) + d.shape[1:])
+                off += w
+        for ids, rows in got.values():
+            k = np.array([pos[int(b)] for b in ids])
+            off = 0
+            for d in data:
+                w = int(np.prod(d.shape[1:]))
+                d[k] = rows[:, off:off + w].reshape((len(k),) + d.shape[1:])
+                off += w
+        del cc, fc
+        for iv in range(1, self.n_var_cell + 1):
+            t_ow.put_cc(iv, data[iv - 1])
+        for iv in range(1, self.n_var_face + 1):
+            t_ow.put_fc(iv, data[self.n_var_cell + iv - 1])
+        del data
+        t_nw = t_ow.regrid(compact_topology(new_topo, W, space))
+        # (4) the new sharded tree from it
+        sh.detach()
+        self.shard = None
+        self.af = probe
+        t = self._set_methods(sh2.make_tree(self.lib, new_topo, self.n_var_cell,
+                                            self.n_var_face, device=self.device))
+        k = np.array([pos[int(b)] for b in t.global_ids])
+        for iv in range(1, self.n_var_cell + 1):
+            a = t_nw.get_cc(iv)
+            out = np.full((t.n_boxes,) + a.shape[1:], np.nan)
+            out[:-1] = a[k]
+            t.put_cc(iv, out)
+        for iv in range(1, self.n_var_face + 1):
+            a = t_nw.get_fc(iv)
+            out = np.full((t.n_boxes,) + a.shape[1:], np.nan)
+            out[:-1] = a[k]
+            t.put_fc(iv, out)
+        t_nw.close()
+        t_ow.close()
+        self.shard = sh2
+        self._bind(t)
+        sh2.attach(t)
+        t_old.close()
+        if self.i_gas_dens and info.n_add:  # m_af_core.f90:866-869
+            self._set_gas([b for l in sorted(info.add) for b in info.add[l]])
         return info
 
     def _set_methods(self, t):

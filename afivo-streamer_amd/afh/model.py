@@ -200,6 +200,18 @@ class Tree:
         self.lib.call("cc_get", self.h, iv, a.ctypes.data_as(capi.P_f64))
         return self._to_global(a)
 
+    def get_cc_local(self, iv):
+        """The stored boxes' array (a sharded tree's local ids; the unused
+        last id NaN) -- no whole-tree array."""
+        a = np.empty(self.cc_shape)
+        self.lib.call("cc_get", self.h, iv, a.ctypes.data_as(capi.P_f64))
+        return a
+
+    def get_fc_local(self, ivf):
+        a = np.empty(self.fc_shape)
+        self.lib.call("fc_get", self.h, ivf, a.ctypes.data_as(capi.P_f64))
+        return a
+
     def put_fc(self, ivf, arr):
         a = np.ascontiguousarray(self._to_local(np.asarray(arr, np.float64)))
         assert a.shape == self.fc_shape

@@ -100,11 +100,15 @@ def test_sharded_driver_hip_threads_bitwise(name, world):
     _run(capi.hip_library(), name, world, device=0)
 
 
-def _run_loop(lib, world, n_steps, device=-1):
+def _run_loop(lib, world, n_steps, device=-1, gather=False, monkeypatch=None):
     """The regression run test_3d sharded from its first step: the whole
     time loop -- step control, output rows, refinement every 2 steps (the
     first regrid that adds boxes is at step 46) -- with the refinement of a
-    sharded run (gathered, refined, sharded again with a fresh partition)."""
+    sharded run: rank-local (each rank regrids its part of the new partition
+    from the boxes it needs, received point to point) or, with gather, the
+    whole tree gathered and regridded on every rank."""
+    if monkeypatch is not None:
+        monkeypatch.setenv("AFH_REGRID_GATHER", "1" if gather else "0")
     base = Simulation(lib, golden.load("rtest_test_3d"), device=device)
     base.start()
     clones = [base.clone(lib, device=device) for _ in range(world)]
@@ -124,6 +128,12 @@ def _run_loop(lib, world, n_steps, device=-1):
 
     with ThreadPoolExecutor(world) as ex:
         outs = list(ex.map(loop, clones))
+    if not gather:
+        # the regrid moved single boxes, not the tree: each rank received
+        # fewer boxes than the new tree holds
+        nb = int(clones[0].af.topology()["n_boxes"])
+        got = [sim.regrid_rows_received for sim in clones]
+        assert all(g < nb for g in got), (got, nb)
     if device >= 0:
         # the sharded V-cycles ran as segment graphs between their exchanges
         # (afh_mg.hip vcycle_segments), all ranks alike
@@ -156,15 +166,16 @@ def _run_loop(lib, world, n_steps, device=-1):
     return base
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_time_loop_with_regrids_oracle(world):
+@pytest.mark.parametrize("world,gather", [(2, False), (3, False), (2, True)])
+def test_sharded_time_loop_with_regrids_oracle(world, gather, monkeypatch):
     # 3 ranks: after the regrid some rank computes no box of a level
-    base = _run_loop(capi.oracle_library(), world, 50)
+    base = _run_loop(capi.oracle_library(), world, 50, gather=gather,
+                     monkeypatch=monkeypatch)
     assert base.af.highest_lvl == 6  # the step-46 regrid added level 6
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("world", [2, 3])
-def test_sharded_time_loop_with_regrids_hip(world):
-    base = _run_loop(capi.hip_library(), world, 50, device=0)
+def test_sharded_time_loop_with_regrids_hip(world, monkeypatch):
+    base = _run_loop(capi.hip_library(), world, 50, device=0, monkeypatch=monkeypatch)
     assert base.af.highest_lvl == 6

@@ -327,3 +327,49 @@ def test_allgather_rows_gloo(tmp_path):
             np.testing.assert_array_equal(
                 d["rows%d" % q],
                 np.arange((q + 1) * 3, dtype=np.float64).reshape(q + 1, 3) + 0.5 * q)
+
+
+def _p2p_worker(rank, world, port, outdir):
+    import os
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # the RCCL transport's path of NativeShard.exchange_rows (the counts
+        # all-gathered, then batched send/recv; gloo here, device tensors
+        # under nccl): rank r sends q + r rows of width 4 to every rank q > r
+        sh = type("S", (), {"transport": capi.DIST_RCCL, "n": world, "rank": rank})()
+        sends = {}
+        for q in range(rank + 1, world):
+            m = q + rank
+            sends[q] = (np.arange(m) + 100 * rank,
+                        np.arange(4 * m, dtype=np.float64).reshape(m, 4) + 1000 * rank + q)
+        got = NativeShard.exchange_rows(sh, sends)
+        np.savez(os.path.join(outdir, "p%d.npz" % rank),
+                 **{"ids%d" % q: g[0] for q, g in got.items()},
+                 **{"rows%d" % q: g[1] for q, g in got.items()})
+    finally:
+        dist.destroy_process_group()
+
+
+def test_exchange_rows_gloo(tmp_path):
+    """The point-to-point exchange of the rank-local regrid (only the boxes a
+    rank needs from another): every rank receives exactly what each sender
+    addressed to it, nothing from ranks that sent it nothing."""
+    import torch.multiprocessing as mp
+    from test_dist import _free_port
+    world = 3
+    mp.start_processes(_p2p_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world,
+                       start_method="spawn", join=True)
+    for r in range(world):
+        d = np.load(tmp_path / ("p%d.npz" % r))
+        assert sorted(k for k in d.files if k.startswith("ids")) == \
+            ["ids%d" % q for q in range(r) if q + r > 0]
+        for q in range(r):
+            m = r + q
+            if not m:
+                continue
+            np.testing.assert_array_equal(d["ids%d" % q], np.arange(m) + 100 * q)
+            np.testing.assert_array_equal(
+                d["rows%d" % q], np.arange(4 * m, dtype=np.float64).reshape(m, 4) + 1000 * q + r)
