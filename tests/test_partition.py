@@ -108,3 +108,43 @@ def test_native_plans_equal_python_mixed_frontier():
                                                   err_msg=str((kind, level, recv, send)))
                     n_regions += len(got)
     assert n_regions > 0
+
+
+def test_compact_topology_ids():
+    """dist.compact_topology (the rank-local regrid's small trees): boxes of
+    a shared id space keep their positions, references to boxes outside the
+    set point to the one unused id, physical / refinement boundaries (<= 0)
+    stay, and the oracle builds a tree from it."""
+    from afh.dist import compact_topology
+    from afh.model import Tree
+    topo = tree("s5")
+    nb = int(topo["n_boxes"])
+    lvl = np.asarray(topo["meta_lvl"])
+    used = np.nonzero(lvl > 0)[0] + 1
+    rng = np.random.default_rng(3)
+    present = np.sort(rng.choice(used, size=len(used) // 3, replace=False))
+    extra = np.setdiff1d(used, present)[:25]
+    space = np.union1d(present, extra)
+    c = compact_topology(topo, present, space)
+    n = len(space)
+    assert int(c["n_boxes"]) == n + 1
+    pos = {int(b): k for k, b in enumerate(space)}
+    inset = set(int(b) for b in present)
+    nbr, cnb = np.asarray(topo["meta_neighbors"]), np.asarray(c["meta_neighbors"])
+    for b in present:
+        k = pos[int(b)]
+        assert c["meta_lvl"][k] == lvl[b - 1]
+        for q in range(6):
+            g = nbr[b - 1][q]
+            want = g if g <= 0 else (pos[g] + 1 if g in inset else n + 1)
+            assert cnb[k][q] == want
+    for b in extra:  # in the id space, not present: holes
+        assert c["meta_lvl"][pos[int(b)]] == 0
+    for l in range(1, int(topo["highest_lvl"]) + 1):
+        ids = np.asarray(topo["lvl_ids_%d" % l])
+        want = [pos[int(b)] + 1 for b in ids if int(b) in inset]
+        assert list(c["lvl_ids_%d" % l]) == want
+    t = Tree(capi.oracle_library(), c, 3, 1)
+    assert t.n_boxes == n + 1
+    t.close()
+    assert nb > n
