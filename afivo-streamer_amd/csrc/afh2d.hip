@@ -1354,12 +1354,15 @@ static int32_t gsrb_boxes(afh_mg *mg, int lvl, bool up) {
   const int nc_ = up ? mg->d.n_cycle_up : mg->d.n_cycle_down;
   for (int s = 1; s <= 2 * nc_; s++) {
     if (n) {
-      prof_mark(t, AFH_PROF_GSRB);
+      // timed on levels of >= 256 boxes, as libafivo_hip's pair: the small
+      // levels' launches are launch-bound, another regime
+      const int pc = n >= 256 ? AFH_PROF_GSRB : -1;
+      prof_mark(t, pc);
       hipLaunchKernelGGL(k2_gsrb, grid2(t->nc * t->nc / 2, n), dim3(NT), 0, t->stream,
                          t->ccv(mg->d.i_phi), t->ccv(mg->d.i_rhs), t->ids.at(lvl), t->nc,
                          t->bsz, mg->lvl_c[lvl - 1], s);
       H2_LAUNCH("k2_gsrb");
-      prof_end(t, AFH_PROF_GSRB, 16.0 * t->nc * t->nc * n);
+      prof_end(t, pc, 16.0 * t->nc * t->nc * n);
     }
     if (int32_t e = gc_lvl(t, lvl, mg->d.i_phi, up && s == 2 * nc_)) return e;
   }

@@ -85,8 +85,9 @@ int32_t afh_tree_regrid(afh_tree *old, const afh_tree_desc *desc, afh_tree **out
 int32_t afh_refine_flags(afh_fluid *f, const afh_refine_desc *d,
                          const uint8_t *electrode_box, int32_t *flags,
                          uint32_t *masks);
-/* kernel timing, as in afivo_hip.h: classes AFH_PROF_GSRB (k2_gsrb, 16 B
- * per cell of a half sweep) and AFH_PROF_FLUX (k2_flux, 48 B per leaf cell) */
+/* kernel timing, as in afivo_hip.h: classes AFH_PROF_GSRB (k2_gsrb on
+ * levels of >= 256 boxes, 16 B per cell of a half sweep) and AFH_PROF_FLUX
+ * (k2_flux, 48 B per leaf cell) */
 int32_t afh_profile_enable(afh_tree *t, int32_t kclass);
 int32_t afh_profile_read(afh_tree *t, double *total_ms, int64_t *launches, double *bytes);
 /* the output_regression_log reductions; loc = (id, i, j, 0) */
