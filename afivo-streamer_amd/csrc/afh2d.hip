@@ -272,6 +272,159 @@ __global__ void __launch_bounds__(NT)
          cf.inv_c1;
 }
 
+// A face ghost of box m the level fill would write (k2_gc's physical and
+// refinement branches), from the box's cells x1, x2 next to the face
+__device__ __forceinline__ double gc2_face(const double *__restrict__ coarse,
+                                          const afh_box_meta *__restrict__ meta,
+                                          const afh_box_meta &m, int nb, int nb_id, int a,
+                                          double x1, double x2, int nc, int bsz,
+                                          const Bc4 &g) {
+  const int d = (nb - 1) >> 1;
+  const bool low = ((nb - 1) & 1) == 0;
+  const int ng = nc + 2, hnc = nc >> 1;
+  auto at = [&](int n, int tg) { return d == 0 ? ix2(ng, n, tg) : ix2(ng, tg, n); };
+  if (nb_id < 0) {
+    double c0, c1, c2;
+    const afh_bc bc = g.bc[nb - 1];
+    switch (bc.type) {
+    case AFH_BC_DIRICHLET: c0 = 2; c1 = -1; c2 = 0; break;
+    case AFH_BC_NEUMANN: c0 = m.dr[d] * (low ? -1 : 1); c1 = 1; c2 = 0; break;
+    case AFH_BC_CONTINUOUS: c0 = 0; c1 = 2; c2 = -1; break;
+    default: c0 = 1; c1 = 0; c2 = 0; break;  // AFH_BC_DIRICHLET_COPY
+    }
+    return c0 * bc.value + c1 * x1 + c2 * x2;
+  }
+  const int p_nb = meta[m.parent - 1].neighbors[nb - 1];
+  const double *cp = coarse + (size_t)(p_nb - 1) * bsz;
+  const int ix_c = low ? nc : 1;
+  const int td = 1 - d;
+  const int off = ((m.ix[td] - 1) & 1) * hnc;
+  if (g.rb == AFH_RB_MG_SIDES) {
+    const int q = (a + 1) >> 1;
+    const double tq = cp[at(ix_c, off + q)];
+    const double grad = 0.125 * (cp[at(ix_c, off + q + 1)] - cp[at(ix_c, off + q - 1)]);
+    const double gcv = (a & 1) ? tq - grad : tq + grad;
+    return 0.5 * gcv + 0.75 * x1 - 0.25 * x2;
+  }
+  const double sixth = 1 / 6.0, third = 1 / 3.0;
+  const int c1i = off + ((a + 1) >> 1), c2i = c1i + 1 - 2 * (a & 1);
+  const double a1 = cp[at(ix_c, c1i)], a2 = cp[at(ix_c, c2i)];
+  double val = 0.5 * a1 + sixth * a2 + third * x1;
+  if (g.rb == AFH_RB_GC_INTERP_LIM && val > 2 * a1) val = 2 * a1;
+  return val;
+}
+
+// Two half-sweeps of a small box (odd cells i + j odd, then even) and the
+// level fills after each, in one workgroup, the box image in LDS: A the odd
+// cells | B the odd face ghosts the fill after A would give -- a same-level
+// neighbour's odd boundary cell recomputed from its own image in src (its
+// ghost facing this box included, so stale ghost cells give the split
+// half-sweeps' numbers too), physical / refinement faces from x1 (even,
+// old), x2 (odd, new) | C the even cells | store: the interior and the
+// corners to dst, and the face ghosts the fill after C would write --
+// pushed into the same-level neighbour's ghost layer, or this box's own
+// physical / refinement value. Every box of the level is in the launch and
+// every face ghost has one writer. src -> dst (phi / spare image, alternating
+// per pair); the coarse data of refinement faces are read from phi (the
+// coarser level, not written here). Bitwise k2_gsrb + k2_gc twice.
+template <int NC>
+__global__ void __launch_bounds__(64)
+    k2_pair_box(const double *__restrict__ src, double *__restrict__ dst,
+                const double *__restrict__ rhs, const double *__restrict__ coarse,
+                const afh_box_meta *__restrict__ meta, const int32_t *__restrict__ ids,
+                int bsz, Coef2 cf, Bc4 g) {
+  constexpr int NG = NC + 2, NB = NG * NG, NT = 64, H = NC / 2;
+  __shared__ double P[NB];
+  const int tid = threadIdx.x;
+  const int id = ids[blockIdx.x];
+  const afh_box_meta &m = meta[id - 1];
+  const double *x = src + (size_t)(id - 1) * bsz, *r = rhs + (size_t)(id - 1) * bsz;
+  double *y = dst + (size_t)(id - 1) * bsz;
+  for (int e = tid; e < NB; e += NT) P[e] = x[e];
+  // B inputs: the odd ghost u < 2 NC (face u / H + 1, its odd positions) of
+  // a same-level neighbour -- the neighbour's boundary cell, its four
+  // neighbours and rhs, loaded before A
+  constexpr int NGH = 2 * NC, GPT = (NGH + NT - 1) / NT;
+  double bl[GPT][5];
+  for (int q = 0; q < GPT; q++) {
+    const int u = tid + NT * q;
+    for (int k = 0; k < 5; k++) bl[q][k] = 0.0;
+    if (u >= NGH) continue;
+    const int nb = u / H + 1, d = (nb - 1) >> 1;
+    const bool low = ((nb - 1) & 1) == 0;
+    const int gi = low ? 0 : NC + 1;
+    const int a = 2 * (u % H) + 1 + ((gi & 1) ? 1 : 0);  // gi + a odd
+    const int nid = m.neighbors[nb - 1];
+    if (nid > 0) {
+      auto at = [&](int n, int tg) { return d == 0 ? ix2(NG, n, tg) : ix2(NG, tg, n); };
+      const double *xs = src + (size_t)(nid - 1) * bsz;
+      const int c = at(low ? NC : 1, a);
+      bl[q][0] = xs[c - 1];
+      bl[q][1] = xs[c + 1];
+      bl[q][2] = xs[c - NG];
+      bl[q][3] = xs[c + NG];
+      bl[q][4] = rhs[(size_t)(nid - 1) * bsz + c];
+    }
+  }
+  __syncthreads();
+  // A: odd cells (k2_gsrb with an odd red-black counter)
+  for (int q = tid; q < NC * H; q += NT) {
+    const int j = q / H + 1, i = 2 - ((1 ^ j) & 1) + 2 * (q % H);
+    const int c = ix2(NG, i, j);
+    P[c] = (r[c] - cf.c[1] * P[c - 1] - cf.c[2] * P[c + 1] - cf.c[3] * P[c - NG] -
+            cf.c[4] * P[c + NG]) *
+           cf.inv_c1;
+  }
+  __syncthreads();
+  // B: odd face ghosts
+  for (int q = 0; q < GPT; q++) {
+    const int u = tid + NT * q;
+    if (u >= NGH) continue;
+    const int nb = u / H + 1, d = (nb - 1) >> 1;
+    const bool low = ((nb - 1) & 1) == 0;
+    const int gi = low ? 0 : NC + 1, i1 = low ? 1 : NC, i2 = low ? 2 : NC - 1;
+    const int a = 2 * (u % H) + 1 + ((gi & 1) ? 1 : 0);
+    auto at = [&](int n, int tg) { return d == 0 ? ix2(NG, n, tg) : ix2(NG, tg, n); };
+    const int nid = m.neighbors[nb - 1];
+    double v;
+    if (nid > 0)
+      v = (bl[q][4] - cf.c[1] * bl[q][0] - cf.c[2] * bl[q][1] - cf.c[3] * bl[q][2] -
+           cf.c[4] * bl[q][3]) *
+          cf.inv_c1;
+    else
+      v = gc2_face(coarse, meta, m, nb, nid, a, P[at(i1, a)], P[at(i2, a)], NC, bsz, g);
+    P[at(gi, a)] = v;
+  }
+  __syncthreads();
+  // C: even cells
+  for (int q = tid; q < NC * H; q += NT) {
+    const int j = q / H + 1, i = 2 - ((0 ^ j) & 1) + 2 * (q % H);
+    const int c = ix2(NG, i, j);
+    P[c] = (r[c] - cf.c[1] * P[c - 1] - cf.c[2] * P[c + 1] - cf.c[3] * P[c - NG] -
+            cf.c[4] * P[c + NG]) *
+           cf.inv_c1;
+  }
+  __syncthreads();
+  // store: interior and corners; the four faces' ghosts pushed
+  for (int e = tid; e < NB; e += NT) {
+    const int i = e % NG, j = e / NG;
+    const int nout = (i == 0 || i == NG - 1) + (j == 0 || j == NG - 1);
+    if (nout != 1) y[e] = P[e];
+  }
+  for (int u = tid; u < 4 * NC; u += NT) {
+    const int nb = u / NC + 1, a = u % NC + 1, d = (nb - 1) >> 1;
+    const bool low = ((nb - 1) & 1) == 0;
+    const int gi = low ? 0 : NC + 1, i1 = low ? 1 : NC, i2 = low ? 2 : NC - 1;
+    auto at = [&](int n, int tg) { return d == 0 ? ix2(NG, n, tg) : ix2(NG, tg, n); };
+    const int nid = m.neighbors[nb - 1];
+    if (nid > 0)
+      dst[(size_t)(nid - 1) * bsz + at(low ? NC + 1 : 0, a)] = P[at(i1, a)];
+    else
+      y[at(gi, a)] = gc2_face(coarse, meta, m, nb, nid, a, P[at(i1, a)], P[at(i2, a)], NC,
+                              bsz, g);
+  }
+}
+
 __device__ __forceinline__ double apply5(const double *p, int x, int ng, const Coef2 &cf) {
   return cf.c[0] * p[x] + cf.c[1] * p[x - 1] + cf.c[2] * p[x + 1] + cf.c[3] * p[x - ng] +
          cf.c[4] * p[x + ng];
@@ -895,6 +1048,10 @@ struct afh_mg {
   int nx = 0, ny = 0;
   double *d_q[2] = {nullptr, nullptr}, *d_e[2] = {nullptr, nullptr};
   int q_bc[4] = {0, 0, 0, 0};
+  // the fused pair (k2_pair_box, AFH_PAIR2D=0: the split half-sweeps) and
+  // its spare phi image
+  bool pair = true;
+  double *alt = nullptr;
 };
 
 struct afh_fluid {
@@ -1278,6 +1435,10 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
   H2(hipMalloc(&mg->d_q[1], sizeof(double) * ny * ny));
   H2(hipMalloc(&mg->d_e[0], sizeof(double) * nx));
   H2(hipMalloc(&mg->d_e[1], sizeof(double) * ny));
+  if (const char *env = getenv("AFH_PAIR2D")) mg->pair = atoi(env) != 0;
+  mg->pair = mg->pair && (t->nc == 4 || t->nc == 8 || t->nc == 16) &&
+             d->n_cycle_down % 2 == 0 && d->n_cycle_up % 2 == 0;
+  if (mg->pair) H2(hipMalloc(&mg->alt, sizeof(double) * (size_t)t->nb * t->bsz));
   *out = mg;
   return AFH_OK;
 }
@@ -1286,6 +1447,7 @@ int32_t afh_mg_destroy(afh_mg *mg) {
   if (!mg) return AFH_OK;
   hipStreamSynchronize(mg->t->stream);
   for (int q = 0; q < 2; q++) hipFree(mg->d_q[q]), hipFree(mg->d_e[q]);
+  hipFree(mg->alt);
   delete mg;
   return AFH_OK;
 }
@@ -1352,6 +1514,33 @@ static int32_t gsrb_boxes(afh_mg *mg, int lvl, bool up) {
   afh_tree *t = mg->t;
   const int n = t->ids.n(lvl);
   const int nc_ = up ? mg->d.n_cycle_up : mg->d.n_cycle_down;
+  if (mg->pair && n) {
+    // n_cycle fused pairs, phi -> alt -> phi (n_cycle even); the corners of
+    // the up leg's last fill after them
+    double *phi = t->ccv(mg->d.i_phi);
+    for (int p = 0; p < nc_; p++) {
+      const double *src = (p & 1) ? mg->alt : phi;
+      double *dst = (p & 1) ? phi : mg->alt;
+      const Coef2 cf = mg->lvl_c[lvl - 1];
+      const Bc4 g = t->bc4(mg->d.i_phi);
+      if (t->nc == 4)
+        hipLaunchKernelGGL(k2_pair_box<4>, dim3(n), dim3(64), 0, t->stream, src, dst,
+                           t->ccv(mg->d.i_rhs), phi, t->d_boxes, t->ids.at(lvl), t->bsz, cf, g);
+      else if (t->nc == 8)
+        hipLaunchKernelGGL(k2_pair_box<8>, dim3(n), dim3(64), 0, t->stream, src, dst,
+                           t->ccv(mg->d.i_rhs), phi, t->d_boxes, t->ids.at(lvl), t->bsz, cf, g);
+      else
+        hipLaunchKernelGGL(k2_pair_box<16>, dim3(n), dim3(64), 0, t->stream, src, dst,
+                           t->ccv(mg->d.i_rhs), phi, t->d_boxes, t->ids.at(lvl), t->bsz, cf, g);
+      H2_LAUNCH("k2_pair_box");
+    }
+    if (up) {
+      hipLaunchKernelGGL(k2_corners, dim3((4 * n + NT - 1) / NT), dim3(NT), 0, t->stream,
+                         phi, t->d_boxes, t->ids.at(lvl), n, t->nc, t->bsz);
+      H2_LAUNCH("k2_corners");
+    }
+    return AFH_OK;
+  }
   for (int s = 1; s <= 2 * nc_; s++) {
     if (n) {
       // timed on levels of >= 256 boxes, as libafivo_hip's pair: the small

@@ -140,6 +140,34 @@ def test_s3_all_level_launches_bitwise(monkeypatch):
         assert np.array_equal(x, y, equal_nan=True)
 
 
+def _case2d(monkeypatch, env, config):
+    import bench
+    from afh import capi
+    from afh.streamer import IV
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    c = bench.build_case(capi.hip_library_2d(), config, 0, 0)
+    out = {"res0": c.field_compute(0, n_vcycles=2)}
+    for k in range(4):
+        out["step%d" % k] = bench.unit_step(c, 1e-13, k)
+    for v in ("e", "pos", "neg", "phi", "efld", "rhs", "tmp"):
+        out[v] = c.tree.get_cc(IV[v])
+    c.tree.close()
+    return out
+
+
+@pytest.mark.parametrize("config", ["2d", "c2d16"])
+def test_2d_pair_bitwise(config, monkeypatch):
+    """The 2-D fused pair with its pushed fills (k2_pair_box, AFH_PAIR2D)
+    against the split half-sweeps + level fills: BASELINE config 1's bench
+    tree (8 levels of 8^2 boxes) and a 16^2-box tree; field solves and four
+    unit steps, every variable bitwise."""
+    import bench
+    monkeypatch.setitem(bench.CONFIGS, "c2d16", (16, (16, 16), 4, (16e-3, 16e-3)))
+    _same(_case2d(monkeypatch, {"AFH_PAIR2D": "1"}, config),
+          _case2d(monkeypatch, {"AFH_PAIR2D": "0"}, config))
+
+
 @pytest.mark.parametrize("switch", ["AFH_PROLONG_PUSH", "AFH_RSTR_PUSH"])
 def test_push_bitwise_8cubed(switch, monkeypatch):
     import bench
