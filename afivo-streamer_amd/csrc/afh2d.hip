@@ -1048,9 +1048,9 @@ struct afh_mg {
   int nx = 0, ny = 0;
   double *d_q[2] = {nullptr, nullptr}, *d_e[2] = {nullptr, nullptr};
   int q_bc[4] = {0, 0, 0, 0};
-  // the fused pair (k2_pair_box, AFH_PAIR2D=0: the split half-sweeps) and
-  // its spare phi image
-  bool pair = true;
+  // the fused pair (k2_pair_box, AFH_PAIR2D=1; off until measured on the
+  // GPU: the split half-sweeps) and its spare phi image
+  bool pair = false;
   double *alt = nullptr;
 };
 

@@ -2554,8 +2554,9 @@ struct afh_mg {
   bool cs_direct_small = true;
   int cs_ds_cells = CS_DS_CELLS;  // AFH_CS_DS_CELLS: its size limit (at most CS_SMALL_CELLS)
   bool pair_push = true;  // AFH_PAIR_PUSH: the small-box pair fills the faces
-  bool prolong_push = true;  // AFH_PROLONG_PUSH: so does the small-box correction
-  bool rstr_push = true;     // AFH_RSTR_PUSH: and the small-box restriction
+  // (round 4; off until measured on the GPU: AFH_PROLONG_PUSH=1 / AFH_RSTR_PUSH=1)
+  bool prolong_push = false;  // AFH_PROLONG_PUSH: so does the small-box correction
+  bool rstr_push = false;     // AFH_RSTR_PUSH: and the small-box restriction
   int *d_cycles = nullptr;
   int cycles_host = 0;
   bool cycles_on_dev = false;
