@@ -384,13 +384,28 @@ struct RbPar {
 // plane below it (as tiles recompute halo rows) and stores its own planes
 // NTL: the streamed plane and rhs loads non-temporal (they are used once;
 // the lines phase B reads from neighbouring boxes should stay in L2)
+// PS (whole boxes, TJ = NC, KS = 1; levels without refinement boundaries):
+// the level's face fill after the pair is
+// done by the pair, as k_gsrb_pair_box<PUSH> does for small boxes. With a
+// plane's final values in LDS (its store, E), the box writes its boundary
+// cells into the ghost layers of its same-level neighbours' dst (x: the
+// row store's ghost cell goes to the neighbour instead; y: the rows facing
+// the neighbour), and its own ghost cells of physical / refinement faces
+// their gc_face_nocopy value; the z faces once planes 1, 2 (after step 3)
+// and NC-1, NC (after the march) are final. Every face ghost of dst then has
+// one writer, and no box reads dst during the pair (the neighbours read
+// src), so dst ends as the pair + k_gc_faces would leave it; edges and
+// corners are not written (the pairs read faces only; k_gc_corners follows
+// the level's last pair). The fill's x faces move one 128-B line per 8-B
+// value in each direction (3.1x their bytes); the push writes those values
+// from LDS, and the box's own x ghost cells come from its neighbours' pushes
 template <bool NTL>
 __device__ __forceinline__ double ld_nt(const double *p) {
   if constexpr (NTL) return __builtin_nontemporal_load(p);
   else return *p;
 }
 template <int NC, int TJ, int DEPTH = 2, int NTM = 0, bool FR = true, bool P3 = true,
-          bool SP = true, int KS = 1, bool NTL = false>
+          bool SP = true, int KS = 1, bool NTL = false, bool PS = false>
 __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
     k_gsrb_pair2(const double *__restrict__ src, double *__restrict__ dst,
                  const double *__restrict__ rhs, const double *__restrict__ coarse,
@@ -401,6 +416,7 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
   constexpr int NG = G::NG, HN = G::HN, NT = G::NT, RPT = G::RPT, PL = G::PL,
                 EPT = G::EPT, OPT = G::OPT;
   constexpr size_t SK = (size_t)NG * NG;
+  static_assert(!PS || (TJ == NC && KS == 1 && FR), "the push form is whole boxes");
   __shared__ double P[4][PL];  // planes s-2 .. s+1 at slot (plane & 3)
   // LDS row layout. SP (split parity): each row holds its even-i cells, then
   // its odd-i cells, so the red (black) cells the lanes of a row update and
@@ -601,8 +617,79 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
   if (DEPTH == 2) load_pf(X0, s0 + 2);
 
   // E: plane k of the tile to dst (in full rows with FR)
+  // PS: a face ghost p of this box on a physical boundary, from the final
+  // values own(q) next to it (the push form runs on levels without
+  // refinement boundaries; the face a compile-time constant, so that
+  // gc_face_nocopy_k's per-dimension indexing stays in registers)
+  auto own_gc = [&](auto NBc, const int p[3], int a, int b, auto own) {
+    constexpr int nb = decltype(NBc)::value;
+    return gc_face_nocopy_k(coarse, meta, m, nb, -1, drof(nb), p, a, b, NC, bsz, bcof(nb),
+                            ga.rb, own);
+  };
+  using F1 = std::integral_constant<int, 1>;
+  using F2 = std::integral_constant<int, 2>;
+  using F3 = std::integral_constant<int, 3>;
+  using F4 = std::integral_constant<int, 4>;
   auto store_plane = [&](const int k, const double *Pk) {
-    if (FR) {
+    if (PS) {
+      // rows 1..NC without their x ghost cells; then the x ghost cells (2 TJ
+      // entries: pushed into the neighbour, or evaluated) and the y ghost
+      // rows (2 NC)
+#pragma unroll
+      for (int q = 0; q < G::OPTF; q++) {
+        const int e = tid + NT * q;
+        if (e < NG * TJ) {
+          const int i = e % NG;
+          if (i != 0 && i != NC + 1)
+            st_nt<AFH_NT_PAIR>(y + ((size_t)k * SK + t0 + NG + e), Pk[perm(NG + e)]);
+        }
+      }
+      for (int u = tid; u < 2 * TJ + 2 * NC; u += NT) {
+        if (u < 2 * TJ) {
+          const int jl = (u >> 1) + 1;
+          auto own = [&](const int *c) { return Pk[L(jl, c[0])]; };
+          double *at;
+          double v;
+          if (!(u & 1)) {
+            if (nb1 > 0) {
+              // this box's boundary cell into the neighbour's ghost cell
+              at = dst + ((size_t)(nb1 - 1) * bsz + (size_t)k * SK + (size_t)jl * NG + NC + 1);
+              v = Pk[L(jl, 1)];
+            } else {
+              const int p[3] = {0, jl, k};
+              at = y + ((size_t)k * SK + (size_t)jl * NG);
+              v = own_gc(F1{}, p, jl, k, own);
+            }
+          } else {
+            if (nb2 > 0) {
+              at = dst + ((size_t)(nb2 - 1) * bsz + (size_t)k * SK + (size_t)jl * NG);
+              v = Pk[L(jl, NC)];
+            } else {
+              const int p[3] = {NC + 1, jl, k};
+              at = y + ((size_t)k * SK + (size_t)jl * NG + NC + 1);
+              v = own_gc(F2{}, p, jl, k, own);
+            }
+          }
+          st_nt<AFH_NT_PAIR>(at, v);
+        } else {
+          const int w = u - 2 * TJ, hi = w / NC, ii = w - hi * NC + 1;
+          const int nid = hi ? nb4 : nb3;
+          auto own = [&](const int *c) { return Pk[L(c[1], ii)]; };
+          if (nid > 0) {
+            st_nt<AFH_NT_PAIR>(dst + ((size_t)(nid - 1) * bsz + (size_t)k * SK +
+                                      (size_t)(hi ? 0 : NC + 1) * NG + ii),
+                               Pk[L(hi ? NC : 1, ii)]);
+          } else if (!hi) {
+            const int p[3] = {ii, 0, k};
+            st_nt<AFH_NT_PAIR>(y + ((size_t)k * SK + ii), own_gc(F3{}, p, ii, k, own));
+          } else {
+            const int p[3] = {ii, NC + 1, k};
+            st_nt<AFH_NT_PAIR>(y + ((size_t)k * SK + (size_t)(NC + 1) * NG + ii),
+                               own_gc(F4{}, p, ii, k, own));
+          }
+        }
+      }
+    } else if (FR) {
 #pragma unroll
       for (int q = 0; q < G::OPTF; q++) {
         const int e = tid + NT * q;
@@ -616,6 +703,27 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
           const int c = (e / NC + 1) * NG + e % NC + 1;
           st_nt<AFH_NT_PAIR>(y + ((size_t)k * SK + t0 + c), Pk[L(e / NC + 1, e % NC + 1)]);
         }
+      }
+    }
+  };
+  // PS: z face ghost plane (nb 5: plane 0 from planes 1, 2; nb 6: plane NC+1
+  // from planes NC, NC-1), pushed into the neighbour or evaluated
+  auto store_zface = [&](auto NBc, const double *X1, const double *X2) {
+    constexpr int nb = decltype(NBc)::value;
+    const int nid = nb == 5 ? nb5 : nb6;
+    for (int e = tid; e < NC * NC; e += NT) {
+      const int jj = e / NC + 1, ii = e - (jj - 1) * NC + 1;
+      const double x1v = X1[L(jj, ii)];
+      if (nid > 0) {
+        st_nt<AFH_NT_PAIR>(dst + ((size_t)(nid - 1) * bsz +
+                                  (size_t)(nb == 5 ? NC + 1 : 0) * SK + (size_t)jj * NG + ii),
+                           x1v);
+      } else {
+        const int p[3] = {ii, jj, nb == 5 ? 0 : NC + 1};
+        st_nt<AFH_NT_PAIR>(y + ix3(NG, p[0], p[1], p[2]),
+                           own_gc(NBc, p, ii, jj, [&](const int *c) {
+                             return (c[2] == 1 || c[2] == NC) ? x1v : X2[L(jj, ii)];
+                           }));
       }
     }
   };
@@ -717,6 +825,11 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
     __syncthreads();
     // E (without P3): plane s-1; D: plane s+2 into the slot of plane s-2
     if (!P3 && s - 1 >= k0 && s - 1 <= k1) store_plane(s - 1, Pm);
+    if (PS && s == 3) {
+      // planes 1 (Pmm) and 2 (Pm) are final; D overwrites plane 1's slot
+      store_zface(std::integral_constant<int, 5>{}, Pmm, Pm);
+      __syncthreads();
+    }
     if (s + 2 <= NC + 1 && s + 2 <= k1 + 2) {
 #pragma unroll
       for (int e = 0; e < EPT; e++) {
@@ -744,6 +857,7 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
     }
   }
   if (P3) store_plane(k1, P[k1 & 3]);
+  if (PS) store_zface(std::integral_constant<int, 6>{}, P[NC & 3], P[(NC - 1) & 3]);
 }
 
 // Whole-box form of the fused pair for small boxes (NC <= 16): the box, its
@@ -2557,6 +2671,10 @@ struct afh_mg {
   // (round 4; off until measured on the GPU: AFH_PROLONG_PUSH=1 / AFH_RSTR_PUSH=1)
   bool prolong_push = false;  // AFH_PROLONG_PUSH: so does the small-box correction
   bool rstr_push = false;     // AFH_RSTR_PUSH: and the small-box restriction
+  // AFH_PAIR2_PUSH: the whole-box pair of bigger boxes (k_gsrb_pair2, TJ =
+  // NC) fills the level's faces too (off until measured on the GPU)
+  bool pair2_push = false;
+  int tiles_min = 256;  // AFH_PAIR_TILES_MIN: levels of fewer boxes run tiles (NC >= 32)
   int *d_cycles = nullptr;
   int cycles_host = 0;
   bool cycles_on_dev = false;
@@ -2842,6 +2960,8 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
   if (const char *env = getenv("AFH_PAIR_PUSH")) mg->pair_push = atoi(env) != 0;
   if (const char *env = getenv("AFH_PROLONG_PUSH")) mg->prolong_push = atoi(env) != 0;
   if (const char *env = getenv("AFH_RSTR_PUSH")) mg->rstr_push = atoi(env) != 0;
+  if (const char *env = getenv("AFH_PAIR2_PUSH")) mg->pair2_push = atoi(env) != 0;
+  if (const char *env = getenv("AFH_PAIR_TILES_MIN")) mg->tiles_min = atoi(env);
   AFH_HIP(hipMalloc(&mg->cs_iters, sizeof(int)));
   AFH_HIP(hipMalloc(&mg->d_cycles, sizeof(int)));
   if (const char *env = getenv("AFH_GSRB_PAIR_BOX")) mg->pair_box = atoi(env) != 0;
@@ -2961,15 +3081,30 @@ static void launch_pair_t(afh_mg *mg, int lvl, const double *src, double *dst,
 // 64 leaf boxes each) splits them, instead of leaving most CUs idle.
 static bool pair_tiles(const afh_mg *mg, int lvl) {
   const int n = mg->t->ids.n(lvl);
-  return mg->t->nc >= 32 && (mg->force_tiles || n < 256);
+  return mg->t->nc >= 32 && (mg->force_tiles || n < mg->tiles_min);
+}
+
+// the whole-box pair of boxes of 16^3 and up pushes the level's faces
+// (k_gsrb_pair2<..., PS>): its default forms only (none of the AFH_GSRB_PAIR_*
+// experiments), not on a sharded tree (a replica's ghosts are its owner's)
+static bool pair2_push(const afh_mg *mg, int lvl) {
+  const int nc = mg->t->nc;
+  if (!mg->pair2_push || mg->t->hook || mg->pair_v1 || nc < 16) return false;
+  // physical faces only (no refinement boundaries on the level)
+  if (lvl >= 2 && mg->t->lvl_rb_coarse[lvl - 2]) return false;
+  if (nc == 16) return !mg->pair_box;
+  if (pair_tiles(mg, lvl)) return false;
+  if (nc == 32) return true;
+  return nc == 64 && mg->pair_tj == 0 && mg->pair_nt == 0 && mg->pair_depth == 1 &&
+         mg->pair_fr && mg->pair_sp && mg->pair_p3 && !mg->pair_ntl && mg->pair_ks_leaf == 1;
 }
 
 template <int NC, int TJ, int DEPTH, int NTM = 0, bool FR = true, bool P3 = true,
-          bool SP = true, int KS = 1, bool NTL = false>
+          bool SP = true, int KS = 1, bool NTL = false, bool PS = false>
 static void launch_pair2(afh_mg *mg, int lvl, const double *src, double *dst,
                          const Coef &cf, double inv_c1, hipEvent_t e0, hipEvent_t e1) {
   afh_tree *t = mg->t;
-  launch_ev((k_gsrb_pair2<NC, TJ, DEPTH, NTM, FR, P3, SP, KS, NTL>), e0, e1,
+  launch_ev((k_gsrb_pair2<NC, TJ, DEPTH, NTM, FR, P3, SP, KS, NTL, PS>), e0, e1,
             dim3(t->ids.n(lvl) * RbPar<NC, TJ, NTM>::NTILE * KS),
             dim3(RbPar<NC, TJ, NTM>::NT), t->stream, src, dst, t->ccv(mg->d.i_rhs),
             t->ccv(mg->d.i_phi), t->d_boxes, t->ids.at(lvl), t->bsz, cf, inv_c1,
@@ -3000,6 +3135,16 @@ static void launch_pair(afh_mg *mg, int lvl, const double *src, double *dst,
                   t->stream, src, dst, t->ccv(mg->d.i_rhs), t->ccv(mg->d.i_phi), t->d_boxes,
                   t->ids.at(lvl), t->bsz, cf, inv_c1, t->gc_args(mg->d.i_phi));
       return;
+    }
+  }
+  if constexpr (NC >= 16) {
+    if (pair2_push(mg, lvl)) {
+      if constexpr (NC == 64)
+        return launch_pair2<NC, NC, 1, 0, true, true, true, 1, false, true>(mg, lvl, src, dst,
+                                                                            cf, inv_c1, e0, e1);
+      else
+        return launch_pair2<NC, NC, 2, 0, true, true, true, 1, false, true>(mg, lvl, src, dst,
+                                                                            cf, inv_c1, e0, e1);
     }
   }
   if constexpr (NC >= 32) {
@@ -3197,7 +3342,7 @@ static int32_t gsrb_boxes(afh_mg *mg, int lvl, bool up, bool stale_ghosts = fals
     if (timed) prof_count(t, 24.0 * nc * nc * nc * nid);
     AFH_LAUNCH_CHECK("k_gsrb_pair");
     (void)dst;
-    if (pair_push(mg)) {
+    if (pair_push(mg) || pair2_push(mg, lvl)) {
       // the pair filled the faces; edges and corners on the leg's last pair
       if (up && n == n_cycle)
         if (int32_t e = gc_lvl_corners(t, lvl, dst_iv)) return e;

@@ -921,9 +921,6 @@ __global__ void __launch_bounds__(AFH_FLUX_LDS_NT, AFH_FLUX_LDS_MINW)
   extern __shared__ double T[];  // 2 n_points (dynamic)
   __shared__ double SN[2][NR * RW], SE[2][ER * EW];
   __shared__ double sv[NT], sd[NT];
-  // the box's x-high faces: face field (from the row's last cell) and the
-  // transport (to it) per row of the tile
-  __shared__ double xs[TJ], xv[TJ], xd[TJ];
   __shared__ double r1[NT / 64], r2[NT / 64];
   const int tid = threadIdx.x;
   const int wg = xcd_swizzle(blockIdx.x, gridDim.x);
@@ -996,12 +993,6 @@ __global__ void __launch_bounds__(AFH_FLUX_LDS_NT, AFH_FLUX_LDS_MINW)
     exh = i == NC ? Ef[fcol + 1] : 0.0;
     eyh = (jr == TJ - 1) ? Ef[FD + fcol + NF] : 0.0;
   }
-  // The x-high face of row j0 + r is evaluated by lane r of wave 0 (r < TJ)
-  // rather than by the row's last lane: that made every wave run a fourth
-  // face in a divergent branch. The last lane hands over the face field
-  // (xs) and takes back the transport for its CFL sum (xv, xd); same
-  // expressions, same values.
-  if (i == NC) xs[jr] = exh;
   __syncthreads();
 
   // LDS indices of the own cell in the staged planes
@@ -1081,18 +1072,14 @@ __global__ void __launch_bounds__(AFH_FLUX_LDS_NT, AFH_FLUX_LDS_MINW)
       smax = fmax(smax, mu * u);
     }
     double vxh = __shfl_down(vx, 1, 64), dxh = __shfl_down(dx, 1, 64);
-    if (tid < TJ) {  // x-high face of row j0 + tid (cell NC's expressions)
-      const int xn = (tid + 2) * RW + (NC + 1), xe = (tid + 1) * EW + NC;
-      const double zx = N0[xn], exx = xs[tid];
-      const double u = upwind_t<LIM>(A.lim, N0[xn - 1], zx, N0[xn + 1], N0[xn + 2], exx);
-      lds_mu_dc(T, A.td, 0.5 * (E0p[xe] + E0p[xe + 1]) * 1e21 * N_inv, mu, dcv);
+    if (i == NC) {
+      const double u = upwind_t<LIM>(A.lim, N0[cn - 1], z0, N0[cn + 1], N0[cn + 2], exh);
+      lds_mu_dc(T, A.td, 0.5 * (e0 + E0p[ce + 1]) * 1e21 * N_inv, mu, dcv);
       mu = mu * N_inv;
-      const double dh = dcv * N_inv, vh = -mu * exx;
-      st_nt<AFH_NT_FLUX>(F + ((k - 1) * (int)FSK + (j0 + tid - 1) * NF + NC),
-                         vh * u - dh * ix * (N0[xn + 1] - zx));
+      dxh = dcv * N_inv;
+      vxh = -mu * exh;
+      st_nt<AFH_NT_FLUX>(F + (fb + 1), vxh * u - dxh * ix * (N0[cn + 1] - z0));
       smax = fmax(smax, mu * u);
-      xv[tid] = vh;
-      xd[tid] = dh;
     }
     // y low face
     double vy, dy;
@@ -1109,7 +1096,6 @@ __global__ void __launch_bounds__(AFH_FLUX_LDS_NT, AFH_FLUX_LDS_MINW)
     sv[tid] = vy;
     sd[tid] = dy;
     __syncthreads();
-    if (i == NC) vxh = xv[jr], dxh = xd[jr];
     double vyh, dyh;
     if (jr + 1 < TJ) {
       vyh = sv[tid + NC];
@@ -1178,7 +1164,6 @@ __global__ void __launch_bounds__(AFH_FLUX_LDS_NT, AFH_FLUX_LDS_MINW)
     } else {
       exl = nexl, eyl = neyl, ezl = nezl, exh = nexh, eyh = neyh;
     }
-    if (i == NC) xs[jr] = exh;  // (read before the barrier above)
     __syncthreads();
   }
   for (int o = 32; o > 0; o >>= 1) {

@@ -22,7 +22,9 @@ for rep in $(seq ${REPS:-2}); do
 import csv, json, re, sys
 tag, trace, log, rx = sys.argv[1:5]
 acc = {}
+tot = 0
 for r in csv.DictReader(open(trace)):
+    tot += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
     name = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("afh::", "")
     if not re.search(rx, name):
         continue
@@ -35,7 +37,8 @@ out = []
 for name, by in sorted(acc.items()):
     g = max(by)
     out.append("%s=%.1fus(x%d)" % (name[:28], sum(by[g]) / len(by[g]) / 1e3, len(by[g])))
-print("%-22s %.3f ms/step | %s" % (tag, line["ms_per_step"], " ".join(out)), flush=True)
+print("%-22s %.3f ms/step kernels %.2f ms | %s" % (tag, line["ms_per_step"], tot / 1e6,
+                                                  " ".join(out)), flush=True)
 PY
   done
 done

@@ -23,7 +23,12 @@ Round 4:
   (k_rstr_box) and the parents' edges, corners and rhs come in one launch
   (k_parent_rhs_box) vs k_rstr_fas_col + a level fill + k_parent_rhs --
   on S1, on a tree of 8^3 boxes and on the S3 and S5 AMR trees (refinement
-  boundaries on every level, physical faces).
+  boundaries on every level, physical faces);
+* AFH_PAIR2_PUSH: the whole-box pair of 16^3 .. 64^3 boxes (k_gsrb_pair2
+  PS) writes the level's face ghosts itself vs the pair + k_gc_faces -- on
+  S1-64 (BASELINE's headline tree, 512 leaf boxes of 64^3), a tree of 32^3
+  boxes, and AMR trees of 16^3 and 32^3 boxes (every level whole-box pairs;
+  the levels with refinement boundaries keep the fill).
 
 The fused forms are also what every other GPU test runs (they are the
 defaults); these tests pin them to the unfused forms on full workloads.
@@ -238,6 +243,48 @@ def test_gradient_folded_into_residual_bitwise(config, monkeypatch):
             out["step%d" % k] = bench.unit_step(c, 1e-13, k)
         for v in ("e", "pos", "neg", "phi", "efld", "rhs", "tmp"):
             out[v] = c.tree.get_cc(IV[v])
+        c.tree.close()
+        outs.append(out)
+    _same(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("config", ["c32l4", "s1-64"])
+def test_pair2_push_bitwise(config, monkeypatch):
+    """The whole-box pair with its pushed face fills (AFH_PAIR2_PUSH) on
+    512 leaf boxes of 32^3 and 64^3 (physical faces on the domain sides): the
+    field solve and four unit steps, every variable bitwise the pair + fill."""
+    import bench
+    monkeypatch.setitem(bench.CONFIGS, "c32l4", (32, (32, 32, 32), 4, (8e-3, 8e-3, 8e-3)))
+    _same(_s1(monkeypatch, {"AFH_PAIR2_PUSH": "1"}, config),
+          _s1(monkeypatch, {"AFH_PAIR2_PUSH": "0"}, config))
+
+
+@pytest.mark.parametrize("name", ["amr16", "amr32"])
+def test_pair2_push_bitwise_amr(name, monkeypatch):
+    """AMR trees of 16^3 (the plane-marching pair, AFH_GSRB_PAIR_BOX=0) and
+    32^3 boxes, every level of two or more boxes smoothed by whole-box
+    pairs: the fully refined levels push, the levels with refinement
+    boundaries keep the fill. Two field solves and a Heun step, bitwise."""
+    from afh import capi
+    from afh.streamer import IV
+    from afh.tree import build_tree
+    from test_face_field import TOPOS, make
+    topo = TOPOS["amr16"]() if name == "amr16" else build_tree(
+        32, (64, 64, 64), (2e-3, 2e-3, 2e-3), 2,
+        refine=lambda lvl, r0, r1: lvl < 3 and np.all(r0 < 1.2e-3) and np.all(r1 > 0.7e-3))
+    monkeypatch.setenv("AFH_GSRB_PAIR_BOX", "0")
+    monkeypatch.setenv("AFH_GSRB_FUSED_MIN_BOXES", "2")
+    monkeypatch.setenv("AFH_PAIR_TILES_MIN", "1")
+    outs = []
+    for v in ("1", "0"):
+        monkeypatch.setenv("AFH_PAIR2_PUSH", v)
+        c = make(capi.hip_library(), topo, 0, True)
+        out = {"res0": c.field_compute(0, check_residual=False)}
+        out["l0"] = list(c.fluid.forward_euler(1e-12, 0, [0], [1.0], 1, False, True))
+        out["res1"] = c.field_compute(1, check_residual=False)
+        out["l1"] = list(c.fluid.forward_euler(1e-12, 1, [0, 1], [0.5, 0.5], 0, True, True))
+        for v2 in ("e", "pos", "neg", "phi", "efld"):
+            out[v2] = c.tree.get_cc(IV[v2])
         c.tree.close()
         outs.append(out)
     _same(outs[0], outs[1])
