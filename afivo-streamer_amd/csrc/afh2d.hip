@@ -1048,9 +1048,10 @@ struct afh_mg {
   int nx = 0, ny = 0;
   double *d_q[2] = {nullptr, nullptr}, *d_e[2] = {nullptr, nullptr};
   int q_bc[4] = {0, 0, 0, 0};
-  // the fused pair (k2_pair_box, AFH_PAIR2D=1; off until measured on the
-  // GPU: the split half-sweeps) and its spare phi image
-  bool pair = false;
+  // the fused pair (k2_pair_box; AFH_PAIR2D=0: the split half-sweeps) and
+  // its spare phi image (config 1: 1.08-1.14 -> 0.85-0.87 ms per step,
+  // profiles/r04_push_ab.txt)
+  bool pair = true;
   double *alt = nullptr;
 };
 
@@ -1523,6 +1524,9 @@ static int32_t gsrb_boxes(afh_mg *mg, int lvl, bool up) {
       double *dst = (p & 1) ? phi : mg->alt;
       const Coef2 cf = mg->lvl_c[lvl - 1];
       const Bc4 g = t->bc4(mg->d.i_phi);
+      // timed on levels of >= 256 boxes, as the split half-sweeps
+      const int pc = n >= 256 ? AFH_PROF_GSRB : -1;
+      prof_mark(t, pc);
       if (t->nc == 4)
         hipLaunchKernelGGL(k2_pair_box<4>, dim3(n), dim3(64), 0, t->stream, src, dst,
                            t->ccv(mg->d.i_rhs), phi, t->d_boxes, t->ids.at(lvl), t->bsz, cf, g);
@@ -1533,6 +1537,8 @@ static int32_t gsrb_boxes(afh_mg *mg, int lvl, bool up) {
         hipLaunchKernelGGL(k2_pair_box<16>, dim3(n), dim3(64), 0, t->stream, src, dst,
                            t->ccv(mg->d.i_rhs), phi, t->d_boxes, t->ids.at(lvl), t->bsz, cf, g);
       H2_LAUNCH("k2_pair_box");
+      // a red+black pair reads phi and rhs and writes phi once = 24 B/cell
+      prof_end(t, pc, 24.0 * t->nc * t->nc * n);
     }
     if (up) {
       hipLaunchKernelGGL(k2_corners, dim3((4 * n + NT - 1) / NT), dim3(NT), 0, t->stream,

@@ -399,6 +399,12 @@ struct RbPar {
 // the level's last pair). The fill's x faces move one 128-B line per 8-B
 // value in each direction (3.1x their bytes); the push writes those values
 // from LDS, and the box's own x ghost cells come from its neighbours' pushes
+#ifndef AFH_PS_NT  // PS: the pushed / evaluated ghost stores non-temporal
+#define AFH_PS_NT AFH_NT_PAIR
+#endif
+#ifndef AFH_PS_ROW_NT  // PS: the row stores (without x ghost cells) non-temporal
+#define AFH_PS_ROW_NT AFH_NT_PAIR
+#endif
 template <bool NTL>
 __device__ __forceinline__ double ld_nt(const double *p) {
   if constexpr (NTL) return __builtin_nontemporal_load(p);
@@ -641,7 +647,7 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
         if (e < NG * TJ) {
           const int i = e % NG;
           if (i != 0 && i != NC + 1)
-            st_nt<AFH_NT_PAIR>(y + ((size_t)k * SK + t0 + NG + e), Pk[perm(NG + e)]);
+            st_nt<AFH_PS_ROW_NT>(y + ((size_t)k * SK + t0 + NG + e), Pk[perm(NG + e)]);
         }
       }
       for (int u = tid; u < 2 * TJ + 2 * NC; u += NT) {
@@ -670,21 +676,21 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
               v = own_gc(F2{}, p, jl, k, own);
             }
           }
-          st_nt<AFH_NT_PAIR>(at, v);
+          st_nt<AFH_PS_NT>(at, v);
         } else {
           const int w = u - 2 * TJ, hi = w / NC, ii = w - hi * NC + 1;
           const int nid = hi ? nb4 : nb3;
           auto own = [&](const int *c) { return Pk[L(c[1], ii)]; };
           if (nid > 0) {
-            st_nt<AFH_NT_PAIR>(dst + ((size_t)(nid - 1) * bsz + (size_t)k * SK +
+            st_nt<AFH_PS_NT>(dst + ((size_t)(nid - 1) * bsz + (size_t)k * SK +
                                       (size_t)(hi ? 0 : NC + 1) * NG + ii),
                                Pk[L(hi ? NC : 1, ii)]);
           } else if (!hi) {
             const int p[3] = {ii, 0, k};
-            st_nt<AFH_NT_PAIR>(y + ((size_t)k * SK + ii), own_gc(F3{}, p, ii, k, own));
+            st_nt<AFH_PS_NT>(y + ((size_t)k * SK + ii), own_gc(F3{}, p, ii, k, own));
           } else {
             const int p[3] = {ii, NC + 1, k};
-            st_nt<AFH_NT_PAIR>(y + ((size_t)k * SK + (size_t)(NC + 1) * NG + ii),
+            st_nt<AFH_PS_NT>(y + ((size_t)k * SK + (size_t)(NC + 1) * NG + ii),
                                own_gc(F4{}, p, ii, k, own));
           }
         }
@@ -715,12 +721,12 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
       const int jj = e / NC + 1, ii = e - (jj - 1) * NC + 1;
       const double x1v = X1[L(jj, ii)];
       if (nid > 0) {
-        st_nt<AFH_NT_PAIR>(dst + ((size_t)(nid - 1) * bsz +
+        st_nt<AFH_PS_NT>(dst + ((size_t)(nid - 1) * bsz +
                                   (size_t)(nb == 5 ? NC + 1 : 0) * SK + (size_t)jj * NG + ii),
                            x1v);
       } else {
         const int p[3] = {ii, jj, nb == 5 ? 0 : NC + 1};
-        st_nt<AFH_NT_PAIR>(y + ix3(NG, p[0], p[1], p[2]),
+        st_nt<AFH_PS_NT>(y + ix3(NG, p[0], p[1], p[2]),
                            own_gc(NBc, p, ii, jj, [&](const int *c) {
                              return (c[2] == 1 || c[2] == NC) ? x1v : X2[L(jj, ii)];
                            }));
@@ -2668,9 +2674,9 @@ struct afh_mg {
   bool cs_direct_small = true;
   int cs_ds_cells = CS_DS_CELLS;  // AFH_CS_DS_CELLS: its size limit (at most CS_SMALL_CELLS)
   bool pair_push = true;  // AFH_PAIR_PUSH: the small-box pair fills the faces
-  // (round 4; off until measured on the GPU: AFH_PROLONG_PUSH=1 / AFH_RSTR_PUSH=1)
-  bool prolong_push = false;  // AFH_PROLONG_PUSH: so does the small-box correction
-  bool rstr_push = false;     // AFH_RSTR_PUSH: and the small-box restriction
+  // (round 4: S3 1.71 -> 1.57 ms per step, profiles/r04_push_ab.txt)
+  bool prolong_push = true;  // AFH_PROLONG_PUSH: so does the small-box correction
+  bool rstr_push = true;     // AFH_RSTR_PUSH: and the small-box restriction
   // AFH_PAIR2_PUSH: the whole-box pair of bigger boxes (k_gsrb_pair2, TJ =
   // NC) fills the level's faces too (off until measured on the GPU)
   bool pair2_push = false;

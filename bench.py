@@ -379,7 +379,9 @@ def main():
     kname = ("k_gsrb_pair2<%d,%d>" % (CONFIGS[args.config][0], CONFIGS[args.config][0])
              if CONFIGS[args.config][0] > 16 else "k_gsrb_pair_box<%d>" % CONFIGS[args.config][0])
     if two_d:
-        kname = "k2_gsrb (half sweep, levels of >= 256 boxes, 16 B/cell)"
+        kname = ("k2_pair_box (red+black pair, levels of >= 256 boxes, 24 B/cell)"
+                 if os.environ.get("AFH_PAIR2D", "1") != "0" else
+                 "k2_gsrb (half sweep, levels of >= 256 boxes, 16 B/cell)")
     if nl.value == 0 and not two_d:
         # no level runs the fused pair (too few boxes per level, or
         # electrode stencils): the split half-sweep k_gsrb is the smoother
