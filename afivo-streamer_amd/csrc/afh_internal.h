@@ -221,8 +221,11 @@ int32_t gc_lvl(afh_tree *t, int lvl, int iv, int corners, bool rims = false);
 // hooks: HALO before, RIMS after when `rims` (the fused smoother reads the
 // replicas' ghost cells next) or when the next level has refinement
 // boundaries (its ghost cells read this level's replicas, ghosts included)
+// xrim: the x ghost cells facing same-level neighbours are current except
+// on rows 1, nc and planes 1, nc (k_gsrb_pair2<..., XR> stored them): only
+// those are filled
 int32_t gc_lvl_var(afh_tree *t, int lvl, int iv, const double *vc,
-                   const GcArgs &ga, int corners, bool rims = false);
+                   const GcArgs &ga, int corners, bool rims = false, bool xrim = false);
 // edges and corners only of level lvl (k_gc_corners), for a level whose
 // faces a producer kernel filled (the fused pair's pushed faces)
 int32_t gc_lvl_corners(afh_tree *t, int lvl, int iv);

@@ -384,34 +384,27 @@ struct RbPar {
 // plane below it (as tiles recompute halo rows) and stores its own planes
 // NTL: the streamed plane and rhs loads non-temporal (they are used once;
 // the lines phase B reads from neighbouring boxes should stay in L2)
-// PS (whole boxes, TJ = NC, KS = 1; levels without refinement boundaries):
-// the level's face fill after the pair is
-// done by the pair, as k_gsrb_pair_box<PUSH> does for small boxes. With a
-// plane's final values in LDS (its store, E), the box writes its boundary
-// cells into the ghost layers of its same-level neighbours' dst (x: the
-// row store's ghost cell goes to the neighbour instead; y: the rows facing
-// the neighbour), and its own ghost cells of physical / refinement faces
-// their gc_face_nocopy value; the z faces once planes 1, 2 (after step 3)
-// and NC-1, NC (after the march) are final. Every face ghost of dst then has
-// one writer, and no box reads dst during the pair (the neighbours read
-// src), so dst ends as the pair + k_gc_faces would leave it; edges and
-// corners are not written (the pairs read faces only; k_gc_corners follows
-// the level's last pair). The fill's x faces move one 128-B line per 8-B
-// value in each direction (3.1x their bytes); the push writes those values
-// from LDS, and the box's own x ghost cells come from its neighbours' pushes
-#ifndef AFH_PS_NT  // PS: the pushed / evaluated ghost stores non-temporal
-#define AFH_PS_NT AFH_NT_PAIR
-#endif
-#ifndef AFH_PS_ROW_NT  // PS: the row stores (without x ghost cells) non-temporal
-#define AFH_PS_ROW_NT AFH_NT_PAIR
-#endif
+// XR (whole boxes, TJ = NC, KS = 1): the x ghost cells the row stores carry
+// are the level fill's values wherever they can be formed inside the box's
+// own march, so that the fill after the pair skips those x faces (one
+// 128-B line per 8-B value on both sides, 3.1x their bytes). Facing a
+// same-level neighbour, the red ghosts are phase B's (the neighbour's new
+// red boundary cells); a black ghost is the neighbour's new black boundary
+// cell, which is formed here in the neighbour's C-phase expression from
+// this box's red boundary cell, phase B's red ghosts of the rows j-1, j+1
+// and the planes k-1, k+1, the neighbour's rhs and its red cell one column
+// further in -- recomputed from the neighbour's old values like phase B's
+// (lanes TJ+NC .. 2TJ+NC-1 in phase B; lanes 2TJ+NC .. 3TJ+NC-1 fetch the
+// rhs). Rows 1, NC and planes 1, NC (whose black ghosts need edge cells)
+// and faces without a same-level neighbour keep the fill (AFH_PAIR_XR; the
+// fill's x faces then only cover those cells).
 template <bool NTL>
 __device__ __forceinline__ double ld_nt(const double *p) {
   if constexpr (NTL) return __builtin_nontemporal_load(p);
   else return *p;
 }
 template <int NC, int TJ, int DEPTH = 2, int NTM = 0, bool FR = true, bool P3 = true,
-          bool SP = true, int KS = 1, bool NTL = false, bool PS = false>
+          bool SP = true, int KS = 1, bool NTL = false, bool XR = false>
 __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
     k_gsrb_pair2(const double *__restrict__ src, double *__restrict__ dst,
                  const double *__restrict__ rhs, const double *__restrict__ coarse,
@@ -422,8 +415,12 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
   constexpr int NG = G::NG, HN = G::HN, NT = G::NT, RPT = G::RPT, PL = G::PL,
                 EPT = G::EPT, OPT = G::OPT;
   constexpr size_t SK = (size_t)NG * NG;
-  static_assert(!PS || (TJ == NC && KS == 1 && FR), "the push form is whole boxes");
-  __shared__ double P[4][PL];  // planes s-2 .. s+1 at slot (plane & 3)
+  static_assert(!XR || (TJ == NC && KS == 1 && FR && P3), "XR: whole boxes");
+  static_assert(!XR || NT >= 3 * TJ + NC, "XR: lanes for the recomputed ghosts");
+  __shared__ double P[4][PL];
+  // XR: the neighbour's red cell one column in (RN) and its rhs at the
+  // boundary cell (RH) of the black ghost of each row, by plane parity
+  __shared__ double RNX[2][XR ? TJ : 1], RHX[2][XR ? TJ : 1];  // planes s-2 .. s+1 at slot (plane & 3)
   // LDS row layout. SP (split parity): each row holds its even-i cells, then
   // its odd-i cells, so the red (black) cells the lanes of a row update and
   // all their neighbours are unit-stride in LDS (no bank conflicts); the
@@ -510,19 +507,43 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
   // column (the last level fill), so its rows j+-1 and planes s+-1 are read
   // from LDS where they are interior cells of the neighbour (unchanged
   // black values); only phi next to it and rhs come from the neighbour
+  // XR: lanes TJ+NC .. 3TJ+NC-1 fetch the inputs of the recomputed black x
+  // ghost cells (kind 1: the neighbour's red cell one column in, 7 values;
+  // kind 2: its rhs at the boundary cell)
+  constexpr int NBL = XR ? 3 * TJ + NC : TJ + NC;
   struct BDesc {
-    int i, j, jl, nb, rep;  // nb 0: none
+    int i, j, jl, nb, rep, kind;  // nb 0: none
     bool pre, lm, lp, zm, zp;
     const double *xs, *rs;
     size_t c;
   };
   auto bdesc = [&](int s) {
     BDesc b;
-    b.i = b.j = b.jl = b.nb = 0;
+    b.i = b.j = b.jl = b.nb = b.kind = 0;
     b.rep = -1;
     b.pre = b.lm = b.lp = b.zm = b.zp = false;
     b.xs = b.rs = nullptr;
     b.c = 0;
+    if (XR && s >= k0 && s <= k1 && tid >= TJ + NC && tid < NBL) {
+      // the row's black ghost cell of plane s is on the low side when
+      // (j + s) is even; the neighbour's cell one column in (kind 1) is red
+      const int w = tid - (TJ + NC);
+      b.kind = w < TJ ? 1 : 2;
+      b.jl = w % TJ + 1;
+      b.j = j0 + b.jl - 1;
+      const bool lowside = ((b.j + s) & 1) == 0;
+      const int nb_id = lowside ? nb1 : nb2;
+      if (nb_id > 0) {
+        b.nb = lowside ? 1 : 2;
+        b.i = lowside ? 0 : NC + 1;
+        const int qi = b.kind == 1 ? (lowside ? NC - 1 : 2) : (lowside ? NC : 1);
+        b.xs = src + (size_t)(nb_id - 1) * bsz;
+        b.rs = rhs + (size_t)(nb_id - 1) * bsz;
+        b.pre = true;
+        b.c = ix3(NG, qi, b.j, s);
+      }
+      return b;
+    }
     if (s >= k0 && s <= k1 && tid < TJ + NC) {
       const int u = tid;
       if (u < TJ) {
@@ -576,7 +597,7 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
     BIn b;
 #pragma unroll
     for (int q = 0; q < 7; q++) b.bl[q] = 0.0;
-    if (s >= k0 && s <= k1 && tid < TJ + NC) {
+    if (s >= k0 && s <= k1 && tid < NBL) {
       // values taken from LDS or replaced later re-read cell c (no extra
       // cache line)
       const double *xs = d.pre ? d.xs : x, *rs = d.pre ? d.rs : r;
@@ -623,79 +644,8 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
   if (DEPTH == 2) load_pf(X0, s0 + 2);
 
   // E: plane k of the tile to dst (in full rows with FR)
-  // PS: a face ghost p of this box on a physical boundary, from the final
-  // values own(q) next to it (the push form runs on levels without
-  // refinement boundaries; the face a compile-time constant, so that
-  // gc_face_nocopy_k's per-dimension indexing stays in registers)
-  auto own_gc = [&](auto NBc, const int p[3], int a, int b, auto own) {
-    constexpr int nb = decltype(NBc)::value;
-    return gc_face_nocopy_k(coarse, meta, m, nb, -1, drof(nb), p, a, b, NC, bsz, bcof(nb),
-                            ga.rb, own);
-  };
-  using F1 = std::integral_constant<int, 1>;
-  using F2 = std::integral_constant<int, 2>;
-  using F3 = std::integral_constant<int, 3>;
-  using F4 = std::integral_constant<int, 4>;
   auto store_plane = [&](const int k, const double *Pk) {
-    if (PS) {
-      // rows 1..NC without their x ghost cells; then the x ghost cells (2 TJ
-      // entries: pushed into the neighbour, or evaluated) and the y ghost
-      // rows (2 NC)
-#pragma unroll
-      for (int q = 0; q < G::OPTF; q++) {
-        const int e = tid + NT * q;
-        if (e < NG * TJ) {
-          const int i = e % NG;
-          if (i != 0 && i != NC + 1)
-            st_nt<AFH_PS_ROW_NT>(y + ((size_t)k * SK + t0 + NG + e), Pk[perm(NG + e)]);
-        }
-      }
-      for (int u = tid; u < 2 * TJ + 2 * NC; u += NT) {
-        if (u < 2 * TJ) {
-          const int jl = (u >> 1) + 1;
-          auto own = [&](const int *c) { return Pk[L(jl, c[0])]; };
-          double *at;
-          double v;
-          if (!(u & 1)) {
-            if (nb1 > 0) {
-              // this box's boundary cell into the neighbour's ghost cell
-              at = dst + ((size_t)(nb1 - 1) * bsz + (size_t)k * SK + (size_t)jl * NG + NC + 1);
-              v = Pk[L(jl, 1)];
-            } else {
-              const int p[3] = {0, jl, k};
-              at = y + ((size_t)k * SK + (size_t)jl * NG);
-              v = own_gc(F1{}, p, jl, k, own);
-            }
-          } else {
-            if (nb2 > 0) {
-              at = dst + ((size_t)(nb2 - 1) * bsz + (size_t)k * SK + (size_t)jl * NG);
-              v = Pk[L(jl, NC)];
-            } else {
-              const int p[3] = {NC + 1, jl, k};
-              at = y + ((size_t)k * SK + (size_t)jl * NG + NC + 1);
-              v = own_gc(F2{}, p, jl, k, own);
-            }
-          }
-          st_nt<AFH_PS_NT>(at, v);
-        } else {
-          const int w = u - 2 * TJ, hi = w / NC, ii = w - hi * NC + 1;
-          const int nid = hi ? nb4 : nb3;
-          auto own = [&](const int *c) { return Pk[L(c[1], ii)]; };
-          if (nid > 0) {
-            st_nt<AFH_PS_NT>(dst + ((size_t)(nid - 1) * bsz + (size_t)k * SK +
-                                      (size_t)(hi ? 0 : NC + 1) * NG + ii),
-                               Pk[L(hi ? NC : 1, ii)]);
-          } else if (!hi) {
-            const int p[3] = {ii, 0, k};
-            st_nt<AFH_PS_NT>(y + ((size_t)k * SK + ii), own_gc(F3{}, p, ii, k, own));
-          } else {
-            const int p[3] = {ii, NC + 1, k};
-            st_nt<AFH_PS_NT>(y + ((size_t)k * SK + (size_t)(NC + 1) * NG + ii),
-                               own_gc(F4{}, p, ii, k, own));
-          }
-        }
-      }
-    } else if (FR) {
+    if (FR) {
 #pragma unroll
       for (int q = 0; q < G::OPTF; q++) {
         const int e = tid + NT * q;
@@ -712,27 +662,6 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
       }
     }
   };
-  // PS: z face ghost plane (nb 5: plane 0 from planes 1, 2; nb 6: plane NC+1
-  // from planes NC, NC-1), pushed into the neighbour or evaluated
-  auto store_zface = [&](auto NBc, const double *X1, const double *X2) {
-    constexpr int nb = decltype(NBc)::value;
-    const int nid = nb == 5 ? nb5 : nb6;
-    for (int e = tid; e < NC * NC; e += NT) {
-      const int jj = e / NC + 1, ii = e - (jj - 1) * NC + 1;
-      const double x1v = X1[L(jj, ii)];
-      if (nid > 0) {
-        st_nt<AFH_PS_NT>(dst + ((size_t)(nid - 1) * bsz +
-                                  (size_t)(nb == 5 ? NC + 1 : 0) * SK + (size_t)jj * NG + ii),
-                           x1v);
-      } else {
-        const int p[3] = {ii, jj, nb == 5 ? 0 : NC + 1};
-        st_nt<AFH_PS_NT>(y + ix3(NG, p[0], p[1], p[2]),
-                           own_gc(NBc, p, ii, jj, [&](const int *c) {
-                             return (c[2] == 1 || c[2] == NC) ? x1v : X2[L(jj, ii)];
-                           }));
-      }
-    }
-  };
   // Step s. P3 (three barriers): A (red cells of plane s) with E of plane
   // s-2 | B (red ghosts of plane s: they are first read by C of step s+1)
   // with C (black cells of plane s-1) | D. At s = 2 and NC+1 the z ghost
@@ -743,7 +672,8 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
     load_pf(ld, s + 1 + DEPTH);
     double *bl = bc.bl;
     const BDesc bd = bdesc(s);
-    const int b_i = bd.i, b_j = bd.j, b_jl = bd.jl, b_nb = bd.nb, b_rep = bd.rep;
+    const int b_i = bd.i, b_j = bd.j, b_jl = bd.jl, b_nb = bd.nb, b_rep = bd.rep,
+              b_kind = bd.kind;
     const bool b_pre = bd.pre, b_lm = bd.lm, b_lp = bd.lp, b_zm = bd.zm, b_zp = bd.zp;
     double *Pm = P[(s - 1) & 3], *P0 = P[s & 3], *Pp = P[(s + 1) & 3];
     double *Pmm = P[(s - 2) & 3];
@@ -796,7 +726,12 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
                              b_i, b_j, s, b_i, s, bsz, cf, inv_c1, bcof(b_nb), ga.rb,
                              P0[L(l1, b_i)], P0[L(l2, b_i)]);
       }
-      P0[L(b_jl, b_i)] = v;
+      if (XR && b_kind == 1)
+        RNX[s & 1][b_jl - 1] = v;
+      else if (XR && b_kind == 2)
+        RHX[s & 1][b_jl - 1] = bl[6];
+      else
+        P0[L(b_jl, b_i)] = v;
     }
     if (s == 2 || s == NC + 1) {
       // z ghost plane 0 (NC+1): red cells; x1 = plane 1 (NC), black, old;
@@ -815,6 +750,25 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
       if (P3) __syncthreads();
     }
     if (!P3) __syncthreads();
+    // XR: the black x ghost cell of each row of plane s-1 (rows and planes
+    // 2 .. NC-1), the neighbour's C-phase expression (its x-1 / x+1 values:
+    // RN or this box's red boundary cell; its rows j+-1 and planes s-2, s:
+    // phase B's red ghosts). C reads no black ghost cell
+    if (XR && tid >= TJ + NC && tid < 2 * TJ + NC) {
+      const int jl = tid - (TJ + NC) + 1, k = s - 1;
+      if (k >= 2 && k <= NC - 1 && jl >= 2 && jl <= NC - 1) {
+        const bool lowside = ((jl + k) & 1) == 0;
+        if ((lowside ? nb1 : nb2) > 0) {
+          const int g = lowside ? 0 : NC + 1;
+          const double rn = RNX[k & 1][jl - 1], me = Pm[L(jl, lowside ? 1 : NC)];
+          const double xm = lowside ? rn : me, xp = lowside ? me : rn;
+          Pm[L(jl, g)] = (RHX[k & 1][jl - 1] - cf.c[1] * xm - cf.c[2] * xp -
+                          cf.c[3] * Pm[L(jl - 1, g)] - cf.c[4] * Pm[L(jl + 1, g)] -
+                          cf.c[5] * Pmm[L(jl, g)] - cf.c[6] * P0[L(jl, g)]) *
+                         inv_c1;
+        }
+      }
+    }
     // C: black cells of plane s-1, in place
     if (s - 1 >= k0 && s - 1 <= k1) {
 #pragma unroll
@@ -831,11 +785,6 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
     __syncthreads();
     // E (without P3): plane s-1; D: plane s+2 into the slot of plane s-2
     if (!P3 && s - 1 >= k0 && s - 1 <= k1) store_plane(s - 1, Pm);
-    if (PS && s == 3) {
-      // planes 1 (Pmm) and 2 (Pm) are final; D overwrites plane 1's slot
-      store_zface(std::integral_constant<int, 5>{}, Pmm, Pm);
-      __syncthreads();
-    }
     if (s + 2 <= NC + 1 && s + 2 <= k1 + 2) {
 #pragma unroll
       for (int e = 0; e < EPT; e++) {
@@ -863,7 +812,6 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
     }
   }
   if (P3) store_plane(k1, P[k1 & 3]);
-  if (PS) store_zface(std::integral_constant<int, 6>{}, P[NC & 3], P[(NC - 1) & 3]);
 }
 
 // Whole-box form of the fused pair for small boxes (NC <= 16): the box, its
@@ -2677,9 +2625,9 @@ struct afh_mg {
   // (round 4: S3 1.71 -> 1.57 ms per step, profiles/r04_push_ab.txt)
   bool prolong_push = true;  // AFH_PROLONG_PUSH: so does the small-box correction
   bool rstr_push = true;     // AFH_RSTR_PUSH: and the small-box restriction
-  // AFH_PAIR2_PUSH: the whole-box pair of bigger boxes (k_gsrb_pair2, TJ =
-  // NC) fills the level's faces too (off until measured on the GPU)
-  bool pair2_push = false;
+  // AFH_PAIR_XR: the whole-box pair of bigger boxes (k_gsrb_pair2, TJ = NC)
+  // stores the fill's x ghost cells (off until measured on the GPU)
+  bool pair_xr = false;
   int tiles_min = 256;  // AFH_PAIR_TILES_MIN: levels of fewer boxes run tiles (NC >= 32)
   int *d_cycles = nullptr;
   int cycles_host = 0;
@@ -2966,7 +2914,7 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
   if (const char *env = getenv("AFH_PAIR_PUSH")) mg->pair_push = atoi(env) != 0;
   if (const char *env = getenv("AFH_PROLONG_PUSH")) mg->prolong_push = atoi(env) != 0;
   if (const char *env = getenv("AFH_RSTR_PUSH")) mg->rstr_push = atoi(env) != 0;
-  if (const char *env = getenv("AFH_PAIR2_PUSH")) mg->pair2_push = atoi(env) != 0;
+  if (const char *env = getenv("AFH_PAIR_XR")) mg->pair_xr = atoi(env) != 0;
   if (const char *env = getenv("AFH_PAIR_TILES_MIN")) mg->tiles_min = atoi(env);
   AFH_HIP(hipMalloc(&mg->cs_iters, sizeof(int)));
   AFH_HIP(hipMalloc(&mg->d_cycles, sizeof(int)));
@@ -3090,14 +3038,13 @@ static bool pair_tiles(const afh_mg *mg, int lvl) {
   return mg->t->nc >= 32 && (mg->force_tiles || n < mg->tiles_min);
 }
 
-// the whole-box pair of boxes of 16^3 and up pushes the level's faces
-// (k_gsrb_pair2<..., PS>): its default forms only (none of the AFH_GSRB_PAIR_*
-// experiments), not on a sharded tree (a replica's ghosts are its owner's)
-static bool pair2_push(const afh_mg *mg, int lvl) {
+// the whole-box pair of boxes of 16^3 and up stores the x ghost cells the
+// level fill would give (k_gsrb_pair2<..., XR>; the fill then skips them):
+// its default forms only (none of the AFH_GSRB_PAIR_* experiments), not on a
+// sharded tree (a replica's ghosts are its owner's)
+static bool pair2_xr(const afh_mg *mg, int lvl) {
   const int nc = mg->t->nc;
-  if (!mg->pair2_push || mg->t->hook || mg->pair_v1 || nc < 16) return false;
-  // physical faces only (no refinement boundaries on the level)
-  if (lvl >= 2 && mg->t->lvl_rb_coarse[lvl - 2]) return false;
+  if (!mg->pair_xr || mg->t->hook || mg->pair_v1 || nc < 16) return false;
   if (nc == 16) return !mg->pair_box;
   if (pair_tiles(mg, lvl)) return false;
   if (nc == 32) return true;
@@ -3106,11 +3053,11 @@ static bool pair2_push(const afh_mg *mg, int lvl) {
 }
 
 template <int NC, int TJ, int DEPTH, int NTM = 0, bool FR = true, bool P3 = true,
-          bool SP = true, int KS = 1, bool NTL = false, bool PS = false>
+          bool SP = true, int KS = 1, bool NTL = false, bool XR = false>
 static void launch_pair2(afh_mg *mg, int lvl, const double *src, double *dst,
                          const Coef &cf, double inv_c1, hipEvent_t e0, hipEvent_t e1) {
   afh_tree *t = mg->t;
-  launch_ev((k_gsrb_pair2<NC, TJ, DEPTH, NTM, FR, P3, SP, KS, NTL, PS>), e0, e1,
+  launch_ev((k_gsrb_pair2<NC, TJ, DEPTH, NTM, FR, P3, SP, KS, NTL, XR>), e0, e1,
             dim3(t->ids.n(lvl) * RbPar<NC, TJ, NTM>::NTILE * KS),
             dim3(RbPar<NC, TJ, NTM>::NT), t->stream, src, dst, t->ccv(mg->d.i_rhs),
             t->ccv(mg->d.i_phi), t->d_boxes, t->ids.at(lvl), t->bsz, cf, inv_c1,
@@ -3144,7 +3091,7 @@ static void launch_pair(afh_mg *mg, int lvl, const double *src, double *dst,
     }
   }
   if constexpr (NC >= 16) {
-    if (pair2_push(mg, lvl)) {
+    if (pair2_xr(mg, lvl)) {
       if constexpr (NC == 64)
         return launch_pair2<NC, NC, 1, 0, true, true, true, 1, false, true>(mg, lvl, src, dst,
                                                                             cf, inv_c1, e0, e1);
@@ -3348,11 +3295,12 @@ static int32_t gsrb_boxes(afh_mg *mg, int lvl, bool up, bool stale_ghosts = fals
     if (timed) prof_count(t, 24.0 * nc * nc * nc * nid);
     AFH_LAUNCH_CHECK("k_gsrb_pair");
     (void)dst;
-    if (pair_push(mg) || pair2_push(mg, lvl)) {
+    if (pair_push(mg)) {
       // the pair filled the faces; edges and corners on the leg's last pair
       if (up && n == n_cycle)
         if (int32_t e = gc_lvl_corners(t, lvl, dst_iv)) return e;
-    } else if (int32_t e = gc_lvl_var(t, lvl, dst_iv, phi, ga, up && n == n_cycle, true)) {
+    } else if (int32_t e = gc_lvl_var(t, lvl, dst_iv, phi, ga, up && n == n_cycle, true,
+                                      pair2_xr(mg, lvl))) {
       return e;
     }
   }

@@ -97,7 +97,7 @@ __global__ void k_gc_faces(double *__restrict__ v,
                            const double *__restrict__ vc,
                            const afh_box_meta *__restrict__ meta,
                            const int32_t *__restrict__ ids, int nc, size_t bsz,
-                           GcArgs ga, int xpair) {
+                           GcArgs ga, int xpair, int xrim) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= nc * nc) return;
   const int id = ids[blockIdx.z];
@@ -124,6 +124,8 @@ __global__ void k_gc_faces(double *__restrict__ v,
   const size_t dst = ix3(ng, p[0], p[1], p[2]);
 
   if (nb_id > 0) {
+    // xrim: the pair stored this x ghost cell (gc_lvl_var)
+    if (xrim && d == 0 && a != 1 && a != nc && b != 1 && b != nc) return;
     if (xpair && d == 0 && meta[nb_id - 1].lvl > 0) {
       // x interface with a stored same-level box, copied both ways by the
       // low-x thread of the box on its high side: its own ghost (0, a, b)
@@ -393,7 +395,7 @@ int32_t call_hook(afh_tree *t, int kind, int lvl, int iv, double *vals, int n) {
 }
 
 int32_t gc_lvl_var(afh_tree *t, int lvl, int iv, const double *vc,
-                   const GcArgs &ga, int corners, bool rims) {
+                   const GcArgs &ga, int corners, bool rims, bool xrim) {
   const int n = t->ids.n(lvl);
   double *v = t->var(iv);
   int32_t e;
@@ -401,7 +403,7 @@ int32_t gc_lvl_var(afh_tree *t, int lvl, int iv, const double *vc,
   if (n > 0) {
     const int nc = t->nc;
     prof_begin(t, AFH_PROF_GHOST);
-    if (t->gc_box && (nc == 4 || nc == 8 || nc == 16)) {
+    if (t->gc_box && !xrim && (nc == 4 || nc == 8 || nc == 16)) {
       const int cr = corners ? 1 : 0;
       if (nc == 4)
         hipLaunchKernelGGL(k_gc_box<4>, dim3(n), dim3(16), 0, t->stream, v, vc, t->d_boxes,
@@ -415,13 +417,13 @@ int32_t gc_lvl_var(afh_tree *t, int lvl, int iv, const double *vc,
       prof_end(t, AFH_PROF_GHOST, 16.0 * 6 * nc * nc * n);
       AFH_LAUNCH_CHECK("k_gc_box");
     } else {
-      if (t->gc_faces6 == 1 || (t->gc_faces6 < 0 && nc <= 16))
+      if (!xrim && (t->gc_faces6 == 1 || (t->gc_faces6 < 0 && nc <= 16)))
         hipLaunchKernelGGL(k_gc_faces6, dim3((nc * nc + 255) / 256, n), dim3(256), 0,
                            t->stream, v, vc, t->d_boxes, t->ids.at(lvl), nc, t->bsz, ga);
       else
         hipLaunchKernelGGL(k_gc_faces, dim3((nc * nc + 255) / 256, 6, n), dim3(256), 0,
                            t->stream, v, vc, t->d_boxes, t->ids.at(lvl), nc, t->bsz, ga,
-                           t->gc_xpair);
+                           t->gc_xpair, xrim ? 1 : 0);
       // algorithmic bytes: read one interior layer + write one ghost layer
       prof_end(t, AFH_PROF_GHOST, 16.0 * 6 * nc * nc * n);
       AFH_LAUNCH_CHECK("k_gc_faces");
@@ -1544,7 +1546,7 @@ int32_t afh_tree_regrid(afh_tree *o, const afh_tree_desc *d, afh_tree **out) {
     for (int iv : t->auto_vars) {
       hipLaunchKernelGGL(k_gc_faces, dim3((nc * nc + 255) / 256, 6, n), dim3(256), 0,
                          t->stream, t->ccv(iv), t->ccv(iv), t->d_boxes, d_list, nc,
-                         t->bsz, t->gc_args(iv), 0);  // new boxes only: no pairing
+                         t->bsz, t->gc_args(iv), 0, 0);  // new boxes only: no pairing
       AFH_LAUNCH_CHECK("k_gc_faces");
       hipLaunchKernelGGL(k_gc_corners, dim3(n), dim3(256), 0, t->stream, t->ccv(iv),
                          t->d_boxes, d_list, nc, t->bsz);

@@ -24,11 +24,12 @@ Round 4:
   (k_parent_rhs_box) vs k_rstr_fas_col + a level fill + k_parent_rhs --
   on S1, on a tree of 8^3 boxes and on the S3 and S5 AMR trees (refinement
   boundaries on every level, physical faces);
-* AFH_PAIR2_PUSH: the whole-box pair of 16^3 .. 64^3 boxes (k_gsrb_pair2
-  PS) writes the level's face ghosts itself vs the pair + k_gc_faces -- on
-  S1-64 (BASELINE's headline tree, 512 leaf boxes of 64^3), a tree of 32^3
-  boxes, and AMR trees of 16^3 and 32^3 boxes (every level whole-box pairs;
-  the levels with refinement boundaries keep the fill).
+* AFH_PAIR_XR: the whole-box pair of 16^3 .. 64^3 boxes (k_gsrb_pair2 XR)
+  stores the x ghost cells the level fill gives (the neighbours' new black
+  boundary cells recomputed) and the fill skips them, vs the pair + the full
+  fill -- on S1-64 (BASELINE's headline tree, 512 leaf boxes of 64^3), a
+  tree of 32^3 boxes, and AMR trees of 16^3 and 32^3 boxes (every level
+  whole-box pairs; refinement boundaries and physical faces).
 
 The fused forms are also what every other GPU test runs (they are the
 defaults); these tests pin them to the unfused forms on full workloads.
@@ -249,22 +250,22 @@ def test_gradient_folded_into_residual_bitwise(config, monkeypatch):
 
 
 @pytest.mark.parametrize("config", ["c32l4", "s1-64"])
-def test_pair2_push_bitwise(config, monkeypatch):
-    """The whole-box pair with its pushed face fills (AFH_PAIR2_PUSH) on
+def test_pair_xr_bitwise(config, monkeypatch):
+    """The whole-box pair storing the fill's x ghost cells (AFH_PAIR_XR) on
     512 leaf boxes of 32^3 and 64^3 (physical faces on the domain sides): the
     field solve and four unit steps, every variable bitwise the pair + fill."""
     import bench
     monkeypatch.setitem(bench.CONFIGS, "c32l4", (32, (32, 32, 32), 4, (8e-3, 8e-3, 8e-3)))
-    _same(_s1(monkeypatch, {"AFH_PAIR2_PUSH": "1"}, config),
-          _s1(monkeypatch, {"AFH_PAIR2_PUSH": "0"}, config))
+    _same(_s1(monkeypatch, {"AFH_PAIR_XR": "1"}, config),
+          _s1(monkeypatch, {"AFH_PAIR_XR": "0"}, config))
 
 
 @pytest.mark.parametrize("name", ["amr16", "amr32"])
-def test_pair2_push_bitwise_amr(name, monkeypatch):
+def test_pair_xr_bitwise_amr(name, monkeypatch):
     """AMR trees of 16^3 (the plane-marching pair, AFH_GSRB_PAIR_BOX=0) and
-    32^3 boxes, every level of two or more boxes smoothed by whole-box
-    pairs: the fully refined levels push, the levels with refinement
-    boundaries keep the fill. Two field solves and a Heun step, bitwise."""
+    32^3 boxes, every level of two or more boxes smoothed by whole-box pairs
+    (AFH_PAIR_XR; refinement-boundary and physical x faces keep the fill).
+    Two field solves and a Heun step, bitwise."""
     from afh import capi
     from afh.streamer import IV
     from afh.tree import build_tree
@@ -277,7 +278,7 @@ def test_pair2_push_bitwise_amr(name, monkeypatch):
     monkeypatch.setenv("AFH_PAIR_TILES_MIN", "1")
     outs = []
     for v in ("1", "0"):
-        monkeypatch.setenv("AFH_PAIR2_PUSH", v)
+        monkeypatch.setenv("AFH_PAIR_XR", v)
         c = make(capi.hip_library(), topo, 0, True)
         out = {"res0": c.field_compute(0, check_residual=False)}
         out["l0"] = list(c.fluid.forward_euler(1e-12, 0, [0], [1.0], 1, False, True))
