@@ -420,7 +420,7 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
   __shared__ double P[4][PL];
   // XR: the neighbour's red cell one column in (RN) and its rhs at the
   // boundary cell (RH) of the black ghost of each row, by plane parity
-  __shared__ double RNX[2][XR ? TJ : 1], RHX[2][XR ? TJ : 1];  // planes s-2 .. s+1 at slot (plane & 3)
+  __shared__ double RNX[2][XR ? TJ : 1], RHX[2][XR ? TJ : 1], ZMX[XR ? TJ : 1];  // planes s-2 .. s+1 at slot (plane & 3)
   // LDS row layout. SP (split parity): each row holds its even-i cells, then
   // its odd-i cells, so the red (black) cells the lanes of a row update and
   // all their neighbours are unit-stride in LDS (no bank conflicts); the
@@ -751,23 +751,20 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
     }
     if (!P3) __syncthreads();
     // XR: the black x ghost cell of each row of plane s-1 (rows and planes
-    // 2 .. NC-1), the neighbour's C-phase expression (its x-1 / x+1 values:
-    // RN or this box's red boundary cell; its rows j+-1 and planes s-2, s:
-    // phase B's red ghosts). C reads no black ghost cell
-    if (XR && tid >= TJ + NC && tid < 2 * TJ + NC) {
-      const int jl = tid - (TJ + NC) + 1, k = s - 1;
-      if (k >= 2 && k <= NC - 1 && jl >= 2 && jl <= NC - 1) {
-        const bool lowside = ((jl + k) & 1) == 0;
-        if ((lowside ? nb1 : nb2) > 0) {
-          const int g = lowside ? 0 : NC + 1;
-          const double rn = RNX[k & 1][jl - 1], me = Pm[L(jl, lowside ? 1 : NC)];
-          const double xm = lowside ? rn : me, xp = lowside ? me : rn;
-          Pm[L(jl, g)] = (RHX[k & 1][jl - 1] - cf.c[1] * xm - cf.c[2] * xp -
-                          cf.c[3] * Pm[L(jl - 1, g)] - cf.c[4] * Pm[L(jl + 1, g)] -
-                          cf.c[5] * Pmm[L(jl, g)] - cf.c[6] * P0[L(jl, g)]) *
-                         inv_c1;
-        }
-      }
+    // 2 .. NC-1) is formed after the barrier that ends B (plane s's red
+    // ghosts) and C; its plane s-2 input is set aside here (D overwrites
+    // that slot)
+    auto xr_at = [&](int &jl, int &g) {
+      jl = tid - (TJ + NC) + 1;
+      const int k = s - 1;
+      const bool low = ((jl + k) & 1) == 0;
+      g = low ? 0 : NC + 1;
+      return XR && tid >= TJ + NC && tid < 2 * TJ + NC && k >= 2 && k <= NC - 1 && jl >= 2 &&
+             jl <= NC - 1 && (low ? nb1 : nb2) > 0;
+    };
+    {
+      int jl, g;
+      if (xr_at(jl, g)) ZMX[jl - 1] = Pmm[L(jl, g)];
     }
     // C: black cells of plane s-1, in place
     if (s - 1 >= k0 && s - 1 <= k1) {
@@ -783,6 +780,22 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
       }
     }
     __syncthreads();
+    {
+      // the neighbour's C-phase expression: its x-1 / x+1 values RN or this
+      // box's red boundary cell, its rows j+-1 and planes s-2, s phase B's
+      // red ghosts, its rhs. D writes neither Pm nor P0; plane s-1 is stored
+      // after the next barrier
+      int jl, g;
+      if (xr_at(jl, g)) {
+        const int kb = (s - 1) & 1;
+        const double rn = RNX[kb][jl - 1], me = Pm[L(jl, g == 0 ? 1 : NC)];
+        const double xm = g == 0 ? rn : me, xp = g == 0 ? me : rn;
+        Pm[L(jl, g)] = (RHX[kb][jl - 1] - cf.c[1] * xm - cf.c[2] * xp -
+                        cf.c[3] * Pm[L(jl - 1, g)] - cf.c[4] * Pm[L(jl + 1, g)] -
+                        cf.c[5] * ZMX[jl - 1] - cf.c[6] * P0[L(jl, g)]) *
+                       inv_c1;
+      }
+    }
     // E (without P3): plane s-1; D: plane s+2 into the slot of plane s-2
     if (!P3 && s - 1 >= k0 && s - 1 <= k1) store_plane(s - 1, Pm);
     if (s + 2 <= NC + 1 && s + 2 <= k1 + 2) {
