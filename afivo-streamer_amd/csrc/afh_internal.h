@@ -136,6 +136,9 @@ struct afh_tree {
   // (S1 leaf fill 13.5 -> 11.8 us); at 64^3 it measured 134 -> 129 us per
   // fill but the step no faster, so k_gc_faces stays (AFH_GC_FACES6=0/1)
   int gc_faces6 = -1;
+  // boxes of 32^3 and up: level face fills with 8 ghost values per thread
+  // (k_gc_faces_r; AFH_GC_FACES_R=1: one per thread, k_gc_faces)
+  int gc_faces_r = 8;
   // boxes up to 16^3: faces, edges and corners of a level in one launch
   // (k_gc_box, AFH_GC_BOX=0 for the two-launch form)
   bool gc_box = true;

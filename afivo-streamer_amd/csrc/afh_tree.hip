@@ -156,6 +156,60 @@ __global__ void k_gc_faces(double *__restrict__ v,
                           });
 }
 
+// k_gc_faces with R ghost values per thread ((a, b .. b+R-1) of one face):
+// the R source values (a neighbour's boundary cells, or gc_face_nocopy's
+// boundary / refinement values) are loaded before the R stores. One value per
+// thread leaves a 64^3 leaf fill latency-bound (49 152 workgroups of one
+// dependent load each); this form has R times fewer. Same values as
+// k_gc_faces (xrim as there; no x-interface pairing).
+template <int R>
+__global__ void __launch_bounds__(256)
+    k_gc_faces_r(double *__restrict__ v, const double *__restrict__ vc,
+                 const afh_box_meta *__restrict__ meta, const int32_t *__restrict__ ids, int nc,
+                 size_t bsz, GcArgs ga, int xrim) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nc * (nc / R)) return;
+  const int id = ids[blockIdx.z];
+  const int nb = blockIdx.y + 1;
+  const int d = (nb - 1) >> 1;
+  const bool low = ((nb - 1) & 1) == 0;
+  const int ta = (d == 0) ? 1 : 0, tb = (d == 2) ? 1 : 2;
+  const int a = t % nc + 1, b0 = (t / nc) * R + 1;
+  const int ng = nc + 2;
+  const afh_box_meta &m = meta[id - 1];
+  double *c = v + (size_t)(id - 1) * bsz;
+  const int nb_id = m.neighbors[nb - 1];
+  double val[R];
+  size_t dst[R];
+  bool on[R];
+#pragma unroll
+  for (int q = 0; q < R; q++) {
+    const int b = b0 + q;
+    int p[3];
+    p[ta] = a;
+    p[tb] = b;
+    p[d] = low ? 0 : nc + 1;
+    dst[q] = ix3(ng, p[0], p[1], p[2]);
+    on[q] = true;
+    if (nb_id > 0) {
+      if (xrim && d == 0 && a != 1 && a != nc && b != 1 && b != nc) {
+        on[q] = false;
+        val[q] = 0.0;
+        continue;
+      }
+      int s[3] = {p[0], p[1], p[2]};
+      s[d] = low ? nc : 1;
+      val[q] = v[(size_t)(nb_id - 1) * bsz + ix3(ng, s[0], s[1], s[2])];
+    } else {
+      val[q] = gc_face_nocopy(vc, meta, m, nb, p, a, b, nc, bsz, ga.bc[nb - 1], ga.rb,
+                              [&](const int *qq) { return c[ix3(ng, qq[0], qq[1], qq[2])]; });
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < R; q++)
+    if (on[q]) c[dst[q]] = val[q];
+}
+
 // The six faces of a box by one thread per (a, b): the six ghost values are
 // loaded (neighbour copies, or gc_face_nocopy's boundary / refinement
 // values, which read only interior and coarse cells) before the six stores,
@@ -420,6 +474,10 @@ int32_t gc_lvl_var(afh_tree *t, int lvl, int iv, const double *vc,
       if (!xrim && (t->gc_faces6 == 1 || (t->gc_faces6 < 0 && nc <= 16)))
         hipLaunchKernelGGL(k_gc_faces6, dim3((nc * nc + 255) / 256, n), dim3(256), 0,
                            t->stream, v, vc, t->d_boxes, t->ids.at(lvl), nc, t->bsz, ga);
+      else if (t->gc_faces_r > 1 && nc >= 32 && !t->gc_xpair)
+        hipLaunchKernelGGL(k_gc_faces_r<8>, dim3((nc * (nc / 8) + 255) / 256, 6, n), dim3(256),
+                           0, t->stream, v, vc, t->d_boxes, t->ids.at(lvl), nc, t->bsz, ga,
+                           xrim ? 1 : 0);
       else
         hipLaunchKernelGGL(k_gc_faces, dim3((nc * nc + 255) / 256, 6, n), dim3(256), 0,
                            t->stream, v, vc, t->d_boxes, t->ids.at(lvl), nc, t->bsz, ga,
@@ -869,6 +927,7 @@ static int32_t tree_create_impl(const afh_tree_desc *d, int32_t device,
   if (const char *env = getenv("AFH_GC_FACES6")) t->gc_faces6 = atoi(env) != 0;
   else t->gc_faces6 = -1;  // by box size
   if (const char *env = getenv("AFH_GC_XPAIR")) t->gc_xpair = atoi(env) != 0;
+  if (const char *env = getenv("AFH_GC_FACES_R")) t->gc_faces_r = atoi(env);
   if (device >= 0) {
     AFH_HIP(hipSetDevice(device));
     t->device = device;
