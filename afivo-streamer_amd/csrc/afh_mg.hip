@@ -1732,17 +1732,36 @@ __global__ void k_box_copy(const double *__restrict__ src,
 
 // stencil_prolong_248 add, a column of K cells along k per thread: the
 // K/2 + 2 parent planes the column touches are loaded once (4 values each)
-template <int K>
+// GX: the rows are NC+2 wide, and the x ghost cells facing a same-level
+// neighbour get the same correction (rows and planes 2 .. NC-1): the ghost
+// holds the neighbour's old boundary value (the level's ghost cells are
+// current in a V-cycle), and the prolongation stencil at its position reads
+// the coarse correction tmp at the same values the neighbour's own stencil
+// reads (its parent's cells, or this parent's face ghost cells, copies of
+// them: k_corr_tmp forms tmp on whole boxes) -- the value the fill after the
+// correction would copy. The fill then skips those cells (xrim).
+template <int K, bool GX = false>
 __global__ void __launch_bounds__(256)
     k_prolong(double *__restrict__ phi, const double *__restrict__ tmp,
               const afh_box_meta *__restrict__ meta,
               const int32_t *__restrict__ ids, int nc, size_t bsz) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= nc * nc * (nc / K)) return;
+  const int nr = GX ? nc + 2 : nc;  // row width
+  if (t >= nr * nc * (nc / K)) return;
   const int id = ids[blockIdx.y];
   const afh_box_meta &m = meta[id - 1];
   int i, j, kq;
-  cell3(t, nc, i, j, kq);
+  if (GX) {
+    const int w = t / nr;
+    i = t - w * nr;  // 0 .. nc+1
+    j = w % nc + 1;
+    kq = w / nc + 1;
+    if (i == 0 || i == nc + 1) {
+      if (m.neighbors[i == 0 ? 0 : 1] <= 0 || j < 2 || j > nc - 1) return;
+    }
+  } else {
+    cell3(t, nc, i, j, kq);
+  }
   const int k0 = (kq - 1) * K + 1;  // odd
   const int ng = nc + 2, hn = nc >> 1;
   const size_t sk = (size_t)ng * ng;
@@ -1765,12 +1784,14 @@ __global__ void __launch_bounds__(256)
   }
 #pragma unroll
   for (int q = 0; q < K; q++) ph[q] = phi[c + q * sk];
+  const bool ghost = GX && (i == 0 || i == nc + 1);
 #pragma unroll
   for (int q = 0; q < K; q++) {
     // cell k0+q: odd q -> (k1, k2) = planes (P+(q-1)/2, P+(q+1)/2);
     // even q -> (P+q/2, P+q/2-1); a, b index pv from plane P-1
     const int a = (q & 1) ? (q + 1) / 2 : q / 2 + 1;
     const int b = (q & 1) ? (q + 3) / 2 : q / 2;
+    if (ghost && (k0 + q == 1 || k0 + q == nc)) continue;  // rim planes: the fill
     st_nt<AFH_NT_MG>(phi + (c + q * sk),
                      ph[q] + (27 / 64.0) * pv[a][0] + (9 / 64.0) * pv[a][1] +
                          (9 / 64.0) * pv[a][2] + (3 / 64.0) * pv[a][3] +
@@ -2641,6 +2662,7 @@ struct afh_mg {
   // AFH_PAIR_XR: the whole-box pair of bigger boxes (k_gsrb_pair2, TJ = NC)
   // stores the fill's x ghost cells (off until measured on the GPU)
   bool pair_xr = false;
+  bool prolong_gx = true;  // AFH_PROLONG_GX: with it, the correction's x ghost cells
   int tiles_min = 256;  // AFH_PAIR_TILES_MIN: levels of fewer boxes run tiles (NC >= 32)
   int *d_cycles = nullptr;
   int cycles_host = 0;
@@ -2928,6 +2950,7 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
   if (const char *env = getenv("AFH_PROLONG_PUSH")) mg->prolong_push = atoi(env) != 0;
   if (const char *env = getenv("AFH_RSTR_PUSH")) mg->rstr_push = atoi(env) != 0;
   if (const char *env = getenv("AFH_PAIR_XR")) mg->pair_xr = atoi(env) != 0;
+  if (const char *env = getenv("AFH_PROLONG_GX")) mg->prolong_gx = atoi(env) != 0;
   if (const char *env = getenv("AFH_PAIR_TILES_MIN")) mg->tiles_min = atoi(env);
   AFH_HIP(hipMalloc(&mg->cs_iters, sizeof(int)));
   AFH_HIP(hipMalloc(&mg->d_cycles, sizeof(int)));
@@ -3439,6 +3462,13 @@ static bool prolong_push(const afh_mg *mg, int lvl) {
          fused_level(mg, lvl);
 }
 
+// the correction of a level smoothed by the XR pair also corrects the x
+// ghost cells facing same-level neighbours (k_prolong<4, GX>); the fill
+// after it skips them (AFH_PROLONG_GX=0: off)
+static bool prolong_gx(const afh_mg *mg, int lvl) {
+  return mg->prolong_gx && !mg->any_var && fused_level(mg, lvl) && pair2_xr(mg, lvl);
+}
+
 static int32_t correct_children(afh_mg *mg, int lvl) {
   afh_tree *t = mg->t;
   const int np = t->parents.n(lvl - 1), nc = t->nc;
@@ -3471,6 +3501,13 @@ static int32_t correct_children(afh_mg *mg, int lvl) {
     const int want = mg->prolong_k;
     const int K = want == 8 && nc % 8 == 0 ? 8 : want >= 4 && nc % 4 == 0 ? 4 : 2;
     const dim3 grid((nc * nc * (nc / K) + 255) / 256, nid);
+    if (K == 4 && prolong_gx(mg, lvl)) {
+      hipLaunchKernelGGL((k_prolong<4, true>), dim3(((nc + 2) * nc * (nc / 4) + 255) / 256, nid),
+                         dim3(256), 0, t->stream, t->ccv(mg->d.i_phi), t->ccv(mg->d.i_tmp),
+                         t->d_boxes, t->ids.at(lvl), nc, t->bsz);
+      AFH_LAUNCH_CHECK("k_prolong");
+      return AFH_OK;
+    }
     if (K == 8)
       hipLaunchKernelGGL(k_prolong<8>, grid, dim3(256), 0, t->stream,
                          t->ccv(mg->d.i_phi), t->ccv(mg->d.i_tmp), t->d_boxes,
@@ -4056,7 +4093,9 @@ static int32_t vcycle_body(afh_mg *mg, int32_t set_residual, int max_lvl, bool m
     if ((e = correct_children(mg, lvl))) return e;
     // (a pushing correction filled the faces, and the pushing pairs read no
     // edges or corners: k_gc_corners follows the leg's last pair)
-    if (!prolong_push(mg, lvl) && (e = gc_lvl(t, lvl, mg->d.i_phi, 1, fused_level(mg, lvl))))
+    if (!prolong_push(mg, lvl) &&
+        (e = gc_lvl_var(t, lvl, mg->d.i_phi, t->ccv(mg->d.i_phi), t->gc_args(mg->d.i_phi), 1,
+                        fused_level(mg, lvl), prolong_gx(mg, lvl))))
       return e;
     if ((e = gsrb_boxes(mg, lvl, true))) return e;
   }

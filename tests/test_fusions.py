@@ -29,7 +29,8 @@ Round 4:
   boundary cells recomputed) and the fill skips them, vs the pair + the full
   fill -- on S1-64 (BASELINE's headline tree, 512 leaf boxes of 64^3), a
   tree of 32^3 boxes, and AMR trees of 16^3 and 32^3 boxes (every level
-  whole-box pairs; refinement boundaries and physical faces).
+  whole-box pairs; refinement boundaries and physical faces); with it the
+  correction's x ghost cells (k_prolong GX, AFH_PROLONG_GX).
 
 The fused forms are also what every other GPU test runs (they are the
 defaults); these tests pin them to the unfused forms on full workloads.
@@ -256,8 +257,10 @@ def test_pair_xr_bitwise(config, monkeypatch):
     field solve and four unit steps, every variable bitwise the pair + fill."""
     import bench
     monkeypatch.setitem(bench.CONFIGS, "c32l4", (32, (32, 32, 32), 4, (8e-3, 8e-3, 8e-3)))
-    _same(_s1(monkeypatch, {"AFH_PAIR_XR": "1"}, config),
-          _s1(monkeypatch, {"AFH_PAIR_XR": "0"}, config))
+    ref = _s1(monkeypatch, {"AFH_PAIR_XR": "0"}, config)
+    _same(_s1(monkeypatch, {"AFH_PAIR_XR": "1"}, config), ref)
+    if config == "c32l4":  # the XR pair without the correction's x ghost cells
+        _same(_s1(monkeypatch, {"AFH_PAIR_XR": "1", "AFH_PROLONG_GX": "0"}, config), ref)
 
 
 @pytest.mark.parametrize("name", ["amr16", "amr32"])
