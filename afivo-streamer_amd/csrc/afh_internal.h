@@ -137,8 +137,10 @@ struct afh_tree {
   // fill but the step no faster, so k_gc_faces stays (AFH_GC_FACES6=0/1)
   int gc_faces6 = -1;
   // boxes of 32^3 and up: level face fills with 8 ghost values per thread
-  // (k_gc_faces_r; AFH_GC_FACES_R=1: one per thread, k_gc_faces)
-  int gc_faces_r = 8;
+  // (k_gc_faces_r, AFH_GC_FACES_R=8): measured slower than one per thread
+  // on S1-64 (10.4 against 7.6 ms of fills per bench run,
+  // profiles/r04_push_ab.txt), so off
+  int gc_faces_r = 1;
   // boxes up to 16^3: faces, edges and corners of a level in one launch
   // (k_gc_box, AFH_GC_BOX=0 for the two-launch form)
   bool gc_box = true;
