@@ -8,6 +8,11 @@
 #   SMOKE=1       __graft_entry__.smoke()
 #   BENCH=1       bench.py (BENCH_ARGS, default "--steps 20 --warmup 5")
 #   AB="v1 v2"    scripts/ab_env_sets.sh over the variants (CFG, REPS, STEPS)
+#   ENVPROF="v1 v2"  scripts/env_sets_prof.sh over the variants (rocprofv3
+#                 kernel totals per run; CFG, REPS, STEPS, KREGEX)
+#   LIBS="a.so b.so"  scripts/ab_kernels.sh over library builds ("default" =
+#                 the in-tree one; scripts/build_variant.sh builds the others)
+#   PLACEMENT=N   scripts/placement_probe.py: N allocations in one process
 #   PROF="s1-64 s3"  scripts/prof_cfg.sh per config (PKTCAP=0 for graphs)
 #   EXTRA="cmd"   one more command, last
 # TAG names the logs under gpurun_out/.
@@ -35,6 +40,19 @@ fi
 if [ -n "$AB" ]; then
   # shellcheck disable=SC2086
   bash scripts/ab_env_sets.sh $AB || exit $?
+fi
+if [ -n "$ENVPROF" ]; then
+  # shellcheck disable=SC2086
+  bash scripts/env_sets_prof.sh $ENVPROF || exit $?
+fi
+if [ -n "$LIBS" ]; then
+  # shellcheck disable=SC2086
+  bash scripts/ab_kernels.sh $LIBS || exit $?
+fi
+if [ -n "$PLACEMENT" ]; then
+  timeout -k 10 400 python3 scripts/placement_probe.py $PLACEMENT \
+    > gpurun_out/placement_$TAG.log 2>&1 || { tail -5 gpurun_out/placement_$TAG.log; exit 1; }
+  grep -E "allocation|afh_pool" gpurun_out/placement_$TAG.log
 fi
 for cfg in $PROF; do
   CFG=$cfg BTIME=300 PTIME=300 bash scripts/prof_cfg.sh || exit $?
