@@ -167,6 +167,8 @@ SIGNATURES = {
     "electrode_species_bc": (i32, [_VP, i32, i32, i32, i32, P_i32]),
     "fluid_set_rhs_output": (i32, [_VP, i32, i32]),
     "fluid_set_field_source": (i32, [_VP, i32, f64]),
+    "fluid_set_ion_se_yield": (i32, [_VP, f64]),
+    "fluid_ion_se_flux": (i32, [_VP]),
     "fluid_rhs_maxabs": (i32, [_VP, i32, P_f64]),
     "fluid_rhs_valid": (i32, [_VP, i32, P_i32]),
     "photoi_set_src": (i32, [_VP, i32, i32, f64]),

@@ -205,8 +205,6 @@ class Simulation:
             mob = c.ra("ion_mobilities")
             if len(fs) != 1 + n_ions or fs[0] != self.i_electron:
                 raise NotImplementedError("electron energy equation")
-            if c.r("ion_se_yield") > 0:
-                raise NotImplementedError("secondary emission from ions (ion_se_yield)")
             plasma_iv = [self.species_itree[n] for n in self.plasma]
             for q in range(n_ions):
                 self.ions.append((plasma_iv.index(fs[1 + q]) + 1, fv[1 + q], float(mob[q])))
@@ -336,6 +334,10 @@ class Simulation:
             i_gas_dens=self.i_gas_dens,
             gas_fractions=self.gas_fractions if self.i_gas_dens else (),
             ions=self.ions)
+        # secondary emission from ions at the walls (input_data%ion_se_yield,
+        # handle_ion_se_flux in forward_euler, m_fluid.f90:63-67)
+        if self.ions and "ion_se_yield" in c.d and c.r("ion_se_yield") > 0:
+            self.fluid.set_ion_se_yield(c.r("ion_se_yield"))
         if self.fused_rhs:
             self.fluid.set_rhs_output(self.i_rhs, True)
         self.faces_from_phi = self._faces_from_phi_ok and self.lsf is None

@@ -468,6 +468,15 @@ class Fluid:
         reading f_field; 0 restores f_field (afh_fluid_set_field_source)."""
         self.lib.call("fluid_set_field_source", self.h, i_phi, float(fac))
 
+    def set_ion_se_yield(self, y):
+        """input_data%ion_se_yield: forward_euler applies handle_ion_se_flux
+        between the flux and the update (afh_fluid_set_ion_se_yield)."""
+        self.lib.call("fluid_set_ion_se_yield", self.h, float(y))
+
+    def ion_se_flux(self):
+        """handle_ion_se_flux over the leaves (afh_fluid_ion_se_flux)."""
+        self.lib.call("fluid_ion_se_flux", self.h)
+
     def rhs_maxabs(self, s_out):
         """max|rhs| of the rhs the last update wrote for state s_out."""
         out = C.c_double()

@@ -1986,6 +1986,7 @@ struct afh_fluid {
   // f_field (0: read f_field)
   int phi_iv = 0;
   double phi_fac = -1.0;
+  double ion_se_yield = 0.0;  // afh_fluid_set_ion_se_yield
   // mobile ions: second ghost layers of each ion [ion][box][6][nc][nc] and
   // the electrons' mu u per face (k_flux_staged -> k_flux_ion)
   double *d_gc2_ion = nullptr, *d_sig = nullptr;
@@ -2532,7 +2533,69 @@ static void flux_dt_limits(const double r[2], double *dt_lim) {
   dt_lim[1] = 8.8541878176e-12 / (1.6022e-19 * std::max(sig_max, 1e-100));
 }
 
+// handle_ion_se_flux (src/m_fluid.f90:584-663): one thread per face cell
+// (a, b) of face blockIdx.y of leaf box ids[blockIdx.z]; physical faces only;
+// the positive mobile ions in order (the host lists only those). The 3-D
+// low-y case is the reference's fc(1:nc, 1:nc, 1, 2) (m_fluid.f90:639-642:
+// the y faces j = 1..nc of the first z plane), as the oracle
+struct IonSeArgs {
+  double *fe;
+  const double *fi[AFH_MAX_IONS];
+  int n;
+  double y;
+};
+__global__ void k_ion_se(IonSeArgs A, const afh_box_meta *__restrict__ meta,
+                         const int32_t *__restrict__ ids, int nc, size_t fsz) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nc * nc) return;
+  const int id = ids[blockIdx.z], nb = blockIdx.y;
+  if (meta[id - 1].neighbors[nb] >= 0) return;  // not a physical boundary
+  const int d = nb >> 1;
+  const bool hi = nb & 1;
+  const int a = t % nc + 1, b = t / nc + 1, f = hi ? nc + 1 : 1;
+  int i = d == 0 ? f : a, j = d == 1 ? f : (d == 0 ? a : b), k = d == 2 ? f : b;
+  if (nb == 2) j = b, k = 1;  // af_neighb_lowy as the reference indexes it
+  const size_t nf = nc + 1;
+  const size_t c = (size_t)(id - 1) * fsz + (size_t)d * nf * nf * nf +
+                   ((size_t)(k - 1) * nf + (j - 1)) * nf + (i - 1);
+  double fe = A.fe[c];
+  for (int n = 0; n < A.n; n++) {
+    const double v = A.fi[n][c];
+    fe = fe - A.y * (hi ? (v > 0.0 ? v : 0.0) : (v < 0.0 ? v : 0.0));
+  }
+  A.fe[c] = fe;
+}
+
+static int32_t ion_se_dev(afh_fluid *f) {
+  afh_tree *t = f->t;
+  IonSeArgs A{};
+  A.fe = t->fcv(f->d.f_flux);
+  A.y = f->ion_se_yield;
+  for (int q = 0; q < f->d.n_ions; q++)
+    if (f->d.species_charge[f->d.ion_species[q] - 1] > 0) A.fi[A.n++] = t->fcv(f->d.f_ion_flux[q]);
+  const int n = t->leaves.off[t->nlvl] - t->leaves.off[0], nc = t->nc;
+  if (!A.n || !n) return AFH_OK;
+  hipLaunchKernelGGL(k_ion_se, dim3((nc * nc + 255) / 256, 6, n), dim3(256), 0, t->stream, A,
+                     t->d_boxes, t->leaves.at(1), nc, t->fsz);
+  AFH_LAUNCH_CHECK("k_ion_se");
+  return AFH_OK;
+}
+
 extern "C" {
+
+int32_t afh_fluid_set_ion_se_yield(afh_fluid *f, double yield) {
+  if (!f) return set_error(AFH_ERR_ARG, "afh_fluid_set_ion_se_yield: null");
+  AFH_LIVE(f->t, "afh_fluid_set_ion_se_yield");
+  if (!(yield >= 0)) return set_error(AFH_ERR_ARG, "ion_se_yield %g", yield);
+  f->ion_se_yield = yield;
+  return AFH_OK;
+}
+
+int32_t afh_fluid_ion_se_flux(afh_fluid *f) {
+  if (!f) return set_error(AFH_ERR_ARG, "afh_fluid_ion_se_flux: null");
+  AFH_LIVE(f->t, "afh_fluid_ion_se_flux");
+  return ion_se_dev(f);
+}
 
 int32_t afh_flux_upwind_tree(afh_fluid *f, int32_t s_deriv, double *dt_lim) {
   if (!f || !dt_lim) return set_error(AFH_ERR_ARG, "null argument");
@@ -2721,11 +2784,14 @@ static int32_t fe_dev(afh_fluid *f, double dt, int32_t s_deriv, int32_t n_prev,
                      (nc == 16 || nc == 32 || nc == 64) && !t->any_cflux &&
                      !f->slow_rates && f->d.n_species <= FE_MAX_SPECIES && f->phi_iv == 0 &&
                      f->rhs_iv == 0 && f->d.i_gas_dens <= 0 && f->d.i_photo <= 0 &&
-                     n_prev <= 2 && !alias && f->d.limiter == AFH_LIM_KOREN;
+                     n_prev <= 2 && !alias && f->d.limiter == AFH_LIM_KOREN &&
+                     f->d.n_ions == 0;
   if (!fused) {
     // flux and update back to back on the stream (the flux maxima are not
-    // needed before the update)
+    // needed before the update); secondary emission from ions at the walls
+    // between them (m_fluid.f90:63-67)
     if ((e = flux_tree_dev(f, s_deriv))) return e;
+    if (f->d.n_ions > 0 && f->ion_se_yield > 0 && (e = ion_se_dev(f))) return e;
     return update_dev(f, dt, s_deriv, n_prev, s_prev, w_prev, s_out, last_step);
   }
   t->touch(iv);

@@ -519,6 +519,21 @@ module m_afivo_hip
        integer(c_int32_t)        :: afh_fluid_set_field_source
      end function afh_fluid_set_field_source
 
+     !> input_data%ion_se_yield: handle_ion_se_flux inside forward_euler
+     function afh_fluid_set_ion_se_yield(f, yield) bind(C, name=afh_pfx//"fluid_set_ion_se_yield")
+       import
+       type(c_ptr), value    :: f
+       real(c_double), value :: yield
+       integer(c_int32_t)    :: afh_fluid_set_ion_se_yield
+     end function afh_fluid_set_ion_se_yield
+
+     !> handle_ion_se_flux over the leaves (src/m_fluid.f90:584-663)
+     function afh_fluid_ion_se_flux(f) bind(C, name=afh_pfx//"fluid_ion_se_flux")
+       import
+       type(c_ptr), value :: f
+       integer(c_int32_t) :: afh_fluid_ion_se_flux
+     end function afh_fluid_ion_se_flux
+
      !> max|rhs| of the rhs the last update wrote for state s_out
      function afh_fluid_rhs_maxabs(f, s_out, max_rhs) bind(C, name=afh_pfx//"fluid_rhs_maxabs")
        import

@@ -402,6 +402,20 @@ int32_t afh_fluid_rhs_maxabs(afh_fluid *f, int32_t s_out, double *max_rhs);
  * f_field. */
 int32_t afh_fluid_set_field_source(afh_fluid *f, int32_t i_phi, double fac);
 int32_t afh_fluid_rhs_valid(afh_fluid *f, int32_t s_out, int32_t *valid);
+/* Secondary emission from ions at the domain walls: input_data%ion_se_yield
+ * (m_transport_data.f90:217, 0 by default; >= 0). afh_fluid_ion_se_flux is
+ * handle_ion_se_flux over the leaves (src/m_fluid.f90:584-663, called by
+ * forward_euler between flux_upwind_tree and flux_update_densities,
+ * m_fluid.f90:63-67): on every physical face of a leaf box, for each mobile
+ * ion of positive charge in order, the electrons' face flux loses the yield
+ * times the ion flux out of the domain (min(0, F) on low faces, max(0, F) on
+ * high faces); the 3-D low-y face as the reference indexes it,
+ * fc(1:nc, 1:nc, 1, 2) (m_fluid.f90:639-642: the y faces j = 1..nc of the
+ * first z plane). afh_fluid_forward_euler[_fold] call it when the yield is
+ * positive and the fluid has mobile ions; a caller of afh_flux_upwind_tree /
+ * afh_flux_update_densities calls it between the two. */
+int32_t afh_fluid_set_ion_se_yield(afh_fluid *f, double yield);
+int32_t afh_fluid_ion_se_flux(afh_fluid *f);
 /* electrode_species_bc over the boxes tagged mg_lsf_box (src/streamer.f90:
  * 578-636, called per step by set_electrode_densities, 569-574): in every
  * cell with lsf < 0 all plasma species (state 0, m_streamer.f90:242) are set

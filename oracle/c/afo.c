@@ -127,6 +127,7 @@ struct afh_fluid {
   int rhs_iv, rhs_state, rhs_ghosts; /* afo_fluid_set_rhs_output */
   int phi_iv;     /* afo_fluid_set_field_source (0: read f_field) */
   double phi_fac;
+  double ion_se_yield; /* afo_fluid_set_ion_se_yield (input_data%ion_se_yield) */
   double rhs_max;
   /* generations of rhs_iv and the densities of rhs_state after the update */
   unsigned long long rhs_snap[AFH_MAX_SPECIES + 1];
@@ -1812,6 +1813,57 @@ int32_t afo_fluid_set_field_source(afh_fluid *f, int32_t i_phi, double fac) {
   return AFH_OK;
 }
 
+int32_t afo_fluid_set_ion_se_yield(afh_fluid *f, double yield) {
+  if (!(yield >= 0)) return fail(AFH_ERR_ARG, "ion_se_yield %g", yield);
+  f->ion_se_yield = yield;
+  return AFH_OK;
+}
+
+/* handle_ion_se_flux (src/m_fluid.f90:584-663) over the leaves
+ * (af_loop_box(tree, handle_ion_se_flux, .true.), m_fluid.f90:63-67): on
+ * every physical face of a leaf box (neighbors < af_no_box), for each mobile
+ * ion of positive charge in order, the electrons' face flux loses
+ * ion_se_yield times the ion flux out of the domain: min(0, F_ion) on the
+ * low faces, max(0, F_ion) on the high ones. The reference's 3-D low-y case
+ * (m_fluid.f90:639-642) indexes fc(1:nc, 1:nc, 1, 2): the y faces j = 1..nc
+ * of the first z plane, not the wall's fc(1:nc, 1, 1:nc, 2); reproduced as
+ * written (its results are the parity target). */
+int32_t afo_fluid_ion_se_flux(afh_fluid *f) {
+  afh_tree *t = f->t;
+  LIVE(t);
+  const int nc = t->nc;
+  const double y = f->ion_se_yield;
+  for (int l = 1; l <= t->nlvl; l++)
+    for (int q = 0; q < LVL_N(t, leaves, l); q++) {
+      const int id = LVL_AT(t, leaves, l, q);
+      const afh_box_meta *m = B(t, id);
+      double *Fe = fcb(t, f->d.f_flux, id);
+      for (int nb = 0; nb < 6; nb++) {
+        if (m->neighbors[nb] >= 0) continue;
+        const int d = nb >> 1, hi = nb & 1, fi = hi ? nc + 1 : 1;
+        for (int n = 0; n < f->d.n_ions; n++) {
+          if (f->d.species_charge[f->d.ion_species[n] - 1] <= 0) continue;
+          const double *Fi = fcb(t, f->d.f_ion_flux[n], id);
+          for (int b = 1; b <= nc; b++)
+            for (int a = 1; a <= nc; a++) {
+              int p[3];
+              if (nb == 2) { /* af_neighb_lowy as the reference indexes it */
+                p[0] = a, p[1] = b, p[2] = 1;
+              } else {
+                p[d] = fi;
+                p[d == 0 ? 1 : 0] = a;
+                p[d == 2 ? 1 : 2] = b;
+              }
+              const size_t c = FX(t, d, p[0], p[1], p[2]);
+              const double v = Fi[c];
+              Fe[c] = Fe[c] - y * (hi ? (v > 0.0 ? v : 0.0) : (v < 0.0 ? v : 0.0));
+            }
+        }
+      }
+    }
+  return AFH_OK;
+}
+
 int32_t afo_fluid_set_rhs_output(afh_fluid *f, int32_t i_rhs, int32_t ghosts) {
   if (i_rhs < 0 || i_rhs > f->t->nvc) return fail(AFH_ERR_ARG, "bad i_rhs");
   f->rhs_iv = i_rhs;
@@ -2559,8 +2611,10 @@ int32_t afo_fluid_forward_euler(afh_fluid *f, double dt, int32_t s_deriv,
   (void)store_flux;
   double a[2], b[2];
   int32_t e;
-  if ((e = afo_flux_upwind_tree(f, s_deriv, a)) ||
-      (e = afo_flux_update_densities(f, dt, s_deriv, n_prev, s_prev, w_prev, s_out,
+  if ((e = afo_flux_upwind_tree(f, s_deriv, a))) return e;
+  /* secondary emission from ions at the walls (m_fluid.f90:63-67) */
+  if (f->d.n_ions > 0 && f->ion_se_yield > 0 && (e = afo_fluid_ion_se_flux(f))) return e;
+  if ((e = afo_flux_update_densities(f, dt, s_deriv, n_prev, s_prev, w_prev, s_out,
                                      last_step, b)))
     return e;
   dt_lim[0] = a[0], dt_lim[1] = a[1], dt_lim[2] = b[0], dt_lim[3] = b[1];

@@ -40,6 +40,8 @@ int32_t afo_restrict_tree(afh_tree *t, int32_t iv);
 int32_t afo_tree_copy_cc(afh_tree *t, int32_t iv_from, int32_t iv_to);
 int32_t afo_fluid_set_rhs_output(afh_fluid *f, int32_t i_rhs, int32_t ghosts);
 int32_t afo_fluid_set_field_source(afh_fluid *f, int32_t i_phi, double fac);
+int32_t afo_fluid_set_ion_se_yield(afh_fluid *f, double yield);
+int32_t afo_fluid_ion_se_flux(afh_fluid *f);
 int32_t afo_fluid_rhs_maxabs(afh_fluid *f, int32_t s_out, double *max_rhs);
 int32_t afo_electrode_species_bc(afh_fluid *f, int32_t i_lsf, int32_t i_1pos_ion,
                                  int32_t neumann_zero, int32_t n_ids,

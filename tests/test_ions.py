@@ -92,3 +92,29 @@ def test_hip_mobile_ions_equal_oracle():
     for iv in sim.densities:
         a, b = sim.tree.get_cc(iv), osim.tree.get_cc(iv)
         assert np.max(np.abs(a - b)) <= 1e-12 * np.max(np.abs(b)), sim.cc_names[iv - 1]
+
+
+@pytest.mark.gpu
+def test_hip_ion_se_equal_oracle():
+    """Secondary emission from ions at the walls (input_data%ion_se_yield =
+    0.5; handle_ion_se_flux, m_fluid.f90:584-663, the oracle pinned to the
+    reference by tests/test_reference_replay.py::
+    test_species_step_replay_ion_se): the HIP driver's state after three
+    steps, handed to the oracle; Heun stage 1's face fluxes (the electrons'
+    with the emission) and CFL / dielectric limits bitwise, the densities to
+    1e-13 (exp in the rate forms)."""
+    g = dict(golden.load("case_ions"))
+    g["ion_se_yield"] = np.array([0.5])
+    sim = Simulation(capi.hip_library(), g, device=0)
+    sim.start()
+    for _ in range(3):
+        sim.step()
+    osim = sim.clone(capi.oracle_library())
+    x = [s.fluid.forward_euler(1e-12, 0, [0], [1.0], 1, False) for s in (sim, osim)]
+    assert list(x[0])[:2] == list(x[1])[:2]
+    leaves = np.array(sim.af.leaves()) - 1
+    for fv in [sim.f_flux] + [q[1] for q in sim.ions]:
+        assert np.array_equal(sim.tree.get_fc(fv)[leaves], osim.tree.get_fc(fv)[leaves]), fv
+    for iv in sim.densities:
+        a, b = sim.tree.get_cc(iv + 1), osim.tree.get_cc(iv + 1)
+        assert np.max(np.abs(a - b)) <= 1e-13 * np.max(np.abs(b)), sim.cc_names[iv - 1]

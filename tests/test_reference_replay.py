@@ -274,3 +274,26 @@ def test_species_step_replay_mobile_ions(tmp_path):
     _replay_state(sim, "ions", 0, [0], [1.0], 1, 1e-12, tmp_path, cfg_args=ION_ARGS)
     _replay_state(sim, "ions", 1, [0, 1], [0.5, 0.5], 0, 5e-13, tmp_path,
                   cfg_args=ION_ARGS)
+
+
+def test_species_step_replay_ion_se(tmp_path):
+    """Secondary emission from ions at the walls (input_data%ion_se_yield;
+    handle_ion_se_flux, src/m_fluid.f90:584-663, called by forward_euler
+    between the flux and the update, 63-67): the mobile-ion case with a yield
+    of 0.5 (the two positive ions' wall fluxes feed the electrons'). Heun
+    stages 1 and 2 bitwise the reference's forward_euler; the yield changes
+    the densities (the emission is not vacuous here)."""
+    g = dict(golden.load("case_ions"))
+    g["ion_se_yield"] = np.array([0.5])
+    args = ION_ARGS + ["-input_data%ion_se_yield=0.5"]
+    sims = []
+    for case in (g, golden.load("case_ions")):
+        sim = Simulation(capi.oracle_library(), case)
+        sim.start()
+        for _ in range(3):
+            sim.step()
+        sims.append(sim)
+    e = sims[0].species_itree[sims[0].plasma[0]]
+    assert not np.array_equal(sims[0].tree.get_cc(e), sims[1].tree.get_cc(e))
+    _replay_state(sims[0], "ions", 0, [0], [1.0], 1, 1e-12, tmp_path, cfg_args=args)
+    _replay_state(sims[0], "ions", 1, [0, 1], [0.5, 0.5], 0, 5e-13, tmp_path, cfg_args=args)
