@@ -172,12 +172,9 @@ struct Bc4 {
 // One thread per side ghost cell (4 nc per box). Every read is an interior
 // cell (of this box, a neighbour, or the parent's neighbour), so the boxes of
 // a level fill in parallel as the reference's OpenMP loop does.
-__global__ void __launch_bounds__(NT)
-    k2_gc(double *__restrict__ v, const afh_box_meta *__restrict__ meta,
-          const int32_t *__restrict__ ids, int nc, int bsz, Bc4 g) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= 4 * nc) return;
-  const int id = ids[blockIdx.y];
+__device__ __forceinline__ void gc2_side(double *__restrict__ v,
+                                         const afh_box_meta *__restrict__ meta, int id, int t,
+                                         int nc, int bsz, const Bc4 &g) {
   const int nb = t / nc + 1, a = t % nc + 1;
   const int d = (nb - 1) >> 1;
   const bool low = ((nb - 1) & 1) == 0;
@@ -226,13 +223,19 @@ __global__ void __launch_bounds__(NT)
   c[at(gi, a)] = val;
 }
 
+__global__ void __launch_bounds__(NT)
+    k2_gc(double *__restrict__ v, const afh_box_meta *__restrict__ meta,
+          const int32_t *__restrict__ ids, int nc, int bsz, Bc4 g) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= 4 * nc) return;
+  gc2_side(v, meta, ids[blockIdx.y], t, nc, bsz, g);
+}
+
 // af_gc_box_corner (2-D): copy from the diagonal neighbour, or extrapolate
 // from the side ghost cells (af_corner_gc_extrap); one thread per corner
-__global__ void k2_corners(double *__restrict__ v, const afh_box_meta *__restrict__ meta,
-                           const int32_t *__restrict__ ids, int n, int nc, int bsz) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= 4 * n) return;
-  const int id = ids[t >> 2], cn = t & 3;
+__device__ __forceinline__ void gc2_corner(double *__restrict__ v,
+                                           const afh_box_meta *__restrict__ meta, int id,
+                                           int cn, int nc, int bsz) {
   const int dx = cn & 1, dy = cn >> 1;  // af_child_dix of corner cn + 1
   const int ng = nc + 2;
   const int ix = dx * (nc + 1), iy = dy * (nc + 1);
@@ -246,6 +249,27 @@ __global__ void k2_corners(double *__restrict__ v, const afh_box_meta *__restric
     c[ix2(ng, ix, iy)] = c[ix2(ng, ix + di, iy)] + c[ix2(ng, ix, iy + dj)] -
                          c[ix2(ng, ix + di, iy + dj)];
   }
+}
+
+__global__ void k2_corners(double *__restrict__ v, const afh_box_meta *__restrict__ meta,
+                           const int32_t *__restrict__ ids, int n, int nc, int bsz) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= 4 * n) return;
+  gc2_corner(v, meta, ids[t >> 2], t & 3, nc, bsz);
+}
+
+// A level fill with corners in one launch: one workgroup per box, its side
+// ghosts (k2_gc), a barrier, its corners (k2_corners: a diagonal
+// neighbour's interior cell, or extrapolated from this box's side ghosts).
+// The side ghosts read interior cells only, so boxes need not wait for each
+// other; the same values as the two launches (AFH2_GC_BOX=0)
+__global__ void __launch_bounds__(64)
+    k2_gc_box(double *__restrict__ v, const afh_box_meta *__restrict__ meta,
+              const int32_t *__restrict__ ids, int nc, int bsz, Bc4 g) {
+  const int id = ids[blockIdx.x];
+  for (int t = threadIdx.x; t < 4 * nc; t += blockDim.x) gc2_side(v, meta, id, t, nc, bsz, g);
+  __syncthreads();
+  if (threadIdx.x < 4) gc2_corner(v, meta, id, threadIdx.x, nc, bsz);
 }
 
 // ------------------------------------------------------------ multigrid
@@ -1010,6 +1034,7 @@ using namespace afh2;
 struct afh_tree {
   int device = 0;
   hipStream_t stream = nullptr;
+  bool gc_box = true;  // level fills with corners in one launch (k2_gc_box; AFH2_GC_BOX=0)
   int nc = 0, ng = 0, nb = 0, nlvl = 0, nvc = 0, nvf = 0;
   int bsz = 0, fsz = 0;
   int cgs[2] = {0, 0};
@@ -1109,6 +1134,12 @@ static void free_list(LevelList &L) {
 static int32_t gc_lvl(afh_tree *t, int lvl, int iv, bool corners) {
   const int n = t->ids.n(lvl);
   if (!n) return AFH_OK;
+  if (corners && t->gc_box) {
+    hipLaunchKernelGGL(k2_gc_box, dim3(n), dim3(64), 0, t->stream, t->ccv(iv), t->d_boxes,
+                       t->ids.at(lvl), t->nc, t->bsz, t->bc4(iv));
+    H2_LAUNCH("k2_gc_box");
+    return AFH_OK;
+  }
   hipLaunchKernelGGL(k2_gc, grid2(4 * t->nc, n), dim3(NT), 0, t->stream, t->ccv(iv),
                      t->d_boxes, t->ids.at(lvl), t->nc, t->bsz, t->bc4(iv));
   H2_LAUNCH("k2_gc");
@@ -1164,6 +1195,7 @@ int32_t afh_tree_create(const afh_tree_desc *desc, int32_t device, afh_tree **ou
   if (device >= 0) H2(hipSetDevice(device));
   afh_tree *t = new afh_tree();
   H2(hipGetDevice(&t->device));
+  if (const char *env = getenv("AFH2_GC_BOX")) t->gc_box = atoi(env) != 0;
   t->nc = nc, t->ng = nc + 2, t->nb = desc->n_boxes, t->nlvl = desc->highest_lvl;
   t->nvc = desc->n_var_cell, t->nvf = desc->n_var_face;
   t->bsz = t->ng * t->ng, t->fsz = 2 * (nc + 1) * (nc + 1);
