@@ -30,7 +30,9 @@ Round 4:
   fill -- on S1-64 (BASELINE's headline tree, 512 leaf boxes of 64^3), a
   tree of 32^3 boxes, and AMR trees of 16^3 and 32^3 boxes (every level
   whole-box pairs; refinement boundaries and physical faces); with it the
-  correction's x ghost cells (k_prolong GX, AFH_PROLONG_GX).
+  correction's x ghost cells (k_prolong GX, AFH_PROLONG_GX);
+* AFH2_GC_BOX: a 2-D level fill with corners in one workgroup per box
+  (k2_gc_box) vs k2_gc + k2_corners.
 
 The fused forms are also what every other GPU test runs (they are the
 defaults); these tests pin them to the unfused forms on full workloads.
