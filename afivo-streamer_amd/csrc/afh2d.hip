@@ -454,18 +454,22 @@ __device__ __forceinline__ double apply5(const double *p, int x, int ng, const C
          cf.c[4] * p[x + ng];
 }
 
-// tmp = rhs - L phi on the interior; with `red` the max |tmp| is folded
+// tmp = rhs - L phi on the interior; with `red` the max |tmp| is folded.
+// lvl_c (with meta): the box's coefficients by its level -- boxes of every
+// level in one launch (they do not interact here)
 __global__ void __launch_bounds__(NT)
     k2_residual(const double *__restrict__ phi, const double *__restrict__ rhs,
                 double *__restrict__ tmp, const int32_t *__restrict__ ids, int nc, int bsz,
-                Coef2 cf, unsigned long long *red) {
+                Coef2 cf, unsigned long long *red, const Coef2 *__restrict__ lvl_c,
+                const afh_box_meta *__restrict__ meta) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   double mx = 0.0;
   if (t < nc * nc) {
     const int i = t % nc + 1, j = t / nc + 1, ng = nc + 2;
-    const size_t o = (size_t)(ids[blockIdx.y] - 1) * bsz;
+    const int id = ids[blockIdx.y];
+    const size_t o = (size_t)(id - 1) * bsz;
     const int x = ix2(ng, i, j);
-    const double r = rhs[o + x] - apply5(phi + o, x, ng, cf);
+    const double r = rhs[o + x] - apply5(phi + o, x, ng, lvl_c ? lvl_c[meta[id - 1].lvl - 1] : cf);
     tmp[o + x] = r;
     mx = fabs(r);
   }
@@ -1070,6 +1074,8 @@ struct afh_mg {
   afh_tree *t = nullptr;
   afh_mg_desc d;
   std::vector<Coef2> lvl_c;
+  Coef2 *d_lvl_c = nullptr;  // lvl_c on the device (residual of every level in one launch)
+  bool all_lvl = true;       // AFH2_ALL_LVL=0: one residual / gradient launch per level
   int nx = 0, ny = 0;
   double *d_q[2] = {nullptr, nullptr}, *d_e[2] = {nullptr, nullptr};
   int q_bc[4] = {0, 0, 0, 0};
@@ -1464,6 +1470,9 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
     c.c[0] = -s - d->helmholtz_lambda;
     c.inv_c1 = 1 / c.c[0];
   }
+  H2(hipMalloc(&mg->d_lvl_c, sizeof(Coef2) * t->nlvl));
+  H2(hipMemcpy(mg->d_lvl_c, mg->lvl_c.data(), sizeof(Coef2) * t->nlvl, hipMemcpyHostToDevice));
+  if (const char *env = getenv("AFH2_ALL_LVL")) mg->all_lvl = atoi(env) != 0;
   H2(hipMalloc(&mg->d_q[0], sizeof(double) * nx * nx));
   H2(hipMalloc(&mg->d_q[1], sizeof(double) * ny * ny));
   H2(hipMalloc(&mg->d_e[0], sizeof(double) * nx));
@@ -1481,6 +1490,7 @@ int32_t afh_mg_destroy(afh_mg *mg) {
   hipStreamSynchronize(mg->t->stream);
   for (int q = 0; q < 2; q++) hipFree(mg->d_q[q]), hipFree(mg->d_e[q]);
   hipFree(mg->alt);
+  hipFree(mg->d_lvl_c);
   delete mg;
   return AFH_OK;
 }
@@ -1640,9 +1650,23 @@ static int32_t residual_lvl(afh_mg *mg, int lvl, const LevelList &L, bool fold) 
   hipLaunchKernelGGL(k2_residual, grid2(t->nc * t->nc, n), dim3(NT), 0, t->stream,
                      t->ccv(mg->d.i_phi), t->ccv(mg->d.i_rhs), t->ccv(mg->d.i_tmp), L.at(lvl),
                      t->nc, t->bsz, mg->lvl_c[lvl - 1],
-                     fold ? t->red + 3 * RED_SHARDS : nullptr);
+                     fold ? t->red + 3 * RED_SHARDS : nullptr, nullptr, nullptr);
   H2_LAUNCH("k2_residual");
   return AFH_OK;
+}
+
+// the residual of levels 1 .. max_lvl of list L in one launch (each box's
+// coefficients by its level; false: max_lvl boxes exceed the grid's y limit)
+static bool residual_all(afh_mg *mg, int max_lvl, const LevelList &L, bool fold) {
+  afh_tree *t = mg->t;
+  const int n = L.off[max_lvl] - L.off[0];
+  if (!mg->all_lvl || n > 65535) return false;
+  if (n)
+    hipLaunchKernelGGL(k2_residual, grid2(t->nc * t->nc, n), dim3(NT), 0, t->stream,
+                       t->ccv(mg->d.i_phi), t->ccv(mg->d.i_rhs), t->ccv(mg->d.i_tmp), L.at(1),
+                       t->nc, t->bsz, mg->lvl_c[0], fold ? t->red + 3 * RED_SHARDS : nullptr,
+                       mg->d_lvl_c, t->d_boxes);
+  return true;
 }
 
 // mg_fas_vcycle (185-264); with max_out the leaf max|tmp| is folded into
@@ -1661,6 +1685,10 @@ static int32_t vcycle(afh_mg *mg, bool set_residual, int max_lvl, bool max_out) 
   if (!set_residual) return AFH_OK;
   afh_tree *t = mg->t;
   if (max_out && (e = red_init(t, 3, 0.0))) return e;
+  if (max_out ? residual_all(mg, max_lvl, t->leaves, true) &&
+                    residual_all(mg, max_lvl, t->parents, false)
+              : residual_all(mg, max_lvl, t->ids, false))
+    return AFH_OK;
   for (int l = 1; l <= max_lvl; l++) {
     if (max_out) {
       // leaves fold, parents do not (the same tmp values)
@@ -1756,6 +1784,18 @@ int32_t afh_mg_compute_phi_gradient(afh_mg *mg, int32_t i_fc, double fac, int32_
   afh_tree *t = mg->t;
   if (i_fc < 1 || i_fc > t->nvf || i_norm < 0 || i_norm > t->nvc)
     return set_error(AFH_ERR_ARG, "bad variable index");
+  // every level in one launch (the box's spacing comes from its meta)
+  const int n_all = t->ids.off[t->nlvl] - t->ids.off[0];
+  if (mg->all_lvl && n_all <= 65535) {
+    if (n_all) {
+      hipLaunchKernelGGL(k2_gradient, grid2((t->nc + 1) * (t->nc + 1), n_all), dim3(NT), 0,
+                         t->stream, t->ccv(mg->d.i_phi), t->fcv(i_fc),
+                         i_norm ? t->ccv(i_norm) : nullptr, t->d_boxes, t->ids.at(1), t->nc,
+                         t->bsz, t->fsz, fac);
+      H2_LAUNCH("k2_gradient");
+    }
+    return AFH_OK;
+  }
   for (int l = 1; l <= t->nlvl; l++) {
     const int n = t->ids.n(l);
     if (!n) continue;

@@ -32,7 +32,9 @@ Round 4:
   whole-box pairs; refinement boundaries and physical faces); with it the
   correction's x ghost cells (k_prolong GX, AFH_PROLONG_GX);
 * AFH2_GC_BOX: a 2-D level fill with corners in one workgroup per box
-  (k2_gc_box) vs k2_gc + k2_corners.
+  (k2_gc_box) vs k2_gc + k2_corners;
+* AFH2_ALL_LVL: the 2-D residual and gradient of every level in one launch
+  vs one launch per level.
 
 The fused forms are also what every other GPU test runs (they are the
 defaults); these tests pin them to the unfused forms on full workloads.
@@ -185,6 +187,17 @@ def test_2d_gc_box_bitwise(config, monkeypatch):
     monkeypatch.setitem(bench.CONFIGS, "c2d16", (16, (16, 16), 4, (16e-3, 16e-3)))
     _same(_case2d(monkeypatch, {"AFH2_GC_BOX": "1"}, config),
           _case2d(monkeypatch, {"AFH2_GC_BOX": "0"}, config))
+
+
+@pytest.mark.parametrize("config", ["2d", "c2d16"])
+def test_2d_all_level_launches_bitwise(config, monkeypatch):
+    """2-D residual and gradient of every level in one launch (the box's
+    level coefficients / spacing from its meta; AFH2_ALL_LVL) against one
+    launch per level: field solves and four unit steps."""
+    import bench
+    monkeypatch.setitem(bench.CONFIGS, "c2d16", (16, (16, 16), 4, (16e-3, 16e-3)))
+    _same(_case2d(monkeypatch, {"AFH2_ALL_LVL": "1"}, config),
+          _case2d(monkeypatch, {"AFH2_ALL_LVL": "0"}, config))
 
 
 @pytest.mark.parametrize("switch", ["AFH_PROLONG_PUSH", "AFH_RSTR_PUSH"])
