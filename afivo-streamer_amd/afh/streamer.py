@@ -92,8 +92,9 @@ class StreamerCase:
         # field_compute(defer=True): the residual list the next species_step
         # fills (AFH_DEFER=0 turns deferral off, for A/B runs)
         self._deferred_res = None
-        # (the 2-D library has no deferred entry points, afivo_hip_2d.h)
-        self._defer_ok = os.environ.get("AFH_DEFER", "1") != "0" and self.ndim == 3
+        # (the 2-D library has them since round 4, afivo_hip_2d.h)
+        self._defer_ok = (os.environ.get("AFH_DEFER", "1") != "0" and
+                          (self.ndim == 3 or lib.has("fluid_fetch_step")))
         self.mg = Multigrid(t, IV["phi"], IV["rhs"], IV["tmp"],
                             coarse_cycles=coarse_cycles)
         self._mg_helm = {}
@@ -223,7 +224,7 @@ class StreamerCase:
         (m_af_advance.f90:160-164, m_fluid.f90:97-98), so the limits of a
         Heun step's first sub-step are never read; a deferred V-cycle
         residual stays pending too (it is overwritten by the next one)."""
-        if not fetch and self.ndim == 2:
+        if not fetch and not self.lib.has("fluid_forward_euler_fold"):
             self.fluid.forward_euler(dt, s_deriv, s_prev, w_prev, s_out, last_step,
                                      self.store_flux)
             return None

@@ -1712,6 +1712,12 @@ int32_t afh_mg_fas_vcycle(afh_mg *mg, int32_t set_residual, int32_t hl) {
   return vcycle(mg, set_residual != 0, max_lvl, false);
 }
 
+int32_t afh_mg_fas_vcycle_fold(afh_mg *mg, int32_t hl) {
+  if (!mg) return set_error(AFH_ERR_ARG, "null mg");
+  const int max_lvl = (hl > 0 && hl <= mg->t->nlvl) ? hl : mg->t->nlvl;
+  return vcycle(mg, true, max_lvl, true);
+}
+
 int32_t afh_mg_fas_vcycle_maxres(afh_mg *mg, int32_t hl, double *max_res) {
   if (!mg || !max_res) return set_error(AFH_ERR_ARG, "afh_mg_fas_vcycle_maxres: null");
   const int max_lvl = (hl > 0 && hl <= mg->t->nlvl) ? hl : mg->t->nlvl;
@@ -1898,7 +1904,16 @@ static DevLT dev_lt(const afh_lt &lt, const double *d) {
 
 // flux_upwind_tree (m_af_flux_schemes.f90:666-712); dt_lim = (1 / max CFL
 // sum, dielectric relaxation time)
-static int32_t flux_tree(afh_fluid *f, int32_t s_deriv, double *dt_lim) {
+// the CFL and dielectric relaxation limits from the folded maxima
+static void flux_limits(const double *r, double *dt_lim) {
+  const double eps0 = 8.8541878176e-12, ec = 1.6022e-19;
+  dt_lim[0] = 1 / r[0];
+  dt_lim[1] = eps0 / (ec * std::max(r[1], 1e-100));
+}
+
+// fetch = false: the CFL and dielectric maxima stay in slots 0, 1 for
+// afh_fluid_fetch_step
+static int32_t flux_tree(afh_fluid *f, int32_t s_deriv, double *dt_lim, bool fetch = true) {
   afh_tree *t = f->t;
   const int iv = f->d.i_electron + s_deriv;
   if (int32_t e = check_iv(t, iv, "afh_flux_upwind_tree")) return e;
@@ -1943,17 +1958,17 @@ static int32_t flux_tree(afh_fluid *f, int32_t s_deriv, double *dt_lim) {
                        t->fcv(f->d.f_flux), t->d_boxes, t->cflux.d, ntask, nc, t->fsz);
     H2_LAUNCH("k2_consistent");
   }
+  if (!fetch) return AFH_OK;
   double r[2];
   if ((e = red_read(t, 0, 2, 3, r))) return e;
-  const double eps0 = 8.8541878176e-12, ec = 1.6022e-19;
-  dt_lim[0] = 1 / r[0];
-  dt_lim[1] = eps0 / (ec * std::max(r[1], 1e-100));
+  flux_limits(r, dt_lim);
   return AFH_OK;
 }
 
+// fetch = false: the chemistry minimum stays in slot 2 (last step)
 static int32_t update(afh_fluid *f, double dt, int32_t s_deriv, int32_t n_prev,
                       const int32_t *s_prev, const double *w_prev, int32_t s_out,
-                      int32_t last_step, double *dt_lim) {
+                      int32_t last_step, double *dt_lim, bool fetch = true) {
   afh_tree *t = f->t;
   if (n_prev < 1 || n_prev > MAXPREV || !s_prev || !w_prev)
     return set_error(AFH_ERR_ARG, "afh_flux_update_densities: previous states");
@@ -1985,7 +2000,7 @@ static int32_t update(afh_fluid *f, double dt, int32_t s_deriv, int32_t n_prev,
     H2_LAUNCH("k2_update");
   }
   dt_lim[0] = 1e100, dt_lim[1] = 1e100;
-  if (A.last_step) return red_read(t, 2, 1, 0, dt_lim);
+  if (A.last_step && fetch) return red_read(t, 2, 1, 0, dt_lim);
   return AFH_OK;
 }
 
@@ -2023,6 +2038,37 @@ int32_t afh_fluid_forward_euler(afh_fluid *f, double dt, int32_t s_deriv, int32_
   int32_t e;
   if ((e = flux_tree(f, s_deriv, dt_lim))) return e;
   return update(f, dt, s_deriv, n_prev, s_prev, w_prev, s_out, last_step, dt_lim + 2);
+}
+
+// Deferred reductions, as libafivo_hip: the step's limits stay in slots 0..2
+// and afh_fluid_fetch_step reads them -- with the V-cycle residual of
+// afh_mg_fas_vcycle_fold (slot 3) -- in one transfer
+int32_t afh_fluid_forward_euler_fold(afh_fluid *f, double dt, int32_t s_deriv, int32_t n_prev,
+                                     const int32_t *s_prev, const double *w_prev, int32_t s_out,
+                                     int32_t last_step, int32_t store_flux) {
+  (void)store_flux;
+  if (!f) return set_error(AFH_ERR_ARG, "afh_fluid_forward_euler_fold: null");
+  double lim[4];
+  int32_t e;
+  if ((e = flux_tree(f, s_deriv, lim, false))) return e;
+  return update(f, dt, s_deriv, n_prev, s_prev, w_prev, s_out, last_step, lim + 2, false);
+}
+
+int32_t afh_fluid_fetch_step(afh_fluid *f, int32_t last_step, int32_t n_extra,
+                             const int32_t *extra_slots, double *dt_lim, double *extra) {
+  if (!f || !dt_lim || (n_extra > 0 && (!extra_slots || !extra)))
+    return set_error(AFH_ERR_ARG, "afh_fluid_fetch_step: null");
+  if (n_extra < 0 || n_extra > 1) return set_error(AFH_ERR_ARG, "%d extra slots", n_extra);
+  if (n_extra && extra_slots[0] != 3)
+    return set_error(AFH_ERR_ARG, "extra slot %d (the 2-D build: 3 only)", extra_slots[0]);
+  // slots 0, 1 maxima (CFL, sigma), 2 the chemistry minimum, 3 max |res|
+  double r[4];
+  if (int32_t e = red_read(f->t, 0, n_extra ? 4 : 3, 0xB, r)) return e;
+  flux_limits(r, dt_lim);
+  dt_lim[2] = last_step ? r[2] : 1e100;
+  dt_lim[3] = 1e100;
+  if (n_extra) extra[0] = r[3];
+  return AFH_OK;
 }
 
 }  // extern "C"

@@ -64,6 +64,8 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *desc, afh_mg **out);
 int32_t afh_mg_destroy(afh_mg *mg);
 int32_t afh_mg_fas_vcycle(afh_mg *mg, int32_t set_residual, int32_t highest_lvl);
 int32_t afh_mg_fas_vcycle_maxres(afh_mg *mg, int32_t highest_lvl, double *max_res);
+/* deferred form: max|res| stays on the device for afh_fluid_fetch_step */
+int32_t afh_mg_fas_vcycle_fold(afh_mg *mg, int32_t highest_lvl);
 int32_t afh_mg_fas_fmg(afh_mg *mg, int32_t set_residual, int32_t have_guess);
 int32_t afh_mg_compute_phi_gradient(afh_mg *mg, int32_t i_fc, double fac, int32_t i_norm);
 int32_t afh_fluid_create(afh_tree *t, const afh_fluid_desc *desc, afh_fluid **out);
@@ -98,6 +100,16 @@ int32_t afh_tree_reduce_loc(afh_tree *t, int32_t iv, int32_t op, double *out,
 int32_t afh_fluid_forward_euler(afh_fluid *f, double dt, int32_t s_deriv, int32_t n_prev,
                                 const int32_t *s_prev, const double *w_prev, int32_t s_out,
                                 int32_t last_step, int32_t store_flux, double *dt_lim);
+/* Deferred reductions, as afivo_hip.h: the step's limits stay on the device
+ * and afh_fluid_fetch_step reads them with at most one extra slot
+ * (AFH_SLOT_MAXRES, the V-cycle residual of afh_mg_fas_vcycle_fold) in one
+ * transfer. */
+int32_t afh_fluid_forward_euler_fold(afh_fluid *f, double dt, int32_t s_deriv,
+                                     int32_t n_prev, const int32_t *s_prev,
+                                     const double *w_prev, int32_t s_out,
+                                     int32_t last_step, int32_t store_flux);
+int32_t afh_fluid_fetch_step(afh_fluid *f, int32_t last_step, int32_t n_extra,
+                             const int32_t *extra_slots, double *dt_lim, double *extra);
 
 #ifdef __cplusplus
 }

@@ -11,7 +11,8 @@ variable -- are bitwise those of the immediate reads (AFH_DEFER=0):
 * sharded (thread ranks), where the fetch reduces over the ranks.
 
 The C oracle's twin of the entry points on the CPU; libafivo_hip on the GPU
-(config 2 / S1 and config 3 / S3 at full size).
+(config 2 / S1 and config 3 / S3 at full size); libafivo_hip_2d's on config
+1's bench tree.
 """
 import numpy as np
 import pytest
@@ -24,7 +25,8 @@ def _unit_steps(lib, monkeypatch, defer, config, device, n=4):
     import bench
     monkeypatch.setenv("AFH_DEFER", "1" if defer else "0")
     c = bench.build_case(lib, config, device, 0)
-    c.fuse_rhs(True, ghosts=False)
+    if c.ndim == 3:
+        c.fuse_rhs(True, ghosts=False)
     out = [c.field_compute(0, n_vcycles=2)]
     for k in range(n):
         res, lim = bench.unit_step(c, 1e-13, k)
@@ -108,3 +110,13 @@ def test_driver_deferred_s3(monkeypatch):
     lib = capi.hip_library()
     _same(_driver_steps(lib, monkeypatch, True, "case_s3", 0),
           _driver_steps(lib, monkeypatch, False, "case_s3", 0))
+
+
+@pytest.mark.gpu
+def test_unit_step_deferred_2d(monkeypatch):
+    """The 2-D build's deferred entry points (round 4) on config 1's bench
+    tree: residuals, limits and every variable bitwise the immediate reads."""
+    lib = capi.hip_library_2d()
+    a = _unit_steps(lib, monkeypatch, True, "2d", 0)
+    _same(a, _unit_steps(lib, monkeypatch, False, "2d", 0))
+    assert all(len(res) == 1 for res, _ in a[0][2::2])
