@@ -47,6 +47,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -1039,6 +1040,9 @@ struct afh_tree {
   int device = 0;
   hipStream_t stream = nullptr;
   bool gc_box = true;  // level fills with corners in one launch (k2_gc_box; AFH2_GC_BOX=0)
+  // bumped by afh_set_cc_methods / afh_set_bc: boundary values and types are
+  // kernel arguments, so captured V-cycles of older generations are dropped
+  uint64_t meth_gen = 0;
   int nc = 0, ng = 0, nb = 0, nlvl = 0, nvc = 0, nvf = 0;
   int bsz = 0, fsz = 0;
   int cgs[2] = {0, 0};
@@ -1076,6 +1080,18 @@ struct afh_mg {
   std::vector<Coef2> lvl_c;
   Coef2 *d_lvl_c = nullptr;  // lvl_c on the device (residual of every level in one launch)
   bool all_lvl = true;       // AFH2_ALL_LVL=0: one residual / gradient launch per level
+  // V-cycles replayed as hipGraphs (launch gaps of the ~70 small launches of
+  // a config-1 V-cycle), one per (highest level, residual, max) variant;
+  // AFH2_GRAPHS=0: eager. The first call of a variant runs eagerly (the
+  // coarse-solve tables are built outside capture); a boundary-condition
+  // change drops the graphs
+  struct Graph {
+    hipGraphExec_t exec = nullptr;
+    bool warm = false;
+    uint64_t gen = 0;
+  };
+  std::map<int, Graph> graphs;
+  bool use_graphs = true;
   int nx = 0, ny = 0;
   double *d_q[2] = {nullptr, nullptr}, *d_e[2] = {nullptr, nullptr};
   int q_bc[4] = {0, 0, 0, 0};
@@ -1341,6 +1357,7 @@ int32_t afh_set_cc_methods(afh_tree *t, int32_t iv, const afh_bc *bc, int32_t rb
   for (int q = 0; q < 4; q++) m.bc[q] = bc[q];
   m.rb = rb;
   m.lim = lim;
+  t->meth_gen++;
   return AFH_OK;
 }
 
@@ -1352,6 +1369,7 @@ int32_t afh_set_bc(afh_tree *t, int32_t iv, int32_t nb, int32_t type, double val
     return set_error(AFH_ERR_ARG, "afh_set_bc: type %d", type);
   t->meth[iv].bc[nb - 1].type = type;
   t->meth[iv].bc[nb - 1].value = value;
+  t->meth_gen++;
   return AFH_OK;
 }
 
@@ -1473,6 +1491,7 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
   H2(hipMalloc(&mg->d_lvl_c, sizeof(Coef2) * t->nlvl));
   H2(hipMemcpy(mg->d_lvl_c, mg->lvl_c.data(), sizeof(Coef2) * t->nlvl, hipMemcpyHostToDevice));
   if (const char *env = getenv("AFH2_ALL_LVL")) mg->all_lvl = atoi(env) != 0;
+  if (const char *env = getenv("AFH2_GRAPHS")) mg->use_graphs = atoi(env) != 0;
   H2(hipMalloc(&mg->d_q[0], sizeof(double) * nx * nx));
   H2(hipMalloc(&mg->d_q[1], sizeof(double) * ny * ny));
   H2(hipMalloc(&mg->d_e[0], sizeof(double) * nx));
@@ -1491,6 +1510,8 @@ int32_t afh_mg_destroy(afh_mg *mg) {
   for (int q = 0; q < 2; q++) hipFree(mg->d_q[q]), hipFree(mg->d_e[q]);
   hipFree(mg->alt);
   hipFree(mg->d_lvl_c);
+  for (auto &g : mg->graphs)
+    if (g.second.exec) hipGraphExecDestroy(g.second.exec);
   delete mg;
   return AFH_OK;
 }
@@ -1702,6 +1723,40 @@ static int32_t vcycle(afh_mg *mg, bool set_residual, int max_lvl, bool max_out) 
   return AFH_OK;
 }
 
+// vcycle, replayed from a captured graph once a variant has run eagerly
+// (not while kernels are being timed: the events are host calls)
+static int32_t vcycle_run(afh_mg *mg, bool set_residual, int max_lvl, bool max_out) {
+  afh_tree *t = mg->t;
+  if (!mg->use_graphs || t->prof_class) return vcycle(mg, set_residual, max_lvl, max_out);
+  const int key = (max_lvl << 2) | (set_residual ? 2 : 0) | (max_out ? 1 : 0);
+  afh_mg::Graph &g = mg->graphs[key];
+  if (g.gen != t->meth_gen) {
+    if (g.exec) hipGraphExecDestroy(g.exec);
+    g = afh_mg::Graph();
+    g.gen = t->meth_gen;
+  }
+  if (!g.warm) {
+    g.warm = true;
+    return vcycle(mg, set_residual, max_lvl, max_out);
+  }
+  if (!g.exec) {
+    hipGraph_t graph;
+    H2(hipStreamBeginCapture(t->stream, hipStreamCaptureModeThreadLocal));
+    const int32_t e = vcycle(mg, set_residual, max_lvl, max_out);
+    const hipError_t ce = hipStreamEndCapture(t->stream, &graph);
+    if (e) {
+      if (ce == hipSuccess) hipGraphDestroy(graph);
+      return e;
+    }
+    H2(ce);
+    const hipError_t ie = hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0);
+    hipGraphDestroy(graph);
+    H2(ie);
+  }
+  H2(hipGraphLaunch(g.exec, t->stream));
+  return AFH_OK;
+}
+
 }  // namespace afh2
 
 extern "C" {
@@ -1709,19 +1764,19 @@ extern "C" {
 int32_t afh_mg_fas_vcycle(afh_mg *mg, int32_t set_residual, int32_t hl) {
   if (!mg) return set_error(AFH_ERR_ARG, "null mg");
   const int max_lvl = (hl > 0 && hl <= mg->t->nlvl) ? hl : mg->t->nlvl;
-  return vcycle(mg, set_residual != 0, max_lvl, false);
+  return vcycle_run(mg, set_residual != 0, max_lvl, false);
 }
 
 int32_t afh_mg_fas_vcycle_fold(afh_mg *mg, int32_t hl) {
   if (!mg) return set_error(AFH_ERR_ARG, "null mg");
   const int max_lvl = (hl > 0 && hl <= mg->t->nlvl) ? hl : mg->t->nlvl;
-  return vcycle(mg, true, max_lvl, true);
+  return vcycle_run(mg, true, max_lvl, true);
 }
 
 int32_t afh_mg_fas_vcycle_maxres(afh_mg *mg, int32_t hl, double *max_res) {
   if (!mg || !max_res) return set_error(AFH_ERR_ARG, "afh_mg_fas_vcycle_maxres: null");
   const int max_lvl = (hl > 0 && hl <= mg->t->nlvl) ? hl : mg->t->nlvl;
-  if (int32_t e = vcycle(mg, true, max_lvl, true)) return e;
+  if (int32_t e = vcycle_run(mg, true, max_lvl, true)) return e;
   return red_read(mg->t, 3, 1, 1, max_res);
 }
 

@@ -34,7 +34,8 @@ Round 4:
 * AFH2_GC_BOX: a 2-D level fill with corners in one workgroup per box
   (k2_gc_box) vs k2_gc + k2_corners;
 * AFH2_ALL_LVL: the 2-D residual and gradient of every level in one launch
-  vs one launch per level.
+  vs one launch per level;
+* AFH2_GRAPHS: 2-D V-cycles replayed from captured graphs vs eager.
 
 The fused forms are also what every other GPU test runs (they are the
 defaults); these tests pin them to the unfused forms on full workloads.
@@ -198,6 +199,17 @@ def test_2d_all_level_launches_bitwise(config, monkeypatch):
     monkeypatch.setitem(bench.CONFIGS, "c2d16", (16, (16, 16), 4, (16e-3, 16e-3)))
     _same(_case2d(monkeypatch, {"AFH2_ALL_LVL": "1"}, config),
           _case2d(monkeypatch, {"AFH2_ALL_LVL": "0"}, config))
+
+
+@pytest.mark.parametrize("config", ["2d", "c2d16"])
+def test_2d_vcycle_graphs_bitwise(config, monkeypatch):
+    """2-D V-cycles replayed from captured hipGraphs (AFH2_GRAPHS) against
+    eager launches: field solves (the first V-cycle of a variant eager, the
+    next captured) and four unit steps, every variable bitwise."""
+    import bench
+    monkeypatch.setitem(bench.CONFIGS, "c2d16", (16, (16, 16), 4, (16e-3, 16e-3)))
+    _same(_case2d(monkeypatch, {"AFH2_GRAPHS": "1"}, config),
+          _case2d(monkeypatch, {"AFH2_GRAPHS": "0"}, config))
 
 
 @pytest.mark.parametrize("switch", ["AFH_PROLONG_PUSH", "AFH_RSTR_PUSH"])
