@@ -936,18 +936,24 @@ __device__ __forceinline__ double rate_of(const UpdArgs &A, const DevReaction &R
 
 // flux_update_densities + add_source_terms of one leaf cell: y = sum_m w_m
 // y_prev_m, chemistry source dt * derivs (+ the chemistry limit on the last
-// step), then the flux divergence of the electrons (flux species)
+// step), then the flux divergence of the electrons (flux species). NS: the
+// species count when it is a compile-time case (the per-cell arrays then stay
+// in registers; wave-uniform indices use VGPR index mode), MAXS for any count
+// (A.ns; the arrays in scratch)
+template <int NS>
 __global__ void __launch_bounds__(NT)
     k2_update(UpdArgs A, const int32_t *__restrict__ ids, const afh_box_meta *__restrict__ meta,
               int nc, int bsz, int fsz, unsigned long long *red) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   double cmin = 1e100;
+  const int ns = NS == MAXS ? A.ns : NS;
   if (t < nc * nc) {
     const int id = ids[blockIdx.y];
     const int i = t % nc + 1, j = t / nc + 1, ng = nc + 2, nf = nc + 1;
     const size_t x = (size_t)(id - 1) * bsz + ix2(ng, i, j);
-    double y[MAXS], dens[MAXS], der[MAXS];
-    for (int s = 0; s < A.ns; s++) {
+    double y[NS], dens[NS], der[NS];
+#pragma unroll
+    for (int s = 0; s < ns; s++) {
       double tmp = 0.0;
       for (int q = 0; q < A.n_prev; q++) tmp = tmp + A.w_prev[q] * A.prev[s][q][x];
       y[s] = tmp;
@@ -968,7 +974,8 @@ __global__ void __launch_bounds__(NT)
     }
     if (A.last_step) {
       const double eps = 1e-100;
-      for (int s = 0; s < A.ns; s++) {
+#pragma unroll
+      for (int s = 0; s < ns; s++) {
         double a, b;
         if (A.dt_chemistry_nmin > 0) {
           a = dens[s] + A.dt_chemistry_nmin;
@@ -981,13 +988,15 @@ __global__ void __launch_bounds__(NT)
         cmin = fmin(cmin, a / b);
       }
     }
-    for (int s = 0; s < A.ns; s++) y[s] = y[s] + A.dt * der[s];
+#pragma unroll
+    for (int s = 0; s < ns; s++) y[s] = y[s] + A.dt * der[s];
     const double *F = A.F + (size_t)(id - 1) * fsz;
     const int f0 = (j - 1) * nf + (i - 1), d2 = nf * nf;
     const double dtx = A.dt / meta[id - 1].dr[0], dty = A.dt / meta[id - 1].dr[1];
     const int e = A.e_index;
     y[e] = y[e] + dtx * (F[f0] - F[f0 + 1]) + dty * (F[d2 + f0] - F[d2 + f0 + nf]);
-    for (int s = 0; s < A.ns; s++) A.out[s][x] = y[s];
+#pragma unroll
+    for (int s = 0; s < ns; s++) A.out[s][x] = y[s];
   }
   if (A.last_step) block_fold<false>(cmin, red);
 }
@@ -1107,6 +1116,9 @@ struct afh_fluid {
   afh_fluid_desc d;
   double *d_td = nullptr, *d_chem = nullptr;
   DevReaction *d_reac = nullptr;
+  // k2_update compiled for the species count (1..12; AFH2_UPD_FIXED=0 for the
+  // any-count form)
+  bool upd_fixed = true;
 };
 
 namespace afh2 {
@@ -1884,6 +1896,7 @@ int32_t afh_fluid_create(afh_tree *t, const afh_fluid_desc *d, afh_fluid **out) 
       return set_error(AFH_ERR_UNSUPPORTED, "2-D: rate type %d", ty);
   }
   afh_fluid *f = new afh_fluid();
+  if (const char *env = getenv("AFH2_UPD_FIXED")) f->upd_fixed = atoi(env) != 0;
   f->t = t;
   f->d = *d;
   f->d.reactions = nullptr;
@@ -2049,9 +2062,19 @@ static int32_t update(afh_fluid *f, double dt, int32_t s_deriv, int32_t n_prev,
   for (int l = 1; l <= t->nlvl; l++) {
     const int n = t->leaves.n(l);
     if (!n) continue;
-    hipLaunchKernelGGL(k2_update, grid2(t->nc * t->nc, n), dim3(NT), 0, t->stream, A,
-                       t->leaves.at(l), t->d_boxes, t->nc, t->bsz, t->fsz,
-                       t->red + 2 * RED_SHARDS);
+    const dim3 g = grid2(t->nc * t->nc, n);
+    const int32_t *ids = t->leaves.at(l);
+    unsigned long long *red = t->red + 2 * RED_SHARDS;
+    switch (f->upd_fixed ? A.ns : 0) {
+#define AFH2_UPD(N) \
+  case N: hipLaunchKernelGGL(k2_update<N>, g, dim3(NT), 0, t->stream, A, ids, t->d_boxes, t->nc, t->bsz, t->fsz, red); break;
+      AFH2_UPD(1) AFH2_UPD(2) AFH2_UPD(3) AFH2_UPD(4) AFH2_UPD(5) AFH2_UPD(6) AFH2_UPD(7)
+      AFH2_UPD(8) AFH2_UPD(9) AFH2_UPD(10) AFH2_UPD(11) AFH2_UPD(12)
+#undef AFH2_UPD
+    default:
+      hipLaunchKernelGGL(k2_update<MAXS>, g, dim3(NT), 0, t->stream, A, ids, t->d_boxes,
+                         t->nc, t->bsz, t->fsz, red);
+    }
     H2_LAUNCH("k2_update");
   }
   dt_lim[0] = 1e100, dt_lim[1] = 1e100;

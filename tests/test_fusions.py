@@ -35,7 +35,8 @@ Round 4:
   (k2_gc_box) vs k2_gc + k2_corners;
 * AFH2_ALL_LVL: the 2-D residual and gradient of every level in one launch
   vs one launch per level;
-* AFH2_GRAPHS: 2-D V-cycles replayed from captured graphs vs eager.
+* AFH2_GRAPHS: 2-D V-cycles replayed from captured graphs vs eager;
+* AFH2_UPD_FIXED: the 2-D update compiled for the species count vs any count.
 
 The fused forms are also what every other GPU test runs (they are the
 defaults); these tests pin them to the unfused forms on full workloads.
@@ -210,6 +211,14 @@ def test_2d_vcycle_graphs_bitwise(config, monkeypatch):
     monkeypatch.setitem(bench.CONFIGS, "c2d16", (16, (16, 16), 4, (16e-3, 16e-3)))
     _same(_case2d(monkeypatch, {"AFH2_GRAPHS": "1"}, config),
           _case2d(monkeypatch, {"AFH2_GRAPHS": "0"}, config))
+
+
+def test_2d_update_fixed_species_bitwise(monkeypatch):
+    """k2_update compiled for the species count (AFH2_UPD_FIXED, arrays in
+    registers) against the any-count form (arrays in scratch): field solves
+    and four unit steps on config 1's tree, every variable bitwise."""
+    _same(_case2d(monkeypatch, {"AFH2_UPD_FIXED": "1"}, "2d"),
+          _case2d(monkeypatch, {"AFH2_UPD_FIXED": "0"}, "2d"))
 
 
 @pytest.mark.parametrize("switch", ["AFH_PROLONG_PUSH", "AFH_RSTR_PUSH"])
