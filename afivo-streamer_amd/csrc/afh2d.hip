@@ -263,14 +263,23 @@ __global__ void k2_corners(double *__restrict__ v, const afh_box_meta *__restric
 // ghosts (k2_gc), a barrier, its corners (k2_corners: a diagonal
 // neighbour's interior cell, or extrapolated from this box's side ghosts).
 // The side ghosts read interior cells only, so boxes need not wait for each
-// other; the same values as the two launches (AFH2_GC_BOX=0)
-__global__ void __launch_bounds__(64)
+// other; the same values as the two launches (AFH2_GC_BOX=0). per > 1: per
+// boxes in one workgroup, 4 nc lanes each (8^2 boxes: 8 per 256 lanes, all
+// lanes busy and a quarter of the waves of one 64-lane workgroup per box)
+__global__ void __launch_bounds__(256)
     k2_gc_box(double *__restrict__ v, const afh_box_meta *__restrict__ meta,
-              const int32_t *__restrict__ ids, int nc, int bsz, Bc4 g) {
-  const int id = ids[blockIdx.x];
-  for (int t = threadIdx.x; t < 4 * nc; t += blockDim.x) gc2_side(v, meta, id, t, nc, bsz, g);
+              const int32_t *__restrict__ ids, int n, int per, int nc, int bsz, Bc4 g) {
+  const int L = 4 * nc;
+  if (per > 1) {
+    const int sub = threadIdx.x / L, b = blockIdx.x * per + sub;
+    if (sub < per && b < n) gc2_side(v, meta, ids[b], threadIdx.x % L, nc, bsz, g);
+  } else {
+    const int id = ids[blockIdx.x];
+    for (int t = threadIdx.x; t < L; t += blockDim.x) gc2_side(v, meta, id, t, nc, bsz, g);
+  }
   __syncthreads();
-  if (threadIdx.x < 4) gc2_corner(v, meta, id, threadIdx.x, nc, bsz);
+  const int b = blockIdx.x * per + (threadIdx.x >> 2);
+  if ((int)threadIdx.x < 4 * per && b < n) gc2_corner(v, meta, ids[b], threadIdx.x & 3, nc, bsz);
 }
 
 // ------------------------------------------------------------ multigrid
@@ -1049,6 +1058,7 @@ struct afh_tree {
   int device = 0;
   hipStream_t stream = nullptr;
   bool gc_box = true;  // level fills with corners in one launch (k2_gc_box; AFH2_GC_BOX=0)
+  bool gc_pack = true;  // several small boxes per k2_gc_box workgroup (AFH2_GC_PACK=0)
   // bumped by afh_set_cc_methods / afh_set_bc: boundary values and types are
   // kernel arguments, so captured V-cycles of older generations are dropped
   uint64_t meth_gen = 0;
@@ -1169,8 +1179,10 @@ static int32_t gc_lvl(afh_tree *t, int lvl, int iv, bool corners) {
   const int n = t->ids.n(lvl);
   if (!n) return AFH_OK;
   if (corners && t->gc_box) {
-    hipLaunchKernelGGL(k2_gc_box, dim3(n), dim3(64), 0, t->stream, t->ccv(iv), t->d_boxes,
-                       t->ids.at(lvl), t->nc, t->bsz, t->bc4(iv));
+    const int L = 4 * t->nc, per = t->gc_pack && L <= 128 ? 256 / L : 1;
+    hipLaunchKernelGGL(k2_gc_box, dim3((n + per - 1) / per), dim3(per > 1 ? per * L : 64), 0,
+                       t->stream, t->ccv(iv), t->d_boxes, t->ids.at(lvl), n, per, t->nc,
+                       t->bsz, t->bc4(iv));
     H2_LAUNCH("k2_gc_box");
     return AFH_OK;
   }
@@ -1230,6 +1242,7 @@ int32_t afh_tree_create(const afh_tree_desc *desc, int32_t device, afh_tree **ou
   afh_tree *t = new afh_tree();
   H2(hipGetDevice(&t->device));
   if (const char *env = getenv("AFH2_GC_BOX")) t->gc_box = atoi(env) != 0;
+  if (const char *env = getenv("AFH2_GC_PACK")) t->gc_pack = atoi(env) != 0;
   t->nc = nc, t->ng = nc + 2, t->nb = desc->n_boxes, t->nlvl = desc->highest_lvl;
   t->nvc = desc->n_var_cell, t->nvf = desc->n_var_face;
   t->bsz = t->ng * t->ng, t->fsz = 2 * (nc + 1) * (nc + 1);

@@ -184,11 +184,14 @@ def test_2d_pair_bitwise(config, monkeypatch):
 @pytest.mark.parametrize("config", ["2d", "c2d16"])
 def test_2d_gc_box_bitwise(config, monkeypatch):
     """2-D level fills with corners in one launch (k2_gc_box, AFH2_GC_BOX)
-    against k2_gc + k2_corners: field solves and four unit steps."""
+    against k2_gc + k2_corners, and with several boxes per workgroup
+    (AFH2_GC_PACK, the default) against one: field solves and four unit
+    steps."""
     import bench
     monkeypatch.setitem(bench.CONFIGS, "c2d16", (16, (16, 16), 4, (16e-3, 16e-3)))
-    _same(_case2d(monkeypatch, {"AFH2_GC_BOX": "1"}, config),
-          _case2d(monkeypatch, {"AFH2_GC_BOX": "0"}, config))
+    packed = _case2d(monkeypatch, {"AFH2_GC_BOX": "1", "AFH2_GC_PACK": "1"}, config)
+    _same(packed, _case2d(monkeypatch, {"AFH2_GC_BOX": "0", "AFH2_GC_PACK": "1"}, config))
+    _same(packed, _case2d(monkeypatch, {"AFH2_GC_BOX": "1", "AFH2_GC_PACK": "0"}, config))
 
 
 @pytest.mark.parametrize("config", ["2d", "c2d16"])
