@@ -1133,8 +1133,18 @@ struct afh_fluid {
 
 namespace afh2 {
 
+// per-box launches: a workgroup of the work rounded up to whole waves (at
+// most NT lanes), so a small box does not dispatch idle waves (8^2 boxes:
+// one wave per box instead of four). AFH2_BLK_FIT=0 (read when a tree is
+// created): NT lanes always
+static bool g_blk_fit = true;
+static inline int blk2n(int work) {
+  return work >= NT || !g_blk_fit ? NT : ((work + 63) / 64) * 64;
+}
+static inline dim3 blk2(int work) { return dim3((unsigned)blk2n(work)); }
 static inline dim3 grid2(int work, int nbox) {
-  return dim3((unsigned)((work + NT - 1) / NT), (unsigned)nbox);
+  const int b = blk2n(work);
+  return dim3((unsigned)((work + b - 1) / b), (unsigned)nbox);
 }
 
 static int32_t upload_list(LevelList &L, const std::vector<std::vector<int32_t>> &lists) {
@@ -1186,7 +1196,7 @@ static int32_t gc_lvl(afh_tree *t, int lvl, int iv, bool corners) {
     H2_LAUNCH("k2_gc_box");
     return AFH_OK;
   }
-  hipLaunchKernelGGL(k2_gc, grid2(4 * t->nc, n), dim3(NT), 0, t->stream, t->ccv(iv),
+  hipLaunchKernelGGL(k2_gc, grid2(4 * t->nc, n), blk2(4 * t->nc), 0, t->stream, t->ccv(iv),
                      t->d_boxes, t->ids.at(lvl), t->nc, t->bsz, t->bc4(iv));
   H2_LAUNCH("k2_gc");
   if (corners) {
@@ -1243,6 +1253,10 @@ int32_t afh_tree_create(const afh_tree_desc *desc, int32_t device, afh_tree **ou
   H2(hipGetDevice(&t->device));
   if (const char *env = getenv("AFH2_GC_BOX")) t->gc_box = atoi(env) != 0;
   if (const char *env = getenv("AFH2_GC_PACK")) t->gc_pack = atoi(env) != 0;
+  {
+    const char *env = getenv("AFH2_BLK_FIT");
+    g_blk_fit = !env || atoi(env) != 0;
+  }
   t->nc = nc, t->ng = nc + 2, t->nb = desc->n_boxes, t->nlvl = desc->highest_lvl;
   t->nvc = desc->n_var_cell, t->nvf = desc->n_var_face;
   t->bsz = t->ng * t->ng, t->fsz = 2 * (nc + 1) * (nc + 1);
@@ -1451,7 +1465,7 @@ int32_t afh_restrict_tree(afh_tree *t, int32_t iv) {
   for (int l = t->nlvl - 1; l >= 1; l--) {
     const int n = t->children_of.n(l);
     if (!n) continue;
-    hipLaunchKernelGGL(k2_restrict, grid2(t->nc * t->nc / 4, n), dim3(NT), 0, t->stream,
+    hipLaunchKernelGGL(k2_restrict, grid2(t->nc * t->nc / 4, n), blk2(t->nc * t->nc / 4), 0, t->stream,
                        t->ccv(iv), t->d_boxes, t->children_of.at(l), t->nc, t->bsz);
     H2_LAUNCH("k2_restrict");
   }
@@ -1473,7 +1487,7 @@ int32_t afh_tree_maxabs_cc(afh_tree *t, int32_t iv, double *out) {
   for (int l = 1; l <= t->nlvl; l++) {
     const int n = t->leaves.n(l);
     if (!n) continue;
-    hipLaunchKernelGGL(k2_maxabs, grid2(t->nc * t->nc, n), dim3(NT), 0, t->stream, t->ccv(iv),
+    hipLaunchKernelGGL(k2_maxabs, grid2(t->nc * t->nc, n), blk2(t->nc * t->nc), 0, t->stream, t->ccv(iv),
                        t->leaves.at(l), t->nc, t->bsz, t->red + 3 * RED_SHARDS);
     H2_LAUNCH("k2_maxabs");
   }
@@ -1641,7 +1655,7 @@ static int32_t gsrb_boxes(afh_mg *mg, int lvl, bool up) {
       // levels' launches are launch-bound, another regime
       const int pc = n >= 256 ? AFH_PROF_GSRB : -1;
       prof_mark(t, pc);
-      hipLaunchKernelGGL(k2_gsrb, grid2(t->nc * t->nc / 2, n), dim3(NT), 0, t->stream,
+      hipLaunchKernelGGL(k2_gsrb, grid2(t->nc * t->nc / 2, n), blk2(t->nc * t->nc / 2), 0, t->stream,
                          t->ccv(mg->d.i_phi), t->ccv(mg->d.i_rhs), t->ids.at(lvl), t->nc,
                          t->bsz, mg->lvl_c[lvl - 1], s);
       H2_LAUNCH("k2_gsrb");
@@ -1657,7 +1671,7 @@ static int32_t update_coarse(afh_mg *mg, int lvl) {
   afh_tree *t = mg->t;
   const int n = t->ids.n(lvl);
   if (n) {
-    hipLaunchKernelGGL(k2_rstr_fas, grid2(t->nc * t->nc / 4, n), dim3(NT), 0, t->stream,
+    hipLaunchKernelGGL(k2_rstr_fas, grid2(t->nc * t->nc / 4, n), blk2(t->nc * t->nc / 4), 0, t->stream,
                        t->ccv(mg->d.i_phi), t->ccv(mg->d.i_rhs), t->ccv(mg->d.i_tmp),
                        t->d_boxes, t->ids.at(lvl), t->nc, t->bsz, mg->lvl_c[lvl - 1]);
     H2_LAUNCH("k2_rstr_fas");
@@ -1665,7 +1679,7 @@ static int32_t update_coarse(afh_mg *mg, int lvl) {
   if (int32_t e = gc_lvl(t, lvl - 1, mg->d.i_phi, true)) return e;
   const int np = t->parents.n(lvl - 1);
   if (np) {
-    hipLaunchKernelGGL(k2_parent_rhs, grid2(t->bsz, np), dim3(NT), 0, t->stream,
+    hipLaunchKernelGGL(k2_parent_rhs, grid2(t->bsz, np), blk2(t->bsz), 0, t->stream,
                        t->ccv(mg->d.i_phi), t->ccv(mg->d.i_rhs), t->ccv(mg->d.i_tmp),
                        t->parents.at(lvl - 1), t->nc, t->bsz, mg->lvl_c[lvl - 2], 1);
     H2_LAUNCH("k2_parent_rhs");
@@ -1679,11 +1693,11 @@ static int32_t correct_children(afh_mg *mg, int lvl) {
   const int np = t->parents.n(lvl - 1);
   if (!np) return AFH_OK;
   double *phi = t->ccv(mg->d.i_phi), *tmp = t->ccv(mg->d.i_tmp);
-  hipLaunchKernelGGL(k2_block, grid2(t->bsz, np), dim3(NT), 0, t->stream, tmp, phi, tmp,
+  hipLaunchKernelGGL(k2_block, grid2(t->bsz, np), blk2(t->bsz), 0, t->stream, tmp, phi, tmp,
                      t->parents.at(lvl - 1), t->bsz, 0);
   H2_LAUNCH("k2_block");
   const int nk = t->children_of.n(lvl - 1);
-  hipLaunchKernelGGL(k2_prolong, grid2(t->nc * t->nc, nk), dim3(NT), 0, t->stream, phi, tmp,
+  hipLaunchKernelGGL(k2_prolong, grid2(t->nc * t->nc, nk), blk2(t->nc * t->nc), 0, t->stream, phi, tmp,
                      t->d_boxes, t->children_of.at(lvl - 1), t->nc, t->bsz);
   H2_LAUNCH("k2_prolong");
   return AFH_OK;
@@ -1693,7 +1707,7 @@ static int32_t residual_lvl(afh_mg *mg, int lvl, const LevelList &L, bool fold) 
   afh_tree *t = mg->t;
   const int n = L.n(lvl);
   if (!n) return AFH_OK;
-  hipLaunchKernelGGL(k2_residual, grid2(t->nc * t->nc, n), dim3(NT), 0, t->stream,
+  hipLaunchKernelGGL(k2_residual, grid2(t->nc * t->nc, n), blk2(t->nc * t->nc), 0, t->stream,
                      t->ccv(mg->d.i_phi), t->ccv(mg->d.i_rhs), t->ccv(mg->d.i_tmp), L.at(lvl),
                      t->nc, t->bsz, mg->lvl_c[lvl - 1],
                      fold ? t->red + 3 * RED_SHARDS : nullptr, nullptr, nullptr);
@@ -1708,7 +1722,7 @@ static bool residual_all(afh_mg *mg, int max_lvl, const LevelList &L, bool fold)
   const int n = L.off[max_lvl] - L.off[0];
   if (!mg->all_lvl || n > 65535) return false;
   if (n)
-    hipLaunchKernelGGL(k2_residual, grid2(t->nc * t->nc, n), dim3(NT), 0, t->stream,
+    hipLaunchKernelGGL(k2_residual, grid2(t->nc * t->nc, n), blk2(t->nc * t->nc), 0, t->stream,
                        t->ccv(mg->d.i_phi), t->ccv(mg->d.i_rhs), t->ccv(mg->d.i_tmp), L.at(1),
                        t->nc, t->bsz, mg->lvl_c[0], fold ? t->red + 3 * RED_SHARDS : nullptr,
                        mg->d_lvl_c, t->d_boxes);
@@ -1819,16 +1833,16 @@ int32_t afh_mg_fas_fmg(afh_mg *mg, int32_t set_residual, int32_t have_guess) {
       if ((e = residual_lvl(mg, l, t->ids, false))) return e;
       const int n = t->ids.n(l);
       if (n) {
-        hipLaunchKernelGGL(k2_restrict, grid2(nc * nc / 4, n), dim3(NT), 0, t->stream, tmp,
+        hipLaunchKernelGGL(k2_restrict, grid2(nc * nc / 4, n), blk2(nc * nc / 4), 0, t->stream, tmp,
                            t->d_boxes, t->ids.at(l), nc, t->bsz);
-        hipLaunchKernelGGL(k2_restrict, grid2(nc * nc / 4, n), dim3(NT), 0, t->stream, phi,
+        hipLaunchKernelGGL(k2_restrict, grid2(nc * nc / 4, n), blk2(nc * nc / 4), 0, t->stream, phi,
                            t->d_boxes, t->ids.at(l), nc, t->bsz);
         H2_LAUNCH("k2_restrict");
       }
       if ((e = gc_lvl(t, l - 1, mg->d.i_phi, true))) return e;
       const int np = t->parents.n(l - 1);
       if (np) {
-        hipLaunchKernelGGL(k2_parent_rhs, grid2(t->bsz, np), dim3(NT), 0, t->stream, phi, rhs,
+        hipLaunchKernelGGL(k2_parent_rhs, grid2(t->bsz, np), blk2(t->bsz), 0, t->stream, phi, rhs,
                            tmp, t->parents.at(l - 1), nc, t->bsz, mg->lvl_c[l - 2], 0);
         H2_LAUNCH("k2_parent_rhs");
       }
@@ -1838,23 +1852,23 @@ int32_t afh_mg_fas_fmg(afh_mg *mg, int32_t set_residual, int32_t have_guess) {
     for (int l = t->nlvl; l >= 2; l--) {
       const int n = t->ids.n(l);
       if (!n) continue;
-      hipLaunchKernelGGL(k2_block, grid2(t->bsz, n), dim3(NT), 0, t->stream, phi,
+      hipLaunchKernelGGL(k2_block, grid2(t->bsz, n), blk2(t->bsz), 0, t->stream, phi,
                          (const double *)nullptr, (const double *)nullptr, t->ids.at(l),
                          t->bsz, 2);
-      hipLaunchKernelGGL(k2_restrict, grid2(nc * nc / 4, n), dim3(NT), 0, t->stream, rhs,
+      hipLaunchKernelGGL(k2_restrict, grid2(nc * nc / 4, n), blk2(nc * nc / 4), 0, t->stream, rhs,
                          t->d_boxes, t->ids.at(l), nc, t->bsz);
       H2_LAUNCH("k2_restrict");
     }
   }
   const int n1 = t->ids.n(1);
-  hipLaunchKernelGGL(k2_block, grid2(t->bsz, n1), dim3(NT), 0, t->stream, tmp, phi,
+  hipLaunchKernelGGL(k2_block, grid2(t->bsz, n1), blk2(t->bsz), 0, t->stream, tmp, phi,
                      (const double *)nullptr, t->ids.at(1), t->bsz, 1);
   H2_LAUNCH("k2_block");
   if ((e = vcycle(mg, set_residual && t->nlvl == 1, 1, false))) return e;
   for (int l = 2; l <= t->nlvl; l++) {
     const int n = t->ids.n(l);
     if (n) {
-      hipLaunchKernelGGL(k2_block, grid2(t->bsz, n), dim3(NT), 0, t->stream, tmp, phi,
+      hipLaunchKernelGGL(k2_block, grid2(t->bsz, n), blk2(t->bsz), 0, t->stream, tmp, phi,
                          (const double *)nullptr, t->ids.at(l), t->bsz, 1);
       H2_LAUNCH("k2_block");
     }
@@ -1874,7 +1888,7 @@ int32_t afh_mg_compute_phi_gradient(afh_mg *mg, int32_t i_fc, double fac, int32_
   const int n_all = t->ids.off[t->nlvl] - t->ids.off[0];
   if (mg->all_lvl && n_all <= 65535) {
     if (n_all) {
-      hipLaunchKernelGGL(k2_gradient, grid2((t->nc + 1) * (t->nc + 1), n_all), dim3(NT), 0,
+      hipLaunchKernelGGL(k2_gradient, grid2((t->nc + 1) * (t->nc + 1), n_all), blk2((t->nc + 1) * (t->nc + 1)), 0,
                          t->stream, t->ccv(mg->d.i_phi), t->fcv(i_fc),
                          i_norm ? t->ccv(i_norm) : nullptr, t->d_boxes, t->ids.at(1), t->nc,
                          t->bsz, t->fsz, fac);
@@ -1885,7 +1899,7 @@ int32_t afh_mg_compute_phi_gradient(afh_mg *mg, int32_t i_fc, double fac, int32_
   for (int l = 1; l <= t->nlvl; l++) {
     const int n = t->ids.n(l);
     if (!n) continue;
-    hipLaunchKernelGGL(k2_gradient, grid2((t->nc + 1) * (t->nc + 1), n), dim3(NT), 0,
+    hipLaunchKernelGGL(k2_gradient, grid2((t->nc + 1) * (t->nc + 1), n), blk2((t->nc + 1) * (t->nc + 1)), 0,
                        t->stream, t->ccv(mg->d.i_phi), t->fcv(i_fc),
                        i_norm ? t->ccv(i_norm) : nullptr, t->d_boxes, t->ids.at(l), t->nc,
                        t->bsz, t->fsz, fac);
@@ -1968,7 +1982,7 @@ static int32_t set_rhs(afh_fluid *f, int32_t i_rhs, int32_t s_in, double *max_rh
   for (int l = 1; l <= t->nlvl; l++) {
     const int n = t->leaves.n(l);
     if (!n) continue;
-    hipLaunchKernelGGL(k2_set_rhs, grid2(t->bsz, n), dim3(NT), 0, t->stream, t->ccv(i_rhs), A,
+    hipLaunchKernelGGL(k2_set_rhs, grid2(t->bsz, n), blk2(t->bsz), 0, t->stream, t->ccv(i_rhs), A,
                        t->leaves.at(l), t->nc, t->bsz,
                        max_rhs ? t->red + 3 * RED_SHARDS : nullptr);
     H2_LAUNCH("k2_set_rhs");
@@ -2004,7 +2018,7 @@ static int32_t flux_tree(afh_fluid *f, int32_t s_deriv, double *dt_lim, bool fet
   for (int l = 1; l <= t->nlvl; l++) {
     const int n = t->refb.n(l);
     if (!n) continue;
-    hipLaunchKernelGGL(k2_restrict, grid2(nc * nc / 4, n), dim3(NT), 0, t->stream,
+    hipLaunchKernelGGL(k2_restrict, grid2(nc * nc / 4, n), blk2(nc * nc / 4), 0, t->stream,
                        t->ccv(iv), t->d_boxes, t->refb.at(l), nc, t->bsz);
     H2_LAUNCH("k2_restrict");
   }
@@ -2022,11 +2036,11 @@ static int32_t flux_tree(afh_fluid *f, int32_t s_deriv, double *dt_lim, bool fet
   for (int l = 1; l <= t->nlvl; l++) {
     const int n = t->leaves.n(l);
     if (!n) continue;
-    hipLaunchKernelGGL(k2_gc2, grid2(4 * nc, n), dim3(NT), 0, t->stream, t->ccv(iv), t->gc2,
+    hipLaunchKernelGGL(k2_gc2, grid2(4 * nc, n), blk2(4 * nc), 0, t->stream, t->ccv(iv), t->gc2,
                        t->d_boxes, t->leaves.at(l), nc, t->bsz, t->bc4(iv));
     H2_LAUNCH("k2_gc2");
     prof_mark(t, AFH_PROF_FLUX);
-    hipLaunchKernelGGL(k2_flux, grid2(nc * nc, n), dim3(NT), 0, t->stream, A,
+    hipLaunchKernelGGL(k2_flux, grid2(nc * nc, n), blk2(nc * nc), 0, t->stream, A,
                        t->leaves.at(l), t->d_boxes, nc, t->bsz, t->fsz, t->red);
     H2_LAUNCH("k2_flux");
     // ne and |E| read, two face fields read and two fluxes written per cell
@@ -2076,16 +2090,17 @@ static int32_t update(afh_fluid *f, double dt, int32_t s_deriv, int32_t n_prev,
     const int n = t->leaves.n(l);
     if (!n) continue;
     const dim3 g = grid2(t->nc * t->nc, n);
+    const dim3 bk = blk2(t->nc * t->nc);
     const int32_t *ids = t->leaves.at(l);
     unsigned long long *red = t->red + 2 * RED_SHARDS;
     switch (f->upd_fixed ? A.ns : 0) {
 #define AFH2_UPD(N) \
-  case N: hipLaunchKernelGGL(k2_update<N>, g, dim3(NT), 0, t->stream, A, ids, t->d_boxes, t->nc, t->bsz, t->fsz, red); break;
+  case N: hipLaunchKernelGGL(k2_update<N>, g, bk, 0, t->stream, A, ids, t->d_boxes, t->nc, t->bsz, t->fsz, red); break;
       AFH2_UPD(1) AFH2_UPD(2) AFH2_UPD(3) AFH2_UPD(4) AFH2_UPD(5) AFH2_UPD(6) AFH2_UPD(7)
       AFH2_UPD(8) AFH2_UPD(9) AFH2_UPD(10) AFH2_UPD(11) AFH2_UPD(12)
 #undef AFH2_UPD
     default:
-      hipLaunchKernelGGL(k2_update<MAXS>, g, dim3(NT), 0, t->stream, A, ids, t->d_boxes,
+      hipLaunchKernelGGL(k2_update<MAXS>, g, bk, 0, t->stream, A, ids, t->d_boxes,
                          t->nc, t->bsz, t->fsz, red);
     }
     H2_LAUNCH("k2_update");
@@ -2483,7 +2498,7 @@ int32_t afh_tree_regrid(afh_tree *o, const afh_tree_desc *d, afh_tree **out) {
   if (!rchild.empty()) {
     if ((e = device_list(rchild, &d_list))) return e;
     for (int iv : o->auto_vars) {
-      hipLaunchKernelGGL(k2_restrict, grid2(nc * nc / 4, (int)rchild.size()), dim3(NT), 0,
+      hipLaunchKernelGGL(k2_restrict, grid2(nc * nc / 4, (int)rchild.size()), blk2(nc * nc / 4), 0,
                          o->stream, o->ccv(iv), o->d_boxes, d_list, nc, o->bsz);
       H2_LAUNCH("k2_restrict");
     }
@@ -2524,13 +2539,13 @@ int32_t afh_tree_regrid(afh_tree *o, const afh_tree_desc *d, afh_tree **out) {
       const Meth &m = t->meth[iv];
       auto kern = m.prolong == AFH_PROLONG_LIMIT ? k2_prolong_new<AFH_PROLONG_LIMIT>
                                                  : k2_prolong_new<AFH_PROLONG_LINEAR>;
-      hipLaunchKernelGGL(kern, grid2(hn * hn, n), dim3(NT), 0, t->stream, t->ccv(iv),
+      hipLaunchKernelGGL(kern, grid2(hn * hn, n), blk2(hn * hn), 0, t->stream, t->ccv(iv),
                          t->d_boxes, d_list, nc, t->bsz, m.prolong_lim);
       H2_LAUNCH("k2_prolong_new");
     }
     // af_gc_box of every new box (sides, then corners) once all are prolonged
     for (int iv : t->auto_vars) {
-      hipLaunchKernelGGL(k2_gc, grid2(4 * nc, n), dim3(NT), 0, t->stream, t->ccv(iv),
+      hipLaunchKernelGGL(k2_gc, grid2(4 * nc, n), blk2(4 * nc), 0, t->stream, t->ccv(iv),
                          t->d_boxes, d_list, nc, t->bsz, t->bc4(iv));
       H2_LAUNCH("k2_gc");
       hipLaunchKernelGGL(k2_corners, dim3((4 * n + NT - 1) / NT), dim3(NT), 0, t->stream,

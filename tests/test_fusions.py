@@ -36,7 +36,9 @@ Round 4:
 * AFH2_ALL_LVL: the 2-D residual and gradient of every level in one launch
   vs one launch per level;
 * AFH2_GRAPHS: 2-D V-cycles replayed from captured graphs vs eager;
-* AFH2_UPD_FIXED: the 2-D update compiled for the species count vs any count.
+* AFH2_UPD_FIXED: the 2-D update compiled for the species count vs any count;
+* AFH2_GC_PACK: several small boxes per 2-D level-fill workgroup vs one;
+* AFH2_BLK_FIT: 2-D per-box workgroups fitted to the box's work vs 256 lanes.
 
 The fused forms are also what every other GPU test runs (they are the
 defaults); these tests pin them to the unfused forms on full workloads.
@@ -214,6 +216,17 @@ def test_2d_vcycle_graphs_bitwise(config, monkeypatch):
     monkeypatch.setitem(bench.CONFIGS, "c2d16", (16, (16, 16), 4, (16e-3, 16e-3)))
     _same(_case2d(monkeypatch, {"AFH2_GRAPHS": "1"}, config),
           _case2d(monkeypatch, {"AFH2_GRAPHS": "0"}, config))
+
+
+@pytest.mark.parametrize("config", ["2d", "c2d16"])
+def test_2d_fitted_workgroups_bitwise(config, monkeypatch):
+    """2-D per-box launches with workgroups of the box's work rounded up to
+    whole waves (AFH2_BLK_FIT, the default) against 256 lanes per box: field
+    solves and four unit steps, every variable bitwise."""
+    import bench
+    monkeypatch.setitem(bench.CONFIGS, "c2d16", (16, (16, 16), 4, (16e-3, 16e-3)))
+    _same(_case2d(monkeypatch, {"AFH2_BLK_FIT": "1"}, config),
+          _case2d(monkeypatch, {"AFH2_BLK_FIT": "0"}, config))
 
 
 def test_2d_update_fixed_species_bitwise(monkeypatch):
