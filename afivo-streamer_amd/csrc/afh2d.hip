@@ -815,7 +815,12 @@ __device__ __forceinline__ void face_vd(const FluxArgs &A, double Elo, double Eh
 // One thread per cell: the low face of the cell in x and y (and the high
 // face on the last cell of a line), reconstruct_upwind_1d + the m_fluid
 // flux_upwind callback; the CFL sum of the cell over both dimensions
-// (cfl_sum = 0 + x term + y term) and the conductivity maximum are folded
+// (cfl_sum = 0 + x term + y term) and the conductivity maximum are folded.
+// SH: the high face's velocity and diffusion are the low face's of the next
+// cell (same arguments in the same order), taken from that lane when it is in
+// the wave; the last cell of a line evaluates them (AFH2_FLUX_SHFL=0: every
+// cell evaluates both faces)
+template <bool SH>
 __global__ void __launch_bounds__(NT)
     k2_flux(FluxArgs A, const int32_t *__restrict__ ids, const afh_box_meta *__restrict__ meta,
             int nc, int bsz, int fsz, unsigned long long *red) {
@@ -854,8 +859,15 @@ __global__ void __launch_bounds__(NT)
       // high face (evaluated by every cell for its CFL term; stored on the
       // last cell of the line)
       const double ex_hi = Ef[face[d] + fst[d]];
-      double vh, dh, muh;
-      face_vd(A, E[c0], E[c0 + st[d]], ex_hi, vh, dh, muh);
+      double vh = 0.0, dh = 0.0, muh = 0.0;
+      bool have = false;
+      if (SH) {
+        const int sd = d == 0 ? 1 : nc;  // lane distance of the next cell along d
+        vh = __shfl_down(vl, sd, 64);
+        dh = __shfl_down(dl, sd, 64);
+        have = c < nc && (int)(threadIdx.x & 63) + sd < 64;
+      }
+      if (!have) face_vd(A, E[c0], E[c0 + st[d]], ex_hi, vh, dh, muh);
       if (c == nc) {
         double uh;
         if (-1 * ex_hi > 0) uh = L0 + 0.5 * limiter(A.lim, Lp1 - L0, L0 - Lm1);
@@ -1059,6 +1071,7 @@ struct afh_tree {
   hipStream_t stream = nullptr;
   bool gc_box = true;  // level fills with corners in one launch (k2_gc_box; AFH2_GC_BOX=0)
   bool gc_pack = true;  // several small boxes per k2_gc_box workgroup (AFH2_GC_PACK=0)
+  bool flux_shfl = true;  // k2_flux's high faces from the next lane (AFH2_FLUX_SHFL=0)
   // bumped by afh_set_cc_methods / afh_set_bc: boundary values and types are
   // kernel arguments, so captured V-cycles of older generations are dropped
   uint64_t meth_gen = 0;
@@ -1253,6 +1266,7 @@ int32_t afh_tree_create(const afh_tree_desc *desc, int32_t device, afh_tree **ou
   H2(hipGetDevice(&t->device));
   if (const char *env = getenv("AFH2_GC_BOX")) t->gc_box = atoi(env) != 0;
   if (const char *env = getenv("AFH2_GC_PACK")) t->gc_pack = atoi(env) != 0;
+  if (const char *env = getenv("AFH2_FLUX_SHFL")) t->flux_shfl = atoi(env) != 0;
   {
     const char *env = getenv("AFH2_BLK_FIT");
     g_blk_fit = !env || atoi(env) != 0;
@@ -2040,8 +2054,12 @@ static int32_t flux_tree(afh_fluid *f, int32_t s_deriv, double *dt_lim, bool fet
                        t->d_boxes, t->leaves.at(l), nc, t->bsz, t->bc4(iv));
     H2_LAUNCH("k2_gc2");
     prof_mark(t, AFH_PROF_FLUX);
-    hipLaunchKernelGGL(k2_flux, grid2(nc * nc, n), blk2(nc * nc), 0, t->stream, A,
-                       t->leaves.at(l), t->d_boxes, nc, t->bsz, t->fsz, t->red);
+    if (t->flux_shfl)
+      hipLaunchKernelGGL(k2_flux<true>, grid2(nc * nc, n), blk2(nc * nc), 0, t->stream, A,
+                         t->leaves.at(l), t->d_boxes, nc, t->bsz, t->fsz, t->red);
+    else
+      hipLaunchKernelGGL(k2_flux<false>, grid2(nc * nc, n), blk2(nc * nc), 0, t->stream, A,
+                         t->leaves.at(l), t->d_boxes, nc, t->bsz, t->fsz, t->red);
     H2_LAUNCH("k2_flux");
     // ne and |E| read, two face fields read and two fluxes written per cell
     prof_end(t, AFH_PROF_FLUX, 48.0 * nc * nc * n);

@@ -38,7 +38,8 @@ Round 4:
 * AFH2_GRAPHS: 2-D V-cycles replayed from captured graphs vs eager;
 * AFH2_UPD_FIXED: the 2-D update compiled for the species count vs any count;
 * AFH2_GC_PACK: several small boxes per 2-D level-fill workgroup vs one;
-* AFH2_BLK_FIT: 2-D per-box workgroups fitted to the box's work vs 256 lanes.
+* AFH2_BLK_FIT: 2-D per-box workgroups fitted to the box's work vs 256 lanes;
+* AFH2_FLUX_SHFL: the 2-D flux's high faces from the next lane vs per cell.
 
 The fused forms are also what every other GPU test runs (they are the
 defaults); these tests pin them to the unfused forms on full workloads.
@@ -227,6 +228,18 @@ def test_2d_fitted_workgroups_bitwise(config, monkeypatch):
     monkeypatch.setitem(bench.CONFIGS, "c2d16", (16, (16, 16), 4, (16e-3, 16e-3)))
     _same(_case2d(monkeypatch, {"AFH2_BLK_FIT": "1"}, config),
           _case2d(monkeypatch, {"AFH2_BLK_FIT": "0"}, config))
+
+
+@pytest.mark.parametrize("config", ["2d", "c2d16"])
+def test_2d_flux_shuffle_bitwise(config, monkeypatch):
+    """k2_flux taking the high faces' velocity / diffusion from the next lane
+    (AFH2_FLUX_SHFL, the default) against evaluating them per cell: field
+    solves and four unit steps (the CFL and conductivity limits included),
+    every variable bitwise."""
+    import bench
+    monkeypatch.setitem(bench.CONFIGS, "c2d16", (16, (16, 16), 4, (16e-3, 16e-3)))
+    _same(_case2d(monkeypatch, {"AFH2_FLUX_SHFL": "1"}, config),
+          _case2d(monkeypatch, {"AFH2_FLUX_SHFL": "0"}, config))
 
 
 def test_2d_update_fixed_species_bitwise(monkeypatch):
