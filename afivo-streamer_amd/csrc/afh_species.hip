@@ -2329,7 +2329,8 @@ static int32_t flux_prelude(afh_fluid *f, int iv, double *gc2) {
     if ((e = call_hook(t, AFH_HOOK_HALO, l, iv))) return e;
     const int n = t->leaves.n(l);
     if (n) {
-      hipLaunchKernelGGL(k_gc2, dim3((nc * nc + 255) / 256, 6, n), dim3(256),
+      const int b2 = fit_blk(nc * nc);
+      hipLaunchKernelGGL(k_gc2, dim3((nc * nc + b2 - 1) / b2, 6, n), dim3(b2),
                          0, t->stream, t->ccv(iv), gc2, t->d_boxes,
                          t->leaves.at(l), nc, t->bsz, t->gc_args(iv));
       AFH_LAUNCH_CHECK("k_gc2");

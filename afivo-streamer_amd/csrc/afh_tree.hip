@@ -486,7 +486,7 @@ int32_t gc_lvl_var(afh_tree *t, int lvl, int iv, const double *vc,
       prof_end(t, AFH_PROF_GHOST, 16.0 * 6 * nc * nc * n);
       AFH_LAUNCH_CHECK("k_gc_faces");
       if (corners) {
-        hipLaunchKernelGGL(k_gc_corners, dim3(n), dim3(256), 0, t->stream, v,
+        hipLaunchKernelGGL(k_gc_corners, dim3(n), dim3(fit_blk(12 * nc)), 0, t->stream, v,
                            t->d_boxes, t->ids.at(lvl), nc, t->bsz);
         AFH_LAUNCH_CHECK("k_gc_corners");
       }
@@ -499,7 +499,7 @@ int32_t gc_lvl_var(afh_tree *t, int lvl, int iv, const double *vc,
 int32_t gc_lvl_corners(afh_tree *t, int lvl, int iv) {
   const int n = t->ids.n(lvl);
   if (!n) return AFH_OK;
-  hipLaunchKernelGGL(k_gc_corners, dim3(n), dim3(256), 0, t->stream, t->var(iv), t->d_boxes,
+  hipLaunchKernelGGL(k_gc_corners, dim3(n), dim3(fit_blk(12 * t->nc)), 0, t->stream, t->var(iv), t->d_boxes,
                      t->ids.at(lvl), t->nc, t->bsz);
   AFH_LAUNCH_CHECK("k_gc_corners");
   return AFH_OK;
@@ -1607,7 +1607,7 @@ int32_t afh_tree_regrid(afh_tree *o, const afh_tree_desc *d, afh_tree **out) {
                          t->stream, t->ccv(iv), t->ccv(iv), t->d_boxes, d_list, nc,
                          t->bsz, t->gc_args(iv), 0, 0);  // new boxes only: no pairing
       AFH_LAUNCH_CHECK("k_gc_faces");
-      hipLaunchKernelGGL(k_gc_corners, dim3(n), dim3(256), 0, t->stream, t->ccv(iv),
+      hipLaunchKernelGGL(k_gc_corners, dim3(n), dim3(fit_blk(12 * nc)), 0, t->stream, t->ccv(iv),
                          t->d_boxes, d_list, nc, t->bsz);
       AFH_LAUNCH_CHECK("k_gc_corners");
     }
