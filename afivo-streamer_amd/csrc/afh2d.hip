@@ -1071,7 +1071,9 @@ struct afh_tree {
   hipStream_t stream = nullptr;
   bool gc_box = true;  // level fills with corners in one launch (k2_gc_box; AFH2_GC_BOX=0)
   bool gc_pack = true;  // several small boxes per k2_gc_box workgroup (AFH2_GC_PACK=0)
-  bool flux_shfl = true;  // k2_flux's high faces from the next lane (AFH2_FLUX_SHFL=0)
+  // k2_flux's high faces from the next lane (AFH2_FLUX_SHFL=1; measured
+  // neutral on config 1, profiles/r04_ab_2d_flux_shfl.txt)
+  bool flux_shfl = false;
   // bumped by afh_set_cc_methods / afh_set_bc: boundary values and types are
   // kernel arguments, so captured V-cycles of older generations are dropped
   uint64_t meth_gen = 0;

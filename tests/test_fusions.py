@@ -39,7 +39,8 @@ Round 4:
 * AFH2_UPD_FIXED: the 2-D update compiled for the species count vs any count;
 * AFH2_GC_PACK: several small boxes per 2-D level-fill workgroup vs one;
 * AFH2_BLK_FIT: 2-D per-box workgroups fitted to the box's work vs 256 lanes;
-* AFH2_FLUX_SHFL: the 2-D flux's high faces from the next lane vs per cell.
+* AFH2_FLUX_SHFL: the 2-D flux's high faces from the next lane vs per cell
+  (off by default).
 
 The fused forms are also what every other GPU test runs (they are the
 defaults); these tests pin them to the unfused forms on full workloads.
@@ -233,7 +234,7 @@ def test_2d_fitted_workgroups_bitwise(config, monkeypatch):
 @pytest.mark.parametrize("config", ["2d", "c2d16"])
 def test_2d_flux_shuffle_bitwise(config, monkeypatch):
     """k2_flux taking the high faces' velocity / diffusion from the next lane
-    (AFH2_FLUX_SHFL, the default) against evaluating them per cell: field
+    (AFH2_FLUX_SHFL; off by default, measured neutral) against evaluating them per cell: field
     solves and four unit steps (the CFL and conductivity limits included),
     every variable bitwise."""
     import bench
