@@ -361,16 +361,22 @@ __device__ __forceinline__ double gc2_face(const double *__restrict__ coarse,
 // every face ghost has one writer. src -> dst (phi / spare image, alternating
 // per pair); the coarse data of refinement faces are read from phi (the
 // coarser level, not written here). Bitwise k2_gsrb + k2_gc twice.
-template <int NC>
+// LPB lanes per box, 64 / LPB boxes per one-wave workgroup (8^2 boxes: 32
+// lanes, one per cell of a half-sweep, two boxes per wave; the lanes of a
+// missing last box load a copy of box n and store nothing)
+template <int NC, int LPB = 64>
 __global__ void __launch_bounds__(64)
     k2_pair_box(const double *__restrict__ src, double *__restrict__ dst,
                 const double *__restrict__ rhs, const double *__restrict__ coarse,
                 const afh_box_meta *__restrict__ meta, const int32_t *__restrict__ ids,
-                int bsz, Coef2 cf, Bc4 g) {
-  constexpr int NG = NC + 2, NB = NG * NG, NT = 64, H = NC / 2;
-  __shared__ double P[NB];
-  const int tid = threadIdx.x;
-  const int id = ids[blockIdx.x];
+                int n, int bsz, Coef2 cf, Bc4 g) {
+  constexpr int NG = NC + 2, NB = NG * NG, NT = LPB, H = NC / 2, PW = 64 / LPB;
+  __shared__ double P_[PW][NB];
+  const int sub = threadIdx.x / LPB, tid = threadIdx.x % LPB;
+  const int bidx = blockIdx.x * PW + sub;
+  const bool valid = bidx < n;
+  double *P = P_[sub];
+  const int id = ids[valid ? bidx : n - 1];
   const afh_box_meta &m = meta[id - 1];
   const double *x = src + (size_t)(id - 1) * bsz, *r = rhs + (size_t)(id - 1) * bsz;
   double *y = dst + (size_t)(id - 1) * bsz;
@@ -443,9 +449,9 @@ __global__ void __launch_bounds__(64)
   for (int e = tid; e < NB; e += NT) {
     const int i = e % NG, j = e / NG;
     const int nout = (i == 0 || i == NG - 1) + (j == 0 || j == NG - 1);
-    if (nout != 1) y[e] = P[e];
+    if (valid && nout != 1) y[e] = P[e];
   }
-  for (int u = tid; u < 4 * NC; u += NT) {
+  for (int u = valid ? tid : 4 * NC; u < 4 * NC; u += NT) {
     const int nb = u / NC + 1, a = u % NC + 1, d = (nb - 1) >> 1;
     const bool low = ((nb - 1) & 1) == 0;
     const int gi = low ? 0 : NC + 1, i1 = low ? 1 : NC, i2 = low ? 2 : NC - 1;
@@ -1126,6 +1132,7 @@ struct afh_mg {
   };
   std::map<int, Graph> graphs;
   bool use_graphs = true;
+  bool pair_pack = true;  // 2 (8^2) / 4 (4^2) boxes per k2_pair_box wave (AFH2_PAIR_PACK=0: one)
   int nx = 0, ny = 0;
   double *d_q[2] = {nullptr, nullptr}, *d_e[2] = {nullptr, nullptr};
   int q_bc[4] = {0, 0, 0, 0};
@@ -1547,6 +1554,7 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
   H2(hipMemcpy(mg->d_lvl_c, mg->lvl_c.data(), sizeof(Coef2) * t->nlvl, hipMemcpyHostToDevice));
   if (const char *env = getenv("AFH2_ALL_LVL")) mg->all_lvl = atoi(env) != 0;
   if (const char *env = getenv("AFH2_GRAPHS")) mg->use_graphs = atoi(env) != 0;
+  if (const char *env = getenv("AFH2_PAIR_PACK")) mg->pair_pack = atoi(env) != 0;
   H2(hipMalloc(&mg->d_q[0], sizeof(double) * nx * nx));
   H2(hipMalloc(&mg->d_q[1], sizeof(double) * ny * ny));
   H2(hipMalloc(&mg->d_e[0], sizeof(double) * nx));
@@ -1645,15 +1653,23 @@ static int32_t gsrb_boxes(afh_mg *mg, int lvl, bool up) {
       // timed on levels of >= 256 boxes, as the split half-sweeps
       const int pc = n >= 256 ? AFH_PROF_GSRB : -1;
       prof_mark(t, pc);
-      if (t->nc == 4)
-        hipLaunchKernelGGL(k2_pair_box<4>, dim3(n), dim3(64), 0, t->stream, src, dst,
-                           t->ccv(mg->d.i_rhs), phi, t->d_boxes, t->ids.at(lvl), t->bsz, cf, g);
+      const double *rh = t->ccv(mg->d.i_rhs);
+      const int32_t *ids = t->ids.at(lvl);
+      if (t->nc == 4 && mg->pair_pack)
+        hipLaunchKernelGGL((k2_pair_box<4, 16>), dim3((n + 3) / 4), dim3(64), 0, t->stream, src,
+                           dst, rh, phi, t->d_boxes, ids, n, t->bsz, cf, g);
+      else if (t->nc == 4)
+        hipLaunchKernelGGL(k2_pair_box<4>, dim3(n), dim3(64), 0, t->stream, src, dst, rh, phi,
+                           t->d_boxes, ids, n, t->bsz, cf, g);
+      else if (t->nc == 8 && mg->pair_pack)
+        hipLaunchKernelGGL((k2_pair_box<8, 32>), dim3((n + 1) / 2), dim3(64), 0, t->stream, src,
+                           dst, rh, phi, t->d_boxes, ids, n, t->bsz, cf, g);
       else if (t->nc == 8)
-        hipLaunchKernelGGL(k2_pair_box<8>, dim3(n), dim3(64), 0, t->stream, src, dst,
-                           t->ccv(mg->d.i_rhs), phi, t->d_boxes, t->ids.at(lvl), t->bsz, cf, g);
+        hipLaunchKernelGGL(k2_pair_box<8>, dim3(n), dim3(64), 0, t->stream, src, dst, rh, phi,
+                           t->d_boxes, ids, n, t->bsz, cf, g);
       else
-        hipLaunchKernelGGL(k2_pair_box<16>, dim3(n), dim3(64), 0, t->stream, src, dst,
-                           t->ccv(mg->d.i_rhs), phi, t->d_boxes, t->ids.at(lvl), t->bsz, cf, g);
+        hipLaunchKernelGGL(k2_pair_box<16>, dim3(n), dim3(64), 0, t->stream, src, dst, rh, phi,
+                           t->d_boxes, ids, n, t->bsz, cf, g);
       H2_LAUNCH("k2_pair_box");
       // a red+black pair reads phi and rhs and writes phi once = 24 B/cell
       prof_end(t, pc, 24.0 * t->nc * t->nc * n);

@@ -40,7 +40,8 @@ Round 4:
 * AFH2_GC_PACK: several small boxes per 2-D level-fill workgroup vs one;
 * AFH2_BLK_FIT: 2-D per-box workgroups fitted to the box's work vs 256 lanes;
 * AFH2_FLUX_SHFL: the 2-D flux's high faces from the next lane vs per cell
-  (off by default).
+  (off by default);
+* AFH2_PAIR_PACK: two 8^2 / four 4^2 boxes per 2-D pair wave vs one.
 
 The fused forms are also what every other GPU test runs (they are the
 defaults); these tests pin them to the unfused forms on full workloads.
@@ -229,6 +230,18 @@ def test_2d_fitted_workgroups_bitwise(config, monkeypatch):
     monkeypatch.setitem(bench.CONFIGS, "c2d16", (16, (16, 16), 4, (16e-3, 16e-3)))
     _same(_case2d(monkeypatch, {"AFH2_BLK_FIT": "1"}, config),
           _case2d(monkeypatch, {"AFH2_BLK_FIT": "0"}, config))
+
+
+@pytest.mark.parametrize("config", ["2d", "c2d4"])
+def test_2d_pair_packed_bitwise(config, monkeypatch):
+    """The 2-D fused pair with two 8^2 (four 4^2) boxes per wave
+    (AFH2_PAIR_PACK, the default; level 1's single box leaves half a wave
+    without a box) against one box per wave: field solves and four unit
+    steps, every variable bitwise."""
+    import bench
+    monkeypatch.setitem(bench.CONFIGS, "c2d4", (4, (4, 4), 6, (16e-3, 16e-3)))
+    _same(_case2d(monkeypatch, {"AFH2_PAIR_PACK": "1"}, config),
+          _case2d(monkeypatch, {"AFH2_PAIR_PACK": "0"}, config))
 
 
 @pytest.mark.parametrize("config", ["2d", "c2d16"])
