@@ -234,22 +234,28 @@ __global__ void __launch_bounds__(NT)
 
 // af_gc_box_corner (2-D): copy from the diagonal neighbour, or extrapolate
 // from the side ghost cells (af_corner_gc_extrap); one thread per corner
-__device__ __forceinline__ void gc2_corner(double *__restrict__ v,
-                                           const afh_box_meta *__restrict__ meta, int id,
-                                           int cn, int nc, int bsz) {
+__device__ __forceinline__ double gc2_corner_val(const double *__restrict__ v,
+                                                 const afh_box_meta *__restrict__ meta, int id,
+                                                 int cn, int nc, int bsz) {
   const int dx = cn & 1, dy = cn >> 1;  // af_child_dix of corner cn + 1
   const int ng = nc + 2;
   const int ix = dx * (nc + 1), iy = dy * (nc + 1);
   const int nb_id = meta[id - 1].neighbor_mat[(2 * dx) + 3 * (2 * dy)];
-  double *c = v + (size_t)(id - 1) * bsz;
+  const double *c = v + (size_t)(id - 1) * bsz;
   if (nb_id > 0) {
     const int sx = 2 * dx - 1, sy = 2 * dy - 1;
-    c[ix2(ng, ix, iy)] = v[(size_t)(nb_id - 1) * bsz + ix2(ng, ix - sx * nc, iy - sy * nc)];
-  } else {
-    const int di = 1 - 2 * (ix & 1), dj = 1 - 2 * (iy & 1);
-    c[ix2(ng, ix, iy)] = c[ix2(ng, ix + di, iy)] + c[ix2(ng, ix, iy + dj)] -
-                         c[ix2(ng, ix + di, iy + dj)];
+    return v[(size_t)(nb_id - 1) * bsz + ix2(ng, ix - sx * nc, iy - sy * nc)];
   }
+  const int di = 1 - 2 * (ix & 1), dj = 1 - 2 * (iy & 1);
+  return c[ix2(ng, ix + di, iy)] + c[ix2(ng, ix, iy + dj)] - c[ix2(ng, ix + di, iy + dj)];
+}
+
+__device__ __forceinline__ void gc2_corner(double *__restrict__ v,
+                                           const afh_box_meta *__restrict__ meta, int id,
+                                           int cn, int nc, int bsz) {
+  const int ng = nc + 2, ix = (cn & 1) * (nc + 1), iy = (cn >> 1) * (nc + 1);
+  const double val = gc2_corner_val(v, meta, id, cn, nc, bsz);
+  v[(size_t)(id - 1) * bsz + ix2(ng, ix, iy)] = val;
 }
 
 __global__ void k2_corners(double *__restrict__ v, const afh_box_meta *__restrict__ meta,
@@ -563,6 +569,29 @@ __global__ void __launch_bounds__(NT)
   if (t >= bsz) return;
   const size_t o = (size_t)(ids[blockIdx.y] - 1) * bsz + t;
   dst[o] = mode == 0 ? a[o] - b[o] : (mode == 1 ? a[o] : 0.0);
+}
+
+// correct_children's tmp = phi - tmp over parent boxes whose corner ghosts
+// of phi are still to be filled (the up leg's corner pass after the fused
+// pair, folded in): a corner thread forms the corner as k2_corners does --
+// from the diagonal neighbour's interior or this box's side ghosts, neither
+// written here -- stores it and uses it
+__global__ void __launch_bounds__(NT)
+    k2_block_corners(double *__restrict__ tmp, double *__restrict__ phi,
+                     const afh_box_meta *__restrict__ meta, const int32_t *__restrict__ ids,
+                     int nc, int bsz) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= bsz) return;
+  const int id = ids[blockIdx.y], ng = nc + 2, i = t % ng, j = t / ng;
+  const size_t o = (size_t)(id - 1) * bsz + t;
+  double p;
+  if ((i == 0 || i == ng - 1) && (j == 0 || j == ng - 1)) {
+    p = gc2_corner_val(phi, meta, id, (i ? 1 : 0) + (j ? 2 : 0), nc, bsz);
+    phi[o] = p;
+  } else {
+    p = phi[o];
+  }
+  tmp[o] = p - tmp[o];
 }
 
 // max |x| over the interiors of a level's leaves (af_tree_maxabs_cc)
@@ -1132,7 +1161,10 @@ struct afh_mg {
   };
   std::map<int, Graph> graphs;
   bool use_graphs = true;
-  bool pair_pack = true;  // 2 (8^2) / 4 (4^2) boxes per k2_pair_box wave (AFH2_PAIR_PACK=0: one)
+  bool pair_pack = true;
+  // the up leg's corner pass folded into the next level's correction
+  // (k2_block_corners; AFH2_CORNER_FOLD=0 for k2_corners)
+  bool corner_fold = true;  // 2 (8^2) / 4 (4^2) boxes per k2_pair_box wave (AFH2_PAIR_PACK=0: one)
   int nx = 0, ny = 0;
   double *d_q[2] = {nullptr, nullptr}, *d_e[2] = {nullptr, nullptr};
   int q_bc[4] = {0, 0, 0, 0};
@@ -1555,6 +1587,7 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
   if (const char *env = getenv("AFH2_ALL_LVL")) mg->all_lvl = atoi(env) != 0;
   if (const char *env = getenv("AFH2_GRAPHS")) mg->use_graphs = atoi(env) != 0;
   if (const char *env = getenv("AFH2_PAIR_PACK")) mg->pair_pack = atoi(env) != 0;
+  if (const char *env = getenv("AFH2_CORNER_FOLD")) mg->corner_fold = atoi(env) != 0;
   H2(hipMalloc(&mg->d_q[0], sizeof(double) * nx * nx));
   H2(hipMalloc(&mg->d_q[1], sizeof(double) * ny * ny));
   H2(hipMalloc(&mg->d_e[0], sizeof(double) * nx));
@@ -1637,7 +1670,9 @@ static int32_t solve_coarse(afh_mg *mg) {
 
 // gsrb_boxes (m_af_multigrid.f90:648-687): 2 n_cycle half sweeps, each
 // followed by the level fill (corners after the last sweep of the up leg)
-static int32_t gsrb_boxes(afh_mg *mg, int lvl, bool up) {
+// skip_corners: the up leg's corner pass is left to correct_children of the
+// next level (every box of lvl a parent; k2_block_corners)
+static int32_t gsrb_boxes(afh_mg *mg, int lvl, bool up, bool skip_corners = false) {
   afh_tree *t = mg->t;
   const int n = t->ids.n(lvl);
   const int nc_ = up ? mg->d.n_cycle_up : mg->d.n_cycle_down;
@@ -1674,7 +1709,7 @@ static int32_t gsrb_boxes(afh_mg *mg, int lvl, bool up) {
       // a red+black pair reads phi and rhs and writes phi once = 24 B/cell
       prof_end(t, pc, 24.0 * t->nc * t->nc * n);
     }
-    if (up) {
+    if (up && !skip_corners) {
       hipLaunchKernelGGL(k2_corners, dim3((4 * n + NT - 1) / NT), dim3(NT), 0, t->stream,
                          phi, t->d_boxes, t->ids.at(lvl), n, t->nc, t->bsz);
       H2_LAUNCH("k2_corners");
@@ -1720,14 +1755,20 @@ static int32_t update_coarse(afh_mg *mg, int lvl) {
 }
 
 // correct_children of the parents of level lvl-1 (624-646)
-static int32_t correct_children(afh_mg *mg, int lvl) {
+static int32_t correct_children(afh_mg *mg, int lvl, bool corners = false) {
   afh_tree *t = mg->t;
   const int np = t->parents.n(lvl - 1);
   if (!np) return AFH_OK;
   double *phi = t->ccv(mg->d.i_phi), *tmp = t->ccv(mg->d.i_tmp);
-  hipLaunchKernelGGL(k2_block, grid2(t->bsz, np), blk2(t->bsz), 0, t->stream, tmp, phi, tmp,
-                     t->parents.at(lvl - 1), t->bsz, 0);
-  H2_LAUNCH("k2_block");
+  if (corners) {
+    hipLaunchKernelGGL(k2_block_corners, grid2(t->bsz, np), blk2(t->bsz), 0, t->stream, tmp,
+                       phi, t->d_boxes, t->parents.at(lvl - 1), t->nc, t->bsz);
+    H2_LAUNCH("k2_block_corners");
+  } else {
+    hipLaunchKernelGGL(k2_block, grid2(t->bsz, np), blk2(t->bsz), 0, t->stream, tmp, phi, tmp,
+                       t->parents.at(lvl - 1), t->bsz, 0);
+    H2_LAUNCH("k2_block");
+  }
   const int nk = t->children_of.n(lvl - 1);
   hipLaunchKernelGGL(k2_prolong, grid2(t->nc * t->nc, nk), blk2(t->nc * t->nc), 0, t->stream, phi, tmp,
                      t->d_boxes, t->children_of.at(lvl - 1), t->nc, t->bsz);
@@ -1769,10 +1810,15 @@ static int32_t vcycle(afh_mg *mg, bool set_residual, int max_lvl, bool max_out) 
     if ((e = gsrb_boxes(mg, l, false)) || (e = update_coarse(mg, l))) return e;
   }
   if ((e = solve_coarse(mg))) return e;
+  afh_tree *tt = mg->t;
+  bool pend = false;  // level l-1's corners left to correct_children(l)
   for (int l = 2; l <= max_lvl; l++) {
-    if ((e = correct_children(mg, l)) || (e = gc_lvl(mg->t, l, mg->d.i_phi, true)) ||
-        (e = gsrb_boxes(mg, l, true)))
+    const bool defer = mg->corner_fold && mg->pair && l < max_lvl && tt->ids.n(l) > 0 &&
+                       tt->parents.n(l) == tt->ids.n(l);
+    if ((e = correct_children(mg, l, pend)) || (e = gc_lvl(tt, l, mg->d.i_phi, true)) ||
+        (e = gsrb_boxes(mg, l, true, defer)))
       return e;
+    pend = defer;
   }
   if (!set_residual) return AFH_OK;
   afh_tree *t = mg->t;

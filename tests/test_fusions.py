@@ -41,7 +41,8 @@ Round 4:
 * AFH2_BLK_FIT: 2-D per-box workgroups fitted to the box's work vs 256 lanes;
 * AFH2_FLUX_SHFL: the 2-D flux's high faces from the next lane vs per cell
   (off by default);
-* AFH2_PAIR_PACK: two 8^2 / four 4^2 boxes per 2-D pair wave vs one.
+* AFH2_PAIR_PACK: two 8^2 / four 4^2 boxes per 2-D pair wave vs one;
+* AFH2_CORNER_FOLD: the 2-D up leg's corners folded into the next correction.
 
 The fused forms are also what every other GPU test runs (they are the
 defaults); these tests pin them to the unfused forms on full workloads.
@@ -230,6 +231,18 @@ def test_2d_fitted_workgroups_bitwise(config, monkeypatch):
     monkeypatch.setitem(bench.CONFIGS, "c2d16", (16, (16, 16), 4, (16e-3, 16e-3)))
     _same(_case2d(monkeypatch, {"AFH2_BLK_FIT": "1"}, config),
           _case2d(monkeypatch, {"AFH2_BLK_FIT": "0"}, config))
+
+
+@pytest.mark.parametrize("config", ["2d", "c2d16"])
+def test_2d_corner_fold_bitwise(config, monkeypatch):
+    """The up leg's corner pass after the 2-D pair folded into the next
+    level's correction (k2_block_corners, AFH2_CORNER_FOLD, the default)
+    against k2_corners: field solves and four unit steps, every variable
+    (ghost cells included) bitwise."""
+    import bench
+    monkeypatch.setitem(bench.CONFIGS, "c2d16", (16, (16, 16), 4, (16e-3, 16e-3)))
+    _same(_case2d(monkeypatch, {"AFH2_CORNER_FOLD": "1"}, config),
+          _case2d(monkeypatch, {"AFH2_CORNER_FOLD": "0"}, config))
 
 
 @pytest.mark.parametrize("config", ["2d", "c2d4"])
