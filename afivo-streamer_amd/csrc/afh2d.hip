@@ -1261,8 +1261,9 @@ static int32_t gc_lvl(afh_tree *t, int lvl, int iv, bool corners) {
   return AFH_OK;
 }
 
-static int32_t red_init(afh_tree *t, int slot, double v) {
-  hipLaunchKernelGGL(k2_red_fill, dim3(1), dim3(RED_SHARDS), 0, t->stream,
+// nslot consecutive slots from slot to v, one launch
+static int32_t red_init(afh_tree *t, int slot, double v, int nslot = 1) {
+  hipLaunchKernelGGL(k2_red_fill, dim3(nslot), dim3(RED_SHARDS), 0, t->stream,
                      t->red + (size_t)slot * RED_SHARDS, host_ord(v));
   H2_LAUNCH("k2_red_fill");
   return AFH_OK;
@@ -2101,7 +2102,7 @@ static int32_t flux_tree(afh_fluid *f, int32_t s_deriv, double *dt_lim, bool fet
     H2_LAUNCH("k2_restrict");
   }
   int32_t e;
-  if ((e = red_init(t, 0, -HUGE_VAL)) || (e = red_init(t, 1, -HUGE_VAL))) return e;
+  if ((e = red_init(t, 0, -HUGE_VAL, 2))) return e;  // CFL and conductivity maxima
   FluxArgs A;
   A.ne = t->ccv(iv), A.E = t->ccv(f->d.i_efld), A.Ef = t->fcv(f->d.f_field);
   A.F = t->fcv(f->d.f_flux), A.gc2 = t->gc2;
