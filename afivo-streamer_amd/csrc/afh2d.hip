@@ -1106,6 +1106,13 @@ struct afh_tree {
   hipStream_t stream = nullptr;
   bool gc_box = true;  // level fills with corners in one launch (k2_gc_box; AFH2_GC_BOX=0)
   bool gc_pack = true;  // several small boxes per k2_gc_box workgroup (AFH2_GC_PACK=0)
+  // a box has a refinement boundary (a side ghost then reads the parent
+  // neighbour's tangential ghost, so levels fill in order)
+  bool any_refb = false;
+  // afh_gc_tree of a tree without refinement boundaries in one launch (every
+  // read an interior cell or, for corners, the box's own side ghosts;
+  // AFH2_GC_TREE_ONE=0 level by level)
+  bool gc_tree_one = true;
   // k2_flux's high faces from the next lane (AFH2_FLUX_SHFL=1; measured
   // neutral on config 1, profiles/r04_ab_2d_flux_shfl.txt)
   bool flux_shfl = false;
@@ -1239,9 +1246,12 @@ static void free_list(LevelList &L) {
   L.d = nullptr;
 }
 
+// lvl = 0: every level in one launch (afh_gc_tree without refinement
+// boundaries)
 static int32_t gc_lvl(afh_tree *t, int lvl, int iv, bool corners) {
-  const int n = t->ids.n(lvl);
+  const int n = lvl ? t->ids.n(lvl) : t->ids.off[t->nlvl] - t->ids.off[0];
   if (!n) return AFH_OK;
+  if (!lvl) lvl = 1;  // ids.at(1): the list of every level from level 1
   if (corners && t->gc_box) {
     const int L = 4 * t->nc, per = t->gc_pack && L <= 128 ? 256 / L : 1;
     hipLaunchKernelGGL(k2_gc_box, dim3((n + per - 1) / per), dim3(per > 1 ? per * L : 64), 0,
@@ -1308,6 +1318,7 @@ int32_t afh_tree_create(const afh_tree_desc *desc, int32_t device, afh_tree **ou
   H2(hipGetDevice(&t->device));
   if (const char *env = getenv("AFH2_GC_BOX")) t->gc_box = atoi(env) != 0;
   if (const char *env = getenv("AFH2_GC_PACK")) t->gc_pack = atoi(env) != 0;
+  if (const char *env = getenv("AFH2_GC_TREE_ONE")) t->gc_tree_one = atoi(env) != 0;
   if (const char *env = getenv("AFH2_FLUX_SHFL")) t->flux_shfl = atoi(env) != 0;
   {
     const char *env = getenv("AFH2_BLK_FIT");
@@ -1340,6 +1351,8 @@ int32_t afh_tree_create(const afh_tree_desc *desc, int32_t device, afh_tree **ou
       const afh_box_meta &m = t->boxes[id - 1];
       t->lvl_dr[2 * (l - 1)] = m.dr[0], t->lvl_dr[2 * (l - 1) + 1] = m.dr[1];
     }
+    for (int id : t->h_ids[l - 1])
+      for (int nb = 0; nb < 4; nb++) t->any_refb = t->any_refb || t->boxes[id - 1].neighbors[nb] == 0;
     for (int id : t->h_leaves[l - 1]) {
       const afh_box_meta &m = t->boxes[id - 1];
       bool rb = false;
@@ -1510,6 +1523,7 @@ int32_t afh_gc_lvl(afh_tree *t, int32_t lvl, int32_t iv, int32_t corners) {
 int32_t afh_gc_tree(afh_tree *t, int32_t iv, int32_t corners) {
   if (int32_t e = check_iv(t, iv, "afh_gc_tree")) return e;
   if (!t->meth[iv].set) return set_error(AFH_ERR_STATE, "afh_gc_tree: no methods for %d", iv);
+  if (t->gc_tree_one && !t->any_refb && corners && t->gc_box) return gc_lvl(t, 0, iv, true);
   for (int l = 1; l <= t->nlvl; l++)
     if (int32_t e = gc_lvl(t, l, iv, corners != 0)) return e;
   return AFH_OK;

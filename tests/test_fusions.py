@@ -42,7 +42,8 @@ Round 4:
 * AFH2_FLUX_SHFL: the 2-D flux's high faces from the next lane vs per cell
   (off by default);
 * AFH2_PAIR_PACK: two 8^2 / four 4^2 boxes per 2-D pair wave vs one;
-* AFH2_CORNER_FOLD: the 2-D up leg's corners folded into the next correction.
+* AFH2_CORNER_FOLD: the 2-D up leg's corners folded into the next correction;
+* AFH2_GC_TREE_ONE: a 2-D tree fill without refinement boundaries in one launch.
 
 The fused forms are also what every other GPU test runs (they are the
 defaults); these tests pin them to the unfused forms on full workloads.
@@ -243,6 +244,17 @@ def test_2d_corner_fold_bitwise(config, monkeypatch):
     monkeypatch.setitem(bench.CONFIGS, "c2d16", (16, (16, 16), 4, (16e-3, 16e-3)))
     _same(_case2d(monkeypatch, {"AFH2_CORNER_FOLD": "1"}, config),
           _case2d(monkeypatch, {"AFH2_CORNER_FOLD": "0"}, config))
+
+
+@pytest.mark.parametrize("config", ["2d", "c2d16"])
+def test_2d_gc_tree_one_launch_bitwise(config, monkeypatch):
+    """afh_gc_tree of a tree without refinement boundaries as one launch over
+    every level (AFH2_GC_TREE_ONE, the default) against level by level: field
+    solves and four unit steps, every variable bitwise."""
+    import bench
+    monkeypatch.setitem(bench.CONFIGS, "c2d16", (16, (16, 16), 4, (16e-3, 16e-3)))
+    _same(_case2d(monkeypatch, {"AFH2_GC_TREE_ONE": "1"}, config),
+          _case2d(monkeypatch, {"AFH2_GC_TREE_ONE": "0"}, config))
 
 
 @pytest.mark.parametrize("config", ["2d", "c2d4"])
