@@ -1168,7 +1168,7 @@ struct afh_mg {
   };
   std::map<int, Graph> graphs;
   bool use_graphs = true;
-  bool pair_pack = true;
+  int pair_pack = 1;  // 2: four 8^2 boxes of 16 lanes per wave
   // the up leg's corner pass folded into the next level's correction
   // (k2_block_corners; AFH2_CORNER_FOLD=0 for k2_corners)
   bool corner_fold = true;  // 2 (8^2) / 4 (4^2) boxes per k2_pair_box wave (AFH2_PAIR_PACK=0: one)
@@ -1601,7 +1601,7 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
   H2(hipMemcpy(mg->d_lvl_c, mg->lvl_c.data(), sizeof(Coef2) * t->nlvl, hipMemcpyHostToDevice));
   if (const char *env = getenv("AFH2_ALL_LVL")) mg->all_lvl = atoi(env) != 0;
   if (const char *env = getenv("AFH2_GRAPHS")) mg->use_graphs = atoi(env) != 0;
-  if (const char *env = getenv("AFH2_PAIR_PACK")) mg->pair_pack = atoi(env) != 0;
+  if (const char *env = getenv("AFH2_PAIR_PACK")) mg->pair_pack = atoi(env);
   if (const char *env = getenv("AFH2_CORNER_FOLD")) mg->corner_fold = atoi(env) != 0;
   H2(hipMalloc(&mg->d_q[0], sizeof(double) * nx * nx));
   H2(hipMalloc(&mg->d_q[1], sizeof(double) * ny * ny));
@@ -1711,6 +1711,9 @@ static int32_t gsrb_boxes(afh_mg *mg, int lvl, bool up, bool skip_corners = fals
       else if (t->nc == 4)
         hipLaunchKernelGGL(k2_pair_box<4>, dim3(n), dim3(64), 0, t->stream, src, dst, rh, phi,
                            t->d_boxes, ids, n, t->bsz, cf, g);
+      else if (t->nc == 8 && mg->pair_pack == 2)
+        hipLaunchKernelGGL((k2_pair_box<8, 16>), dim3((n + 3) / 4), dim3(64), 0, t->stream, src,
+                           dst, rh, phi, t->d_boxes, ids, n, t->bsz, cf, g);
       else if (t->nc == 8 && mg->pair_pack)
         hipLaunchKernelGGL((k2_pair_box<8, 32>), dim3((n + 1) / 2), dim3(64), 0, t->stream, src,
                            dst, rh, phi, t->d_boxes, ids, n, t->bsz, cf, g);
