@@ -1168,10 +1168,12 @@ struct afh_mg {
   };
   std::map<int, Graph> graphs;
   bool use_graphs = true;
-  int pair_pack = 1;  // 2: four 8^2 boxes of 16 lanes per wave
+  // boxes per k2_pair_box wave (AFH2_PAIR_PACK): 1 = two 8^2 / four 4^2,
+  // 0 = one, 2 = four 8^2 boxes of 16 lanes
+  int pair_pack = 1;
   // the up leg's corner pass folded into the next level's correction
   // (k2_block_corners; AFH2_CORNER_FOLD=0 for k2_corners)
-  bool corner_fold = true;  // 2 (8^2) / 4 (4^2) boxes per k2_pair_box wave (AFH2_PAIR_PACK=0: one)
+  bool corner_fold = true;
   int nx = 0, ny = 0;
   double *d_q[2] = {nullptr, nullptr}, *d_e[2] = {nullptr, nullptr};
   int q_bc[4] = {0, 0, 0, 0};
