@@ -28,7 +28,7 @@ RATE_TABULATED_FIELD, RATE_CONSTANT, RATE_LINEAR, RATE_EXP_V1, RATE_EXP_V2 = ran
 RATE_K1, RATE_K3 = 6, 8
 (RATE_K4, RATE_K5, RATE_K6, RATE_K7, RATE_K8, RATE_K9, RATE_K10, RATE_K11,
  RATE_K12, RATE_K13, RATE_K14, RATE_K15) = range(9, 21)
-COARSE_CYCLES, COARSE_DIRECT = 1, 2
+COARSE_CYCLES, COARSE_DIRECT, COARSE_PFMG = 1, 2, 3
 MAX_SPECIES = 32
 MAX_IONS = 8
 MAX_REACTIONS = 128

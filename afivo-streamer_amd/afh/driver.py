@@ -122,17 +122,21 @@ class Simulation:
     """One streamer simulation (src/streamer.f90) over a C-ABI library."""
 
     def __init__(self, lib, case, device=-1, coarse_cycles=0, capacity_factor=2.0,
-                 fuse_rhs=True, user=None, coarse_tol=0.0):
+                 fuse_rhs=True, user=None, coarse_tol=0.0, coarse_mode=None):
         """user: the program's m_user hooks (afh.users), e.g. the gas density
         function and initial conditions of programs/3d_sprite.
         coarse_cycles / coarse_tol: the level-1 solve (0: exact; else at most
         coarse_cycles MG cycles, stopped at |r| < coarse_tol |b| when
-        coarse_tol > 0 -- HYPRE PFMG's rule, the reference's solver)."""
+        coarse_tol > 0 -- HYPRE PFMG's rule). coarse_mode=capi.COARSE_PFMG:
+        the reference's solver itself, HYPRE StructPFMG restated
+        (csrc/afh_pfmg.h), at most coarse_cycles iterations to coarse_tol
+        (the reference: 50, 1e-6)."""
         c = case if isinstance(case, Case) else Case(case)
         self.c, self.lib, self.device = c, lib, device
         self.user = user
         self.coarse_cycles = coarse_cycles
         self.coarse_tol = coarse_tol
+        self.coarse_mode = coarse_mode
         self.capacity_factor = capacity_factor
         # NDIM: the exported coarse grid has one entry per dimension (2: the
         # reference's 2-D build, programs/standard_2d, on libafivo_hip_2d.so)
@@ -312,14 +316,16 @@ class Simulation:
             self.fluid.close()
         self.tree = tree
         self.mg = Multigrid(tree, self.i_phi, self.i_rhs, self.i_tmp,
-                            coarse_cycles=self.coarse_cycles, coarse_tol=self.coarse_tol)
+                            coarse_cycles=self.coarse_cycles, coarse_tol=self.coarse_tol,
+                            coarse_mode=self.coarse_mode)
         self.helm = []
         if self.photoi:
             for iv, lam in zip(self.helm_iv, self.helm_lambdas):
                 self.helm.append(Multigrid(tree, iv, self.i_rhs, self.i_tmp,
                                            helmholtz_lambda=lam * lam,
                                            coarse_cycles=self.coarse_cycles,
-                                           coarse_tol=self.coarse_tol))
+                                           coarse_tol=self.coarse_tol,
+                                           coarse_mode=self.coarse_mode))
         c = self.c
         td_cols = c.ia("td_cols")
         self.fluid = Fluid(
@@ -993,7 +999,7 @@ class Simulation:
         for a CPU baseline): topology, every cell and face variable, time."""
         import copy
         other = Simulation(lib, self.c, device=device, coarse_cycles=self.coarse_cycles,
-                           coarse_tol=self.coarse_tol,
+                           coarse_tol=self.coarse_tol, coarse_mode=self.coarse_mode,
                            capacity_factor=self.capacity_factor, fuse_rhs=self.fused_rhs,
                            user=self.user)
         other.af = copy.deepcopy(self.af)

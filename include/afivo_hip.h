@@ -86,6 +86,10 @@ extern "C" {
 #define AFH_COARSE_CYCLES 1 /* fixed number of device MG cycles */
 #define AFH_COARSE_DIRECT 2 /* exact solve: the folded operator is separable;
                                cosine / sine eigenbases per dimension */
+#define AFH_COARSE_PFMG 3   /* the reference's solver, HYPRE StructPFMG, restated
+                               (csrc/afh_pfmg.h): at most coarse_cycles
+                               iterations, tolerance coarse_tol (50, 1e-6 in
+                               the reference, m_af_types.f90:560-565) */
 
 #define AFH_MAX_SPECIES 32
 #define AFH_MAX_GAS_SPECIES 8
@@ -215,7 +219,7 @@ typedef struct afh_mg_desc {
   int32_t i_phi, i_rhs, i_tmp;
   int32_t n_cycle_down, n_cycle_up; /* 2, 2 */
   double helmholtz_lambda;
-  int32_t coarse_mode;   /* AFH_COARSE_CYCLES or AFH_COARSE_DIRECT */
+  int32_t coarse_mode;   /* AFH_COARSE_CYCLES, _DIRECT or _PFMG */
   int32_t coarse_cycles; /* AFH_COARSE_CYCLES: MG V(2,2) cycles on the
                             level-1 grid (at most, with coarse_tol) */
   /* AFH_COARSE_CYCLES: stop once the level-1 residual's 2-norm is below
