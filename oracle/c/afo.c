@@ -1610,6 +1610,22 @@ static int32_t solve_coarse_pfmg(afh_mg *mg) {
   return gc_lvl(t, 1, mg->d.i_phi, 1) ? AFH_ERR_STATE : AFH_OK;
 }
 
+int32_t afo_pfmg_probe(int32_t nx, int32_t ny, int32_t nz, const double *a7, int32_t maxl,
+                       int32_t *nl, int32_t *cdir, int32_t *active, double *w) {
+  afh_pfmg h;
+  if (!a7 || !nl || !cdir || !active || !w || nx < 1 || ny < 1 || nz < 1)
+    return fail(AFH_ERR_ARG, "afo_pfmg_probe: bad argument");
+  if (afh_pfmg_setup(&h, nx, ny, nz, nz > 1 ? 3 : 2, a7)) return fail(AFH_ERR_STATE, "setup");
+  *nl = h.nl;
+  for (int l = 0; l < h.nl && l < maxl; l++) {
+    cdir[l] = l + 1 < h.nl ? h.cdir[l] : -1;
+    active[l] = h.active[l];
+    w[l] = h.w[l];
+  }
+  afh_pfmg_free(&h);
+  return AFH_OK;
+}
+
 /* solve_coarse_grid, m_af_multigrid.f90:266-291 */
 int32_t afo_mg_solve_coarse(afh_mg *mg) {
   afh_tree *t = mg->t;

@@ -9,9 +9,12 @@
  * in tests/golden/ (generated from the reference's own afivo numerics, see
  * oracle/Makefile and oracle/make_golden.py).
  *
- * The level-1 solve restates OUR device coarse solver (the reference calls
- * HYPRE, absent here): a V(2,2) geometric multigrid on the coarse grid with
- * boundary conditions folded into the operator (m_coarse_solver.f90:442-491).
+ * The level-1 solve: AFH_COARSE_PFMG restates the reference's own solver,
+ * HYPRE 2.31.0 StructPFMG (absent here; afivo-streamer_amd/csrc/afh_pfmg.h
+ * has the algorithm), pinned by the reference's regression logs (rows within
+ * 5e-8, tests/test_rtest.py); AFH_COARSE_DIRECT / _CYCLES are our exact
+ * solve and V(2,2) cycles. The boundary conditions are folded into the
+ * operator as stencil_handle_boundaries does (m_coarse_solver.f90:442-491).
  */
 #ifndef AFO_H
 #define AFO_H
@@ -22,6 +25,11 @@ extern "C" {
 #endif
 
 const char *afo_last_error(void);
+/* Test probe of the PFMG setup (afh_pfmg.h) on a folded 7-point operator a7
+ * (7 per point): level count, coarsening direction, relaxed flag and Jacobi
+ * weight per level (at most maxl). */
+int32_t afo_pfmg_probe(int32_t nx, int32_t ny, int32_t nz, const double *a7, int32_t maxl,
+                       int32_t *nl, int32_t *cdir, int32_t *active, double *w);
 int32_t afo_tree_create(const afh_tree_desc *desc, int32_t device,
                         afh_tree **out);
 int32_t afo_tree_destroy(afh_tree *t);

@@ -11,18 +11,17 @@ own initializers (tests/golden/rtest_*.npz, oracle/make_cases.py), AMR set-up,
 photoionization every 5 steps -- over the C oracle (CPU) and the HIP library
 (GPU), and compares against those committed rows.
 
-What is expected, and why (profiles/r03_rtest_coarse_sensitivity.json,
-scripts/rtest_coarse_sensitivity.py):
-* the reference's level-1 solve is HYPRE PFMG stopped at a relative residual
-  of 1e-6 (afivo/src/m_coarse_solver.f90:393-439; HYPRE is absent from the
-  snapshot) and field_compute stops at a residual of 1e-4 max|rhs|, so the
-  rows depend on the coarse solver at the 1e-5 level: the same runs with the
-  level-1 solve exact or stopped at 1e-8 ... 1e-4 differ by up to 1.2e-5;
-* with PFMG's stopping rule (coarse_tol 1e-6, at most 50 cycles) test_3d
-  matches every row within compare_logs' own tolerance (max 8.9e-6); the
-  chemistry cases every row within 3e-5;
-* with the exact level-1 solve (the driver's default) every row of every
-  case is within 4e-5.
+What is expected, and why:
+* the reference's level-1 solve is HYPRE StructPFMG stopped at a relative
+  residual of 1e-6 (afivo/src/m_coarse_solver.f90:393-439), and
+  field_compute stops at a residual of 1e-4 max|rhs|, so the rows depend on
+  the level-1 solver at the 1e-5 level (profiles/r03_rtest_coarse_sensitivity.json:
+  other level-1 solves move them by up to 3e-5);
+* with HYPRE's PFMG restated (round 5, AFH_COARSE_PFMG,
+  afivo-streamer_amd/csrc/afh_pfmg.h) every row of all three logs matches
+  within 5e-8 -- the logs' print precision (E20.8, src/m_output.f90:829) --
+  so the bound is 1e-7, a hundred times tighter than compare_logs' 1e-5;
+* with our exact level-1 solve (the bench's) the rows are within 4e-5.
 Until round 3 the rows diverged by 1e-3 .. 2e-2 after 1.4 ns: the field
 solve after the first regrid (level 6 created at step 46) started from
 phi = 0 in the new boxes, because the driver did not make phi an auto
@@ -38,15 +37,16 @@ from afh import capi
 from afh.driver import Simulation
 
 CASES = ["test_3d", "test_3d_chem", "test_3d_photoi_chem"]
-# level-1 solves: (max cycles, tolerance) -- exact (AFH_COARSE_DIRECT), and
-# HYPRE PFMG's stopping rule with our V(2,2) cycles
-EXACT, PFMG = (0, 0.0), (50, 1e-6)
+# level-1 solves: (max cycles, tolerance, mode) -- our exact solve
+# (AFH_COARSE_DIRECT), and the reference's HYPRE PFMG restated (50, 1e-6:
+# the reference's settings, m_af_types.f90:560-565)
+EXACT, PFMG = (0, 0.0, None), (50, 1e-6, capi.COARSE_PFMG)
 # bound on every row's relative deviation from the reference, per level-1
-# solve: compare_logs' 1e-5 where the table shows it met, else the bound the
-# table justifies (measured max + the 1.2e-5 coarse-solve spread, rounded up)
-BOUND = {("test_3d", PFMG): 1e-5, ("test_3d", EXACT): 2.5e-5,
-         ("test_3d_chem", PFMG): 5e-5, ("test_3d_chem", EXACT): 5e-5,
-         ("test_3d_photoi_chem", PFMG): 5e-5, ("test_3d_photoi_chem", EXACT): 5e-5}
+# solve: PFMG 1e-7 (measured 4.8e-8, the print precision); exact: measured
+# max + the coarse-solve spread, rounded up
+BOUND = {("test_3d", PFMG): 1e-7, ("test_3d", EXACT): 2.5e-5,
+         ("test_3d_chem", PFMG): 1e-7, ("test_3d_chem", EXACT): 5e-5,
+         ("test_3d_photoi_chem", PFMG): 1e-7, ("test_3d_photoi_chem", EXACT): 5e-5}
 
 
 def load(name):
@@ -55,7 +55,8 @@ def load(name):
 
 def run(lib, name, device=-1, solve=EXACT):
     d = load(name)
-    sim = Simulation(lib, d, device=device, coarse_cycles=solve[0], coarse_tol=solve[1])
+    sim = Simulation(lib, d, device=device, coarse_cycles=solve[0], coarse_tol=solve[1],
+                     coarse_mode=solve[2])
     return sim, sim.run(), d["rtest_log"]
 
 
