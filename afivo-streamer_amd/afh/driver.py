@@ -343,6 +343,10 @@ class Simulation:
         # secondary emission from ions at the walls (input_data%ion_se_yield,
         # handle_ion_se_flux in forward_euler, m_fluid.f90:63-67)
         if self.ions and "ion_se_yield" in c.d and c.r("ion_se_yield") > 0:
+            if not self.lib.has("fluid_set_ion_se_yield"):
+                raise NotImplementedError(
+                    "ion secondary emission (ion_se_yield > 0) is not built in this "
+                    "library (the 2-D build: include/afivo_hip_2d.h)")
             self.fluid.set_ion_se_yield(c.r("ion_se_yield"))
         if self.fused_rhs:
             self.fluid.set_rhs_output(self.i_rhs, True)

@@ -57,7 +57,7 @@ class StreamerCase:
 
     def __init__(self, lib, topo, td, chem, voltage, n_gas=None,
                  coarse_cycles=20, device=-1, shard=None, n_var_cell=N_VAR_CELL,
-                 box_capacity=0):
+                 box_capacity=0, coarse_mode=None, coarse_tol=0.0):
         """shard: an afh.dist.Shard or NativeShard -- this rank's part of a sharded tree
         (the tree is created from the rank's level lists and the exchange
         hooks are attached); None for a single-rank tree."""
@@ -83,6 +83,9 @@ class StreamerCase:
         for s in (0, 1):
             t.set_cc_methods(IV["phi"] + s, self.phi_bc(voltage, self.ndim), capi.RB_MG_SIDES)
         self.coarse_cycles = coarse_cycles
+        # coarse_mode=capi.COARSE_PFMG: the reference's HYPRE PFMG restated
+        # (coarse_cycles iterations at most, to coarse_tol)
+        self.coarse_mode, self.coarse_tol = coarse_mode, coarse_tol
         self.i_lsf = 0  # level-set variable of an electrode (set_electrode)
         # keep the face fluxes of the species step in FV["flux"] (the fused
         # device step otherwise leaves them on chip)
@@ -96,7 +99,8 @@ class StreamerCase:
         self._defer_ok = (os.environ.get("AFH_DEFER", "1") != "0" and
                           (self.ndim == 3 or lib.has("fluid_fetch_step")))
         self.mg = Multigrid(t, IV["phi"], IV["rhs"], IV["tmp"],
-                            coarse_cycles=coarse_cycles)
+                            coarse_cycles=coarse_cycles, coarse_mode=coarse_mode,
+                            coarse_tol=coarse_tol)
         self._mg_helm = {}
         self.n_gas = gas_number_density() if n_gas is None else n_gas
         self.fluid = Fluid(t, [IV["e"], IV["pos"], IV["neg"]], [-1, 1, -1],
@@ -120,7 +124,8 @@ class StreamerCase:
         if lambda2 not in self._mg_helm:
             self._mg_helm[lambda2] = Multigrid(
                 self.tree, IV["phi"], IV["rhs"], IV["tmp"],
-                helmholtz_lambda=lambda2, coarse_cycles=self.coarse_cycles)
+                helmholtz_lambda=lambda2, coarse_cycles=self.coarse_cycles,
+                coarse_mode=self.coarse_mode, coarse_tol=self.coarse_tol)
         return self._mg_helm[lambda2]
 
     def set_electrode(self, i_lsf, stencils, lsf_faces):

@@ -52,6 +52,7 @@
 #include <vector>
 
 #include "../../include/afivo_hip_2d.h"
+#include "afh_pfmg_dev.h"
 
 namespace afh2 {
 
@@ -693,6 +694,55 @@ __global__ void __launch_bounds__(1024)
   }
 }
 
+// AFH_COARSE_PFMG: the reference's HYPRE StructPFMG restated
+// (afh_pfmg_dev.h), the NDIM = 2 grid: gather rhs + boundary terms (the
+// folded operator's coefficients, b2r per face) and phi, solve, scatter;
+// the vectors and the wave levels' operators in LDS
+__global__ void __launch_bounds__(1024)
+    k2_cs_pfmg(const afh_pf::PfLvl *__restrict__ Lg, int nl, int wave_from,
+               const double *__restrict__ A, const double *__restrict__ Pw,
+               const double *__restrict__ b2r, const uint8_t *__restrict__ fmask,
+               double *__restrict__ phi, const double *__restrict__ rhs,
+               const afh_box_meta *__restrict__ meta, const int32_t *__restrict__ ids, int nid,
+               int nc, int bsz, Bc4 g, double tol, int max_iter, int *__restrict__ iters_out) {
+  extern __shared__ double pf_sm[];
+  __shared__ double slot;
+  const afh_pf::PfLvl L0 = Lg[0];
+  const int np = Lg[nl - 1].off + Lg[nl - 1].np;
+  const int soff = wave_from < nl ? Lg[wave_from].off : np;
+  double *X0 = pf_sm, *X1 = X0 + np, *b = X0 + 2 * np, *r = X0 + 3 * np;
+  double *As = pf_sm + 4 * np;
+  for (int u = threadIdx.x; u < 27 * (np - soff); u += blockDim.x)
+    As[u] = A[(size_t)27 * soff + u];
+  const int n2 = nc * nc, ng = nc + 2, nx = L0.n[0];
+  for (int u = threadIdx.x; u < nid * n2; u += blockDim.x) {
+    const int id = ids[u / n2], t = u % n2;
+    const afh_box_meta &m = meta[id - 1];
+    const int i = t % nc + 1, j = t / nc + 1;
+    const int p = ((m.ix[1] - 1) * nc + j - 1) * nx + (m.ix[0] - 1) * nc + i - 1;
+    const size_t c = (size_t)(id - 1) * bsz + ix2(ng, i, j);
+    double rv = rhs[c];
+    const int fm = fmask[p];
+    for (int nb = 0; nb < 4; nb++)
+      if ((fm >> nb) & 1) rv = rv + b2r[(size_t)nb * L0.np + p] * g.bc[nb].value;
+    b[p] = rv;
+    X0[p] = phi[c];
+  }
+  __syncthreads();
+  int cur = 0;
+  const int iters = afh_pf::pf_solve_block(Lg, nl, wave_from, A, As, soff, Pw, X0, X1, b, r,
+                                           &slot, tol, max_iter, &cur);
+  const double *x = cur ? X1 : X0;
+  for (int u = threadIdx.x; u < nid * n2; u += blockDim.x) {
+    const int id = ids[u / n2], t = u % n2;
+    const afh_box_meta &m = meta[id - 1];
+    const int i = t % nc + 1, j = t / nc + 1;
+    phi[(size_t)(id - 1) * bsz + ix2(ng, i, j)] =
+        x[((m.ix[1] - 1) * nc + j - 1) * nx + (m.ix[0] - 1) * nc + i - 1];
+  }
+  if (threadIdx.x == 0 && iters_out) *iters_out = iters;
+}
+
 // mg_box_lpl_gradient (fc = fac / dr * (phi_i - phi_{i-1})) + mg_box_field_norm
 __global__ void __launch_bounds__(NT)
     k2_gradient(const double *__restrict__ phi, double *__restrict__ fc,
@@ -1182,6 +1232,14 @@ struct afh_mg {
   // profiles/r04_push_ab.txt)
   bool pair = true;
   double *alt = nullptr;
+  // AFH_COARSE_PFMG (afh_pfmg_dev.h, k2_cs_pfmg): the hierarchy's device
+  // tables, built for the boundary types pf_bc (b2r: the boundary values'
+  // factors per face, fmask: the faces a point touches); iterations
+  int pf_nl = 0, pf_lds = 0, pf_wave = 0, pf_bc[4] = {-1, -1, -1, -1};
+  afh_pf::PfLvl *d_pf_lvl = nullptr;
+  double *d_pf_A = nullptr, *d_pf_P = nullptr, *d_pf_b2r = nullptr;
+  uint8_t *d_pf_fmask = nullptr;
+  int *d_pf_iters = nullptr;
 };
 
 struct afh_fluid {
@@ -1573,8 +1631,9 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
       d->i_tmp < 1 || d->i_tmp > t->nvc)
     return set_error(AFH_ERR_ARG, "afh_mg_create: bad variable index");
   if (!t->meth[d->i_phi].set) return set_error(AFH_ERR_STATE, "set cc methods for phi first");
-  if (d->coarse_mode != AFH_COARSE_DIRECT)
-    return set_error(AFH_ERR_UNSUPPORTED, "2-D: only AFH_COARSE_DIRECT is built");
+  if (d->coarse_mode != AFH_COARSE_DIRECT &&
+      !(d->coarse_mode == AFH_COARSE_PFMG && d->coarse_cycles >= 1 && d->coarse_tol >= 0))
+    return set_error(AFH_ERR_UNSUPPORTED, "2-D: AFH_COARSE_DIRECT or AFH_COARSE_PFMG");
   if (d->n_cycle_down < 1 || d->n_cycle_up < 1)
     return set_error(AFH_ERR_ARG, "afh_mg_create: cycles");
   const int nx = t->cgs[0], ny = t->cgs[1];
@@ -1623,6 +1682,8 @@ int32_t afh_mg_destroy(afh_mg *mg) {
   for (int q = 0; q < 2; q++) hipFree(mg->d_q[q]), hipFree(mg->d_e[q]);
   hipFree(mg->alt);
   hipFree(mg->d_lvl_c);
+  hipFree(mg->d_pf_lvl), hipFree(mg->d_pf_A), hipFree(mg->d_pf_P), hipFree(mg->d_pf_b2r);
+  hipFree(mg->d_pf_fmask), hipFree(mg->d_pf_iters);
   for (auto &g : mg->graphs)
     if (g.second.exec) hipGraphExecDestroy(g.second.exec);
   delete mg;
@@ -1655,6 +1716,97 @@ static void cs_tables(int n, int bc_lo, int bc_hi, double h, double *q, double *
   }
 }
 
+// AFH_COARSE_PFMG: the folded level-1 operator (stencil_handle_boundaries,
+// the 3-D library's pf_prepare with NDIM = 2), the hierarchy when the
+// boundary types change, then k2_cs_pfmg
+static int32_t solve_coarse_pfmg(afh_mg *mg) {
+  afh_tree *t = mg->t;
+  const Meth &M = t->meth[mg->d.i_phi];
+  const int nc = t->nc, nid = t->ids.n(1), nx = mg->nx, ny = mg->ny;
+  const size_t n0 = (size_t)nx * ny;
+  bool fresh = !mg->d_pf_lvl;
+  for (int q = 0; q < 4; q++) fresh = fresh || mg->pf_bc[q] != M.bc[q].type;
+  if (fresh) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    H2(hipStreamIsCapturing(t->stream, &cs));
+    if (cs != hipStreamCaptureStatusNone)
+      return set_error(AFH_ERR_STATE, "pfmg: setup changed during a graph capture");
+    std::vector<double> a7(7 * n0, 0.0), b2r(4 * n0, 0.0);
+    std::vector<uint8_t> fm(n0, 0);
+    const int dims[2] = {nx, ny};
+    for (int q = 0; q < nid; q++) {
+      const int id = t->h_ids[0][q];
+      const afh_box_meta &m = t->boxes[id - 1];
+      for (int j = 1; j <= nc; j++)
+        for (int i = 1; i <= nc; i++) {
+          const int gi[2] = {(m.ix[0] - 1) * nc + i, (m.ix[1] - 1) * nc + j};
+          const size_t g = (size_t)(gi[1] - 1) * nx + (gi[0] - 1);
+          double c[7] = {mg->lvl_c[0].c[0], mg->lvl_c[0].c[1], mg->lvl_c[0].c[2],
+                         mg->lvl_c[0].c[3], mg->lvl_c[0].c[4], 0.0, 0.0};
+          for (int nb = 1; nb <= 4; nb++) {
+            const int dd = (nb - 1) >> 1;
+            const bool low = ((nb - 1) & 1) == 0;
+            if (!(low ? gi[dd] == 1 : gi[dd] == dims[dd])) continue;
+            double k2;
+            if (M.bc[nb - 1].type == AFH_BC_DIRICHLET) {
+              c[0] = c[0] - c[nb];
+              k2 = -2 * c[nb];
+            } else {
+              c[0] = c[0] + c[nb];
+              k2 = -(c[nb] * m.dr[dd]) * (low ? -1 : 1);
+            }
+            b2r[(size_t)(nb - 1) * n0 + g] = k2;
+            fm[g] |= (uint8_t)(1 << (nb - 1));
+            c[nb] = 0.0;
+          }
+          memcpy(&a7[7 * g], c, sizeof c);
+        }
+    }
+    afh_pfmg h;
+    if (afh_pfmg_setup(&h, nx, ny, 1, 2, a7.data()))
+      return set_error(AFH_ERR_DEVICE, "pfmg: host setup allocation");
+    std::vector<afh_pf::PfLvl> lv;
+    std::vector<double> A, P;
+    afh_pf::pf_device_tables(h, lv, A, P);
+    const size_t np = h.off[h.nl];
+    afh_pfmg_free(&h);
+    H2(hipStreamSynchronize(t->stream));
+    hipFree(mg->d_pf_lvl), hipFree(mg->d_pf_A), hipFree(mg->d_pf_P);
+    H2(hipMalloc(&mg->d_pf_lvl, sizeof(afh_pf::PfLvl) * lv.size()));
+    H2(hipMalloc(&mg->d_pf_A, sizeof(double) * A.size()));
+    H2(hipMalloc(&mg->d_pf_P, sizeof(double) * P.size()));
+    if (!mg->d_pf_b2r) {
+      H2(hipMalloc(&mg->d_pf_b2r, sizeof(double) * 4 * n0));
+      H2(hipMalloc(&mg->d_pf_fmask, n0));
+      H2(hipMalloc(&mg->d_pf_iters, sizeof(int)));
+    }
+    H2(hipMemcpy(mg->d_pf_lvl, lv.data(), sizeof(afh_pf::PfLvl) * lv.size(),
+                 hipMemcpyHostToDevice));
+    H2(hipMemcpy(mg->d_pf_A, A.data(), sizeof(double) * A.size(), hipMemcpyHostToDevice));
+    H2(hipMemcpy(mg->d_pf_P, P.data(), sizeof(double) * P.size(), hipMemcpyHostToDevice));
+    H2(hipMemcpy(mg->d_pf_b2r, b2r.data(), sizeof(double) * b2r.size(), hipMemcpyHostToDevice));
+    H2(hipMemcpy(mg->d_pf_fmask, fm.data(), n0, hipMemcpyHostToDevice));
+    (void)np;
+    mg->pf_nl = (int)lv.size();
+    mg->pf_wave = afh_pf::pf_wave_from(lv);
+    const size_t lds = afh_pf::pf_lds_bytes(lv, true);
+    if (lds + 64 > 160 * 1024)
+      return set_error(AFH_ERR_UNSUPPORTED, "2-D pfmg: level-1 grid %d x %d", nx, ny);
+    mg->pf_lds = (int)lds;
+    H2(hipFuncSetAttribute((const void *)k2_cs_pfmg,
+                           hipFuncAttributeMaxDynamicSharedMemorySize, mg->pf_lds));
+    for (int q = 0; q < 4; q++) mg->pf_bc[q] = M.bc[q].type;
+  }
+  const int nt = std::min(1024, std::max(256, (int)((n0 + 63) / 64 * 64)));
+  hipLaunchKernelGGL(k2_cs_pfmg, dim3(1), dim3(nt), mg->pf_lds, t->stream, mg->d_pf_lvl,
+                     mg->pf_nl, mg->pf_wave, mg->d_pf_A, mg->d_pf_P, mg->d_pf_b2r, mg->d_pf_fmask,
+                     t->ccv(mg->d.i_phi), t->ccv(mg->d.i_rhs), t->d_boxes, t->ids.at(1), nid,
+                     t->nc, t->bsz, t->bc4(mg->d.i_phi), mg->d.coarse_tol, mg->d.coarse_cycles,
+                     mg->d_pf_iters);
+  H2_LAUNCH("k2_cs_pfmg");
+  return gc_lvl(t, 1, mg->d.i_phi, true);
+}
+
 static int32_t solve_coarse(afh_mg *mg) {
   afh_tree *t = mg->t;
   const Meth &M = t->meth[mg->d.i_phi];
@@ -1662,6 +1814,7 @@ static int32_t solve_coarse(afh_mg *mg) {
     if (M.bc[q].type != AFH_BC_DIRICHLET && M.bc[q].type != AFH_BC_NEUMANN)
       return set_error(AFH_ERR_UNSUPPORTED, "2-D coarse solve: bc type %d", M.bc[q].type);
   }
+  if (mg->d.coarse_mode == AFH_COARSE_PFMG) return solve_coarse_pfmg(mg);
   bool fresh = false;
   for (int q = 0; q < 4; q++) fresh = fresh || mg->q_bc[q] != M.bc[q].type;
   const double hx = mg->lvl_c[0].c[1], hy = mg->lvl_c[0].c[3];

@@ -21,7 +21,7 @@
 
 #include "afh_internal.h"
 #include "afh_cs_direct.h"
-#include "afh_pfmg.h"
+#include "afh_pfmg_dev.h"
 
 #include <mutex>
 
@@ -2607,179 +2607,39 @@ __global__ void __launch_bounds__(1024)
   }
 }
 
-// ---- AFH_COARSE_PFMG: the reference's level-1 solver, HYPRE StructPFMG,
-// restated (afh_pfmg.h: the algorithm, its sources, the host setup). The
-// whole solve -- gather with the boundary fold, the V-cycles with the
-// stopping test, scatter -- is one workgroup: the level vectors x, b, r in
-// LDS when they fit (else in the global scratch gx), the operators (SoA per
-// level) and interpolation weights in global memory. Each operation is
-// oracle/c/afo.c's pf_* in the same order of arithmetic, so the two agree
-// bitwise (the only liberty: stencil entries zero on a whole level are
-// skipped, which changes at most the sign of a zero).
-struct PfLvl {
-  int n[3];
-  int cdir;
-  int active;
-  int off;        // first point of the level
-  int np;         // points
-  uint32_t mask;  // stencil entries nonzero somewhere on the level
-  double w;       // Jacobi weight
-};
-
-constexpr int PF_NPART = 256;  // = AFH_PFMG_NPART of the oracle's dot product
-
-__device__ __forceinline__ void pf_decode(const PfLvl &L, int p, int &i, int &j, int &k) {
-  i = p % L.n[0] + 1;
-  j = (p / L.n[0]) % L.n[1] + 1;
-  k = p / (L.n[0] * L.n[1]) + 1;
-}
-
-__device__ __forceinline__ int pf_pt(const PfLvl &L, int i, int j, int k) {
-  return ((k - 1) * L.n[1] + (j - 1)) * L.n[0] + (i - 1);
-}
-
-// weighted Jacobi (pf_relax)
-__device__ void pf_relax_d(const PfLvl &L, const double *__restrict__ A, double *x,
-                           const double *b, double *t, bool zero) {
-  const double *Al = A + (size_t)27 * L.off;
-  for (int p = threadIdx.x; p < L.np; p += blockDim.x) {
-    const double ac = Al[(size_t)13 * L.np + p];
-    if (zero) {
-      double v = b[L.off + p] / ac;
-      if (L.w != 1.0) v = L.w * v;
-      x[L.off + p] = v;
-      continue;
-    }
-    int i, j, k;
-    pf_decode(L, p, i, j, k);
-    double v = b[L.off + p];
-    for (int s = 0; s < 27; s++) {
-      if (s == 13 || !((L.mask >> s) & 1)) continue;
-      const int ii = i + s % 3 - 1, jj = j + (s / 3) % 3 - 1, kk = k + s / 9 - 1;
-      if (ii < 1 || ii > L.n[0] || jj < 1 || jj > L.n[1] || kk < 1 || kk > L.n[2]) continue;
-      v = v - Al[(size_t)s * L.np + p] * x[L.off + pf_pt(L, ii, jj, kk)];
-    }
-    t[L.off + p] = v / ac;
-  }
-  __syncthreads();
-  if (zero) return;
-  for (int p = threadIdx.x; p < L.np; p += blockDim.x) {
-    const int q = L.off + p;
-    if (L.w == 1.0) x[q] = t[q];
-    else x[q] = (1.0 - L.w) * x[q] + L.w * t[q];
-  }
-  __syncthreads();
-}
-
-// r = b - A x (pf_residual)
-__device__ void pf_residual_d(const PfLvl &L, const double *__restrict__ A, const double *x,
-                              const double *b, double *r) {
-  const double *Al = A + (size_t)27 * L.off;
-  for (int p = threadIdx.x; p < L.np; p += blockDim.x) {
-    int i, j, k;
-    pf_decode(L, p, i, j, k);
-    double a = 0.0;
-    for (int s = 0; s < 27; s++) {
-      if (!((L.mask >> s) & 1)) continue;
-      const int ii = i + s % 3 - 1, jj = j + (s / 3) % 3 - 1, kk = k + s / 9 - 1;
-      if (ii < 1 || ii > L.n[0] || jj < 1 || jj > L.n[1] || kk < 1 || kk > L.n[2]) continue;
-      a = a + Al[(size_t)s * L.np + p] * x[L.off + pf_pt(L, ii, jj, kk)];
-    }
-    r[L.off + p] = b[L.off + p] - a;
-  }
-  __syncthreads();
-}
-
-// v.v on level 0 (pf_dot: 256 strided partials, pairwise tree)
-__device__ double pf_dot_d(const PfLvl &L, const double *v, double *part) {
-  if (threadIdx.x < PF_NPART) {
-    double s = 0.0;
-    for (int p = threadIdx.x; p < L.np; p += PF_NPART) s = s + v[p] * v[p];
-    part[threadIdx.x] = s;
-  }
-  __syncthreads();
-  for (int st = PF_NPART / 2; st > 0; st >>= 1) {
-    if ((int)threadIdx.x < st) part[threadIdx.x] = part[threadIdx.x] + part[threadIdx.x + st];
-    __syncthreads();
-  }
-  const double out = part[0];
-  __syncthreads();
-  return out;
-}
-
-// b_{l+1} = R r_l (pf_restrict)
-__device__ void pf_restrict_d(const PfLvl &F, const PfLvl &C, const double *__restrict__ Pw,
-                              const double *r, double *b) {
-  const int cd = F.cdir;
-  const double *Pl = Pw + (size_t)2 * F.off;
-  for (int p = threadIdx.x; p < C.np; p += blockDim.x) {
-    int c[3];
-    pf_decode(C, p, c[0], c[1], c[2]);
-    int f[3] = {c[0], c[1], c[2]};
-    f[cd] = 2 * f[cd];
-    double v = r[F.off + pf_pt(F, f[0], f[1], f[2])];
-    f[cd] -= 1;
-    {
-      const int q = pf_pt(F, f[0], f[1], f[2]);
-      v = v + Pl[(size_t)F.np + q] * r[F.off + q];
-    }
-    f[cd] += 2;
-    if (f[cd] <= F.n[cd]) {
-      const int q = pf_pt(F, f[0], f[1], f[2]);
-      v = v + Pl[q] * r[F.off + q];
-    }
-    b[C.off + p] = v;
-  }
-  __syncthreads();
-}
-
-// x_l += P x_{l+1} (pf_interp_add)
-__device__ void pf_interp_d(const PfLvl &F, const PfLvl &C, const double *__restrict__ Pw,
-                            double *x) {
-  const int cd = F.cdir;
-  const double *Pl = Pw + (size_t)2 * F.off;
-  for (int p = threadIdx.x; p < F.np; p += blockDim.x) {
-    int f[3];
-    pf_decode(F, p, f[0], f[1], f[2]);
-    int c[3] = {f[0], f[1], f[2]};
-    double e;
-    if (!(f[cd] & 1)) {
-      c[cd] = f[cd] / 2;
-      e = x[C.off + pf_pt(C, c[0], c[1], c[2])];
-    } else {
-      e = 0.0;
-      if (f[cd] >= 3) {
-        c[cd] = (f[cd] - 1) / 2;
-        e = Pl[p] * x[C.off + pf_pt(C, c[0], c[1], c[2])];
-      }
-      if (f[cd] + 1 <= F.n[cd]) {
-        c[cd] = (f[cd] + 1) / 2;
-        e = e + Pl[(size_t)F.np + p] * x[C.off + pf_pt(C, c[0], c[1], c[2])];
-      }
-    }
-    x[F.off + p] = x[F.off + p] + e;
-  }
-  __syncthreads();
-}
+// ---- AFH_COARSE_PFMG (afh_pfmg_dev.h): the level-1 boxes gathered with
+// the boundary fold and the level-set term, the solve, the scatter
+using afh_pf::PfLvl;
+using afh_pf::PF_NPART;
 
 struct PfBc {
   afh_bc bc[6];
 };
 
+// LDS: x images, b, r and the wave levels' operators in LDS (else the
+// global scratch gx, 4 np doubles, and the operators from A)
+template <bool LDS>
 __global__ void __launch_bounds__(1024)
-    k_cs_pfmg(const PfLvl *__restrict__ Lg, int nl, const double *__restrict__ A,
+    k_cs_pfmg(const PfLvl *__restrict__ Lg, int nl, int wave_from, const double *__restrict__ A,
               const double *__restrict__ Pw, const double *__restrict__ b2r,
               const uint8_t *__restrict__ fmask, const double *const *__restrict__ vbc,
-              double *__restrict__ gx, int use_lds, double *__restrict__ phi,
+              double *__restrict__ gx, double *__restrict__ phi,
               const double *__restrict__ rhs, const afh_box_meta *__restrict__ meta,
               const int32_t *__restrict__ ids, int nid, int nc, size_t bsz, PfBc B,
               double tol, int max_iter, int *__restrict__ iters_out) {
   extern __shared__ double pf_sm[];
-  __shared__ double part[PF_NPART];
+  __shared__ double slot;
   const PfLvl L0 = Lg[0];
   const int np = Lg[nl - 1].off + Lg[nl - 1].np;
-  double *x = use_lds ? pf_sm : gx;
-  double *b = x + np, *r = x + 2 * np;
+  const int soff = wave_from < nl ? Lg[wave_from].off : np;
+  double *X0 = LDS ? pf_sm : gx;
+  double *X1 = X0 + np, *b = X0 + 2 * np, *r = X0 + 3 * np;
+  const double *Aw = A + (size_t)27 * soff;
+  if (LDS) {
+    double *As = pf_sm + 4 * np;
+    for (int u = threadIdx.x; u < 27 * (np - soff); u += blockDim.x) As[u] = Aw[u];
+    Aw = As;
+  }
   const int n3 = nc * nc * nc, nx = L0.n[0], ny = L0.n[1];
   // coarse_solver_set_rhs_phi: rhs + boundary values (+ level-set term), phi
   for (int u = threadIdx.x; u < nid * n3; u += blockDim.x) {
@@ -2796,63 +2656,19 @@ __global__ void __launch_bounds__(1024)
       if ((fm >> nb) & 1) rv = rv + b2r[(size_t)nb * L0.np + p] * B.bc[nb].value;
     if (vbc[q]) rv = rv + vbc[q][e];
     b[p] = rv;
-    x[p] = phi[c];
+    X0[p] = phi[c];
   }
   __syncthreads();
-  int iters = 0;
-  const double bb = pf_dot_d(L0, b, part);
-  if (bb == 0.0) {
-    for (int p = threadIdx.x; p < L0.np; p += blockDim.x) x[p] = 0.0;
-    __syncthreads();
-  } else {
-    const double eps = tol * tol;
-    for (int it = 0; it < max_iter; it++) {
-      pf_relax_d(L0, A, x, b, r, false);
-      pf_residual_d(L0, A, x, b, r);
-      if (tol > 0.0) {
-        const double rr = pf_dot_d(L0, r, part);
-        if (rr / bb < eps && it > 0) break;
-      }
-      if (nl > 1) {
-        pf_restrict_d(L0, Lg[1], Pw, r, b);
-        int l;
-        for (l = 1; l <= nl - 2; l++) {
-          const PfLvl Ll = Lg[l];
-          if (Ll.active) {
-            pf_relax_d(Ll, A, x, b, r, true);
-            pf_residual_d(Ll, A, x, b, r);
-          } else {
-            for (int p = threadIdx.x; p < Ll.np; p += blockDim.x) {
-              x[Ll.off + p] = 0.0;
-              r[Ll.off + p] = b[Ll.off + p];
-            }
-            __syncthreads();
-          }
-          pf_restrict_d(Ll, Lg[l + 1], Pw, r, b);
-        }
-        const PfLvl Lb = Lg[l];
-        if (Lb.active) {
-          pf_relax_d(Lb, A, x, b, r, true);
-        } else {
-          for (int p = threadIdx.x; p < Lb.np; p += blockDim.x) x[Lb.off + p] = 0.0;
-          __syncthreads();
-        }
-        for (l = nl - 2; l >= 1; l--) {
-          const PfLvl Ll = Lg[l];
-          pf_interp_d(Ll, Lg[l + 1], Pw, x);
-          if (Ll.active) pf_relax_d(Ll, A, x, b, r, false);
-        }
-        pf_interp_d(L0, Lg[1], Pw, x);
-      }
-      pf_relax_d(L0, A, x, b, r, false);
-      iters = it + 1;
-    }
-  }
+  int cur = 0;
+  const int iters = afh_pf::pf_solve_block(Lg, nl, wave_from, A, Aw, soff, Pw, X0, X1, b, r,
+                                           &slot, tol, max_iter, &cur);
+  const double *x = cur ? X1 : X0;
   // coarse_solver_get_phi
   for (int u = threadIdx.x; u < nid * n3; u += blockDim.x) {
     const int q = u / n3, e = u % n3, id = ids[q];
     const afh_box_meta &m = meta[id - 1];
     const int i = e % nc + 1, j = (e / nc) % nc + 1, k = e / (nc * nc) + 1;
+    (void)q;
     const int p = (((m.ix[2] - 1) * nc + k - 1) * ny + (m.ix[1] - 1) * nc + j - 1) * nx +
                   (m.ix[0] - 1) * nc + i - 1;
     phi[(size_t)(id - 1) * bsz + ix3(nc + 2, i, j, k)] = x[p];
@@ -3000,7 +2816,7 @@ struct afh_mg {
   std::map<int, std::vector<double>> h_vl1;
   std::vector<double> pf_a7;
   uint64_t pf_v1_gen = 0, pf_meth_gen = UINT64_MAX;
-  int pf_nl = 0, pf_np = 0, pf_lds = 0;
+  int pf_nl = 0, pf_np = 0, pf_lds = 0, pf_wave = 0;
   PfLvl *d_pf_lvl = nullptr;
   double *d_pf_A = nullptr, *d_pf_P = nullptr, *d_pf_b2r = nullptr, *d_pf_x = nullptr;
   uint8_t *d_pf_fmask = nullptr;
@@ -4150,27 +3966,9 @@ static int32_t pf_prepare(afh_mg *mg) {
     if (afh_pfmg_setup(&h, nx, ny, nz, 3, a7.data()))
       return set_error(AFH_ERR_DEVICE, "pfmg: host setup allocation");
     const int np = (int)h.off[h.nl];
-    std::vector<PfLvl> lv(h.nl);
-    std::vector<double> A((size_t)27 * np), P((size_t)2 * np);
-    for (int l = 0; l < h.nl; l++) {
-      PfLvl &L = lv[l];
-      for (int d = 0; d < 3; d++) L.n[d] = h.n[l][d];
-      L.cdir = l + 1 < h.nl ? h.cdir[l] : -1;
-      L.active = h.active[l];
-      L.off = (int)h.off[l];
-      L.np = (int)(h.off[l + 1] - h.off[l]);
-      L.w = h.w[l];
-      L.mask = 0;
-      for (int p = 0; p < L.np; p++)
-        for (int s2 = 0; s2 < 27; s2++) {
-          const double a = h.A[27 * ((size_t)L.off + p) + s2];
-          A[(size_t)27 * L.off + (size_t)s2 * L.np + p] = a;
-          if (a != 0.0) L.mask |= 1u << s2;
-        }
-      for (int p = 0; p < L.np; p++)
-        for (int c2 = 0; c2 < 2; c2++)
-          P[(size_t)2 * L.off + (size_t)c2 * L.np + p] = h.P[2 * ((size_t)L.off + p) + c2];
-    }
+    std::vector<PfLvl> lv;
+    std::vector<double> A, P;
+    afh_pf::pf_device_tables(h, lv, A, P);
     afh_pfmg_free(&h);
     hipFree(mg->d_pf_lvl), hipFree(mg->d_pf_A), hipFree(mg->d_pf_P), hipFree(mg->d_pf_x);
     mg->d_pf_x = nullptr;
@@ -4182,14 +3980,15 @@ static int32_t pf_prepare(afh_mg *mg) {
     AFH_HIP(hipMemcpy(mg->d_pf_P, P.data(), sizeof(double) * P.size(), hipMemcpyHostToDevice));
     mg->pf_nl = (int)lv.size();
     mg->pf_np = np;
-    // x, b, r in LDS up to 120 KB, else in global memory
-    const size_t vbytes = sizeof(double) * 3 * (size_t)np;
-    mg->pf_lds = vbytes <= 120 * 1024 ? (int)vbytes : 0;
+    // the vectors and the wave levels' operators in LDS when they fit
+    mg->pf_wave = afh_pf::pf_wave_from(lv);
+    const size_t lds = afh_pf::pf_lds_bytes(lv, true);
+    mg->pf_lds = lds + 64 <= 160 * 1024 ? (int)lds : 0;
     if (mg->pf_lds)
-      AFH_HIP(hipFuncSetAttribute((const void *)k_cs_pfmg,
+      AFH_HIP(hipFuncSetAttribute((const void *)k_cs_pfmg<true>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, mg->pf_lds));
     else
-      AFH_HIP(hipMalloc(&mg->d_pf_x, vbytes));
+      AFH_HIP(hipMalloc(&mg->d_pf_x, sizeof(double) * 4 * (size_t)np));
     mg->pf_a7.swap(a7);
   }
   if (!mg->d_pf_b2r) {
@@ -4216,12 +4015,12 @@ static int32_t solve_coarse_pfmg(afh_mg *mg) {
   const int nid = t->ids.n(1);
   // workgroup: the level-0 points over whole waves, 256 .. 1024 lanes
   const int n0 = (int)(mg->pf_a7.size() / 7);
-  const int nt = std::min(1024, std::max(PF_NPART, (n0 + 63) / 64 * 64));
-  hipLaunchKernelGGL(k_cs_pfmg, dim3(1), dim3(nt), mg->pf_lds, t->stream, mg->d_pf_lvl,
-                     mg->pf_nl, mg->d_pf_A, mg->d_pf_P, mg->d_pf_b2r, mg->d_pf_fmask,
-                     mg->d_pf_vbc, mg->d_pf_x, mg->pf_lds ? 1 : 0, t->ccv(mg->d.i_phi),
-                     t->ccv(mg->d.i_rhs), t->d_boxes, t->ids.at(1), nid, t->nc, t->bsz, B,
-                     mg->d.coarse_tol, mg->d.coarse_cycles, mg->d_cycles);
+  const int nt = std::min(1024, std::max(256, (n0 + 63) / 64 * 64));
+  hipLaunchKernelGGL(mg->pf_lds ? k_cs_pfmg<true> : k_cs_pfmg<false>, dim3(1), dim3(nt),
+                     mg->pf_lds, t->stream, mg->d_pf_lvl, mg->pf_nl, mg->pf_wave, mg->d_pf_A,
+                     mg->d_pf_P, mg->d_pf_b2r, mg->d_pf_fmask, mg->d_pf_vbc, mg->d_pf_x,
+                     t->ccv(mg->d.i_phi), t->ccv(mg->d.i_rhs), t->d_boxes, t->ids.at(1), nid,
+                     t->nc, t->bsz, B, mg->d.coarse_tol, mg->d.coarse_cycles, mg->d_cycles);
   AFH_LAUNCH_CHECK("k_cs_pfmg");
   mg->cycles_host = 0, mg->cycles_on_dev = true;
   return gc_lvl(t, 1, mg->d.i_phi, 1);

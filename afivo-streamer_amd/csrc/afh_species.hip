@@ -2576,9 +2576,14 @@ static int32_t ion_se_dev(afh_fluid *f) {
     if (f->d.species_charge[f->d.ion_species[q] - 1] > 0) A.fi[A.n++] = t->fcv(f->d.f_ion_flux[q]);
   const int n = t->leaves.off[t->nlvl] - t->leaves.off[0], nc = t->nc;
   if (!A.n || !n) return AFH_OK;
-  hipLaunchKernelGGL(k_ion_se, dim3((nc * nc + 255) / 256, 6, n), dim3(256), 0, t->stream, A,
-                     t->d_boxes, t->leaves.at(1), nc, t->fsz);
-  AFH_LAUNCH_CHECK("k_ion_se");
+  // every leaf of every level, at most 65535 per launch (the grid's z limit)
+  const int blk = fit_blk(nc * nc);
+  for (int q0 = 0; q0 < n; q0 += 65535) {
+    const int nq = std::min(65535, n - q0);
+    hipLaunchKernelGGL(k_ion_se, dim3((nc * nc + blk - 1) / blk, 6, nq), dim3(blk), 0,
+                       t->stream, A, t->d_boxes, t->leaves.at(1) + q0, nc, t->fsz);
+    AFH_LAUNCH_CHECK("k_ion_se");
+  }
   return AFH_OK;
 }
 

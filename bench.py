@@ -64,7 +64,23 @@ DRIVER_CONFIGS = ("s3", "s4", "s5")
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E peak (spec)
 
 
-def build_case(lib, config, device, coarse_cycles, shard_ranks=None):
+# level-1 solves (--coarse): the reference's HYPRE PFMG restated (50
+# iterations at most, tolerance 1e-6: m_af_types.f90:560-565), or our exact
+# separable solve
+COARSE = {"pfmg": dict(coarse_cycles=50, coarse_tol=1e-6, coarse_mode=3),
+          "direct": dict(coarse_cycles=0, coarse_tol=0.0, coarse_mode=None)}
+
+
+def coarse_choice(arg, config):
+    """auto: the reference's PFMG on its own configurations (s3, s4, s5, 2d),
+    the exact solve on the synthetic uniform trees (s1, s1-64: a 64^3 level 1
+    is one workgroup's worth of PFMG too many)."""
+    if arg != "auto":
+        return arg
+    return "pfmg" if config in DRIVER_CONFIGS or config == "2d" else "direct"
+
+
+def build_case(lib, config, device, coarse, shard_ranks=None):
     """shard_ranks = (world, rank, "native" | "python"): this rank's part of
     the sharded tree."""
     from afh.streamer import StreamerCase, seed_state, tables_from
@@ -92,8 +108,8 @@ def build_case(lib, config, device, coarse_cycles, shard_ranks=None):
         else:
             from afh.dist import Partition, Shard
             shard = Shard(Partition(topo, world), rank, "nccl", device="cuda:%d" % device)
-    case = StreamerCase(lib, topo, td, chem, voltage, coarse_cycles=coarse_cycles,
-                        device=device, shard=shard)
+    case = StreamerCase(lib, topo, td, chem, voltage, device=device, shard=shard,
+                        **COARSE[coarse])
     seed_state(case, width=0.05 * dom[-1])
     return case
 
@@ -167,12 +183,12 @@ class DriverCase:
         self.sim.fused_rhs = on
 
 
-def build_driver_case(lib, device, config="s3"):
+def build_driver_case(lib, device, config="s3", coarse="pfmg"):
     import golden
     from afh.driver import Simulation
     from afh.users import USERS
     sim = Simulation(lib, golden.load("case_" + config), device=device,
-                     user=USERS.get(config))
+                     user=USERS.get(config), **COARSE[coarse])
     sim.set_initial_conditions()
     return sim
 
@@ -196,7 +212,7 @@ def cpu_baseline_driver(sim, steps=2, config="s3"):
                       "OpenMP" % (steps, config.upper(), ncell)}
 
 
-def cpu_baseline(config, coarse_cycles, steps=2):
+def cpu_baseline(config, coarse, steps=2):
     """The C oracle (oracle/lib/libafo.so, OpenMP) on a bounded sample of the
     same workload: the same 64^3 boxes but a 3-level tree (64 leaf boxes)."""
     from afh import capi
@@ -209,8 +225,7 @@ def cpu_baseline(config, coarse_cycles, steps=2):
     g = golden.load("uni8")
     td, chem = tables_from(g)
     lib = capi.oracle_library()
-    case = StreamerCase(lib, topo, td, chem, -dom[2] * (-2.5e6),
-                        coarse_cycles=coarse_cycles)
+    case = StreamerCase(lib, topo, td, chem, -dom[2] * (-2.5e6), **COARSE[coarse])
     seed_state(case, width=0.05 * dom[2])
     unit_step(case, 1e-13, 0)
     unit_step(case, 1e-13, 1)
@@ -266,9 +281,10 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="s1-64", choices=sorted(CONFIGS))
-    ap.add_argument("--coarse-cycles", type=int, default=0,
-                    help="level-1 solve: N MG cycles, or 0 = exact separable "
-                         "solve (AFH_COARSE_DIRECT)")
+    ap.add_argument("--coarse", choices=("auto", "pfmg", "direct"), default="auto",
+                    help="level-1 solve: the reference's HYPRE PFMG restated "
+                         "(AFH_COARSE_PFMG) or our exact separable solve "
+                         "(AFH_COARSE_DIRECT); auto: PFMG on s3/s4/s5/2d")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-fused-rhs", action="store_true",
                     help="separate field_set_rhs pass instead of the rhs folded "
@@ -286,6 +302,7 @@ def main():
                     help="V-cycles replayed as captured hipGraphs (auto: on for the "
                          "small-box configs s1 / s3, whose steps are launch-bound)")
     args = ap.parse_args()
+    coarse = coarse_choice(args.coarse, args.config)
 
     if args.graphs == "off":
         os.environ["AFH_GRAPHS"] = "0"  # read by afh_mg_create
@@ -307,7 +324,7 @@ def main():
     if two_d and sharded:
         raise SystemExit("the 2-D build does not shard (--replicas runs one per GPU)")
     if args.config in DRIVER_CONFIGS:
-        sim = build_driver_case(lib, local, args.config)
+        sim = build_driver_case(lib, local, args.config, coarse)
         if sharded:
             # every rank built the same AMR tree (the set-up is deterministic);
             # its part of it continues sharded, exchanges over RCCL
@@ -317,7 +334,7 @@ def main():
                                        comm=rccl_comm(lib, rank, world, local)))
         case = DriverCase(sim)
     else:
-        case = build_case(lib, args.config, local, args.coarse_cycles,
+        case = build_case(lib, args.config, local, coarse,
                           (world, rank, args.shard) if sharded else None)
     from afh.streamer import cells
     ncell = cells(case.topo)  # leaf cells of the whole tree
@@ -425,8 +442,8 @@ def main():
             "config": {"workload": args.config, "n_cell": CONFIGS[args.config][0],
                        "leaf_cells": ncell, "boxes": int(case.topo["n_boxes"]),
                        "levels": int(case.topo["highest_lvl"]),
-                       "coarse_solve": ("direct" if args.coarse_cycles == 0 else
-                                        "mg%d" % args.coarse_cycles),
+                       "coarse_solve": {"pfmg": "HYPRE PFMG restated (tol 1e-6, <= 50 it.)",
+                                        "direct": "exact separable"}[coarse],
                        "fused_rhs": "interior" if not args.no_fused_rhs else False,
                        "face_field": "from phi in the flux" if faces_from_phi else "stored",
                        "vcycle_graphs": graphs,
@@ -449,32 +466,27 @@ def main():
         if two_d:
             # BASELINE's CPU-runnable case, not the headline: its roofline
             # line is the half-sweep smoother over all levels
-            out["config"]["coarse_solve"] = "direct"
             out["config"]["ndim"] = 2
             out["config"]["fused_rhs"] = False
         if sharded:
             out["exchanges_per_step"] = case.shard.n_exchanges / max(1, args.steps + args.warmup + 1)
         if args.config == "s3":
             out["config"]["chemistry"] = "air_chemistry_v2 (9 species, 25 reactions)"
-            out["config"]["coarse_solve"] = "direct"
         if args.config == "s4":
             out["config"]["chemistry"] = "air_chemistry_v2 (9 species, 25 reactions)"
             out["config"]["electrode"] = ("grounded rod (0.5,0.5,0)-(0.5,0.5,0.15) L, r = 1 mm, "
                                           "%d electrode boxes" % len(sim.electrode_ids))
-            out["config"]["coarse_solve"] = (
-                "electrode level 1: red-black GS to stationarity"
-                if os.environ.get("AFH_CS_ELEC_DIRECT", "1") == "0" else
-                "electrode level 1: dense inverse product (one 8^3 box)")
+            if coarse == "direct":
+                out["config"]["coarse_solve"] = "electrode level 1: dense inverse product (one 8^3 box)"
         if args.config == "s5":
             out["config"]["chemistry"] = "sprite_chemistry_v0 (10 species, 12 reactions)"
             out["config"]["gas_density"] = "variable (3d_sprite m_user: 2.5e25 exp(-z/7.2 km))"
             out["config"]["photoionization"] = ("Helmholtz Bourdon-3, every %d time steps"
                                                 % sim.c.i("photoi%per_steps"))
-            out["config"]["coarse_solve"] = "direct"
         if not args.no_cpu_baseline and world == 1 and not two_d:
             out["cpu_baseline"] = (cpu_baseline_driver(sim, config=args.config)
                                    if args.config in DRIVER_CONFIGS else
-                                   cpu_baseline(args.config, args.coarse_cycles))
+                                   cpu_baseline(args.config, coarse))
         print(json.dumps(out))
     if dist is not None:
         dist.barrier()

@@ -23,17 +23,20 @@
  * Built: the tree with its ghost cells (af_gc_box with neighbour copy,
  * bc_to_gc, af_gc_interp / af_gc_interp_lim / mg_sides_rb, corners),
  * restriction, the FAS V-cycle and FMG of a Poisson / Helmholtz operator with
- * the exact level-1 solve (AFH_COARSE_DIRECT only), the field gradient and
+ * the exact level-1 solve (AFH_COARSE_DIRECT) or the reference's HYPRE PFMG
+ * restated (AFH_COARSE_PFMG, round 5), the field gradient and
  * |E|, field_set_rhs, the species step (af_restrict_ref_boundary, af_gc2_box,
  * flux_upwind_box with the m_fluid callbacks, af_consistent_fluxes,
  * flux_update_densities with the field-dependent rate forms). Not built in
  * 2-D (AFH_ERR_UNSUPPORTED or not exported): cylindrical coordinates
  * (af_cyl), electrodes / level sets, variable gas density, photoionization,
- * the temperature rate forms, sharding, deferred reductions. Built in round 4
- * for the 2-D time loop (afh.driver over this library, programs/standard_2d/
- * tests/test_2d_rtest.log): the device regrid with the prolongation of the
- * automatic variables, default_refinement's flags, and the regression-log
- * sums and extrema.
+ * the temperature rate forms, sharding, ion secondary emission. Built in
+ * round 4 for the 2-D time loop (afh.driver over this library,
+ * programs/standard_2d/tests/test_2d_rtest.log): the device regrid with the
+ * prolongation of the automatic variables, default_refinement's flags, the
+ * regression-log sums and extrema, and the deferred reductions
+ * (afh_mg_fas_vcycle_fold, afh_fluid_forward_euler_fold,
+ * afh_fluid_fetch_step, below).
  */
 #ifndef AFIVO_HIP_2D_H
 #define AFIVO_HIP_2D_H

@@ -13,6 +13,7 @@
 
 #include <float.h>
 #include <math.h>
+#include <pthread.h>
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -1255,6 +1256,10 @@ static struct {
   double dr[3];
   int valid, singular;
 } csd_last;
+/* thread ranks (tests/test_dist_driver.py) solve level 1 concurrently
+ * through ctypes, which releases the GIL: the cache's lookup, build and use
+ * are one critical section (the device library's csd_mu) */
+static pthread_mutex_t csd_mu = PTHREAD_MUTEX_INITIALIZER;
 
 static int solve_coarse_direct(afh_mg *mg) {
   afh_tree *t = mg->t;
@@ -1269,6 +1274,7 @@ static int solve_coarse_direct(afh_mg *mg) {
     if (m->neighbors[q] >= 0) return 1;
   const afh_bc *bc = t->meth[mg->d.i_phi].bc;
   const size_t n = AFH_CSD_N;
+  pthread_mutex_lock(&csd_mu);
   if (!csd_last.valid || memcmp(csd_last.v, mg->vst[id - 1], sizeof(double) * 7 * n) ||
       memcmp(csd_last.bc, bc, sizeof csd_last.bc) ||
       memcmp(csd_last.dr, m->dr, sizeof csd_last.dr)) {
@@ -1286,7 +1292,10 @@ static int solve_coarse_direct(afh_mg *mg) {
     free(work);
     csd_last.valid = 1;
   }
-  if (csd_last.singular) return 1;
+  if (csd_last.singular) {
+    pthread_mutex_unlock(&csd_mu);
+    return 1;
+  }
   double b[AFH_CSD_N];
   const double *r = ccb(t, mg->d.i_rhs, id), *bcc = mg->vbc[id - 1];
   double *x = ccb(t, mg->d.i_phi, id);
@@ -1304,6 +1313,7 @@ static int solve_coarse_direct(afh_mg *mg) {
     const int i = row % nc + 1, j = (row / nc) % nc + 1, k = row / (nc * nc) + 1;
     x[IX(t, i, j, k)] = acc;
   }
+  pthread_mutex_unlock(&csd_mu);
   mg->cs_iters = 1;
   return gc_lvl(t, 1, mg->d.i_phi, 1) ? -1 : 0;
 }
@@ -1405,8 +1415,8 @@ static void pf_residual(afh_mg *mg, int l) {
 }
 
 /* r.r (or b.b) on level 0: AFH_PFMG_NPART strided partial sums, then a
- * pairwise tree (the device's workgroup reduction) */
-#define AFH_PFMG_NPART 256
+ * pairwise tree (the device's wave reduction, afh_pfmg_dev.h pf_dot) */
+#define AFH_PFMG_NPART 64
 static double pf_dot(afh_mg *mg, const double *v) {
   double part[AFH_PFMG_NPART];
   const size_t n = mg->pf.off[1];
