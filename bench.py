@@ -80,9 +80,9 @@ def coarse_choice(arg, config):
     return "pfmg" if config in DRIVER_CONFIGS or config == "2d" else "direct"
 
 
-def build_case(lib, config, device, coarse, shard_ranks=None):
+def build_case(lib, config, device, coarse, shard_ranks=None, shard=None):
     """shard_ranks = (world, rank, "native" | "python"): this rank's part of
-    the sharded tree."""
+    the sharded tree; or shard: a prepared afh.dist shard (thread ranks)."""
     from afh.streamer import StreamerCase, seed_state, tables_from
     from afh.tree import uniform_tree
     import golden
@@ -95,7 +95,6 @@ def build_case(lib, config, device, coarse, shard_ranks=None):
     g = golden.load("uni8")  # transport/chemistry tables exported from the reference
     td, chem = tables_from(g)
     voltage = -dom[-1] * (-2.5e6)
-    shard = None
     if shard_ranks is not None:
         world, rank, kind = shard_ranks
         if kind == "native":
@@ -275,6 +274,157 @@ def write_topology(case, config, path, faces_from_phi=False, fused_rhs=False):
                    "fused_rhs": bool(fused_rhs)}, f)
 
 
+def _hip_stream():
+    """A HIP stream shared by the thread ranks of --shared-stream."""
+    import ctypes as C
+    hip = C.CDLL("libamdhip64.so")
+    st = C.c_void_p()
+    if hip.hipStreamCreate(C.byref(st)) != 0:
+        raise RuntimeError("hipStreamCreate")
+    return st
+
+
+def local_ranks(lib, config, world, device, coarse, shared_stream=False):
+    """--transport local: the sharded workload on `world` thread ranks of this
+    process (afh_dist AFH_DIST_LOCAL: pack, host barrier, peer copies,
+    unpack), every rank on `device`. The same partition, plans and hooks the
+    RCCL transport uses; only the transport differs. Returns (cases, shards,
+    group, base): base is the unsharded set-up (driver configs) or None."""
+    from afh import capi
+    from afh.dist import NativeGroup, NativeShard
+    group = NativeGroup(lib, world)
+    base = None
+    if config in DRIVER_CONFIGS:
+        base = build_driver_case(lib, device, config, coarse)
+        topo = base.af.topology()
+        sims = [base.clone(lib, device=device) for _ in range(world)]
+        shards = [NativeShard(lib, topo, world, r, transport=capi.DIST_LOCAL, group=group)
+                  for r in range(world)]
+        for sim, sh in zip(sims, shards):
+            sim.shard_over(sh)
+        cases = [DriverCase(sim) for sim in sims]
+    else:
+        from afh.tree import uniform_tree
+        nc, cgs, lvls, dom = CONFIGS[config]
+        topo = uniform_tree(nc, cgs, dom, lvls)
+        shards = [NativeShard(lib, topo, world, r, transport=capi.DIST_LOCAL, group=group)
+                  for r in range(world)]
+        # (the set-up fills ghost cells: exchanges, so every rank on its thread)
+        cases = run_ranks(shards, lambda r, sh: build_case(lib, config, device, coarse,
+                                                           shard=sh))
+    if shared_stream:
+        st = _hip_stream()
+        for c in cases:
+            lib.call("tree_set_stream", c.tree.h, st)
+    return cases, shards, group, base
+
+
+def run_ranks(cases, fn):
+    """fn(rank, case) on one thread per rank; the results in rank order."""
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(len(cases)) as ex:
+        futs = [ex.submit(fn, r, c) for r, c in enumerate(cases)]
+        return [f.result() for f in futs]
+
+
+def dist_stats(lib, shard):
+    import ctypes as C
+    n, b = C.c_int64(), C.c_int64()
+    lib.call("dist_stats", shard.h, C.byref(n), C.byref(b))
+    return n.value, b.value
+
+
+def bench_local(args, coarse):
+    """--transport local --gpus N: N thread ranks on ONE device run the
+    sharded unit step; not the metric (the ranks share one GPU), but every
+    line of the sharded bench except the RCCL calls, plus what a scaling
+    projection needs: per rank the leaf cells it owns, the exchanges and the
+    bytes per step."""
+    import threading
+    from afh import capi
+    from afh.streamer import cells
+    lib = capi.hip_library() if not args.oracle else capi.oracle_library()
+    device = -1 if args.oracle else 0
+    world = args.gpus
+    # one stream for all ranks: no V-cycle graphs (a capture on a stream
+    # other threads launch into would take their work too)
+    graphs_env = os.environ.get("AFH_GRAPHS")
+    if args.shared_stream:
+        os.environ["AFH_GRAPHS"] = "0"
+    try:
+        cases, shards, group, base = local_ranks(lib, args.config, world, device, coarse,
+                                                 args.shared_stream)
+    finally:
+        if args.shared_stream:
+            if graphs_env is None:
+                os.environ.pop("AFH_GRAPHS", None)
+            else:
+                os.environ["AFH_GRAPHS"] = graphs_env
+    dt = 1e-13
+    bar = threading.Barrier(world)
+    clock = {}
+
+    def work(r, case):
+        if not args.no_fused_rhs:
+            case.fuse_rhs(True, ghosts=False)
+        if args.config not in DRIVER_CONFIGS and not args.stored_face_field:
+            case.faces_from_phi(True)
+        case.field_compute(0, n_vcycles=2)
+        for k in range(args.warmup):
+            unit_step(case, dt, k)
+        case.tree.sync()
+        s0 = dist_stats(lib, shards[r])
+        bar.wait()
+        if r == 0:
+            clock["t0"] = time.perf_counter()
+            clock["ns0"] = time.clock_gettime_ns(time.CLOCK_MONOTONIC)
+        bar.wait()
+        for k in range(args.steps):
+            unit_step(case, dt, args.warmup + k)
+        case.tree.sync()
+        bar.wait()
+        if r == 0:
+            clock["t1"] = time.perf_counter()
+            clock["ns1"] = time.clock_gettime_ns(time.CLOCK_MONOTONIC)
+        s1 = dist_stats(lib, shards[r])
+        return s1[0] - s0[0], s1[1] - s0[1]
+
+    try:
+        stats = run_ranks(cases, work)
+    finally:
+        for sh in shards:
+            sh.detach()
+        group.close()
+    elapsed = clock["t1"] - clock["t0"]
+    topo = base.af.topology() if base is not None else shards[0].topo
+    ncell = cells(topo)
+    nc = int(topo["nc"])
+    leaves = set()
+    for l in range(1, int(topo["highest_lvl"]) + 1):
+        leaves.update(int(i) for i in topo["lvl_leaves_%d" % l])
+    owned = []
+    for sh in shards:
+        own = [i for i in leaves if sh.owner[i - 1] == sh.rank]
+        owned.append(len(own) * nc ** 3)
+    steps = max(1, args.steps)
+    return {
+        "metric": "cell-updates/s (fluid+MG V-cycle), thread ranks sharing one GPU",
+        "value": ncell * args.steps / elapsed, "unit": "cell-updates/s",
+        "n_ranks": world, "transport": "local (AFH_DIST_LOCAL thread ranks, one device)",
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / steps,
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic", "shared_stream": bool(args.shared_stream),
+        "config": {"workload": args.config, "leaf_cells": ncell, "boxes": int(topo["n_boxes"]),
+                   "coarse_solve": coarse},
+        "owned_leaf_cells": owned,
+        "exchanges_per_step": [n / steps for n, _ in stats],
+        "exchange_bytes_per_step": [b / steps for _, b in stats],
+        "note": "not the metric: the ranks share one device; see scripts/project_scaling.py",
+        # the timed region on CLOCK_MONOTONIC (a kernel trace's clock)
+        "window_ns": [clock["ns0"], clock["ns1"]],
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -298,11 +448,25 @@ def main():
     ap.add_argument("--shard", choices=("native", "python"), default="native",
                     help="N>1 sharding: the library's (afh_dist, RCCL transport, owned-box "
                          "storage) or the Python hook over torch.distributed (afh.dist.Shard)")
+    ap.add_argument("--transport", choices=("rccl", "local"), default="rccl",
+                    help="N>1: one process per GPU over RCCL (torchrun), or local: N thread "
+                         "ranks of this process on one GPU (AFH_DIST_LOCAL; a rehearsal of "
+                         "the sharded step and the input of the scaling projection)")
+    ap.add_argument("--shared-stream", action="store_true",
+                    help="--transport local: every rank on one HIP stream (kernels "
+                         "serialised, so that a kernel trace gives each rank's own time)")
+    ap.add_argument("--oracle", action="store_true",
+                    help="--transport local on the C oracle (CPU), for tests")
     ap.add_argument("--graphs", choices=("auto", "on", "off"), default="auto",
                     help="V-cycles replayed as captured hipGraphs (auto: on for the "
                          "small-box configs s1 / s3, whose steps are launch-bound)")
     args = ap.parse_args()
     coarse = coarse_choice(args.coarse, args.config)
+    if args.transport == "local":
+        if args.graphs == "off":
+            os.environ["AFH_GRAPHS"] = "0"
+        print(json.dumps(bench_local(args, coarse)))
+        return
 
     if args.graphs == "off":
         os.environ["AFH_GRAPHS"] = "0"  # read by afh_mg_create
@@ -378,6 +542,7 @@ def main():
     barrier()
     case.tree.sync()
     t0 = time.perf_counter()
+    ns0 = time.clock_gettime_ns(time.CLOCK_MONOTONIC)
     last_res = None
     for k in range(args.steps):
         last = unit_step(case, dt, args.warmup + k)
@@ -386,6 +551,7 @@ def main():
     case.tree.sync()
     barrier()
     elapsed = time.perf_counter() - t0
+    ns1 = time.clock_gettime_ns(time.CLOCK_MONOTONIC)
     if graphs or two_d:
         lib.call("profile_enable", case.tree.h, capi.PROF_GSRB if two_d else capi.PROF_GSRB_PAIR)
         for k in range(2):
@@ -462,6 +628,9 @@ def main():
             "last_residual": last_res[-1] if last_res else None,
             # one FAS V(2,2)-cycle per step (SURVEY.md 8(d) reports both)
             "vcycles_per_s": args.steps / elapsed,
+            # the timed region on CLOCK_MONOTONIC (a kernel trace's clock;
+            # scripts/project_scaling.py)
+            "window_ns": [ns0, ns1],
         }
         if two_d:
             # BASELINE's CPU-runnable case, not the headline: its roofline
