@@ -54,13 +54,15 @@ CONFIGS = {
     # stencils on the boxes the rod crosses (afh.electrode), the electrode's
     # species boundary condition every time step, 5 levels of 8^3 boxes
     "s4": (8, None, None, (16e-3, 16e-3, 16e-3)),
-    # BASELINE.json config 1 (programs/standard_2d, streamer_2d.cfg's box size
-    # and domain) on the 2-D build (libafivo_hip_2d.so): 8^2 boxes, one
-    # level-1 box, uniformly refined to level 8 (128 x 128 leaf boxes, 1024^2
-    # cells), the old-style 3-species model; the unit step as for s1
-    "2d": (8, (8, 8), 8, (32e-3, 32e-3)),
+    # BASELINE.json config 1: programs/standard_2d/streamer_2d.cfg itself on
+    # the 2-D build (libafivo_hip_2d.so) -- air_chemistry_v1 (8 species, 25
+    # reactions), the AMR tree of 8^2 boxes its set_initial_conditions
+    # builds (tests/golden/case_s2d.npz, exported from the reference's own
+    # initializers)
+    "2d": (8, None, None, (32e-3, 32e-3)),
 }
-DRIVER_CONFIGS = ("s3", "s4", "s5")
+DRIVER_CONFIGS = ("s3", "s4", "s5", "2d")
+DRIVER_FIXTURE = {"s3": "case_s3", "s4": "case_s4", "s5": "case_s5", "2d": "case_s2d"}
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E peak (spec)
 
 
@@ -182,13 +184,29 @@ class DriverCase:
         self.sim.fused_rhs = on
 
 
-def build_driver_case(lib, device, config="s3", coarse="pfmg"):
+def build_driver_case(lib, device, config="s3", coarse="pfmg", grow_cells=0,
+                      grow_seconds=240.0):
+    """The reference's set-up (set_initial_conditions) of a driver config;
+    with grow_cells, then the time loop (streamer.f90's main loop: Heun
+    steps with step control, refinement every refine_per_steps, output rows)
+    until the tree holds at least grow_cells leaf cells, or grow_seconds
+    pass, or the end time is reached."""
     import golden
     from afh.driver import Simulation
     from afh.users import USERS
-    sim = Simulation(lib, golden.load("case_" + config), device=device,
+    sim = Simulation(lib, golden.load(DRIVER_FIXTURE[config]), device=device,
                      user=USERS.get(config), **COARSE[coarse])
     sim.set_initial_conditions()
+    sim.grown = {"steps": 0, "time_s": 0.0, "leaf_cells_initial": sim.af.n_leaf_cells()}
+    if grow_cells:
+        sim.output_cnt = 0
+        sim.output_write()
+        sim.time_last_output = sim.time
+        t0 = time.perf_counter()
+        while (sim.af.n_leaf_cells() < grow_cells and
+               time.perf_counter() - t0 < grow_seconds and sim.step()):
+            sim.grown["steps"] += 1
+        sim.grown["time_s"] = sim.time
     return sim
 
 
@@ -284,7 +302,7 @@ def _hip_stream():
     return st
 
 
-def local_ranks(lib, config, world, device, coarse, shared_stream=False):
+def local_ranks(lib, config, world, device, coarse, shared_stream=False, grow_cells=0):
     """--transport local: the sharded workload on `world` thread ranks of this
     process (afh_dist AFH_DIST_LOCAL: pack, host barrier, peer copies,
     unpack), every rank on `device`. The same partition, plans and hooks the
@@ -295,7 +313,7 @@ def local_ranks(lib, config, world, device, coarse, shared_stream=False):
     group = NativeGroup(lib, world)
     base = None
     if config in DRIVER_CONFIGS:
-        base = build_driver_case(lib, device, config, coarse)
+        base = build_driver_case(lib, device, config, coarse, grow_cells)
         topo = base.af.topology()
         sims = [base.clone(lib, device=device) for _ in range(world)]
         shards = [NativeShard(lib, topo, world, r, transport=capi.DIST_LOCAL, group=group)
@@ -353,7 +371,7 @@ def bench_local(args, coarse):
         os.environ["AFH_GRAPHS"] = "0"
     try:
         cases, shards, group, base = local_ranks(lib, args.config, world, device, coarse,
-                                                 args.shared_stream)
+                                                 args.shared_stream, args.grow_cells)
     finally:
         if args.shared_stream:
             if graphs_env is None:
@@ -455,6 +473,11 @@ def main():
     ap.add_argument("--shared-stream", action="store_true",
                     help="--transport local: every rank on one HIP stream (kernels "
                          "serialised, so that a kernel trace gives each rank's own time)")
+    ap.add_argument("--grow-cells", type=float, default=0,
+                    help="driver configs: advance the time loop (untimed) until the tree "
+                         "holds this many leaf cells (or --grow-seconds pass), then bench "
+                         "on that tree")
+    ap.add_argument("--grow-seconds", type=float, default=240.0)
     ap.add_argument("--oracle", action="store_true",
                     help="--transport local on the C oracle (CPU), for tests")
     ap.add_argument("--graphs", choices=("auto", "on", "off"), default="auto",
@@ -488,7 +511,8 @@ def main():
     if two_d and sharded:
         raise SystemExit("the 2-D build does not shard (--replicas runs one per GPU)")
     if args.config in DRIVER_CONFIGS:
-        sim = build_driver_case(lib, local, args.config, coarse)
+        sim = build_driver_case(lib, local, args.config, coarse, int(args.grow_cells),
+                                args.grow_seconds)
         if sharded:
             # every rank built the same AMR tree (the set-up is deterministic);
             # its part of it continues sharded, exchanges over RCCL
@@ -565,6 +589,15 @@ def main():
         kname = ("k2_pair_box (red+black pair, levels of >= 256 boxes, 24 B/cell)"
                  if os.environ.get("AFH_PAIR2D", "1") != "0" else
                  "k2_gsrb (half sweep, levels of >= 256 boxes, 16 B/cell)")
+    if nl.value == 0 and two_d:
+        # no level of >= 256 boxes runs the pair in the timed window: the
+        # split half-sweep on every level
+        kname = "k2_gsrb (half sweep, 16 B/cell)"
+        lib.call("profile_enable", case.tree.h, capi.PROF_GSRB)
+        for k in range(2):
+            unit_step(case, dt, args.warmup + args.steps + 2 + k)
+        case.tree.sync()
+        lib.call("profile_read", case.tree.h, C.byref(ms), C.byref(nl), C.byref(by))
     if nl.value == 0 and not two_d:
         # no level runs the fused pair (too few boxes per level, or
         # electrode stencils): the split half-sweep k_gsrb is the smoother
@@ -633,10 +666,21 @@ def main():
             "window_ns": [ns0, ns1],
         }
         if two_d:
-            # BASELINE's CPU-runnable case, not the headline: its roofline
-            # line is the half-sweep smoother over all levels
+            # BASELINE's config 1 (streamer_2d.cfg), not the headline: its
+            # roofline line is the 2-D fused pair on levels of >= 256 boxes
             out["config"]["ndim"] = 2
             out["config"]["fused_rhs"] = False
+            out["config"]["chemistry"] = "air_chemistry_v1 (8 species, 25 reactions)"
+            out["cpu_baseline_note"] = (
+                "no 2-D CPU port travels to the box (the C oracle is 3-D); the reference's "
+                "own 2-D forward_euler timed in the build container: profiles/"
+                "r05_ref_cpu_timing_2d.json")
+        if args.config in DRIVER_CONFIGS:
+            g = sim.grown
+            out["config"]["tree"] = {"leaf_cells_setup": g["leaf_cells_initial"],
+                                     "grown_steps": g["steps"],
+                                     "grown_to_time_s": g["time_s"],
+                                     "highest_lvl": int(sim.af.highest_lvl)}
         if sharded:
             out["exchanges_per_step"] = case.shard.n_exchanges / max(1, args.steps + args.warmup + 1)
         if args.config == "s3":
