@@ -901,11 +901,8 @@ __device__ __forceinline__ void face_vd(const FluxArgs &A, double Elo, double Eh
 // face on the last cell of a line), reconstruct_upwind_1d + the m_fluid
 // flux_upwind callback; the CFL sum of the cell over both dimensions
 // (cfl_sum = 0 + x term + y term) and the conductivity maximum are folded.
-// SH: the high face's velocity and diffusion are the low face's of the next
-// cell (same arguments in the same order), taken from that lane when it is in
-// the wave; the last cell of a line evaluates them (AFH2_FLUX_SHFL=0: every
-// cell evaluates both faces)
-template <bool SH>
+// (Round 4 measured taking the high face's velocity and diffusion from the
+// next cell's lane: neutral, profiles/r04_ab_2d_flux_shfl.txt; removed.)
 __global__ void __launch_bounds__(NT)
     k2_flux(FluxArgs A, const int32_t *__restrict__ ids, const afh_box_meta *__restrict__ meta,
             int nc, int bsz, int fsz, unsigned long long *red) {
@@ -945,14 +942,7 @@ __global__ void __launch_bounds__(NT)
       // last cell of the line)
       const double ex_hi = Ef[face[d] + fst[d]];
       double vh = 0.0, dh = 0.0, muh = 0.0;
-      bool have = false;
-      if (SH) {
-        const int sd = d == 0 ? 1 : nc;  // lane distance of the next cell along d
-        vh = __shfl_down(vl, sd, 64);
-        dh = __shfl_down(dl, sd, 64);
-        have = c < nc && (int)(threadIdx.x & 63) + sd < 64;
-      }
-      if (!have) face_vd(A, E[c0], E[c0 + st[d]], ex_hi, vh, dh, muh);
+      face_vd(A, E[c0], E[c0 + st[d]], ex_hi, vh, dh, muh);
       if (c == nc) {
         double uh;
         if (-1 * ex_hi > 0) uh = L0 + 0.5 * limiter(A.lim, Lp1 - L0, L0 - Lm1);
@@ -1155,7 +1145,7 @@ struct afh_tree {
   int device = 0;
   hipStream_t stream = nullptr;
   bool gc_box = true;  // level fills with corners in one launch (k2_gc_box; AFH2_GC_BOX=0)
-  bool gc_pack = true;  // several small boxes per k2_gc_box workgroup (AFH2_GC_PACK=0)
+  bool gc_pack = true;  // several small boxes per k2_gc_box workgroup
   // a box has a refinement boundary (a side ghost then reads the parent
   // neighbour's tangential ghost, so levels fill in order)
   bool any_refb = false;
@@ -1163,9 +1153,6 @@ struct afh_tree {
   // read an interior cell or, for corners, the box's own side ghosts;
   // AFH2_GC_TREE_ONE=0 level by level)
   bool gc_tree_one = true;
-  // k2_flux's high faces from the next lane (AFH2_FLUX_SHFL=1; measured
-  // neutral on config 1, profiles/r04_ab_2d_flux_shfl.txt)
-  bool flux_shfl = false;
   // bumped by afh_set_cc_methods / afh_set_bc: boundary values and types are
   // kernel arguments, so captured V-cycles of older generations are dropped
   uint64_t meth_gen = 0;
@@ -1218,9 +1205,6 @@ struct afh_mg {
   };
   std::map<int, Graph> graphs;
   bool use_graphs = true;
-  // boxes per k2_pair_box wave (AFH2_PAIR_PACK): 1 = two 8^2 / four 4^2,
-  // 0 = one, 2 = four 8^2 boxes of 16 lanes
-  int pair_pack = 1;
   // the up leg's corner pass folded into the next level's correction
   // (k2_block_corners; AFH2_CORNER_FOLD=0 for k2_corners)
   bool corner_fold = true;
@@ -1247,21 +1231,15 @@ struct afh_fluid {
   afh_fluid_desc d;
   double *d_td = nullptr, *d_chem = nullptr;
   DevReaction *d_reac = nullptr;
-  // k2_update compiled for the species count (1..12; AFH2_UPD_FIXED=0 for the
-  // any-count form)
-  bool upd_fixed = true;
+  // (k2_update is compiled for the species count, 1..12)
 };
 
 namespace afh2 {
 
 // per-box launches: a workgroup of the work rounded up to whole waves (at
 // most NT lanes), so a small box does not dispatch idle waves (8^2 boxes:
-// one wave per box instead of four). AFH2_BLK_FIT=0 (read when a tree is
-// created): NT lanes always
-static bool g_blk_fit = true;
-static inline int blk2n(int work) {
-  return work >= NT || !g_blk_fit ? NT : ((work + 63) / 64) * 64;
-}
+// one wave per box instead of four)
+static inline int blk2n(int work) { return work >= NT ? NT : ((work + 63) / 64) * 64; }
 static inline dim3 blk2(int work) { return dim3((unsigned)blk2n(work)); }
 static inline dim3 grid2(int work, int nbox) {
   const int b = blk2n(work);
@@ -1377,13 +1355,7 @@ int32_t afh_tree_create(const afh_tree_desc *desc, int32_t device, afh_tree **ou
   afh_tree *t = new afh_tree();
   H2(hipGetDevice(&t->device));
   if (const char *env = getenv("AFH2_GC_BOX")) t->gc_box = atoi(env) != 0;
-  if (const char *env = getenv("AFH2_GC_PACK")) t->gc_pack = atoi(env) != 0;
   if (const char *env = getenv("AFH2_GC_TREE_ONE")) t->gc_tree_one = atoi(env) != 0;
-  if (const char *env = getenv("AFH2_FLUX_SHFL")) t->flux_shfl = atoi(env) != 0;
-  {
-    const char *env = getenv("AFH2_BLK_FIT");
-    g_blk_fit = !env || atoi(env) != 0;
-  }
   t->nc = nc, t->ng = nc + 2, t->nb = desc->n_boxes, t->nlvl = desc->highest_lvl;
   t->nvc = desc->n_var_cell, t->nvf = desc->n_var_face;
   t->bsz = t->ng * t->ng, t->fsz = 2 * (nc + 1) * (nc + 1);
@@ -1662,7 +1634,6 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
   H2(hipMemcpy(mg->d_lvl_c, mg->lvl_c.data(), sizeof(Coef2) * t->nlvl, hipMemcpyHostToDevice));
   if (const char *env = getenv("AFH2_ALL_LVL")) mg->all_lvl = atoi(env) != 0;
   if (const char *env = getenv("AFH2_GRAPHS")) mg->use_graphs = atoi(env) != 0;
-  if (const char *env = getenv("AFH2_PAIR_PACK")) mg->pair_pack = atoi(env);
   if (const char *env = getenv("AFH2_CORNER_FOLD")) mg->corner_fold = atoi(env) != 0;
   H2(hipMalloc(&mg->d_q[0], sizeof(double) * nx * nx));
   H2(hipMalloc(&mg->d_q[1], sizeof(double) * ny * ny));
@@ -1860,21 +1831,13 @@ static int32_t gsrb_boxes(afh_mg *mg, int lvl, bool up, bool skip_corners = fals
       prof_mark(t, pc);
       const double *rh = t->ccv(mg->d.i_rhs);
       const int32_t *ids = t->ids.at(lvl);
-      if (t->nc == 4 && mg->pair_pack)
+      // several boxes per wave: four 4^2, two 8^2
+      if (t->nc == 4)
         hipLaunchKernelGGL((k2_pair_box<4, 16>), dim3((n + 3) / 4), dim3(64), 0, t->stream, src,
                            dst, rh, phi, t->d_boxes, ids, n, t->bsz, cf, g);
-      else if (t->nc == 4)
-        hipLaunchKernelGGL(k2_pair_box<4>, dim3(n), dim3(64), 0, t->stream, src, dst, rh, phi,
-                           t->d_boxes, ids, n, t->bsz, cf, g);
-      else if (t->nc == 8 && mg->pair_pack == 2)
-        hipLaunchKernelGGL((k2_pair_box<8, 16>), dim3((n + 3) / 4), dim3(64), 0, t->stream, src,
-                           dst, rh, phi, t->d_boxes, ids, n, t->bsz, cf, g);
-      else if (t->nc == 8 && mg->pair_pack)
+      else if (t->nc == 8)
         hipLaunchKernelGGL((k2_pair_box<8, 32>), dim3((n + 1) / 2), dim3(64), 0, t->stream, src,
                            dst, rh, phi, t->d_boxes, ids, n, t->bsz, cf, g);
-      else if (t->nc == 8)
-        hipLaunchKernelGGL(k2_pair_box<8>, dim3(n), dim3(64), 0, t->stream, src, dst, rh, phi,
-                           t->d_boxes, ids, n, t->bsz, cf, g);
       else
         hipLaunchKernelGGL(k2_pair_box<16>, dim3(n), dim3(64), 0, t->stream, src, dst, rh, phi,
                            t->d_boxes, ids, n, t->bsz, cf, g);
@@ -2174,7 +2137,6 @@ int32_t afh_fluid_create(afh_tree *t, const afh_fluid_desc *d, afh_fluid **out) 
       return set_error(AFH_ERR_UNSUPPORTED, "2-D: rate type %d", ty);
   }
   afh_fluid *f = new afh_fluid();
-  if (const char *env = getenv("AFH2_UPD_FIXED")) f->upd_fixed = atoi(env) != 0;
   f->t = t;
   f->d = *d;
   f->d.reactions = nullptr;
@@ -2291,12 +2253,8 @@ static int32_t flux_tree(afh_fluid *f, int32_t s_deriv, double *dt_lim, bool fet
                        t->d_boxes, t->leaves.at(l), nc, t->bsz, t->bc4(iv));
     H2_LAUNCH("k2_gc2");
     prof_mark(t, AFH_PROF_FLUX);
-    if (t->flux_shfl)
-      hipLaunchKernelGGL(k2_flux<true>, grid2(nc * nc, n), blk2(nc * nc), 0, t->stream, A,
-                         t->leaves.at(l), t->d_boxes, nc, t->bsz, t->fsz, t->red);
-    else
-      hipLaunchKernelGGL(k2_flux<false>, grid2(nc * nc, n), blk2(nc * nc), 0, t->stream, A,
-                         t->leaves.at(l), t->d_boxes, nc, t->bsz, t->fsz, t->red);
+    hipLaunchKernelGGL(k2_flux, grid2(nc * nc, n), blk2(nc * nc), 0, t->stream, A,
+                       t->leaves.at(l), t->d_boxes, nc, t->bsz, t->fsz, t->red);
     H2_LAUNCH("k2_flux");
     // ne and |E| read, two face fields read and two fluxes written per cell
     prof_end(t, AFH_PROF_FLUX, 48.0 * nc * nc * n);
@@ -2348,7 +2306,7 @@ static int32_t update(afh_fluid *f, double dt, int32_t s_deriv, int32_t n_prev,
     const dim3 bk = blk2(t->nc * t->nc);
     const int32_t *ids = t->leaves.at(l);
     unsigned long long *red = t->red + 2 * RED_SHARDS;
-    switch (f->upd_fixed ? A.ns : 0) {
+    switch (A.ns) {
 #define AFH2_UPD(N) \
   case N: hipLaunchKernelGGL(k2_update<N>, g, bk, 0, t->stream, A, ids, t->d_boxes, t->nc, t->bsz, t->fsz, red); break;
       AFH2_UPD(1) AFH2_UPD(2) AFH2_UPD(3) AFH2_UPD(4) AFH2_UPD(5) AFH2_UPD(6) AFH2_UPD(7)

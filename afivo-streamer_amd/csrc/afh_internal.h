@@ -25,10 +25,9 @@ namespace afh {
 
 int32_t set_error(int32_t code, const char *fmt, ...);
 int32_t check_hip(hipError_t e, const char *what);
-// Data pools (cc, fc, gc2, the spare image): hipMalloc, or with
-// AFH_POOL_CONTIG=1 hipExtMallocWithFlags(hipDeviceMallocContiguous) (falls
-// back to hipMalloc if the runtime refuses); AFH_LOG_POOLS=1 prints each
-// pool's address and its offsets modulo 4 KiB / 64 KiB / 2 MiB to stderr.
+// Data pools (cc, fc, gc2, the spare image). (Round 4's placement
+// experiments -- contiguous allocations, padding between variables, an
+// offset spare image -- changed nothing measurable and were removed.)
 int32_t pool_alloc(void **p, size_t bytes, const char *what);
 #define AFH_HIP(call)                                                         \
   do {                                                                        \
@@ -131,22 +130,6 @@ struct afh_tree {
   // live inside one fused pair); freed with the last of them
   double *alt = nullptr;
   int alt_refs = 0;
-  // level face fills: six faces per thread (k_gc_faces6) or one thread per
-  // ghost cell (k_gc_faces). Default (-1): k_gc_faces6 for boxes up to 16^3
-  // (S1 leaf fill 13.5 -> 11.8 us); at 64^3 it measured 134 -> 129 us per
-  // fill but the step no faster, so k_gc_faces stays (AFH_GC_FACES6=0/1)
-  int gc_faces6 = -1;
-  // boxes of 32^3 and up: level face fills with 8 ghost values per thread
-  // (k_gc_faces_r, AFH_GC_FACES_R=8): measured slower than one per thread
-  // on S1-64 (10.4 against 7.6 ms of fills per bench run,
-  // profiles/r04_push_ab.txt), so off
-  int gc_faces_r = 1;
-  // boxes up to 16^3: faces, edges and corners of a level in one launch
-  // (k_gc_box, AFH_GC_BOX=0 for the two-launch form)
-  bool gc_box = true;
-  // k_gc_faces pairs same-level x interfaces (one thread copies both ghost
-  // values; AFH_GC_XPAIR=0 for one thread per ghost value)
-  int gc_xpair = 0;
   // independent per-box work of every leaf level in one launch where the
   // kernel reads the box's level data from its meta record (flux of small
   // boxes, density update, residual; AFH_ALL_LVL=0: one launch per level)
@@ -179,9 +162,9 @@ struct afh_tree {
   // empty on an unsharded tree
   std::vector<char> sum_skip;
 
-  // cc variable stride (doubles): cap * bsz, plus AFH_POOL_PAD bytes
+  // cc variable stride (doubles): cap * bsz
   size_t vstride = 0;
-  double *alt_base = nullptr;  // allocation of alt (alt = alt_base + AFH_ALT_OFF)
+  double *alt_base = nullptr;  // allocation of alt (alt = alt_base)
   double *ccv(int iv) const { return cc + (size_t)(iv - 1) * vstride; }
   // cc variable iv, or the smoother's spare image of phi for iv == 0
   double *var(int iv) const { return iv == 0 ? alt : ccv(iv); }
@@ -241,7 +224,7 @@ int32_t gc_lvl(afh_tree *t, int lvl, int iv, int corners, bool rims = false);
 // on rows 1, nc and planes 1, nc (k_gsrb_pair2<..., XR> stored them): only
 // those are filled
 int32_t gc_lvl_var(afh_tree *t, int lvl, int iv, const double *vc,
-                   const GcArgs &ga, int corners, bool rims = false, bool xrim = false);
+                   const GcArgs &ga, int corners, bool rims = false);
 // edges and corners only of level lvl (k_gc_corners), for a level whose
 // faces a producer kernel filled (the fused pair's pushed faces)
 int32_t gc_lvl_corners(afh_tree *t, int lvl, int iv);

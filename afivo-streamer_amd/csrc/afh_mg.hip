@@ -376,60 +376,35 @@ struct RbPar {
 // k_gsrb_pair). Same arithmetic in the same order as k_gsrb_pair: bitwise
 // identical results.
 // DEPTH: planes of phi / rhs in flight per workgroup (1: loaded and stored
-// in the same step; 2: loaded one step earlier); NTM: workgroup size cap
-// FR: store plane rows whole, x ghost cells included (one contiguous run per
-// tile plane, no partially written cache lines; the level fill after the
-// pair rewrites every ghost cell of dst)
+// in the same step; 2: loaded one step earlier). Plane rows are stored
+// whole, x ghost cells included (one contiguous run per tile plane, no
+// partially written cache lines; the level fill after the pair rewrites
+// every ghost cell of dst).
 // KS: the k planes split into KS chunks, one workgroup each (levels with
 // too few boxes to fill the chip): a chunk recomputes the red cells of the
-// plane below it (as tiles recompute halo rows) and stores its own planes
-// NTL: the streamed plane and rhs loads non-temporal (they are used once;
-// the lines phase B reads from neighbouring boxes should stay in L2)
-// XR (whole boxes, TJ = NC, KS = 1): the x ghost cells the row stores carry
-// are the level fill's values wherever they can be formed inside the box's
-// own march, so that the fill after the pair skips those x faces (one
-// 128-B line per 8-B value on both sides, 3.1x their bytes). Facing a
-// same-level neighbour, the red ghosts are phase B's (the neighbour's new
-// red boundary cells); a black ghost is the neighbour's new black boundary
-// cell, which is formed here in the neighbour's C-phase expression from
-// this box's red boundary cell, phase B's red ghosts of the rows j-1, j+1
-// and the planes k-1, k+1, the neighbour's rhs and its red cell one column
-// further in -- recomputed from the neighbour's old values like phase B's
-// (lanes TJ+NC .. 2TJ+NC-1 in phase B; lanes 2TJ+NC .. 3TJ+NC-1 fetch the
-// rhs). Rows 1, NC and planes 1, NC (whose black ghosts need edge cells)
-// and faces without a same-level neighbour keep the fill (AFH_PAIR_XR; the
-// fill's x faces then only cover those cells).
-template <bool NTL>
-__device__ __forceinline__ double ld_nt(const double *p) {
-  if constexpr (NTL) return __builtin_nontemporal_load(p);
-  else return *p;
-}
-template <int NC, int TJ, int DEPTH = 2, int NTM = 0, bool FR = true, bool P3 = true,
-          bool SP = true, int KS = 1, bool NTL = false, bool XR = false>
-__global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
+// plane below it (as tiles recompute halo rows) and stores its own planes.
+// (Measured and removed in round 5: non-temporal plane loads, interior-only
+// row stores, four barriers per plane, natural LDS row order, 512-thread
+// whole boxes, the x ghost cells of the fill formed in the pair --
+// profiles/r03_ab_*, r04_ab_*.)
+template <int NC, int TJ, int DEPTH = 2, int KS = 1>
+__global__ void __launch_bounds__((RbPar<NC, TJ>::NT))
     k_gsrb_pair2(const double *__restrict__ src, double *__restrict__ dst,
                  const double *__restrict__ rhs, const double *__restrict__ coarse,
                  const afh_box_meta *__restrict__ meta,
                  const int32_t *__restrict__ ids, size_t bsz, Coef cf,
                  double inv_c1, GcArgs ga) {
-  using G = RbPar<NC, TJ, NTM>;
+  using G = RbPar<NC, TJ>;
   constexpr int NG = G::NG, HN = G::HN, NT = G::NT, RPT = G::RPT, PL = G::PL,
-                EPT = G::EPT, OPT = G::OPT;
+                EPT = G::EPT;
   constexpr size_t SK = (size_t)NG * NG;
-  static_assert(!XR || (TJ == NC && KS == 1 && FR && P3), "XR: whole boxes");
-  static_assert(!XR || NT >= 3 * TJ + NC, "XR: lanes for the recomputed ghosts");
-  __shared__ double P[4][PL];
-  // XR: the neighbour's red cell one column in (RN) and its rhs at the
-  // boundary cell (RH) of the black ghost of each row, by plane parity
-  __shared__ double RNX[2][XR ? TJ : 1], RHX[2][XR ? TJ : 1], ZMX[XR ? TJ : 1];  // planes s-2 .. s+1 at slot (plane & 3)
-  // LDS row layout. SP (split parity): each row holds its even-i cells, then
+  __shared__ double P[4][PL];  // planes s-2 .. s+1 at slot (plane & 3)
+  // LDS row layout (split parity): each row holds its even-i cells, then
   // its odd-i cells, so the red (black) cells the lanes of a row update and
   // all their neighbours are unit-stride in LDS (no bank conflicts); the
   // plane image is permuted on its way in (D) and out (E).
   constexpr int HG = NG / 2;
-  auto L = [](int jl, int i) {
-    return jl * NG + (SP ? ((i & 1) ? HG + (i >> 1) : (i >> 1)) : i);
-  };
+  auto L = [](int jl, int i) { return jl * NG + ((i & 1) ? HG + (i >> 1) : (i >> 1)); };
   auto perm = [&](int e) { return L(e / NG, e % NG); };  // plane entry -> LDS
   const int tid = threadIdx.x;
   const int wgs = xcd_swizzle(blockIdx.x, gridDim.x);
@@ -508,43 +483,20 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
   // column (the last level fill), so its rows j+-1 and planes s+-1 are read
   // from LDS where they are interior cells of the neighbour (unchanged
   // black values); only phi next to it and rhs come from the neighbour
-  // XR: lanes TJ+NC .. 3TJ+NC-1 fetch the inputs of the recomputed black x
-  // ghost cells (kind 1: the neighbour's red cell one column in, 7 values;
-  // kind 2: its rhs at the boundary cell)
-  constexpr int NBL = XR ? 3 * TJ + NC : TJ + NC;
+  constexpr int NBL = TJ + NC;
   struct BDesc {
-    int i, j, jl, nb, rep, kind;  // nb 0: none
+    int i, j, jl, nb, rep;  // nb 0: none
     bool pre, lm, lp, zm, zp;
     const double *xs, *rs;
     size_t c;
   };
   auto bdesc = [&](int s) {
     BDesc b;
-    b.i = b.j = b.jl = b.nb = b.kind = 0;
+    b.i = b.j = b.jl = b.nb = 0;
     b.rep = -1;
     b.pre = b.lm = b.lp = b.zm = b.zp = false;
     b.xs = b.rs = nullptr;
     b.c = 0;
-    if (XR && s >= k0 && s <= k1 && tid >= TJ + NC && tid < NBL) {
-      // the row's black ghost cell of plane s is on the low side when
-      // (j + s) is even; the neighbour's cell one column in (kind 1) is red
-      const int w = tid - (TJ + NC);
-      b.kind = w < TJ ? 1 : 2;
-      b.jl = w % TJ + 1;
-      b.j = j0 + b.jl - 1;
-      const bool lowside = ((b.j + s) & 1) == 0;
-      const int nb_id = lowside ? nb1 : nb2;
-      if (nb_id > 0) {
-        b.nb = lowside ? 1 : 2;
-        b.i = lowside ? 0 : NC + 1;
-        const int qi = b.kind == 1 ? (lowside ? NC - 1 : 2) : (lowside ? NC : 1);
-        b.xs = src + (size_t)(nb_id - 1) * bsz;
-        b.rs = rhs + (size_t)(nb_id - 1) * bsz;
-        b.pre = true;
-        b.c = ix3(NG, qi, b.j, s);
-      }
-      return b;
-    }
     if (s >= k0 && s <= k1 && tid < TJ + NC) {
       const int u = tid;
       if (u < TJ) {
@@ -630,51 +582,39 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
 #pragma unroll
     for (int e = 0; e < EPT; e++) {
       const int xx = tid + NT * e;
-      f.nx[e] = ld_nt<NTL>(x + ((size_t)kx * SK + t0 + (xx < PL ? xx : PL - 1)));
+      f.nx[e] = x[(size_t)kx * SK + t0 + (xx < PL ? xx : PL - 1)];
     }
 #pragma unroll
     for (int q = 0; q < RPT; q++) {
       const int rr = tid + NT * q;
       const int j = j0 + rr / HN, i1 = 2 * (rr % HN) + 1;
       const size_t g = (size_t)kr * SK + (size_t)j * NG + i1;
-      f.nlo[q] = ld_nt<NTL>(r + g);
-      f.nhi[q] = ld_nt<NTL>(r + g + 1);
+      f.nlo[q] = r[g];
+      f.nhi[q] = r[g + 1];
     }
   };
   Pf X0, X1;
   if (DEPTH == 2) load_pf(X0, s0 + 2);
 
-  // E: plane k of the tile to dst (in full rows with FR)
+  // E: plane k of the tile to dst, in full rows
   auto store_plane = [&](const int k, const double *Pk) {
-    if (FR) {
 #pragma unroll
-      for (int q = 0; q < G::OPTF; q++) {
-        const int e = tid + NT * q;
-        if (e < NG * TJ) st_nt<AFH_NT_PAIR>(y + ((size_t)k * SK + t0 + NG + e), Pk[perm(NG + e)]);
-      }
-    } else {
-#pragma unroll
-      for (int q = 0; q < OPT; q++) {
-        const int e = tid + NT * q;
-        if (e < NC * TJ) {
-          const int c = (e / NC + 1) * NG + e % NC + 1;
-          st_nt<AFH_NT_PAIR>(y + ((size_t)k * SK + t0 + c), Pk[L(e / NC + 1, e % NC + 1)]);
-        }
-      }
+    for (int q = 0; q < G::OPTF; q++) {
+      const int e = tid + NT * q;
+      if (e < NG * TJ) st_nt<AFH_NT_PAIR>(y + ((size_t)k * SK + t0 + NG + e), Pk[perm(NG + e)]);
     }
   };
-  // Step s. P3 (three barriers): A (red cells of plane s) with E of plane
-  // s-2 | B (red ghosts of plane s: they are first read by C of step s+1)
-  // with C (black cells of plane s-1) | D. At s = 2 and NC+1 the z ghost
-  // plane is written between B and C (C reads it; it reads the black cells
-  // C updates). Otherwise A | B | C | E, D.
+  // Step s, three barriers: A (red cells of plane s) with E of plane s-2 |
+  // B (red ghosts of plane s: they are first read by C of step s+1) with C
+  // (black cells of plane s-1) | D. At s = 2 and NC+1 the z ghost plane is
+  // written between B and C (C reads it; it reads the black cells C
+  // updates).
   auto step = [&](const int s, Pf &ld, const Pf &cn) {
     const BIn bn = load_b(s + 1);
     load_pf(ld, s + 1 + DEPTH);
     double *bl = bc.bl;
     const BDesc bd = bdesc(s);
-    const int b_i = bd.i, b_j = bd.j, b_jl = bd.jl, b_nb = bd.nb, b_rep = bd.rep,
-              b_kind = bd.kind;
+    const int b_i = bd.i, b_j = bd.j, b_jl = bd.jl, b_nb = bd.nb, b_rep = bd.rep;
     const bool b_pre = bd.pre, b_lm = bd.lm, b_lp = bd.lp, b_zm = bd.zm, b_zp = bd.zp;
     double *Pm = P[(s - 1) & 3], *P0 = P[s & 3], *Pp = P[(s + 1) & 3];
     double *Pmm = P[(s - 2) & 3];
@@ -691,7 +631,7 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
                 inv_c1;
       }
     }
-    if (P3 && s - 2 >= k0 && s - 2 < k1) store_plane(s - 2, Pmm);
+    if (s - 2 >= k0 && s - 2 < k1) store_plane(s - 2, Pmm);
     __syncthreads();
     // B: red values around the tile: x ghost cells of its rows; the halo
     // rows (ghost row of the box, or the red cells of the adjacent tile
@@ -727,12 +667,7 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
                              b_i, b_j, s, b_i, s, bsz, cf, inv_c1, bcof(b_nb), ga.rb,
                              P0[L(l1, b_i)], P0[L(l2, b_i)]);
       }
-      if (XR && b_kind == 1)
-        RNX[s & 1][b_jl - 1] = v;
-      else if (XR && b_kind == 2)
-        RHX[s & 1][b_jl - 1] = bl[6];
-      else
-        P0[L(b_jl, b_i)] = v;
+      P0[L(b_jl, b_i)] = v;
     }
     if (s == 2 || s == NC + 1) {
       // z ghost plane 0 (NC+1): red cells; x1 = plane 1 (NC), black, old;
@@ -748,24 +683,7 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
                                  i, j, k, i, j, bsz, cf, inv_c1,
                                  s == 2 ? ga.bc[4] : ga.bc[5], ga.rb, Pm[c], X2[c]);
       }
-      if (P3) __syncthreads();
-    }
-    if (!P3) __syncthreads();
-    // XR: the black x ghost cell of each row of plane s-1 (rows and planes
-    // 2 .. NC-1) is formed after the barrier that ends B (plane s's red
-    // ghosts) and C; its plane s-2 input is set aside here (D overwrites
-    // that slot)
-    auto xr_at = [&](int &jl, int &g) {
-      jl = tid - (TJ + NC) + 1;
-      const int k = s - 1;
-      const bool low = ((jl + k) & 1) == 0;
-      g = low ? 0 : NC + 1;
-      return XR && tid >= TJ + NC && tid < 2 * TJ + NC && k >= 2 && k <= NC - 1 && jl >= 2 &&
-             jl <= NC - 1 && (low ? nb1 : nb2) > 0;
-    };
-    {
-      int jl, g;
-      if (xr_at(jl, g)) ZMX[jl - 1] = Pmm[L(jl, g)];
+      __syncthreads();
     }
     // C: black cells of plane s-1, in place
     if (s - 1 >= k0 && s - 1 <= k1) {
@@ -781,24 +699,7 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
       }
     }
     __syncthreads();
-    {
-      // the neighbour's C-phase expression: its x-1 / x+1 values RN or this
-      // box's red boundary cell, its rows j+-1 and planes s-2, s phase B's
-      // red ghosts, its rhs. D writes neither Pm nor P0; plane s-1 is stored
-      // after the next barrier
-      int jl, g;
-      if (xr_at(jl, g)) {
-        const int kb = (s - 1) & 1;
-        const double rn = RNX[kb][jl - 1], me = Pm[L(jl, g == 0 ? 1 : NC)];
-        const double xm = g == 0 ? rn : me, xp = g == 0 ? me : rn;
-        Pm[L(jl, g)] = (RHX[kb][jl - 1] - cf.c[1] * xm - cf.c[2] * xp -
-                        cf.c[3] * Pm[L(jl - 1, g)] - cf.c[4] * Pm[L(jl + 1, g)] -
-                        cf.c[5] * ZMX[jl - 1] - cf.c[6] * P0[L(jl, g)]) *
-                       inv_c1;
-      }
-    }
-    // E (without P3): plane s-1; D: plane s+2 into the slot of plane s-2
-    if (!P3 && s - 1 >= k0 && s - 1 <= k1) store_plane(s - 1, Pm);
+    // D: plane s+2 into the slot of plane s-2
     if (s + 2 <= NC + 1 && s + 2 <= k1 + 2) {
 #pragma unroll
       for (int e = 0; e < EPT; e++) {
@@ -825,7 +726,7 @@ __global__ void __launch_bounds__((RbPar<NC, TJ, NTM>::NT))
       if (s + 1 <= k1 + 1) step(s + 1, X0, X1);
     }
   }
-  if (P3) store_plane(k1, P[k1 & 3]);
+  store_plane(k1, P[k1 & 3]);
 }
 
 // Whole-box form of the fused pair for small boxes (NC <= 16): the box, its
@@ -1734,36 +1635,17 @@ __global__ void k_box_copy(const double *__restrict__ src,
 
 // stencil_prolong_248 add, a column of K cells along k per thread: the
 // K/2 + 2 parent planes the column touches are loaded once (4 values each)
-// GX: the rows are NC+2 wide, and the x ghost cells facing a same-level
-// neighbour get the same correction (rows and planes 2 .. NC-1): the ghost
-// holds the neighbour's old boundary value (the level's ghost cells are
-// current in a V-cycle), and the prolongation stencil at its position reads
-// the coarse correction tmp at the same values the neighbour's own stencil
-// reads (its parent's cells, or this parent's face ghost cells, copies of
-// them: k_corr_tmp forms tmp on whole boxes) -- the value the fill after the
-// correction would copy. The fill then skips those cells (xrim).
-template <int K, bool GX = false>
+template <int K>
 __global__ void __launch_bounds__(256)
     k_prolong(double *__restrict__ phi, const double *__restrict__ tmp,
               const afh_box_meta *__restrict__ meta,
               const int32_t *__restrict__ ids, int nc, size_t bsz) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  const int nr = GX ? nc + 2 : nc;  // row width
-  if (t >= nr * nc * (nc / K)) return;
+  if (t >= nc * nc * (nc / K)) return;
   const int id = ids[blockIdx.y];
   const afh_box_meta &m = meta[id - 1];
   int i, j, kq;
-  if (GX) {
-    const int w = t / nr;
-    i = t - w * nr;  // 0 .. nc+1
-    j = w % nc + 1;
-    kq = w / nc + 1;
-    if (i == 0 || i == nc + 1) {
-      if (m.neighbors[i == 0 ? 0 : 1] <= 0 || j < 2 || j > nc - 1) return;
-    }
-  } else {
-    cell3(t, nc, i, j, kq);
-  }
+  cell3(t, nc, i, j, kq);
   const int k0 = (kq - 1) * K + 1;  // odd
   const int ng = nc + 2, hn = nc >> 1;
   const size_t sk = (size_t)ng * ng;
@@ -1786,14 +1668,12 @@ __global__ void __launch_bounds__(256)
   }
 #pragma unroll
   for (int q = 0; q < K; q++) ph[q] = phi[c + q * sk];
-  const bool ghost = GX && (i == 0 || i == nc + 1);
 #pragma unroll
   for (int q = 0; q < K; q++) {
     // cell k0+q: odd q -> (k1, k2) = planes (P+(q-1)/2, P+(q+1)/2);
     // even q -> (P+q/2, P+q/2-1); a, b index pv from plane P-1
     const int a = (q & 1) ? (q + 1) / 2 : q / 2 + 1;
     const int b = (q & 1) ? (q + 3) / 2 : q / 2;
-    if (ghost && (k0 + q == 1 || k0 + q == nc)) continue;  // rim planes: the fill
     st_nt<AFH_NT_MG>(phi + (c + q * sk),
                      ph[q] + (27 / 64.0) * pv[a][0] + (9 / 64.0) * pv[a][1] +
                          (9 / 64.0) * pv[a][2] + (3 / 64.0) * pv[a][3] +
@@ -2700,13 +2580,6 @@ struct afh_mg {
   // (default: enough boxes for one workgroup per CU, 256 tiles)
   int fused_min = 0;
   bool force_tiles = false;  // AFH_GSRB_TILES
-  bool pair_v1 = false;      // AFH_GSRB_PAIR_V1: column-mapped whole-box kernel
-  int pair_tj = 0;           // AFH_GSRB_PAIR_TJ=32: half-box tiles (NC = 64)
-  int pair_depth = 1;        // AFH_GSRB_PAIR_DEPTH=2: two planes in flight (NC = 64)
-  int pair_nt = 0;           // AFH_GSRB_PAIR_NT=512: 512-thread whole-box pair (NC = 64)
-  bool pair_fr = true;       // AFH_GSRB_PAIR_FR=0: interior-only row stores (NC = 64)
-  bool pair_p3 = true;       // AFH_GSRB_PAIR_P3=0: four barriers per plane (NC = 64)
-  bool pair_sp = true;       // AFH_GSRB_PAIR_SP=0: natural LDS row order (NC = 64)
   bool pair_box = true;      // AFH_GSRB_PAIR_BOX=0: plane-marching pair for NC <= 16
   bool grad_nt = true;       // AFH_GRAD_NT: the gradient's face fields and |E| stored
                              // nontemporal (streaming): -9 % on S1-64 (scripts/grad_ab.py)
@@ -2725,16 +2598,12 @@ struct afh_mg {
   // AFH_CS_DIRECT_SMALL: the direct solve of a level-1 grid of at most
   // CS_DS_CELLS cells in one workgroup (k_cs_direct_small), default on
   bool cs_direct_small = true;
-  int cs_ds_cells = CS_DS_CELLS;  // AFH_CS_DS_CELLS: its size limit (at most CS_SMALL_CELLS)
+  int cs_ds_cells = CS_DS_CELLS;  // its size limit (at most CS_SMALL_CELLS)
   bool pair_push = true;  // AFH_PAIR_PUSH: the small-box pair fills the faces
   // (round 4: S3 1.71 -> 1.57 ms per step, profiles/r04_push_ab.txt)
   bool prolong_push = true;  // AFH_PROLONG_PUSH: so does the small-box correction
   bool rstr_push = true;     // AFH_RSTR_PUSH: and the small-box restriction
-  // AFH_PAIR_XR: the whole-box pair of bigger boxes (k_gsrb_pair2, TJ = NC)
-  // stores the fill's x ghost cells (off until measured on the GPU)
-  bool pair_xr = false;
-  bool prolong_gx = true;  // AFH_PROLONG_GX: with it, the correction's x ghost cells
-  int tiles_min = 256;  // AFH_PAIR_TILES_MIN: levels of fewer boxes run tiles (NC >= 32)
+  int tiles_min = 256;  // levels of fewer boxes run tiles (NC >= 32)
   int *d_cycles = nullptr;
   int cycles_host = 0;
   bool cycles_on_dev = false;
@@ -2745,12 +2614,8 @@ struct afh_mg {
   int rstr_k = AFH_RSTR_K;     // coarse cells per column (AFH_RSTR_K=2|4|8 at run time)
   int res_k = AFH_RES_K;       // residual cells per column (AFH_RES_K=2|4|8 at run time)
   int prolong_k = 4;           // prolongation cells per column (AFH_PROLONG_K=2|4|8)
-  int rstr_bs = 256;           // k_rstr_fas_col workgroup size (AFH_RSTR_BS=128|256)
-  bool pair_ntl = false;       // AFH_GSRB_PAIR_NTL: non-temporal plane loads in the 64^3 pair
-  int pair_ks_leaf = 1;      // AFH_PAIR_KS_LEAF (experiment)
-  int pair_ks = 4;           // AFH_GSRB_PAIR_KS: k chunks on 64..255-box levels (NC = 64;
-                             // 4 whole-box chunks, 44 quarter-box tiles x 4, 0 tiles)
-  int wave_cells = CS_WAVE_CELLS;  // AFH_CS_WAVE_CELLS
+  int rstr_bs = 256;           // k_rstr_fas_col workgroup size
+  int wave_cells = CS_WAVE_CELLS;
   // AFH_COARSE_DIRECT: eigenvectors Q and Q^T per dim, eigenvalues, work
   double *d_q[3] = {nullptr, nullptr, nullptr}, *d_qt[3] = {nullptr, nullptr, nullptr};
   double *d_e[3] = {nullptr, nullptr, nullptr};
@@ -3005,13 +2870,6 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
     // (test_3d every row, scripts/rtest_determinism.py)
     mg->fused_min = t->nc >= 32 ? 64 : (t->nc <= 16 && mg->pair_box ? 1 : 256);
   if (const char *env = getenv("AFH_GSRB_TILES")) mg->force_tiles = atoi(env) != 0;
-  if (const char *env = getenv("AFH_GSRB_PAIR_V1")) mg->pair_v1 = atoi(env) != 0;
-  if (const char *env = getenv("AFH_GSRB_PAIR_TJ")) mg->pair_tj = atoi(env);
-  if (const char *env = getenv("AFH_GSRB_PAIR_DEPTH")) mg->pair_depth = atoi(env);
-  if (const char *env = getenv("AFH_GSRB_PAIR_NT")) mg->pair_nt = atoi(env);
-  if (const char *env = getenv("AFH_GSRB_PAIR_FR")) mg->pair_fr = atoi(env) != 0;
-  if (const char *env = getenv("AFH_GSRB_PAIR_P3")) mg->pair_p3 = atoi(env) != 0;
-  if (const char *env = getenv("AFH_GSRB_PAIR_SP")) mg->pair_sp = atoi(env) != 0;
   if (const char *env = getenv("AFH_GRAPHS")) mg->use_graphs = atoi(env) != 0;
   if (const char *env = getenv("AFH_SEG_GRAPHS")) mg->seg_graphs = atoi(env) != 0;
   if (const char *env = getenv("AFH_RSTR_COL")) mg->rstr_col = atoi(env) != 0;
@@ -3019,8 +2877,6 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
     const int k = atoi(env);
     mg->rstr_k = k == 8 ? 8 : k == 4 ? 4 : 2;
   }
-  if (const char *env = getenv("AFH_GSRB_PAIR_NTL")) mg->pair_ntl = atoi(env) != 0;
-  if (const char *env = getenv("AFH_RSTR_BS")) mg->rstr_bs = atoi(env) == 128 ? 128 : 256;
   if (const char *env = getenv("AFH_RES_K"))
     mg->res_k = atoi(env) == 8 ? 8 : atoi(env) == 2 ? 2 : 4;
   if (const char *env = getenv("AFH_PROLONG_K"))
@@ -3028,34 +2884,23 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
   if (const char *env = getenv("AFH_CS_FUSED")) mg->cs_fused = atoi(env) != 0;
   if (const char *env = getenv("AFH_CS_ELEC_DIRECT")) mg->csd_on = atoi(env) != 0;
   if (const char *env = getenv("AFH_CS_DIRECT_SMALL")) mg->cs_direct_small = atoi(env) != 0;
-  if (const char *env = getenv("AFH_CS_DS_CELLS"))
-    mg->cs_ds_cells = std::min(CS_SMALL_CELLS, std::max(0, atoi(env)));
   if (const char *env = getenv("AFH_PAIR_PUSH")) mg->pair_push = atoi(env) != 0;
   if (const char *env = getenv("AFH_PROLONG_PUSH")) mg->prolong_push = atoi(env) != 0;
   if (const char *env = getenv("AFH_RSTR_PUSH")) mg->rstr_push = atoi(env) != 0;
-  if (const char *env = getenv("AFH_PAIR_XR")) mg->pair_xr = atoi(env) != 0;
-  if (const char *env = getenv("AFH_PROLONG_GX")) mg->prolong_gx = atoi(env) != 0;
-  if (const char *env = getenv("AFH_PAIR_TILES_MIN")) mg->tiles_min = atoi(env);
   AFH_HIP(hipMalloc(&mg->cs_iters, sizeof(int)));
   AFH_HIP(hipMalloc(&mg->d_cycles, sizeof(int)));
   if (const char *env = getenv("AFH_GSRB_PAIR_BOX")) mg->pair_box = atoi(env) != 0;
-  if (const char *env = getenv("AFH_GSRB_PAIR_KS")) mg->pair_ks = atoi(env);
-  if (const char *env = getenv("AFH_PAIR_KS_LEAF")) mg->pair_ks_leaf = atoi(env);
   if (const char *env = getenv("AFH_GRAD_NT")) mg->grad_nt = atoi(env) != 0;
-  if (const char *env = getenv("AFH_CS_WAVE_CELLS")) mg->wave_cells = atoi(env);
   if (fused_nc_ok(t->nc) && mg->fused_min > 0) {
     bool any = false;
     for (int l = 2; l <= t->nlvl; l++) any |= t->lvl_total[l - 1] >= mg->fused_min;
     if (any) {
       // one spare image per tree: the level fills after a pair fill t->alt
       if (!t->alt) {
-        // AFH_ALT_OFF: the spare image starts that many bytes into its
-        // allocation (placement experiments)
-        const size_t off = getenv("AFH_ALT_OFF") ? (size_t)atoll(getenv("AFH_ALT_OFF")) / 8 : 0;
         if (int32_t e2 = pool_alloc((void **)&t->alt_base,
-                                    ((size_t)t->nb * t->bsz + off) * sizeof(double), "alt"))
+                                    (size_t)t->nb * t->bsz * sizeof(double), "alt"))
           return e2;
-        t->alt = t->alt_base + off;
+        t->alt = t->alt_base;
         AFH_HIP(hipMemsetAsync(t->alt, 0, (size_t)t->nb * t->bsz * sizeof(double),
                                t->stream));
       }
@@ -3160,30 +3005,14 @@ static bool pair_tiles(const afh_mg *mg, int lvl) {
   return mg->t->nc >= 32 && (mg->force_tiles || n < mg->tiles_min);
 }
 
-// the whole-box pair of boxes of 16^3 and up stores the x ghost cells the
-// level fill would give (k_gsrb_pair2<..., XR>; the fill then skips them):
-// its default forms only (none of the AFH_GSRB_PAIR_* experiments), not on a
-// sharded tree (a replica's ghosts are its owner's)
-static bool pair2_xr(const afh_mg *mg, int lvl) {
-  const int nc = mg->t->nc;
-  if (!mg->pair_xr || mg->t->hook || mg->pair_v1 || nc < 16) return false;
-  if (nc == 16) return !mg->pair_box;
-  if (pair_tiles(mg, lvl)) return false;
-  if (nc == 32) return true;
-  return nc == 64 && mg->pair_tj == 0 && mg->pair_nt == 0 && mg->pair_depth == 1 &&
-         mg->pair_fr && mg->pair_sp && mg->pair_p3 && !mg->pair_ntl && mg->pair_ks_leaf == 1;
-}
-
-template <int NC, int TJ, int DEPTH, int NTM = 0, bool FR = true, bool P3 = true,
-          bool SP = true, int KS = 1, bool NTL = false, bool XR = false>
+template <int NC, int TJ, int DEPTH, int KS = 1>
 static void launch_pair2(afh_mg *mg, int lvl, const double *src, double *dst,
                          const Coef &cf, double inv_c1, hipEvent_t e0, hipEvent_t e1) {
   afh_tree *t = mg->t;
-  launch_ev((k_gsrb_pair2<NC, TJ, DEPTH, NTM, FR, P3, SP, KS, NTL, XR>), e0, e1,
-            dim3(t->ids.n(lvl) * RbPar<NC, TJ, NTM>::NTILE * KS),
-            dim3(RbPar<NC, TJ, NTM>::NT), t->stream, src, dst, t->ccv(mg->d.i_rhs),
-            t->ccv(mg->d.i_phi), t->d_boxes, t->ids.at(lvl), t->bsz, cf, inv_c1,
-            t->gc_args(mg->d.i_phi));
+  launch_ev((k_gsrb_pair2<NC, TJ, DEPTH, KS>), e0, e1,
+            dim3(t->ids.n(lvl) * RbPar<NC, TJ>::NTILE * KS), dim3(RbPar<NC, TJ>::NT),
+            t->stream, src, dst, t->ccv(mg->d.i_rhs), t->ccv(mg->d.i_phi), t->d_boxes,
+            t->ids.at(lvl), t->bsz, cf, inv_c1, t->gc_args(mg->d.i_phi));
 }
 
 // the small-box pair fills the level's faces itself (k_gsrb_pair_box PUSH)
@@ -3212,70 +3041,18 @@ static void launch_pair(afh_mg *mg, int lvl, const double *src, double *dst,
       return;
     }
   }
-  if constexpr (NC >= 16) {
-    if (pair2_xr(mg, lvl)) {
-      if constexpr (NC == 64)
-        return launch_pair2<NC, NC, 1, 0, true, true, true, 1, false, true>(mg, lvl, src, dst,
-                                                                            cf, inv_c1, e0, e1);
-      else
-        return launch_pair2<NC, NC, 2, 0, true, true, true, 1, false, true>(mg, lvl, src, dst,
-                                                                            cf, inv_c1, e0, e1);
-    }
-  }
   if constexpr (NC >= 32) {
     if (pair_tiles(mg, lvl)) {
-      if (mg->pair_v1) return launch_pair_t<NC, NC / 4>(mg, lvl, src, dst, cf, inv_c1, e0, e1);
-      if constexpr (NC == 64) {
-        // too few boxes for the chip: split the march over k
-        if (mg->pair_ks == 4)
-          return launch_pair2<NC, NC, 1, 0, true, true, true, 4>(mg, lvl, src, dst, cf,
-                                                                 inv_c1, e0, e1);
-        if (mg->pair_ks == 44)
-          return launch_pair2<NC, NC / 4, 1, 0, true, true, true, 4>(mg, lvl, src, dst, cf,
-                                                                     inv_c1, e0, e1);
-      }
+      // too few boxes for the chip: 64^3 splits the march over k, 32^3 runs
+      // quarter-box tiles
+      if constexpr (NC == 64)
+        return launch_pair2<NC, NC, 1, 4>(mg, lvl, src, dst, cf, inv_c1, e0, e1);
       return launch_pair2<NC, NC / 4, 2>(mg, lvl, src, dst, cf, inv_c1, e0, e1);
     }
   }
   if constexpr (NC >= 16) {
-    if (!mg->pair_v1) {
-      if constexpr (NC == 64) {
-        if (mg->pair_tj == 32)
-          return launch_pair2<NC, 32, 2>(mg, lvl, src, dst, cf, inv_c1, e0, e1);
-        if (mg->pair_nt == 512 && !mg->pair_sp)
-          return launch_pair2<NC, NC, 2, 512, true, true, false>(mg, lvl, src, dst, cf, inv_c1,
-                                                                 e0, e1);
-        if (mg->pair_nt == 512)
-          return launch_pair2<NC, NC, 2, 512>(mg, lvl, src, dst, cf, inv_c1, e0, e1);
-        if (mg->pair_depth == 2 && !mg->pair_sp)
-          return launch_pair2<NC, NC, 2, 0, true, true, false>(mg, lvl, src, dst, cf, inv_c1,
-                                                               e0, e1);
-        if (mg->pair_depth == 2)
-          return launch_pair2<NC, NC, 2>(mg, lvl, src, dst, cf, inv_c1, e0, e1);
-        if (!mg->pair_fr)
-          return launch_pair2<NC, NC, 1, 0, false>(mg, lvl, src, dst, cf, inv_c1, e0, e1);
-        if (!mg->pair_sp)
-          return launch_pair2<NC, NC, 1, 0, true, true, false>(mg, lvl, src, dst, cf, inv_c1,
-                                                               e0, e1);
-        if (!mg->pair_p3)
-          return launch_pair2<NC, NC, 1, 0, true, false>(mg, lvl, src, dst, cf, inv_c1, e0,
-                                                         e1);
-        if (mg->pair_ntl)
-          return launch_pair2<NC, NC, 1, 0, true, true, true, 1, true>(mg, lvl, src, dst, cf,
-                                                                       inv_c1, e0, e1);
-        // AFH_PAIR_KS_LEAF=2|4: the k-split march on the leaf level too
-        // (workgroups of one box start at different planes: an experiment
-        // on the placement sensitivity of the lock-stepped plane streams)
-        if (mg->pair_ks_leaf == 2)
-          return launch_pair2<NC, NC, 1, 0, true, true, true, 2>(mg, lvl, src, dst, cf,
-                                                                 inv_c1, e0, e1);
-        if (mg->pair_ks_leaf == 4)
-          return launch_pair2<NC, NC, 1, 0, true, true, true, 4>(mg, lvl, src, dst, cf,
-                                                                 inv_c1, e0, e1);
-        return launch_pair2<NC, NC, 1>(mg, lvl, src, dst, cf, inv_c1, e0, e1);
-      }
-      return launch_pair2<NC, NC, 2>(mg, lvl, src, dst, cf, inv_c1, e0, e1);
-    }
+    if constexpr (NC == 64) return launch_pair2<NC, NC, 1>(mg, lvl, src, dst, cf, inv_c1, e0, e1);
+    return launch_pair2<NC, NC, 2>(mg, lvl, src, dst, cf, inv_c1, e0, e1);
   }
   launch_pair_t<NC, NC>(mg, lvl, src, dst, cf, inv_c1, e0, e1);
 }
@@ -3421,8 +3198,7 @@ static int32_t gsrb_boxes(afh_mg *mg, int lvl, bool up, bool stale_ghosts = fals
       // the pair filled the faces; edges and corners on the leg's last pair
       if (up && n == n_cycle)
         if (int32_t e = gc_lvl_corners(t, lvl, dst_iv)) return e;
-    } else if (int32_t e = gc_lvl_var(t, lvl, dst_iv, phi, ga, up && n == n_cycle, true,
-                                      pair2_xr(mg, lvl))) {
+    } else if (int32_t e = gc_lvl_var(t, lvl, dst_iv, phi, ga, up && n == n_cycle, true)) {
       return e;
     }
   }
@@ -3548,13 +3324,6 @@ static bool prolong_push(const afh_mg *mg, int lvl) {
          fused_level(mg, lvl);
 }
 
-// the correction of a level smoothed by the XR pair also corrects the x
-// ghost cells facing same-level neighbours (k_prolong<4, GX>); the fill
-// after it skips them (AFH_PROLONG_GX=0: off)
-static bool prolong_gx(const afh_mg *mg, int lvl) {
-  return mg->prolong_gx && !mg->any_var && fused_level(mg, lvl) && pair2_xr(mg, lvl);
-}
-
 static int32_t correct_children(afh_mg *mg, int lvl) {
   afh_tree *t = mg->t;
   const int np = t->parents.n(lvl - 1), nc = t->nc;
@@ -3587,13 +3356,6 @@ static int32_t correct_children(afh_mg *mg, int lvl) {
     const int want = mg->prolong_k;
     const int K = want == 8 && nc % 8 == 0 ? 8 : want >= 4 && nc % 4 == 0 ? 4 : 2;
     const dim3 grid((nc * nc * (nc / K) + 255) / 256, nid);
-    if (K == 4 && prolong_gx(mg, lvl)) {
-      hipLaunchKernelGGL((k_prolong<4, true>), dim3(((nc + 2) * nc * (nc / 4) + 255) / 256, nid),
-                         dim3(256), 0, t->stream, t->ccv(mg->d.i_phi), t->ccv(mg->d.i_tmp),
-                         t->d_boxes, t->ids.at(lvl), nc, t->bsz);
-      AFH_LAUNCH_CHECK("k_prolong");
-      return AFH_OK;
-    }
     if (K == 8)
       hipLaunchKernelGGL(k_prolong<8>, grid, dim3(256), 0, t->stream,
                          t->ccv(mg->d.i_phi), t->ccv(mg->d.i_tmp), t->d_boxes,
@@ -4302,7 +4064,7 @@ static int32_t vcycle_body(afh_mg *mg, int32_t set_residual, int max_lvl, bool m
     // edges or corners: k_gc_corners follows the leg's last pair)
     if (!prolong_push(mg, lvl) &&
         (e = gc_lvl_var(t, lvl, mg->d.i_phi, t->ccv(mg->d.i_phi), t->gc_args(mg->d.i_phi), 1,
-                        fused_level(mg, lvl), prolong_gx(mg, lvl))))
+                        fused_level(mg, lvl))))
       return e;
     if ((e = gsrb_boxes(mg, lvl, true))) return e;
   }

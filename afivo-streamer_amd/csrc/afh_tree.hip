@@ -35,25 +35,9 @@ int32_t check_hip(hipError_t e, const char *what) {
 }
 
 int32_t pool_alloc(void **p, size_t bytes, const char *what) {
-  static const bool contig = getenv("AFH_POOL_CONTIG") && atoi(getenv("AFH_POOL_CONTIG"));
-  static const bool log = getenv("AFH_LOG_POOLS") && atoi(getenv("AFH_LOG_POOLS"));
-  bool got_contig = false;
+  (void)what;
   *p = nullptr;
-  if (contig) {
-    if (hipExtMallocWithFlags(p, bytes, hipDeviceMallocContiguous) == hipSuccess) {
-      got_contig = true;
-    } else {
-      (void)hipGetLastError();
-      *p = nullptr;
-    }
-  }
-  if (!*p) AFH_HIP(hipMalloc(p, bytes));
-  if (log) {
-    const uintptr_t a = (uintptr_t)*p;
-    fprintf(stderr, "afh_pool %s %p bytes %zu mod4K %zu mod64K %zu mod2M %zu contig %d\n",
-            what, *p, bytes, (size_t)(a & 4095), (size_t)(a & 65535),
-            (size_t)(a & ((1u << 21) - 1)), (int)got_contig);
-  }
+  AFH_HIP(hipMalloc(p, bytes));
   return AFH_OK;
 }
 
@@ -97,7 +81,7 @@ __global__ void k_gc_faces(double *__restrict__ v,
                            const double *__restrict__ vc,
                            const afh_box_meta *__restrict__ meta,
                            const int32_t *__restrict__ ids, int nc, size_t bsz,
-                           GcArgs ga, int xpair, int xrim) {
+                           GcArgs ga) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= nc * nc) return;
   const int id = ids[blockIdx.z];
@@ -124,26 +108,6 @@ __global__ void k_gc_faces(double *__restrict__ v,
   const size_t dst = ix3(ng, p[0], p[1], p[2]);
 
   if (nb_id > 0) {
-    // xrim: the pair stored this x ghost cell (gc_lvl_var)
-    if (xrim && d == 0 && a != 1 && a != nc && b != 1 && b != nc) return;
-    if (xpair && d == 0 && meta[nb_id - 1].lvl > 0) {
-      // x interface with a stored same-level box, copied both ways by the
-      // low-x thread of the box on its high side: its own ghost (0, a, b)
-      // and the neighbour's ghost (nc+1, a, b) sit in the lines of the two
-      // interior values it reads (row start of this box, row end of the
-      // neighbour), so each line is read once and written back once instead
-      // of being fetched by two faces. (The sentinel id of a sharded tree,
-      // level 0, stands for boxes the rank does not store: never written.)
-      // xpair: ids is every stored box of the level (a whole-level fill),
-      // so every such interface has its low-x thread in the launch
-      if (!low) return;  // the neighbour's low-x thread copies this one
-      double *cn = v + (size_t)(nb_id - 1) * bsz;
-      const size_t sa = ix3(ng, nc, a, b), sb = ix3(ng, 1, a, b);
-      const double va = cn[sa], vb = c[sb];
-      c[dst] = va;
-      cn[sa + 1] = vb;
-      return;
-    }
     // copy_from_nb: ghost(lo) = neighbor(lo - dnb * nc)
     int q[3] = {p[0], p[1], p[2]};
     q[d] = low ? nc : 1;
@@ -156,108 +120,6 @@ __global__ void k_gc_faces(double *__restrict__ v,
                           });
 }
 
-// k_gc_faces with R ghost values per thread ((a, b .. b+R-1) of one face):
-// the R source values (a neighbour's boundary cells, or gc_face_nocopy's
-// boundary / refinement values) are loaded before the R stores. One value per
-// thread leaves a 64^3 leaf fill latency-bound (49 152 workgroups of one
-// dependent load each); this form has R times fewer. Same values as
-// k_gc_faces (xrim as there; no x-interface pairing).
-template <int R>
-__global__ void __launch_bounds__(256)
-    k_gc_faces_r(double *__restrict__ v, const double *__restrict__ vc,
-                 const afh_box_meta *__restrict__ meta, const int32_t *__restrict__ ids, int nc,
-                 size_t bsz, GcArgs ga, int xrim) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= nc * (nc / R)) return;
-  const int id = ids[blockIdx.z];
-  const int nb = blockIdx.y + 1;
-  const int d = (nb - 1) >> 1;
-  const bool low = ((nb - 1) & 1) == 0;
-  const int ta = (d == 0) ? 1 : 0, tb = (d == 2) ? 1 : 2;
-  const int a = t % nc + 1, b0 = (t / nc) * R + 1;
-  const int ng = nc + 2;
-  const afh_box_meta &m = meta[id - 1];
-  double *c = v + (size_t)(id - 1) * bsz;
-  const int nb_id = m.neighbors[nb - 1];
-  double val[R];
-  size_t dst[R];
-  bool on[R];
-#pragma unroll
-  for (int q = 0; q < R; q++) {
-    const int b = b0 + q;
-    int p[3];
-    p[ta] = a;
-    p[tb] = b;
-    p[d] = low ? 0 : nc + 1;
-    dst[q] = ix3(ng, p[0], p[1], p[2]);
-    on[q] = true;
-    if (nb_id > 0) {
-      if (xrim && d == 0 && a != 1 && a != nc && b != 1 && b != nc) {
-        on[q] = false;
-        val[q] = 0.0;
-        continue;
-      }
-      int s[3] = {p[0], p[1], p[2]};
-      s[d] = low ? nc : 1;
-      val[q] = v[(size_t)(nb_id - 1) * bsz + ix3(ng, s[0], s[1], s[2])];
-    } else {
-      val[q] = gc_face_nocopy(vc, meta, m, nb, p, a, b, nc, bsz, ga.bc[nb - 1], ga.rb,
-                              [&](const int *qq) { return c[ix3(ng, qq[0], qq[1], qq[2])]; });
-    }
-  }
-#pragma unroll
-  for (int q = 0; q < R; q++)
-    if (on[q]) c[dst[q]] = val[q];
-}
-
-// The six faces of a box by one thread per (a, b): the six ghost values are
-// loaded (neighbour copies, or gc_face_nocopy's boundary / refinement
-// values, which read only interior and coarse cells) before the six stores,
-// six independent chains per thread instead of one. Same values as
-// k_gc_faces.
-__global__ void __launch_bounds__(256)
-    k_gc_faces6(double *__restrict__ v, const double *__restrict__ vc,
-                const afh_box_meta *__restrict__ meta, const int32_t *__restrict__ ids,
-                int nc, size_t bsz, GcArgs ga) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= nc * nc) return;
-  const int id = ids[blockIdx.y];
-  int a, b;
-  if ((nc & (nc - 1)) == 0) {
-    a = (t & (nc - 1)) + 1;
-    b = (t >> __builtin_ctz(nc)) + 1;
-  } else {
-    a = t % nc + 1;
-    b = t / nc + 1;
-  }
-  const int ng = nc + 2;
-  const afh_box_meta &m = meta[id - 1];
-  double *c = v + (size_t)(id - 1) * bsz;
-  double val[6];
-  size_t dst[6];
-#pragma unroll
-  for (int nb = 1; nb <= 6; nb++) {
-    const int d = (nb - 1) >> 1;
-    const bool low = ((nb - 1) & 1) == 0;
-    const int ta = (d == 0) ? 1 : 0, tb = (d == 2) ? 1 : 2;
-    int p[3];
-    p[ta] = a;
-    p[tb] = b;
-    p[d] = low ? 0 : nc + 1;
-    dst[nb - 1] = ix3(ng, p[0], p[1], p[2]);
-    const int nb_id = m.neighbors[nb - 1];
-    if (nb_id > 0) {
-      int q[3] = {p[0], p[1], p[2]};
-      q[d] = low ? nc : 1;
-      val[nb - 1] = v[(size_t)(nb_id - 1) * bsz + ix3(ng, q[0], q[1], q[2])];
-    } else {
-      val[nb - 1] = gc_face_nocopy(vc, meta, m, nb, p, a, b, nc, bsz, ga.bc[nb - 1], ga.rb,
-                                   [&](const int *q) { return c[ix3(ng, q[0], q[1], q[2])]; });
-    }
-  }
-#pragma unroll
-  for (int nb = 0; nb < 6; nb++) c[dst[nb]] = val[nb];
-}
 
 // ------------------------------------------------------------ edges+corners
 __constant__ int c_edge_dim[12] = {0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2};
@@ -449,7 +311,7 @@ int32_t call_hook(afh_tree *t, int kind, int lvl, int iv, double *vals, int n) {
 }
 
 int32_t gc_lvl_var(afh_tree *t, int lvl, int iv, const double *vc,
-                   const GcArgs &ga, int corners, bool rims, bool xrim) {
+                   const GcArgs &ga, int corners, bool rims) {
   const int n = t->ids.n(lvl);
   double *v = t->var(iv);
   int32_t e;
@@ -457,7 +319,8 @@ int32_t gc_lvl_var(afh_tree *t, int lvl, int iv, const double *vc,
   if (n > 0) {
     const int nc = t->nc;
     prof_begin(t, AFH_PROF_GHOST);
-    if (t->gc_box && !xrim && (nc == 4 || nc == 8 || nc == 16)) {
+    if (nc == 4 || nc == 8 || nc == 16) {
+      // small boxes: faces, then edges and corners, one workgroup per box
       const int cr = corners ? 1 : 0;
       if (nc == 4)
         hipLaunchKernelGGL(k_gc_box<4>, dim3(n), dim3(16), 0, t->stream, v, vc, t->d_boxes,
@@ -471,17 +334,8 @@ int32_t gc_lvl_var(afh_tree *t, int lvl, int iv, const double *vc,
       prof_end(t, AFH_PROF_GHOST, 16.0 * 6 * nc * nc * n);
       AFH_LAUNCH_CHECK("k_gc_box");
     } else {
-      if (!xrim && (t->gc_faces6 == 1 || (t->gc_faces6 < 0 && nc <= 16)))
-        hipLaunchKernelGGL(k_gc_faces6, dim3((nc * nc + 255) / 256, n), dim3(256), 0,
-                           t->stream, v, vc, t->d_boxes, t->ids.at(lvl), nc, t->bsz, ga);
-      else if (t->gc_faces_r > 1 && nc >= 32 && !t->gc_xpair)
-        hipLaunchKernelGGL(k_gc_faces_r<8>, dim3((nc * (nc / 8) + 255) / 256, 6, n), dim3(256),
-                           0, t->stream, v, vc, t->d_boxes, t->ids.at(lvl), nc, t->bsz, ga,
-                           xrim ? 1 : 0);
-      else
-        hipLaunchKernelGGL(k_gc_faces, dim3((nc * nc + 255) / 256, 6, n), dim3(256), 0,
-                           t->stream, v, vc, t->d_boxes, t->ids.at(lvl), nc, t->bsz, ga,
-                           t->gc_xpair, xrim ? 1 : 0);
+      hipLaunchKernelGGL(k_gc_faces, dim3((nc * nc + 255) / 256, 6, n), dim3(256), 0,
+                         t->stream, v, vc, t->d_boxes, t->ids.at(lvl), nc, t->bsz, ga);
       // algorithmic bytes: read one interior layer + write one ghost layer
       prof_end(t, AFH_PROF_GHOST, 16.0 * 6 * nc * nc * n);
       AFH_LAUNCH_CHECK("k_gc_faces");
@@ -922,12 +776,7 @@ static int32_t tree_create_impl(const afh_tree_desc *d, int32_t device,
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1)
     return set_error(AFH_ERR_DEVICE, "no HIP device available");
   afh_tree *t = new afh_tree();
-  if (const char *env = getenv("AFH_GC_BOX")) t->gc_box = atoi(env) != 0;
   if (const char *env = getenv("AFH_ALL_LVL")) t->all_lvl_launch = atoi(env) != 0;
-  if (const char *env = getenv("AFH_GC_FACES6")) t->gc_faces6 = atoi(env) != 0;
-  else t->gc_faces6 = -1;  // by box size
-  if (const char *env = getenv("AFH_GC_XPAIR")) t->gc_xpair = atoi(env) != 0;
-  if (const char *env = getenv("AFH_GC_FACES_R")) t->gc_faces_r = atoi(env);
   if (device >= 0) {
     AFH_HIP(hipSetDevice(device));
     t->device = device;
@@ -1036,10 +885,7 @@ static int32_t tree_create_impl(const afh_tree_desc *d, int32_t device,
     adopt->cc = adopt->fc = adopt->gc2 = nullptr;
     adopt->retired = true;
   } else {
-    // AFH_POOL_PAD: bytes between cc variables (placement experiments:
-    // the relative offsets of the streams a kernel reads in HBM)
-    const size_t pad = getenv("AFH_POOL_PAD") ? (size_t)atoll(getenv("AFH_POOL_PAD")) / 8 : 0;
-    t->vstride = (size_t)t->cap * t->bsz + pad;
+    t->vstride = (size_t)t->cap * t->bsz;
     size_t ncc = (size_t)t->nvc * t->vstride;
     size_t nfc = (size_t)std::max(1, t->nvf) * t->cap * t->fsz;
     if (int32_t e2 = pool_alloc((void **)&t->cc, ncc * sizeof(double), "cc")) return e2;
@@ -1605,7 +1451,7 @@ int32_t afh_tree_regrid(afh_tree *o, const afh_tree_desc *d, afh_tree **out) {
     for (int iv : t->auto_vars) {
       hipLaunchKernelGGL(k_gc_faces, dim3((nc * nc + 255) / 256, 6, n), dim3(256), 0,
                          t->stream, t->ccv(iv), t->ccv(iv), t->d_boxes, d_list, nc,
-                         t->bsz, t->gc_args(iv), 0, 0);  // new boxes only: no pairing
+                         t->bsz, t->gc_args(iv));
       AFH_LAUNCH_CHECK("k_gc_faces");
       hipLaunchKernelGGL(k_gc_corners, dim3(n), dim3(fit_blk(12 * nc)), 0, t->stream, t->ccv(iv),
                          t->d_boxes, d_list, nc, t->bsz);

@@ -60,6 +60,10 @@ CONFIGS = {
     # builds (tests/golden/case_s2d.npz, exported from the reference's own
     # initializers)
     "2d": (8, None, None, (32e-3, 32e-3)),
+    # a uniform 2-D tree with config 1's box size and domain (8 levels of 8^2
+    # boxes, 1024^2 cells, the old-style 3-species model): the 2-D tests'
+    # synthetic workload
+    "2d-uniform": (8, (8, 8), 8, (32e-3, 32e-3)),
 }
 DRIVER_CONFIGS = ("s3", "s4", "s5", "2d")
 DRIVER_FIXTURE = {"s3": "case_s3", "s4": "case_s4", "s5": "case_s5", "2d": "case_s2d"}
@@ -71,6 +75,14 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E peak (spec)
 # separable solve
 COARSE = {"pfmg": dict(coarse_cycles=50, coarse_tol=1e-6, coarse_mode=3),
           "direct": dict(coarse_cycles=0, coarse_tol=0.0, coarse_mode=None)}
+
+
+def coarse_kw(coarse):
+    """Level-1 solve keywords: "pfmg" / "direct", or an int (the tests'
+    form): 0 = the exact solve, N > 0 = N of our MG cycles."""
+    if isinstance(coarse, str):
+        return COARSE[coarse]
+    return dict(coarse_cycles=int(coarse)) if coarse else COARSE["direct"]
 
 
 def coarse_choice(arg, config):
@@ -110,7 +122,7 @@ def build_case(lib, config, device, coarse, shard_ranks=None, shard=None):
             from afh.dist import Partition, Shard
             shard = Shard(Partition(topo, world), rank, "nccl", device="cuda:%d" % device)
     case = StreamerCase(lib, topo, td, chem, voltage, device=device, shard=shard,
-                        **COARSE[coarse])
+                        **coarse_kw(coarse))
     seed_state(case, width=0.05 * dom[-1])
     return case
 
@@ -195,7 +207,7 @@ def build_driver_case(lib, device, config="s3", coarse="pfmg", grow_cells=0,
     from afh.driver import Simulation
     from afh.users import USERS
     sim = Simulation(lib, golden.load(DRIVER_FIXTURE[config]), device=device,
-                     user=USERS.get(config), **COARSE[coarse])
+                     user=USERS.get(config), **coarse_kw(coarse))
     sim.set_initial_conditions()
     sim.grown = {"steps": 0, "time_s": 0.0, "leaf_cells_initial": sim.af.n_leaf_cells()}
     if grow_cells:
@@ -242,7 +254,7 @@ def cpu_baseline(config, coarse, steps=2):
     g = golden.load("uni8")
     td, chem = tables_from(g)
     lib = capi.oracle_library()
-    case = StreamerCase(lib, topo, td, chem, -dom[2] * (-2.5e6), **COARSE[coarse])
+    case = StreamerCase(lib, topo, td, chem, -dom[2] * (-2.5e6), **coarse_kw(coarse))
     seed_state(case, width=0.05 * dom[2])
     unit_step(case, 1e-13, 0)
     unit_step(case, 1e-13, 1)

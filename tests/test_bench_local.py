@@ -93,7 +93,7 @@ def test_bench_local_json():
     import argparse
     args = argparse.Namespace(gpus=4, config="s5", steps=2, warmup=1, oracle=False,
                               shared_stream=True, no_fused_rhs=False,
-                              stored_face_field=False)
+                              stored_face_field=False, grow_cells=0)
     out = bench.bench_local(args, bench.coarse_choice("auto", "s5"))
     assert out["n_ranks"] == 4 and out["value"] > 0
     assert len(out["owned_leaf_cells"]) == 4 and min(out["owned_leaf_cells"]) > 0

@@ -117,6 +117,6 @@ def test_unit_step_deferred_2d(monkeypatch):
     """The 2-D build's deferred entry points (round 4) on config 1's bench
     tree: residuals, limits and every variable bitwise the immediate reads."""
     lib = capi.hip_library_2d()
-    a = _unit_steps(lib, monkeypatch, True, "2d", 0)
-    _same(a, _unit_steps(lib, monkeypatch, False, "2d", 0))
+    a = _unit_steps(lib, monkeypatch, True, "2d-uniform", 0)
+    _same(a, _unit_steps(lib, monkeypatch, False, "2d-uniform", 0))
     assert all(len(res) == 1 for res, _ in a[0][2::2])
