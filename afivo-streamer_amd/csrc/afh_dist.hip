@@ -52,13 +52,15 @@ struct afh_dist {
   int rank = 0, n = 1, transport = 0, device = 0;
   afh_dist_group *group = nullptr;
   ncclComm_t comm = nullptr;
-  struct Side {
-    int32_t plan = -1;
-    int64_t n = 0;
-    double *buf = nullptr;
-  };
+  // One exchange: the regions this rank sends to every peer as ONE plan
+  // (packed by one launch into one buffer, peer q's values at send_off[q]),
+  // the regions it receives likewise (one unpack launch) -- instead of a
+  // pack and an unpack launch per peer (round 5: 1586 plan-copy launches
+  // per S5 step on 8 ranks, profiles/r05_scaling_*.json)
   struct Plan {
-    std::vector<Side> send, recv;  // per peer
+    int32_t send_plan = -1, recv_plan = -1;
+    double *send_buf = nullptr, *recv_buf = nullptr;
+    std::vector<int64_t> send_off, send_n, recv_off, recv_n;  // per peer
   };
   std::map<std::pair<int, int>, Plan> plans;  // (hook kind, level)
   double *d_red = nullptr;
@@ -75,8 +77,7 @@ int32_t exchange(afh_dist *d, const Key &key, int iv) {
   const afh_dist::Plan &p = it->second;
   afh_tree *t = d->t;
   int32_t e = AFH_OK;
-  for (int q = 0; q < d->n && !e; q++)
-    if (p.send[q].n) e = afh_plan_pack(t, p.send[q].plan, iv, p.send[q].buf);
+  if (p.send_plan >= 0) e = afh_plan_pack(t, p.send_plan, iv, p.send_buf);
   if (d->transport == AFH_DIST_RCCL) {
     // the grouped send/recv is posted even after a failed pack (the buffer
     // then carries stale values), so the peers' matching calls complete and
@@ -84,11 +85,12 @@ int32_t exchange(afh_dist *d, const Key &key, int iv) {
     const int32_t e_pack = e;
     bool posted = ncclGroupStart() == ncclSuccess;
     for (int q = 0; q < d->n && posted; q++) {
-      if (p.send[q].n &&
-          ncclSend(p.send[q].buf, p.send[q].n, ncclDouble, q, d->comm, t->stream) != ncclSuccess)
+      if (p.send_n[q] && ncclSend(p.send_buf + p.send_off[q], p.send_n[q], ncclDouble, q,
+                                  d->comm, t->stream) != ncclSuccess)
         posted = false;
-      if (posted && p.recv[q].n &&
-          ncclRecv(p.recv[q].buf, p.recv[q].n, ncclDouble, q, d->comm, t->stream) != ncclSuccess)
+      if (posted && p.recv_n[q] &&
+          ncclRecv(p.recv_buf + p.recv_off[q], p.recv_n[q], ncclDouble, q, d->comm,
+                   t->stream) != ncclSuccess)
         posted = false;
     }
     if (ncclGroupEnd() != ncclSuccess) posted = false;
@@ -105,15 +107,17 @@ int32_t exchange(afh_dist *d, const Key &key, int iv) {
       e = set_error(AFH_ERR_DEVICE, "stream sync");
     d->group->bar.wait();
     for (int q = 0; q < d->n && !e; q++) {
-      if (!p.recv[q].n) continue;
+      if (!p.recv_n[q]) continue;
       const afh_dist *peer = d->group->rank[q];
-      const afh_dist::Side &src = peer->plans.at(key).send[d->rank];
-      if (src.n != p.recv[q].n)
+      const afh_dist::Plan &src = peer->plans.at(key);
+      const int64_t n = src.send_n[d->rank];
+      if (n != p.recv_n[q])
         e = set_error(AFH_ERR_STATE, "exchange %d/%d: rank %d sends %lld values, rank %d "
-                      "expects %lld", key.first, key.second, q, (long long)src.n, d->rank,
-                      (long long)p.recv[q].n);
-      else if (hipMemcpyPeerAsync(p.recv[q].buf, d->device, src.buf, peer->device,
-                                  sizeof(double) * src.n, t->stream) != hipSuccess)
+                      "expects %lld", key.first, key.second, q, (long long)n, d->rank,
+                      (long long)p.recv_n[q]);
+      else if (hipMemcpyPeerAsync(p.recv_buf + p.recv_off[q], d->device,
+                                  src.send_buf + src.send_off[d->rank], peer->device,
+                                  sizeof(double) * n, t->stream) != hipSuccess)
         e = set_error(AFH_ERR_DEVICE, "peer copy");
     }
     if (!e && hipStreamSynchronize(t->stream) != hipSuccess)
@@ -121,11 +125,10 @@ int32_t exchange(afh_dist *d, const Key &key, int iv) {
     d->group->bar.wait();
     if (e) return e;
   }
-  for (int q = 0; q < d->n && !e; q++)
-    if (p.recv[q].n) e = afh_plan_unpack(t, p.recv[q].plan, iv, p.recv[q].buf);
+  if (p.recv_plan >= 0) e = afh_plan_unpack(t, p.recv_plan, iv, p.recv_buf);
   if (e) return e;
   d->n_exchanges++;
-  for (int q = 0; q < d->n; q++) d->bytes += 8 * (p.send[q].n + p.recv[q].n);
+  for (int q = 0; q < d->n; q++) d->bytes += 8 * (p.send_n[q] + p.recv_n[q]);
   return AFH_OK;
 }
 
@@ -339,26 +342,42 @@ int32_t afh_dist_create(afh_tree *t, const afh_tree_desc *desc, const int32_t *o
   }
   auto add = [&](int kind, int level) -> int32_t {
     afh_dist::Plan p;
-    p.send.resize(n_ranks), p.recv.resize(n_ranks);
+    p.send_off.assign(n_ranks, 0), p.send_n.assign(n_ranks, 0);
+    p.recv_off.assign(n_ranks, 0), p.recv_n.assign(n_ranks, 0);
     const bool fc = kind == AFH_HOOK_CFLUX;
-    for (int q = 0; q < n_ranks; q++) {
-      if (q == rank) continue;
-      for (int side = 0; side < 2; side++) {
+    const int w = fc ? 8 : 7, lo = fc ? 2 : 1;
+    for (int side = 0; side < 2; side++) {
+      // the regions of every peer, peer after peer, in one plan
+      std::vector<int32_t> flat;
+      int64_t total = 0;
+      std::vector<int64_t> &off = side == 0 ? p.send_off : p.recv_off;
+      std::vector<int64_t> &cnt = side == 0 ? p.send_n : p.recv_n;
+      for (int q = 0; q < n_ranks; q++) {
+        off[q] = total;
+        if (q == rank) continue;
         const auto rs = side == 0 ? plan_regions(tp, own, lp, kind, level, q, rank)
                                   : plan_regions(tp, own, lp, kind, level, rank, q);
-        afh_dist::Side &sd = side == 0 ? p.send[q] : p.recv[q];
-        if (rs.empty()) continue;
-        std::vector<int32_t> flat;
         for (const Region &r : rs) {
-          flat.insert(flat.end(), r.begin(), r.begin() + (fc ? 8 : 7));
-          flat[flat.size() - (fc ? 8 : 7)] = g2l[r[0]];
+          flat.insert(flat.end(), r.begin(), r.begin() + w);
+          flat[flat.size() - w] = g2l[r[0]];
+          int64_t cells = 1;
+          for (int dd = 0; dd < 3; dd++) cells *= r[lo + 3 + dd] - r[lo + dd] + 1;
+          cnt[q] += cells;
         }
-        int32_t e = fc ? afh_plan_create_fc(t, flat.data(), (int32_t)rs.size(), &sd.plan, &sd.n)
-                       : afh_plan_create(t, flat.data(), (int32_t)rs.size(), &sd.plan, &sd.n);
-        if (e) return e;
-        if (sd.n && hipMalloc(&sd.buf, sizeof(double) * sd.n) != hipSuccess)
-          return set_error(AFH_ERR_DEVICE, "exchange buffer");
+        total += cnt[q];
       }
+      if (flat.empty()) continue;
+      int32_t &plan = side == 0 ? p.send_plan : p.recv_plan;
+      double *&buf = side == 0 ? p.send_buf : p.recv_buf;
+      int64_t n = 0;
+      const int32_t nr = (int32_t)(flat.size() / w);
+      int32_t e = fc ? afh_plan_create_fc(t, flat.data(), nr, &plan, &n)
+                     : afh_plan_create(t, flat.data(), nr, &plan, &n);
+      if (e) return e;
+      if (n != total) return set_error(AFH_ERR_STATE, "exchange plan: %lld != %lld values",
+                                       (long long)n, (long long)total);
+      if (n && hipMalloc(&buf, sizeof(double) * n) != hipSuccess)
+        return set_error(AFH_ERR_DEVICE, "exchange buffer");
     }
     d->plans[Key(kind, level)] = std::move(p);
     return AFH_OK;
@@ -391,9 +410,10 @@ int32_t afh_dist_destroy(afh_dist *d) {
     d->t->dev_reduce = nullptr;
   }
   if (d->t) hipStreamSynchronize(d->t->stream);
-  for (auto &kv : d->plans)
-    for (auto *v : {&kv.second.send, &kv.second.recv})
-      for (auto &sd : *v) hipFree(sd.buf);
+  for (auto &kv : d->plans) {
+    hipFree(kv.second.send_buf);
+    hipFree(kv.second.recv_buf);
+  }
   hipFree(d->d_red);
   if (d->group && d->group->rank[d->rank] == d) d->group->rank[d->rank] = nullptr;
   delete d;

@@ -11,7 +11,8 @@ Inputs, per configuration (scripts/scaling_runs.sh makes them on the GPU box):
          run one at a time and each kernel's duration is its own) and its
          kernel trace.
 Per rank (host thread that launched the kernels) the kernel busy time inside
-the timed window, per step: b_r. With the N = 1 run's busy time b_1 and wall
+the timed window, per step: b_r (the peer-copy blits of the thread ranks
+excluded: they stand in for the RCCL transfer, priced by alpha and beta). With the N = 1 run's busy time b_1 and wall
 time T_1, the launch / host overhead ratio rho = T_1 / b_1. The projected
 step time of N GPUs, one rank each:
 
@@ -36,8 +37,10 @@ ALPHA_S = 15e-6
 BETA_BS = 64e9
 
 
-def busy_by_thread(trace, window):
-    """Kernel time per launching host thread inside [t0, t1] (ns)."""
+def busy_by_thread(trace, window, kernels=None):
+    """Kernel time per launching host thread inside [t0, t1] (ns); with
+    kernels (a dict), also per thread the time and launches per kernel name
+    (template arguments cut)."""
     t0, t1 = window
     out = {}
     with open(trace) as f:
@@ -45,22 +48,41 @@ def busy_by_thread(trace, window):
             s, e = int(row["Start_Timestamp"]), int(row["End_Timestamp"])
             if s < t0 or e > t1:
                 continue
+            # the thread ranks' peer copies stand in for the RCCL transfer,
+            # which the model prices separately (alpha, beta)
+            if row["Kernel_Name"].startswith("__amd_rocclr_copyBuffer"):
+                continue
             tid = row.get("Thread_Id", "0")
             out[tid] = out.get(tid, 0) + (e - s)
+            if kernels is not None:
+                name = row["Kernel_Name"].split("(")[0]
+                k = kernels.setdefault(tid, {}).setdefault(name, [0, 0])
+                k[0] += e - s
+                k[1] += 1
     return out
+
+
+def top_kernels(per_kernel, steps, n=12):
+    """The n kernels of most time: (name, ms per step, launches per step)."""
+    items = sorted(per_kernel.items(), key=lambda kv: -kv[1][0])[:n]
+    return [(k, round(v[0] / steps * 1e-6, 4), round(v[1] / steps, 1)) for k, v in items]
 
 
 def main(config, d, out_path):
     n1 = json.load(open(os.path.join(d, "n1.json")))
     steps1 = n1["steps"]
-    b1 = busy_by_thread(os.path.join(d, "n1_trace.csv"), n1["window_ns"])
+    k1 = {}
+    b1 = busy_by_thread(os.path.join(d, "n1_trace.csv"), n1["window_ns"], k1)
     busy1 = sum(b1.values()) / steps1 * 1e-9
     T1 = n1["ms_per_step"] * 1e-3
     rho = T1 / busy1 if busy1 > 0 else 1.0
     res = {"config": config, "label": "projection, not measured",
            "model": "T_N = rho * max_r busy_r + E_N * alpha + max_r bytes_r / beta",
            "alpha_s": ALPHA_S, "beta_Bps": BETA_BS,
-           "n1": {"ms_per_step": T1 * 1e3, "kernel_busy_ms": busy1 * 1e3, "rho": rho},
+           "n1": {"ms_per_step": T1 * 1e3, "kernel_busy_ms": busy1 * 1e3, "rho": rho,
+                  "top_kernels": top_kernels(max(k1.values(), key=lambda v: sum(x[0] for x in
+                                                                                 v.values())),
+                                             steps1)},
            "ranks": {}}
     for path in sorted(glob.glob(os.path.join(d, "n*.json"))):
         name = os.path.basename(path)[:-5]
@@ -68,7 +90,9 @@ def main(config, d, out_path):
             continue
         j = json.load(open(path))
         n = j["n_ranks"]
-        b = busy_by_thread(os.path.join(d, name + "_trace.csv"), j["window_ns"])
+        kk = {}
+        b = busy_by_thread(os.path.join(d, name + "_trace.csv"), j["window_ns"], kk)
+        busiest = max(b, key=b.get)
         per = sorted((v / j["steps"] * 1e-9 for v in b.values()), reverse=True)[:n]
         E = max(j["exchanges_per_step"])
         B = max(j["exchange_bytes_per_step"])
@@ -83,6 +107,7 @@ def main(config, d, out_path):
             "exchange_latency_ms": E * ALPHA_S * 1e3,
             "exchange_bw_ms": B / BETA_BS * 1e3,
             "projected_speedup": T1 / TN,
+            "busiest_rank_top_kernels": top_kernels(kk[busiest], j["steps"]),
         }
     with open(out_path, "w") as f:
         json.dump(res, f, indent=1)

@@ -26,6 +26,9 @@ for CFG in $CFGS; do
   done
   rm -rf $D/prof_n*
   python3 scripts/project_scaling.py $CFG $D $D/projection.json > /dev/null || exit 1
+  # (the traces are large: keep the bench lines and the projection)
+  for f in $D/n*_trace.csv; do wc -l $f; done
+  rm -f $D/n*_trace.csv
   python3 -c "import json; d = json.load(open('$D/projection.json')); \
 print('$CFG', {n: round(v['projected_speedup'], 2) for n, v in d['ranks'].items()})"
 done
