@@ -762,13 +762,25 @@ struct RbBox {
 // neighbour), and every box of the level is in the launch; so dst ends as
 // pair + k_gc_faces would leave it (edges and corners: src's, as without
 // corners; k_gc_corners follows when the fill wants them).
-template <int NC, bool PUSH = false>
+//
+// VAR (round 5): levels with electrode boxes, whose variable 7-point
+// stencils v(7, nc^3) and bc_correction come per box id from vp / bp (null:
+// the level's constant stencil). stencil_gsrb_357's variable branch
+// (m_af_stencil.f90:836-841, 958-978) on those boxes: rhs + bc_correction,
+// the sum over the neighbours divided by c(1), rhs - bc_correction -- the
+// red cells with rhs (r + b), the black cells with ((r + b) - b) + b, the
+// first half-sweep's round trip; phase B recomputes a variable neighbour's
+// red boundary cell with its own stencil the same way. The pair leaves rhs
+// alone (a neighbour's workgroup reads it); k_rhs_roundtrip applies the two
+// round trips after the launch. Bitwise k_gsrb_v + k_gsrb + fills.
+template <int NC, bool PUSH = false, bool VAR = false>
 __global__ void __launch_bounds__(RbBox<NC>::NT)
     k_gsrb_pair_box(const double *__restrict__ src, double *__restrict__ dst,
                     const double *__restrict__ rhs, const double *__restrict__ coarse,
                     const afh_box_meta *__restrict__ meta,
                     const int32_t *__restrict__ ids, size_t bsz, Coef cf,
-                    double inv_c1, GcArgs ga) {
+                    double inv_c1, GcArgs ga, const double *const *__restrict__ vp = nullptr,
+                    const double *const *__restrict__ bp = nullptr) {
   using G = RbBox<NC>;
   constexpr int NG = G::NG, HN = G::HN, NT = G::NT, RPT = G::RPT, GPT = G::GPT;
   constexpr int SK = NG * NG, NB = NG * NG * NG;
@@ -793,6 +805,8 @@ __global__ void __launch_bounds__(RbBox<NC>::NT)
   const double *x = src + (size_t)(id - 1) * bsz;
   double *y = dst + (size_t)(id - 1) * bsz;
   const double *r = rhs + (size_t)(id - 1) * bsz;
+  // VAR: this box's stencil and correction (null: constant)
+  const double *bv = VAR ? vp[id - 1] : nullptr, *bb = VAR ? bp[id - 1] : nullptr;
 
   // red cell q of this thread: row (j, k), i = 2 ih + 1 + ((j + k) & 1);
   // the black cell of the same pair of columns is the other parity
@@ -822,6 +836,8 @@ __global__ void __launch_bounds__(RbBox<NC>::NT)
   // neighbour values of the same-level face ghosts
   for (int e = tid; e < NB; e += NT) P[e] = x[e];
   double rR[RPT], rB[RPT];
+  // VAR: the red / black cells' stencils (c(1) first, as v stores them)
+  double vR[VAR ? RPT : 1][7], vB[VAR ? RPT : 1][7];
 #pragma unroll
   for (int q = 0; q < RPT; q++) {
     int i, j, k;
@@ -830,8 +846,25 @@ __global__ void __launch_bounds__(RbBox<NC>::NT)
     int i2, j2, k2;
     cell(q, false, i2, j2, k2);
     rB[q] = ok ? r[(size_t)(k2 * NG + j2) * NG + i2] : 0.0;
+    if constexpr (VAR) {
+      if (ok && bv) {
+        const int eR = ((k - 1) * NC + (j - 1)) * NC + (i - 1);
+        const int eB = ((k2 - 1) * NC + (j2 - 1)) * NC + (i2 - 1);
+#pragma unroll
+        for (int s = 0; s < 7; s++) vR[q][s] = bv[7 * eR + s], vB[q][s] = bv[7 * eB + s];
+        if (bb) {
+          // rhs + bc_correction of the red sweep; the black sweep's after
+          // the red sweep's round trip
+          rR[q] = rR[q] + bb[eR];
+          rB[q] = ((rB[q] + bb[eB]) - bb[eB]) + bb[eB];
+        }
+      }
+    }
   }
   double bl[GPT][7];
+  // VAR: a variable neighbour's stencil at its boundary cell (vn[g][0] = 0:
+  // constant) and its rhs + bc_correction in bl[g][6]
+  double vn[VAR ? GPT : 1][7];
   int brep[GPT];
   bool bpre[GPT];
 #pragma unroll
@@ -839,6 +872,7 @@ __global__ void __launch_bounds__(RbBox<NC>::NT)
     const int u = tid + NT * g;
     brep[g] = -1;
     bpre[g] = false;
+    if constexpr (VAR) vn[g][0] = 0.0;
 #pragma unroll
     for (int q = 0; q < 7; q++) bl[g][q] = 0.0;
     if (u < G::NGH) {
@@ -861,6 +895,17 @@ __global__ void __launch_bounds__(RbBox<NC>::NT)
         bl[g][4] = xs[c - SK];
         bl[g][5] = xs[c + SK];
         bl[g][6] = rhs[(size_t)(nid - 1) * bsz + c];
+        if constexpr (VAR) {
+          vn[g][0] = 0.0;
+          const double *nv = vp[nid - 1];
+          if (nv) {
+            const int en = ((q3[2] - 1) * NC + (q3[1] - 1)) * NC + (q3[0] - 1);
+#pragma unroll
+            for (int s = 0; s < 7; s++) vn[g][s] = nv[7 * en + s];
+            const double *nbc = bp[nid - 1];
+            if (nbc) bl[g][6] = bl[g][6] + nbc[en];
+          }
+        }
       }
     }
   }
@@ -871,9 +916,16 @@ __global__ void __launch_bounds__(RbBox<NC>::NT)
     int i, j, k;
     if (!cell(q, true, i, j, k)) continue;
     const int c = (k * NG + j) * NG + i;
-    P[c] = (rR[q] - cf.c[1] * P[c - 1] - cf.c[2] * P[c + 1] - cf.c[3] * P[c - NG] -
-            cf.c[4] * P[c + NG] - cf.c[5] * P[c - SK] - cf.c[6] * P[c + SK]) *
-           inv_c1;
+    if (VAR && bv) {
+      const double *v = vR[VAR ? q : 0];
+      P[c] = (rR[q] - v[1] * P[c - 1] - v[2] * P[c + 1] - v[3] * P[c - NG] -
+              v[4] * P[c + NG] - v[5] * P[c - SK] - v[6] * P[c + SK]) /
+             v[0];
+    } else {
+      P[c] = (rR[q] - cf.c[1] * P[c - 1] - cf.c[2] * P[c + 1] - cf.c[3] * P[c - NG] -
+              cf.c[4] * P[c + NG] - cf.c[5] * P[c - SK] - cf.c[6] * P[c + SK]) *
+             inv_c1;
+    }
   }
   __syncthreads();
   // B: red face ghosts
@@ -897,9 +949,16 @@ __global__ void __launch_bounds__(RbBox<NC>::NT)
 #pragma unroll
       for (int q = 0; q < 6; q++)
         if (q == brep[g]) b[q] = x1v;
-      v = (b[6] - cf.c[1] * b[0] - cf.c[2] * b[1] - cf.c[3] * b[2] - cf.c[4] * b[3] -
-           cf.c[5] * b[4] - cf.c[6] * b[5]) *
-          inv_c1;
+      if (VAR && vn[VAR ? g : 0][0] != 0.0) {
+        const double *w = vn[VAR ? g : 0];
+        v = (b[6] - w[1] * b[0] - w[2] * b[1] - w[3] * b[2] - w[4] * b[3] - w[5] * b[4] -
+             w[6] * b[5]) /
+            w[0];
+      } else {
+        v = (b[6] - cf.c[1] * b[0] - cf.c[2] * b[1] - cf.c[3] * b[2] - cf.c[4] * b[3] -
+             cf.c[5] * b[4] - cf.c[6] * b[5]) *
+            inv_c1;
+      }
     } else {
       const double x2v = P[ix3(NG, q2[0], q2[1], q2[2])];  // red, new
       const int ta = d == 0 ? 1 : 0, tb = d == 2 ? 1 : 2;
@@ -916,9 +975,16 @@ __global__ void __launch_bounds__(RbBox<NC>::NT)
     int i, j, k;
     if (!cell(q, false, i, j, k)) continue;
     const int c = (k * NG + j) * NG + i;
-    P[c] = (rB[q] - cf.c[1] * P[c - 1] - cf.c[2] * P[c + 1] - cf.c[3] * P[c - NG] -
-            cf.c[4] * P[c + NG] - cf.c[5] * P[c - SK] - cf.c[6] * P[c + SK]) *
-           inv_c1;
+    if (VAR && bv) {
+      const double *v = vB[VAR ? q : 0];
+      P[c] = (rB[q] - v[1] * P[c - 1] - v[2] * P[c + 1] - v[3] * P[c - NG] -
+              v[4] * P[c + NG] - v[5] * P[c - SK] - v[6] * P[c + SK]) /
+             v[0];
+    } else {
+      P[c] = (rB[q] - cf.c[1] * P[c - 1] - cf.c[2] * P[c + 1] - cf.c[3] * P[c - NG] -
+              cf.c[4] * P[c + NG] - cf.c[5] * P[c - SK] - cf.c[6] * P[c + SK]) *
+             inv_c1;
+    }
   }
   __syncthreads();
   if constexpr (!PUSH) {
@@ -1430,6 +1496,25 @@ __global__ void k_gsrb_v(double *__restrict__ phi, double *__restrict__ rhs,
             v[4] * x[c + sj] - v[5] * x[c - sk] - v[6] * x[c + sk]) /
            v[0];
   if (b) r[c] = r1 - b[t];
+}
+
+// The rhs round trips (rhs + bc_correction - bc_correction) of the n
+// half-sweeps a fused variable pair did (k_gsrb_pair_box<.., VAR>), in the
+// order k_gsrb_v applies them
+__global__ void k_rhs_roundtrip(double *__restrict__ rhs, const int32_t *__restrict__ ids,
+                                int nc, size_t bsz, const double *const *__restrict__ bp,
+                                int n) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nc * nc * nc) return;
+  const int id = ids[blockIdx.y];
+  const double *b = bp[id - 1];
+  if (!b) return;
+  int i, j, k;
+  cell3(t, nc, i, j, k);
+  double *r = rhs + (size_t)(id - 1) * bsz + ix3(nc + 2, i, j, k);
+  double v = *r;
+  for (int q = 0; q < n; q++) v = (v + b[t]) - b[t];
+  *r = v;
 }
 
 // residual_box with the variable stencil: tmp = rhs - (L phi - bc_correction)
@@ -3029,15 +3114,25 @@ static void launch_pair(afh_mg *mg, int lvl, const double *src, double *dst,
   if (t->ids.n(lvl) == 0) return;
   if constexpr (NC <= 16) {
     if (mg->pair_box) {
+      const bool var = mg->any_var && mg->lvl_var[lvl - 1];
+      auto go = [&](auto kern) {
+        launch_ev(kern, e0, e1, dim3(t->ids.n(lvl)), dim3(RbBox<NC>::NT), t->stream, src, dst,
+                  t->ccv(mg->d.i_rhs), t->ccv(mg->d.i_phi), t->d_boxes, t->ids.at(lvl),
+                  t->bsz, cf, inv_c1, t->gc_args(mg->d.i_phi),
+                  (const double *const *)mg->d_vp, (const double *const *)mg->d_bp);
+      };
       if (pair_push(mg))
-        launch_ev((k_gsrb_pair_box<NC, true>), e0, e1, dim3(t->ids.n(lvl)),
-                  dim3(RbBox<NC>::NT), t->stream, src, dst, t->ccv(mg->d.i_rhs),
-                  t->ccv(mg->d.i_phi), t->d_boxes, t->ids.at(lvl), t->bsz, cf, inv_c1,
-                  t->gc_args(mg->d.i_phi));
+        var ? go(k_gsrb_pair_box<NC, true, true>) : go(k_gsrb_pair_box<NC, true>);
       else
-        launch_ev((k_gsrb_pair_box<NC>), e0, e1, dim3(t->ids.n(lvl)), dim3(RbBox<NC>::NT),
-                  t->stream, src, dst, t->ccv(mg->d.i_rhs), t->ccv(mg->d.i_phi), t->d_boxes,
-                  t->ids.at(lvl), t->bsz, cf, inv_c1, t->gc_args(mg->d.i_phi));
+        var ? go(k_gsrb_pair_box<NC, false, true>) : go(k_gsrb_pair_box<NC>);
+      if (var && mg->ids_v.n(lvl)) {
+        // the two half-sweeps' rhs round trips on the electrode boxes
+        const int nc = t->nc;
+        hipLaunchKernelGGL(k_rhs_roundtrip, dim3((nc * nc * nc + 255) / 256, mg->ids_v.n(lvl)),
+                           dim3(256), 0, t->stream, t->ccv(mg->d.i_rhs), mg->ids_v.at(lvl),
+                           nc, t->bsz, (const double *const *)mg->d_bp, 2);
+        // (the caller's launch check covers it)
+      }
       return;
     }
   }
@@ -3062,7 +3157,9 @@ extern "C" {
 // gsrb_boxes smooths level lvl with the fused pair kernel (same answer on
 // every rank of a sharded tree: decided on the level's total box count)
 static bool fused_level(const afh_mg *mg, int lvl) {
-  if (mg->any_var && mg->lvl_var[lvl - 1]) return false;  // electrode stencils
+  // electrode stencils: the small-box pair has a variable form (VAR)
+  if (mg->any_var && mg->lvl_var[lvl - 1] && !(mg->pair_box && mg->t->nc <= 16))
+    return false;
   return mg->alt && mg->t->lvl_total[lvl - 1] >= mg->fused_min;
 }
 
