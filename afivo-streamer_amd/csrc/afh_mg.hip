@@ -2688,6 +2688,10 @@ struct afh_mg {
   // (round 4: S3 1.71 -> 1.57 ms per step, profiles/r04_push_ab.txt)
   bool prolong_push = true;  // AFH_PROLONG_PUSH: so does the small-box correction
   bool rstr_push = true;     // AFH_RSTR_PUSH: and the small-box restriction
+  // inside afh_mg_fas_fmg's V-cycles: the levels below the cycle's top had
+  // their ghost cells filled by the previous (one level lower) V-cycle's up
+  // leg or the level-1 solve, so the restriction may push faces there too
+  bool in_fmg = false;
   int tiles_min = 256;  // levels of fewer boxes run tiles (NC >= 32)
   int *d_cycles = nullptr;
   int cycles_host = 0;
@@ -4059,7 +4063,10 @@ int32_t afh_mg_fas_fmg(afh_mg *mg, int32_t set_residual, int32_t have_guess) {
       return e;
     mg->phi_gc_gen = t->gen[i_phi];  // the cycle's top level was just filled
     mg->phi_gc_meth = t->meth_gen;
-    if ((e = afh_mg_fas_vcycle(mg, set_residual && lvl == nl, lvl))) return e;
+    mg->in_fmg = true;
+    e = afh_mg_fas_vcycle(mg, set_residual && lvl == nl, lvl);
+    mg->in_fmg = false;
+    if (e) return e;
   }
   return AFH_OK;
 }
@@ -4149,8 +4156,9 @@ static int32_t vcycle_body(afh_mg *mg, int32_t set_residual, int max_lvl, bool m
   for (int lvl = max_lvl; lvl >= 2; lvl--) {
     if ((e = gsrb_boxes(mg, lvl, false, top_stale && lvl == max_lvl))) return e;
     // (ghosts of the levels below valid: phi and the boundary conditions
-    // unchanged since a V-cycle over the whole tree filled them)
-    if ((e = update_coarse(mg, lvl, !top_stale && max_lvl == t->nlvl &&
+    // unchanged since a V-cycle over the whole tree filled them, or the
+    // previous V-cycle of an FMG)
+    if ((e = update_coarse(mg, lvl, !top_stale && (max_lvl == t->nlvl || mg->in_fmg) &&
                                         mg->phi_gc_meth == t->meth_gen)))
       return e;
   }
@@ -4235,8 +4243,8 @@ static int32_t vcycle_graph(afh_mg *mg, int32_t set_residual, int max_lvl, bool 
        !cs_electrode_fused(mg) && !mg->csd_ok) ||
       (mg->d.coarse_mode == AFH_COARSE_CYCLES && mg->d.coarse_tol > 0 && mg->small_from > 0))
     return AFH_OK;
-  const int key = (max_lvl << 3) | (top_stale ? 4 : 0) | (set_residual ? 2 : 0) |
-                  (max_out ? 1 : 0);
+  const int key = (max_lvl << 4) | (mg->in_fmg ? 8 : 0) | (top_stale ? 4 : 0) |
+                  (set_residual ? 2 : 0) | (max_out ? 1 : 0);
   afh_mg::Graph &g = mg->graphs[key];
   if (g.meth_gen != t->meth_gen) {
     // new boundary values or types since the warm call / capture: run

@@ -214,10 +214,15 @@ def build_driver_case(lib, device, config="s3", coarse="pfmg", grow_cells=0,
         sim.output_cnt = 0
         sim.output_write()
         sim.time_last_output = sim.time
-        t0 = time.perf_counter()
+        t0 = t_print = time.perf_counter()
         while (sim.af.n_leaf_cells() < grow_cells and
                time.perf_counter() - t0 < grow_seconds and sim.step()):
             sim.grown["steps"] += 1
+            if time.perf_counter() - t_print > 20:  # progress (a long growth is not a hang)
+                t_print = time.perf_counter()
+                print("grow: %d steps, t = %.4g s, %d leaf cells, %.0f s" %
+                      (sim.grown["steps"], sim.time, sim.af.n_leaf_cells(), t_print - t0),
+                      file=sys.stderr, flush=True)
         sim.grown["time_s"] = sim.time
     return sim
 
@@ -455,6 +460,16 @@ def bench_local(args, coarse):
     }
 
 
+def _roctx():
+    """--profile-steps: the ROCTx pause / resume of rocprofv3's
+    --selected-regions (collection paused from the start, so that the kernel
+    trace of a grown tree holds only the profile window, not the growth)."""
+    import ctypes as C
+    lib = C.CDLL("/opt/rocm/lib/librocprofiler-sdk-roctx.so")
+    lib.roctxProfilerPause.argtypes = lib.roctxProfilerResume.argtypes = [C.c_uint64]
+    return lib
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -490,12 +505,19 @@ def main():
                          "holds this many leaf cells (or --grow-seconds pass), then bench "
                          "on that tree")
     ap.add_argument("--grow-seconds", type=float, default=240.0)
+    ap.add_argument("--profile-steps", type=int, default=0,
+                    help="after the timed region, this many more unit steps inside a "
+                         "ROCTx resume / pause (run under rocprofv3 --selected-regions: "
+                         "the trace holds these steps only)")
     ap.add_argument("--oracle", action="store_true",
                     help="--transport local on the C oracle (CPU), for tests")
     ap.add_argument("--graphs", choices=("auto", "on", "off"), default="auto",
                     help="V-cycles replayed as captured hipGraphs (auto: on for the "
                          "small-box configs s1 / s3, whose steps are launch-bound)")
     args = ap.parse_args()
+    # (rocprofv3 --selected-regions starts paused; --marker-trace routes the
+    # ROCTx calls to it)
+    roctx = _roctx() if args.profile_steps else None
     coarse = coarse_choice(args.coarse, args.config)
     if args.transport == "local":
         if args.graphs == "off":
@@ -620,6 +642,15 @@ def main():
             unit_step(case, dt, args.warmup + args.steps + 2 + k)
         case.tree.sync()
         lib.call("profile_read", case.tree.h, C.byref(ms), C.byref(nl), C.byref(by))
+    if roctx:
+        lib.call("profile_enable", case.tree.h, 0)
+        k0 = args.warmup + args.steps + 6  # even: the window starts on a Heun stage 1
+        case.tree.sync()
+        roctx.roctxProfilerResume(0)
+        for k in range(args.profile_steps):
+            unit_step(case, dt, k0 + k)
+        case.tree.sync()
+        roctx.roctxProfilerPause(0)
 
     if dist is not None:
         import torch
