@@ -306,3 +306,28 @@ def test_gradient_folded_into_residual_bitwise(config, monkeypatch):
         c.tree.close()
         outs.append(out)
     _same(outs[0], outs[1])
+
+@pytest.mark.parametrize("config,cgs,dom", [
+    ("c64", (64, 64, 64), (8e-3, 8e-3, 8e-3)),
+    ("c64y", (64, 128, 64), (8e-3, 16e-3, 8e-3))])
+def test_dpair_bitwise_64cubed(config, cgs, dom, monkeypatch):
+    """Two red-black iterations in one pass (k_gsrb_dpair, AFH_GSRB_DPAIR) vs
+    two fused pairs with the level fill between: 64^3 boxes, three levels,
+    the dpair on the top level of 64 (128) boxes (AFH_GSRB_DPAIR_MIN=64);
+    halos from face, edge and corner neighbours and the physical faces'
+    ghosts formed in the kernel (Dirichlet z, Neumann x / y). Field solve
+    and four unit steps bitwise."""
+    import bench
+    monkeypatch.setitem(bench.CONFIGS, config, (64, cgs, 3, dom))
+    monkeypatch.setenv("AFH_GSRB_DPAIR_MIN", "64")
+    a = _s1(monkeypatch, {"AFH_GSRB_DPAIR": "1"}, config)
+    b = _s1(monkeypatch, {"AFH_GSRB_DPAIR": "0"}, config)
+    _same(a, b)
+
+
+def test_dpair_bitwise_s1_64(monkeypatch):
+    """The same on the headline tree (S1-64: the 512 leaf boxes of 64^3, the
+    default dpair level)."""
+    a = _s1(monkeypatch, {"AFH_GSRB_DPAIR": "1"}, "s1-64")
+    b = _s1(monkeypatch, {"AFH_GSRB_DPAIR": "0"}, "s1-64")
+    _same(a, b)
