@@ -1921,6 +1921,67 @@ __global__ void k_lsf_gradient(const double *__restrict__ phi,
   }
 }
 
+// The same with one thread per entry (boxes of at most 16^3 cells): a face
+// two entries write (an entry's low face is its low neighbour cell's high
+// face) keeps the value of the later entry in the list, as the serial loop
+// leaves it -- each entry skips the faces a later entry rewrites (the
+// entry of each cell in LDS)
+template <int NC>
+__global__ void __launch_bounds__(256)
+    k_lsf_gradient_par(const double *__restrict__ phi, const double *__restrict__ lsf,
+                       double *__restrict__ fcv, const int32_t *__restrict__ ids,
+                       size_t bsz, size_t fsz, const int *__restrict__ cnt,
+                       const int32_t *const *__restrict__ ixp,
+                       const double *const *__restrict__ ddp,
+                       const double *const *__restrict__ bvp, double ix_, double iy,
+                       double iz) {
+  constexpr int NG = NC + 2, NF = NC + 1, N3 = NC * NC * NC;
+  constexpr size_t D3 = (size_t)NF * NF * NF;
+  __shared__ int emap[N3];
+  const int id = ids[blockIdx.x];
+  const int n = cnt[id - 1];
+  for (int c = threadIdx.x; c < N3; c += blockDim.x) emap[c] = -1;
+  __syncthreads();
+  const int32_t *X = ixp[id - 1];
+  for (int e = threadIdx.x; e < n; e += blockDim.x) {
+    const int c = ((X[3 * e + 2] - 1) * NC + (X[3 * e + 1] - 1)) * NC + (X[3 * e] - 1);
+    atomicMax(&emap[c], e);
+  }
+  __syncthreads();
+  const double *p = phi + (size_t)(id - 1) * bsz, *l = lsf + (size_t)(id - 1) * bsz;
+  double *f = fcv + (size_t)(id - 1) * fsz;
+  const double *D = ddp[id - 1], *bv = bvp[id - 1];
+  auto fx = [&](int d, int a, int b, int c) {
+    return (size_t)d * D3 + ((size_t)(c - 1) * NF + (b - 1)) * NF + (a - 1);
+  };
+  for (int e = threadIdx.x; e < n; e += blockDim.x) {
+    const int i = X[3 * e], j = X[3 * e + 1], k = X[3 * e + 2];
+    const int ce = ((k - 1) * NC + (j - 1)) * NC + (i - 1);
+    if (emap[ce] > e) continue;  // a later entry of the same cell
+    const size_t c = ix3(NG, i, j, k);
+    if (l[c] < 0) continue;
+    const double *dd = D + 6 * e;
+    const double pc = p[c], bc = bv[ce];
+    // the face of direction q is also written by the entry of the cell
+    // across it (direction q ^ 1) if that entry is later and writes it
+    auto later = [&](int q) {
+      const int d = q >> 1, sgn = (q & 1) ? 1 : -1;
+      int a[3] = {i, j, k};
+      a[d] += sgn;
+      if (a[d] < 1 || a[d] > NC) return false;
+      const int cn = ((a[2] - 1) * NC + (a[1] - 1)) * NC + (a[0] - 1);
+      const int e2 = emap[cn];
+      return e2 > e && !(l[ix3(NG, a[0], a[1], a[2])] < 0) && D[6 * e2 + (q ^ 1)] < 1;
+    };
+    if (dd[0] < 1 && !later(0)) f[fx(0, i, j, k)] = ix_ * (pc - bc) / dd[0];
+    if (dd[1] < 1 && !later(1)) f[fx(0, i + 1, j, k)] = ix_ * (bc - pc) / dd[1];
+    if (dd[2] < 1 && !later(2)) f[fx(1, i, j, k)] = iy * (pc - bc) / dd[2];
+    if (dd[3] < 1 && !later(3)) f[fx(1, i, j + 1, k)] = iy * (bc - pc) / dd[3];
+    if (dd[4] < 1 && !later(4)) f[fx(2, i, j, k)] = iz * (pc - bc) / dd[4];
+    if (dd[5] < 1 && !later(5)) f[fx(2, i, j, k + 1)] = iz * (bc - pc) / dd[5];
+  }
+}
+
 // mg_box_field_norm (m_af_multigrid.f90:1995-2025) from the stored faces
 __global__ void k_field_norm(const double *__restrict__ fcv,
                              double *__restrict__ nrm,
@@ -4700,11 +4761,21 @@ int32_t afh_mg_compute_phi_gradient(afh_mg *mg, int32_t i_fc, double fac,
     const int n = mg->lsf_leaves.n(l);
     if (!n) continue;
     const double *dr = &t->lvl_dr[3 * (l - 1)];
-    hipLaunchKernelGGL(k_lsf_gradient, dim3(n), dim3(64), 0, t->stream,
-                       t->ccv(mg->d.i_phi), t->ccv(mg->i_lsf), t->fcv(i_fc),
-                       mg->lsf_leaves.at(l), nc, t->bsz, t->fsz, mg->d_lsf_n,
-                       mg->d_ix, mg->d_dd, mg->d_bv, fac / dr[0], fac / dr[1],
-                       fac / dr[2]);
+    auto par = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3(n), dim3(256), 0, t->stream, t->ccv(mg->d.i_phi),
+                         t->ccv(mg->i_lsf), t->fcv(i_fc), mg->lsf_leaves.at(l), t->bsz,
+                         t->fsz, mg->d_lsf_n, mg->d_ix, mg->d_dd, mg->d_bv, fac / dr[0],
+                         fac / dr[1], fac / dr[2]);
+    };
+    if (nc == 4) par(k_lsf_gradient_par<4>);
+    else if (nc == 8) par(k_lsf_gradient_par<8>);
+    else if (nc == 16) par(k_lsf_gradient_par<16>);
+    else
+      hipLaunchKernelGGL(k_lsf_gradient, dim3(n), dim3(64), 0, t->stream,
+                         t->ccv(mg->d.i_phi), t->ccv(mg->i_lsf), t->fcv(i_fc),
+                         mg->lsf_leaves.at(l), nc, t->bsz, t->fsz, mg->d_lsf_n,
+                         mg->d_ix, mg->d_dd, mg->d_bv, fac / dr[0], fac / dr[1],
+                         fac / dr[2]);
     AFH_LAUNCH_CHECK("k_lsf_gradient");
     if (nrm) {
       hipLaunchKernelGGL(k_field_norm, dim3((n3 + 255) / 256, n), dim3(256), 0,
