@@ -169,6 +169,14 @@ int32_t dist_dev_reduce(void *ctx, int kind, unsigned long long *keys, int n) {
   return AFH_OK;
 }
 
+// RCCL: the SUM of afh_tree_sum_cc, all-reduced in place on the device
+int32_t dist_dev_sum(void *ctx, double *val) {
+  afh_dist *d = static_cast<afh_dist *>(ctx);
+  if (ncclAllReduce(val, val, 1, ncclDouble, ncclSum, d->comm, d->t->stream) != ncclSuccess)
+    return set_error(AFH_ERR_DEVICE, "ncclAllReduce (device sum)");
+  return AFH_OK;
+}
+
 int32_t dist_hook(void *ctx, int32_t kind, int32_t level, int32_t iv, double *vals, int32_t n) {
   afh_dist *d = static_cast<afh_dist *>(ctx);
   switch (kind) {
@@ -393,7 +401,11 @@ int32_t afh_dist_create(afh_tree *t, const afh_tree_desc *desc, const int32_t *o
   if (!e && transport == AFH_DIST_RCCL && hipMalloc(&d->d_red, 16 * sizeof(double)) != hipSuccess)
     e = set_error(AFH_ERR_DEVICE, "reduction buffer");
   if (!e) e = afh_tree_set_hook(t, dist_hook, d);
-  if (!e && transport == AFH_DIST_RCCL) t->dev_reduce = dist_dev_reduce;
+  if (!e && transport == AFH_DIST_RCCL) {
+    t->dev_reduce = dist_dev_reduce;
+    t->dev_sum = dist_dev_sum;
+    t->hook_capturable = true;  // exchanges are stream operations
+  }
   if (e) {
     afh_dist_destroy(d);
     return e;
@@ -408,6 +420,8 @@ int32_t afh_dist_destroy(afh_dist *d) {
   if (d->t && !d->t->retired && d->t->hook_ctx == d) {
     afh_tree_set_hook(d->t, nullptr, nullptr);
     d->t->dev_reduce = nullptr;
+    d->t->dev_sum = nullptr;
+    d->t->hook_capturable = false;
   }
   if (d->t) hipStreamSynchronize(d->t->stream);
   for (auto &kv : d->plans) {

@@ -116,6 +116,15 @@ struct afh_tree {
   // all-reduced on the device, on the ordered keys in place (stream-ordered,
   // no host round trip); the one fetch afterwards reads the global value
   int32_t (*dev_reduce)(void *ctx, int kind, unsigned long long *keys, int n) = nullptr;
+  // and the SUM of afh_tree_sum_cc (a double on the device, summed in place)
+  int32_t (*dev_sum)(void *ctx, double *val) = nullptr;
+  // the hook's exchanges are stream operations only (RCCL): a V-cycle may be
+  // captured with them inside (AFH_RCCL_CAPTURE)
+  bool hook_capturable = false;
+  // afh_tree_sum_cc on the device: per leaf (level order) the level's cell
+  // volume, or 0 where sum_skip drops the box (built on first use)
+  double *d_sumw = nullptr;
+  int sumw_n = -1;
   // segmented capture of a sharded V-cycle (afh_mg.hip vcycle_graph): while
   // seg_rec is set the stream is capturing, and call_hook ends the capture at
   // each exchange, records the exchange and begins the next segment; a

@@ -2974,6 +2974,11 @@ struct afh_mg {
   // between them (off: 1.54 ms per launch against 2 x 0.75 ms, the step
   // within the bimodal clock's spread; DESIGN.md, "Two iterations per pass")
   bool dpair = false;
+  // AFH_RCCL_CAPTURE=1: a V-cycle of a tree sharded over RCCL is captured as
+  // ONE graph with its exchanges (pack, grouped send / recv, unpack) inside,
+  // instead of segments between host-driven exchanges. Off until measured on
+  // more than one GPU (a capture failure falls back to the eager cycle)
+  bool rccl_capture = false;
   int dpair_min = 256;  // AFH_GSRB_DPAIR_MIN (tests: smaller trees)
   std::vector<char> lvl_uniform;  // level: every face and edge neighbour same-level or physical
   int in_alt = 0;  // a level whose phi lives in alt between the legs of a V-cycle (dpair)
@@ -3262,6 +3267,7 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
   if (const char *env = getenv("AFH_GSRB_PAIR_BOX")) mg->pair_box = atoi(env) != 0;
   if (const char *env = getenv("AFH_GSRB_DPAIR")) mg->dpair = atoi(env) != 0;
   if (const char *env = getenv("AFH_GSRB_DPAIR_MIN")) mg->dpair_min = atoi(env);
+  if (const char *env = getenv("AFH_RCCL_CAPTURE")) mg->rccl_capture = atoi(env) != 0;
   if (const char *env = getenv("AFH_GSRB_FUSED_MIN_BOXES"))
     mg->fused_min = atoi(env);
   else if (fused_nc_ok(t->nc))
@@ -3294,6 +3300,7 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
   if (const char *env = getenv("AFH_GSRB_PAIR_BOX")) mg->pair_box = atoi(env) != 0;
   if (const char *env = getenv("AFH_GSRB_DPAIR")) mg->dpair = atoi(env) != 0;
   if (const char *env = getenv("AFH_GSRB_DPAIR_MIN")) mg->dpair_min = atoi(env);
+  if (const char *env = getenv("AFH_RCCL_CAPTURE")) mg->rccl_capture = atoi(env) != 0;
   if (const char *env = getenv("AFH_GRAD_NT")) mg->grad_nt = atoi(env) != 0;
   if (fused_nc_ok(t->nc) && mg->fused_min > 0) {
     bool any = false;
@@ -4625,12 +4632,20 @@ static int32_t vcycle_graph(afh_mg *mg, int32_t set_residual, int max_lvl, bool 
     return AFH_OK;  // this call runs eagerly
   }
   if (g.eager_only) return AFH_OK;
-  if (t->hook) return vcycle_segments(mg, g, set_residual, max_lvl, max_out, top_stale, done);
+  const bool whole = !t->hook || (mg->rccl_capture && t->hook_capturable);
+  if (!whole) return vcycle_segments(mg, g, set_residual, max_lvl, max_out, top_stale, done);
   if (!g.exec) {
     hipGraph_t graph;
     AFH_HIP(hipStreamBeginCapture(t->stream, hipStreamCaptureModeThreadLocal));
     const int32_t e = vcycle_body(mg, set_residual, max_lvl, max_out, top_stale);
     const hipError_t ce = hipStreamEndCapture(t->stream, &graph);
+    if (t->hook && (e || ce != hipSuccess)) {
+      // (the exchanges would not capture: this variant stays eager)
+      if (ce == hipSuccess) hipGraphDestroy(graph);
+      (void)hipGetLastError();
+      g.eager_only = true;
+      return AFH_OK;
+    }
     if (e) {
       if (ce == hipSuccess) hipGraphDestroy(graph);
       return e;

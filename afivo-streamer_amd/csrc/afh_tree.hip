@@ -963,6 +963,7 @@ int32_t afh_tree_destroy(afh_tree *t) {
   hipFree(t->fc);
   hipFree(t->gc2);
   hipFree(t->scratch);
+  hipFree(t->d_sumw);
   hipFree(t->d_boxred);
   hipHostFree(t->h_scratch);
   if (t->own_stream) hipStreamDestroy(t->stream);
@@ -1113,7 +1114,7 @@ int32_t afh_tree_maxabs_cc(afh_tree *t, int32_t iv, double *out) {
 
 // per-box partial results over all leaves (level order), on the host
 static int32_t box_reduce(afh_tree *t, int iv, int op, int power,
-                          std::vector<double> &res) {
+                          std::vector<double> &res, bool fetch = true) {
   const int nl = t->leaves.off[t->nlvl];
   res.assign(2 * (size_t)nl, 0.0);
   if (!nl) return AFH_OK;
@@ -1143,10 +1144,23 @@ static int32_t box_reduce(afh_tree *t, int iv, int op, int power,
                        t->ccv(iv), t->leaves.d, t->nc, t->bsz, power, t->d_boxred);
   }
   AFH_LAUNCH_CHECK("k_box_reduce");
+  if (!fetch) return AFH_OK;
   AFH_HIP(hipMemcpyAsync(res.data(), t->d_boxred, sizeof(double) * 2 * nl,
                          hipMemcpyDeviceToHost, t->stream));
   AFH_HIP(hipStreamSynchronize(t->stream));
   return AFH_OK;
+}
+
+// afh_tree_sum_cc's fold on the device: the host loop's order and operations
+// (sum = sum + fac * box sum, leaves in level order, skipped boxes left out)
+// in one thread
+__global__ void k_sum_fold(const double *__restrict__ res, const double *__restrict__ w,
+                           int n, double *__restrict__ out) {
+  if (threadIdx.x != 0) return;
+  double sum = 0.0;
+  for (int q = 0; q < n; q++)
+    if (w[q] != 0.0) sum = sum + w[q] * res[2 * q];
+  *out = sum;
 }
 
 int32_t afh_tree_sum_cc(afh_tree *t, int32_t iv, int32_t power, double *out) {
@@ -1155,6 +1169,37 @@ int32_t afh_tree_sum_cc(afh_tree *t, int32_t iv, int32_t power, double *out) {
     return set_error(AFH_ERR_ARG, "afh_tree_sum_cc: bad argument");
   std::vector<double> res;
   int32_t e;
+  if (t->hook && t->dev_sum) {
+    // sharded over RCCL: box sums, their fold and the all-reduce on the
+    // device, one transfer at the end (bitwise the host path below)
+    const int nl = t->leaves.off[t->nlvl];
+    if (t->sumw_n != nl) {
+      std::vector<double> w(nl > 0 ? nl : 1, 0.0);
+      size_t q = 0;
+      for (int l = 1; l <= t->nlvl; l++) {
+        const double *dr = &t->lvl_dr[3 * (l - 1)];
+        const double fac = dr[0] * dr[1] * dr[2];
+        for (int b = 0; b < t->leaves.n(l); b++, q++)
+          w[q] = (t->sum_skip.empty() || !t->sum_skip[t->h_leaves[l - 1][b] - 1]) ? fac : 0.0;
+      }
+      AFH_HIP(hipStreamSynchronize(t->stream));
+      hipFree(t->d_sumw);
+      t->d_sumw = nullptr;
+      AFH_HIP(hipMalloc(&t->d_sumw, sizeof(double) * w.size()));
+      AFH_HIP(hipMemcpy(t->d_sumw, w.data(), sizeof(double) * w.size(), hipMemcpyHostToDevice));
+      t->sumw_n = nl;
+    }
+    if ((e = box_reduce(t, iv, 0, power, res, false))) return e;
+    // (after the slots' shards and their fold outputs)
+    double *d_out = t->scratch + (size_t)RED_SLOTS * RED_SHARDS + RED_SLOTS;
+    hipLaunchKernelGGL(k_sum_fold, dim3(1), dim3(64), 0, t->stream, t->d_boxred, t->d_sumw, nl,
+                       d_out);
+    AFH_LAUNCH_CHECK("k_sum_fold");
+    if ((e = t->dev_sum(t->hook_ctx, d_out))) return e;
+    AFH_HIP(hipMemcpyAsync(out, d_out, sizeof(double), hipMemcpyDeviceToHost, t->stream));
+    AFH_HIP(hipStreamSynchronize(t->stream));
+    return AFH_OK;
+  }
   if ((e = box_reduce(t, iv, 0, power, res))) return e;
   // my_sum = my_sum + fac * tmp, fac = product(af_lvl_dr(tree, lvl))
   double sum = 0.0;
@@ -1231,6 +1276,8 @@ int32_t afh_tree_set_hook(afh_tree *t, afh_hook_fn fn, void *ctx) {
   t->hook = fn;
   t->hook_ctx = ctx;
   t->dev_reduce = nullptr;  // the library's RCCL transport sets its own
+  t->dev_sum = nullptr;
+  t->hook_capturable = false;
   t->meth_gen++;            // captured V-cycles recorded the old exchanges
   return AFH_OK;
 }

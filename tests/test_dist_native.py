@@ -26,7 +26,7 @@ from afh import capi
 import golden
 from afh.dist import NativeGroup, NativeShard, Partition, rccl_comm
 from afh.streamer import FV, IV
-from test_dist import CC_VARS, TOPOS, _run
+from test_dist import CC_VARS, FV, TOPOS, _run
 
 KINDS = [capi.HOOK_HALO, capi.HOOK_RIMS, capi.HOOK_CFLUX, capi.HOOK_RESTRICT]
 
@@ -373,3 +373,69 @@ def test_exchange_rows_gloo(tmp_path):
             np.testing.assert_array_equal(d["ids%d" % q], np.arange(m) + 100 * q)
             np.testing.assert_array_equal(
                 d["rows%d" % q], np.arange(4 * m, dtype=np.float64).reshape(m, 4) + 1000 * q + r)
+
+
+@pytest.mark.gpu
+def test_rccl_single_rank_device_sum():
+    """af_tree_sum_cc on a tree sharded over RCCL (round 5): the box sums,
+    their fold (k_sum_fold, the host loop's order) and the ncclAllReduce stay
+    on the device, one transfer at the end -- bitwise the unsharded tree's
+    host fold with one rank."""
+    lib = capi.hip_library()
+    topo = _sum_topo()
+    rng = np.random.default_rng(3)
+    from afh.model import Tree
+    ref_tree = Tree(lib, topo, 2, 1, device=0)
+    x = rng.random(ref_tree.cc_shape)
+    ref_tree.put_cc(1, x)
+    ref = [ref_tree.sum_cc(1), ref_tree.sum_cc(1, 2)]
+    ref_tree.close()
+    comm = rccl_comm(lib, 0, 1, 0)
+    try:
+        sh = NativeShard(lib, topo, 1, 0, transport=capi.DIST_RCCL, comm=comm)
+        t = sh.make_tree(lib, topo, 2, 1, device=0)
+        sh.attach(t)
+        t.put_cc(1, x)
+        got = [t.sum_cc(1), t.sum_cc(1, 2)]
+        sh.detach()
+        t.close()
+    finally:
+        lib.call("dist_rccl_comm_destroy", comm)
+    assert got == ref
+
+
+@pytest.mark.gpu
+def test_rccl_capture_single_rank_bitwise(monkeypatch):
+    """AFH_RCCL_CAPTURE=1: the V-cycles of a tree sharded over RCCL are
+    captured as whole graphs with their exchanges inside (one rank here: the
+    exchange posts an empty group), bitwise the unsharded run."""
+    monkeypatch.setenv("AFH_RCCL_CAPTURE", "1")
+    import golden
+    from afh.streamer import IV, StreamerCase, seed_state, tables_from
+    lib = capi.hip_library()
+    topo = TOPOS["amr8"]()
+    ref = _run(lib, topo)
+    comm = rccl_comm(lib, 0, 1, 0)
+    try:
+        sh = NativeShard(lib, topo, 1, 0, transport=capi.DIST_RCCL, comm=comm)
+        g = golden.load("uni8")
+        td, chem = tables_from(g)
+        c = StreamerCase(lib, topo, td, chem, float(g["current_voltage"]), coarse_cycles=12,
+                         shard=sh)
+        seed_state(c)
+        c.fluid.field_set_rhs(IV["rhs"], 0)
+        c.mg.fas_fmg(True, have_guess=False)
+        res = c.field_compute(0)
+        lim = c.heun_step(1e-12)
+        replays, segmented = c.mg.graph_stats()
+        out = {"res": np.asarray(res), "lim": np.asarray(lim)}
+        for k in ref:
+            if k.startswith("cc"):
+                out[k] = c.tree.get_cc(int(k[2:]))
+        out["fc_flux"] = c.tree.get_fc(FV["flux"])
+        sh.detach()
+    finally:
+        lib.call("dist_rccl_comm_destroy", comm)
+    _compare(ref, [sh], [out])
+    # whole-graph replays (a segment replay would count as segmented)
+    assert replays > 0 and segmented == 0, (replays, segmented)
