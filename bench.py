@@ -39,7 +39,7 @@ CONFIGS = {
     "s1": (16, (16, 16, 16), 4, (16e-3, 16e-3, 16e-3)),
     # BASELINE.json config 3: programs/standard_3d/streamer_3d.cfg with
     # air_chemistry_v2 (9 species, 25 reactions), the AMR tree the reference's
-    # set_initial_conditions builds (tests/golden/case_s3.npz, exported from
+    # set_initial_conditions builds (afivo-streamer_amd/afh/decks/case_s3.npz, exported from
     # the reference's own initializers; afh.driver builds the tree on the
     # device)
     "s3": (8, None, None, (16e-3, 16e-3, 16e-3)),
@@ -47,17 +47,17 @@ CONFIGS = {
     # chemistry (10 species, 12 reactions), the exponential atmosphere of its
     # m_user.f90 as a variable gas density, Helmholtz photoionization every
     # photoi%per_steps time steps, the 8-level AMR tree of 8^3 boxes its
-    # initial refinement builds (tests/golden/case_s5.npz, afh.users.Sprite3D)
+    # initial refinement builds (afivo-streamer_amd/afh/decks/case_s5.npz, afh.users.Sprite3D)
     "s5": (8, None, None, (5e3, 5e3, 20e3)),
     # BASELINE.json config 4 on one device: config 3 with the grounded rod
-    # electrode of SURVEY 8(d) S4 (tests/golden/case_s4.npz): level-set
+    # electrode of SURVEY 8(d) S4 (afivo-streamer_amd/afh/decks/case_s4.npz): level-set
     # stencils on the boxes the rod crosses (afh.electrode), the electrode's
     # species boundary condition every time step, 5 levels of 8^3 boxes
     "s4": (8, None, None, (16e-3, 16e-3, 16e-3)),
     # BASELINE.json config 1: programs/standard_2d/streamer_2d.cfg itself on
     # the 2-D build (libafivo_hip_2d.so) -- air_chemistry_v1 (8 species, 25
     # reactions), the AMR tree of 8^2 boxes its set_initial_conditions
-    # builds (tests/golden/case_s2d.npz, exported from the reference's own
+    # builds (afivo-streamer_amd/afh/decks/case_s2d.npz, exported from the reference's own
     # initializers)
     "2d": (8, None, None, (32e-3, 32e-3)),
     # a uniform 2-D tree with config 1's box size and domain (8 levels of 8^2
@@ -99,15 +99,15 @@ def build_case(lib, config, device, coarse, shard_ranks=None, shard=None):
     the sharded tree; or shard: a prepared afh.dist shard (thread ranks)."""
     from afh.streamer import StreamerCase, seed_state, tables_from
     from afh.tree import uniform_tree
-    import golden
+    from afh import decks
     nc, cgs, lvls, dom = CONFIGS[config]
     if len(dom) == 2:
         from afh.tree import uniform_tree_2d
         topo = uniform_tree_2d(nc, cgs, dom, lvls)
     else:
         topo = uniform_tree(nc, cgs, dom, lvls)
-    g = golden.load("uni8")  # transport/chemistry tables exported from the reference
-    td, chem = tables_from(g)
+    # transport / chemistry tables exported from the reference (package data)
+    td, chem = tables_from(decks.load("tables_air_siglo"))
     voltage = -dom[-1] * (-2.5e6)
     if shard_ranks is not None:
         world, rank, kind = shard_ranks
@@ -203,10 +203,10 @@ def build_driver_case(lib, device, config="s3", coarse="pfmg", grow_cells=0,
     steps with step control, refinement every refine_per_steps, output rows)
     until the tree holds at least grow_cells leaf cells, or grow_seconds
     pass, or the end time is reached."""
-    import golden
+    from afh import decks
     from afh.driver import Simulation
     from afh.users import USERS
-    sim = Simulation(lib, golden.load(DRIVER_FIXTURE[config]), device=device,
+    sim = Simulation(lib, decks.load(DRIVER_FIXTURE[config]), device=device,
                      user=USERS.get(config), **coarse_kw(coarse))
     sim.set_initial_conditions()
     sim.grown = {"steps": 0, "time_s": 0.0, "leaf_cells_initial": sim.af.n_leaf_cells()}
@@ -252,12 +252,11 @@ def cpu_baseline(config, coarse, steps=2):
     from afh import capi
     from afh.streamer import StreamerCase, seed_state, tables_from
     from afh.tree import uniform_tree
-    import golden
+    from afh import decks
     nc, cgs, lvls, dom = CONFIGS[config]
     sample_lvls = 3 if config == "s1-64" else lvls
     topo = uniform_tree(nc, cgs, dom, sample_lvls)
-    g = golden.load("uni8")
-    td, chem = tables_from(g)
+    td, chem = tables_from(decks.load("tables_air_siglo"))
     lib = capi.oracle_library()
     case = StreamerCase(lib, topo, td, chem, -dom[2] * (-2.5e6), **coarse_kw(coarse))
     seed_state(case, width=0.05 * dom[2])

@@ -17,7 +17,8 @@ tests/golden/rtest_<name>.npz. Only numbers and names are stored.
 The 2-D cases (BASELINE config 1: programs/standard_2d) use the NDIM = 2
 build of the same harness (make -C oracle _ref/2d/export_case):
 tests/golden/rtest_test_2d.npz (tests/test_2d.cfg with its regression log)
-and tests/golden/case_s2d.npz (streamer_2d.cfg itself: air_chemistry_v1).
+and afivo-streamer_amd/afh/decks/case_s2d.npz (streamer_2d.cfg itself:
+air_chemistry_v1; the case_*.npz decks are package data the bench reads).
 """
 import os
 import subprocess
@@ -121,7 +122,8 @@ def run(exe, tests, cases, extra_cases, only):
         subprocess.run([exe, dump, cfg] + extra, cwd=cwd, check=True,
                        stdout=subprocess.DEVNULL)
         d = parse_dump(dump)
-        out = os.path.join(REPO, "tests", "golden", "case_%s.npz" % name)
+        # (input decks of the bench: package data)
+        out = os.path.join(REPO, "afivo-streamer_amd", "afh", "decks", "case_%s.npz" % name)
         np.savez_compressed(out, **d)
         os.remove(dump)
         print("wrote", out, len(d), "arrays")
