@@ -191,6 +191,7 @@ class Simulation:
             self.i_gas_dens = list(self.cc_names).index("M") + 1
             self.gas_fractions = list(c.ra("gas_fractions"))
         self.n_var_cell, self.n_var_face = len(self.cc_names), len(c.sa("fc_names"))
+        self.n_scratch = 0  # (set with photoionization below)
         (self.i_phi, self.i_electron, self.i_1pos_ion, self.i_efld, self.i_rhs,
          self.i_tmp, self.i_photo, self.f_flux, self.f_field, self.i_lsf) = c.ia("ivars")
         n_species, self.n_gas, n_reac = c.ia("n_species")
@@ -242,6 +243,13 @@ class Simulation:
             qp = c.r("photoi%quenching_pressure")
             self.photoi_coeff = c.r("photoi%eta") * (qp / (c.r("gas_pressure_value") + qp))
             self.photo_species = c.i("photoi_species_index") - self.n_gas
+        # the Helmholtz modes 1 .. n-1 get an rhs and a tmp variable of their
+        # own (after the reference's variables): afh_photoi_helmh_compute then
+        # solves the modes concurrently, bitwise the one-after-another solve
+        # (AFH_HELMH_CONC=0: the shared variables, modes in turn)
+        self.n_scratch = 0
+        if self.photoi and os.environ.get("AFH_HELMH_CONC", "1") != "0":
+            self.n_scratch = 2 * (len(BOURDON3_LAMBDAS) - 1)
         self.td = c.lt("td")
         self.chem = c.lt("chem")
         self.reactions = []
@@ -292,6 +300,12 @@ class Simulation:
         self.graph_replays = [0, 0]
 
     # ------------------------------------------------------------- device
+    @property
+    def n_var_tree(self):
+        """cc variables of the device tree: the reference's, then the
+        concurrent Helmholtz modes' scratch (rhs, tmp per mode but the last)."""
+        return self.n_var_cell + self.n_scratch
+
     def _capacity(self):
         return max(64, int(self.capacity_factor * self.af.highest_id))
 
@@ -320,8 +334,11 @@ class Simulation:
                             coarse_mode=self.coarse_mode)
         self.helm = []
         if self.photoi:
-            for iv, lam in zip(self.helm_iv, self.helm_lambdas):
-                self.helm.append(Multigrid(tree, iv, self.i_rhs, self.i_tmp,
+            for k, (iv, lam) in enumerate(zip(self.helm_iv, self.helm_lambdas)):
+                own = self.n_scratch and k + 1 < len(self.helm_iv)
+                i_rhs = self.n_var_cell + 1 + 2 * k if own else self.i_rhs
+                i_tmp = self.n_var_cell + 2 + 2 * k if own else self.i_tmp
+                self.helm.append(Multigrid(tree, iv, i_rhs, i_tmp,
                                            helmholtz_lambda=lam * lam,
                                            coarse_cycles=self.coarse_cycles,
                                            coarse_tol=self.coarse_tol,
@@ -403,7 +420,7 @@ class Simulation:
         self.tree.put_cc(self.i_lsf, lsf)
 
     def _create_tree(self):
-        t = Tree(self.lib, self.af.topology(), self.n_var_cell, self.n_var_face,
+        t = Tree(self.lib, self.af.topology(), self.n_var_tree, self.n_var_face,
                  device=self.device, box_capacity=self._capacity())
         return self._set_methods(t)
 
@@ -431,7 +448,7 @@ class Simulation:
         sharding (afh.dist.NativeShard); with the Python Shard it raises."""
         topo = self.af.topology()
         full = self.tree
-        t = self._set_methods(shard.make_tree(self.lib, topo, self.n_var_cell,
+        t = self._set_methods(shard.make_tree(self.lib, topo, self.n_var_tree,
                                               self.n_var_face, device=self.device))
         for iv in range(1, self.n_var_cell + 1):
             t.put_cc(iv, full.get_cc(iv))
@@ -597,7 +614,7 @@ class Simulation:
         space = sorted(set(W) | set(W_old))
         pos = {b: k for k, b in enumerate(space)}
         t_ow = self._set_methods(Tree(self.lib, compact_topology(old_topo, W_old, space),
-                                      self.n_var_cell, self.n_var_face, device=self.device))
+                                      self.n_var_tree, self.n_var_face, device=self.device))
         local = [b for b in W_old if owner_old[b - 1] == me or owner_old[b - 1] < 0]
         data = [np.full((len(space) + 1,) + a.shape[1:], np.nan) for a in cc + fc]
         if local:
@@ -626,7 +643,7 @@ class Simulation:
         sh.detach()
         self.shard = None
         self.af = probe
-        t = self._set_methods(sh2.make_tree(self.lib, new_topo, self.n_var_cell,
+        t = self._set_methods(sh2.make_tree(self.lib, new_topo, self.n_var_tree,
                                             self.n_var_face, device=self.device))
         k = np.array([pos[int(b)] for b in t.global_ids])
         for iv in range(1, self.n_var_cell + 1):

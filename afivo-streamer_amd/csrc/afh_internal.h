@@ -121,6 +121,10 @@ struct afh_tree {
   // the hook's exchanges are stream operations only (RCCL): a V-cycle may be
   // captured with them inside (AFH_RCCL_CAPTURE)
   bool hook_capturable = false;
+  // side streams of concurrent multigrid solves (afh_photoi_helmh_compute:
+  // one per Helmholtz mode) and their fork / join events, created on use
+  hipStream_t side[4] = {nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t side_ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
   // afh_tree_sum_cc on the device: per leaf (level order) the level's cell
   // volume, or 0 where sum_skip drops the box (built on first use)
   double *d_sumw = nullptr;

@@ -3027,6 +3027,9 @@ struct afh_mg {
   double *w1 = nullptr, *w2 = nullptr;
   int q_bc[6] = {0, 0, 0, 0, 0, 0};
   double *alt = nullptr;  // spare image of phi (all boxes) for the ping-pong
+  // a spare image of its own (afh_photoi_helmh_compute's concurrent modes):
+  // t->alt and alt point to it while this multigrid's work is issued
+  double *alt_priv = nullptr;
   // electrode boxes (afh_mg_set_box_stencil / afh_mg_set_box_lsf): device
   // arrays per box id (null: none), their device pointer tables, and the
   // level lists split into constant- and variable-stencil boxes
@@ -3358,6 +3361,7 @@ int32_t afh_mg_destroy(afh_mg *mg) {
   hipFree(mg->d_csd_ainv), hipFree(mg->d_csd_g);
   hipFree(mg->d_pf_lvl), hipFree(mg->d_pf_A), hipFree(mg->d_pf_P), hipFree(mg->d_pf_b2r);
   hipFree(mg->d_pf_x), hipFree(mg->d_pf_fmask), hipFree((void *)mg->d_pf_vbc);
+  hipFree(mg->alt_priv);
   if (mg->alt && --mg->t->alt_refs == 0) {
     hipFree(mg->t->alt_base);
     mg->t->alt = mg->t->alt_base = nullptr;
@@ -4883,6 +4887,20 @@ __global__ void k_box_axpy(double *__restrict__ y, const double *__restrict__ x,
 
 extern "C" {
 
+// one FMG of mode mg issued on stream st with its own spare image (the
+// tree's stream and spare image swapped in for the issue, restored after)
+static int32_t fmg_on(afh_mg *mg, hipStream_t st) {
+  afh_tree *t = mg->t;
+  hipStream_t s0 = t->stream;
+  double *a0 = t->alt, *m0 = mg->alt;
+  t->stream = st;
+  if (mg->alt_priv) t->alt = mg->alt = mg->alt_priv;
+  const int32_t e = afh_mg_fas_fmg(mg, 1, 1);
+  t->stream = s0;
+  t->alt = a0, mg->alt = m0;
+  return e;
+}
+
 int32_t afh_photoi_helmh_compute(afh_mg *const *modes, int32_t n_modes,
                                  const double *coeffs, int32_t i_photo,
                                  double max_rel_res, int32_t max_fmg,
@@ -4898,17 +4916,65 @@ int32_t afh_photoi_helmh_compute(afh_mg *const *modes, int32_t n_modes,
   t->touch(i_photo);
   // af_tree_clear_cc(tree, i_photo)
   AFH_HIP(hipMemsetAsync(t->ccv(i_photo), 0, sizeof(double) * t->bsz * t->nb, t->stream));
-  double max_rhs;
+  // the source is the last mode's rhs (photoi_set_src's i_rhs); modes with
+  // an rhs and a tmp variable of their own get a copy of it and run
+  // concurrently, one side stream each (unsharded trees, at most 4 modes):
+  // every mode's solve is the same as alone, the sum below keeps the mode
+  // order, and the shared variables end as the last mode leaves them
+  const int src = modes[n_modes - 1]->d.i_rhs;
+  bool conc = !t->hook && n_modes > 1 && n_modes <= 4;
+  for (int n = 0; n < n_modes && conc; n++)
+    for (int m = n + 1; m < n_modes; m++)
+      if (modes[n]->d.i_rhs == modes[m]->d.i_rhs || modes[n]->d.i_tmp == modes[m]->d.i_tmp)
+        conc = false;
   int32_t e;
-  if ((e = afh_tree_maxabs_cc(t, modes[0]->d.i_rhs, &max_rhs))) return e;
+  for (int n = 0; n + 1 < n_modes; n++)
+    if (modes[n]->d.i_rhs != src) {
+      t->touch(modes[n]->d.i_rhs);
+      AFH_HIP(hipMemcpyAsync(t->ccv(modes[n]->d.i_rhs), t->ccv(src),
+                             sizeof(double) * t->bsz * t->nb, hipMemcpyDeviceToDevice,
+                             t->stream));
+    }
+  double max_rhs;
+  if ((e = afh_tree_maxabs_cc(t, src, &max_rhs))) return e;
   max_rhs = std::max(max_rhs, std::sqrt(DBL_EPSILON));
+  std::vector<int> done(n_modes, 0);
+  if (conc) {
+    for (int n = 0; n < n_modes; n++)
+      if (!t->side[n]) AFH_HIP(hipStreamCreateWithFlags(&t->side[n], hipStreamNonBlocking));
+    for (int n = 0; n <= n_modes; n++)
+      if (!t->side_ev[n]) AFH_HIP(hipEventCreateWithFlags(&t->side_ev[n], hipEventDisableTiming));
+    for (int n = 0; n + 1 < n_modes; n++)
+      if (!modes[n]->alt_priv && modes[n]->alt) {
+        const size_t bytes = (size_t)t->nb * t->bsz * sizeof(double);
+        AFH_HIP(hipMalloc(&modes[n]->alt_priv, bytes));
+        AFH_HIP(hipMemsetAsync(modes[n]->alt_priv, 0, bytes, t->stream));
+      }
+    // fork: every side stream after the work so far; join: the tree's
+    // stream after every side stream
+    AFH_HIP(hipEventRecord(t->side_ev[n_modes], t->stream));
+    for (int n = 0; n < n_modes; n++) {
+      AFH_HIP(hipStreamWaitEvent(t->side[n], t->side_ev[n_modes], 0));
+      if ((e = fmg_on(modes[n], t->side[n]))) return e;
+      AFH_HIP(hipEventRecord(t->side_ev[n], t->side[n]));
+    }
+    for (int n = 0; n < n_modes; n++) AFH_HIP(hipStreamWaitEvent(t->stream, t->side_ev[n], 0));
+    for (int n = 0; n < n_modes; n++) {
+      double residu;
+      if ((e = afh_tree_maxabs_cc(t, modes[n]->d.i_tmp, &residu))) return e;
+      done[n] = residu / max_rhs < max_rel_res ? 1 : 0;
+    }
+  }
   for (int n = 0; n < n_modes; n++) {
     afh_mg *mg = modes[n];
     int i;
-    for (i = 1; i <= max_fmg; i++) {
+    for (i = conc ? 2 : 1; i <= max_fmg; i++) {
+      if (conc && i == 2 && done[n]) {
+        i = 1;
+        break;
+      }
       double residu;
-      if ((e = afh_mg_fas_fmg(mg, 1, 1)) ||
-          (e = afh_tree_maxabs_cc(t, mg->d.i_tmp, &residu)))
+      if ((e = fmg_on(mg, t->stream)) || (e = afh_tree_maxabs_cc(t, mg->d.i_tmp, &residu)))
         return e;
       if (residu / max_rhs < max_rel_res) break;
     }

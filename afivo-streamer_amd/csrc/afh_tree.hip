@@ -964,6 +964,10 @@ int32_t afh_tree_destroy(afh_tree *t) {
   hipFree(t->gc2);
   hipFree(t->scratch);
   hipFree(t->d_sumw);
+  for (hipStream_t &q : t->side)
+    if (q) hipStreamDestroy(q);
+  for (hipEvent_t &q : t->side_ev)
+    if (q) hipEventDestroy(q);
   hipFree(t->d_boxred);
   hipHostFree(t->h_scratch);
   if (t->own_stream) hipStreamDestroy(t->stream);
@@ -1184,6 +1188,10 @@ int32_t afh_tree_sum_cc(afh_tree *t, int32_t iv, int32_t power, double *out) {
       }
       AFH_HIP(hipStreamSynchronize(t->stream));
       hipFree(t->d_sumw);
+  for (hipStream_t &q : t->side)
+    if (q) hipStreamDestroy(q);
+  for (hipEvent_t &q : t->side_ev)
+    if (q) hipEventDestroy(q);
       t->d_sumw = nullptr;
       AFH_HIP(hipMalloc(&t->d_sumw, sizeof(double) * w.size()));
       AFH_HIP(hipMemcpy(t->d_sumw, w.data(), sizeof(double) * w.size(), hipMemcpyHostToDevice));

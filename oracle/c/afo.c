@@ -3441,9 +3441,18 @@ int32_t afo_photoi_helmh_compute(afh_mg *const *modes, int32_t n_modes,
   if (i_photo < 1 || i_photo > t->nvc) return fail(AFH_ERR_ARG, "bad i_photo");
   touch(t, i_photo);
   memset(ccb(t, i_photo, 1), 0, sizeof(double) * t->bsz * t->nb);
+  /* the source is the last mode's rhs; a mode with an rhs variable of its
+     own solves with a copy of it (the library's concurrent modes; here one
+     after another) */
+  const int src = modes[n_modes - 1]->d.i_rhs;
+  for (int n = 0; n + 1 < n_modes; n++)
+    if (modes[n]->d.i_rhs != src) {
+      touch(t, modes[n]->d.i_rhs);
+      memcpy(ccb(t, modes[n]->d.i_rhs, 1), ccb(t, src, 1), sizeof(double) * t->bsz * t->nb);
+    }
   double max_rhs;
   int32_t e;
-  if ((e = afo_tree_maxabs_cc(t, modes[0]->d.i_rhs, &max_rhs))) return e;
+  if ((e = afo_tree_maxabs_cc(t, src, &max_rhs))) return e;
   if (max_rhs < sqrt(DBL_EPSILON)) max_rhs = sqrt(DBL_EPSILON);
   for (int n = 0; n < n_modes; n++) {
     afh_mg *mg = modes[n];

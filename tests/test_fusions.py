@@ -331,3 +331,34 @@ def test_dpair_bitwise_s1_64(monkeypatch):
     a = _s1(monkeypatch, {"AFH_GSRB_DPAIR": "1"}, "s1-64")
     b = _s1(monkeypatch, {"AFH_GSRB_DPAIR": "0"}, "s1-64")
     _same(a, b)
+
+
+def _s5_steps(monkeypatch, conc, steps=12):
+    import bench
+    from afh import capi
+    monkeypatch.setenv("AFH_HELMH_CONC", conc)
+    sim = bench.build_driver_case(capi.hip_library(), 0, "s5", "pfmg")
+    case = bench.DriverCase(sim)
+    case.fuse_rhs(True, ghosts=False)
+    case.field_compute(0)
+    res = [bench.unit_step(case, 1e-13, k) for k in range(steps)]
+    sim.photoi_set_src()
+    out = {"res": str(res), "n_var_tree": sim.n_var_tree}
+    for iv in range(1, sim.n_var_cell + 1):
+        if iv not in (sim.i_rhs, sim.i_tmp):  # (scratch of the last solve)
+            out["cc%d" % iv] = sim.tree.get_cc(iv)
+    sim.tree.close()
+    return out
+
+
+def test_helmholtz_modes_concurrent_bitwise(monkeypatch):
+    """S5's Bourdon-3 Helmholtz modes solved concurrently (one side stream
+    each, their own rhs / tmp / spare image: AFH_HELMH_CONC, the default) vs
+    one after another on the shared variables: every variable of the
+    reference's list bitwise after twelve unit steps (photoionization every
+    photoi%per_steps steps) and one more photoi_set_src."""
+    a = _s5_steps(monkeypatch, "1")
+    b = _s5_steps(monkeypatch, "0")
+    assert a["n_var_tree"] == b["n_var_tree"] + 4
+    a.pop("n_var_tree"), b.pop("n_var_tree")
+    _same(a, b)
