@@ -713,10 +713,17 @@ def main():
             out["config"]["ndim"] = 2
             out["config"]["fused_rhs"] = False
             out["config"]["chemistry"] = "air_chemistry_v1 (8 species, 25 reactions)"
-            out["cpu_baseline_note"] = (
-                "no 2-D CPU port travels to the box (the C oracle is 3-D); the reference's "
-                "own 2-D forward_euler timed in the build container: profiles/"
-                "r05_ref_cpu_timing_2d.json")
+            # the C oracle is 3-D: the reference's own 2-D code, timed in the
+            # build container (its binary does not travel to the GPU box)
+            ref = json.load(open(os.path.join(REPO, "profiles", "r05_ref_cpu_timing_2d.json")))
+            best = max(ref["threads"].items(), key=lambda kv: kv[1]["cell_updates_per_s"])
+            out["cpu_baseline"] = {
+                "value": best[1]["cell_updates_per_s"], "unit": "cell-updates/s",
+                "cores": int(best[0]), "kind": "reference",
+                "sample": "the reference's 2-D forward_euler + one V(2,2)-cycle (no level-1 "
+                          "solve) on a uniform %d-cell tree of streamer_2d.cfg, measured in "
+                          "the build container (profiles/r05_ref_cpu_timing_2d.json), not on "
+                          "this host" % ref["cells"]}
         if args.config in DRIVER_CONFIGS:
             g = sim.grown
             out["config"]["tree"] = {"leaf_cells_setup": g["leaf_cells_initial"],
