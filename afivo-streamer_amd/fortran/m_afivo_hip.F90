@@ -55,6 +55,7 @@ module m_afivo_hip
 
   integer(c_int32_t), parameter :: AFH_COARSE_CYCLES = 1
   integer(c_int32_t), parameter :: AFH_COARSE_DIRECT = 2
+  integer(c_int32_t), parameter :: AFH_COARSE_PFMG = 3
   integer, parameter :: AFH_MAX_SPECIES = 32
   integer, parameter :: AFH_MAX_REACTIONS = 128
 
