@@ -986,7 +986,11 @@ template <int NC>
 struct RbBox {
   static constexpr int NG = NC + 2, HN = NC / 2;
   static constexpr int NRED = NC * NC * HN;                  // red cells per box
-  static constexpr int NT = NRED >= 512 ? 512 : (NRED < 64 ? 64 : NRED);
+#ifndef AFH_RBBOX_DIV  // (A/B builds: fewer threads per box, more boxes per CU)
+#define AFH_RBBOX_DIV 1
+#endif
+  static constexpr int NT0 = NRED >= 512 ? 512 : (NRED < 64 ? 64 : NRED);
+  static constexpr int NT = NT0 / AFH_RBBOX_DIV >= 64 ? NT0 / AFH_RBBOX_DIV : 64;
   static constexpr int RPT = (NRED + NT - 1) / NT;           // red cells per thread
   static constexpr int NGH = 3 * NC * NC;                    // red face ghosts
   static constexpr int GPT = (NGH + NT - 1) / NT;            // ghosts per thread
