@@ -631,6 +631,16 @@ def main():
             unit_step(case, dt, args.warmup + args.steps + 2 + k)
         case.tree.sync()
         lib.call("profile_read", case.tree.h, C.byref(ms), C.byref(nl), C.byref(by))
+    if nl.value == 0 and two_d:
+        # no level of >= 256 boxes at all (config 1's set-up tree): the flux
+        # over every leaf (48 B/cell: the densities' two ghost layers read,
+        # the face fluxes written) is the line
+        kname = "k2_flux (all leaves, 48 B/cell)"
+        lib.call("profile_enable", case.tree.h, capi.PROF_FLUX)
+        for k in range(2):
+            unit_step(case, dt, args.warmup + args.steps + 4 + k)
+        case.tree.sync()
+        lib.call("profile_read", case.tree.h, C.byref(ms), C.byref(nl), C.byref(by))
     if nl.value == 0 and not two_d:
         # no level runs the fused pair (too few boxes per level, or
         # electrode stencils): the split half-sweep k_gsrb is the smoother
