@@ -1464,48 +1464,58 @@ void launch_update(const UpdArgs &A, afh_tree *t, int l, int n_boxes,
 // row evaluates the whole face), z-hi evaluated from the register window and
 // carried as z-lo of step k + 1. The cell is then advanced with k_update's
 // expressions (states and |E| of the cell; the flux species' s_deriv value is
-// the staged n_e). Face fluxes leave the kernel only with wf; the reductions
-// are k_flux_lds's (CFL, sigma) and k_update's (chemistry, on the last step).
-// Bitwise the results of k_flux_lds + k_update: same expressions, same
-// operand order. NP = number of previous states (1 or 2).
-// NS: species slots (>= ns); NP: previous states; SD: the derivative state
-// is not one of them (der_q < 0)
+// the staged n_e), the chemistry of a compiled network (NET) or the generic
+// reaction loop, and with an rhs output field_set_rhs of the new state
+// (k_update's). PHI: the face fields from the potential (k_flux_lds<PHI>'s
+// expressions). Face fluxes leave the kernel only with wf; the reductions are
+// k_flux_lds's (CFL, sigma) and k_update's (chemistry on the last step,
+// max|rhs|). Bitwise the results of k_flux_lds + k_update: same expressions,
+// same operand order. The n_e and |E| of the cell's own plane stay in LDS /
+// registers and the face fluxes never go through HBM: 64 B per cell fewer
+// than the two kernels.
+// NS: species slots (>= ns; NET::NS with a network); NP: previous states;
+// SD: the derivative state is not one of them (der_q < 0); NTT: threads
+#ifndef AFH_FE_NT  // threads of a k_fe_lds workgroup (NC * rows)
+#define AFH_FE_NT 256
+#endif
 #ifndef AFH_FE_MINW
 #define AFH_FE_MINW 2
 #endif
-#ifndef AFH_FE_LATE  // issue the cell's state loads after the x / y faces
-#define AFH_FE_LATE 0
-#endif
-template <int NC, int LIM, int NS, int NP, bool SD>
-__global__ void __launch_bounds__(256, AFH_FE_MINW)
+template <int NC, int LIM, int NS, int NP, bool SD, bool PHI = false, class NET = void,
+          int NTT = AFH_FE_NT>
+__global__ void __launch_bounds__(NTT, AFH_FE_MINW)
     k_fe_lds(FluxArgs A, UpdArgs U, const double *__restrict__ tdi,
              const int32_t *__restrict__ ids, size_t bsz, size_t fsz,
              unsigned long long *red, int wf) {
-  using G = FluxLds<NC, 256>;
+  using G = FluxLds<NC, NTT>;
   constexpr int NG = NC + 2, NF = NC + 1, TJ = G::TJ, NT = G::NT, RW = G::RW,
                 NR = G::NR, EW = G::EW, ER = G::ER, NPE = G::NPE, EPE = G::EPE;
   // box-local offsets as 32-bit ints: scalar base + vector offset loads
   constexpr int SK = NG * NG, FSK = NF * NF, FD = NF * NF * NF;
   constexpr int NN = NC * NC;
+  constexpr bool HAS_NET = !std::is_void<NET>::value;
   extern __shared__ double T[];  // 2 n_points (dynamic)
   __shared__ double SN[2][NR * RW], SE[2][ER * EW];
   __shared__ double sv[NT], sd[NT], sf[NT];
-  __shared__ double r1[NT / 64], r2[NT / 64], r3[NT / 64];
+  __shared__ double r1[NT / 64], r2[NT / 64], r3[NT / 64], r4[NT / 64];
   const int tid = threadIdx.x;
-  const int id = ids[blockIdx.x / G::NTILE];
+  const int wg = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int id = ids[wg / G::NTILE];
   const int i = tid % NC + 1;
   const int jr = tid / NC;
-  const int j0 = (blockIdx.x % G::NTILE) * TJ + 1, j = j0 + jr;
+  const int j0 = (wg % G::NTILE) * TJ + 1, j = j0 + jr;
   const size_t boff = (size_t)(id - 1) * bsz;
   const double *ne = A.ne + boff;
   const double *E = A.E + boff;
   const double *Ef = A.Ef + (size_t)(id - 1) * fsz;
+  const double *ph = PHI ? A.phi + boff : nullptr;
   double *F = A.F + (size_t)(id - 1) * fsz;
   const double *g2 = A.gc2 + (size_t)(id - 1) * 6 * NN;
   const double ix = A.inv_dx[0], iy = A.inv_dx[1], iz = A.inv_dx[2];
+  const double gfx = A.gfac[0], gfy = A.gfac[1], gfz = A.gfac[2];
   const double N_inv = A.N_inv;
   const int np = A.td.n_points;
-  const int eix = U.e_index, dq = U.der_q, ns = U.ns;
+  const int eix = U.e_index, dq = U.der_q, ns = HAS_NET ? NS : U.ns;
   for (int e = tid; e < 2 * np; e += NT) T[e] = tdi[e];
 
   auto ne_at = [&](int k, int e) -> double {
@@ -1543,15 +1553,27 @@ __global__ void __launch_bounds__(256, AFH_FE_MINW)
     const int e = tid + NT * q;
     if (e < ER * EW) SE[1][e] = e_at(1, e);
   }
-  double exl = Ef[fcol], eyl = Ef[FD + fcol];
-  double exh = i == NC ? Ef[fcol + 1] : 0.0;
-  double eyh = (jr == TJ - 1) ? Ef[FD + fcol + NF] : 0.0;
+  // face fields of plane 1 (PHI: k_flux_lds<PHI>'s expressions; pk = phi of
+  // the own cell in the current plane)
+  double exl, eyl, exh, eyh, pk = 0.0;
+  if (PHI) {
+    const int c1 = SK + cc;
+    pk = ph[c1];
+    exl = gfx * (pk - ph[c1 - 1]);
+    eyl = gfy * (pk - ph[c1 - NG]);
+    exh = i == NC ? gfx * (ph[c1 + 1] - pk) : 0.0;
+    eyh = (jr == TJ - 1) ? gfy * (ph[c1 + NG] - pk) : 0.0;
+  } else {
+    exl = Ef[fcol], eyl = Ef[FD + fcol];
+    exh = i == NC ? Ef[fcol + 1] : 0.0;
+    eyh = (jr == TJ - 1) ? Ef[FD + fcol + NF] : 0.0;
+  }
   double mu, dcv;
-  double cmax = -HUGE_VAL, smax = -HUGE_VAL, cmin = 1e100;
+  double cmax = -HUGE_VAL, smax = -HUGE_VAL, cmin = 1e100, rmax = 0.0;
   // z low face of the box (between planes 0 and 1)
   double vz_lo, dz_lo, fz_lo;
   {
-    const double ezl = Ef[2 * FD + fcol];
+    const double ezl = PHI ? gfz * (pk - ph[cc]) : Ef[2 * FD + fcol];
     const double u = upwind_t<LIM>(A.lim, zm2, zm1, z0, zp1, ezl);
     lds_mu_dc(tdi, A.td, 0.5 * (E[cc] + E[SK + cc]) * 1e21 * N_inv, mu, dcv);
     mu = mu * N_inv;
@@ -1575,28 +1597,38 @@ __global__ void __launch_bounds__(256, AFH_FE_MINW)
                                        : g2[5 * NN + gz];
     const double ep1 = E[(k + 1) * SK + cc];
     const int fbn = k * FSK + fcol;
-    const double ezh = Ef[2 * FD + fbn];
     const int x = k * SK + cc;
     double pv[NS][NP], dv[NS];
-    auto load_states = [&]() {
 #pragma unroll
-      for (int s = 0; s < NS; s++) {
+    for (int s = 0; s < NS; s++) {
 #pragma unroll
-        for (int q = 0; q < NP; q++)
-          pv[s][q] = (s >= ns || (!SD && s == eix && q == dq)) ? 0.0
-                                                                : (U.prev[s][q] + boff)[x];
-        dv[s] = (!SD || s >= ns || s == eix) ? 0.0 : (U.der[s] + boff)[x];
+      for (int q = 0; q < NP; q++)
+        pv[s][q] = (s >= ns || (!SD && s == eix && q == dq)) ? 0.0
+                                                              : (U.prev[s][q] + boff)[x];
+      dv[s] = (!SD || s >= ns || s == eix) ? 0.0 : (U.der[s] + boff)[x];
+    }
+    // the next plane's face fields (PHI: the potential of plane k+1, raw --
+    // own cell, x-1, y-1, and x+1 / y+1 on the last column / row -- formed
+    // where the window advances, below)
+    double ezh, nexl = 0, neyl = 0, nexh = 0, neyh = 0, npk = 0;
+    if (PHI) {
+      const int cn1 = (k + 1) * SK + cc;  // own cell, plane k+1
+      npk = ph[cn1];
+      if (more) {
+        nexl = ph[cn1 - 1];
+        neyl = ph[cn1 - NG];
+        if (i == NC) nexh = ph[cn1 + 1];
+        if (jr == TJ - 1) neyh = ph[cn1 + NG];
       }
-    };
-#if !AFH_FE_LATE
-    load_states();
-#endif
-    double nexl = 0, neyl = 0, nexh = 0, neyh = 0;
-    if (more) {
-      nexl = Ef[fbn];
-      neyl = Ef[FD + fbn];
-      if (i == NC) nexh = Ef[fbn + 1];
-      if (jr == TJ - 1) neyh = Ef[FD + fbn + NF];
+      ezh = gfz * (npk - pk);
+    } else {
+      ezh = Ef[2 * FD + fbn];
+      if (more) {
+        nexl = Ef[fbn];
+        neyl = Ef[FD + fbn];
+        if (i == NC) nexh = Ef[fbn + 1];
+        if (jr == TJ - 1) neyh = Ef[FD + fbn + NF];
+      }
     }
     double pn[NPE], pe[EPE];
 #pragma unroll
@@ -1647,9 +1679,6 @@ __global__ void __launch_bounds__(256, AFH_FE_MINW)
     sd[tid] = dy;
     sf[tid] = fy;
     __syncthreads();
-#if AFH_FE_LATE
-    load_states();
-#endif
     double vyh, dyh, fyh;
     if (jr + 1 < TJ) {
       vyh = sv[tid + NC];
@@ -1714,15 +1743,23 @@ __global__ void __launch_bounds__(256, AFH_FE_MINW)
       }
       const double field = 1e21 * U.inv_N * e0;
       double Te = -1.0;
-      for (int r = 0; r < U.nr; r++) {
-        const DevReaction &R = U.reac[r];
-        double rate = rate_of<false>(U, R, field, Te);
-        double prod = 1.0;
-        for (int q = 0; q < R.n_in; q++) prod = prod * sel(dens, R.ix_in[q] - 1);
-        rate = rate * prod;
-        for (int q = 0; q < R.n_in; q++) add_at(der, R.ix_in[q] - 1, -rate);
-        for (int q = 0; q < R.n_out; q++)
-          add_at(der, R.ix_out[q] - 1, rate * R.mult_out[q]);
+      int clow = -1;
+      double clf = 0.0;
+      if (U.chem.rm) lt_loc(U.chem, field, clow, clf);
+      if constexpr (HAS_NET) {
+        net_all<NET, false>(U, field, Te, clow, clf, dens, der,
+                            std::make_index_sequence<NET::NR>{});
+      } else {
+        for (int r = 0; r < U.nr; r++) {
+          const DevReaction &R = U.reac[r];
+          double rate = rate_of<false>(U, R, field, Te, clow, clf);
+          double prod = 1.0;
+          for (int q = 0; q < R.n_in; q++) prod = prod * sel(dens, R.ix_in[q] - 1);
+          rate = rate * prod;
+          for (int q = 0; q < R.n_in; q++) add_at(der, R.ix_in[q] - 1, -rate);
+          for (int q = 0; q < R.n_out; q++)
+            add_at(der, R.ix_out[q] - 1, rate * R.mult_out[q]);
+        }
       }
       if (U.last_step) {
         const double eps = 1e-100;
@@ -1751,7 +1788,15 @@ __global__ void __launch_bounds__(256, AFH_FE_MINW)
         if (s == eix) y[s] = y[s] + div + dvy + dvz;
 #pragma unroll
       for (int s = 0; s < NS; s++)
-        if (s < ns) (U.out[s] + boff)[x] = y[s];
+        if (s < ns) st_nt<AFH_NT_UPD>(U.out[s] + boff + x, y[s]);
+      if (U.rhs) {
+        double r = 0.0;
+#pragma unroll
+        for (int s = 0; s < NS; s++)
+          if (s < ns && U.rq[s] != 0.0) r = r + U.rq[s] * y[s];
+        st_nt<AFH_NT_UPD>(U.rhs + boff + x, r);
+        rmax = fmax(rmax, fabs(r));
+      }
     }
     if (more) {
 #pragma unroll
@@ -1769,23 +1814,36 @@ __global__ void __launch_bounds__(256, AFH_FE_MINW)
     z0 = zp1;
     zp1 = zp2;
     vz_lo = vzh, dz_lo = dzh, fz_lo = fzh;
-    exl = nexl, eyl = neyl, exh = nexh, eyh = neyh;
+    if (PHI) {
+      if (more) {
+        exl = gfx * (npk - nexl);
+        eyl = gfy * (npk - neyl);
+        exh = i == NC ? gfx * (nexh - npk) : 0.0;
+        eyh = (jr == TJ - 1) ? gfy * (neyh - npk) : 0.0;
+      }
+      pk = npk;
+    } else {
+      exl = nexl, eyl = neyl, exh = nexh, eyh = neyh;
+    }
     __syncthreads();
   }
   for (int o = 32; o > 0; o >>= 1) {
     cmax = fmax(cmax, __shfl_xor(cmax, o, 64));
     smax = fmax(smax, __shfl_xor(smax, o, 64));
     cmin = fmin(cmin, __shfl_xor(cmin, o, 64));
+    rmax = fmax(rmax, __shfl_xor(rmax, o, 64));
   }
   const int lane = tid & 63, w = tid >> 6;
-  if (lane == 0) r1[w] = cmax, r2[w] = smax, r3[w] = cmin;
+  if (lane == 0) r1[w] = cmax, r2[w] = smax, r3[w] = cmin, r4[w] = rmax;
   __syncthreads();
   if (tid == 0) {
     for (int q = 1; q < NT / 64; q++)
-      cmax = fmax(cmax, r1[q]), smax = fmax(smax, r2[q]), cmin = fmin(cmin, r3[q]);
+      cmax = fmax(cmax, r1[q]), smax = fmax(smax, r2[q]), cmin = fmin(cmin, r3[q]),
+      rmax = fmax(rmax, r4[q]);
     atomicMax(&red[red_shard()], dbl_to_ord(cmax));
     atomicMax(&red[RED_SHARDS + red_shard()], dbl_to_ord(smax));
     if (U.last_step) atomicMin(&red[2 * RED_SHARDS + red_shard()], dbl_to_ord(cmin));
+    if (U.rhs) atomicMax(&U.rhs_red[red_shard()], dbl_to_ord(rmax));
   }
 }
 
@@ -2708,26 +2766,42 @@ int32_t afh_flux_update_densities(afh_fluid *f, double dt, int32_t s_deriv,
 // species slots of the fused kernel (runtime ns <= FE_MAX_SPECIES)
 constexpr int FE_MAX_SPECIES = 4;
 
-template <int NC, int NP, bool SD>
+template <int NC, int NS, int NP, bool SD, bool PHI, class NET>
 static void launch_fe(afh_tree *t, const FluxArgs &A, const UpdArgs &U,
                       const double *tdi, int l, unsigned long long *red, int wf) {
-  const dim3 grid(t->leaves.n(l) * FluxLds<NC, 256>::NTILE);
+  using G = FluxLds<NC, AFH_FE_NT>;
+  const dim3 grid(t->leaves.n(l) * G::NTILE);
   const size_t lds = 2 * sizeof(double) * A.td.n_points;
-  hipLaunchKernelGGL((k_fe_lds<NC, AFH_LIM_KOREN, FE_MAX_SPECIES, NP, SD>), grid,
-                     dim3(FluxLds<NC, 256>::NT), lds, t->stream, A, U, tdi,
-                     t->leaves.at(l), t->bsz, t->fsz, red, wf);
+  hipLaunchKernelGGL((k_fe_lds<NC, AFH_LIM_KOREN, NS, NP, SD, PHI, NET>), grid, dim3(G::NT),
+                     lds, t->stream, A, U, tdi, t->leaves.at(l), t->bsz, t->fsz, red, wf);
 }
 
+// the fused kernel's variants: previous states (1, 2), derivative state among
+// them or not, face field from phi or stored, the compiled network of the
+// 3-species air chemistry (net 1) or the generic reaction loop
 template <int NC>
 static void launch_fe_nc(afh_tree *t, const FluxArgs &A, const UpdArgs &U,
-                         const double *tdi, int l, unsigned long long *red, int wf) {
-  const bool sd = U.der_q < 0;
-  if (U.n_prev == 1)
-    sd ? launch_fe<NC, 1, true>(t, A, U, tdi, l, red, wf)
-       : launch_fe<NC, 1, false>(t, A, U, tdi, l, red, wf);
-  else
-    sd ? launch_fe<NC, 2, true>(t, A, U, tdi, l, red, wf)
-       : launch_fe<NC, 2, false>(t, A, U, tdi, l, red, wf);
+                         const double *tdi, int l, unsigned long long *red, int wf,
+                         int net) {
+  const bool sd = U.der_q < 0, phi = A.phi != nullptr;
+  const int v = (U.n_prev == 2 ? 1 : 0) | (sd ? 2 : 0) | (phi ? 4 : 0);
+#define AFH_FE_CASES(NSX, NETX)                                                    \
+  switch (v) {                                                                     \
+  case 0: launch_fe<NC, NSX, 1, false, false, NETX>(t, A, U, tdi, l, red, wf); break; \
+  case 1: launch_fe<NC, NSX, 2, false, false, NETX>(t, A, U, tdi, l, red, wf); break; \
+  case 2: launch_fe<NC, NSX, 1, true, false, NETX>(t, A, U, tdi, l, red, wf); break;  \
+  case 3: launch_fe<NC, NSX, 2, true, false, NETX>(t, A, U, tdi, l, red, wf); break;  \
+  case 4: launch_fe<NC, NSX, 1, false, true, NETX>(t, A, U, tdi, l, red, wf); break;  \
+  case 5: launch_fe<NC, NSX, 2, false, true, NETX>(t, A, U, tdi, l, red, wf); break;  \
+  case 6: launch_fe<NC, NSX, 1, true, true, NETX>(t, A, U, tdi, l, red, wf); break;   \
+  default: launch_fe<NC, NSX, 2, true, true, NETX>(t, A, U, tdi, l, red, wf); break;  \
+  }
+  if (net == 1) {
+    AFH_FE_CASES(net::Airsiglo::NS, net::Airsiglo)
+  } else {
+    AFH_FE_CASES(FE_MAX_SPECIES, void)
+  }
+#undef AFH_FE_CASES
 }
 
 extern "C" {
@@ -2782,16 +2856,15 @@ static int32_t fe_dev(afh_fluid *f, double dt, int32_t s_deriv, int32_t n_prev,
     const int ivo = f->d.species_iv[s] + s_out;
     alias |= ivo == iv || ivo == f->d.i_efld;
   }
-  // k_fe_lds is opt-in (AFH_FE_FUSED=1): it moves 56 B/cell less than the
-  // two kernels, but at the occupancy its registers allow (2 waves per SIMD)
-  // it measured 20 % slower on S1-64 (profiles/r01_fe_ab.txt)
+  // k_fe_lds is opt-in (AFH_FE_FUSED=1): it moves 64 B/cell less than the
+  // two kernels (the face fluxes, n_e and |E| are not written and read back)
   const char *fused_env = getenv("AFH_FE_FUSED");
+  const bool net_ok = f->net == 1 || (f->net == 0 && f->d.n_species <= FE_MAX_SPECIES);
   const bool fused = fused_env && atoi(fused_env) && f->d_tdi &&
                      (nc == 16 || nc == 32 || nc == 64) && !t->any_cflux &&
-                     !f->slow_rates && f->d.n_species <= FE_MAX_SPECIES && f->phi_iv == 0 &&
-                     f->rhs_iv == 0 && f->d.i_gas_dens <= 0 && f->d.i_photo <= 0 &&
-                     n_prev <= 2 && !alias && f->d.limiter == AFH_LIM_KOREN &&
-                     f->d.n_ions == 0;
+                     !f->slow_rates && net_ok && f->d.i_gas_dens <= 0 &&
+                     f->d.i_photo <= 0 && n_prev <= 2 && !alias &&
+                     f->d.limiter == AFH_LIM_KOREN && f->d.n_ions == 0;
   if (!fused) {
     // flux and update back to back on the stream (the flux maxima are not
     // needed before the update); secondary emission from ions at the walls
@@ -2801,11 +2874,10 @@ static int32_t fe_dev(afh_fluid *f, double dt, int32_t s_deriv, int32_t n_prev,
     return update_dev(f, dt, s_deriv, n_prev, s_prev, w_prev, s_out, last_step);
   }
   t->touch(iv);
-  f->touch_state(s_out);
   f->rhs_state = -1;
   if ((e = flux_prelude(f, iv, t->gc2))) return e;
   if ((e = red_init(t, 0, -HUGE_VAL)) || (e = red_init(t, 1, -HUGE_VAL)) ||
-      (e = red_init(t, 2, 1e100)))
+      (e = red_init(t, 2, 1e100)) || (U.rhs && (e = red_init(t, 4, 0.0))))
     return e;
   auto *red = reinterpret_cast<unsigned long long *>(t->scratch);
   const FluxArgs A0 = flux_args(f, iv);
@@ -2820,20 +2892,43 @@ static int32_t fe_dev(afh_fluid *f, double dt, int32_t s_deriv, int32_t n_prev,
     FluxArgs A = A0;
     for (int q = 0; q < 3; q++) {
       A.inv_dx[q] = 1 / t->lvl_dr[3 * (l - 1) + q];
+      A.gfac[q] = A.fac / t->lvl_dr[3 * (l - 1) + q];  // fac / box%dr, as the flux
       U.dt_dr[q] = dt / t->lvl_dr[3 * (l - 1) + q];
     }
     prof_begin(t, AFH_PROF_FE);
     switch (nc) {
-    case 16: launch_fe_nc<16>(t, A, U, f->d_tdi, l, red, store_flux != 0); break;
-    case 32: launch_fe_nc<32>(t, A, U, f->d_tdi, l, red, store_flux != 0); break;
-    default: launch_fe_nc<64>(t, A, U, f->d_tdi, l, red, store_flux != 0); break;
+    case 16: launch_fe_nc<16>(t, A, U, f->d_tdi, l, red, store_flux != 0, f->net); break;
+    case 32: launch_fe_nc<32>(t, A, U, f->d_tdi, l, red, store_flux != 0, f->net); break;
+    default: launch_fe_nc<64>(t, A, U, f->d_tdi, l, red, store_flux != 0, f->net); break;
     }
     prof_end(t, AFH_PROF_FE, fe_bytes * n3 * n);
     AFH_LAUNCH_CHECK("k_fe_lds");
   }
-  const int slots[3] = {0, 1, 2};
-  const bool mx[3] = {true, true, false};
-  return red_finish_n(t, last_step ? 3 : 2, slots, mx);
+  if (U.rhs) {
+    // update_dev's rhs epilogue: the ghost shell from the new state's ghost
+    // cells, then the bookkeeping of the folded rhs
+    const RhsArgs R = rhs_args(f, s_out);
+    for (int l = 1; l <= t->nlvl && f->rhs_ghosts; l++) {
+      const int n = t->leaves.n(l);
+      if (!n) continue;
+      hipLaunchKernelGGL(k_rhs_shell, dim3((t->ng * t->ng + 255) / 256, 6, n),
+                         dim3(256), 0, t->stream, U.rhs, R, t->leaves.at(l),
+                         t->bsz, t->ng);
+      AFH_LAUNCH_CHECK("k_rhs_shell");
+    }
+  }
+  f->touch_state(s_out);
+  if (U.rhs) {
+    t->touch(f->rhs_iv);
+    f->rhs_state = s_out;
+    f->rhs_snap.clear();
+    for (int v : f->rhs_vars(s_out)) f->rhs_snap.push_back(t->gen[v]);
+  }
+  int slots[4] = {0, 1}, n_fold = 2;
+  bool mx[4] = {true, true};
+  if (last_step) slots[n_fold] = 2, mx[n_fold++] = false;
+  if (U.rhs) slots[n_fold] = 4, mx[n_fold++] = true;
+  return red_finish_n(t, n_fold, slots, mx);
 }
 
 extern "C" {

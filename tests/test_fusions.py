@@ -44,7 +44,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def _s1(monkeypatch, env, config="s1"):
+def _s1(monkeypatch, env, config="s1", phi_faces=False):
     import bench
     from afh import capi
     from afh.streamer import IV
@@ -52,6 +52,8 @@ def _s1(monkeypatch, env, config="s1"):
         monkeypatch.setenv(k, v)
     c = bench.build_case(capi.hip_library(), config, 0, 0)
     c.fuse_rhs(True, ghosts=False)
+    if phi_faces:
+        c.faces_from_phi(True)
     out = {"res0": c.field_compute(0, n_vcycles=2)}
     for k in range(4):
         out["step%d" % k] = bench.unit_step(c, 1e-13, k)
@@ -330,6 +332,19 @@ def test_dpair_bitwise_s1_64(monkeypatch):
     default dpair level)."""
     a = _s1(monkeypatch, {"AFH_GSRB_DPAIR": "1"}, "s1-64")
     b = _s1(monkeypatch, {"AFH_GSRB_DPAIR": "0"}, "s1-64")
+    _same(a, b)
+
+
+@pytest.mark.parametrize("config", ["s1-64", "s1"])
+def test_fused_species_step_bitwise(config, monkeypatch):
+    """The fused forward-Euler species step (k_fe_lds: flux + update in one
+    plane march, AFH_FE_FUSED=1) as the bench runs it -- face fields from
+    phi, rhs folded into the update, the compiled 3-species network -- against
+    k_flux_lds + k_update: field solve and four unit steps (both Heun stages,
+    the chemistry limit on the second), every variable and every returned
+    limit bitwise. S1 (16^3 boxes) exercises the 16^3 tiles of the kernel."""
+    a = _s1(monkeypatch, {"AFH_FE_FUSED": "1"}, config, phi_faces=True)
+    b = _s1(monkeypatch, {"AFH_FE_FUSED": "0"}, config, phi_faces=True)
     _same(a, b)
 
 
