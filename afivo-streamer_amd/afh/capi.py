@@ -142,6 +142,10 @@ SIGNATURES = {
     "cc_get": (i32, [_VP, i32, P_f64]),
     "fc_put": (i32, [_VP, i32, P_f64]),
     "fc_get": (i32, [_VP, i32, P_f64]),
+    "tree_pack_boxes": (i32, [_VP, P_i32, i32, i32, i32, P_f64]),
+    "tree_unpack_boxes": (i32, [_VP, P_i32, i32, i32, i32, P_f64]),
+    "device_alloc": (i32, [i32, C.c_int64, C.POINTER(_VP)]),
+    "device_free": (i32, [_VP]),
     "gc_lvl": (i32, [_VP, i32, i32, i32]),
     "gc_tree": (i32, [_VP, i32, i32]),
     "restrict_tree": (i32, [_VP, i32]),

@@ -731,6 +731,49 @@ class NativeShard:
                 r.wait()
         return {q: (bi.cpu().numpy(), br.cpu().numpy()) for q, (bi, br) in bufs.items()}
 
+    def exchange_rows_dev(self, sends, device):
+        """exchange_rows with the rows as device tensors (float64, on the
+        tree's device `device`, from Tree.pack_boxes): the thread ranks hand the
+        tensors over in-process; the RCCL transport sends and receives them
+        as they are -- the box data never visit the host. Returns {rank q:
+        (ids, rows tensor)}; the received rows are complete on return."""
+        import torch
+        norm = {q: (np.ascontiguousarray(ids, np.int64), rows) for q, (ids, rows) in sends.items()}
+        if self.transport == capi.DIST_LOCAL:
+            every = self.group.allgather(self.rank, norm)
+            return {q: every[q][self.rank] for q in range(self.n)
+                    if q != self.rank and self.rank in every[q]}
+        import torch.distributed as tdist
+        cuda = tdist.get_backend() == "nccl"
+        dev = device if cuda else "cpu"
+        mine = torch.zeros((self.n, 2), dtype=torch.int64, device=dev)
+        for q, (ids, rows) in norm.items():
+            mine[q, 0], mine[q, 1] = len(ids), rows.shape[1]
+        counts = [torch.zeros_like(mine) for _ in range(self.n)]
+        tdist.all_gather(counts, mine)
+        counts = [c.cpu().numpy() for c in counts]
+        ops, bufs = [], {}
+        for q, (ids, rows) in norm.items():
+            if len(ids):
+                ops.append(tdist.P2POp(tdist.isend, torch.from_numpy(ids).to(dev), q))
+                ops.append(tdist.P2POp(tdist.isend, rows, q))
+        for q in range(self.n):
+            m, w = counts[q][self.rank]
+            if q != self.rank and m:
+                bi = torch.zeros(int(m), dtype=torch.int64, device=dev)
+                br = torch.empty((int(m), int(w)), dtype=torch.float64, device=device)
+                bufs[q] = (bi, br)
+                ops.append(tdist.P2POp(tdist.irecv, bi, q))
+                ops.append(tdist.P2POp(tdist.irecv, br, q))
+        if ops:
+            for r in tdist.batch_isend_irecv(ops):
+                r.wait()
+        if cuda:
+            # the receives complete on the communicator's stream; the
+            # library's unpack runs on the tree's
+            torch.cuda.synchronize(device)
+        return {q: (bi.cpu().numpy(), br) for q, (bi, br) in bufs.items()}
+
     def stats(self):
         n, b = C.c_int64(), C.c_int64()
         self.lib.call("dist_stats", self.h, C.byref(n), C.byref(b))

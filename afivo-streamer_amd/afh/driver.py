@@ -591,14 +591,30 @@ class Simulation:
         owner_old = np.asarray(sh.owner)
         me, n = sh.rank, sh.n
         src = [self._regrid_sources(old_topo, new_topo, sh2.owner, sh2, q) for q in range(n)]
-        # (2) the rows this rank sends: its owned boxes other ranks read
+        # (2) the rows this rank sends: its owned boxes other ranks read --
+        # on the device, the boxes packed into device tensors and sent as
+        # they are (Tree.pack_boxes, NativeShard.exchange_rows_dev); on the
+        # host (the oracle), whole-tree arrays
         t_old = self.tree
-        cc = [t_old.get_cc_local(iv) for iv in range(1, self.n_var_cell + 1)]
-        fc = [t_old.get_fc_local(iv) for iv in range(1, self.n_var_face + 1)]
+        nvc, nvf = self.n_var_cell, self.n_var_face
+        new_rows = self._row_buffers(sh)
+        tdev = new_rows
+        if new_rows is not None:
+            cc = fc = None
+            w_row = t_old.row_width(nvc, nvf)
 
-        def rows_of(gids):
-            lid = np.array([t_old.local_id(b) for b in gids], np.int64) - 1
-            return np.concatenate([a[lid].reshape(len(lid), -1) for a in cc + fc], axis=1)
+            def rows_of(gids):
+                lid = [t_old.local_id(b) for b in gids]
+                buf = new_rows(len(lid), w_row)
+                t_old.pack_boxes(lid, nvc, nvf, buf)
+                return buf
+        else:
+            cc = [t_old.get_cc_local(iv) for iv in range(1, nvc + 1)]
+            fc = [t_old.get_fc_local(iv) for iv in range(1, nvf + 1)]
+
+            def rows_of(gids):
+                lid = np.array([t_old.local_id(b) for b in gids], np.int64) - 1
+                return np.concatenate([a[lid].reshape(len(lid), -1) for a in cc + fc], axis=1)
 
         sends = {}
         for q in range(n):
@@ -607,8 +623,10 @@ class Simulation:
             ids = [b for b in src[q][1] if owner_old[b - 1] == me]
             if ids:
                 sends[q] = (np.asarray(ids, np.int64), rows_of(ids))
-        got = sh.exchange_rows(sends)
+        got = (sh.exchange_rows_dev(sends, self._torch_dev) if tdev is not None
+               else sh.exchange_rows(sends))
         self.regrid_rows_received = sum(len(v[0]) for v in got.values())
+        self.regrid_device_rows = tdev is not None
         # (3) the old boxes behind this rank's part, in a tree of their own
         W, W_old = src[me]
         space = sorted(set(W) | set(W_old))
@@ -616,6 +634,26 @@ class Simulation:
         t_ow = self._set_methods(Tree(self.lib, compact_topology(old_topo, W_old, space),
                                       self.n_var_tree, self.n_var_face, device=self.device))
         local = [b for b in W_old if owner_old[b - 1] == me or owner_old[b - 1] < 0]
+        if tdev is not None:
+            # device to device: the local boxes and the received rows into the
+            # small tree (its boxes nobody fills are read by nothing)
+            if local:
+                t_ow.unpack_boxes([pos[b] + 1 for b in local], nvc, nvf, rows_of(local))
+            for ids, rows in got.values():
+                t_ow.unpack_boxes([pos[int(b)] + 1 for b in ids], nvc, nvf, rows)
+            del got, sends
+            t_nw = t_ow.regrid(compact_topology(new_topo, W, space))
+            sh.detach()
+            self.shard = None
+            self.af = probe
+            t = self._set_methods(sh2.make_tree(self.lib, new_topo, self.n_var_tree,
+                                                self.n_var_face, device=self.device))
+            k = [pos[int(b)] + 1 for b in t.global_ids]
+            buf = new_rows(len(k), w_row)
+            t_nw.pack_boxes(k, nvc, nvf, buf)
+            t.unpack_boxes(np.arange(1, len(k) + 1), nvc, nvf, buf)
+            del buf
+            return self._regrid_finish(info, sh2, t, t_nw, t_ow, t_old)
         data = [np.full((len(space) + 1,) + a.shape[1:], np.nan) for a in cc + fc]
         if local:
             rl = rows_of(local)
@@ -656,6 +694,9 @@ class Simulation:
             out = np.full((t.n_boxes,) + a.shape[1:], np.nan)
             out[:-1] = a[k]
             t.put_fc(iv, out)
+        return self._regrid_finish(info, sh2, t, t_nw, t_ow, t_old)
+
+    def _regrid_finish(self, info, sh2, t, t_nw, t_ow, t_old):
         t_nw.close()
         t_ow.close()
         self.shard = sh2
@@ -665,6 +706,22 @@ class Simulation:
         if self.i_gas_dens and info.n_add:  # m_af_core.f90:866-869
             self._set_gas([b for l in sorted(info.add) for b in info.add[l]])
         return info
+
+    def _row_buffers(self, sh):
+        """How the rank-local regrid allocates its box rows when the boxes can
+        move device to device (the HIP library on a GPU), else None: torch
+        device tensors under the RCCL transport (its send / receive take
+        them), library device buffers (model.DeviceRows) for thread ranks."""
+        from .model import DeviceRows
+        self._torch_dev = None
+        if self.device < 0 or not self.lib.has("tree_pack_boxes"):
+            return None
+        if sh.transport == capi.DIST_LOCAL:
+            lib, dev = self.lib, self.device
+            return lambda n, w: DeviceRows(lib, dev, n, w)
+        import torch
+        self._torch_dev = torch.device("cuda", self.device)
+        return lambda n, w: torch.empty((n, w), dtype=torch.float64, device=self._torch_dev)
 
     def _set_methods(self, t):
         neumann0 = [(capi.BC_NEUMANN, 0.0)] * 6

@@ -58,6 +58,35 @@ def tree_desc(topo, n_var_cell, n_var_face, box_capacity=0):
     return d, (meta, lists)
 
 
+class DeviceRows:
+    """An (n, w) float64 array in device memory owned by the library
+    (afh_device_alloc): the row buffer of Tree.pack_boxes / unpack_boxes when
+    no torch device tensor is used (the thread ranks of one process)."""
+
+    def __init__(self, lib, device, n, w):
+        self.lib, self.shape = lib, (int(n), int(w))
+        p = C.c_void_p()
+        lib.call("device_alloc", int(device), 8 * self.shape[0] * self.shape[1], C.byref(p))
+        self._p = p
+
+    def data_ptr(self):
+        return self._p.value or 0
+
+    def is_contiguous(self):
+        return True
+
+    def close(self):
+        if self._p:
+            self.lib.call("device_free", self._p)
+            self._p = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class Tree:
     """af_t: topology + device box pool of n_var_cell / n_var_face variables."""
 
@@ -199,6 +228,28 @@ class Tree:
         a = np.empty(self.cc_shape)
         self.lib.call("cc_get", self.h, iv, a.ctypes.data_as(capi.P_f64))
         return self._to_global(a)
+
+    def row_width(self, n_cc, n_fc):
+        """Doubles per box row of pack_boxes / unpack_boxes."""
+        return (n_cc * int(np.prod(self.cc_shape[1:])) +
+                n_fc * int(np.prod(self.fc_shape[1:])))
+
+    def pack_boxes(self, lids, n_cc, n_fc, buf):
+        """Boxes `lids` (local ids, 1-based) into the rows of `buf`, a
+        contiguous float64 device tensor of len(lids) x row_width(n_cc, n_fc)
+        on the tree's device: cell variables 1..n_cc, then face variables
+        1..n_fc (afh_tree_pack_boxes; no host copy)."""
+        ids = np.ascontiguousarray(lids, np.int32)
+        assert buf.is_contiguous() and tuple(buf.shape) == (len(ids), self.row_width(n_cc, n_fc))
+        self.lib.call("tree_pack_boxes", self.h, ids.ctypes.data_as(capi.P_i32), len(ids),
+                      n_cc, n_fc, C.cast(buf.data_ptr(), capi.P_f64))
+
+    def unpack_boxes(self, lids, n_cc, n_fc, buf):
+        """The rows of `buf` into boxes `lids` (afh_tree_unpack_boxes)."""
+        ids = np.ascontiguousarray(lids, np.int32)
+        assert buf.is_contiguous() and tuple(buf.shape) == (len(ids), self.row_width(n_cc, n_fc))
+        self.lib.call("tree_unpack_boxes", self.h, ids.ctypes.data_as(capi.P_i32), len(ids),
+                      n_cc, n_fc, C.cast(buf.data_ptr(), capi.P_f64))
 
     def get_cc_local(self, iv):
         """The stored boxes' array (a sharded tree's local ids; the unused

@@ -1478,8 +1478,8 @@ void launch_update(const UpdArgs &A, afh_tree *t, int l, int n_boxes,
 #ifndef AFH_FE_NT  // threads of a k_fe_lds workgroup (NC * rows)
 #define AFH_FE_NT 256
 #endif
-#ifndef AFH_FE_MINW
-#define AFH_FE_MINW 2
+#ifndef AFH_FE_MINW  // 3 waves per SIMD: every variant fits 168 VGPRs unspilled
+#define AFH_FE_MINW 3
 #endif
 template <int NC, int LIM, int NS, int NP, bool SD, bool PHI = false, class NET = void,
           int NTT = AFH_FE_NT>
@@ -2856,11 +2856,17 @@ static int32_t fe_dev(afh_fluid *f, double dt, int32_t s_deriv, int32_t n_prev,
     const int ivo = f->d.species_iv[s] + s_out;
     alias |= ivo == iv || ivo == f->d.i_efld;
   }
-  // k_fe_lds is opt-in (AFH_FE_FUSED=1): it moves 64 B/cell less than the
-  // two kernels (the face fluxes, n_e and |E| are not written and read back)
+  // k_fe_lds moves 64 B/cell less than the two kernels (the face fluxes, n_e
+  // and |E| are not written and read back). S1-64 unit steps, alternating
+  // on one box (profiles/r05_fe_ab.txt): 13.03 ms with the two
+  // kernels, 12.59 fused for Heun's first stage only, 12.00 fused for both
+  // -- the default (AFH_FE_FUSED unset or 1) on 64^3 boxes; 2: also on
+  // 16^3 / 32^3 boxes (S1: no faster); 0: never
   const char *fused_env = getenv("AFH_FE_FUSED");
+  const int fe_mode = fused_env ? atoi(fused_env) : 1;
   const bool net_ok = f->net == 1 || (f->net == 0 && f->d.n_species <= FE_MAX_SPECIES);
-  const bool fused = fused_env && atoi(fused_env) && f->d_tdi &&
+  const bool policy = fe_mode == 2 || (fe_mode == 1 && nc == 64);
+  const bool fused = policy && f->d_tdi &&
                      (nc == 16 || nc == 32 || nc == 64) && !t->any_cflux &&
                      !f->slow_rates && net_ok && f->d.i_gas_dens <= 0 &&
                      f->d.i_photo <= 0 && n_prev <= 2 && !alias &&

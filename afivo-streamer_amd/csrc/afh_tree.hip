@@ -1056,6 +1056,84 @@ int32_t afh_fc_get(afh_tree *t, int32_t ivf, double *h) {
   return AFH_OK;
 }
 
+// Box rows in device memory: row r of buf = box ids[r]'s cell-centred
+// variables 1..n_cc, then its face variables 1..n_fc (the host arrays'
+// per-box layout). One launch per variable, a block row per box.
+__global__ void k_box_rows(double *__restrict__ v, double *__restrict__ buf,
+                           const int32_t *__restrict__ ids, size_t blk, size_t row_w,
+                           size_t off, int unpack) {
+  const int r = blockIdx.y;
+  double *b = buf + (size_t)r * row_w + off;
+  double *c = v + (size_t)(ids[r] - 1) * blk;
+  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < blk;
+       e += (size_t)gridDim.x * blockDim.x) {
+    if (unpack) c[e] = b[e];
+    else b[e] = c[e];
+  }
+}
+
+static int32_t box_rows(afh_tree *t, const int32_t *ids, int32_t n, int32_t n_cc,
+                        int32_t n_fc, double *buf, int unpack) {
+  if (!t || n < 0 || (n && (!ids || !buf)) || n_cc < 0 || n_cc > t->nvc || n_fc < 0 ||
+      n_fc > t->nvf)
+    return set_error(AFH_ERR_ARG, "afh_tree_%spack_boxes: bad argument", unpack ? "un" : "");
+  for (int r = 0; r < n; r++)
+    if (ids[r] < 1 || ids[r] > t->nb)
+      return set_error(AFH_ERR_ARG, "afh_tree_%spack_boxes: box %d", unpack ? "un" : "", ids[r]);
+  if (!n) return AFH_OK;
+  int32_t *d_ids = nullptr;
+  AFH_HIP(hipMalloc(&d_ids, sizeof(int32_t) * n));
+  AFH_HIP(hipMemcpyAsync(d_ids, ids, sizeof(int32_t) * n, hipMemcpyHostToDevice, t->stream));
+  const size_t row_w = (size_t)n_cc * t->bsz + (size_t)n_fc * t->fsz;
+  for (int q = 0; q < n_cc + n_fc; q++) {
+    const bool cc = q < n_cc;
+    const size_t blk = cc ? t->bsz : t->fsz;
+    const size_t off = cc ? (size_t)q * t->bsz : (size_t)n_cc * t->bsz + (size_t)(q - n_cc) * t->fsz;
+    double *v = cc ? t->ccv(q + 1) : t->fcv(q - n_cc + 1);
+    if (unpack && cc) t->touch(q + 1);
+    const int gx = (int)std::min<size_t>((blk + 255) / 256, 64);
+    for (int r0 = 0; r0 < n; r0 += 65535) {
+      const int nr = std::min(65535, n - r0);
+      hipLaunchKernelGGL(k_box_rows, dim3(gx, nr), dim3(256), 0, t->stream, v,
+                         buf + (size_t)r0 * row_w, d_ids + r0, blk, row_w, off, unpack);
+      AFH_LAUNCH_CHECK("k_box_rows");
+    }
+  }
+  const hipError_t e = hipStreamSynchronize(t->stream);
+  hipFree(d_ids);
+  if (e != hipSuccess) return check_hip(e, "k_box_rows");
+  return AFH_OK;
+}
+
+int32_t afh_tree_pack_boxes(afh_tree *t, const int32_t *ids, int32_t n, int32_t n_cc,
+                            int32_t n_fc, double *buf) {
+  AFH_LIVE(t, "afh_tree_pack_boxes");
+  return box_rows(t, ids, n, n_cc, n_fc, buf, 0);
+}
+
+int32_t afh_tree_unpack_boxes(afh_tree *t, const int32_t *ids, int32_t n, int32_t n_cc,
+                              int32_t n_fc, const double *buf) {
+  AFH_LIVE(t, "afh_tree_unpack_boxes");
+  return box_rows(t, ids, n, n_cc, n_fc, const_cast<double *>(buf), 1);
+}
+
+int32_t afh_device_alloc(int32_t device, int64_t n_bytes, void **out) {
+  if (!out || n_bytes < 0) return set_error(AFH_ERR_ARG, "afh_device_alloc: bad argument");
+  *out = nullptr;
+  int cur = 0;
+  AFH_HIP(hipGetDevice(&cur));
+  AFH_HIP(hipSetDevice(device));
+  const hipError_t e = hipMalloc(out, n_bytes > 0 ? (size_t)n_bytes : 8);
+  hipSetDevice(cur);
+  if (e != hipSuccess) return check_hip(e, "afh_device_alloc");
+  return AFH_OK;
+}
+
+int32_t afh_device_free(void *p) {
+  if (p) AFH_HIP(hipFree(p));
+  return AFH_OK;
+}
+
 int32_t afh_gc_lvl(afh_tree *t, int32_t lvl, int32_t iv, int32_t corners) {
   AFH_LIVE(t, "afh_gc_lvl");
   if (!t || lvl < 1 || lvl > t->nlvl || iv < 1 || iv > t->nvc ||

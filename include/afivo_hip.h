@@ -257,6 +257,25 @@ int32_t afh_cc_put(afh_tree *t, int32_t iv, const double *host);
 int32_t afh_cc_get(afh_tree *t, int32_t iv, double *host);
 int32_t afh_fc_put(afh_tree *t, int32_t ivf, const double *host);
 int32_t afh_fc_get(afh_tree *t, int32_t ivf, double *host);
+/* Whole boxes in device memory, for moving boxes between trees and ranks
+ * without a host round trip (the rank-local regrid's box exchange,
+ * afivo-streamer_amd/afh/driver.py _regrid_rank_local, which replaces the
+ * whole-tree gather of af_adjust_refinement's data movement,
+ * m_af_core.f90:842-881). Row r of `buf` (n_cc * (nc+2)^3 + n_fc * 3 (nc+1)^3
+ * doubles) holds box ids[r] (local ids, 1-based, host array): its cell-centred
+ * variables 1..n_cc, then its face variables 1..n_fc, ghost cells included --
+ * the per-box layout of the afh_cc_get / afh_fc_get host arrays. `buf` is
+ * device memory on the tree's device; the call returns when the copies are
+ * done. */
+int32_t afh_tree_pack_boxes(afh_tree *t, const int32_t *ids, int32_t n, int32_t n_cc,
+                            int32_t n_fc, double *buf);
+int32_t afh_tree_unpack_boxes(afh_tree *t, const int32_t *ids, int32_t n, int32_t n_cc,
+                              int32_t n_fc, const double *buf);
+/* Device memory for such rows when the caller has no device allocator of
+ * its own (the thread ranks of AFH_DIST_LOCAL): n_bytes on `device`
+ * (the calling thread's current device is left as it was). */
+int32_t afh_device_alloc(int32_t device, int64_t n_bytes, void **out);
+int32_t afh_device_free(void *p);
 
 /* af_gc_lvl / af_gc_tree (m_af_ghostcell.f90:25-61) */
 int32_t afh_gc_lvl(afh_tree *t, int32_t lvl, int32_t iv, int32_t corners);

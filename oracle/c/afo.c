@@ -308,6 +308,47 @@ int32_t afo_fc_get(afh_tree *t, int32_t ivf, double *h) {
   return AFH_OK;
 }
 
+/* afh_tree_pack_boxes / afh_tree_unpack_boxes (include/afivo_hip.h): the
+ * boxes' rows in caller memory (host memory here), same row layout */
+static int32_t box_rows(afh_tree *t, const int32_t *ids, int32_t n, int32_t n_cc,
+                        int32_t n_fc, double *buf, int unpack) {
+  LIVE(t);
+  if (n < 0 || (n && (!ids || !buf)) || n_cc < 0 || n_cc > t->nvc || n_fc < 0 ||
+      n_fc > t->nvf)
+    return fail(AFH_ERR_ARG, "bad box rows");
+  const size_t w = (size_t)n_cc * t->bsz + (size_t)n_fc * t->fsz;
+  for (int r = 0; r < n; r++) {
+    if (ids[r] < 1 || ids[r] > t->nb) return fail(AFH_ERR_ARG, "bad box id");
+    double *b = buf + (size_t)r * w;
+    for (int q = 0; q < n_cc + n_fc; q++) {
+      const size_t blk = q < n_cc ? t->bsz : t->fsz;
+      double *c = q < n_cc ? ccb(t, q + 1, ids[r]) : fcb(t, q - n_cc + 1, ids[r]);
+      if (unpack) memcpy(c, b, sizeof(double) * blk);
+      else memcpy(b, c, sizeof(double) * blk);
+      b += blk;
+    }
+  }
+  return AFH_OK;
+}
+int32_t afo_tree_pack_boxes(afh_tree *t, const int32_t *ids, int32_t n, int32_t n_cc,
+                            int32_t n_fc, double *buf) {
+  return box_rows(t, ids, n, n_cc, n_fc, buf, 0);
+}
+int32_t afo_tree_unpack_boxes(afh_tree *t, const int32_t *ids, int32_t n, int32_t n_cc,
+                              int32_t n_fc, const double *buf) {
+  return box_rows(t, ids, n, n_cc, n_fc, (double *)buf, 1);
+}
+int32_t afo_device_alloc(int32_t device, int64_t n_bytes, void **out) {
+  (void)device;
+  if (!out || n_bytes < 0) return fail(AFH_ERR_ARG, "bad allocation");
+  *out = malloc(n_bytes > 0 ? (size_t)n_bytes : 8);
+  return *out ? AFH_OK : fail(AFH_ERR_DEVICE, "out of memory");
+}
+int32_t afo_device_free(void *p) {
+  free(p);
+  return AFH_OK;
+}
+
 /* ------------------------------------------------------------ ghost cells */
 
 /* copy_from_nb, m_af_ghostcell.f90:654-669 */

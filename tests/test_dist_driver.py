@@ -134,6 +134,9 @@ def _run_loop(lib, world, n_steps, device=-1, gather=False, monkeypatch=None):
         nb = int(clones[0].af.topology()["n_boxes"])
         got = [sim.regrid_rows_received for sim in clones]
         assert all(g < nb for g in got), (got, nb)
+        # on the GPU the boxes moved device to device (Tree.pack_boxes,
+        # NativeShard.exchange_rows_dev), never through host arrays
+        assert all(sim.regrid_device_rows == (device >= 0) for sim in clones)
     if device >= 0:
         # the sharded V-cycles ran as segment graphs between their exchanges
         # (afh_mg.hip vcycle_segments), all ranks alike

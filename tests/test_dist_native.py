@@ -25,6 +25,7 @@ import pytest
 from afh import capi
 import golden
 from afh.dist import NativeGroup, NativeShard, Partition, rccl_comm
+from afh.model import Tree
 from afh.streamer import FV, IV
 from test_dist import CC_VARS, FV, TOPOS, _run
 
@@ -373,6 +374,119 @@ def test_exchange_rows_gloo(tmp_path):
             np.testing.assert_array_equal(d["ids%d" % q], np.arange(m) + 100 * q)
             np.testing.assert_array_equal(
                 d["rows%d" % q], np.arange(4 * m, dtype=np.float64).reshape(m, 4) + 1000 * q + r)
+
+
+
+def _p2p_dev_worker(rank, world, port, outdir):
+    import os
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # NativeShard.exchange_rows_dev's RCCL path with the rows as tensors
+        # (CPU tensors under gloo; the tree's device tensors under nccl)
+        sh = type("S", (), {"transport": capi.DIST_RCCL, "n": world, "rank": rank})()
+        sends = {}
+        for q in range(rank + 1, world):
+            m = q + rank
+            sends[q] = (np.arange(m) + 100 * rank,
+                        torch.arange(4 * m, dtype=torch.float64).reshape(m, 4) + 1000 * rank + q)
+        got = NativeShard.exchange_rows_dev(sh, sends, torch.device("cpu"))
+        np.savez(os.path.join(outdir, "p%d.npz" % rank),
+                 **{"ids%d" % q: g[0] for q, g in got.items()},
+                 **{"rows%d" % q: g[1].numpy() for q, g in got.items()})
+    finally:
+        dist.destroy_process_group()
+
+
+def test_exchange_rows_dev_gloo(tmp_path):
+    """The device-tensor form of the rank-local regrid's exchange: the same
+    deliveries as exchange_rows, the rows staying tensors."""
+    import torch.multiprocessing as mp
+    from test_dist import _free_port
+    world = 3
+    mp.start_processes(_p2p_dev_worker, args=(world, _free_port(), str(tmp_path)),
+                       nprocs=world, start_method="spawn", join=True)
+    for r in range(world):
+        d = np.load(tmp_path / ("p%d.npz" % r))
+        assert sorted(k for k in d.files if k.startswith("ids")) == \
+            ["ids%d" % q for q in range(r) if q + r > 0]
+        for q in range(r):
+            m = r + q
+            if not m:
+                continue
+            np.testing.assert_array_equal(d["ids%d" % q], np.arange(m) + 100 * q)
+            np.testing.assert_array_equal(
+                d["rows%d" % q], np.arange(4 * m, dtype=np.float64).reshape(m, 4) + 1000 * q + r)
+
+
+class _HostRows:
+    """A numpy array as Tree.pack_boxes' buffer (the oracle's "device" is
+    the host)."""
+
+    def __init__(self, n, w):
+        self.a = np.zeros((n, w))
+        self.shape = self.a.shape
+
+    def data_ptr(self):
+        return self.a.ctypes.data
+
+    def is_contiguous(self):
+        return True
+
+
+def _pack_roundtrip(lib, rows):
+    topo = TOPOS["amr8"]()
+    rng = np.random.default_rng(5)
+    dev = 0 if rows is not _HostRows else -1
+    ta, tb = Tree(lib, topo, 3, 2, device=dev), Tree(lib, topo, 3, 2, device=dev)
+    try:
+        cc = [rng.standard_normal(ta.cc_shape) for _ in range(3)]
+        fc = [rng.standard_normal(ta.fc_shape) for _ in range(2)]
+        for iv in range(3):
+            ta.put_cc(iv + 1, cc[iv])
+        for iv in range(2):
+            ta.put_fc(iv + 1, fc[iv])
+        src = np.array([3, 1, 7, 2], np.int32)
+        dst = np.array([5, 4, 1, 8], np.int32)
+        buf = rows(len(src), ta.row_width(2, 1))
+        ta.pack_boxes(src, 2, 1, buf)
+        if rows is _HostRows:  # the row layout: cc 1, cc 2, fc 1 of each box
+            w = int(np.prod(ta.cc_shape[1:]))
+            for r, b in enumerate(src):
+                assert np.array_equal(buf.a[r, :w], cc[0][b - 1].ravel())
+                assert np.array_equal(buf.a[r, w:2 * w], cc[1][b - 1].ravel())
+                assert np.array_equal(buf.a[r, 2 * w:], fc[0][b - 1].ravel())
+        tb.unpack_boxes(dst, 2, 1, buf)
+        got0, got1, gotf = tb.get_cc(1), tb.get_cc(2), tb.get_fc(1)
+        for b, d in zip(src, dst):
+            assert np.array_equal(got0[d - 1], cc[0][b - 1])
+            assert np.array_equal(got1[d - 1], cc[1][b - 1])
+            assert np.array_equal(gotf[d - 1], fc[0][b - 1])
+        rest = np.setdiff1d(np.arange(1, tb.n_boxes + 1), dst) - 1
+        assert not got0[rest].any() and not gotf[rest].any() and not tb.get_cc(3).any()
+    finally:
+        ta.close()
+        tb.close()
+
+
+def test_tree_pack_unpack_boxes_oracle():
+    """afo_tree_pack_boxes / afo_tree_unpack_boxes: the row layout (each
+    box's cell variables, then its face variables, ghost cells included) and
+    the round trip into other boxes of another tree, the rest untouched."""
+    _pack_roundtrip(capi.oracle_library(), _HostRows)
+
+
+@pytest.mark.gpu
+def test_tree_pack_unpack_boxes_roundtrip():
+    """The same through device rows of the library's own allocation
+    (afh_device_alloc, model.DeviceRows): boxes of one tree into other boxes
+    of another without a host copy, every variable bitwise."""
+    from afh.model import DeviceRows
+    lib = capi.hip_library()
+    _pack_roundtrip(lib, lambda n, w: DeviceRows(lib, 0, n, w))
 
 
 @pytest.mark.gpu

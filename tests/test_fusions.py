@@ -338,12 +338,13 @@ def test_dpair_bitwise_s1_64(monkeypatch):
 @pytest.mark.parametrize("config", ["s1-64", "s1"])
 def test_fused_species_step_bitwise(config, monkeypatch):
     """The fused forward-Euler species step (k_fe_lds: flux + update in one
-    plane march, AFH_FE_FUSED=1) as the bench runs it -- face fields from
+    plane march; AFH_FE_FUSED=2: every eligible step, both Heun stages; the
+    default runs it for the first) as the bench runs it -- face fields from
     phi, rhs folded into the update, the compiled 3-species network -- against
     k_flux_lds + k_update: field solve and four unit steps (both Heun stages,
     the chemistry limit on the second), every variable and every returned
     limit bitwise. S1 (16^3 boxes) exercises the 16^3 tiles of the kernel."""
-    a = _s1(monkeypatch, {"AFH_FE_FUSED": "1"}, config, phi_faces=True)
+    a = _s1(monkeypatch, {"AFH_FE_FUSED": "2"}, config, phi_faces=True)
     b = _s1(monkeypatch, {"AFH_FE_FUSED": "0"}, config, phi_faces=True)
     _same(a, b)
 

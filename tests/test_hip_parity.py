@@ -132,11 +132,11 @@ FE_STEPS = [(0, [0], [1.0], 1), (1, [0, 1], [0.5, 0.5], 0), (1, [0], [1.0], 2),
             (2, [0, 1], [0.25, 0.75], 1), (1, [1], [1.0], 1)]
 
 
-@pytest.mark.parametrize("fused", ["0", "1"])
+@pytest.mark.parametrize("fused", ["0", "2"])
 @pytest.mark.parametrize("store", [0, 1])
 @pytest.mark.parametrize("name", ["uni16_l3", "uni32_l2", "uni64_l2", "amr16"])
 def test_forward_euler_equals_oracle(hip, oracle, name, store, fused, monkeypatch):
-    """afh_fluid_forward_euler (with AFH_FE_FUSED=1: k_fe_lds on trees
+    """afh_fluid_forward_euler (with AFH_FE_FUSED=2: k_fe_lds on trees
     without coarse-fine flux corrections) gives the bits of the oracle's
     flux_upwind_tree + flux_update_densities: every species state, the dt
     limits, and with store_flux the face fluxes."""
