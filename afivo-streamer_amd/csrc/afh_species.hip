@@ -2887,11 +2887,14 @@ static int32_t fe_dev(afh_fluid *f, double dt, int32_t s_deriv, int32_t n_prev,
     return e;
   auto *red = reinterpret_cast<unsigned long long *>(t->scratch);
   const FluxArgs A0 = flux_args(f, iv);
-  // algorithmic bytes per cell: the update's states and outputs, of which
-  // n_e(s_deriv) is the flux kernel's, + |E| and the 3 face fields (40 B,
-  // the 32 B of |E| + 3 fluxes k_update would read + the 8 B of n_e), + the
-  // 3 face fluxes with store_flux
-  const double fe_bytes = upd_bytes + (store_flux ? 24.0 : 0.0);
+  // algorithmic bytes per cell: the update's states and outputs (n_e of
+  // s_deriv among them, read once for flux and update) + |E| + the face
+  // field's input -- the 3 stored components, or phi (PHI) -- + the 3 face
+  // fluxes with store_flux. upd_bytes counts |E| + 3 fluxes (32 B): the same
+  // as |E| + 3 face-field components, 16 B more than |E| + phi. S1-64:
+  // 72 B/cell with one previous state, 96 with two.
+  const double fe_bytes =
+      upd_bytes - (f->phi_iv > 0 ? 16.0 : 0.0) + (store_flux ? 24.0 : 0.0);
   for (int l = 1; l <= t->nlvl; l++) {
     const int n = t->leaves.n(l);
     if (!n) continue;

@@ -276,16 +276,20 @@ def cpu_baseline(config, coarse, steps=2):
                       (steps, sample_lvls, ncell // nc ** 3, nc, ncell)}
 
 
-def pmc_traffic(config):
-    """HBM bytes per launch of the dominant kernel from the PMC passes
-    (scripts/pmc.sh -> scripts/pmc_summary.py -> profiles/*pmc*.json), or
-    None when no summary for this workload is committed."""
+def pmc_traffic(config, kernel="k_gsrb_pair2"):
+    """HBM bytes per launch of `kernel` from the PMC passes (scripts/pmc.sh ->
+    scripts/pmc_summary.py -> profiles/*pmc*.json, newest round first), or
+    None when no summary for this workload and kernel is committed."""
     import glob
-    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_%s.json" % config)),
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_*%s.json" % config)),
                        reverse=True):
+        if not path.endswith("_pmc_%s.json" % config) and \
+                not path.endswith("_%s.json" % config):
+            continue
         with open(path) as f:
             d = json.load(f)
-        return d.get("hbm_bytes_per_launch")
+        if kernel in d.get("kernel", "") and "hbm_bytes_per_launch" in d:
+            return d["hbm_bytes_per_launch"]
     return None
 
 
@@ -651,6 +655,21 @@ def main():
             unit_step(case, dt, args.warmup + args.steps + 2 + k)
         case.tree.sync()
         lib.call("profile_read", case.tree.h, C.byref(ms), C.byref(nl), C.byref(by))
+    # the fused species step (k_fe_lds, 64^3 boxes) over two eager unit steps
+    # after the timed region -- one Heun stage of each kind: when it takes
+    # more of a step than the smoother it is the dominant kernel of the line
+    fe = None
+    if not two_d and not sharded and CONFIGS[args.config][0] == 64:
+        lib.call("profile_enable", case.tree.h, capi.PROF_FE)
+        k0 = args.warmup + args.steps + 8
+        for k in range(2):
+            unit_step(case, dt, k0 + (k0 % 2) + k)
+        case.tree.sync()
+        fms, fnl, fby = C.c_double(), C.c_int64(), C.c_double()
+        lib.call("profile_read", case.tree.h, C.byref(fms), C.byref(fnl), C.byref(fby))
+        lib.call("profile_enable", case.tree.h, 0)
+        if fnl.value:
+            fe = (fms.value, fnl.value, fby.value)
     if roctx:
         lib.call("profile_enable", case.tree.h, 0)
         k0 = args.warmup + args.steps + 6  # even: the window starts on a Heun stage 1
@@ -717,6 +736,31 @@ def main():
             # scripts/project_scaling.py)
             "window_ns": [ns0, ns1],
         }
+        if fe is not None:
+            # the fused species step per unit step against the smoother's
+            # (its launches over the timed region): the larger is the line
+            fe_ms, fe_nl, fe_by = fe
+            pair_ms_step = ms.value / (2 if graphs else max(1, args.steps))
+            fe_ms_step = fe_ms / 2
+            fe_s = fe_ms / 1e3 / fe_nl
+            fe_ach = fe_by / fe_nl / fe_s / 1e9
+            fe_line = {"bound": "hbm",
+                       "kernel": "k_fe_lds<64> (flux + density update fused; 72 / 96 B/cell "
+                                 "for one / two previous states)",
+                       "achieved": fe_ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                       "frac": fe_ach / HBM_PEAK_GBS,
+                       "traffic": pmc_traffic(args.config, "k_fe_lds"),
+                       "avg_launch_us": fe_s * 1e6,
+                       "algorithmic_bytes_per_launch": fe_by / fe_nl, "launches": fe_nl,
+                       "ms_per_step": fe_ms_step,
+                       "timed_over": "2 eager unit steps after the timed region (one per "
+                                     "Heun stage)"}
+            out["roofline"]["ms_per_step"] = pair_ms_step
+            if fe_ms_step > pair_ms_step:
+                out["roofline_smoother"] = out["roofline"]
+                out["roofline"] = fe_line
+            else:
+                out["roofline_species"] = fe_line
         if two_d:
             # BASELINE's config 1 (streamer_2d.cfg), not the headline: its
             # roofline line is the 2-D fused pair on levels of >= 256 boxes
