@@ -836,6 +836,15 @@ __device__ __forceinline__ void net_all(const UpdArgs &A, double field, double &
   (net_one<NET, SLOW, (int)R, NT>(A, field, Te, clow, clf, dens, der), ...);
 }
 
+template <class NET>
+struct net_nr {
+  static constexpr int v = NET::NR;
+};
+template <>
+struct net_nr<void> {
+  static constexpr int v = 1;
+};
+
 // does the fluid's reaction list have network NET's structure?
 template <class NET>
 static bool net_matches(const afh_fluid_desc *d) {
@@ -1482,11 +1491,14 @@ void launch_update(const UpdArgs &A, afh_tree *t, int l, int n_boxes,
 #define AFH_FE_MINW 3
 #endif
 template <int NC, int LIM, int NS, int NP, bool SD, bool PHI = false, class NET = void,
-          int NTT = AFH_FE_NT>
+          bool WF = false, int NTT = AFH_FE_NT>
 __global__ void __launch_bounds__(NTT, AFH_FE_MINW)
     k_fe_lds(FluxArgs A, UpdArgs U, const double *__restrict__ tdi,
              const int32_t *__restrict__ ids, size_t bsz, size_t fsz,
-             unsigned long long *red, int wf) {
+             unsigned long long *red) {
+  // WF: the face fluxes are stored too (store_flux); a compile-time switch,
+  // so that no conditional store sits between a load and its wait
+  constexpr bool wf = WF;
   using G = FluxLds<NC, NTT>;
   constexpr int NG = NC + 2, NF = NC + 1, TJ = G::TJ, NT = G::NT, RW = G::RW,
                 NR = G::NR, EW = G::EW, ER = G::ER, NPE = G::NPE, EPE = G::EPE;
@@ -1517,6 +1529,18 @@ __global__ void __launch_bounds__(NTT, AFH_FE_MINW)
   const int np = A.td.n_points;
   const int eix = U.e_index, dq = U.der_q, ns = HAS_NET ? NS : U.ns;
   for (int e = tid; e < 2 * np; e += NT) T[e] = tdi[e];
+  // the network's reaction records in LDS: per-cell reads of them from
+  // global memory wait on the vector-memory counter, which drains the next
+  // plane's prefetch
+  constexpr int NRS = net_nr<NET>::v;
+  __shared__ DevReaction sreac[NRS];
+  if (HAS_NET) {
+    const int nw = (int)(sizeof(DevReaction) / sizeof(int)) * NRS;
+    for (int e = tid; e < nw; e += NT)
+      reinterpret_cast<int *>(sreac)[e] = reinterpret_cast<const int *>(U.reac)[e];
+  }
+  UpdArgs Ul = U;
+  if (HAS_NET) Ul.reac = sreac;
 
   auto ne_at = [&](int k, int e) -> double {
     if (e >= NR * RW) return 0.0;
@@ -1598,15 +1622,6 @@ __global__ void __launch_bounds__(NTT, AFH_FE_MINW)
     const double ep1 = E[(k + 1) * SK + cc];
     const int fbn = k * FSK + fcol;
     const int x = k * SK + cc;
-    double pv[NS][NP], dv[NS];
-#pragma unroll
-    for (int s = 0; s < NS; s++) {
-#pragma unroll
-      for (int q = 0; q < NP; q++)
-        pv[s][q] = (s >= ns || (!SD && s == eix && q == dq)) ? 0.0
-                                                              : (U.prev[s][q] + boff)[x];
-      dv[s] = (!SD || s >= ns || s == eix) ? 0.0 : (U.der[s] + boff)[x];
-    }
     // the next plane's face fields (PHI: the potential of plane k+1, raw --
     // own cell, x-1, y-1, and x+1 / y+1 on the last column / row -- formed
     // where the window advances, below)
@@ -1629,6 +1644,17 @@ __global__ void __launch_bounds__(NTT, AFH_FE_MINW)
         if (i == NC) nexh = Ef[fbn + 1];
         if (jr == TJ - 1) neyh = Ef[FD + fbn + NF];
       }
+    }
+    // the cell's states (used at the end of the step: issued after the
+    // loads the step's z-high face waits for)
+    double pv[NS][NP], dv[NS];
+#pragma unroll
+    for (int s = 0; s < NS; s++) {
+#pragma unroll
+      for (int q = 0; q < NP; q++)
+        pv[s][q] = (s >= ns || (!SD && s == eix && q == dq)) ? 0.0
+                                                              : (U.prev[s][q] + boff)[x];
+      dv[s] = (!SD || s >= ns || s == eix) ? 0.0 : (U.der[s] + boff)[x];
     }
     double pn[NPE], pe[EPE];
 #pragma unroll
@@ -1747,7 +1773,7 @@ __global__ void __launch_bounds__(NTT, AFH_FE_MINW)
       double clf = 0.0;
       if (U.chem.rm) lt_loc(U.chem, field, clow, clf);
       if constexpr (HAS_NET) {
-        net_all<NET, false>(U, field, Te, clow, clf, dens, der,
+        net_all<NET, false>(Ul, field, Te, clow, clf, dens, der,
                             std::make_index_sequence<NET::NR>{});
       } else {
         for (int r = 0; r < U.nr; r++) {
@@ -2772,8 +2798,14 @@ static void launch_fe(afh_tree *t, const FluxArgs &A, const UpdArgs &U,
   using G = FluxLds<NC, AFH_FE_NT>;
   const dim3 grid(t->leaves.n(l) * G::NTILE);
   const size_t lds = 2 * sizeof(double) * A.td.n_points;
-  hipLaunchKernelGGL((k_fe_lds<NC, AFH_LIM_KOREN, NS, NP, SD, PHI, NET>), grid, dim3(G::NT),
-                     lds, t->stream, A, U, tdi, t->leaves.at(l), t->bsz, t->fsz, red, wf);
+  if (wf)
+    hipLaunchKernelGGL((k_fe_lds<NC, AFH_LIM_KOREN, NS, NP, SD, PHI, NET, true>), grid,
+                       dim3(G::NT), lds, t->stream, A, U, tdi, t->leaves.at(l), t->bsz,
+                       t->fsz, red);
+  else
+    hipLaunchKernelGGL((k_fe_lds<NC, AFH_LIM_KOREN, NS, NP, SD, PHI, NET, false>), grid,
+                       dim3(G::NT), lds, t->stream, A, U, tdi, t->leaves.at(l), t->bsz,
+                       t->fsz, red);
 }
 
 // the fused kernel's variants: previous states (1, 2), derivative state among
