@@ -1490,6 +1490,7 @@ void launch_update(const UpdArgs &A, afh_tree *t, int l, int n_boxes,
 #ifndef AFH_FE_MINW  // 3 waves per SIMD: every variant fits 168 VGPRs unspilled
 #define AFH_FE_MINW 3
 #endif
+constexpr int FE_CHEM_LDS = 2048;  // rate-table doubles staged in LDS (16 KB)
 template <int NC, int LIM, int NS, int NP, bool SD, bool PHI = false, class NET = void,
           bool WF = false, int NTT = AFH_FE_NT>
 __global__ void __launch_bounds__(NTT, AFH_FE_MINW)
@@ -1541,6 +1542,17 @@ __global__ void __launch_bounds__(NTT, AFH_FE_MINW)
   }
   UpdArgs Ul = U;
   if (HAS_NET) Ul.reac = sreac;
+  // with a network, its row-major rate table too, after the transport
+  // table in the dynamic LDS (the host runs the fused step with a network
+  // only when the table fits FE_CHEM_LDS doubles): the per-cell table rows
+  // come from LDS (unconditionally, so that the compiler addresses them as
+  // LDS)
+  if constexpr (HAS_NET) {
+    double *Tc = T + 2 * np;
+    const int nch = U.chem.n_points * U.chem.n_cols;
+    for (int e = tid; e < nch; e += NT) Tc[e] = U.chem.rm[e];
+    Ul.chem.rm = Tc;
+  }
 
   auto ne_at = [&](int k, int e) -> double {
     if (e >= NR * RW) return 0.0;
@@ -2797,7 +2809,8 @@ static void launch_fe(afh_tree *t, const FluxArgs &A, const UpdArgs &U,
                       const double *tdi, int l, unsigned long long *red, int wf) {
   using G = FluxLds<NC, AFH_FE_NT>;
   const dim3 grid(t->leaves.n(l) * G::NTILE);
-  const size_t lds = 2 * sizeof(double) * A.td.n_points;
+  size_t lds = 2 * sizeof(double) * A.td.n_points;
+  if (!std::is_void<NET>::value) lds += sizeof(double) * U.chem.n_points * U.chem.n_cols;
   if (wf)
     hipLaunchKernelGGL((k_fe_lds<NC, AFH_LIM_KOREN, NS, NP, SD, PHI, NET, true>), grid,
                        dim3(G::NT), lds, t->stream, A, U, tdi, t->leaves.at(l), t->bsz,
@@ -2896,7 +2909,10 @@ static int32_t fe_dev(afh_fluid *f, double dt, int32_t s_deriv, int32_t n_prev,
   // 16^3 / 32^3 boxes (S1: no faster); 0: never
   const char *fused_env = getenv("AFH_FE_FUSED");
   const int fe_mode = fused_env ? atoi(fused_env) : 1;
-  const bool net_ok = f->net == 1 || (f->net == 0 && f->d.n_species <= FE_MAX_SPECIES);
+  // (a network's rate table is staged in the kernel's LDS)
+  const bool net_ok =
+      (f->net == 1 && f->chem.rm && f->chem.n_points * f->chem.n_cols <= FE_CHEM_LDS) ||
+      (f->net == 0 && f->d.n_species <= FE_MAX_SPECIES);
   const bool policy = fe_mode == 2 || (fe_mode == 1 && nc == 64);
   const bool fused = policy && f->d_tdi &&
                      (nc == 16 || nc == 32 || nc == 64) && !t->any_cflux &&
