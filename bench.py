@@ -661,9 +661,12 @@ def main():
     fe = None
     if not two_d and not sharded and CONFIGS[args.config][0] == 64:
         lib.call("profile_enable", case.tree.h, capi.PROF_FE)
-        k0 = args.warmup + args.steps + 8
+        # the Heun sequence continued (after the smoother's two eager steps
+        # when V-cycle graphs ran): the rhs folded by the previous update
+        # stays valid, as in the timed region
+        k0 = args.warmup + args.steps + (2 if graphs else 0)
         for k in range(2):
-            unit_step(case, dt, k0 + (k0 % 2) + k)
+            unit_step(case, dt, k0 + k)
         case.tree.sync()
         fms, fnl, fby = C.c_double(), C.c_int64(), C.c_double()
         lib.call("profile_read", case.tree.h, C.byref(fms), C.byref(fnl), C.byref(fby))
