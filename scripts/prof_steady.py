@@ -50,7 +50,7 @@ def rules(topo):
         return 8 * ns * ((np_ if np_ in (1, 2) else 2) + 1) + 32 + (8 if rhs else 0)
 
     return [
-        (r"k_gsrb_pair2<64, 64, 1, 0, true, true, true, 4[,>]", 24, "ids", small),
+        (r"k_gsrb_pair2<64, 64, 1, 4>", 24, "ids", small),
         (r"k_gsrb_pair", 24, "ids", None),
         (r"k_gsrb_v", 16, "ids", None),
         (r"k_gsrb\(", 16, "ids", split),
@@ -69,6 +69,10 @@ def rules(topo):
         (r"k_gradient", 16 if phi else 40, "all", None),
         (r"k_flux_lds|k_flux_staged", (48 if phi else 64) + 192 / nc, "leaves", None),
         (r"k_update<(\d+), \w+(?:, (\d+))?", upd, "leaves", None),
+        # the fused species step: the update's bytes less the 3 fluxes read,
+        # plus the flux's face-field input (phi: 16 B fewer than upd's 32)
+        (r"k_fe_lds<\d+, \d+, (\d+), (\d+)", lambda m: upd(m) - (16 if phi else 0),
+         "leaves", None),
         (r"k_gc_faces", 96 / nc, "ids", None),
         (r"k_gc2", 192 / nc, "leaves", None),
         (r"k_set_rhs<", 8 * (nq + 1), "leaves", None),
