@@ -195,13 +195,9 @@ namespace afh {
 // entry-point guard: a null or retired tree handle is an error
 // Workgroup lanes for a per-box launch of `work` items: the work rounded up
 // to whole waves, at most 256 (an 8^3 box's 64-cell face or 96 edge cells
-// without the idle waves of a 256-lane workgroup). AFH_BLK_FIT=0: 256.
+// without the idle waves of a 256-lane workgroup).
 inline int fit_blk(int work) {
-  static const bool on = [] {
-    const char *e = getenv("AFH_BLK_FIT");
-    return !e || atoi(e) != 0;
-  }();
-  return on && work < 256 ? ((work + 63) / 64) * 64 : 256;
+  return work < 256 ? ((work + 63) / 64) * 64 : 256;
 }
 
 inline int32_t live(const afh_tree *t, const char *what) {

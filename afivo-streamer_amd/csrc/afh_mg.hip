@@ -2996,7 +2996,6 @@ struct afh_mg {
   // an upload, a copy) smooths its top level with split half-sweeps first
   uint64_t phi_gc_gen = UINT64_MAX;
   uint64_t phi_gc_meth = UINT64_MAX;  // t->meth_gen of that fill (boundary values)
-  bool cs_fused = true;       // AFH_CS_FUSED=0: the electrode coarse solve launch per pair
   int *cs_iters = nullptr;     // pairs the last k_cs_electrode took
   // level-1 cycles of the last coarse solve (afh_mg_coarse_iterations): on
   // the device when k_cs_small applied the stopping rule, else on the host
@@ -3296,7 +3295,6 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
     mg->res_k = atoi(env) == 8 ? 8 : atoi(env) == 2 ? 2 : 4;
   if (const char *env = getenv("AFH_PROLONG_K"))
     mg->prolong_k = atoi(env) == 8 ? 8 : atoi(env) == 2 ? 2 : 4;
-  if (const char *env = getenv("AFH_CS_FUSED")) mg->cs_fused = atoi(env) != 0;
   if (const char *env = getenv("AFH_CS_ELEC_DIRECT")) mg->csd_on = atoi(env) != 0;
   if (const char *env = getenv("AFH_CS_DIRECT_SMALL")) mg->cs_direct_small = atoi(env) != 0;
   if (const char *env = getenv("AFH_PAIR_PUSH")) mg->pair_push = atoi(env) != 0;
@@ -3980,7 +3978,7 @@ __global__ void __launch_bounds__(1024)
 // with an electrode stencil and six physical faces, no sharding hook)
 static bool cs_electrode_fused(const afh_mg *mg) {
   const afh_tree *t = mg->t;
-  if (t->ids.n(1) != 1 || t->hook || (t->nc != 8 && t->nc != 16) || !mg->cs_fused)
+  if (t->ids.n(1) != 1 || t->hook || (t->nc != 8 && t->nc != 16))
     return false;
   const int id = t->h_ids[0][0];
   bool phys = mg->h_vp[id - 1] != nullptr;
