@@ -756,12 +756,13 @@ class NativeShard:
         for q, (ids, rows) in norm.items():
             if len(ids):
                 ops.append(tdist.P2POp(tdist.isend, torch.from_numpy(ids).to(dev), q))
-                ops.append(tdist.P2POp(tdist.isend, rows, q))
+                # a backend without device tensors (gloo) sends host copies
+                ops.append(tdist.P2POp(tdist.isend, rows if cuda else rows.cpu(), q))
         for q in range(self.n):
             m, w = counts[q][self.rank]
             if q != self.rank and m:
                 bi = torch.zeros(int(m), dtype=torch.int64, device=dev)
-                br = torch.empty((int(m), int(w)), dtype=torch.float64, device=device)
+                br = torch.empty((int(m), int(w)), dtype=torch.float64, device=dev)
                 bufs[q] = (bi, br)
                 ops.append(tdist.P2POp(tdist.irecv, bi, q))
                 ops.append(tdist.P2POp(tdist.irecv, br, q))
@@ -772,7 +773,7 @@ class NativeShard:
             # the receives complete on the communicator's stream; the
             # library's unpack runs on the tree's
             torch.cuda.synchronize(device)
-        return {q: (bi.cpu().numpy(), br) for q, (bi, br) in bufs.items()}
+        return {q: (bi.cpu().numpy(), br if cuda else br.to(device)) for q, (bi, br) in bufs.items()}
 
     def stats(self):
         n, b = C.c_int64(), C.c_int64()

@@ -717,6 +717,13 @@ class Simulation:
         if self.device < 0 or not self.lib.has("tree_pack_boxes"):
             return None
         if sh.transport == capi.DIST_LOCAL:
+            # a receiver's unpack reads the sender's buffer directly, so the
+            # rows stay on the device only when every thread rank of the
+            # group runs on the same GPU (no peer access is enabled); a group
+            # spread over several GPUs moves them through host arrays
+            devices = sh.allgather(self.device)
+            if len(set(devices)) != 1:
+                return None
             lib, dev = self.lib, self.device
             return lambda n, w: DeviceRows(lib, dev, n, w)
         import torch

@@ -48,6 +48,7 @@
 
 #include <algorithm>
 #include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -1764,8 +1765,19 @@ static int32_t solve_coarse_pfmg(afh_mg *mg) {
     if (lds + 64 > 160 * 1024)
       return set_error(AFH_ERR_UNSUPPORTED, "2-D pfmg: level-1 grid %d x %d", nx, ny);
     mg->pf_lds = (int)lds;
-    H2(hipFuncSetAttribute((const void *)k2_cs_pfmg,
-                           hipFuncAttributeMaxDynamicSharedMemorySize, mg->pf_lds));
+    {
+      // the attribute is per kernel, not per multigrid: only ever raised
+      static std::mutex m;
+      static std::map<int, int> top;
+      int dev = 0;
+      H2(hipGetDevice(&dev));
+      std::lock_guard<std::mutex> g(m);
+      if (mg->pf_lds > top[dev]) {
+        H2(hipFuncSetAttribute((const void *)k2_cs_pfmg,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, mg->pf_lds));
+        top[dev] = mg->pf_lds;
+      }
+    }
     for (int q = 0; q < 4; q++) mg->pf_bc[q] = M.bc[q].type;
   }
   const int nt = std::min(1024, std::max(256, (int)((n0 + 63) / 64 * 64)));

@@ -18,6 +18,9 @@
 #include <string>
 #include <array>
 #include <vector>
+#include <map>
+#include <mutex>
+#include <utility>
 
 #include "../../include/afivo_hip.h"
 
@@ -198,6 +201,23 @@ namespace afh {
 // without the idle waves of a 256-lane workgroup).
 inline int fit_blk(int work) {
   return work < 256 ? ((work + 63) / 64) * 64 : 256;
+}
+
+// hipFuncAttributeMaxDynamicSharedMemorySize is per kernel (and device), not
+// per object: several multigrids in one process each need their own LDS size,
+// so the limit is only ever raised
+inline hipError_t raise_dyn_lds(const void *f, int bytes) {
+  static std::mutex m;
+  static std::map<std::pair<int, const void *>, int> top;
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  std::lock_guard<std::mutex> g(m);
+  int &cur = top[{dev, f}];
+  if (bytes <= cur) return hipSuccess;
+  e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  if (e == hipSuccess) cur = bytes;
+  return e;
 }
 
 inline int32_t live(const afh_tree *t, const char *what) {

@@ -729,247 +729,6 @@ __global__ void __launch_bounds__((RbPar<NC, TJ>::NT))
   store_plane(k1, P[k1 & 3]);
 }
 
-// Two red-black iterations in one pass (gsrb_boxes' n_cycle = 2: one leg of
-// the V(2,2)-cycle), on a level whose boxes all have same-level or physical
-// neighbours, so that the level is one uniform grid: temporal blocking of
-// the plane march. A workgroup holds TJ rows of a box plus a halo of H = 4
-// cells in x, y and z taken from the neighbour boxes themselves
-// (neighbor_mat: their cells, never ghost cells), and runs four half-sweeps
-// as a wavefront -- in step s the red cells of plane s (iteration 1), the
-// black cells of plane s-1, the red cells of plane s-2 (iteration 2) and the
-// black cells of plane s-3 -- each on the cells whose values the next one
-// reads (halo 3, 2, 1, 0). A physical face's ghost is formed where it is
-// read, from the cells next to it (gc_face_nocopy's physical branch: the
-// fill after every half-sweep stores exactly that value, of the same cells).
-// Every cell is updated with k_gsrb's arithmetic in k_gsrb's order from the
-// same values, so the result is bitwise two pairs with their level fills,
-// at one read of phi and rhs and one write of phi (plus the halos) instead
-// of two, and without the fill between the pairs.
-// src is read (other workgroups read their halos from it), dst written: the
-// tile's rows, x ghost positions included (one contiguous run per row; the
-// level fill after the pair rewrites every face ghost of dst).
-template <int NC, int TJ>
-struct Dp {
-  static constexpr int H = 4;                        // halo cells
-  static constexpr int NG = NC + 2;
-  static constexpr int RX = NC + 2 * H, RY = TJ + 2 * H, PS = RX * RY;
-  static constexpr int NSL = 6;                      // planes s+1 .. s-4
-  static constexpr int NT = 1024;
-  static constexpr int EPT = (PS + NT - 1) / NT;     // plane entries per thread
-  // owned columns: the cells of one colour in the iteration-1 red region
-  // (halo 3): rows j0-3 .. j1+3, HC cells of the colour per row
-  static constexpr int HC = (NC + 6) / 2, NCOL = HC * (TJ + 6);
-  static constexpr int CPT = (NCOL + NT - 1) / NT;   // columns per thread
-};
-
-template <int NC, int TJ>
-__global__ void __launch_bounds__(1024)
-    k_gsrb_dpair(const double *__restrict__ src, double *__restrict__ dst,
-                 const double *__restrict__ rhs, const afh_box_meta *__restrict__ meta,
-                 const int32_t *__restrict__ ids, size_t bsz, Coef cf, double inv_c1,
-                 GcArgs ga) {
-  using D = Dp<NC, TJ>;
-  constexpr int H = D::H, NG = D::NG, RX = D::RX, PS = D::PS, NT = D::NT, EPT = D::EPT;
-  constexpr int NSL = D::NSL, HC = D::HC, NCOL = D::NCOL, CPT = D::CPT;
-  constexpr int SK = NG * NG;
-  constexpr int NTILE = NC / TJ;
-  __shared__ double P[NSL][PS];
-  __shared__ int nm[27];
-  // physical faces: the ghost of face f is gco[3f] + gco[3f+1] x1 +
-  // gco[3f+2] x2, x1 the cell next to the face, x2 the one after
-  // (gc_face_nocopy_k's physical branch)
-  __shared__ double gco[18];
-  const int tid = threadIdx.x;
-  const int wg = xcd_swizzle(blockIdx.x, gridDim.x);
-  const int id = ids[wg / NTILE];
-  const int j0 = (wg % NTILE) * TJ + 1;
-  const afh_box_meta &m = meta[id - 1];
-  if (tid < 27) nm[tid] = tid == 13 ? id : m.neighbor_mat[tid];
-  if (tid < 6) {
-    const int f = tid;
-    const afh_bc b = ga.bc[f];
-    const bool low = (f & 1) == 0;
-    double c0, c1, c2;
-    switch (b.type) {
-    case AFH_BC_DIRICHLET: c0 = 2; c1 = -1; c2 = 0; break;
-    case AFH_BC_NEUMANN: c0 = m.dr[f >> 1] * (low ? -1 : 1); c1 = 1; c2 = 0; break;
-    case AFH_BC_CONTINUOUS: c0 = 0; c1 = 2; c2 = -1; break;
-    default: c0 = 1; c1 = 0; c2 = 0; break;
-    }
-    gco[3 * f] = c0 * b.value;
-    gco[3 * f + 1] = c1;
-    gco[3 * f + 2] = c2;
-  }
-  // physical faces as bits (wave-uniform)
-  int phm = 0;
-#pragma unroll
-  for (int f = 0; f < 6; f++) phm |= (m.neighbors[f] < 0 ? 1 : 0) << f;
-  auto ghost = [&](int f, double x1, double x2) {
-    return gco[3 * f] + gco[3 * f + 1] * x1 + gco[3 * f + 2] * x2;
-  };
-  auto slot = [](int k) { return (k + 4 * NSL) % NSL; };
-  // (row-major planes; the split-parity row layout of k_gsrb_pair2 measured
-  // slower here: its index arithmetic spills)
-  auto L = [](int jj, int ii) { return jj * RX + ii; };
-  // neighbour-box selection along one axis: 0 below the box, 1 in it, 2 above
-  auto sel = [](int x) { return x < 1 ? 0 : x > NC ? 2 : 1; };
-  __syncthreads();  // nm, gco
-
-  auto load_plane = [&](int k, double (&v)[EPT]) {
-    const bool zr = !((k < 1 && (phm & 16)) || (k > NC && (phm & 32)));
-    const int sz = sel(k);
-    const int ko = (k - (sz - 1) * NC) * SK;
-#pragma unroll
-    for (int q = 0; q < EPT; q++) {
-      v[q] = 0.0;
-      const int e = tid + NT * q;
-      if (e < PS && zr) {
-        const int jj = e / RX, ii = e - jj * RX;
-        const int i = ii - (H - 1), j = j0 - H + jj;
-        const int sx = sel(i), sy = sel(j);
-        const int bid = nm[9 * sz + 3 * sy + sx];
-        if (bid > 0)
-          v[q] = src[(size_t)(bid - 1) * bsz +
-                     (size_t)(ko + (j - (sy - 1) * NC) * NG + (i - (sx - 1) * NC))];
-      }
-    }
-  };
-  auto put_plane = [&](int k, const double (&v)[EPT]) {
-    double *Pk = P[slot(k)];
-#pragma unroll
-    for (int q = 0; q < EPT; q++) {
-      const int e = tid + NT * q;
-      if (e < PS) Pk[L(e / RX, e % RX)] = v[q];
-    }
-  };
-  const int s_first = (phm & 16) ? 1 : -2, s_last = NC + 5;
-  {
-    double v[EPT];
-    load_plane(s_first - 1, v);
-    put_plane(s_first - 1, v);
-    load_plane(s_first, v);
-    put_plane(s_first, v);
-  }
-  double pre[EPT];
-  load_plane(s_first + 1, pre);
-
-  // owned columns u = tid + NT c: row j = j0 - 3 + u / HC; in step s the
-  // column i of the row whose cell of plane s is red (i + j + s odd). Every
-  // sweep of the step works on that column: red of plane s, black of s-1,
-  // red of s-2, black of s-3. rhs: plane s (red 1) and s-1 (black 1) loaded
-  // in step s; iteration 2 reuses the values loaded two steps earlier (the
-  // same column: the parity repeats), rotated through R1, R2 / B1, B2.
-  double R0[CPT], R1[CPT], R2[CPT], B0[CPT], B1[CPT], B2[CPT];
-#pragma unroll
-  for (int c = 0; c < CPT; c++) R1[c] = R2[c] = B1[c] = B2[c] = 0.0;
-  auto column = [&](int c, int s, int &i, int &j) {
-    const int u = tid + NT * c;
-    const int row = u / HC, ih = u - row * HC;
-    j = j0 - 3 + row;
-    i = -2 + 2 * ih + ((j + s + 1) & 1);
-    return u < NCOL;
-  };
-  // a real cell: inside the domain along x and y (z is checked per plane)
-  auto realxy = [&](int i, int j) {
-    return !((i < 1 && (phm & 1)) || (i > NC && (phm & 2)) || (j < 1 && (phm & 4)) ||
-             (j > NC && (phm & 8)));
-  };
-  auto realz = [&](int k) { return !((k < 1 && (phm & 16)) || (k > NC && (phm & 32))); };
-  auto rhs_at = [&](int i, int j, int k) {
-    const int sx = sel(i), sy = sel(j), sz = sel(k);
-    const int bid = nm[9 * sz + 3 * sy + sx];
-    return rhs[(size_t)(bid - 1) * bsz + (size_t)((k - (sz - 1) * NC) * SK +
-                                                  (j - (sy - 1) * NC) * NG +
-                                                  (i - (sx - 1) * NC))];
-  };
-  // rhs of step s's iteration-1 cells: red of plane s, black of s-1
-  auto rhs_step = [&](int s) {
-#pragma unroll
-    for (int c = 0; c < CPT; c++) {
-      int i, j;
-      R0[c] = B0[c] = 0.0;
-      if (column(c, s, i, j) && realxy(i, j)) {
-        if (s <= NC + 3 && realz(s)) R0[c] = rhs_at(i, j, s);
-        if (s - 1 <= NC + 2 && s - 1 >= -1 && realz(s - 1)) B0[c] = rhs_at(i, j, s - 1);
-      }
-    }
-  };
-  // the update of cell (i, j) of plane k (region halo h) with rhs r
-  auto update = [&](int i, int j, int k, int h, double r) {
-    if (i < 1 - h || i > NC + h || j < j0 - h || j > j0 + TJ - 1 + h || k < 1 - h ||
-        k > NC + h || !realz(k) || !realxy(i, j))
-      return;
-    double *Pc = P[slot(k)];
-    const double *Pm = P[slot(k - 1)], *Pp = P[slot(k + 1)];
-    const int jj = j - j0 + H, ii = i + H - 1;
-    const int ix = L(jj, ii), iw = ix - 1, ie = ix + 1;
-    const double x0 = Pc[ix];
-    const double W = (i == 1 && (phm & 1)) ? ghost(0, x0, Pc[ie]) : Pc[iw];
-    const double E = (i == NC && (phm & 2)) ? ghost(1, x0, Pc[iw]) : Pc[ie];
-    const double S = (j == 1 && (phm & 4)) ? ghost(2, x0, Pc[ix + RX]) : Pc[ix - RX];
-    const double N = (j == NC && (phm & 8)) ? ghost(3, x0, Pc[ix - RX]) : Pc[ix + RX];
-    const double Dn = (k == 1 && (phm & 16)) ? ghost(4, x0, Pp[ix]) : Pm[ix];
-    const double Up = (k == NC && (phm & 32)) ? ghost(5, x0, Pm[ix]) : Pp[ix];
-    Pc[ix] = (r - cf.c[1] * W - cf.c[2] * E - cf.c[3] * S - cf.c[4] * N - cf.c[5] * Dn -
-              cf.c[6] * Up) *
-             inv_c1;
-  };
-
-  for (int s = s_first; s <= s_last; s++) {
-    // L: plane s-5 (final) to dst, its slot <- plane s+1; prefetch s+2
-    {
-      const int ko = s - 5;
-      double *Pk = P[slot(s + 1)];
-      const bool st = ko >= 1 && ko <= NC;
-#pragma unroll
-      for (int q = 0; q < EPT; q++) {
-        const int e = tid + NT * q;
-        if (e < PS) {
-          if (st) {
-            const int jj = e / RX, ii = e - jj * RX;
-            const int i = ii - (H - 1), jr = jj - H;
-            if (jr >= 0 && jr < TJ && i >= 0 && i <= NC + 1)
-              st_nt<AFH_NT_PAIR>(dst + (size_t)(id - 1) * bsz +
-                                     (size_t)(ko * SK + (j0 + jr) * NG + i),
-                                 Pk[L(jj, ii)]);
-          }
-          Pk[L(e / RX, e % RX)] = pre[q];
-        }
-      }
-    }
-    if (s + 2 <= NC + H) load_plane(s + 2, pre);
-    rhs_step(s);
-    __syncthreads();
-#pragma unroll
-    for (int c = 0; c < CPT; c++) {
-      int i, j;
-      if (column(c, s, i, j)) update(i, j, s, 3, R0[c]);
-    }
-    __syncthreads();
-#pragma unroll
-    for (int c = 0; c < CPT; c++) {
-      int i, j;
-      if (column(c, s, i, j)) update(i, j, s - 1, 2, B0[c]);
-    }
-    __syncthreads();
-#pragma unroll
-    for (int c = 0; c < CPT; c++) {
-      int i, j;
-      if (column(c, s, i, j)) update(i, j, s - 2, 1, R2[c]);
-    }
-    __syncthreads();
-#pragma unroll
-    for (int c = 0; c < CPT; c++) {
-      int i, j;
-      if (column(c, s, i, j)) update(i, j, s - 3, 0, B2[c]);
-      R2[c] = R1[c], R1[c] = R0[c];
-      B2[c] = B1[c], B1[c] = B0[c];
-
-    }
-    __syncthreads();
-  }
-}
-
 // Whole-box form of the fused pair for small boxes (NC <= 16): the box, its
 // ghost layer included, sits in LDS ((NC+2)^3 doubles, 47 KB at NC = 16), so
 // the pair is four phases over the whole box -- A all red cells | B the red
@@ -2972,21 +2731,13 @@ struct afh_mg {
   // (default: enough boxes for one workgroup per CU, 256 tiles)
   int fused_min = 0;
   bool force_tiles = false;  // AFH_GSRB_TILES
-  bool pair_box = true;      // AFH_GSRB_PAIR_BOX=0: plane-marching pair for NC <= 16
-  // AFH_GSRB_DPAIR=1: on uniform 64^3 levels of >= 256 boxes, the two pairs
-  // of a leg one k_gsrb_dpair each instead of two k_gsrb_pair2 and the fill
-  // between them (off: 1.54 ms per launch against 2 x 0.75 ms, the step
-  // within the bimodal clock's spread; DESIGN.md, "Two iterations per pass")
-  bool dpair = false;
+  bool pair_box = true;      // false: plane-marching pair for NC <= 16
   // AFH_RCCL_CAPTURE=1: a V-cycle of a tree sharded over RCCL is captured as
   // ONE graph with its exchanges (pack, grouped send / recv, unpack) inside,
   // instead of segments between host-driven exchanges. Off until measured on
   // more than one GPU (a capture failure falls back to the eager cycle)
   bool rccl_capture = false;
-  int dpair_min = 256;  // AFH_GSRB_DPAIR_MIN (tests: smaller trees)
-  std::vector<char> lvl_uniform;  // level: every face and edge neighbour same-level or physical
-  int in_alt = 0;  // a level whose phi lives in alt between the legs of a V-cycle (dpair)
-  bool grad_nt = true;       // AFH_GRAD_NT: the gradient's face fields and |E| stored
+  bool grad_nt = true;       // the gradient's face fields and |E| stored
                              // nontemporal (streaming): -9 % on S1-64 (scripts/grad_ab.py)
   // t->gen[i_phi] when this multigrid last left phi's ghost cells current
   // (a V-cycle over all levels, or an FMG fill); anything else that writes
@@ -3066,7 +2817,7 @@ struct afh_mg {
   };
   std::map<int, Graph> graphs;
   bool use_graphs = true;
-  bool seg_graphs = true;  // sharded V-cycles as segment graphs (AFH_SEG_GRAPHS=0: eager)
+  bool seg_graphs = true;  // sharded V-cycles as segment graphs (false: eager)
   int64_t n_replays = 0, n_seg_replays = 0;  // afh_mg_graph_stats
   std::vector<char> lvl_var;  // level has variable-stencil boxes
   LevelList ids_c, ids_v, leaves_c, leaves_v, parents_c, parents_v, lsf_leaves;
@@ -3263,16 +3014,11 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
   }
   if (mg->small_lds + sizeof(CsParams) + MAXMG * 128 * sizeof(double) > 160 * 1024)
     return set_error(AFH_ERR_UNSUPPORTED, "coarse-solver LDS levels too large");
-  AFH_HIP(hipFuncSetAttribute((const void *)k_cs_small,
-                              hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)mg->small_lds));
+  AFH_HIP(raise_dyn_lds((const void *)k_cs_small, (int)mg->small_lds));
   AFH_HIP(hipMalloc(&mg->d_dtab, (size_t)MAXMG * 64 * 2 * sizeof(double)));
   if (int32_t e = build_table(mg)) return e;
   // AFH_GSRB_FUSED_MIN_BOXES: smallest level (in boxes) smoothed with the
   // fused red-black kernel; 0 disables it
-  if (const char *env = getenv("AFH_GSRB_PAIR_BOX")) mg->pair_box = atoi(env) != 0;
-  if (const char *env = getenv("AFH_GSRB_DPAIR")) mg->dpair = atoi(env) != 0;
-  if (const char *env = getenv("AFH_GSRB_DPAIR_MIN")) mg->dpair_min = atoi(env);
   if (const char *env = getenv("AFH_RCCL_CAPTURE")) mg->rccl_capture = atoi(env) != 0;
   if (const char *env = getenv("AFH_GSRB_FUSED_MIN_BOXES"))
     mg->fused_min = atoi(env);
@@ -3285,7 +3031,6 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
     mg->fused_min = t->nc >= 32 ? 64 : (t->nc <= 16 && mg->pair_box ? 1 : 256);
   if (const char *env = getenv("AFH_GSRB_TILES")) mg->force_tiles = atoi(env) != 0;
   if (const char *env = getenv("AFH_GRAPHS")) mg->use_graphs = atoi(env) != 0;
-  if (const char *env = getenv("AFH_SEG_GRAPHS")) mg->seg_graphs = atoi(env) != 0;
   if (const char *env = getenv("AFH_RSTR_COL")) mg->rstr_col = atoi(env) != 0;
   if (const char *env = getenv("AFH_RSTR_K")) {
     const int k = atoi(env);
@@ -3302,11 +3047,6 @@ int32_t afh_mg_create(afh_tree *t, const afh_mg_desc *d, afh_mg **out) {
   if (const char *env = getenv("AFH_RSTR_PUSH")) mg->rstr_push = atoi(env) != 0;
   AFH_HIP(hipMalloc(&mg->cs_iters, sizeof(int)));
   AFH_HIP(hipMalloc(&mg->d_cycles, sizeof(int)));
-  if (const char *env = getenv("AFH_GSRB_PAIR_BOX")) mg->pair_box = atoi(env) != 0;
-  if (const char *env = getenv("AFH_GSRB_DPAIR")) mg->dpair = atoi(env) != 0;
-  if (const char *env = getenv("AFH_GSRB_DPAIR_MIN")) mg->dpair_min = atoi(env);
-  if (const char *env = getenv("AFH_RCCL_CAPTURE")) mg->rccl_capture = atoi(env) != 0;
-  if (const char *env = getenv("AFH_GRAD_NT")) mg->grad_nt = atoi(env) != 0;
   if (fused_nc_ok(t->nc) && mg->fused_min > 0) {
     bool any = false;
     for (int l = 2; l <= t->nlvl; l++) any |= t->lvl_total[l - 1] >= mg->fused_min;
@@ -3547,42 +3287,6 @@ static const LevelList &cst(const afh_mg *mg, const LevelList &all,
   return mg->any_var ? c : all;
 }
 
-// k_gsrb_dpair's level: 64^3 boxes, >= 256 of them (whole boxes fill the
-// chip), constant stencils, unsharded, and a uniform grid: no box of the
-// level has a face or edge / corner neighbour missing (af_no_box) -- every
-// neighbor_mat entry is a same-level box or a physical boundary
-static bool dpair_level(afh_mg *mg, int lvl) {
-  afh_tree *t = mg->t;
-  if (!mg->dpair || t->nc != 64 || t->hook || t->lvl_total[lvl - 1] < mg->dpair_min ||
-      (mg->any_var && mg->lvl_var[lvl - 1]))
-    return false;
-  if ((int)mg->lvl_uniform.size() != t->nlvl) {
-    mg->lvl_uniform.assign(t->nlvl, 1);
-    for (int l = 1; l <= t->nlvl; l++)
-      for (int32_t id : t->h_ids[l - 1]) {
-        const afh_box_meta &b = t->boxes[id - 1];
-        for (int q = 0; q < 27; q++)
-          if (b.neighbor_mat[q] == 0) mg->lvl_uniform[l - 1] = 0;
-      }
-  }
-  return mg->lvl_uniform[lvl - 1] != 0;
-}
-
-static void launch_dpair(afh_mg *mg, int lvl, const double *src, double *dst) {
-  afh_tree *t = mg->t;
-  const int nid = t->ids.n(lvl);
-  const Coef cf = mg->lvl_c[lvl - 1];
-  constexpr int TJ = 32;
-  hipEvent_t e0 = nullptr, e1 = nullptr;
-  const bool timed = prof_ext(t, AFH_PROF_GSRB_PAIR, e0, e1);
-  launch_ev((k_gsrb_dpair<64, TJ>), e0, e1, dim3(nid * (64 / TJ)), dim3(Dp<64, TJ>::NT),
-            t->stream, src, dst, t->ccv(mg->d.i_rhs), t->d_boxes, t->ids.at(lvl), t->bsz, cf,
-            1 / cf.c[0], t->gc_args(mg->d.i_phi));
-  // phi and rhs read, phi written once = 24 B/cell for the
-  // two iterations
-  if (timed) prof_count(t, 24.0 * 64 * 64 * 64 * nid);
-}
-
 static int32_t gsrb_half(afh_mg *mg, int lvl, int n, bool corners) {
   afh_tree *t = mg->t;
   const LevelList &L = cst(mg, t->ids, mg->ids_c);
@@ -3633,15 +3337,6 @@ static int32_t gsrb_boxes(afh_mg *mg, int lvl, bool up, bool stale_ghosts = fals
   }
   double *phi = t->ccv(mg->d.i_phi);
   const afh::GcArgs ga = t->gc_args(mg->d.i_phi);
-  if (n_cycle == 2 && n0 == 1 && dpair_level(mg, lvl) &&
-      mg->in_alt == (up ? lvl : 0)) {
-    // down leg: phi -> alt (the level's phi lives in alt until the up leg);
-    // up leg: alt -> phi. The fill after: faces, corners on the up leg
-    launch_dpair(mg, lvl, up ? mg->alt : phi, up ? phi : mg->alt);
-    AFH_LAUNCH_CHECK("k_gsrb_dpair");
-    mg->in_alt = up ? 0 : lvl;
-    return gc_lvl_var(t, lvl, up ? mg->d.i_phi : 0, phi, ga, up, true);
-  }
   // the pair recomputes neighbours' red boundary cells from their rhs
   if (int32_t e = call_hook(t, AFH_HOOK_HALO, lvl, mg->d.i_rhs)) return e;
   for (int n = n0; n <= n_cycle; n++) {
@@ -3727,10 +3422,7 @@ static int32_t update_coarse(afh_mg *mg, int lvl, bool ghosts_valid = false) {
     }
     return AFH_OK;
   }
-  // the fine level's phi: in alt between the legs of a dpair level
-  const double *fine = mg->in_alt == lvl ? mg->alt : t->ccv(mg->d.i_phi);
-  if (nid && mg->in_alt == lvl && !(mg->rstr_col && hn % 2 == 0))
-    return set_error(AFH_ERR_STATE, "update_coarse: column restriction needed");
+  const double *fine = t->ccv(mg->d.i_phi);
   if (nid) {
     // column length (AFH_RSTR_K = 2, 4 or 8): a column reads 2K + 2 fine
     // planes for 2K; each doubling of K halves that excess at twice the
@@ -3828,8 +3520,7 @@ static int32_t correct_children(afh_mg *mg, int lvl) {
                          t->bsz, ga);
     AFH_LAUNCH_CHECK("k_prolong_box");
   } else if (nid) {
-    // (the level's phi in alt between the legs of a dpair level)
-    double *fphi = mg->in_alt == lvl ? mg->alt : t->ccv(mg->d.i_phi);
+    double *fphi = t->ccv(mg->d.i_phi);
     // column length 4; AFH_PROLONG_K=8 where nc allows: the launch is
     // faster (195 against 223 us on S1-64) but the pair after it slower,
     // 13.32 against 12.57-12.60 ms per step (profiles/r03_ab_prolong_k.txt)
@@ -4227,8 +3918,7 @@ static int32_t pf_prepare(afh_mg *mg) {
     const size_t lds = afh_pf::pf_lds_bytes(lv, true);
     mg->pf_lds = lds + 64 <= 160 * 1024 ? (int)lds : 0;
     if (mg->pf_lds)
-      AFH_HIP(hipFuncSetAttribute((const void *)k_cs_pfmg<true>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, mg->pf_lds));
+      AFH_HIP(raise_dyn_lds((const void *)k_cs_pfmg<true>, mg->pf_lds));
     else
       AFH_HIP(hipMalloc(&mg->d_pf_x, sizeof(double) * 4 * (size_t)np));
     mg->pf_a7.swap(a7);
@@ -4532,7 +4222,6 @@ static int32_t vcycle_body(afh_mg *mg, int32_t set_residual, int max_lvl, bool m
                            bool top_stale) {
   afh_tree *t = mg->t;
   int32_t e;
-  mg->in_alt = 0;
   for (int lvl = max_lvl; lvl >= 2; lvl--) {
     if ((e = gsrb_boxes(mg, lvl, false, top_stale && lvl == max_lvl))) return e;
     // (ghosts of the levels below valid: phi and the boundary conditions
@@ -4548,7 +4237,7 @@ static int32_t vcycle_body(afh_mg *mg, int32_t set_residual, int max_lvl, bool m
     // (a pushing correction filled the faces, and the pushing pairs read no
     // edges or corners: k_gc_corners follows the leg's last pair)
     if (!prolong_push(mg, lvl) &&
-        (e = gc_lvl_var(t, lvl, mg->in_alt == lvl ? 0 : mg->d.i_phi, t->ccv(mg->d.i_phi),
+        (e = gc_lvl_var(t, lvl, mg->d.i_phi, t->ccv(mg->d.i_phi),
                         t->gc_args(mg->d.i_phi), 1, fused_level(mg, lvl))))
       return e;
     if ((e = gsrb_boxes(mg, lvl, true))) return e;

@@ -2065,7 +2065,7 @@ struct afh_fluid {
   int e_index = -1;
   DevLT td, chem;
   // k_flux_lds: transport table interleaved per row (mu N, D N); unset when
-  // the table does not fit LDS or AFH_FLUX_STAGED=1 selects k_flux_staged
+  // the table does not fit LDS: k_flux_staged
   double *d_tdi = nullptr;
   bool slow_rates = false;  // a reaction with a temperature-dependent form
   // compiled network of the reaction list (afh_networks.h, 1-based; 0: the
@@ -2166,11 +2166,9 @@ int32_t afh_fluid_create(afh_tree *t, const afh_fluid_desc *d, afh_fluid **out) 
                       sizeof(double) * d->n_ions * (size_t)t->cap * 6 * t->nc * t->nc));
     AFH_HIP(hipMalloc(&f->d_sig, sizeof(double) * (size_t)t->cap * t->fsz));
   }
-  const char *staged_env = getenv("AFH_FLUX_STAGED");
   // a variable gas density takes k_flux_staged (per-face 1/N); so do mobile
   // ions (k_flux_staged hands the electrons' mu u to k_flux_ion)
-  if (!gas && d->n_ions == 0 && d->td.n_points <= FLUX_LDS_MAX_POINTS &&
-      !(staged_env && atoi(staged_env))) {
+  if (!gas && d->n_ions == 0 && d->td.n_points <= FLUX_LDS_MAX_POINTS) {
     const int n = d->td.n_points;
     std::vector<double> ti(2 * (size_t)n);
     for (int r = 0; r < n; r++) {

@@ -1266,10 +1266,6 @@ int32_t afh_tree_sum_cc(afh_tree *t, int32_t iv, int32_t power, double *out) {
       }
       AFH_HIP(hipStreamSynchronize(t->stream));
       hipFree(t->d_sumw);
-  for (hipStream_t &q : t->side)
-    if (q) hipStreamDestroy(q);
-  for (hipEvent_t &q : t->side_ev)
-    if (q) hipEventDestroy(q);
       t->d_sumw = nullptr;
       AFH_HIP(hipMalloc(&t->d_sumw, sizeof(double) * w.size()));
       AFH_HIP(hipMemcpy(t->d_sumw, w.data(), sizeof(double) * w.size(), hipMemcpyHostToDevice));
@@ -1373,7 +1369,6 @@ static int32_t plan_create(afh_tree *t, const int32_t *reg, int32_t n,
   AFH_LIVE(t, "afh_plan_create");
   if (!t || n < 0 || (n > 0 && !reg) || !plan || !n_values)
     return set_error(AFH_ERR_ARG, "afh_plan_create: bad argument");
-  if (n > 65535) return set_error(AFH_ERR_UNSUPPORTED, "more than 65535 regions");
   const int w = fc ? 8 : 7, lo = fc ? 2 : 1;
   const int vmin = fc ? 1 : 0, vmax = t->nc + 1;
   afh_tree::Plan p;
@@ -1425,17 +1420,22 @@ static int32_t plan_copy(afh_tree *t, int32_t plan, int32_t iv, double *buf,
   if (p.fc ? (iv < 1 || iv > t->nvf) : (iv < 0 || iv > t->nvc || (iv == 0 && !t->alt)))
     return set_error(AFH_ERR_ARG, "afh_plan_pack/unpack: bad variable");
   if (p.n == 0) return AFH_OK;
-  if (p.fc) {
-    hipLaunchKernelGGL(k_plan_copy_fc, dim3((p.max_cells + 255) / 256, p.n),
-                       dim3(256), 0, t->stream, t->fcv(iv), buf, p.d_reg, p.d_off,
-                       t->nc + 1, t->fsz, unpack);
-    AFH_LAUNCH_CHECK("k_plan_copy_fc");
-    return AFH_OK;
+  // one block row per region, in chunks of the grid's 65535 rows (a plan
+  // merges every peer's regions of an exchange)
+  for (int r0 = 0; r0 < p.n; r0 += 65535) {
+    const int nr = std::min(65535, p.n - r0);
+    if (p.fc) {
+      hipLaunchKernelGGL(k_plan_copy_fc, dim3((p.max_cells + 255) / 256, nr), dim3(256), 0,
+                         t->stream, t->fcv(iv), buf, p.d_reg + 8 * (size_t)r0, p.d_off + r0,
+                         t->nc + 1, t->fsz, unpack);
+      AFH_LAUNCH_CHECK("k_plan_copy_fc");
+    } else {
+      hipLaunchKernelGGL(k_plan_copy, dim3((p.max_cells + 255) / 256, nr), dim3(256), 0,
+                         t->stream, t->var(iv), buf, p.d_reg + 7 * (size_t)r0, p.d_off + r0,
+                         t->ng, t->bsz, unpack);
+      AFH_LAUNCH_CHECK("k_plan_copy");
+    }
   }
-  hipLaunchKernelGGL(k_plan_copy, dim3((p.max_cells + 255) / 256, p.n), dim3(256),
-                     0, t->stream, t->var(iv), buf, p.d_reg, p.d_off, t->ng,
-                     t->bsz, unpack);
-  AFH_LAUNCH_CHECK("k_plan_copy");
   return AFH_OK;
 }
 

@@ -277,6 +277,43 @@ module m_afivo_hip
        integer(c_int32_t)        :: afh_fc_get
      end function afh_fc_get
 
+     ! whole boxes as device rows (the rank-local regrid's box exchange):
+     ! buf is device memory on the tree's device (c_ptr by value)
+     function afh_tree_pack_boxes(t, ids, n, n_cc, n_fc, buf) &
+          bind(C, name=afh_pfx//"tree_pack_boxes")
+       import
+       type(c_ptr), value              :: t
+       integer(c_int32_t), intent(in)  :: ids(*)
+       integer(c_int32_t), value       :: n, n_cc, n_fc
+       type(c_ptr), value              :: buf
+       integer(c_int32_t)              :: afh_tree_pack_boxes
+     end function afh_tree_pack_boxes
+
+     function afh_tree_unpack_boxes(t, ids, n, n_cc, n_fc, buf) &
+          bind(C, name=afh_pfx//"tree_unpack_boxes")
+       import
+       type(c_ptr), value              :: t
+       integer(c_int32_t), intent(in)  :: ids(*)
+       integer(c_int32_t), value       :: n, n_cc, n_fc
+       type(c_ptr), value              :: buf
+       integer(c_int32_t)              :: afh_tree_unpack_boxes
+     end function afh_tree_unpack_boxes
+
+     ! device memory for such rows (n_bytes on `device`)
+     function afh_device_alloc(device, n_bytes, out) bind(C, name=afh_pfx//"device_alloc")
+       import
+       integer(c_int32_t), value       :: device
+       integer(c_int64_t), value       :: n_bytes
+       type(c_ptr), intent(out)        :: out
+       integer(c_int32_t)              :: afh_device_alloc
+     end function afh_device_alloc
+
+     function afh_device_free(p) bind(C, name=afh_pfx//"device_free")
+       import
+       type(c_ptr), value              :: p
+       integer(c_int32_t)              :: afh_device_free
+     end function afh_device_free
+
      function afh_gc_lvl(t, lvl, iv, corners) bind(C, name=afh_pfx//"gc_lvl")
        import
        type(c_ptr), value        :: t
@@ -851,7 +888,7 @@ contains
   !> failure (e.g. m_af_stencil.f90:338), with the library's message.
   subroutine afh_check(ierr, what)
     integer(c_int32_t), intent(in) :: ierr
-    character(len=*), intent(in)   :: what
+    character(len=*), intent(in), optional :: what
     character(kind=c_char), pointer :: msg(:)
     type(c_ptr)                     :: p
     integer                         :: n
@@ -862,7 +899,11 @@ contains
     call c_f_pointer(p, msg, [n])
     allocate(character(len=n) :: text)
     text = transfer(msg(1:n), text)
-    write(*, '(A,A,A,I0,A,A)') "afivo_hip: ", what, " failed (", ierr, "): ", text
+    if (present(what)) then
+      write(*, '(A,A,A,I0,A,A)') "afivo_hip: ", what, " failed (", ierr, "): ", text
+    else
+      write(*, '(A,I0,A,A)') "afivo_hip: call failed (", ierr, "): ", text
+    end if
     error stop "afivo_hip call failed"
   end subroutine afh_check
 

@@ -23,6 +23,7 @@ residual, which may cover every leaf level in one launch -- takes its boxes
 from the launch's grid.
 
 Usage: prof_steady.py <run_kernel_trace.csv> <K> <out.json> <topo.json>
+       prof_steady.py --rescore <summary.json> ...
 """
 import collections
 import csv
@@ -102,16 +103,39 @@ def key(name):
 # kernels whose grid is (cells of a box, boxes): one launch may cover every
 # leaf level (AFH_ALL_LVL), so the boxes are read from the launch's grid
 BOX_GRID = re.compile(r"k_update<|k_flux_staged|k_residual<")
+# the fused pair's grid is (boxes x NC/TJ row tiles x KS k-splits) workgroups
+# (afh_mg.hip launch_pair2): its boxes follow from the launch's workgroups
+PAIR2 = re.compile(r"k_gsrb_pair2<(\d+), (\d+), \d+, (\d+)>")
 
 
-def algorithmic(name, topo, grid_y=1):
+def algorithmic(name, topo, grid_y=1, groups=0):
+    """Algorithmic bytes of the launch: bytes per cell x cells. The boxes come
+    from the launch's grid where its shape gives them (BOX_GRID, PAIR2), else
+    from the level the kernel's list and filter select."""
     for pat, b, lst, filt in rules(topo):
         m = re.search(pat, name)
         if m:
             per_cell = b(m) if callable(b) else b
-            boxes = grid_y if BOX_GRID.search(name) and grid_y > 1 else largest(topo, lst, filt)
+            p2 = PAIR2.search(name)
+            if p2 and groups:
+                nc, tj, ks = (int(x) for x in p2.groups())
+                boxes = groups // ((nc // tj) * ks)
+            elif BOX_GRID.search(name) and grid_y > 1:
+                boxes = grid_y
+            else:
+                boxes = largest(topo, lst, filt)
             return per_cell * topo["nc"] ** 3 * boxes
     return None
+
+
+def guard(ent):
+    """A fraction of the HBM peak above 1 is a byte-model error, never a
+    measurement: such an entry keeps its time and loses its fraction."""
+    if ent.get("frac_of_8TBps", 0) > 1:
+        for k in ("algorithmic_bytes", "achieved_TBps", "frac_of_8TBps"):
+            ent.pop(k, None)
+        ent["frac_note"] = "byte model does not fit this launch; no fraction reported"
+    return ent
 
 
 def main(path, k_steps, out, topo_path):
@@ -134,23 +158,26 @@ def main(path, k_steps, out, topo_path):
         k = key(r["Kernel_Name"])
         d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
         g = int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
+        wg = int(r.get("Workgroup_Size_X") or 1) * int(r.get("Workgroup_Size_Y") or 1) * \
+            int(r.get("Workgroup_Size_Z") or 1)
         per[k][0] += 1
         per[k][1] += d
-        per[k][2].append((g, d, int(r["Grid_Size_Y"])))
+        per[k][2].append((g, d, int(r["Grid_Size_Y"]), g // max(wg, 1)))
     table = []
     for k, (n, tot, lst) in sorted(per.items(), key=lambda kv: -kv[1][1]):
-        gmax = max(g for g, _, _ in lst)
-        big = [d for g, d, _ in lst if g == gmax]
-        gy = max(y for g, _, y in lst if g == gmax)
+        gmax = max(g for g, _, _, _ in lst)
+        big = [d for g, d, _, _ in lst if g == gmax]
+        gy = max(y for g, _, y, _ in lst if g == gmax)
+        groups = max(w for g, _, _, w in lst if g == gmax)
         avg = sum(big) / len(big)
         ent = {"kernel": k, "launches_per_step": n / k_steps,
                "us_per_step": tot / k_steps, "share": tot * 1e3 / busy,
                "largest_launch_avg_us": avg}
-        b = algorithmic(k, topo, gy)
+        b = algorithmic(k, topo, gy, groups)
         if b:
             ent.update({"algorithmic_bytes": b, "achieved_TBps": b / (avg * 1e-6) / 1e12,
                         "frac_of_8TBps": b / (avg * 1e-6) / PEAK})
-        table.append(ent)
+        table.append(guard(ent))
     res = {"config": topo.get("config"), "nc": topo["nc"],
            "leaf_cells": topo["nc"] ** 3 * sum(topo["leaves"]),
            "boxes_per_level": topo["ids"], "leaves_per_level": topo["leaves"],
@@ -169,10 +196,22 @@ def main(path, k_steps, out, topo_path):
             e["largest_launch_avg_us"],
             ("%.2f TB/s frac %.3f" % (e["achieved_TBps"], e["frac_of_8TBps"]))
             if "achieved_TBps" in e else ""))
-    bad = [e["kernel"] for e in table if e.get("frac_of_8TBps", 0) > 1]
+    bad = [e["kernel"] for e in table if "frac_note" in e]
     if bad:
-        print("WARNING: fraction above 1 (byte model wrong) for", bad)
+        print("no fraction (the byte model does not fit the launch):", bad)
+
+
+def rescore(path):
+    """Apply the guard to a committed summary (JSON): an entry whose fraction
+    exceeds 1 keeps its times and loses the fraction."""
+    d = json.load(open(path))
+    d["kernels"] = [guard(e) for e in d["kernels"]]
+    json.dump(d, open(path, "w"), indent=1)
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], int(sys.argv[2]), sys.argv[3], sys.argv[4])
+    if sys.argv[1] == "--rescore":
+        for f in sys.argv[2:]:
+            rescore(f)
+    else:
+        main(sys.argv[1], int(sys.argv[2]), sys.argv[3], sys.argv[4])

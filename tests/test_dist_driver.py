@@ -100,6 +100,40 @@ def test_sharded_driver_hip_threads_bitwise(name, world):
     _run(capi.hip_library(), name, world, device=0)
 
 
+@pytest.mark.gpu
+def test_rccl_single_rank_photoi_sum_destroy():
+    """the first device SUM of a tree sharded over RCCL (which
+    builds the fold weights) must not touch the side streams the concurrent
+    Helmholtz modes created before it. Photoionization, then the sum, then
+    photoionization again on the same tree, then destroy: bitwise the
+    unsharded run."""
+    from afh.dist import rccl_comm
+    lib = capi.hip_library()
+    base = Simulation(lib, golden.load("rtest_test_3d_photoi_chem"), device=0)
+    base.start()
+    sim = base.clone(lib, device=0)
+    iv = base.cc_names.index("e") + 1
+
+    def run(s):
+        a = _steps(s, 1)
+        total = s.tree.sum_cc(iv)
+        return a + _steps(s, 1) + [total]
+
+    ref = run(base)
+    comm = rccl_comm(lib, 0, 1, 0)
+    try:
+        sh = NativeShard(lib, sim.af.topology(), 1, 0, transport=capi.DIST_RCCL, comm=comm)
+        sim.shard_over(sh)
+        got = run(sim)
+        phi = sim.tree.get_cc(base.cc_names.index("phi") + 1)
+        sh.detach()
+        sim.tree.close()
+    finally:
+        lib.call("dist_rccl_comm_destroy", comm)
+    assert got == ref
+    assert np.array_equal(phi, base.tree.get_cc(base.cc_names.index("phi") + 1))
+
+
 def _run_loop(lib, world, n_steps, device=-1, gather=False, monkeypatch=None):
     """The regression run test_3d sharded from its first step: the whole
     time loop -- step control, output rows, refinement every 2 steps (the
