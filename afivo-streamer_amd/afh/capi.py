@@ -196,6 +196,7 @@ SIGNATURES = {
     "plan_unpack": (i32, [_VP, i32, i32, _VP]),
     # native box sharding
     "dist_partition": (i32, [C.POINTER(TreeDesc), i32, P_i32, P_i32]),
+    "dist_partition_levels": (i32, [C.POINTER(TreeDesc), i32, C.c_int64, P_i32, P_i32]),
     "dist_plan": (i32, [C.POINTER(TreeDesc), P_i32, i32, i32, i32, i32, P_i32, i32, P_i32]),
     "dist_local_ids": (i32, [C.POINTER(TreeDesc), P_i32, i32, P_i32, i32, P_i32]),
     "tree_create_sharded": (i32, [C.POINTER(TreeDesc), P_i32, i32, i32, _PVP]),

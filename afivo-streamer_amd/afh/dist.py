@@ -131,8 +131,9 @@ def compact_topology(topo, present, space):
 class Partition:
     """Ownership of every box for n_ranks (owner -1: replicated)."""
 
-    def __init__(self, topo, n_ranks):
+    def __init__(self, topo, n_ranks, min_level_cells=0):
         self.topo = topo
+        self.min_level_cells = int(min_level_cells)
         self.n_ranks = n_ranks
         self.nc = int(topo["nc"])
         self.nb = int(topo["n_boxes"])
@@ -161,8 +162,20 @@ class Partition:
                 ch = self.children[i - 1]
                 w[i] = 1 if ch[0] == 0 else w[ch].sum()
         if nlvl < 2:
+            if self.min_level_cells > 0:
+                return
             raise ValueError("no level >= 2 has enough boxes to shard over %d ranks" % n)
-        roots = [int(i) for i in ids[2]]
+        ls = 2
+        if self.min_level_cells > 0:
+            # the frontier starts at the first level holding min_level_cells
+            # cells (and n boxes); the levels below are replicated; none such:
+            # the whole tree replicated (lp None)
+            big = [l for l in range(2, nlvl + 1)
+                   if len(ids[l]) * self.nc ** 3 >= self.min_level_cells and len(ids[l]) >= n]
+            if not big:
+                return
+            ls = big[0]
+        roots = [int(i) for i in ids[ls]]
 
         def code(b):  # Morton index of the lower corner at the finest resolution
             sh = nlvl - int(self.lvl[b - 1])
@@ -196,7 +209,7 @@ class Partition:
         if not ok:
             rk = (np.arange(len(order)) * n) // len(order)
         self.owner[np.asarray(order, np.int64) - 1] = rk
-        for l in range(3, nlvl + 1):
+        for l in range(ls + 1, nlvl + 1):
             for i in ids[l]:
                 p = self.parent[i - 1]
                 if self.owner[p - 1] >= 0:
@@ -582,7 +595,7 @@ class NativeShard:
     threads of this process) or capi.DIST_RCCL with `comm` (rccl_comm)."""
 
     def __init__(self, lib, topo, n_ranks, rank, transport=capi.DIST_LOCAL, group=None,
-                 comm=None):
+                 comm=None, min_level_cells=0):
         from .model import tree_desc
         self.lib = lib
         self.topo = topo
@@ -594,7 +607,9 @@ class NativeShard:
         self._desc, self._keep = tree_desc(topo, 1, 1)
         self.owner = np.zeros(int(topo["n_boxes"]), np.int32)
         lp = C.c_int32()
-        lib.call("dist_partition", C.byref(self._desc), n_ranks,
+        # min_level_cells: levels smaller than that replicated (afh_dist_partition_levels)
+        self.min_level_cells = int(min_level_cells)
+        lib.call("dist_partition_levels", C.byref(self._desc), n_ranks, self.min_level_cells,
                  self.owner.ctypes.data_as(capi.P_i32), C.byref(lp))
         self.lp = lp.value or None
         self.tree = None
@@ -648,7 +663,8 @@ class NativeShard:
         """A shard of a new topology (after a regrid) over the same ranks and
         transport: a fresh partition."""
         return NativeShard(self.lib, topo, self.n, self.rank, self.transport,
-                           group=self.group, comm=self.comm)
+                           group=self.group, comm=self.comm,
+                           min_level_cells=self.min_level_cells)
 
     def allgather(self, obj):
         """Every rank's obj, in rank order: the thread ranks' group (objects

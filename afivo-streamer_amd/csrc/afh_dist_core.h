@@ -62,10 +62,29 @@ inline int64_t morton3(const int32_t ix[3], int shift = 0) {
 // than ranks), its heaviest refined box is replaced by its children and
 // becomes replicated. Descendants follow their frontier box. Returns the
 // first level with an owned box, or -1.
-inline int partition(const Topo &t, int n, std::vector<int32_t> &owner) {
+//
+// min_level_cells > 0 (round 6): the frontier starts at the first level >= 2
+// whose boxes hold at least that many cells; the levels below it, leaves
+// included, are replicated -- computed by every rank, with no exchange. A
+// level smaller than that is launch-bound on one GPU already: sharding it
+// saves no kernel time and adds its exchanges. When no level
+// is that large the whole tree is replicated (returns 0: every rank computes
+// every box, as one GPU would).
+inline int partition(const Topo &t, int n, std::vector<int32_t> &owner,
+                     int64_t min_level_cells = 0) {
   owner.assign(t.nb, -1);
   if (n <= 1) return 0;
-  if (t.nlvl < 2) return -1;
+  if (t.nlvl < 2) return min_level_cells > 0 ? 0 : -1;
+  int ls = 2;
+  if (min_level_cells > 0) {
+    const int64_t box_cells = (int64_t)t.nc * t.nc * t.nc;
+    ls = 0;
+    for (int l = 2; l <= t.nlvl && !ls; l++)
+      if ((int64_t)t.ids[l - 1].size() * box_cells >= min_level_cells &&
+          (int)t.ids[l - 1].size() >= n)
+        ls = l;
+    if (!ls) return 0;
+  }
   std::vector<int64_t> w(t.nb + 1, 0);
   for (int l = t.nlvl; l >= 1; l--)
     for (int32_t i : t.ids[l - 1]) {
@@ -78,7 +97,7 @@ inline int partition(const Topo &t, int n, std::vector<int32_t> &owner) {
         w[i] = s;
       }
     }
-  std::vector<int32_t> roots = t.ids[1];
+  std::vector<int32_t> roots = t.ids[ls - 1];
   auto code = [&](int32_t b) { return morton3(t.m[b - 1].ix, t.nlvl - t.m[b - 1].lvl); };
   std::vector<int32_t> order;
   std::vector<int64_t> rk;
@@ -122,7 +141,7 @@ inline int partition(const Topo &t, int n, std::vector<int32_t> &owner) {
   if (!split(mx, total))  // every rank gets a frontier box: an even split
     for (size_t q = 0; q < order.size(); q++) rk[q] = ((int64_t)q * n) / (int64_t)order.size();
   for (size_t q = 0; q < order.size(); q++) owner[order[q] - 1] = (int32_t)rk[q];
-  for (int l = 3; l <= t.nlvl; l++)
+  for (int l = ls + 1; l <= t.nlvl; l++)
     for (int32_t i : t.ids[l - 1]) {
       const int32_t p = t.m[i - 1].parent;
       if (owner[p - 1] >= 0) owner[i - 1] = owner[p - 1];

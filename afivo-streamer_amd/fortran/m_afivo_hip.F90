@@ -680,6 +680,16 @@ module m_afivo_hip
        integer(c_int32_t)              :: afh_dist_partition
      end function afh_dist_partition
 
+     function afh_dist_partition_levels(desc, n_ranks, min_level_cells, owner, lp) &
+          bind(C, name=afh_pfx//"dist_partition_levels")
+       import
+       type(afh_tree_desc), intent(in) :: desc
+       integer(c_int32_t), value       :: n_ranks
+       integer(c_int64_t), value       :: min_level_cells
+       integer(c_int32_t), intent(out) :: owner(*), lp
+       integer(c_int32_t)              :: afh_dist_partition_levels
+     end function afh_dist_partition_levels
+
      function afh_dist_plan(desc, owner, kind, level, recv_rank, send_rank, regions, cap, n) &
           bind(C, name=afh_pfx//"dist_plan")
        import

@@ -674,6 +674,13 @@ typedef struct afh_dist afh_dist;
 typedef struct afh_dist_group afh_dist_group;
 int32_t afh_dist_partition(const afh_tree_desc *desc, int32_t n_ranks, int32_t *owner,
                            int32_t *lp);
+/* The same with a size floor (round 6): the partition frontier starts at the
+ * first level >= 2 whose boxes hold at least min_level_cells cells (and at
+ * least n_ranks boxes); the levels below it are replicated -- every rank
+ * computes them, no exchange. No such level: the whole tree is replicated
+ * (*lp = 0). min_level_cells = 0 is afh_dist_partition. */
+int32_t afh_dist_partition_levels(const afh_tree_desc *desc, int32_t n_ranks,
+                                  int64_t min_level_cells, int32_t *owner, int32_t *lp);
 int32_t afh_dist_plan(const afh_tree_desc *desc, const int32_t *owner, int32_t kind,
                       int32_t level, int32_t recv_rank, int32_t send_rank, int32_t *regions,
                       int32_t cap, int32_t *n);

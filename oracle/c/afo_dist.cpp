@@ -127,17 +127,23 @@ int32_t dist_hook(void *ctx, int32_t kind, int32_t level, int32_t iv, double *va
 
 extern "C" {
 
-int32_t afo_dist_partition(const afh_tree_desc *desc, int32_t n_ranks, int32_t *owner,
-                           int32_t *lp) {
-  if (!desc || !owner || n_ranks < 1) return fail(AFH_ERR_ARG, "afo_dist_partition");
+int32_t afo_dist_partition_levels(const afh_tree_desc *desc, int32_t n_ranks,
+                                  int64_t min_level_cells, int32_t *owner, int32_t *lp) {
+  if (!desc || !owner || n_ranks < 1 || min_level_cells < 0)
+    return fail(AFH_ERR_ARG, "afo_dist_partition");
   const Topo t = topo_of(desc);
   std::vector<int32_t> own;
-  const int l = partition(t, n_ranks, own);
+  const int l = partition(t, n_ranks, own, min_level_cells);
   if (l < 0)
     return fail(AFH_ERR_ARG, "no level >= 2 has enough boxes to shard over %d ranks", n_ranks);
   std::copy(own.begin(), own.end(), owner);
   if (lp) *lp = l;
   return AFH_OK;
+}
+
+int32_t afo_dist_partition(const afh_tree_desc *desc, int32_t n_ranks, int32_t *owner,
+                           int32_t *lp) {
+  return afo_dist_partition_levels(desc, n_ranks, 0, owner, lp);
 }
 
 int32_t afo_dist_plan(const afh_tree_desc *desc, const int32_t *owner, int32_t kind,

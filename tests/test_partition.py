@@ -148,3 +148,41 @@ def test_compact_topology_ids():
     assert t.n_boxes == n + 1
     t.close()
     assert nb > n
+
+
+@pytest.mark.parametrize("cfg,n,cells", [("s5", 8, 64 * 512), ("s5", 3, 100 * 512),
+                                         ("s4", 8, 150 * 512), ("s5", 8, 10 ** 9)])
+def test_native_partition_levels_equals_python(cfg, n, cells):
+    """The size floor (round 6): the frontier starts at the first level of at
+    least `cells` cells; everything below it is replicated, leaves included;
+    no such level: the whole tree replicated (lp None)."""
+    topo = tree(cfg)
+    part = Partition(topo, n, min_level_cells=cells)
+    sh = NativeShard(capi.oracle_library(), topo, n, 0, transport=capi.DIST_LOCAL,
+                     group=type("G", (), {"h": None})(), min_level_cells=cells)
+    np.testing.assert_array_equal(sh.owner, part.owner)
+    assert sh.lp == part.lp
+    lvl = np.asarray(topo["meta_lvl"])
+    nc3 = int(topo["nc"]) ** 3
+    big = [l for l in range(2, int(topo["highest_lvl"]) + 1)
+           if np.sum(lvl == l) * nc3 >= cells and np.sum(lvl == l) >= n]
+    if not big:
+        assert part.lp is None and np.all(part.owner < 0)
+        return
+    assert part.lp >= big[0]
+    assert np.all(part.owner[(lvl >= 1) & (lvl < big[0])] < 0)
+    loads = leaf_loads(topo, part.owner, n)
+    assert loads.min() > 0
+
+
+def test_uniform_tree_levels_floor():
+    """A uniform tree of 8^3 boxes (8, 64, 512, 4096 per level) with a floor
+    above level 2's cells: levels 1-2 replicated, the frontier on level 3
+    (512 boxes, 64 per rank)."""
+    from afh.tree import uniform_tree
+    topo = uniform_tree(8, (16, 16, 16), (2e-3, 2e-3, 2e-3), 4)
+    part = Partition(topo, 8, min_level_cells=65 * 512)
+    lvl = np.asarray(topo["meta_lvl"])
+    assert part.lp == 3
+    assert np.all(part.owner[lvl <= 2] < 0) and np.all(part.owner[lvl >= 3] >= 0)
+    assert np.bincount(part.owner[lvl == 3], minlength=8).tolist() == [64] * 8
