@@ -225,24 +225,26 @@ class Partition:
         return local_topology(self.topo, self.owner, rank)
 
     # ---------------------------------------------------------------- plans
-    def _region(self, b, d, rims):
-        """Cells of box b within DEPTH layers of the box in direction -d
+    def _region(self, b, d, rims, depth=DEPTH):
+        """Cells of box b within `depth` layers of the box in direction -d
         (b lies at direction d of the owned box); with rims, b's ghost
         layers are included (along d and across it)."""
         nc = self.nc
         lo, hi = [], []
         for x in d:
             if x < 0:
-                lo.append(nc - DEPTH + 1), hi.append(nc + 1 if rims else nc)
+                lo.append(nc - depth + 1), hi.append(nc + 1 if rims else nc)
             elif x > 0:
-                lo.append(0 if rims else 1), hi.append(DEPTH)
+                lo.append(0 if rims else 1), hi.append(depth)
             else:
                 lo.append(0 if rims else 1), hi.append(nc + 1 if rims else nc)
         return (int(b), *lo, *hi)
 
-    def halo_regions(self, recv_rank, send_rank, level, rims):
+    def halo_regions(self, recv_rank, send_rank, level, rims, depth=DEPTH):
         """Regions of boxes owned by send_rank that recv_rank reads around its
-        boxes of `level` (sorted, duplicates and contained regions removed)."""
+        boxes of `level` (sorted, duplicates and contained regions removed),
+        `depth` layers deep (the library asks for one layer where no fused
+        pair reads the second: the hook's n)."""
         if self.lp is None or level < self.lp:
             return []
         regs = set()
@@ -253,18 +255,40 @@ class Partition:
             for d in DIRS:
                 b = self.nmat[a - 1][(d[0] + 1) + 3 * (d[1] + 1) + 9 * (d[2] + 1)]
                 if b > 0 and self.owner[b - 1] == send_rank:
-                    regs.add(self._region(b, d, rims))
+                    regs.add(self._region(b, d, rims, depth))
         out = []
         by_box = {}
         for r in regs:
             by_box.setdefault(r[0], []).append(r)
+        nc = self.nc
         for b in sorted(by_box):
             rs = by_box[b]
             for r in sorted(rs):
                 inside = any(q != r and all(q[1 + k] <= r[1 + k] and r[4 + k] <= q[4 + k]
                                             for k in range(3)) for q in rs)
-                if not inside:
+                if inside:
+                    continue
+                if not rims:
                     out.append(r)
+                    continue
+                # RIMS follows the HALO of the same variable and level with
+                # only a ghost fill between: the interior arrived with the
+                # HALO, only the ghost cells travel -- the region less
+                # [1, nc]^3 as disjoint slabs (afh_dist_core.h halo_regions)
+                for k in range(3):
+                    for side in (0, 1):
+                        g = list(r)
+                        for j in range(k):
+                            g[1 + j], g[4 + j] = max(r[1 + j], 1), min(r[4 + j], nc)
+                        if side == 0:
+                            if r[1 + k] >= 1:
+                                continue
+                            g[4 + k] = 0
+                        else:
+                            if r[4 + k] <= nc:
+                                continue
+                            g[1 + k] = nc + 1
+                        out.append(tuple(g))
         return out
 
     def cflux_regions(self, recv_rank, send_rank):

@@ -62,14 +62,16 @@ struct afh_dist {
     double *send_buf = nullptr, *recv_buf = nullptr;
     std::vector<int64_t> send_off, send_n, recv_off, recv_n;  // per peer
   };
-  std::map<std::pair<int, int>, Plan> plans;  // (hook kind, level)
+  std::map<std::tuple<int, int, int>, Plan> plans;  // (hook kind, level, layers)
   double *d_red = nullptr;
   int64_t n_exchanges = 0, bytes = 0;
 };
 
 namespace {
 
-using Key = std::pair<int, int>;  // (hook kind, level)
+// (hook kind, level, layers): HALO / RIMS plans exist for one and two
+// layers (the hook's n: the layers the next reader needs, 0 = DEPTH)
+using Key = std::tuple<int, int, int>;
 
 int32_t exchange(afh_dist *d, const Key &key, int iv) {
   auto it = d->plans.find(key);
@@ -96,7 +98,7 @@ int32_t exchange(afh_dist *d, const Key &key, int iv) {
     if (ncclGroupEnd() != ncclSuccess) posted = false;
     if (!posted)
       return set_error(AFH_ERR_DEVICE, "exchange %d/%d: posting the RCCL send/recv failed",
-                       key.first, key.second);
+                       std::get<0>(key), std::get<1>(key));
     if (e_pack) return e_pack;
   } else {
     // every rank's packs complete, then each copies the peers' packed
@@ -113,7 +115,7 @@ int32_t exchange(afh_dist *d, const Key &key, int iv) {
       const int64_t n = src.send_n[d->rank];
       if (n != p.recv_n[q])
         e = set_error(AFH_ERR_STATE, "exchange %d/%d: rank %d sends %lld values, rank %d "
-                      "expects %lld", key.first, key.second, q, (long long)n, d->rank,
+                      "expects %lld", std::get<0>(key), std::get<1>(key), q, (long long)n, d->rank,
                       (long long)p.recv_n[q]);
       else if (hipMemcpyPeerAsync(p.recv_buf + p.recv_off[q], d->device,
                                   src.send_buf + src.send_off[d->rank], peer->device,
@@ -183,8 +185,10 @@ int32_t dist_hook(void *ctx, int32_t kind, int32_t level, int32_t iv, double *va
   case AFH_HOOK_MAX:
   case AFH_HOOK_MIN:
   case AFH_HOOK_SUM: return reduce(d, kind, vals, n);
-  case AFH_HOOK_CFLUX: return exchange(d, Key(kind, 0), iv);
-  default: return exchange(d, Key(kind, level), iv);
+  case AFH_HOOK_CFLUX: return exchange(d, Key(kind, 0, DEPTH), iv);
+  case AFH_HOOK_HALO:
+  case AFH_HOOK_RIMS: return exchange(d, Key(kind, level, n == 1 ? 1 : DEPTH), iv);
+  default: return exchange(d, Key(kind, level, DEPTH), iv);
   }
 }
 
@@ -272,12 +276,14 @@ int32_t afh_tree_create_sharded(const afh_tree_desc *desc, const int32_t *owner,
   if (rank != 0)
     for (size_t k = 0; k < c.ids.size(); k++) tr->sum_skip[k] = owner[c.ids[k] - 1] < 0;
   tr->lvl_total.assign(t.nlvl, 0);
+  tr->lvl_leaves_total.assign(t.nlvl, 0);
   tr->lvl_rb_coarse.assign(t.nlvl, 0);
   tr->any_cflux = false;
   for (int id = 1; id <= t.nb; id++) {
     const afh_box_meta &m = t.m[id - 1];
     if (m.lvl < 1) continue;
     tr->lvl_total[m.lvl - 1]++;
+    if (m.children[0] == 0) tr->lvl_leaves_total[m.lvl - 1]++;
     for (int q = 0; q < 6; q++) {
       if (m.lvl >= 2 && m.neighbors[q] == 0) tr->lvl_rb_coarse[m.lvl - 2] = 1;
       if (m.children[0] && m.neighbors[q] > 0 && t.m[m.neighbors[q] - 1].children[0] == 0)
@@ -354,7 +360,7 @@ int32_t afh_dist_create(afh_tree *t, const afh_tree_desc *desc, const int32_t *o
   } else {
     d->comm = static_cast<ncclComm_t>(group_or_comm);
   }
-  auto add = [&](int kind, int level) -> int32_t {
+  auto add = [&](int kind, int level, int depth = DEPTH) -> int32_t {
     afh_dist::Plan p;
     p.send_off.assign(n_ranks, 0), p.send_n.assign(n_ranks, 0);
     p.recv_off.assign(n_ranks, 0), p.recv_n.assign(n_ranks, 0);
@@ -369,8 +375,8 @@ int32_t afh_dist_create(afh_tree *t, const afh_tree_desc *desc, const int32_t *o
       for (int q = 0; q < n_ranks; q++) {
         off[q] = total;
         if (q == rank) continue;
-        const auto rs = side == 0 ? plan_regions(tp, own, lp, kind, level, q, rank)
-                                  : plan_regions(tp, own, lp, kind, level, rank, q);
+        const auto rs = side == 0 ? plan_regions(tp, own, lp, kind, level, q, rank, depth)
+                                  : plan_regions(tp, own, lp, kind, level, rank, q, depth);
         for (const Region &r : rs) {
           flat.insert(flat.end(), r.begin(), r.begin() + w);
           flat[flat.size() - w] = g2l[r[0]];
@@ -393,13 +399,14 @@ int32_t afh_dist_create(afh_tree *t, const afh_tree_desc *desc, const int32_t *o
       if (n && hipMalloc(&buf, sizeof(double) * n) != hipSuccess)
         return set_error(AFH_ERR_DEVICE, "exchange buffer");
     }
-    d->plans[Key(kind, level)] = std::move(p);
+    d->plans[Key(kind, level, depth)] = std::move(p);
     return AFH_OK;
   };
   int32_t e = AFH_OK;
   if (lp) {
     for (int l = lp; l <= tp.nlvl && !e; l++)
-      if (!(e = add(AFH_HOOK_HALO, l))) e = add(AFH_HOOK_RIMS, l);
+      for (int depth = 1; depth <= DEPTH && !e; depth++)
+        if (!(e = add(AFH_HOOK_HALO, l, depth))) e = add(AFH_HOOK_RIMS, l, depth);
     if (!e) e = add(AFH_HOOK_CFLUX, 0);
     for (int l : restrict_levels(tp, own, lp))
       if (!e) e = add(AFH_HOOK_RESTRICT, l);

@@ -151,16 +151,17 @@ inline int partition(const Topo &t, int n, std::vector<int32_t> &owner,
   return lp;
 }
 
-// Partition._region: cells of box b within DEPTH layers, b at direction d
-inline Region region(const Topo &t, int32_t b, const int d[3], bool rims) {
+// Partition._region: cells of box b within `depth` layers (DEPTH unless the
+// reader needs fewer), b at direction d
+inline Region region(const Topo &t, int32_t b, const int d[3], bool rims, int depth = DEPTH) {
   Region r{};
   r[0] = b;
   for (int k = 0; k < 3; k++) {
     int lo, hi;
     if (d[k] < 0)
-      lo = t.nc - DEPTH + 1, hi = rims ? t.nc + 1 : t.nc;
+      lo = t.nc - depth + 1, hi = rims ? t.nc + 1 : t.nc;
     else if (d[k] > 0)
-      lo = rims ? 0 : 1, hi = DEPTH;
+      lo = rims ? 0 : 1, hi = depth;
     else
       lo = rims ? 0 : 1, hi = rims ? t.nc + 1 : t.nc;
     r[1 + k] = lo, r[4 + k] = hi;
@@ -170,7 +171,8 @@ inline Region region(const Topo &t, int32_t b, const int d[3], bool rims) {
 
 // Partition.halo_regions
 inline std::vector<Region> halo_regions(const Topo &t, const std::vector<int32_t> &owner, int lp,
-                                 int recv, int send, int level, bool rims) {
+                                 int recv, int send, int level, bool rims,
+                                 int depth = DEPTH) {
   std::vector<Region> out;
   if (!lp || level < lp) return out;
   std::set<Region> regs;
@@ -183,7 +185,7 @@ inline std::vector<Region> halo_regions(const Topo &t, const std::vector<int32_t
           if (!dx && !dy && !dz) continue;
           const int b = t.m[a - 1].neighbor_mat[(dx + 1) + 3 * (dy + 1) + 9 * (dz + 1)];
           const int d[3] = {dx, dy, dz};
-          if (b > 0 && owner[b - 1] == send) regs.insert(region(t, b, d, rims));
+          if (b > 0 && owner[b - 1] == send) regs.insert(region(t, b, d, rims, depth));
         }
   }
   std::map<int32_t, std::vector<Region>> by_box;
@@ -197,7 +199,31 @@ inline std::vector<Region> halo_regions(const Topo &t, const std::vector<int32_t
         if (q != r && q[1] <= r[1] && q[2] <= r[2] && q[3] <= r[3] && r[4] <= q[4] &&
             r[5] <= q[5] && r[6] <= q[6])
           inside = true;
-      if (!inside) out.push_back(r);
+      if (inside) continue;
+      if (!rims) {
+        out.push_back(r);
+        continue;
+      }
+      // RIMS follows the HALO exchange of the same variable and level, with
+      // only a ghost-cell fill between them: the region's interior cells
+      // arrived with the HALO and are unchanged, so only its ghost cells
+      // travel (round 6) -- the region less the box interior [1, nc]^3, as
+      // disjoint slabs: along dimension k, the cells outside [1, nc] whose
+      // coordinates in the dimensions before k lie inside it
+      for (int k = 0; k < 3; k++)
+        for (int side = 0; side < 2; side++) {
+          Region g = r;
+          for (int j = 0; j < k; j++)
+            g[1 + j] = std::max(r[1 + j], 1), g[4 + j] = std::min(r[4 + j], t.nc);
+          if (side == 0) {
+            if (r[1 + k] >= 1) continue;
+            g[4 + k] = 0;
+          } else {
+            if (r[4 + k] <= t.nc) continue;
+            g[1 + k] = t.nc + 1;
+          }
+          out.push_back(g);
+        }
     }
   }
   return out;
@@ -283,10 +309,11 @@ inline std::vector<int> restrict_levels(const Topo &t, const std::vector<int32_t
 }
 
 inline std::vector<Region> plan_regions(const Topo &t, const std::vector<int32_t> &owner, int lp,
-                                 int kind, int level, int recv, int send) {
+                                 int kind, int level, int recv, int send,
+                                 int depth = DEPTH) {
   switch (kind) {
-  case AFH_HOOK_HALO: return halo_regions(t, owner, lp, recv, send, level, false);
-  case AFH_HOOK_RIMS: return halo_regions(t, owner, lp, recv, send, level, true);
+  case AFH_HOOK_HALO: return halo_regions(t, owner, lp, recv, send, level, false, depth);
+  case AFH_HOOK_RIMS: return halo_regions(t, owner, lp, recv, send, level, true, depth);
   case AFH_HOOK_CFLUX: return cflux_regions(t, owner, lp, recv, send);
   case AFH_HOOK_RESTRICT: return octant_regions(t, owner, lp, send, level);
   default: return {};

@@ -102,6 +102,7 @@ struct afh_tree {
   // of a level has the same bits; verified at tree creation)
   std::vector<double> lvl_dr;  // 3 per level
   std::vector<int> lvl_total;  // boxes per level over all ranks (topology)
+  std::vector<int> lvl_leaves_total;  // leaves per level over all ranks
   // level l+1 has a refinement boundary (a face without same-level neighbour)
   std::vector<int> lvl_rb_coarse;
   bool own_stream = true;
@@ -138,7 +139,7 @@ struct afh_tree {
   // reduction (host values) marks the recording unusable
   struct SegRec {
     std::vector<hipGraph_t> graphs;
-    std::vector<std::array<int32_t, 3>> ops;  // (kind, level, iv) after graphs[k]
+    std::vector<std::array<int32_t, 4>> ops;  // (kind, level, iv, n) after graphs[k]
     bool bad = false;
   };
   SegRec *seg_rec = nullptr;
@@ -243,17 +244,20 @@ void prof_end(afh_tree *t, int kc, double bytes);
 bool prof_ext(afh_tree *t, int kc, hipEvent_t &e0, hipEvent_t &e1);
 void prof_count(afh_tree *t, double bytes);
 // Host launchers shared between translation units (afh_tree.hip).
-int32_t gc_lvl(afh_tree *t, int lvl, int iv, int corners, bool rims = false);
+int32_t gc_lvl(afh_tree *t, int lvl, int iv, int corners, bool rims = false, int depth = 2);
 // ghost fill of level lvl of variable iv (0: the spare phi image), with the
 // coarse data of refinement boundaries read from vc; calls the sharding
 // hooks: HALO before, RIMS after when `rims` (the fused smoother reads the
 // replicas' ghost cells next) or when the next level has refinement
 // boundaries (its ghost cells read this level's replicas, ghosts included)
+// depth: the replica layers the next reader of the level needs (2: a fused
+// pair follows -- it recomputes neighbours' boundary cells --, 1: only
+// ghost cells are read), handed to the hooks as their n
 // xrim: the x ghost cells facing same-level neighbours are current except
 // on rows 1, nc and planes 1, nc (k_gsrb_pair2<..., XR> stored them): only
 // those are filled
 int32_t gc_lvl_var(afh_tree *t, int lvl, int iv, const double *vc,
-                   const GcArgs &ga, int corners, bool rims = false);
+                   const GcArgs &ga, int corners, bool rims = false, int depth = 2);
 // edges and corners only of level lvl (k_gc_corners), for a level whose
 // faces a producer kernel filled (the fused pair's pushed faces)
 int32_t gc_lvl_corners(afh_tree *t, int lvl, int iv);

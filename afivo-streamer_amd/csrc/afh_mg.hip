@@ -2737,6 +2737,9 @@ struct afh_mg {
   // instead of segments between host-driven exchanges. Off until measured on
   // more than one GPU (a capture failure falls back to the eager cycle)
   bool rccl_capture = false;
+  // per level: the rhs replicas exchanged by this V-cycle's down leg
+  std::vector<char> rhs_halo;
+  int vc_max_lvl = 0;  // the highest level of the V-cycle being issued
   bool grad_nt = true;       // the gradient's face fields and |E| stored
                              // nontemporal (streaming): -9 % on S1-64 (scripts/grad_ab.py)
   // t->gen[i_phi] when this multigrid last left phi's ghost cells current
@@ -2804,7 +2807,7 @@ struct afh_mg {
     // sharded (a hook): the V-cycle as segments between its exchanges, each
     // replayed as a graph, the exchange (ops[k]) run after segs[k]
     std::vector<hipGraphExec_t> segs;
-    std::vector<std::array<int32_t, 3>> ops;
+    std::vector<std::array<int32_t, 4>> ops;
     bool eager_only = false;  // the recording met a reduction
     void release() {
       if (exec) hipGraphExecDestroy(exec);
@@ -3309,7 +3312,9 @@ static int32_t gsrb_half(afh_mg *mg, int lvl, int n, bool corners) {
                        mg->ids_v.at(lvl), nc, t->bsz, mg->d_vp, mg->d_bp, n);
     AFH_LAUNCH_CHECK("k_gsrb_v");
   }
-  return gc_lvl(t, lvl, mg->d.i_phi, corners, fused_level(mg, lvl));
+  // (a split half-sweep reads ghost cells only; a fused level's pair may
+  // follow)
+  return gc_lvl(t, lvl, mg->d.i_phi, corners, fused_level(mg, lvl), fused_level(mg, lvl) ? 2 : 1);
 }
 
 // gsrb_boxes (m_af_multigrid.f90:741-760): 2 n_cycle half-sweeps, each
@@ -3337,8 +3342,13 @@ static int32_t gsrb_boxes(afh_mg *mg, int lvl, bool up, bool stale_ghosts = fals
   }
   double *phi = t->ccv(mg->d.i_phi);
   const afh::GcArgs ga = t->gc_args(mg->d.i_phi);
-  // the pair recomputes neighbours' red boundary cells from their rhs
-  if (int32_t e = call_hook(t, AFH_HOOK_HALO, lvl, mg->d.i_rhs)) return e;
+  // the pair recomputes neighbours' red boundary cells from their rhs; the
+  // up leg's pairs read the rhs the down leg's exchange brought (nothing
+  // writes a level's rhs between its two legs)
+  if ((int)mg->rhs_halo.size() < t->nlvl) mg->rhs_halo.assign(t->nlvl, 0);
+  if (!(up && mg->rhs_halo[lvl - 1]))
+    if (int32_t e = call_hook(t, AFH_HOOK_HALO, lvl, mg->d.i_rhs)) return e;
+  mg->rhs_halo[lvl - 1] = !up;
   for (int n = n0; n <= n_cycle; n++) {
     const bool to_alt = ((n - n0) & 1) == 0;
     const double *src = to_alt ? phi : mg->alt;
@@ -3367,7 +3377,12 @@ static int32_t gsrb_boxes(afh_mg *mg, int lvl, bool up, bool stale_ghosts = fals
       // the pair filled the faces; edges and corners on the leg's last pair
       if (up && n == n_cycle)
         if (int32_t e = gc_lvl_corners(t, lvl, dst_iv)) return e;
-    } else if (int32_t e = gc_lvl_var(t, lvl, dst_iv, phi, ga, up && n == n_cycle, true)) {
+    } else if (int32_t e = gc_lvl_var(t, lvl, dst_iv, phi, ga, up && n == n_cycle, true,
+                                      // another pair reads the replicas'
+                                      // second layer: the leg's next pair, or
+                                      // the next V-cycle's first on the
+                                      // highest level (no fill between)
+                                      n < n_cycle || (up && lvl == mg->vc_max_lvl) ? 2 : 1)) {
       return e;
     }
   }
@@ -3465,7 +3480,9 @@ static int32_t update_coarse(afh_mg *mg, int lvl, bool ghosts_valid = false) {
   if ((e = call_hook(t, AFH_HOOK_RESTRICT, lvl, mg->d.i_phi)) ||
       (e = call_hook(t, AFH_HOOK_RESTRICT, lvl, mg->d.i_tmp)))
     return e;
-  if ((e = gc_lvl(t, lvl - 1, mg->d.i_phi, 1, fused_level(mg, lvl - 1)))) return e;
+  if ((e = gc_lvl(t, lvl - 1, mg->d.i_phi, 1, fused_level(mg, lvl - 1),
+                  fused_level(mg, lvl - 1) ? 2 : 1)))
+    return e;
   const LevelList &P = cst(mg, t->parents, mg->parents_c);
   const int np = P.n(lvl - 1);
   if (np) {
@@ -4222,6 +4239,8 @@ static int32_t vcycle_body(afh_mg *mg, int32_t set_residual, int max_lvl, bool m
                            bool top_stale) {
   afh_tree *t = mg->t;
   int32_t e;
+  mg->rhs_halo.assign(t->nlvl, 0);
+  mg->vc_max_lvl = max_lvl;
   for (int lvl = max_lvl; lvl >= 2; lvl--) {
     if ((e = gsrb_boxes(mg, lvl, false, top_stale && lvl == max_lvl))) return e;
     // (ghosts of the levels below valid: phi and the boundary conditions
@@ -4238,7 +4257,8 @@ static int32_t vcycle_body(afh_mg *mg, int32_t set_residual, int max_lvl, bool m
     // edges or corners: k_gc_corners follows the leg's last pair)
     if (!prolong_push(mg, lvl) &&
         (e = gc_lvl_var(t, lvl, mg->d.i_phi, t->ccv(mg->d.i_phi),
-                        t->gc_args(mg->d.i_phi), 1, fused_level(mg, lvl))))
+                        t->gc_args(mg->d.i_phi), 1, fused_level(mg, lvl),
+                        fused_level(mg, lvl) ? 2 : 1)))
       return e;
     if ((e = gsrb_boxes(mg, lvl, true))) return e;
   }
@@ -4289,7 +4309,8 @@ static int32_t vcycle_segments(afh_mg *mg, afh_mg::Graph &g, int32_t set_residua
   for (size_t k = 0; k < g.segs.size(); k++) {
     if (g.segs[k]) AFH_HIP(hipGraphLaunch(g.segs[k], t->stream));
     if (k < g.ops.size())
-      if (int32_t e = call_hook(t, g.ops[k][0], g.ops[k][1], g.ops[k][2])) return e;
+      if (int32_t e = call_hook(t, g.ops[k][0], g.ops[k][1], g.ops[k][2], nullptr, g.ops[k][3]))
+        return e;
   }
   mg->n_replays++, mg->n_seg_replays++;
   done = true;

@@ -2420,7 +2420,12 @@ static int32_t flux_prelude(afh_fluid *f, int iv, double *gc2) {
   }
   // two ghost layers, level by level (coarse write-back before fine reads)
   for (int l = 1; l <= t->nlvl; l++) {
-    if ((e = call_hook(t, AFH_HOOK_HALO, l, iv))) return e;
+    // (a level without leaves anywhere is read only as the coarse side of
+    // the next level's refinement boundaries: no exchange when there are
+    // none)
+    if ((t->lvl_leaves_total[l - 1] > 0 || t->lvl_rb_coarse[l - 1]) &&
+        (e = call_hook(t, AFH_HOOK_HALO, l, iv)))
+      return e;
     const int n = t->leaves.n(l);
     if (n) {
       const int b2 = fit_blk(nc * nc);

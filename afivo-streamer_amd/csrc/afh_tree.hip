@@ -301,7 +301,7 @@ int32_t call_hook(afh_tree *t, int kind, int lvl, int iv, double *vals, int n) {
     hipGraph_t g = nullptr;
     AFH_HIP(hipStreamEndCapture(t->stream, &g));
     r->graphs.push_back(g);
-    r->ops.push_back({kind, lvl, iv});
+    r->ops.push_back({kind, lvl, iv, n});
     AFH_HIP(hipStreamBeginCapture(t->stream, hipStreamCaptureModeThreadLocal));
     return AFH_OK;
   }
@@ -311,11 +311,11 @@ int32_t call_hook(afh_tree *t, int kind, int lvl, int iv, double *vals, int n) {
 }
 
 int32_t gc_lvl_var(afh_tree *t, int lvl, int iv, const double *vc,
-                   const GcArgs &ga, int corners, bool rims) {
+                   const GcArgs &ga, int corners, bool rims, int depth) {
   const int n = t->ids.n(lvl);
   double *v = t->var(iv);
   int32_t e;
-  if ((e = call_hook(t, AFH_HOOK_HALO, lvl, iv))) return e;
+  if ((e = call_hook(t, AFH_HOOK_HALO, lvl, iv, nullptr, depth))) return e;
   if (n > 0) {
     const int nc = t->nc;
     prof_begin(t, AFH_PROF_GHOST);
@@ -346,7 +346,8 @@ int32_t gc_lvl_var(afh_tree *t, int lvl, int iv, const double *vc,
       }
     }
   }
-  if (rims || t->lvl_rb_coarse[lvl - 1]) return call_hook(t, AFH_HOOK_RIMS, lvl, iv);
+  if (rims || t->lvl_rb_coarse[lvl - 1])
+    return call_hook(t, AFH_HOOK_RIMS, lvl, iv, nullptr, depth);
   return AFH_OK;
 }
 
@@ -359,8 +360,8 @@ int32_t gc_lvl_corners(afh_tree *t, int lvl, int iv) {
   return AFH_OK;
 }
 
-int32_t gc_lvl(afh_tree *t, int lvl, int iv, int corners, bool rims) {
-  return gc_lvl_var(t, lvl, iv, t->ccv(iv), t->gc_args(iv), corners, rims);
+int32_t gc_lvl(afh_tree *t, int lvl, int iv, int corners, bool rims, int depth) {
+  return gc_lvl_var(t, lvl, iv, t->ccv(iv), t->gc_args(iv), corners, rims, depth);
 }
 
 // ------------------------------------------------------------ plans
@@ -827,6 +828,9 @@ static int32_t tree_create_impl(const afh_tree_desc *d, int32_t device,
     seen[l] = 1;
     t->lvl_total[l]++;
   }
+  t->lvl_leaves_total.assign(t->nlvl, 0);
+  for (int l = 0; l < t->nlvl; l++)
+    t->lvl_leaves_total[l] = (int)t->h_leaves[l].size();
   t->lvl_rb_coarse.assign(t->nlvl, 0);
   for (int id = 1; id <= t->nb; id++) {
     const afh_box_meta &m = t->boxes[id - 1];

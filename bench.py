@@ -94,7 +94,14 @@ def coarse_choice(arg, config):
     return "pfmg" if config in DRIVER_CONFIGS or config == "2d" else "direct"
 
 
-def build_case(lib, config, device, coarse, shard_ranks=None, shard=None):
+# levels smaller than this are replicated on every rank instead of sharded
+# (afh_dist_partition_levels): such a level's kernels are launch-bound on one
+# GPU already, so sharding it only adds its exchanges
+MIN_LEVEL_CELLS = 1 << 21
+
+
+def build_case(lib, config, device, coarse, shard_ranks=None, shard=None,
+               min_level_cells=MIN_LEVEL_CELLS):
     """shard_ranks = (world, rank, "native" | "python"): this rank's part of
     the sharded tree; or shard: a prepared afh.dist shard (thread ranks)."""
     from afh.streamer import StreamerCase, seed_state, tables_from
@@ -117,7 +124,8 @@ def build_case(lib, config, device, coarse, shard_ranks=None, shard=None):
             from afh import capi
             from afh.dist import NativeShard, rccl_comm
             shard = NativeShard(lib, topo, world, rank, transport=capi.DIST_RCCL,
-                                comm=rccl_comm(lib, rank, world, device))
+                                comm=rccl_comm(lib, rank, world, device),
+                                min_level_cells=min_level_cells)
         else:
             from afh.dist import Partition, Shard
             shard = Shard(Partition(topo, world), rank, "nccl", device="cuda:%d" % device)
@@ -322,7 +330,8 @@ def _hip_stream():
     return st
 
 
-def local_ranks(lib, config, world, device, coarse, shared_stream=False, grow_cells=0):
+def local_ranks(lib, config, world, device, coarse, shared_stream=False, grow_cells=0,
+                min_level_cells=MIN_LEVEL_CELLS):
     """--transport local: the sharded workload on `world` thread ranks of this
     process (afh_dist AFH_DIST_LOCAL: pack, host barrier, peer copies,
     unpack), every rank on `device`. The same partition, plans and hooks the
@@ -336,8 +345,8 @@ def local_ranks(lib, config, world, device, coarse, shared_stream=False, grow_ce
         base = build_driver_case(lib, device, config, coarse, grow_cells)
         topo = base.af.topology()
         sims = [base.clone(lib, device=device) for _ in range(world)]
-        shards = [NativeShard(lib, topo, world, r, transport=capi.DIST_LOCAL, group=group)
-                  for r in range(world)]
+        shards = [NativeShard(lib, topo, world, r, transport=capi.DIST_LOCAL, group=group,
+                              min_level_cells=min_level_cells) for r in range(world)]
         for sim, sh in zip(sims, shards):
             sim.shard_over(sh)
         cases = [DriverCase(sim) for sim in sims]
@@ -345,8 +354,8 @@ def local_ranks(lib, config, world, device, coarse, shared_stream=False, grow_ce
         from afh.tree import uniform_tree
         nc, cgs, lvls, dom = CONFIGS[config]
         topo = uniform_tree(nc, cgs, dom, lvls)
-        shards = [NativeShard(lib, topo, world, r, transport=capi.DIST_LOCAL, group=group)
-                  for r in range(world)]
+        shards = [NativeShard(lib, topo, world, r, transport=capi.DIST_LOCAL, group=group,
+                              min_level_cells=min_level_cells) for r in range(world)]
         # (the set-up fills ghost cells: exchanges, so every rank on its thread)
         cases = run_ranks(shards, lambda r, sh: build_case(lib, config, device, coarse,
                                                            shard=sh))
@@ -391,7 +400,8 @@ def bench_local(args, coarse):
         os.environ["AFH_GRAPHS"] = "0"
     try:
         cases, shards, group, base = local_ranks(lib, args.config, world, device, coarse,
-                                                 args.shared_stream, args.grow_cells)
+                                                 args.shared_stream, args.grow_cells,
+                                                 args.min_level_cells)
     finally:
         if args.shared_stream:
             if graphs_env is None:
@@ -453,7 +463,8 @@ def bench_local(args, coarse):
         "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic", "shared_stream": bool(args.shared_stream),
         "config": {"workload": args.config, "leaf_cells": ncell, "boxes": int(topo["n_boxes"]),
-                   "coarse_solve": coarse},
+                   "coarse_solve": coarse, "min_level_cells": args.min_level_cells,
+                   "partition_level": shards[0].lp},
         "owned_leaf_cells": owned,
         "exchanges_per_step": [n / steps for n, _ in stats],
         "exchange_bytes_per_step": [b / steps for _, b in stats],
@@ -503,6 +514,9 @@ def main():
     ap.add_argument("--shared-stream", action="store_true",
                     help="--transport local: every rank on one HIP stream (kernels "
                          "serialised, so that a kernel trace gives each rank's own time)")
+    ap.add_argument("--min-level-cells", type=int, default=MIN_LEVEL_CELLS,
+                    help="N>1: levels holding fewer cells are replicated on every rank, "
+                         "not sharded (0: shard from level 2, as before round 6)")
     ap.add_argument("--grow-cells", type=float, default=0,
                     help="driver configs: advance the time loop (untimed) until the tree "
                          "holds this many leaf cells (or --grow-seconds pass), then bench "
@@ -556,11 +570,13 @@ def main():
             from afh.dist import NativeShard, rccl_comm
             sim.shard_over(NativeShard(lib, sim.af.topology(), world, rank,
                                        transport=capi.DIST_RCCL,
-                                       comm=rccl_comm(lib, rank, world, local)))
+                                       comm=rccl_comm(lib, rank, world, local),
+                                       min_level_cells=args.min_level_cells))
         case = DriverCase(sim)
     else:
         case = build_case(lib, args.config, local, coarse,
-                          (world, rank, args.shard) if sharded else None)
+                          (world, rank, args.shard) if sharded else None,
+                          min_level_cells=args.min_level_cells)
     from afh.streamer import cells
     ncell = cells(case.topo)  # leaf cells of the whole tree
     dt = 1e-13

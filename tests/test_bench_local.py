@@ -46,11 +46,13 @@ def _single(lib, config, coarse, device):
     return bench.build_case(lib, config, device, coarse)
 
 
-def _bitwise(lib, config, world, device=-1):
+def _bitwise(lib, config, world, device=-1, floor=0):
+    """floor: bench's min_level_cells (0: every level from 2 sharded)."""
     coarse = bench.coarse_choice("auto", config)
     one = _single(lib, config, coarse, device)
     ref = _steps(one)
-    cases, shards, group, base = bench.local_ranks(lib, config, world, device, coarse)
+    cases, shards, group, base = bench.local_ranks(lib, config, world, device, coarse,
+                                                   min_level_cells=floor)
     try:
         outs = bench.run_ranks(cases, lambda r, c: _steps(c))
         stats = [bench.dist_stats(lib, sh) for sh in shards]
@@ -58,7 +60,10 @@ def _bitwise(lib, config, world, device=-1):
         for sh in shards:
             sh.detach()
         group.close()
-    assert all(n > 0 for n, _ in stats)
+    if shards[0].lp is not None:
+        assert all(n > 0 for n, _ in stats)
+    else:  # the whole tree replicated: no exchange at all
+        assert all(n == 0 for n, _ in stats)
     for o in outs:
         assert o == ref, (o, ref)
     for iv in range(1, one.tree.n_var_cell + 1):
@@ -78,6 +83,14 @@ def test_local_transport_bitwise_single_rank(config, world):
     _bitwise(capi.oracle_library(), config, world)
 
 
+@pytest.mark.parametrize("config,world", [("s1", 8), ("s5", 3)])
+def test_local_transport_bitwise_level_floor(config, world):
+    """bench's default partition (round 6): levels under MIN_LEVEL_CELLS
+    replicated -- s1: levels 1-3 on every rank, level 4 sharded; s5's set-up
+    tree: every level below the floor, the whole tree replicated."""
+    _bitwise(capi.oracle_library(), config, world, floor=bench.MIN_LEVEL_CELLS)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("config,world", [("s1", 2), ("s1", 4), ("s5", 2), ("s5", 8)])
 def test_local_transport_bitwise_single_rank_hip(config, world):
@@ -87,13 +100,22 @@ def test_local_transport_bitwise_single_rank_hip(config, world):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("config,world", [("s1", 8), ("s1-64", 2)])
+def test_local_transport_bitwise_level_floor_hip(config, world):
+    """bench's default partition on the GPU: s1 with levels 1-3 replicated;
+    s1-64 at N = 2 (the headline tree: fused 64^3 pairs with one- and
+    two-layer halos, ghost-only rims)."""
+    _bitwise(capi.hip_library(), config, world, device=0, floor=bench.MIN_LEVEL_CELLS)
+
+
+@pytest.mark.gpu
 def test_bench_local_json():
     """bench.py --transport local --gpus 4 --shared-stream, the line the
     scaling projection reads (scripts/project_scaling.py)."""
     import argparse
     args = argparse.Namespace(gpus=4, config="s5", steps=2, warmup=1, oracle=False,
                               shared_stream=True, no_fused_rhs=False,
-                              stored_face_field=False, grow_cells=0)
+                              stored_face_field=False, grow_cells=0, min_level_cells=0)
     out = bench.bench_local(args, bench.coarse_choice("auto", "s5"))
     assert out["n_ranks"] == 4 and out["value"] > 0
     assert len(out["owned_leaf_cells"]) == 4 and min(out["owned_leaf_cells"]) > 0
