@@ -208,6 +208,7 @@ SIGNATURES = {
     "dist_create": (i32, [_VP, C.POINTER(TreeDesc), P_i32, i32, i32, i32, _VP, _PVP]),
     "dist_destroy": (i32, [_VP]),
     "dist_stats": (i32, [_VP, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
+    "dist_peer_bytes": (i32, [_VP, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
 }
 DIST_LOCAL, DIST_RCCL = 1, 2
 HOOK_HALO, HOOK_RIMS, HOOK_RESTRICT, HOOK_MAX, HOOK_MIN, HOOK_CFLUX = 1, 2, 3, 4, 5, 6

@@ -65,6 +65,7 @@ struct afh_dist {
   std::map<std::tuple<int, int, int>, Plan> plans;  // (hook kind, level, layers)
   double *d_red = nullptr;
   int64_t n_exchanges = 0, bytes = 0;
+  std::vector<int64_t> peer_sent, peer_recv;  // bytes per peer (afh_dist_peer_bytes)
 };
 
 namespace {
@@ -130,7 +131,11 @@ int32_t exchange(afh_dist *d, const Key &key, int iv) {
   if (p.recv_plan >= 0) e = afh_plan_unpack(t, p.recv_plan, iv, p.recv_buf);
   if (e) return e;
   d->n_exchanges++;
-  for (int q = 0; q < d->n; q++) d->bytes += 8 * (p.send_n[q] + p.recv_n[q]);
+  for (int q = 0; q < d->n; q++) {
+    d->bytes += 8 * (p.send_n[q] + p.recv_n[q]);
+    d->peer_sent[q] += 8 * p.send_n[q];
+    d->peer_recv[q] += 8 * p.recv_n[q];
+  }
   return AFH_OK;
 }
 
@@ -350,6 +355,7 @@ int32_t afh_dist_create(afh_tree *t, const afh_tree_desc *desc, const int32_t *o
   for (size_t k = 0; k < local.size(); k++) g2l[local[k]] = (int32_t)k + 1;
   afh_dist *d = new afh_dist;
   d->t = t, d->rank = rank, d->n = n_ranks, d->transport = transport;
+  d->peer_sent.assign(n_ranks, 0), d->peer_recv.assign(n_ranks, 0);
   hipGetDevice(&d->device);
   if (transport == AFH_DIST_LOCAL) {
     d->group = static_cast<afh_dist_group *>(group_or_comm);
@@ -451,6 +457,15 @@ int32_t afh_dist_stats(afh_dist *d, int64_t *n_exchanges, int64_t *bytes) {
   if (!d) return set_error(AFH_ERR_ARG, "null dist");
   if (n_exchanges) *n_exchanges = d->n_exchanges;
   if (bytes) *bytes = d->bytes;
+  return AFH_OK;
+}
+
+int32_t afh_dist_peer_bytes(afh_dist *d, int64_t *sent, int64_t *received) {
+  if (!d) return set_error(AFH_ERR_ARG, "null dist");
+  for (int q = 0; q < d->n; q++) {
+    if (sent) sent[q] = d->peer_sent[q];
+    if (received) received[q] = d->peer_recv[q];
+  }
   return AFH_OK;
 }
 

@@ -781,6 +781,13 @@ module m_afivo_hip
        integer(c_int32_t)              :: afh_dist_stats
      end function afh_dist_stats
 
+     function afh_dist_peer_bytes(d, sent, received) bind(C, name=afh_pfx//"dist_peer_bytes")
+       import
+       type(c_ptr), value              :: d
+       integer(c_int64_t), intent(out) :: sent(*), received(*)
+       integer(c_int32_t)              :: afh_dist_peer_bytes
+     end function afh_dist_peer_bytes
+
      !> electrode_species_bc (src/streamer.f90:578-636) over the mg_lsf_box boxes
      function afh_electrode_species_bc(f, i_lsf, i_1pos_ion, neumann_zero, n_ids, ids) &
           bind(C, name=afh_pfx//"electrode_species_bc")

@@ -381,6 +381,14 @@ def dist_stats(lib, shard):
     return n.value, b.value
 
 
+def dist_peer_bytes(lib, shard):
+    """(sent, received) bytes per peer so far (afh_dist_peer_bytes)."""
+    import ctypes as C
+    s, r = (C.c_int64 * shard.n)(), (C.c_int64 * shard.n)()
+    lib.call("dist_peer_bytes", shard.h, s, r)
+    return np.array(s[:], np.int64), np.array(r[:], np.int64)
+
+
 def bench_local(args, coarse):
     """--transport local --gpus N: N thread ranks on ONE device run the
     sharded unit step; not the metric (the ranks share one GPU), but every
@@ -411,6 +419,7 @@ def bench_local(args, coarse):
     dt = 1e-13
     bar = threading.Barrier(world)
     clock = {}
+    peer = {}
 
     def work(r, case):
         if not args.no_fused_rhs:
@@ -422,6 +431,7 @@ def bench_local(args, coarse):
             unit_step(case, dt, k)
         case.tree.sync()
         s0 = dist_stats(lib, shards[r])
+        p0 = dist_peer_bytes(lib, shards[r])
         bar.wait()
         if r == 0:
             clock["t0"] = time.perf_counter()
@@ -435,6 +445,8 @@ def bench_local(args, coarse):
             clock["t1"] = time.perf_counter()
             clock["ns1"] = time.clock_gettime_ns(time.CLOCK_MONOTONIC)
         s1 = dist_stats(lib, shards[r])
+        p1 = dist_peer_bytes(lib, shards[r])
+        peer[r] = ((p1[0] - p0[0]).tolist(), (p1[1] - p0[1]).tolist())
         return s1[0] - s0[0], s1[1] - s0[1]
 
     try:
@@ -468,6 +480,10 @@ def bench_local(args, coarse):
         "owned_leaf_cells": owned,
         "exchanges_per_step": [n / steps for n, _ in stats],
         "exchange_bytes_per_step": [b / steps for _, b in stats],
+        # per rank r, per peer q: bytes sent to q / received from q per step
+        "peer_bytes_per_step": [{"sent": [x / steps for x in peer[r][0]],
+                                 "received": [x / steps for x in peer[r][1]]}
+                                for r in range(world)],
         "note": "not the metric: the ranks share one device; see scripts/project_scaling.py",
         # the timed region on CLOCK_MONOTONIC (a kernel trace's clock)
         "window_ns": [clock["ns0"], clock["ns1"]],

@@ -699,6 +699,9 @@ int32_t afh_dist_create(afh_tree *t, const afh_tree_desc *desc, const int32_t *o
                         afh_dist **out);
 int32_t afh_dist_destroy(afh_dist *d);
 int32_t afh_dist_stats(afh_dist *d, int64_t *n_exchanges, int64_t *bytes);
+/* The bytes this rank sent to / received from each peer so far (n_ranks
+ * entries each; null to skip): the per-link input of the scaling model. */
+int32_t afh_dist_peer_bytes(afh_dist *d, int64_t *sent, int64_t *received);
 
 #ifdef __cplusplus
 }

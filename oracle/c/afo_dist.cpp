@@ -61,6 +61,7 @@ struct afh_dist {
   };
   std::map<std::pair<int, int>, Plan> plans;
   int64_t n_exchanges = 0, bytes = 0;
+  std::vector<int64_t> peer_sent, peer_recv;
 };
 
 namespace {
@@ -91,7 +92,12 @@ int32_t exchange(afh_dist *d, const Key &key, int iv) {
     if (p.recv[q].n) e = afo_plan_unpack(d->t, p.recv[q].plan, iv, p.recv[q].buf.data());
   if (e) return e;
   d->n_exchanges++;
-  for (int q = 0; q < d->n; q++) d->bytes += 8 * (p.send[q].n + p.recv[q].n);
+  if ((int)d->peer_sent.size() != d->n) d->peer_sent.assign(d->n, 0), d->peer_recv.assign(d->n, 0);
+  for (int q = 0; q < d->n; q++) {
+    d->bytes += 8 * (p.send[q].n + p.recv[q].n);
+    d->peer_sent[q] += 8 * p.send[q].n;
+    d->peer_recv[q] += 8 * p.recv[q].n;
+  }
   return AFH_OK;
 }
 
@@ -289,6 +295,16 @@ int32_t afo_dist_stats(afh_dist *d, int64_t *n_exchanges, int64_t *bytes) {
   if (!d) return fail(AFH_ERR_ARG, "null dist");
   if (n_exchanges) *n_exchanges = d->n_exchanges;
   if (bytes) *bytes = d->bytes;
+  return AFH_OK;
+}
+
+int32_t afo_dist_peer_bytes(afh_dist *d, int64_t *sent, int64_t *received) {
+  if (!d) return fail(AFH_ERR_ARG, "null dist");
+  for (int q = 0; q < d->n; q++) {
+    const bool any = (int)d->peer_sent.size() == d->n;
+    if (sent) sent[q] = any ? d->peer_sent[q] : 0;
+    if (received) received[q] = any ? d->peer_recv[q] : 0;
+  }
   return AFH_OK;
 }
 

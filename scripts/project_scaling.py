@@ -19,10 +19,18 @@ step time of N GPUs, one rank each:
     T_N = rho * max_r b_r + E_N * alpha + max_r B_r / beta
 
 E_N: exchanges per step (each a grouped RCCL send/recv or an all-reduce, and
-a graph-segment boundary), B_r: bytes rank r sends per step, alpha: 15 us per
-exchange (RCCL point-to-point latency over xGMI plus the segment launch; an
-assumption), beta: 64 GB/s (a conservative half of one xGMI link). Speed-up
-T_1 / T_N.
+a graph-segment boundary), B_r: bytes rank r sends and receives per step (all
+peers, summed: as if every byte crossed one link, one direction at a time),
+alpha: 15 us per exchange (RCCL point-to-point latency over xGMI plus the
+segment launch; an assumption), beta: 64 GB/s (a conservative half of one
+xGMI link). Speed-up T_1 / T_N.
+
+Beside it (round 6), the per-link variant: an MI355X node joins every pair of
+its 8 GPUs by an xGMI link of its own, and a link moves both directions at
+once, so the bytes term is max over ranks r and peers q of
+max(sent_rq, received_rq) / beta (bench.py's peer_bytes_per_step; the same
+alpha and beta). Still a projection: the link's real bandwidth and the
+overlap of several links are unmeasured here.
 
 Usage: project_scaling.py <config> <dir> <out.json>
   <dir>/n1.json, <dir>/n1_trace.csv, <dir>/nN.json, <dir>/nN_trace.csv
@@ -97,6 +105,10 @@ def main(config, d, out_path):
         E = max(j["exchanges_per_step"])
         B = max(j["exchange_bytes_per_step"])
         TN = rho * per[0] + E * ALPHA_S + B / BETA_BS
+        link = None
+        if "peer_bytes_per_step" in j:
+            link = max(max(max(s, r) for s, r in zip(p["sent"], p["received"]))
+                       for p in j["peer_bytes_per_step"])
         res["ranks"][str(n)] = {
             "busy_ms_per_rank": [x * 1e3 for x in per],
             "busy_sum_ms": sum(per) * 1e3,
@@ -107,6 +119,13 @@ def main(config, d, out_path):
             "exchange_latency_ms": E * ALPHA_S * 1e3,
             "exchange_bw_ms": B / BETA_BS * 1e3,
             "projected_speedup": T1 / TN,
+            "link_bytes_per_step_max": link,
+            "projected_ms_per_step_per_link": None if link is None else
+            (rho * per[0] + E * ALPHA_S + link / BETA_BS) * 1e3,
+            "projected_speedup_per_link": None if link is None else
+            T1 / (rho * per[0] + E * ALPHA_S + link / BETA_BS),
+            "partition_level": j["config"].get("partition_level"),
+            "min_level_cells": j["config"].get("min_level_cells"),
             "busiest_rank_top_kernels": top_kernels(kk[busiest], j["steps"]),
         }
     with open(out_path, "w") as f:
