@@ -1677,6 +1677,46 @@ int32_t afo_pfmg_probe(int32_t nx, int32_t ny, int32_t nz, const double *a7, int
   return AFH_OK;
 }
 
+/* The whole hierarchy of afh_pfmg_setup (tests/test_pfmg.py checks it
+ * against an independent numpy statement): per level dims (3), cdir, active,
+ * w; the point offsets (nl + 1); A (27 per point) and P (2 per point) of all
+ * levels. Call with A = P = NULL to get *nl and *np first. */
+int32_t afo_pfmg_probe_full(int32_t nx, int32_t ny, int32_t nz, const double *a7, int32_t maxl,
+                            int32_t *nl, int64_t *np, int32_t *dims, int32_t *cdir,
+                            int32_t *active, double *w, int64_t *off, double *A, double *P) {
+  afh_pfmg h;
+  if (!a7 || !nl || !np || nx < 1 || ny < 1 || nz < 1)
+    return fail(AFH_ERR_ARG, "afo_pfmg_probe_full: bad argument");
+  if (afh_pfmg_setup(&h, nx, ny, nz, nz > 1 ? 3 : 2, a7)) return fail(AFH_ERR_STATE, "setup");
+  *nl = h.nl;
+  *np = (int64_t)h.off[h.nl];
+  if (h.nl > maxl) return afh_pfmg_free(&h), fail(AFH_ERR_ARG, "afo_pfmg_probe_full: maxl");
+  for (int l = 0; l < h.nl; l++) {
+    if (dims)
+      for (int d = 0; d < 3; d++) dims[3 * l + d] = h.n[l][d];
+    if (cdir) cdir[l] = l + 1 < h.nl ? h.cdir[l] : -1;
+    if (active) active[l] = h.active[l];
+    if (w) w[l] = h.w[l];
+  }
+  if (off)
+    for (int l = 0; l <= h.nl; l++) off[l] = (int64_t)h.off[l];
+  if (A) memcpy(A, h.A, sizeof(double) * AFH_PFMG_S * h.off[h.nl]);
+  if (P) memcpy(P, h.P, sizeof(double) * 2 * h.off[h.nl]);
+  afh_pfmg_free(&h);
+  return AFH_OK;
+}
+
+/* The folded level-1 operator of the last PFMG solve of mg (a7: 7 per point
+ * of the level-1 grid, dims nx ny nz), for the probes above */
+int32_t afo_mg_pfmg_operator(afh_mg *mg, int32_t *dims, double *a7) {
+  if (!mg || !dims) return fail(AFH_ERR_ARG, "afo_mg_pfmg_operator: null");
+  for (int d = 0; d < 3; d++) dims[d] = mg->dims[0][d];
+  if (!mg->pf_a7) return fail(AFH_ERR_STATE, "afo_mg_pfmg_operator: no PFMG solve yet");
+  const size_t n0 = (size_t)mg->dims[0][0] * mg->dims[0][1] * mg->dims[0][2];
+  if (a7) memcpy(a7, mg->pf_a7, sizeof(double) * 7 * n0);
+  return AFH_OK;
+}
+
 /* solve_coarse_grid, m_af_multigrid.f90:266-291 */
 int32_t afo_mg_solve_coarse(afh_mg *mg) {
   afh_tree *t = mg->t;

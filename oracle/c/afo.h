@@ -28,6 +28,10 @@ const char *afo_last_error(void);
 /* Test probe of the PFMG setup (afh_pfmg.h) on a folded 7-point operator a7
  * (7 per point): level count, coarsening direction, relaxed flag and Jacobi
  * weight per level (at most maxl). */
+int32_t afo_pfmg_probe_full(int32_t nx, int32_t ny, int32_t nz, const double *a7, int32_t maxl,
+                            int32_t *nl, int64_t *np, int32_t *dims, int32_t *cdir,
+                            int32_t *active, double *w, int64_t *off, double *A, double *P);
+int32_t afo_mg_pfmg_operator(afh_mg *mg, int32_t *dims, double *a7);
 int32_t afo_pfmg_probe(int32_t nx, int32_t ny, int32_t nz, const double *a7, int32_t maxl,
                        int32_t *nl, int32_t *cdir, int32_t *active, double *w);
 int32_t afo_tree_create(const afh_tree_desc *desc, int32_t device,

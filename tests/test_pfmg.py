@@ -142,3 +142,90 @@ def test_pfmg_hip_equals_oracle(case):
     # exp/pow in the rate forms
     rel = np.max(np.abs(qa - qb)) / max(np.max(np.abs(qb)), 1e-300)
     assert rel <= 1e-12, rel
+
+
+def _probe_full(n, a7):
+    """The oracle's (and the library's) afh_pfmg_setup, whole."""
+    lib = C.CDLL(capi.ORACLE_LIB)
+    maxl = 64
+    nl, np_ = C.c_int32(), C.c_int64()
+    dims = (C.c_int32 * (3 * maxl))()
+    cdir, act = (C.c_int32 * maxl)(), (C.c_int32 * maxl)()
+    w, off = (C.c_double * maxl)(), (C.c_int64 * (maxl + 1))()
+    args = [C.c_int32(n[0]), C.c_int32(n[1]), C.c_int32(n[2]), a7.ctypes.data_as(C.c_void_p),
+            C.c_int32(maxl), C.byref(nl), C.byref(np_)]
+    assert lib.afo_pfmg_probe_full(*args, None, None, None, None, None, None, None) == 0
+    A = np.zeros(27 * np_.value)
+    P = np.zeros(2 * np_.value)
+    assert lib.afo_pfmg_probe_full(*args, dims, cdir, act, w, off, A.ctypes.data_as(C.c_void_p),
+                                   P.ctypes.data_as(C.c_void_p)) == 0
+    k = nl.value
+    return dict(dims=[list(dims[3 * l:3 * l + 3]) for l in range(k)], cdir=list(cdir[:k]),
+                active=list(act[:k]), w=list(w[:k]), off=list(off[:k + 1]),
+                A=A.reshape(-1, 27), P=P.reshape(-1, 2))
+
+
+def _mg_operator(mg_h):
+    """The folded level-1 operator of an oracle multigrid's last PFMG solve."""
+    lib = C.CDLL(capi.ORACLE_LIB)
+    dims = (C.c_int32 * 3)()
+    assert lib.afo_mg_pfmg_operator(mg_h, dims, None) == 0
+    n = list(dims)
+    a7 = np.zeros((n[0] * n[1] * n[2], 7))
+    assert lib.afo_mg_pfmg_operator(mg_h, dims, a7.ctypes.data_as(C.c_void_p)) == 0
+    return n, a7
+
+
+def _independent_setup_check(n, a7):
+    import pfmg_numpy
+    got = _probe_full(n, a7)
+    want = pfmg_numpy.setup(a7, n)
+    assert got["dims"] == want["dims"]
+    assert got["cdir"] == want["cdir"]
+    assert got["active"] == want["active"]
+    assert got["w"] == want["w"]
+    for l in range(len(want["dims"])):
+        a, b = got["off"][l], got["off"][l + 1]
+        A_c = got["A"][a:b]
+        A_n = pfmg_numpy.stencil_of(want["mats"][l], want["dims"][l])
+        # the Galerkin products sum in another order: to rounding
+        scale = np.abs(A_n).max()
+        np.testing.assert_allclose(A_c, A_n, rtol=1e-12, atol=1e-13 * scale,
+                                   err_msg="operator of level %d" % l)
+        if l < len(want["weights"]):
+            np.testing.assert_allclose(got["P"][a:b], want["weights"][l], rtol=1e-13,
+                                       atol=1e-15, err_msg="interpolation of level %d" % l)
+    return got
+
+
+def test_independent_setup_cube_and_elongated():
+    """The numpy statement of the set-up (tests/pfmg_numpy.py: matrix
+    products R A P instead of afh_pfmg.h's stencil loops) against the shared
+    set-up on the two Poisson grids above."""
+    for n, h in (((8, 8, 8), (2e-3,) * 3), ((8, 8, 32), (625.0,) * 3)):
+        _independent_setup_check(n, _folded_poisson(n, h, "NNNNDD"))
+
+
+@pytest.mark.parametrize("case", ["case_s4", "case_s5"])
+def test_independent_setup_configs(case):
+    """The operators the configurations hand to PFMG, taken from the
+    oracle's multigrids after the set-up's field solves: S4's level-set
+    (electrode) operator on its 8^3 level 1 -- a non-symmetric matrix --,
+    and S5's 8 x 8 x 32 Poisson operator plus its three Helmholtz modes
+    (photoionization: lambda^2 on the diagonal)."""
+    import pfmg_numpy
+    sim = _field_solve_state(case, capi.oracle_library())
+    mgs = [sim.mg]
+    if case == "case_s5":
+        sim.photoi_set_src()
+        mgs += list(sim.helm)
+    for m in mgs:
+        n, a7 = _mg_operator(m.h)
+        got = _independent_setup_check(n, a7)
+        M = pfmg_numpy.setup(a7, n)["mats"][0]
+        if case == "case_s4":
+            assert n == [8, 8, 8]
+            assert abs(M - M.T).max() > 1e-3 * abs(M).max()  # non-symmetric
+        else:
+            assert n == [8, 8, 32] and len(got["cdir"]) == 12
+    assert len(mgs) == (4 if case == "case_s5" else 1)
