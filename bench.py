@@ -331,7 +331,7 @@ def _hip_stream():
 
 
 def local_ranks(lib, config, world, device, coarse, shared_stream=False, grow_cells=0,
-                min_level_cells=MIN_LEVEL_CELLS):
+                min_level_cells=MIN_LEVEL_CELLS, base=None):
     """--transport local: the sharded workload on `world` thread ranks of this
     process (afh_dist AFH_DIST_LOCAL: pack, host barrier, peer copies,
     unpack), every rank on `device`. The same partition, plans and hooks the
@@ -340,9 +340,10 @@ def local_ranks(lib, config, world, device, coarse, shared_stream=False, grow_ce
     from afh import capi
     from afh.dist import NativeGroup, NativeShard
     group = NativeGroup(lib, world)
-    base = None
     if config in DRIVER_CONFIGS:
-        base = build_driver_case(lib, device, config, coarse, grow_cells)
+        # (base: a prepared set-up, e.g. one grown tree for several rank counts)
+        if base is None:
+            base = build_driver_case(lib, device, config, coarse, grow_cells)
         topo = base.af.topology()
         sims = [base.clone(lib, device=device) for _ in range(world)]
         shards = [NativeShard(lib, topo, world, r, transport=capi.DIST_LOCAL, group=group,
@@ -389,7 +390,7 @@ def dist_peer_bytes(lib, shard):
     return np.array(s[:], np.int64), np.array(r[:], np.int64)
 
 
-def bench_local(args, coarse):
+def bench_local(args, coarse, base=None):
     """--transport local --gpus N: N thread ranks on ONE device run the
     sharded unit step; not the metric (the ranks share one GPU), but every
     line of the sharded bench except the RCCL calls, plus what a scaling
@@ -409,7 +410,7 @@ def bench_local(args, coarse):
     try:
         cases, shards, group, base = local_ranks(lib, args.config, world, device, coarse,
                                                  args.shared_stream, args.grow_cells,
-                                                 args.min_level_cells)
+                                                 args.min_level_cells, base)
     finally:
         if args.shared_stream:
             if graphs_env is None:
