@@ -169,6 +169,7 @@ SIGNATURES = {
     "fluid_create": (i32, [_VP, C.POINTER(FluidDesc), _PVP]),
     "fluid_destroy": (i32, [_VP]),
     "electrode_species_bc": (i32, [_VP, i32, i32, i32, i32, P_i32]),
+    "fluid_set_update_mask": (i32, [_VP, i32]),
     "fluid_set_rhs_output": (i32, [_VP, i32, i32]),
     "fluid_set_field_source": (i32, [_VP, i32, f64]),
     "fluid_set_ion_se_yield": (i32, [_VP, f64]),

@@ -372,6 +372,9 @@ class Simulation:
             self.fluid.set_field_source(self.i_phi, -1.0)
             self.mg.set_gradient_output(self.i_efld, -1.0)
         if self.lsf is not None:
+            # forward_euler's flux_update_densities with set_box_mask
+            # (m_fluid.f90:73, 469-483): no update inside the electrode
+            self.fluid.set_update_mask(self.i_lsf)
             self._set_electrode()
 
     def lsf_boundary_value(self):

@@ -508,6 +508,13 @@ class Fluid:
         self.lib.call("electrode_species_bc", self.h, i_lsf, i_1pos_ion,
                       int(neumann_zero), len(ids), ids.ctypes.data_as(capi.P_i32))
 
+    def set_update_mask(self, i_lsf):
+        """set_box_mask's electrode part (src/m_fluid.f90:469-483): cells
+        whose level set cc(i_lsf) is <= 0 are not updated, and boxes of such
+        cells only add no chemistry limit (afh_fluid_set_update_mask; 0:
+        off)."""
+        self.lib.call("fluid_set_update_mask", self.h, int(i_lsf))
+
     def set_rhs_output(self, i_rhs, ghosts=True):
         """Fold field_set_rhs(i_rhs, s_out) into every density update (0: off);
         ghosts=False leaves the rhs ghost cells alone (no solver reads them)."""

@@ -659,6 +659,13 @@ struct UpdArgs {
   int n_ion;
   int ion_s[AFH_MAX_IONS];
   const double *Fion[AFH_MAX_IONS];
+  // set_box_mask's electrode part (src/m_fluid.f90:469-483), or null: a cell
+  // with mlsf <= 0 keeps the weighted sum of the previous states (no source,
+  // no photoionization, no flux divergence); mstat[id - 1] = 0 for a box
+  // with no other cell, which adds no chemistry limit either
+  // (add_source_terms returns early, m_fluid.f90:332)
+  const double *mlsf;
+  const uint8_t *mstat;
 };
 
 // Register-resident species arrays indexed by runtime reaction data (the
@@ -1269,6 +1276,9 @@ __global__ void __launch_bounds__(256, AFH_UPD_MINW)
     fz_carry = fz1;
     const double ev = A.E[x];
     const double pho = A.photo ? A.photo[x] : 0.0;
+    // set_box_mask: `where (lsf <= 0) mask = .false.` (a NaN stays true)
+    const bool upd = !A.mlsf || !(A.mlsf[x] <= 0.0);
+    const bool src = !A.mlsf || A.mstat[id - 1] != 0;
     const int n_prev = NP == MAXPREV ? A.n_prev : NP;
     const int der_q = (NP == MAXPREV || SD) ? A.der_q : -2;  // -2: see below
     double pv[NS][NP], dv[NS];
@@ -1328,7 +1338,7 @@ __global__ void __launch_bounds__(256, AFH_UPD_MINW)
           add_at(der, R.ix_out[q] - 1, rate * R.mult_out[q]);
       }
     }
-    if (A.last_step) {
+    if (A.last_step && src) {
       const double eps = 1e-100;
 #pragma unroll
       for (int s = 0; s < NT; s++) {
@@ -1349,8 +1359,10 @@ __global__ void __launch_bounds__(256, AFH_UPD_MINW)
       add_at(der, A.e_index, pho);
       add_at(der, A.photo_s, pho);
     }
+    if (upd) {
 #pragma unroll
-    for (int s = 0; s < NS; s++) y[s] = y[s] + A.dt * der[s];
+      for (int s = 0; s < NS; s++) y[s] = y[s] + A.dt * der[s];
+    }
     double dtr[3];
 #pragma unroll
     for (int d = 0; d < 3; d++) dtr[d] = A.meta ? A.dt / A.meta[id - 1].dr[d] : A.dt_dr[d];
@@ -1359,8 +1371,8 @@ __global__ void __launch_bounds__(256, AFH_UPD_MINW)
     const double dvz = dtr[2] * (fz0 - fz1);
 #pragma unroll
     for (int s = 0; s < NS; s++)
-      if (s == A.e_index) y[s] = y[s] + div + dvy + dvz;
-    for (int n = 0; n < A.n_ion; n++) {
+      if (s == A.e_index && upd) y[s] = y[s] + div + dvy + dvz;
+    for (int n = 0; n < A.n_ion && upd; n++) {
       const double *G = A.Fion[n] + (size_t)(id - 1) * fsz;
       const double gx0 = G[f0], gx1 = G[f0 + 1], gy0 = G[d3 + f0], gy1 = G[d3 + f0 + nf],
                    gz0 = G[2 * d3 + f0], gz1 = G[2 * d3 + f0 + nf * nf];
@@ -2088,6 +2100,11 @@ struct afh_fluid {
   int net = 0;
   int32_t *d_ids = nullptr;  // box list of afh_electrode_species_bc
   int ids_cap = 0;
+  // afh_fluid_set_update_mask: the level set whose cells <= 0 the update
+  // leaves alone (0: none); per box whether any cell is updated
+  int mask_iv = 0;
+  uint8_t *d_mstat = nullptr;
+  int mstat_cap = 0;
   // afh_fluid_set_rhs_output: the update also writes field_set_rhs(rhs_iv,
   // s_out); rhs_state = the state it was written for (-1: none)
   int rhs_iv = 0, rhs_state = -1;
@@ -2262,6 +2279,7 @@ int32_t afh_fluid_destroy(afh_fluid *f) {
   hipFree(f->d_ids);
   hipFree(f->d_gc2_ion);
   hipFree(f->d_sig);
+  hipFree(f->d_mstat);
   delete f;
   return AFH_OK;
 }
@@ -2302,6 +2320,14 @@ int32_t afh_electrode_species_bc(afh_fluid *f, int32_t i_lsf, int32_t i_1pos_ion
   hipLaunchKernelGGL(k_electrode_bc, dim3((n3 + 255) / 256, n_ids), dim3(256), 0,
                      t->stream, A, f->d_ids, t->nc, t->bsz);
   AFH_LAUNCH_CHECK("k_electrode_bc");
+  return AFH_OK;
+}
+
+int32_t afh_fluid_set_update_mask(afh_fluid *f, int32_t i_lsf) {
+  if (!f) return set_error(AFH_ERR_ARG, "afh_fluid_set_update_mask: null");
+  AFH_LIVE(f->t, "afh_fluid_set_update_mask");
+  if (i_lsf < 0 || i_lsf > f->t->nvc) return set_error(AFH_ERR_ARG, "bad i_lsf");
+  f->mask_iv = i_lsf;
   return AFH_OK;
 }
 
@@ -2535,6 +2561,8 @@ static int32_t upd_args(afh_fluid *f, double dt, int32_t s_deriv, int32_t n_prev
     A.Fion[q] = q < A.n_ion ? t->fcv(f->d.f_ion_flux[q]) : nullptr;
   }
   A.meta = nullptr;
+  A.mlsf = f->mask_iv > 0 ? t->ccv(f->mask_iv) : nullptr;
+  A.mstat = f->d_mstat;
   // algorithmic bytes per cell: each distinct species state read once, the
   // output written once, |E| and 3 fluxes read
   int distinct = n_prev;
@@ -2732,6 +2760,22 @@ int32_t afh_flux_upwind_tree(afh_fluid *f, int32_t s_deriv, double *dt_lim) {
 
 }  // extern "C"
 
+// set_box_mask's box summary: stat[id - 1] = 1 when some interior cell of
+// leaf box ids[blockIdx.x] has lsf > 0 (or NaN: `.not. (lsf <= 0)`), else 0
+__global__ void k_mask_status(const double *__restrict__ lsf, const int32_t *__restrict__ ids,
+                              int nc, size_t bsz, uint8_t *__restrict__ stat) {
+  const int id = ids[blockIdx.x];
+  const double *c = lsf + (size_t)(id - 1) * bsz;
+  const int ng = nc + 2, n3 = nc * nc * nc;
+  int any = 0;
+  for (int q = threadIdx.x; q < n3 && !any; q += blockDim.x) {
+    const int i = q % nc + 1, j = (q / nc) % nc + 1, k = q / (nc * nc) + 1;
+    any = !(c[(k * ng + j) * ng + i] <= 0.0);
+  }
+  any = __syncthreads_or(any);
+  if (threadIdx.x == 0) stat[id - 1] = any ? 1 : 0;
+}
+
 // flux_update_densities' device work; on the last step the chemistry dt
 // minimum folded into reduction slot 2 for the caller to fetch
 static int32_t update_dev(afh_fluid *f, double dt, int32_t s_deriv, int32_t n_prev,
@@ -2748,6 +2792,24 @@ static int32_t update_dev(afh_fluid *f, double dt, int32_t s_deriv, int32_t n_pr
   if ((e = red_init(t, 2, 1e100))) return e;
   f->rhs_state = -1;
   if (A.rhs && (e = red_init(t, 4, 0.0))) return e;
+  if (A.mlsf) {
+    // the boxes' mask summary from the level set as it is now
+    if (f->mstat_cap < t->cap) {
+      // (a queued update may still read the old summary)
+      AFH_HIP(hipStreamSynchronize(t->stream));
+      hipFree(f->d_mstat);
+      f->d_mstat = nullptr;
+      AFH_HIP(hipMalloc(&f->d_mstat, (size_t)t->cap));
+      f->mstat_cap = t->cap;
+    }
+    A.mstat = f->d_mstat;
+    const int nl = t->leaves.off[t->nlvl];
+    for (int c0 = 0; c0 < nl; c0 += 65535) {
+      hipLaunchKernelGGL(k_mask_status, dim3(std::min(65535, nl - c0)), dim3(256), 0,
+                         t->stream, A.mlsf, t->leaves.at(1) + c0, nc, t->bsz, f->d_mstat);
+      AFH_LAUNCH_CHECK("k_mask_status");
+    }
+  }
   auto *red = reinterpret_cast<unsigned long long *>(t->scratch) + 2 * RED_SHARDS;
   // dt / dr from each box's meta record: every leaf level in one launch
   const bool all_lvls = t->all_lvl_launch && t->leaves.off[t->nlvl] <= 65535;
@@ -2936,7 +2998,7 @@ static int32_t fe_dev(afh_fluid *f, double dt, int32_t s_deriv, int32_t n_prev,
                      (nc == 16 || nc == 32 || nc == 64) && !t->any_cflux &&
                      !f->slow_rates && net_ok && f->d.i_gas_dens <= 0 &&
                      f->d.i_photo <= 0 && n_prev <= 2 && !alias &&
-                     f->d.limiter == AFH_LIM_KOREN && f->d.n_ions == 0;
+                     f->d.limiter == AFH_LIM_KOREN && f->d.n_ions == 0 && !f->mask_iv;
   if (!fused) {
     // flux and update back to back on the stream (the flux maxima are not
     // needed before the update); secondary emission from ions at the walls

@@ -824,6 +824,15 @@ module m_afivo_hip
        integer(c_int32_t)          :: afh_flux_upwind_tree
      end function afh_flux_upwind_tree
 
+     ! set_box_mask's electrode part (src/m_fluid.f90:469-483): cells with
+     ! cc(i_lsf) <= 0 are not updated; 0: no mask
+     function afh_fluid_set_update_mask(f, i_lsf) bind(C, name=afh_pfx//"fluid_set_update_mask")
+       import
+       type(c_ptr), value        :: f
+       integer(c_int32_t), value :: i_lsf
+       integer(c_int32_t)        :: afh_fluid_set_update_mask
+     end function afh_fluid_set_update_mask
+
      function afh_flux_update_densities(f, dt, s_deriv, n_prev, s_prev, w_prev, &
           s_out, last_step, dt_lim) bind(C, name=afh_pfx//"flux_update_densities")
        import

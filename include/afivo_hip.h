@@ -477,6 +477,14 @@ int32_t afh_photoi_helmh_compute(afh_mg *const *modes, int32_t n_modes,
  * (m_af_flux_schemes.f90:666-848, src/m_fluid.f90:102-227); dt_lim[2] =
  * (CFL limit for CFL number 1, dielectric relaxation time). */
 int32_t afh_flux_upwind_tree(afh_fluid *f, int32_t s_deriv, double *dt_lim);
+/* set_box_mask's electrode part (src/m_fluid.f90:469-483) for
+ * afh_flux_update_densities / afh_fluid_forward_euler: a cell whose level set
+ * cc(i_lsf) is <= 0 keeps the weighted sum of the previous states -- no
+ * chemistry source, no photoionization, no flux divergence
+ * (m_af_flux_schemes.f90:371-429 with the mask) -- and a leaf box with no
+ * other cell adds no chemistry time-step limit (add_source_terms returns
+ * before it, m_fluid.f90:332). i_lsf = 0: no mask (the default). */
+int32_t afh_fluid_set_update_mask(afh_fluid *f, int32_t i_lsf);
 /* flux_update_densities with add_source_terms / set_box_mask
  * (m_af_flux_schemes.f90:320-436, src/m_fluid.f90:298-515); dt_lim[2] =
  * (chemistry limit on the last step, 1e100 otherwise; energy limit). */

@@ -135,6 +135,7 @@ struct afh_fluid {
   double phi_fac;
   double ion_se_yield; /* afo_fluid_set_ion_se_yield (input_data%ion_se_yield) */
   double rhs_max;
+  int mask_iv; /* afo_fluid_set_update_mask: set_box_mask's level set (0: none) */
   /* generations of rhs_iv and the densities of rhs_state after the update */
   unsigned long long rhs_snap[AFH_MAX_SPECIES + 1];
 };
@@ -2246,6 +2247,13 @@ int32_t afo_fluid_ion_se_flux(afh_fluid *f) {
   return AFH_OK;
 }
 
+/* set_box_mask's electrode part (src/m_fluid.f90:469-483) */
+int32_t afo_fluid_set_update_mask(afh_fluid *f, int32_t i_lsf) {
+  if (!f || i_lsf < 0 || i_lsf > f->t->nvc) return fail(AFH_ERR_ARG, "bad i_lsf");
+  f->mask_iv = i_lsf;
+  return AFH_OK;
+}
+
 int32_t afo_fluid_set_rhs_output(afh_fluid *f, int32_t i_rhs, int32_t ghosts) {
   if (i_rhs < 0 || i_rhs > f->t->nvc) return fail(AFH_ERR_ARG, "bad i_rhs");
   f->rhs_iv = i_rhs;
@@ -2812,8 +2820,11 @@ int32_t afo_flux_upwind_tree(afh_fluid *f, int32_t s_deriv, double *dt_lim) {
 
 /* flux_update_densities (m_af_flux_schemes.f90:320-436) with
  * add_source_terms, get_rates, get_derivatives (src/m_fluid.f90:298-466,
- * src/m_chemistry.f90:565-688); mask is all true (set_box_mask without
- * electrode / dielectric / plasma region). */
+ * src/m_chemistry.f90:565-688) and set_box_mask (469-515): with an electrode
+ * (afo_fluid_set_update_mask) a cell with lsf <= 0 keeps the weighted sum of
+ * the previous states -- its rates still count for the chemistry limit --
+ * and a box without another cell is skipped by add_source_terms altogether
+ * (m_fluid.f90:332); no dielectric or plasma region. */
 int32_t afo_flux_update_densities(afh_fluid *fl, double dt, int32_t s_deriv,
                                   int32_t n_prev, const int32_t *s_prev,
                                   const double *w_prev, int32_t s_out,
@@ -2832,10 +2843,22 @@ int32_t afo_flux_update_densities(afh_fluid *fl, double dt, int32_t s_deriv,
       for (int d = 0; d < 3; d++) dt_dr[d] = dt / B(t, id)->dr[d];
       double *E = ccb(t, fl->d.i_efld, id);
       double *F = fcb(t, fl->d.f_flux, id);
+      const double *lsf = fl->mask_iv > 0 ? ccb(t, fl->mask_iv, id) : NULL;
+      /* if (.not. any(mask)) return (m_fluid.f90:332) */
+      int any_mask = 1;
+      if (lsf) {
+        any_mask = 0;
+        for (int k = 1; k <= nc && !any_mask; k++)
+          for (int j = 1; j <= nc && !any_mask; j++)
+            for (int i = 1; i <= nc && !any_mask; i++)
+              if (!(lsf[IX(t, i, j, k)] <= 0.0)) any_mask = 1;
+      }
       for (int k = 1; k <= nc; k++)
         for (int j = 1; j <= nc; j++)
           for (int i = 1; i <= nc; i++) {
             size_t x = IX(t, i, j, k);
+            /* where (lsf <= 0) mask = .false. */
+            const int upd = !lsf || !(lsf[x] <= 0.0);
             /* weighted sum of previous states */
             for (int s = 0; s < ns; s++) {
               int iv = fl->d.species_iv[s];
@@ -2881,7 +2904,7 @@ int32_t afo_flux_update_densities(afh_fluid *fl, double dt, int32_t s_deriv,
                 der[R->ix_out[m] - 1] =
                     der[R->ix_out[m] - 1] + rate * R->mult_out[m];
             }
-            if (last_step) {
+            if (last_step && any_mask) {
               for (int s = 0; s < ng + ns; s++) {
                 double a, b;
                 if (fl->d.dt_chemistry_nmin > 0) {
@@ -2896,6 +2919,7 @@ int32_t afo_flux_update_densities(afh_fluid *fl, double dt, int32_t s_deriv,
                 if (r < chem_min) chem_min = r;
               }
             }
+            if (!upd) continue; /* masked: the weighted sum only */
             /* photoionization (m_fluid.f90:435-440) */
             if (fl->d.i_photo > 0) {
               const double pho = ccb(t, fl->d.i_photo, id)[x];

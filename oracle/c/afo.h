@@ -51,6 +51,7 @@ int32_t afo_gc_tree(afh_tree *t, int32_t iv, int32_t corners);
 int32_t afo_restrict_tree(afh_tree *t, int32_t iv);
 int32_t afo_tree_copy_cc(afh_tree *t, int32_t iv_from, int32_t iv_to);
 int32_t afo_fluid_set_rhs_output(afh_fluid *f, int32_t i_rhs, int32_t ghosts);
+int32_t afo_fluid_set_update_mask(afh_fluid *f, int32_t i_lsf);
 int32_t afo_fluid_set_field_source(afh_fluid *f, int32_t i_phi, double fac);
 int32_t afo_fluid_set_ion_se_yield(afh_fluid *f, double yield);
 int32_t afo_fluid_ion_se_flux(afh_fluid *f);

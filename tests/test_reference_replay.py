@@ -297,3 +297,27 @@ def test_species_step_replay_ion_se(tmp_path):
     assert not np.array_equal(sims[0].tree.get_cc(e), sims[1].tree.get_cc(e))
     _replay_state(sims[0], "ions", 0, [0], [1.0], 1, 1e-12, tmp_path, cfg_args=args)
     _replay_state(sims[0], "ions", 1, [0, 1], [0.5, 0.5], 0, 5e-13, tmp_path, cfg_args=args)
+
+
+S4_ARGS = ["streamer_3d.cfg", "-input_data%file=../../transport_data/air_chemistry_v2.txt",
+           "-input_data%old_style=f", "-use_electrode=T", "-field_electrode_grounded=T",
+           "-field_rod_r0=0.5 0.5 0.0", "-field_rod_r1=0.5 0.5 0.15",
+           "-field_rod_radius=1e-3", "-refine_electrode_dx=2e-4", "-refine_min_dx=1e-4"]
+
+
+def test_species_step_replay_s4(tmp_path):
+    """BASELINE config 4 (streamer_3d.cfg + air_chemistry_v2 + the grounded
+    rod electrode): after the initial refinement and two time steps, Heun
+    stages 1 and 2 bitwise equal to the reference's forward_euler -- whose
+    flux_update_densities masks the cells inside the electrode (set_box_mask,
+    src/m_fluid.f90:469-483: no sources, no flux divergence where lsf <= 0,
+    and no chemistry time-step limit from boxes wholly inside)."""
+    from afh.driver import Simulation as Sim
+    sim = Sim(capi.oracle_library(), golden.load("case_s4"))
+    sim.start()
+    for _ in range(2):
+        sim.step()
+    cwd = "/root/reference/programs/standard_3d"
+    _replay_state(sim, "s4", 0, [0], [1.0], 1, 1e-12, tmp_path, cwd=cwd, cfg_args=S4_ARGS)
+    _replay_state(sim, "s4", 1, [0, 1], [0.5, 0.5], 0, 5e-13, tmp_path, cwd=cwd,
+                  cfg_args=S4_ARGS)
