@@ -948,6 +948,14 @@ class Simulation:
                     p = p + dens
                 else:
                     raise ValueError("Invalid seed_charge_type")
+            if self.lsf is not None:
+                # every density zero inside the electrode (m_init_cond.f90:
+                # 284-288; lsf as set_lsf_box gives it, _set_electrode)
+                nc = self.af.nc
+                inside = self.lsf(electrode.cell_centers(
+                    self.af.r_min[b], self.af.dr[b], nc, 0, nc + 1)[None])[0] <= 0
+                e = np.where(inside.ravel(), 0.0, e)
+                p = np.where(inside.ravel(), 0.0, p)
             ne[b - 1] = e.reshape(shape)
             ni[b - 1] = p.reshape(shape)
 

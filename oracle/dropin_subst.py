@@ -13,7 +13,7 @@ src = sys.stdin.read()
 subs = [
     ("  use m_model\n", "  use m_model\n  use m_dropin\n", 1),
     ("time_integrator, forward_euler)", "time_integrator, dropin_forward_euler)", 1),
-    ("call mg_init(tree, mg)", "call dropin_mg_init(tree, mg)", None),
+    ("call mg_init(tree, mg)", "call dropin_mg_init(tree, mg, cfg)", None),
     ("call field_compute(tree, mg,", "call dropin_field_compute(tree, mg,", None),
     ("call field_from_potential(tree, mg)", "call dropin_field_from_potential(tree, mg)", None),
 ]

@@ -16,7 +16,14 @@
 !> downloaded into the af_t boxes. Built against the C oracle (symbol
 !> prefix afo_, libafo.so): a CPU run of programs/standard_3d/tests/
 !> test_3d.cfg (tests/test_dropin_streamer.py). Covers what test_3d.cfg
-!> uses: no electrode, dielectric or photoionization, constant gas density.
+!> uses -- no dielectric or photoionization, constant gas density -- and the
+!> electrode (round 6, BASELINE config 4): the reference's own mg_use sets
+!> the level-set box tags and stencils on the af_t tree
+!> (mg_set_operators_tree), which afh_mg_stencils_from_af hands to the
+!> library before every solve and gradient; the density update leaves the
+!> electrode's cells alone (set_box_mask, afh_fluid_set_update_mask); and
+!> set_electrode_densities (electrode_species_bc) is the reference's own, on
+!> the af_t boxes the shim keeps current.
 !>
 !> The level-1 solve is the library's restatement of HYPRE StructPFMG
 !> (AFH_COARSE_PFMG, tol 1e-6, <= 50 iterations: m_af_types.f90:560-565),
@@ -34,6 +41,7 @@ module m_dropin
   use m_lookup_table
   use m_afivo_hip
   use m_afivo_hip_tree
+  use m_config
   implicit none
   private
 
@@ -51,15 +59,23 @@ module m_dropin
   type(afh_reaction), allocatable, target, save :: reac(:)
   type(afh_fluid_desc), save :: fdesc
   logical, save :: have_fdesc = .false.
+  ! field_electrode_grounded (m_field.f90:42, private there): read from the
+  ! configuration in dropin_mg_init
+  logical, save :: electrode_grounded = .false.
 
 contains
 
   !> mg_init (m_af_multigrid.f90:43-109) without the coarse solver's HYPRE
   !> set-up: the operator keys, phi's methods and the box stencils on the
   !> af_t tree (the library builds its own level-1 solver)
-  subroutine dropin_mg_init(tree, mg)
+  subroutine dropin_mg_init(tree, mg, cfg)
     type(af_t), intent(inout) :: tree
     type(mg_t), intent(inout) :: mg
+    type(CFG_t), intent(inout) :: cfg
+    if (ST_use_electrode) call CFG_get(cfg, "field_electrode_grounded", electrode_grounded)
+    ! the level set of the operator (mg_init, m_af_multigrid.f90:75-90)
+    if (iand(mg%operator_mask, mg_lsf_box) > 0) mg%i_lsf = tree%mg_i_lsf
+    if (mg%i_lsf /= -1 .and. .not. associated(mg%lsf_dist)) mg%lsf_dist => mg_lsf_dist_linear
     tree%n_stencil_keys_stored = tree%n_stencil_keys_stored + 1
     mg%operator_key = tree%n_stencil_keys_stored
     tree%n_stencil_keys_stored = tree%n_stencil_keys_stored + 1
@@ -89,18 +105,27 @@ contains
     integer, parameter        :: max_initial_iterations = 100
     real(dp), parameter       :: max_residual = 1e8_dp, min_residual = 1e-6_dp
     real(c_double)            :: max_rhs, residuals(max_initial_iterations)
-    real(dp)                  :: residual_threshold, residual_ratio
+    real(dp)                  :: residual_threshold, residual_ratio, conv_fac
     integer                   :: i
 
-    if (ST_use_electrode .or. ST_use_dielectric) &
-         error stop "dropin: electrode / dielectric cases are not covered"
+    if (ST_use_dielectric) error stop "dropin: dielectric cases are not covered"
     call field_set_voltage(tree, time)
+    ! the electrode's potential (m_field.f90:439-443)
+    if (ST_use_electrode) then
+       if (electrode_grounded) then
+          mg%lsf_boundary_value = 0.0_dp
+       else
+          mg%lsf_boundary_value = current_voltage
+       end if
+    end if
     call bind(tree)
     call afh_check(afh_field_set_rhs_maxabs(fl_h, int(mg%i_rhs, c_int32_t), &
          int(s_in, c_int32_t), max_rhs), "field_set_rhs")
+    ! with an electrode the convergence test is less strict (m_field.f90:426-430)
+    conv_fac = merge(1e-8_dp, 1e-10_dp, ST_use_electrode)
     residual_threshold = max(min_residual, &
          max_rhs * ST_multigrid_max_rel_residual, &
-         1e-10_dp * abs(current_voltage)/(ST_domain_len(NDIM) * af_min_dr(tree)))
+         conv_fac * abs(current_voltage)/(ST_domain_len(NDIM) * af_min_dr(tree)))
 
     if (.not. have_guess) then
        do i = 1, max_initial_iterations
@@ -219,6 +244,9 @@ contains
        call afh_check(afh_mg_create(t_h, md, mg_h), "mg_create")
        if (.not. have_fdesc) call fluid_desc()
        call afh_check(afh_fluid_create(t_h, fdesc, fl_h), "fluid_create")
+       ! forward_euler's set_box_mask (m_fluid.f90:469-483)
+       if (ST_use_electrode) &
+            call afh_check(afh_fluid_set_update_mask(fl_h, int(i_lsf, c_int32_t)), "mask")
     end if
     call set_phi_bc()
     do iv = 1, tree%n_var_cell
@@ -227,6 +255,13 @@ contains
     do iv = 1, tree%n_var_face
        call afh_put_fc_tree(t_h, tree, iv)
     end do
+    if (ST_use_electrode) then
+       ! mg_use (m_af_multigrid.f90:118-126), as the reference's solvers
+       ! begin: box tags and stencils of new boxes, bc_correction with the
+       ! current electrode potential -- then to the library
+       call mg_use(tree, mg)
+       call afh_mg_stencils_from_af(mg_h, tree, mg)
+    end if
   end subroutine bind
 
   !> phi and its copy: field_bc_homogeneous (m_field.f90:547-567) with the

@@ -58,3 +58,50 @@ def test_streamer_program_through_shim_test_3d(tmp_path):
     drv = sim.run()
     assert drv.shape == rows.shape
     assert np.allclose(drv, rows, rtol=1e-7, atol=1e-8)
+
+
+S4_CFG = ["streamer_3d.cfg", "-input_data%file=../../transport_data/air_chemistry_v2.txt",
+          "-input_data%old_style=f", "-use_electrode=T", "-field_electrode_grounded=T",
+          "-field_rod_r0=0.5 0.5 0.0", "-field_rod_r1=0.5 0.5 0.15",
+          "-field_rod_radius=1e-3", "-refine_electrode_dx=2e-4", "-refine_min_dx=1e-4"]
+
+
+def run_dropin_s4(tmp_path, end_time, output_dt):
+    """The reference's streamer program on BASELINE config 4 (streamer_3d.cfg
+    with the grounded rod electrode) through the shim on the C oracle:
+    mg_use's level-set stencils handed over per solve, set_box_mask in the
+    update, the reference's own set_electrode_densities. Returns its
+    regression-log rows."""
+    env = dict(os.environ, OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "8"),
+               OMP_STACKSIZE="512M")
+    cwd = os.path.dirname(TESTS)  # programs/standard_3d
+    out = subprocess.run([EXE] + S4_CFG + ["-output%name=" + str(tmp_path / "s4"),
+                                           "-output%regression_test=T", "-silo_write=f",
+                                           "-end_time=" + repr(end_time),
+                                           "-output%dt=" + repr(output_dt)],
+                         cwd=cwd, env=env, capture_output=True, text=True, timeout=1800)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
+    return np.loadtxt(tmp_path / "s4_rtest.log", skiprows=1, ndmin=2)
+
+
+def test_streamer_program_through_shim_s4(tmp_path):
+    """Config 4's time loop driven by the reference's own streamer.f90
+    (round 6) against afh.driver's restatement of it on the
+    same library: every regression-log row (it, time, dt, the species' sums
+    and maxima) within 1e-7 over the first 40 ps (~80 steps, with regrids),
+    as for test_3d above."""
+    end_time, output_dt = 4e-11, 1e-11
+    rows = run_dropin_s4(tmp_path, end_time, output_dt)
+    import golden
+    from afh import capi
+    from afh.driver import Simulation
+    g = dict(golden.load("case_s4"))
+    g["end_time"] = np.array([end_time])
+    g["output%dt"] = np.array([output_dt])
+    sim = Simulation(capi.oracle_library(), g, coarse_cycles=50, coarse_tol=1e-6,
+                     coarse_mode=capi.COARSE_PFMG)
+    drv = sim.run()
+    assert drv.shape == rows.shape, (drv.shape, rows.shape)
+    rel = np.abs(drv - rows) / np.maximum(np.abs(rows), 1e-300)
+    print("afh.driver vs the reference's streamer (s4), max rel per row", rel.max(axis=1))
+    assert np.allclose(drv, rows, rtol=1e-7, atol=1e-8)
