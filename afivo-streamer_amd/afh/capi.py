@@ -222,6 +222,7 @@ SLOT_MAXRES, SLOT_RHS = 3, 4
 HOOK_FN = C.CFUNCTYPE(i32, C.c_void_p, i32, i32, i32, P_f64, i32)
 PROF_GSRB, PROF_GHOST, PROF_FLUX, PROF_UPDATE, PROF_GSRB_PAIR, PROF_GSRB_PAIR_TILED = 1, 2, 3, 4, 5, 6
 PROF_FE = 7
+PROF_CS = 8
 PROLONG_NONE, PROLONG_LINEAR, PROLONG_LIMIT = 0, 1, 2
 ORACLE_EXTRA = {
     "mg_gsrb_boxes": (i32, [_VP, i32, i32]),

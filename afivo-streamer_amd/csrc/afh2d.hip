@@ -1451,8 +1451,9 @@ int32_t afh_tree_sync(afh_tree *t) {
 
 int32_t afh_profile_enable(afh_tree *t, int32_t kclass) {
   if (!t) return set_error(AFH_ERR_ARG, "afh_profile_enable: null");
-  if (kclass != 0 && kclass != AFH_PROF_GSRB && kclass != AFH_PROF_FLUX)
-    return set_error(AFH_ERR_UNSUPPORTED, "afh_profile_enable: class %d (2-D: GSRB, FLUX)",
+  if (kclass != 0 && kclass != AFH_PROF_GSRB && kclass != AFH_PROF_FLUX &&
+      kclass != AFH_PROF_CS)
+    return set_error(AFH_ERR_UNSUPPORTED, "afh_profile_enable: class %d (2-D: GSRB, FLUX, CS)",
                      kclass);
   H2(hipStreamSynchronize(t->stream));
   t->prof_class = kclass;
@@ -1781,12 +1782,14 @@ static int32_t solve_coarse_pfmg(afh_mg *mg) {
     for (int q = 0; q < 4; q++) mg->pf_bc[q] = M.bc[q].type;
   }
   const int nt = std::min(1024, std::max(256, (int)((n0 + 63) / 64 * 64)));
+  prof_mark(t, AFH_PROF_CS);
   hipLaunchKernelGGL(k2_cs_pfmg, dim3(1), dim3(nt), mg->pf_lds, t->stream, mg->d_pf_lvl,
                      mg->pf_nl, mg->pf_wave, mg->d_pf_A, mg->d_pf_P, mg->d_pf_b2r, mg->d_pf_fmask,
                      t->ccv(mg->d.i_phi), t->ccv(mg->d.i_rhs), t->d_boxes, t->ids.at(1), nid,
                      t->nc, t->bsz, t->bc4(mg->d.i_phi), mg->d.coarse_tol, mg->d.coarse_cycles,
                      mg->d_pf_iters);
   H2_LAUNCH("k2_cs_pfmg");
+  prof_end(t, AFH_PROF_CS, 0.0);
   return gc_lvl(t, 1, mg->d.i_phi, true);
 }
 

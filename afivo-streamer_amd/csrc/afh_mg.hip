@@ -3214,9 +3214,14 @@ static void launch_pair(afh_mg *mg, int lvl, const double *src, double *dst,
   if constexpr (NC >= 32) {
     if (pair_tiles(mg, lvl)) {
       // too few boxes for the chip: 64^3 splits the march over k, 32^3 runs
-      // quarter-box tiles
-      if constexpr (NC == 64)
+      // quarter-box tiles. A rank's share of a sharded level can be a few
+      // boxes (S1-64's level 3 on 8 ranks: 8): 16 chunks of 4 planes then
+      // (round 6; bitwise any split)
+      if constexpr (NC == 64) {
+        if (t->ids.n(lvl) <= 16)
+          return launch_pair2<NC, NC, 1, 16>(mg, lvl, src, dst, cf, inv_c1, e0, e1);
         return launch_pair2<NC, NC, 1, 4>(mg, lvl, src, dst, cf, inv_c1, e0, e1);
+      }
       return launch_pair2<NC, NC / 4, 2>(mg, lvl, src, dst, cf, inv_c1, e0, e1);
     }
   }

@@ -1566,32 +1566,6 @@ __global__ void __launch_bounds__(NTT, AFH_FE_MINW)
     Ul.chem.rm = Tc;
   }
 
-  // The box's x-high faces (behind column i = NC) of the tile's rows, every
-  // plane, one face per thread before the march (TJ rows x NC planes = NT):
-  // inside the march only lane NC - 1 of a wave needs one, and evaluating it
-  // there costs the whole wave a face evaluation per plane (round 6). The
-  // same expressions and operands as the march's (the table read from tdi,
-  // of which T is a copy).
-  __shared__ double xh_v[NT], xh_d[NT], xh_f[NT];
-  double smax_xh;
-  {
-    const int jj = j0 + tid / NC, kk = tid % NC + 1;
-    const int c = (kk * NG + jj) * NG + NC;  // cell (NC, jj, kk)
-    const double n0c = ne[c], np1 = ne[c + 1];
-    const double exq = PHI ? gfx * (ph[c + 1] - ph[c]) : Ef[(kk - 1) * FSK + (jj - 1) * NF + NC];
-    const double u = upwind_t<LIM>(A.lim, ne[c - 1], n0c, np1,
-                                   g2[1 * NN + (kk - 1) * NC + (jj - 1)], exq);
-    double mq, dq2;
-    lds_mu_dc(tdi, A.td, 0.5 * (E[c] + E[c + 1]) * 1e21 * N_inv, mq, dq2);
-    mq = mq * N_inv;
-    const double dxq = dq2 * N_inv;
-    const double vxq = -mq * exq;
-    const double fxq = vxq * u - dxq * ix * (np1 - n0c);
-    if (wf) F[(kk - 1) * FSK + (jj - 1) * NF + NC] = fxq;
-    smax_xh = mq * u;
-    xh_v[tid] = vxq, xh_d[tid] = dxq, xh_f[tid] = fxq;
-  }
-
   auto ne_at = [&](int k, int e) -> double {
     if (e >= NR * RW) return 0.0;
     const int jj = j0 - 2 + e / RW, ii = e % RW - 1;
@@ -1629,19 +1603,21 @@ __global__ void __launch_bounds__(NTT, AFH_FE_MINW)
   }
   // face fields of plane 1 (PHI: k_flux_lds<PHI>'s expressions; pk = phi of
   // the own cell in the current plane)
-  double exl, eyl, eyh, pk = 0.0;
+  double exl, eyl, exh, eyh, pk = 0.0;
   if (PHI) {
     const int c1 = SK + cc;
     pk = ph[c1];
     exl = gfx * (pk - ph[c1 - 1]);
     eyl = gfy * (pk - ph[c1 - NG]);
+    exh = i == NC ? gfx * (ph[c1 + 1] - pk) : 0.0;
     eyh = (jr == TJ - 1) ? gfy * (ph[c1 + NG] - pk) : 0.0;
   } else {
     exl = Ef[fcol], eyl = Ef[FD + fcol];
+    exh = i == NC ? Ef[fcol + 1] : 0.0;
     eyh = (jr == TJ - 1) ? Ef[FD + fcol + NF] : 0.0;
   }
   double mu, dcv;
-  double cmax = -HUGE_VAL, smax = fmax(-HUGE_VAL, smax_xh), cmin = 1e100, rmax = 0.0;
+  double cmax = -HUGE_VAL, smax = -HUGE_VAL, cmin = 1e100, rmax = 0.0;
   // z low face of the box (between planes 0 and 1)
   double vz_lo, dz_lo, fz_lo;
   {
@@ -1671,15 +1647,16 @@ __global__ void __launch_bounds__(NTT, AFH_FE_MINW)
     const int fbn = k * FSK + fcol;
     const int x = k * SK + cc;
     // the next plane's face fields (PHI: the potential of plane k+1, raw --
-    // own cell, x-1, y-1, and y+1 on the last row -- formed
+    // own cell, x-1, y-1, and x+1 / y+1 on the last column / row -- formed
     // where the window advances, below)
-    double ezh, nexl = 0, neyl = 0, neyh = 0, npk = 0;
+    double ezh, nexl = 0, neyl = 0, nexh = 0, neyh = 0, npk = 0;
     if (PHI) {
       const int cn1 = (k + 1) * SK + cc;  // own cell, plane k+1
       npk = ph[cn1];
       if (more) {
         nexl = ph[cn1 - 1];
         neyl = ph[cn1 - NG];
+        if (i == NC) nexh = ph[cn1 + 1];
         if (jr == TJ - 1) neyh = ph[cn1 + NG];
       }
       ezh = gfz * (npk - pk);
@@ -1688,6 +1665,7 @@ __global__ void __launch_bounds__(NTT, AFH_FE_MINW)
       if (more) {
         nexl = Ef[fbn];
         neyl = Ef[FD + fbn];
+        if (i == NC) nexh = Ef[fbn + 1];
         if (jr == TJ - 1) neyh = Ef[FD + fbn + NF];
       }
     }
@@ -1724,9 +1702,15 @@ __global__ void __launch_bounds__(NTT, AFH_FE_MINW)
     }
     double vxh = __shfl_down(vx, 1, 64), dxh = __shfl_down(dx, 1, 64);
     double fxh = __shfl_down(fx, 1, 64);
-    if (i == NC) {  // the box's x-high face: from the pre-pass
-      const int q = jr * NC + (k - 1);
-      vxh = xh_v[q], dxh = xh_d[q], fxh = xh_f[q];
+    if (i == NC) {
+      const double u = upwind_t<LIM>(A.lim, N0[cn - 1], z0, N0[cn + 1], N0[cn + 2], exh);
+      lds_mu_dc(T, A.td, 0.5 * (e0 + E0p[ce + 1]) * 1e21 * N_inv, mu, dcv);
+      mu = mu * N_inv;
+      dxh = dcv * N_inv;
+      vxh = -mu * exh;
+      fxh = vxh * u - dxh * ix * (N0[cn + 1] - z0);
+      if (wf) F[fb + 1] = fxh;
+      smax = fmax(smax, mu * u);
     }
     // y low face
     double vy, dy, fy;
@@ -1884,11 +1868,12 @@ __global__ void __launch_bounds__(NTT, AFH_FE_MINW)
       if (more) {
         exl = gfx * (npk - nexl);
         eyl = gfy * (npk - neyl);
+        exh = i == NC ? gfx * (nexh - npk) : 0.0;
         eyh = (jr == TJ - 1) ? gfy * (neyh - npk) : 0.0;
       }
       pk = npk;
     } else {
-      exl = nexl, eyl = neyl, eyh = neyh;
+      exl = nexl, eyl = neyl, exh = nexh, eyh = neyh;
     }
     __syncthreads();
   }

@@ -597,6 +597,7 @@ int32_t afh_refine_cell_flags(int32_t flag, uint32_t mask, int32_t nc, int32_t b
 #define AFH_PROF_GSRB_PAIR 5 /* fused red+black Gauss-Seidel pair (whole boxes) */
 #define AFH_PROF_GSRB_PAIR_TILED 6 /* the same with NC/4-row tiles */
 #define AFH_PROF_FE 7        /* fused flux + density update (afh_fluid_forward_euler) */
+#define AFH_PROF_CS 8        /* the level-1 solve (2-D build: k2_cs_pfmg; no bytes) */
 int32_t afh_profile_enable(afh_tree *t, int32_t kclass);
 int32_t afh_profile_read(afh_tree *t, double *total_ms, int64_t *launches,
                          double *bytes);

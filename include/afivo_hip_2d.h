@@ -91,8 +91,9 @@ int32_t afh_refine_flags(afh_fluid *f, const afh_refine_desc *d,
                          const uint8_t *electrode_box, int32_t *flags,
                          uint32_t *masks);
 /* kernel timing, as in afivo_hip.h: classes AFH_PROF_GSRB (k2_gsrb on
- * levels of >= 256 boxes, 16 B per cell of a half sweep) and AFH_PROF_FLUX
- * (k2_flux, 48 B per leaf cell) */
+ * levels of >= 256 boxes, 16 B per cell of a half sweep), AFH_PROF_FLUX
+ * (k2_flux, 48 B per leaf cell) and AFH_PROF_CS (the PFMG level-1 solve,
+ * k2_cs_pfmg; 0 bytes) */
 int32_t afh_profile_enable(afh_tree *t, int32_t kclass);
 int32_t afh_profile_read(afh_tree *t, double *total_ms, int64_t *launches, double *bytes);
 /* the output_regression_log reductions; loc = (id, i, j, 0) */

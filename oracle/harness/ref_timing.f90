@@ -18,7 +18,13 @@
 !> mg_init is replaced by its stencil set-up (mg_set_operators_tree), as in
 !> golden_gen, since its coarse-solver set-up needs HYPRE.
 !>
-!> Usage: ref_timing <levels> <repeats> <cfg> [-key=value ...]
+!> Record mode (round 6): instead of <levels>, a record file of
+!> replay_step's format (the topology and every variable of a state the
+!> device driver reached, e.g. streamer_2d.cfg's own set-up tree): the tree
+!> is rebuilt with af_adjust_refinement box for box and loaded, so the
+!> reference is timed on the very tree the GPU bench line runs.
+!>
+!> Usage: ref_timing <levels|record> <repeats> <cfg> [-key=value ...]
 !> Prints "TIMING species_s <s per step> vcycle_s <s per V-cycle> cells <n>".
 #include "cpp_macros.h"
 program ref_timing
@@ -41,12 +47,17 @@ program ref_timing
 
   type(CFG_t)        :: cfg
   type(af_t)         :: tree
-  character(len=512) :: arg
-  integer            :: n, levels, reps, k, lvl
+  type(ref_info_t)   :: ref_info
+  character(len=512) :: arg, rec_file
+  integer            :: n, levels, reps, k, lvl, ios, ur, hid, nvc, nvf, nc_rec, id, iv
+  integer, allocatable :: parent(:), blvl(:), bix(:, :), in_use(:), rid(:)
   real(dp)           :: t0, t_species, t_vcycle, dt_lim, dt, time
+  logical            :: from_record
 
   call get_command_argument(1, arg)
-  read(arg, *) levels
+  read(arg, *, iostat=ios) levels
+  from_record = ios /= 0
+  if (from_record) rec_file = arg
   call get_command_argument(2, arg)
   read(arg, *) reps
   do n = 3, command_argument_count()
@@ -82,7 +93,37 @@ program ref_timing
   call af_init(tree, ST_box_size, ST_domain_origin + ST_domain_len, &
        ST_coarse_grid_size, periodic=ST_periodic, coord=af_xyz, &
        r_min=ST_domain_origin, mem_limit_gb=200.0_dp)
-  call af_refine_up_to_lvl(tree, levels)
+  if (from_record) then
+     ! the recorded topology (replay_step.f90's record layout)
+     open(newunit=ur, file=trim(rec_file), access="stream", form="unformatted", &
+          action="read")
+     read(ur) hid, nvc, nvf, nc_rec
+     if (nvc /= tree%n_var_cell .or. nvf /= tree%n_var_face) &
+          error stop "record: variable registry differs"
+     allocate(parent(hid), blvl(hid), bix(3, hid), in_use(hid), rid(hid))
+     do id = 1, hid
+        read(ur) parent(id), blvl(id), bix(:, id), in_use(id)
+     end do
+     do lvl = 1, 29
+        call af_adjust_refinement(tree, refine_as_recorded, ref_info)
+        if (ref_info%n_add == 0) exit
+     end do
+     rid = 0
+     do id = 1, hid
+        if (in_use(id) == 0) cycle
+        do n = 1, tree%highest_id
+           if (tree%boxes(n)%in_use .and. tree%boxes(n)%lvl == blvl(id)) then
+              if (all(tree%boxes(n)%ix == bix(1:NDIM, id))) then
+                 rid(id) = n
+                 exit
+              end if
+           end if
+        end do
+        if (rid(id) == 0) error stop "recorded box missing in the rebuilt tree"
+     end do
+  else
+     call af_refine_up_to_lvl(tree, levels)
+  end if
 
   ! mg_init (m_af_multigrid.f90:43-109) without the HYPRE set-up
   tree%n_stencil_keys_stored = tree%n_stencil_keys_stored + 1
@@ -96,12 +137,35 @@ program ref_timing
        call af_set_cc_methods(tree, mg%i_phi, mg%sides_bc, mg%sides_rb)
   call mg_set_operators_tree(tree, mg)
 
-  call af_loop_box(tree, init_cond_set_box)
-  call af_loop_box(tree, set_phi)
-  call af_gc_tree(tree, all_densities)
-  call af_gc_tree(tree, [i_phi])
-  call field_from_potential(tree, mg)
-  call af_loop_box(tree, set_rhs)
+  if (from_record) then
+     ! the recorded state (skipping dt .. s_out), every variable of every box
+     read(ur) dt, time, k, k
+     do n = 1, k
+        read(ur) lvl
+     end do
+     do n = 1, k
+        read(ur) t0
+     end do
+     read(ur) lvl
+     do iv = 1, nvc
+        do id = 1, hid
+           if (in_use(id) /= 0) read(ur) tree%boxes(rid(id))%cc(DTIMES(:), iv)
+        end do
+     end do
+     do iv = 1, nvf
+        do id = 1, hid
+           if (in_use(id) /= 0) read(ur) tree%boxes(rid(id))%fc(DTIMES(:), :, iv)
+        end do
+     end do
+     close(ur)
+  else
+     call af_loop_box(tree, init_cond_set_box)
+     call af_loop_box(tree, set_phi)
+     call af_gc_tree(tree, all_densities)
+     call af_gc_tree(tree, [i_phi])
+     call field_from_potential(tree, mg)
+     call af_loop_box(tree, set_rhs)
+  end if
 
   ! species: forward_euler, Heun stages alternating (one warm-up pair)
   dt = 1e-13_dp
@@ -136,11 +200,33 @@ program ref_timing
   end do
   t_vcycle = t_vcycle / reps
 
-  write(*, '(A,ES12.4,A,ES12.4,A,I0,A,I0)') "TIMING species_s ", t_species, &
-       " vcycle_s ", t_vcycle, " cells ", af_num_leaves_used(tree) * ST_box_size**3, &
-       " threads ", omp_get_max_threads()
+  write(*, '(A,ES12.4,A,ES12.4,A,I0,A,I0,A,I0)') "TIMING species_s ", t_species, &
+       " vcycle_s ", t_vcycle, " cells ", af_num_leaves_used(tree) * ST_box_size**NDIM, &
+       " threads ", omp_get_max_threads(), " boxes ", af_num_boxes_used(tree)
 
 contains
+
+  !> Refine the boxes the record lists as parents (replay_step.f90)
+  subroutine refine_as_recorded(box, cell_flags)
+    type(box_t), intent(in) :: box
+    integer, intent(out)    :: cell_flags(DTIMES(box%n_cell))
+    integer                 :: c
+    logical                 :: has_child
+    has_child = .false.
+    do c = 1, hid
+       if (in_use(c) /= 0 .and. blvl(c) == box%lvl + 1) then
+          if (all((bix(1:NDIM, c) + 1) / 2 == box%ix)) then
+             has_child = .true.
+             exit
+          end if
+       end if
+    end do
+    if (has_child) then
+       cell_flags = af_do_ref
+    else
+       cell_flags = af_keep_ref
+    end if
+  end subroutine refine_as_recorded
 
   !> mg_auto_rb (m_af_multigrid.f90:926-940) for a constant-coefficient box
   subroutine auto_rb(boxes, id, nb, iv, op_mask)

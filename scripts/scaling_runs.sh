@@ -3,12 +3,14 @@
 # "s1-64 s5"): the N = 1 bench line + its rocprofv3 kernel trace, and for
 # N in NS (default "2 4 8") the thread-rank bench (--transport local
 # --shared-stream) + its kernel trace; then the projection. Each step under
-# its own time limit; stops at the first failure.
+# its own time limit; stops at the first failure. BENCH_EXTRA: more
+# arguments of the thread-rank runs (e.g. --min-level-cells); TAG: a suffix
+# of the output directory.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 CFGS=${CFGS:-"s1-64 s5"}; NS=${NS:-"2 4 8"}; K=${K:-5}
 for CFG in $CFGS; do
-  D=gpurun_out/scale_$CFG
+  D=gpurun_out/scale_$CFG${TAG}
   mkdir -p $D
   DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 timeout -k 10 ${PTIME:-400} rocprofv3 --kernel-trace \
     --output-format csv -d $D/prof_n1 -o run -- \
@@ -20,7 +22,7 @@ for CFG in $CFGS; do
     timeout -k 10 ${PTIME:-400} rocprofv3 --kernel-trace --output-format csv \
       -d $D/prof_n$N -o run -- \
       python3 bench.py --config $CFG --transport local --gpus $N --shared-stream \
-      --steps $K --warmup 2 > $D/n$N.json 2> $D/n$N.err
+      --steps $K --warmup 2 ${BENCH_EXTRA} > $D/n$N.json 2> $D/n$N.err
     rc=$?; echo "n$N $CFG rc=$rc"; [ $rc -eq 0 ] || { tail -5 $D/n$N.err; exit $rc; }
     cp "$(find $D/prof_n$N -name "*kernel_trace.csv" | head -n 1)" $D/n${N}_trace.csv || exit 1
   done

@@ -314,3 +314,27 @@ def test_electrode_bitwise_equals_oracle(hip, oracle, smoother, coarse):
     ra, rb = (golden.download(c, names[:3]) for c in cases)
     for n in names[:3]:
         assert np.array_equal(ra[n], rb[n]), n
+
+
+@pytest.mark.gpu
+def test_pair_ksplit16_bitwise_split(monkeypatch):
+    """The fused pair on a 64^3 level of at most 16 boxes (a rank's share of
+    a sharded level: S1-64's level 3 on 8 ranks) splits each box's march into
+    16 chunks of 4 planes (k_gsrb_pair2<64, 64, 1, 16>, round 6): bitwise the
+    split half-sweeps with their fills, over two V-cycles."""
+    from afh.streamer import IV, StreamerCase, seed_state, tables_from
+    from afh.tree import uniform_tree
+    from afh import decks
+    td, chem = tables_from(decks.load("tables_air_siglo"))
+    topo = uniform_tree(64, (64, 64, 64), (2e-3, 2e-3, 2e-3), 2)  # 1 + 8 boxes
+    out = []
+    for fused in ("0", "1"):
+        monkeypatch.setenv("AFH_GSRB_FUSED_MIN_BOXES", fused)
+        monkeypatch.setenv("AFH_GRAPHS", "0")
+        c = StreamerCase(capi.hip_library(), topo, td, chem, 5e3, device=0, coarse_cycles=0)
+        seed_state(c, width=1e-4)
+        res = c.field_compute(0, n_vcycles=2, check_residual=False)
+        out.append((np.asarray(res), c.tree.get_cc(IV["phi"])))
+        c.tree.close()
+    assert np.array_equal(out[0][0], out[1][0])
+    assert np.array_equal(out[0][1], out[1][1])
