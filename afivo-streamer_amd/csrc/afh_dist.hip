@@ -71,7 +71,10 @@ struct afh_dist {
 namespace {
 
 // (hook kind, level, layers): HALO / RIMS plans exist for one and two
-// layers (the hook's n: the layers the next reader needs, 0 = DEPTH)
+// layers -- the hook's n: the layers the next reader needs after a fill of
+// every box of the level (RIMS then leaves out the ghost slabs the
+// receiver's own fill copied, afh_dist_core.h halo_regions); n = 0: DEPTH
+// layers after any fill (key layers 0 for RIMS: every ghost cell)
 using Key = std::tuple<int, int, int>;
 
 int32_t exchange(afh_dist *d, const Key &key, int iv) {
@@ -191,8 +194,8 @@ int32_t dist_hook(void *ctx, int32_t kind, int32_t level, int32_t iv, double *va
   case AFH_HOOK_MIN:
   case AFH_HOOK_SUM: return reduce(d, kind, vals, n);
   case AFH_HOOK_CFLUX: return exchange(d, Key(kind, 0, DEPTH), iv);
-  case AFH_HOOK_HALO:
-  case AFH_HOOK_RIMS: return exchange(d, Key(kind, level, n == 1 ? 1 : DEPTH), iv);
+  case AFH_HOOK_HALO: return exchange(d, Key(kind, level, n == 1 ? 1 : DEPTH), iv);
+  case AFH_HOOK_RIMS: return exchange(d, Key(kind, level, n == 1 || n == 2 ? n : 0), iv);
   default: return exchange(d, Key(kind, level, DEPTH), iv);
   }
 }
@@ -381,8 +384,11 @@ int32_t afh_dist_create(afh_tree *t, const afh_tree_desc *desc, const int32_t *o
       for (int q = 0; q < n_ranks; q++) {
         off[q] = total;
         if (q == rank) continue;
-        const auto rs = side == 0 ? plan_regions(tp, own, lp, kind, level, q, rank, depth)
-                                  : plan_regions(tp, own, lp, kind, level, rank, q, depth);
+        // (RIMS key layers 0: DEPTH layers, every ghost cell)
+        const int dep = depth > 0 ? depth : DEPTH;
+        const bool lf = kind == AFH_HOOK_RIMS && depth > 0;
+        const auto rs = side == 0 ? plan_regions(tp, own, lp, kind, level, q, rank, dep, lf)
+                                  : plan_regions(tp, own, lp, kind, level, rank, q, dep, lf);
         for (const Region &r : rs) {
           flat.insert(flat.end(), r.begin(), r.begin() + w);
           flat[flat.size() - w] = g2l[r[0]];
@@ -411,8 +417,8 @@ int32_t afh_dist_create(afh_tree *t, const afh_tree_desc *desc, const int32_t *o
   int32_t e = AFH_OK;
   if (lp) {
     for (int l = lp; l <= tp.nlvl && !e; l++)
-      for (int depth = 1; depth <= DEPTH && !e; depth++)
-        if (!(e = add(AFH_HOOK_HALO, l, depth))) e = add(AFH_HOOK_RIMS, l, depth);
+      for (int depth = 0; depth <= DEPTH && !e; depth++)
+        if (!(e = depth ? add(AFH_HOOK_HALO, l, depth) : AFH_OK)) e = add(AFH_HOOK_RIMS, l, depth);
     if (!e) e = add(AFH_HOOK_CFLUX, 0);
     for (int l : restrict_levels(tp, own, lp))
       if (!e) e = add(AFH_HOOK_RESTRICT, l);

@@ -170,9 +170,11 @@ inline Region region(const Topo &t, int32_t b, const int d[3], bool rims, int de
 }
 
 // Partition.halo_regions
+// local_faces (RIMS after a fill of every box of the level): a ghost slab
+// facing a box the receiver computes is left out (below)
 inline std::vector<Region> halo_regions(const Topo &t, const std::vector<int32_t> &owner, int lp,
                                  int recv, int send, int level, bool rims,
-                                 int depth = DEPTH) {
+                                 int depth = DEPTH, bool local_faces = false) {
   std::vector<Region> out;
   if (!lp || level < lp) return out;
   std::set<Region> regs;
@@ -209,7 +211,14 @@ inline std::vector<Region> halo_regions(const Topo &t, const std::vector<int32_t
       // arrived with the HALO and are unchanged, so only its ghost cells
       // travel (round 6) -- the region less the box interior [1, nc]^3, as
       // disjoint slabs: along dimension k, the cells outside [1, nc] whose
-      // coordinates in the dimensions before k lie inside it
+      // coordinates in the dimensions before k lie inside it. And when the
+      // fill between covered every box of the level (local_faces: a level
+      // fill, not the flux's leaves-only two-layer fill), of a slab whose
+      // face neighbour the receiver computes (its own box or a replicated
+      // one) the part facing that neighbour is left out too: the
+      // receiver's own fill copied it from current data; only the slab's
+      // rims (edge and corner ghosts) travel
+      const afh_box_meta &mb = t.m[r[0] - 1];
       for (int k = 0; k < 3; k++)
         for (int side = 0; side < 2; side++) {
           Region g = r;
@@ -222,7 +231,31 @@ inline std::vector<Region> halo_regions(const Topo &t, const std::vector<int32_t
             if (r[4 + k] <= t.nc) continue;
             g[1 + k] = t.nc + 1;
           }
-          out.push_back(g);
+          const int nb = mb.neighbors[2 * k + side];
+          if (!local_faces || !(nb > 0 && (owner[nb - 1] == recv || owner[nb - 1] < 0))) {
+            out.push_back(g);
+            continue;
+          }
+          // the slab less its face part (transverse coordinates in [1, nc])
+          int jj = 0;
+          for (int j = 0; j < 3; j++) {
+            if (j == k) continue;
+            for (int s2 = 0; s2 < 2; s2++) {
+              Region h = g;
+              for (int q = 0; q < 3; q++)
+                if (q != k && q != j && (jj > 0 && q < j))
+                  h[1 + q] = std::max(g[1 + q], 1), h[4 + q] = std::min(g[4 + q], t.nc);
+              if (s2 == 0) {
+                if (g[1 + j] >= 1) continue;
+                h[4 + j] = 0;
+              } else {
+                if (g[4 + j] <= t.nc) continue;
+                h[1 + j] = t.nc + 1;
+              }
+              out.push_back(h);
+            }
+            jj++;
+          }
         }
     }
   }
@@ -310,10 +343,11 @@ inline std::vector<int> restrict_levels(const Topo &t, const std::vector<int32_t
 
 inline std::vector<Region> plan_regions(const Topo &t, const std::vector<int32_t> &owner, int lp,
                                  int kind, int level, int recv, int send,
-                                 int depth = DEPTH) {
+                                 int depth = DEPTH, bool local_faces = false) {
   switch (kind) {
   case AFH_HOOK_HALO: return halo_regions(t, owner, lp, recv, send, level, false, depth);
-  case AFH_HOOK_RIMS: return halo_regions(t, owner, lp, recv, send, level, true, depth);
+  case AFH_HOOK_RIMS:
+    return halo_regions(t, owner, lp, recv, send, level, true, depth, local_faces);
   case AFH_HOOK_CFLUX: return cflux_regions(t, owner, lp, recv, send);
   case AFH_HOOK_RESTRICT: return octant_regions(t, owner, lp, send, level);
   default: return {};

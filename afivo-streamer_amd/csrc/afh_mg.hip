@@ -3351,8 +3351,10 @@ static int32_t gsrb_boxes(afh_mg *mg, int lvl, bool up, bool stale_ghosts = fals
   // up leg's pairs read the rhs the down leg's exchange brought (nothing
   // writes a level's rhs between its two legs)
   if ((int)mg->rhs_halo.size() < t->nlvl) mg->rhs_halo.assign(t->nlvl, 0);
+  // (one layer: the pair recomputes the neighbours' cells next to the box,
+  // whose rhs is all it reads of theirs)
   if (!(up && mg->rhs_halo[lvl - 1]))
-    if (int32_t e = call_hook(t, AFH_HOOK_HALO, lvl, mg->d.i_rhs)) return e;
+    if (int32_t e = call_hook(t, AFH_HOOK_HALO, lvl, mg->d.i_rhs, nullptr, 1)) return e;
   mg->rhs_halo[lvl - 1] = !up;
   for (int n = n0; n <= n_cycle; n++) {
     const bool to_alt = ((n - n0) & 1) == 0;

@@ -688,6 +688,20 @@ def main():
             unit_step(case, dt, args.warmup + args.steps + 2 + k)
         case.tree.sync()
         lib.call("profile_read", case.tree.h, C.byref(ms), C.byref(nl), C.byref(by))
+    # config 1: the level-1 solve (k2_cs_pfmg) per unit step over two eager
+    # steps, so that the line can also be read without it -- the reference's
+    # CPU timing cannot run it (HYPRE is absent)
+    cs_ms_step = None
+    if two_d:
+        lib.call("profile_enable", case.tree.h, capi.PROF_CS)
+        k0 = args.warmup + args.steps + 8
+        for k in range(2):
+            unit_step(case, dt, k0 + k)
+        case.tree.sync()
+        cms, cnl, cby = C.c_double(), C.c_int64(), C.c_double()
+        lib.call("profile_read", case.tree.h, C.byref(cms), C.byref(cnl), C.byref(cby))
+        lib.call("profile_enable", case.tree.h, 0)
+        cs_ms_step = cms.value / 2
     # the fused species step (k_fe_lds, 64^3 boxes) over two eager unit steps
     # after the timed region -- one Heun stage of each kind: when it takes
     # more of a step than the smoother it is the dominant kernel of the line
@@ -803,17 +817,34 @@ def main():
             out["config"]["ndim"] = 2
             out["config"]["fused_rhs"] = False
             out["config"]["chemistry"] = "air_chemistry_v1 (8 species, 25 reactions)"
-            # the C oracle is 3-D: the reference's own 2-D code, timed in the
-            # build container (its binary does not travel to the GPU box)
-            ref = json.load(open(os.path.join(REPO, "profiles", "r05_ref_cpu_timing_2d.json")))
+            # the line without the level-1 solve, as the reference is timed
+            ms_x = 1e3 * elapsed / args.steps - cs_ms_step
+            out["level1_solve_ms_per_step"] = cs_ms_step
+            out["ms_per_step_without_level1"] = ms_x
+            out["value_without_level1"] = ncell / (ms_x * 1e-3)
+            # a set-up tree of 17.5 K cells is launch-bound: no kernel's HBM
+            # fraction says anything about it
+            out["roofline"]["note"] = ("launch-bound configuration (tens of kernels per "
+                                       "step, microseconds each): the fraction is not a "
+                                       "measure of kernel quality here")
+            # the C oracle is 3-D: the reference's own 2-D code on the same
+            # set-up tree (scripts/record_setup_state.py -> ref_timing's
+            # record mode), timed in the build container -- its binary does
+            # not travel to the GPU box
+            ref = json.load(open(os.path.join(REPO, "profiles", "r06_ref_cpu_timing_2d.json")))
             best = max(ref["threads"].items(), key=lambda kv: kv[1]["cell_updates_per_s"])
             out["cpu_baseline"] = {
                 "value": best[1]["cell_updates_per_s"], "unit": "cell-updates/s",
                 "cores": int(best[0]), "kind": "reference",
-                "sample": "the reference's 2-D forward_euler + one V(2,2)-cycle (no level-1 "
-                          "solve) on a uniform %d-cell tree of streamer_2d.cfg, measured in "
-                          "the build container (profiles/r05_ref_cpu_timing_2d.json), not on "
-                          "this host" % ref["cells"]}
+                "compare_with": "value_without_level1",
+                "sample": "the reference's 2-D forward_euler + one V(2,2)-cycle without the "
+                          "level-1 solve on streamer_2d.cfg's own set-up tree (%d boxes, %d "
+                          "leaf cells: the tree of this line), measured in the build "
+                          "container (profiles/r06_ref_cpu_timing_2d.json), not on this host"
+                          % (ref["boxes"], ref["cells"])}
+            if ref["cells"] != ncell:
+                out["cpu_baseline"]["warning"] = "timed on a %d-cell tree, this line %d" % (
+                    ref["cells"], ncell)
         if args.config in DRIVER_CONFIGS:
             g = sim.grown
             out["config"]["tree"] = {"leaf_cells_setup": g["leaf_cells_initial"],
