@@ -142,7 +142,6 @@ class Partition:
         self.parent = np.asarray(topo["meta_parent"])
         self.children = np.asarray(topo["meta_children"])
         self.nmat = np.asarray(topo["meta_neighbor_mat"]).reshape(self.nb, 27)
-        self.neighbors = np.asarray(topo["meta_neighbors"]).reshape(self.nb, 6)
         self.ix = np.asarray(topo["meta_ix"])
         ids = {l: np.asarray(topo["lvl_ids_%d" % l], np.int64)
                for l in range(1, self.nlvl + 1)}
@@ -241,7 +240,7 @@ class Partition:
                 lo.append(0 if rims else 1), hi.append(nc + 1 if rims else nc)
         return (int(b), *lo, *hi)
 
-    def halo_regions(self, recv_rank, send_rank, level, rims, depth=DEPTH, local_faces=False):
+    def halo_regions(self, recv_rank, send_rank, level, rims, depth=DEPTH):
         """Regions of boxes owned by send_rank that recv_rank reads around its
         boxes of `level` (sorted, duplicates and contained regions removed),
         `depth` layers deep (the library asks for one layer where no fused
@@ -275,10 +274,9 @@ class Partition:
                 # RIMS follows the HALO of the same variable and level with
                 # only a ghost fill between: the interior arrived with the
                 # HALO, only the ghost cells travel -- the region less
-                # [1, nc]^3 as disjoint slabs -- and of a slab whose face
-                # neighbour the receiver computes, only the rims (the face
-                # part its own fill copied from current data; afh_dist_core.h
-                # halo_regions)
+                # [1, nc]^3 as disjoint slabs (afh_dist_core.h halo_regions;
+                # a rank's fills do not write its replicas' ghost cells, so
+                # all of them travel)
                 for k in range(3):
                     for side in (0, 1):
                         g = list(r)
@@ -292,27 +290,7 @@ class Partition:
                             if r[4 + k] <= nc:
                                 continue
                             g[1 + k] = nc + 1
-                        nb = int(self.neighbors[r[0] - 1][2 * k + side])
-                        if not local_faces or not (nb > 0 and (
-                                self.owner[nb - 1] == recv_rank or self.owner[nb - 1] < 0)):
-                            out.append(tuple(g))
-                            continue
-                        trans = [j for j in range(3) if j != k]
-                        for jj, j in enumerate(trans):
-                            for s2 in (0, 1):
-                                h = list(g)
-                                if jj > 0:
-                                    q = trans[0]
-                                    h[1 + q], h[4 + q] = max(g[1 + q], 1), min(g[4 + q], nc)
-                                if s2 == 0:
-                                    if g[1 + j] >= 1:
-                                        continue
-                                    h[4 + j] = 0
-                                else:
-                                    if g[4 + j] <= nc:
-                                        continue
-                                    h[1 + j] = nc + 1
-                                out.append(tuple(h))
+                        out.append(tuple(g))
         return out
 
     def cflux_regions(self, recv_rank, send_rank):

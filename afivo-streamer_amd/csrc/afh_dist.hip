@@ -61,6 +61,11 @@ struct afh_dist {
     int32_t send_plan = -1, recv_plan = -1;
     double *send_buf = nullptr, *recv_buf = nullptr;
     std::vector<int64_t> send_off, send_n, recv_off, recv_n;  // per peer
+    // RIMS with local faces: (local box, face 1..6) pairs whose face ghosts
+    // this rank copies from its own face neighbour after the exchange
+    int32_t *d_fc = nullptr;
+    int32_t n_fc = 0;
+    bool local_only = false;  // the same on every rank: nothing to send anywhere
   };
   std::map<std::tuple<int, int, int>, Plan> plans;  // (hook kind, level, layers)
   double *d_red = nullptr;
@@ -72,16 +77,75 @@ namespace {
 
 // (hook kind, level, layers): HALO / RIMS plans exist for one and two
 // layers -- the hook's n: the layers the next reader needs after a fill of
-// every box of the level (RIMS then leaves out the ghost slabs the
-// receiver's own fill copied, afh_dist_core.h halo_regions); n = 0: DEPTH
-// layers after any fill (key layers 0 for RIMS: every ghost cell)
+// every box of the level (RIMS then leaves out the face ghosts of replicas
+// next to a box this rank computes, afh_dist_core.h halo_regions, and
+// copies them here: k_face_copy); n = 0: DEPTH layers after any fill (key
+// layers 0 for RIMS: every ghost cell travels)
 using Key = std::tuple<int, int, int>;
+
+// The face part ([1, nc]^2) of the ghost layer of face nb of box list[2 q],
+// nb = list[2 q + 1], filled by the receiver: copied from the same-level
+// neighbour's boundary layer, or the domain boundary's condition from the
+// box's own cells (af_gc_box, m_af_ghostcell.f90:64-120, bc_to_gc 173-279).
+// One thread per cell, one block row per pair.
+__global__ void k_face_fill(double *__restrict__ v, const afh_box_meta *__restrict__ meta,
+                            const int32_t *__restrict__ list, int nc, size_t bsz, GcArgs ga) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nc * nc) return;
+  const int id = list[2 * blockIdx.y], nb = list[2 * blockIdx.y + 1];
+  const int d = (nb - 1) >> 1;
+  const bool low = ((nb - 1) & 1) == 0;
+  const afh_box_meta &m = meta[id - 1];
+  const int src = m.neighbors[nb - 1];
+  const int a = t % nc + 1, b = t / nc + 1;
+  const int ta = (d == 0) ? 1 : 0, tb = (d == 2) ? 1 : 2;
+  int p[3];
+  p[ta] = a;
+  p[tb] = b;
+  p[d] = low ? 0 : nc + 1;
+  const int ng = nc + 2;
+  double *c = v + (size_t)(id - 1) * bsz;
+  if (src > 0) {
+    int q[3] = {p[0], p[1], p[2]};
+    q[d] = low ? nc : 1;
+    c[ix3(ng, p[0], p[1], p[2])] = v[(size_t)(src - 1) * bsz + ix3(ng, q[0], q[1], q[2])];
+    return;
+  }
+  c[ix3(ng, p[0], p[1], p[2])] =
+      gc_face_nocopy(v, meta, m, nb, p, a, b, nc, bsz, ga.bc[nb - 1], ga.rb,
+                     [&](const int *q) { return c[ix3(ng, q[0], q[1], q[2])]; });
+}
+
+// the receiver's own face fills of a RIMS plan (k_face_fill); the bc of the
+// alt image is its source variable's
+int32_t face_fill(afh_tree *t, const afh_dist::Plan &p, int iv) {
+  const GcArgs ga = t->gc_args(iv ? iv : t->alt_of);
+  for (int q0 = 0; q0 < p.n_fc; q0 += 65535) {
+    hipLaunchKernelGGL(k_face_fill, dim3((t->nc * t->nc + 255) / 256, std::min(65535, p.n_fc - q0)),
+                       dim3(256), 0, t->stream, t->var(iv), t->d_boxes, p.d_fc + 2 * (size_t)q0,
+                       t->nc, t->bsz, ga);
+    AFH_LAUNCH_CHECK("k_face_fill");
+  }
+  return AFH_OK;
+}
 
 int32_t exchange(afh_dist *d, const Key &key, int iv) {
   auto it = d->plans.find(key);
   if (it == d->plans.end()) return AFH_OK;
   const afh_dist::Plan &p = it->second;
   afh_tree *t = d->t;
+  // no rank sends anything (every rank fills the faces itself): no exchange
+  if (p.local_only) return face_fill(t, p, iv);
+  // AFH_DIST_LOG=1: one stderr line per exchange (rank, kind, level,
+  // layers, variable, doubles sent) -- what a step exchanges, for the
+  // scaling work
+  static const bool log = getenv("AFH_DIST_LOG") && atoi(getenv("AFH_DIST_LOG"));
+  if (log) {
+    int64_t n = 0;
+    for (int q = 0; q < d->n; q++) n += p.send_n[q];
+    fprintf(stderr, "XCHG r%d k%d l%d n%d v%d %lld\n", d->rank, std::get<0>(key),
+            std::get<1>(key), std::get<2>(key), iv, (long long)n);
+  }
   int32_t e = AFH_OK;
   if (p.send_plan >= 0) e = afh_plan_pack(t, p.send_plan, iv, p.send_buf);
   if (d->transport == AFH_DIST_RCCL) {
@@ -133,6 +197,7 @@ int32_t exchange(afh_dist *d, const Key &key, int iv) {
   }
   if (p.recv_plan >= 0) e = afh_plan_unpack(t, p.recv_plan, iv, p.recv_buf);
   if (e) return e;
+  if ((e = face_fill(t, p, iv))) return e;
   d->n_exchanges++;
   for (int q = 0; q < d->n; q++) {
     d->bytes += 8 * (p.send_n[q] + p.recv_n[q]);
@@ -195,7 +260,8 @@ int32_t dist_hook(void *ctx, int32_t kind, int32_t level, int32_t iv, double *va
   case AFH_HOOK_SUM: return reduce(d, kind, vals, n);
   case AFH_HOOK_CFLUX: return exchange(d, Key(kind, 0, DEPTH), iv);
   case AFH_HOOK_HALO: return exchange(d, Key(kind, level, n == 1 ? 1 : DEPTH), iv);
-  case AFH_HOOK_RIMS: return exchange(d, Key(kind, level, n == 1 || n == 2 ? n : 0), iv);
+  case AFH_HOOK_RIMS:
+    return exchange(d, Key(kind, level, (n >= 1 && n <= 2) || (n >= 11 && n <= 12) ? n : 0), iv);
   default: return exchange(d, Key(kind, level, DEPTH), iv);
   }
 }
@@ -375,6 +441,15 @@ int32_t afh_dist_create(afh_tree *t, const afh_tree_desc *desc, const int32_t *o
     p.recv_off.assign(n_ranks, 0), p.recv_n.assign(n_ranks, 0);
     const bool fc = kind == AFH_HOOK_CFLUX;
     const int w = fc ? 8 : 7, lo = fc ? 2 : 1;
+    std::set<int32_t> fc_boxes;
+    const bool pair = kind == AFH_HOOK_RIMS && depth > 10;
+    std::map<int, std::vector<char>> stored;
+    auto stored_of = [&](int r) -> const std::vector<char> & {
+      auto it = stored.find(r);
+      if (it == stored.end())
+        it = stored.emplace(r, level_stored(tp, own, lp, r, n_ranks, level)).first;
+      return it->second;
+    };
     for (int side = 0; side < 2; side++) {
       // the regions of every peer, peer after peer, in one plan
       std::vector<int32_t> flat;
@@ -384,11 +459,22 @@ int32_t afh_dist_create(afh_tree *t, const afh_tree_desc *desc, const int32_t *o
       for (int q = 0; q < n_ranks; q++) {
         off[q] = total;
         if (q == rank) continue;
-        // (RIMS key layers 0: DEPTH layers, every ghost cell)
-        const int dep = depth > 0 ? depth : DEPTH;
-        const bool lf = kind == AFH_HOOK_RIMS && depth > 0;
-        const auto rs = side == 0 ? plan_regions(tp, own, lp, kind, level, q, rank, dep, lf)
-                                  : plan_regions(tp, own, lp, kind, level, rank, q, dep, lf);
+        const int dep = depth > 10 ? depth - 10 : depth > 0 ? depth : DEPTH;
+        const bool lf = kind == AFH_HOOK_RIMS && depth > 0 && depth < 10;
+        // (pair mode, layers 11 / 12: the sender's regions follow the
+        // receiver's stored boxes)
+        const std::vector<char> *pm = nullptr;
+        if (pair) pm = side == 0 ? &stored_of(q) : &stored_of(rank);
+        const auto rs = side == 0 ? plan_regions(tp, own, lp, kind, level, q, rank, dep, lf, pm)
+                                  : plan_regions(tp, own, lp, kind, level, rank, q, dep, lf, pm);
+        // the faces this rank fills itself: of the boxes whose ghost cells
+        // it receives, the faces next to a box it computes (local faces), or
+        // next to a stored box or the domain boundary (pair mode)
+        if (lf && side == 1)
+          for (const Region &r : rs) fc_boxes.insert(r[0]);
+        if (pair && side == 1)
+          for (const Region &r : halo_regions(tp, own, lp, rank, q, level, true, dep))
+            fc_boxes.insert(r[0]);
         for (const Region &r : rs) {
           flat.insert(flat.end(), r.begin(), r.begin() + w);
           flat[flat.size() - w] = g2l[r[0]];
@@ -411,14 +497,41 @@ int32_t afh_dist_create(afh_tree *t, const afh_tree_desc *desc, const int32_t *o
       if (n && hipMalloc(&buf, sizeof(double) * n) != hipSuccess)
         return set_error(AFH_ERR_DEVICE, "exchange buffer");
     }
+    std::vector<int32_t> fcl;
+    for (int32_t b : fc_boxes)
+      for (int f = 0; f < 6; f++) {
+        const int nb = tp.m[b - 1].neighbors[f];
+        const bool fill = pair ? (nb < 0 || (nb > 0 && stored_of(rank)[nb]))
+                               : (nb > 0 && (own[nb - 1] == rank || own[nb - 1] < 0));
+        if (fill) fcl.push_back(g2l[b]), fcl.push_back(f + 1);
+      }
+    if (pair) {
+      // nothing to send between any two ranks: every rank only fills
+      bool any = false;
+      for (int r = 0; r < n_ranks && !any; r++)
+        for (int q = 0; q < n_ranks && !any; q++)
+          if (q != r)
+            any = !halo_regions(tp, own, lp, r, q, level, true, depth - 10, false, &stored_of(r))
+                       .empty();
+      p.local_only = !any;
+    }
+    if (!fcl.empty()) {
+      if (hipMalloc(&p.d_fc, sizeof(int32_t) * fcl.size()) != hipSuccess ||
+          hipMemcpy(p.d_fc, fcl.data(), sizeof(int32_t) * fcl.size(), hipMemcpyHostToDevice) !=
+              hipSuccess)
+        return set_error(AFH_ERR_DEVICE, "face copy list");
+      p.n_fc = (int32_t)(fcl.size() / 2);
+    }
     d->plans[Key(kind, level, depth)] = std::move(p);
     return AFH_OK;
   };
   int32_t e = AFH_OK;
   if (lp) {
     for (int l = lp; l <= tp.nlvl && !e; l++)
-      for (int depth = 0; depth <= DEPTH && !e; depth++)
+      for (int depth = 0; depth <= DEPTH && !e; depth++) {
         if (!(e = depth ? add(AFH_HOOK_HALO, l, depth) : AFH_OK)) e = add(AFH_HOOK_RIMS, l, depth);
+        if (!e && depth) e = add(AFH_HOOK_RIMS, l, 10 + depth);
+      }
     if (!e) e = add(AFH_HOOK_CFLUX, 0);
     for (int l : restrict_levels(tp, own, lp))
       if (!e) e = add(AFH_HOOK_RESTRICT, l);
@@ -452,6 +565,7 @@ int32_t afh_dist_destroy(afh_dist *d) {
   for (auto &kv : d->plans) {
     hipFree(kv.second.send_buf);
     hipFree(kv.second.recv_buf);
+    hipFree(kv.second.d_fc);
   }
   hipFree(d->d_red);
   if (d->group && d->group->rank[d->rank] == d) d->group->rank[d->rank] = nullptr;

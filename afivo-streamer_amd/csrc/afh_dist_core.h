@@ -172,9 +172,18 @@ inline Region region(const Topo &t, int32_t b, const int d[3], bool rims, int de
 // Partition.halo_regions
 // local_faces (RIMS after a fill of every box of the level): a ghost slab
 // facing a box the receiver computes is left out (below)
+// pair (round 6: RIMS before a fused pair on a level no finer level
+// interpolates from): of the ghost slabs only the face parts ([1, nc] in
+// both tangential directions; the 6-point stencil of the pair's recomputed
+// neighbour cells reads no edge or corner ghost) of faces the receiver
+// cannot fill itself -- faces at a refinement boundary, or whose same-level
+// neighbour it does not store (`stored`, by global id); a face next to a
+// stored box or the domain boundary it fills itself (afh_dist.hip
+// k_face_fill)
 inline std::vector<Region> halo_regions(const Topo &t, const std::vector<int32_t> &owner, int lp,
                                  int recv, int send, int level, bool rims,
-                                 int depth = DEPTH, bool local_faces = false) {
+                                 int depth = DEPTH, bool local_faces = false,
+                                 const std::vector<char> *pair = nullptr) {
   std::vector<Region> out;
   if (!lp || level < lp) return out;
   std::set<Region> regs;
@@ -211,12 +220,13 @@ inline std::vector<Region> halo_regions(const Topo &t, const std::vector<int32_t
       // arrived with the HALO and are unchanged, so only its ghost cells
       // travel (round 6) -- the region less the box interior [1, nc]^3, as
       // disjoint slabs: along dimension k, the cells outside [1, nc] whose
-      // coordinates in the dimensions before k lie inside it. And when the
-      // fill between covered every box of the level (local_faces: a level
-      // fill, not the flux's leaves-only two-layer fill), of a slab whose
-      // face neighbour the receiver computes (its own box or a replicated
-      // one) the part facing that neighbour is left out too: the
-      // receiver's own fill copied it from current data; only the slab's
+      // coordinates in the dimensions before k lie inside it. And with
+      // local_faces (the level fills of the multigrid, not the flux's
+      // leaves-only fill), of a slab whose face neighbour the receiver
+      // computes (its own box or a replicated one) the part facing that
+      // neighbour is left out too: the receiver copies it from that
+      // neighbour itself after the exchange (afh_dist.hip face_copies, a
+      // same-level face copy as the owner's fill made); only the slab's
       // rims (edge and corner ghosts) travel
       const afh_box_meta &mb = t.m[r[0] - 1];
       for (int k = 0; k < 3; k++)
@@ -232,6 +242,13 @@ inline std::vector<Region> halo_regions(const Topo &t, const std::vector<int32_t
             g[1 + k] = t.nc + 1;
           }
           const int nb = mb.neighbors[2 * k + side];
+          if (pair) {
+            if (nb < 0 || (nb > 0 && (*pair)[nb])) continue;  // filled by the receiver
+            for (int j = 0; j < 3; j++)
+              if (j != k) g[1 + j] = std::max(g[1 + j], 1), g[4 + j] = std::min(g[4 + j], t.nc);
+            out.push_back(g);
+            continue;
+          }
           if (!local_faces || !(nb > 0 && (owner[nb - 1] == recv || owner[nb - 1] < 0))) {
             out.push_back(g);
             continue;
@@ -260,6 +277,19 @@ inline std::vector<Region> halo_regions(const Topo &t, const std::vector<int32_t
     }
   }
   return out;
+}
+
+// The boxes of `level` a rank holds current data of around its boxes: the
+// ones it computes and the HALO replicas (by global id; RIMS pair mode)
+inline std::vector<char> level_stored(const Topo &t, const std::vector<int32_t> &owner, int lp,
+                                      int rank, int n_ranks, int level) {
+  std::vector<char> st(t.nb + 1, 0);
+  for (int32_t a : t.ids[level - 1])
+    if (owner[a - 1] == rank || owner[a - 1] < 0) st[a] = 1;
+  for (int q = 0; q < n_ranks; q++)
+    if (q != rank)
+      for (const Region &r : halo_regions(t, owner, lp, rank, q, level, false)) st[r[0]] = 1;
+  return st;
 }
 
 // Partition.cflux_regions (8 ints: id, dim, lo, hi; face indices)
@@ -343,11 +373,12 @@ inline std::vector<int> restrict_levels(const Topo &t, const std::vector<int32_t
 
 inline std::vector<Region> plan_regions(const Topo &t, const std::vector<int32_t> &owner, int lp,
                                  int kind, int level, int recv, int send,
-                                 int depth = DEPTH, bool local_faces = false) {
+                                 int depth = DEPTH, bool local_faces = false,
+                                 const std::vector<char> *pair = nullptr) {
   switch (kind) {
   case AFH_HOOK_HALO: return halo_regions(t, owner, lp, recv, send, level, false, depth);
   case AFH_HOOK_RIMS:
-    return halo_regions(t, owner, lp, recv, send, level, true, depth, local_faces);
+    return halo_regions(t, owner, lp, recv, send, level, true, depth, local_faces, pair);
   case AFH_HOOK_CFLUX: return cflux_regions(t, owner, lp, recv, send);
   case AFH_HOOK_RESTRICT: return octant_regions(t, owner, lp, send, level);
   default: return {};

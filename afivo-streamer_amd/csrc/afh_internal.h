@@ -146,6 +146,7 @@ struct afh_tree {
   // shared by every multigrid on the tree (one stream: the image is only
   // live inside one fused pair); freed with the last of them
   double *alt = nullptr;
+  int alt_of = 0;  // the variable whose image alt holds (its ghost-cell methods)
   int alt_refs = 0;
   // independent per-box work of every leaf level in one launch where the
   // kernel reads the box's level data from its meta record (flux of small

@@ -2647,9 +2647,9 @@ struct PfBc {
   afh_bc bc[6];
 };
 
-// LDS: x images, b, r and the wave levels' operators in LDS (else the
-// global scratch gx, 4 np doubles, and the operators from A)
-template <bool LDS>
+// LDS: x images, b, r in LDS (else the global scratch gx, 4 np doubles);
+// STAGE: the wave levels' operators too (else read from A)
+template <bool LDS, bool STAGE>
 __global__ void __launch_bounds__(1024)
     k_cs_pfmg(const PfLvl *__restrict__ Lg, int nl, int wave_from, const double *__restrict__ A,
               const double *__restrict__ Pw, const double *__restrict__ b2r,
@@ -2660,13 +2660,20 @@ __global__ void __launch_bounds__(1024)
               double tol, int max_iter, int *__restrict__ iters_out) {
   extern __shared__ double pf_sm[];
   __shared__ double slot;
+#ifdef AFH_PFMG_TIMING
+  if (threadIdx.x == 0) {
+    for (int q = 0; q < 23; q++) afh_pf::pf_tacc()[q] = 0;
+    afh_pf::pf_tacc()[23] = clock64();
+  }
+  const unsigned long long w0 = wall_clock64();
+#endif
   const PfLvl L0 = Lg[0];
   const int np = Lg[nl - 1].off + Lg[nl - 1].np;
   const int soff = wave_from < nl ? Lg[wave_from].off : np;
   double *X0 = LDS ? pf_sm : gx;
   double *X1 = X0 + np, *b = X0 + 2 * np, *r = X0 + 3 * np;
   const double *Aw = A + (size_t)27 * soff;
-  if (LDS) {
+  if (LDS && STAGE) {
     double *As = pf_sm + 4 * np;
     for (int u = threadIdx.x; u < 27 * (np - soff); u += blockDim.x) As[u] = Aw[u];
     Aw = As;
@@ -2683,6 +2690,7 @@ __global__ void __launch_bounds__(1024)
     const size_t c = (size_t)(id - 1) * bsz + ix3(nc + 2, i, j, k);
     double rv = rhs[c];
     const int fm = fmask[p];
+#pragma unroll
     for (int nb = 0; nb < 6; nb++)
       if ((fm >> nb) & 1) rv = rv + b2r[(size_t)nb * L0.np + p] * B.bc[nb].value;
     if (vbc[q]) rv = rv + vbc[q][e];
@@ -2690,6 +2698,7 @@ __global__ void __launch_bounds__(1024)
     X0[p] = phi[c];
   }
   __syncthreads();
+  PF_T(10);
   int cur = 0;
   const int iters = afh_pf::pf_solve_block(Lg, nl, wave_from, A, Aw, soff, Pw, X0, X1, b, r,
                                            &slot, tol, max_iter, &cur);
@@ -2705,6 +2714,18 @@ __global__ void __launch_bounds__(1024)
     phi[(size_t)(id - 1) * bsz + ix3(nc + 2, i, j, k)] = x[p];
   }
   if (threadIdx.x == 0 && iters_out) *iters_out = iters;
+#ifdef AFH_PFMG_TIMING
+  PF_T(11);
+  if (threadIdx.x == 0) {
+    const unsigned long long *a = afh_pf::pf_tacc();
+    printf("PFTIME nt %d np %d nl %d wave %d iters %d wall10ns %llu | relax %llu/%llu res %llu/%llu "
+           "rstr %llu/%llu interp %llu/%llu dot %llu/%llu handoff %llu | wave relax %llu/%llu "
+           "res %llu/%llu rstr %llu/%llu interp %llu/%llu | gather %llu scatter %llu\n",
+           (int)blockDim.x, np, nl, wave_from, iters, wall_clock64() - w0, a[0], a[12], a[1],
+           a[13], a[2], a[14], a[3], a[15], a[4], a[16], a[5], a[6], a[18], a[7], a[19], a[8],
+           a[20], a[9], a[21], a[10], a[11]);
+  }
+#endif
 }
 
 }  // namespace afh
@@ -2847,6 +2868,7 @@ struct afh_mg {
   std::vector<double> pf_a7;
   uint64_t pf_v1_gen = 0, pf_meth_gen = UINT64_MAX;
   int pf_nl = 0, pf_np = 0, pf_lds = 0, pf_wave = 0;
+  bool pf_stage = false;
   PfLvl *d_pf_lvl = nullptr;
   double *d_pf_A = nullptr, *d_pf_P = nullptr, *d_pf_b2r = nullptr, *d_pf_x = nullptr;
   uint8_t *d_pf_fmask = nullptr;
@@ -3347,6 +3369,7 @@ static int32_t gsrb_boxes(afh_mg *mg, int lvl, bool up, bool stale_ghosts = fals
   }
   double *phi = t->ccv(mg->d.i_phi);
   const afh::GcArgs ga = t->gc_args(mg->d.i_phi);
+  t->alt_of = mg->d.i_phi;
   // the pair recomputes neighbours' red boundary cells from their rhs; the
   // up leg's pairs read the rhs the down leg's exchange brought (nothing
   // writes a level's rhs between its two legs)
@@ -3937,12 +3960,21 @@ static int32_t pf_prepare(afh_mg *mg) {
     AFH_HIP(hipMemcpy(mg->d_pf_P, P.data(), sizeof(double) * P.size(), hipMemcpyHostToDevice));
     mg->pf_nl = (int)lv.size();
     mg->pf_np = np;
-    // the vectors and the wave levels' operators in LDS when they fit
-    mg->pf_wave = afh_pf::pf_wave_from(lv);
-    const size_t lds = afh_pf::pf_lds_bytes(lv, true);
-    mg->pf_lds = lds + 64 <= 160 * 1024 ? (int)lds : 0;
+    // the vectors and the wave levels' operators in LDS when they fit, else
+    // the vectors alone (AFH_PFMG_WAVE: the largest level run by wave 0)
+    static const int wave_pts = [] {
+      const char *e = getenv("AFH_PFMG_WAVE");
+      return e && atoi(e) > 0 ? atoi(e) : afh_pf::PF_WAVE_PTS;
+    }();
+    mg->pf_wave = afh_pf::pf_wave_from(lv, wave_pts);
+    const size_t lds = afh_pf::pf_lds_bytes(lv, true, wave_pts);
+    const size_t lds_x = afh_pf::pf_lds_bytes(lv, false, wave_pts);
+    mg->pf_stage = lds + 64 <= 160 * 1024;
+    mg->pf_lds = mg->pf_stage ? (int)lds : lds_x + 64 <= 160 * 1024 ? (int)lds_x : 0;
     if (mg->pf_lds)
-      AFH_HIP(raise_dyn_lds((const void *)k_cs_pfmg<true>, mg->pf_lds));
+      AFH_HIP(raise_dyn_lds(mg->pf_stage ? (const void *)k_cs_pfmg<true, true>
+                                         : (const void *)k_cs_pfmg<true, false>,
+                            mg->pf_lds));
     else
       AFH_HIP(hipMalloc(&mg->d_pf_x, sizeof(double) * 4 * (size_t)np));
     mg->pf_a7.swap(a7);
@@ -3971,13 +4003,21 @@ static int32_t solve_coarse_pfmg(afh_mg *mg) {
   const int nid = t->ids.n(1);
   // workgroup: the level-0 points over whole waves, 256 .. 1024 lanes
   const int n0 = (int)(mg->pf_a7.size() / 7);
-  const int nt = std::min(1024, std::max(256, (n0 + 63) / 64 * 64));
-  hipLaunchKernelGGL(mg->pf_lds ? k_cs_pfmg<true> : k_cs_pfmg<false>, dim3(1), dim3(nt),
+  static const int nt_max = [] {
+    const char *e = getenv("AFH_PFMG_NT");
+    return e && atoi(e) >= 64 ? std::min(1024, atoi(e) / 64 * 64) : 1024;
+  }();
+  const int nt = std::min(nt_max, std::max(std::min(256, nt_max), (n0 + 63) / 64 * 64));
+  auto *kern = !mg->pf_lds ? k_cs_pfmg<false, false>
+               : mg->pf_stage ? k_cs_pfmg<true, true> : k_cs_pfmg<true, false>;
+  prof_begin(t, AFH_PROF_CS);
+  hipLaunchKernelGGL(kern, dim3(1), dim3(nt),
                      mg->pf_lds, t->stream, mg->d_pf_lvl, mg->pf_nl, mg->pf_wave, mg->d_pf_A,
                      mg->d_pf_P, mg->d_pf_b2r, mg->d_pf_fmask, mg->d_pf_vbc, mg->d_pf_x,
                      t->ccv(mg->d.i_phi), t->ccv(mg->d.i_rhs), t->d_boxes, t->ids.at(1), nid,
                      t->nc, t->bsz, B, mg->d.coarse_tol, mg->d.coarse_cycles, mg->d_cycles);
   AFH_LAUNCH_CHECK("k_cs_pfmg");
+  prof_end(t, AFH_PROF_CS, 0.0);
   mg->cycles_host = 0, mg->cycles_on_dev = true;
   return gc_lvl(t, 1, mg->d.i_phi, 1);
 }

@@ -72,13 +72,39 @@ __device__ __forceinline__ void pf_sync() {
   }
 }
 
+// -DAFH_PFMG_TIMING (an experiment build, never the product): thread 0
+// accumulates the shader clock spent per operation kind (each including
+// its barrier) and prints the sums at the end of the kernel
+#ifdef AFH_PFMG_TIMING
+__device__ __forceinline__ unsigned long long *pf_tacc() {
+  __shared__ unsigned long long acc[24];
+  return acc;
+}
+#define PF_T(slot)                                        \
+  do {                                                    \
+    if (threadIdx.x == 0) {                               \
+      unsigned long long *a_ = afh_pf::pf_tacc();         \
+      const unsigned long long now_ = clock64();          \
+      a_[slot] += now_ - a_[23];                          \
+      a_[12 + (slot)] += 1;                               \
+      a_[23] = now_;                                      \
+    }                                                     \
+  } while (0)
+#else
+#define PF_T(slot) \
+  do {             \
+  } while (0)
+#endif
+
 template <bool WAVE>
 __device__ __forceinline__ int pf_nthr() {
   return WAVE ? 64 : (int)blockDim.x;
 }
 
 // sum over the level's stencil entries s (mask) of a_s x(p + s), from start
-// value v0, subtracted (sub) or added -- pf_relax / pf_residual's loops
+// value v0, subtracted (sub) or added -- pf_relax / pf_residual's loops.
+// (Round 6 measured and left: all operand loads first, branch-free; the
+// solve was no faster)
 template <bool SUB>
 __device__ __forceinline__ double pf_stencil(const PfLvl &L, const double *__restrict__ Al,
                                              const double *x, int p, double v0, bool center) {
@@ -115,6 +141,7 @@ __device__ __forceinline__ void pf_relax(const PfLvl &L, const double *__restric
     }
   }
   pf_sync<WAVE>();
+  PF_T(WAVE ? 6 : 0);
 }
 
 // r = b - A x (pf_residual)
@@ -124,6 +151,16 @@ __device__ __forceinline__ void pf_residual(const PfLvl &L, const double *__rest
   for (int p = threadIdx.x; p < L.np; p += pf_nthr<WAVE>())
     r[L.off + p] = b[L.off + p] - pf_stencil<false>(L, Al, x + L.off, p, 0.0, true);
   pf_sync<WAVE>();
+  PF_T(WAVE ? 7 : 1);
+}
+
+// the level's stride and size along its coarsening direction (no indexing
+// of a per-lane array by cdir: that would live in scratch memory)
+__device__ __forceinline__ int pf_cstride(const PfLvl &F) {
+  return F.cdir == 0 ? 1 : F.cdir == 1 ? F.n[0] : F.n[0] * F.n[1];
+}
+__device__ __forceinline__ int pf_csize(const PfLvl &F) {
+  return F.cdir == 0 ? F.n[0] : F.cdir == 1 ? F.n[1] : F.n[2];
 }
 
 // b_{l+1} = R src_l (pf_restrict; src = r, or b on a skipped level)
@@ -131,27 +168,27 @@ template <bool WAVE>
 __device__ __forceinline__ void pf_restrict(const PfLvl &F, const PfLvl &C,
                                             const double *__restrict__ Pw, const double *src,
                                             double *b) {
-  const int cd = F.cdir;
+  const int cd = F.cdir, st = pf_cstride(F), nf = pf_csize(F);
   const double *Pl = Pw + (size_t)2 * F.off;
   for (int p = threadIdx.x; p < C.np; p += pf_nthr<WAVE>()) {
-    int c[3];
-    pf_decode(C, p, c[0], c[1], c[2]);
-    int f[3] = {c[0], c[1], c[2]};
-    f[cd] = 2 * f[cd];
-    double v = src[F.off + pf_pt(F, f[0], f[1], f[2])];
-    f[cd] -= 1;
+    int c0, c1, c2;
+    pf_decode(C, p, c0, c1, c2);
+    const int cc = cd == 0 ? c0 : cd == 1 ? c1 : c2;
+    // the fine point 2 c along cdir, then its two neighbours along it
+    const int q0 = pf_pt(F, cd == 0 ? 2 * c0 : c0, cd == 1 ? 2 * c1 : c1, cd == 2 ? 2 * c2 : c2);
+    double v = src[F.off + q0];
     {
-      const int q = pf_pt(F, f[0], f[1], f[2]);
+      const int q = q0 - st;
       v = v + Pl[(size_t)F.np + q] * src[F.off + q];
     }
-    f[cd] += 2;
-    if (f[cd] <= F.n[cd]) {
-      const int q = pf_pt(F, f[0], f[1], f[2]);
+    if (2 * cc + 1 <= nf) {
+      const int q = q0 + st;
       v = v + Pl[q] * src[F.off + q];
     }
     b[C.off + p] = v;
   }
   pf_sync<WAVE>();
+  PF_T(WAVE ? 8 : 2);
 }
 
 // x_l += P x_{l+1} (pf_interp_add); assign: x_l = P x_{l+1} (a skipped level)
@@ -159,30 +196,27 @@ template <bool WAVE>
 __device__ __forceinline__ void pf_interp(const PfLvl &F, const PfLvl &C,
                                           const double *__restrict__ Pw, const double *xc,
                                           double *x, bool assign) {
-  const int cd = F.cdir;
+  const int cd = F.cdir, nf = pf_csize(F);
+  const int cst = cd == 0 ? 1 : cd == 1 ? C.n[0] : C.n[0] * C.n[1];
   const double *Pl = Pw + (size_t)2 * F.off;
   for (int p = threadIdx.x; p < F.np; p += pf_nthr<WAVE>()) {
-    int f[3];
-    pf_decode(F, p, f[0], f[1], f[2]);
-    int c[3] = {f[0], f[1], f[2]};
+    int f0, f1, f2;
+    pf_decode(F, p, f0, f1, f2);
+    const int fc = cd == 0 ? f0 : cd == 1 ? f1 : f2;
+    // the coarse point with cdir coordinate 1 (then + (m - 1) cst for m)
+    const int pc1 = pf_pt(C, cd == 0 ? 1 : f0, cd == 1 ? 1 : f1, cd == 2 ? 1 : f2);
     double e;
-    if (!(f[cd] & 1)) {
-      c[cd] = f[cd] / 2;
-      e = xc[C.off + pf_pt(C, c[0], c[1], c[2])];
+    if (!(fc & 1)) {
+      e = xc[C.off + pc1 + (fc / 2 - 1) * cst];
     } else {
       e = 0.0;
-      if (f[cd] >= 3) {
-        c[cd] = (f[cd] - 1) / 2;
-        e = Pl[p] * xc[C.off + pf_pt(C, c[0], c[1], c[2])];
-      }
-      if (f[cd] + 1 <= F.n[cd]) {
-        c[cd] = (f[cd] + 1) / 2;
-        e = e + Pl[(size_t)F.np + p] * xc[C.off + pf_pt(C, c[0], c[1], c[2])];
-      }
+      if (fc >= 3) e = Pl[p] * xc[C.off + pc1 + ((fc - 1) / 2 - 1) * cst];
+      if (fc + 1 <= nf) e = e + Pl[(size_t)F.np + p] * xc[C.off + pc1 + ((fc + 1) / 2 - 1) * cst];
     }
     x[F.off + p] = assign ? e : x[F.off + p] + e;
   }
   pf_sync<WAVE>();
+  PF_T(WAVE ? 9 : 3);
 }
 
 // v.v on level 0 (pf_dot: 64 strided partial sums, pairwise tree); every
@@ -197,6 +231,7 @@ __device__ __forceinline__ double pf_dot(const PfLvl &L, const double *v, double
   __syncthreads();
   const double out = *slot;
   __syncthreads();
+  PF_T(4);
   return out;
 }
 
@@ -239,17 +274,18 @@ inline void pf_device_tables(const afh_pfmg &h, std::vector<PfLvl> &lv, std::vec
 
 // First level of at most PF_WAVE_PTS points below level 0 (nl: none; 1 at
 // the least, level 0 always runs on the workgroup)
-inline int pf_wave_from(const std::vector<PfLvl> &lv) {
+inline int pf_wave_from(const std::vector<PfLvl> &lv, int wave_pts = PF_WAVE_PTS) {
   int ls = (int)lv.size();
-  for (int l = (int)lv.size() - 1; l >= 1 && lv[l].np <= PF_WAVE_PTS; l--) ls = l;
+  for (int l = (int)lv.size() - 1; l >= 1 && lv[l].np <= wave_pts; l--) ls = l;
   return ls;
 }
 
 // LDS bytes of pf_solve_block: two x images, b, r (np each), the staged
 // operators of the wave levels, the dot product's slot
-inline size_t pf_lds_bytes(const std::vector<PfLvl> &lv, bool stage) {
+inline size_t pf_lds_bytes(const std::vector<PfLvl> &lv, bool stage,
+                           int wave_pts = PF_WAVE_PTS) {
   const size_t np = lv.back().off + lv.back().np;
-  const int ls = pf_wave_from(lv);
+  const int ls = pf_wave_from(lv, wave_pts);
   const size_t nsm = ls < (int)lv.size() ? np - lv[ls].off : 0;
   return sizeof(double) * (4 * np + (stage ? 27 * nsm : 0) + 1);
 }
@@ -263,15 +299,15 @@ __device__ __forceinline__ void pf_legs(const PfLvl *__restrict__ Lg, int nl, in
                                         const double *Aw, int soff,
                                         const double *__restrict__ Pw, double *X0, double *X1,
                                         uint64_t &cur, double *b, double *r) {
-  double *X[2] = {X0, X1};
+  auto X = [&](int c) { return c ? X1 : X0; };
   auto Al = [&](const PfLvl &L) { return Aw + (size_t)27 * (L.off - soff); };
   int l;
   for (l = from; l <= nl - 2; l++) {
     const PfLvl L = Lg[l];
     const int c = (cur >> l) & 1;
     if (L.active) {
-      pf_relax<WAVE>(L, Al(L), X[c], X[c], b, true);
-      pf_residual<WAVE>(L, Al(L), X[c], b, r);
+      pf_relax<WAVE>(L, Al(L), X(c), X(c), b, true);
+      pf_residual<WAVE>(L, Al(L), X(c), b, r);
       pf_restrict<WAVE>(L, Lg[l + 1], Pw, r, b);
     } else {
       pf_restrict<WAVE>(L, Lg[l + 1], Pw, b, b);
@@ -280,14 +316,14 @@ __device__ __forceinline__ void pf_legs(const PfLvl *__restrict__ Lg, int nl, in
   {
     const PfLvl L = Lg[nl - 1];  // the bottom (always relaxed)
     const int c = (cur >> (nl - 1)) & 1;
-    pf_relax<WAVE>(L, Al(L), X[c], X[c], b, true);
+    pf_relax<WAVE>(L, Al(L), X(c), X(c), b, true);
   }
   for (l = nl - 2; l >= from; l--) {
     const PfLvl L = Lg[l];
     const int c = (cur >> l) & 1, cc = (cur >> (l + 1)) & 1;
-    pf_interp<WAVE>(L, Lg[l + 1], Pw, X[cc], X[c], !L.active);
+    pf_interp<WAVE>(L, Lg[l + 1], Pw, X(cc), X(c), !L.active);
     if (L.active) {
-      pf_relax<WAVE>(L, Al(L), X[c], X[c ^ 1], b, false);
+      pf_relax<WAVE>(L, Al(L), X(c), X(c ^ 1), b, false);
       cur ^= 1ull << l;
     }
   }
@@ -305,7 +341,7 @@ __device__ inline int pf_solve_block(const PfLvl *__restrict__ Lg, int nl, int w
                                      double *b, double *r, double *slot, double tol,
                                      int max_iter, int *cur_out) {
   const PfLvl L0 = Lg[0];
-  double *X[2] = {X0, X1};
+  auto X = [&](int c) { return c ? X1 : X0; };
   auto Al = [&](const PfLvl &L) { return A + (size_t)27 * L.off; };
   uint64_t cur = 0;  // per level: the image holding its x
   int iters = 0;
@@ -318,9 +354,9 @@ __device__ inline int pf_solve_block(const PfLvl *__restrict__ Lg, int nl, int w
   }
   const double eps = tol * tol;
   for (int it = 0; it < max_iter; it++) {
-    pf_relax<false>(L0, Al(L0), X[cur & 1], X[(cur & 1) ^ 1], b, false);
+    pf_relax<false>(L0, Al(L0), X(cur & 1), X((cur & 1) ^ 1), b, false);
     cur ^= 1;
-    pf_residual<false>(L0, Al(L0), X[cur & 1], b, r);
+    pf_residual<false>(L0, Al(L0), X(cur & 1), b, r);
     if (tol > 0.0) {
       const double rr = pf_dot(L0, r, slot);
       if (rr / bb < eps && it > 0) break;
@@ -334,8 +370,8 @@ __device__ inline int pf_solve_block(const PfLvl *__restrict__ Lg, int nl, int w
         const PfLvl L = Lg[l];
         const int c = (cur >> l) & 1;
         if (L.active) {
-          pf_relax<false>(L, Al(L), X[c], X[c], b, true);
-          pf_residual<false>(L, Al(L), X[c], b, r);
+          pf_relax<false>(L, Al(L), X(c), X(c), b, true);
+          pf_residual<false>(L, Al(L), X(c), b, r);
           pf_restrict<false>(L, Lg[l + 1], Pw, r, b);
         } else {
           pf_restrict<false>(L, Lg[l + 1], Pw, b, b);
@@ -345,12 +381,13 @@ __device__ inline int pf_solve_block(const PfLvl *__restrict__ Lg, int nl, int w
         // no wave part: the bottom on the workgroup
         const PfLvl L = Lg[nl - 1];
         const int c = (cur >> (nl - 1)) & 1;
-        pf_relax<false>(L, Al(L), X[c], X[c], b, true);
+        pf_relax<false>(L, Al(L), X(c), X(c), b, true);
       } else {
         if (threadIdx.x < 64) pf_legs<true>(Lg, nl, wave_from, Aw, soff, Pw, X0, X1, cur, b, r);
         // wave 0's images of the wave levels, to every lane
         __shared__ unsigned long long pf_cur;
         __syncthreads();
+        PF_T(5);
         if (threadIdx.x == 0) pf_cur = cur;
         __syncthreads();
         cur = pf_cur;
@@ -359,15 +396,15 @@ __device__ inline int pf_solve_block(const PfLvl *__restrict__ Lg, int nl, int w
       for (l = top - 1; l >= 1; l--) {
         const PfLvl L = Lg[l];
         const int c = (cur >> l) & 1, cc = (cur >> (l + 1)) & 1;
-        pf_interp<false>(L, Lg[l + 1], Pw, X[cc], X[c], !L.active);
+        pf_interp<false>(L, Lg[l + 1], Pw, X(cc), X(c), !L.active);
         if (L.active) {
-          pf_relax<false>(L, Al(L), X[c], X[c ^ 1], b, false);
+          pf_relax<false>(L, Al(L), X(c), X(c ^ 1), b, false);
           cur ^= 1ull << l;
         }
       }
-      pf_interp<false>(L0, Lg[1], Pw, X[(cur >> 1) & 1], X[cur & 1], false);
+      pf_interp<false>(L0, Lg[1], Pw, X((cur >> 1) & 1), X(cur & 1), false);
     }
-    pf_relax<false>(L0, Al(L0), X[cur & 1], X[(cur & 1) ^ 1], b, false);
+    pf_relax<false>(L0, Al(L0), X(cur & 1), X((cur & 1) ^ 1), b, false);
     cur ^= 1;
     iters = it + 1;
   }

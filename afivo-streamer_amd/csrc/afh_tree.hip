@@ -346,8 +346,11 @@ int32_t gc_lvl_var(afh_tree *t, int lvl, int iv, const double *vc,
       }
     }
   }
-  if (rims || t->lvl_rb_coarse[lvl - 1])
-    return call_hook(t, AFH_HOOK_RIMS, lvl, iv, nullptr, depth);
+  // replicas' ghost cells: a finer level's fill interpolates from this
+  // level's (every ghost cell), or only a fused pair reads them (their face
+  // ghosts next to its box: n = 10 + depth, most filled by the receiver)
+  if (t->lvl_rb_coarse[lvl - 1]) return call_hook(t, AFH_HOOK_RIMS, lvl, iv, nullptr, depth);
+  if (rims) return call_hook(t, AFH_HOOK_RIMS, lvl, iv, nullptr, 10 + depth);
   return AFH_OK;
 }
 

@@ -55,9 +55,13 @@ program ref_timing
   logical            :: from_record
 
   call get_command_argument(1, arg)
-  read(arg, *, iostat=ios) levels
-  from_record = ios /= 0
-  if (from_record) rec_file = arg
+  ! (a path is not read as a number: list-directed input ends at its '/')
+  from_record = verify(trim(arg), "0123456789") /= 0
+  if (from_record) then
+     rec_file = arg
+  else
+     read(arg, *, iostat=ios) levels
+  end if
   call get_command_argument(2, arg)
   read(arg, *) reps
   do n = 3, command_argument_count()
