@@ -1072,12 +1072,16 @@ class Simulation:
         self.dt = min(tmp * self.global_dt, self.dt_safety * min(dt_lim, self.dt_max))
         self.global_dt = self.dt
         self.global_time = self.time
+        # dt below dt_min: the reference writes the output (its regression
+        # row included) and then stops (streamer.f90:357-378)
         if self.global_dt < self.dt_min:
-            raise RuntimeError("dt too small")
+            write_out = True
         if write_out:
             self.output_cnt += 1
             self.time_last_output = self.global_time
             self.output_write()
+        if self.global_dt < self.dt_min:
+            raise RuntimeError("dt too small")
         if self.it % c.i("refine_per_steps") == 0:
             for iv in self.densities:
                 self.tree.restrict_tree(iv)

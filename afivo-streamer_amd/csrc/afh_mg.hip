@@ -2506,6 +2506,9 @@ __global__ void __launch_bounds__(256)
   c[d] = in_halo;
   const double *src = in + ((size_t)c[2] * hy + c[1]) * hx + c[0];
   double s = 0.0;
+  // (unrolled: the loads of 16 terms in flight together; the sum keeps the
+  // p order)
+#pragma unroll 16
   for (int p = 0; p < n; p++) s = s + M[(size_t)p * n + co] * src[p * st];
   if (div) {
     const double den = ((e0[i] + e1[j]) + e2[k]) - lam;
@@ -3961,14 +3964,11 @@ static int32_t pf_prepare(afh_mg *mg) {
     mg->pf_nl = (int)lv.size();
     mg->pf_np = np;
     // the vectors and the wave levels' operators in LDS when they fit, else
-    // the vectors alone (AFH_PFMG_WAVE: the largest level run by wave 0)
-    static const int wave_pts = [] {
-      const char *e = getenv("AFH_PFMG_WAVE");
-      return e && atoi(e) > 0 ? atoi(e) : afh_pf::PF_WAVE_PTS;
-    }();
-    mg->pf_wave = afh_pf::pf_wave_from(lv, wave_pts);
-    const size_t lds = afh_pf::pf_lds_bytes(lv, true, wave_pts);
-    const size_t lds_x = afh_pf::pf_lds_bytes(lv, false, wave_pts);
+    // the vectors alone (round 6: levels of up to 128 or 256 points on wave
+    // 0 measured slower, scripts/pfmg_probe.py)
+    mg->pf_wave = afh_pf::pf_wave_from(lv);
+    const size_t lds = afh_pf::pf_lds_bytes(lv, true);
+    const size_t lds_x = afh_pf::pf_lds_bytes(lv, false);
     mg->pf_stage = lds + 64 <= 160 * 1024;
     mg->pf_lds = mg->pf_stage ? (int)lds : lds_x + 64 <= 160 * 1024 ? (int)lds_x : 0;
     if (mg->pf_lds)
@@ -4003,11 +4003,8 @@ static int32_t solve_coarse_pfmg(afh_mg *mg) {
   const int nid = t->ids.n(1);
   // workgroup: the level-0 points over whole waves, 256 .. 1024 lanes
   const int n0 = (int)(mg->pf_a7.size() / 7);
-  static const int nt_max = [] {
-    const char *e = getenv("AFH_PFMG_NT");
-    return e && atoi(e) >= 64 ? std::min(1024, atoi(e) / 64 * 64) : 1024;
-  }();
-  const int nt = std::min(nt_max, std::max(std::min(256, nt_max), (n0 + 63) / 64 * 64));
+  // (256 or 512 lanes on S4 / S5's 512 / 2048 points measured slower)
+  const int nt = std::min(1024, std::max(256, (n0 + 63) / 64 * 64));
   auto *kern = !mg->pf_lds ? k_cs_pfmg<false, false>
                : mg->pf_stage ? k_cs_pfmg<true, true> : k_cs_pfmg<true, false>;
   prof_begin(t, AFH_PROF_CS);

@@ -5,8 +5,9 @@ usage: python scripts/pfmg_probe.py OUT.json [configs...] (default s3 s4 s5)
 Builds each configuration's set-up tree (bench.build_driver_case), runs
 field_compute a few times eagerly (AFH_GRAPHS=0) with the AFH_PROF_CS events
 around every k_cs_pfmg launch, and writes the mean launch time, the PFMG
-iteration count and the level-0 size. AFH_PFMG_WAVE / AFH_PFMG_NT in the
-environment select the variant (read once per process)."""
+iteration count. With AFH_HIP_LIB naming a -DAFH_PFMG_TIMING build
+of the library, the kernel also prints its per-operation clock sums
+(PFTIME lines)."""
 import ctypes as C
 import json
 import os
@@ -37,9 +38,7 @@ def probe(lib, config, reps=6):
     return {"config": config, "launches": nl.value,
             "us_per_launch": 1e3 * ms.value / max(nl.value, 1),
             "iterations": sim.mg.coarse_iterations(),
-            "field_compute_wall_ms": 1e3 * wall,
-            "wave": os.environ.get("AFH_PFMG_WAVE", "64"),
-            "nt": os.environ.get("AFH_PFMG_NT", "1024")}
+            "field_compute_wall_ms": 1e3 * wall}
 
 
 def main():

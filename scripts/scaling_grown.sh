@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 CFG=${CFG:-s5}; CELLS=${CELLS:-4.4e6}; FLOORS=${FLOORS:-"0 1048576"}; NS=${NS:-"2 4 8"}
 D=gpurun_out/scale_grown_$CFG
 mkdir -p $D
-timeout -k 10 ${PTIME:-900} rocprofv3 --kernel-trace --output-format csv -d $D/prof -o run -- \
+DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 timeout -k 10 ${PTIME:-900} rocprofv3 --kernel-trace --output-format csv -d $D/prof -o run -- \
   python3 scripts/scaling_grown.py $CFG $CELLS $D --ns $NS --floors $FLOORS --steps ${K:-5} \
   > $D/run.log 2> $D/run.err
 rc=$?; echo "grown $CFG rc=$rc"; [ $rc -eq 0 ] || { tail -5 $D/run.err; exit $rc; }
