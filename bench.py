@@ -824,9 +824,21 @@ def main():
             out["value_without_level1"] = ncell / (ms_x * 1e-3)
             # a set-up tree of 17.5 K cells is launch-bound: no kernel's HBM
             # fraction says anything about it
-            out["roofline"]["note"] = ("launch-bound configuration (tens of kernels per "
-                                       "step, microseconds each): the fraction is not a "
-                                       "measure of kernel quality here")
+            out["roofline"]["note"] = ("launch-bound configuration (a hundred-odd kernels "
+                                       "per step, microseconds each): the fraction is not a "
+                                       "measure of kernel quality here; see launch_bound")
+            # what bounds it instead: launches per step and their mean time,
+            # from the committed steady-step kernel trace of this config
+            # (scripts/prof_cfg.sh -> scripts/prof_steady.py)
+            sp = os.path.join(REPO, "profiles", "r06_steady_2d.json")
+            if os.path.exists(sp):
+                st = json.load(open(sp))
+                out["launch_bound"] = {
+                    "launches_per_step": st["launches_per_step"],
+                    "us_per_launch": 1e3 * st["busy_ms_per_step"] / st["launches_per_step"],
+                    "gap_share": st["gap_share"],
+                    "source": "profiles/r06_steady_2d.json (rocprofv3 kernel trace of this "
+                              "command, the timed window's unit steps)"}
             # the C oracle is 3-D: the reference's own 2-D code on the same
             # set-up tree (scripts/record_setup_state.py -> ref_timing's
             # record mode), timed in the build container -- its binary does

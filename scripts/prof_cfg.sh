@@ -22,3 +22,5 @@ rc=$?; echo "rocprof $CFG rc=$rc"; [ $rc -eq 0 ] || { tail -20 gpurun_out/prof_$
 unset DEBUG_CLR_GRAPH_PACKET_CAPTURE
 python3 scripts/prof_steady.py gpurun_out/prof_$CFG/run_kernel_trace.csv $K \
   gpurun_out/steady_$CFG.json gpurun_out/topo_$CFG.json
+# (the trace of a grown tree is large: keep the summaries)
+rm -f gpurun_out/prof_$CFG/run_kernel_trace.csv
