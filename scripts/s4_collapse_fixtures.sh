@@ -20,8 +20,8 @@ if [ ! -f $W/s4_rtest.log ] || [ -n "$RERUN" ]; then
     -refine_min_dx=1e-4 -output%name=$W/s4 -output%regression_test=T -silo_write=f \
     -end_time=2.5e-9 -output%dt=0.05e-9 > $W/stdout.txt 2>&1 || true
 fi
-cp $W/s4_rtest.log $REPO/tests/golden/s4_collapse_ref_rtest.log
+cp $W/s4_rtest.log $REPO/tests/golden/s4_collapse_ref_rtest.txt
 tail -n 12 $W/stdout.txt > $REPO/tests/golden/s4_collapse_ref_stop.txt
 cp ${1:-$REPO/gpurun_out/s4_rows_hip.json} $REPO/tests/golden/s4_collapse_hip_rows.json
 python3 $REPO/scripts/s4_collapse_compare.py $REPO/tests/golden/s4_collapse_hip_rows.json \
-  $REPO/tests/golden/s4_collapse_ref_rtest.log $W/stdout.txt $REPO/profiles/r06_s4_collapse.json
+  $REPO/tests/golden/s4_collapse_ref_rtest.txt $W/stdout.txt $REPO/profiles/r06_s4_collapse.json

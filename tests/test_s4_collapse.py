@@ -2,7 +2,7 @@
 reference's own streamer.f90 stop where afh.driver stops?
 
 Fixtures (tests/golden/, made by scripts/s4_collapse_fixtures.sh):
-- s4_collapse_ref_rtest.log: the regression log of the reference's
+- s4_collapse_ref_rtest.txt: the regression log of the reference's
   src/streamer.f90 itself, built from the reference sources and run through
   the shim on the C oracle (oracle/_ref/dropin_streamer, build container),
   on BASELINE config 4 (tests/test_dropin_streamer.py's S4 arguments,
@@ -25,7 +25,7 @@ import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLD = os.path.join(REPO, "tests", "golden")
-REF_LOG = os.path.join(GOLD, "s4_collapse_ref_rtest.log")
+REF_LOG = os.path.join(GOLD, "s4_collapse_ref_rtest.txt")
 REF_STOP = os.path.join(GOLD, "s4_collapse_ref_stop.txt")
 HIP_ROWS = os.path.join(GOLD, "s4_collapse_hip_rows.json")
 # measured 4.7e-8 over all 46 rows (the rows are printed in E20.8); the
