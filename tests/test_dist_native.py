@@ -17,6 +17,8 @@ the tree, builds the exchange plans and runs the exchange hook itself.
   result is bitwise the unsharded run. Multi-rank RCCL is unmeasured here.
 """
 import ctypes as C
+import os
+import sys
 from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
@@ -553,3 +555,34 @@ def test_rccl_capture_single_rank_bitwise(monkeypatch):
     _compare(ref, [sh], [out])
     # whole-graph replays (a segment replay would count as segmented)
     assert replays > 0 and segmented == 0, (replays, segmented)
+
+
+def _peer_bytes_consistent(lib, name, world, monkeypatch):
+    """afh_dist_peer_bytes (round 6): what rank r sent to q is what q
+    received from r, and nothing goes to a rank itself (read as each rank
+    detaches)."""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    pb = {}
+    detach = NativeShard.detach
+
+    def record(self):
+        pb[self.rank] = bench.dist_peer_bytes(self.lib, self)
+        detach(self)
+    monkeypatch.setattr(NativeShard, "detach", record)
+    _run_threads(lib, name, world)
+    assert sorted(pb) == list(range(world))
+    for r in range(world):
+        assert pb[r][0][r] == 0 and pb[r][1][r] == 0
+        for q in range(world):
+            assert pb[r][0][q] == pb[q][1][r], (r, q)
+    assert sum(int(pb[r][0].sum()) for r in range(world)) > 0
+
+
+def test_peer_bytes_consistent_oracle(monkeypatch):
+    _peer_bytes_consistent(capi.oracle_library(), "amr8", 3, monkeypatch)
+
+
+@pytest.mark.gpu
+def test_peer_bytes_consistent_hip(monkeypatch):
+    _peer_bytes_consistent(capi.hip_library(), "amr8", 3, monkeypatch)
