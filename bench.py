@@ -626,11 +626,11 @@ def main():
     import ctypes as C
     graphs = args.graphs == "on" or (args.graphs == "auto" and args.config != "s1-64")
     if two_d:
-        # no graphs in the 2-D build; its smoother is the split half sweep
-        # k2_gsrb on every level (one thread per cell pair of 8^2 boxes),
-        # timed after the timed region (its launches are a few us each, the
-        # events around them would weigh on the step clock)
-        graphs = False
+        # the 2-D library replays its V-cycles as hipGraphs by itself
+        # (AFH2_GRAPHS, default on: nothing is profiled in the timed region);
+        # its kernels are timed after the timed region (launches of a few us
+        # each, the events around them would weigh on the step clock)
+        graphs = os.environ.get("AFH2_GRAPHS", "1") != "0"
     elif not graphs:
         lib.call("profile_enable", case.tree.h, capi.PROF_GSRB_PAIR)
     barrier()
