@@ -784,7 +784,7 @@ __global__ void __launch_bounds__(RbBox<NC>::NT)
                     const afh_box_meta *__restrict__ meta,
                     const int32_t *__restrict__ ids, size_t bsz, Coef cf,
                     double inv_c1, GcArgs ga, const double *const *__restrict__ vp = nullptr,
-                    const double *const *__restrict__ bp = nullptr) {
+                    const double *const *__restrict__ bp = nullptr, int pend = 0) {
   using G = RbBox<NC>;
   constexpr int NG = G::NG, HN = G::HN, NT = G::NT, RPT = G::RPT, GPT = G::GPT;
   constexpr int SK = NG * NG, NB = NG * NG * NG;
@@ -811,6 +811,13 @@ __global__ void __launch_bounds__(RbBox<NC>::NT)
   const double *r = rhs + (size_t)(id - 1) * bsz;
   // VAR: this box's stencil and correction (null: constant)
   const double *bv = VAR ? vp[id - 1] : nullptr, *bb = VAR ? bp[id - 1] : nullptr;
+  // VAR, pend: the rhs round trips of the level's earlier pairs of this leg
+  // not yet stored (k_rhs_roundtrip runs once, after the leg's last pair):
+  // an electrode box's rhs is read through them, in k_rhs_roundtrip's order
+  auto rtp = [&](double v, double c) {
+    for (int q = 0; q < pend; q++) v = (v + c) - c;
+    return v;
+  };
 
   // red cell q of this thread: row (j, k), i = 2 ih + 1 + ((j + k) & 1);
   // the black cell of the same pair of columns is the other parity
@@ -859,8 +866,8 @@ __global__ void __launch_bounds__(RbBox<NC>::NT)
         if (bb) {
           // rhs + bc_correction of the red sweep; the black sweep's after
           // the red sweep's round trip
-          rR[q] = rR[q] + bb[eR];
-          rB[q] = ((rB[q] + bb[eB]) - bb[eB]) + bb[eB];
+          rR[q] = rtp(rR[q], bb[eR]) + bb[eR];
+          rB[q] = ((rtp(rB[q], bb[eB]) + bb[eB]) - bb[eB]) + bb[eB];
         }
       }
     }
@@ -907,7 +914,7 @@ __global__ void __launch_bounds__(RbBox<NC>::NT)
 #pragma unroll
             for (int s = 0; s < 7; s++) vn[g][s] = nv[7 * en + s];
             const double *nbc = bp[nid - 1];
-            if (nbc) bl[g][6] = bl[g][6] + nbc[en];
+            if (nbc) bl[g][6] = rtp(bl[g][6], nbc[en]) + nbc[en];
           }
         }
       }
@@ -3207,9 +3214,13 @@ static bool pair_push(const afh_mg *mg) {
   return mg->pair_push && mg->pair_box && mg->t->nc <= 16 && !mg->t->hook;
 }
 
+// pend: rhs round trips of earlier pairs of the leg not yet stored (read
+// through by the variable small-box pair); last: the leg's last pair, after
+// which they are stored with its own (the other pair forms store their own)
 template <int NC>
 static void launch_pair(afh_mg *mg, int lvl, const double *src, double *dst,
-                        const Coef &cf, double inv_c1, hipEvent_t e0, hipEvent_t e1) {
+                        const Coef &cf, double inv_c1, hipEvent_t e0, hipEvent_t e1,
+                        int pend = 0, bool last = true) {
   afh_tree *t = mg->t;
   if (t->ids.n(lvl) == 0) return;
   if constexpr (NC <= 16) {
@@ -3219,18 +3230,20 @@ static void launch_pair(afh_mg *mg, int lvl, const double *src, double *dst,
         launch_ev(kern, e0, e1, dim3(t->ids.n(lvl)), dim3(RbBox<NC>::NT), t->stream, src, dst,
                   t->ccv(mg->d.i_rhs), t->ccv(mg->d.i_phi), t->d_boxes, t->ids.at(lvl),
                   t->bsz, cf, inv_c1, t->gc_args(mg->d.i_phi),
-                  (const double *const *)mg->d_vp, (const double *const *)mg->d_bp);
+                  (const double *const *)mg->d_vp, (const double *const *)mg->d_bp,
+                  var ? pend : 0);
       };
       if (pair_push(mg))
         var ? go(k_gsrb_pair_box<NC, true, true>) : go(k_gsrb_pair_box<NC, true>);
       else
         var ? go(k_gsrb_pair_box<NC, false, true>) : go(k_gsrb_pair_box<NC>);
-      if (var && mg->ids_v.n(lvl)) {
-        // the two half-sweeps' rhs round trips on the electrode boxes
+      if (var && mg->ids_v.n(lvl) && last) {
+        // the half-sweeps' rhs round trips on the electrode boxes: two per
+        // pair, this pair's and the pending ones, in one launch (round 6)
         const int nc = t->nc;
         hipLaunchKernelGGL(k_rhs_roundtrip, dim3((nc * nc * nc + 255) / 256, mg->ids_v.n(lvl)),
                            dim3(256), 0, t->stream, t->ccv(mg->d.i_rhs), mg->ids_v.at(lvl),
-                           nc, t->bsz, (const double *const *)mg->d_bp, 2);
+                           nc, t->bsz, (const double *const *)mg->d_bp, pend + 2);
         // (the caller's launch check covers it)
       }
       return;
@@ -3394,10 +3407,14 @@ static int32_t gsrb_boxes(afh_mg *mg, int lvl, bool up, bool stale_ghosts = fals
                                                                      : -1;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     const bool timed = prof_ext(t, pclass, e0, e1);
+    // (the variable small-box pair: the leg's rhs round trips stored once,
+    // after its last pair; nothing else reads the rhs in between)
+    const int pend = 2 * (n - n0);
+    const bool last = n == n_cycle;
     switch (nc) {
-    case 4: launch_pair<4>(mg, lvl, src, dst, cf, inv_c1, e0, e1); break;
-    case 8: launch_pair<8>(mg, lvl, src, dst, cf, inv_c1, e0, e1); break;
-    case 16: launch_pair<16>(mg, lvl, src, dst, cf, inv_c1, e0, e1); break;
+    case 4: launch_pair<4>(mg, lvl, src, dst, cf, inv_c1, e0, e1, pend, last); break;
+    case 8: launch_pair<8>(mg, lvl, src, dst, cf, inv_c1, e0, e1, pend, last); break;
+    case 16: launch_pair<16>(mg, lvl, src, dst, cf, inv_c1, e0, e1, pend, last); break;
     case 32: launch_pair<32>(mg, lvl, src, dst, cf, inv_c1, e0, e1); break;
     default: launch_pair<64>(mg, lvl, src, dst, cf, inv_c1, e0, e1); break;
     }
